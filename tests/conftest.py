@@ -1,0 +1,40 @@
+import base64
+import json
+import os
+import sys
+import zlib
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "java-rsync_amd"))
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) device")
+    config.addinivalue_line("markers", "slow: long-running parity sweep")
+
+
+_GOLD = None
+
+
+def golden():
+    """tests/golden/cases.json with input blobs decoded (bytes)."""
+    global _GOLD
+    if _GOLD is None:
+        with open(os.path.join(ROOT, "tests", "golden", "cases.json")) as f:
+            d = json.load(f)
+        blobs = {k: zlib.decompress(base64.b64decode(v)) for k, v in d["blobs"].items()}
+        for c in d["cases"]:
+            c["basis_bytes"] = None if c["basis"] is None else blobs[c["basis"]]
+            c["src_bytes"] = blobs[c["src"]]
+            c["seed_bytes"] = bytes.fromhex(c["seed"])
+        _GOLD = d["cases"]
+    return _GOLD
+
+
+@pytest.fixture(scope="session")
+def golden_cases():
+    return golden()
