@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident rolling+MD5 scan throughput of java-rsync's delta-transfer checksum path.
+
+One step = the hot path over one file pair already resident in HBM:
+  Generator block sums over the basis  (Generator.sendItemizeAndChecksums, Generator.java:886-895)
+  + Sender match scan over the source  (Sender.sendMatchesAndData, Sender.java:1235-1327)
+through the C-ABI (rsh_block_sums_device + rsh_match_scan_device).  Workload (BASELINE.json config 5):
+a 16 GiB source against a 50%-modified basis (every other block replaced), B = 131072, dl = 4, seed
+01 02 03 04, splitmix64 synthetic bytes generated on the device.  The serial whole-file MD5 runs on the
+host in the product (rsh_match_scan) and is excluded here (see DESIGN.md "Measurement").
+
+Multi-GPU: one process per GPU (torch.distributed.run), each rank scans its own file pair (file-parallel
+sharding, no collective on the data path); value = all ranks' bytes / max-over-ranks time.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "java-rsync_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import rsync_hip as R  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+KEY_SRC = 0x5EED5EED << 32
+KEY_EDIT = (0x5EED5EED << 32) | 0xED17
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--size-gib", type=float, default=16.0)
+    ap.add_argument("--block", type=int, default=131072)
+    ap.add_argument("--digest", type=int, default=4)
+    ap.add_argument("--variant", choices=["half", "identical"], default="half")
+    ap.add_argument("--cpu-sample-mib", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    if not os.path.exists(R.LIB_PATH):
+        R.build()
+    L = R.lib()
+    ctx = R.Context(local)
+    stream = torch.cuda.ExternalStream(L.rsh_ctx_stream(ctx.handle))
+
+    n = int(a.size_gib * (1 << 30))
+    B, dl = a.block, a.digest
+    seed = np.frombuffer(bytes([1, 2, 3, 4]), np.uint8).copy()
+    h = R.header_make(B, dl, n)
+    R.header_validate(h)  # what the Sender's Connection.receiveChecksumHeader enforces
+    C = h.chunk_count
+
+    # ---- synthetic, device-resident inputs (per-rank file: key depends on the rank)
+    key = KEY_SRC ^ (rank << 20)
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    basis = torch.empty(n, dtype=torch.uint8, device="cuda")
+    assert L.rsh_fill_splitmix_device(ctx.handle, src.data_ptr(), n, key, 0) == 0
+    assert L.rsh_fill_splitmix_device(ctx.handle, basis.data_ptr(), n, key, 0) == 0
+    if a.variant == "half":
+        other = torch.empty(n, dtype=torch.uint8, device="cuda")
+        assert L.rsh_fill_splitmix_device(ctx.handle, other.data_ptr(), n, KEY_EDIT ^ (rank << 20), 0) == 0
+        ctx.sync()
+        full = (n // B) * B
+        basis[:full].view(-1, B)[1::2] = other[:full].view(-1, B)[1::2]
+        del other
+    torch.cuda.synchronize()
+    ctx.sync()
+    d_weak = torch.empty(max(C, 1), dtype=torch.int32, device="cuda")
+    d_strong = torch.empty(max(C * dl, 1), dtype=torch.uint8, device="cuda")
+    cap = C + (n // B) + 4096
+    ev = np.zeros(cap, R.EVENT_DTYPE)
+    n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    st = R.ScanStats()
+    gen_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+
+    def step(i=None):
+        if i is not None:
+            gen_ev[i][0].record(stream)
+        rc = L.rsh_block_sums_device(ctx.handle, ctypes.c_void_p(basis.data_ptr()), n, ctypes.byref(h),
+                                     seed.ctypes.data, ctypes.c_void_p(d_weak.data_ptr()),
+                                     ctypes.c_void_p(d_strong.data_ptr()))
+        assert rc == 0, rc
+        if i is not None:
+            gen_ev[i][1].record(stream)
+        rc = L.rsh_match_scan_device(ctx.handle, ctypes.c_void_p(src.data_ptr()), n, ctypes.byref(h),
+                                     ctypes.c_void_p(d_weak.data_ptr()), ctypes.c_void_p(d_strong.data_ptr()),
+                                     seed.ctypes.data, ev.ctypes.data, cap, ctypes.byref(n_ev), ctypes.byref(lit),
+                                     ctypes.byref(mat), ctypes.byref(st))
+        assert rc == 0, rc
+        assert lit.value + mat.value == n  # Sender.java:1325
+
+    for _ in range(a.warmup):
+        step()
+    ctx.sync()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i)
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    gen_ms = float(np.mean([s.elapsed_time(e) for s, e in gen_ev]))
+
+    # ---- spot parity: a few chunks of the device table against the oracle (cheap, every run)
+    import oracle_ctypes as O
+    spot = [0, 1, C // 2, C - 1]
+    hw = d_weak.cpu().numpy()
+    hs = d_strong.cpu().numpy()
+    for k in spot:
+        blk = basis[k * B:min(n, (k + 1) * B)].cpu().numpy()
+        oh = O.header(B, dl, blk.size)
+        ow, os_ = O.generator(blk, oh, bytes([1, 2, 3, 4]))
+        assert int(ow[0]) == int(hw[k]) and os_.tobytes() == hs[k * dl:(k + 1) * dl].tobytes(), f"chunk {k}"
+
+    bytes_step = 2 * n
+    value = world * a.steps * bytes_step / dt / (1 << 30)
+    achieved = n / (gen_ms / 1e3) / 1e9
+    res = {
+        "metric": "GiB/s device-resident rolling+MD5 scan (Generator block sums + Sender match scan)",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 on device)",
+        "config": {
+            "workload": f"config5: {a.size_gib:g} GiB source vs {'50%-modified' if a.variant == 'half' else 'identical'}"
+                        f" basis per GPU, B={B}, dl={dl}",
+            "bytes_per_step_per_gpu": bytes_step,
+            "block_length": B,
+            "digest_length": dl,
+            "chunks": C,
+            "parallelism": f"file-sharded x{world} (no collectives)",
+        },
+        "roofline": {
+            "kernel": "block_sums_kernel (Generator; also the Sender's aligned speculation)",
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel_ms": round(gen_ms, 4),
+            "algorithmic_bytes": n,
+        },
+        "scan": {
+            "events": int(n_ev.value), "literal": int(lit.value), "matched": int(mat.value),
+            "stats": st.as_dict(),
+        },
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(src, basis, B, dl, a.cpu_sample_mib << 20)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(src, basis, B, dl, sample):
+    """The oracle (C restatement of the Java path, 1 core) on a bounded prefix of the same workload."""
+    import oracle_ctypes as O
+    sample = min(sample, src.numel())
+    s = src[:sample].cpu().numpy()
+    b = basis[:sample].cpu().numpy()
+    seed = bytes([1, 2, 3, 4])
+    h = O.header(B, dl, sample)
+    t0 = time.perf_counter()
+    w, st = O.generator(b, h, seed)
+    t1 = time.perf_counter()
+    ev, fm, lit, mat, _ = O.sender(s, h, w, st, seed)
+    t2 = time.perf_counter()
+    return {
+        "value": round(2 * sample / (t2 - t0) / (1 << 30), 4),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"first {sample >> 20} MiB of the same source/basis pair (B={B}, dl={dl}): oracle Generator "
+                  f"{(t1 - t0) * 1e3:.0f} ms + Sender scan incl. file MD5 {(t2 - t1) * 1e3:.0f} ms",
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,136 @@
+/*
+ * rsync_hip.h -- C-ABI of librsynchip.so: java-rsync's delta-transfer checksum path on MI355X (gfx950).
+ *
+ * The reference (alpapad/java-rsync, Java 8) has no native/FFI seam; the seam this library fills is
+ * the two private hot methods and their helpers (paths relative to
+ * core/src/main/java/com/github/java/rsync/internal/):
+ *
+ *   Generator.sendItemizeAndChecksums  session/Generator.java:866-909  -> rsh_block_sums[_device]
+ *   Sender.sendMatchesAndData          session/Sender.java:1235-1327   -> rsh_match_scan[_device]
+ *   Sender.skipMatchSendData           session/Sender.java:1386-1399   -> rsh_match_scan (block_length 0)
+ *   Generator.getBlockLengthFor        session/Generator.java:198-206  -> rsh_block_length_for
+ *   Generator.getDigestLength          session/Generator.java:208-212  -> rsh_digest_length_for
+ *   Checksum.Header(int,int,long)      session/Checksum.java:94-113    -> rsh_header_make
+ *   Checksum.Header(int,int,int,int)   session/Checksum.java:75-92     -> rsh_header_validate
+ *   Sender.sendDataFrom + putInt(...)  session/Sender.java:794-809,1274,1316,1148 -> rsh_tokens_write
+ *
+ * A JNI shim (java-rsync_amd/jni/) binds these for the Java side; see INTEGRATION.md.
+ * Plain pointers and sizes only; the caller owns every host buffer.  One rsh_ctx per calling thread
+ * (the reference runs Generator and Sender on separate threads, RsyncClient.java:431); contexts are
+ * independent and may target different devices (file-parallel sharding).
+ */
+#ifndef RSYNC_HIP_H
+#define RSYNC_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSH_ABI_VERSION 1
+
+/* Status codes (the JNI shim maps them onto the reference's exception types). */
+#define RSH_OK 0
+#define RSH_E_INVAL (-1)    /* bad argument (IllegalArgumentException)                      */
+#define RSH_E_PROTOCOL (-2) /* header fails Checksum.Header 4-arg validation (RsyncProtocolException,
+                               Connection.java:28-38)                                        */
+#define RSH_E_OVERFLOW (-3) /* chunk count > Integer.MAX_VALUE (Checksum.ChunkOverflow, :107-111) */
+#define RSH_E_NOSPACE (-4)  /* event buffer too small; *n_ev holds the count needed          */
+#define RSH_E_DEVICE (-5)   /* HIP runtime / kernel failure, or no gfx950 device present     */
+#define RSH_E_NOMEM (-6)    /* host or device allocation failed                              */
+
+/* Checksum.Header; wire order of Connection.sendChecksumHeader (Connection.java:40-45) is
+ * chunk_count, block_length, digest_length, remainder (4 x little-endian int32). */
+typedef struct {
+    int32_t chunk_count;
+    int32_t block_length;
+    int32_t digest_length;
+    int32_t remainder;
+} rsh_header;
+
+/* One Sender action.  RSH_EV_LITERAL = one sendDataFrom(buf, offset, length) call (length > 0; the
+ * 8 KiB token split happens at replay, Sender.java:794-809).  RSH_EV_MATCH = `count` consecutive
+ * putInt(-(i+1)) for chunks index .. index+count-1, matched at consecutive windows starting at file
+ * offset `offset`; `length` = the bytes those windows add to sizeMatch (Sender.java:1269). */
+enum { RSH_EV_LITERAL = 1, RSH_EV_MATCH = 2 };
+typedef struct {
+    int64_t offset;
+    int64_t length;
+    int32_t kind;
+    int32_t index;
+    int32_t count;
+    int32_t reserved;
+} rsh_event;
+
+/* Per-scan counters (diagnostics; not part of the reference's output). */
+typedef struct {
+    int64_t chain_matches;   /* matches resolved by the aligned speculation fast path          */
+    int64_t events;          /* candidate events the resolver evaluated                       */
+    int64_t probe_launches;  /* range-probe kernel launches                                   */
+    int64_t host_md5_windows;/* single-window digests computed on the host (resolver misses)  */
+    int64_t flushes;         /* FileView.isFull flushes (Sender.java:1294-1302)                */
+    double device_ms;        /* time inside device work (kernels + copies) for this scan      */
+    double resolver_ms;      /* host resolver time                                             */
+} rsh_scan_stats;
+
+typedef struct rsh_ctx rsh_ctx;
+
+int rsh_abi_version(void);
+const char* rsh_strerror(int status);
+int rsh_device_count(int* count);
+int rsh_ctx_create(int device, rsh_ctx** out);
+void rsh_ctx_destroy(rsh_ctx* ctx);
+/* hipStream_t the context launches on (opaque), for callers composing with their own streams. */
+void* rsh_ctx_stream(rsh_ctx* ctx);
+
+/* ---- sizing / header (pure host functions) ---- */
+int32_t rsh_block_length_for(int64_t file_size);                                    /* Generator.java:198-206 */
+int32_t rsh_digest_length_for(int64_t file_size, int32_t block_length, int32_t min_digest_length); /* :208-212,:873 */
+int rsh_header_make(int32_t block_length, int32_t digest_length, int64_t file_size, rsh_header* out);
+int rsh_header_validate(const rsh_header* h);
+
+/* ---- Generator: per-chunk weak + MD5(chunk || seed)[0:digest_length] (Generator.java:886-895) ----
+ * weak_out[chunk_count]; strong_out[chunk_count * digest_length].  Host buffers. */
+int rsh_block_sums(rsh_ctx* ctx, const uint8_t* data, int64_t n, const rsh_header* h, const uint8_t seed[4],
+                   int32_t* weak_out, uint8_t* strong_out);
+/* Device-resident form: d_data, d_weak, d_strong are device pointers; runs on the context stream and
+ * returns after the work is enqueued (rsh_ctx_sync waits). */
+int rsh_block_sums_device(rsh_ctx* ctx, const void* d_data, int64_t n, const rsh_header* h, const uint8_t seed[4],
+                          void* d_weak, void* d_strong);
+int rsh_ctx_sync(rsh_ctx* ctx);
+
+/* ---- Sender (Sender.java:1098-1148 per-file glue, :1235-1327 scan, :1386-1399 new file) ----
+ * h: the header received from the Generator (validated here exactly as Connection.receiveChecksumHeader
+ * does); weak[chunk_count], strong[chunk_count * digest_length]: the received table.
+ * Events are written to ev[0..ev_cap); *n_ev receives the count (RSH_E_NOSPACE if ev_cap is short).
+ * file_md5 = MD5 of the whole source (Sender.java:1241,1326); literal/matched = sizeLiteral/sizeMatch. */
+int rsh_match_scan(rsh_ctx* ctx, const uint8_t* src, int64_t n, const rsh_header* h, const int32_t* weak,
+                   const uint8_t* strong, const uint8_t seed[4], rsh_event* ev, int64_t ev_cap, int64_t* n_ev,
+                   uint8_t file_md5[16], int64_t* literal, int64_t* matched, rsh_scan_stats* stats);
+/* Device-resident form: source and table already in HBM (d_src, d_weak, d_strong).  The serial
+ * whole-file MD5 is not computed here (see rsh_file_md5); everything else is identical. */
+int rsh_match_scan_device(rsh_ctx* ctx, const void* d_src, int64_t n, const rsh_header* h, const void* d_weak,
+                          const void* d_strong, const uint8_t seed[4], rsh_event* ev, int64_t ev_cap,
+                          int64_t* n_ev, int64_t* literal, int64_t* matched, rsh_scan_stats* stats);
+
+/* Whole-file MD5 on the host (one serial chain; runs beside the device work). */
+int rsh_file_md5(const uint8_t* data, int64_t n, uint8_t out[16]);
+
+/* ---- channel bytes ----
+ * Exact bytes Sender writes for one file: per literal event the 8 KiB-split putInt(len)+bytes tokens,
+ * per matched chunk putInt(-(index+1)), then putInt(0) and the 16-byte file MD5. */
+int64_t rsh_tokens_size(const rsh_event* ev, int64_t n_ev);
+int rsh_tokens_write(const uint8_t* src, const rsh_event* ev, int64_t n_ev, const uint8_t file_md5[16],
+                     uint8_t* out, int64_t cap);
+/* Generator channel bytes: header + per chunk putInt(weak) + digest_length bytes. */
+int64_t rsh_generator_bytes(const rsh_header* h, const int32_t* weak, const uint8_t* strong, uint8_t* out,
+                            int64_t cap);
+
+/* ---- synthetic input for benchmarks: splitmix64 counter stream generated on the device ---- */
+int rsh_fill_splitmix_device(rsh_ctx* ctx, void* d_out, int64_t n, uint64_t key, int64_t byte_offset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

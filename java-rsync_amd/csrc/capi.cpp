@@ -1,0 +1,552 @@
+// capi.cpp -- the C-ABI of include/rsync_hip.h: contexts, device memory, the HIP scan backend and the
+// host-side glue that mirrors Generator.sendItemizeAndChecksums / Sender.sendFiles per-file handling.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <thread>
+#include <vector>
+
+#include "device.h"
+#include "host_md5.h"
+#include "resolver.h"
+#include "rsync_hip.h"
+
+namespace {
+
+constexpr int64_t kChunkSize = 8192;        // Sender.java:230 CHUNK_SIZE
+constexpr int64_t kDefaultBlock = 8192;     // FileView.java:38 DEFAULT_BLOCK_SIZE
+constexpr int32_t kMaxBlockLength = 1 << 17;  // Checksum.java:151
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, n ? n : 1);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+uint32_t seed_word(const uint8_t seed[4]) {
+    return (uint32_t)seed[0] | ((uint32_t)seed[1] << 8) | ((uint32_t)seed[2] << 16) | ((uint32_t)seed[3] << 24);
+}
+
+uint32_t pow2_at_least(uint64_t v) {
+    uint32_t p = 64;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace
+
+struct rsh_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf data, weak, strong;                   // host-input staging
+    DevBuf src_weak, src_strong, flags;          // aligned speculation over the source
+    DevBuf slots, dslots, dkeys, pos, out, first, win;
+    ~rsh_ctx() {
+        for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &slots, &dslots, &dkeys, &pos, &out,
+                          &first, &win})
+            b->release();
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+#define RSH_HIP(call)                                   \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return RSH_E_DEVICE;      \
+    } while (0)
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// HIP implementation of the resolver's services.
+// ------------------------------------------------------------------------------------------------
+class HipBackend : public rsh::ScanBackend {
+  public:
+    HipBackend(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh::ChunkTable& t, const uint8_t seed[4])
+        : c_(c), x_(d_src), n_(n), t_(t), B_(t.block_length), dl_(t.digest_length) {
+        memcpy(seed_, seed, 4);
+    }
+    hipError_t err = hipSuccess;
+    std::vector<int32_t> aw;
+    std::vector<uint8_t> as;
+    std::vector<uint8_t> fl;
+    rsh::ProbeTable table{};
+
+    int64_t aligned_count() override { return (int64_t)aw.size(); }
+    const int32_t* aligned_weak() override { return aw.data(); }
+    const uint8_t* aligned_strong() override { return as.data(); }
+    const uint8_t* chain_flags() override { return fl.data(); }
+
+    int32_t weak_at(int64_t p) override {
+        int32_t r = 0;
+        ok(c_->pos.ensure(sizeof(int64_t)));
+        ok(c_->out.ensure(sizeof(int32_t)));
+        ok(hipMemcpyAsync(c_->pos.p, &p, sizeof(p), hipMemcpyHostToDevice, c_->stream));
+        ok(rsh::launch_window_weak(x_, n_, (uint32_t)B_, c_->pos.as<int64_t>(), 1, c_->out.as<int32_t>(), c_->stream));
+        ok(hipMemcpyAsync(&r, c_->out.p, sizeof(r), hipMemcpyDeviceToHost, c_->stream));
+        ok(hipStreamSynchronize(c_->stream));
+        return r;
+    }
+    // A single window's digest is one serial MD5 chain: 64-wide waves give it nothing, so the rare
+    // resolver misses (first table hit after a reset) are digested on the host from a D2H copy.
+    void md5_at(int64_t p, uint8_t out[16]) override {
+        const int64_t w = std::min<int64_t>(B_, n_ - p);
+        win_.resize((size_t)w);
+        ok(hipMemcpyAsync(win_.data(), x_ + p, (size_t)w, hipMemcpyDeviceToHost, c_->stream));
+        ok(hipStreamSynchronize(c_->stream));
+        rsh::HostMd5 h;
+        h.update(win_.data(), (size_t)w);
+        h.update(seed_, 4);
+        h.final(out);
+    }
+    uint8_t byte_at(int64_t p) override {
+        uint8_t b = 0;
+        ok(hipMemcpyAsync(&b, x_ + p, 1, hipMemcpyDeviceToHost, c_->stream));
+        ok(hipStreamSynchronize(c_->stream));
+        return b;
+    }
+    int64_t first_hit(int64_t a, int64_t b, int64_t anchor, uint32_t e_lo, uint32_t e_hi,
+                      const std::vector<int32_t>* keys) override {
+        rsh::ProbeTable tab = table;
+        if (keys) {
+            const uint32_t ns = pow2_at_least(2 * keys->size() + 2);
+            ok(c_->dslots.ensure(ns * sizeof(unsigned long long)));
+            ok(c_->dkeys.ensure((keys->size() + 1) * sizeof(int32_t)));
+            if (!keys->empty())
+                ok(hipMemcpyAsync(c_->dkeys.p, keys->data(), keys->size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                                  c_->stream));
+            ok(rsh::launch_table_clear(c_->dslots.as<unsigned long long>(), ns, c_->stream));
+            ok(rsh::launch_table_insert(c_->dslots.as<unsigned long long>(), ns - 1, c_->dkeys.as<int32_t>(),
+                                        (uint32_t)keys->size(), c_->stream));
+            tab.slots = c_->dslots.as<unsigned long long>();
+            tab.mask = ns - 1;
+        }
+        ok(c_->first.ensure(sizeof(unsigned long long)));
+        rsh::ProbeArgs A;
+        A.data = x_;
+        A.n = n_;
+        A.B = (uint32_t)B_;
+        A.a = a;
+        A.b = b;
+        A.anchor = anchor;
+        A.e_lo = e_lo & 0xFFFFu;
+        A.e_hi = e_hi & 0xFFFFu;
+        A.aligned_weak = c_->src_weak.as<int32_t>();
+        A.table = tab;
+        A.first = c_->first.as<unsigned long long>();
+        ok(rsh::launch_probe_first(A, c_->stream));
+        unsigned long long r = ~0ull;
+        ok(hipMemcpyAsync(&r, c_->first.p, sizeof(r), hipMemcpyDeviceToHost, c_->stream));
+        ok(hipStreamSynchronize(c_->stream));
+        return r == ~0ull ? -1 : (int64_t)r;
+    }
+
+  private:
+    void ok(hipError_t e) {
+        if (e != hipSuccess && err == hipSuccess) err = e;
+    }
+    rsh_ctx* c_;
+    const uint8_t* x_;
+    int64_t n_;
+    const rsh::ChunkTable& t_;
+    int64_t B_;
+    int dl_;
+    uint8_t seed_[4];
+    std::vector<uint8_t> win_;
+};
+
+// Header consistency for the Generator side (3-arg ctor semantics, Checksum.java:94-113).
+int check_generator_header(int64_t n, const rsh_header* h) {
+    if (!h || n < 0) return RSH_E_INVAL;
+    if (h->block_length == 0) return (h->chunk_count == 0) ? RSH_OK : RSH_E_INVAL;
+    if (h->block_length < 0 || h->digest_length < 0 || h->digest_length > 16) return RSH_E_INVAL;
+    const int64_t B = h->block_length;
+    const int64_t rem = n % B;
+    const int64_t cc = n / B + (rem > 0 ? 1 : 0);
+    if (cc > 2147483647LL) return RSH_E_OVERFLOW;
+    if (cc != h->chunk_count || rem != h->remainder) return RSH_E_INVAL;
+    return RSH_OK;
+}
+
+// The device-resident Sender scan (everything but the whole-file MD5).  h validated by the caller;
+// n > 0, block_length > 0.  host_weak/host_strong may be null (then copied back from the device).
+int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h, const int32_t* d_weak,
+                const uint8_t* d_strong, const int32_t* host_weak, const uint8_t* host_strong, const uint8_t seed[4],
+                rsh::ResolveResult* res) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t B = h->block_length;
+    const int32_t C = h->chunk_count;
+    const int32_t dl = h->digest_length;
+    std::vector<int32_t> hw;
+    std::vector<uint8_t> hs;
+    if (!host_weak || !host_strong) {
+        hw.resize(C > 0 ? C : 1);
+        hs.resize((size_t)C * dl + 1);
+        if (C > 0) {
+            RSH_HIP(hipMemcpyAsync(hw.data(), d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, c->stream));
+            if (dl > 0)
+                RSH_HIP(hipMemcpyAsync(hs.data(), d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, c->stream));
+        }
+        host_weak = hw.data();
+        host_strong = hs.data();
+    }
+    rsh::ChunkTable table;
+    table.chunk_count = C;
+    table.block_length = (int32_t)B;
+    table.remainder = h->remainder;
+    table.digest_length = dl;
+    table.weak = host_weak;
+    table.strong = host_strong;
+
+    // device probe table over the basis weak keys
+    const uint32_t ns = pow2_at_least(2 * (uint64_t)C + 2);
+    RSH_HIP(c->slots.ensure((size_t)ns * sizeof(unsigned long long)));
+    RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, c->stream));
+    RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, c->stream));
+
+    // aligned speculation: the source's own block sums with the basis header's B and dl
+    const int64_t na = (n + B - 1) / B;
+    if (na > 2147483647LL) return RSH_E_OVERFLOW;
+    RSH_HIP(c->src_weak.ensure((size_t)na * 4));
+    RSH_HIP(c->src_strong.ensure((size_t)na * dl + 1));
+    RSH_HIP(rsh::launch_block_sums(d_src, n, (uint32_t)B, (uint32_t)na, (uint32_t)dl, seed_word(seed),
+                                   c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->stream));
+    const int64_t nf = std::min<int64_t>(na, C);
+    RSH_HIP(c->flags.ensure((size_t)nf + 1));
+    RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
+                                    (uint32_t)nf, (uint32_t)dl, c->flags.as<uint8_t>(), c->stream));
+
+    HipBackend be(c, d_src, n, table, seed);
+    be.table.slots = c->slots.as<unsigned long long>();
+    be.table.mask = ns - 1;
+    be.aw.resize((size_t)na);
+    be.as.resize((size_t)na * dl + 1);
+    be.fl.resize((size_t)nf + 1);
+    RSH_HIP(hipMemcpyAsync(be.aw.data(), c->src_weak.p, (size_t)na * 4, hipMemcpyDeviceToHost, c->stream));
+    if (dl > 0)
+        RSH_HIP(hipMemcpyAsync(be.as.data(), c->src_strong.p, (size_t)na * dl, hipMemcpyDeviceToHost, c->stream));
+    if (nf > 0) RSH_HIP(hipMemcpyAsync(be.fl.data(), c->flags.p, (size_t)nf, hipMemcpyDeviceToHost, c->stream));
+    table.build();  // host radix sort overlaps the device work above
+    RSH_HIP(hipStreamSynchronize(c->stream));
+    const double dev_ms = ms_since(t0);
+
+    rsh::resolve_scan(n, table, be, res);
+    if (be.err != hipSuccess) return RSH_E_DEVICE;
+    res->stats.device_ms += dev_ms;
+    return RSH_OK;
+}
+
+int emit_events(const rsh::ResolveResult& r, rsh_event* ev, int64_t cap, int64_t* n_ev) {
+    *n_ev = (int64_t)r.ev.size();
+    if ((int64_t)r.ev.size() > cap || (!ev && !r.ev.empty())) return RSH_E_NOSPACE;
+    if (!r.ev.empty()) memcpy(ev, r.ev.data(), r.ev.size() * sizeof(rsh_event));
+    return RSH_OK;
+}
+
+// Sender.skipMatchSendData (Sender.java:1386-1399): one sendDataFrom per 8 KiB FileView window.
+void skip_events(int64_t n, rsh::ResolveResult* r) {
+    for (int64_t s = 0; s < n; s += kDefaultBlock)
+        r->ev.push_back(rsh_event{s, std::min<int64_t>(kDefaultBlock, n - s), RSH_EV_LITERAL, 0, 0, 0});
+    r->literal = n;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rsh_abi_version(void) { return RSH_ABI_VERSION; }
+
+const char* rsh_strerror(int status) {
+    switch (status) {
+        case RSH_OK: return "ok";
+        case RSH_E_INVAL: return "invalid argument";
+        case RSH_E_PROTOCOL: return "checksum header rejected (RsyncProtocolException)";
+        case RSH_E_OVERFLOW: return "chunk count is negative or greater than int max (ChunkOverflow)";
+        case RSH_E_NOSPACE: return "event buffer too small";
+        case RSH_E_DEVICE: return "HIP device error or no gfx950 device";
+        case RSH_E_NOMEM: return "out of memory";
+        default: return "unknown status";
+    }
+}
+
+int rsh_device_count(int* count) {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    if (count) *count = c;
+    return c > 0 ? RSH_OK : RSH_E_DEVICE;
+}
+
+int rsh_ctx_create(int device, rsh_ctx** out) {
+    if (!out) return RSH_E_INVAL;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return RSH_E_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return RSH_E_DEVICE;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return RSH_E_DEVICE;  // kernels are built for gfx950 only
+    RSH_HIP(hipSetDevice(device));
+    rsh_ctx* c = new (std::nothrow) rsh_ctx();
+    if (!c) return RSH_E_NOMEM;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return RSH_E_DEVICE;
+    }
+    *out = c;
+    return RSH_OK;
+}
+
+void rsh_ctx_destroy(rsh_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    delete ctx;
+}
+
+void* rsh_ctx_stream(rsh_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int rsh_ctx_sync(rsh_ctx* ctx) {
+    if (!ctx) return RSH_E_INVAL;
+    RSH_HIP(hipSetDevice(ctx->device));
+    RSH_HIP(hipStreamSynchronize(ctx->stream));
+    return RSH_OK;
+}
+
+// Generator.getBlockLengthFor / pow2SquareRoot (Generator.java:198-206, 219-236).
+int32_t rsh_block_length_for(int64_t file_size) {
+    if (file_size <= 0) return 0;
+    const int exponent = 63 - __builtin_clzll((unsigned long long)file_size);
+    const int32_t bl = (int32_t)(1u << (exponent / 2));
+    return bl > 512 ? bl : 512;  // MIN_BLOCK_SIZE (:186)
+}
+
+// Generator.getDigestLength (:208-212) with Util.log2 = Math.log(n) / Math.log(2) (Util.java:128-130),
+// then max(minDigestLength, ...) (:873).
+int32_t rsh_digest_length_for(int64_t file_size, int32_t block_length, int32_t min_digest_length) {
+    if (file_size <= 0) return 0;  // Generator.java:873: digestLength 0 for an empty file
+    const int64_t lf = (int64_t)(__builtin_log((double)file_size) / __builtin_log(2.0));
+    const int64_t lb = (int64_t)(__builtin_log((double)block_length) / __builtin_log(2.0));
+    int32_t r = ((int32_t)(10 + 2 * lf - lb) - 24) / 8;
+    r = std::min(r, 16);
+    r = std::max(r, 2);
+    return std::max(r, min_digest_length);
+}
+
+int rsh_header_make(int32_t block_length, int32_t digest_length, int64_t file_size, rsh_header* out) {
+    if (!out || block_length < 0 || file_size < 0) return RSH_E_INVAL;
+    if (block_length == 0) {
+        *out = rsh_header{0, 0, 0, 0};
+        return RSH_OK;
+    }
+    const int64_t rem = file_size % block_length;
+    const int64_t cc = file_size / block_length + (rem > 0 ? 1 : 0);
+    if (cc > 2147483647LL) return RSH_E_OVERFLOW;
+    *out = rsh_header{(int32_t)cc, block_length, digest_length, (int32_t)rem};
+    return RSH_OK;
+}
+
+// Checksum.Header 4-arg ctor (Checksum.java:75-92); IllegalArgumentException -> RsyncProtocolException
+// in Connection.receiveChecksumHeader (Connection.java:28-38).
+int rsh_header_validate(const rsh_header* h) {
+    if (!h) return RSH_E_INVAL;
+    if (h->chunk_count < 0) return RSH_E_PROTOCOL;
+    if (h->block_length == 0 && h->chunk_count > 0) return RSH_E_PROTOCOL;
+    if (h->block_length < 0 || h->block_length > kMaxBlockLength) return RSH_E_PROTOCOL;
+    if (h->remainder < 0 || h->remainder > h->block_length) return RSH_E_PROTOCOL;
+    if (h->digest_length < 0) return RSH_E_PROTOCOL;
+    return RSH_OK;
+}
+
+int rsh_block_sums_device(rsh_ctx* ctx, const void* d_data, int64_t n, const rsh_header* h, const uint8_t seed[4],
+                          void* d_weak, void* d_strong) {
+    if (!ctx || !seed) return RSH_E_INVAL;
+    const int rc = check_generator_header(n, h);
+    if (rc != RSH_OK) return rc;
+    if (h->chunk_count == 0) return RSH_OK;
+    if (!d_data || !d_weak || (!d_strong && h->digest_length > 0)) return RSH_E_INVAL;
+    RSH_HIP(hipSetDevice(ctx->device));
+    RSH_HIP(rsh::launch_block_sums(static_cast<const uint8_t*>(d_data), n, (uint32_t)h->block_length,
+                                   (uint32_t)h->chunk_count, (uint32_t)h->digest_length, seed_word(seed),
+                                   static_cast<int32_t*>(d_weak), static_cast<uint8_t*>(d_strong), ctx->stream));
+    return RSH_OK;
+}
+
+int rsh_block_sums(rsh_ctx* ctx, const uint8_t* data, int64_t n, const rsh_header* h, const uint8_t seed[4],
+                   int32_t* weak_out, uint8_t* strong_out) {
+    if (!ctx || !seed) return RSH_E_INVAL;
+    const int rc = check_generator_header(n, h);
+    if (rc != RSH_OK) return rc;
+    if (h->chunk_count == 0) return RSH_OK;
+    if (!data || !weak_out || (!strong_out && h->digest_length > 0)) return RSH_E_INVAL;
+    RSH_HIP(hipSetDevice(ctx->device));
+    const size_t C = (size_t)h->chunk_count, dl = (size_t)h->digest_length;
+    RSH_HIP(ctx->data.ensure((size_t)n));
+    RSH_HIP(ctx->weak.ensure(C * 4));
+    RSH_HIP(ctx->strong.ensure(C * dl + 1));
+    RSH_HIP(hipMemcpyAsync(ctx->data.p, data, (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    const int r2 = rsh_block_sums_device(ctx, ctx->data.p, n, h, seed, ctx->weak.p, ctx->strong.p);
+    if (r2 != RSH_OK) return r2;
+    RSH_HIP(hipMemcpyAsync(weak_out, ctx->weak.p, C * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (dl) RSH_HIP(hipMemcpyAsync(strong_out, ctx->strong.p, C * dl, hipMemcpyDeviceToHost, ctx->stream));
+    RSH_HIP(hipStreamSynchronize(ctx->stream));
+    return RSH_OK;
+}
+
+int rsh_match_scan_device(rsh_ctx* ctx, const void* d_src, int64_t n, const rsh_header* h, const void* d_weak,
+                          const void* d_strong, const uint8_t seed[4], rsh_event* ev, int64_t ev_cap,
+                          int64_t* n_ev, int64_t* literal, int64_t* matched, rsh_scan_stats* stats) {
+    if (!ctx || !h || !seed || !n_ev || n < 0) return RSH_E_INVAL;
+    const int v = rsh_header_validate(h);
+    if (v != RSH_OK) return v;
+    RSH_HIP(hipSetDevice(ctx->device));
+    rsh::ResolveResult r;
+    if (h->block_length == 0) {
+        skip_events(n, &r);
+    } else if (n > 0) {
+        if (!d_src || (h->chunk_count > 0 && (!d_weak || (!d_strong && h->digest_length > 0)))) return RSH_E_INVAL;
+        const int rc = scan_device(ctx, static_cast<const uint8_t*>(d_src), n, h, static_cast<const int32_t*>(d_weak),
+                                   static_cast<const uint8_t*>(d_strong), nullptr, nullptr, seed, &r);
+        if (rc != RSH_OK) return rc;
+    }
+    if (literal) *literal = r.literal;
+    if (matched) *matched = r.matched;
+    if (stats) *stats = r.stats;
+    return emit_events(r, ev, ev_cap, n_ev);
+}
+
+int rsh_match_scan(rsh_ctx* ctx, const uint8_t* src, int64_t n, const rsh_header* h, const int32_t* weak,
+                   const uint8_t* strong, const uint8_t seed[4], rsh_event* ev, int64_t ev_cap, int64_t* n_ev,
+                   uint8_t file_md5[16], int64_t* literal, int64_t* matched, rsh_scan_stats* stats) {
+    if (!ctx || !h || !seed || !n_ev || !file_md5 || n < 0 || (n > 0 && !src)) return RSH_E_INVAL;
+    const int v = rsh_header_validate(h);
+    if (v != RSH_OK) return v;
+    RSH_HIP(hipSetDevice(ctx->device));
+    // the whole-file digest (Sender.java:1241,1326) is one serial chain: host thread, beside the device
+    std::thread md5_thread([&] {
+        rsh::HostMd5 m;
+        if (n > 0) m.update(src, (size_t)n);
+        m.final(file_md5);
+    });
+    rsh::ResolveResult r;
+    int rc = RSH_OK;
+    if (h->block_length == 0) {
+        skip_events(n, &r);
+    } else if (n > 0) {
+        const size_t C = (size_t)h->chunk_count, dl = (size_t)h->digest_length;
+        if (C > 0 && (!weak || (!strong && dl > 0))) rc = RSH_E_INVAL;
+        if (rc == RSH_OK && (ctx->data.ensure((size_t)n) != hipSuccess || ctx->weak.ensure(C * 4 + 4) != hipSuccess ||
+                             ctx->strong.ensure(C * dl + 1) != hipSuccess))
+            rc = RSH_E_NOMEM;
+        if (rc == RSH_OK) {
+            bool okc = hipMemcpyAsync(ctx->data.p, src, (size_t)n, hipMemcpyHostToDevice, ctx->stream) == hipSuccess;
+            if (C) okc = okc && hipMemcpyAsync(ctx->weak.p, weak, C * 4, hipMemcpyHostToDevice, ctx->stream) == hipSuccess;
+            if (C && dl)
+                okc = okc && hipMemcpyAsync(ctx->strong.p, strong, C * dl, hipMemcpyHostToDevice, ctx->stream) == hipSuccess;
+            rc = okc ? scan_device(ctx, ctx->data.as<uint8_t>(), n, h, ctx->weak.as<int32_t>(), ctx->strong.as<uint8_t>(),
+                                   weak, strong, seed, &r)
+                     : RSH_E_DEVICE;
+        }
+    }
+    md5_thread.join();
+    if (rc != RSH_OK) return rc;
+    if (literal) *literal = r.literal;
+    if (matched) *matched = r.matched;
+    if (stats) *stats = r.stats;
+    return emit_events(r, ev, ev_cap, n_ev);
+}
+
+int rsh_file_md5(const uint8_t* data, int64_t n, uint8_t out[16]) {
+    if (!out || n < 0 || (n > 0 && !data)) return RSH_E_INVAL;
+    rsh::HostMd5 m;
+    if (n > 0) m.update(data, (size_t)n);
+    m.final(out);
+    return RSH_OK;
+}
+
+int64_t rsh_tokens_size(const rsh_event* ev, int64_t n_ev) {
+    int64_t size = 4 + 16;  // putInt(0) + file MD5
+    for (int64_t i = 0; i < n_ev; ++i) {
+        if (ev[i].kind == RSH_EV_LITERAL) size += ev[i].length + 4 * ((ev[i].length + kChunkSize - 1) / kChunkSize);
+        else size += 4 * (int64_t)ev[i].count;
+    }
+    return size;
+}
+
+static inline uint8_t* put_int(uint8_t* o, int32_t v) {  // BufferedOutputChannel is little-endian (:50)
+    for (int i = 0; i < 4; ++i) o[i] = (uint8_t)((uint32_t)v >> (8 * i));
+    return o + 4;
+}
+
+int rsh_tokens_write(const uint8_t* src, const rsh_event* ev, int64_t n_ev, const uint8_t file_md5[16], uint8_t* out,
+                     int64_t cap) {
+    if (!out || !file_md5 || (n_ev > 0 && !ev)) return RSH_E_INVAL;
+    if (rsh_tokens_size(ev, n_ev) > cap) return RSH_E_NOSPACE;
+    uint8_t* o = out;
+    for (int64_t i = 0; i < n_ev; ++i) {
+        if (ev[i].kind == RSH_EV_LITERAL) {  // Sender.sendDataFrom (:794-809)
+            if (!src) return RSH_E_INVAL;
+            for (int64_t cur = ev[i].offset, end = ev[i].offset + ev[i].length; cur < end;) {
+                const int64_t len = std::min<int64_t>(kChunkSize, end - cur);
+                o = put_int(o, (int32_t)len);
+                memcpy(o, src + cur, (size_t)len);
+                o += len;
+                cur += len;
+            }
+        } else {
+            for (int32_t j = 0; j < ev[i].count; ++j) o = put_int(o, -(ev[i].index + j + 1));  // :1274
+        }
+    }
+    o = put_int(o, 0);          // :1316
+    memcpy(o, file_md5, 16);    // sendFiles :1148
+    return RSH_OK;
+}
+
+int64_t rsh_generator_bytes(const rsh_header* h, const int32_t* weak, const uint8_t* strong, uint8_t* out, int64_t cap) {
+    if (!h) return RSH_E_INVAL;
+    const int64_t size = 16 + (int64_t)h->chunk_count * (4 + h->digest_length);
+    if (!out) return size;
+    if (cap < size || (h->chunk_count > 0 && (!weak || (!strong && h->digest_length > 0)))) return RSH_E_NOSPACE;
+    uint8_t* o = out;
+    o = put_int(o, h->chunk_count);  // Connection.sendChecksumHeader (Connection.java:40-45)
+    o = put_int(o, h->block_length);
+    o = put_int(o, h->digest_length);
+    o = put_int(o, h->remainder);
+    for (int32_t i = 0; i < h->chunk_count; ++i) {  // Generator.java:890-893
+        o = put_int(o, weak[i]);
+        memcpy(o, strong + (int64_t)i * h->digest_length, (size_t)h->digest_length);
+        o += h->digest_length;
+    }
+    return size;
+}
+
+int rsh_fill_splitmix_device(rsh_ctx* ctx, void* d_out, int64_t n, uint64_t key, int64_t byte_offset) {
+    if (!ctx || (n > 0 && !d_out) || n < 0 || byte_offset < 0) return RSH_E_INVAL;
+    RSH_HIP(hipSetDevice(ctx->device));
+    RSH_HIP(rsh::launch_fill_splitmix(static_cast<uint8_t*>(d_out), n, key, byte_offset, ctx->stream));
+    return RSH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,53 @@
+// device.h -- internal launchers for the gfx950 kernels in device.hip (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsh {
+
+// Generator block sums (Generator.java:886-895): chunk c covers [c*B, min((c+1)*B, n)).
+// Writes weak[c] and strong[c*dl .. c*dl+dl).  Also used by the Sender as aligned speculation.
+hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks, uint32_t dl,
+                             uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s);
+
+// Chain flags for the Sender fast path: flag[k] = 1 iff source window k (aligned, from the source's
+// own block sums) has the same weak key and the same dl-byte digest as basis chunk k.
+hipError_t launch_chain_flags(const int32_t* d_wsrc, const uint8_t* d_ssrc, const int32_t* d_wbas,
+                              const uint8_t* d_sbas, uint32_t count, uint32_t dl, uint8_t* d_flags,
+                              hipStream_t s);
+
+// Probe table: open-addressing hash of the distinct weak keys (key -> 1).  slots = power of two.
+struct ProbeTable {
+    const unsigned long long* slots;
+    uint32_t mask;
+};
+hipError_t launch_table_clear(unsigned long long* d_slots, uint32_t nslots, hipStream_t s);
+hipError_t launch_table_insert(unsigned long long* d_slots, uint32_t mask, const int32_t* d_keys, uint32_t nkeys,
+                               hipStream_t s);
+
+// First position p in [a, b) whose Sender-side rolling key R(p) = T(p) + E(p) is in the table, where
+// T(p) is the true weak sum of window [p, p + min(B, n - p)) and E(p) = (e_lo, e_hi + e_lo * (min(p, n-B) -
+// min(anchor, n-B))) mod 2^16 (the post-flush desync of Sender.java:1292-1310).  aligned_weak[k] = T(k*B)
+// (the source's own block sums).  *d_first (int64, preset to INT64_MAX by the launcher) receives the
+// position.  Positions are processed in aligned blocks of B; work per launch is O(b - a + B).
+struct ProbeArgs {
+    const uint8_t* data;
+    int64_t n;
+    uint32_t B;
+    int64_t a, b;
+    int64_t anchor;
+    uint32_t e_lo, e_hi;
+    const int32_t* aligned_weak;
+    ProbeTable table;
+    unsigned long long* first;
+};
+hipError_t launch_probe_first(const ProbeArgs& args, hipStream_t s);
+
+// True weak sums at arbitrary positions: out[i] = Rolling.compute(data + pos[i], min(B, n - pos[i])).
+hipError_t launch_window_weak(const uint8_t* d_data, int64_t n, uint32_t B, const int64_t* d_pos, uint32_t npos,
+                              int32_t* d_out, hipStream_t s);
+
+// splitmix64 counter stream (bench input): byte i = byte (i % 8) of mix(key + (i / 8 + 1) * golden).
+hipError_t launch_fill_splitmix(uint8_t* d_out, int64_t n, uint64_t key, int64_t byte_offset, hipStream_t s);
+
+}  // namespace rsh

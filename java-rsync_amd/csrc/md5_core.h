@@ -1,0 +1,117 @@
+// md5_core.h -- MD5 compression (RFC 1321) and the rsync weak-sum block update, shared by the gfx950
+// kernels (one lane = one message) and the host side (whole-file digest, single resolver windows).
+//
+// The reference's strong checksum is java.security.MessageDigest("MD5") (util/MD5.java:35-41) over
+// block || seed4 truncated to the digest length (Generator.java:891-893, Sender.java:1260-1262).
+// The weak sum is Rolling.compute (util/Rolling.java:31-46) over signed bytes, CHAR_OFFSET = 0.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define RSH_HD __host__ __device__ __forceinline__
+#else
+#define RSH_HD static inline
+#endif
+
+namespace rsh {
+
+struct Md5State {
+    uint32_t a, b, c, d;
+};
+
+RSH_HD Md5State md5_init() { return Md5State{0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u}; }
+
+RSH_HD uint32_t rotl32(uint32_t x, int s) { return (x << s) | (x >> (32 - s)); }
+
+// Round functions in the forms the gfx950 backend turns into one v_bfi_b32 / v_xor3_b32 each.
+#define RSH_MD5_F(x, y, z) ((z) ^ ((x) & ((y) ^ (z))))
+#define RSH_MD5_G(x, y, z) ((y) ^ ((z) & ((x) ^ (y))))
+#define RSH_MD5_H(x, y, z) ((x) ^ (y) ^ (z))
+#define RSH_MD5_I(x, y, z) ((y) ^ ((x) | ~(z)))
+#define RSH_MD5_STEP(f, a, b, c, d, m, k, s) (a) = (b) + rsh::rotl32((a) + f((b), (c), (d)) + (m) + (k), (s))
+
+// One 64-byte block; m[0..15] are the little-endian message words.
+RSH_HD void md5_compress(Md5State& st, const uint32_t (&m)[16]) {
+    uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
+    RSH_MD5_STEP(RSH_MD5_F, a, b, c, d, m[0], 0xd76aa478u, 7);
+    RSH_MD5_STEP(RSH_MD5_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
+    RSH_MD5_STEP(RSH_MD5_F, c, d, a, b, m[2], 0x242070dbu, 17);
+    RSH_MD5_STEP(RSH_MD5_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
+    RSH_MD5_STEP(RSH_MD5_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
+    RSH_MD5_STEP(RSH_MD5_F, d, a, b, c, m[5], 0x4787c62au, 12);
+    RSH_MD5_STEP(RSH_MD5_F, c, d, a, b, m[6], 0xa8304613u, 17);
+    RSH_MD5_STEP(RSH_MD5_F, b, c, d, a, m[7], 0xfd469501u, 22);
+    RSH_MD5_STEP(RSH_MD5_F, a, b, c, d, m[8], 0x698098d8u, 7);
+    RSH_MD5_STEP(RSH_MD5_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
+    RSH_MD5_STEP(RSH_MD5_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
+    RSH_MD5_STEP(RSH_MD5_F, b, c, d, a, m[11], 0x895cd7beu, 22);
+    RSH_MD5_STEP(RSH_MD5_F, a, b, c, d, m[12], 0x6b901122u, 7);
+    RSH_MD5_STEP(RSH_MD5_F, d, a, b, c, m[13], 0xfd987193u, 12);
+    RSH_MD5_STEP(RSH_MD5_F, c, d, a, b, m[14], 0xa679438eu, 17);
+    RSH_MD5_STEP(RSH_MD5_F, b, c, d, a, m[15], 0x49b40821u, 22);
+
+    RSH_MD5_STEP(RSH_MD5_G, a, b, c, d, m[1], 0xf61e2562u, 5);
+    RSH_MD5_STEP(RSH_MD5_G, d, a, b, c, m[6], 0xc040b340u, 9);
+    RSH_MD5_STEP(RSH_MD5_G, c, d, a, b, m[11], 0x265e5a51u, 14);
+    RSH_MD5_STEP(RSH_MD5_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
+    RSH_MD5_STEP(RSH_MD5_G, a, b, c, d, m[5], 0xd62f105du, 5);
+    RSH_MD5_STEP(RSH_MD5_G, d, a, b, c, m[10], 0x02441453u, 9);
+    RSH_MD5_STEP(RSH_MD5_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
+    RSH_MD5_STEP(RSH_MD5_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+    RSH_MD5_STEP(RSH_MD5_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
+    RSH_MD5_STEP(RSH_MD5_G, d, a, b, c, m[14], 0xc33707d6u, 9);
+    RSH_MD5_STEP(RSH_MD5_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
+    RSH_MD5_STEP(RSH_MD5_G, b, c, d, a, m[8], 0x455a14edu, 20);
+    RSH_MD5_STEP(RSH_MD5_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
+    RSH_MD5_STEP(RSH_MD5_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
+    RSH_MD5_STEP(RSH_MD5_G, c, d, a, b, m[7], 0x676f02d9u, 14);
+    RSH_MD5_STEP(RSH_MD5_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
+
+    RSH_MD5_STEP(RSH_MD5_H, a, b, c, d, m[5], 0xfffa3942u, 4);
+    RSH_MD5_STEP(RSH_MD5_H, d, a, b, c, m[8], 0x8771f681u, 11);
+    RSH_MD5_STEP(RSH_MD5_H, c, d, a, b, m[11], 0x6d9d6122u, 16);
+    RSH_MD5_STEP(RSH_MD5_H, b, c, d, a, m[14], 0xfde5380cu, 23);
+    RSH_MD5_STEP(RSH_MD5_H, a, b, c, d, m[1], 0xa4beea44u, 4);
+    RSH_MD5_STEP(RSH_MD5_H, d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    RSH_MD5_STEP(RSH_MD5_H, c, d, a, b, m[7], 0xf6bb4b60u, 16);
+    RSH_MD5_STEP(RSH_MD5_H, b, c, d, a, m[10], 0xbebfbc70u, 23);
+    RSH_MD5_STEP(RSH_MD5_H, a, b, c, d, m[13], 0x289b7ec6u, 4);
+    RSH_MD5_STEP(RSH_MD5_H, d, a, b, c, m[0], 0xeaa127fau, 11);
+    RSH_MD5_STEP(RSH_MD5_H, c, d, a, b, m[3], 0xd4ef3085u, 16);
+    RSH_MD5_STEP(RSH_MD5_H, b, c, d, a, m[6], 0x04881d05u, 23);
+    RSH_MD5_STEP(RSH_MD5_H, a, b, c, d, m[9], 0xd9d4d039u, 4);
+    RSH_MD5_STEP(RSH_MD5_H, d, a, b, c, m[12], 0xe6db99e5u, 11);
+    RSH_MD5_STEP(RSH_MD5_H, c, d, a, b, m[15], 0x1fa27cf8u, 16);
+    RSH_MD5_STEP(RSH_MD5_H, b, c, d, a, m[2], 0xc4ac5665u, 23);
+
+    RSH_MD5_STEP(RSH_MD5_I, a, b, c, d, m[0], 0xf4292244u, 6);
+    RSH_MD5_STEP(RSH_MD5_I, d, a, b, c, m[7], 0x432aff97u, 10);
+    RSH_MD5_STEP(RSH_MD5_I, c, d, a, b, m[14], 0xab9423a7u, 15);
+    RSH_MD5_STEP(RSH_MD5_I, b, c, d, a, m[5], 0xfc93a039u, 21);
+    RSH_MD5_STEP(RSH_MD5_I, a, b, c, d, m[12], 0x655b59c3u, 6);
+    RSH_MD5_STEP(RSH_MD5_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
+    RSH_MD5_STEP(RSH_MD5_I, c, d, a, b, m[10], 0xffeff47du, 15);
+    RSH_MD5_STEP(RSH_MD5_I, b, c, d, a, m[1], 0x85845dd1u, 21);
+    RSH_MD5_STEP(RSH_MD5_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
+    RSH_MD5_STEP(RSH_MD5_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+    RSH_MD5_STEP(RSH_MD5_I, c, d, a, b, m[6], 0xa3014314u, 15);
+    RSH_MD5_STEP(RSH_MD5_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
+    RSH_MD5_STEP(RSH_MD5_I, a, b, c, d, m[4], 0xf7537e82u, 6);
+    RSH_MD5_STEP(RSH_MD5_I, d, a, b, c, m[11], 0xbd3af235u, 10);
+    RSH_MD5_STEP(RSH_MD5_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+    RSH_MD5_STEP(RSH_MD5_I, b, c, d, a, m[9], 0xeb86d391u, 21);
+
+    st.a += a;
+    st.b += b;
+    st.c += c;
+    st.d += d;
+}
+
+// Little-endian 16-byte digest from the state.
+RSH_HD void md5_digest_bytes(const Md5State& st, uint8_t out[16]) {
+    const uint32_t w[4] = {st.a, st.b, st.c, st.d};
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(w[i] >> (8 * j));
+}
+
+}  // namespace rsh

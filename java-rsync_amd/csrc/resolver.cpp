@@ -1,0 +1,281 @@
+// resolver.cpp -- sequential Sender state machine over device-computed events (see resolver.h).
+// Reference: session/Sender.java:1235-1327 (loop), session/Checksum.java:175-276 (candidate order),
+// io/FileView.java:143-185,235-278 (window, mark, isFull), util/Rolling.java:25-60 (add/subtract).
+#include "resolver.h"
+
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <limits>
+
+namespace rsh {
+
+void ChunkTable::build() {
+    const int32_t n = chunk_count;
+    std::vector<uint32_t> k2(n);
+    std::vector<int32_t> i2(n);
+    sorted_key.resize(n);
+    sorted_idx.resize(n);
+    for (int32_t i = 0; i < n; ++i) {
+        sorted_key[i] = (uint32_t)weak[i];
+        sorted_idx[i] = i;
+    }
+    // LSD radix sort, two stable 16-bit passes: ties keep ascending chunk index (Multimap insertion order).
+    std::vector<uint32_t> cnt(65537);
+    for (int pass = 0; pass < 2; ++pass) {
+        const int sh = 16 * pass;
+        std::vector<uint32_t>& ks = pass == 0 ? sorted_key : k2;
+        std::vector<int32_t>& is = pass == 0 ? sorted_idx : i2;
+        std::vector<uint32_t>& kd = pass == 0 ? k2 : sorted_key;
+        std::vector<int32_t>& id = pass == 0 ? i2 : sorted_idx;
+        std::fill(cnt.begin(), cnt.end(), 0u);
+        for (int32_t i = 0; i < n; ++i) cnt[((ks[i] >> sh) & 0xFFFFu) + 1]++;
+        for (int d = 0; d < 65536; ++d) cnt[d + 1] += cnt[d];
+        for (int32_t i = 0; i < n; ++i) {
+            const uint32_t dgt = (ks[i] >> sh) & 0xFFFFu;
+            kd[cnt[dgt]] = ks[i];
+            id[cnt[dgt]] = is[i];
+            cnt[dgt]++;
+        }
+    }
+}
+
+void ChunkTable::bucket(int32_t key, int32_t* lo, int32_t* hi) const {
+    const uint32_t k = (uint32_t)key;
+    auto a = std::lower_bound(sorted_key.begin(), sorted_key.end(), k);
+    auto b = std::upper_bound(a, sorted_key.end(), k);
+    *lo = (int32_t)(a - sorted_key.begin());
+    *hi = (int32_t)(b - sorted_key.begin());
+}
+
+void ChunkTable::keys_with_digest(const uint8_t* d, std::vector<int32_t>* keys) const {
+    keys->clear();
+    for (int32_t i = 0; i < chunk_count; ++i)
+        if (memcmp(strong + (int64_t)i * digest_length, d, (size_t)digest_length) == 0) keys->push_back(weak[i]);
+    std::sort(keys->begin(), keys->end());
+    keys->erase(std::unique(keys->begin(), keys->end()), keys->end());
+}
+
+namespace {
+
+inline uint32_t lo16(int32_t v) { return (uint32_t)v & 0xFFFFu; }
+inline uint32_t hi16(int32_t v) { return (uint32_t)v >> 16; }
+inline int32_t pack16(uint32_t lo, uint32_t hi) { return (int32_t)((lo & 0xFFFFu) | (hi << 16)); }
+inline int32_t jbyte(uint8_t v) { return (int32_t)(int8_t)v; }
+inline int32_t roll_sub(int32_t cs, int32_t w, uint8_t x) {  // Rolling.java:56-60
+    return pack16(lo16(cs) - (uint32_t)jbyte(x), hi16(cs) - (uint32_t)w * (uint32_t)jbyte(x));
+}
+inline int32_t roll_add(int32_t cs, uint8_t x) {  // Rolling.java:25-29
+    const uint32_t lo = lo16(cs) + (uint32_t)jbyte(x);
+    return pack16(lo, hi16(cs) + lo);
+}
+
+// Checksum.java:175-195 binarySearch + :206-213 closeIndexOf over one bucket (ascending chunk index).
+int32_t close_index_of(const int32_t* bucket, int32_t size, int32_t chunk_index) {
+    int32_t l = 0, r = size - 1;
+    while (l <= r) {
+        const int32_t m = l + (r - l) / 2;
+        if (bucket[m] == chunk_index) return m;
+        if (bucket[m] < chunk_index) l = m + 1;
+        else r = m - 1;
+    }
+    return l < size - 1 ? l : size - 1;
+}
+
+}  // namespace
+
+void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveResult* out) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t B = table.block_length;
+    const int dl = table.digest_length;
+    const int64_t S = table.remainder > 0 ? table.remainder : B;  // getSmallestChunkSize, Checksum.java:131-137
+    const int64_t last = n - S;  // visited positions satisfy wl(s) >= S  <=>  s <= n - S
+    const int64_t nB = n - B;
+    const int64_t nal = be.aligned_count();
+    const int32_t* aw = be.aligned_weak();
+    const uint8_t* as = be.aligned_strong();
+    const uint8_t* fl = be.chain_flags();
+    const int64_t nflags = std::min<int64_t>(nal, table.chunk_count);
+    auto wl = [&](int64_t s) { return std::min<int64_t>(B, n - s); };  // FileView window length
+    auto clampB = [&](int64_t p) { return std::min<int64_t>(p, nB); };
+
+    std::vector<rsh_event>& ev = out->ev;
+    rsh_scan_stats& st = out->stats;
+    auto emit_lit = [&](int64_t off, int64_t len) {  // sendDataFrom; zero-length calls write nothing
+        if (len <= 0) return;
+        ev.push_back(rsh_event{off, len, RSH_EV_LITERAL, 0, 0, 0});
+        out->literal += len;
+    };
+    auto emit_match = [&](int64_t off, int64_t len, int32_t idx, int32_t cnt) {
+        if (!ev.empty()) {
+            rsh_event& b = ev.back();
+            if (b.kind == RSH_EV_MATCH && b.index + b.count == idx && b.offset + b.length == off) {
+                b.count += cnt;
+                b.length += len;
+                out->matched += len;
+                return;
+            }
+        }
+        ev.push_back(rsh_event{off, len, RSH_EV_MATCH, idx, cnt, 0});
+        out->matched += len;
+    };
+
+    // Sender state (file coordinates).  E = R - T is kept as its value at `anchor` (quirk A).
+    int64_t s = 0, m = 0;
+    int32_t pref = 0;
+    uint32_t elo = 0, ehi = 0;
+    int64_t anchor = 0;
+    bool md5c_valid = false;  // localChunkMd5sum != null (Sender.java:1248)
+    uint8_t md5c[16];
+    std::vector<int32_t> dkeys;
+    bool dkeys_ready = false;
+
+    auto E_at = [&](int64_t p, uint32_t* lo, uint32_t* hi) {
+        *lo = elo;
+        *hi = ehi + elo * (uint32_t)(clampB(p) - clampB(anchor));
+    };
+    auto T_at = [&](int64_t p) -> int32_t {
+        if (p % B == 0 && p / B < nal) return aw[p / B];
+        return be.weak_at(p);
+    };
+    // FileView flush at f (isFull, Sender.java:1294-1302) with rolling value R at f: the Java code
+    // subtracts x_f with the full window, slides by B and keeps rolling the old value.
+    auto flush = [&](int64_t f, int32_t R) {
+        emit_lit(m, f + B - m);
+        st.flushes++;
+        const int32_t R1 = roll_sub(R, (int32_t)B, be.byte_at(f));
+        const int64_t s2 = f + B;
+        m = s2;
+        s = s2;
+        if (s2 <= last) {
+            int32_t R2 = R1;
+            if (wl(s2) == B) R2 = roll_add(R1, be.byte_at(s2 + B - 1));  // :1308-1310
+            const int32_t T2 = T_at(s2);
+            elo = (lo16(R2) - lo16(T2)) & 0xFFFFu;
+            ehi = (hi16(R2) - hi16(T2)) & 0xFFFFu;
+            anchor = s2;
+        }
+    };
+
+    while (s <= last) {
+        const bool synced = (elo == 0 && ehi == 0);
+        // (1) aligned chain: preferred index == k and source window k carries chunk k's sums.
+        if (!md5c_valid && synced && s % B == 0) {
+            const int64_t k = s / B;
+            if (k == pref && k < nflags && fl[k]) {
+                int64_t j = k, p = s;
+                while (j < nflags && fl[j] && p <= last) {
+                    p += wl(p);
+                    ++j;
+                }
+                emit_lit(m, s - m);
+                emit_match(s, p - s, (int32_t)k, (int32_t)(j - k));
+                st.chain_matches += j - k;
+                s = p;
+                m = p;
+                pref = (int32_t)j;
+                anchor = s;
+                continue;
+            }
+        }
+        // (2) next candidate event in [s, stop]: the first flush point bounds the state's validity.
+        const int64_t f = (m + 10 * B <= n) ? m + 9 * B : std::numeric_limits<int64_t>::max();
+        const int64_t stop = std::min(f, last);
+        const std::vector<int32_t>* keys = nullptr;
+        bool none = false;
+        if (md5c_valid) {  // stale digest: only chunks whose digest is md5c can ever match
+            if (!dkeys_ready) {
+                table.keys_with_digest(md5c, &dkeys);
+                dkeys_ready = true;
+            }
+            keys = &dkeys;
+            none = dkeys.empty();
+        }
+        int64_t p = -1;
+        if (!none) {
+            int64_t a = s;
+            if (!md5c_valid && synced && s % B == 0 && s / B < nal) {  // key known from aligned sums
+                int32_t lo, hi;
+                table.bucket(aw[s / B], &lo, &hi);
+                if (hi > lo) p = s;
+                else a = s + 1;
+            }
+            if (p < 0 && a <= stop) {
+                uint32_t el, eh;
+                E_at(a, &el, &eh);
+                p = be.first_hit(a, stop + 1, a, el, eh, keys);
+                st.probe_launches++;
+            }
+        }
+        if (p >= 0) {
+            uint32_t el, eh;
+            E_at(p, &el, &eh);
+            const int32_t T = T_at(p);
+            const int32_t R = pack16(lo16(T) + el, hi16(T) + eh);
+            const int64_t w = wl(p);
+            st.events++;
+            int32_t lo, hi;
+            table.bucket(R, &lo, &hi);
+            int32_t hit = -1;
+            if (hi > lo) {  // getCandidateChunks order (Checksum.java:215-276)
+                const int32_t size = hi - lo;
+                const int32_t* bk = &table.sorted_idx[lo];
+                const int32_t init = close_index_of(bk, size, pref);
+                for (int32_t it = -1; it < size; ++it) {
+                    int32_t pos;
+                    if (it < 0) {
+                        pos = init;
+                    } else {
+                        if (it == init || table.chunk_length(bk[it]) != w) continue;
+                        pos = it;
+                    }
+                    const int32_t c = bk[pos];
+                    if (!md5c_valid) {  // Sender.java:1259-1263
+                        if (p % B == 0 && p / B < nal) {
+                            memcpy(md5c, as + (p / B) * dl, (size_t)dl);
+                        } else {
+                            uint8_t full[16];
+                            be.md5_at(p, full);
+                            memcpy(md5c, full, (size_t)dl);
+                            st.host_md5_windows++;
+                        }
+                        md5c_valid = true;
+                        dkeys_ready = false;
+                    }
+                    if (memcmp(md5c, table.strong + (int64_t)c * dl, (size_t)dl) == 0) {
+                        hit = c;
+                        break;
+                    }
+                }
+            }
+            if (hit >= 0) {  // Sender.java:1265-1288
+                emit_lit(m, p - m);
+                emit_match(p, w, hit, 1);
+                pref = hit + 1;
+                s = p + w;
+                m = s;
+                elo = ehi = 0;
+                anchor = s;
+                md5c_valid = false;
+                dkeys_ready = false;
+                continue;
+            }
+            if (p == f) flush(p, R);
+            else s = p + 1;
+            continue;
+        }
+        if (f <= last) {  // no candidate before the flush point: flush at f
+            uint32_t el, eh;
+            E_at(f, &el, &eh);
+            const int32_t T = T_at(f);
+            flush(f, pack16(lo16(T) + el, hi16(T) + eh));
+            continue;
+        }
+        break;
+    }
+    emit_lit(m, n - m);  // Sender.java:1313-1316 (firstOffset == mark once the loop ends)
+    st.resolver_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace rsh

@@ -1,0 +1,72 @@
+// resolver.h -- the sequential part of Sender.sendMatchesAndData (Sender.java:1235-1327), driven by
+// sparse events that the device computes in bulk.
+//
+// The Java loop is byte-serial and history dependent (preferred index, the cached localChunkMd5sum
+// declared outside the loop, the rolling sum that is not recomputed after a FileView flush).  The
+// resolver reproduces it exactly while touching only O(events) positions:
+//   * aligned chains: the device computes the source's own block sums (same B, dl as the basis
+//     table) and a flag per k "source window k has chunk k's weak key and digest"; a run of flags
+//     starting where the preferred index equals k is a run of matches (no per-byte work);
+//   * otherwise the next candidate event is the first position whose rolling key R(p) = T(p) + E(p)
+//     hits the table (or, once the cached digest D is stale, hits a chunk whose digest is D); the
+//     device answers that with one range probe per state change;
+//   * flushes (FileView.isFull) happen at mark + 9B exactly and are applied in closed form, including
+//     the desync E they introduce (E_lo constant, E_hi += E_lo per full-window step).
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "rsync_hip.h"
+
+namespace rsh {
+
+// Host view of the received chunk table (Checksum + Multimap, Checksum.java:156-276).
+struct ChunkTable {
+    int32_t chunk_count = 0;
+    int32_t block_length = 0;
+    int32_t remainder = 0;
+    int32_t digest_length = 0;
+    const int32_t* weak = nullptr;   // chunk_count, receive order
+    const uint8_t* strong = nullptr; // chunk_count * digest_length
+    std::vector<uint32_t> sorted_key; // bucket keys, sorted (stable: ascending chunk index per key)
+    std::vector<int32_t> sorted_idx;
+
+    void build();  // radix sort of (weak, index)
+    void bucket(int32_t key, int32_t* lo, int32_t* hi) const;
+    int32_t chunk_length(int32_t idx) const {  // Checksum.java:197-203
+        return (idx == chunk_count - 1 && remainder > 0) ? remainder : block_length;
+    }
+    // Distinct weak keys of the chunks whose digest equals d (the only ones a stale digest can match).
+    void keys_with_digest(const uint8_t* d, std::vector<int32_t>* keys) const;
+};
+
+// Device (or test) services used by the resolver.  Positions are source file offsets.
+class ScanBackend {
+  public:
+    virtual ~ScanBackend() {}
+    // Aligned speculation over the source: window k = [kB, min(kB + B, n)), k < aligned_count().
+    virtual int64_t aligned_count() = 0;
+    virtual const int32_t* aligned_weak() = 0;
+    virtual const uint8_t* aligned_strong() = 0;  // digest_length bytes per window
+    virtual const uint8_t* chain_flags() = 0;     // min(aligned_count, chunk_count) entries
+    virtual int32_t weak_at(int64_t p) = 0;       // T(p) over min(B, n - p) bytes
+    virtual void md5_at(int64_t p, uint8_t out[16]) = 0;  // MD5(x[p, p + min(B, n-p)) || seed)
+    virtual uint8_t byte_at(int64_t p) = 0;
+    // First p in [a, b) with (T(p) + E(p)) in the key set (keys == nullptr: the whole chunk table),
+    // E(p) = (e_lo, e_hi + e_lo * (min(p, n-B) - min(anchor, n-B))) mod 2^16; -1 if none.
+    virtual int64_t first_hit(int64_t a, int64_t b, int64_t anchor, uint32_t e_lo, uint32_t e_hi,
+                              const std::vector<int32_t>* keys) = 0;
+};
+
+struct ResolveResult {
+    std::vector<rsh_event> ev;
+    int64_t literal = 0;
+    int64_t matched = 0;
+    rsh_scan_stats stats{};
+};
+
+// n > 0 and h->block_length > 0 (skipMatchSendData / empty sources are handled by the caller).
+void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveResult* out);
+
+}  // namespace rsh

@@ -1,0 +1,265 @@
+"""rsync_hip.py -- Python host binding of librsynchip.so (the C-ABI in include/rsync_hip.h).
+
+Mirrors the reference's hot-path surface (paths relative to core/src/main/java/com/github/java/rsync/internal/):
+
+  Generator.getBlockLengthFor / getDigestLength   session/Generator.java:198-212  -> block_length_for, digest_length_for
+  Checksum.Header(3-arg) / (4-arg)                session/Checksum.java:75-113    -> Header.make, Header.validate
+  Generator.sendItemizeAndChecksums (hot loop)    session/Generator.java:866-909  -> Context.block_sums
+  Sender.sendMatchesAndData / skipMatchSendData   session/Sender.java:1235-1399   -> Context.match_scan
+  Sender channel bytes (sendDataFrom / putInt)    session/Sender.java:794-809     -> tokens
+
+Errors raise the Python analogue of the reference's exception (ValueError ~ IllegalArgumentException,
+ProtocolError ~ RsyncProtocolException, OverflowError ~ Checksum.ChunkOverflow).  There is no CPU
+fallback: without a gfx950 device Context() raises DeviceError.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "librsynchip.so")
+
+RSH_OK, RSH_E_INVAL, RSH_E_PROTOCOL, RSH_E_OVERFLOW, RSH_E_NOSPACE, RSH_E_DEVICE, RSH_E_NOMEM = 0, -1, -2, -3, -4, -5, -6
+EV_LITERAL, EV_MATCH = 1, 2
+
+
+class ProtocolError(Exception):
+    """RsyncProtocolException (Connection.receiveChecksumHeader, Connection.java:28-38)."""
+
+
+class DeviceError(RuntimeError):
+    """HIP failure or no gfx950 device."""
+
+
+class Header(ctypes.Structure):
+    _fields_ = [("chunk_count", ctypes.c_int32), ("block_length", ctypes.c_int32),
+                ("digest_length", ctypes.c_int32), ("remainder", ctypes.c_int32)]
+
+    def as_dict(self):
+        return dict(chunk_count=self.chunk_count, block_length=self.block_length,
+                    digest_length=self.digest_length, remainder=self.remainder)
+
+    def smallest_chunk_size(self):  # Checksum.java:131-137
+        return self.remainder if self.remainder > 0 else self.block_length
+
+
+class Event(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_int64), ("length", ctypes.c_int64), ("kind", ctypes.c_int32),
+                ("index", ctypes.c_int32), ("count", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class ScanStats(ctypes.Structure):
+    _fields_ = [("chain_matches", ctypes.c_int64), ("events", ctypes.c_int64), ("probe_launches", ctypes.c_int64),
+                ("host_md5_windows", ctypes.c_int64), ("flushes", ctypes.c_int64),
+                ("device_ms", ctypes.c_double), ("resolver_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+EVENT_DTYPE = np.dtype([("offset", "<i8"), ("length", "<i8"), ("kind", "<i4"), ("index", "<i4"),
+                        ("count", "<i4"), ("reserved", "<i4")])
+
+# every symbol include/rsync_hip.h declares
+EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_device_count", "rsh_ctx_create", "rsh_ctx_destroy",
+           "rsh_ctx_stream", "rsh_block_length_for", "rsh_digest_length_for", "rsh_header_make",
+           "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
+           "rsh_match_scan_device", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
+           "rsh_fill_splitmix_device"]
+
+_LIB = None
+
+
+def build(force=False):
+    """Compile librsynchip.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    cmd = ["make", "-s", "-C", HERE] + (["-B"] if force else [])
+    subprocess.run(cmd, check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise DeviceError(f"{LIB_PATH} missing: run rsync_hip.build() (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    HP = ctypes.POINTER(Header)
+    sig = {
+        "rsh_abi_version": ([], ctypes.c_int),
+        "rsh_strerror": ([ctypes.c_int], ctypes.c_char_p),
+        "rsh_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+        "rsh_ctx_create": ([ctypes.c_int, ctypes.POINTER(P)], ctypes.c_int),
+        "rsh_ctx_destroy": ([P], None),
+        "rsh_ctx_stream": ([P], P),
+        "rsh_block_length_for": ([I64], I32),
+        "rsh_digest_length_for": ([I64, I32, I32], I32),
+        "rsh_header_make": ([I32, I32, I64, HP], ctypes.c_int),
+        "rsh_header_validate": ([HP], ctypes.c_int),
+        "rsh_block_sums": ([P, P, I64, HP, P, P, P], ctypes.c_int),
+        "rsh_block_sums_device": ([P, P, I64, HP, P, P, P], ctypes.c_int),
+        "rsh_ctx_sync": ([P], ctypes.c_int),
+        "rsh_match_scan": ([P, P, I64, HP, P, P, P, P, I64, ctypes.POINTER(I64), P, ctypes.POINTER(I64),
+                            ctypes.POINTER(I64), ctypes.POINTER(ScanStats)], ctypes.c_int),
+        "rsh_match_scan_device": ([P, P, I64, HP, P, P, P, P, I64, ctypes.POINTER(I64), ctypes.POINTER(I64),
+                                   ctypes.POINTER(I64), ctypes.POINTER(ScanStats)], ctypes.c_int),
+        "rsh_file_md5": ([P, I64, P], ctypes.c_int),
+        "rsh_tokens_size": ([P, I64], I64),
+        "rsh_tokens_write": ([P, P, I64, P, P, I64], ctypes.c_int),
+        "rsh_generator_bytes": ([HP, P, P, P, I64], I64),
+        "rsh_fill_splitmix_device": ([P, P, I64, ctypes.c_uint64, I64], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _LIB = L
+    return L
+
+
+def _check(rc):
+    if rc == RSH_OK:
+        return
+    msg = lib().rsh_strerror(rc).decode()
+    if rc == RSH_E_INVAL:
+        raise ValueError(msg)
+    if rc == RSH_E_PROTOCOL:
+        raise ProtocolError(msg)
+    if rc == RSH_E_OVERFLOW:
+        raise OverflowError(msg)
+    if rc == RSH_E_NOMEM:
+        raise MemoryError(msg)
+    raise DeviceError(msg)
+
+
+def _ptr(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def _u8(data):
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data.view(np.uint8).reshape(-1))
+    return np.frombuffer(bytes(data), dtype=np.uint8)
+
+
+def block_length_for(n):
+    return lib().rsh_block_length_for(n)
+
+
+def digest_length_for(n, blen, min_digest=2):
+    return lib().rsh_digest_length_for(n, blen, min_digest)
+
+
+def header_make(blen, dlen, n):
+    h = Header()
+    _check(lib().rsh_header_make(blen, dlen, n, ctypes.byref(h)))
+    return h
+
+
+def header_validate(h):
+    _check(lib().rsh_header_validate(ctypes.byref(h)))
+
+
+def file_md5(data):
+    a = _u8(data)
+    out = np.zeros(16, np.uint8)
+    _check(lib().rsh_file_md5(_ptr(a), a.size, _ptr(out)))
+    return out.tobytes()
+
+
+def events_as_tuples(ev, block_length):
+    """Expand MATCH runs into one (MATCH, offset, length, index) per chunk, the oracle's granularity.
+    Every window of a run is a full block except possibly the file's last one."""
+    out = []
+    for e in ev:
+        if e["kind"] == EV_LITERAL:
+            out.append((EV_LITERAL, int(e["offset"]), int(e["length"]), 0))
+        else:
+            off, left, cnt = int(e["offset"]), int(e["length"]), int(e["count"])
+            for j in range(cnt):
+                w = left if j == cnt - 1 else block_length
+                out.append((EV_MATCH, off, w, int(e["index"]) + j))
+                off += w
+                left -= w
+    return out
+
+
+def tokens(src, ev, file_md5_bytes):
+    a = _u8(src)
+    ev = np.ascontiguousarray(ev, dtype=EVENT_DTYPE)
+    n = ev.size
+    size = lib().rsh_tokens_size(_ptr(ev) if n else None, n)
+    out = np.zeros(size, np.uint8)
+    fm = np.frombuffer(file_md5_bytes, np.uint8).copy()
+    _check(lib().rsh_tokens_write(_ptr(a), _ptr(ev) if n else None, n, _ptr(fm), _ptr(out), size))
+    return out.tobytes()
+
+
+def device_count():
+    c = ctypes.c_int(0)
+    rc = lib().rsh_device_count(ctypes.byref(c))
+    return c.value if rc == RSH_OK else 0
+
+
+class Context:
+    """One per calling thread (the reference's Generator and Sender threads each get their own)."""
+
+    def __init__(self, device=0):
+        self._p = ctypes.c_void_p()
+        _check(lib().rsh_ctx_create(device, ctypes.byref(self._p)))
+
+    def close(self):
+        if self._p:
+            lib().rsh_ctx_destroy(self._p)
+            self._p = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._p
+
+    def sync(self):
+        _check(lib().rsh_ctx_sync(self._p))
+
+    def block_sums(self, data, h, seed):
+        """Generator.sendItemizeAndChecksums hot loop: (weak int32[C], strong uint8[C*dl])."""
+        a = _u8(data)
+        s = np.frombuffer(bytes(seed), np.uint8).copy()
+        weak = np.zeros(max(h.chunk_count, 1), np.int32)
+        strong = np.zeros(max(h.chunk_count * h.digest_length, 1), np.uint8)
+        _check(lib().rsh_block_sums(self._p, _ptr(a), a.size, ctypes.byref(h), _ptr(s), _ptr(weak), _ptr(strong)))
+        return weak[:h.chunk_count], strong[:h.chunk_count * h.digest_length]
+
+    def match_scan(self, src, h, weak, strong, seed, ev_cap=None):
+        """Sender.sendMatchesAndData: (events ndarray[EVENT_DTYPE], file_md5, literal, matched, stats)."""
+        a = _u8(src)
+        s = np.frombuffer(bytes(seed), np.uint8).copy()
+        w = np.ascontiguousarray(weak, dtype=np.int32)
+        st = np.ascontiguousarray(strong, dtype=np.uint8)
+        cap = ev_cap if ev_cap is not None else 1024
+        while True:
+            ev = np.zeros(max(cap, 1), EVENT_DTYPE)
+            n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+            fm = np.zeros(16, np.uint8)
+            stats = ScanStats()
+            rc = lib().rsh_match_scan(self._p, _ptr(a), a.size, ctypes.byref(h), _ptr(w) if w.size else None,
+                                      _ptr(st) if st.size else None, _ptr(s), _ptr(ev), cap, ctypes.byref(n_ev),
+                                      _ptr(fm), ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(stats))
+            if rc == RSH_E_NOSPACE and ev_cap is None:
+                cap = n_ev.value
+                continue
+            _check(rc)
+            return ev[:n_ev.value], fm.tobytes(), lit.value, mat.value, stats.as_dict()

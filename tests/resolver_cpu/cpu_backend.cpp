@@ -1,0 +1,122 @@
+// TEST INFRASTRUCTURE ONLY -- a host implementation of rsh::ScanBackend so the resolver's state
+// machine (java-rsync_amd/csrc/resolver.cpp) can be checked against the oracle on machines without
+// a GPU.  Never linked into librsynchip.so: the product's backend is the HIP one in capi.cpp.
+#include <string.h>
+
+#include <vector>
+
+#include "host_md5.h"
+#include "resolver.h"
+#include "rsync_hip.h"
+
+namespace {
+
+int32_t weak_of(const uint8_t* p, int64_t L) {
+    uint32_t s1 = 0, s2 = 0;
+    for (int64_t i = 0; i < L; ++i) {
+        s1 += (uint32_t)(int32_t)(int8_t)p[i];
+        s2 += s1;
+    }
+    return (int32_t)((s1 & 0xFFFFu) | (s2 << 16));
+}
+
+class CpuBackend : public rsh::ScanBackend {
+  public:
+    CpuBackend(const uint8_t* x, int64_t n, const rsh::ChunkTable& t, const uint8_t seed[4])
+        : x_(x), n_(n), t_(t), B_(t.block_length), dl_(t.digest_length) {
+        memcpy(seed_, seed, 4);
+        const int64_t na = (n + B_ - 1) / B_;
+        aw_.resize(na);
+        as_.resize(na * dl_);
+        for (int64_t k = 0; k < na; ++k) {
+            aw_[k] = weak_at(k * B_);
+            uint8_t d[16];
+            md5_at(k * B_, d);
+            memcpy(&as_[k * dl_], d, dl_);
+        }
+        const int64_t nf = na < t.chunk_count ? na : t.chunk_count;
+        fl_.resize(nf > 0 ? nf : 1);
+        for (int64_t k = 0; k < nf; ++k)
+            fl_[k] = aw_[k] == t.weak[k] && memcmp(&as_[k * dl_], t.strong + k * dl_, dl_) == 0;
+    }
+    int64_t aligned_count() override { return (int64_t)aw_.size(); }
+    const int32_t* aligned_weak() override { return aw_.data(); }
+    const uint8_t* aligned_strong() override { return as_.data(); }
+    const uint8_t* chain_flags() override { return fl_.data(); }
+    int32_t weak_at(int64_t p) override { return weak_of(x_ + p, wl(p)); }
+    void md5_at(int64_t p, uint8_t out[16]) override {
+        rsh::HostMd5 h;
+        h.update(x_ + p, (size_t)wl(p));
+        h.update(seed_, 4);
+        h.final(out);
+    }
+    uint8_t byte_at(int64_t p) override { return x_[p]; }
+    int64_t first_hit(int64_t a, int64_t b, int64_t anchor, uint32_t e_lo, uint32_t e_hi,
+                      const std::vector<int32_t>* keys) override {
+        const int64_t nB = n_ - B_;
+        auto cl = [&](int64_t p) { return p < nB ? p : nB; };
+        int32_t T = a < b ? weak_at(a) : 0;
+        for (int64_t p = a; p < b; ++p) {
+            const uint32_t eh = e_hi + e_lo * (uint32_t)(cl(p) - cl(anchor));
+            const int32_t R = (int32_t)(((((uint32_t)T & 0xFFFFu) + e_lo) & 0xFFFFu) | ((((uint32_t)T >> 16) + eh) << 16));
+            bool hit;
+            if (keys) {
+                hit = false;
+                for (int32_t k : *keys) hit |= (k == R);
+            } else {
+                int32_t lo, hi;
+                t_.bucket(R, &lo, &hi);
+                hit = hi > lo;
+            }
+            if (hit) return p;
+            // true weak sum of the next window (Rolling subtract/add with the FileView window rule)
+            const int64_t w = wl(p);
+            const int32_t x = (int32_t)(int8_t)x_[p];
+            uint32_t lo = ((uint32_t)T & 0xFFFFu) - (uint32_t)x;
+            uint32_t hi = ((uint32_t)T >> 16) - (uint32_t)w * (uint32_t)x;
+            if (n_ - (p + 1) >= B_) {
+                lo += (uint32_t)(int32_t)(int8_t)x_[p + B_];
+                hi += lo;
+            }
+            T = (int32_t)((lo & 0xFFFFu) | (hi << 16));
+        }
+        return -1;
+    }
+
+  private:
+    int64_t wl(int64_t p) const { return n_ - p < B_ ? n_ - p : B_; }
+    const uint8_t* x_;
+    int64_t n_;
+    const rsh::ChunkTable& t_;
+    int64_t B_;
+    int dl_;
+    uint8_t seed_[4];
+    std::vector<int32_t> aw_;
+    std::vector<uint8_t> as_;
+    std::vector<uint8_t> fl_;
+};
+
+}  // namespace
+
+extern "C" int rtest_scan(const uint8_t* src, int64_t n, const rsh_header* h, const int32_t* weak,
+                          const uint8_t* strong, const uint8_t seed[4], rsh_event* ev, int64_t cap, int64_t* n_ev,
+                          int64_t* lit, int64_t* mat, rsh_scan_stats* stats) {
+    rsh::ChunkTable t;
+    t.chunk_count = h->chunk_count;
+    t.block_length = h->block_length;
+    t.remainder = h->remainder;
+    t.digest_length = h->digest_length;
+    t.weak = weak;
+    t.strong = strong;
+    t.build();
+    CpuBackend be(src, n, t, seed);
+    rsh::ResolveResult r;
+    rsh::resolve_scan(n, t, be, &r);
+    *n_ev = (int64_t)r.ev.size();
+    *lit = r.literal;
+    *mat = r.matched;
+    if (stats) *stats = r.stats;
+    if ((int64_t)r.ev.size() > cap) return RSH_E_NOSPACE;
+    memcpy(ev, r.ev.data(), r.ev.size() * sizeof(rsh_event));
+    return 0;
+}

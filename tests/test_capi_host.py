@@ -1,0 +1,106 @@
+"""CPU tests of librsynchip.so's host-side surface: it loads, exports every symbol include/rsync_hip.h
+declares, and its pure-host functions (sizing rule, header validation, channel bytes) agree with the
+oracle.  No compute calls that need a GPU."""
+import ctypes
+import hashlib
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+import rsync_hip as R
+from conftest import ROOT, golden
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    R.build()
+
+
+def test_header_declares_exports():
+    text = open(os.path.join(ROOT, "include", "rsync_hip.h")).read()
+    declared = set(re.findall(r"\b(rsh_[a-z0-9_]+)\s*\(", text))
+    assert declared == set(R.EXPORTS)
+
+
+def test_library_exports_every_symbol():
+    L = ctypes.CDLL(R.LIB_PATH)
+    for name in R.EXPORTS:
+        assert hasattr(L, name), name
+    assert R.lib().rsh_abi_version() == 1
+
+
+@pytest.mark.parametrize("n", [1, 511, 512, 557, 1000, 64 << 20, 128 << 20, 4 << 30, 16 << 30, 64 << 30, (1 << 40) + 3])
+def test_sizing_matches_oracle(n):
+    L = O.lib()
+    b = R.block_length_for(n)
+    assert b == L.orc_block_length_for(n)
+    assert R.digest_length_for(n, b, 2) == max(2, L.orc_digest_length(n, b))
+    assert R.digest_length_for(n, b, 16) == 16  # redo pass (Generator.java:371)
+
+
+def test_header_make_and_validate():
+    h = R.header_make(512, 2, 557)
+    assert h.as_dict() == dict(chunk_count=2, block_length=512, digest_length=2, remainder=45)
+    R.header_validate(h)
+    with pytest.raises(OverflowError):
+        R.header_make(1, 2, 1 << 40)
+    for bad in [(1, (1 << 17) + 1, 2, 0), (1, 0, 2, 0), (2, 512, 2, 513), (-1, 512, 2, 0), (1, 512, -1, 0)]:
+        with pytest.raises(R.ProtocolError):
+            R.header_validate(R.Header(*bad))
+    R.header_validate(R.Header(131072, 1 << 17, 4, 0))  # config 5 is accepted (check is '>')
+    with pytest.raises(R.ProtocolError):                # config 3 (B = 2^18) is rejected
+        R.header_validate(R.header_make(1 << 18, 5, 64 << 30))
+
+
+def test_file_md5_host():
+    for n in [0, 1, 55, 56, 63, 64, 65, 1000, 100000]:
+        d = O.splitmix(n, 7).tobytes()
+        assert R.file_md5(d) == hashlib.md5(d).digest()
+
+
+@pytest.mark.parametrize("case", golden()[:12] + golden()[-8:], ids=lambda c: c["name"])
+def test_tokens_match_oracle(case):
+    ev = np.zeros(len(case["events"]), R.EVENT_DTYPE)
+    for i, (k, off, ln, idx) in enumerate(case["events"]):
+        ev[i] = (off, ln, k, idx, 1 if k == R.EV_MATCH else 0, 0)
+    tok = R.tokens(case["src_bytes"], ev, bytes.fromhex(case["file_md5"]))
+    assert hashlib.sha256(tok).hexdigest() == case["tokens_sha256"]
+
+
+def test_tokens_match_runs():
+    src = bytes(range(256)) * 100
+    ev = np.zeros(3, R.EVENT_DTYPE)
+    ev[0] = (0, 20000, R.EV_LITERAL, 0, 0, 0)
+    ev[1] = (20000, 1536, R.EV_MATCH, 7, 3, 0)
+    ev[2] = (21536, 5, R.EV_LITERAL, 0, 0, 0)
+    tok = R.tokens(src, ev, bytes(16))
+    oev = [(1, 0, 20000, 0), (2, 20000, 512, 7), (2, 20512, 512, 8), (2, 21024, 512, 9), (1, 21536, 5, 0)]
+    assert tok == O.tokens(src, oev, bytes(16))
+    assert R.events_as_tuples(ev, 512) == oev
+
+
+def test_generator_bytes():
+    g = {c["name"]: c for c in golden()}["systemtest_copy_twice_557"]
+    h = R.Header(**g["header"])
+    weak = np.array(g["weak"], np.int32)
+    strong = np.frombuffer(bytes.fromhex(g["strong"]), np.uint8).copy()
+    size = R.lib().rsh_generator_bytes(ctypes.byref(h), None, None, None, 0)
+    out = np.zeros(size, np.uint8)
+    assert R.lib().rsh_generator_bytes(ctypes.byref(h), weak.ctypes.data, strong.ctypes.data, out.ctypes.data,
+                                       size) == size
+    oh = O.Header(**g["header"])
+    ref = np.zeros(size, np.uint8)
+    O.lib().orc_generator_bytes(ctypes.byref(oh), weak.ctypes.data, strong.ctypes.data, ref.ctypes.data)
+    assert out.tobytes() == ref.tobytes()
+
+
+def test_no_device_fails_loudly():
+    """Without a gfx950 GPU the product refuses to run: there is no CPU fallback."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(R.DeviceError):
+        R.Context(0)

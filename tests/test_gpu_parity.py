@@ -1,0 +1,133 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the oracle and the golden fixtures.
+Integer/byte work: bit-exact equality is the bar everywhere."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+import rsync_hip as R
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+SEED = bytes([1, 2, 3, 4])
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    R.build()
+    c = R.Context(0)
+    yield c
+    c.close()
+
+
+def gen_both(ctx, basis, blen, dlen, seed=SEED):
+    h = O.header(blen, dlen, len(basis))
+    ow, os_ = O.generator(basis, h, seed)
+    rh = R.Header(**h.as_dict())
+    gw, gs = ctx.block_sums(basis, rh, seed)
+    return h, rh, ow, os_, gw, gs
+
+
+@pytest.mark.parametrize("case", [c for c in golden() if c["basis_bytes"]], ids=lambda c: c["name"])
+def test_generator_golden(ctx, case):
+    h = R.Header(**case["header"])
+    w, s = ctx.block_sums(case["basis_bytes"], h, case["seed_bytes"])
+    assert [int(x) for x in w] == case["weak"]
+    assert s.tobytes().hex() == case["strong"]
+
+
+@pytest.mark.parametrize("n,blen,dlen", [
+    (1, 512, 2), (63, 512, 2), (64, 512, 3), (65, 512, 2), (511, 512, 2), (512, 512, 2), (513, 512, 2),
+    (5 * 512 + 45, 512, 2), (700 * 13 + 5, 700, 2), (702 * 7 + 3, 702, 5), (4099, 1024, 16),
+    (1 << 20, 512, 3), ((1 << 20) + 123, 8192, 3), (3 << 20, 65536, 4), ((1 << 22) + 9, 131072, 4),
+])
+def test_generator_vs_oracle(ctx, n, blen, dlen):
+    basis = O.splitmix(n, 0x5EED5EED00000000 ^ n).tobytes()
+    h, rh, ow, os_, gw, gs = gen_both(ctx, basis, blen, dlen)
+    assert np.array_equal(ow, gw)
+    assert np.array_equal(os_, gs)
+
+
+def test_generator_config1_64MiB(ctx):
+    """BASELINE config 1: 64 MiB basis at B = 512 (override), dl = 3: 131,072 chunks, bit-exact."""
+    n = 64 << 20
+    basis = O.splitmix(n, 0x5EED5EED00000001)
+    h, rh, ow, os_, gw, gs = gen_both(ctx, basis, 512, 3)
+    assert np.array_equal(ow, gw) and np.array_equal(os_, gs)
+
+
+def _sender_both(ctx, basis, src, blen, dlen, seed=SEED):
+    h = O.header(blen, dlen, len(basis))
+    w, s = O.generator(basis, h, seed)
+    oev, ofm, olit, omat, _ = O.sender(src, h, w, s, seed)
+    rh = R.Header(**h.as_dict())
+    ev, fm, lit, mat, stats = ctx.match_scan(src, rh, w, s, seed)
+    assert R.events_as_tuples(ev, blen) == [tuple(e) for e in oev]
+    assert (fm, lit, mat) == (ofm, olit, omat)
+    assert R.tokens(src, ev, fm) == O.tokens(src, oev, ofm)
+    return stats
+
+
+@pytest.mark.parametrize("case", golden(), ids=lambda c: c["name"])
+def test_sender_golden(ctx, case):
+    h = R.Header(**case["header"])
+    weak = np.array(case["weak"], np.int32)
+    strong = np.frombuffer(bytes.fromhex(case["strong"]), np.uint8)
+    ev, fm, lit, mat, _ = ctx.match_scan(case["src_bytes"], h, weak, strong, case["seed_bytes"])
+    assert R.events_as_tuples(ev, max(h.block_length, 1)) == [tuple(e) for e in case["events"]]
+    assert fm.hex() == case["file_md5"]
+    assert (lit, mat) == (case["literal"], case["matched"])
+    assert hashlib.sha256(R.tokens(case["src_bytes"], ev, fm)).hexdigest() == case["tokens_sha256"]
+
+
+def test_sender_fuzz(ctx):
+    from test_resolver_cpu import _mutate
+    rng = random.Random(77)
+    for _ in range(40):
+        B = rng.choice([512, 512, 576, 1024, 2048, 700])
+        nb = rng.randrange(1, 40 * B)
+        key = rng.randrange(1 << 62)
+        basis = O.splitmix(nb, key).tobytes()
+        if rng.random() < 0.15:
+            blk = O.splitmix(B, key).tobytes()
+            basis = (blk * (nb // B + 1))[:nb]
+        src = _mutate(rng, basis, B, key)
+        if src:
+            _sender_both(ctx, basis, src, B, rng.choice([2, 3, 4, 16]))
+
+
+def test_sender_large_table_desync(ctx):
+    B = 512
+    basis = O.splitmix(65536 * B, 101).tobytes()
+    src = basis[:3 * B] + O.splitmix(10 * B + 37, 3).tobytes() + basis[3 * B + 1:]
+    st = _sender_both(ctx, basis, src, B, 2)
+    assert st["flushes"] > 1000
+
+
+@pytest.mark.parametrize("blen,dlen,mode", [(65536, 4, "identical"), (65536, 4, "half"), (131072, 4, "half"),
+                                            (8192, 3, "insert")])
+def test_sender_config_shapes(ctx, blen, dlen, mode):
+    """BASELINE config shapes at 64-128 MiB: identical basis, every-other-block modified basis, insertion."""
+    n = 64 << 20
+    basis = O.splitmix(n, 0x5EED5EED00000005)
+    if mode == "identical":
+        src = basis
+    elif mode == "half":
+        src = basis.copy()
+        other = O.splitmix(n, 0x5EED5EED00000006)
+        for k in range(1, n // blen, 2):
+            src[k * blen:(k + 1) * blen] = other[k * blen:(k + 1) * blen]
+    else:
+        src = np.concatenate([basis[:1000003], O.splitmix(777, 9), basis[1000003:]])
+    _sender_both(ctx, basis.tobytes(), src.tobytes(), blen, dlen)
+
+
+def test_device_fill_matches_oracle(ctx):
+    import torch
+    n = (1 << 20) + 13
+    d = torch.empty(n, dtype=torch.uint8, device="cuda")
+    assert R.lib().rsh_fill_splitmix_device(ctx.handle, d.data_ptr(), n, 0x5EED5EED00000000, 0) == 0
+    ctx.sync()
+    assert np.array_equal(d.cpu().numpy(), O.splitmix(n, 0x5EED5EED00000000))

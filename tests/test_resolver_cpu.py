@@ -1,0 +1,147 @@
+"""CPU tests of the Sender resolver state machine (java-rsync_amd/csrc/resolver.cpp) driven by a host
+test backend (tests/resolver_cpu/cpu_backend.cpp), against the oracle and the golden fixtures.
+This validates the event-driven restatement (aligned chains, range probes, closed-form flushes and the
+quirk-A desync) independently of the GPU kernels; the GPU tests then run the same resolver on HIP."""
+import ctypes
+import hashlib
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+import rsync_hip as R
+from conftest import ROOT, golden
+
+_LIB = None
+
+
+def rlib():
+    global _LIB
+    if _LIB is None:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "resolver_cpu")], check=True)
+        L = ctypes.CDLL(os.path.join(ROOT, "tests", "build", "libresolver_cpu.so"))
+        P = ctypes.c_void_p
+        L.rtest_scan.argtypes = [P, ctypes.c_int64, ctypes.POINTER(R.Header), P, P, P, P, ctypes.c_int64,
+                                 ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                 ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(R.ScanStats)]
+        _LIB = L
+    return _LIB
+
+
+def resolve(src, h, weak, strong, seed):
+    a = np.frombuffer(bytes(src), np.uint8)
+    w = np.ascontiguousarray(weak, np.int32)
+    st = np.ascontiguousarray(strong, np.uint8)
+    s = np.frombuffer(bytes(seed), np.uint8).copy()
+    cap = 4 * (len(src) // max(h.block_length, 1) + 16)
+    ev = np.zeros(cap, R.EVENT_DTYPE)
+    n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    stats = R.ScanStats()
+    rc = rlib().rtest_scan(a.ctypes.data, a.size, ctypes.byref(h), w.ctypes.data if w.size else None,
+                           st.ctypes.data if st.size else None, s.ctypes.data, ev.ctypes.data, cap,
+                           ctypes.byref(n_ev), ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(stats))
+    assert rc == 0
+    return ev[:n_ev.value], lit.value, mat.value, stats.as_dict()
+
+
+def check_case(basis, src, blen, dlen, seed):
+    h = O.header(blen, dlen, len(basis))
+    weak, strong = O.generator(basis, h, seed)
+    oev, ofm, olit, omat, _ = O.sender(src, h, weak, strong, seed)
+    rh = R.Header(**h.as_dict())
+    ev, lit, mat, stats = resolve(src, rh, weak, strong, seed)
+    got = R.events_as_tuples(ev, blen)
+    assert got == [tuple(e) for e in oev]
+    assert (lit, mat) == (olit, omat)
+    return stats
+
+
+@pytest.mark.parametrize("case", [c for c in golden() if c["header"]["block_length"] > 0 and c["src_len"] > 0],
+                         ids=lambda c: c["name"])
+def test_resolver_golden(case):
+    h = R.Header(**case["header"])
+    weak = np.array(case["weak"], np.int32)
+    strong = np.frombuffer(bytes.fromhex(case["strong"]), np.uint8)
+    ev, lit, mat, _ = resolve(case["src_bytes"], h, weak, strong, case["seed_bytes"])
+    assert R.events_as_tuples(ev, h.block_length) == [tuple(e) for e in case["events"]]
+    assert (lit, mat) == (case["literal"], case["matched"])
+
+
+def _mutate(rng, basis, B, key):
+    kind = rng.randrange(8)
+    nb = len(basis)
+    if kind == 0 or nb < 8:
+        return basis
+    if kind == 1:
+        return O.splitmix(rng.randrange(1, 30 * B), key + 1).tobytes()
+    if kind == 2:  # insertion
+        a = rng.randrange(nb)
+        return basis[:a] + O.splitmix(rng.randrange(1, 14 * B), key + 2).tobytes() + basis[a:]
+    if kind == 3:  # deletion
+        a = rng.randrange(nb)
+        return basis[:a] + basis[min(nb, a + rng.randrange(1, 4 * B)):]
+    if kind == 4:  # block replacements (every other / random)
+        out = bytearray(basis)
+        for k in range(0, nb // B):
+            if rng.random() < 0.5:
+                out[k * B:(k + 1) * B] = O.splitmix(B, key + 10 + k).tobytes()
+        return bytes(out)
+    if kind == 5:  # weak-preserving tweaks (poison)
+        out = bytearray(basis)
+        for _ in range(rng.randrange(1, 4)):
+            i = rng.randrange(max(1, nb - 3))
+            x = [((v + 128) % 256) - 128 for v in out[i:i + 3]]
+            if len(x) == 3 and x[0] <= 126 and x[1] >= -126 and x[2] <= 126:
+                out[i], out[i + 1], out[i + 2] = (x[0] + 1) & 255, (x[1] - 2) & 255, (x[2] + 1) & 255
+        return bytes(out)
+    if kind == 6:  # long edit runs around 9B..11B (quirk A)
+        a = rng.randrange(nb)
+        return basis[:a] + O.splitmix(rng.randrange(8 * B, 12 * B), key + 3).tobytes() + basis[a:]
+    return basis[rng.randrange(nb):] + basis[:rng.randrange(nb)]
+
+
+@pytest.mark.parametrize("seed_i", range(12))
+def test_resolver_fuzz(seed_i):
+    rng = random.Random(1000 + seed_i)
+    for _ in range(12):
+        B = rng.choice([512, 512, 576, 1024, 2048])
+        nb = rng.randrange(1, 40 * B)
+        key = rng.randrange(1 << 62)
+        if rng.random() < 0.15:  # low entropy: repeated block patterns
+            blk = O.splitmix(B, key).tobytes()
+            basis = (blk * (nb // B + 1))[:nb]
+        else:
+            basis = O.splitmix(nb, key).tobytes()
+        src = _mutate(rng, basis, B, key)
+        if not src:
+            continue
+        dl = rng.choice([2, 2, 3, 4, 16])
+        check_case(basis, src, B, dl, bytes([1, 2, 3, 4]))
+
+
+def test_resolver_small_digest_collisions():
+    """dl = 2 with thousands of chunks: truncated-digest collisions give a non-empty stale-digest key
+    set (matches after poisoning), the rarest branch of the state machine."""
+    rng = random.Random(7)
+    hits = 0
+    for i in range(6):
+        B = 512
+        basis = O.splitmix(3000 * B, 99 + i).tobytes()
+        src = _mutate(rng, basis, B, 500 + i)
+        st = check_case(basis, src, B, 2, bytes([5, 6, 7, 8]))
+        hits += st["events"]
+    assert hits > 0
+
+
+def test_resolver_large_table_desync():
+    """65536-chunk table, dl = 2: an unmatched 10*B run desyncs the rolling sum (quirk A), random
+    table hits then occur under the desync, poison the cached digest (quirk B) and the truncated
+    digest collides with other chunks' digests (non-empty stale-digest key set)."""
+    B = 512
+    basis = O.splitmix(65536 * B, 101).tobytes()
+    src = basis[:3 * B] + O.splitmix(10 * B + 37, 3).tobytes() + basis[3 * B + 1:]
+    st = check_case(basis, src, B, 2, bytes([1, 2, 3, 4]))
+    assert st["flushes"] > 1000 and st["chain_matches"] == 3 and st["events"] >= 1
