@@ -127,6 +127,12 @@ int rsh_tokens_write(const uint8_t* src, const rsh_event* ev, int64_t n_ev, cons
 int64_t rsh_generator_bytes(const rsh_header* h, const int32_t* weak, const uint8_t* strong, uint8_t* out,
                             int64_t cap);
 
+/* ---- device buffers for the *_device entry points (callers without their own allocator, e.g. JNI) ---- */
+int rsh_dev_alloc(rsh_ctx* ctx, int64_t bytes, void** out);
+int rsh_dev_free(rsh_ctx* ctx, void* p);
+int rsh_memcpy_h2d(rsh_ctx* ctx, void* dst, const void* src, int64_t bytes);  /* synchronous */
+int rsh_memcpy_d2h(rsh_ctx* ctx, void* dst, const void* src, int64_t bytes);  /* synchronous */
+
 /* ---- synthetic input for benchmarks: splitmix64 counter stream generated on the device ---- */
 int rsh_fill_splitmix_device(rsh_ctx* ctx, void* d_out, int64_t n, uint64_t key, int64_t byte_offset);
 

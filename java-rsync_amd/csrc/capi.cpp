@@ -542,6 +542,35 @@ int64_t rsh_generator_bytes(const rsh_header* h, const int32_t* weak, const uint
     return size;
 }
 
+int rsh_dev_alloc(rsh_ctx* ctx, int64_t bytes, void** out) {
+    if (!ctx || !out || bytes < 0) return RSH_E_INVAL;
+    RSH_HIP(hipSetDevice(ctx->device));
+    return hipMalloc(out, (size_t)(bytes ? bytes : 1)) == hipSuccess ? RSH_OK : RSH_E_NOMEM;
+}
+
+int rsh_dev_free(rsh_ctx* ctx, void* p) {
+    if (!ctx) return RSH_E_INVAL;
+    RSH_HIP(hipSetDevice(ctx->device));
+    if (p) RSH_HIP(hipFree(p));
+    return RSH_OK;
+}
+
+int rsh_memcpy_h2d(rsh_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+    if (!ctx || bytes < 0 || (bytes > 0 && (!dst || !src))) return RSH_E_INVAL;
+    RSH_HIP(hipSetDevice(ctx->device));
+    RSH_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+    RSH_HIP(hipStreamSynchronize(ctx->stream));
+    return RSH_OK;
+}
+
+int rsh_memcpy_d2h(rsh_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+    if (!ctx || bytes < 0 || (bytes > 0 && (!dst || !src))) return RSH_E_INVAL;
+    RSH_HIP(hipSetDevice(ctx->device));
+    RSH_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, ctx->stream));
+    RSH_HIP(hipStreamSynchronize(ctx->stream));
+    return RSH_OK;
+}
+
 int rsh_fill_splitmix_device(rsh_ctx* ctx, void* d_out, int64_t n, uint64_t key, int64_t byte_offset) {
     if (!ctx || (n > 0 && !d_out) || n < 0 || byte_offset < 0) return RSH_E_INVAL;
     RSH_HIP(hipSetDevice(ctx->device));

@@ -192,6 +192,17 @@ void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveRe
             keys = &dkeys;
             none = dkeys.empty();
         }
+        if (none) {
+            // Stale digest that no chunk carries: no candidate can ever match again, so md5c and the
+            // state never change; only the flushes at mark + 9B remain (closed form, no device work).
+            while (m + 10 * B <= n) {
+                emit_lit(m, 10 * B);
+                m += 10 * B;
+                st.flushes++;
+            }
+            s = m;
+            break;
+        }
         int64_t p = -1;
         if (!none) {
             int64_t a = s;

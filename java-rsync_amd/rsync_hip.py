@@ -67,7 +67,7 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_device_count", "rsh_ctx_creat
            "rsh_ctx_stream", "rsh_block_length_for", "rsh_digest_length_for", "rsh_header_make",
            "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
            "rsh_match_scan_device", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
-           "rsh_fill_splitmix_device"]
+           "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 
 _LIB = None
 
@@ -109,6 +109,10 @@ def lib():
         "rsh_tokens_size": ([P, I64], I64),
         "rsh_tokens_write": ([P, P, I64, P, P, I64], ctypes.c_int),
         "rsh_generator_bytes": ([HP, P, P, P, I64], I64),
+        "rsh_dev_alloc": ([P, I64, ctypes.POINTER(P)], ctypes.c_int),
+        "rsh_dev_free": ([P, P], ctypes.c_int),
+        "rsh_memcpy_h2d": ([P, P, P, I64], ctypes.c_int),
+        "rsh_memcpy_d2h": ([P, P, P, I64], ctypes.c_int),
         "rsh_fill_splitmix_device": ([P, P, I64, ctypes.c_uint64, I64], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
@@ -234,6 +238,10 @@ class Context:
     def sync(self):
         _check(lib().rsh_ctx_sync(self._p))
 
+    def alloc(self, nbytes):
+        """Device buffer (DeviceBuffer) owned by this context's device."""
+        return DeviceBuffer(self, nbytes)
+
     def block_sums(self, data, h, seed):
         """Generator.sendItemizeAndChecksums hot loop: (weak int32[C], strong uint8[C*dl])."""
         a = _u8(data)
@@ -263,3 +271,35 @@ class Context:
                 continue
             _check(rc)
             return ev[:n_ev.value], fm.tobytes(), lit.value, mat.value, stats.as_dict()
+
+
+class DeviceBuffer:
+    """A hipMalloc'd buffer for the *_device entry points (no torch needed)."""
+
+    def __init__(self, ctx, nbytes):
+        self.ctx, self.nbytes = ctx, int(nbytes)
+        self.ptr = ctypes.c_void_p()
+        _check(lib().rsh_dev_alloc(ctx.handle, self.nbytes, ctypes.byref(self.ptr)))
+
+    def upload(self, arr, offset=0):
+        a = np.ascontiguousarray(arr)
+        _check(lib().rsh_memcpy_h2d(self.ctx.handle, ctypes.c_void_p(self.ptr.value + offset),
+                                    ctypes.c_void_p(a.ctypes.data), a.nbytes))
+
+    def download(self, nbytes=None, dtype=np.uint8, offset=0):
+        nbytes = self.nbytes - offset if nbytes is None else nbytes
+        out = np.empty(nbytes // np.dtype(dtype).itemsize, dtype)
+        _check(lib().rsh_memcpy_d2h(self.ctx.handle, ctypes.c_void_p(out.ctypes.data),
+                                    ctypes.c_void_p(self.ptr.value + offset), out.nbytes))
+        return out
+
+    def free(self):
+        if self.ptr:
+            lib().rsh_dev_free(self.ctx.handle, self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

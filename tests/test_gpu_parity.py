@@ -125,9 +125,38 @@ def test_sender_config_shapes(ctx, blen, dlen, mode):
 
 
 def test_device_fill_matches_oracle(ctx):
-    import torch
     n = (1 << 20) + 13
-    d = torch.empty(n, dtype=torch.uint8, device="cuda")
-    assert R.lib().rsh_fill_splitmix_device(ctx.handle, d.data_ptr(), n, 0x5EED5EED00000000, 0) == 0
+    d = ctx.alloc(n)
+    assert R.lib().rsh_fill_splitmix_device(ctx.handle, d.ptr, n, 0x5EED5EED00000000, 0) == 0
     ctx.sync()
-    assert np.array_equal(d.cpu().numpy(), O.splitmix(n, 0x5EED5EED00000000))
+    assert np.array_equal(d.download(), O.splitmix(n, 0x5EED5EED00000000))
+
+
+def test_device_resident_entry_points(ctx):
+    """rsh_block_sums_device + rsh_match_scan_device on device buffers == the host-buffer entry points."""
+    import ctypes
+    B, dl = 2048, 3
+    n = 300 * B + 17
+    d_basis, d_src = ctx.alloc(n), ctx.alloc(n + 5000)
+    R.lib().rsh_fill_splitmix_device(ctx.handle, d_basis.ptr, n, 11, 0)
+    R.lib().rsh_fill_splitmix_device(ctx.handle, d_src.ptr, n + 5000, 12, 0)
+    basis = d_basis.download()
+    src = np.concatenate([basis[:100 * B], d_src.download()[:5000], basis[100 * B:]])
+    d_src.upload(src)
+    h = R.header_make(B, dl, n)
+    d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
+    seed = np.frombuffer(SEED, np.uint8).copy()
+    assert R.lib().rsh_block_sums_device(ctx.handle, d_basis.ptr, n, ctypes.byref(h), seed.ctypes.data,
+                                         d_w.ptr, d_s.ptr) == 0
+    ctx.sync()
+    w, s = d_w.download(dtype=np.int32), d_s.download()
+    hw, hs = ctx.block_sums(basis, h, SEED)
+    assert np.array_equal(w, hw) and np.array_equal(s, hs)
+    ev = np.zeros(4096, R.EVENT_DTYPE)
+    n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    assert R.lib().rsh_match_scan_device(ctx.handle, d_src.ptr, src.size, ctypes.byref(h), d_w.ptr, d_s.ptr,
+                                         seed.ctypes.data, ev.ctypes.data, 4096, ctypes.byref(n_ev),
+                                         ctypes.byref(lit), ctypes.byref(mat), None) == 0
+    hev, fm, hlit, hmat, _ = ctx.match_scan(src, h, hw, hs, SEED)
+    assert R.events_as_tuples(ev[:n_ev.value], B) == R.events_as_tuples(hev, B)
+    assert (lit.value, mat.value) == (hlit, hmat)
