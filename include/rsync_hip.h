@@ -70,8 +70,9 @@ typedef struct {
     int64_t probe_launches;  /* range-probe kernel launches                                   */
     int64_t host_md5_windows;/* single-window digests computed on the host (resolver misses)  */
     int64_t flushes;         /* FileView.isFull flushes (Sender.java:1294-1302)                */
-    double device_ms;        /* time inside device work (kernels + copies) for this scan      */
-    double resolver_ms;      /* host resolver time                                             */
+    double device_ms;        /* wall time of the bulk device phase (speculation kernels + copies) */
+    double resolver_ms;      /* host resolver time (including its small device round trips)   */
+    double table_ms;         /* host sort of the received table (overlaps the device phase)   */
 } rsh_scan_stats;
 
 typedef struct rsh_ctx rsh_ctx;

@@ -42,6 +42,30 @@ struct DevBuf {
     }
 };
 
+// Page-locked host staging (true async D2H).
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipHostMalloc(&p, n ? n : 1, hipHostMallocDefault);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 uint32_t seed_word(const uint8_t seed[4]) {
     return (uint32_t)seed[0] | ((uint32_t)seed[1] << 8) | ((uint32_t)seed[2] << 16) | ((uint32_t)seed[3] << 24);
 }
@@ -64,10 +88,17 @@ struct rsh_ctx {
     DevBuf data, weak, strong;                   // host-input staging
     DevBuf src_weak, src_strong, flags;          // aligned speculation over the source
     DevBuf slots, dslots, dkeys, pos, out, first, win;
+    hipStream_t aux = nullptr;                   // basis-table download beside the speculation kernel
+    hipEvent_t ev_in = nullptr, ev_tab = nullptr;
+    PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
     ~rsh_ctx() {
         for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &slots, &dslots, &dkeys, &pos, &out,
                           &first, &win})
             b->release();
+        for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl}) b->release();
+        if (ev_in) (void)hipEventDestroy(ev_in);
+        if (ev_tab) (void)hipEventDestroy(ev_tab);
+        if (aux) (void)hipStreamDestroy(aux);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -90,15 +121,16 @@ class HipBackend : public rsh::ScanBackend {
         memcpy(seed_, seed, 4);
     }
     hipError_t err = hipSuccess;
-    std::vector<int32_t> aw;
-    std::vector<uint8_t> as;
-    std::vector<uint8_t> fl;
+    int64_t na = 0;
+    const int32_t* aw = nullptr;  // pinned host copies of the aligned speculation
+    const uint8_t* as = nullptr;
+    const uint8_t* fl = nullptr;
     rsh::ProbeTable table{};
 
-    int64_t aligned_count() override { return (int64_t)aw.size(); }
-    const int32_t* aligned_weak() override { return aw.data(); }
-    const uint8_t* aligned_strong() override { return as.data(); }
-    const uint8_t* chain_flags() override { return fl.data(); }
+    int64_t aligned_count() override { return na; }
+    const int32_t* aligned_weak() override { return aw; }
+    const uint8_t* aligned_strong() override { return as; }
+    const uint8_t* chain_flags() override { return fl; }
 
     int32_t weak_at(int64_t p) override {
         int32_t r = 0;
@@ -200,19 +232,47 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     const int64_t B = h->block_length;
     const int32_t C = h->chunk_count;
     const int32_t dl = h->digest_length;
-    std::vector<int32_t> hw;
-    std::vector<uint8_t> hs;
-    if (!host_weak || !host_strong) {
-        hw.resize(C > 0 ? C : 1);
-        hs.resize((size_t)C * dl + 1);
+    const int64_t na = (n + B - 1) / B;
+    if (na > 2147483647LL) return RSH_E_OVERFLOW;
+    const int64_t nf = std::min<int64_t>(na, C);
+
+    // (aux stream) the basis table, once whatever produced it on the main stream is done
+    RSH_HIP(hipEventRecord(c->ev_in, c->stream));
+    const bool download = !host_weak || !host_strong;
+    if (download) {
+        RSH_HIP(c->h_weak.ensure((size_t)C * 4 + 4));
+        RSH_HIP(c->h_strong.ensure((size_t)C * dl + 1));
+        RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
         if (C > 0) {
-            RSH_HIP(hipMemcpyAsync(hw.data(), d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, c->stream));
-            if (dl > 0)
-                RSH_HIP(hipMemcpyAsync(hs.data(), d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, c->stream));
+            RSH_HIP(hipMemcpyAsync(c->h_weak.p, d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, c->aux));
+            if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_strong.p, d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, c->aux));
         }
-        host_weak = hw.data();
-        host_strong = hs.data();
+        RSH_HIP(hipEventRecord(c->ev_tab, c->aux));
+        host_weak = c->h_weak.as<int32_t>();
+        host_strong = c->h_strong.as<uint8_t>();
     }
+
+    // (main stream) device probe table, then the aligned speculation: the source's own block sums
+    // with the basis header's B and dl, the chain flags, and their download
+    const uint32_t ns = pow2_at_least(2 * (uint64_t)C + 2);
+    RSH_HIP(c->slots.ensure((size_t)ns * sizeof(unsigned long long)));
+    RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, c->stream));
+    RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, c->stream));
+    RSH_HIP(c->src_weak.ensure((size_t)na * 4));
+    RSH_HIP(c->src_strong.ensure((size_t)na * dl + 1));
+    RSH_HIP(rsh::launch_block_sums(d_src, n, (uint32_t)B, (uint32_t)na, (uint32_t)dl, seed_word(seed),
+                                   c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->stream));
+    RSH_HIP(c->flags.ensure((size_t)nf + 1));
+    RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
+                                    (uint32_t)nf, (uint32_t)dl, c->flags.as<uint8_t>(), c->stream));
+    RSH_HIP(c->h_aw.ensure((size_t)na * 4));
+    RSH_HIP(c->h_as.ensure((size_t)na * dl + 1));
+    RSH_HIP(c->h_fl.ensure((size_t)nf + 1));
+    RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)na * 4, hipMemcpyDeviceToHost, c->stream));
+    if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)na * dl, hipMemcpyDeviceToHost, c->stream));
+    if (nf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)nf, hipMemcpyDeviceToHost, c->stream));
+
+    // (host) sort the table while the speculation kernel runs
     rsh::ChunkTable table;
     table.chunk_count = C;
     table.block_length = (int32_t)B;
@@ -220,42 +280,24 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     table.digest_length = dl;
     table.weak = host_weak;
     table.strong = host_strong;
-
-    // device probe table over the basis weak keys
-    const uint32_t ns = pow2_at_least(2 * (uint64_t)C + 2);
-    RSH_HIP(c->slots.ensure((size_t)ns * sizeof(unsigned long long)));
-    RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, c->stream));
-    RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, c->stream));
-
-    // aligned speculation: the source's own block sums with the basis header's B and dl
-    const int64_t na = (n + B - 1) / B;
-    if (na > 2147483647LL) return RSH_E_OVERFLOW;
-    RSH_HIP(c->src_weak.ensure((size_t)na * 4));
-    RSH_HIP(c->src_strong.ensure((size_t)na * dl + 1));
-    RSH_HIP(rsh::launch_block_sums(d_src, n, (uint32_t)B, (uint32_t)na, (uint32_t)dl, seed_word(seed),
-                                   c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->stream));
-    const int64_t nf = std::min<int64_t>(na, C);
-    RSH_HIP(c->flags.ensure((size_t)nf + 1));
-    RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
-                                    (uint32_t)nf, (uint32_t)dl, c->flags.as<uint8_t>(), c->stream));
+    if (download) RSH_HIP(hipEventSynchronize(c->ev_tab));
+    const auto t1 = std::chrono::steady_clock::now();
+    table.build();
+    const double table_ms = ms_since(t1);
+    RSH_HIP(hipStreamSynchronize(c->stream));
+    const double dev_ms = ms_since(t0);
 
     HipBackend be(c, d_src, n, table, seed);
     be.table.slots = c->slots.as<unsigned long long>();
     be.table.mask = ns - 1;
-    be.aw.resize((size_t)na);
-    be.as.resize((size_t)na * dl + 1);
-    be.fl.resize((size_t)nf + 1);
-    RSH_HIP(hipMemcpyAsync(be.aw.data(), c->src_weak.p, (size_t)na * 4, hipMemcpyDeviceToHost, c->stream));
-    if (dl > 0)
-        RSH_HIP(hipMemcpyAsync(be.as.data(), c->src_strong.p, (size_t)na * dl, hipMemcpyDeviceToHost, c->stream));
-    if (nf > 0) RSH_HIP(hipMemcpyAsync(be.fl.data(), c->flags.p, (size_t)nf, hipMemcpyDeviceToHost, c->stream));
-    table.build();  // host radix sort overlaps the device work above
-    RSH_HIP(hipStreamSynchronize(c->stream));
-    const double dev_ms = ms_since(t0);
-
+    be.na = na;
+    be.aw = c->h_aw.as<int32_t>();
+    be.as = c->h_as.as<uint8_t>();
+    be.fl = c->h_fl.as<uint8_t>();
     rsh::resolve_scan(n, table, be, res);
     if (be.err != hipSuccess) return RSH_E_DEVICE;
     res->stats.device_ms += dev_ms;
+    res->stats.table_ms += table_ms;
     return RSH_OK;
 }
 
@@ -311,7 +353,10 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
     rsh_ctx* c = new (std::nothrow) rsh_ctx();
     if (!c) return RSH_E_NOMEM;
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_tab, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return RSH_E_DEVICE;
     }

@@ -10,6 +10,10 @@ namespace rsh {
 hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks, uint32_t dl,
                              uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s);
 
+hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks,
+                                     uint32_t dl, uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong,
+                                     hipStream_t s);
+
 // Chain flags for the Sender fast path: flag[k] = 1 iff source window k (aligned, from the source's
 // own block sums) has the same weak key and the same dl-byte digest as basis chunk k.
 hipError_t launch_chain_flags(const int32_t* d_wsrc, const uint8_t* d_ssrc, const int32_t* d_wbas,

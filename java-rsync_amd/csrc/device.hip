@@ -8,6 +8,8 @@
 #include "device.h"
 #include "md5_core.h"
 
+#include <algorithm>
+
 namespace rsh {
 
 // ------------------------------------------------------------------------------------------------
@@ -73,16 +75,20 @@ __device__ __forceinline__ void unpack(const uint4 (&q)[4], uint32_t (&m)[16]) {
     }
 }
 
-template <int ALIGN>
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
+    const u32x4* v = reinterpret_cast<const u32x4*>(p);
+    const u32x4 t = NT ? __builtin_nontemporal_load(v) : *v;
+    return make_uint4(t.x, t.y, t.z, t.w);
+}
+
+template <int ALIGN, bool NT = true>
 __device__ __forceinline__ void load_block(const uint8_t* p, uint4 (&q)[4]) {
     if constexpr (ALIGN == 16) {
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4* v = reinterpret_cast<const u32x4*>(p);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const u32x4 t = __builtin_nontemporal_load(v + i);
-            q[i] = make_uint4(t.x, t.y, t.z, t.w);
-        }
+        for (int i = 0; i < 4; ++i) q[i] = ld16<NT>(p + 16 * i);
     } else if constexpr (ALIGN == 4) {
         const uint32_t* v = reinterpret_cast<const uint32_t*>(p);
 #pragma unroll
@@ -103,12 +109,12 @@ __device__ __forceinline__ void load_block(const uint8_t* p, uint4 (&q)[4]) {
 // the unit of parallelism); each lane streams its chunk 64 B at a time with a PF-deep register ring
 // of in-flight loads so HBM latency hides behind the MD5 rounds of the blocks already loaded.
 // ------------------------------------------------------------------------------------------------
-template <int ALIGN, int PF>
+template <int ALIGN, int PF, bool NT = true>
 __global__ __launch_bounds__(64) void block_sums_kernel(const uint8_t* __restrict__ data, int64_t n, uint32_t B,
                                                         uint32_t nchunks, uint32_t dl, uint32_t seed,
                                                         int32_t* __restrict__ weak_out,
-                                                        uint8_t* __restrict__ strong_out) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+                                                        uint8_t* __restrict__ strong_out, uint32_t c_first) {
+    const uint32_t c = c_first + blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= nchunks) return;
     const int64_t base = (int64_t)c * B;
     const int64_t rem = n - base;
@@ -121,7 +127,7 @@ __global__ __launch_bounds__(64) void block_sums_kernel(const uint8_t* __restric
     uint4 q[PF][4];
 #pragma unroll
     for (int j = 0; j < PF; ++j)
-        if ((uint32_t)j < nfull) load_block<ALIGN>(p + 64 * j, q[j]);
+        if ((uint32_t)j < nfull) load_block<ALIGN, NT>(p + 64 * j, q[j]);
 
     uint32_t i = 0;
     // Steady state: every consumed slot is refilled PF blocks ahead, unconditionally.
@@ -130,7 +136,7 @@ __global__ __launch_bounds__(64) void block_sums_kernel(const uint8_t* __restric
         for (int j = 0; j < PF; ++j) {
             uint32_t m[16];
             unpack(q[j], m);
-            load_block<ALIGN>(p + 64 * (size_t)(i + j + PF), q[j]);
+            load_block<ALIGN, NT>(p + 64 * (size_t)(i + j + PF), q[j]);
             weak_block(m, s1, u, 64 * (i + j));
             md5_compress(st, m);
         }
@@ -143,7 +149,7 @@ __global__ __launch_bounds__(64) void block_sums_kernel(const uint8_t* __restric
             if (blk < nfull) {
                 uint32_t m[16];
                 unpack(q[j], m);
-                if (blk + PF < nfull) load_block<ALIGN>(p + 64 * (size_t)(blk + PF), q[j]);
+                if (blk + PF < nfull) load_block<ALIGN, NT>(p + 64 * (size_t)(blk + PF), q[j]);
                 weak_block(m, s1, u, 64 * blk);
                 md5_compress(st, m);
             }
@@ -160,22 +166,309 @@ __global__ __launch_bounds__(64) void block_sums_kernel(const uint8_t* __restric
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// K1 (coalesced): one wave owns 64 consecutive full-length chunks (L = B, B % 128 == 0).  A stage is
+// the next 128 B of every chunk: 8 global_load_dwordx4 per lane, each instruction reading 8 whole
+// 128-B lines (8 lanes per line) instead of 64 scattered 16-B pieces; the wave transposes the stage
+// through LDS (row = 8 data slots + 1 pad slot, so the 16-lane ds_read_b128 groups and the 8-lane
+// ds_write_b128 groups are both bank-conflict free) and each lane then runs its chunk's MD5 over the
+// two 64-B blocks.  D stages stay in flight in registers.
+// ------------------------------------------------------------------------------------------------
+// Wave-local ordering of the stage transpose: LDS operations of one wave execute in order, so only
+// the compiler has to be kept from moving the lane-crossing ds_read above the ds_write (or the next
+// stage's ds_write above this stage's ds_read).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// MODE (diagnostics only, never in the production launch): 0 = real, 1 = compute only (no global
+// loads; stage data synthesised in registers), 2 = loads only (no MD5/weak; words xor-folded).
+template <int D, bool NT, int WAVES = 1, int MODE = 0>
+__global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const uint8_t* __restrict__ data, uint32_t B,
+                                                                  uint32_t dl, uint32_t seed,
+                                                                  int32_t* __restrict__ weak_out,
+                                                                  uint8_t* __restrict__ strong_out) {
+    constexpr int ROW = 9;
+    extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // sized at launch (occupancy control)
+    const int l = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    uint4* lds = lds_all + wv * 64 * ROW;
+    const uint32_t c0 = (blockIdx.x * WAVES + wv) * 64u;
+    const uint32_t nst = B >> 7;
+    const uint8_t* lp = data + ((size_t)c0 + (size_t)(l >> 3)) * B + 16 * (l & 7);
+    const size_t jstride = (size_t)8 * B;
+    const int wr0 = (l >> 3) * ROW + (l & 7);
+    const int rd0 = l * ROW;
+
+    uint4 q[D][8];
+    uint32_t fold = 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        if ((uint32_t)d < nst) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if constexpr (MODE == 1) q[d][j] = make_uint4(l + d, j, c0, 7);
+                else q[d][j] = ld16<NT>(lp + 128 * (size_t)d + j * jstride);
+            }
+        }
+    Md5State st = md5_init();
+    int32_t s1 = 0, u = 0;
+    for (uint32_t s = 0; s < nst; s += D) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const uint32_t si = s + d;
+            if (si < nst) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) lds[wr0 + j * 8 * ROW] = q[d][j];
+                if (si + D < nst) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        if constexpr (MODE == 1) q[d][j] = make_uint4(q[d][j].y + si, q[d][j].x, q[d][j].w ^ si, q[d][j].z);
+                        else q[d][j] = ld16<NT>(lp + 128 * (size_t)(si + D) + j * jstride);
+                    }
+                }
+                if constexpr (WAVES == 1) __syncthreads();
+                else wave_lds_sync();
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    uint4 r[4];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) r[k] = lds[rd0 + 4 * h + k];
+                    uint32_t m[16];
+                    unpack(r, m);
+                    if constexpr (MODE == 2) {
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) fold ^= m[k];
+                    } else {
+                        weak_block(m, s1, u, 128 * si + 64 * h);
+                        md5_compress(st, m);
+                    }
+                }
+                if constexpr (WAVES == 1) __syncthreads();
+                else wave_lds_sync();
+            }
+        }
+    }
+    // final block: seed || 0x80 || zero pad || bit length of (B + 4) bytes
+    {
+        const uint64_t bits = ((uint64_t)B + 4) * 8;
+        uint32_t m[16] = {seed, 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, (uint32_t)bits, (uint32_t)(bits >> 32)};
+        md5_compress(st, m);
+    }
+    const uint32_t c = c0 + l;
+    if constexpr (MODE == 2) st.a ^= fold;
+    const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
+    weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
+    uint8_t* o = strong_out + (size_t)c * dl;
+    for (uint32_t k = 0; k < dl; ++k) {
+        const uint32_t word = k < 4 ? st.a : k < 8 ? st.b : k < 12 ? st.c : st.d;
+        o[k] = (uint8_t)(word >> (8 * (k & 3)));
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K1 (LDS-DMA): as the coalesced kernel, but each stage goes HBM -> LDS directly with
+// global_load_lds_dwordx4 (no VGPR staging, no ds_write).  LDS-DMA writes lane l's 16 B at slot
+// base + l, so the lane -> (chunk, piece) mapping of each DMA instruction fixes the layout: in
+// instruction j lane l fetches chunk c = 8j + (l >> 3), piece q = (l & 7) ^ ((c >> 1) & 7), which puts
+// (c, q) at slot 8c + (q ^ ((c >> 1) & 7)): the transposed ds_read_b128 (lane c, piece k) then hits 16
+// distinct bank quads in every 16-lane group.  S stages of 8 KiB ring per wave.
+// ------------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <int S>
+__global__ __launch_bounds__(64) void block_sums_dma_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
+                                                            uint32_t seed, int32_t* __restrict__ weak_out,
+                                                            uint8_t* __restrict__ strong_out) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lds_ring[];  // S * 512 slots
+    const int l = threadIdx.x;
+    const uint32_t c0 = blockIdx.x * 64u;
+    const uint32_t nst = B >> 7;
+    const uint8_t* wbase = data + (size_t)c0 * B;
+    // per-lane byte offsets for even / odd DMA instructions (the swizzle depends on j & 1 only)
+    const uint32_t row = (uint32_t)(l >> 3) * B;
+    const uint32_t voff0 = row + 16u * ((uint32_t)(l & 7) ^ (uint32_t)((l >> 4) & 7));
+    const uint32_t voff1 = row + 16u * ((uint32_t)(l & 7) ^ (uint32_t)((4 + (l >> 4)) & 7));
+    const size_t jstride = (size_t)8 * B;
+    auto issue = [&](uint32_t st) {
+        uint4* ring = lds_ring + (st % S) * 512;
+        const uint8_t* g = wbase + 128 * (size_t)st;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            __builtin_amdgcn_global_load_lds(g + j * jstride + ((j & 1) ? voff1 : voff0),
+                                             (lds_void_t*)(ring + 64 * j), 16, 0, 0);
+    };
+    const int sw = (l >> 1) & 7;
+#pragma unroll
+    for (int d = 0; d < S; ++d)
+        if ((uint32_t)d < nst) issue(d);
+
+    Md5State st = md5_init();
+    int32_t s1 = 0, u = 0;
+    for (uint32_t s = 0; s < nst; ++s) {
+        // stage s landed once at most (S - 1) later stages (8 DMA instructions each) are outstanding
+        const uint32_t ahead = nst - 1 - s < (uint32_t)(S - 1) ? nst - 1 - s : (uint32_t)(S - 1);
+        switch (ahead) {
+            case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+            case 1: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+            case 2: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+            default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+        }
+        const uint4* ring = lds_ring + (s % S) * 512 + 8 * l;
+        uint4 r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = ring[k ^ sw];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free before it is refilled
+        if (s + S < nst) issue(s + S);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint32_t m[16];
+            unpack(*reinterpret_cast<const uint4(*)[4]>(&r[4 * h]), m);
+            weak_block(m, s1, u, 128 * s + 64 * h);
+            md5_compress(st, m);
+        }
+    }
+    {
+        const uint64_t bits = ((uint64_t)B + 4) * 8;
+        uint32_t m[16] = {seed, 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, (uint32_t)bits, (uint32_t)(bits >> 32)};
+        md5_compress(st, m);
+    }
+    const uint32_t c = c0 + l;
+    const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
+    weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
+    uint8_t* o = strong_out + (size_t)c * dl;
+    for (uint32_t k = 0; k < dl; ++k) {
+        const uint32_t word = k < 4 ? st.a : k < 8 ? st.b : k < 12 ? st.c : st.d;
+        o[k] = (uint8_t)(word >> (8 * (k & 3)));
+    }
+}
+
+constexpr uint32_t kCUs = 256;            // MI355X compute units
+constexpr uint32_t kLdsPerCU = 160 * 1024; // bytes
+
+// Dynamic LDS above 64 KiB must be enabled per kernel.
+template <class K>
+void allow_full_lds(K kernel) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kLdsPerCU);
+}
+
+// variant: -1 = production choice; 0..2 per-lane (NT PF4, plain PF4, NT PF8); 3..6 coalesced
+// (D=2 NT, D=3 NT, D=2 plain, D=4 NT).  Non-coalesced variants handle every chunk shape.
+hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks,
+                                     uint32_t dl, uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong,
+                                     hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    const uintptr_t addr = reinterpret_cast<uintptr_t>(d_data);
+    if (variant < 0) variant = 4;
+    uint32_t c_first = 0;
+    if (variant >= 3 && (B % 128) == 0 && (addr % 16) == 0) {
+        const uint32_t nfullc = (uint32_t)std::min<int64_t>(n / B, nchunks);  // chunks with L == B
+        const uint32_t waves = nfullc / 64;
+        const size_t wave_lds = 64 * 9 * sizeof(uint4);
+        // LDS per workgroup chosen so that the dispatcher can place at most ceil(groups / CUs) groups
+        // on a CU: every SIMD then holds the same number of equal-work waves (no stacking imbalance).
+        auto lds_for = [&](uint32_t groups, uint32_t waves_per_group) -> size_t {
+            const uint32_t per_cu = std::max<uint32_t>(1, (groups + kCUs - 1) / kCUs);
+            size_t bytes = (size_t)kLdsPerCU / per_cu;
+            bytes &= ~(size_t)255;
+            return std::max(bytes, wave_lds * waves_per_group);
+        };
+        if ((variant == 7 || variant == 8) && waves >= 4) {
+            const uint32_t groups = waves / 4;
+            const size_t lb = lds_for(groups, 4);
+            if (variant == 8) {
+                allow_full_lds(block_sums_coalesced_kernel<2, false, 4>);
+                hipLaunchKernelGGL((block_sums_coalesced_kernel<2, false, 4>), dim3(groups), dim3(256), lb, s, d_data,
+                                   B, dl, seed_word, d_weak, d_strong);
+            } else {
+                allow_full_lds(block_sums_coalesced_kernel<3, false, 4>);
+                hipLaunchKernelGGL((block_sums_coalesced_kernel<3, false, 4>), dim3(groups), dim3(256), lb, s, d_data,
+                                   B, dl, seed_word, d_weak, d_strong);
+            }
+            c_first = groups * 256;
+            variant = 0;
+        } else if (waves > 0) {
+            const size_t lb = variant == 9 ? lds_for(waves, 1) : wave_lds;
+            switch (variant) {
+                case 3:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true>), dim3(waves), dim3(64), lb, s, d_data, B,
+                                       dl, seed_word, d_weak, d_strong);
+                    break;
+                case 5:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, false>), dim3(waves), dim3(64), lb, s, d_data,
+                                       B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 6:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<4, true>), dim3(waves), dim3(64), lb, s, d_data, B,
+                                       dl, seed_word, d_weak, d_strong);
+                    break;
+                case 13:
+                    hipLaunchKernelGGL((block_sums_dma_kernel<2>), dim3(waves), dim3(64), 2 * 512 * 16, s, d_data, B,
+                                       dl, seed_word, d_weak, d_strong);
+                    break;
+                case 14:
+                    hipLaunchKernelGGL((block_sums_dma_kernel<3>), dim3(waves), dim3(64), 3 * 512 * 16, s, d_data, B,
+                                       dl, seed_word, d_weak, d_strong);
+                    break;
+                case 15:
+                    hipLaunchKernelGGL((block_sums_dma_kernel<4>), dim3(waves), dim3(64), 4 * 512 * 16, s, d_data, B,
+                                       dl, seed_word, d_weak, d_strong);
+                    break;
+                case 10:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, false, 1, 1>), dim3(waves), dim3(64), lb, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 11:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, false, 1, 2>), dim3(waves), dim3(64), lb, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 12:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<4, false, 1, 2>), dim3(waves), dim3(64), lb, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 9:
+                    allow_full_lds(block_sums_coalesced_kernel<3, false>);
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, false>), dim3(waves), dim3(64), lb, s, d_data,
+                                       B, dl, seed_word, d_weak, d_strong);
+                    break;
+                default:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true>), dim3(waves), dim3(64), lb, s, d_data, B,
+                                       dl, seed_word, d_weak, d_strong);
+            }
+            c_first = waves * 64;
+        }
+        variant = 0;
+    }
+    if (c_first >= nchunks) return hipGetLastError();
+    const uint32_t rest = nchunks - c_first;
+    const dim3 block(64);
+    const dim3 grid((rest + 63) / 64);
+    if ((B % 16) == 0 && (addr % 16) == 0) {
+        if (variant == 1)
+            hipLaunchKernelGGL((block_sums_kernel<16, 4, false>), grid, block, 0, s, d_data, n, B, nchunks, dl,
+                               seed_word, d_weak, d_strong, c_first);
+        else if (variant == 2)
+            hipLaunchKernelGGL((block_sums_kernel<16, 8, true>), grid, block, 0, s, d_data, n, B, nchunks, dl,
+                               seed_word, d_weak, d_strong, c_first);
+        else
+            hipLaunchKernelGGL((block_sums_kernel<16, 4, true>), grid, block, 0, s, d_data, n, B, nchunks, dl,
+                               seed_word, d_weak, d_strong, c_first);
+    } else if ((B % 4) == 0 && (addr % 4) == 0) {
+        hipLaunchKernelGGL((block_sums_kernel<4, 2>), grid, block, 0, s, d_data, n, B, nchunks, dl, seed_word, d_weak,
+                           d_strong, c_first);
+    } else {
+        hipLaunchKernelGGL((block_sums_kernel<1, 1>), grid, block, 0, s, d_data, n, B, nchunks, dl, seed_word, d_weak,
+                           d_strong, c_first);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks, uint32_t dl,
                              uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s) {
-    if (nchunks == 0) return hipSuccess;
-    const dim3 block(64);
-    const dim3 grid((nchunks + 63) / 64);
-    const uintptr_t addr = reinterpret_cast<uintptr_t>(d_data);
-    if ((B % 16) == 0 && (addr % 16) == 0)
-        hipLaunchKernelGGL((block_sums_kernel<16, 4>), grid, block, 0, s, d_data, n, B, nchunks, dl, seed_word,
-                           d_weak, d_strong);
-    else if ((B % 4) == 0 && (addr % 4) == 0)
-        hipLaunchKernelGGL((block_sums_kernel<4, 2>), grid, block, 0, s, d_data, n, B, nchunks, dl, seed_word,
-                           d_weak, d_strong);
-    else
-        hipLaunchKernelGGL((block_sums_kernel<1, 1>), grid, block, 0, s, d_data, n, B, nchunks, dl, seed_word,
-                           d_weak, d_strong);
-    return hipGetLastError();
+    return launch_block_sums_variant(-1, d_data, n, B, nchunks, dl, seed_word, d_weak, d_strong, s);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -252,12 +545,108 @@ __device__ __forceinline__ bool table_has(const ProbeTable& t, uint32_t key) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Probe: first position in [a, b) whose Sender rolling key hits the table.  One workgroup per
-// aligned block [kB, kB + B); 256 lanes each own a contiguous segment of positions.  Lane start sums
-// come from a workgroup scan of per-segment byte sums of the two streams x[p] and x[p + B] (prefix
-// identities in the header comment of device.h), then each lane rolls with the exact Java updates.
+// Weighted byte sums over a range: S1 = sum x_j, S2 = sum (j - org) * x_j (signed bytes, mod 2^32),
+// accumulated by one workgroup with 16-byte loads where the range is 16-aligned.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void dword_sums(uint32_t w, uint32_t rel, int32_t& s1, int32_t& s2) {
+    const int32_t a = __builtin_amdgcn_sdot4((int)w, 0x01010101, 0, false);
+    s1 += a;
+    s2 += (int32_t)(rel * (uint32_t)a) + __builtin_amdgcn_sdot4((int)w, 0x03020100, 0, false);
+}
+
+// Sums of bytes [lo, hi) (clipped to [0, n)) relative to origin org, over all threads of the block.
+// Returns this thread's partial; the caller reduces.
+__device__ __forceinline__ void range_sums(const uint8_t* __restrict__ x, int64_t n, int64_t lo, int64_t hi, int64_t org,
+                                           int32_t& s1, int32_t& s2) {
+    if (hi > n) hi = n;
+    if (lo >= hi) return;
+    const int t = threadIdx.x, T = blockDim.x;
+    int64_t a16 = (lo + 15) & ~(int64_t)15;
+    if (a16 > hi) a16 = hi;
+    const int64_t b16 = a16 + ((hi - a16) & ~(int64_t)15);
+    for (int64_t j = lo + t; j < a16; j += T) {  // unaligned head
+        const int32_t v = sbyte(x[j]);
+        s1 += v;
+        s2 += (int32_t)((uint32_t)(j - org) * (uint32_t)v);
+    }
+    for (int64_t j = a16 + 16 * (int64_t)t; j < b16; j += 16 * (int64_t)T) {
+        const uint4 v = *reinterpret_cast<const uint4*>(x + j);
+        const uint32_t rel = (uint32_t)(j - org);
+        dword_sums(v.x, rel, s1, s2);
+        dword_sums(v.y, rel + 4, s1, s2);
+        dword_sums(v.z, rel + 8, s1, s2);
+        dword_sums(v.w, rel + 12, s1, s2);
+    }
+    for (int64_t j = b16 + t; j < hi; j += T) {  // tail
+        const int32_t v = sbyte(x[j]);
+        s1 += v;
+        s2 += (int32_t)((uint32_t)(j - org) * (uint32_t)v);
+    }
+}
+
+template <int NV>
+__device__ __forceinline__ void block_reduce(int32_t (&v)[NV], int32_t* sh /* NV * blockDim / 64 */) {
+    const int t = threadIdx.x, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        int32_t x = v[i];
+        for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+        v[i] = x;
+    }
+    __syncthreads();
+    if ((t & 63) == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) sh[i * nw + (t >> 6)] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        int32_t x = 0;
+        for (int w = 0; w < nw; ++w) x += sh[i * nw + w];
+        v[i] = x;
+    }
+    __syncthreads();
+}
+
+// exclusive scan over the block's threads (thread order), NV values at once
+template <int NV>
+__device__ __forceinline__ void block_exscan(int32_t (&v)[NV], int32_t* sh /* NV * blockDim / 64 */) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, nw = blockDim.x >> 6;
+    int32_t incl[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        int32_t x = v[i];
+        for (int d = 1; d < 64; d <<= 1) {
+            const int32_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        incl[i] = x;
+    }
+    __syncthreads();
+    if (lane == 63)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) sh[i * nw + wv] = incl[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        int32_t base = 0;
+        for (int w = 0; w < wv; ++w) base += sh[i * nw + w];
+        v[i] = base + incl[i] - v[i];
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Probe: first position in [a, b) whose Sender rolling key hits the table.  Positions are tiled in
+// aligned-block coordinates (block k = [kB, kB + B), tile = 4096 positions); one 256-lane workgroup per
+// tile, 16 positions per lane.  With o = kB and P1/P2 the prefix sums of x and (j - o) x from o:
+//   T(p) = (s1, s2),  s1 = P1(e) - P1(p),  s2 = (e - o) s1 - (P2(e) - P2(p)),  e = min(p + B, n),
+// and P1(o + B) = s1(o), P2(o + B) = B s1(o) - s2(o) from the source's own aligned sum T(o).  Lane start
+// values come from the workgroup's prefix of both streams (x[p] and x[p + B]); each lane then rolls its
+// 16 positions with the exact Java updates (Rolling.java:25-60) on R = T + E.
 // ------------------------------------------------------------------------------------------------
 constexpr int PROBE_THREADS = 256;
+constexpr int PROBE_PPT = 16;
+constexpr int PROBE_TILE = PROBE_THREADS * PROBE_PPT;
 
 __device__ __forceinline__ int32_t roll_sub(int32_t cs, int32_t w, int32_t x) {  // Rolling.java:56-60
     const uint32_t lo = ((uint32_t)cs & 0xFFFFu) - (uint32_t)x;
@@ -270,85 +659,78 @@ __device__ __forceinline__ int32_t roll_add(int32_t cs, int32_t x) {  // Rolling
     return (int32_t)((lo & 0xFFFFu) | (hi << 16));
 }
 
-__global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A, int64_t k0) {
-    const int64_t k = k0 + blockIdx.x;
-    const int64_t o = k * (int64_t)A.B;
-    const int64_t n = A.n;
-    const int64_t B = A.B;
-    const int64_t lo_pos = A.a > o ? A.a : o;
-    const int64_t hi_pos = A.b < o + B ? A.b : o + B;
-    if (lo_pos >= hi_pos) return;  // uniform over the workgroup
+__device__ __forceinline__ void load16(const uint8_t* __restrict__ x, int64_t n, int64_t p, uint8_t (&v)[16]) {
+    if (p + 16 <= n && ((reinterpret_cast<uintptr_t>(x + p) & 15) == 0)) {
+        const uint4 q = *reinterpret_cast<const uint4*>(x + p);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = (p + i < n && p + i >= 0) ? x[p + i] : (uint8_t)0;
+    }
+}
+
+__global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A, int64_t k0, uint32_t tiles_per_block) {
+    __shared__ int32_t sh[4 * PROBE_THREADS / 64];
+    const int64_t n = A.n, B = A.B;
+    const int64_t k = k0 + blockIdx.x / tiles_per_block;
+    const int64_t o = k * B;
+    const int64_t q0 = o + (int64_t)(blockIdx.x % tiles_per_block) * PROBE_TILE;
+    int64_t qend = q0 + PROBE_TILE;
+    if (qend > o + B) qend = o + B;
+    if (q0 >= A.b || qend <= A.a || q0 >= n) return;  // uniform over the workgroup
+
+    // prefix of both streams from the block origin up to the tile
+    int32_t head[4] = {0, 0, 0, 0};
+    range_sums(A.data, n, o, q0, o, head[0], head[1]);
+    range_sums(A.data, n, o + B, q0 + B, o, head[2], head[3]);
+    block_reduce<4>(head, sh);
 
     const int t = threadIdx.x;
-    const int64_t seg = (B + PROBE_THREADS - 1) / PROBE_THREADS;
-    const int64_t q = o + t * seg;
-    const int64_t qend_a = (q + seg < n ? q + seg : n);
+    const int64_t p0 = q0 + (int64_t)t * PROBE_PPT;
+    uint8_t xa[16], xb[16];
+    load16(A.data, n, p0, xa);
+    load16(A.data, n, p0 + B, xb);
+    int32_t part[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int32_t va = (p0 + i < n) ? sbyte(xa[i]) : 0;
+        const int32_t vb = (p0 + B + i < n) ? sbyte(xb[i]) : 0;
+        part[0] += va;
+        part[1] += (int32_t)((uint32_t)(p0 + i - o) * (uint32_t)va);
+        part[2] += vb;
+        part[3] += (int32_t)((uint32_t)(p0 + B + i - o) * (uint32_t)vb);
+    }
+    int32_t pre[4] = {part[0], part[1], part[2], part[3]};
+    block_exscan<4>(pre, sh);
+    if (p0 >= qend || p0 >= A.b || p0 + PROBE_PPT <= A.a) return;
 
-    // per-segment sums of stream A: [q, q+seg) and stream B: [q+B, q+B+seg), both clipped at n
-    int32_t sa = 0, sa2 = 0, sb = 0, sb2 = 0;
-    for (int64_t j = q; j < qend_a; ++j) {
-        const int32_t x = sbyte(A.data[j]);
-        sa += x;
-        sa2 += (int32_t)((uint32_t)(j - o) * (uint32_t)x);
-    }
-    const int64_t qb = q + B;
-    const int64_t qend_b = (qb + seg < n ? qb + seg : n);
-    for (int64_t j = qb; j < qend_b; ++j) {
-        const int32_t x = sbyte(A.data[j]);
-        sb += x;
-        sb2 += (int32_t)((uint32_t)(j - o) * (uint32_t)x);
-    }
-    // exclusive scan over lanes (simple LDS Hillis-Steele; 4 values)
-    __shared__ int32_t sh[4][PROBE_THREADS];
-    sh[0][t] = sa;
-    sh[1][t] = sa2;
-    sh[2][t] = sb;
-    sh[3][t] = sb2;
-    __syncthreads();
-    for (int d = 1; d < PROBE_THREADS; d <<= 1) {
-        int32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
-        if (t >= d) {
-            v0 = sh[0][t - d];
-            v1 = sh[1][t - d];
-            v2 = sh[2][t - d];
-            v3 = sh[3][t - d];
-        }
-        __syncthreads();
-        sh[0][t] += v0;
-        sh[1][t] += v1;
-        sh[2][t] += v2;
-        sh[3][t] += v3;
-        __syncthreads();
-    }
-    const int32_t pa = sh[0][t] - sa, pa2 = sh[1][t] - sa2;  // P1'(q), P2'(q)
-    const int32_t pb = sh[2][t] - sb, pb2 = sh[3][t] - sb2;  // sums over [o+B, q+B) clipped
-    if (q >= hi_pos || q >= n) return;
-
-    // T(o) -> P1'(e0), P2'(e0) with e0 = min(o + B, n)
+    const uint32_t pa = (uint32_t)(head[0] + pre[0]), pa2 = (uint32_t)(head[1] + pre[1]);  // P1(p0), P2(p0)
+    const uint32_t pb = (uint32_t)(head[2] + pre[2]), pb2 = (uint32_t)(head[3] + pre[3]);  // sums over [o+B, p0+B)
     const int32_t To = A.aligned_weak[k];
     const int64_t e0 = (o + B < n ? o + B : n);
-    const uint32_t s1o = (uint32_t)To & 0xFFFFu;
-    const uint32_t s2o = (uint32_t)To >> 16;
-    const uint32_t P1e = s1o + (uint32_t)pb;
-    const uint32_t P2e = (uint32_t)(e0 - o) * s1o - s2o + (uint32_t)pb2;
-    const int64_t endq = (q + B < n ? q + B : n);
-    const uint32_t s1 = P1e - (uint32_t)pa;
-    const uint32_t s2 = (uint32_t)(endq - o) * s1 - (P2e - (uint32_t)pa2);
-    // R(q) = T(q) + E(q)
+    const uint32_t s1o = (uint32_t)To & 0xFFFFu, s2o = (uint32_t)To >> 16;
+    const uint32_t P1e = s1o + pb;
+    const uint32_t P2e = (uint32_t)(e0 - o) * s1o - s2o + pb2;
+    const int64_t endq = (p0 + B < n ? p0 + B : n);
+    const uint32_t s1 = P1e - pa;
+    const uint32_t s2 = (uint32_t)(endq - o) * s1 - (P2e - pa2);
     const int64_t nb = n - B;
     auto clampB = [&](int64_t p) { return p < nb ? p : nb; };
-    const uint32_t ehi = A.e_hi + A.e_lo * (uint32_t)(clampB(q) - clampB(A.anchor));
+    const uint32_t ehi = A.e_hi + A.e_lo * (uint32_t)(clampB(p0) - clampB(A.anchor));
     int32_t R = (int32_t)(((s1 + A.e_lo) & 0xFFFFu) | ((s2 + ehi) << 16));
-
-    const int64_t pend = (q + seg < hi_pos ? q + seg : hi_pos);
-    for (int64_t p = q; p < pend; ++p) {
-        if (p >= lo_pos && table_has(A.table, (uint32_t)R)) {
+#pragma unroll
+    for (int i = 0; i < PROBE_PPT; ++i) {
+        const int64_t p = p0 + i;
+        if (p >= A.b || p >= qend) break;
+        if (p >= A.a && table_has(A.table, (uint32_t)R)) {
             atomicMin(A.first, (unsigned long long)p);
             return;
         }
         const int64_t w = (n - p < B ? n - p : B);
-        R = roll_sub(R, (int32_t)w, sbyte(A.data[p]));
-        if (n - (p + 1) >= B) R = roll_add(R, sbyte(A.data[p + B]));
+        R = roll_sub(R, (int32_t)w, sbyte(xa[i]));
+        if (n - (p + 1) >= B) R = roll_add(R, sbyte(xb[i]));
     }
 }
 
@@ -358,37 +740,26 @@ hipError_t launch_probe_first(const ProbeArgs& args, hipStream_t s) {
     if (args.a >= args.b) return hipSuccess;
     const int64_t k0 = args.a / args.B;
     const int64_t k1 = (args.b - 1) / args.B;
-    hipLaunchKernelGGL(probe_first_kernel, dim3((uint32_t)(k1 - k0 + 1)), dim3(PROBE_THREADS), 0, s, args, k0);
+    const uint32_t tpb = (uint32_t)((args.B + PROBE_TILE - 1) / PROBE_TILE);
+    const int64_t grid = (k1 - k0 + 1) * (int64_t)tpb;
+    hipLaunchKernelGGL(probe_first_kernel, dim3((uint32_t)grid), dim3(PROBE_THREADS), 0, s, args, k0, tpb);
     return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------------
-// True weak sums at arbitrary positions (one workgroup per position, wave-reduced).
+// True weak sums at arbitrary positions (one workgroup per position).
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void window_weak_kernel(const uint8_t* __restrict__ data, int64_t n, uint32_t B,
                                                           const int64_t* __restrict__ pos, int32_t* __restrict__ out) {
+    __shared__ int32_t sh[2 * 256 / 64];
     const int64_t p = pos[blockIdx.x];
     const int64_t w = (n - p < (int64_t)B ? n - p : (int64_t)B);
-    int32_t s1 = 0, u = 0;
-    for (int64_t i = threadIdx.x; i < w; i += blockDim.x) {
-        const int32_t x = sbyte(data[p + i]);
-        s1 += x;
-        u += (int32_t)((uint32_t)i * (uint32_t)x);
-    }
-    __shared__ int32_t r1[256], r2[256];
-    r1[threadIdx.x] = s1;
-    r2[threadIdx.x] = u;
-    __syncthreads();
-    for (int d = 128; d > 0; d >>= 1) {
-        if ((int)threadIdx.x < d) {
-            r1[threadIdx.x] += r1[threadIdx.x + d];
-            r2[threadIdx.x] += r2[threadIdx.x + d];
-        }
-        __syncthreads();
-    }
+    int32_t v[2] = {0, 0};
+    range_sums(data, n, p, p + w, p, v[0], v[1]);
+    block_reduce<2>(v, sh);
     if (threadIdx.x == 0) {
-        const uint32_t S1 = (uint32_t)r1[0];
-        const uint32_t S2 = (uint32_t)w * S1 - (uint32_t)r2[0];
+        const uint32_t S1 = (uint32_t)v[0];
+        const uint32_t S2 = (uint32_t)w * S1 - (uint32_t)v[1];
         out[blockIdx.x] = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
     }
 }

@@ -30,6 +30,22 @@ RSH_HD uint32_t rotl32(uint32_t x, int s) { return (x << s) | (x >> (32 - s)); }
 #define RSH_MD5_I(x, y, z) ((y) ^ ((x) | ~(z)))
 #define RSH_MD5_STEP(f, a, b, c, d, m, k, s) (a) = (b) + rsh::rotl32((a) + f((b), (c), (d)) + (m) + (k), (s))
 
+#if defined(__HIP_DEVICE_COMPILE__) && defined(__gfx950__)
+// Round 3 on gfx950: one v_bitop3_b32 (0x96 = x ^ y ^ z) -- the backend canonicalises every XOR3 form
+// to two v_xor_b32.  t = a + m + k is formed off the critical path; only H + t, the rotate and the
+// final add depend on the previous step.
+__device__ __forceinline__ uint32_t rsh_h_plus(uint32_t t, uint32_t x, uint32_t y, uint32_t z) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %2, %3, %4 bitop3:0x96\n\tv_add_u32_e32 %0, %1, %0"
+        : "=&v"(r)
+        : "v"(t), "v"(x), "v"(y), "v"(z));
+    return r;
+}
+#define RSH_MD5_STEP3(a, b, c, d, m, k, s) (a) = (b) + rsh::rotl32(rsh_h_plus((a) + (m) + (k), (b), (c), (d)), (s))
+#else
+#define RSH_MD5_STEP3(a, b, c, d, m, k, s) RSH_MD5_STEP(RSH_MD5_H, a, b, c, d, m, k, s)
+#endif
+
 // One 64-byte block; m[0..15] are the little-endian message words.
 RSH_HD void md5_compress(Md5State& st, const uint32_t (&m)[16]) {
     uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
@@ -67,22 +83,22 @@ RSH_HD void md5_compress(Md5State& st, const uint32_t (&m)[16]) {
     RSH_MD5_STEP(RSH_MD5_G, c, d, a, b, m[7], 0x676f02d9u, 14);
     RSH_MD5_STEP(RSH_MD5_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
 
-    RSH_MD5_STEP(RSH_MD5_H, a, b, c, d, m[5], 0xfffa3942u, 4);
-    RSH_MD5_STEP(RSH_MD5_H, d, a, b, c, m[8], 0x8771f681u, 11);
-    RSH_MD5_STEP(RSH_MD5_H, c, d, a, b, m[11], 0x6d9d6122u, 16);
-    RSH_MD5_STEP(RSH_MD5_H, b, c, d, a, m[14], 0xfde5380cu, 23);
-    RSH_MD5_STEP(RSH_MD5_H, a, b, c, d, m[1], 0xa4beea44u, 4);
-    RSH_MD5_STEP(RSH_MD5_H, d, a, b, c, m[4], 0x4bdecfa9u, 11);
-    RSH_MD5_STEP(RSH_MD5_H, c, d, a, b, m[7], 0xf6bb4b60u, 16);
-    RSH_MD5_STEP(RSH_MD5_H, b, c, d, a, m[10], 0xbebfbc70u, 23);
-    RSH_MD5_STEP(RSH_MD5_H, a, b, c, d, m[13], 0x289b7ec6u, 4);
-    RSH_MD5_STEP(RSH_MD5_H, d, a, b, c, m[0], 0xeaa127fau, 11);
-    RSH_MD5_STEP(RSH_MD5_H, c, d, a, b, m[3], 0xd4ef3085u, 16);
-    RSH_MD5_STEP(RSH_MD5_H, b, c, d, a, m[6], 0x04881d05u, 23);
-    RSH_MD5_STEP(RSH_MD5_H, a, b, c, d, m[9], 0xd9d4d039u, 4);
-    RSH_MD5_STEP(RSH_MD5_H, d, a, b, c, m[12], 0xe6db99e5u, 11);
-    RSH_MD5_STEP(RSH_MD5_H, c, d, a, b, m[15], 0x1fa27cf8u, 16);
-    RSH_MD5_STEP(RSH_MD5_H, b, c, d, a, m[2], 0xc4ac5665u, 23);
+    RSH_MD5_STEP3(a, b, c, d, m[5], 0xfffa3942u, 4);
+    RSH_MD5_STEP3(d, a, b, c, m[8], 0x8771f681u, 11);
+    RSH_MD5_STEP3(c, d, a, b, m[11], 0x6d9d6122u, 16);
+    RSH_MD5_STEP3(b, c, d, a, m[14], 0xfde5380cu, 23);
+    RSH_MD5_STEP3(a, b, c, d, m[1], 0xa4beea44u, 4);
+    RSH_MD5_STEP3(d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    RSH_MD5_STEP3(c, d, a, b, m[7], 0xf6bb4b60u, 16);
+    RSH_MD5_STEP3(b, c, d, a, m[10], 0xbebfbc70u, 23);
+    RSH_MD5_STEP3(a, b, c, d, m[13], 0x289b7ec6u, 4);
+    RSH_MD5_STEP3(d, a, b, c, m[0], 0xeaa127fau, 11);
+    RSH_MD5_STEP3(c, d, a, b, m[3], 0xd4ef3085u, 16);
+    RSH_MD5_STEP3(b, c, d, a, m[6], 0x04881d05u, 23);
+    RSH_MD5_STEP3(a, b, c, d, m[9], 0xd9d4d039u, 4);
+    RSH_MD5_STEP3(d, a, b, c, m[12], 0xe6db99e5u, 11);
+    RSH_MD5_STEP3(c, d, a, b, m[15], 0x1fa27cf8u, 16);
+    RSH_MD5_STEP3(b, c, d, a, m[2], 0xc4ac5665u, 23);
 
     RSH_MD5_STEP(RSH_MD5_I, a, b, c, d, m[0], 0xf4292244u, 6);
     RSH_MD5_STEP(RSH_MD5_I, d, a, b, c, m[7], 0x432aff97u, 10);

@@ -1,0 +1,75 @@
+// kbench -- developer micro-benchmark of the block-sum kernel variants (device.hip) on one GPU.
+// Times each variant with hipEvents on its stream and checks every variant's output against
+// variant 0 bit for bit.  usage: kbench <MiB> <B> <dl> <reps> <variant>...
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "device.h"
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e = (x);                                                     \
+        if (e != hipSuccess) {                                                  \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+            exit(1);                                                            \
+        }                                                                       \
+    } while (0)
+
+int main(int argc, char** argv) {
+    if (argc < 6) {
+        fprintf(stderr, "usage: kbench <MiB> <B> <dl> <reps> <variant>...\n");
+        return 2;
+    }
+    const int64_t n = (int64_t)atoll(argv[1]) << 20;
+    const uint32_t B = (uint32_t)atoi(argv[2]), dl = (uint32_t)atoi(argv[3]);
+    const int reps = atoi(argv[4]);
+    const uint32_t C = (uint32_t)((n + B - 1) / B);
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    uint8_t* d;
+    int32_t *w0, *w;
+    uint8_t *s0, *sx;
+    CK(hipMalloc(&d, n));
+    CK(hipMalloc(&w0, C * 4));
+    CK(hipMalloc(&w, C * 4));
+    CK(hipMalloc(&s0, (size_t)C * dl + 1));
+    CK(hipMalloc(&sx, (size_t)C * dl + 1));
+    CK(rsh::launch_fill_splitmix(d, n, 0x5EED5EED00000000ull, 0, s));
+    CK(rsh::launch_block_sums_variant(0, d, n, B, C, dl, 0x04030201u, w0, s0, s));
+    CK(hipStreamSynchronize(s));
+    std::vector<int32_t> hw0(C), hw(C);
+    std::vector<uint8_t> hs0((size_t)C * dl), hs((size_t)C * dl);
+    CK(hipMemcpy(hw0.data(), w0, C * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hs0.data(), s0, (size_t)C * dl, hipMemcpyDeviceToHost));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int a = 5; a < argc; ++a) {
+        const int v = atoi(argv[a]);
+        CK(hipMemset(w, 0, C * 4));
+        CK(rsh::launch_block_sums_variant(v, d, n, B, C, dl, 0x04030201u, w, sx, s));
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(hw.data(), w, C * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hs.data(), sx, (size_t)C * dl, hipMemcpyDeviceToHost));
+        const bool same = hw == hw0 && hs == hs0;
+        float best = 1e30f, tot = 0;
+        for (int r = 0; r < reps; ++r) {
+            CK(hipEventRecord(e0, s));
+            CK(rsh::launch_block_sums_variant(v, d, n, B, C, dl, 0x04030201u, w, sx, s));
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            best = ms < best ? ms : best;
+            tot += ms;
+        }
+        printf("variant %d  n=%lld B=%u C=%u  avg %.3f ms  best %.3f ms  %.1f GB/s  parity=%s\n", v, (long long)n, B, C,
+               tot / reps, best, n / (tot / reps / 1e3) / 1e9, same ? "ok" : "MISMATCH");
+        fflush(stdout);
+    }
+    return 0;
+}
