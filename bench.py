@@ -26,6 +26,7 @@ sys.path.insert(0, os.path.join(ROOT, "java-rsync_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import rsync_hip as R  # noqa: E402
+import shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 KEY_SRC = 0x5EED5EED << 32
@@ -51,12 +52,10 @@ def main():
     import torch
     import torch.distributed as dist
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = shard.env_rank()
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if world > 1:  # one process per GPU; RCCL only for the barrier and the max-over-ranks time
+        shard.init_distributed("nccl", torch.device("cuda", local))
 
     def barrier():
         if world > 1:
@@ -125,11 +124,7 @@ def main():
     ctx.sync()
     torch.cuda.synchronize()
     barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device="cuda")
     gen_ms = float(np.mean([s.elapsed_time(e) for s, e in gen_ev]))
 
     # ---- spot parity: a few chunks of the device table against the oracle (cheap, every run)
@@ -169,13 +164,14 @@ def main():
             "parallelism": f"file-sharded x{world} (no collectives)",
         },
         "roofline": {
-            "kernel": "block_sums_kernel (Generator; also the Sender's aligned speculation)",
+            "kernel": "block_sums_coalesced_kernel (Generator; also the Sender's aligned speculation)",
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": pmc_traffic(os.path.join(ROOT, "profiles", "r1_pmc", "pmc2_fetch_size.csv"),
+                                   "block_sums_coalesced_kernel<3, true", n),
             "kernel_ms": round(gen_ms, 4),
             "algorithmic_bytes": n,
         },
@@ -191,6 +187,25 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(path, kernel_substr, n):
+    """HBM read bytes per launch of the dominant kernel from a committed rocprofv3 --pmc FETCH_SIZE pass.
+    gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE (KiB) reports half the bytes of a wide
+    coalesced stream, so bytes = FETCH_SIZE * 1024 * 2.  Only used when the profile was taken on the
+    same kernel and the same per-launch size (16 GiB)."""
+    import csv
+    try:
+        rows = [r for r in csv.DictReader(open(path)) if kernel_substr in r["Kernel_Name"]
+                and r["Counter_Name"] == "FETCH_SIZE"]
+    except (OSError, KeyError):
+        return None
+    if not rows or n != 16 << 30:
+        return None
+    per = {}
+    for r in rows:
+        per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return round(sum(per.values()) / len(per) * 1024 * 2)
 
 
 def cpu_baseline(src, basis, B, dl, sample):

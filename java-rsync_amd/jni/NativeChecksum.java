@@ -1,0 +1,78 @@
+/*
+ * NativeChecksum.java -- the Java side of the JNI shim (java-rsync_amd/jni/rsync_hip_jni.c).
+ *
+ * A maintainer adds this class to core/src/main/java/com/github/java/rsync/internal/session/ (same
+ * package as the package-private Checksum, Generator and Sender) and switches the two hot methods to
+ * it when the system property "rsync.hip" is true (Environment-style switch, util/Environment.java:15-25).
+ * Default off: the reference path is unchanged.  See INTEGRATION.md for the call-site diffs.
+ *
+ * Not compiled in this repository's CI (no JDK in the build image); it is the binding a maintainer
+ * would add, kept next to the C shim so the two stay in sync.
+ */
+package com.github.java.rsync.internal.session;
+
+import java.nio.ByteBuffer;
+
+final class NativeChecksum implements AutoCloseable {
+    static final boolean ENABLED = Boolean.getBoolean("rsync.hip");
+    static final int EV_LITERAL = 1;
+    static final int EV_MATCH = 2;
+
+    static {
+        if (ENABLED) {
+            System.loadLibrary("rsynchip_jni"); // links librsynchip.so
+        }
+    }
+
+    // one context per calling thread (Generator and Sender run on separate threads, RsyncClient.java:431)
+    private static final ThreadLocal<NativeChecksum> PER_THREAD = ThreadLocal.withInitial(() -> new NativeChecksum(
+            Integer.getInteger("rsync.hip.device", (int) (Thread.currentThread().getId() % Math.max(1,
+                    Integer.getInteger("rsync.hip.devices", 1))))));
+
+    static NativeChecksum forThread() {
+        return PER_THREAD.get();
+    }
+
+    private final long ctx;
+
+    private NativeChecksum(int device) {
+        ctx = ctxCreate(device);
+    }
+
+    @Override
+    public void close() {
+        ctxDestroy(ctx);
+    }
+
+    /** Generator.java:886-895: weak[i] and strong[i*dl .. i*dl+dl) for every chunk of the basis. */
+    void blockSums(ByteBuffer basis, long size, Checksum.Header h, byte[] seed, int[] weak, byte[] strong) {
+        blockSums(ctx, basis, size, toArray(h), seed, weak, strong);
+    }
+
+    /**
+     * Sender.java:1235-1327: returns {kind, offset, length, index | count << 32} quadruples; the caller
+     * replays them with sendDataFrom / putInt(-(index + j + 1)) and writes putInt(0) + fileMd5.
+     */
+    long[] matchScan(ByteBuffer source, long size, Checksum.Header h, int[] weak, byte[] strong, byte[] seed,
+            byte[] fileMd5, long[] sizes) {
+        return matchScan(ctx, source, size, toArray(h), weak, strong, seed, fileMd5, sizes);
+    }
+
+    private static int[] toArray(Checksum.Header h) {
+        return new int[] { h.getChunkCount(), h.getBlockLength(), h.getDigestLength(), h.getRemainder() };
+    }
+
+    static native long ctxCreate(int device);
+
+    static native void ctxDestroy(long ctx);
+
+    static native int blockLengthFor(long fileSize);
+
+    static native int digestLengthFor(long fileSize, int blockLength, int minDigestLength);
+
+    static native void blockSums(long ctx, ByteBuffer data, long n, int[] header, byte[] seed, int[] weakOut,
+            byte[] strongOut);
+
+    static native long[] matchScan(long ctx, ByteBuffer src, long n, int[] header, int[] weak, byte[] strong,
+            byte[] seed, byte[] fileMd5Out, long[] sizesOut);
+}

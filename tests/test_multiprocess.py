@@ -1,0 +1,73 @@
+"""World-size-2 gloo tests of the multi-GPU plumbing (file-parallel sharding, max-over-ranks timing),
+run on CPU with the oracle standing in for the per-rank work."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+import shard
+
+
+def test_shard_files_lpt():
+    sizes = [128, 64, 64, 32, 32, 32, 16, 8, 8, 1]
+    sh = shard.shard_files(sizes, 3)
+    assert sorted(i for s in sh for i in s) == list(range(len(sizes)))
+    loads = [sum(sizes[i] for i in s) for s in sh]
+    assert max(loads) - min(loads) <= 16
+    # config 4 shape: 1024 equal files over 8 GPUs -> 128 each
+    sh8 = shard.shard_files([128 << 20] * 1024, 8)
+    assert [len(s) for s in sh8] == [128] * 8
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import oracle_ctypes as O
+    dist = shard.init_distributed("gloo")
+    seed = bytes([1, 2, 3, 4])
+    sizes = [3000 + 517 * i for i in range(9)]
+    mine = shard.shard_files(sizes, world)[rank]
+    lit = mat = 0
+    for i in mine:
+        basis = O.splitmix(sizes[i], 1000 + i)
+        src = basis.copy()
+        src[100:900] = O.splitmix(800, 2000 + i)
+        h = O.header(512, 2, basis.size)
+        w, s = O.generator(basis, h, seed)
+        _, _, l, m, _ = O.sender(src, h, w, s, seed)
+        lit += l
+        mat += m
+    tot_lit = shard.reduce_over_ranks(lit, "sum")
+    tot_mat = shard.reduce_over_ranks(mat, "sum")
+    tmax = shard.reduce_over_ranks(float(rank + 1), "max")
+    out[rank] = (tot_lit, tot_mat, tmax, len(mine))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_file_sharding():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    import oracle_ctypes as O
+    seed = bytes([1, 2, 3, 4])
+    sizes = [3000 + 517 * i for i in range(9)]
+    lit = mat = 0
+    for i in range(len(sizes)):
+        basis = O.splitmix(sizes[i], 1000 + i)
+        src = basis.copy()
+        src[100:900] = O.splitmix(800, 2000 + i)
+        h = O.header(512, 2, basis.size)
+        w, s = O.generator(basis, h, seed)
+        _, _, l, m, _ = O.sender(src, h, w, s, seed)
+        lit += l
+        mat += m
+    assert out[0][:3] == out[1][:3] == (lit, mat, 2.0)
+    assert out[0][3] + out[1][3] == len(sizes)
