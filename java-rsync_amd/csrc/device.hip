@@ -9,6 +9,7 @@
 #include "md5_core.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace rsh {
 
@@ -31,6 +32,15 @@ __device__ __forceinline__ void weak_block(const uint32_t (&m)[16], int32_t& s1,
 }
 
 __device__ __forceinline__ int32_t sbyte(uint8_t v) { return (int32_t)(int8_t)v; }
+
+// MD5 of one 64-byte block plus its weak-sum contribution at chunk offset `off`.
+__device__ __forceinline__ void md5_weak_block(Md5State& st, const uint32_t (&m)[16], int32_t& s1, int32_t& u,
+                                               uint32_t off) {
+    int32_t a, b;
+    md5_compress_weak(st, m, a, b);
+    s1 += a;
+    u += (int32_t)(off * (uint32_t)a) + b;
+}
 
 // Final 1-2 MD5 blocks: r (< 64) trailing data bytes at p, then the 4 seed bytes, 0x80, zero pad and
 // the 64-bit bit length of (chunk || seed).  Also folds the r bytes into the weak sums.
@@ -185,7 +195,20 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // MODE (diagnostics only, never in the production launch): 0 = real, 1 = compute only (no global
 // loads; stage data synthesised in registers), 2 = loads only (no MD5/weak; words xor-folded).
-template <int D, bool NT, int WAVES = 1, int MODE = 0>
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+
+// Weak sums on the matrix pipe (MFMAW): per stage, for each group g of 16 chunks and K-half h,
+// C_g += W_h x X_{g,h} with v_mfma_i32_16x16x64_i8, where X holds 64 signed bytes of 16 chunks
+// (columns) and W_h has row 0 = ones and row 1 = the byte's index in the 128-B stage (<= 127, int8).
+// Row 0 of C accumulates s1; row 1 accumulates the in-stage-index-weighted sums; R_g += row 0 after
+// every stage gives sum_s P_s, so u = sum_i i x_i = 128 (nst * P_last - R) + row1.  Column j of group g
+// is chunk 16g + kPi[j] and K-slice s reads piece 4h + kSigma[s]: with the 9-slot LDS rows every
+// 16-lane ds_read_b128 group then hits 16 distinct bank quads (checked exhaustively).
+__device__ __forceinline__ int mfma_pi(int j) { return (int)((0xECA8FDB975316420ull >> (4 * j)) & 15); }
+__device__ __forceinline__ int mfma_pi_inv(int c) { return (int)((0xBFAE9D8C73625140ull >> (4 * c)) & 15); }
+__device__ __forceinline__ int mfma_sigma(int s) { return (0x1302 >> (4 * s)) & 15; }
+
+template <int D, bool NT, int WAVES = 1, int MODE = 0, bool FUSED = false, bool MFMAW = false, bool STEADY = true>
 __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const uint8_t* __restrict__ data, uint32_t B,
                                                                   uint32_t dl, uint32_t seed,
                                                                   int32_t* __restrict__ weak_out,
@@ -204,58 +227,133 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
 
     uint4 q[D][8];
     uint32_t fold = 0;
+    // MFMAW state: weights (row 0 ones, row 1 in-stage byte index), accumulators, running R
+    v4i32 wA[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    v4i32 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    int32_t Racc[4] = {0, 0, 0, 0};
+    int rdB = 0;
+    if constexpr (MFMAW) {
+        const int row = l & 15, ks = l >> 4;
 #pragma unroll
-    for (int d = 0; d < D; ++d)
-        if ((uint32_t)d < nst) {
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if constexpr (MODE == 1) q[d][j] = make_uint4(l + d, j, c0, 7);
-                else q[d][j] = ld16<NT>(lp + 128 * (size_t)d + j * jstride);
+            for (int w = 0; w < 4; ++w) {
+                uint32_t word = 0;
+                if (row == 0) word = 0x01010101u;
+                else if (row == 1)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) word |= (uint32_t)(16 * (4 * h + mfma_sigma(ks)) + 4 * w + b) << (8 * b);
+                wA[h][w] = (int)word;
             }
+        rdB = mfma_pi(l & 15) * ROW + mfma_sigma(ks);
+    }
+    // host guarantees nst >= 2 * D: the prologue is unconditional (exact vmcnt bookkeeping)
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if constexpr (MODE == 1) q[d][j] = make_uint4(l + d, j, c0, 7);
+            else q[d][j] = ld16<NT>(lp + 128 * (size_t)d + j * jstride);
         }
+    }
     Md5State st = md5_init();
     int32_t s1 = 0, u = 0;
-    for (uint32_t s = 0; s < nst; s += D) {
+    // One stage: registers -> LDS (transpose), refill the registers PF stages ahead, weak sums on the
+    // matrix pipe (MFMAW) and the two MD5 blocks.  Inlined with a compile-time slot d.
+    auto stage = [&](auto dc, uint32_t si, bool refill) __attribute__((always_inline)) {
+        constexpr int d = decltype(dc)::value;
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const uint32_t si = s + d;
-            if (si < nst) {
+        for (int j = 0; j < 8; ++j) lds[wr0 + j * 8 * ROW] = q[d][j];
+        if (refill) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) lds[wr0 + j * 8 * ROW] = q[d][j];
-                if (si + D < nst) {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        if constexpr (MODE == 1) q[d][j] = make_uint4(q[d][j].y + si, q[d][j].x, q[d][j].w ^ si, q[d][j].z);
-                        else q[d][j] = ld16<NT>(lp + 128 * (size_t)(si + D) + j * jstride);
-                    }
-                }
-                if constexpr (WAVES == 1) __syncthreads();
-                else wave_lds_sync();
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    uint4 r[4];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) r[k] = lds[rd0 + 4 * h + k];
-                    uint32_t m[16];
-                    unpack(r, m);
-                    if constexpr (MODE == 2) {
-#pragma unroll
-                        for (int k = 0; k < 16; ++k) fold ^= m[k];
-                    } else {
-                        weak_block(m, s1, u, 128 * si + 64 * h);
-                        md5_compress(st, m);
-                    }
-                }
-                if constexpr (WAVES == 1) __syncthreads();
-                else wave_lds_sync();
+            for (int j = 0; j < 8; ++j) {
+                if constexpr (MODE == 1) q[d][j] = make_uint4(q[d][j].y + si, q[d][j].x, q[d][j].w ^ si, q[d][j].z);
+                else q[d][j] = ld16<NT>(lp + 128 * (size_t)(si + D) + j * jstride);
             }
         }
+        if constexpr (WAVES == 1) __syncthreads();
+        else wave_lds_sync();
+        if constexpr (MFMAW) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) Racc[g] += acc[g][0];  // R += P_{s-1}
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const uint4 bv = lds[16 * ROW * g + rdB + 4 * h];
+                    const v4i32 b4 = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
+                    acc[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wA[h], b4, acc[g], 0, 0, 0);
+                }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint4 r[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) r[k] = lds[rd0 + 4 * h + k];
+            uint32_t m[16];
+            unpack(r, m);
+            if constexpr (MODE == 2) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) fold ^= m[k];
+            } else if constexpr (MFMAW) {
+                md5_compress(st, m);
+            } else if constexpr (FUSED) {
+                md5_weak_block(st, m, s1, u, 128 * si + 64 * h);
+            } else {
+                weak_block(m, s1, u, 128 * si + 64 * h);
+                md5_compress(st, m);
+            }
+        }
+        if constexpr (WAVES == 1) __syncthreads();
+        else wave_lds_sync();
+    };
+    uint32_t s = 0;
+    if constexpr (!STEADY) {  // A/B reference: conditional refills in one loop
+        for (; s < nst; s += D) {
+            if (s < nst) stage(std::integral_constant<int, 0>{}, s, s + D < nst);
+            if constexpr (D > 1) if (s + 1 < nst) stage(std::integral_constant<int, 1>{}, s + 1, s + 1 + D < nst);
+            if constexpr (D > 2) if (s + 2 < nst) stage(std::integral_constant<int, 2>{}, s + 2, s + 2 + D < nst);
+        }
+    }
+    // steady state: branch-free, every slot refilled, so the compiler's vmcnt bookkeeping stays exact
+    // (with conditional refills it waits for every outstanding load at each stage: prefetch depth 1)
+    for (; s + 2 * D <= nst; s += D) {
+        stage(std::integral_constant<int, 0>{}, s, true);
+        if constexpr (D > 1) stage(std::integral_constant<int, 1>{}, s + 1, true);
+        if constexpr (D > 2) stage(std::integral_constant<int, 2>{}, s + 2, true);
+        if constexpr (D > 3) stage(std::integral_constant<int, 3>{}, s + 3, true);
+    }
+    for (; s < nst; s += D) {  // drain (fewer than 2 * D stages left)
+        if (s < nst) stage(std::integral_constant<int, 0>{}, s, s + D < nst);
+        if constexpr (D > 1) if (s + 1 < nst) stage(std::integral_constant<int, 1>{}, s + 1, s + 1 + D < nst);
+        if constexpr (D > 2) if (s + 2 < nst) stage(std::integral_constant<int, 2>{}, s + 2, s + 2 + D < nst);
+        if constexpr (D > 3) if (s + 3 < nst) stage(std::integral_constant<int, 3>{}, s + 3, s + 3 + D < nst);
     }
     // final block: seed || 0x80 || zero pad || bit length of (B + 4) bytes
     {
         const uint64_t bits = ((uint64_t)B + 4) * 8;
         uint32_t m[16] = {seed, 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, (uint32_t)bits, (uint32_t)(bits >> 32)};
         md5_compress(st, m);
+    }
+    if constexpr (MFMAW) {
+        // lanes 0..15 of group g hold (P_last, row1, R) for chunk 16g + pi(lane); move them to lane c
+        int32_t s1g[4], ug[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            Racc[g] += acc[g][0];
+            s1g[g] = acc[g][0];
+            ug[g] = (int32_t)(128u * (nst * (uint32_t)acc[g][0] - (uint32_t)Racc[g])) + acc[g][1];
+        }
+        const int src = mfma_pi_inv(l & 15);
+        int32_t t1[4], tu[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            t1[g] = __shfl(s1g[g], src, 64);
+            tu[g] = __shfl(ug[g], src, 64);
+        }
+        const int gs = l >> 4;
+        s1 = gs == 0 ? t1[0] : gs == 1 ? t1[1] : gs == 2 ? t1[2] : t1[3];
+        u = gs == 0 ? tu[0] : gs == 1 ? tu[1] : gs == 2 ? tu[2] : tu[3];
     }
     const uint32_t c = c0 + l;
     if constexpr (MODE == 2) st.a ^= fold;
@@ -362,11 +460,15 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                                      hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     const uintptr_t addr = reinterpret_cast<uintptr_t>(d_data);
-    if (variant < 0) variant = 4;
+    if (variant < 0) variant = 19;  // coalesced, 2 stages in flight, weak sums on the matrix pipe
     uint32_t c_first = 0;
-    if (variant >= 3 && (B % 128) == 0 && (addr % 16) == 0) {
+    const bool deep = variant == 4 || variant == 6 || variant == 7 || variant == 9 || variant == 10 ||
+                      variant == 11 || variant == 12 || variant == 14 || variant == 15 || variant == 16 ||
+                      variant == 18 || variant == 21;  // D >= 3 variants need nst >= 2D = 6 (8 for D = 4)
+    if (variant >= 3 && (B % 128) == 0 && (B >> 7) >= (deep ? 8u : 4u) && (addr % 16) == 0) {
         const uint32_t nfullc = (uint32_t)std::min<int64_t>(n / B, nchunks);  // chunks with L == B
         const uint32_t waves = nfullc / 64;
+        const uint32_t nst = B >> 7;
         const size_t wave_lds = 64 * 9 * sizeof(uint4);
         // LDS per workgroup chosen so that the dispatcher can place at most ceil(groups / CUs) groups
         // on a CU: every SIMD then holds the same number of equal-work waves (no stacking imbalance).
@@ -416,6 +518,40 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                 case 15:
                     hipLaunchKernelGGL((block_sums_dma_kernel<4>), dim3(waves), dim3(64), 4 * 512 * 16, s, d_data, B,
                                        dl, seed_word, d_weak, d_strong);
+                    break;
+                case 18:
+                    if (nst <= 1024) {
+                        hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true, 1, 0, false, true>), dim3(waves), dim3(64),
+                                           lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    } else {
+                        hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true>), dim3(waves), dim3(64), lb, s, d_data,
+                                           B, dl, seed_word, d_weak, d_strong);
+                    }
+                    break;
+                case 19:
+                    if (nst <= 1024) {
+                        hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true>), dim3(waves), dim3(64),
+                                           lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    } else {
+                        hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true>), dim3(waves), dim3(64), lb, s, d_data,
+                                           B, dl, seed_word, d_weak, d_strong);
+                    }
+                    break;
+                case 20:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, false>), dim3(waves),
+                                       dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 21:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true, 1, 0, false, true, false>), dim3(waves),
+                                       dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 16:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true, 1, 0, true>), dim3(waves), dim3(64), lb, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 17:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, false, 1, 0, true>), dim3(waves), dim3(64), lb,
+                                       s, d_data, B, dl, seed_word, d_weak, d_strong);
                     break;
                 case 10:
                     hipLaunchKernelGGL((block_sums_coalesced_kernel<3, false, 1, 1>), dim3(waves), dim3(64), lb, s,

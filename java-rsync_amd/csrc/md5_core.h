@@ -123,6 +123,132 @@ RSH_HD void md5_compress(Md5State& st, const uint32_t (&m)[16]) {
     st.d += d;
 }
 
+#if defined(__HIP__)
+// md5_compress with the block's weak-sum dot products (Rolling.compute, two v_dot4_i32_i8 per word)
+// threaded through rounds 1-2, one per step, into four independent accumulators: they fill the issue
+// bubbles of the MD5 dependency chain instead of forming two serial 16-deep dot4 chains of their own.
+// On return: a_out = sum of the 64 signed bytes, b_out = sum k * x_k (k = 0..63 within the block).
+__device__ __forceinline__ void md5_compress_weak(Md5State& st, const uint32_t (&m)[16], int32_t& a_out,
+                                                  int32_t& b_out) {
+    int32_t wa0 = 0, wa1 = 0, wb0 = 0, wb1 = 0;
+#define RSH_WA(j) ((j) & 1 ? wa1 : wa0) = __builtin_amdgcn_sdot4((int)m[j], 0x01010101, (j) & 1 ? wa1 : wa0, false)
+#define RSH_WB(j)                                                                                            \
+    ((j) & 1 ? wb1 : wb0) = __builtin_amdgcn_sdot4(                                                          \
+        (int)m[j], (4 * (j)) | ((4 * (j) + 1) << 8) | ((4 * (j) + 2) << 16) | ((4 * (j) + 3) << 24),           \
+        (j) & 1 ? wb1 : wb0, false)
+    uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
+    RSH_MD5_STEP(RSH_MD5_F, a, b, c, d, m[0], 0xd76aa478u, 7);
+    RSH_WA(0);
+    RSH_MD5_STEP(RSH_MD5_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
+    RSH_WA(1);
+    RSH_MD5_STEP(RSH_MD5_F, c, d, a, b, m[2], 0x242070dbu, 17);
+    RSH_WA(2);
+    RSH_MD5_STEP(RSH_MD5_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
+    RSH_WA(3);
+    RSH_MD5_STEP(RSH_MD5_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
+    RSH_WA(4);
+    RSH_MD5_STEP(RSH_MD5_F, d, a, b, c, m[5], 0x4787c62au, 12);
+    RSH_WA(5);
+    RSH_MD5_STEP(RSH_MD5_F, c, d, a, b, m[6], 0xa8304613u, 17);
+    RSH_WA(6);
+    RSH_MD5_STEP(RSH_MD5_F, b, c, d, a, m[7], 0xfd469501u, 22);
+    RSH_WA(7);
+    RSH_MD5_STEP(RSH_MD5_F, a, b, c, d, m[8], 0x698098d8u, 7);
+    RSH_WA(8);
+    RSH_MD5_STEP(RSH_MD5_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
+    RSH_WA(9);
+    RSH_MD5_STEP(RSH_MD5_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
+    RSH_WA(10);
+    RSH_MD5_STEP(RSH_MD5_F, b, c, d, a, m[11], 0x895cd7beu, 22);
+    RSH_WA(11);
+    RSH_MD5_STEP(RSH_MD5_F, a, b, c, d, m[12], 0x6b901122u, 7);
+    RSH_WA(12);
+    RSH_MD5_STEP(RSH_MD5_F, d, a, b, c, m[13], 0xfd987193u, 12);
+    RSH_WA(13);
+    RSH_MD5_STEP(RSH_MD5_F, c, d, a, b, m[14], 0xa679438eu, 17);
+    RSH_WA(14);
+    RSH_MD5_STEP(RSH_MD5_F, b, c, d, a, m[15], 0x49b40821u, 22);
+    RSH_WA(15);
+
+    RSH_MD5_STEP(RSH_MD5_G, a, b, c, d, m[1], 0xf61e2562u, 5);
+    RSH_WB(0);
+    RSH_MD5_STEP(RSH_MD5_G, d, a, b, c, m[6], 0xc040b340u, 9);
+    RSH_WB(1);
+    RSH_MD5_STEP(RSH_MD5_G, c, d, a, b, m[11], 0x265e5a51u, 14);
+    RSH_WB(2);
+    RSH_MD5_STEP(RSH_MD5_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
+    RSH_WB(3);
+    RSH_MD5_STEP(RSH_MD5_G, a, b, c, d, m[5], 0xd62f105du, 5);
+    RSH_WB(4);
+    RSH_MD5_STEP(RSH_MD5_G, d, a, b, c, m[10], 0x02441453u, 9);
+    RSH_WB(5);
+    RSH_MD5_STEP(RSH_MD5_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
+    RSH_WB(6);
+    RSH_MD5_STEP(RSH_MD5_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+    RSH_WB(7);
+    RSH_MD5_STEP(RSH_MD5_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
+    RSH_WB(8);
+    RSH_MD5_STEP(RSH_MD5_G, d, a, b, c, m[14], 0xc33707d6u, 9);
+    RSH_WB(9);
+    RSH_MD5_STEP(RSH_MD5_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
+    RSH_WB(10);
+    RSH_MD5_STEP(RSH_MD5_G, b, c, d, a, m[8], 0x455a14edu, 20);
+    RSH_WB(11);
+    RSH_MD5_STEP(RSH_MD5_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
+    RSH_WB(12);
+    RSH_MD5_STEP(RSH_MD5_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
+    RSH_WB(13);
+    RSH_MD5_STEP(RSH_MD5_G, c, d, a, b, m[7], 0x676f02d9u, 14);
+    RSH_WB(14);
+    RSH_MD5_STEP(RSH_MD5_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
+    RSH_WB(15);
+
+    RSH_MD5_STEP3(a, b, c, d, m[5], 0xfffa3942u, 4);
+    RSH_MD5_STEP3(d, a, b, c, m[8], 0x8771f681u, 11);
+    RSH_MD5_STEP3(c, d, a, b, m[11], 0x6d9d6122u, 16);
+    RSH_MD5_STEP3(b, c, d, a, m[14], 0xfde5380cu, 23);
+    RSH_MD5_STEP3(a, b, c, d, m[1], 0xa4beea44u, 4);
+    RSH_MD5_STEP3(d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    RSH_MD5_STEP3(c, d, a, b, m[7], 0xf6bb4b60u, 16);
+    RSH_MD5_STEP3(b, c, d, a, m[10], 0xbebfbc70u, 23);
+    RSH_MD5_STEP3(a, b, c, d, m[13], 0x289b7ec6u, 4);
+    RSH_MD5_STEP3(d, a, b, c, m[0], 0xeaa127fau, 11);
+    RSH_MD5_STEP3(c, d, a, b, m[3], 0xd4ef3085u, 16);
+    RSH_MD5_STEP3(b, c, d, a, m[6], 0x04881d05u, 23);
+    RSH_MD5_STEP3(a, b, c, d, m[9], 0xd9d4d039u, 4);
+    RSH_MD5_STEP3(d, a, b, c, m[12], 0xe6db99e5u, 11);
+    RSH_MD5_STEP3(c, d, a, b, m[15], 0x1fa27cf8u, 16);
+    RSH_MD5_STEP3(b, c, d, a, m[2], 0xc4ac5665u, 23);
+
+    RSH_MD5_STEP(RSH_MD5_I, a, b, c, d, m[0], 0xf4292244u, 6);
+    RSH_MD5_STEP(RSH_MD5_I, d, a, b, c, m[7], 0x432aff97u, 10);
+    RSH_MD5_STEP(RSH_MD5_I, c, d, a, b, m[14], 0xab9423a7u, 15);
+    RSH_MD5_STEP(RSH_MD5_I, b, c, d, a, m[5], 0xfc93a039u, 21);
+    RSH_MD5_STEP(RSH_MD5_I, a, b, c, d, m[12], 0x655b59c3u, 6);
+    RSH_MD5_STEP(RSH_MD5_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
+    RSH_MD5_STEP(RSH_MD5_I, c, d, a, b, m[10], 0xffeff47du, 15);
+    RSH_MD5_STEP(RSH_MD5_I, b, c, d, a, m[1], 0x85845dd1u, 21);
+    RSH_MD5_STEP(RSH_MD5_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
+    RSH_MD5_STEP(RSH_MD5_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+    RSH_MD5_STEP(RSH_MD5_I, c, d, a, b, m[6], 0xa3014314u, 15);
+    RSH_MD5_STEP(RSH_MD5_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
+    RSH_MD5_STEP(RSH_MD5_I, a, b, c, d, m[4], 0xf7537e82u, 6);
+    RSH_MD5_STEP(RSH_MD5_I, d, a, b, c, m[11], 0xbd3af235u, 10);
+    RSH_MD5_STEP(RSH_MD5_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+    RSH_MD5_STEP(RSH_MD5_I, b, c, d, a, m[9], 0xeb86d391u, 21);
+
+    st.a += a;
+    st.b += b;
+    st.c += c;
+    st.d += d;
+    a_out = wa0 + wa1;
+    b_out = wb0 + wb1;
+#undef RSH_WA
+#undef RSH_WB
+}
+#endif
+
+
 // Little-endian 16-byte digest from the state.
 RSH_HD void md5_digest_bytes(const Md5State& st, uint8_t out[16]) {
     const uint32_t w[4] = {st.a, st.b, st.c, st.d};
