@@ -29,6 +29,9 @@ import rsync_hip as R  # noqa: E402
 import shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# production K1 instantiation (device.hip launch_block_sums_variant default); the committed PMC profile
+# for `traffic` is matched on this name so a stale profile of another kernel is never reported
+PROD_KERNEL = "block_sums_coalesced_kernel<2, true, 1, 0, false, true, true>"
 KEY_SRC = 0x5EED5EED << 32
 KEY_EDIT = (0x5EED5EED << 32) | 0xED17
 
@@ -170,8 +173,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(os.path.join(ROOT, "profiles", "r1_pmc", "pmc2_fetch_size.csv"),
-                                   "block_sums_coalesced_kernel<3, true", n),
+            "traffic": pmc_traffic(os.path.join(ROOT, "profiles", "r1_pmc", "bench_fetch_size.csv"),
+                                   PROD_KERNEL, n),
             "kernel_ms": round(gen_ms, 4),
             "algorithmic_bytes": n,
         },
