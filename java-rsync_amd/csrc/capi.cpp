@@ -87,13 +87,13 @@ struct rsh_ctx {
     hipStream_t stream = nullptr;
     DevBuf data, weak, strong;                   // host-input staging
     DevBuf src_weak, src_strong, flags;          // aligned speculation over the source
-    DevBuf slots, dslots, dkeys, pos, out, first, win;
+    DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf;
     hipStream_t aux = nullptr;                   // basis-table download beside the speculation kernel
     hipEvent_t ev_in = nullptr, ev_tab = nullptr;
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
     ~rsh_ctx() {
         for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &slots, &dslots, &dkeys, &pos, &out,
-                          &first, &win})
+                          &first, &win, &ivbuf, &tilebuf})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl}) b->release();
         if (ev_in) (void)hipEventDestroy(ev_in);
@@ -132,15 +132,26 @@ class HipBackend : public rsh::ScanBackend {
     const uint8_t* aligned_strong() override { return as; }
     const uint8_t* chain_flags() override { return fl; }
 
-    int32_t weak_at(int64_t p) override {
-        int32_t r = 0;
-        ok(c_->pos.ensure(sizeof(int64_t)));
-        ok(c_->out.ensure(sizeof(int32_t)));
-        ok(hipMemcpyAsync(c_->pos.p, &p, sizeof(p), hipMemcpyHostToDevice, c_->stream));
-        ok(rsh::launch_window_weak(x_, n_, (uint32_t)B_, c_->pos.as<int64_t>(), 1, c_->out.as<int32_t>(), c_->stream));
-        ok(hipMemcpyAsync(&r, c_->out.p, sizeof(r), hipMemcpyDeviceToHost, c_->stream));
+    void weak_many(const int64_t* pos, int64_t count, int32_t* out) override {
+        if (count <= 0) return;
+        ok(c_->pos.ensure((size_t)count * sizeof(int64_t)));
+        ok(c_->out.ensure((size_t)count * sizeof(int32_t)));
+        if (err != hipSuccess) return;
+        ok(hipMemcpyAsync(c_->pos.p, pos, (size_t)count * sizeof(int64_t), hipMemcpyHostToDevice, c_->stream));
+        ok(rsh::launch_window_weak(x_, n_, (uint32_t)B_, c_->pos.as<int64_t>(), (uint32_t)count, c_->out.as<int32_t>(),
+                                   c_->stream));
+        ok(hipMemcpyAsync(out, c_->out.p, (size_t)count * sizeof(int32_t), hipMemcpyDeviceToHost, c_->stream));
         ok(hipStreamSynchronize(c_->stream));
-        return r;
+    }
+    void bytes_many(const int64_t* pos, int64_t count, uint8_t* out) override {
+        if (count <= 0) return;
+        ok(c_->pos.ensure((size_t)count * sizeof(int64_t)));
+        ok(c_->out.ensure((size_t)count * sizeof(int32_t)));
+        if (err != hipSuccess) return;
+        ok(hipMemcpyAsync(c_->pos.p, pos, (size_t)count * sizeof(int64_t), hipMemcpyHostToDevice, c_->stream));
+        ok(rsh::launch_gather_bytes(x_, c_->pos.as<int64_t>(), (uint32_t)count, c_->out.as<uint8_t>(), c_->stream));
+        ok(hipMemcpyAsync(out, c_->out.p, (size_t)count, hipMemcpyDeviceToHost, c_->stream));
+        ok(hipStreamSynchronize(c_->stream));
     }
     // A single window's digest is one serial MD5 chain: 64-wide waves give it nothing, so the rare
     // resolver misses (first table hit after a reset) are digested on the host from a D2H copy.
@@ -154,19 +165,13 @@ class HipBackend : public rsh::ScanBackend {
         h.update(seed_, 4);
         h.final(out);
     }
-    uint8_t byte_at(int64_t p) override {
-        uint8_t b = 0;
-        ok(hipMemcpyAsync(&b, x_ + p, 1, hipMemcpyDeviceToHost, c_->stream));
-        ok(hipStreamSynchronize(c_->stream));
-        return b;
-    }
-    int64_t first_hit(int64_t a, int64_t b, int64_t anchor, uint32_t e_lo, uint32_t e_hi,
-                      const std::vector<int32_t>* keys) override {
+    int64_t first_hit(const rsh::ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) override {
         rsh::ProbeTable tab = table;
         if (keys) {
             const uint32_t ns = pow2_at_least(2 * keys->size() + 2);
             ok(c_->dslots.ensure(ns * sizeof(unsigned long long)));
             ok(c_->dkeys.ensure((keys->size() + 1) * sizeof(int32_t)));
+            if (err != hipSuccess) return -1;
             if (!keys->empty())
                 ok(hipMemcpyAsync(c_->dkeys.p, keys->data(), keys->size() * sizeof(int32_t), hipMemcpyHostToDevice,
                                   c_->stream));
@@ -176,20 +181,32 @@ class HipBackend : public rsh::ScanBackend {
             tab.slots = c_->dslots.as<unsigned long long>();
             tab.mask = ns - 1;
         }
+        ivs_.resize((size_t)count);
+        tiles_.clear();
+        for (int64_t i = 0; i < count; ++i) {
+            ivs_[i] = rsh::ProbeIv{iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo & 0xFFFFu, iv[i].e_hi & 0xFFFFu};
+            rsh::probe_tiles(iv[i].a, iv[i].b, B_, (int32_t)i, &tiles_);
+        }
         ok(c_->first.ensure(sizeof(unsigned long long)));
+        ok(c_->ivbuf.ensure(ivs_.size() * sizeof(rsh::ProbeIv) + 1));
+        ok(c_->tilebuf.ensure(tiles_.size() * sizeof(rsh::ProbeTile) + 1));
+        if (err != hipSuccess) return -1;
+        if (!ivs_.empty())
+            ok(hipMemcpyAsync(c_->ivbuf.p, ivs_.data(), ivs_.size() * sizeof(rsh::ProbeIv), hipMemcpyHostToDevice,
+                              c_->stream));
+        if (!tiles_.empty())
+            ok(hipMemcpyAsync(c_->tilebuf.p, tiles_.data(), tiles_.size() * sizeof(rsh::ProbeTile),
+                              hipMemcpyHostToDevice, c_->stream));
         rsh::ProbeArgs A;
         A.data = x_;
         A.n = n_;
         A.B = (uint32_t)B_;
-        A.a = a;
-        A.b = b;
-        A.anchor = anchor;
-        A.e_lo = e_lo & 0xFFFFu;
-        A.e_hi = e_hi & 0xFFFFu;
         A.aligned_weak = c_->src_weak.as<int32_t>();
         A.table = tab;
+        A.ivs = c_->ivbuf.as<rsh::ProbeIv>();
+        A.tiles = c_->tilebuf.as<rsh::ProbeTile>();
         A.first = c_->first.as<unsigned long long>();
-        ok(rsh::launch_probe_first(A, c_->stream));
+        ok(rsh::launch_probe_first(A, (uint32_t)tiles_.size(), c_->stream));
         unsigned long long r = ~0ull;
         ok(hipMemcpyAsync(&r, c_->first.p, sizeof(r), hipMemcpyDeviceToHost, c_->stream));
         ok(hipStreamSynchronize(c_->stream));
@@ -208,6 +225,8 @@ class HipBackend : public rsh::ScanBackend {
     int dl_;
     uint8_t seed_[4];
     std::vector<uint8_t> win_;
+    std::vector<rsh::ProbeIv> ivs_;
+    std::vector<rsh::ProbeTile> tiles_;
 };
 
 // Header consistency for the Generator side (3-arg ctor semantics, Checksum.java:94-113).

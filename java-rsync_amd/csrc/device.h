@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace rsh {
 
 // Generator block sums (Generator.java:886-895): chunk c covers [c*B, min((c+1)*B, n)).
@@ -29,23 +31,39 @@ hipError_t launch_table_clear(unsigned long long* d_slots, uint32_t nslots, hipS
 hipError_t launch_table_insert(unsigned long long* d_slots, uint32_t mask, const int32_t* d_keys, uint32_t nkeys,
                                hipStream_t s);
 
-// First position p in [a, b) whose Sender-side rolling key R(p) = T(p) + E(p) is in the table, where
-// T(p) is the true weak sum of window [p, p + min(B, n - p)) and E(p) = (e_lo, e_hi + e_lo * (min(p, n-B) -
-// min(anchor, n-B))) mod 2^16 (the post-flush desync of Sender.java:1292-1310).  aligned_weak[k] = T(k*B)
-// (the source's own block sums).  *d_first (int64, preset to INT64_MAX by the launcher) receives the
-// position.  Positions are processed in aligned blocks of B; work per launch is O(b - a + B).
+// Sender-side rolling key probe.  For each interval [a, b) the key is R(p) = T(p) + E(p), where T(p) is
+// the true weak sum of window [p, p + min(B, n - p)) and E(p) = (e_lo, e_hi + e_lo * (min(p, n-B) -
+// min(anchor, n-B))) mod 2^16 (the post-flush desync of Sender.java:1292-1310).  The work is cut into
+// tiles of PROBE_TILE positions inside aligned blocks [kB, kB + B); aligned_weak[k] = T(kB) (the
+// source's own block sums) anchors each block.  *first (uint64, preset to ~0) receives the smallest
+// hitting position over all tiles.
+constexpr int PROBE_TILE = 4096;
+struct ProbeIv {
+    int64_t a, b, anchor;
+    uint32_t e_lo, e_hi;
+};
+struct ProbeTile {
+    int64_t q0;  // tile start (multiple of PROBE_TILE from its block start)
+    int32_t iv;  // interval index
+    int32_t pad;
+};
 struct ProbeArgs {
     const uint8_t* data;
     int64_t n;
     uint32_t B;
-    int64_t a, b;
-    int64_t anchor;
-    uint32_t e_lo, e_hi;
     const int32_t* aligned_weak;
     ProbeTable table;
+    const ProbeIv* ivs;
+    const ProbeTile* tiles;
     unsigned long long* first;
 };
-hipError_t launch_probe_first(const ProbeArgs& args, hipStream_t s);
+// Appends the tiles covering [a, b) for interval `iv` (host side).
+void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeTile>* out);
+hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, hipStream_t s);
+
+// Bytes at arbitrary positions.
+hipError_t launch_gather_bytes(const uint8_t* d_data, const int64_t* d_pos, uint32_t npos, uint8_t* d_out,
+                               hipStream_t s);
 
 // True weak sums at arbitrary positions: out[i] = Rolling.compute(data + pos[i], min(B, n - pos[i])).
 hipError_t launch_window_weak(const uint8_t* d_data, int64_t n, uint32_t B, const int64_t* d_pos, uint32_t npos,

@@ -782,7 +782,7 @@ __device__ __forceinline__ void block_exscan(int32_t (&v)[NV], int32_t* sh /* NV
 // ------------------------------------------------------------------------------------------------
 constexpr int PROBE_THREADS = 256;
 constexpr int PROBE_PPT = 16;
-constexpr int PROBE_TILE = PROBE_THREADS * PROBE_PPT;
+static_assert(PROBE_TILE == PROBE_THREADS * PROBE_PPT, "tile = threads x positions per thread");
 
 __device__ __forceinline__ int32_t roll_sub(int32_t cs, int32_t w, int32_t x) {  // Rolling.java:56-60
     const uint32_t lo = ((uint32_t)cs & 0xFFFFu) - (uint32_t)x;
@@ -807,15 +807,17 @@ __device__ __forceinline__ void load16(const uint8_t* __restrict__ x, int64_t n,
     }
 }
 
-__global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A, int64_t k0, uint32_t tiles_per_block) {
+__global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A) {
     __shared__ int32_t sh[4 * PROBE_THREADS / 64];
     const int64_t n = A.n, B = A.B;
-    const int64_t k = k0 + blockIdx.x / tiles_per_block;
+    const ProbeTile tile = A.tiles[blockIdx.x];
+    const ProbeIv I = A.ivs[tile.iv];
+    const int64_t k = tile.q0 / B;
     const int64_t o = k * B;
-    const int64_t q0 = o + (int64_t)(blockIdx.x % tiles_per_block) * PROBE_TILE;
+    const int64_t q0 = tile.q0;
     int64_t qend = q0 + PROBE_TILE;
     if (qend > o + B) qend = o + B;
-    if (q0 >= A.b || qend <= A.a || q0 >= n) return;  // uniform over the workgroup
+    if (q0 >= I.b || qend <= I.a || q0 >= n) return;  // uniform over the workgroup
 
     // prefix of both streams from the block origin up to the tile
     int32_t head[4] = {0, 0, 0, 0};
@@ -840,7 +842,7 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A,
     }
     int32_t pre[4] = {part[0], part[1], part[2], part[3]};
     block_exscan<4>(pre, sh);
-    if (p0 >= qend || p0 >= A.b || p0 + PROBE_PPT <= A.a) return;
+    if (p0 >= qend || p0 >= I.b || p0 + PROBE_PPT <= I.a) return;
 
     const uint32_t pa = (uint32_t)(head[0] + pre[0]), pa2 = (uint32_t)(head[1] + pre[1]);  // P1(p0), P2(p0)
     const uint32_t pb = (uint32_t)(head[2] + pre[2]), pb2 = (uint32_t)(head[3] + pre[3]);  // sums over [o+B, p0+B)
@@ -854,13 +856,13 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A,
     const uint32_t s2 = (uint32_t)(endq - o) * s1 - (P2e - pa2);
     const int64_t nb = n - B;
     auto clampB = [&](int64_t p) { return p < nb ? p : nb; };
-    const uint32_t ehi = A.e_hi + A.e_lo * (uint32_t)(clampB(p0) - clampB(A.anchor));
-    int32_t R = (int32_t)(((s1 + A.e_lo) & 0xFFFFu) | ((s2 + ehi) << 16));
+    const uint32_t ehi = I.e_hi + I.e_lo * (uint32_t)(clampB(p0) - clampB(I.anchor));
+    int32_t R = (int32_t)(((s1 + I.e_lo) & 0xFFFFu) | ((s2 + ehi) << 16));
 #pragma unroll
     for (int i = 0; i < PROBE_PPT; ++i) {
         const int64_t p = p0 + i;
-        if (p >= A.b || p >= qend) break;
-        if (p >= A.a && table_has(A.table, (uint32_t)R)) {
+        if (p >= I.b || p >= qend) break;
+        if (p >= I.a && table_has(A.table, (uint32_t)R)) {
             atomicMin(A.first, (unsigned long long)p);
             return;
         }
@@ -870,15 +872,34 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A,
     }
 }
 
-hipError_t launch_probe_first(const ProbeArgs& args, hipStream_t s) {
+void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeTile>* out) {
+    if (a >= b) return;
+    for (int64_t k = a / B; k <= (b - 1) / B; ++k) {
+        const int64_t o = k * B;
+        const int64_t lo = a > o ? a : o;
+        const int64_t hi = b < o + B ? b : o + B;
+        for (int64_t t = (lo - o) / PROBE_TILE; t <= (hi - 1 - o) / PROBE_TILE; ++t)
+            out->push_back(ProbeTile{o + t * PROBE_TILE, iv, 0});
+    }
+}
+
+hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, hipStream_t s) {
     hipError_t e = hipMemsetAsync(args.first, 0xFF, sizeof(unsigned long long), s);  // "none" = all ones
-    if (e != hipSuccess) return e;
-    if (args.a >= args.b) return hipSuccess;
-    const int64_t k0 = args.a / args.B;
-    const int64_t k1 = (args.b - 1) / args.B;
-    const uint32_t tpb = (uint32_t)((args.B + PROBE_TILE - 1) / PROBE_TILE);
-    const int64_t grid = (k1 - k0 + 1) * (int64_t)tpb;
-    hipLaunchKernelGGL(probe_first_kernel, dim3((uint32_t)grid), dim3(PROBE_THREADS), 0, s, args, k0, tpb);
+    if (e != hipSuccess || ntiles == 0) return e;
+    hipLaunchKernelGGL(probe_first_kernel, dim3(ntiles), dim3(PROBE_THREADS), 0, s, args);
+    return hipGetLastError();
+}
+
+__global__ void gather_bytes_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ pos, uint32_t npos,
+                                    uint8_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < npos) out[i] = data[pos[i]];
+}
+
+hipError_t launch_gather_bytes(const uint8_t* d_data, const int64_t* d_pos, uint32_t npos, uint8_t* d_out,
+                               hipStream_t s) {
+    if (npos == 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_bytes_kernel, dim3((npos + 255) / 256), dim3(256), 0, s, d_data, d_pos, npos, d_out);
     return hipGetLastError();
 }
 

@@ -130,6 +130,7 @@ void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveRe
     uint8_t md5c[16];
     std::vector<int32_t> dkeys;
     bool dkeys_ready = false;
+    int64_t batch = 1;  // flush intervals speculated per batched probe
 
     auto E_at = [&](int64_t p, uint32_t* lo, uint32_t* hi) {
         *lo = elo;
@@ -138,6 +139,17 @@ void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveRe
     auto T_at = [&](int64_t p) -> int32_t {
         if (p % B == 0 && p / B < nal) return aw[p / B];
         return be.weak_at(p);
+    };
+    // Flush bookkeeping shared by the single and the batched path: from the rolling value R at the
+    // flush point f (window B), the state after FileView slides by a whole window (quirk A).
+    auto after_flush = [&](int64_t f, int32_t R, uint8_t xf, uint8_t xlast, int32_t T2, uint32_t* nelo,
+                           uint32_t* nehi) {
+        const int32_t R1 = roll_sub(R, (int32_t)B, xf);
+        const int64_t s2 = f + B;
+        int32_t R2 = R1;
+        if (s2 <= last && wl(s2) == B) R2 = roll_add(R1, xlast);  // :1308-1310
+        *nelo = (lo16(R2) - lo16(T2)) & 0xFFFFu;
+        *nehi = (hi16(R2) - hi16(T2)) & 0xFFFFu;
     };
     // FileView flush at f (isFull, Sender.java:1294-1302) with rolling value R at f: the Java code
     // subtracts x_f with the full window, slides by B and keeps rolling the old value.
@@ -215,7 +227,8 @@ void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveRe
             if (p < 0 && a <= stop) {
                 uint32_t el, eh;
                 E_at(a, &el, &eh);
-                p = be.first_hit(a, stop + 1, a, el, eh, keys);
+                const ProbeInterval one{a, stop + 1, a, el, eh};
+                p = be.first_hit(&one, 1, keys);
                 st.probe_launches++;
             }
         }
@@ -260,6 +273,7 @@ void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveRe
                     }
                 }
             }
+            batch = 1;
             if (hit >= 0) {  // Sender.java:1265-1288
                 emit_lit(m, p - m);
                 emit_match(p, w, hit, 1);
@@ -276,12 +290,77 @@ void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveRe
             else s = p + 1;
             continue;
         }
-        if (f <= last) {  // no candidate before the flush point: flush at f
+        if (f <= last) {
+            // No candidate before the flush point.  Speculate that none occurs in the next K flush
+            // intervals either: their flush points are f + 10B i (FileView.isFull at mark + 9B), the
+            // rolling value's desync E after each one is a closed-form function of T and two bytes at
+            // the flush, so one batched gather, a host chain and one probe over all K intervals
+            // replace K round trips.  K doubles while no event turns up (wasted probing <= 2x).
+            // flush i sits at f_i = f + 10B i and happens iff its mark m_i = f_i - 9B has m_i + 10B <= n
+            int64_t K = 1;
+            while (K < batch && f + 10 * B * K + B <= n) ++K;
+            std::vector<int64_t> tpos, bpos;
+            for (int64_t i = 0; i < K; ++i) {
+                const int64_t fi = f + 10 * B * i;
+                tpos.push_back(fi);
+                tpos.push_back(fi + B);
+                bpos.push_back(fi);
+                bpos.push_back(fi + 2 * B - 1 < n ? fi + 2 * B - 1 : fi);
+            }
+            std::vector<int32_t> tv(tpos.size());
+            std::vector<uint8_t> bv(bpos.size());
+            be.weak_many(tpos.data(), (int64_t)tpos.size(), tv.data());
+            be.bytes_many(bpos.data(), (int64_t)bpos.size(), bv.data());
+            // host chain: state after each flush, the interval it opens
+            struct Step {
+                int64_t s2;
+                uint32_t elo, ehi;
+            };
+            std::vector<Step> chain;
+            std::vector<ProbeInterval> iv;
             uint32_t el, eh;
             E_at(f, &el, &eh);
-            const int32_t T = T_at(f);
-            flush(f, pack16(lo16(T) + el, hi16(T) + eh));
-            continue;
+            int32_t R = pack16(lo16(tv[0]) + el, hi16(tv[0]) + eh);
+            int64_t mm = m;
+            for (int64_t i = 0; i < K; ++i) {
+                const int64_t fi = f + 10 * B * i;
+                Step stp;
+                stp.s2 = fi + B;
+                after_flush(fi, R, bv[2 * i], bv[2 * i + 1], tv[2 * i + 1], &stp.elo, &stp.ehi);
+                chain.push_back(stp);
+                mm = stp.s2;
+                if (stp.s2 > last) break;
+                const int64_t fn = (mm + 10 * B <= n) ? mm + 9 * B : std::numeric_limits<int64_t>::max();
+                iv.push_back(ProbeInterval{stp.s2, std::min(fn, last) + 1, stp.s2, stp.elo, stp.ehi});
+                if (i + 1 < K) {  // rolling value at the next flush point
+                    const uint32_t elo2 = stp.elo;
+                    const uint32_t ehi2 = stp.ehi + stp.elo * (uint32_t)(clampB(fn) - clampB(stp.s2));
+                    R = pack16(lo16(tv[2 * i + 2]) + elo2, hi16(tv[2 * i + 2]) + ehi2);
+                }
+            }
+            int64_t hit = -1;
+            if (!iv.empty()) {
+                hit = be.first_hit(iv.data(), (int64_t)iv.size(), keys);
+                st.probe_launches++;
+            }
+            // commit every flush whose following interval holds no candidate
+            int64_t commit = (int64_t)chain.size();
+            if (hit >= 0)
+                for (size_t j = 0; j < iv.size(); ++j)
+                    if (hit >= iv[j].a && hit < iv[j].b) {
+                        commit = (int64_t)j + 1;  // flushes 0..j happen before the event
+                        break;
+                    }
+            for (int64_t i = 0; i < commit; ++i) {
+                emit_lit(m, 10 * B);
+                st.flushes++;
+                m = s = chain[i].s2;
+                elo = chain[i].elo;
+                ehi = chain[i].ehi;
+                anchor = s;
+            }
+            batch = hit >= 0 ? 1 : std::min<int64_t>(batch * 2, 4096);
+            continue;  // the loop re-finds the event (if any) in [s, stop] and resolves it
         }
         break;
     }

@@ -41,6 +41,13 @@ struct ChunkTable {
     void keys_with_digest(const uint8_t* d, std::vector<int32_t>* keys) const;
 };
 
+// One probe interval: positions [a, b) with the key R(p) = T(p) + E(p),
+// E(p) = (e_lo, e_hi + e_lo * (min(p, n-B) - min(anchor, n-B))) mod 2^16.
+struct ProbeInterval {
+    int64_t a, b, anchor;
+    uint32_t e_lo, e_hi;
+};
+
 // Device (or test) services used by the resolver.  Positions are source file offsets.
 class ScanBackend {
   public:
@@ -50,13 +57,23 @@ class ScanBackend {
     virtual const int32_t* aligned_weak() = 0;
     virtual const uint8_t* aligned_strong() = 0;  // digest_length bytes per window
     virtual const uint8_t* chain_flags() = 0;     // min(aligned_count, chunk_count) entries
-    virtual int32_t weak_at(int64_t p) = 0;       // T(p) over min(B, n - p) bytes
+    virtual void weak_many(const int64_t* pos, int64_t count, int32_t* out) = 0;  // T(p) over min(B, n-p) bytes
+    virtual void bytes_many(const int64_t* pos, int64_t count, uint8_t* out) = 0;
     virtual void md5_at(int64_t p, uint8_t out[16]) = 0;  // MD5(x[p, p + min(B, n-p)) || seed)
-    virtual uint8_t byte_at(int64_t p) = 0;
-    // First p in [a, b) with (T(p) + E(p)) in the key set (keys == nullptr: the whole chunk table),
-    // E(p) = (e_lo, e_hi + e_lo * (min(p, n-B) - min(anchor, n-B))) mod 2^16; -1 if none.
-    virtual int64_t first_hit(int64_t a, int64_t b, int64_t anchor, uint32_t e_lo, uint32_t e_hi,
-                              const std::vector<int32_t>* keys) = 0;
+    // Smallest p over all intervals whose key is in the key set (keys == nullptr: the whole chunk
+    // table); -1 if none.
+    virtual int64_t first_hit(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) = 0;
+
+    int32_t weak_at(int64_t p) {
+        int32_t r;
+        weak_many(&p, 1, &r);
+        return r;
+    }
+    uint8_t byte_at(int64_t p) {
+        uint8_t r;
+        bytes_many(&p, 1, &r);
+        return r;
+    }
 };
 
 struct ResolveResult {

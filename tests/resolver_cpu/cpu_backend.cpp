@@ -29,7 +29,7 @@ class CpuBackend : public rsh::ScanBackend {
         aw_.resize(na);
         as_.resize(na * dl_);
         for (int64_t k = 0; k < na; ++k) {
-            aw_[k] = weak_at(k * B_);
+            aw_[k] = weak1(k * B_);
             uint8_t d[16];
             md5_at(k * B_, d);
             memcpy(&as_[k * dl_], d, dl_);
@@ -43,19 +43,31 @@ class CpuBackend : public rsh::ScanBackend {
     const int32_t* aligned_weak() override { return aw_.data(); }
     const uint8_t* aligned_strong() override { return as_.data(); }
     const uint8_t* chain_flags() override { return fl_.data(); }
-    int32_t weak_at(int64_t p) override { return weak_of(x_ + p, wl(p)); }
+    int32_t weak1(int64_t p) { return weak_of(x_ + p, p < n_ ? wl(p) : 0); }
+    void weak_many(const int64_t* pos, int64_t count, int32_t* out) override {
+        for (int64_t i = 0; i < count; ++i) out[i] = weak1(pos[i]);
+    }
+    void bytes_many(const int64_t* pos, int64_t count, uint8_t* out) override {
+        for (int64_t i = 0; i < count; ++i) out[i] = x_[pos[i]];
+    }
     void md5_at(int64_t p, uint8_t out[16]) override {
         rsh::HostMd5 h;
         h.update(x_ + p, (size_t)wl(p));
         h.update(seed_, 4);
         h.final(out);
     }
-    uint8_t byte_at(int64_t p) override { return x_[p]; }
-    int64_t first_hit(int64_t a, int64_t b, int64_t anchor, uint32_t e_lo, uint32_t e_hi,
-                      const std::vector<int32_t>* keys) override {
+    int64_t first_hit(const rsh::ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) override {
+        for (int64_t i = 0; i < count; ++i) {
+            const int64_t p = first_hit1(iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo, iv[i].e_hi, keys);
+            if (p >= 0) return p;  // intervals are in increasing position order
+        }
+        return -1;
+    }
+    int64_t first_hit1(int64_t a, int64_t b, int64_t anchor, uint32_t e_lo, uint32_t e_hi,
+                       const std::vector<int32_t>* keys) {
         const int64_t nB = n_ - B_;
         auto cl = [&](int64_t p) { return p < nB ? p : nB; };
-        int32_t T = a < b ? weak_at(a) : 0;
+        int32_t T = a < b ? weak1(a) : 0;
         for (int64_t p = a; p < b; ++p) {
             const uint32_t eh = e_hi + e_lo * (uint32_t)(cl(p) - cl(anchor));
             const int32_t R = (int32_t)(((((uint32_t)T & 0xFFFFu) + e_lo) & 0xFFFFu) | ((((uint32_t)T >> 16) + eh) << 16));

@@ -160,3 +160,14 @@ def test_device_resident_entry_points(ctx):
     hev, fm, hlit, hmat, _ = ctx.match_scan(src, h, hw, hs, SEED)
     assert R.events_as_tuples(ev[:n_ev.value], B) == R.events_as_tuples(hev, B)
     assert (lit.value, mat.value) == (hlit, hmat)
+
+
+def test_sender_unrelated_batched_flush_chain(ctx):
+    """New content against a small table: the scan stays unpoisoned and desynced for thousands of
+    flush intervals, which the resolver speculates in geometrically growing batches (one probe launch
+    per batch instead of per interval)."""
+    B = 8192
+    basis = O.splitmix(8 << 20, 0x5EED5EED00000011).tobytes()
+    src = O.splitmix(64 << 20, 0x5EED5EED00000012).tobytes()
+    st = _sender_both(ctx, basis, src, B, 3)
+    assert st["flushes"] > 700 and st["probe_launches"] < 40
