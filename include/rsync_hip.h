@@ -115,6 +115,10 @@ int rsh_match_scan_device(rsh_ctx* ctx, const void* d_src, int64_t n, const rsh_
                           const void* d_strong, const uint8_t seed[4], rsh_event* ev, int64_t ev_cap,
                           int64_t* n_ev, int64_t* literal, int64_t* matched, rsh_scan_stats* stats);
 
+/* After RSH_E_NOSPACE from rsh_match_scan[_device] the context keeps that scan's events: fetch them into
+ * a buffer of at least *n_ev entries without recomputing (valid until the context's next scan). */
+int rsh_fetch_events(rsh_ctx* ctx, rsh_event* ev, int64_t ev_cap, int64_t* n_ev);
+
 /* Whole-file MD5 on the host (one serial chain; runs beside the device work). */
 int rsh_file_md5(const uint8_t* data, int64_t n, uint8_t out[16]);
 

@@ -91,6 +91,7 @@ struct rsh_ctx {
     hipStream_t aux = nullptr;                   // basis-table download beside the speculation kernel
     hipEvent_t ev_in = nullptr, ev_tab = nullptr;
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
+    std::vector<rsh_event> last_ev;  // kept when the caller's event buffer was too small
     ~rsh_ctx() {
         for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &slots, &dslots, &dkeys, &pos, &out,
                           &first, &win, &ivbuf, &tilebuf})
@@ -320,9 +321,13 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     return RSH_OK;
 }
 
-int emit_events(const rsh::ResolveResult& r, rsh_event* ev, int64_t cap, int64_t* n_ev) {
+int emit_events(rsh_ctx* c, rsh::ResolveResult& r, rsh_event* ev, int64_t cap, int64_t* n_ev) {
     *n_ev = (int64_t)r.ev.size();
-    if ((int64_t)r.ev.size() > cap || (!ev && !r.ev.empty())) return RSH_E_NOSPACE;
+    if ((int64_t)r.ev.size() > cap || (!ev && !r.ev.empty())) {
+        c->last_ev.swap(r.ev);  // rsh_fetch_events hands them out without a rescan
+        return RSH_E_NOSPACE;
+    }
+    c->last_ev.clear();
     if (!r.ev.empty()) memcpy(ev, r.ev.data(), r.ev.size() * sizeof(rsh_event));
     return RSH_OK;
 }
@@ -498,7 +503,7 @@ int rsh_match_scan_device(rsh_ctx* ctx, const void* d_src, int64_t n, const rsh_
     if (literal) *literal = r.literal;
     if (matched) *matched = r.matched;
     if (stats) *stats = r.stats;
-    return emit_events(r, ev, ev_cap, n_ev);
+    return emit_events(ctx, r, ev, ev_cap, n_ev);
 }
 
 int rsh_match_scan(rsh_ctx* ctx, const uint8_t* src, int64_t n, const rsh_header* h, const int32_t* weak,
@@ -539,7 +544,15 @@ int rsh_match_scan(rsh_ctx* ctx, const uint8_t* src, int64_t n, const rsh_header
     if (literal) *literal = r.literal;
     if (matched) *matched = r.matched;
     if (stats) *stats = r.stats;
-    return emit_events(r, ev, ev_cap, n_ev);
+    return emit_events(ctx, r, ev, ev_cap, n_ev);
+}
+
+int rsh_fetch_events(rsh_ctx* ctx, rsh_event* ev, int64_t ev_cap, int64_t* n_ev) {
+    if (!ctx || !n_ev) return RSH_E_INVAL;
+    *n_ev = (int64_t)ctx->last_ev.size();
+    if (*n_ev > ev_cap || (!ev && *n_ev > 0)) return RSH_E_NOSPACE;
+    if (*n_ev > 0) memcpy(ev, ctx->last_ev.data(), ctx->last_ev.size() * sizeof(rsh_event));
+    return RSH_OK;
 }
 
 int rsh_file_md5(const uint8_t* data, int64_t n, uint8_t out[16]) {

@@ -107,12 +107,17 @@ JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksu
     }
     jbyte s4[4];
     (*env)->GetByteArrayRegion(env, seed, 0, 4, s4);
-    jint* w = (*env)->GetPrimitiveArrayCritical(env, weakOut, NULL);
-    jbyte* st = (*env)->GetPrimitiveArrayCritical(env, strongOut, NULL);
-    rc = (w && st) ? rsh_block_sums((rsh_ctx*)(intptr_t)ctx, p, n, &h, (const uint8_t*)s4, (int32_t*)w, (uint8_t*)st)
-                   : RSH_E_NOMEM;
-    if (st) (*env)->ReleasePrimitiveArrayCritical(env, strongOut, st, 0);
-    if (w) (*env)->ReleasePrimitiveArrayCritical(env, weakOut, w, 0);
+    /* the call can run for seconds: native buffers, not JNI critical regions (which would stall GC) */
+    const size_t C = (size_t)(h.chunk_count > 0 ? h.chunk_count : 0), dl = (size_t)(h.digest_length > 0 ? h.digest_length : 0);
+    int32_t* w = (int32_t*)malloc(C * 4 + 4);
+    uint8_t* st = (uint8_t*)malloc(C * dl + 1);
+    rc = (w && st) ? rsh_block_sums((rsh_ctx*)(intptr_t)ctx, p, n, &h, (const uint8_t*)s4, w, st) : RSH_E_NOMEM;
+    if (rc == RSH_OK) {
+        (*env)->SetIntArrayRegion(env, weakOut, 0, (jsize)C, (const jint*)w);
+        (*env)->SetByteArrayRegion(env, strongOut, 0, (jsize)(C * dl), (const jbyte*)st);
+    }
+    free(st);
+    free(w);
     if (rc != RSH_OK) throw_status(env, rc);
 }
 
@@ -139,24 +144,38 @@ JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeC
     }
     jbyte s4[4];
     (*env)->GetByteArrayRegion(env, seed, 0, 4, s4);
-    int64_t cap = 1024, n_ev = 0, lit = 0, mat = 0;
-    rsh_event* ev = NULL;
+    /* one literal per flush interval plus a literal and a match run per chunk; a short buffer is not
+       a rescan: the context keeps the events for rsh_fetch_events */
+    int64_t cap = (n / (10 * (int64_t)(h.block_length > 0 ? h.block_length : 8192))) + 2 * (int64_t)h.chunk_count + 64;
+    int64_t n_ev = 0, lit = 0, mat = 0;
+    rsh_event* ev = (rsh_event*)malloc((size_t)cap * sizeof(rsh_event));
     uint8_t md5[16];
-    for (;;) {
-        rsh_event* grown = (rsh_event*)realloc(ev, (size_t)cap * sizeof(rsh_event));
-        if (!grown) {
+    if (!ev) {
+        rc = RSH_E_NOMEM;
+    } else {
+        /* copies of the (small) received table: no JNI critical region across a long scan */
+        const jsize nw = weak ? (*env)->GetArrayLength(env, weak) : 0;
+        const jsize ns = strong ? (*env)->GetArrayLength(env, strong) : 0;
+        int32_t* w = (int32_t*)malloc((size_t)nw * 4 + 4);
+        uint8_t* st = (uint8_t*)malloc((size_t)ns + 1);
+        if (!w || !st) {
             rc = RSH_E_NOMEM;
-            break;
+        } else {
+            if (nw) (*env)->GetIntArrayRegion(env, weak, 0, nw, (jint*)w);
+            if (ns) (*env)->GetByteArrayRegion(env, strong, 0, ns, (jbyte*)st);
+            rc = rsh_match_scan((rsh_ctx*)(intptr_t)ctx, p, n, &h, nw ? w : NULL, ns ? st : NULL, (const uint8_t*)s4,
+                                ev, cap, &n_ev, md5, &lit, &mat, NULL);
         }
-        ev = grown;
-        jint* w = weak ? (*env)->GetPrimitiveArrayCritical(env, weak, NULL) : NULL;
-        jbyte* st = strong ? (*env)->GetPrimitiveArrayCritical(env, strong, NULL) : NULL;
-        rc = rsh_match_scan((rsh_ctx*)(intptr_t)ctx, p, n, &h, (const int32_t*)w, (const uint8_t*)st,
-                            (const uint8_t*)s4, ev, cap, &n_ev, md5, &lit, &mat, NULL);
-        if (st) (*env)->ReleasePrimitiveArrayCritical(env, strong, st, JNI_ABORT);
-        if (w) (*env)->ReleasePrimitiveArrayCritical(env, weak, w, JNI_ABORT);
-        if (rc != RSH_E_NOSPACE) break;
-        cap = n_ev;
+        free(st);
+        free(w);
+        if (rc == RSH_E_NOSPACE) {
+            rsh_event* grown = (rsh_event*)realloc(ev, (size_t)n_ev * sizeof(rsh_event));
+            if (!grown) rc = RSH_E_NOMEM;
+            else {
+                ev = grown;
+                rc = rsh_fetch_events((rsh_ctx*)(intptr_t)ctx, ev, n_ev, &n_ev);
+            }
+        }
     }
     if (rc != RSH_OK) {
         free(ev);

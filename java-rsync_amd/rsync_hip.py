@@ -66,7 +66,7 @@ EVENT_DTYPE = np.dtype([("offset", "<i8"), ("length", "<i8"), ("kind", "<i4"), (
 EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_device_count", "rsh_ctx_create", "rsh_ctx_destroy",
            "rsh_ctx_stream", "rsh_block_length_for", "rsh_digest_length_for", "rsh_header_make",
            "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
-           "rsh_match_scan_device", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
+           "rsh_match_scan_device", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
            "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 
 _LIB = None
@@ -105,6 +105,7 @@ def lib():
                             ctypes.POINTER(I64), ctypes.POINTER(ScanStats)], ctypes.c_int),
         "rsh_match_scan_device": ([P, P, I64, HP, P, P, P, P, I64, ctypes.POINTER(I64), ctypes.POINTER(I64),
                                    ctypes.POINTER(I64), ctypes.POINTER(ScanStats)], ctypes.c_int),
+        "rsh_fetch_events": ([P, P, I64, ctypes.POINTER(I64)], ctypes.c_int),
         "rsh_file_md5": ([P, I64, P], ctypes.c_int),
         "rsh_tokens_size": ([P, I64], I64),
         "rsh_tokens_write": ([P, P, I64, P, P, I64], ctypes.c_int),
@@ -257,20 +258,20 @@ class Context:
         s = np.frombuffer(bytes(seed), np.uint8).copy()
         w = np.ascontiguousarray(weak, dtype=np.int32)
         st = np.ascontiguousarray(strong, dtype=np.uint8)
-        cap = ev_cap if ev_cap is not None else 1024
-        while True:
-            ev = np.zeros(max(cap, 1), EVENT_DTYPE)
-            n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-            fm = np.zeros(16, np.uint8)
-            stats = ScanStats()
-            rc = lib().rsh_match_scan(self._p, _ptr(a), a.size, ctypes.byref(h), _ptr(w) if w.size else None,
-                                      _ptr(st) if st.size else None, _ptr(s), _ptr(ev), cap, ctypes.byref(n_ev),
-                                      _ptr(fm), ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(stats))
-            if rc == RSH_E_NOSPACE and ev_cap is None:
-                cap = n_ev.value
-                continue
-            _check(rc)
-            return ev[:n_ev.value], fm.tobytes(), lit.value, mat.value, stats.as_dict()
+        # upper estimate: one literal per flush interval plus a literal and a match run per chunk
+        cap = ev_cap if ev_cap is not None else int(a.size // max(10 * h.block_length, 1) + 2 * h.chunk_count + 64)
+        ev = np.zeros(max(cap, 1), EVENT_DTYPE)
+        n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        fm = np.zeros(16, np.uint8)
+        stats = ScanStats()
+        rc = lib().rsh_match_scan(self._p, _ptr(a), a.size, ctypes.byref(h), _ptr(w) if w.size else None,
+                                  _ptr(st) if st.size else None, _ptr(s), _ptr(ev), cap, ctypes.byref(n_ev),
+                                  _ptr(fm), ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(stats))
+        if rc == RSH_E_NOSPACE and ev_cap is None:  # the context kept them: fetch, no rescan
+            ev = np.zeros(n_ev.value, EVENT_DTYPE)
+            rc = lib().rsh_fetch_events(self._p, _ptr(ev), n_ev.value, ctypes.byref(n_ev))
+        _check(rc)
+        return ev[:n_ev.value], fm.tobytes(), lit.value, mat.value, stats.as_dict()
 
 
 class DeviceBuffer:
