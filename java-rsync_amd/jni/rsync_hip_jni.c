@@ -160,6 +160,8 @@ JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeC
         uint8_t* st = (uint8_t*)malloc((size_t)ns + 1);
         if (!w || !st) {
             rc = RSH_E_NOMEM;
+        } else if (h.chunk_count > 0 && (nw < h.chunk_count || (jlong)ns < (jlong)h.chunk_count * h.digest_length)) {
+            rc = RSH_E_INVAL; /* received table shorter than its header says */
         } else {
             if (nw) (*env)->GetIntArrayRegion(env, weak, 0, nw, (jint*)w);
             if (ns) (*env)->GetByteArrayRegion(env, strong, 0, ns, (jbyte*)st);
