@@ -16,6 +16,7 @@ import argparse
 import ctypes
 import json
 import os
+import queue
 import sys
 import time
 
@@ -45,6 +46,11 @@ def parse():
     ap.add_argument("--block", type=int, default=131072)
     ap.add_argument("--digest", type=int, default=4)
     ap.add_argument("--variant", choices=["half", "identical"], default="half")
+    ap.add_argument("--workload", choices=["file", "files"], default="file",
+                    help="file: config 5 (one 16 GiB pair per GPU); files: config 4 (many 128 MiB pairs per GPU)")
+    ap.add_argument("--files", type=int, default=128, help="files per GPU for --workload files")
+    ap.add_argument("--file-mib", type=int, default=128)
+    ap.add_argument("--threads", type=int, default=8, help="Sender scan contexts per GPU (--workload files)")
     ap.add_argument("--cpu-sample-mib", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -52,6 +58,8 @@ def parse():
 
 def main():
     a = parse()
+    if a.workload == "files":
+        return main_files(a)
     import torch
     import torch.distributed as dist
 
@@ -187,6 +195,119 @@ def main():
         res["cpu_baseline"] = cpu_baseline(src, basis, B, dl, a.cpu_sample_mib << 20)
     if rank == 0:
         print(json.dumps(res), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_files(a):
+    """BASELINE config 4: F files x S MiB per GPU (1024 x 128 MiB over 8 GPUs).  Every file is a multiple of
+    B, so the F basis files laid end to end form one array whose chunk table is the per-file tables back
+    to back: the Generator is one launch.  The F Sender scans (one per file, each with its own table) run
+    on a pool of contexts, one stream each, so their speculation kernels and resolvers overlap."""
+    import concurrent.futures as cf
+
+    import torch
+    rank, world, local = shard.env_rank()
+    torch.cuda.set_device(local)
+    if world > 1:
+        shard.init_distributed("nccl", torch.device("cuda", local))
+    if not os.path.exists(R.LIB_PATH):
+        R.build()
+    L = R.lib()
+    F, S = a.files, a.file_mib << 20
+    B = R.block_length_for(S)
+    dl = R.digest_length_for(S, B)
+    h1 = R.header_make(B, dl, S)
+    C1 = h1.chunk_count
+    assert S % B == 0
+    n = F * S
+    seed = np.frombuffer(bytes([1, 2, 3, 4]), np.uint8).copy()
+    hall = R.header_make(B, dl, n)
+    ctx = R.Context(local)
+    pool_ctx = [R.Context(local) for _ in range(a.threads)]
+    key = KEY_SRC ^ (rank << 20) ^ 0x4F11E5
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    basis = torch.empty(n, dtype=torch.uint8, device="cuda")
+    assert L.rsh_fill_splitmix_device(ctx.handle, src.data_ptr(), n, key, 0) == 0
+    assert L.rsh_fill_splitmix_device(ctx.handle, basis.data_ptr(), n, key, 0) == 0
+    if a.variant == "half":
+        other = torch.empty(n, dtype=torch.uint8, device="cuda")
+        assert L.rsh_fill_splitmix_device(ctx.handle, other.data_ptr(), n, KEY_EDIT ^ key, 0) == 0
+        ctx.sync()
+        basis.view(-1, B)[1::2] = other.view(-1, B)[1::2]
+        del other
+    torch.cuda.synchronize()
+    ctx.sync()
+    d_weak = torch.empty(F * C1, dtype=torch.int32, device="cuda")
+    d_strong = torch.empty(F * C1 * dl, dtype=torch.uint8, device="cuda")
+    caps = C1 + S // B + 4096
+
+    free_ctx = queue.SimpleQueue()  # a context serves one call at a time (rsync_hip.h)
+    for c in pool_ctx:
+        free_ctx.put(c)
+
+    def scan(i):
+        c = free_ctx.get()
+        try:
+            return scan_on(i, c)
+        finally:
+            free_ctx.put(c)
+
+    def scan_on(i, c):
+        ev = np.zeros(caps, R.EVENT_DTYPE)
+        n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        rc = L.rsh_match_scan_device(c.handle, ctypes.c_void_p(src.data_ptr() + i * S), S, ctypes.byref(h1),
+                                     ctypes.c_void_p(d_weak.data_ptr() + 4 * i * C1),
+                                     ctypes.c_void_p(d_strong.data_ptr() + i * C1 * dl), seed.ctypes.data,
+                                     ev.ctypes.data, caps, ctypes.byref(n_ev), ctypes.byref(lit), ctypes.byref(mat),
+                                     None)
+        assert rc == 0, (rc, L.rsh_last_error().decode())
+        assert lit.value + mat.value == S
+        return mat.value
+
+    ex = cf.ThreadPoolExecutor(max_workers=a.threads)
+
+    def step():
+        rc = L.rsh_block_sums_device(ctx.handle, ctypes.c_void_p(basis.data_ptr()), n, ctypes.byref(hall),
+                                     seed.ctypes.data, ctypes.c_void_p(d_weak.data_ptr()),
+                                     ctypes.c_void_p(d_strong.data_ptr()))
+        assert rc == 0
+        ctx.sync()  # tables ready before the scans (other streams)
+        futs = [ex.submit(scan, i) for i in range(F)]
+        return sum(f.result() for f in futs)
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    matched = 0
+    for _ in range(a.steps):
+        matched = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device="cuda")
+    value = world * a.steps * 2 * n / dt / (1 << 30)
+    res = {
+        "metric": "GiB/s device-resident rolling+MD5 scan (Generator block sums + Sender match scan)",
+        "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64 on device)",
+        "config": {"workload": f"config4: {F} files x {a.file_mib} MiB per GPU "
+                               f"({'50%-modified' if a.variant == 'half' else 'identical'} bases), B={B}, dl={dl}",
+                   "bytes_per_step_per_gpu": 2 * n, "files_per_gpu": F, "block_length": B, "digest_length": dl,
+                   "parallelism": f"file-sharded x{world} (no collectives), {a.threads} scan contexts per GPU"},
+        "scan": {"matched_bytes_per_step_per_gpu": int(matched)},
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    ex.shutdown()
+    for c in pool_ctx:
+        c.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

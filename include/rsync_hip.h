@@ -39,6 +39,7 @@ extern "C" {
 #define RSH_E_NOSPACE (-4)  /* event buffer too small; *n_ev holds the count needed          */
 #define RSH_E_DEVICE (-5)   /* HIP runtime / kernel failure, or no gfx950 device present     */
 #define RSH_E_NOMEM (-6)    /* host or device allocation failed                              */
+#define RSH_E_BUSY (-7)     /* the context is serving a call on another thread               */
 
 /* Checksum.Header; wire order of Connection.sendChecksumHeader (Connection.java:40-45) is
  * chunk_count, block_length, digest_length, remainder (4 x little-endian int32). */
@@ -79,6 +80,8 @@ typedef struct rsh_ctx rsh_ctx;
 
 int rsh_abi_version(void);
 const char* rsh_strerror(int status);
+/* Text of the calling thread's last HIP failure (error string and source line), "" if none. */
+const char* rsh_last_error(void);
 int rsh_device_count(int* count);
 int rsh_ctx_create(int device, rsh_ctx** out);
 void rsh_ctx_destroy(rsh_ctx* ctx);

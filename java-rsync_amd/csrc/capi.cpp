@@ -1,9 +1,11 @@
 // capi.cpp -- the C-ABI of include/rsync_hip.h: contexts, device memory, the HIP scan backend and the
 // host-side glue that mirrors Generator.sendItemizeAndChecksums / Sender.sendFiles per-file handling.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <thread>
 #include <vector>
@@ -92,6 +94,7 @@ struct rsh_ctx {
     hipEvent_t ev_in = nullptr, ev_tab = nullptr;
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
     std::vector<rsh_event> last_ev;  // kept when the caller's event buffer was too small
+    std::atomic<bool> busy{false};   // the staging buffers and last_ev serve one call at a time
     ~rsh_ctx() {
         for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &slots, &dslots, &dkeys, &pos, &out,
                           &first, &win, &ivbuf, &tilebuf})
@@ -104,13 +107,40 @@ struct rsh_ctx {
     }
 };
 
+// Last HIP failure of the calling thread (rsh_last_error): error text and the capi.cpp line.
+static thread_local char g_last_err[256] = "";
+static void note_error(hipError_t e, int line) {
+    snprintf(g_last_err, sizeof(g_last_err), "%s (capi.cpp:%d)", hipGetErrorString(e), line);
+}
+
 #define RSH_HIP(call)                                   \
     do {                                                \
         hipError_t e_ = (call);                         \
-        if (e_ != hipSuccess) return RSH_E_DEVICE;      \
+        if (e_ != hipSuccess) {                         \
+            note_error(e_, __LINE__);                   \
+            return RSH_E_DEVICE;                        \
+        }                                               \
     } while (0)
 
 namespace {
+
+// Claims a context for one call that uses its buffers; a second thread gets RSH_E_BUSY instead of
+// racing on them (one rsh_ctx per calling thread, rsync_hip.h).
+struct CtxClaim {
+    rsh_ctx* c;
+    bool held;
+    explicit CtxClaim(rsh_ctx* ctx) : c(ctx), held(!ctx->busy.exchange(true, std::memory_order_acquire)) {}
+    ~CtxClaim() {
+        if (held) c->busy.store(false, std::memory_order_release);
+    }
+};
+
+#define RSH_CLAIM(ctx)                                                                   \
+    CtxClaim claim_(ctx);                                                                \
+    if (!claim_.held) {                                                                  \
+        snprintf(g_last_err, sizeof(g_last_err), "context in use by another thread");   \
+        return RSH_E_BUSY;                                                               \
+    }
 
 // ------------------------------------------------------------------------------------------------
 // HIP implementation of the resolver's services.
@@ -215,8 +245,11 @@ class HipBackend : public rsh::ScanBackend {
     }
 
   private:
-    void ok(hipError_t e) {
-        if (e != hipSuccess && err == hipSuccess) err = e;
+    void ok(hipError_t e, int line = __builtin_LINE()) {
+        if (e != hipSuccess && err == hipSuccess) {
+            err = e;
+            note_error(e, line);
+        }
     }
     rsh_ctx* c_;
     const uint8_t* x_;
@@ -345,6 +378,8 @@ extern "C" {
 
 int rsh_abi_version(void) { return RSH_ABI_VERSION; }
 
+const char* rsh_last_error(void) { return g_last_err; }
+
 const char* rsh_strerror(int status) {
     switch (status) {
         case RSH_OK: return "ok";
@@ -354,6 +389,7 @@ const char* rsh_strerror(int status) {
         case RSH_E_NOSPACE: return "event buffer too small";
         case RSH_E_DEVICE: return "HIP device error or no gfx950 device";
         case RSH_E_NOMEM: return "out of memory";
+        case RSH_E_BUSY: return "context in use by another thread";
         default: return "unknown status";
     }
 }
@@ -470,6 +506,7 @@ int rsh_block_sums(rsh_ctx* ctx, const uint8_t* data, int64_t n, const rsh_heade
     if (rc != RSH_OK) return rc;
     if (h->chunk_count == 0) return RSH_OK;
     if (!data || !weak_out || (!strong_out && h->digest_length > 0)) return RSH_E_INVAL;
+    RSH_CLAIM(ctx);
     RSH_HIP(hipSetDevice(ctx->device));
     const size_t C = (size_t)h->chunk_count, dl = (size_t)h->digest_length;
     RSH_HIP(ctx->data.ensure((size_t)n));
@@ -490,6 +527,7 @@ int rsh_match_scan_device(rsh_ctx* ctx, const void* d_src, int64_t n, const rsh_
     if (!ctx || !h || !seed || !n_ev || n < 0) return RSH_E_INVAL;
     const int v = rsh_header_validate(h);
     if (v != RSH_OK) return v;
+    RSH_CLAIM(ctx);
     RSH_HIP(hipSetDevice(ctx->device));
     rsh::ResolveResult r;
     if (h->block_length == 0) {
@@ -512,6 +550,7 @@ int rsh_match_scan(rsh_ctx* ctx, const uint8_t* src, int64_t n, const rsh_header
     if (!ctx || !h || !seed || !n_ev || !file_md5 || n < 0 || (n > 0 && !src)) return RSH_E_INVAL;
     const int v = rsh_header_validate(h);
     if (v != RSH_OK) return v;
+    RSH_CLAIM(ctx);
     RSH_HIP(hipSetDevice(ctx->device));
     // the whole-file digest (Sender.java:1241,1326) is one serial chain: host thread, beside the device
     std::thread md5_thread([&] {
@@ -549,6 +588,7 @@ int rsh_match_scan(rsh_ctx* ctx, const uint8_t* src, int64_t n, const rsh_header
 
 int rsh_fetch_events(rsh_ctx* ctx, rsh_event* ev, int64_t ev_cap, int64_t* n_ev) {
     if (!ctx || !n_ev) return RSH_E_INVAL;
+    RSH_CLAIM(ctx);
     *n_ev = (int64_t)ctx->last_ev.size();
     if (*n_ev > ev_cap || (!ev && *n_ev > 0)) return RSH_E_NOSPACE;
     if (*n_ev > 0) memcpy(ev, ctx->last_ev.data(), ctx->last_ev.size() * sizeof(rsh_event));

@@ -9,6 +9,7 @@
  *   RSH_E_OVERFLOW -> ...internal.session.Checksum$ChunkOverflow     (Checksum.java:58-64,107-111)
  *   RSH_E_INVAL    -> java.lang.IllegalArgumentException
  *   RSH_E_NOMEM    -> java.lang.OutOfMemoryError
+ *   RSH_E_BUSY     -> java.lang.IllegalStateException (a context shared across threads; use forThread())
  *   RSH_E_DEVICE   -> java.lang.IllegalStateException (caller falls back to the Java path only if it
  *                     chose to; the library itself never falls back)
  * File I/O stays in Java (FileView semantics incl. zero-fill after read errors, FileView.java:209-271);

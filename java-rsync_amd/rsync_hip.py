@@ -21,12 +21,17 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "librsynchip.so")
 
-RSH_OK, RSH_E_INVAL, RSH_E_PROTOCOL, RSH_E_OVERFLOW, RSH_E_NOSPACE, RSH_E_DEVICE, RSH_E_NOMEM = 0, -1, -2, -3, -4, -5, -6
+RSH_OK, RSH_E_INVAL, RSH_E_PROTOCOL, RSH_E_OVERFLOW, RSH_E_NOSPACE, RSH_E_DEVICE, RSH_E_NOMEM, RSH_E_BUSY = \
+    0, -1, -2, -3, -4, -5, -6, -7
 EV_LITERAL, EV_MATCH = 1, 2
 
 
 class ProtocolError(Exception):
     """RsyncProtocolException (Connection.receiveChecksumHeader, Connection.java:28-38)."""
+
+
+class ContextBusyError(RuntimeError):
+    """RSH_E_BUSY: a Context was called from two threads at once (use one Context per thread)."""
 
 
 class DeviceError(RuntimeError):
@@ -63,7 +68,7 @@ EVENT_DTYPE = np.dtype([("offset", "<i8"), ("length", "<i8"), ("kind", "<i4"), (
                         ("count", "<i4"), ("reserved", "<i4")])
 
 # every symbol include/rsync_hip.h declares
-EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_device_count", "rsh_ctx_create", "rsh_ctx_destroy",
+EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_count", "rsh_ctx_create", "rsh_ctx_destroy",
            "rsh_ctx_stream", "rsh_block_length_for", "rsh_digest_length_for", "rsh_header_make",
            "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
            "rsh_match_scan_device", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
@@ -90,6 +95,7 @@ def lib():
     sig = {
         "rsh_abi_version": ([], ctypes.c_int),
         "rsh_strerror": ([ctypes.c_int], ctypes.c_char_p),
+        "rsh_last_error": ([], ctypes.c_char_p),
         "rsh_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "rsh_ctx_create": ([ctypes.c_int, ctypes.POINTER(P)], ctypes.c_int),
         "rsh_ctx_destroy": ([P], None),
@@ -136,7 +142,10 @@ def _check(rc):
         raise OverflowError(msg)
     if rc == RSH_E_NOMEM:
         raise MemoryError(msg)
-    raise DeviceError(msg)
+    if rc == RSH_E_BUSY:
+        raise ContextBusyError(msg)
+    detail = lib().rsh_last_error().decode()
+    raise DeviceError(f"{msg}: {detail}" if detail else msg)
 
 
 def _ptr(a):

@@ -104,3 +104,16 @@ def test_no_device_fails_loudly():
         pytest.skip("GPU present")
     with pytest.raises(R.DeviceError):
         R.Context(0)
+
+
+def test_status_strings_and_last_error():
+    L = R.lib()
+    codes = [R.RSH_OK, R.RSH_E_INVAL, R.RSH_E_PROTOCOL, R.RSH_E_OVERFLOW, R.RSH_E_NOSPACE, R.RSH_E_DEVICE,
+             R.RSH_E_NOMEM, R.RSH_E_BUSY]
+    texts = [L.rsh_strerror(c).decode() for c in codes]
+    assert len(set(texts)) == len(texts) and "unknown status" not in texts
+    assert "another thread" in L.rsh_strerror(R.RSH_E_BUSY).decode()
+    assert L.rsh_strerror(-99).decode() == "unknown status"
+    assert isinstance(L.rsh_last_error(), bytes)  # "" until a HIP call of this thread fails
+    with pytest.raises(R.ContextBusyError):
+        R._check(R.RSH_E_BUSY)

@@ -171,3 +171,80 @@ def test_sender_unrelated_batched_flush_chain(ctx):
     src = O.splitmix(64 << 20, 0x5EED5EED00000012).tobytes()
     st = _sender_both(ctx, basis, src, B, 3)
     assert st["flushes"] > 700 and st["probe_launches"] < 40
+
+
+def test_fetch_events_no_rescan(ctx):
+    """A too-small event buffer returns RSH_E_NOSPACE; rsh_fetch_events then hands out the same events
+    without re-running the scan."""
+    import ctypes
+    B = 512
+    basis = O.splitmix(60 * B, 21).tobytes()
+    src = O.splitmix(30 * B, 22).tobytes() + basis
+    h = R.header_make(B, 2, len(basis))
+    w, s = ctx.block_sums(basis, h, SEED)
+    full, fm, lit, mat, _ = ctx.match_scan(src, h, w, s, SEED)
+    a = np.frombuffer(src, np.uint8)
+    seed = np.frombuffer(SEED, np.uint8).copy()
+    ev = np.zeros(1, R.EVENT_DTYPE)
+    n_ev, l2, m2 = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    md5 = np.zeros(16, np.uint8)
+    rc = R.lib().rsh_match_scan(ctx.handle, a.ctypes.data, a.size, ctypes.byref(h), w.ctypes.data, s.ctypes.data,
+                                seed.ctypes.data, ev.ctypes.data, 1, ctypes.byref(n_ev), md5.ctypes.data,
+                                ctypes.byref(l2), ctypes.byref(m2), None)
+    assert rc == R.RSH_E_NOSPACE and n_ev.value == len(full) > 1
+    ev = np.zeros(n_ev.value, R.EVENT_DTYPE)
+    assert R.lib().rsh_fetch_events(ctx.handle, ev.ctypes.data, n_ev.value, ctypes.byref(n_ev)) == 0
+    assert R.events_as_tuples(ev, B) == R.events_as_tuples(full, B)
+    assert md5.tobytes() == fm and (l2.value, m2.value) == (lit, mat)
+
+
+def test_concurrent_contexts_and_busy(ctx):
+    """One context per thread (the reference runs Generator and Sender on separate threads): concurrent
+    scans on several contexts of one device equal the serial ones.  A context shared by two threads
+    answers RSH_E_BUSY to the loser instead of racing on its staging buffers."""
+    import concurrent.futures as cf
+    import threading
+    B = 2048
+    files = []
+    for i in range(12):
+        basis = O.splitmix(200 * B + 3 * i, 300 + i).tobytes()
+        src = basis[:50 * B] + O.splitmix(B // 2 + i, 400 + i).tobytes() + basis[50 * B + 7:]
+        h = R.header_make(B, 3, len(basis))
+        w, s = ctx.block_sums(basis, h, SEED)
+        files.append((src, h, w, s, ctx.match_scan(src, h, w, s, SEED)))
+    ctxs = [R.Context(0) for _ in range(4)]
+    try:
+        pool = {id(c): threading.Lock() for c in ctxs}
+
+        def run(i):
+            c = ctxs[i % len(ctxs)]
+            with pool[id(c)]:
+                src, h, w, s, _ = files[i]
+                return c.match_scan(src, h, w, s, SEED)
+
+        with cf.ThreadPoolExecutor(4) as ex:
+            got = list(ex.map(run, range(len(files))))
+        for (src, h, w, s, want), g in zip(files, got):
+            assert R.events_as_tuples(g[0], B) == R.events_as_tuples(want[0], B)
+            assert g[1:4] == want[1:4]
+
+        shared = ctxs[0]
+        src, h, w, s, want = files[0]
+        big = O.splitmix(48 << 20, 77).tobytes()
+        hb = R.header_make(8192, 3, len(big))
+        wb, sb = shared.block_sums(big, hb, SEED)
+        outcome = []
+
+        def on_shared(args):
+            try:
+                outcome.append(shared.match_scan(*args, SEED)[1:4])
+            except R.ContextBusyError:
+                outcome.append("busy")
+
+        with cf.ThreadPoolExecutor(2) as ex:
+            list(ex.map(on_shared, [(big, hb, wb, sb), (src, h, w, s)] * 3))
+        assert all(o == "busy" or isinstance(o, tuple) for o in outcome)
+        assert want[1:4] in outcome or "busy" in outcome
+    finally:
+        for c in ctxs:
+            c.close()
