@@ -2,6 +2,7 @@
 // host-side glue that mirrors Generator.sendItemizeAndChecksums / Sender.sendFiles per-file handling.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -89,19 +90,29 @@ struct rsh_ctx {
     hipStream_t stream = nullptr;
     DevBuf data, weak, strong;                   // host-input staging
     DevBuf src_weak, src_strong, flags;          // aligned speculation over the source
-    DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf;
-    hipStream_t aux = nullptr;                   // basis-table download beside the speculation kernel
-    hipEvent_t ev_in = nullptr, ev_tab = nullptr;
+    DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw;
+    hipStream_t aux = nullptr;                   // table download, then the aligned speculation
+    hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr;
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
+    // resolver round trips: the small kernels read their inputs from and write their outputs to pinned
+    // host memory directly (no staging copies); the probe result and digest windows come back by copy
+    PinnedBuf h_pos, h_out, h_iv, h_tiles, h_keys, h_first, h_win;
+    uint64_t first_used = 0;    // probe result slots handed out (see HipBackend::first_hit)
+    int* abort_word = nullptr;  // device, uncached: the speculation launch of generation g stops once it reads g
+    int gen = 0;
     std::vector<rsh_event> last_ev;  // kept when the caller's event buffer was too small
     std::atomic<bool> busy{false};   // the staging buffers and last_ev serve one call at a time
     ~rsh_ctx() {
         for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &slots, &dslots, &dkeys, &pos, &out,
-                          &first, &win, &ivbuf, &tilebuf})
+                          &first, &win, &ivbuf, &tilebuf, &haw})
             b->release();
-        for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl}) b->release();
+        for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pos, &h_out, &h_iv, &h_tiles, &h_keys, &h_first,
+                             &h_win})
+            b->release();
+        if (abort_word) (void)hipFree(abort_word);
         if (ev_in) (void)hipEventDestroy(ev_in);
         if (ev_tab) (void)hipEventDestroy(ev_tab);
+        if (ev_spec) (void)hipEventDestroy(ev_spec);
         if (aux) (void)hipStreamDestroy(aux);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -145,6 +156,8 @@ struct CtxClaim {
 // ------------------------------------------------------------------------------------------------
 // HIP implementation of the resolver's services.
 // ------------------------------------------------------------------------------------------------
+constexpr size_t kFirstSlots = 1024;
+
 class HipBackend : public rsh::ScanBackend {
   public:
     HipBackend(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh::ChunkTable& t, const uint8_t seed[4])
@@ -157,42 +170,48 @@ class HipBackend : public rsh::ScanBackend {
     const uint8_t* as = nullptr;
     const uint8_t* fl = nullptr;
     rsh::ProbeTable table{};
+    // Head mode: the speculation is still running on its own stream.  The resolver then sees no aligned
+    // data, batched probes stay short, and the probe kernel's per-block anchors T(kB) come from c_->haw,
+    // filled on demand for the blocks a probe touches.
+    bool head = false;
+    std::vector<uint8_t> haw_ready;
 
-    int64_t aligned_count() override { return na; }
+    int64_t aligned_count() override { return head ? 0 : na; }
+    int64_t max_batch() override { return head ? 4 : 4096; }
     const int32_t* aligned_weak() override { return aw; }
     const uint8_t* aligned_strong() override { return as; }
     const uint8_t* chain_flags() override { return fl; }
 
     void weak_many(const int64_t* pos, int64_t count, int32_t* out) override {
         if (count <= 0) return;
-        ok(c_->pos.ensure((size_t)count * sizeof(int64_t)));
-        ok(c_->out.ensure((size_t)count * sizeof(int32_t)));
+        int64_t* hp = pin<int64_t>(c_->h_pos, count);
+        int32_t* ho = pin<int32_t>(c_->h_out, count);
         if (err != hipSuccess) return;
-        ok(hipMemcpyAsync(c_->pos.p, pos, (size_t)count * sizeof(int64_t), hipMemcpyHostToDevice, c_->stream));
-        ok(rsh::launch_window_weak(x_, n_, (uint32_t)B_, c_->pos.as<int64_t>(), (uint32_t)count, c_->out.as<int32_t>(),
-                                   c_->stream));
-        ok(hipMemcpyAsync(out, c_->out.p, (size_t)count * sizeof(int32_t), hipMemcpyDeviceToHost, c_->stream));
+        memcpy(hp, pos, (size_t)count * sizeof(int64_t));
+        ok(rsh::launch_window_weak(x_, n_, (uint32_t)B_, hp, (uint32_t)count, ho, c_->stream));
         ok(hipStreamSynchronize(c_->stream));
+        memcpy(out, ho, (size_t)count * sizeof(int32_t));
     }
     void bytes_many(const int64_t* pos, int64_t count, uint8_t* out) override {
         if (count <= 0) return;
-        ok(c_->pos.ensure((size_t)count * sizeof(int64_t)));
-        ok(c_->out.ensure((size_t)count * sizeof(int32_t)));
+        int64_t* hp = pin<int64_t>(c_->h_pos, count);
+        uint8_t* ho = pin<uint8_t>(c_->h_out, count);
         if (err != hipSuccess) return;
-        ok(hipMemcpyAsync(c_->pos.p, pos, (size_t)count * sizeof(int64_t), hipMemcpyHostToDevice, c_->stream));
-        ok(rsh::launch_gather_bytes(x_, c_->pos.as<int64_t>(), (uint32_t)count, c_->out.as<uint8_t>(), c_->stream));
-        ok(hipMemcpyAsync(out, c_->out.p, (size_t)count, hipMemcpyDeviceToHost, c_->stream));
+        memcpy(hp, pos, (size_t)count * sizeof(int64_t));
+        ok(rsh::launch_gather_bytes(x_, hp, (uint32_t)count, ho, c_->stream));
         ok(hipStreamSynchronize(c_->stream));
+        memcpy(out, ho, (size_t)count);
     }
     // A single window's digest is one serial MD5 chain: 64-wide waves give it nothing, so the rare
     // resolver misses (first table hit after a reset) are digested on the host from a D2H copy.
     void md5_at(int64_t p, uint8_t out[16]) override {
         const int64_t w = std::min<int64_t>(B_, n_ - p);
-        win_.resize((size_t)w);
-        ok(hipMemcpyAsync(win_.data(), x_ + p, (size_t)w, hipMemcpyDeviceToHost, c_->stream));
+        uint8_t* hw = pin<uint8_t>(c_->h_win, w);
+        if (err != hipSuccess) return;
+        ok(hipMemcpyAsync(hw, x_ + p, (size_t)w, hipMemcpyDeviceToHost, c_->stream));
         ok(hipStreamSynchronize(c_->stream));
         rsh::HostMd5 h;
-        h.update(win_.data(), (size_t)w);
+        h.update(hw, (size_t)w);
         h.update(seed_, 4);
         h.final(out);
     }
@@ -201,50 +220,67 @@ class HipBackend : public rsh::ScanBackend {
         if (keys) {
             const uint32_t ns = pow2_at_least(2 * keys->size() + 2);
             ok(c_->dslots.ensure(ns * sizeof(unsigned long long)));
-            ok(c_->dkeys.ensure((keys->size() + 1) * sizeof(int32_t)));
+            int32_t* hk = pin<int32_t>(c_->h_keys, (int64_t)keys->size() + 1);
             if (err != hipSuccess) return -1;
-            if (!keys->empty())
-                ok(hipMemcpyAsync(c_->dkeys.p, keys->data(), keys->size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                                  c_->stream));
+            if (!keys->empty()) memcpy(hk, keys->data(), keys->size() * sizeof(int32_t));
             ok(rsh::launch_table_clear(c_->dslots.as<unsigned long long>(), ns, c_->stream));
-            ok(rsh::launch_table_insert(c_->dslots.as<unsigned long long>(), ns - 1, c_->dkeys.as<int32_t>(),
-                                        (uint32_t)keys->size(), c_->stream));
+            ok(rsh::launch_table_insert(c_->dslots.as<unsigned long long>(), ns - 1, hk, (uint32_t)keys->size(),
+                                        c_->stream));
             tab.slots = c_->dslots.as<unsigned long long>();
             tab.mask = ns - 1;
         }
-        ivs_.resize((size_t)count);
         tiles_.clear();
-        for (int64_t i = 0; i < count; ++i) {
-            ivs_[i] = rsh::ProbeIv{iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo & 0xFFFFu, iv[i].e_hi & 0xFFFFu};
-            rsh::probe_tiles(iv[i].a, iv[i].b, B_, (int32_t)i, &tiles_);
-        }
-        ok(c_->first.ensure(sizeof(unsigned long long)));
-        ok(c_->ivbuf.ensure(ivs_.size() * sizeof(rsh::ProbeIv) + 1));
-        ok(c_->tilebuf.ensure(tiles_.size() * sizeof(rsh::ProbeTile) + 1));
+        for (int64_t i = 0; i < count; ++i) rsh::probe_tiles(iv[i].a, iv[i].b, B_, (int32_t)i, &tiles_);
+        rsh::ProbeIv* hiv = pin<rsh::ProbeIv>(c_->h_iv, count + 1);
+        rsh::ProbeTile* ht = pin<rsh::ProbeTile>(c_->h_tiles, (int64_t)tiles_.size() + 1);
+        unsigned long long* hf = pin<unsigned long long>(c_->h_first, 1);
+        // result slots preset to ~0 ("none") in batches: one memset per kFirstSlots probes
+        ok(c_->first.ensure(kFirstSlots * sizeof(unsigned long long)));
         if (err != hipSuccess) return -1;
-        if (!ivs_.empty())
-            ok(hipMemcpyAsync(c_->ivbuf.p, ivs_.data(), ivs_.size() * sizeof(rsh::ProbeIv), hipMemcpyHostToDevice,
-                              c_->stream));
-        if (!tiles_.empty())
-            ok(hipMemcpyAsync(c_->tilebuf.p, tiles_.data(), tiles_.size() * sizeof(rsh::ProbeTile),
-                              hipMemcpyHostToDevice, c_->stream));
+        if (c_->first_used % kFirstSlots == 0)
+            ok(hipMemsetAsync(c_->first.p, 0xFF, kFirstSlots * sizeof(unsigned long long), c_->stream));
+        unsigned long long* d_first = c_->first.as<unsigned long long>() + c_->first_used++ % kFirstSlots;
+        for (int64_t i = 0; i < count; ++i)
+            hiv[i] = rsh::ProbeIv{iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo & 0xFFFFu, iv[i].e_hi & 0xFFFFu};
+        if (!tiles_.empty()) memcpy(ht, tiles_.data(), tiles_.size() * sizeof(rsh::ProbeTile));
+        if (head) {  // anchors T(kB) for the blocks these tiles sit in
+            anchors_.clear();
+            for (const rsh::ProbeTile& t : tiles_) {
+                const int64_t k = t.q0 / B_;
+                if (!haw_ready[(size_t)k]) {
+                    haw_ready[(size_t)k] = 1;
+                    anchors_.push_back(k * B_);
+                }
+            }
+            if (!anchors_.empty()) {
+                int64_t* hp = pin<int64_t>(c_->h_pos, (int64_t)anchors_.size());
+                if (err != hipSuccess) return -1;
+                memcpy(hp, anchors_.data(), anchors_.size() * sizeof(int64_t));
+                ok(rsh::launch_window_weak(x_, n_, (uint32_t)B_, hp, (uint32_t)anchors_.size(), c_->haw.as<int32_t>(),
+                                           c_->stream, true));
+            }
+        }
         rsh::ProbeArgs A;
         A.data = x_;
         A.n = n_;
         A.B = (uint32_t)B_;
-        A.aligned_weak = c_->src_weak.as<int32_t>();
+        A.aligned_weak = head ? c_->haw.as<int32_t>() : c_->src_weak.as<int32_t>();
         A.table = tab;
-        A.ivs = c_->ivbuf.as<rsh::ProbeIv>();
-        A.tiles = c_->tilebuf.as<rsh::ProbeTile>();
-        A.first = c_->first.as<unsigned long long>();
+        A.ivs = hiv;
+        A.tiles = ht;
+        A.first = d_first;
         ok(rsh::launch_probe_first(A, (uint32_t)tiles_.size(), c_->stream));
-        unsigned long long r = ~0ull;
-        ok(hipMemcpyAsync(&r, c_->first.p, sizeof(r), hipMemcpyDeviceToHost, c_->stream));
+        ok(hipMemcpyAsync(hf, d_first, sizeof(unsigned long long), hipMemcpyDeviceToHost, c_->stream));
         ok(hipStreamSynchronize(c_->stream));
-        return r == ~0ull ? -1 : (int64_t)r;
+        return *hf == ~0ull ? -1 : (int64_t)*hf;
     }
 
   private:
+    template <class T>
+    T* pin(PinnedBuf& b, int64_t count, int line = __builtin_LINE()) {
+        ok(b.ensure((size_t)std::max<int64_t>(count, 1) * sizeof(T)), line);
+        return b.as<T>();
+    }
     void ok(hipError_t e, int line = __builtin_LINE()) {
         if (e != hipSuccess && err == hipSuccess) {
             err = e;
@@ -258,9 +294,8 @@ class HipBackend : public rsh::ScanBackend {
     int64_t B_;
     int dl_;
     uint8_t seed_[4];
-    std::vector<uint8_t> win_;
-    std::vector<rsh::ProbeIv> ivs_;
     std::vector<rsh::ProbeTile> tiles_;
+    std::vector<int64_t> anchors_;
 };
 
 // Header consistency for the Generator side (3-arg ctor semantics, Checksum.java:94-113).
@@ -278,6 +313,14 @@ int check_generator_header(int64_t n, const rsh_header* h) {
 
 // The device-resident Sender scan (everything but the whole-file MD5).  h validated by the caller;
 // n > 0, block_length > 0.  host_weak/host_strong may be null (then copied back from the device).
+//
+// Streams (two per context, so that contexts rarely share one of the device's few hardware queues):
+// `aux` downloads the received table and then runs the aligned speculation (K1 over the source +
+// chain flags + their download); `stream` builds the probe hash and carries the resolver's small
+// round trips.  The resolver starts in head mode as soon as the table is sorted, while the speculation
+// is still running; when the speculation lands it resumes with it.  If the scan ends first -- e.g. the
+// stale digest (quirk B) matches no chunk, after which only the closed-form flushes remain -- the
+// speculation launch is told to stop (abort word) and its results are never read.
 int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h, const int32_t* d_weak,
                 const uint8_t* d_strong, const int32_t* host_weak, const uint8_t* host_strong, const uint8_t seed[4],
                 rsh::ResolveResult* res) {
@@ -288,13 +331,26 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     const int64_t na = (n + B - 1) / B;
     if (na > 2147483647LL) return RSH_E_OVERFLOW;
     const int64_t nf = std::min<int64_t>(na, C);
+    const uint32_t ns = pow2_at_least(2 * (uint64_t)C + 2);
 
-    // (aux stream) the basis table, once whatever produced it on the main stream is done
-    RSH_HIP(hipEventRecord(c->ev_in, c->stream));
+    // every buffer first (hipMalloc may synchronise), then the asynchronous work
     const bool download = !host_weak || !host_strong;
     if (download) {
         RSH_HIP(c->h_weak.ensure((size_t)C * 4 + 4));
         RSH_HIP(c->h_strong.ensure((size_t)C * dl + 1));
+    }
+    RSH_HIP(c->slots.ensure((size_t)ns * sizeof(unsigned long long)));
+    RSH_HIP(c->src_weak.ensure((size_t)na * 4));
+    RSH_HIP(c->src_strong.ensure((size_t)na * dl + 1));
+    RSH_HIP(c->flags.ensure((size_t)nf + 1));
+    RSH_HIP(c->h_aw.ensure((size_t)na * 4));
+    RSH_HIP(c->h_as.ensure((size_t)na * dl + 1));
+    RSH_HIP(c->h_fl.ensure((size_t)nf + 1));
+    RSH_HIP(c->haw.ensure((size_t)na * 4));
+
+    RSH_HIP(hipEventRecord(c->ev_in, c->stream));  // whatever produced the inputs on the caller's stream
+    // (aux) the received table
+    if (download) {
         RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
         if (C > 0) {
             RSH_HIP(hipMemcpyAsync(c->h_weak.p, d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, c->aux));
@@ -304,28 +360,25 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         host_weak = c->h_weak.as<int32_t>();
         host_strong = c->h_strong.as<uint8_t>();
     }
-
-    // (main stream) device probe table, then the aligned speculation: the source's own block sums
-    // with the basis header's B and dl, the chain flags, and their download
-    const uint32_t ns = pow2_at_least(2 * (uint64_t)C + 2);
-    RSH_HIP(c->slots.ensure((size_t)ns * sizeof(unsigned long long)));
+    // (aux) the aligned speculation: the source's own block sums with the basis header's B and dl,
+    // the chain flags, and their download
+    const int gen = ++c->gen;
+    static const int diag = getenv("RSH_SCAN_DIAG") ? atoi(getenv("RSH_SCAN_DIAG")) : 0;  // A/B switches
+    if (!download) RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
+    RSH_HIP(rsh::launch_block_sums(d_src, n, (uint32_t)B, (uint32_t)na, (uint32_t)dl, seed_word(seed),
+                                   c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->aux,
+                                   (diag & 2) ? nullptr : c->abort_word, gen));
+    RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
+                                    (uint32_t)nf, (uint32_t)dl, c->flags.as<uint8_t>(), c->aux));
+    RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)na * 4, hipMemcpyDeviceToHost, c->aux));
+    if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)na * dl, hipMemcpyDeviceToHost, c->aux));
+    if (nf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)nf, hipMemcpyDeviceToHost, c->aux));
+    RSH_HIP(hipEventRecord(c->ev_spec, c->aux));
+    // (stream) the device probe hash
     RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, c->stream));
     RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, c->stream));
-    RSH_HIP(c->src_weak.ensure((size_t)na * 4));
-    RSH_HIP(c->src_strong.ensure((size_t)na * dl + 1));
-    RSH_HIP(rsh::launch_block_sums(d_src, n, (uint32_t)B, (uint32_t)na, (uint32_t)dl, seed_word(seed),
-                                   c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->stream));
-    RSH_HIP(c->flags.ensure((size_t)nf + 1));
-    RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
-                                    (uint32_t)nf, (uint32_t)dl, c->flags.as<uint8_t>(), c->stream));
-    RSH_HIP(c->h_aw.ensure((size_t)na * 4));
-    RSH_HIP(c->h_as.ensure((size_t)na * dl + 1));
-    RSH_HIP(c->h_fl.ensure((size_t)nf + 1));
-    RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)na * 4, hipMemcpyDeviceToHost, c->stream));
-    if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)na * dl, hipMemcpyDeviceToHost, c->stream));
-    if (nf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)nf, hipMemcpyDeviceToHost, c->stream));
 
-    // (host) sort the table while the speculation kernel runs
+    // (host) sort the table
     rsh::ChunkTable table;
     table.chunk_count = C;
     table.block_length = (int32_t)B;
@@ -338,7 +391,6 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     table.build();
     const double table_ms = ms_since(t1);
     RSH_HIP(hipStreamSynchronize(c->stream));
-    const double dev_ms = ms_since(t0);
 
     HipBackend be(c, d_src, n, table, seed);
     be.table.slots = c->slots.as<unsigned long long>();
@@ -347,9 +399,30 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     be.aw = c->h_aw.as<int32_t>();
     be.as = c->h_as.as<uint8_t>();
     be.fl = c->h_fl.as<uint8_t>();
-    rsh::resolve_scan(n, table, be, res);
+    be.head = !(diag & 1);
+    be.haw_ready.assign((size_t)na, 0);
+    rsh::ResolveState rs;
+    bool landed = false;
+    const bool done = rsh::resolve_run(n, table, be, &rs, res, [&] {
+        if (be.err != hipSuccess || !be.head) return true;
+        landed = hipEventQuery(c->ev_spec) != hipErrorNotReady;
+        if (!landed) res->stats.head_steps++;
+        return landed;
+    });
     if (be.err != hipSuccess) return RSH_E_DEVICE;
-    res->stats.device_ms += dev_ms;
+    if (done && !landed && hipEventQuery(c->ev_spec) == hipErrorNotReady) {
+        RSH_HIP(hipStreamWriteValue32(c->stream, c->abort_word, (uint32_t)gen, 0));  // the rest is dead work
+        res->stats.speculation_aborted = 1;
+        res->stats.device_ms += ms_since(t0);
+    } else {
+        RSH_HIP(hipEventSynchronize(c->ev_spec));
+        res->stats.device_ms += ms_since(t0);
+        if (!done) {
+            be.head = false;
+            rsh::resolve_run(n, table, be, &rs, res, nullptr);
+        }
+    }
+    if (be.err != hipSuccess) return RSH_E_DEVICE;
     res->stats.table_ms += table_ms;
     return RSH_OK;
 }
@@ -413,10 +486,14 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
     rsh_ctx* c = new (std::nothrow) rsh_ctx();
     if (!c) return RSH_E_NOMEM;
     c->device = device;
+    c->abort_word = nullptr;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_tab, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_tab, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming) != hipSuccess ||
+        hipExtMallocWithFlags(reinterpret_cast<void**>(&c->abort_word), 256, hipDeviceMallocUncached) != hipSuccess ||
+        hipMemset(c->abort_word, 0, 256) != hipSuccess) {  // generations start at 1
         delete c;
         return RSH_E_DEVICE;
     }
@@ -427,7 +504,8 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
 void rsh_ctx_destroy(rsh_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
+    for (hipStream_t st : {ctx->stream, ctx->aux})
+        if (st) (void)hipStreamSynchronize(st);
     delete ctx;
 }
 
@@ -437,6 +515,7 @@ int rsh_ctx_sync(rsh_ctx* ctx) {
     if (!ctx) return RSH_E_INVAL;
     RSH_HIP(hipSetDevice(ctx->device));
     RSH_HIP(hipStreamSynchronize(ctx->stream));
+    RSH_HIP(hipStreamSynchronize(ctx->aux));  // includes a cancelled speculation draining
     return RSH_OK;
 }
 

@@ -9,12 +9,15 @@ namespace rsh {
 
 // Generator block sums (Generator.java:886-895): chunk c covers [c*B, min((c+1)*B, n)).
 // Writes weak[c] and strong[c*dl .. c*dl+dl).  Also used by the Sender as aligned speculation.
+// abort_flag (optional, host-pinned): the launch stops early, leaving its outputs undefined, once
+// *abort_flag == abort_gen (the Sender's speculation when the resolver no longer needs it).
 hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks, uint32_t dl,
-                             uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s);
+                             uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s,
+                             const int* abort_flag = nullptr, int abort_gen = 0);
 
 hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks,
                                      uint32_t dl, uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong,
-                                     hipStream_t s);
+                                     hipStream_t s, const int* abort_flag = nullptr, int abort_gen = 0);
 
 // Chain flags for the Sender fast path: flag[k] = 1 iff source window k (aligned, from the source's
 // own block sums) has the same weak key and the same dl-byte digest as basis chunk k.
@@ -35,8 +38,8 @@ hipError_t launch_table_insert(unsigned long long* d_slots, uint32_t mask, const
 // the true weak sum of window [p, p + min(B, n - p)) and E(p) = (e_lo, e_hi + e_lo * (min(p, n-B) -
 // min(anchor, n-B))) mod 2^16 (the post-flush desync of Sender.java:1292-1310).  The work is cut into
 // tiles of PROBE_TILE positions inside aligned blocks [kB, kB + B); aligned_weak[k] = T(kB) (the
-// source's own block sums) anchors each block.  *first (uint64, preset to ~0) receives the smallest
-// hitting position over all tiles.
+// source's own block sums) anchors each block.  *first (uint64, preset to ~0 by the caller) receives
+// the smallest hitting position over all tiles.
 constexpr int PROBE_TILE = 4096;
 struct ProbeIv {
     int64_t a, b, anchor;
@@ -65,9 +68,10 @@ hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, hipStream_
 hipError_t launch_gather_bytes(const uint8_t* d_data, const int64_t* d_pos, uint32_t npos, uint8_t* d_out,
                                hipStream_t s);
 
-// True weak sums at arbitrary positions: out[i] = Rolling.compute(data + pos[i], min(B, n - pos[i])).
+// True weak sums at arbitrary positions: out[i] = Rolling.compute(data + pos[i], min(B, n - pos[i]))
+// (by_block: written to out[pos[i] / B] instead, for aligned positions).
 hipError_t launch_window_weak(const uint8_t* d_data, int64_t n, uint32_t B, const int64_t* d_pos, uint32_t npos,
-                              int32_t* d_out, hipStream_t s);
+                              int32_t* d_out, hipStream_t s, bool by_block = false);
 
 // splitmix64 counter stream (bench input): byte i = byte (i % 8) of mix(key + (i / 8 + 1) * golden).
 hipError_t launch_fill_splitmix(uint8_t* d_out, int64_t n, uint64_t key, int64_t byte_offset, hipStream_t s);

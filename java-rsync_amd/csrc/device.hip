@@ -208,11 +208,24 @@ __device__ __forceinline__ int mfma_pi(int j) { return (int)((0xECA8FDB975316420
 __device__ __forceinline__ int mfma_pi_inv(int c) { return (int)((0xBFAE9D8C73625140ull >> (4 * c)) & 15); }
 __device__ __forceinline__ int mfma_sigma(int s) { return (0x1302 >> (4 * s)) & 15; }
 
-template <int D, bool NT, int WAVES = 1, int MODE = 0, bool FUSED = false, bool MFMAW = false, bool STEADY = true>
+// ABORT (the Sender's speculation only): every 16 stages the wave reads *abort_flag (uncached device
+// memory, set by a stream write-value packet) with a cache-bypassing scalar load and exits when it
+// equals abort_gen -- the resolver finished without needing this launch's results.  The read waits
+// for itself only (the LDS traffic of the iteration is consumed by then; vector loads are untouched).
+__device__ __forceinline__ int poll_abort(const int* flag) {
+    int v;
+    asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(flag));
+    return v;
+}
+
+template <int D, bool NT, int WAVES = 1, int MODE = 0, bool FUSED = false, bool MFMAW = false, bool STEADY = true,
+          bool ABORT = false>
 __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const uint8_t* __restrict__ data, uint32_t B,
                                                                   uint32_t dl, uint32_t seed,
                                                                   int32_t* __restrict__ weak_out,
-                                                                  uint8_t* __restrict__ strong_out) {
+                                                                  uint8_t* __restrict__ strong_out,
+                                                                  const int* abort_flag = nullptr,
+                                                                  int abort_gen = 0) {
     constexpr int ROW = 9;
     extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // sized at launch (occupancy control)
     const int l = threadIdx.x & 63;
@@ -322,6 +335,9 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
         if constexpr (D > 1) stage(std::integral_constant<int, 1>{}, s + 1, true);
         if constexpr (D > 2) stage(std::integral_constant<int, 2>{}, s + 2, true);
         if constexpr (D > 3) stage(std::integral_constant<int, 3>{}, s + 3, true);
+        if constexpr (ABORT) {
+            if ((s & 15) == 0 && poll_abort(abort_flag) == abort_gen) return;
+        }
     }
     for (; s < nst; s += D) {  // drain (fewer than 2 * D stages left)
         if (s < nst) stage(std::integral_constant<int, 0>{}, s, s + D < nst);
@@ -457,7 +473,7 @@ void allow_full_lds(K kernel) {
 // (D=2 NT, D=3 NT, D=2 plain, D=4 NT).  Non-coalesced variants handle every chunk shape.
 hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks,
                                      uint32_t dl, uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong,
-                                     hipStream_t s) {
+                                     hipStream_t s, const int* abort_flag, int abort_gen) {
     if (nchunks == 0) return hipSuccess;
     const uintptr_t addr = reinterpret_cast<uintptr_t>(d_data);
     if (variant < 0) variant = 19;  // coalesced, 2 stages in flight, weak sums on the matrix pipe
@@ -529,7 +545,11 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     }
                     break;
                 case 19:
-                    if (nst <= 1024) {
+                    if (nst <= 1024 && abort_flag) {
+                        hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, true>),
+                                           dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong,
+                                           abort_flag, abort_gen);
+                    } else if (nst <= 1024) {
                         hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true>), dim3(waves), dim3(64),
                                            lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
                     } else {
@@ -603,8 +623,10 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
 }
 
 hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks, uint32_t dl,
-                             uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s) {
-    return launch_block_sums_variant(-1, d_data, n, B, nchunks, dl, seed_word, d_weak, d_strong, s);
+                             uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s,
+                             const int* abort_flag, int abort_gen) {
+    return launch_block_sums_variant(-1, d_data, n, B, nchunks, dl, seed_word, d_weak, d_strong, s, abort_flag,
+                                     abort_gen);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -638,11 +660,13 @@ __device__ __forceinline__ uint32_t slot_hash(uint32_t key) {
 }
 
 __global__ void table_clear_kernel(unsigned long long* slots, uint32_t nslots) {
+    __builtin_amdgcn_s_setprio(3);
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += gridDim.x * blockDim.x) slots[i] = 0ull;
 }
 
 __global__ void table_insert_kernel(unsigned long long* slots, uint32_t mask, const int32_t* __restrict__ keys,
                                     uint32_t nkeys) {
+    __builtin_amdgcn_s_setprio(3);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nkeys) return;
     const uint32_t key = (uint32_t)keys[i];
@@ -808,6 +832,7 @@ __device__ __forceinline__ void load16(const uint8_t* __restrict__ x, int64_t n,
 }
 
 __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A) {
+    __builtin_amdgcn_s_setprio(3);  // resolver latency path: ahead of a co-running speculation launch
     __shared__ int32_t sh[4 * PROBE_THREADS / 64];
     const int64_t n = A.n, B = A.B;
     const ProbeTile tile = A.tiles[blockIdx.x];
@@ -884,14 +909,14 @@ void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeT
 }
 
 hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(args.first, 0xFF, sizeof(unsigned long long), s);  // "none" = all ones
-    if (e != hipSuccess || ntiles == 0) return e;
+    if (ntiles == 0) return hipSuccess;
     hipLaunchKernelGGL(probe_first_kernel, dim3(ntiles), dim3(PROBE_THREADS), 0, s, args);
     return hipGetLastError();
 }
 
 __global__ void gather_bytes_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ pos, uint32_t npos,
                                     uint8_t* __restrict__ out) {
+    __builtin_amdgcn_s_setprio(3);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < npos) out[i] = data[pos[i]];
 }
@@ -907,7 +932,9 @@ hipError_t launch_gather_bytes(const uint8_t* d_data, const int64_t* d_pos, uint
 // True weak sums at arbitrary positions (one workgroup per position).
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void window_weak_kernel(const uint8_t* __restrict__ data, int64_t n, uint32_t B,
-                                                          const int64_t* __restrict__ pos, int32_t* __restrict__ out) {
+                                                          const int64_t* __restrict__ pos, int32_t* __restrict__ out,
+                                                          bool by_block) {
+    __builtin_amdgcn_s_setprio(3);
     __shared__ int32_t sh[2 * 256 / 64];
     const int64_t p = pos[blockIdx.x];
     const int64_t w = (n - p < (int64_t)B ? n - p : (int64_t)B);
@@ -917,14 +944,14 @@ __global__ __launch_bounds__(256) void window_weak_kernel(const uint8_t* __restr
     if (threadIdx.x == 0) {
         const uint32_t S1 = (uint32_t)v[0];
         const uint32_t S2 = (uint32_t)w * S1 - (uint32_t)v[1];
-        out[blockIdx.x] = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
+        out[by_block ? p / B : blockIdx.x] = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
     }
 }
 
 hipError_t launch_window_weak(const uint8_t* d_data, int64_t n, uint32_t B, const int64_t* d_pos, uint32_t npos,
-                              int32_t* d_out, hipStream_t s) {
+                              int32_t* d_out, hipStream_t s, bool by_block) {
     if (npos == 0) return hipSuccess;
-    hipLaunchKernelGGL(window_weak_kernel, dim3(npos), dim3(256), 0, s, d_data, n, B, d_pos, d_out);
+    hipLaunchKernelGGL(window_weak_kernel, dim3(npos), dim3(256), 0, s, d_data, n, B, d_pos, d_out, by_block);
     return hipGetLastError();
 }
 

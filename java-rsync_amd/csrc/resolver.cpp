@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <functional>
 #include <limits>
 
 namespace rsh {
@@ -85,18 +86,22 @@ int32_t close_index_of(const int32_t* bucket, int32_t size, int32_t chunk_index)
 
 }  // namespace
 
-void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveResult* out) {
+bool resolve_run(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveState* state, ResolveResult* out,
+                 const std::function<bool()>& yield) {
     const auto t0 = std::chrono::steady_clock::now();
     const int64_t B = table.block_length;
     const int dl = table.digest_length;
     const int64_t S = table.remainder > 0 ? table.remainder : B;  // getSmallestChunkSize, Checksum.java:131-137
     const int64_t last = n - S;  // visited positions satisfy wl(s) >= S  <=>  s <= n - S
     const int64_t nB = n - B;
+    // the speculation the backend has now (none while it is still in flight: every lookup below then
+    // takes the generic path, which gives the same answer)
     const int64_t nal = be.aligned_count();
     const int32_t* aw = be.aligned_weak();
     const uint8_t* as = be.aligned_strong();
     const uint8_t* fl = be.chain_flags();
     const int64_t nflags = std::min<int64_t>(nal, table.chunk_count);
+    const int64_t max_batch = be.max_batch();
     auto wl = [&](int64_t s) { return std::min<int64_t>(B, n - s); };  // FileView window length
     auto clampB = [&](int64_t p) { return std::min<int64_t>(p, nB); };
 
@@ -121,16 +126,19 @@ void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveRe
         out->matched += len;
     };
 
-    // Sender state (file coordinates).  E = R - T is kept as its value at `anchor` (quirk A).
-    int64_t s = 0, m = 0;
-    int32_t pref = 0;
-    uint32_t elo = 0, ehi = 0;
-    int64_t anchor = 0;
-    bool md5c_valid = false;  // localChunkMd5sum != null (Sender.java:1248)
-    uint8_t md5c[16];
-    std::vector<int32_t> dkeys;
-    bool dkeys_ready = false;
-    int64_t batch = 1;  // flush intervals speculated per batched probe
+    // Sender state (file coordinates), kept in *state between calls
+    int64_t& s = state->s;
+    int64_t& m = state->m;
+    int32_t& pref = state->pref;
+    uint32_t& elo = state->elo;
+    uint32_t& ehi = state->ehi;
+    int64_t& anchor = state->anchor;
+    bool& md5c_valid = state->md5c_valid;
+    uint8_t* md5c = state->md5c;
+    std::vector<int32_t>& dkeys = state->dkeys;
+    bool& dkeys_ready = state->dkeys_ready;
+    int64_t& batch = state->batch;
+    if (state->done) return true;
 
     auto E_at = [&](int64_t p, uint32_t* lo, uint32_t* hi) {
         *lo = elo;
@@ -170,7 +178,14 @@ void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveRe
         }
     };
 
+    auto elapsed = [&] {
+        st.resolver_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    };
     while (s <= last) {
+        if (yield && yield()) {  // between two steps: the caller resumes with the same state
+            elapsed();
+            return false;
+        }
         const bool synced = (elo == 0 && ehi == 0);
         // (1) aligned chain: preferred index == k and source window k carries chunk k's sums.
         if (!md5c_valid && synced && s % B == 0) {
@@ -298,7 +313,7 @@ void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveRe
             // replace K round trips.  K doubles while no event turns up (wasted probing <= 2x).
             // flush i sits at f_i = f + 10B i and happens iff its mark m_i = f_i - 9B has m_i + 10B <= n
             int64_t K = 1;
-            while (K < batch && f + 10 * B * K + B <= n) ++K;
+            while (K < std::min(batch, max_batch) && f + 10 * B * K + B <= n) ++K;
             std::vector<int64_t> tpos, bpos;
             for (int64_t i = 0; i < K; ++i) {
                 const int64_t fi = f + 10 * B * i;
@@ -365,7 +380,14 @@ void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveRe
         break;
     }
     emit_lit(m, n - m);  // Sender.java:1313-1316 (firstOffset == mark once the loop ends)
-    st.resolver_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    state->done = true;
+    elapsed();
+    return true;
+}
+
+void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveResult* out) {
+    ResolveState state;
+    resolve_run(n, table, be, &state, out, nullptr);
 }
 
 }  // namespace rsh

@@ -15,6 +15,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <functional>
 #include <vector>
 
 #include "rsync_hip.h"
@@ -63,6 +64,8 @@ class ScanBackend {
     // Smallest p over all intervals whose key is in the key set (keys == nullptr: the whole chunk
     // table); -1 if none.
     virtual int64_t first_hit(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) = 0;
+    // Upper bound on the flush intervals one batched probe may cover.
+    virtual int64_t max_batch() { return 4096; }
 
     int32_t weak_at(int64_t p) {
         int32_t r;
@@ -83,7 +86,27 @@ struct ResolveResult {
     rsh_scan_stats stats{};
 };
 
+// The Sender's state between resolver steps (Sender.java:1241-1249 locals + FileView mark/start).
+// E = R - T is kept as its value at `anchor` (quirk A).
+struct ResolveState {
+    int64_t s = 0, m = 0;
+    int32_t pref = 0;
+    uint32_t elo = 0, ehi = 0;
+    int64_t anchor = 0;
+    bool md5c_valid = false;  // localChunkMd5sum != null (Sender.java:1248)
+    uint8_t md5c[16] = {};
+    std::vector<int32_t> dkeys;  // weak keys of the chunks whose digest is md5c
+    bool dkeys_ready = false;
+    int64_t batch = 1;  // flush intervals speculated per batched probe
+    bool done = false;
+};
+
 // n > 0 and h->block_length > 0 (skipMatchSendData / empty sources are handled by the caller).
+// Runs the scan from *state to the end (returns true) or until yield() -- asked between two steps --
+// returns true (returns false; call again with the same state and result to resume).  The backend's
+// aligned speculation is re-read on every call, so a scan can start before it exists.
+bool resolve_run(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveState* state, ResolveResult* out,
+                 const std::function<bool()>& yield);
 void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveResult* out);
 
 }  // namespace rsh

@@ -58,7 +58,8 @@ class Event(ctypes.Structure):
 class ScanStats(ctypes.Structure):
     _fields_ = [("chain_matches", ctypes.c_int64), ("events", ctypes.c_int64), ("probe_launches", ctypes.c_int64),
                 ("host_md5_windows", ctypes.c_int64), ("flushes", ctypes.c_int64),
-                ("device_ms", ctypes.c_double), ("resolver_ms", ctypes.c_double), ("table_ms", ctypes.c_double)]
+                ("device_ms", ctypes.c_double), ("resolver_ms", ctypes.c_double), ("table_ms", ctypes.c_double),
+                ("head_steps", ctypes.c_int64), ("speculation_aborted", ctypes.c_int64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

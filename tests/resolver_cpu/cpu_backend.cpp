@@ -39,7 +39,9 @@ class CpuBackend : public rsh::ScanBackend {
         for (int64_t k = 0; k < nf; ++k)
             fl_[k] = aw_[k] == t.weak[k] && memcmp(&as_[k * dl_], t.strong + k * dl_, dl_) == 0;
     }
-    int64_t aligned_count() override { return (int64_t)aw_.size(); }
+    bool head = false;  // speculation "still in flight": the resolver must take the generic paths
+    int64_t aligned_count() override { return head ? 0 : (int64_t)aw_.size(); }
+    int64_t max_batch() override { return head ? 4 : 4096; }
     const int32_t* aligned_weak() override { return aw_.data(); }
     const uint8_t* aligned_strong() override { return as_.data(); }
     const uint8_t* chain_flags() override { return fl_.data(); }
@@ -110,9 +112,11 @@ class CpuBackend : public rsh::ScanBackend {
 
 }  // namespace
 
-extern "C" int rtest_scan(const uint8_t* src, int64_t n, const rsh_header* h, const int32_t* weak,
-                          const uint8_t* strong, const uint8_t seed[4], rsh_event* ev, int64_t cap, int64_t* n_ev,
-                          int64_t* lit, int64_t* mat, rsh_scan_stats* stats) {
+// head_steps < 0: one plain resolve_scan.  Otherwise the scan runs head_steps resolver steps with no
+// aligned speculation (as while the device kernel is still running), then resumes with it.
+extern "C" int rtest_scan_staged(const uint8_t* src, int64_t n, const rsh_header* h, const int32_t* weak,
+                                 const uint8_t* strong, const uint8_t seed[4], rsh_event* ev, int64_t cap,
+                                 int64_t* n_ev, int64_t* lit, int64_t* mat, rsh_scan_stats* stats, int64_t head_steps) {
     rsh::ChunkTable t;
     t.chunk_count = h->chunk_count;
     t.block_length = h->block_length;
@@ -123,7 +127,16 @@ extern "C" int rtest_scan(const uint8_t* src, int64_t n, const rsh_header* h, co
     t.build();
     CpuBackend be(src, n, t, seed);
     rsh::ResolveResult r;
-    rsh::resolve_scan(n, t, be, &r);
+    if (head_steps < 0) {
+        rsh::resolve_scan(n, t, be, &r);
+    } else {
+        rsh::ResolveState st;
+        int64_t steps = 0;
+        be.head = true;
+        const bool done = rsh::resolve_run(n, t, be, &st, &r, [&] { return steps++ >= head_steps; });
+        be.head = false;
+        if (!done) rsh::resolve_run(n, t, be, &st, &r, nullptr);
+    }
     *n_ev = (int64_t)r.ev.size();
     *lit = r.literal;
     *mat = r.matched;
@@ -131,4 +144,10 @@ extern "C" int rtest_scan(const uint8_t* src, int64_t n, const rsh_header* h, co
     if ((int64_t)r.ev.size() > cap) return RSH_E_NOSPACE;
     memcpy(ev, r.ev.data(), r.ev.size() * sizeof(rsh_event));
     return 0;
+}
+
+extern "C" int rtest_scan(const uint8_t* src, int64_t n, const rsh_header* h, const int32_t* weak,
+                          const uint8_t* strong, const uint8_t seed[4], rsh_event* ev, int64_t cap, int64_t* n_ev,
+                          int64_t* lit, int64_t* mat, rsh_scan_stats* stats) {
+    return rtest_scan_staged(src, n, h, weak, strong, seed, ev, cap, n_ev, lit, mat, stats, -1);
 }

@@ -27,11 +27,12 @@ def rlib():
         L.rtest_scan.argtypes = [P, ctypes.c_int64, ctypes.POINTER(R.Header), P, P, P, P, ctypes.c_int64,
                                  ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                  ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(R.ScanStats)]
+        L.rtest_scan_staged.argtypes = L.rtest_scan.argtypes + [ctypes.c_int64]
         _LIB = L
     return _LIB
 
 
-def resolve(src, h, weak, strong, seed):
+def resolve(src, h, weak, strong, seed, head_steps=-1):
     a = np.frombuffer(bytes(src), np.uint8)
     w = np.ascontiguousarray(weak, np.int32)
     st = np.ascontiguousarray(strong, np.uint8)
@@ -40,19 +41,20 @@ def resolve(src, h, weak, strong, seed):
     ev = np.zeros(cap, R.EVENT_DTYPE)
     n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     stats = R.ScanStats()
-    rc = rlib().rtest_scan(a.ctypes.data, a.size, ctypes.byref(h), w.ctypes.data if w.size else None,
-                           st.ctypes.data if st.size else None, s.ctypes.data, ev.ctypes.data, cap,
-                           ctypes.byref(n_ev), ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(stats))
+    rc = rlib().rtest_scan_staged(a.ctypes.data, a.size, ctypes.byref(h), w.ctypes.data if w.size else None,
+                                  st.ctypes.data if st.size else None, s.ctypes.data, ev.ctypes.data, cap,
+                                  ctypes.byref(n_ev), ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(stats),
+                                  head_steps)
     assert rc == 0
     return ev[:n_ev.value], lit.value, mat.value, stats.as_dict()
 
 
-def check_case(basis, src, blen, dlen, seed):
+def check_case(basis, src, blen, dlen, seed, head_steps=-1):
     h = O.header(blen, dlen, len(basis))
     weak, strong = O.generator(basis, h, seed)
     oev, ofm, olit, omat, _ = O.sender(src, h, weak, strong, seed)
     rh = R.Header(**h.as_dict())
-    ev, lit, mat, stats = resolve(src, rh, weak, strong, seed)
+    ev, lit, mat, stats = resolve(src, rh, weak, strong, seed, head_steps)
     got = R.events_as_tuples(ev, blen)
     assert got == [tuple(e) for e in oev]
     assert (lit, mat) == (olit, omat)
@@ -145,3 +147,23 @@ def test_resolver_large_table_desync():
     src = basis[:3 * B] + O.splitmix(10 * B + 37, 3).tobytes() + basis[3 * B + 1:]
     st = check_case(basis, src, B, 2, bytes([1, 2, 3, 4]))
     assert st["flushes"] > 1000 and st["chain_matches"] == 3 and st["events"] >= 1
+
+
+@pytest.mark.parametrize("seed_i", range(8))
+def test_resolver_staged_head_mode(seed_i):
+    """The scan starts before the aligned speculation exists (head mode: every lookup takes the generic
+    path, batched probes capped) and resumes with it after a random number of steps: same events."""
+    rng = random.Random(5000 + seed_i)
+    for _ in range(10):
+        B = rng.choice([512, 576, 1024])
+        nb = rng.randrange(1, 40 * B)
+        key = rng.randrange(1 << 62)
+        basis = O.splitmix(nb, key).tobytes()
+        if rng.random() < 0.2:
+            blk = O.splitmix(B, key).tobytes()
+            basis = (blk * (nb // B + 1))[:nb]
+        src = _mutate(rng, basis, B, key)
+        if not src:
+            continue
+        check_case(basis, src, B, rng.choice([2, 3, 16]), bytes([1, 2, 3, 4]),
+                   head_steps=rng.choice([0, 1, 2, 5, 17, 1 << 40]))
