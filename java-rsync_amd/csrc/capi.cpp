@@ -158,6 +158,21 @@ struct CtxClaim {
 // ------------------------------------------------------------------------------------------------
 constexpr size_t kFirstSlots = 1024;
 
+// RSH_SCAN_TRACE=1: one stderr line per resolver round trip (diagnostics).
+struct CallTrace {
+    const char* what;
+    int64_t arg;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    static bool on() {
+        static const bool v = getenv("RSH_SCAN_TRACE") != nullptr;
+        return v;
+    }
+    CallTrace(const char* w, int64_t a) : what(w), arg(a) {}
+    ~CallTrace() {
+        if (on()) fprintf(stderr, "[rsh] %-10s %10lld %9.3f ms\n", what, (long long)arg, ms_since(t0));
+    }
+};
+
 class HipBackend : public rsh::ScanBackend {
   public:
     HipBackend(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh::ChunkTable& t, const uint8_t seed[4])
@@ -184,6 +199,7 @@ class HipBackend : public rsh::ScanBackend {
 
     void weak_many(const int64_t* pos, int64_t count, int32_t* out) override {
         if (count <= 0) return;
+        CallTrace tr("weak_many", count);
         int64_t* hp = pin<int64_t>(c_->h_pos, count);
         int32_t* ho = pin<int32_t>(c_->h_out, count);
         if (err != hipSuccess) return;
@@ -194,6 +210,7 @@ class HipBackend : public rsh::ScanBackend {
     }
     void bytes_many(const int64_t* pos, int64_t count, uint8_t* out) override {
         if (count <= 0) return;
+        CallTrace tr("bytes_many", count);
         int64_t* hp = pin<int64_t>(c_->h_pos, count);
         uint8_t* ho = pin<uint8_t>(c_->h_out, count);
         if (err != hipSuccess) return;
@@ -205,10 +222,11 @@ class HipBackend : public rsh::ScanBackend {
     // A single window's digest is one serial MD5 chain: 64-wide waves give it nothing, so the rare
     // resolver misses (first table hit after a reset) are digested on the host from a D2H copy.
     void md5_at(int64_t p, uint8_t out[16]) override {
+        CallTrace tr("md5_at", p);
         const int64_t w = std::min<int64_t>(B_, n_ - p);
         uint8_t* hw = pin<uint8_t>(c_->h_win, w);
         if (err != hipSuccess) return;
-        ok(hipMemcpyAsync(hw, x_ + p, (size_t)w, hipMemcpyDeviceToHost, c_->stream));
+        ok(rsh::launch_copy_to_host(x_ + p, w, hw, c_->stream));
         ok(hipStreamSynchronize(c_->stream));
         rsh::HostMd5 h;
         h.update(hw, (size_t)w);
@@ -216,6 +234,7 @@ class HipBackend : public rsh::ScanBackend {
         h.final(out);
     }
     int64_t first_hit(const rsh::ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) override {
+        CallTrace tr("first_hit", count);
         rsh::ProbeTable tab = table;
         if (keys) {
             const uint32_t ns = pow2_at_least(2 * keys->size() + 2);
@@ -386,11 +405,14 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     table.digest_length = dl;
     table.weak = host_weak;
     table.strong = host_strong;
-    if (download) RSH_HIP(hipEventSynchronize(c->ev_tab));
-    const auto t1 = std::chrono::steady_clock::now();
-    table.build();
-    const double table_ms = ms_since(t1);
-    RSH_HIP(hipStreamSynchronize(c->stream));
+    {
+        CallTrace tr("table_dl", C);
+        if (download) RSH_HIP(hipEventSynchronize(c->ev_tab));
+    }
+    {
+        CallTrace tr("hash_sync", ns);
+        RSH_HIP(hipStreamSynchronize(c->stream));
+    }
 
     HipBackend be(c, d_src, n, table, seed);
     be.table.slots = c->slots.as<unsigned long long>();
@@ -405,6 +427,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     bool landed = false;
     const bool done = rsh::resolve_run(n, table, be, &rs, res, [&] {
         if (be.err != hipSuccess || !be.head) return true;
+        CallTrace tr("ev_query", res->stats.head_steps);
         landed = hipEventQuery(c->ev_spec) != hipErrorNotReady;
         if (!landed) res->stats.head_steps++;
         return landed;
@@ -423,7 +446,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         }
     }
     if (be.err != hipSuccess) return RSH_E_DEVICE;
-    res->stats.table_ms += table_ms;
+    res->stats.table_ms += table.sort_ms;  // 0 when the scan never needed the sorted table
     return RSH_OK;
 }
 

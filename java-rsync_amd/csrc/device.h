@@ -64,6 +64,9 @@ struct ProbeArgs {
 void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeTile>* out);
 hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, hipStream_t s);
 
+// n bytes of device memory into pinned host memory (h_dst 16-byte aligned), by a kernel.
+hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s);
+
 // Bytes at arbitrary positions.
 hipError_t launch_gather_bytes(const uint8_t* d_data, const int64_t* d_pos, uint32_t npos, uint8_t* d_out,
                                hipStream_t s);

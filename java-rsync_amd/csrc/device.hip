@@ -928,6 +928,31 @@ hipError_t launch_gather_bytes(const uint8_t* d_data, const int64_t* d_pos, uint
     return hipGetLastError();
 }
 
+// Device bytes -> pinned host memory, as a kernel: the runtime's copy path can queue behind a
+// co-running speculation launch, a high-priority kernel does not.  Thread t assembles bytes
+// [16t, 16t + 16) and writes them with one 16-byte store.
+__global__ __launch_bounds__(256) void copy_to_host_kernel(const uint8_t* __restrict__ src, int64_t n,
+                                                           uint8_t* __restrict__ dst) {
+    __builtin_amdgcn_s_setprio(3);
+    const int64_t o = 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (o >= n) return;
+    if (o + 16 <= n) {
+        uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i >> 2] |= (uint32_t)src[o + i] << (8 * (i & 3));
+        *reinterpret_cast<uint4*>(dst + o) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+        for (int64_t i = o; i < n; ++i) dst[i] = src[i];
+    }
+}
+
+hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t threads = (n + 15) / 16;
+    hipLaunchKernelGGL(copy_to_host_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, d_src, n, h_dst);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------------
 // True weak sums at arbitrary positions (one workgroup per position).
 // ------------------------------------------------------------------------------------------------

@@ -7,6 +7,8 @@
 
 #include "md5_core.h"
 
+static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "host MD5 loads message words as little-endian");
+
 namespace rsh {
 
 class HostMd5 {
@@ -54,9 +56,7 @@ class HostMd5 {
   private:
     void block(const uint8_t* p) {
         uint32_t m[16];
-        for (int i = 0; i < 16; i++)
-            m[i] = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) | ((uint32_t)p[4 * i + 2] << 16) |
-                   ((uint32_t)p[4 * i + 3] << 24);
+        memcpy(m, p, 64);  // MD5 words are little-endian, as is every host this builds for
         md5_compress(st_, m);
     }
     Md5State st_;

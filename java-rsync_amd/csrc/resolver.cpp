@@ -13,6 +13,10 @@
 namespace rsh {
 
 void ChunkTable::build() {
+    if (sorted_) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint32_t>& sorted_key = sorted_key_;
+    std::vector<int32_t>& sorted_idx = sorted_idx_;
     const int32_t n = chunk_count;
     std::vector<uint32_t> k2(n);
     std::vector<int32_t> i2(n);
@@ -22,38 +26,73 @@ void ChunkTable::build() {
         sorted_key[i] = (uint32_t)weak[i];
         sorted_idx[i] = i;
     }
-    // LSD radix sort, two stable 16-bit passes: ties keep ascending chunk index (Multimap insertion order).
-    std::vector<uint32_t> cnt(65537);
-    for (int pass = 0; pass < 2; ++pass) {
-        const int sh = 16 * pass;
-        std::vector<uint32_t>& ks = pass == 0 ? sorted_key : k2;
-        std::vector<int32_t>& is = pass == 0 ? sorted_idx : i2;
-        std::vector<uint32_t>& kd = pass == 0 ? k2 : sorted_key;
-        std::vector<int32_t>& id = pass == 0 ? i2 : sorted_idx;
-        std::fill(cnt.begin(), cnt.end(), 0u);
-        for (int32_t i = 0; i < n; ++i) cnt[((ks[i] >> sh) & 0xFFFFu) + 1]++;
-        for (int d = 0; d < 65536; ++d) cnt[d + 1] += cnt[d];
+    // LSD radix sort, three stable passes of 11/11/10 bits (cache-resident counters): ties keep
+    // ascending chunk index (Multimap insertion order, Multimap.java:27-61).
+    uint32_t cnt[2049];
+    std::vector<uint32_t>* ks = &sorted_key;
+    std::vector<int32_t>* is = &sorted_idx;
+    std::vector<uint32_t>* kd = &k2;
+    std::vector<int32_t>* id = &i2;
+    for (int pass = 0; pass < 3; ++pass) {
+        const int sh = 11 * pass;
+        const uint32_t mask = pass < 2 ? 0x7FFu : 0x3FFu;
+        std::fill(cnt, cnt + 2049, 0u);
+        const uint32_t* kp = ks->data();
+        for (int32_t i = 0; i < n; ++i) cnt[((kp[i] >> sh) & mask) + 1]++;
+        for (int d = 0; d < 2048; ++d) cnt[d + 1] += cnt[d];
+        const int32_t* ip = is->data();
+        uint32_t* kdp = kd->data();
+        int32_t* idp = id->data();
         for (int32_t i = 0; i < n; ++i) {
-            const uint32_t dgt = (ks[i] >> sh) & 0xFFFFu;
-            kd[cnt[dgt]] = ks[i];
-            id[cnt[dgt]] = is[i];
-            cnt[dgt]++;
+            const uint32_t dgt = (kp[i] >> sh) & mask;
+            const uint32_t at = cnt[dgt]++;
+            kdp[at] = kp[i];
+            idp[at] = ip[i];
         }
+        std::swap(ks, kd);
+        std::swap(is, id);
     }
+    if (ks != &sorted_key) {  // odd pass count: the result sits in the scratch pair
+        sorted_key.swap(*ks);
+        sorted_idx.swap(*is);
+    }
+    sorted_ = true;
+    sort_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-void ChunkTable::bucket(int32_t key, int32_t* lo, int32_t* hi) const {
-    const uint32_t k = (uint32_t)key;
-    auto a = std::lower_bound(sorted_key.begin(), sorted_key.end(), k);
-    auto b = std::upper_bound(a, sorted_key.end(), k);
-    *lo = (int32_t)(a - sorted_key.begin());
-    *hi = (int32_t)(b - sorted_key.begin());
+const int32_t* ChunkTable::bucket(int32_t key, int32_t* size) {
+    if (!sorted_ && scan_lookups_ >= kScanLookups) build();
+    if (sorted_) {
+        const uint32_t k = (uint32_t)key;
+        auto a = std::lower_bound(sorted_key_.begin(), sorted_key_.end(), k);
+        auto b = std::upper_bound(a, sorted_key_.end(), k);
+        *size = (int32_t)(b - a);
+        return sorted_idx_.data() + (a - sorted_key_.begin());
+    }
+    ++scan_lookups_;
+    int32_t cnt = 0;  // counting pass (vectorises); most lookups find nothing
+    for (int32_t i = 0; i < chunk_count; ++i) cnt += weak[i] == key;
+    scratch_.clear();
+    if (cnt) {
+        scratch_.reserve(cnt);
+        for (int32_t i = 0; i < chunk_count; ++i)
+            if (weak[i] == key) scratch_.push_back(i);
+    }
+    *size = cnt;
+    return scratch_.data();
 }
 
 void ChunkTable::keys_with_digest(const uint8_t* d, std::vector<int32_t>* keys) const {
     keys->clear();
-    for (int32_t i = 0; i < chunk_count; ++i)
-        if (memcmp(strong + (int64_t)i * digest_length, d, (size_t)digest_length) == 0) keys->push_back(weak[i]);
+    const int64_t dl = digest_length;
+    if (dl == 0) {  // every chunk carries the empty digest
+        keys->assign(weak, weak + chunk_count);
+    } else {
+        const uint8_t d0 = d[0];
+        const uint8_t* sp = strong;
+        for (int32_t i = 0; i < chunk_count; ++i, sp += dl)  // first-byte filter, then the full compare
+            if (sp[0] == d0 && memcmp(sp, d, (size_t)dl) == 0) keys->push_back(weak[i]);
+    }
     std::sort(keys->begin(), keys->end());
     keys->erase(std::unique(keys->begin(), keys->end()), keys->end());
 }
@@ -86,7 +125,7 @@ int32_t close_index_of(const int32_t* bucket, int32_t size, int32_t chunk_index)
 
 }  // namespace
 
-bool resolve_run(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveState* state, ResolveResult* out,
+bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* state, ResolveResult* out,
                  const std::function<bool()>& yield) {
     const auto t0 = std::chrono::steady_clock::now();
     const int64_t B = table.block_length;
@@ -234,9 +273,9 @@ bool resolve_run(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveSta
         if (!none) {
             int64_t a = s;
             if (!md5c_valid && synced && s % B == 0 && s / B < nal) {  // key known from aligned sums
-                int32_t lo, hi;
-                table.bucket(aw[s / B], &lo, &hi);
-                if (hi > lo) p = s;
+                int32_t size;
+                table.bucket(aw[s / B], &size);
+                if (size > 0) p = s;
                 else a = s + 1;
             }
             if (p < 0 && a <= stop) {
@@ -254,12 +293,10 @@ bool resolve_run(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveSta
             const int32_t R = pack16(lo16(T) + el, hi16(T) + eh);
             const int64_t w = wl(p);
             st.events++;
-            int32_t lo, hi;
-            table.bucket(R, &lo, &hi);
+            int32_t size;
+            const int32_t* bk = table.bucket(R, &size);
             int32_t hit = -1;
-            if (hi > lo) {  // getCandidateChunks order (Checksum.java:215-276)
-                const int32_t size = hi - lo;
-                const int32_t* bk = &table.sorted_idx[lo];
+            if (size > 0) {  // getCandidateChunks order (Checksum.java:215-276)
                 const int32_t init = close_index_of(bk, size, pref);
                 for (int32_t it = -1; it < size; ++it) {
                     int32_t pos;
@@ -385,7 +422,7 @@ bool resolve_run(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveSta
     return true;
 }
 
-void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveResult* out) {
+void resolve_scan(int64_t n, ChunkTable& table, ScanBackend& be, ResolveResult* out) {
     ResolveState state;
     resolve_run(n, table, be, &state, out, nullptr);
 }

@@ -30,16 +30,29 @@ struct ChunkTable {
     int32_t digest_length = 0;
     const int32_t* weak = nullptr;   // chunk_count, receive order
     const uint8_t* strong = nullptr; // chunk_count * digest_length
-    std::vector<uint32_t> sorted_key; // bucket keys, sorted (stable: ascending chunk index per key)
-    std::vector<int32_t> sorted_idx;
 
-    void build();  // radix sort of (weak, index)
-    void bucket(int32_t key, int32_t* lo, int32_t* hi) const;
+    // Ascending chunk indices whose weak key is `key` (a Multimap bucket, in insertion order); valid
+    // until the next call.  The first kScanLookups lookups are linear scans of `weak`; after that the
+    // table is radix-sorted once and lookups binary-search it.  A scan that poisons early (quirk B)
+    // needs a handful of lookups and never pays for the sort.
+    const int32_t* bucket(int32_t key, int32_t* size);
+    void build();  // sort now (radix sort of (weak, index))
+    bool sorted() const { return sorted_; }
+    double sort_ms = 0;  // time spent in build()
     int32_t chunk_length(int32_t idx) const {  // Checksum.java:197-203
         return (idx == chunk_count - 1 && remainder > 0) ? remainder : block_length;
     }
     // Distinct weak keys of the chunks whose digest equals d (the only ones a stale digest can match).
     void keys_with_digest(const uint8_t* d, std::vector<int32_t>* keys) const;
+
+    static constexpr int kScanLookups = 16;
+
+  private:
+    bool sorted_ = false;
+    int scan_lookups_ = 0;
+    std::vector<uint32_t> sorted_key_;  // bucket keys, sorted (stable: ascending chunk index per key)
+    std::vector<int32_t> sorted_idx_;
+    std::vector<int32_t> scratch_;
 };
 
 // One probe interval: positions [a, b) with the key R(p) = T(p) + E(p),
@@ -105,8 +118,8 @@ struct ResolveState {
 // Runs the scan from *state to the end (returns true) or until yield() -- asked between two steps --
 // returns true (returns false; call again with the same state and result to resume).  The backend's
 // aligned speculation is re-read on every call, so a scan can start before it exists.
-bool resolve_run(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveState* state, ResolveResult* out,
+bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* state, ResolveResult* out,
                  const std::function<bool()>& yield);
-void resolve_scan(int64_t n, const ChunkTable& table, ScanBackend& be, ResolveResult* out);
+void resolve_scan(int64_t n, ChunkTable& table, ScanBackend& be, ResolveResult* out);
 
 }  // namespace rsh

@@ -22,7 +22,7 @@ int32_t weak_of(const uint8_t* p, int64_t L) {
 
 class CpuBackend : public rsh::ScanBackend {
   public:
-    CpuBackend(const uint8_t* x, int64_t n, const rsh::ChunkTable& t, const uint8_t seed[4])
+    CpuBackend(const uint8_t* x, int64_t n, rsh::ChunkTable& t, const uint8_t seed[4])
         : x_(x), n_(n), t_(t), B_(t.block_length), dl_(t.digest_length) {
         memcpy(seed_, seed, 4);
         const int64_t na = (n + B_ - 1) / B_;
@@ -78,9 +78,9 @@ class CpuBackend : public rsh::ScanBackend {
                 hit = false;
                 for (int32_t k : *keys) hit |= (k == R);
             } else {
-                int32_t lo, hi;
-                t_.bucket(R, &lo, &hi);
-                hit = hi > lo;
+                int32_t size;
+                t_.bucket(R, &size);
+                hit = size > 0;
             }
             if (hit) return p;
             // true weak sum of the next window (Rolling subtract/add with the FileView window rule)
@@ -101,7 +101,7 @@ class CpuBackend : public rsh::ScanBackend {
     int64_t wl(int64_t p) const { return n_ - p < B_ ? n_ - p : B_; }
     const uint8_t* x_;
     int64_t n_;
-    const rsh::ChunkTable& t_;
+    rsh::ChunkTable& t_;
     int64_t B_;
     int dl_;
     uint8_t seed_[4];
@@ -124,7 +124,7 @@ extern "C" int rtest_scan_staged(const uint8_t* src, int64_t n, const rsh_header
     t.digest_length = h->digest_length;
     t.weak = weak;
     t.strong = strong;
-    t.build();
+    if (head_steps < 0) t.build();  // staged runs leave the table lazy (linear-scan lookups first)
     CpuBackend be(src, n, t, seed);
     rsh::ResolveResult r;
     if (head_steps < 0) {
