@@ -219,7 +219,7 @@ __device__ __forceinline__ int poll_abort(const int* flag) {
 }
 
 template <int D, bool NT, int WAVES = 1, int MODE = 0, bool FUSED = false, bool MFMAW = false, bool STEADY = true,
-          bool ABORT = false>
+          bool ABORT = false, bool LIT = true, bool PIN = false>
 __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const uint8_t* __restrict__ data, uint32_t B,
                                                                   uint32_t dl, uint32_t seed,
                                                                   int32_t* __restrict__ weak_out,
@@ -227,6 +227,10 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
                                                                   const int* abort_flag = nullptr,
                                                                   int abort_gen = 0) {
     constexpr int ROW = 9;
+    // PIN: claim VGPRs up to v183 so that at most 2 waves fit a SIMD (512 / 184).  The MFMAW body needs 156,
+    // which admits 3; a launch with exactly 2 waves per SIMD of work (16 GiB at B = 128 KiB) then may stack
+    // 3 on some SIMDs and 1 on others when it starts while another kernel drains (5.1 ms instead of 3.2).
+    if constexpr (PIN) asm volatile("; occupancy pin" ::: "v183");
     extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // sized at launch (occupancy control)
     const int l = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
@@ -309,7 +313,8 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
 #pragma unroll
                 for (int k = 0; k < 16; ++k) fold ^= m[k];
             } else if constexpr (MFMAW) {
-                md5_compress(st, m);
+                if constexpr (LIT) md5_compress_lit(st, m);
+                else md5_compress(st, m);
             } else if constexpr (FUSED) {
                 md5_weak_block(st, m, s1, u, 128 * si + 64 * h);
             } else {
@@ -545,10 +550,19 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     }
                     break;
                 case 19:
-                    if (nst <= 1024 && abort_flag) {
+                    if (nst <= 1024 && abort_flag && waves <= 2 * 4 * kCUs) {
+                        hipLaunchKernelGGL(
+                            (block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, true, true, true>),
+                            dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag,
+                            abort_gen);
+                    } else if (nst <= 1024 && abort_flag) {
                         hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, true>),
                                            dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong,
                                            abort_flag, abort_gen);
+                    } else if (nst <= 1024 && waves <= 2 * 4 * kCUs) {
+                        hipLaunchKernelGGL(
+                            (block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, true, true>),
+                            dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
                     } else if (nst <= 1024) {
                         hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true>), dim3(waves), dim3(64),
                                            lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
@@ -564,6 +578,18 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                 case 21:
                     hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true, 1, 0, false, true, false>), dim3(waves),
                                        dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 24:  // A/B: production with the compiler's MD5 step form
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, false>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 22:  // diagnostic: compute only (synthetic stage data), production instantiation otherwise
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 1, false, true>), dim3(waves), dim3(64),
+                                       lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 23:  // diagnostic: loads + transpose + weak sums, no MD5
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 2, false, true>), dim3(waves), dim3(64),
+                                       lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
                     break;
                 case 16:
                     hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true, 1, 0, true>), dim3(waves), dim3(64), lb, s,
@@ -625,7 +651,9 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
 hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks, uint32_t dl,
                              uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s,
                              const int* abort_flag, int abort_gen) {
-    return launch_block_sums_variant(-1, d_data, n, B, nchunks, dl, seed_word, d_weak, d_strong, s, abort_flag,
+    // RSH_K1_VARIANT (diagnostic A/B, off by default) replaces the production variant for non-abortable launches
+    static const int forced = getenv("RSH_K1_VARIANT") ? atoi(getenv("RSH_K1_VARIANT")) : -1;
+    return launch_block_sums_variant(abort_flag ? -1 : forced, d_data, n, B, nchunks, dl, seed_word, d_weak, d_strong, s, abort_flag,
                                      abort_gen);
 }
 

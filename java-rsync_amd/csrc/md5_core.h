@@ -123,6 +123,97 @@ RSH_HD void md5_compress(Md5State& st, const uint32_t (&m)[16]) {
     st.d += d;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__) && defined(__gfx950__)
+// md5_compress for the streaming kernels on gfx950.  Per step, six instructions of which only
+// v_alignbit_b32 is half-rate: m + K (VOP2 with a 32-bit literal), + a, F = v_bitop3_b32, + F, rotate,
+// + b.  The compiler's own form puts a half-rate v_add3_u32 (a + m, F, K from an SGPR) on the
+// dependency chain; at the 2 waves/SIMD a 16 GiB file at B = 128 KiB leaves, that chain, not issue, set
+// the pace (tools/valu_lat.hip: 37 vs 29 cycles per step per wave; 29 = 96% of the SIMD's issue
+// bandwidth at 2 waves).  Truth tables for (S0, S1, S2) = (b, c, d): F 0xca, G 0xe4, H 0x96, I 0x39.
+#define RSH_LSTEP(BOP, a, b, c, d, m, k, s)                                                              \
+    do {                                                                                                 \
+        uint32_t t_, f_;                                                                                 \
+        asm("v_add_u32 %1, %8, %6\n\tv_add_u32 %1, %1, %0\n\tv_bitop3_b32 %2, %3, %4, %5 bitop3:" BOP      \
+            "\n\tv_add_u32 %1, %1, %2\n\tv_alignbit_b32 %1, %1, %1, %7\n\tv_add_u32 %0, %1, %3"              \
+            : "+v"(a), "=&v"(t_), "=&v"(f_)                                                              \
+            : "v"(b), "v"(c), "v"(d), "v"(m), "i"(32 - (s)), "i"((int)(k)));                             \
+    } while (0)
+__device__ __forceinline__ void md5_compress_lit(Md5State& st, const uint32_t (&m)[16]) {
+    uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
+    RSH_LSTEP("0xca", a, b, c, d, m[0], 0xd76aa478u, 7);
+    RSH_LSTEP("0xca", d, a, b, c, m[1], 0xe8c7b756u, 12);
+    RSH_LSTEP("0xca", c, d, a, b, m[2], 0x242070dbu, 17);
+    RSH_LSTEP("0xca", b, c, d, a, m[3], 0xc1bdceeeu, 22);
+    RSH_LSTEP("0xca", a, b, c, d, m[4], 0xf57c0fafu, 7);
+    RSH_LSTEP("0xca", d, a, b, c, m[5], 0x4787c62au, 12);
+    RSH_LSTEP("0xca", c, d, a, b, m[6], 0xa8304613u, 17);
+    RSH_LSTEP("0xca", b, c, d, a, m[7], 0xfd469501u, 22);
+    RSH_LSTEP("0xca", a, b, c, d, m[8], 0x698098d8u, 7);
+    RSH_LSTEP("0xca", d, a, b, c, m[9], 0x8b44f7afu, 12);
+    RSH_LSTEP("0xca", c, d, a, b, m[10], 0xffff5bb1u, 17);
+    RSH_LSTEP("0xca", b, c, d, a, m[11], 0x895cd7beu, 22);
+    RSH_LSTEP("0xca", a, b, c, d, m[12], 0x6b901122u, 7);
+    RSH_LSTEP("0xca", d, a, b, c, m[13], 0xfd987193u, 12);
+    RSH_LSTEP("0xca", c, d, a, b, m[14], 0xa679438eu, 17);
+    RSH_LSTEP("0xca", b, c, d, a, m[15], 0x49b40821u, 22);
+    RSH_LSTEP("0xe4", a, b, c, d, m[1], 0xf61e2562u, 5);
+    RSH_LSTEP("0xe4", d, a, b, c, m[6], 0xc040b340u, 9);
+    RSH_LSTEP("0xe4", c, d, a, b, m[11], 0x265e5a51u, 14);
+    RSH_LSTEP("0xe4", b, c, d, a, m[0], 0xe9b6c7aau, 20);
+    RSH_LSTEP("0xe4", a, b, c, d, m[5], 0xd62f105du, 5);
+    RSH_LSTEP("0xe4", d, a, b, c, m[10], 0x02441453u, 9);
+    RSH_LSTEP("0xe4", c, d, a, b, m[15], 0xd8a1e681u, 14);
+    RSH_LSTEP("0xe4", b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+    RSH_LSTEP("0xe4", a, b, c, d, m[9], 0x21e1cde6u, 5);
+    RSH_LSTEP("0xe4", d, a, b, c, m[14], 0xc33707d6u, 9);
+    RSH_LSTEP("0xe4", c, d, a, b, m[3], 0xf4d50d87u, 14);
+    RSH_LSTEP("0xe4", b, c, d, a, m[8], 0x455a14edu, 20);
+    RSH_LSTEP("0xe4", a, b, c, d, m[13], 0xa9e3e905u, 5);
+    RSH_LSTEP("0xe4", d, a, b, c, m[2], 0xfcefa3f8u, 9);
+    RSH_LSTEP("0xe4", c, d, a, b, m[7], 0x676f02d9u, 14);
+    RSH_LSTEP("0xe4", b, c, d, a, m[12], 0x8d2a4c8au, 20);
+    RSH_LSTEP("0x96", a, b, c, d, m[5], 0xfffa3942u, 4);
+    RSH_LSTEP("0x96", d, a, b, c, m[8], 0x8771f681u, 11);
+    RSH_LSTEP("0x96", c, d, a, b, m[11], 0x6d9d6122u, 16);
+    RSH_LSTEP("0x96", b, c, d, a, m[14], 0xfde5380cu, 23);
+    RSH_LSTEP("0x96", a, b, c, d, m[1], 0xa4beea44u, 4);
+    RSH_LSTEP("0x96", d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    RSH_LSTEP("0x96", c, d, a, b, m[7], 0xf6bb4b60u, 16);
+    RSH_LSTEP("0x96", b, c, d, a, m[10], 0xbebfbc70u, 23);
+    RSH_LSTEP("0x96", a, b, c, d, m[13], 0x289b7ec6u, 4);
+    RSH_LSTEP("0x96", d, a, b, c, m[0], 0xeaa127fau, 11);
+    RSH_LSTEP("0x96", c, d, a, b, m[3], 0xd4ef3085u, 16);
+    RSH_LSTEP("0x96", b, c, d, a, m[6], 0x04881d05u, 23);
+    RSH_LSTEP("0x96", a, b, c, d, m[9], 0xd9d4d039u, 4);
+    RSH_LSTEP("0x96", d, a, b, c, m[12], 0xe6db99e5u, 11);
+    RSH_LSTEP("0x96", c, d, a, b, m[15], 0x1fa27cf8u, 16);
+    RSH_LSTEP("0x96", b, c, d, a, m[2], 0xc4ac5665u, 23);
+    RSH_LSTEP("0x39", a, b, c, d, m[0], 0xf4292244u, 6);
+    RSH_LSTEP("0x39", d, a, b, c, m[7], 0x432aff97u, 10);
+    RSH_LSTEP("0x39", c, d, a, b, m[14], 0xab9423a7u, 15);
+    RSH_LSTEP("0x39", b, c, d, a, m[5], 0xfc93a039u, 21);
+    RSH_LSTEP("0x39", a, b, c, d, m[12], 0x655b59c3u, 6);
+    RSH_LSTEP("0x39", d, a, b, c, m[3], 0x8f0ccc92u, 10);
+    RSH_LSTEP("0x39", c, d, a, b, m[10], 0xffeff47du, 15);
+    RSH_LSTEP("0x39", b, c, d, a, m[1], 0x85845dd1u, 21);
+    RSH_LSTEP("0x39", a, b, c, d, m[8], 0x6fa87e4fu, 6);
+    RSH_LSTEP("0x39", d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+    RSH_LSTEP("0x39", c, d, a, b, m[6], 0xa3014314u, 15);
+    RSH_LSTEP("0x39", b, c, d, a, m[13], 0x4e0811a1u, 21);
+    RSH_LSTEP("0x39", a, b, c, d, m[4], 0xf7537e82u, 6);
+    RSH_LSTEP("0x39", d, a, b, c, m[11], 0xbd3af235u, 10);
+    RSH_LSTEP("0x39", c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+    RSH_LSTEP("0x39", b, c, d, a, m[9], 0xeb86d391u, 21);
+    st.a += a;
+    st.b += b;
+    st.c += c;
+    st.d += d;
+}
+#undef RSH_LSTEP
+#else
+RSH_HD void md5_compress_lit(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+#endif
+
 #if defined(__HIP__)
 // md5_compress with the block's weak-sum dot products (Rolling.compute, two v_dot4_i32_i8 per word)
 // threaded through rounds 1-2, one per step, into four independent accumulators: they fill the issue
