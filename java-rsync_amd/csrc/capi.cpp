@@ -435,6 +435,10 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     if (be.err != hipSuccess) return RSH_E_DEVICE;
     if (done && !landed && hipEventQuery(c->ev_spec) == hipErrorNotReady) {
         RSH_HIP(hipStreamWriteValue32(c->stream, c->abort_word, (uint32_t)gen, 0));  // the rest is dead work
+        // Later work on this context starts only once the stopped launch has left the CUs: K1 fills every
+        // wave slot of the chip exactly once (2 per SIMD at 16 GiB, B = 128 KiB), and a launch that finds
+        // slots still held by the draining waves (or their LDS fragmented) runs a second round of waves.
+        RSH_HIP(hipStreamWaitEvent(c->stream, c->ev_spec, 0));
         res->stats.speculation_aborted = 1;
         res->stats.device_ms += ms_since(t0);
     } else {

@@ -219,7 +219,7 @@ __device__ __forceinline__ int poll_abort(const int* flag) {
 }
 
 template <int D, bool NT, int WAVES = 1, int MODE = 0, bool FUSED = false, bool MFMAW = false, bool STEADY = true,
-          bool ABORT = false, bool LIT = true, bool PIN = false>
+          bool ABORT = false, int MD5F = 2, bool PIN = false>
 __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const uint8_t* __restrict__ data, uint32_t B,
                                                                   uint32_t dl, uint32_t seed,
                                                                   int32_t* __restrict__ weak_out,
@@ -227,6 +227,9 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
                                                                   const int* abort_flag = nullptr,
                                                                   int abort_gen = 0) {
     constexpr int ROW = 9;
+    // MODE (diagnostics): 0 production, 1 synthetic stage data (no loads), 2 no MD5, 3 = 1 without the weak-sum
+    // MFMAs, 4 = 3 without the LDS transpose (MD5 on the raw register words)
+    constexpr bool SYN = MODE == 1 || MODE == 3 || MODE == 4;
     // PIN: claim VGPRs up to v183 so that at most 2 waves fit a SIMD (512 / 184).  The MFMAW body needs 156,
     // which admits 3; a launch with exactly 2 waves per SIMD of work (16 GiB at B = 128 KiB) then may stack
     // 3 on some SIMDs and 1 on others when it starts while another kernel drains (5.1 ms instead of 3.2).
@@ -269,7 +272,7 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
     for (int d = 0; d < D; ++d) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            if constexpr (MODE == 1) q[d][j] = make_uint4(l + d, j, c0, 7);
+            if constexpr (SYN) q[d][j] = make_uint4(l + d, j, c0, 7);
             else q[d][j] = ld16<NT>(lp + 128 * (size_t)d + j * jstride);
         }
     }
@@ -279,18 +282,23 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
     // matrix pipe (MFMAW) and the two MD5 blocks.  Inlined with a compile-time slot d.
     auto stage = [&](auto dc, uint32_t si, bool refill) __attribute__((always_inline)) {
         constexpr int d = decltype(dc)::value;
+        uint4 qs[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) lds[wr0 + j * 8 * ROW] = q[d][j];
+        for (int j = 0; j < 8; ++j) {
+            qs[j] = q[d][j];
+            if constexpr (MODE != 4) lds[wr0 + j * 8 * ROW] = q[d][j];
+        }
         if (refill) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                if constexpr (MODE == 1) q[d][j] = make_uint4(q[d][j].y + si, q[d][j].x, q[d][j].w ^ si, q[d][j].z);
+                if constexpr (SYN) q[d][j] = make_uint4(q[d][j].y + si, q[d][j].x, q[d][j].w ^ si, q[d][j].z);
                 else q[d][j] = ld16<NT>(lp + 128 * (size_t)(si + D) + j * jstride);
             }
         }
-        if constexpr (WAVES == 1) __syncthreads();
+        if constexpr (MODE == 4) {
+        } else if constexpr (WAVES == 1) __syncthreads();
         else wave_lds_sync();
-        if constexpr (MFMAW) {
+        if constexpr (MFMAW && MODE != 3 && MODE != 4) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) Racc[g] += acc[g][0];  // R += P_{s-1}
 #pragma unroll
@@ -306,15 +314,27 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
         for (int h = 0; h < 2; ++h) {
             uint4 r[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) r[k] = lds[rd0 + 4 * h + k];
+            for (int k = 0; k < 4; ++k) r[k] = MODE == 4 ? qs[4 * h + k] : lds[rd0 + 4 * h + k];
             uint32_t m[16];
             unpack(r, m);
             if constexpr (MODE == 2) {
 #pragma unroll
                 for (int k = 0; k < 16; ++k) fold ^= m[k];
             } else if constexpr (MFMAW) {
-                if constexpr (LIT) md5_compress_lit(st, m);
+                if constexpr (MD5F == 8) md5_compress_rot16n(st, m);
+                else if constexpr (MD5F == 7) md5_compress_rot4n(st, m);
+                else if constexpr (MD5F == 6) md5_compress_rot16(st, m);
+                else if constexpr (MD5F == 5) md5_compress_rot4(st, m);
+                else if constexpr (MD5F == 4) md5_compress_asm16(st, m);
+                else if constexpr (MD5F == 3) md5_compress_asm4(st, m);
+                else if constexpr (MD5F == 2) md5_compress_asm(st, m);
+                else if constexpr (MD5F == 1) md5_compress_lit(st, m);
                 else md5_compress(st, m);
+            } else if constexpr (FUSED && MD5F == 1) {
+                int32_t wa, wb;
+                md5_compress_lit_weak(st, m, wa, wb);
+                s1 += wa;
+                u += (int32_t)((128 * si + 64 * h) * (uint32_t)wa) + wb;
             } else if constexpr (FUSED) {
                 md5_weak_block(st, m, s1, u, 128 * si + 64 * h);
             } else {
@@ -322,7 +342,8 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
                 md5_compress(st, m);
             }
         }
-        if constexpr (WAVES == 1) __syncthreads();
+        if constexpr (MODE == 4) {
+        } else if constexpr (WAVES == 1) __syncthreads();
         else wave_lds_sync();
     };
     uint32_t s = 0;
@@ -378,6 +399,194 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
     }
     const uint32_t c = c0 + l;
     if constexpr (MODE == 2) st.a ^= fold;
+    const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
+    weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
+    uint8_t* o = strong_out + (size_t)c * dl;
+    for (uint32_t k = 0; k < dl; ++k) {
+        const uint32_t word = k < 4 ? st.a : k < 8 ? st.b : k < 12 ? st.c : st.d;
+        o[k] = (uint8_t)(word >> (8 * (k & 3)));
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// K1, software-pipelined (production).  Same data path as block_sums_coalesced_kernel (coalesced
+// 128-B-line loads, LDS transpose with 9-slot rows, weak sums on the matrix pipe, one lane = one chunk),
+// but no LDS round trip ever sits on a wave's critical path: stage s+1 is written to the second LDS
+// buffer at the top of stage s, its message words and MFMA operands are read back into registers
+// between the two MD5 blocks of stage s, so they have landed long before stage s+1 starts.  The weak-sum
+// MFMAs of stage s sit between its MD5 blocks too.  Two stages of loads stay in flight (slots q[0..1]).
+// LDS operations of one wave execute in order, so a compiler-only barrier orders the write and the
+// reads of a buffer; no s_waitcnt lgkmcnt(0) / s_barrier per stage.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+
+template <int MD5F>
+__device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&m)[16]) {
+    if constexpr (MD5F == 8) md5_compress_rot16n(st, m);
+    else if constexpr (MD5F == 7) md5_compress_rot4n(st, m);
+    else if constexpr (MD5F == 1) md5_compress_lit(st, m);
+    else md5_compress(st, m);
+}
+
+// amdgpu_num_vgpr(192): two waves fill 384 of a SIMD's 512 registers, leaving room for one wave of the
+// resolver's range probe (104) to run beside the Sender's speculation launch in head mode.
+template <int MD5F, bool ABORT, bool PIN, int MODE = 0>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void block_sums_pipe_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
+                                                             uint32_t seed, int32_t* __restrict__ weak_out,
+                                                             uint8_t* __restrict__ strong_out,
+                                                             const int* abort_flag = nullptr, int abort_gen = 0) {
+    constexpr int ROW = 9;
+    constexpr int BUF = 64 * ROW;  // uint4 slots per LDS buffer
+    if constexpr (PIN) asm volatile("; occupancy pin" ::: "v175");
+    extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // 2 buffers (sized at launch)
+    const int l = threadIdx.x;
+    const uint32_t c0 = blockIdx.x * 64u;
+    const uint32_t nst = B >> 7;  // host guarantees nst >= 4
+    const int wr0 = (l >> 3) * ROW + (l & 7);
+    const int rd0 = l * ROW;
+
+    v4i32 wA[2];
+    v4i32 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    int32_t Racc[4] = {0, 0, 0, 0};
+    {
+        const int row = l & 15, ks = l >> 4;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                uint32_t word = 0;
+                if (row == 0) word = 0x01010101u;
+                else if (row == 1)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) word |= (uint32_t)(16 * (4 * h + mfma_sigma(ks)) + 4 * w + b) << (8 * b);
+                wA[h][w] = (int)word;
+            }
+    }
+    const int rdB = mfma_pi(l & 15) * ROW + mfma_sigma(l >> 4);
+
+    uint4 q[2][8];  // load slots: stage s+1 and s+2 in flight while stage s computes
+    uint4 Wa[4];    // words of the current stage's block 0 (then: the next stage's block 0)
+    uint4 Wb[4];    // words of the current stage's block 1
+    uint4 Bv[8];    // MFMA operands of the current stage
+    // Buffer loads: the wave's 64 chunks (64 * B <= 8 MiB) behind one descriptor, a 32-bit lane offset and
+    // a scalar offset per 8-chunk row j -- one VGPR of addressing instead of eight 64-bit pointers.
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data) + (size_t)c0 * B, 0, (int)(64 * B), 0x00020000);
+    const uint32_t lane_off = (uint32_t)(l >> 3) * B + 16u * (uint32_t)(l & 7);
+    auto load = [&](uint4 (&dst)[8], uint32_t stg) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if constexpr (MODE == 1) {
+                dst[j] = make_uint4(l + stg, j, c0, 7);
+            } else {
+                const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_off + 128u * stg, (int)(j * 8u * B), 2);
+                dst[j] = make_uint4(t.x, t.y, t.z, t.w);
+            }
+        }
+    };
+    auto put = [&](const uint4 (&src)[8], int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lds_all[buf * BUF + wr0 + j * 8 * ROW] = src[j];
+    };
+    auto get_words = [&](uint4 (&w)[4], int buf, int h) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = lds_all[buf * BUF + rd0 + 4 * h + k];
+    };
+    auto get_mfma = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) Bv[4 * h + g] = lds_all[buf * BUF + 16 * ROW * g + rdB + 4 * h];
+    };
+    Md5State st = md5_init();
+    auto md5_block = [&](const uint4 (&w)[4]) __attribute__((always_inline)) {
+        uint32_t m[16];
+        unpack(w, m);
+        md5_stream_block<MD5F>(st, m);
+    };
+    auto weak_mfma = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) Racc[g] += acc[g][0];  // R += P_{s-1}
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const uint4 bv = Bv[4 * h + g];
+                const v4i32 b4 = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
+                acc[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wA[h], b4, acc[g], 0, 0, 0);
+            }
+    };
+    // One stage with compile-time parity P: LDS buffer P holds it, q[P ^ 1] the next stage's data.
+    // Block-1 words and MFMA operands are read at the top (they land during block 0); the next stage's
+    // block-0 words are read between the blocks (they land during block 1).
+    auto stage = [&](auto pc, uint32_t si, bool has_next, bool refill) __attribute__((always_inline)) {
+        constexpr int P = decltype(pc)::value;
+        if (has_next) {
+            put(q[P ^ 1], P ^ 1);
+            if (refill) load(q[P ^ 1], si + 3);
+        }
+        get_words(Wb, P, 1);
+        get_mfma(P);
+        md5_block(Wa);
+        weak_mfma();
+        compiler_fence();
+        if (has_next) get_words(Wa, P ^ 1, 0);
+        md5_block(Wb);
+        compiler_fence();
+    };
+
+    load(q[0], 0);
+    load(q[1], 1);
+    put(q[0], 0);
+    load(q[0], 2);
+    compiler_fence();
+    get_words(Wa, 0, 0);
+    uint32_t s = 0;
+    // steady state: every stage has a next stage and a refill (branch-free: exact vmcnt bookkeeping)
+    // ABORT: one scalar load (glc: from L2, not the scalar cache) of the abort word per 2 stages, issued at
+    // the top of the iteration and compared at the bottom, so its latency hides behind the two stages.
+    // The compiler does not see the load; its own lgkmcnt(N) waits for LDS stay safe with one extra
+    // operation in flight (they only get stricter).
+    [[maybe_unused]] int flag = 0;
+    for (; s + 5 <= nst && (!ABORT || flag != abort_gen); s += 2) {
+        if constexpr (ABORT) asm volatile("s_load_dword %0, %1, 0x0 glc" : "=s"(flag) : "s"(abort_flag));
+        stage(std::integral_constant<int, 0>{}, s, true, true);
+        stage(std::integral_constant<int, 1>{}, s + 1, true, true);
+        if constexpr (ABORT) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(flag));
+    }
+    if constexpr (ABORT) {
+        if (flag == abort_gen) return;
+    }
+    for (; s < nst; s += 2) {  // drain
+        stage(std::integral_constant<int, 0>{}, s, s + 1 < nst, s + 3 < nst);
+        if (s + 1 < nst) stage(std::integral_constant<int, 1>{}, s + 1, s + 2 < nst, s + 4 < nst);
+    }
+    {
+        const uint64_t bits = ((uint64_t)B + 4) * 8;
+        uint32_t m[16] = {seed, 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, (uint32_t)bits, (uint32_t)(bits >> 32)};
+        md5_compress(st, m);
+    }
+    int32_t s1, u;
+    {
+        int32_t s1g[4], ug[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            Racc[g] += acc[g][0];
+            s1g[g] = acc[g][0];
+            ug[g] = (int32_t)(128u * (nst * (uint32_t)acc[g][0] - (uint32_t)Racc[g])) + acc[g][1];
+        }
+        const int src = mfma_pi_inv(l & 15);
+        int32_t t1[4], tu[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            t1[g] = __shfl(s1g[g], src, 64);
+            tu[g] = __shfl(ug[g], src, 64);
+        }
+        const int gs = l >> 4;
+        s1 = gs == 0 ? t1[0] : gs == 1 ? t1[1] : gs == 2 ? t1[2] : t1[3];
+        u = gs == 0 ? tu[0] : gs == 1 ? tu[1] : gs == 2 ? tu[2] : tu[3];
+    }
+    const uint32_t c = c0 + l;
     const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
     weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
     uint8_t* o = strong_out + (size_t)c * dl;
@@ -464,6 +673,9 @@ __global__ __launch_bounds__(64) void block_sums_dma_kernel(const uint8_t* __res
     }
 }
 
+// MD5 step form of the production K1: 0 compiler, 1 one asm statement per step, 2 generated blocks
+// (tools/gen_md5_asm.py)
+constexpr int kMd5Form = 2;
 constexpr uint32_t kCUs = 256;            // MI355X compute units
 constexpr uint32_t kLdsPerCU = 160 * 1024; // bytes
 
@@ -485,7 +697,7 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
     uint32_t c_first = 0;
     const bool deep = variant == 4 || variant == 6 || variant == 7 || variant == 9 || variant == 10 ||
                       variant == 11 || variant == 12 || variant == 14 || variant == 15 || variant == 16 ||
-                      variant == 18 || variant == 21;  // D >= 3 variants need nst >= 2D = 6 (8 for D = 4)
+                      variant == 18 || variant == 21 || variant >= 50;  // D >= 3 variants need nst >= 2D = 6 (8 for D = 4)
     if (variant >= 3 && (B % 128) == 0 && (B >> 7) >= (deep ? 8u : 4u) && (addr % 16) == 0) {
         const uint32_t nfullc = (uint32_t)std::min<int64_t>(n / B, nchunks);  // chunks with L == B
         const uint32_t waves = nfullc / 64;
@@ -550,9 +762,15 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     }
                     break;
                 case 19:
-                    if (nst <= 1024 && abort_flag && waves <= 2 * 4 * kCUs) {
+                    if (nst <= 1024 && nst >= 4 && abort_flag && waves <= 2 * 4 * kCUs) {
+                        hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true>), dim3(waves), dim3(64), 2 * wave_lds,
+                                           s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen);
+                    } else if (nst <= 1024 && nst >= 4 && waves <= 2 * 4 * kCUs) {
+                        hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true>), dim3(waves), dim3(64), 2 * wave_lds,
+                                           s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    } else if (nst <= 1024 && abort_flag && waves <= 2 * 4 * kCUs) {
                         hipLaunchKernelGGL(
-                            (block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, true, true, true>),
+                            (block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, true, kMd5Form, true>),
                             dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag,
                             abort_gen);
                     } else if (nst <= 1024 && abort_flag) {
@@ -561,7 +779,7 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                                            abort_flag, abort_gen);
                     } else if (nst <= 1024 && waves <= 2 * 4 * kCUs) {
                         hipLaunchKernelGGL(
-                            (block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, true, true>),
+                            (block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, kMd5Form, true>),
                             dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
                     } else if (nst <= 1024) {
                         hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true>), dim3(waves), dim3(64),
@@ -580,15 +798,119 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                                        dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
                     break;
                 case 24:  // A/B: production with the compiler's MD5 step form
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, false>),
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 0, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 25:  // A/B: one asm statement per MD5 step
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 1, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 30:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 3, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 31:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 4, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 32:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 1, false, true, true, false, 1, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 33:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 3, false, true, true, false, 1, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 34:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 3, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 35:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 4, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 36:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, true, false, true, false, 1, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 37:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 5, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 38:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 6, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 39:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 5, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 40:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 6, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 41:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, true, false, true, false, 1, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 42:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 7, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 43:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 8, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 44:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 7, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 45:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 8, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 50:
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 0>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 51:
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<1, false, true, 0>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 52:
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 1>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 53:
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<1, false, true, 1>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 54:
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, false, 0>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 26:  // diagnostics (wrong results): synthetic data, no weak-sum MFMAs
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 3, false, true, true, false, 2, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 27:  // ... and no LDS transpose, MD5 forms 2 / 1 / 0
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 2, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 28:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 1, true>),
+                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 29:
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 0, true>),
                                        dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
                     break;
                 case 22:  // diagnostic: compute only (synthetic stage data), production instantiation otherwise
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 1, false, true>), dim3(waves), dim3(64),
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 1, false, true, true, false, 2, true>), dim3(waves), dim3(64),
                                        lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
                     break;
                 case 23:  // diagnostic: loads + transpose + weak sums, no MD5
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 2, false, true>), dim3(waves), dim3(64),
+                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 2, false, true, true, false, 2, true>), dim3(waves), dim3(64),
                                        lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
                     break;
                 case 16:

@@ -209,9 +209,140 @@ __device__ __forceinline__ void md5_compress_lit(Md5State& st, const uint32_t (&
     st.c += c;
     st.d += d;
 }
+// md5_compress_lit with the block's weak-sum dot products threaded through rounds 1-2 (as md5_compress_weak).
+__device__ __forceinline__ void md5_compress_lit_weak(Md5State& st, const uint32_t (&m)[16], int32_t& a_out,
+                                                  int32_t& b_out) {
+    int32_t wa0 = 0, wa1 = 0, wb0 = 0, wb1 = 0;
+#define RSH_LWA(j) ((j) & 1 ? wa1 : wa0) = __builtin_amdgcn_sdot4((int)m[j], 0x01010101, (j) & 1 ? wa1 : wa0, false)
+#define RSH_LWB(j)                                                                                            \
+    ((j) & 1 ? wb1 : wb0) = __builtin_amdgcn_sdot4(                                                          \
+        (int)m[j], (4 * (j)) | ((4 * (j) + 1) << 8) | ((4 * (j) + 2) << 16) | ((4 * (j) + 3) << 24),           \
+        (j) & 1 ? wb1 : wb0, false)
+    uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
+    RSH_LSTEP("0xca", a, b, c, d, m[0], 0xd76aa478u, 7);
+    RSH_LWA(0);
+    RSH_LSTEP("0xca", d, a, b, c, m[1], 0xe8c7b756u, 12);
+    RSH_LWA(1);
+    RSH_LSTEP("0xca", c, d, a, b, m[2], 0x242070dbu, 17);
+    RSH_LWA(2);
+    RSH_LSTEP("0xca", b, c, d, a, m[3], 0xc1bdceeeu, 22);
+    RSH_LWA(3);
+    RSH_LSTEP("0xca", a, b, c, d, m[4], 0xf57c0fafu, 7);
+    RSH_LWA(4);
+    RSH_LSTEP("0xca", d, a, b, c, m[5], 0x4787c62au, 12);
+    RSH_LWA(5);
+    RSH_LSTEP("0xca", c, d, a, b, m[6], 0xa8304613u, 17);
+    RSH_LWA(6);
+    RSH_LSTEP("0xca", b, c, d, a, m[7], 0xfd469501u, 22);
+    RSH_LWA(7);
+    RSH_LSTEP("0xca", a, b, c, d, m[8], 0x698098d8u, 7);
+    RSH_LWA(8);
+    RSH_LSTEP("0xca", d, a, b, c, m[9], 0x8b44f7afu, 12);
+    RSH_LWA(9);
+    RSH_LSTEP("0xca", c, d, a, b, m[10], 0xffff5bb1u, 17);
+    RSH_LWA(10);
+    RSH_LSTEP("0xca", b, c, d, a, m[11], 0x895cd7beu, 22);
+    RSH_LWA(11);
+    RSH_LSTEP("0xca", a, b, c, d, m[12], 0x6b901122u, 7);
+    RSH_LWA(12);
+    RSH_LSTEP("0xca", d, a, b, c, m[13], 0xfd987193u, 12);
+    RSH_LWA(13);
+    RSH_LSTEP("0xca", c, d, a, b, m[14], 0xa679438eu, 17);
+    RSH_LWA(14);
+    RSH_LSTEP("0xca", b, c, d, a, m[15], 0x49b40821u, 22);
+    RSH_LWA(15);
+
+    RSH_LSTEP("0xe4", a, b, c, d, m[1], 0xf61e2562u, 5);
+    RSH_LWB(0);
+    RSH_LSTEP("0xe4", d, a, b, c, m[6], 0xc040b340u, 9);
+    RSH_LWB(1);
+    RSH_LSTEP("0xe4", c, d, a, b, m[11], 0x265e5a51u, 14);
+    RSH_LWB(2);
+    RSH_LSTEP("0xe4", b, c, d, a, m[0], 0xe9b6c7aau, 20);
+    RSH_LWB(3);
+    RSH_LSTEP("0xe4", a, b, c, d, m[5], 0xd62f105du, 5);
+    RSH_LWB(4);
+    RSH_LSTEP("0xe4", d, a, b, c, m[10], 0x02441453u, 9);
+    RSH_LWB(5);
+    RSH_LSTEP("0xe4", c, d, a, b, m[15], 0xd8a1e681u, 14);
+    RSH_LWB(6);
+    RSH_LSTEP("0xe4", b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+    RSH_LWB(7);
+    RSH_LSTEP("0xe4", a, b, c, d, m[9], 0x21e1cde6u, 5);
+    RSH_LWB(8);
+    RSH_LSTEP("0xe4", d, a, b, c, m[14], 0xc33707d6u, 9);
+    RSH_LWB(9);
+    RSH_LSTEP("0xe4", c, d, a, b, m[3], 0xf4d50d87u, 14);
+    RSH_LWB(10);
+    RSH_LSTEP("0xe4", b, c, d, a, m[8], 0x455a14edu, 20);
+    RSH_LWB(11);
+    RSH_LSTEP("0xe4", a, b, c, d, m[13], 0xa9e3e905u, 5);
+    RSH_LWB(12);
+    RSH_LSTEP("0xe4", d, a, b, c, m[2], 0xfcefa3f8u, 9);
+    RSH_LWB(13);
+    RSH_LSTEP("0xe4", c, d, a, b, m[7], 0x676f02d9u, 14);
+    RSH_LWB(14);
+    RSH_LSTEP("0xe4", b, c, d, a, m[12], 0x8d2a4c8au, 20);
+    RSH_LWB(15);
+
+    RSH_LSTEP("0x96", a, b, c, d, m[5], 0xfffa3942u, 4);
+    RSH_LSTEP("0x96", d, a, b, c, m[8], 0x8771f681u, 11);
+    RSH_LSTEP("0x96", c, d, a, b, m[11], 0x6d9d6122u, 16);
+    RSH_LSTEP("0x96", b, c, d, a, m[14], 0xfde5380cu, 23);
+    RSH_LSTEP("0x96", a, b, c, d, m[1], 0xa4beea44u, 4);
+    RSH_LSTEP("0x96", d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    RSH_LSTEP("0x96", c, d, a, b, m[7], 0xf6bb4b60u, 16);
+    RSH_LSTEP("0x96", b, c, d, a, m[10], 0xbebfbc70u, 23);
+    RSH_LSTEP("0x96", a, b, c, d, m[13], 0x289b7ec6u, 4);
+    RSH_LSTEP("0x96", d, a, b, c, m[0], 0xeaa127fau, 11);
+    RSH_LSTEP("0x96", c, d, a, b, m[3], 0xd4ef3085u, 16);
+    RSH_LSTEP("0x96", b, c, d, a, m[6], 0x04881d05u, 23);
+    RSH_LSTEP("0x96", a, b, c, d, m[9], 0xd9d4d039u, 4);
+    RSH_LSTEP("0x96", d, a, b, c, m[12], 0xe6db99e5u, 11);
+    RSH_LSTEP("0x96", c, d, a, b, m[15], 0x1fa27cf8u, 16);
+    RSH_LSTEP("0x96", b, c, d, a, m[2], 0xc4ac5665u, 23);
+
+    RSH_LSTEP("0x39", a, b, c, d, m[0], 0xf4292244u, 6);
+    RSH_LSTEP("0x39", d, a, b, c, m[7], 0x432aff97u, 10);
+    RSH_LSTEP("0x39", c, d, a, b, m[14], 0xab9423a7u, 15);
+    RSH_LSTEP("0x39", b, c, d, a, m[5], 0xfc93a039u, 21);
+    RSH_LSTEP("0x39", a, b, c, d, m[12], 0x655b59c3u, 6);
+    RSH_LSTEP("0x39", d, a, b, c, m[3], 0x8f0ccc92u, 10);
+    RSH_LSTEP("0x39", c, d, a, b, m[10], 0xffeff47du, 15);
+    RSH_LSTEP("0x39", b, c, d, a, m[1], 0x85845dd1u, 21);
+    RSH_LSTEP("0x39", a, b, c, d, m[8], 0x6fa87e4fu, 6);
+    RSH_LSTEP("0x39", d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+    RSH_LSTEP("0x39", c, d, a, b, m[6], 0xa3014314u, 15);
+    RSH_LSTEP("0x39", b, c, d, a, m[13], 0x4e0811a1u, 21);
+    RSH_LSTEP("0x39", a, b, c, d, m[4], 0xf7537e82u, 6);
+    RSH_LSTEP("0x39", d, a, b, c, m[11], 0xbd3af235u, 10);
+    RSH_LSTEP("0x39", c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+    RSH_LSTEP("0x39", b, c, d, a, m[9], 0xeb86d391u, 21);
+
+    st.a += a;
+    st.b += b;
+    st.c += c;
+    st.d += d;
+    a_out = wa0 + wa1;
+    b_out = wb0 + wb1;
+#undef RSH_LWA
+#undef RSH_LWB
+}
 #undef RSH_LSTEP
+#include "md5_asm.inc"
 #else
 RSH_HD void md5_compress_lit(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+RSH_HD void md5_compress_asm(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+__host__ __device__ inline void md5_compress_lit_weak(Md5State& st, const uint32_t (&m)[16], int32_t& a, int32_t& b) {
+    md5_compress(st, m);
+    a = b = 0;
+}
+RSH_HD void md5_compress_rot4(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+RSH_HD void md5_compress_rot16(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+RSH_HD void md5_compress_rot4n(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+RSH_HD void md5_compress_rot16n(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+RSH_HD void md5_compress_asm4(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+RSH_HD void md5_compress_asm16(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
 #endif
 
 #if defined(__HIP__)
