@@ -333,7 +333,7 @@ __device__ __forceinline__ void md5_compress_lit_weak(Md5State& st, const uint32
 #else
 RSH_HD void md5_compress_lit(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
 RSH_HD void md5_compress_asm(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
-__host__ __device__ inline void md5_compress_lit_weak(Md5State& st, const uint32_t (&m)[16], int32_t& a, int32_t& b) {
+RSH_HD void md5_compress_lit_weak(Md5State& st, const uint32_t (&m)[16], int32_t& a, int32_t& b) {
     md5_compress(st, m);
     a = b = 0;
 }
