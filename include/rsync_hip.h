@@ -75,7 +75,8 @@ typedef struct {
     double resolver_ms;      /* host resolver time (including its small device round trips)   */
     double table_ms;         /* host sort of the received table (overlaps the device phase)   */
     int64_t head_steps;      /* resolver steps taken before the aligned speculation landed    */
-    int64_t speculation_aborted; /* 1: the scan ended first and the speculation launch was stopped */
+    int64_t speculation_aborted; /* 1: the scan ended first and the speculation launch was stopped;
+                                    2: the scan ended in head mode before the speculation was launched */
 } rsh_scan_stats;
 
 typedef struct rsh_ctx rsh_ctx;

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -90,13 +91,16 @@ struct rsh_ctx {
     hipStream_t stream = nullptr;
     DevBuf data, weak, strong;                   // host-input staging
     DevBuf src_weak, src_strong, flags;          // aligned speculation over the source
-    DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw;
+    DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw, partials, bucket;
     hipStream_t aux = nullptr;                   // table download, then the aligned speculation
     hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr;
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
     // resolver round trips: the small kernels read their inputs from and write their outputs to pinned
     // host memory directly (no staging copies); the probe result and digest windows come back by copy
-    PinnedBuf h_pos, h_out, h_iv, h_tiles, h_keys, h_first, h_win;
+    PinnedBuf h_pos, h_out, h_iv, h_tiles, h_keys, h_first, h_win, h_ptiles;
+    PinnedBuf h_hit;  // after a probe hit: T(p) (bytes 0..3) and the window at p (from byte 16)
+    PinnedBuf h_win0;    // window 0 of the current scan (its digest is computed on a host thread)
+    PinnedBuf h_bucket;  // after a probe hit: {count, key, chunk indices} of the key that hit
     uint64_t first_used = 0;    // probe result slots handed out (see HipBackend::first_hit)
     int* abort_word = nullptr;  // device, uncached: the speculation launch of generation g stops once it reads g
     int gen = 0;
@@ -104,10 +108,10 @@ struct rsh_ctx {
     std::atomic<bool> busy{false};   // the staging buffers and last_ev serve one call at a time
     ~rsh_ctx() {
         for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &slots, &dslots, &dkeys, &pos, &out,
-                          &first, &win, &ivbuf, &tilebuf, &haw})
+                          &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pos, &h_out, &h_iv, &h_tiles, &h_keys, &h_first,
-                             &h_win})
+                             &h_win, &h_ptiles, &h_hit, &h_win0, &h_bucket})
             b->release();
         if (abort_word) (void)hipFree(abort_word);
         if (ev_in) (void)hipEventDestroy(ev_in);
@@ -157,6 +161,9 @@ struct CtxClaim {
 // HIP implementation of the resolver's services.
 // ------------------------------------------------------------------------------------------------
 constexpr size_t kFirstSlots = 1024;
+// Head mode launches the aligned speculation after this many resolver steps or milliseconds.
+constexpr int64_t kDeferSteps = 2;
+constexpr double kDeferMs = 0.25;
 
 // RSH_SCAN_TRACE=1: one stderr line per resolver round trip (diagnostics).
 struct CallTrace {
@@ -175,8 +182,9 @@ struct CallTrace {
 
 class HipBackend : public rsh::ScanBackend {
   public:
-    HipBackend(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh::ChunkTable& t, const uint8_t seed[4])
-        : c_(c), x_(d_src), n_(n), t_(t), B_(t.block_length), dl_(t.digest_length) {
+    HipBackend(rsh_ctx* c, const uint8_t* d_src, int64_t n, rsh::ChunkTable& t, const int32_t* d_table_weak,
+               const uint8_t seed[4])
+        : c_(c), x_(d_src), n_(n), t_(t), d_table_weak_(d_table_weak), B_(t.block_length), dl_(t.digest_length) {
         memcpy(seed_, seed, 4);
     }
     hipError_t err = hipSuccess;
@@ -190,6 +198,7 @@ class HipBackend : public rsh::ScanBackend {
     // filled on demand for the blocks a probe touches.
     bool head = false;
     std::vector<uint8_t> haw_ready;
+    std::function<void(uint8_t*)> md5_0;  // digest of window 0 (joins its host thread)
 
     int64_t aligned_count() override { return head ? 0 : na; }
     int64_t max_batch() override { return head ? 4 : 4096; }
@@ -199,6 +208,10 @@ class HipBackend : public rsh::ScanBackend {
 
     void weak_many(const int64_t* pos, int64_t count, int32_t* out) override {
         if (count <= 0) return;
+        if (count == 1 && pos[0] == hit_pos_) {  // fetched with the probe result
+            out[0] = hit_weak_;
+            return;
+        }
         CallTrace tr("weak_many", count);
         int64_t* hp = pin<int64_t>(c_->h_pos, count);
         int32_t* ho = pin<int32_t>(c_->h_out, count);
@@ -224,6 +237,17 @@ class HipBackend : public rsh::ScanBackend {
     void md5_at(int64_t p, uint8_t out[16]) override {
         CallTrace tr("md5_at", p);
         const int64_t w = std::min<int64_t>(B_, n_ - p);
+        if (p == 0 && md5_0) {  // computed on a host thread since the scan started
+            md5_0(out);
+            return;
+        }
+        if (p == hit_pos_) {  // the window came back with the probe result
+            rsh::HostMd5 h;
+            h.update(c_->h_hit.as<uint8_t>() + 16, (size_t)w);
+            h.update(seed_, 4);
+            h.final(out);
+            return;
+        }
         uint8_t* hw = pin<uint8_t>(c_->h_win, w);
         if (err != hipSuccess) return;
         ok(rsh::launch_copy_to_host(x_ + p, w, hw, c_->stream));
@@ -250,9 +274,13 @@ class HipBackend : public rsh::ScanBackend {
         }
         tiles_.clear();
         for (int64_t i = 0; i < count; ++i) rsh::probe_tiles(iv[i].a, iv[i].b, B_, (int32_t)i, &tiles_);
+        rsh::probe_partials(&tiles_, B_, &ptiles_);
         rsh::ProbeIv* hiv = pin<rsh::ProbeIv>(c_->h_iv, count + 1);
         rsh::ProbeTile* ht = pin<rsh::ProbeTile>(c_->h_tiles, (int64_t)tiles_.size() + 1);
+        rsh::PartialTile* hpt = pin<rsh::PartialTile>(c_->h_ptiles, (int64_t)ptiles_.size() + 1);
         unsigned long long* hf = pin<unsigned long long>(c_->h_first, 1);
+        uint8_t* hh = pin<uint8_t>(c_->h_hit, 16 + B_);
+        ok(c_->partials.ensure((ptiles_.size() + 1) * sizeof(int4)));
         // result slots preset to ~0 ("none") in batches: one memset per kFirstSlots probes
         ok(c_->first.ensure(kFirstSlots * sizeof(unsigned long long)));
         if (err != hipSuccess) return -1;
@@ -262,6 +290,7 @@ class HipBackend : public rsh::ScanBackend {
         for (int64_t i = 0; i < count; ++i)
             hiv[i] = rsh::ProbeIv{iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo & 0xFFFFu, iv[i].e_hi & 0xFFFFu};
         if (!tiles_.empty()) memcpy(ht, tiles_.data(), tiles_.size() * sizeof(rsh::ProbeTile));
+        if (!ptiles_.empty()) memcpy(hpt, ptiles_.data(), ptiles_.size() * sizeof(rsh::PartialTile));
         if (head) {  // anchors T(kB) for the blocks these tiles sit in
             anchors_.clear();
             for (const rsh::ProbeTile& t : tiles_) {
@@ -288,10 +317,28 @@ class HipBackend : public rsh::ScanBackend {
         A.ivs = hiv;
         A.tiles = ht;
         A.first = d_first;
-        ok(rsh::launch_probe_first(A, (uint32_t)tiles_.size(), c_->stream));
+        A.partials = c_->partials.as<int4>();
+        ok(rsh::launch_probe_first(A, (uint32_t)tiles_.size(), hpt, (uint32_t)ptiles_.size(), c_->partials.as<int4>(),
+                                   c_->stream));
+        // the resolver's next questions at a hit are T(p), the bucket of the key that hit and (usually) the
+        // MD5 of the window at p: answer them in this round trip
+        ok(c_->bucket.ensure((2 + rsh::HIT_BUCKET_CAP) * sizeof(int32_t)));
+        int32_t* hb = pin<int32_t>(c_->h_bucket, 2 + rsh::HIT_BUCKET_CAP);
+        if (err != hipSuccess) return -1;
+        ok(rsh::launch_hit_window(x_, n_, (uint32_t)B_, d_first, hiv, (int32_t)count, d_table_weak_, t_.chunk_count,
+                                  c_->bucket.as<int32_t>(), reinterpret_cast<int32_t*>(hh), hh + 16, c_->stream));
         ok(hipMemcpyAsync(hf, d_first, sizeof(unsigned long long), hipMemcpyDeviceToHost, c_->stream));
+        ok(hipMemcpyAsync(hb, c_->bucket.p, (2 + rsh::HIT_BUCKET_CAP) * sizeof(int32_t), hipMemcpyDeviceToHost,
+                          c_->stream));
         ok(hipStreamSynchronize(c_->stream));
-        return *hf == ~0ull ? -1 : (int64_t)*hf;
+        if (*hf == ~0ull) return -1;
+        hit_pos_ = (int64_t)*hf;
+        hit_weak_ = *reinterpret_cast<const int32_t*>(hh);
+        if (hb[0] <= rsh::HIT_BUCKET_CAP) {  // ascending chunk order, as the Multimap keeps it
+            std::sort(hb + 2, hb + 2 + hb[0]);
+            t_.prime(hb[1], hb + 2, hb[0]);
+        }
+        return hit_pos_;
     }
 
   private:
@@ -309,12 +356,16 @@ class HipBackend : public rsh::ScanBackend {
     rsh_ctx* c_;
     const uint8_t* x_;
     int64_t n_;
-    const rsh::ChunkTable& t_;
+    rsh::ChunkTable& t_;
+    const int32_t* d_table_weak_;  // the received table's weak sums on the device
     int64_t B_;
     int dl_;
     uint8_t seed_[4];
     std::vector<rsh::ProbeTile> tiles_;
+    std::vector<rsh::PartialTile> ptiles_;
     std::vector<int64_t> anchors_;
+    int64_t hit_pos_ = -1;  // position of the last probe hit (its weak sum and window are on the host)
+    int32_t hit_weak_ = 0;
 };
 
 // Header consistency for the Generator side (3-arg ctor semantics, Checksum.java:94-113).
@@ -380,22 +431,41 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         host_strong = c->h_strong.as<uint8_t>();
     }
     // (aux) the aligned speculation: the source's own block sums with the basis header's B and dl,
-    // the chain flags, and their download
+    // the chain flags, and their download.  It is a bet on long runs of aligned matches; in head mode it
+    // is launched only once the resolver has taken kDeferSteps steps or kDeferMs without finishing
+    // (until then the resolver's round trips run on an otherwise idle device: a range probe beside the
+    // speculation takes ~0.16 ms instead of tens of microseconds).
     const int gen = ++c->gen;
     static const int diag = getenv("RSH_SCAN_DIAG") ? atoi(getenv("RSH_SCAN_DIAG")) : 0;  // A/B switches
-    if (!download) RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
-    RSH_HIP(rsh::launch_block_sums(d_src, n, (uint32_t)B, (uint32_t)na, (uint32_t)dl, seed_word(seed),
-                                   c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->aux,
-                                   (diag & 2) ? nullptr : c->abort_word, gen));
-    RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
-                                    (uint32_t)nf, (uint32_t)dl, c->flags.as<uint8_t>(), c->aux));
-    RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)na * 4, hipMemcpyDeviceToHost, c->aux));
-    if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)na * dl, hipMemcpyDeviceToHost, c->aux));
-    if (nf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)nf, hipMemcpyDeviceToHost, c->aux));
-    RSH_HIP(hipEventRecord(c->ev_spec, c->aux));
+    auto launch_spec = [&]() -> int {
+        if (!download) RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
+        RSH_HIP(rsh::launch_block_sums(d_src, n, (uint32_t)B, (uint32_t)na, (uint32_t)dl, seed_word(seed),
+                                       c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->aux,
+                                       (diag & 2) ? nullptr : c->abort_word, gen));
+        RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
+                                        (uint32_t)nf, (uint32_t)dl, c->flags.as<uint8_t>(), c->aux));
+        RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)na * 4, hipMemcpyDeviceToHost, c->aux));
+        if (dl > 0)
+            RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)na * dl, hipMemcpyDeviceToHost, c->aux));
+        if (nf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)nf, hipMemcpyDeviceToHost, c->aux));
+        RSH_HIP(hipEventRecord(c->ev_spec, c->aux));
+        return RSH_OK;
+    };
+    const bool head = !(diag & 1);
+    bool spec_launched = false;
+    if (!head || (diag & 4)) {  // RSH_SCAN_DIAG bit 2: launch at once even in head mode (A/B)
+        const int rc = launch_spec();
+        if (rc != RSH_OK) return rc;
+        spec_launched = true;
+    }
     // (stream) the device probe hash
     RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, c->stream));
     RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, c->stream));
+    // (stream + a host thread) the digest of window 0: the first event of a scan over a similar file is
+    // at position 0, and its MD5 (one serial chain, ~0.13 ms for 128 KiB) then overlaps the first probe
+    const int64_t w0 = std::min<int64_t>(B, n);
+    RSH_HIP(c->h_win0.ensure((size_t)w0 + 16));
+    RSH_HIP(rsh::launch_copy_to_host(d_src, w0, c->h_win0.as<uint8_t>(), c->stream));
 
     // (host) sort the table
     rsh::ChunkTable table;
@@ -413,27 +483,59 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         CallTrace tr("hash_sync", ns);
         RSH_HIP(hipStreamSynchronize(c->stream));
     }
+    uint8_t md5_0[16];
+    std::thread md5_0_thread([&] {
+        rsh::HostMd5 hm;
+        hm.update(c->h_win0.as<uint8_t>(), (size_t)w0);
+        hm.update(seed, 4);
+        hm.final(md5_0);
+    });
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() {
+            if (t.joinable()) t.join();
+        }
+    } joiner{md5_0_thread};
 
-    HipBackend be(c, d_src, n, table, seed);
+    HipBackend be(c, d_src, n, table, d_weak, seed);
     be.table.slots = c->slots.as<unsigned long long>();
     be.table.mask = ns - 1;
     be.na = na;
     be.aw = c->h_aw.as<int32_t>();
     be.as = c->h_as.as<uint8_t>();
     be.fl = c->h_fl.as<uint8_t>();
-    be.head = !(diag & 1);
+    be.head = head;
+    be.md5_0 = [&](uint8_t out[16]) {
+        if (md5_0_thread.joinable()) md5_0_thread.join();
+        memcpy(out, md5_0, 16);
+    };
     be.haw_ready.assign((size_t)na, 0);
     rsh::ResolveState rs;
     bool landed = false;
+    int spec_rc = RSH_OK;
+    const auto t_head = std::chrono::steady_clock::now();
     const bool done = rsh::resolve_run(n, table, be, &rs, res, [&] {
         if (be.err != hipSuccess || !be.head) return true;
         CallTrace tr("ev_query", res->stats.head_steps);
+        if (!spec_launched) {
+            if (res->stats.head_steps >= kDeferSteps || ms_since(t_head) >= kDeferMs) {
+                spec_rc = launch_spec();
+                spec_launched = true;
+                if (spec_rc != RSH_OK) return true;
+            }
+            res->stats.head_steps++;
+            return false;
+        }
         landed = hipEventQuery(c->ev_spec) != hipErrorNotReady;
         if (!landed) res->stats.head_steps++;
         return landed;
     });
+    if (spec_rc != RSH_OK) return spec_rc;
     if (be.err != hipSuccess) return RSH_E_DEVICE;
-    if (done && !landed && hipEventQuery(c->ev_spec) == hipErrorNotReady) {
+    if (done && !spec_launched) {
+        res->stats.speculation_aborted = 2;  // the scan ended in head mode before the speculation was needed
+        res->stats.device_ms += ms_since(t0);
+    } else if (done && !landed && hipEventQuery(c->ev_spec) == hipErrorNotReady) {
         RSH_HIP(hipStreamWriteValue32(c->stream, c->abort_word, (uint32_t)gen, 0));  // the rest is dead work
         // Later work on this context starts only once the stopped launch has left the CUs: K1 fills every
         // wave slot of the chip exactly once (2 per SIMD at 16 GiB, B = 128 KiB), and a launch that finds

@@ -46,9 +46,15 @@ struct ProbeIv {
     uint32_t e_lo, e_hi;
 };
 struct ProbeTile {
-    int64_t q0;  // tile start (multiple of PROBE_TILE from its block start)
-    int32_t iv;  // interval index
-    int32_t pad;
+    int64_t q0;     // tile start (multiple of PROBE_TILE from its block start)
+    int32_t iv;     // interval index
+    int32_t pbase;  // index of its block's tile-0 partial sums in ProbeArgs::partials (unused for tile 0)
+};
+// Pass 1 of a probe: the four byte sums (x[j], (j - o) x[j] over the tile, and the same over the tile
+// shifted by B) of every tile of a block that lies before a probed tile of that block, so that pass 2
+// gets each tile's block prefix from at most 31 partials instead of re-reading up to B bytes per tile.
+struct PartialTile {
+    int64_t q0;
 };
 struct ProbeArgs {
     const uint8_t* data;
@@ -58,11 +64,25 @@ struct ProbeArgs {
     ProbeTable table;
     const ProbeIv* ivs;
     const ProbeTile* tiles;
+    const int4* partials;  // written by pass 1
     unsigned long long* first;
 };
 // Appends the tiles covering [a, b) for interval `iv` (host side).
 void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeTile>* out);
-hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, hipStream_t s);
+// Assigns ProbeTile::pbase and lists the partial tiles pass 1 computes (host side).
+void probe_partials(std::vector<ProbeTile>* tiles, int64_t B, std::vector<PartialTile>* out);
+// Both passes, back to back on stream s.
+hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const PartialTile* d_ptiles, uint32_t nptiles,
+                              int4* d_partials, hipStream_t s);
+// After a probe: if *d_first holds a position p, the resolver's next questions answered in the same
+// round trip, on stream s: the true weak sum T(p) into *h_weak, the window [p, p + min(B, n - p)) into
+// pinned host memory h_win, and the bucket of the key R(p) = T(p) + E(p) (E from the interval holding
+// p) in the received table d_table_weak[C]: *d_bucket = {count, key, idx[0 .. min(count, cap))}, in
+// no particular order.
+constexpr int HIT_BUCKET_CAP = 256;
+hipError_t launch_hit_window(const uint8_t* d_data, int64_t n, uint32_t B, const unsigned long long* d_first,
+                             const ProbeIv* ivs, int32_t niv, const int32_t* d_table_weak, int32_t C,
+                             int32_t* d_bucket, int32_t* h_weak, uint8_t* h_win, hipStream_t s);
 
 // n bytes of device memory into pinned host memory (h_dst 16-byte aligned), by a kernel.
 hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s);

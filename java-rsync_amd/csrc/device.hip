@@ -1079,13 +1079,35 @@ __device__ __forceinline__ void range_sums(const uint8_t* __restrict__ x, int64_
         s1 += v;
         s2 += (int32_t)((uint32_t)(j - org) * (uint32_t)v);
     }
-    for (int64_t j = a16 + 16 * (int64_t)t; j < b16; j += 16 * (int64_t)T) {
-        const uint4 v = *reinterpret_cast<const uint4*>(x + j);
-        const uint32_t rel = (uint32_t)(j - org);
-        dword_sums(v.x, rel, s1, s2);
-        dword_sums(v.y, rel + 4, s1, s2);
-        dword_sums(v.z, rel + 8, s1, s2);
-        dword_sums(v.w, rel + 12, s1, s2);
+    // 64-B pieces per lane, eight 16-B loads in flight before any use (a 128 KiB window in a few round
+    // trips instead of one per 4 KiB: these single-workgroup reductions sit on the resolver's latency path)
+    int64_t j = a16 + 64 * (int64_t)t;
+    for (; j + 64 * (int64_t)T + 64 <= b16; j += 128 * (int64_t)T) {
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const uint4*>(x + j + 16 * k);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[4 + k] = *reinterpret_cast<const uint4*>(x + j + 64 * (int64_t)T + 16 * k);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t rel = (uint32_t)(j + (k >= 4 ? 64 * (int64_t)T : 0) + 16 * (k & 3) - org);
+            dword_sums(v[k].x, rel, s1, s2);
+            dword_sums(v[k].y, rel + 4, s1, s2);
+            dword_sums(v[k].z, rel + 8, s1, s2);
+            dword_sums(v[k].w, rel + 12, s1, s2);
+        }
+    }
+    for (; j < b16; j += 64 * (int64_t)T) {  // remaining 64-B pieces (the last may be 16..48 B)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (j + 16 * k >= b16) break;
+            const uint4 v = *reinterpret_cast<const uint4*>(x + j + 16 * k);
+            const uint32_t rel = (uint32_t)(j + 16 * k - org);
+            dword_sums(v.x, rel, s1, s2);
+            dword_sums(v.y, rel + 4, s1, s2);
+            dword_sums(v.z, rel + 8, s1, s2);
+            dword_sums(v.w, rel + 12, s1, s2);
+        }
     }
     for (int64_t j = b16 + t; j < hi; j += T) {  // tail
         const int32_t v = sbyte(x[j]);
@@ -1169,16 +1191,24 @@ __device__ __forceinline__ int32_t roll_add(int32_t cs, int32_t x) {  // Rolling
     return (int32_t)((lo & 0xFFFFu) | (hi << 16));
 }
 
-__device__ __forceinline__ void load16(const uint8_t* __restrict__ x, int64_t n, int64_t p, uint8_t (&v)[16]) {
-    if (p + 16 <= n && ((reinterpret_cast<uintptr_t>(x + p) & 15) == 0)) {
+// 16 bytes at p (zero outside [0, n)) as 4 little-endian words: bytes stay packed in 4 VGPRs
+__device__ __forceinline__ void load16(const uint8_t* __restrict__ x, int64_t n, int64_t p, uint32_t (&w)[4]) {
+    if (p >= 0 && p + 16 <= n && ((reinterpret_cast<uintptr_t>(x + p) & 15) == 0)) {
         const uint4 q = *reinterpret_cast<const uint4*>(x + p);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+        w[0] = q.x;
+        w[1] = q.y;
+        w[2] = q.z;
+        w[3] = q.w;
     } else {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = (p + i < n && p + i >= 0) ? x[p + i] : (uint8_t)0;
+        for (int k = 0; k < 4; ++k) w[k] = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (p + i < n && p + i >= 0) w[i >> 2] |= (uint32_t)x[p + i] << (8 * (i & 3));
     }
+}
+__device__ __forceinline__ int32_t sbyte_of(const uint32_t (&w)[4], int i) {
+    return (int32_t)(int8_t)(uint8_t)(w[i >> 2] >> (8 * (i & 3)));
 }
 
 __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A) {
@@ -1194,22 +1224,30 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A)
     if (qend > o + B) qend = o + B;
     if (q0 >= I.b || qend <= I.a || q0 >= n) return;  // uniform over the workgroup
 
-    // prefix of both streams from the block origin up to the tile
+    // prefix of both streams from the block origin up to the tile: the partial sums of the tiles before it
     int32_t head[4] = {0, 0, 0, 0};
-    range_sums(A.data, n, o, q0, o, head[0], head[1]);
-    range_sums(A.data, n, o + B, q0 + B, o, head[2], head[3]);
-    block_reduce<4>(head, sh);
+    const int ti = (int)((q0 - o) / PROBE_TILE);
+    if (ti > 0) {
+        if (threadIdx.x < ti) {
+            const int4 v = A.partials[tile.pbase + threadIdx.x];
+            head[0] = v.x;
+            head[1] = v.y;
+            head[2] = v.z;
+            head[3] = v.w;
+        }
+        block_reduce<4>(head, sh);
+    }
 
     const int t = threadIdx.x;
     const int64_t p0 = q0 + (int64_t)t * PROBE_PPT;
-    uint8_t xa[16], xb[16];
+    uint32_t xa[4], xb[4];
     load16(A.data, n, p0, xa);
     load16(A.data, n, p0 + B, xb);
     int32_t part[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        const int32_t va = (p0 + i < n) ? sbyte(xa[i]) : 0;
-        const int32_t vb = (p0 + B + i < n) ? sbyte(xb[i]) : 0;
+        const int32_t va = (p0 + i < n) ? sbyte_of(xa, i) : 0;
+        const int32_t vb = (p0 + B + i < n) ? sbyte_of(xb, i) : 0;
         part[0] += va;
         part[1] += (int32_t)((uint32_t)(p0 + i - o) * (uint32_t)va);
         part[2] += vb;
@@ -1233,18 +1271,145 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A)
     auto clampB = [&](int64_t p) { return p < nb ? p : nb; };
     const uint32_t ehi = I.e_hi + I.e_lo * (uint32_t)(clampB(p0) - clampB(I.anchor));
     int32_t R = (int32_t)(((s1 + I.e_lo) & 0xFFFFu) | ((s2 + ehi) << 16));
+    // keys of all 16 positions first (ALU only), then their first hash slots in one burst of independent
+    // loads: a hit/miss is decided by the first slot for most keys (load factor <= 1/2), so a lane waits
+    // for about one L2 round trip instead of 16 serial ones
+    uint32_t key[PROBE_PPT];
+#pragma unroll
+    for (int i = 0; i < PROBE_PPT; ++i) {
+        key[i] = (uint32_t)R;
+        const int64_t p = p0 + i;
+        const int64_t w = (n - p < B ? n - p : B);
+        R = roll_sub(R, (int32_t)w, sbyte_of(xa, i));
+        if (n - (p + 1) >= B) R = roll_add(R, sbyte_of(xb, i));
+    }
+    unsigned long long sl[PROBE_PPT];
+#pragma unroll
+    for (int i = 0; i < PROBE_PPT; ++i) sl[i] = A.table.slots[slot_hash(key[i]) & A.table.mask];
 #pragma unroll
     for (int i = 0; i < PROBE_PPT; ++i) {
         const int64_t p = p0 + i;
         if (p >= I.b || p >= qend) break;
-        if (p >= I.a && table_has(A.table, (uint32_t)R)) {
+        if (p < I.a) continue;
+        const unsigned long long v = (1ull << 32) | key[i];
+        bool hit = sl[i] == v;
+        if (!hit && sl[i] != 0ull) hit = table_has(A.table, key[i]);
+        if (hit) {
             atomicMin(A.first, (unsigned long long)p);
             return;
         }
-        const int64_t w = (n - p < B ? n - p : B);
-        R = roll_sub(R, (int32_t)w, sbyte(xa[i]));
-        if (n - (p + 1) >= B) R = roll_add(R, sbyte(xb[i]));
     }
+}
+
+// Pass 1: one workgroup per partial tile [q0, min(q0 + PROBE_TILE, o + B)), o = its block start.
+__global__ __launch_bounds__(256) void probe_partials_kernel(const uint8_t* __restrict__ data, int64_t n, uint32_t B,
+                                                             const PartialTile* __restrict__ pt,
+                                                             int4* __restrict__ out) {
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ int32_t sh[4 * 256 / 64];
+    const int64_t q0 = pt[blockIdx.x].q0;
+    const int64_t o = q0 / B * B;
+    const int64_t qe = q0 + PROBE_TILE < o + B ? q0 + PROBE_TILE : o + B;
+    int32_t v[4] = {0, 0, 0, 0};
+    range_sums(data, n, q0, qe, o, v[0], v[1]);
+    range_sums(data, n, q0 + B, qe + B, o, v[2], v[3]);
+    block_reduce<4>(v, sh);
+    if (threadIdx.x == 0) out[blockIdx.x] = make_int4(v[0], v[1], v[2], v[3]);
+}
+
+void probe_partials(std::vector<ProbeTile>* tiles, int64_t B, std::vector<PartialTile>* out) {
+    out->clear();
+    int64_t cur_block = -1, covered = 0;  // tiles of cur_block already listed: [0, covered)
+    int32_t base = 0;
+    for (ProbeTile& t : *tiles) {
+        const int64_t k = t.q0 / B;
+        const int64_t ti = (t.q0 - k * B) / PROBE_TILE;
+        if (k != cur_block) {  // tiles arrive in increasing position order
+            cur_block = k;
+            covered = 0;
+            base = (int32_t)out->size();
+        }
+        for (; covered < ti; ++covered) out->push_back(PartialTile{k * B + covered * PROBE_TILE});
+        t.pbase = base;
+    }
+}
+
+__global__ __launch_bounds__(256) void hit_window_kernel(const uint8_t* __restrict__ data, int64_t n, uint32_t B,
+                                                         const unsigned long long* __restrict__ first,
+                                                         const ProbeIv* __restrict__ ivs, int32_t niv,
+                                                         int32_t* __restrict__ d_bucket, int32_t* __restrict__ h_weak,
+                                                         uint8_t* __restrict__ h_win) {
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ int32_t sh[2 * 256 / 64];
+    const unsigned long long f = *first;
+    if (f == ~0ull) return;
+    const int64_t p = (int64_t)f;
+    const int64_t w = (n - p < (int64_t)B ? n - p : (int64_t)B);
+    if (blockIdx.x == 0) {
+        int32_t v[2] = {0, 0};
+        range_sums(data, n, p, p + w, p, v[0], v[1]);
+        block_reduce<2>(v, sh);
+        if (threadIdx.x == 0) {
+            const uint32_t S1 = (uint32_t)v[0];
+            const uint32_t S2 = (uint32_t)w * S1 - (uint32_t)v[1];
+            const int32_t T = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
+            *h_weak = T;
+            // the interval holding p (disjoint, ascending) gives E(p); R = T + E is the key that hit
+            int32_t lo = 0, hi = niv - 1;
+            while (lo < hi) {
+                const int32_t mid = (lo + hi + 1) / 2;
+                if (ivs[mid].a <= p) lo = mid;
+                else hi = mid - 1;
+            }
+            const ProbeIv I = ivs[lo];
+            const int64_t nb = n - B;
+            const int64_t cp = p < nb ? p : nb, ca = I.anchor < nb ? I.anchor : nb;
+            const uint32_t ehi = I.e_hi + I.e_lo * (uint32_t)(cp - ca);
+            d_bucket[0] = 0;
+            d_bucket[1] = (int32_t)((((uint32_t)T + I.e_lo) & 0xFFFFu) | ((((uint32_t)T >> 16) + ehi) << 16));
+        }
+        return;
+    }
+    for (int64_t o = 16 * ((int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x); o < w;
+         o += 16 * (int64_t)(gridDim.x - 1) * blockDim.x) {
+        if (o + 16 <= w) {
+            uint32_t q[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < 16; ++i) q[i >> 2] |= (uint32_t)data[p + o + i] << (8 * (i & 3));
+            *reinterpret_cast<uint4*>(h_win + o) = make_uint4(q[0], q[1], q[2], q[3]);
+        } else {
+            for (int64_t i = o; i < w; ++i) h_win[i] = data[p + i];
+        }
+    }
+}
+
+// The bucket of the hit key: chunk indices i with weak[i] == key (8 per lane).
+__global__ __launch_bounds__(256) void hit_bucket_kernel(const unsigned long long* __restrict__ first,
+                                                         const int32_t* __restrict__ weak, int32_t C,
+                                                         int32_t* __restrict__ d_bucket) {
+    __builtin_amdgcn_s_setprio(3);
+    if (*first == ~0ull) return;
+    const int32_t key = d_bucket[1];
+    const int32_t i0 = 8 * (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int32_t i = i0 + k;
+        if (i < C && weak[i] == key) {
+            const int32_t at = atomicAdd(&d_bucket[0], 1);
+            if (at < HIT_BUCKET_CAP) d_bucket[2 + at] = i;
+        }
+    }
+}
+
+hipError_t launch_hit_window(const uint8_t* d_data, int64_t n, uint32_t B, const unsigned long long* d_first,
+                             const ProbeIv* ivs, int32_t niv, const int32_t* d_table_weak, int32_t C,
+                             int32_t* d_bucket, int32_t* h_weak, uint8_t* h_win, hipStream_t s) {
+    hipLaunchKernelGGL(hit_window_kernel, dim3(1 + 16), dim3(256), 0, s, d_data, n, B, d_first, ivs, niv, d_bucket,
+                       h_weak, h_win);
+    if (C > 0)
+        hipLaunchKernelGGL(hit_bucket_kernel, dim3((uint32_t)((C + 8 * 256 - 1) / (8 * 256))), dim3(256), 0, s, d_first,
+                           d_table_weak, C, d_bucket);
+    return hipGetLastError();
 }
 
 void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeTile>* out) {
@@ -1254,12 +1419,16 @@ void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeT
         const int64_t lo = a > o ? a : o;
         const int64_t hi = b < o + B ? b : o + B;
         for (int64_t t = (lo - o) / PROBE_TILE; t <= (hi - 1 - o) / PROBE_TILE; ++t)
-            out->push_back(ProbeTile{o + t * PROBE_TILE, iv, 0});
+            out->push_back(ProbeTile{o + t * PROBE_TILE, iv, -1});
     }
 }
 
-hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, hipStream_t s) {
+hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const PartialTile* d_ptiles, uint32_t nptiles,
+                              int4* d_partials, hipStream_t s) {
     if (ntiles == 0) return hipSuccess;
+    if (nptiles > 0)
+        hipLaunchKernelGGL(probe_partials_kernel, dim3(nptiles), dim3(256), 0, s, args.data, args.n, args.B, d_ptiles,
+                           d_partials);
     hipLaunchKernelGGL(probe_first_kernel, dim3(ntiles), dim3(PROBE_THREADS), 0, s, args);
     return hipGetLastError();
 }

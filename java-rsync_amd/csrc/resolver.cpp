@@ -3,6 +3,8 @@
 // io/FileView.java:143-185,235-278 (window, mark, isFull), util/Rolling.java:25-60 (add/subtract).
 #include "resolver.h"
 
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -12,7 +14,24 @@
 
 namespace rsh {
 
+namespace {
+// RSH_SCAN_TRACE=1: one stderr line per host-side table operation (diagnostics)
+struct HostTrace {
+    const char* what;
+    int64_t arg;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    HostTrace(const char* w, int64_t a) : what(w), arg(a) {}
+    ~HostTrace() {
+        static const bool on = getenv("RSH_SCAN_TRACE") != nullptr;
+        if (on)
+            fprintf(stderr, "[rsh] %-10s %10lld %9.3f ms\n", what, (long long)arg,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+}  // namespace
+
 void ChunkTable::build() {
+    HostTrace tr("tab_sort", chunk_count);
     if (sorted_) return;
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<uint32_t>& sorted_key = sorted_key_;
@@ -61,6 +80,11 @@ void ChunkTable::build() {
 }
 
 const int32_t* ChunkTable::bucket(int32_t key, int32_t* size) {
+    if (primed_valid_ && key == primed_key_) {
+        *size = (int32_t)primed_.size();
+        return primed_.data();
+    }
+    HostTrace tr("bucket", key);
     if (!sorted_ && scan_lookups_ >= kScanLookups) build();
     if (sorted_) {
         const uint32_t k = (uint32_t)key;
@@ -83,6 +107,7 @@ const int32_t* ChunkTable::bucket(int32_t key, int32_t* size) {
 }
 
 void ChunkTable::keys_with_digest(const uint8_t* d, std::vector<int32_t>* keys) const {
+    HostTrace tr("dkeys", chunk_count);
     keys->clear();
     const int64_t dl = digest_length;
     if (dl == 0) {  // every chunk carries the empty digest

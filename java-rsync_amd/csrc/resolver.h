@@ -46,8 +46,18 @@ struct ChunkTable {
     void keys_with_digest(const uint8_t* d, std::vector<int32_t>* keys) const;
 
     static constexpr int kScanLookups = 16;
+    // The bucket of `key` computed elsewhere (the device, in the round trip that found a probe hit):
+    // idx ascending.  The next bucket(key) returns it without touching the table.
+    void prime(int32_t key, const int32_t* idx, int32_t count) {
+        primed_key_ = key;
+        primed_.assign(idx, idx + count);
+        primed_valid_ = true;
+    }
 
   private:
+    bool primed_valid_ = false;
+    int32_t primed_key_ = 0;
+    std::vector<int32_t> primed_;
     bool sorted_ = false;
     int scan_lookups_ = 0;
     std::vector<uint32_t> sorted_key_;  // bucket keys, sorted (stable: ascending chunk index per key)
