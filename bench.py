@@ -32,7 +32,7 @@ import shard  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 # production K1 instantiation (device.hip launch_block_sums_variant default); the committed PMC profile
 # for `traffic` is matched on this name so a stale profile of another kernel is never reported
-PROD_KERNEL = "block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false>"
+PROD_KERNEL = "block_sums_pipe_kernel<8, false, true, 0>"
 KEY_SRC = 0x5EED5EED << 32
 KEY_EDIT = (0x5EED5EED << 32) | 0xED17
 
@@ -166,8 +166,8 @@ def main():
         "dtype": "u8",
         "data": "synthetic (splitmix64 on device)",
         "config": {
-            "workload": f"config5: {a.size_gib:g} GiB source vs {'50%-modified' if a.variant == 'half' else 'identical'}"
-                        f" basis per GPU, B={B}, dl={dl}",
+            "workload": f"{cfg_name(n, B)}: {a.size_gib:g} GiB source vs "
+                        f"{'50%-modified' if a.variant == 'half' else 'identical'} basis per GPU, B={B}, dl={dl}",
             "bytes_per_step_per_gpu": bytes_step,
             "block_length": B,
             "digest_length": dl,
@@ -175,7 +175,7 @@ def main():
             "parallelism": f"file-sharded x{world} (no collectives)",
         },
         "roofline": {
-            "kernel": "block_sums_coalesced_kernel (Generator; also the Sender's aligned speculation)",
+            "kernel": "block_sums_pipe_kernel (K1: Generator; also the Sender's aligned speculation)",
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
@@ -311,6 +311,13 @@ def main_files(a):
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def cfg_name(n, B):
+    """BASELINE.json config the single-pair workload corresponds to (config 3 runs its scan at B = 2^17,
+    the Sender's maximum, since the reference rejects its rule's B = 2^18: Checksum.java:81-82)."""
+    return {(16 << 30, 131072): "config5", (4 << 30, 65536): "config2",
+            (64 << 30, 131072): "config3"}.get((n, B), "custom")
 
 
 def pmc_traffic(path, kernel_substr, n):

@@ -1,0 +1,184 @@
+"""Parity at BASELINE.json's full sizes (config 2: 4 GiB, B = 65536; config 5: 16 GiB, B = 131072).
+
+The oracle cannot replay a 4-16 GiB Sender scan within a test's time limit (it walks every byte, ~0.05 GiB/s),
+so the full-size checks are the size-independent properties of the path:
+
+  * Generator (Generator.java:886-895): every chunk's weak and strong sum bit-exact against the oracle, which
+    runs over chunk-aligned slices of the same basis on a thread pool (chunks are independent).
+  * Sender (Sender.java:1235-1327): the event list is a delta that reconstructs the source (the Receiver's
+    decode): events tile [0, n) in order, every MATCH run's bytes equal the basis chunks it names, and
+    literal + matched == n (Sender.java:1325).  Where the reference's outcome is structurally known it is
+    asserted exactly: an identical basis is one MATCH run over all chunks; a file whose first k blocks are
+    unchanged starts with MATCH(0 .. k-1), since after each match the scan jumps a whole window and never
+    rolls through a position where a false weak hit could occur (Sender.java:1282-1287).
+
+Inputs are splitmix64 bytes generated on the device (the same generator the oracle restates)."""
+import concurrent.futures as cf
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+import rsync_hip as R
+
+pytestmark = pytest.mark.gpu
+SEED = bytes([1, 2, 3, 4])
+SEED_NP = np.frombuffer(SEED, np.uint8).copy()
+KEY = 0x5EED5EED00000000
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+    R.build()
+    torch.cuda.set_device(0)
+    c = R.Context(0)
+    yield c, torch
+    c.close()
+    torch.cuda.empty_cache()
+
+
+def _fill(ctx, t, key, offset=0):
+    assert R.lib().rsh_fill_splitmix_device(ctx.handle, t.data_ptr(), t.numel(), key, offset) == 0
+
+
+def _block_sums(ctx, torch, basis, h):
+    C, dl = h.chunk_count, h.digest_length
+    d_w = torch.empty(max(C, 1), dtype=torch.int32, device="cuda")
+    d_s = torch.empty(max(C * dl, 1), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    assert R.lib().rsh_block_sums_device(ctx.handle, ctypes.c_void_p(basis.data_ptr()), basis.numel(),
+                                         ctypes.byref(h), SEED_NP.ctypes.data, ctypes.c_void_p(d_w.data_ptr()),
+                                         ctypes.c_void_p(d_s.data_ptr())) == 0
+    ctx.sync()
+    return d_w, d_s
+
+
+def _oracle_generator_threaded(host_basis, B, dl, workers=16):
+    """The oracle over chunk-aligned slices of the basis, in parallel (ctypes releases the GIL)."""
+    n = host_basis.size
+    C = (n + B - 1) // B
+    per = (C + workers - 1) // workers
+    parts = [(k * per, min(C, (k + 1) * per)) for k in range(workers) if k * per < C]
+
+    def run(p):
+        a, b = p
+        sl = host_basis[a * B:min(n, b * B)]
+        return O.generator(sl, O.header(B, dl, sl.size), SEED)
+
+    with cf.ThreadPoolExecutor(len(parts)) as ex:
+        res = list(ex.map(run, parts))
+    return np.concatenate([w for w, _ in res]), np.concatenate([s for _, s in res])
+
+
+def _scan(ctx, torch, src, h, d_w, d_s):
+    n = src.numel()
+    cap = h.chunk_count + n // max(h.block_length, 1) + 4096
+    ev = np.zeros(cap, R.EVENT_DTYPE)
+    n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    st = R.ScanStats()
+    torch.cuda.synchronize()
+    rc = R.lib().rsh_match_scan_device(ctx.handle, ctypes.c_void_p(src.data_ptr()), n, ctypes.byref(h),
+                                       ctypes.c_void_p(d_w.data_ptr()), ctypes.c_void_p(d_s.data_ptr()),
+                                       SEED_NP.ctypes.data, ev.ctypes.data, cap, ctypes.byref(n_ev),
+                                       ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(st))
+    assert rc == 0, R.lib().rsh_last_error()
+    return ev[:n_ev.value], lit.value, mat.value, st.as_dict()
+
+
+def _check_delta(torch, ev, src, basis, h, lit, mat):
+    """The event list decodes back to the source: contiguous tiling, MATCH bytes == basis chunk bytes."""
+    n, B, C = src.numel(), h.block_length, h.chunk_count
+    pos = tot_lit = tot_mat = 0
+    for e in ev:
+        off, ln = int(e["offset"]), int(e["length"])
+        assert off == pos, f"gap/overlap at {pos}: event starts at {off}"
+        if e["kind"] == R.EV_LITERAL:
+            tot_lit += ln
+        else:
+            i, cnt = int(e["index"]), int(e["count"])
+            assert 0 <= i and i + cnt <= C and cnt >= 1
+            # every window of a run but the last is a full block; the last has chunk i+cnt-1's length
+            last_len = h.remainder if (i + cnt == C and h.remainder) else B
+            assert ln == (cnt - 1) * B + last_len
+            assert torch.equal(src[off:off + ln], basis[i * B:i * B + ln]), f"MATCH run {i}+{cnt} at {off}"
+            tot_mat += ln
+        pos = off + ln
+    assert pos == n
+    assert (tot_lit, tot_mat) == (lit, mat) and lit + mat == n
+
+
+def _gen_parity(ctx, torch, basis, B, dl):
+    h = R.header_make(B, dl, basis.numel())
+    d_w, d_s = _block_sums(ctx, torch, basis, h)
+    ow, os_ = _oracle_generator_threaded(basis.cpu().numpy(), B, dl)
+    assert np.array_equal(d_w.cpu().numpy(), ow)
+    assert np.array_equal(d_s.cpu().numpy(), os_)
+    return h, d_w, d_s
+
+
+def test_config2_4GiB_generator_and_scans(env):
+    """Config 2: 4 GiB, B = 65536 (the README rule), dl = 4."""
+    ctx, torch = env
+    n = 4 << 30
+    B = R.block_length_for(n)
+    dl = R.digest_length_for(n, B)
+    assert (B, dl) == (65536, 4)
+    basis = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _fill(ctx, basis, KEY ^ 2)
+    ctx.sync()
+    h, d_w, d_s = _gen_parity(ctx, torch, basis, B, dl)
+
+    # identical source: one MATCH run over every chunk, no literal
+    ev, lit, mat, _ = _scan(ctx, torch, basis, h, d_w, d_s)
+    assert len(ev) == 1 and ev[0]["kind"] == R.EV_MATCH and ev[0]["index"] == 0 and ev[0]["count"] == h.chunk_count
+    _check_delta(torch, ev, basis, basis, h, lit, mat)
+
+    # 1 GiB unchanged, 1000 inserted bytes, a rewritten block at 3 GiB, a 33-byte tail
+    k = (1 << 30) // B
+    ins = torch.empty(1000, dtype=torch.uint8, device="cuda")
+    _fill(ctx, ins, KEY ^ 0x1A5)
+    tail = torch.empty(33, dtype=torch.uint8, device="cuda")
+    _fill(ctx, tail, KEY ^ 0x7A1)
+    ctx.sync()
+    src = torch.cat([basis[:k * B], ins, basis[k * B:], tail])
+    blk = 3 * (1 << 30) // B
+    src[blk * B + 500:(blk + 1) * B + 500] = src[blk * B + 500:(blk + 1) * B + 500].flip(0)
+    ev, lit, mat, st = _scan(ctx, torch, src, h, d_w, d_s)
+    assert ev[0]["kind"] == R.EV_MATCH and ev[0]["index"] == 0 and ev[0]["count"] >= k
+    _check_delta(torch, ev, src, basis, h, lit, mat)
+    del src
+
+
+@pytest.mark.parametrize("variant", ["identical", "half"])
+def test_config5_16GiB(env, variant):
+    """Config 5: 16 GiB, B = 131072 (= the Sender's maximum), dl = 4; the bench's exact workload."""
+    ctx, torch = env
+    n = 16 << 30
+    B, dl = 131072, 4
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _fill(ctx, src, KEY ^ 5)
+    ctx.sync()
+    if variant == "identical":
+        basis = src
+    else:  # every other block of the basis replaced (bench.py's "50%-modified basis")
+        basis = src.clone()
+        other = torch.empty(n, dtype=torch.uint8, device="cuda")
+        _fill(ctx, other, KEY ^ 0xED17)
+        ctx.sync()
+        basis.view(-1, B)[1::2] = other.view(-1, B)[1::2]
+        del other
+    torch.cuda.synchronize()
+    if variant == "half":
+        h, d_w, d_s = _gen_parity(ctx, torch, basis, B, dl)
+    else:
+        h = R.header_make(B, dl, n)
+        d_w, d_s = _block_sums(ctx, torch, basis, h)
+    ev, lit, mat, st = _scan(ctx, torch, src, h, d_w, d_s)
+    assert ev[0]["kind"] == R.EV_MATCH and ev[0]["index"] == 0
+    if variant == "identical":
+        assert len(ev) == 1 and ev[0]["count"] == h.chunk_count and lit == 0
+    _check_delta(torch, ev, src, basis, h, lit, mat)
+    del src, basis
+    torch.cuda.empty_cache()
