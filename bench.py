@@ -50,7 +50,10 @@ def parse():
                     help="file: config 5 (one 16 GiB pair per GPU); files: config 4 (many 128 MiB pairs per GPU)")
     ap.add_argument("--files", type=int, default=128, help="files per GPU for --workload files")
     ap.add_argument("--file-mib", type=int, default=128)
-    ap.add_argument("--threads", type=int, default=8, help="Sender scan contexts per GPU (--workload files)")
+    ap.add_argument("--threads", type=int, default=8, help="Sender scan contexts per GPU (--files-api single)")
+    ap.add_argument("--files-api", choices=["batch", "single"], default="batch",
+                    help="files workload: the batched entry points (one K1 launch per segment, one round trip "
+                         "per round for all files) or one rsh_match_scan_device per file on a context pool")
     ap.add_argument("--cpu-sample-mib", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -268,7 +271,7 @@ def main_files(a):
 
     ex = cf.ThreadPoolExecutor(max_workers=a.threads)
 
-    def step():
+    def step_single():
         rc = L.rsh_block_sums_device(ctx.handle, ctypes.c_void_p(basis.data_ptr()), n, ctypes.byref(hall),
                                      seed.ctypes.data, ctypes.c_void_p(d_weak.data_ptr()),
                                      ctypes.c_void_p(d_strong.data_ptr()))
@@ -276,6 +279,35 @@ def main_files(a):
         ctx.sync()  # tables ready before the scans (other streams)
         futs = [ex.submit(scan, i) for i in range(F)]
         return sum(f.result() for f in futs)
+
+    # batched: F basis files -> one rsh_block_sums_batch_device; F sources -> one rsh_match_scan_batch_device
+    bjobs = (R.BlockJob * F)()
+    sjobs = (R.ScanJob * F)()
+    evbufs = [np.zeros(caps, R.EVENT_DTYPE) for _ in range(F)]
+    for i in range(F):
+        bjobs[i].d_data = basis.data_ptr() + i * S
+        bjobs[i].n = S
+        bjobs[i].h = h1
+        bjobs[i].d_weak = d_weak.data_ptr() + 4 * i * C1
+        bjobs[i].d_strong = d_strong.data_ptr() + i * C1 * dl
+        sjobs[i].d_src = src.data_ptr() + i * S
+        sjobs[i].n = S
+        sjobs[i].h = h1
+        sjobs[i].d_weak = bjobs[i].d_weak
+        sjobs[i].d_strong = bjobs[i].d_strong
+        sjobs[i].ev = evbufs[i].ctypes.data
+        sjobs[i].ev_cap = caps
+    bst = R.ScanStats()
+
+    def step_batch():
+        assert L.rsh_block_sums_batch_device(ctx.handle, bjobs, F, seed.ctypes.data) == 0
+        rc = L.rsh_match_scan_batch_device(ctx.handle, sjobs, F, seed.ctypes.data, ctypes.byref(bst))
+        assert rc == 0, (rc, L.rsh_last_error().decode())
+        for i in range(F):
+            assert sjobs[i].literal + sjobs[i].matched == S
+        return sum(sjobs[i].matched for i in range(F))
+
+    step = step_batch if a.files_api == "batch" else step_single
 
     for _ in range(a.warmup):
         step()
@@ -300,8 +332,10 @@ def main_files(a):
         "config": {"workload": f"config4: {F} files x {a.file_mib} MiB per GPU "
                                f"({'50%-modified' if a.variant == 'half' else 'identical'} bases), B={B}, dl={dl}",
                    "bytes_per_step_per_gpu": 2 * n, "files_per_gpu": F, "block_length": B, "digest_length": dl,
-                   "parallelism": f"file-sharded x{world} (no collectives), {a.threads} scan contexts per GPU"},
-        "scan": {"matched_bytes_per_step_per_gpu": int(matched)},
+                   "parallelism": f"file-sharded x{world} (no collectives), " + (
+                       "batched entry points" if a.files_api == "batch" else f"{a.threads} scan contexts per GPU")},
+        "scan": {"matched_bytes_per_step_per_gpu": int(matched),
+                 "stats": bst.as_dict() if a.files_api == "batch" else None},
     }
     if rank == 0:
         print(json.dumps(res), flush=True)

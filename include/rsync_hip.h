@@ -138,6 +138,42 @@ int rsh_tokens_write(const uint8_t* src, const rsh_event* ev, int64_t n_ev, cons
 int64_t rsh_generator_bytes(const rsh_header* h, const int32_t* weak, const uint8_t* strong, uint8_t* out,
                             int64_t cap);
 
+/* ---- batched files (one segment of the file list) ----
+ * The reference handles a segment's files one after another: the Generator sends every file's header +
+ * table (Generator.java:558-614, sendItemizeAndChecksums :866-909 per file) and the Sender answers each in
+ * turn (Sender.sendFiles :1098-1148 -> sendMatchesAndData :1235-1327).  The batched forms take all the
+ * files of a segment at once, so their kernels fill the device: one K1 launch for every file's block
+ * sums, and one resolver per file whose device round trips are gathered into one launch per round.
+ * Results are per file and identical to the single-file calls.  All pointers in a job are device
+ * pointers except ev (host).  Returns RSH_OK, or the first failing job's status (every job's own status
+ * is in its `status`). */
+typedef struct {
+    const void* d_data;  /* the basis file */
+    int64_t n;
+    rsh_header h;        /* as for rsh_block_sums (3-arg Checksum.Header semantics) */
+    void* d_weak;        /* out: chunk_count weak sums */
+    void* d_strong;      /* out: chunk_count * digest_length digest bytes */
+} rsh_block_job;
+int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t njobs, const uint8_t seed[4]);
+
+typedef struct {
+    const void* d_src;     /* the source file */
+    int64_t n;
+    rsh_header h;          /* the received header (validated as by rsh_match_scan) */
+    const void* d_weak;    /* the received table */
+    const void* d_strong;
+    rsh_event* ev;         /* host, caller-owned: ev_cap entries */
+    int64_t ev_cap;
+    int64_t n_ev;          /* out: event count (RSH_E_NOSPACE in status if > ev_cap; events then lost) */
+    int64_t literal;       /* out */
+    int64_t matched;       /* out */
+    int32_t status;        /* out: RSH_OK or an error code for this file */
+    int32_t reserved;
+} rsh_scan_job;
+/* stats (optional): summed over the files (device_ms / resolver_ms: wall time of the whole batch). */
+int rsh_match_scan_batch_device(rsh_ctx* ctx, rsh_scan_job* jobs, int32_t njobs, const uint8_t seed[4],
+                                rsh_scan_stats* stats);
+
 /* ---- device buffers for the *_device entry points (callers without their own allocator, e.g. JNI) ---- */
 int rsh_dev_alloc(rsh_ctx* ctx, int64_t bytes, void** out);
 int rsh_dev_free(rsh_ctx* ctx, void* p);

@@ -1,0 +1,921 @@
+// batch.cpp -- the batched (multi-file) entry points of include/rsync_hip.h.
+//
+// Generator side: every file of a segment in one K1 launch (Generator.java:558-614 calls
+// sendItemizeAndChecksums :866-909 once per file; here the per-chunk work of all of them is one grid).
+//
+// Sender side (Sender.sendFiles :1098-1148 -> sendMatchesAndData :1235-1327 per file): one resolver per
+// file, each on its own host thread, exactly the single-file resolver (resolver.cpp).  A resolver's
+// device questions (a range probe, weak sums or bytes at a few positions, a digest window) are posted to
+// the batch and the thread blocks; once every live resolver is blocked or finished, the coordinator (the
+// calling thread) answers all of them with one launch per kind and one stream synchronisation -- one
+// round trip per round for the whole segment instead of one per question per file.  The aligned
+// speculation (the sources' own block sums) is one batched K1 launch, deferred like the single-file
+// scan's and cancelled when every resolver finishes first.
+#include <sched.h>
+#include <ucontext.h>
+
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+
+#include "ctx.h"
+#include "host_md5.h"
+#include "resolver.h"
+
+namespace rsh {
+
+namespace {
+constexpr int32_t kMaxLive = 256;     // files resolved concurrently (one host thread each)
+constexpr int kDeferRounds = 2;       // rounds in head mode before the speculation is launched
+constexpr int32_t kMaxWorkers = 32;   // host threads running the resolvers
+constexpr size_t kFiberStack = 512 * 1024;
+constexpr int64_t kPad = 16;
+
+int64_t pad16(int64_t v) { return (v + kPad - 1) / kPad * kPad; }
+}  // namespace
+
+struct BatchState {
+    // Generator batch
+    DevBuf g_groups, g_lanes;
+    // Sender batch: device
+    DevBuf slots, dslots, src_weak, src_strong, flags, haw, partials, bucket, first, k1_groups, k1_lanes;
+    // Sender batch: pinned host (read or written by the kernels directly)
+    PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl, h_files, h_hit, h_win0, h_bucket, h_first, h_iv, h_tiles,
+        h_ptiles, h_req, h_gw, h_gb, h_ow, h_ob, h_win, h_copies, h_tabents, h_flagents, h_dkeys, h_ccopies;
+    ~BatchState() {
+        for (DevBuf* b : {&g_groups, &g_lanes, &slots, &dslots, &src_weak, &src_strong, &flags, &haw, &partials, &bucket,
+                          &first, &k1_groups, &k1_lanes})
+            b->release();
+        for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_files, &h_hit, &h_win0, &h_bucket, &h_first,
+                             &h_iv, &h_tiles, &h_ptiles, &h_req, &h_gw, &h_gb, &h_ow, &h_ob, &h_win, &h_copies,
+                             &h_tabents, &h_flagents, &h_dkeys, &h_ccopies})
+            b->release();
+    }
+};
+
+void destroy_batch_state(BatchState* b) { delete b; }
+
+namespace {
+
+BatchState* state_of(rsh_ctx* c) {
+    if (!c->batch) c->batch = new (std::nothrow) BatchState();
+    return c->batch;
+}
+
+template <class T>
+hipError_t pin(PinnedBuf& b, int64_t count, T** out) {
+    const hipError_t e = b.ensure((size_t)std::max<int64_t>(count, 1) * sizeof(T));
+    *out = b.as<T>();
+    return e;
+}
+
+#define RSH_BHIP(call)                                  \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) {                         \
+            note_error(e_, __LINE__, "batch.cpp");      \
+            return RSH_E_DEVICE;                        \
+        }                                               \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// Sender batch
+// ------------------------------------------------------------------------------------------------
+struct Req {
+    enum Kind { WEAK, BYTES, WIN, PROBE } kind = WEAK;
+    const int64_t* pos = nullptr;  // WEAK / BYTES
+    int64_t count = 0;
+    int32_t* out_w = nullptr;
+    uint8_t* out_b = nullptr;
+    int64_t p = 0, w = 0;          // WIN: window [p, p + w) lands at win
+    const uint8_t* win = nullptr;
+    const ProbeInterval* iv = nullptr;  // PROBE
+    int64_t niv = 0;
+    const std::vector<int32_t>* keys = nullptr;
+    bool head = false;
+    int64_t result = -1;
+    const ProbeOut* out = nullptr;  // the probe's full answer (pinned), for the hit cache
+};
+
+struct Batch;
+
+class BatchBackend : public ScanBackend {
+  public:
+    Batch* b = nullptr;
+    int32_t f = 0;
+    bool head = true;
+    int64_t na = 0;
+    const int32_t* aw = nullptr;
+    const uint8_t* as = nullptr;
+    const uint8_t* fl = nullptr;
+    const uint8_t* win0 = nullptr;  // window 0 (pinned), w0 bytes
+    int64_t w0 = 0;
+    const uint8_t* hit = nullptr;   // this file's hit buffer (pinned): T(p), then the window at p
+    const int32_t* bucket = nullptr;
+    int64_t n = 0, B = 0;
+    uint8_t seed[4];
+    ChunkTable* table = nullptr;
+    std::vector<uint8_t> haw_ready;
+    int64_t win_pos = -1;  // the last probe's first hit: its window is in `hit`
+    int64_t t_pos = -1;    // the last hit returned: its weak sum t_val is known
+    int32_t t_val = 0;
+    HitCache cache;
+
+    int64_t aligned_count() override { return head ? 0 : na; }
+    int64_t max_batch() override { return head ? 4 : 4096; }
+    const int32_t* aligned_weak() override { return aw; }
+    const uint8_t* aligned_strong() override { return as; }
+    const uint8_t* chain_flags() override { return fl; }
+    void weak_many(const int64_t* pos, int64_t count, int32_t* out) override;
+    void bytes_many(const int64_t* pos, int64_t count, uint8_t* out) override;
+    void md5_at(int64_t p, uint8_t out[16]) override;
+    int64_t first_hit(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) override;
+};
+
+struct FileScan {
+    int32_t job = 0;
+    const uint8_t* d_src = nullptr;
+    const int32_t* d_weak = nullptr;
+    const uint8_t* d_strong = nullptr;
+    int64_t n = 0, B = 0, na = 0, nf = 0;
+    int32_t C = 0, dl = 0;
+    uint32_t ns = 0;
+    int64_t off_tw = 0, off_ts = 0, off_na = 0, off_as = 0, off_nf = 0, off_ns = 0, off_hit = 0, off_w0 = 0;
+    ChunkTable table;
+    ResolveState rs;
+    ResolveResult res;
+    BatchBackend be;
+    // rendezvous: the resolver runs as a fiber on one of the batch's worker threads
+    Req req;
+    bool pending = false;
+    bool done = false;
+    bool started = false;
+    int32_t worker = 0;
+    ucontext_t uc;
+    std::unique_ptr<char[]> stack;  // uninitialised: only the pages the fiber touches are committed
+};
+
+// Rounds: W worker threads (one per host core of the process, at most kMaxWorkers) each own a share of
+// the resolvers, run as fibers (ucontext): a resolver that needs the device posts its request and switches
+// back to its worker, which runs its next resolver.  When every worker has run all its resolvers up to
+// their next request (or their end), the coordinator serves the round and starts the next one.  No more
+// OS threads than cores, so a round's host work (digests of hit windows, bucket lookups) is not stretched
+// by the scheduler.
+struct Batch {
+    std::mutex mu;
+    std::condition_variable cv_coord, cv_work;
+    int32_t nworkers = 0, idle = 0;
+    uint64_t gen = 0;
+    bool quit = false;
+    std::atomic<bool> landed{false};
+    std::vector<FileScan>* files = nullptr;
+    std::vector<ucontext_t> worker_uc;
+    std::vector<double> busy_ms, max_fiber_ms;  // per worker, this round (trace)
+    std::vector<HostTimes> times;               // per worker, cumulative (trace)
+
+    // in a resolver fiber: hand the request to the coordinator, yield to the worker until it is answered
+    void post(FileScan& fs) {
+        fs.pending = true;
+        swapcontext(&fs.uc, &worker_uc[(size_t)fs.worker]);
+    }
+};
+
+FileScan& scan_of(Batch* b, int32_t f) { return (*b->files)[(size_t)f]; }
+
+// A resolver fiber: head mode until the batched speculation lands, then resume with it (resolve_run is
+// resumable); returning switches to uc_link (its worker).
+void fiber_main(uint32_t hi, uint32_t lo) {
+    FileScan& fs = *reinterpret_cast<FileScan*>(((uintptr_t)hi << 32) | lo);
+    BatchBackend& be = fs.be;
+    Batch& b = *be.b;
+    while (!resolve_run(fs.n, fs.table, be, &fs.rs, &fs.res,
+                        [&] { return be.head && b.landed.load(std::memory_order_acquire); }))
+        be.head = false;
+    fs.done = true;
+}
+
+void BatchBackend::weak_many(const int64_t* pos, int64_t count, int32_t* out) {
+    if (count <= 0) return;
+    if (count == 1 && pos[0] == t_pos) {  // came back with (or derived from) a probe result
+        out[0] = t_val;
+        return;
+    }
+    FileScan& fs = scan_of(b, f);
+    fs.req = Req{};
+    fs.req.kind = Req::WEAK;
+    fs.req.pos = pos;
+    fs.req.count = count;
+    fs.req.out_w = out;
+    b->post(fs);
+}
+
+void BatchBackend::bytes_many(const int64_t* pos, int64_t count, uint8_t* out) {
+    if (count <= 0) return;
+    FileScan& fs = scan_of(b, f);
+    fs.req = Req{};
+    fs.req.kind = Req::BYTES;
+    fs.req.pos = pos;
+    fs.req.count = count;
+    fs.req.out_b = out;
+    b->post(fs);
+}
+
+void BatchBackend::md5_at(int64_t p, uint8_t out[16]) {
+    const int64_t w = std::min<int64_t>(B, n - p);
+    const uint8_t* src = nullptr;
+    if (p == 0 && win0) src = win0;                 // copied to the host before the first round
+    else if (p == win_pos) src = hit + 16;          // came back with the probe result
+    else {
+        FileScan& fs = scan_of(b, f);
+        fs.req = Req{};
+        fs.req.kind = Req::WIN;
+        fs.req.p = p;
+        fs.req.w = w;
+        b->post(fs);
+        src = fs.req.win;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    HostMd5 h;  // one serial chain per window: on this file's host thread, beside the other files' work
+    h.update(src, (size_t)w);
+    h.update(seed, 4);
+    h.final(out);
+    host_times().md5_ms += ms_since(t0);
+}
+
+int64_t BatchBackend::first_hit(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) {
+    ProbeInterval one;
+    if (count == 1) {  // answered by the previous probe's hit list, or cut to its unprobed part
+        int64_t p = -1, a2 = iv[0].a;
+        int32_t T = 0;
+        if (cache.lookup(iv[0], keys, &p, &T, &a2)) {
+            if (p >= 0) {
+                t_pos = p;
+                t_val = T;
+            }
+            return p;
+        }
+        one = iv[0];
+        one.a = a2;
+        iv = &one;
+    }
+    FileScan& fs = scan_of(b, f);
+    fs.req = Req{};
+    fs.req.kind = Req::PROBE;
+    fs.req.iv = iv;
+    fs.req.niv = count;
+    fs.req.keys = keys;
+    fs.req.head = head;
+    b->post(fs);
+    const int64_t p = fs.req.result;
+    if (count == 1 && fs.req.out) cache.fill(iv[0], keys, *fs.req.out, n - B);
+    else cache.valid = false;
+    if (p < 0) return -1;
+    win_pos = t_pos = p;
+    t_val = *reinterpret_cast<const int32_t*>(hit);
+    if (bucket[0] <= HIT_BUCKET_CAP) {  // ascending chunk order, as the Multimap keeps it
+        std::vector<int32_t> idx(bucket + 2, bucket + 2 + bucket[0]);
+        std::sort(idx.begin(), idx.end());
+        table->prime(bucket[1], idx.data(), (int32_t)idx.size());
+    }
+    return p;
+}
+
+// One round: answer every pending request of the batch.  Returns a HIP error (then every request is
+// answered with "nothing": the resolvers run to completion on garbage and the batch reports the error).
+hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, const std::vector<int32_t>& pend) {
+    hipStream_t st = c->stream;
+    std::vector<GatherEnt> gw, gb;
+    std::vector<CopyEnt> copies;
+    std::vector<ProbeIv> ivs;
+    std::vector<ProbeTile> tiles;
+    std::vector<PartialTile> ptiles;
+    std::vector<int32_t> preq;
+    std::vector<int64_t> gw_at(files.size(), -1), gb_at(files.size(), -1), win_at(files.size(), -1);
+    int64_t win_bytes = 0, max_win = 0;
+    int32_t max_C = 0;
+    std::vector<uint64_t> dkeys;  // host-built probe hashes of stale-digest key sets
+    struct DkeyTab {
+        int32_t f;
+        int64_t off;
+        uint32_t mask;
+    };
+    std::vector<DkeyTab> dtabs;
+
+    ScanFile* F = S->h_files.as<ScanFile>();
+    for (int32_t f : pend) {
+        FileScan& fs = files[(size_t)f];
+        Req& r = fs.req;
+        switch (r.kind) {
+            case Req::WEAK:
+                gw_at[(size_t)f] = (int64_t)gw.size();
+                for (int64_t i = 0; i < r.count; ++i) gw.push_back(GatherEnt{r.pos[i], f, 0});
+                break;
+            case Req::BYTES:
+                gb_at[(size_t)f] = (int64_t)gb.size();
+                for (int64_t i = 0; i < r.count; ++i) gb.push_back(GatherEnt{r.pos[i], f, 0});
+                break;
+            case Req::WIN:
+                win_at[(size_t)f] = win_bytes;
+                copies.push_back(CopyEnt{fs.d_src + r.p, nullptr, r.w});  // dst fixed below
+                win_bytes += pad16(r.w);
+                max_win = std::max(max_win, r.w);
+                break;
+            case Req::PROBE: {
+                BatchBackend& be = fs.be;
+                F[f].aligned_weak = r.head ? S->haw.as<int32_t>() + fs.off_na : S->src_weak.as<int32_t>() + fs.off_na;
+                F[f].slots = S->slots.as<unsigned long long>() + fs.off_ns;
+                F[f].mask = fs.ns - 1;
+                if (r.keys) {  // stale digest: only its chunks' keys (a handful), hashed here
+                    const uint32_t nsl = pow2_at_least(2 * r.keys->size() + 2);
+                    const int64_t off = (int64_t)dkeys.size();
+                    dkeys.resize(dkeys.size() + nsl, 0ull);
+                    for (int32_t k : *r.keys) {
+                        const unsigned long long v = (1ull << 32) | (uint32_t)k;
+                        uint32_t h = slot_hash_host((uint32_t)k) & (nsl - 1);
+                        while (dkeys[(size_t)(off + h)] != 0ull && dkeys[(size_t)(off + h)] != v) h = (h + 1) & (nsl - 1);
+                        dkeys[(size_t)(off + h)] = v;
+                    }
+                    dtabs.push_back(DkeyTab{f, off, nsl - 1});
+                }
+                F[f].iv0 = (int32_t)ivs.size();
+                F[f].niv = (int32_t)r.niv;
+                const size_t t0 = tiles.size();
+                for (int64_t i = 0; i < r.niv; ++i) {
+                    const ProbeInterval& v = r.iv[i];
+                    ivs.push_back(ProbeIv{v.a, v.b, v.anchor, v.e_lo & 0xFFFFu, v.e_hi & 0xFFFFu, f, 0});
+                    probe_tiles(v.a, v.b, fs.B, (int32_t)(ivs.size() - 1), &tiles);
+                }
+                probe_partials(&tiles, t0, fs.B, f, &ptiles);
+                if (r.head) {  // anchors T(kB) of the blocks these tiles sit in
+                    for (size_t t = t0; t < tiles.size(); ++t) {
+                        const int64_t k = tiles[t].q0 / fs.B;
+                        if (!be.haw_ready[(size_t)k]) {
+                            be.haw_ready[(size_t)k] = 1;
+                            gw.push_back(GatherEnt{k * fs.B, f, 1});
+                        }
+                    }
+                }
+                preq.push_back(f);
+                max_C = std::max(max_C, fs.C);
+                break;
+            }
+        }
+    }
+    // pinned staging of this round's inputs
+    GatherEnt *hgw, *hgb;
+    int32_t *how, *hreq;
+    uint8_t *hob, *hwin;
+    CopyEnt* hcp;
+    ProbeIv* hiv;
+    ProbeTile* ht;
+    PartialTile* hpt;
+    unsigned long long* hdk;
+    hipError_t e = hipSuccess;
+    auto chk = [&](hipError_t x) {
+        if (x != hipSuccess && e == hipSuccess) e = x;
+    };
+    chk(pin(S->h_gw, (int64_t)gw.size(), &hgw));
+    chk(pin(S->h_gb, (int64_t)gb.size(), &hgb));
+    chk(pin(S->h_ow, (int64_t)gw.size(), &how));
+    chk(pin(S->h_ob, (int64_t)gb.size(), &hob));
+    chk(pin(S->h_win, win_bytes, &hwin));
+    chk(pin(S->h_copies, (int64_t)copies.size(), &hcp));
+    chk(pin(S->h_iv, (int64_t)ivs.size(), &hiv));
+    chk(pin(S->h_tiles, (int64_t)tiles.size(), &ht));
+    chk(pin(S->h_ptiles, (int64_t)ptiles.size(), &hpt));
+    chk(pin(S->h_req, (int64_t)preq.size(), &hreq));
+    chk(pin(S->h_dkeys, (int64_t)dkeys.size(), &hdk));
+    chk(S->partials.ensure((ptiles.size() + 1) * sizeof(int4)));
+    chk(S->dslots.ensure((dkeys.size() + 1) * sizeof(unsigned long long)));
+    if (e != hipSuccess) return e;
+    if (!gw.empty()) memcpy(hgw, gw.data(), gw.size() * sizeof(GatherEnt));
+    if (!gb.empty()) memcpy(hgb, gb.data(), gb.size() * sizeof(GatherEnt));
+    for (size_t i = 0, k = 0; i < pend.size(); ++i) {
+        const int32_t f = pend[i];
+        if (win_at[(size_t)f] >= 0) {
+            copies[k].dst = hwin + win_at[(size_t)f];
+            ++k;
+        }
+    }
+    if (!copies.empty()) memcpy(hcp, copies.data(), copies.size() * sizeof(CopyEnt));
+    if (!ivs.empty()) memcpy(hiv, ivs.data(), ivs.size() * sizeof(ProbeIv));
+    if (!tiles.empty()) memcpy(ht, tiles.data(), tiles.size() * sizeof(ProbeTile));
+    if (!ptiles.empty()) memcpy(hpt, ptiles.data(), ptiles.size() * sizeof(PartialTile));
+    if (!preq.empty()) memcpy(hreq, preq.data(), preq.size() * sizeof(int32_t));
+    if (!dkeys.empty()) memcpy(hdk, dkeys.data(), dkeys.size() * sizeof(uint64_t));
+    for (const DkeyTab& d : dtabs) {
+        F[d.f].slots = S->dslots.as<unsigned long long>() + d.off;
+        F[d.f].mask = d.mask;
+    }
+
+    // launches, one per kind, then one synchronisation
+    if (!dkeys.empty())
+        chk(hipMemcpyAsync(S->dslots.p, hdk, dkeys.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    if (!preq.empty())
+        chk(launch_probe_out_reset(S->first.as<ProbeOut>(), (uint32_t)files.size(), st));
+    chk(launch_window_weak(F, hgw, (uint32_t)gw.size(), how, st));  // weak sums + head-mode anchors
+    chk(launch_gather_bytes(F, hgb, (uint32_t)gb.size(), hob, st));
+    chk(launch_copy_many(hcp, (uint32_t)copies.size(), max_win, st));
+    if (!preq.empty()) {
+        ProbeArgs A;
+        A.files = F;
+        A.ivs = hiv;
+        A.tiles = ht;
+        A.partials = S->partials.as<int4>();
+        chk(launch_probe_first(A, (uint32_t)tiles.size(), hpt, (uint32_t)ptiles.size(), st));
+        chk(launch_hit_window(F, hiv, hreq, (int32_t)preq.size(), max_C, st));
+        chk(hipMemcpyAsync(S->h_first.p, S->first.p, files.size() * sizeof(ProbeOut), hipMemcpyDeviceToHost, st));
+        chk(hipMemcpyAsync(S->h_bucket.p, S->bucket.p, files.size() * (2 + HIT_BUCKET_CAP) * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, st));
+    }
+    chk(hipStreamSynchronize(st));
+
+    // answers
+    const ProbeOut* hf = S->h_first.as<ProbeOut>();
+    for (int32_t f : pend) {
+        FileScan& fs = files[(size_t)f];
+        Req& r = fs.req;
+        switch (r.kind) {
+            case Req::WEAK:
+                for (int64_t i = 0; i < r.count; ++i) r.out_w[i] = e == hipSuccess ? how[gw_at[(size_t)f] + i] : 0;
+                break;
+            case Req::BYTES:
+                for (int64_t i = 0; i < r.count; ++i) r.out_b[i] = e == hipSuccess ? hob[gb_at[(size_t)f] + i] : 0;
+                break;
+            case Req::WIN:
+                r.win = hwin + win_at[(size_t)f];
+                break;
+            case Req::PROBE:
+                r.out = e == hipSuccess ? &hf[f] : nullptr;
+                r.result = (e == hipSuccess && hf[f].first != ~0ull) ? (int64_t)hf[f].first : -1;
+                break;
+        }
+    }
+    return e;
+}
+
+int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which, const uint8_t seed[4],
+               rsh_scan_stats* agg) {
+    BatchState* S = state_of(c);
+    if (!S) return RSH_E_NOMEM;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int32_t NF = (int32_t)which.size();
+    std::vector<FileScan> files((size_t)NF);
+    int64_t tw = 0, ts = 0, tna = 0, tas = 0, tnf = 0, tns = 0, thit = 0, tw0 = 0, maxC = 0;
+    for (int32_t f = 0; f < NF; ++f) {
+        FileScan& fs = files[(size_t)f];
+        const rsh_scan_job& j = jobs[which[(size_t)f]];
+        fs.job = which[(size_t)f];
+        fs.d_src = static_cast<const uint8_t*>(j.d_src);
+        fs.d_weak = static_cast<const int32_t*>(j.d_weak);
+        fs.d_strong = static_cast<const uint8_t*>(j.d_strong);
+        fs.n = j.n;
+        fs.B = j.h.block_length;
+        fs.C = j.h.chunk_count;
+        fs.dl = j.h.digest_length;
+        fs.na = (fs.n + fs.B - 1) / fs.B;
+        fs.nf = std::min<int64_t>(fs.na, fs.C);
+        fs.ns = pow2_at_least(2 * (uint64_t)fs.C + 2);
+        fs.off_tw = tw, tw += fs.C;
+        fs.off_ts = ts, ts += (int64_t)fs.C * fs.dl;
+        fs.off_na = tna, tna += fs.na;
+        fs.off_as = tas, tas += fs.na * fs.dl;
+        fs.off_nf = tnf, tnf += fs.nf;
+        fs.off_ns = tns, tns += fs.ns;
+        fs.off_hit = thit, thit += pad16(16 + fs.B);
+        fs.off_w0 = tw0, tw0 += pad16(std::min<int64_t>(fs.B, fs.n));
+        maxC = std::max<int64_t>(maxC, fs.C);
+    }
+    // buffers first (allocation may synchronise), then the asynchronous work
+    RSH_BHIP(S->h_weak.ensure((size_t)tw * 4 + 4));
+    RSH_BHIP(S->h_strong.ensure((size_t)ts + 1));
+    RSH_BHIP(S->slots.ensure((size_t)tns * 8));
+    RSH_BHIP(S->src_weak.ensure((size_t)tna * 4));
+    RSH_BHIP(S->src_strong.ensure((size_t)tas + 1));
+    RSH_BHIP(S->flags.ensure((size_t)tnf + 1));
+    RSH_BHIP(S->haw.ensure((size_t)tna * 4));
+    RSH_BHIP(S->h_aw.ensure((size_t)tna * 4));
+    RSH_BHIP(S->h_as.ensure((size_t)tas + 1));
+    RSH_BHIP(S->h_fl.ensure((size_t)tnf + 1));
+    RSH_BHIP(S->h_files.ensure((size_t)NF * sizeof(ScanFile)));
+    RSH_BHIP(S->h_hit.ensure((size_t)thit));
+    RSH_BHIP(S->h_win0.ensure((size_t)tw0));
+    RSH_BHIP(S->first.ensure((size_t)NF * sizeof(ProbeOut)));
+    RSH_BHIP(S->h_first.ensure((size_t)NF * sizeof(ProbeOut)));
+    RSH_BHIP(S->bucket.ensure((size_t)NF * (2 + HIT_BUCKET_CAP) * 4));
+    RSH_BHIP(S->h_bucket.ensure((size_t)NF * (2 + HIT_BUCKET_CAP) * 4));
+    RSH_BHIP(S->h_copies.ensure((size_t)2 * NF * sizeof(CopyEnt)));
+    RSH_BHIP(S->h_ccopies.ensure((size_t)NF * sizeof(CopyEnt) + (size_t)3 * NF * sizeof(CopyEnt)));
+    RSH_BHIP(S->h_tabents.ensure((size_t)NF * sizeof(TableEnt)));
+    RSH_BHIP(S->h_flagents.ensure((size_t)NF * sizeof(FlagEnt)));
+    std::vector<K1File> k1;
+    for (FileScan& fs : files)
+        k1.push_back(K1File{fs.d_src, fs.n, (uint32_t)fs.B, (uint32_t)fs.dl, (uint32_t)fs.na,
+                            S->src_weak.as<int32_t>() + fs.off_na, S->src_strong.as<uint8_t>() + fs.off_as});
+    std::vector<K1Group> groups;
+    std::vector<K1Lane> lanes;
+    int lane_align = 16;
+    plan_block_sums_batch(k1.data(), NF, &groups, &lanes, &lane_align);
+    RSH_BHIP(S->k1_groups.ensure((groups.size() + 1) * sizeof(K1Group)));
+    RSH_BHIP(S->k1_lanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
+
+    hipStream_t st = c->stream, aux = c->aux;
+    RSH_BHIP(hipEventRecord(c->ev_in, st));  // whatever produced the inputs on the context stream
+    // (aux) the received tables, to pinned host memory in one kernel
+    CopyEnt* tc = S->h_copies.as<CopyEnt>();
+    int64_t max_tab = 0;
+    uint32_t ntc = 0;
+    for (FileScan& fs : files) {
+        if (fs.C == 0) continue;
+        tc[ntc++] = CopyEnt{reinterpret_cast<const uint8_t*>(fs.d_weak), S->h_weak.as<uint8_t>() + 4 * fs.off_tw,
+                            (int64_t)fs.C * 4};
+        if (fs.dl > 0)
+            tc[ntc++] = CopyEnt{fs.d_strong, S->h_strong.as<uint8_t>() + fs.off_ts, (int64_t)fs.C * fs.dl};
+        max_tab = std::max<int64_t>(max_tab, (int64_t)fs.C * 4);
+    }
+    RSH_BHIP(hipStreamWaitEvent(aux, c->ev_in, 0));
+    RSH_BHIP(launch_copy_many(tc, ntc, max_tab, aux));
+    RSH_BHIP(hipEventRecord(c->ev_tab, aux));
+    // (stream) the probe hashes and windows 0
+    RSH_BHIP(hipMemsetAsync(S->slots.p, 0, (size_t)tns * 8, st));
+    TableEnt* te = S->h_tabents.as<TableEnt>();
+    for (int32_t f = 0; f < NF; ++f) {
+        FileScan& fs = files[(size_t)f];
+        te[f] = TableEnt{S->slots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
+    }
+    RSH_BHIP(launch_table_insert_many(te, (uint32_t)NF, (int32_t)maxC, st));
+    CopyEnt* wc = S->h_ccopies.as<CopyEnt>();
+    int64_t max_w0 = 0;
+    for (int32_t f = 0; f < NF; ++f) {
+        FileScan& fs = files[(size_t)f];
+        const int64_t w0 = std::min<int64_t>(fs.B, fs.n);
+        wc[f] = CopyEnt{fs.d_src, S->h_win0.as<uint8_t>() + fs.off_w0, w0};
+        max_w0 = std::max(max_w0, w0);
+    }
+    RSH_BHIP(launch_copy_many(wc, (uint32_t)NF, max_w0, st));
+
+    // the batched aligned speculation (deferred; see scan_device in capi.cpp)
+    const int gen = ++c->gen;
+    CopyEnt* sc = S->h_ccopies.as<CopyEnt>() + NF;
+    auto launch_spec = [&]() -> int {
+        if (!groups.empty())
+            RSH_BHIP(hipMemcpyAsync(S->k1_groups.p, groups.data(), groups.size() * sizeof(K1Group),
+                                    hipMemcpyHostToDevice, aux));
+        if (!lanes.empty())
+            RSH_BHIP(hipMemcpyAsync(S->k1_lanes.p, lanes.data(), lanes.size() * sizeof(K1Lane), hipMemcpyHostToDevice,
+                                    aux));
+        RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>(), (uint32_t)groups.size(), S->k1_lanes.as<K1Lane>(),
+                                         (uint32_t)lanes.size(), lane_align, seed_word(seed), aux, c->abort_word, gen));
+        FlagEnt* fe = S->h_flagents.as<FlagEnt>();
+        uint32_t max_nf = 0, nsc = 0;
+        int64_t max_len = 0;
+        for (int32_t f = 0; f < NF; ++f) {
+            FileScan& fs = files[(size_t)f];
+            fe[f] = FlagEnt{S->src_weak.as<int32_t>() + fs.off_na, S->src_strong.as<uint8_t>() + fs.off_as, fs.d_weak,
+                            fs.d_strong, S->flags.as<uint8_t>() + fs.off_nf, (uint32_t)fs.nf, (uint32_t)fs.dl};
+            max_nf = std::max<uint32_t>(max_nf, (uint32_t)fs.nf);
+            sc[nsc++] = CopyEnt{S->src_weak.as<uint8_t>() + 4 * fs.off_na, S->h_aw.as<uint8_t>() + 4 * fs.off_na,
+                                fs.na * 4};
+            if (fs.dl > 0)
+                sc[nsc++] = CopyEnt{S->src_strong.as<uint8_t>() + fs.off_as, S->h_as.as<uint8_t>() + fs.off_as,
+                                    fs.na * fs.dl};
+            if (fs.nf > 0)
+                sc[nsc++] = CopyEnt{S->flags.as<uint8_t>() + fs.off_nf, S->h_fl.as<uint8_t>() + fs.off_nf, fs.nf};
+            max_len = std::max<int64_t>(max_len, fs.na * 4);
+        }
+        RSH_BHIP(launch_chain_flags_many(fe, (uint32_t)NF, max_nf, aux));
+        RSH_BHIP(launch_copy_many(sc, nsc, max_len, aux));
+        RSH_BHIP(hipEventRecord(c->ev_spec, aux));
+        return RSH_OK;
+    };
+
+    const double enq_ms = ms_since(t0);
+    RSH_BHIP(hipEventSynchronize(c->ev_tab));
+    RSH_BHIP(hipStreamSynchronize(st));
+    const double setup_ms = ms_since(t0);
+
+    // per-file host state
+    ScanFile* F = S->h_files.as<ScanFile>();
+    Batch b;
+    b.files = &files;
+    for (int32_t f = 0; f < NF; ++f) {
+        FileScan& fs = files[(size_t)f];
+        const rsh_scan_job& j = jobs[fs.job];
+        fs.table.chunk_count = fs.C;
+        fs.table.block_length = (int32_t)fs.B;
+        fs.table.remainder = j.h.remainder;
+        fs.table.digest_length = fs.dl;
+        fs.table.weak = S->h_weak.as<int32_t>() + fs.off_tw;
+        fs.table.strong = S->h_strong.as<uint8_t>() + fs.off_ts;
+        BatchBackend& be = fs.be;
+        be.b = &b;
+        be.f = f;
+        be.na = fs.na;
+        be.aw = S->h_aw.as<int32_t>() + fs.off_na;
+        be.as = S->h_as.as<uint8_t>() + fs.off_as;
+        be.fl = S->h_fl.as<uint8_t>() + fs.off_nf;
+        be.win0 = S->h_win0.as<uint8_t>() + fs.off_w0;
+        be.w0 = std::min<int64_t>(fs.B, fs.n);
+        be.hit = S->h_hit.as<uint8_t>() + fs.off_hit;
+        be.bucket = S->h_bucket.as<int32_t>() + (int64_t)f * (2 + HIT_BUCKET_CAP);
+        be.n = fs.n;
+        be.B = fs.B;
+        memcpy(be.seed, seed, 4);
+        be.table = &fs.table;
+        be.haw_ready.assign((size_t)fs.na, 0);
+        F[f] = ScanFile{};
+        F[f].data = fs.d_src;
+        F[f].n = fs.n;
+        F[f].B = (uint32_t)fs.B;
+        F[f].out = S->first.as<ProbeOut>() + f;
+        F[f].table_weak = fs.d_weak;
+        F[f].C = fs.C;
+        F[f].bucket = S->bucket.as<int32_t>() + (int64_t)f * (2 + HIT_BUCKET_CAP);
+        F[f].hit = S->h_hit.as<uint8_t>() + fs.off_hit;
+        F[f].aligned_weak = S->haw.as<int32_t>() + fs.off_na;
+    }
+
+    // policy (A/B via RSH_BATCH_SPEC): "wait" = land the speculation before the resolvers start (no head
+    // mode), otherwise = head mode, speculation launched after that many rounds
+    static const char* pol = getenv("RSH_BATCH_SPEC");
+    static const bool wait_spec = pol && strcmp(pol, "wait") == 0;
+    static const int defer_rounds = (pol && !wait_spec) ? atoi(pol) : kDeferRounds;
+    int spec_rc = RSH_OK;
+    bool spec_launched = false;
+    if (wait_spec) {
+        spec_rc = launch_spec();
+        if (spec_rc != RSH_OK) return spec_rc;
+        spec_launched = true;
+        RSH_BHIP(hipEventSynchronize(c->ev_spec));
+        if (getenv("RSH_SCAN_TRACE")) fprintf(stderr, "[rsh-batch] speculation landed at %.3f ms\n", ms_since(t0));
+        b.landed.store(true);
+        for (FileScan& fs : files) fs.be.head = false;
+    }
+
+    cpu_set_t cpus;
+    int ncpu = 8;
+    if (sched_getaffinity(0, sizeof(cpus), &cpus) == 0) ncpu = CPU_COUNT(&cpus);
+    const int32_t W = std::max<int32_t>(1, std::min<int32_t>({NF, (int32_t)ncpu, kMaxWorkers}));
+    b.nworkers = W;
+    b.worker_uc.resize((size_t)W);
+    b.busy_ms.assign((size_t)W, 0.0);
+    b.times.assign((size_t)W, HostTimes{});
+    b.max_fiber_ms.assign((size_t)W, 0.0);
+    for (int32_t f = 0; f < NF; ++f) files[(size_t)f].worker = f % W;
+    std::vector<std::thread> th;
+    th.reserve((size_t)W);
+    for (int32_t w = 0; w < W; ++w) {
+        th.emplace_back([&b, &files, w, NF, W] {
+            uint64_t seen = 0;
+            for (;;) {
+                {
+                    std::unique_lock<std::mutex> l(b.mu);
+                    b.cv_work.wait(l, [&] { return b.gen != seen || b.quit; });
+                    if (b.quit) return;
+                    seen = b.gen;
+                }
+                for (int32_t f = w; f < NF; f += W) {
+                    FileScan& fs = files[(size_t)f];
+                    if (fs.done) continue;
+                    fs.pending = false;
+                    if (!fs.started) {
+                        fs.started = true;
+                        fs.stack.reset(new char[kFiberStack]);
+                        getcontext(&fs.uc);
+                        fs.uc.uc_stack.ss_sp = fs.stack.get();
+                        fs.uc.uc_stack.ss_size = kFiberStack;
+                        fs.uc.uc_link = &b.worker_uc[(size_t)w];
+                        const uintptr_t a = reinterpret_cast<uintptr_t>(&fs);
+                        makecontext(&fs.uc, reinterpret_cast<void (*)()>(&fiber_main), 2, (uint32_t)(a >> 32),
+                                    (uint32_t)a);
+                    }
+                    const auto tf = std::chrono::steady_clock::now();
+                    swapcontext(&b.worker_uc[(size_t)w], &fs.uc);  // until its next request or its end
+                    const double dt = ms_since(tf);
+                    b.busy_ms[(size_t)w] += dt;
+                    b.max_fiber_ms[(size_t)w] = std::max(b.max_fiber_ms[(size_t)w], dt);
+                }
+                std::lock_guard<std::mutex> l(b.mu);
+                b.times[(size_t)w] = host_times();
+                if (++b.idle == b.nworkers) b.cv_coord.notify_one();
+            }
+        });
+    }
+    {
+        std::lock_guard<std::mutex> l(b.mu);
+        b.gen = 1;
+    }
+    b.cv_work.notify_all();
+
+    // coordinator: one round per "every live resolver is waiting or done"
+    hipError_t err = hipSuccess;
+    int rounds = 0;
+    std::vector<int32_t> pend;
+    static const bool trace = getenv("RSH_SCAN_TRACE") != nullptr;
+    auto t_round = std::chrono::steady_clock::now();
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> l(b.mu);
+            b.cv_coord.wait(l, [&] { return b.idle == b.nworkers; });
+            pend.clear();
+            for (int32_t f = 0; f < NF; ++f)
+                if (!files[(size_t)f].done && files[(size_t)f].pending) pend.push_back(f);
+            if (pend.empty()) {
+                b.quit = true;
+                break;
+            }
+        }
+        ++rounds;
+        if (!spec_launched && rounds > defer_rounds) {
+            spec_rc = launch_spec();
+            spec_launched = true;
+        }
+        if (spec_launched && spec_rc == RSH_OK && !b.landed.load() && hipEventQuery(c->ev_spec) == hipSuccess)
+            b.landed.store(true, std::memory_order_release);
+        const double wait_ms = ms_since(t_round);
+        const auto t_serve = std::chrono::steady_clock::now();
+        const hipError_t e = serve_round(c, S, files, pend);
+        if (trace) {
+            int kinds[4] = {0, 0, 0, 0};
+            for (int32_t f : pend) kinds[files[(size_t)f].req.kind]++;
+            double bsum = 0, bmax = 0, fmax = 0;
+            for (int32_t w = 0; w < b.nworkers; ++w) {
+                bsum += b.busy_ms[(size_t)w];
+                bmax = std::max(bmax, b.busy_ms[(size_t)w]);
+                fmax = std::max(fmax, b.max_fiber_ms[(size_t)w]);
+            }
+            fprintf(stderr, "[rsh-batch] round %3d  pending %3zu (weak %d bytes %d win %d probe %d)  wait %.3f ms "
+                    "(host work: sum %.3f, max worker %.3f, max fiber %.3f)  serve %.3f ms%s\n",
+                    rounds, pend.size(), kinds[0], kinds[1], kinds[2], kinds[3], wait_ms, bsum, bmax, fmax,
+                    ms_since(t_serve), b.landed.load() ? "  [aligned]" : "");
+            std::fill(b.busy_ms.begin(), b.busy_ms.end(), 0.0);
+            std::fill(b.max_fiber_ms.begin(), b.max_fiber_ms.end(), 0.0);
+        }
+        t_round = std::chrono::steady_clock::now();
+        if (e != hipSuccess && err == hipSuccess) {
+            err = e;
+            note_error(e, __LINE__, "batch.cpp");
+        }
+        {
+            std::lock_guard<std::mutex> l(b.mu);
+            b.idle = 0;
+            ++b.gen;
+        }
+        b.cv_work.notify_all();
+    }
+    b.cv_work.notify_all();  // quit
+    const double rounds_end_ms = ms_since(t0);
+    for (std::thread& t : th) t.join();
+    const double resolve_ms = ms_since(t0) - setup_ms;
+    if (trace) {
+        HostTimes tt;
+        for (const HostTimes& x : b.times) {
+            tt.bucket_ms += x.bucket_ms;
+            tt.sort_ms += x.sort_ms;
+            tt.dkeys_ms += x.dkeys_ms;
+            tt.md5_ms += x.md5_ms;
+        }
+        fprintf(stderr, "[rsh-batch] host totals (cumulative per thread): bucket %.3f sort %.3f dkeys %.3f md5 %.3f ms\n",
+                tt.bucket_ms, tt.sort_ms, tt.dkeys_ms, tt.md5_ms);
+    }
+    if (trace)
+        fprintf(stderr, "[rsh-batch] %d files: enqueued %.3f, tables+hashes ready %.3f, rounds done %.3f, joined %.3f ms\n",
+                NF, enq_ms, setup_ms, rounds_end_ms, ms_since(t0));
+
+    if (spec_launched) {
+        if (hipEventQuery(c->ev_spec) == hipErrorNotReady) {  // every resolver finished first: stop it
+            RSH_BHIP(hipStreamWriteValue32(st, c->abort_word, (uint32_t)gen, 0));
+            RSH_BHIP(hipStreamWaitEvent(st, c->ev_spec, 0));
+        }
+    }
+    if (spec_rc != RSH_OK) return spec_rc;
+    if (err != hipSuccess) return RSH_E_DEVICE;
+
+    for (FileScan& fs : files) {
+        rsh_scan_job& j = jobs[fs.job];
+        j.literal = fs.res.literal;
+        j.matched = fs.res.matched;
+        j.n_ev = (int64_t)fs.res.ev.size();
+        if (j.n_ev > j.ev_cap || (!j.ev && j.n_ev > 0)) {
+            j.status = RSH_E_NOSPACE;
+        } else {
+            if (j.n_ev > 0) memcpy(j.ev, fs.res.ev.data(), fs.res.ev.size() * sizeof(rsh_event));
+            j.status = RSH_OK;
+        }
+        if (agg) {
+            const rsh_scan_stats& s = fs.res.stats;
+            agg->chain_matches += s.chain_matches;
+            agg->events += s.events;
+            agg->host_md5_windows += s.host_md5_windows;
+            agg->flushes += s.flushes;
+            agg->table_ms += s.table_ms + fs.table.sort_ms;
+        }
+    }
+    if (agg) {
+        agg->probe_launches += rounds;  // one batched launch set per round
+        agg->device_ms += setup_ms;
+        agg->resolver_ms += resolve_ms;
+        agg->speculation_aborted = spec_launched ? (b.landed.load() ? 0 : 1) : 2;
+    }
+    return RSH_OK;
+}
+
+}  // namespace
+}  // namespace rsh
+
+using namespace rsh;
+
+extern "C" {
+
+int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t njobs, const uint8_t seed[4]) {
+    if (!ctx || !seed || njobs < 0 || (njobs > 0 && !jobs)) return RSH_E_INVAL;
+    std::vector<K1File> files;
+    for (int32_t i = 0; i < njobs; ++i) {
+        const rsh_block_job& j = jobs[i];
+        const int rc = check_generator_header(j.n, &j.h);
+        if (rc != RSH_OK) return rc;
+        if (j.h.chunk_count == 0) continue;
+        if (!j.d_data || !j.d_weak || (!j.d_strong && j.h.digest_length > 0)) return RSH_E_INVAL;
+        files.push_back(K1File{static_cast<const uint8_t*>(j.d_data), j.n, (uint32_t)j.h.block_length,
+                               (uint32_t)j.h.digest_length, (uint32_t)j.h.chunk_count, static_cast<int32_t*>(j.d_weak),
+                               static_cast<uint8_t*>(j.d_strong)});
+    }
+    if (files.empty()) return RSH_OK;
+    RSH_CLAIM(ctx);
+    BatchState* S = state_of(ctx);
+    if (!S) return RSH_E_NOMEM;
+    RSH_BHIP(hipSetDevice(ctx->device));
+    std::vector<K1Group> groups;
+    std::vector<K1Lane> lanes;
+    int lane_align = 16;
+    plan_block_sums_batch(files.data(), (int32_t)files.size(), &groups, &lanes, &lane_align);
+    RSH_BHIP(S->g_groups.ensure((groups.size() + 1) * sizeof(K1Group)));
+    RSH_BHIP(S->g_lanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
+    // pageable sources: the copies are staged before hipMemcpyAsync returns, so the vectors may go
+    if (!groups.empty())
+        RSH_BHIP(hipMemcpyAsync(S->g_groups.p, groups.data(), groups.size() * sizeof(K1Group), hipMemcpyHostToDevice,
+                                ctx->stream));
+    if (!lanes.empty())
+        RSH_BHIP(hipMemcpyAsync(S->g_lanes.p, lanes.data(), lanes.size() * sizeof(K1Lane), hipMemcpyHostToDevice,
+                                ctx->stream));
+    RSH_BHIP(launch_block_sums_batch(S->g_groups.as<K1Group>(), (uint32_t)groups.size(), S->g_lanes.as<K1Lane>(),
+                                     (uint32_t)lanes.size(), lane_align, seed_word(seed), ctx->stream));
+    return RSH_OK;
+}
+
+int rsh_match_scan_batch_device(rsh_ctx* ctx, rsh_scan_job* jobs, int32_t njobs, const uint8_t seed[4],
+                                rsh_scan_stats* stats) {
+    if (!ctx || !seed || njobs < 0 || (njobs > 0 && !jobs)) return RSH_E_INVAL;
+    if (stats) *stats = rsh_scan_stats{};
+    std::vector<int32_t> scan;
+    for (int32_t i = 0; i < njobs; ++i) {
+        rsh_scan_job& j = jobs[i];
+        j.n_ev = j.literal = j.matched = 0;
+        j.status = RSH_OK;
+        if (j.n < 0) {
+            j.status = RSH_E_INVAL;
+            continue;
+        }
+        const int v = rsh_header_validate(&j.h);
+        if (v != RSH_OK) {
+            j.status = v;
+            continue;
+        }
+        if (j.h.block_length == 0 || j.n == 0) {  // new file (skipMatchSendData) or empty source
+            ResolveResult r;
+            if (j.h.block_length == 0) skip_events(j.n, &r);
+            j.literal = r.literal;
+            j.n_ev = (int64_t)r.ev.size();
+            if (j.n_ev > j.ev_cap || (!j.ev && j.n_ev > 0)) j.status = RSH_E_NOSPACE;
+            else if (j.n_ev > 0) memcpy(j.ev, r.ev.data(), r.ev.size() * sizeof(rsh_event));
+            continue;
+        }
+        if (!j.d_src || (j.h.chunk_count > 0 && (!j.d_weak || (!j.d_strong && j.h.digest_length > 0)))) {
+            j.status = RSH_E_INVAL;
+            continue;
+        }
+        if ((j.n + j.h.block_length - 1) / j.h.block_length > 2147483647LL) {
+            j.status = RSH_E_OVERFLOW;
+            continue;
+        }
+        scan.push_back(i);
+    }
+    if (!scan.empty()) {
+        RSH_CLAIM(ctx);
+        RSH_BHIP(hipSetDevice(ctx->device));
+        for (size_t k = 0; k < scan.size(); k += kMaxLive) {
+            const std::vector<int32_t> part(scan.begin() + (ptrdiff_t)k,
+                                            scan.begin() + (ptrdiff_t)std::min(scan.size(), k + kMaxLive));
+            const int rc = scan_batch(ctx, jobs, part, seed, stats);
+            if (rc != RSH_OK) {
+                for (int32_t i : part) jobs[i].status = rc;
+                return rc;
+            }
+        }
+    }
+    for (int32_t i = 0; i < njobs; ++i)
+        if (jobs[i].status != RSH_OK) return jobs[i].status;
+    return RSH_OK;
+}
+
+}  // extern "C"

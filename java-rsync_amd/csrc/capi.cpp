@@ -17,146 +17,9 @@
 #include "resolver.h"
 #include "rsync_hip.h"
 
-namespace {
-
-constexpr int64_t kChunkSize = 8192;        // Sender.java:230 CHUNK_SIZE
-constexpr int64_t kDefaultBlock = 8192;     // FileView.java:38 DEFAULT_BLOCK_SIZE
-constexpr int32_t kMaxBlockLength = 1 << 17;  // Checksum.java:151
-
-struct DevBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    hipError_t ensure(size_t n) {
-        if (n <= cap) return hipSuccess;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        hipError_t e = hipMalloc(&p, n ? n : 1);
-        if (e == hipSuccess) cap = n;
-        return e;
-    }
-    template <class T>
-    T* as() const {
-        return static_cast<T*>(p);
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-};
-
-// Page-locked host staging (true async D2H).
-struct PinnedBuf {
-    void* p = nullptr;
-    size_t cap = 0;
-    hipError_t ensure(size_t n) {
-        if (n <= cap) return hipSuccess;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-        hipError_t e = hipHostMalloc(&p, n ? n : 1, hipHostMallocDefault);
-        if (e == hipSuccess) cap = n;
-        return e;
-    }
-    template <class T>
-    T* as() const {
-        return static_cast<T*>(p);
-    }
-    void release() {
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-};
-
-uint32_t seed_word(const uint8_t seed[4]) {
-    return (uint32_t)seed[0] | ((uint32_t)seed[1] << 8) | ((uint32_t)seed[2] << 16) | ((uint32_t)seed[3] << 24);
-}
-
-uint32_t pow2_at_least(uint64_t v) {
-    uint32_t p = 64;
-    while (p < v) p <<= 1;
-    return p;
-}
-
-double ms_since(std::chrono::steady_clock::time_point t0) {
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-}
-
-}  // namespace
-
-struct rsh_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    DevBuf data, weak, strong;                   // host-input staging
-    DevBuf src_weak, src_strong, flags;          // aligned speculation over the source
-    DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw, partials, bucket;
-    hipStream_t aux = nullptr;                   // table download, then the aligned speculation
-    hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr;
-    PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
-    // resolver round trips: the small kernels read their inputs from and write their outputs to pinned
-    // host memory directly (no staging copies); the probe result and digest windows come back by copy
-    PinnedBuf h_pos, h_out, h_iv, h_tiles, h_keys, h_first, h_win, h_ptiles;
-    PinnedBuf h_hit;  // after a probe hit: T(p) (bytes 0..3) and the window at p (from byte 16)
-    PinnedBuf h_win0;    // window 0 of the current scan (its digest is computed on a host thread)
-    PinnedBuf h_bucket;  // after a probe hit: {count, key, chunk indices} of the key that hit
-    uint64_t first_used = 0;    // probe result slots handed out (see HipBackend::first_hit)
-    int* abort_word = nullptr;  // device, uncached: the speculation launch of generation g stops once it reads g
-    int gen = 0;
-    std::vector<rsh_event> last_ev;  // kept when the caller's event buffer was too small
-    std::atomic<bool> busy{false};   // the staging buffers and last_ev serve one call at a time
-    ~rsh_ctx() {
-        for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &slots, &dslots, &dkeys, &pos, &out,
-                          &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket})
-            b->release();
-        for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pos, &h_out, &h_iv, &h_tiles, &h_keys, &h_first,
-                             &h_win, &h_ptiles, &h_hit, &h_win0, &h_bucket})
-            b->release();
-        if (abort_word) (void)hipFree(abort_word);
-        if (ev_in) (void)hipEventDestroy(ev_in);
-        if (ev_tab) (void)hipEventDestroy(ev_tab);
-        if (ev_spec) (void)hipEventDestroy(ev_spec);
-        if (aux) (void)hipStreamDestroy(aux);
-        if (stream) (void)hipStreamDestroy(stream);
-    }
-};
-
-// Last HIP failure of the calling thread (rsh_last_error): error text and the capi.cpp line.
-static thread_local char g_last_err[256] = "";
-static void note_error(hipError_t e, int line) {
-    snprintf(g_last_err, sizeof(g_last_err), "%s (capi.cpp:%d)", hipGetErrorString(e), line);
-}
-
-#define RSH_HIP(call)                                   \
-    do {                                                \
-        hipError_t e_ = (call);                         \
-        if (e_ != hipSuccess) {                         \
-            note_error(e_, __LINE__);                   \
-            return RSH_E_DEVICE;                        \
-        }                                               \
-    } while (0)
+#include "ctx.h"
 
 namespace {
-
-// Claims a context for one call that uses its buffers; a second thread gets RSH_E_BUSY instead of
-// racing on them (one rsh_ctx per calling thread, rsync_hip.h).
-struct CtxClaim {
-    rsh_ctx* c;
-    bool held;
-    explicit CtxClaim(rsh_ctx* ctx) : c(ctx), held(!ctx->busy.exchange(true, std::memory_order_acquire)) {}
-    ~CtxClaim() {
-        if (held) c->busy.store(false, std::memory_order_release);
-    }
-};
-
-#define RSH_CLAIM(ctx)                                                                   \
-    CtxClaim claim_(ctx);                                                                \
-    if (!claim_.held) {                                                                  \
-        snprintf(g_last_err, sizeof(g_last_err), "context in use by another thread");   \
-        return RSH_E_BUSY;                                                               \
-    }
-
 // ------------------------------------------------------------------------------------------------
 // HIP implementation of the resolver's services.
 // ------------------------------------------------------------------------------------------------
@@ -208,27 +71,29 @@ class HipBackend : public rsh::ScanBackend {
 
     void weak_many(const int64_t* pos, int64_t count, int32_t* out) override {
         if (count <= 0) return;
-        if (count == 1 && pos[0] == hit_pos_) {  // fetched with the probe result
-            out[0] = hit_weak_;
+        if (count == 1 && pos[0] == t_pos_) {  // fetched with (or derived from) a probe result
+            out[0] = t_val_;
             return;
         }
         CallTrace tr("weak_many", count);
-        int64_t* hp = pin<int64_t>(c_->h_pos, count);
+        rsh::GatherEnt* hp = pin<rsh::GatherEnt>(c_->h_pos, count);
         int32_t* ho = pin<int32_t>(c_->h_out, count);
+        rsh::ScanFile* F = file();
         if (err != hipSuccess) return;
-        memcpy(hp, pos, (size_t)count * sizeof(int64_t));
-        ok(rsh::launch_window_weak(x_, n_, (uint32_t)B_, hp, (uint32_t)count, ho, c_->stream));
+        for (int64_t i = 0; i < count; ++i) hp[i] = rsh::GatherEnt{pos[i], 0, 0};
+        ok(rsh::launch_window_weak(F, hp, (uint32_t)count, ho, c_->stream));
         ok(hipStreamSynchronize(c_->stream));
         memcpy(out, ho, (size_t)count * sizeof(int32_t));
     }
     void bytes_many(const int64_t* pos, int64_t count, uint8_t* out) override {
         if (count <= 0) return;
         CallTrace tr("bytes_many", count);
-        int64_t* hp = pin<int64_t>(c_->h_pos, count);
+        rsh::GatherEnt* hp = pin<rsh::GatherEnt>(c_->h_pos, count);
         uint8_t* ho = pin<uint8_t>(c_->h_out, count);
+        rsh::ScanFile* F = file();
         if (err != hipSuccess) return;
-        memcpy(hp, pos, (size_t)count * sizeof(int64_t));
-        ok(rsh::launch_gather_bytes(x_, hp, (uint32_t)count, ho, c_->stream));
+        for (int64_t i = 0; i < count; ++i) hp[i] = rsh::GatherEnt{pos[i], 0, 0};
+        ok(rsh::launch_gather_bytes(F, hp, (uint32_t)count, ho, c_->stream));
         ok(hipStreamSynchronize(c_->stream));
         memcpy(out, ho, (size_t)count);
     }
@@ -241,7 +106,7 @@ class HipBackend : public rsh::ScanBackend {
             md5_0(out);
             return;
         }
-        if (p == hit_pos_) {  // the window came back with the probe result
+        if (p == win_pos_) {  // the window came back with the probe result
             rsh::HostMd5 h;
             h.update(c_->h_hit.as<uint8_t>() + 16, (size_t)w);
             h.update(seed_, 4);
@@ -258,6 +123,21 @@ class HipBackend : public rsh::ScanBackend {
         h.final(out);
     }
     int64_t first_hit(const rsh::ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) override {
+        rsh::ProbeInterval one;
+        if (count == 1) {  // answered by the previous probe's hit list, or cut to its unprobed part
+            int64_t p = -1, a2 = iv[0].a;
+            int32_t T = 0;
+            if (cache_.lookup(iv[0], keys, &p, &T, &a2)) {
+                if (p >= 0) {
+                    t_pos_ = p;
+                    t_val_ = T;
+                }
+                return p;
+            }
+            one = iv[0];
+            one.a = a2;
+            iv = &one;
+        }
         CallTrace tr("first_hit", count);
         rsh::ProbeTable tab = table;
         if (keys) {
@@ -273,72 +153,77 @@ class HipBackend : public rsh::ScanBackend {
             tab.mask = ns - 1;
         }
         tiles_.clear();
+        ptiles_.clear();
         for (int64_t i = 0; i < count; ++i) rsh::probe_tiles(iv[i].a, iv[i].b, B_, (int32_t)i, &tiles_);
-        rsh::probe_partials(&tiles_, B_, &ptiles_);
+        rsh::probe_partials(&tiles_, 0, B_, 0, &ptiles_);
         rsh::ProbeIv* hiv = pin<rsh::ProbeIv>(c_->h_iv, count + 1);
         rsh::ProbeTile* ht = pin<rsh::ProbeTile>(c_->h_tiles, (int64_t)tiles_.size() + 1);
         rsh::PartialTile* hpt = pin<rsh::PartialTile>(c_->h_ptiles, (int64_t)ptiles_.size() + 1);
-        unsigned long long* hf = pin<unsigned long long>(c_->h_first, 1);
+        rsh::ProbeOut* hf = pin<rsh::ProbeOut>(c_->h_first, 1);
         uint8_t* hh = pin<uint8_t>(c_->h_hit, 16 + B_);
+        int32_t* hb = pin<int32_t>(c_->h_bucket, 2 + rsh::HIT_BUCKET_CAP + 1);  // + the request list {0}
+        rsh::ScanFile* F = file();
         ok(c_->partials.ensure((ptiles_.size() + 1) * sizeof(int4)));
-        // result slots preset to ~0 ("none") in batches: one memset per kFirstSlots probes
-        ok(c_->first.ensure(kFirstSlots * sizeof(unsigned long long)));
+        ok(c_->bucket.ensure((2 + rsh::HIT_BUCKET_CAP) * sizeof(int32_t)));
+        // result records preset ("none") in batches: one reset launch per kFirstSlots probes
+        ok(c_->first.ensure(kFirstSlots * sizeof(rsh::ProbeOut)));
         if (err != hipSuccess) return -1;
         if (c_->first_used % kFirstSlots == 0)
-            ok(hipMemsetAsync(c_->first.p, 0xFF, kFirstSlots * sizeof(unsigned long long), c_->stream));
-        unsigned long long* d_first = c_->first.as<unsigned long long>() + c_->first_used++ % kFirstSlots;
+            ok(rsh::launch_probe_out_reset(c_->first.as<rsh::ProbeOut>(), (uint32_t)kFirstSlots, c_->stream));
+        rsh::ProbeOut* d_first = c_->first.as<rsh::ProbeOut>() + c_->first_used++ % kFirstSlots;
         for (int64_t i = 0; i < count; ++i)
-            hiv[i] = rsh::ProbeIv{iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo & 0xFFFFu, iv[i].e_hi & 0xFFFFu};
+            hiv[i] = rsh::ProbeIv{iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo & 0xFFFFu, iv[i].e_hi & 0xFFFFu, 0, 0};
         if (!tiles_.empty()) memcpy(ht, tiles_.data(), tiles_.size() * sizeof(rsh::ProbeTile));
         if (!ptiles_.empty()) memcpy(hpt, ptiles_.data(), ptiles_.size() * sizeof(rsh::PartialTile));
+        F->aligned_weak = head ? c_->haw.as<int32_t>() : c_->src_weak.as<int32_t>();
+        F->slots = tab.slots;
+        F->mask = tab.mask;
+        F->out = d_first;
+        F->iv0 = 0;
+        F->niv = (int32_t)count;
+        F->bucket = c_->bucket.as<int32_t>();
+        F->hit = hh;
         if (head) {  // anchors T(kB) for the blocks these tiles sit in
             anchors_.clear();
             for (const rsh::ProbeTile& t : tiles_) {
                 const int64_t k = t.q0 / B_;
                 if (!haw_ready[(size_t)k]) {
                     haw_ready[(size_t)k] = 1;
-                    anchors_.push_back(k * B_);
+                    anchors_.push_back(rsh::GatherEnt{k * B_, 0, 1});
                 }
             }
             if (!anchors_.empty()) {
-                int64_t* hp = pin<int64_t>(c_->h_pos, (int64_t)anchors_.size());
+                rsh::GatherEnt* hp = pin<rsh::GatherEnt>(c_->h_pos, (int64_t)anchors_.size());
                 if (err != hipSuccess) return -1;
-                memcpy(hp, anchors_.data(), anchors_.size() * sizeof(int64_t));
-                ok(rsh::launch_window_weak(x_, n_, (uint32_t)B_, hp, (uint32_t)anchors_.size(), c_->haw.as<int32_t>(),
-                                           c_->stream, true));
+                memcpy(hp, anchors_.data(), anchors_.size() * sizeof(rsh::GatherEnt));
+                ok(rsh::launch_window_weak(F, hp, (uint32_t)anchors_.size(), nullptr, c_->stream));
             }
         }
         rsh::ProbeArgs A;
-        A.data = x_;
-        A.n = n_;
-        A.B = (uint32_t)B_;
-        A.aligned_weak = head ? c_->haw.as<int32_t>() : c_->src_weak.as<int32_t>();
-        A.table = tab;
+        A.files = F;
         A.ivs = hiv;
         A.tiles = ht;
-        A.first = d_first;
         A.partials = c_->partials.as<int4>();
-        ok(rsh::launch_probe_first(A, (uint32_t)tiles_.size(), hpt, (uint32_t)ptiles_.size(), c_->partials.as<int4>(),
-                                   c_->stream));
+        ok(rsh::launch_probe_first(A, (uint32_t)tiles_.size(), hpt, (uint32_t)ptiles_.size(), c_->stream));
         // the resolver's next questions at a hit are T(p), the bucket of the key that hit and (usually) the
         // MD5 of the window at p: answer them in this round trip
-        ok(c_->bucket.ensure((2 + rsh::HIT_BUCKET_CAP) * sizeof(int32_t)));
-        int32_t* hb = pin<int32_t>(c_->h_bucket, 2 + rsh::HIT_BUCKET_CAP);
-        if (err != hipSuccess) return -1;
-        ok(rsh::launch_hit_window(x_, n_, (uint32_t)B_, d_first, hiv, (int32_t)count, d_table_weak_, t_.chunk_count,
-                                  c_->bucket.as<int32_t>(), reinterpret_cast<int32_t*>(hh), hh + 16, c_->stream));
-        ok(hipMemcpyAsync(hf, d_first, sizeof(unsigned long long), hipMemcpyDeviceToHost, c_->stream));
+        int32_t* req = hb + 2 + rsh::HIT_BUCKET_CAP;
+        *req = 0;
+        ok(rsh::launch_hit_window(F, hiv, req, 1, t_.chunk_count, c_->stream));
+        ok(hipMemcpyAsync(hf, d_first, sizeof(rsh::ProbeOut), hipMemcpyDeviceToHost, c_->stream));
         ok(hipMemcpyAsync(hb, c_->bucket.p, (2 + rsh::HIT_BUCKET_CAP) * sizeof(int32_t), hipMemcpyDeviceToHost,
                           c_->stream));
         ok(hipStreamSynchronize(c_->stream));
-        if (*hf == ~0ull) return -1;
-        hit_pos_ = (int64_t)*hf;
-        hit_weak_ = *reinterpret_cast<const int32_t*>(hh);
+        if (count == 1) cache_.fill(iv[0], keys, *hf, n_ - B_);
+        else cache_.valid = false;
+        if (hf->first == ~0ull) return -1;
+        win_pos_ = t_pos_ = (int64_t)hf->first;
+        t_val_ = *reinterpret_cast<const int32_t*>(hh);
         if (hb[0] <= rsh::HIT_BUCKET_CAP) {  // ascending chunk order, as the Multimap keeps it
             std::sort(hb + 2, hb + 2 + hb[0]);
             t_.prime(hb[1], hb + 2, hb[0]);
         }
-        return hit_pos_;
+        return t_pos_;
     }
 
   private:
@@ -363,23 +248,24 @@ class HipBackend : public rsh::ScanBackend {
     uint8_t seed_[4];
     std::vector<rsh::ProbeTile> tiles_;
     std::vector<rsh::PartialTile> ptiles_;
-    std::vector<int64_t> anchors_;
-    int64_t hit_pos_ = -1;  // position of the last probe hit (its weak sum and window are on the host)
-    int32_t hit_weak_ = 0;
+    std::vector<rsh::GatherEnt> anchors_;
+    // the scan as a batch of one file for the probe / gather kernels (pinned, device-readable)
+    rsh::ScanFile* file() {
+        rsh::ScanFile* F = pin<rsh::ScanFile>(c_->h_files, 1);
+        if (err != hipSuccess) return F;
+        F->data = x_;
+        F->n = n_;
+        F->B = (uint32_t)B_;
+        F->aligned_weak = head ? c_->haw.as<int32_t>() : c_->src_weak.as<int32_t>();
+        F->table_weak = d_table_weak_;
+        F->C = t_.chunk_count;
+        return F;
+    }
+    int64_t win_pos_ = -1;  // position of the last probe's first hit: its window is on the host (h_hit)
+    int64_t t_pos_ = -1;    // position of the last hit returned: its weak sum t_val_ is known
+    int32_t t_val_ = 0;
+    HitCache cache_;
 };
-
-// Header consistency for the Generator side (3-arg ctor semantics, Checksum.java:94-113).
-int check_generator_header(int64_t n, const rsh_header* h) {
-    if (!h || n < 0) return RSH_E_INVAL;
-    if (h->block_length == 0) return (h->chunk_count == 0) ? RSH_OK : RSH_E_INVAL;
-    if (h->block_length < 0 || h->digest_length < 0 || h->digest_length > 16) return RSH_E_INVAL;
-    const int64_t B = h->block_length;
-    const int64_t rem = n % B;
-    const int64_t cc = n / B + (rem > 0 ? 1 : 0);
-    if (cc > 2147483647LL) return RSH_E_OVERFLOW;
-    if (cc != h->chunk_count || rem != h->remainder) return RSH_E_INVAL;
-    return RSH_OK;
-}
 
 // The device-resident Sender scan (everything but the whole-file MD5).  h validated by the caller;
 // n > 0, block_length > 0.  host_weak/host_strong may be null (then copied back from the device).
@@ -565,13 +451,6 @@ int emit_events(rsh_ctx* c, rsh::ResolveResult& r, rsh_event* ev, int64_t cap, i
     c->last_ev.clear();
     if (!r.ev.empty()) memcpy(ev, r.ev.data(), r.ev.size() * sizeof(rsh_event));
     return RSH_OK;
-}
-
-// Sender.skipMatchSendData (Sender.java:1386-1399): one sendDataFrom per 8 KiB FileView window.
-void skip_events(int64_t n, rsh::ResolveResult* r) {
-    for (int64_t s = 0; s < n; s += kDefaultBlock)
-        r->ev.push_back(rsh_event{s, std::min<int64_t>(kDefaultBlock, n - s), RSH_EV_LITERAL, 0, 0, 0});
-    r->literal = n;
 }
 
 }  // namespace

@@ -1,0 +1,190 @@
+// ctx.h -- internals shared by capi.cpp and batch.cpp (not part of the C-ABI): device / pinned buffers,
+// the rsh_ctx definition, error capture and the one-call-per-context claim.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <memory>
+#include <vector>
+
+#include "device.h"
+#include "hit_cache.h"
+#include "resolver.h"
+#include "rsync_hip.h"
+
+namespace rsh {
+struct BatchState;  // batch.cpp
+void destroy_batch_state(BatchState* b);
+}  // namespace rsh
+
+namespace rshi {
+
+constexpr int64_t kChunkSize = 8192;        // Sender.java:230 CHUNK_SIZE
+constexpr int64_t kDefaultBlock = 8192;     // FileView.java:38 DEFAULT_BLOCK_SIZE
+constexpr int32_t kMaxBlockLength = 1 << 17;  // Checksum.java:151
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, n ? n : 1);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// Page-locked host staging (true async D2H).
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipHostMalloc(&p, n ? n : 1, hipHostMallocDefault);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+inline uint32_t seed_word(const uint8_t seed[4]) {
+    return (uint32_t)seed[0] | ((uint32_t)seed[1] << 8) | ((uint32_t)seed[2] << 16) | ((uint32_t)seed[3] << 24);
+}
+
+inline uint32_t pow2_at_least(uint64_t v) {
+    uint32_t p = 64;
+    while (p < v) p <<= 1;
+    return p;
+}
+
+inline double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace rshi
+using namespace rshi;
+using rsh::HitCache;
+
+struct rsh_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf data, weak, strong;                   // host-input staging
+    DevBuf src_weak, src_strong, flags;          // aligned speculation over the source
+    DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw, partials, bucket;
+    hipStream_t aux = nullptr;                   // table download, then the aligned speculation
+    hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr;
+    PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
+    // resolver round trips: the small kernels read their inputs from and write their outputs to pinned
+    // host memory directly (no staging copies); the probe result and digest windows come back by copy
+    PinnedBuf h_pos, h_out, h_iv, h_tiles, h_keys, h_first, h_win, h_ptiles;
+    PinnedBuf h_hit;  // after a probe hit: T(p) (bytes 0..3) and the window at p (from byte 16)
+    PinnedBuf h_win0;    // window 0 of the current scan (its digest is computed on a host thread)
+    PinnedBuf h_bucket;  // after a probe hit: {count, key, chunk indices} of the key that hit
+    PinnedBuf h_files;   // the scan's rsh::ScanFile (a batch of one for the probe / gather kernels)
+    uint64_t first_used = 0;    // probe result slots handed out (see HipBackend::first_hit)
+    int* abort_word = nullptr;  // device, uncached: the speculation launch of generation g stops once it reads g
+    int gen = 0;
+    std::vector<rsh_event> last_ev;  // kept when the caller's event buffer was too small
+    std::atomic<bool> busy{false};   // the staging buffers and last_ev serve one call at a time
+    rsh::BatchState* batch = nullptr;  // buffers of the batched (multi-file) entry points, on first use
+    ~rsh_ctx() {
+        if (batch) rsh::destroy_batch_state(batch);
+        for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &slots, &dslots, &dkeys, &pos, &out,
+                          &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket})
+            b->release();
+        for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pos, &h_out, &h_iv, &h_tiles, &h_keys, &h_first,
+                             &h_win, &h_ptiles, &h_hit, &h_win0, &h_bucket, &h_files})
+            b->release();
+        if (abort_word) (void)hipFree(abort_word);
+        if (ev_in) (void)hipEventDestroy(ev_in);
+        if (ev_tab) (void)hipEventDestroy(ev_tab);
+        if (ev_spec) (void)hipEventDestroy(ev_spec);
+        if (aux) (void)hipStreamDestroy(aux);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+// Last HIP failure of the calling thread (rsh_last_error): error text and the capi.cpp line.
+inline thread_local char g_last_err[256] = "";
+inline void note_error(hipError_t e, int line, const char* file = "capi.cpp") {
+    snprintf(g_last_err, sizeof(g_last_err), "%s (%s:%d)", hipGetErrorString(e), file, line);
+}
+
+#define RSH_HIP(call)                                   \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) {                         \
+            note_error(e_, __LINE__);                   \
+            return RSH_E_DEVICE;                        \
+        }                                               \
+    } while (0)
+
+namespace rshi {
+
+// Claims a context for one call that uses its buffers; a second thread gets RSH_E_BUSY instead of
+// racing on them (one rsh_ctx per calling thread, rsync_hip.h).
+struct CtxClaim {
+    rsh_ctx* c;
+    bool held;
+    explicit CtxClaim(rsh_ctx* ctx) : c(ctx), held(!ctx->busy.exchange(true, std::memory_order_acquire)) {}
+    ~CtxClaim() {
+        if (held) c->busy.store(false, std::memory_order_release);
+    }
+};
+
+#define RSH_CLAIM(ctx)                                                                   \
+    CtxClaim claim_(ctx);                                                                \
+    if (!claim_.held) {                                                                  \
+        snprintf(g_last_err, sizeof(g_last_err), "context in use by another thread");   \
+        return RSH_E_BUSY;                                                               \
+    }
+
+// Header consistency for the Generator side (3-arg ctor semantics, Checksum.java:94-113).
+inline int check_generator_header(int64_t n, const rsh_header* h) {
+    if (!h || n < 0) return RSH_E_INVAL;
+    if (h->block_length == 0) return (h->chunk_count == 0) ? RSH_OK : RSH_E_INVAL;
+    if (h->block_length < 0 || h->digest_length < 0 || h->digest_length > 16) return RSH_E_INVAL;
+    const int64_t B = h->block_length;
+    const int64_t rem = n % B;
+    const int64_t cc = n / B + (rem > 0 ? 1 : 0);
+    if (cc > 2147483647LL) return RSH_E_OVERFLOW;
+    if (cc != h->chunk_count || rem != h->remainder) return RSH_E_INVAL;
+    return RSH_OK;
+}
+
+// Sender.skipMatchSendData (Sender.java:1386-1399): one sendDataFrom per 8 KiB FileView window.
+inline void skip_events(int64_t n, rsh::ResolveResult* r) {
+    for (int64_t s = 0; s < n; s += kDefaultBlock)
+        r->ev.push_back(rsh_event{s, std::min<int64_t>(kDefaultBlock, n - s), RSH_EV_LITERAL, 0, 0, 0});
+    r->literal = n;
+}
+
+}  // namespace rshi

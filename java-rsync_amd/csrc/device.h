@@ -5,6 +5,8 @@
 
 #include <vector>
 
+#include "hit_cache.h"
+
 namespace rsh {
 
 // Generator block sums (Generator.java:886-895): chunk c covers [c*B, min((c+1)*B, n)).
@@ -18,6 +20,37 @@ hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint3
 hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks,
                                      uint32_t dl, uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong,
                                      hipStream_t s, const int* abort_flag = nullptr, int abort_gen = 0);
+
+// Batched files (a segment's files in one launch; Generator.java:558-614 / Sender.sendFiles :1098-1148).
+// K1File: one file's chunk set.  plan_block_sums_batch cuts every file into waves of 64 chunks: the
+// pipelined coalesced K1 (K1Group: 64 full-length chunks, B % 128 == 0, 512 <= B <= 128 KiB, 16-B aligned
+// data) and one lane per chunk for the rest (K1Lane: the file's tail group, or every chunk of a file
+// whose shape the coalesced kernel does not take).  The descriptors must be device-readable.
+struct K1File {
+    const uint8_t* data;
+    int64_t n;
+    uint32_t B, dl, nchunks;
+    int32_t* weak;
+    uint8_t* strong;
+};
+struct K1Group {
+    const uint8_t* data;  // chunk 0 of the group
+    int32_t* weak;        // its output slots
+    uint8_t* strong;
+    uint32_t B, dl;
+};
+struct K1Lane {
+    const uint8_t* data;  // the file
+    int64_t n;
+    int32_t* weak;        // the file's output arrays
+    uint8_t* strong;
+    uint32_t B, dl, c_first, nchunks;
+};
+void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Group>* groups,
+                           std::vector<K1Lane>* lanes, int* lane_align);
+hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
+                                   int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag = nullptr,
+                                   int abort_gen = 0);
 
 // Chain flags for the Sender fast path: flag[k] = 1 iff source window k (aligned, from the source's
 // own block sums) has the same weak key and the same dl-byte digest as basis chunk k.
@@ -38,12 +71,33 @@ hipError_t launch_table_insert(unsigned long long* d_slots, uint32_t mask, const
 // the true weak sum of window [p, p + min(B, n - p)) and E(p) = (e_lo, e_hi + e_lo * (min(p, n-B) -
 // min(anchor, n-B))) mod 2^16 (the post-flush desync of Sender.java:1292-1310).  The work is cut into
 // tiles of PROBE_TILE positions inside aligned blocks [kB, kB + B); aligned_weak[k] = T(kB) (the
-// source's own block sums) anchors each block.  *first (uint64, preset to ~0 by the caller) receives
-// the smallest hitting position over all tiles.
+// source's own block sums) anchors each block.  The file's ProbeOut receives the smallest hitting position
+// over all its tiles and the list of hits.
+//
+// One launch serves a batch of files (a round of the batched Sender, or a single scan as a batch of one):
+// every interval names its file, and a file's per-scan state is a ScanFile in device-readable memory.
 constexpr int PROBE_TILE = 4096;
+constexpr int HIT_BUCKET_CAP = 256;
+struct ScanFile {
+    const uint8_t* data;
+    int64_t n;
+    uint32_t B;
+    uint32_t mask;                    // the round's probe key set: slots[0 .. mask]
+    const unsigned long long* slots;
+    int32_t* aligned_weak;            // T(kB) anchors (the speculation's weak sums, or head-mode window sums)
+    ProbeOut* out;                    // probe result (device)
+    const int32_t* table_weak;        // the received table's weak sums (device), C entries
+    int32_t C;
+    int32_t iv0, niv;                 // the file's intervals in the round's ProbeIv array
+    int32_t pad;
+    int32_t* bucket;                  // device: {count, key, idx[0 .. HIT_BUCKET_CAP)}
+    uint8_t* hit;                     // pinned host: T(p) in bytes 0..3, the window at p from byte 16
+};
 struct ProbeIv {
     int64_t a, b, anchor;
     uint32_t e_lo, e_hi;
+    int32_t file;
+    int32_t pad;
 };
 struct ProbeTile {
     int64_t q0;     // tile start (multiple of PROBE_TILE from its block start)
@@ -55,46 +109,76 @@ struct ProbeTile {
 // gets each tile's block prefix from at most 31 partials instead of re-reading up to B bytes per tile.
 struct PartialTile {
     int64_t q0;
+    int32_t file;
+    int32_t pad;
 };
 struct ProbeArgs {
-    const uint8_t* data;
-    int64_t n;
-    uint32_t B;
-    const int32_t* aligned_weak;
-    ProbeTable table;
+    const ScanFile* files;
     const ProbeIv* ivs;
     const ProbeTile* tiles;
-    const int4* partials;  // written by pass 1
-    unsigned long long* first;
+    int4* partials;  // written by pass 1
 };
 // Appends the tiles covering [a, b) for interval `iv` (host side).
 void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeTile>* out);
-// Assigns ProbeTile::pbase and lists the partial tiles pass 1 computes (host side).
-void probe_partials(std::vector<ProbeTile>* tiles, int64_t B, std::vector<PartialTile>* out);
+// Assigns ProbeTile::pbase for tiles[t0 ..] (one file's tiles, ascending) and appends the partial tiles
+// pass 1 computes for them (host side).
+void probe_partials(std::vector<ProbeTile>* tiles, size_t t0, int64_t B, int32_t file, std::vector<PartialTile>* out);
 // Both passes, back to back on stream s.
-hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const PartialTile* d_ptiles, uint32_t nptiles,
-                              int4* d_partials, hipStream_t s);
-// After a probe: if *d_first holds a position p, the resolver's next questions answered in the same
-// round trip, on stream s: the true weak sum T(p) into *h_weak, the window [p, p + min(B, n - p)) into
-// pinned host memory h_win, and the bucket of the key R(p) = T(p) + E(p) (E from the interval holding
-// p) in the received table d_table_weak[C]: *d_bucket = {count, key, idx[0 .. min(count, cap))}, in
-// no particular order.
-constexpr int HIT_BUCKET_CAP = 256;
-hipError_t launch_hit_window(const uint8_t* d_data, int64_t n, uint32_t B, const unsigned long long* d_first,
-                             const ProbeIv* ivs, int32_t niv, const int32_t* d_table_weak, int32_t C,
-                             int32_t* d_bucket, int32_t* h_weak, uint8_t* h_win, hipStream_t s);
+hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const PartialTile* ptiles, uint32_t nptiles,
+                              hipStream_t s);
+// After a probe, for each file req[r] (r < nreq) whose *first holds a position p: the resolver's next
+// questions answered in the same round trip: the true weak sum T(p) and the window [p, p + min(B, n - p))
+// into the file's pinned `hit` buffer, and the bucket of the key R(p) = T(p) + E(p) (E from the interval
+// holding p) in the received table: bucket = {count, key, idx[0 .. min(count, cap))}, in no particular
+// order.  max_C: the largest C among the files.
+hipError_t launch_hit_window(const ScanFile* files, const ProbeIv* ivs, const int32_t* req, int32_t nreq, int32_t max_C,
+                             hipStream_t s);
 
+// Presets n ProbeOut records (first = ~0, count = 0).
+hipError_t launch_probe_out_reset(ProbeOut* d_out, uint32_t n, hipStream_t s);
+
+// Small gathers for a batch of files (pinned-host or device entries; outputs in device-readable memory).
+struct GatherEnt {
+    int64_t p;
+    int32_t file;
+    int32_t by_block;  // window_weak: 1 = write files[file].aligned_weak[p / B] instead of out[i]
+};
+// Bytes at arbitrary positions: out[i] = files[e.file].data[e.p].
+hipError_t launch_gather_bytes(const ScanFile* files, const GatherEnt* ents, uint32_t n, uint8_t* out, hipStream_t s);
+// True weak sums at arbitrary positions: Rolling.compute(data + p, min(B, n - p)).
+hipError_t launch_window_weak(const ScanFile* files, const GatherEnt* ents, uint32_t n, int32_t* out, hipStream_t s);
+// Many device ranges into pinned host memory (or device memory), one kernel.
+struct CopyEnt {
+    const uint8_t* src;
+    uint8_t* dst;
+    int64_t len;
+};
+hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hipStream_t s);
 // n bytes of device memory into pinned host memory (h_dst 16-byte aligned), by a kernel.
 hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s);
-
-// Bytes at arbitrary positions.
-hipError_t launch_gather_bytes(const uint8_t* d_data, const int64_t* d_pos, uint32_t npos, uint8_t* d_out,
-                               hipStream_t s);
-
-// True weak sums at arbitrary positions: out[i] = Rolling.compute(data + pos[i], min(B, n - pos[i]))
-// (by_block: written to out[pos[i] / B] instead, for aligned positions).
-hipError_t launch_window_weak(const uint8_t* d_data, int64_t n, uint32_t B, const int64_t* d_pos, uint32_t npos,
-                              int32_t* d_out, hipStream_t s, bool by_block = false);
+// Probe hashes of many files (slots cleared by the caller): keys[i] into slots/mask.
+struct TableEnt {
+    unsigned long long* slots;
+    const int32_t* keys;
+    uint32_t mask;
+    int32_t nkeys;
+};
+hipError_t launch_table_insert_many(const TableEnt* ents, uint32_t n, int32_t max_keys, hipStream_t s);
+// Chain flags of many files.
+struct FlagEnt {
+    const int32_t* wsrc;
+    const uint8_t* ssrc;
+    const int32_t* wbas;
+    const uint8_t* sbas;
+    uint8_t* flags;
+    uint32_t count, dl;
+};
+hipError_t launch_chain_flags_many(const FlagEnt* ents, uint32_t n, uint32_t max_count, hipStream_t s);
+// Host mirror of the device probe hash (key sets built on the host, e.g. the stale-digest keys).
+inline uint32_t slot_hash_host(uint32_t key) {
+    const uint32_t h = key * 0x9E3779B1u;
+    return h ^ (h >> 15);
+}
 
 // splitmix64 counter stream (bench input): byte i = byte (i % 8) of mix(key + (i / 8 + 1) * golden).
 hipError_t launch_fill_splitmix(uint8_t* d_out, int64_t n, uint64_t key, int64_t byte_offset, hipStream_t s);

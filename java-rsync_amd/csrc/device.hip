@@ -120,12 +120,9 @@ __device__ __forceinline__ void load_block(const uint8_t* p, uint4 (&q)[4]) {
 // of in-flight loads so HBM latency hides behind the MD5 rounds of the blocks already loaded.
 // ------------------------------------------------------------------------------------------------
 template <int ALIGN, int PF, bool NT = true>
-__global__ __launch_bounds__(64) void block_sums_kernel(const uint8_t* __restrict__ data, int64_t n, uint32_t B,
-                                                        uint32_t nchunks, uint32_t dl, uint32_t seed,
-                                                        int32_t* __restrict__ weak_out,
-                                                        uint8_t* __restrict__ strong_out, uint32_t c_first) {
-    const uint32_t c = c_first + blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nchunks) return;
+__device__ __forceinline__ void lane_chunk_sums(const uint8_t* __restrict__ data, int64_t n, uint32_t B, uint32_t c,
+                                                uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
+                                                uint8_t* __restrict__ strong_out) {
     const int64_t base = (int64_t)c * B;
     const int64_t rem = n - base;
     const uint32_t L = rem < (int64_t)B ? (uint32_t)rem : B;
@@ -174,6 +171,25 @@ __global__ __launch_bounds__(64) void block_sums_kernel(const uint8_t* __restric
         const uint32_t word = k < 4 ? st.a : k < 8 ? st.b : k < 12 ? st.c : st.d;
         o[k] = (uint8_t)(word >> (8 * (k & 3)));
     }
+}
+
+template <int ALIGN, int PF, bool NT = true>
+__global__ __launch_bounds__(64) void block_sums_kernel(const uint8_t* __restrict__ data, int64_t n, uint32_t B,
+                                                        uint32_t nchunks, uint32_t dl, uint32_t seed,
+                                                        int32_t* __restrict__ weak_out,
+                                                        uint8_t* __restrict__ strong_out, uint32_t c_first) {
+    const uint32_t c = c_first + blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks) return;
+    lane_chunk_sums<ALIGN, PF, NT>(data, n, B, c, dl, seed, weak_out, strong_out);
+}
+
+// Batched files, one lane per chunk: wave w takes chunks [c_first, c_first + 64) of lanes[w]'s file.
+template <int ALIGN>
+__global__ __launch_bounds__(64) void block_sums_lane_batch_kernel(const K1Lane* __restrict__ lanes, uint32_t seed) {
+    const K1Lane e = lanes[blockIdx.x];
+    const uint32_t c = e.c_first + threadIdx.x;
+    if (c >= e.nchunks) return;
+    lane_chunk_sums<ALIGN, ALIGN == 16 ? 4 : ALIGN == 4 ? 2 : 1>(e.data, e.n, e.B, c, e.dl, seed, e.weak, e.strong);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -430,17 +446,30 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 
 // amdgpu_num_vgpr(192): two waves fill 384 of a SIMD's 512 registers, leaving room for one wave of the
 // resolver's range probe (104) to run beside the Sender's speculation launch in head mode.
-template <int MD5F, bool ABORT, bool PIN, int MODE = 0>
+// MULTI (batched files, K1Group per wave): the wave's 64 chunks, B, dl and output slots come from
+// groups[blockIdx.x] instead of (data, B, dl, weak_out, strong_out) + blockIdx.x * 64 chunks.
+template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void block_sums_pipe_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
                                                              uint8_t* __restrict__ strong_out,
-                                                             const int* abort_flag = nullptr, int abort_gen = 0) {
+                                                             const int* abort_flag = nullptr, int abort_gen = 0,
+                                                             const K1Group* __restrict__ groups = nullptr) {
     constexpr int ROW = 9;
     constexpr int BUF = 64 * ROW;  // uint4 slots per LDS buffer
     if constexpr (PIN) asm volatile("; occupancy pin" ::: "v175");
     extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // 2 buffers (sized at launch)
     const int l = threadIdx.x;
-    const uint32_t c0 = blockIdx.x * 64u;
+    uint32_t c0 = blockIdx.x * 64u;
+    const uint8_t* gdata = data + (size_t)c0 * B;
+    if constexpr (MULTI) {
+        const K1Group g = groups[blockIdx.x];
+        gdata = g.data;
+        B = g.B;
+        dl = g.dl;
+        weak_out = g.weak;
+        strong_out = g.strong;
+        c0 = 0;
+    }
     const uint32_t nst = B >> 7;  // host guarantees nst >= 4
     const int wr0 = (l >> 3) * ROW + (l & 7);
     const int rd0 = l * ROW;
@@ -471,7 +500,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void bl
     // Buffer loads: the wave's 64 chunks (64 * B <= 8 MiB) behind one descriptor, a 32-bit lane offset and
     // a scalar offset per 8-chunk row j -- one VGPR of addressing instead of eight 64-bit pointers.
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(data) + (size_t)c0 * B, 0, (int)(64 * B), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(gdata), 0, (int)(64 * B), 0x00020000);
     const uint32_t lane_off = (uint32_t)(l >> 3) * B + 16u * (uint32_t)(l & 7);
     auto load = [&](uint4 (&dst)[8], uint32_t stg) __attribute__((always_inline)) {
 #pragma unroll
@@ -970,6 +999,53 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
     return hipGetLastError();
 }
 
+void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Group>* groups,
+                           std::vector<K1Lane>* lanes, int* lane_align) {
+    groups->clear();
+    lanes->clear();
+    *lane_align = 16;
+    for (int32_t f = 0; f < nfiles; ++f) {
+        const K1File& F = files[f];
+        if (F.nchunks == 0 || F.B == 0) continue;
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(F.data);
+        const uint32_t nst = F.B >> 7;
+        uint32_t c = 0;
+        if ((F.B % 128) == 0 && nst >= 4 && nst <= 1024 && (addr % 16) == 0) {  // the pipelined K1's shape
+            const uint32_t nfullc = (uint32_t)std::min<int64_t>(F.n / F.B, F.nchunks);
+            for (; c + 64 <= nfullc; c += 64)
+                groups->push_back(K1Group{F.data + (size_t)c * F.B, F.weak + c, F.strong + (size_t)c * F.dl, F.B, F.dl});
+        }
+        for (; c < F.nchunks; c += 64) {
+            lanes->push_back(K1Lane{F.data, F.n, F.weak, F.strong, F.B, F.dl, c, F.nchunks});
+            const int a = ((F.B % 16) == 0 && (addr % 16) == 0) ? 16 : ((F.B % 4) == 0 && (addr % 4) == 0) ? 4 : 1;
+            *lane_align = std::min(*lane_align, a);
+        }
+    }
+}
+
+hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
+                                   int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag,
+                                   int abort_gen) {
+    const size_t lb = 2 * 64 * 9 * sizeof(uint4);
+    if (ngroups > 0) {
+        if (abort_flag)
+            hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, false, 0, true>), dim3(ngroups), dim3(64), lb, s,
+                               nullptr, 0u, 0u, seed_word, nullptr, nullptr, abort_flag, abort_gen, d_groups);
+        else
+            hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, false, 0, true>), dim3(ngroups), dim3(64), lb, s,
+                               nullptr, 0u, 0u, seed_word, nullptr, nullptr, nullptr, 0, d_groups);
+    }
+    if (nlanes > 0) {
+        if (lane_align == 16)
+            hipLaunchKernelGGL((block_sums_lane_batch_kernel<16>), dim3(nlanes), dim3(64), 0, s, d_lanes, seed_word);
+        else if (lane_align == 4)
+            hipLaunchKernelGGL((block_sums_lane_batch_kernel<4>), dim3(nlanes), dim3(64), 0, s, d_lanes, seed_word);
+        else
+            hipLaunchKernelGGL((block_sums_lane_batch_kernel<1>), dim3(nlanes), dim3(64), 0, s, d_lanes, seed_word);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks, uint32_t dl,
                              uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s,
                              const int* abort_flag, int abort_gen) {
@@ -1214,9 +1290,12 @@ __device__ __forceinline__ int32_t sbyte_of(const uint32_t (&w)[4], int i) {
 __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A) {
     __builtin_amdgcn_s_setprio(3);  // resolver latency path: ahead of a co-running speculation launch
     __shared__ int32_t sh[4 * PROBE_THREADS / 64];
-    const int64_t n = A.n, B = A.B;
     const ProbeTile tile = A.tiles[blockIdx.x];
     const ProbeIv I = A.ivs[tile.iv];
+    const ScanFile& F = A.files[I.file];
+    const int64_t n = F.n, B = F.B;
+    const uint8_t* __restrict__ data = F.data;
+    const ProbeTable table{F.slots, F.mask};
     const int64_t k = tile.q0 / B;
     const int64_t o = k * B;
     const int64_t q0 = tile.q0;
@@ -1241,8 +1320,8 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A)
     const int t = threadIdx.x;
     const int64_t p0 = q0 + (int64_t)t * PROBE_PPT;
     uint32_t xa[4], xb[4];
-    load16(A.data, n, p0, xa);
-    load16(A.data, n, p0 + B, xb);
+    load16(data, n, p0, xa);
+    load16(data, n, p0 + B, xb);
     int32_t part[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -1259,7 +1338,7 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A)
 
     const uint32_t pa = (uint32_t)(head[0] + pre[0]), pa2 = (uint32_t)(head[1] + pre[1]);  // P1(p0), P2(p0)
     const uint32_t pb = (uint32_t)(head[2] + pre[2]), pb2 = (uint32_t)(head[3] + pre[3]);  // sums over [o+B, p0+B)
-    const int32_t To = A.aligned_weak[k];
+    const int32_t To = F.aligned_weak[k];
     const int64_t e0 = (o + B < n ? o + B : n);
     const uint32_t s1o = (uint32_t)To & 0xFFFFu, s2o = (uint32_t)To >> 16;
     const uint32_t P1e = s1o + pb;
@@ -1285,7 +1364,7 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A)
     }
     unsigned long long sl[PROBE_PPT];
 #pragma unroll
-    for (int i = 0; i < PROBE_PPT; ++i) sl[i] = A.table.slots[slot_hash(key[i]) & A.table.mask];
+    for (int i = 0; i < PROBE_PPT; ++i) sl[i] = table.slots[slot_hash(key[i]) & table.mask];
 #pragma unroll
     for (int i = 0; i < PROBE_PPT; ++i) {
         const int64_t p = p0 + i;
@@ -1293,58 +1372,81 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A)
         if (p < I.a) continue;
         const unsigned long long v = (1ull << 32) | key[i];
         bool hit = sl[i] == v;
-        if (!hit && sl[i] != 0ull) hit = table_has(A.table, key[i]);
+        if (!hit && sl[i] != 0ull) hit = table_has(table, key[i]);
         if (hit) {
-            atomicMin(A.first, (unsigned long long)p);
-            return;
+            atomicMin(&F.out->first, (unsigned long long)p);
+            const unsigned long long at = atomicAdd(&F.out->count, 1ull);
+            if (at < (unsigned long long)PROBE_HITS_CAP) {
+                F.out->pos[at] = (unsigned long long)p;
+                F.out->key[at] = key[i];
+            }
         }
     }
 }
 
+__global__ void probe_out_reset_kernel(ProbeOut* out, uint32_t n) {
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        out[i].first = ~0ull;
+        out[i].count = 0ull;
+    }
+}
+
+hipError_t launch_probe_out_reset(ProbeOut* d_out, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(probe_out_reset_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d_out, n);
+    return hipGetLastError();
+}
+
 // Pass 1: one workgroup per partial tile [q0, min(q0 + PROBE_TILE, o + B)), o = its block start.
-__global__ __launch_bounds__(256) void probe_partials_kernel(const uint8_t* __restrict__ data, int64_t n, uint32_t B,
+__global__ __launch_bounds__(256) void probe_partials_kernel(const ScanFile* __restrict__ files,
                                                              const PartialTile* __restrict__ pt,
                                                              int4* __restrict__ out) {
     __builtin_amdgcn_s_setprio(3);
     __shared__ int32_t sh[4 * 256 / 64];
-    const int64_t q0 = pt[blockIdx.x].q0;
+    const PartialTile t = pt[blockIdx.x];
+    const ScanFile& F = files[t.file];
+    const int64_t B = F.B, q0 = t.q0;
     const int64_t o = q0 / B * B;
     const int64_t qe = q0 + PROBE_TILE < o + B ? q0 + PROBE_TILE : o + B;
     int32_t v[4] = {0, 0, 0, 0};
-    range_sums(data, n, q0, qe, o, v[0], v[1]);
-    range_sums(data, n, q0 + B, qe + B, o, v[2], v[3]);
+    range_sums(F.data, F.n, q0, qe, o, v[0], v[1]);
+    range_sums(F.data, F.n, q0 + B, qe + B, o, v[2], v[3]);
     block_reduce<4>(v, sh);
     if (threadIdx.x == 0) out[blockIdx.x] = make_int4(v[0], v[1], v[2], v[3]);
 }
 
-void probe_partials(std::vector<ProbeTile>* tiles, int64_t B, std::vector<PartialTile>* out) {
-    out->clear();
+void probe_partials(std::vector<ProbeTile>* tiles, size_t t0, int64_t B, int32_t file, std::vector<PartialTile>* out) {
     int64_t cur_block = -1, covered = 0;  // tiles of cur_block already listed: [0, covered)
     int32_t base = 0;
-    for (ProbeTile& t : *tiles) {
+    for (size_t i = t0; i < tiles->size(); ++i) {
+        ProbeTile& t = (*tiles)[i];
         const int64_t k = t.q0 / B;
         const int64_t ti = (t.q0 - k * B) / PROBE_TILE;
-        if (k != cur_block) {  // tiles arrive in increasing position order
+        if (k != cur_block) {  // one file's tiles arrive in increasing position order
             cur_block = k;
             covered = 0;
             base = (int32_t)out->size();
         }
-        for (; covered < ti; ++covered) out->push_back(PartialTile{k * B + covered * PROBE_TILE});
+        for (; covered < ti; ++covered) out->push_back(PartialTile{k * B + covered * PROBE_TILE, file, 0});
         t.pbase = base;
     }
 }
 
-__global__ __launch_bounds__(256) void hit_window_kernel(const uint8_t* __restrict__ data, int64_t n, uint32_t B,
-                                                         const unsigned long long* __restrict__ first,
-                                                         const ProbeIv* __restrict__ ivs, int32_t niv,
-                                                         int32_t* __restrict__ d_bucket, int32_t* __restrict__ h_weak,
-                                                         uint8_t* __restrict__ h_win) {
+// grid (1 + 16, nreq): block 0 computes T(p) and the key, blocks 1..16 copy the window.
+__global__ __launch_bounds__(256) void hit_window_kernel(const ScanFile* __restrict__ files,
+                                                         const ProbeIv* __restrict__ ivs,
+                                                         const int32_t* __restrict__ req) {
     __builtin_amdgcn_s_setprio(3);
     __shared__ int32_t sh[2 * 256 / 64];
-    const unsigned long long f = *first;
+    const ScanFile& F = files[req[blockIdx.y]];
+    const unsigned long long f = F.out->first;
     if (f == ~0ull) return;
+    const int64_t n = F.n, B = F.B;
+    const uint8_t* __restrict__ data = F.data;
     const int64_t p = (int64_t)f;
-    const int64_t w = (n - p < (int64_t)B ? n - p : (int64_t)B);
+    const int64_t w = (n - p < B ? n - p : B);
     if (blockIdx.x == 0) {
         int32_t v[2] = {0, 0};
         range_sums(data, n, p, p + w, p, v[0], v[1]);
@@ -1353,9 +1455,9 @@ __global__ __launch_bounds__(256) void hit_window_kernel(const uint8_t* __restri
             const uint32_t S1 = (uint32_t)v[0];
             const uint32_t S2 = (uint32_t)w * S1 - (uint32_t)v[1];
             const int32_t T = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
-            *h_weak = T;
-            // the interval holding p (disjoint, ascending) gives E(p); R = T + E is the key that hit
-            int32_t lo = 0, hi = niv - 1;
+            *reinterpret_cast<int32_t*>(F.hit) = T;
+            // the file's interval holding p (disjoint, ascending) gives E(p); R = T + E is the key that hit
+            int32_t lo = F.iv0, hi = F.iv0 + F.niv - 1;
             while (lo < hi) {
                 const int32_t mid = (lo + hi + 1) / 2;
                 if (ivs[mid].a <= p) lo = mid;
@@ -1365,11 +1467,12 @@ __global__ __launch_bounds__(256) void hit_window_kernel(const uint8_t* __restri
             const int64_t nb = n - B;
             const int64_t cp = p < nb ? p : nb, ca = I.anchor < nb ? I.anchor : nb;
             const uint32_t ehi = I.e_hi + I.e_lo * (uint32_t)(cp - ca);
-            d_bucket[0] = 0;
-            d_bucket[1] = (int32_t)((((uint32_t)T + I.e_lo) & 0xFFFFu) | ((((uint32_t)T >> 16) + ehi) << 16));
+            F.bucket[0] = 0;
+            F.bucket[1] = (int32_t)((((uint32_t)T + I.e_lo) & 0xFFFFu) | ((((uint32_t)T >> 16) + ehi) << 16));
         }
         return;
     }
+    uint8_t* __restrict__ h_win = F.hit + 16;
     for (int64_t o = 16 * ((int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x); o < w;
          o += 16 * (int64_t)(gridDim.x - 1) * blockDim.x) {
         if (o + 16 <= w) {
@@ -1383,32 +1486,34 @@ __global__ __launch_bounds__(256) void hit_window_kernel(const uint8_t* __restri
     }
 }
 
-// The bucket of the hit key: chunk indices i with weak[i] == key (8 per lane).
-__global__ __launch_bounds__(256) void hit_bucket_kernel(const unsigned long long* __restrict__ first,
-                                                         const int32_t* __restrict__ weak, int32_t C,
-                                                         int32_t* __restrict__ d_bucket) {
+// The bucket of the hit key: chunk indices i with weak[i] == key (8 per lane); grid (., nreq).
+__global__ __launch_bounds__(256) void hit_bucket_kernel(const ScanFile* __restrict__ files,
+                                                         const int32_t* __restrict__ req) {
     __builtin_amdgcn_s_setprio(3);
-    if (*first == ~0ull) return;
-    const int32_t key = d_bucket[1];
+    const ScanFile& F = files[req[blockIdx.y]];
+    if (F.out->first == ~0ull) return;
+    const int32_t C = F.C;
     const int32_t i0 = 8 * (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i0 >= C) return;
+    const int32_t key = F.bucket[1];
+    const int32_t* __restrict__ weak = F.table_weak;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int32_t i = i0 + k;
         if (i < C && weak[i] == key) {
-            const int32_t at = atomicAdd(&d_bucket[0], 1);
-            if (at < HIT_BUCKET_CAP) d_bucket[2 + at] = i;
+            const int32_t at = atomicAdd(&F.bucket[0], 1);
+            if (at < HIT_BUCKET_CAP) F.bucket[2 + at] = i;
         }
     }
 }
 
-hipError_t launch_hit_window(const uint8_t* d_data, int64_t n, uint32_t B, const unsigned long long* d_first,
-                             const ProbeIv* ivs, int32_t niv, const int32_t* d_table_weak, int32_t C,
-                             int32_t* d_bucket, int32_t* h_weak, uint8_t* h_win, hipStream_t s) {
-    hipLaunchKernelGGL(hit_window_kernel, dim3(1 + 16), dim3(256), 0, s, d_data, n, B, d_first, ivs, niv, d_bucket,
-                       h_weak, h_win);
-    if (C > 0)
-        hipLaunchKernelGGL(hit_bucket_kernel, dim3((uint32_t)((C + 8 * 256 - 1) / (8 * 256))), dim3(256), 0, s, d_first,
-                           d_table_weak, C, d_bucket);
+hipError_t launch_hit_window(const ScanFile* files, const ProbeIv* ivs, const int32_t* req, int32_t nreq, int32_t max_C,
+                             hipStream_t s) {
+    if (nreq <= 0) return hipSuccess;
+    hipLaunchKernelGGL(hit_window_kernel, dim3(1 + 16, (uint32_t)nreq), dim3(256), 0, s, files, ivs, req);
+    if (max_C > 0)
+        hipLaunchKernelGGL(hit_bucket_kernel, dim3((uint32_t)((max_C + 8 * 256 - 1) / (8 * 256)), (uint32_t)nreq),
+                           dim3(256), 0, s, files, req);
     return hipGetLastError();
 }
 
@@ -1423,38 +1528,36 @@ void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeT
     }
 }
 
-hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const PartialTile* d_ptiles, uint32_t nptiles,
-                              int4* d_partials, hipStream_t s) {
+hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const PartialTile* ptiles, uint32_t nptiles,
+                              hipStream_t s) {
     if (ntiles == 0) return hipSuccess;
     if (nptiles > 0)
-        hipLaunchKernelGGL(probe_partials_kernel, dim3(nptiles), dim3(256), 0, s, args.data, args.n, args.B, d_ptiles,
-                           d_partials);
+        hipLaunchKernelGGL(probe_partials_kernel, dim3(nptiles), dim3(256), 0, s, args.files, ptiles, args.partials);
     hipLaunchKernelGGL(probe_first_kernel, dim3(ntiles), dim3(PROBE_THREADS), 0, s, args);
     return hipGetLastError();
 }
 
-__global__ void gather_bytes_kernel(const uint8_t* __restrict__ data, const int64_t* __restrict__ pos, uint32_t npos,
+__global__ void gather_bytes_kernel(const ScanFile* __restrict__ files, const GatherEnt* __restrict__ ents, uint32_t n,
                                     uint8_t* __restrict__ out) {
     __builtin_amdgcn_s_setprio(3);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < npos) out[i] = data[pos[i]];
+    if (i < n) {
+        const GatherEnt e = ents[i];
+        out[i] = files[e.file].data[e.p];
+    }
 }
 
-hipError_t launch_gather_bytes(const uint8_t* d_data, const int64_t* d_pos, uint32_t npos, uint8_t* d_out,
-                               hipStream_t s) {
-    if (npos == 0) return hipSuccess;
-    hipLaunchKernelGGL(gather_bytes_kernel, dim3((npos + 255) / 256), dim3(256), 0, s, d_data, d_pos, npos, d_out);
+hipError_t launch_gather_bytes(const ScanFile* files, const GatherEnt* ents, uint32_t n, uint8_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_bytes_kernel, dim3((n + 255) / 256), dim3(256), 0, s, files, ents, n, out);
     return hipGetLastError();
 }
 
 // Device bytes -> pinned host memory, as a kernel: the runtime's copy path can queue behind a
 // co-running speculation launch, a high-priority kernel does not.  Thread t assembles bytes
-// [16t, 16t + 16) and writes them with one 16-byte store.
-__global__ __launch_bounds__(256) void copy_to_host_kernel(const uint8_t* __restrict__ src, int64_t n,
-                                                           uint8_t* __restrict__ dst) {
-    __builtin_amdgcn_s_setprio(3);
-    const int64_t o = 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-    if (o >= n) return;
+// [16t, 16t + 16) and writes them with one 16-byte store (dst 16-byte aligned).
+__device__ __forceinline__ void copy_piece(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int64_t n,
+                                           int64_t o) {
     if (o + 16 <= n) {
         uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -1465,6 +1568,13 @@ __global__ __launch_bounds__(256) void copy_to_host_kernel(const uint8_t* __rest
     }
 }
 
+__global__ __launch_bounds__(256) void copy_to_host_kernel(const uint8_t* __restrict__ src, int64_t n,
+                                                           uint8_t* __restrict__ dst) {
+    __builtin_amdgcn_s_setprio(3);
+    const int64_t o = 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (o < n) copy_piece(src, dst, n, o);
+}
+
 hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int64_t threads = (n + 15) / 16;
@@ -1472,30 +1582,87 @@ hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, 
     return hipGetLastError();
 }
 
+// grid (., n): entry blockIdx.y, 16 bytes per thread, grid-strided over the entry's length
+__global__ __launch_bounds__(256) void copy_many_kernel(const CopyEnt* __restrict__ ents) {
+    __builtin_amdgcn_s_setprio(3);
+    const CopyEnt e = ents[blockIdx.y];
+    for (int64_t o = 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); o < e.len;
+         o += 16 * (int64_t)gridDim.x * blockDim.x)
+        copy_piece(e.src, e.dst, e.len, o);
+}
+
+hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hipStream_t s) {
+    if (n == 0 || max_len <= 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((max_len + 16 * 256 - 1) / (16 * 256), 64);
+    hipLaunchKernelGGL(copy_many_kernel, dim3((uint32_t)blocks, n), dim3(256), 0, s, ents);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------------
 // True weak sums at arbitrary positions (one workgroup per position).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void window_weak_kernel(const uint8_t* __restrict__ data, int64_t n, uint32_t B,
-                                                          const int64_t* __restrict__ pos, int32_t* __restrict__ out,
-                                                          bool by_block) {
+__global__ __launch_bounds__(256) void window_weak_kernel(const ScanFile* __restrict__ files,
+                                                          const GatherEnt* __restrict__ ents,
+                                                          int32_t* __restrict__ out) {
     __builtin_amdgcn_s_setprio(3);
     __shared__ int32_t sh[2 * 256 / 64];
-    const int64_t p = pos[blockIdx.x];
-    const int64_t w = (n - p < (int64_t)B ? n - p : (int64_t)B);
+    const GatherEnt e = ents[blockIdx.x];
+    const ScanFile& F = files[e.file];
+    const int64_t p = e.p, n = F.n, B = F.B;
+    const int64_t w = (n - p < B ? n - p : B);
     int32_t v[2] = {0, 0};
-    range_sums(data, n, p, p + w, p, v[0], v[1]);
+    range_sums(F.data, n, p, p + w, p, v[0], v[1]);
     block_reduce<2>(v, sh);
     if (threadIdx.x == 0) {
         const uint32_t S1 = (uint32_t)v[0];
         const uint32_t S2 = (uint32_t)w * S1 - (uint32_t)v[1];
-        out[by_block ? p / B : blockIdx.x] = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
+        const int32_t T = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
+        if (e.by_block) F.aligned_weak[p / B] = T;
+        else out[blockIdx.x] = T;
     }
 }
 
-hipError_t launch_window_weak(const uint8_t* d_data, int64_t n, uint32_t B, const int64_t* d_pos, uint32_t npos,
-                              int32_t* d_out, hipStream_t s, bool by_block) {
-    if (npos == 0) return hipSuccess;
-    hipLaunchKernelGGL(window_weak_kernel, dim3(npos), dim3(256), 0, s, d_data, n, B, d_pos, d_out, by_block);
+hipError_t launch_window_weak(const ScanFile* files, const GatherEnt* ents, uint32_t n, int32_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(window_weak_kernel, dim3(n), dim3(256), 0, s, files, ents, out);
+    return hipGetLastError();
+}
+
+__global__ void table_insert_many_kernel(const TableEnt* __restrict__ ents) {
+    __builtin_amdgcn_s_setprio(3);
+    const TableEnt e = ents[blockIdx.y];
+    for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < e.nkeys; i += gridDim.x * blockDim.x) {
+        const uint32_t key = (uint32_t)e.keys[i];
+        const unsigned long long v = (1ull << 32) | key;
+        uint32_t h = slot_hash(key) & e.mask;
+        for (uint32_t probes = 0; probes <= e.mask; ++probes) {
+            const unsigned long long prev = atomicCAS(&e.slots[h], 0ull, v);
+            if (prev == 0ull || prev == v) break;
+            h = (h + 1) & e.mask;
+        }
+    }
+}
+
+hipError_t launch_table_insert_many(const TableEnt* ents, uint32_t n, int32_t max_keys, hipStream_t s) {
+    if (n == 0 || max_keys <= 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)std::min<int64_t>((max_keys + 255) / 256, 256);
+    hipLaunchKernelGGL(table_insert_many_kernel, dim3(blocks, n), dim3(256), 0, s, ents);
+    return hipGetLastError();
+}
+
+__global__ void chain_flags_many_kernel(const FlagEnt* __restrict__ ents) {
+    const FlagEnt e = ents[blockIdx.y];
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < e.count; k += gridDim.x * blockDim.x) {
+        bool eq = e.wsrc[k] == e.wbas[k];
+        for (uint32_t j = 0; j < e.dl; ++j) eq &= e.ssrc[(size_t)k * e.dl + j] == e.sbas[(size_t)k * e.dl + j];
+        e.flags[k] = eq ? 1 : 0;
+    }
+}
+
+hipError_t launch_chain_flags_many(const FlagEnt* ents, uint32_t n, uint32_t max_count, hipStream_t s) {
+    if (n == 0 || max_count == 0) return hipSuccess;
+    const uint32_t blocks = std::min<uint32_t>((max_count + 255) / 256, 256);
+    hipLaunchKernelGGL(chain_flags_many_kernel, dim3(blocks, n), dim3(256), 0, s, ents);
     return hipGetLastError();
 }
 

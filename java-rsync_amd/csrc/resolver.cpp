@@ -14,24 +14,31 @@
 
 namespace rsh {
 
+HostTimes& host_times() {
+    static thread_local HostTimes t;
+    return t;
+}
+
 namespace {
-// RSH_SCAN_TRACE=1: one stderr line per host-side table operation (diagnostics)
+// RSH_SCAN_TRACE=1: one stderr line per host-side table operation (=2: totals only, see host_times)
 struct HostTrace {
     const char* what;
     int64_t arg;
+    double* acc;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-    HostTrace(const char* w, int64_t a) : what(w), arg(a) {}
+    HostTrace(const char* w, int64_t a, double* total) : what(w), arg(a), acc(total) {}
     ~HostTrace() {
-        static const bool on = getenv("RSH_SCAN_TRACE") != nullptr;
-        if (on)
-            fprintf(stderr, "[rsh] %-10s %10lld %9.3f ms\n", what, (long long)arg,
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        static const int on = getenv("RSH_SCAN_TRACE") ? atoi(getenv("RSH_SCAN_TRACE")) : 0;
+        if (!on) return;
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        *acc += ms;
+        if (on == 1) fprintf(stderr, "[rsh] %-10s %10lld %9.3f ms\n", what, (long long)arg, ms);
     }
 };
 }  // namespace
 
 void ChunkTable::build() {
-    HostTrace tr("tab_sort", chunk_count);
+    HostTrace tr("tab_sort", chunk_count, &host_times().sort_ms);
     if (sorted_) return;
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<uint32_t>& sorted_key = sorted_key_;
@@ -79,12 +86,32 @@ void ChunkTable::build() {
     sort_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+void ChunkTable::build_filter() {
+    // the received table usually sits in pinned (uncached for the CPU) memory: take a cacheable copy first
+    weak_copy_.assign(weak, weak + chunk_count);
+    weak = weak_copy_.data();
+    uint32_t bits = 1u << 12;
+    while (bits < 32u * (uint32_t)chunk_count && bits < (1u << 26)) bits <<= 1;
+    filter_mask_ = bits - 1;
+    filter_.assign(bits / 64, 0ull);
+    for (int32_t i = 0; i < chunk_count; ++i) {
+        const uint32_t h = ((uint32_t)weak[i] * 0x9E3779B1u) >> 7;
+        filter_[(h & filter_mask_) >> 6] |= 1ull << (h & 63);
+    }
+    has_filter_ = true;
+}
+
 const int32_t* ChunkTable::bucket(int32_t key, int32_t* size) {
     if (primed_valid_ && key == primed_key_) {
         *size = (int32_t)primed_.size();
         return primed_.data();
     }
-    HostTrace tr("bucket", key);
+    if (!has_filter_ && scan_lookups_ >= 2) build_filter();  // a scan that needs one or two lookups skips it
+    if (has_filter_ && !maybe_has(key)) {
+        *size = 0;
+        return nullptr;
+    }
+    HostTrace tr("bucket", key, &host_times().bucket_ms);
     if (!sorted_ && scan_lookups_ >= kScanLookups) build();
     if (sorted_) {
         const uint32_t k = (uint32_t)key;
@@ -107,7 +134,7 @@ const int32_t* ChunkTable::bucket(int32_t key, int32_t* size) {
 }
 
 void ChunkTable::keys_with_digest(const uint8_t* d, std::vector<int32_t>* keys) const {
-    HostTrace tr("dkeys", chunk_count);
+    HostTrace tr("dkeys", chunk_count, &host_times().dkeys_ms);
     keys->clear();
     const int64_t dl = digest_length;
     if (dl == 0) {  // every chunk carries the empty digest

@@ -22,6 +22,12 @@
 
 namespace rsh {
 
+// Host time in the table operations of the calling thread (RSH_SCAN_TRACE diagnostics).
+struct HostTimes {
+    double bucket_ms = 0, sort_ms = 0, dkeys_ms = 0, md5_ms = 0;
+};
+HostTimes& host_times();
+
 // Host view of the received chunk table (Checksum + Multimap, Checksum.java:156-276).
 struct ChunkTable {
     int32_t chunk_count = 0;
@@ -55,6 +61,18 @@ struct ChunkTable {
     }
 
   private:
+    // membership filter over the keys (one bit per hash slot, >= 32 slots per chunk): most lookups are
+    // for keys that are not in the table (the next aligned window after a match, in an edited file)
+    // and are answered by one bit test, without a scan and without counting towards the sort
+    bool has_filter_ = false;
+    uint32_t filter_mask_ = 0;
+    std::vector<uint64_t> filter_;
+    std::vector<int32_t> weak_copy_;
+    void build_filter();
+    bool maybe_has(int32_t key) const {
+        const uint32_t h = ((uint32_t)key * 0x9E3779B1u) >> 7;
+        return (filter_[(h & filter_mask_) >> 6] >> (h & 63)) & 1;
+    }
     bool primed_valid_ = false;
     int32_t primed_key_ = 0;
     std::vector<int32_t> primed_;

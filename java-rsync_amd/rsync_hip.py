@@ -65,6 +65,20 @@ class ScanStats(ctypes.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+class BlockJob(ctypes.Structure):
+    """rsh_block_job: one basis file of a batched Generator pass (device pointers)."""
+    _fields_ = [("d_data", ctypes.c_void_p), ("n", ctypes.c_int64), ("h", Header), ("d_weak", ctypes.c_void_p),
+                ("d_strong", ctypes.c_void_p)]
+
+
+class ScanJob(ctypes.Structure):
+    """rsh_scan_job: one source file of a batched Sender scan (device pointers; ev is host memory)."""
+    _fields_ = [("d_src", ctypes.c_void_p), ("n", ctypes.c_int64), ("h", Header), ("d_weak", ctypes.c_void_p),
+                ("d_strong", ctypes.c_void_p), ("ev", ctypes.c_void_p), ("ev_cap", ctypes.c_int64),
+                ("n_ev", ctypes.c_int64), ("literal", ctypes.c_int64), ("matched", ctypes.c_int64),
+                ("status", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
 EVENT_DTYPE = np.dtype([("offset", "<i8"), ("length", "<i8"), ("kind", "<i4"), ("index", "<i4"),
                         ("count", "<i4"), ("reserved", "<i4")])
 
@@ -73,7 +87,7 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_coun
            "rsh_ctx_stream", "rsh_block_length_for", "rsh_digest_length_for", "rsh_header_make",
            "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
            "rsh_match_scan_device", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
-           "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
+           "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 
 _LIB = None
 
@@ -117,6 +131,9 @@ def lib():
         "rsh_tokens_size": ([P, I64], I64),
         "rsh_tokens_write": ([P, P, I64, P, P, I64], ctypes.c_int),
         "rsh_generator_bytes": ([HP, P, P, P, I64], I64),
+        "rsh_block_sums_batch_device": ([P, ctypes.POINTER(BlockJob), I32, P], ctypes.c_int),
+        "rsh_match_scan_batch_device": ([P, ctypes.POINTER(ScanJob), I32, P, ctypes.POINTER(ScanStats)],
+                                        ctypes.c_int),
         "rsh_dev_alloc": ([P, I64, ctypes.POINTER(P)], ctypes.c_int),
         "rsh_dev_free": ([P, P], ctypes.c_int),
         "rsh_memcpy_h2d": ([P, P, P, I64], ctypes.c_int),

@@ -5,6 +5,7 @@
 
 #include <vector>
 
+#include "hit_cache.h"
 #include "host_md5.h"
 #include "resolver.h"
 #include "rsync_hip.h"
@@ -58,7 +59,39 @@ class CpuBackend : public rsh::ScanBackend {
         h.update(seed_, 4);
         h.final(out);
     }
+    // Hit-cache mode mirrors the HIP backends: a single-interval probe first asks the previous probe's hit
+    // list (rsh::HitCache), and a probe that runs fills a ProbeOut the way probe_first_kernel does.
+    bool use_cache = false;
+    int64_t cache_answers = 0;
+    rsh::HitCache cache;
     int64_t first_hit(const rsh::ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) override {
+        if (use_cache && count == 1) {
+            int64_t p = -1, a2 = iv[0].a;
+            int32_t T = 0;
+            if (cache.lookup(iv[0], keys, &p, &T, &a2)) {
+                ++cache_answers;
+                if (p >= 0 && T != weak1(p)) return -2;  // the cache's weak sum must be the true one
+                return p;
+            }
+            rsh::ProbeInterval one = iv[0];
+            one.a = a2;
+            rsh::ProbeOut o;
+            o.first = ~0ull;
+            o.count = 0;
+            for (int64_t a = one.a; a < one.b;) {  // every hit, in order, as the kernel lists them
+                const int64_t p1 = first_hit1(a, one.b, one.anchor, one.e_lo, one.e_hi, keys);
+                if (p1 < 0) break;
+                if (o.first == ~0ull) o.first = (unsigned long long)p1;
+                if (o.count < (unsigned long long)rsh::PROBE_HITS_CAP) {
+                    o.pos[o.count] = (unsigned long long)p1;
+                    o.key[o.count] = (uint32_t)last_key_;
+                }
+                ++o.count;
+                a = p1 + 1;
+            }
+            cache.fill(one, keys, o, n_ - B_);
+            return o.first == ~0ull ? -1 : (int64_t)o.first;
+        }
         for (int64_t i = 0; i < count; ++i) {
             const int64_t p = first_hit1(iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo, iv[i].e_hi, keys);
             if (p >= 0) return p;  // intervals are in increasing position order
@@ -82,7 +115,10 @@ class CpuBackend : public rsh::ScanBackend {
                 t_.bucket(R, &size);
                 hit = size > 0;
             }
-            if (hit) return p;
+            if (hit) {
+                last_key_ = R;
+                return p;
+            }
             // true weak sum of the next window (Rolling subtract/add with the FileView window rule)
             const int64_t w = wl(p);
             const int32_t x = (int32_t)(int8_t)x_[p];
@@ -98,6 +134,7 @@ class CpuBackend : public rsh::ScanBackend {
     }
 
   private:
+    int32_t last_key_ = 0;
     int64_t wl(int64_t p) const { return n_ - p < B_ ? n_ - p : B_; }
     const uint8_t* x_;
     int64_t n_;
@@ -114,6 +151,17 @@ class CpuBackend : public rsh::ScanBackend {
 
 // head_steps < 0: one plain resolve_scan.  Otherwise the scan runs head_steps resolver steps with no
 // aligned speculation (as while the device kernel is still running), then resumes with it.
+static int g_use_cache = 0;
+static int64_t g_cache_answers = 0;
+// 1: single-interval probes go through rsh::HitCache (as in the HIP backends); returns the number of
+// probes the cache answered since the last call.
+extern "C" int64_t rtest_hit_cache(int on) {
+    g_use_cache = on;
+    const int64_t a = g_cache_answers;
+    g_cache_answers = 0;
+    return a;
+}
+
 extern "C" int rtest_scan_staged(const uint8_t* src, int64_t n, const rsh_header* h, const int32_t* weak,
                                  const uint8_t* strong, const uint8_t seed[4], rsh_event* ev, int64_t cap,
                                  int64_t* n_ev, int64_t* lit, int64_t* mat, rsh_scan_stats* stats, int64_t head_steps) {
@@ -126,6 +174,7 @@ extern "C" int rtest_scan_staged(const uint8_t* src, int64_t n, const rsh_header
     t.strong = strong;
     if (head_steps < 0) t.build();  // staged runs leave the table lazy (linear-scan lookups first)
     CpuBackend be(src, n, t, seed);
+    be.use_cache = g_use_cache != 0;
     rsh::ResolveResult r;
     if (head_steps < 0) {
         rsh::resolve_scan(n, t, be, &r);
@@ -137,6 +186,7 @@ extern "C" int rtest_scan_staged(const uint8_t* src, int64_t n, const rsh_header
         be.head = false;
         if (!done) rsh::resolve_run(n, t, be, &st, &r, nullptr);
     }
+    g_cache_answers += be.cache_answers;
     *n_ev = (int64_t)r.ev.size();
     *lit = r.literal;
     *mat = r.matched;

@@ -1,0 +1,179 @@
+"""Batched (multi-file) entry points against the oracle, file by file.
+
+rsh_block_sums_batch_device: one K1 launch over every file of a segment (Generator.java:558-614 calling
+sendItemizeAndChecksums :866-909 per file).  rsh_match_scan_batch_device: one resolver per file, device
+round trips gathered per round (Sender.sendFiles :1098-1148 -> sendMatchesAndData :1235-1327).  Each
+file's weak/strong sums, event list and literal/matched counts must equal the oracle's for that file
+alone: batching may change nothing in any file's result.  The segment mixes block lengths (multiples of
+128 that take the coalesced K1, and others that take the per-lane kernel), misaligned file starts, short
+and empty files, a new file (B = 0: skipMatchSendData) and every edit shape of the single-file fuzz."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+import rsync_hip as R
+
+pytestmark = pytest.mark.gpu
+SEED = bytes([1, 2, 3, 4])
+SEED_NP = np.frombuffer(SEED, np.uint8).copy()
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    R.build()
+    c = R.Context(0)
+    yield c
+    c.close()
+
+
+def _segment(rng, count):
+    from test_resolver_cpu import _mutate
+    files = []
+    for i in range(count):
+        B = rng.choice([512, 640, 700, 1024, 2048, 8192, 8192])
+        kind = rng.random()
+        if kind < 0.1:
+            nb = rng.randrange(1, B)                 # shorter than one block
+        elif kind < 0.2:
+            nb = 64 * B * rng.randrange(1, 3)        # whole coalesced groups only
+        else:
+            nb = rng.randrange(B, 300 * B)
+        key = rng.randrange(1 << 62)
+        basis = O.splitmix(nb, key).tobytes()
+        if rng.random() < 0.1:
+            blk = O.splitmix(B, key).tobytes()
+            basis = (blk * (nb // B + 1))[:nb]
+        r = rng.random()
+        if r < 0.15:
+            src = basis
+        elif r < 0.3:  # every other block replaced
+            other = O.splitmix(nb, key ^ 0xED17).tobytes()
+            src = b"".join(other[k:k + B] if (k // B) % 2 else basis[k:k + B] for k in range(0, nb, B))
+        else:
+            src = _mutate(rng, basis, B, key) or basis
+        dl = rng.choice([2, 3, 4, 16])
+        files.append((basis, src, B, dl))
+    return files
+
+
+def _pack(ctx, blobs, misalign):
+    """All blobs in one device buffer; file i starts at a 256-B boundary + misalign[i]."""
+    offs, pos = [], 0
+    for b, m in zip(blobs, misalign):
+        pos = (pos + 255) // 256 * 256 + m
+        offs.append(pos)
+        pos += max(len(b), 1)
+    host = np.zeros(pos + 1, np.uint8)
+    for b, o in zip(blobs, offs):
+        host[o:o + len(b)] = np.frombuffer(b, np.uint8)
+    d = ctx.alloc(host.size)
+    d.upload(host)
+    return d, offs
+
+
+def test_batch_generator_and_scan_match_oracle(ctx):
+    rng = random.Random(2024)
+    files = _segment(rng, 48)
+    mis = [0 if rng.random() < 0.8 else rng.choice([1, 3, 4, 8]) for _ in files]
+    d_basis, boffs = _pack(ctx, [f[0] for f in files], mis)
+    d_src, soffs = _pack(ctx, [f[1] for f in files], mis[::-1])
+    heads = [R.header_make(B, dl, len(basis)) for basis, _, B, dl in files]
+    woffs, soffs_t, wtot, stot = [], [], 0, 0
+    for h in heads:
+        woffs.append(wtot)
+        soffs_t.append(stot)
+        wtot += 4 * h.chunk_count
+        stot += h.chunk_count * h.digest_length
+    d_w, d_s = ctx.alloc(wtot + 4), ctx.alloc(stot + 1)
+
+    bj = (R.BlockJob * len(files))()
+    for i, (h, (basis, _, B, dl)) in enumerate(zip(heads, files)):
+        bj[i].d_data = d_basis.ptr.value + boffs[i]
+        bj[i].n = len(basis)
+        bj[i].h = h
+        bj[i].d_weak = d_w.ptr.value + woffs[i]
+        bj[i].d_strong = d_s.ptr.value + soffs_t[i]
+    assert R.lib().rsh_block_sums_batch_device(ctx.handle, bj, len(files), SEED_NP.ctypes.data) == 0
+    ctx.sync()
+    all_w, all_s = d_w.download(dtype=np.int32)[:wtot // 4], d_s.download()[:stot]
+    tables = []
+    for i, (h, (basis, src, B, dl)) in enumerate(zip(heads, files)):
+        ow, os_ = O.generator(basis, O.header(B, dl, len(basis)), SEED)
+        gw = all_w[woffs[i] // 4:woffs[i] // 4 + h.chunk_count]
+        gs = all_s[soffs_t[i]:soffs_t[i] + h.chunk_count * dl]
+        assert np.array_equal(gw, ow) and np.array_equal(gs, os_), f"file {i}: B={B} n={len(basis)} mis={mis[i]}"
+        tables.append((ow, os_))
+
+    # scan jobs: the segment's files, plus a new file (B = 0) and an empty source
+    nj = len(files) + 2
+    sj = (R.ScanJob * nj)()
+    evs = []
+    for i, (h, (basis, src, B, dl)) in enumerate(zip(heads, files)):
+        cap = len(src) // (10 * B) + 2 * h.chunk_count + 64
+        ev = np.zeros(cap, R.EVENT_DTYPE)
+        evs.append(ev)
+        sj[i].d_src = d_src.ptr.value + soffs[i]
+        sj[i].n = len(src)
+        sj[i].h = h
+        sj[i].d_weak = d_w.ptr.value + woffs[i]
+        sj[i].d_strong = d_s.ptr.value + soffs_t[i]
+        sj[i].ev = ev.ctypes.data
+        sj[i].ev_cap = cap
+    new_ev = np.zeros(64, R.EVENT_DTYPE)
+    sj[nj - 2].d_src = d_src.ptr.value + soffs[0]
+    sj[nj - 2].n = len(files[0][1])
+    sj[nj - 2].h = R.Header(0, 0, 0, 0)
+    sj[nj - 2].ev = new_ev.ctypes.data
+    sj[nj - 2].ev_cap = 64
+    sj[nj - 1].n = 0
+    sj[nj - 1].h = heads[1]
+    sj[nj - 1].d_weak = d_w.ptr.value + woffs[1]
+    sj[nj - 1].d_strong = d_s.ptr.value + soffs_t[1]
+    st = R.ScanStats()
+    rc = R.lib().rsh_match_scan_batch_device(ctx.handle, sj, nj, SEED_NP.ctypes.data, ctypes.byref(st))
+    assert rc == 0, (rc, R.lib().rsh_last_error())
+    for i, (h, (basis, src, B, dl)) in enumerate(zip(heads, files)):
+        ow, os_ = tables[i]
+        oev, _, olit, omat, _ = O.sender(src, O.header(B, dl, len(basis)), ow, os_, SEED)
+        got = R.events_as_tuples(evs[i][:sj[i].n_ev], B)
+        assert sj[i].status == 0
+        assert got == [tuple(e) for e in oev], f"file {i}: B={B} n={len(src)}"
+        assert (sj[i].literal, sj[i].matched) == (olit, omat)
+    n0 = len(files[0][1])
+    oev, _, olit, _, _ = O.sender(files[0][1], O.header(0, 0, 0), np.zeros(0, np.int32), np.zeros(0, np.uint8), SEED)
+    assert R.events_as_tuples(new_ev[:sj[nj - 2].n_ev], 1) == [tuple(e) for e in oev] and sj[nj - 2].literal == n0
+    assert sj[nj - 1].status == 0 and sj[nj - 1].n_ev == 0 and sj[nj - 1].literal == 0
+    assert st.probe_launches > 0
+
+
+def test_batch_scan_nospace_is_per_file(ctx):
+    """A file whose event buffer is too small gets RSH_E_NOSPACE (and its count); the others succeed."""
+    B, dl = 512, 2
+    basis = O.splitmix(100 * B, 5).tobytes()
+    srcs = [basis, O.splitmix(30 * B, 6).tobytes() + basis]
+    h = R.header_make(B, dl, len(basis))
+    w, s = ctx.block_sums(basis, h, SEED)
+    d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
+    d_w.upload(w)
+    d_s.upload(s)
+    d_src, offs = _pack(ctx, srcs, [0, 0])
+    evs = [np.zeros(64, R.EVENT_DTYPE), np.zeros(1, R.EVENT_DTYPE)]
+    sj = (R.ScanJob * 2)()
+    for i in range(2):
+        sj[i].d_src = d_src.ptr.value + offs[i]
+        sj[i].n = len(srcs[i])
+        sj[i].h = h
+        sj[i].d_weak = d_w.ptr.value
+        sj[i].d_strong = d_s.ptr.value
+        sj[i].ev = evs[i].ctypes.data
+        sj[i].ev_cap = len(evs[i])
+    rc = R.lib().rsh_match_scan_batch_device(ctx.handle, sj, 2, SEED_NP.ctypes.data, None)
+    assert rc == R.RSH_E_NOSPACE
+    assert sj[0].status == 0 and sj[1].status == R.RSH_E_NOSPACE and sj[1].n_ev > 1
+    full, _, lit, mat, _ = ctx.match_scan(srcs[1], h, w, s, SEED)
+    assert sj[1].n_ev == len(full) and (sj[1].literal, sj[1].matched) == (lit, mat)
+    want0, _, _, _, _ = ctx.match_scan(srcs[0], h, w, s, SEED)
+    assert R.events_as_tuples(evs[0][:sj[0].n_ev], B) == R.events_as_tuples(want0, B)

@@ -167,3 +167,36 @@ def test_resolver_staged_head_mode(seed_i):
             continue
         check_case(basis, src, B, rng.choice([2, 3, 16]), bytes([1, 2, 3, 4]),
                    head_steps=rng.choice([0, 1, 2, 5, 17, 1 << 40]))
+
+
+@pytest.mark.parametrize("seed_i", range(6))
+def test_resolver_hit_cache(seed_i):
+    """The HIP backends answer a single-interval probe from the previous probe's hit list (rsh::HitCache)
+    or cut it to the unprobed part.  The CPU backend in the same mode must still give the oracle's events;
+    the cache must actually answer probes (every-other-block edits: several matches per probed range), and
+    must stay exact when the list overflows (low-entropy data: every aligned position hits)."""
+    L = rlib()
+    L.rtest_hit_cache.argtypes = [ctypes.c_int]
+    L.rtest_hit_cache.restype = ctypes.c_int64
+    rng = random.Random(3000 + seed_i)
+    L.rtest_hit_cache(1)
+    try:
+        for i in range(10):
+            B = rng.choice([512, 576, 1024])
+            nb = rng.randrange(20 * B, 60 * B)
+            key = rng.randrange(1 << 62)
+            if i % 4 == 3:
+                blk = O.splitmix(B, key).tobytes()
+                basis = (blk * (nb // B + 1))[:nb]
+            else:
+                basis = O.splitmix(nb, key).tobytes()
+            if i % 2 == 0:  # every other block replaced: a match every 2B inside each probed range
+                other = O.splitmix(nb, key ^ 0xED17).tobytes()
+                src = b"".join(other[k:k + B] if (k // B) % 2 else basis[k:k + B] for k in range(0, nb, B))
+            else:
+                src = _mutate(rng, basis, B, key) or basis
+            check_case(basis, src, B, rng.choice([2, 3, 4]), bytes([1, 2, 3, 4]), head_steps=rng.choice([-1, 3, 40]))
+        answered = L.rtest_hit_cache(0)
+    finally:
+        L.rtest_hit_cache(0)
+    assert answered > 0
