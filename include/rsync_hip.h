@@ -174,6 +174,37 @@ typedef struct {
 int rsh_match_scan_batch_device(rsh_ctx* ctx, rsh_scan_job* jobs, int32_t njobs, const uint8_t seed[4],
                                 rsh_scan_stats* stats);
 
+/* ---- Receiver (Receiver.java:459-555 combineDataToFile, :557-578 copies, :204-209 blockSize) ----
+ * Replays one file's de-multiplexed token stream -- putInt(len)+bytes, putInt(-(i+1)), putInt(0), exactly
+ * what rsh_tokens_write produces -- against the replica (the basis the Generator summed; NULL when the
+ * Receiver has none: matches are then skipped, :487-494).  The target receives the literal bytes and the
+ * replica blocks in token order; with defer_write (and a replica) nothing is written while the matches
+ * are 0, 1, 2, ... in order with no literal, and a stream that matched all chunk_count blocks that way
+ * leaves the file intact (out->intact = 1, the replica is the result, :529-545).  out->md5 is the digest
+ * the Receiver computes over the file content; compare it with the 16 bytes that follow the stream
+ * (isRemoteAndLocalFileIdentical, :824-842).  Status: RSH_E_PROTOCOL for a block index out of range or a
+ * match against block_length 0 (RsyncProtocolException, :480-485); RSH_E_INVAL for a truncated stream
+ * or a replica shorter than a block it names (IllegalStateException, :1012-1017); RSH_E_NOSPACE when
+ * target_cap < out->target_len (nothing written). */
+typedef struct {
+    int64_t tokens_used;  /* bytes consumed, including the terminating putInt(0) */
+    int64_t target_len;   /* bytes of the rebuilt file written to the target (0 when intact) */
+    int64_t literal;      /* sizeLiteral */
+    int64_t matched;      /* sizeMatch */
+    int32_t intact;       /* combineDataToFile's return value */
+    int32_t reserved;
+    uint8_t md5[16];
+} rsh_combine_result;
+/* Host buffers (the replica is uploaded, the target downloaded). */
+int rsh_receiver_combine(rsh_ctx* ctx, const uint8_t* tokens, int64_t tokens_len, const rsh_header* h,
+                         const uint8_t* replica, int64_t replica_len, int32_t defer_write, uint8_t* target,
+                         int64_t target_cap, rsh_combine_result* out);
+/* Device-resident replica and target (the tokens stay in host memory); the blocks are gathered by a
+ * kernel, the literal bytes uploaded in one copy; the digest is computed on the host from the result. */
+int rsh_receiver_combine_device(rsh_ctx* ctx, const uint8_t* tokens, int64_t tokens_len, const rsh_header* h,
+                                const void* d_replica, int64_t replica_len, int32_t defer_write, void* d_target,
+                                int64_t target_cap, rsh_combine_result* out);
+
 /* ---- device buffers for the *_device entry points (callers without their own allocator, e.g. JNI) ---- */
 int rsh_dev_alloc(rsh_ctx* ctx, int64_t bytes, void** out);
 int rsh_dev_free(rsh_ctx* ctx, void* p);

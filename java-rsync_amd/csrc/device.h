@@ -156,6 +156,14 @@ struct CopyEnt {
 hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hipStream_t s);
 // n bytes of device memory into pinned host memory (h_dst 16-byte aligned), by a kernel.
 hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s);
+// Byte ranges between arbitrary (unaligned) device addresses: one op per workgroup, 16-byte stores to
+// the aligned middle of each destination (Receiver block gather).
+struct GatherOp {
+    const uint8_t* src;
+    uint8_t* dst;
+    int64_t len;
+};
+hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s);
 // Probe hashes of many files (slots cleared by the caller): keys[i] into slots/mask.
 struct TableEnt {
     unsigned long long* slots;

@@ -1628,6 +1628,38 @@ hipError_t launch_window_weak(const ScanFile* files, const GatherEnt* ents, uint
     return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void gather_ops_kernel(const GatherOp* __restrict__ ops) {
+    const GatherOp op = ops[blockIdx.x];
+    const uintptr_t d = reinterpret_cast<uintptr_t>(op.dst);
+    int64_t head = (int64_t)((16 - (d & 15)) & 15);
+    if (head > op.len) head = op.len;
+    const int t = threadIdx.x;
+    if (t < head) op.dst[t] = op.src[t];
+    const int64_t body = (op.len - head) & ~(int64_t)15;
+    const uint8_t* __restrict__ s = op.src + head;
+    uint8_t* __restrict__ o = op.dst + head;
+    if ((reinterpret_cast<uintptr_t>(s) & 3) == 0) {  // word-aligned source: four dword loads per store
+        for (int64_t k = 16 * (int64_t)t; k < body; k += 16 * (int64_t)blockDim.x) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(s + k);
+            *reinterpret_cast<uint4*>(o + k) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    } else {
+        for (int64_t k = 16 * (int64_t)t; k < body; k += 16 * (int64_t)blockDim.x) {
+            uint32_t q[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < 16; ++i) q[i >> 2] |= (uint32_t)s[k + i] << (8 * (i & 3));
+            *reinterpret_cast<uint4*>(o + k) = make_uint4(q[0], q[1], q[2], q[3]);
+        }
+    }
+    for (int64_t k = head + body + t; k < op.len; k += blockDim.x) op.dst[k] = op.src[k];
+}
+
+hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_ops_kernel, dim3(n), dim3(256), 0, s, ops);
+    return hipGetLastError();
+}
+
 __global__ void table_insert_many_kernel(const TableEnt* __restrict__ ents) {
     __builtin_amdgcn_s_setprio(3);
     const TableEnt e = ents[blockIdx.y];

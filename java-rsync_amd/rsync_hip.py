@@ -79,6 +79,13 @@ class ScanJob(ctypes.Structure):
                 ("status", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class CombineResult(ctypes.Structure):
+    """rsh_combine_result (Receiver.combineDataToFile outcome)."""
+    _fields_ = [("tokens_used", ctypes.c_int64), ("target_len", ctypes.c_int64), ("literal", ctypes.c_int64),
+                ("matched", ctypes.c_int64), ("intact", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("md5", ctypes.c_uint8 * 16)]
+
+
 EVENT_DTYPE = np.dtype([("offset", "<i8"), ("length", "<i8"), ("kind", "<i4"), ("index", "<i4"),
                         ("count", "<i4"), ("reserved", "<i4")])
 
@@ -87,7 +94,8 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_coun
            "rsh_ctx_stream", "rsh_block_length_for", "rsh_digest_length_for", "rsh_header_make",
            "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
            "rsh_match_scan_device", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
-           "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
+           "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_receiver_combine",
+           "rsh_receiver_combine_device", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 
 _LIB = None
 
@@ -133,6 +141,9 @@ def lib():
         "rsh_generator_bytes": ([HP, P, P, P, I64], I64),
         "rsh_block_sums_batch_device": ([P, ctypes.POINTER(BlockJob), I32, P], ctypes.c_int),
         "rsh_match_scan_batch_device": ([P, ctypes.POINTER(ScanJob), I32, P, ctypes.POINTER(ScanStats)],
+                                        ctypes.c_int),
+        "rsh_receiver_combine": ([P, P, I64, HP, P, I64, I32, P, I64, ctypes.POINTER(CombineResult)], ctypes.c_int),
+        "rsh_receiver_combine_device": ([P, P, I64, HP, P, I64, I32, P, I64, ctypes.POINTER(CombineResult)],
                                         ctypes.c_int),
         "rsh_dev_alloc": ([P, I64, ctypes.POINTER(P)], ctypes.c_int),
         "rsh_dev_free": ([P, P], ctypes.c_int),
@@ -299,6 +310,20 @@ class Context:
             rc = lib().rsh_fetch_events(self._p, _ptr(ev), n_ev.value, ctypes.byref(n_ev))
         _check(rc)
         return ev[:n_ev.value], fm.tobytes(), lit.value, mat.value, stats.as_dict()
+
+
+    def receiver_combine(self, tokens, h, replica, defer_write=False, target_cap=None):
+        """Receiver.combineDataToFile (Receiver.java:459-555): (target bytes, CombineResult).  The target is
+        empty when the deferred write left the file intact (result.intact)."""
+        t = _u8(tokens)
+        rep = None if replica is None else _u8(replica)
+        cap = target_cap if target_cap is not None else t.size + (t.size // 4) * max(h.block_length, 1) + 16
+        tgt = np.zeros(max(cap, 1), np.uint8)
+        r = CombineResult()
+        _check(lib().rsh_receiver_combine(self._p, _ptr(t), t.size, ctypes.byref(h), _ptr(rep),
+                                          0 if rep is None else rep.size, int(bool(defer_write)), _ptr(tgt), cap,
+                                          ctypes.byref(r)))
+        return tgt[:r.target_len].tobytes(), r
 
 
 class DeviceBuffer:

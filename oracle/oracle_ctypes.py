@@ -66,6 +66,9 @@ def lib():
         L.orc_tokens.restype = ctypes.c_int64
         L.orc_generator_bytes.argtypes = [ctypes.POINTER(Header), P, P, P]
         L.orc_generator_bytes.restype = ctypes.c_int64
+        L.orc_receiver_combine.argtypes = [P, ctypes.c_int64, ctypes.POINTER(Header), P, ctypes.c_int64, ctypes.c_int,
+                                           P, ctypes.c_int64, ctypes.POINTER(CombineResult)]
+        L.orc_receiver_combine.restype = ctypes.c_int64
         L.orc_fill_splitmix.argtypes = [P, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64]
         _LIB = L
     return _LIB
@@ -130,6 +133,25 @@ def tokens(src, events, file_md5):
     out = np.zeros(size, np.uint8)
     lib().orc_tokens(_ptr(a), evs, n, _ptr(fm), _ptr(out))
     return out.tobytes()
+
+
+class CombineResult(ctypes.Structure):
+    _fields_ = [("target_len", ctypes.c_int64), ("literal", ctypes.c_int64), ("matched", ctypes.c_int64),
+                ("intact", ctypes.c_int32), ("md5", ctypes.c_uint8 * 16)]
+
+
+def receiver_combine(tokens, h, replica, defer_write=False, target_cap=None):
+    """Receiver.combineDataToFile: (rc, target bytes, literal, matched, intact, md5).  rc = tokens consumed
+    (>= 4) or a negative error (-1 protocol, -2 truncated stream, -3 target too small, -4 replica short)."""
+    t = _u8(tokens)
+    rep = None if replica is None else _u8(replica)
+    cap = target_cap if target_cap is not None else t.size + (t.size // 4) * max(h.block_length, 1) + 16
+    tgt = np.zeros(max(cap, 1), np.uint8)
+    r = CombineResult()
+    rc = lib().orc_receiver_combine(_ptr(t), t.size, ctypes.byref(h), None if rep is None else _ptr(rep),
+                                    0 if rep is None else rep.size, int(bool(defer_write)), _ptr(tgt), cap,
+                                    ctypes.byref(r))
+    return rc, tgt[:r.target_len].tobytes(), r.literal, r.matched, r.intact, bytes(r.md5)
 
 
 def splitmix(n, key, offset=0):

@@ -515,3 +515,92 @@ void orc_fill_splitmix(uint8_t* out, int64_t n, uint64_t key, int64_t byte_offse
         out[i] = (uint8_t)(wd >> (8 * (pos % 8)));
     }
 }
+
+/* ---- Receiver.combineDataToFile (Receiver.java:459-555) ---- */
+static int32_t get_int(const uint8_t* p) { /* BufferedInputChannel little-endian getInt */
+    return (int32_t)((uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24));
+}
+
+static int32_t block_size(int32_t index, const orc_header* h) { /* Receiver.java:204-209 */
+    if (index == h->chunk_count - 1 && h->remainder != 0) return h->remainder;
+    return h->block_length;
+}
+
+/* copyFromReplicaAndUpdateDigest (:570-578) with readFromReplica (:1006-1020) */
+static int copy_block(const uint8_t* replica, int64_t replica_len, int32_t index, const orc_header* h,
+                      uint8_t* target, int64_t cap, int64_t* tlen, orc_md5_ctx* md) {
+    const int32_t len = block_size(index, h);
+    const int64_t off = (int64_t)index * h->block_length;
+    if (off + len > replica_len) return -4; /* truncated read from replica: IllegalStateException */
+    if (*tlen + len > cap) return -3;
+    memcpy(target + *tlen, replica + off, (size_t)len);
+    *tlen += len;
+    orc_md5_update(md, replica + off, (size_t)len);
+    return 0;
+}
+
+int64_t orc_receiver_combine(const uint8_t* tokens, int64_t tokens_len, const orc_header* h,
+                             const uint8_t* replica, int64_t replica_len, int defer_write, uint8_t* target,
+                             int64_t target_cap, orc_combine_result* out) {
+    orc_md5_ctx md;
+    orc_md5_init(&md);
+    int deferrable = defer_write && replica != NULL; /* :465 */
+    int64_t pos = 0, tlen = 0, lit = 0, mat = 0;
+    int32_t expected = 0;
+    int rc;
+    for (;;) {
+        if (pos + 4 > tokens_len) return -2;
+        const int32_t token = get_int(tokens + pos);
+        pos += 4;
+        if (token == 0) break; /* :471-473 */
+        if (token < 0) {
+            const int32_t index = -(token + 1);
+            if (index > h->chunk_count - 1) return -1; /* :480-482 */
+            if (h->block_length == 0) return -1;       /* :483-485 */
+            if (replica == NULL) continue;             /* :487-494 */
+            mat += block_size(index, h);               /* :496 */
+            if (deferrable) {                          /* :498-510 */
+                if (index == expected) {
+                    expected++;
+                    continue;
+                }
+                deferrable = 0;
+                for (int32_t i = 0; i < expected; i++)
+                    if ((rc = copy_block(replica, replica_len, i, h, target, target_cap, &tlen, &md)) != 0) return rc;
+            }
+            if ((rc = copy_block(replica, replica_len, index, h, target, target_cap, &tlen, &md)) != 0) return rc;
+        } else { /* literal data (:512-525), copyFromPeerAndUpdateDigest (:557-568) */
+            if (deferrable) {
+                deferrable = 0;
+                for (int32_t i = 0; i < expected; i++)
+                    if ((rc = copy_block(replica, replica_len, i, h, target, target_cap, &tlen, &md)) != 0) return rc;
+            }
+            if (pos + token > tokens_len) return -2;
+            if (tlen + token > target_cap) return -3;
+            memcpy(target + tlen, tokens + pos, (size_t)token);
+            orc_md5_update(&md, tokens + pos, (size_t)token);
+            tlen += token;
+            lit += token;
+            pos += token;
+        }
+    }
+    if (deferrable && expected != h->chunk_count) { /* :529-538: truncation of whole blocks */
+        deferrable = 0;
+        for (int32_t i = 0; i < expected; i++)
+            if ((rc = copy_block(replica, replica_len, i, h, target, target_cap, &tlen, &md)) != 0) return rc;
+    }
+    if (deferrable) { /* :539-545: digest of the untouched replica */
+        for (int32_t i = 0; i < expected; i++) {
+            const int32_t len = block_size(i, h);
+            const int64_t off = (int64_t)i * h->block_length;
+            if (off + len > replica_len) return -4;
+            orc_md5_update(&md, replica + off, (size_t)len);
+        }
+    }
+    out->target_len = tlen;
+    out->literal = lit;
+    out->matched = mat;
+    out->intact = deferrable;
+    orc_md5_final(&md, out->md5);
+    return pos;
+}

@@ -106,6 +106,28 @@ int64_t orc_generator_bytes(const orc_header* h, const int32_t* weak, const uint
 /* ---- synthetic input (bench / golden): splitmix64 counter stream ---- */
 void orc_fill_splitmix(uint8_t* out, int64_t n, uint64_t key, int64_t byte_offset);
 
+/* ---- Receiver.combineDataToFile (session/Receiver.java:459-555, 565-578, 204-209, 1006-1020) ----
+ * Replays one file's de-multiplexed token stream (putInt(len)+bytes, putInt(-(i+1)), putInt(0)) against
+ * the replica (NULL = the Receiver has none: matches are skipped, :487-494).  The target receives the
+ * literal bytes and the replica blocks in token order, except when the write is deferred
+ * (defer_write && replica, :465): then nothing is written while the matches are 0, 1, 2, ... in order and
+ * no literal arrives, and if the stream ends with all chunk_count blocks matched that way the file is
+ * intact (returns 1 in *intact; the target stays empty, the replica is the result).  md5 = the digest
+ * the Receiver computes over the file content (:541-544, 565-578).
+ * Returns bytes of `tokens` consumed (including the terminating 0), or -1 RsyncProtocolException
+ * (block index out of range :480-482, a match against a header with block_length 0 :483-485), -2 a
+ * truncated token stream, -3 target_cap too small, -4 replica shorter than a block it names. */
+typedef struct {
+    int64_t target_len; /* bytes written to target */
+    int64_t literal;    /* sizeLiteral */
+    int64_t matched;    /* sizeMatch */
+    int32_t intact;     /* combineDataToFile's return value */
+    uint8_t md5[16];
+} orc_combine_result;
+int64_t orc_receiver_combine(const uint8_t* tokens, int64_t tokens_len, const orc_header* h,
+                             const uint8_t* replica, int64_t replica_len, int defer_write, uint8_t* target,
+                             int64_t target_cap, orc_combine_result* out);
+
 #ifdef __cplusplus
 }
 #endif

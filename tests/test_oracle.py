@@ -174,3 +174,59 @@ def test_oracle_vs_pyref_fuzz():
         assert [tuple(e) for e in ev] == [tuple(e) for e in pev]
         assert (fmd5, lit, mat) == (pfmd5, plit, pmat)
         assert fmd5 == hashlib.md5(src).digest()
+
+
+# ---- Receiver.combineDataToFile restatement (Receiver.java:459-555) ----
+
+def _round_trip(basis, src, B, dl, seed=bytes([1, 2, 3, 4])):
+    h = O.header(B, dl, len(basis))
+    w, s = O.generator(basis, h, seed)
+    ev, fm, lit, mat, _ = O.sender(src, h, w, s, seed)
+    return h, O.tokens(src, ev, fm), fm, lit, mat
+
+
+@pytest.mark.parametrize("seed_i", range(4))
+def test_receiver_combine_round_trip(seed_i):
+    """Sender tokens replayed against the replica rebuild the source; the Receiver's digest equals the
+    Sender's file MD5 (isRemoteAndLocalFileIdentical, Receiver.java:824-842); sizes agree."""
+    import random
+    from test_resolver_cpu import _mutate
+    rng = random.Random(500 + seed_i)
+    for _ in range(15):
+        B = rng.choice([512, 700, 1024])
+        nb = rng.randrange(1, 30 * B)
+        key = rng.randrange(1 << 62)
+        basis = O.splitmix(nb, key).tobytes()
+        src = _mutate(rng, basis, B, key) or basis
+        h, tok, fm, lit, mat = _round_trip(basis, src, B, rng.choice([2, 4, 16]))
+        defer = rng.random() < 0.5
+        rc, tgt, rl, rm, intact, md5 = O.receiver_combine(tok, h, basis, defer)
+        assert rc == len(tok) - 16  # the file MD5 follows the terminating 0
+        assert (rl, rm) == (lit, mat) and md5 == fm == O.md5(src)
+        if intact:
+            assert defer and tgt == b"" and src == basis[:len(src)] and lit == 0
+        else:
+            assert tgt == src
+
+
+def test_receiver_combine_deferred_and_errors():
+    B = 512
+    basis = O.splitmix(10 * B + 100, 9).tobytes()
+    h, tok, fm, lit, mat = _round_trip(basis, basis, B, 2)
+    rc, tgt, rl, rm, intact, md5 = O.receiver_combine(tok, h, basis, True)
+    assert intact == 1 and tgt == b"" and md5 == O.md5(basis) and rm == len(basis)
+    rc, tgt, rl, rm, intact, md5 = O.receiver_combine(tok, h, basis, False)
+    assert intact == 0 and tgt == basis
+    # a whole-block truncation: matches 0..9 of 11 then end -> not intact, blocks written (:529-538)
+    trunc = b"".join(int.to_bytes((-(i + 1)) & 0xFFFFFFFF, 4, "little") for i in range(10)) + bytes(4)
+    rc, tgt, rl, rm, intact, md5 = O.receiver_combine(trunc, h, basis, True)
+    assert rc == len(trunc) and intact == 0 and tgt == basis[:10 * B]
+    # no replica: matches are skipped (:487-494), literals kept
+    mixed = int.to_bytes(3, 4, "little") + b"xyz" + int.to_bytes((-1) & 0xFFFFFFFF, 4, "little") + bytes(4)
+    rc, tgt, rl, rm, intact, md5 = O.receiver_combine(mixed, h, None, True)
+    assert tgt == b"xyz" and (rl, rm) == (3, 0) and md5 == O.md5(b"xyz")
+    # block index out of range (:480-482) and a match against block_length 0 (:483-485)
+    bad = int.to_bytes((-(h.chunk_count + 1)) & 0xFFFFFFFF, 4, "little") + bytes(4)
+    assert O.receiver_combine(bad, h, basis)[0] == -1
+    assert O.receiver_combine(mixed, O.header(0, 0, 0), basis)[0] == -1
+    assert O.receiver_combine(tok[:5], h, basis)[0] == -2
