@@ -40,6 +40,8 @@ extern "C" {
 #define RSH_E_DEVICE (-5)   /* HIP runtime / kernel failure, or no gfx950 device present     */
 #define RSH_E_NOMEM (-6)    /* host or device allocation failed                              */
 #define RSH_E_BUSY (-7)     /* the context is serving a call on another thread               */
+#define RSH_E_NOTFOUND (-8) /* the file does not exist (FileViewNotFound, FileView.java:74-75)    */
+#define RSH_E_OPEN (-9)     /* the file cannot be opened (FileViewOpenFailed, FileView.java:76-78) */
 
 /* Checksum.Header; wire order of Connection.sendChecksumHeader (Connection.java:40-45) is
  * chunk_count, block_length, digest_length, remainder (4 x little-endian int32). */
@@ -173,6 +175,23 @@ typedef struct {
 /* stats (optional): summed over the files (device_ms / resolver_ms: wall time of the whole batch). */
 int rsh_match_scan_batch_device(rsh_ctx* ctx, rsh_scan_job* jobs, int32_t njobs, const uint8_t seed[4],
                                 rsh_scan_stats* stats);
+
+/* ---- file ingest: the FileView reads of the two passes (FileView.java:51-80 open, :187-278 reads) ----
+ * The file is read straight into pinned staging buffers by several threads (large preads), copied to the
+ * device piece by piece while the next piece is read, and summed there.  `size` is the size the caller's
+ * FileInfo holds (FileView reads exactly that many bytes): a file that ends early or fails to read is
+ * zero-filled from that point, the result is computed over those bytes, and *read_error is set -- the
+ * reference's deferred FileViewException at close() (the Sender then flips md5[0], Sender.java:1136-1143).
+ * size == 0 opens nothing (FileView.java:62-72).
+ * rsh_block_sums_file: the Generator pass; the device holds two pieces at a time, so the file may be
+ * larger than HBM.  rsh_match_scan_file: the Sender pass; the source is assembled in HBM while a host
+ * thread digests the pieces in order (the whole-file MD5 of Sender.java:1241,1326). */
+int rsh_block_sums_file(rsh_ctx* ctx, const char* path, int64_t size, const rsh_header* h, const uint8_t seed[4],
+                        int32_t* weak_out, uint8_t* strong_out, int32_t* read_error);
+int rsh_match_scan_file(rsh_ctx* ctx, const char* path, int64_t size, const rsh_header* h, const int32_t* weak,
+                        const uint8_t* strong, const uint8_t seed[4], rsh_event* ev, int64_t ev_cap, int64_t* n_ev,
+                        uint8_t file_md5[16], int64_t* literal, int64_t* matched, rsh_scan_stats* stats,
+                        int32_t* read_error);
 
 /* ---- Receiver (Receiver.java:459-555 combineDataToFile, :557-578 copies, :204-209 blockSize) ----
  * Replays one file's de-multiplexed token stream -- putInt(len)+bytes, putInt(-(i+1)), putInt(0), exactly

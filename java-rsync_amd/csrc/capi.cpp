@@ -267,6 +267,9 @@ class HipBackend : public rsh::ScanBackend {
     HitCache cache_;
 };
 
+}  // namespace
+
+namespace rshi {
 // The device-resident Sender scan (everything but the whole-file MD5).  h validated by the caller;
 // n > 0, block_length > 0.  host_weak/host_strong may be null (then copied back from the device).
 //
@@ -453,7 +456,7 @@ int emit_events(rsh_ctx* c, rsh::ResolveResult& r, rsh_event* ev, int64_t cap, i
     return RSH_OK;
 }
 
-}  // namespace
+}  // namespace rshi
 
 extern "C" {
 
@@ -471,6 +474,8 @@ const char* rsh_strerror(int status) {
         case RSH_E_DEVICE: return "HIP device error or no gfx950 device";
         case RSH_E_NOMEM: return "out of memory";
         case RSH_E_BUSY: return "context in use by another thread";
+        case RSH_E_NOTFOUND: return "file not found (FileViewNotFound)";
+        case RSH_E_OPEN: return "file cannot be opened (FileViewOpenFailed)";
         default: return "unknown status";
     }
 }

@@ -109,6 +109,7 @@ struct rsh_ctx {
     PinnedBuf h_win0;    // window 0 of the current scan (its digest is computed on a host thread)
     PinnedBuf h_bucket;  // after a probe hit: {count, key, chunk indices} of the key that hit
     PinnedBuf h_files;   // the scan's rsh::ScanFile (a batch of one for the probe / gather kernels)
+    PinnedBuf h_stage;   // file ingest ring (ingest.cpp); never shared with the scan's buffers
     uint64_t first_used = 0;    // probe result slots handed out (see HipBackend::first_hit)
     int* abort_word = nullptr;  // device, uncached: the speculation launch of generation g stops once it reads g
     int gen = 0;
@@ -121,7 +122,7 @@ struct rsh_ctx {
                           &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pos, &h_out, &h_iv, &h_tiles, &h_keys, &h_first,
-                             &h_win, &h_ptiles, &h_hit, &h_win0, &h_bucket, &h_files})
+                             &h_win, &h_ptiles, &h_hit, &h_win0, &h_bucket, &h_files, &h_stage})
             b->release();
         if (abort_word) (void)hipFree(abort_word);
         if (ev_in) (void)hipEventDestroy(ev_in);
@@ -186,5 +187,11 @@ inline void skip_events(int64_t n, rsh::ResolveResult* r) {
         r->ev.push_back(rsh_event{s, std::min<int64_t>(kDefaultBlock, n - s), RSH_EV_LITERAL, 0, 0, 0});
     r->literal = n;
 }
+
+// capi.cpp: the device-resident Sender scan (everything but the whole-file MD5) and the event hand-out.
+int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h, const int32_t* d_weak,
+                const uint8_t* d_strong, const int32_t* host_weak, const uint8_t* host_strong, const uint8_t seed[4],
+                rsh::ResolveResult* res);
+int emit_events(rsh_ctx* c, rsh::ResolveResult& r, rsh_event* ev, int64_t cap, int64_t* n_ev);
 
 }  // namespace rshi

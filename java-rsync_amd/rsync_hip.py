@@ -23,11 +23,20 @@ LIB_PATH = os.path.join(HERE, "lib", "librsynchip.so")
 
 RSH_OK, RSH_E_INVAL, RSH_E_PROTOCOL, RSH_E_OVERFLOW, RSH_E_NOSPACE, RSH_E_DEVICE, RSH_E_NOMEM, RSH_E_BUSY = \
     0, -1, -2, -3, -4, -5, -6, -7
+RSH_E_NOTFOUND, RSH_E_OPEN = -8, -9
 EV_LITERAL, EV_MATCH = 1, 2
 
 
 class ProtocolError(Exception):
     """RsyncProtocolException (Connection.receiveChecksumHeader, Connection.java:28-38)."""
+
+
+class FileViewNotFound(FileNotFoundError):
+    """RSH_E_NOTFOUND (io/FileViewNotFound: new FileView on a missing file, FileView.java:74-75)."""
+
+
+class FileViewOpenFailed(OSError):
+    """RSH_E_OPEN (io/FileViewOpenFailed, FileView.java:76-78)."""
 
 
 class ContextBusyError(RuntimeError):
@@ -95,7 +104,7 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_coun
            "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
            "rsh_match_scan_device", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
            "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_receiver_combine",
-           "rsh_receiver_combine_device", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
+           "rsh_receiver_combine_device", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 
 _LIB = None
 
@@ -145,6 +154,10 @@ def lib():
         "rsh_receiver_combine": ([P, P, I64, HP, P, I64, I32, P, I64, ctypes.POINTER(CombineResult)], ctypes.c_int),
         "rsh_receiver_combine_device": ([P, P, I64, HP, P, I64, I32, P, I64, ctypes.POINTER(CombineResult)],
                                         ctypes.c_int),
+        "rsh_block_sums_file": ([P, ctypes.c_char_p, I64, HP, P, P, P, ctypes.POINTER(I32)], ctypes.c_int),
+        "rsh_match_scan_file": ([P, ctypes.c_char_p, I64, HP, P, P, P, P, I64, ctypes.POINTER(I64), P,
+                                 ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(ScanStats),
+                                 ctypes.POINTER(I32)], ctypes.c_int),
         "rsh_dev_alloc": ([P, I64, ctypes.POINTER(P)], ctypes.c_int),
         "rsh_dev_free": ([P, P], ctypes.c_int),
         "rsh_memcpy_h2d": ([P, P, P, I64], ctypes.c_int),
@@ -173,6 +186,10 @@ def _check(rc):
         raise MemoryError(msg)
     if rc == RSH_E_BUSY:
         raise ContextBusyError(msg)
+    if rc == RSH_E_NOTFOUND:
+        raise FileViewNotFound(msg)
+    if rc == RSH_E_OPEN:
+        raise FileViewOpenFailed(msg)
     detail = lib().rsh_last_error().decode()
     raise DeviceError(f"{msg}: {detail}" if detail else msg)
 
@@ -311,6 +328,37 @@ class Context:
         _check(rc)
         return ev[:n_ev.value], fm.tobytes(), lit.value, mat.value, stats.as_dict()
 
+
+    def block_sums_file(self, path, size, h, seed):
+        """Generator pass over a file (FileView reads of `size` bytes): (weak, strong, read_error)."""
+        s = np.frombuffer(bytes(seed), np.uint8).copy()
+        weak = np.zeros(max(h.chunk_count, 1), np.int32)
+        strong = np.zeros(max(h.chunk_count * h.digest_length, 1), np.uint8)
+        err = ctypes.c_int32()
+        _check(lib().rsh_block_sums_file(self._p, os.fsencode(path), size, ctypes.byref(h), _ptr(s), _ptr(weak),
+                                         _ptr(strong), ctypes.byref(err)))
+        return weak[:h.chunk_count], strong[:h.chunk_count * h.digest_length], bool(err.value)
+
+    def match_scan_file(self, path, size, h, weak, strong, seed):
+        """Sender pass over a file: (events, file_md5, literal, matched, stats, read_error)."""
+        s = np.frombuffer(bytes(seed), np.uint8).copy()
+        w = np.ascontiguousarray(weak, dtype=np.int32)
+        st = np.ascontiguousarray(strong, dtype=np.uint8)
+        cap = int(size // max(10 * h.block_length, 1) + 2 * h.chunk_count + 64) if h.block_length else size // 8192 + 2
+        ev = np.zeros(max(cap, 1), EVENT_DTYPE)
+        n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        fm = np.zeros(16, np.uint8)
+        stats = ScanStats()
+        err = ctypes.c_int32()
+        rc = lib().rsh_match_scan_file(self._p, os.fsencode(path), size, ctypes.byref(h), _ptr(w) if w.size else None,
+                                       _ptr(st) if st.size else None, _ptr(s), _ptr(ev), cap, ctypes.byref(n_ev),
+                                       _ptr(fm), ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(stats),
+                                       ctypes.byref(err))
+        if rc == RSH_E_NOSPACE:
+            ev = np.zeros(n_ev.value, EVENT_DTYPE)
+            rc = lib().rsh_fetch_events(self._p, _ptr(ev), n_ev.value, ctypes.byref(n_ev))
+        _check(rc)
+        return ev[:n_ev.value], fm.tobytes(), lit.value, mat.value, stats.as_dict(), bool(err.value)
 
     def receiver_combine(self, tokens, h, replica, defer_write=False, target_cap=None):
         """Receiver.combineDataToFile (Receiver.java:459-555): (target bytes, CombineResult).  The target is

@@ -4,7 +4,9 @@ Times, on one GPU, for a file pair held in host memory:
   rsh_block_sums  (H2D of the basis + Generator kernel + D2H of the table)
   rsh_match_scan  (H2D of source/table + scan + the serial whole-file MD5 on a host thread)
   rsh_file_md5    (the serial chain alone)
-and prints one JSON line.  usage: python e2e.py [GiB] [block]
+  rsh_block_sums_file / rsh_match_scan_file  (the same passes reading the files themselves, FileView
+                                              semantics; files in /dev/shm, i.e. the page cache)
+and prints one JSON line.  usage: python e2e.py [GiB] [block] [dir]
 """
 import ctypes
 import json
@@ -48,6 +50,26 @@ def main():
         out["match_scan_GBps"] = n / out["match_scan_s"] / 1e9
         out["file_md5_GBps"] = n / out["file_md5_s"] / 1e9
         out["scan_stats"] = st
+        d = sys.argv[3] if len(sys.argv) > 3 else "/dev/shm"
+        pb, ps = os.path.join(d, "rsh_e2e_basis"), os.path.join(d, "rsh_e2e_src")
+        try:
+            basis.tofile(pb)
+            src.tofile(ps)
+            del basis
+            t = time.perf_counter()
+            wf, sf, err = ctx.block_sums_file(pb, n, h, seed)
+            out["block_sums_file_s"] = time.perf_counter() - t
+            assert not err and (wf == w).all() and (sf == s).all()
+            t = time.perf_counter()
+            evf, md5f, litf, matf, _, err = ctx.match_scan_file(ps, n, h, w, s, seed)
+            out["match_scan_file_s"] = time.perf_counter() - t
+            assert not err and md5f == md5 and (litf, matf) == (lit, mat)
+            out["block_sums_file_GBps"] = n / out["block_sums_file_s"] / 1e9
+            out["match_scan_file_GBps"] = n / out["match_scan_file_s"] / 1e9
+        finally:
+            for f in (pb, ps):
+                if os.path.exists(f):
+                    os.remove(f)
         print(json.dumps(out))
 
 
