@@ -56,6 +56,7 @@ def parse():
                          "per round for all files) or one rsh_match_scan_device per file on a context pool")
     ap.add_argument("--cpu-sample-mib", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-identical", action="store_true", help="skip the identical-basis companion measurement")
     return ap.parse_args()
 
 
@@ -152,6 +153,39 @@ def main():
         ow, os_ = O.generator(blk, oh, bytes([1, 2, 3, 4]))
         assert int(ow[0]) == int(hw[k]) and os_.tobytes() == hs[k * dl:(k + 1) * dl].tobytes(), f"chunk {k}"
 
+    # the conservative companion: the same step against an identical basis (the basis table is the source's
+    # own), where the Sender must digest every source block -- a second full K1 -- and nothing poisons
+    ident = None
+    if a.variant == "half" and not a.no_identical:
+        d_weak2 = torch.empty_like(d_weak)
+        d_strong2 = torch.empty_like(d_strong)
+
+        def step_ident():
+            rc = L.rsh_block_sums_device(ctx.handle, ctypes.c_void_p(src.data_ptr()), n, ctypes.byref(h),
+                                         seed.ctypes.data, ctypes.c_void_p(d_weak2.data_ptr()),
+                                         ctypes.c_void_p(d_strong2.data_ptr()))
+            assert rc == 0, rc
+            rc = L.rsh_match_scan_device(ctx.handle, ctypes.c_void_p(src.data_ptr()), n, ctypes.byref(h),
+                                         ctypes.c_void_p(d_weak2.data_ptr()), ctypes.c_void_p(d_strong2.data_ptr()),
+                                         seed.ctypes.data, ev.ctypes.data, cap, ctypes.byref(n_ev),
+                                         ctypes.byref(lit), ctypes.byref(mat), None)
+            assert rc == 0 and mat.value == n, (rc, mat.value)  # every block matches
+
+        step_ident()
+        ctx.sync()
+        barrier()
+        t1 = time.perf_counter()
+        for _ in range(a.steps):
+            step_ident()
+        ctx.sync()
+        barrier()
+        dti = shard.reduce_over_ranks(time.perf_counter() - t1, "max", device="cuda")
+        ident = {"value": round(world * a.steps * 2 * n / dti / (1 << 30), 3),
+                 "ms_per_step": round(dti / a.steps * 1e3, 3),
+                 "note": "same step, basis identical to the source: the Sender digests every block "
+                         "(one MATCH run over all chunks)"}
+        del d_weak2, d_strong2
+
     bytes_step = 2 * n
     value = world * a.steps * bytes_step / dt / (1 << 30)
     achieved = n / (gen_ms / 1e3) / 1e9
@@ -194,6 +228,8 @@ def main():
             "stats": st.as_dict(),
         },
     }
+    if ident is not None:
+        res["identical_basis"] = ident
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(src, basis, B, dl, a.cpu_sample_mib << 20)
     if rank == 0:
