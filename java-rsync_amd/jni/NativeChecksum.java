@@ -58,6 +58,27 @@ final class NativeChecksum implements AutoCloseable {
         return matchScan(ctx, source, size, toArray(h), weak, strong, seed, fileMd5, sizes);
     }
 
+    /** As blockSums, reading the file natively (FileView semantics); true = read error (FileViewException). */
+    boolean blockSumsFile(String path, long size, Checksum.Header h, byte[] seed, int[] weak, byte[] strong) {
+        return blockSumsFile(ctx, path, size, toArray(h), seed, weak, strong);
+    }
+
+    /** As matchScan, reading the file natively; sizes = {sizeLiteral, sizeMatch, readError}. */
+    long[] matchScanFile(String path, long size, Checksum.Header h, int[] weak, byte[] strong, byte[] seed,
+            byte[] fileMd5, long[] sizes) {
+        return matchScanFile(ctx, path, size, toArray(h), weak, strong, seed, fileMd5, sizes);
+    }
+
+    /**
+     * Receiver.combineDataToFile (Receiver.java:459-555): result = {tokensUsed, targetLength, sizeLiteral,
+     * sizeMatch}; returns true when the deferred write left the replica as the file.
+     */
+    boolean receiverCombine(ByteBuffer tokens, long tokensLen, Checksum.Header h, ByteBuffer replica, long replicaLen,
+            boolean deferWrite, ByteBuffer target, long targetCap, long[] result, byte[] md5) {
+        return receiverCombine(ctx, tokens, tokensLen, toArray(h), replica, replicaLen, deferWrite, target, targetCap,
+                result, md5);
+    }
+
     private static int[] toArray(Checksum.Header h) {
         return new int[] { h.getChunkCount(), h.getBlockLength(), h.getDigestLength(), h.getRemainder() };
     }
@@ -75,4 +96,14 @@ final class NativeChecksum implements AutoCloseable {
 
     static native long[] matchScan(long ctx, ByteBuffer src, long n, int[] header, int[] weak, byte[] strong,
             byte[] seed, byte[] fileMd5Out, long[] sizesOut);
+
+    static native boolean blockSumsFile(long ctx, String path, long size, int[] header, byte[] seed, int[] weakOut,
+            byte[] strongOut);
+
+    static native long[] matchScanFile(long ctx, String path, long size, int[] header, int[] weak, byte[] strong,
+            byte[] seed, byte[] fileMd5Out, long[] sizesOut);
+
+    static native boolean receiverCombine(long ctx, ByteBuffer tokens, long tokensLen, int[] header,
+            ByteBuffer replica, long replicaLen, boolean deferWrite, ByteBuffer target, long targetCap,
+            long[] resultOut, byte[] md5Out);
 }

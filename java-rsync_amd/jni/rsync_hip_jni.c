@@ -12,9 +12,13 @@
  *   RSH_E_BUSY     -> java.lang.IllegalStateException (a context shared across threads; use forThread())
  *   RSH_E_DEVICE   -> java.lang.IllegalStateException (caller falls back to the Java path only if it
  *                     chose to; the library itself never falls back)
- * File I/O stays in Java (FileView semantics incl. zero-fill after read errors, FileView.java:209-271);
- * the Sender replays the returned events through its own sendDataFrom/putInt so channel framing is
- * untouched (Sender.java:794-809).
+ *   RSH_E_NOTFOUND -> ...internal.io.FileViewNotFound                (FileView.java:74-75)
+ *   RSH_E_OPEN     -> ...internal.io.FileViewOpenFailed              (FileView.java:76-78)
+ * blockSums / matchScan take the file bytes from Java (FileView semantics incl. zero-fill after read
+ * errors stay in Java, FileView.java:209-271); blockSumsFile / matchScanFile read the file natively with
+ * the same semantics and report a read error as a flag (the FileViewException the Java code would get
+ * at close()).  The Sender replays the returned events through its own sendDataFrom/putInt so channel
+ * framing is untouched (Sender.java:794-809).
  *
  * Build (needs a JDK): make -C java-rsync_amd jni JAVA_HOME=/path/to/jdk
  */
@@ -32,6 +36,8 @@ static void throw_status(JNIEnv* env, int rc) {
         case RSH_E_OVERFLOW: cls = "com/github/java/rsync/internal/session/Checksum$ChunkOverflow"; break;
         case RSH_E_INVAL: cls = "java/lang/IllegalArgumentException"; break;
         case RSH_E_NOMEM: cls = "java/lang/OutOfMemoryError"; break;
+        case RSH_E_NOTFOUND: cls = "com/github/java/rsync/internal/io/FileViewNotFound"; break;
+        case RSH_E_OPEN: cls = "com/github/java/rsync/internal/io/FileViewOpenFailed"; break;
         default: cls = "java/lang/IllegalStateException"; break;
     }
     jclass c = (*env)->FindClass(env, cls);
@@ -201,4 +207,136 @@ JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeC
     }
     free(ev);
     return out;
+}
+
+/* ---- the same passes reading the file natively (rsh_*_file: FileView.java:51-80,187-278 semantics) ---- */
+
+/* Returns true when the file could not be read to `size` (zero-filled from there: FileViewException). */
+JNIEXPORT jboolean JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_blockSumsFile(
+    JNIEnv* env, jclass cls, jlong ctx, jstring path, jlong size, jintArray hdr4, jbyteArray seed, jintArray weakOut,
+    jbyteArray strongOut) {
+    (void)cls;
+    rsh_header h;
+    int rc = header_from(env, hdr4, &h);
+    if (rc != RSH_OK || !path || (*env)->GetArrayLength(env, seed) != 4 ||
+        (*env)->GetArrayLength(env, weakOut) < h.chunk_count ||
+        (*env)->GetArrayLength(env, strongOut) < (jlong)h.chunk_count * h.digest_length) {
+        throw_status(env, rc != RSH_OK ? rc : RSH_E_INVAL);
+        return JNI_FALSE;
+    }
+    jbyte s4[4];
+    (*env)->GetByteArrayRegion(env, seed, 0, 4, s4);
+    const size_t C = (size_t)(h.chunk_count > 0 ? h.chunk_count : 0), dl = (size_t)(h.digest_length > 0 ? h.digest_length : 0);
+    int32_t* w = (int32_t*)malloc(C * 4 + 4);
+    uint8_t* st = (uint8_t*)malloc(C * dl + 1);
+    const char* cpath = (*env)->GetStringUTFChars(env, path, NULL);
+    int32_t read_error = 0;
+    rc = (w && st && cpath) ? rsh_block_sums_file((rsh_ctx*)(intptr_t)ctx, cpath, size, &h, (const uint8_t*)s4, w, st,
+                                                  &read_error)
+                            : RSH_E_NOMEM;
+    if (cpath) (*env)->ReleaseStringUTFChars(env, path, cpath);
+    if (rc == RSH_OK) {
+        (*env)->SetIntArrayRegion(env, weakOut, 0, (jsize)C, (const jint*)w);
+        (*env)->SetByteArrayRegion(env, strongOut, 0, (jsize)(C * dl), (const jbyte*)st);
+    }
+    free(st);
+    free(w);
+    if (rc != RSH_OK) throw_status(env, rc);
+    return read_error ? JNI_TRUE : JNI_FALSE;
+}
+
+/* As matchScan, reading the source natively; sizesOut[3] = {sizeLiteral, sizeMatch, readError}. */
+JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_matchScanFile(
+    JNIEnv* env, jclass cls, jlong ctx, jstring path, jlong size, jintArray hdr4, jintArray weak, jbyteArray strong,
+    jbyteArray seed, jbyteArray fileMd5Out, jlongArray sizesOut) {
+    (void)cls;
+    rsh_header h;
+    int rc = header_from(env, hdr4, &h);
+    if (rc != RSH_OK || !path || (*env)->GetArrayLength(env, seed) != 4 ||
+        (*env)->GetArrayLength(env, fileMd5Out) != 16 || (*env)->GetArrayLength(env, sizesOut) < 3) {
+        throw_status(env, rc != RSH_OK ? rc : RSH_E_INVAL);
+        return NULL;
+    }
+    jbyte s4[4];
+    (*env)->GetByteArrayRegion(env, seed, 0, 4, s4);
+    int64_t cap = (size / (10 * (int64_t)(h.block_length > 0 ? h.block_length : 8192))) + 2 * (int64_t)h.chunk_count + 64;
+    int64_t n_ev = 0, lit = 0, mat = 0;
+    int32_t read_error = 0;
+    rsh_event* ev = (rsh_event*)malloc((size_t)cap * sizeof(rsh_event));
+    const jsize nw = weak ? (*env)->GetArrayLength(env, weak) : 0;
+    const jsize ns = strong ? (*env)->GetArrayLength(env, strong) : 0;
+    int32_t* w = (int32_t*)malloc((size_t)nw * 4 + 4);
+    uint8_t* st = (uint8_t*)malloc((size_t)ns + 1);
+    const char* cpath = (*env)->GetStringUTFChars(env, path, NULL);
+    uint8_t md5[16];
+    if (!ev || !w || !st || !cpath) {
+        rc = RSH_E_NOMEM;
+    } else if (h.chunk_count > 0 && (nw < h.chunk_count || (jlong)ns < (jlong)h.chunk_count * h.digest_length)) {
+        rc = RSH_E_INVAL;
+    } else {
+        if (nw) (*env)->GetIntArrayRegion(env, weak, 0, nw, (jint*)w);
+        if (ns) (*env)->GetByteArrayRegion(env, strong, 0, ns, (jbyte*)st);
+        rc = rsh_match_scan_file((rsh_ctx*)(intptr_t)ctx, cpath, size, &h, nw ? w : NULL, ns ? st : NULL,
+                                 (const uint8_t*)s4, ev, cap, &n_ev, md5, &lit, &mat, NULL, &read_error);
+        if (rc == RSH_E_NOSPACE) {
+            rsh_event* grown = (rsh_event*)realloc(ev, (size_t)n_ev * sizeof(rsh_event));
+            if (!grown) rc = RSH_E_NOMEM;
+            else {
+                ev = grown;
+                rc = rsh_fetch_events((rsh_ctx*)(intptr_t)ctx, ev, n_ev, &n_ev);
+            }
+        }
+    }
+    if (cpath) (*env)->ReleaseStringUTFChars(env, path, cpath);
+    free(st);
+    free(w);
+    jlongArray out = NULL;
+    if (rc == RSH_OK) out = (*env)->NewLongArray(env, (jsize)(4 * n_ev));
+    if (out) {
+        jlong* o = (*env)->GetLongArrayElements(env, out, NULL);
+        for (int64_t i = 0; i < n_ev; ++i) {
+            o[4 * i + 0] = ev[i].kind;
+            o[4 * i + 1] = ev[i].offset;
+            o[4 * i + 2] = ev[i].length;
+            o[4 * i + 3] = (jlong)(uint32_t)ev[i].index | ((jlong)ev[i].count << 32);
+        }
+        (*env)->ReleaseLongArrayElements(env, out, o, 0);
+        (*env)->SetByteArrayRegion(env, fileMd5Out, 0, 16, (const jbyte*)md5);
+        jlong sizes[3] = {lit, mat, read_error};
+        (*env)->SetLongArrayRegion(env, sizesOut, 0, 3, sizes);
+    }
+    free(ev);
+    if (rc != RSH_OK) throw_status(env, rc);
+    return out;
+}
+
+/* ---- Receiver.combineDataToFile (Receiver.java:459-555) over direct buffers ----
+ * tokens: the file's de-multiplexed token stream; replica may be null; target receives the file.
+ * resultOut[4] = {tokensUsed, targetLength, sizeLiteral, sizeMatch}; md5Out[16] = the Receiver's digest.
+ * Returns combineDataToFile's value (true: deferred write, the replica is the file). */
+JNIEXPORT jboolean JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_receiverCombine(
+    JNIEnv* env, jclass cls, jlong ctx, jobject tokens, jlong tokensLen, jintArray hdr4, jobject replica,
+    jlong replicaLen, jboolean deferWrite, jobject target, jlong targetCap, jlongArray resultOut, jbyteArray md5Out) {
+    (void)cls;
+    rsh_header h;
+    int rc = header_from(env, hdr4, &h);
+    const uint8_t* t = tokens ? (const uint8_t*)(*env)->GetDirectBufferAddress(env, tokens) : NULL;
+    const uint8_t* r = replica ? (const uint8_t*)(*env)->GetDirectBufferAddress(env, replica) : NULL;
+    uint8_t* o = target ? (uint8_t*)(*env)->GetDirectBufferAddress(env, target) : NULL;
+    if (rc != RSH_OK || !t || (replica && !r) || (*env)->GetArrayLength(env, resultOut) < 4 ||
+        (*env)->GetArrayLength(env, md5Out) != 16) {
+        throw_status(env, rc != RSH_OK ? rc : RSH_E_INVAL);
+        return JNI_FALSE;
+    }
+    rsh_combine_result res;
+    rc = rsh_receiver_combine((rsh_ctx*)(intptr_t)ctx, t, tokensLen, &h, r, r ? replicaLen : 0, deferWrite ? 1 : 0, o,
+                              o ? targetCap : 0, &res);
+    if (rc != RSH_OK) {
+        throw_status(env, rc);
+        return JNI_FALSE;
+    }
+    jlong vals[4] = {res.tokens_used, res.target_len, res.literal, res.matched};
+    (*env)->SetLongArrayRegion(env, resultOut, 0, 4, vals);
+    (*env)->SetByteArrayRegion(env, md5Out, 0, 16, (const jbyte*)res.md5);
+    return res.intact ? JNI_TRUE : JNI_FALSE;
 }
