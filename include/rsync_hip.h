@@ -75,7 +75,7 @@ typedef struct {
     int64_t flushes;         /* FileView.isFull flushes (Sender.java:1294-1302)                */
     double device_ms;        /* wall time of the bulk device phase (speculation kernels + copies) */
     double resolver_ms;      /* host resolver time (including its small device round trips)   */
-    double table_ms;         /* host sort of the received table (overlaps the device phase)   */
+    double table_ms;         /* host index of the received table (chained hash, built lazily)  */
     int64_t head_steps;      /* resolver steps taken before the aligned speculation landed    */
     int64_t speculation_aborted; /* 1: the scan ended first and the speculation launch was stopped;
                                     2: the scan ended in head mode before the speculation was launched */

@@ -29,6 +29,7 @@ constexpr int32_t kMaxLive = 256;     // files resolved concurrently (one host t
 constexpr int kDeferRounds = 2;       // rounds in head mode before the speculation is launched
 constexpr int32_t kMaxWorkers = 32;   // host threads running the resolvers
 constexpr size_t kFiberStack = 512 * 1024;
+constexpr int32_t kEagerSortChunks = 1 << 16;  // tables up to this size are sorted before the first round
 constexpr int64_t kPad = 16;
 
 int64_t pad16(int64_t v) { return (v + kPad - 1) / kPad * kPad; }
@@ -188,6 +189,9 @@ void fiber_main(uint32_t hi, uint32_t lo) {
     FileScan& fs = *reinterpret_cast<FileScan*>(((uintptr_t)hi << 32) | lo);
     BatchBackend& be = fs.be;
     Batch& b = *be.b;
+    // small tables are sorted up front, here on the worker threads (in parallel across files): a segment's
+    // resolvers would otherwise spend their first rounds in linear bucket scans before the lazy sort
+    if (fs.C <= kEagerSortChunks) fs.table.build();
     while (!resolve_run(fs.n, fs.table, be, &fs.rs, &fs.res,
                         [&] { return be.head && b.landed.load(std::memory_order_acquire); }))
         be.head = false;
@@ -521,7 +525,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
 
     hipStream_t st = c->stream, aux = c->aux;
     RSH_BHIP(hipEventRecord(c->ev_in, st));  // whatever produced the inputs on the context stream
-    // (aux) the received tables, to pinned host memory in one kernel
+    // (stream) the received tables, to pinned host memory in one kernel
     CopyEnt* tc = S->h_copies.as<CopyEnt>();
     int64_t max_tab = 0;
     uint32_t ntc = 0;
@@ -533,9 +537,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             tc[ntc++] = CopyEnt{fs.d_strong, S->h_strong.as<uint8_t>() + fs.off_ts, (int64_t)fs.C * fs.dl};
         max_tab = std::max<int64_t>(max_tab, (int64_t)fs.C * 4);
     }
-    RSH_BHIP(hipStreamWaitEvent(aux, c->ev_in, 0));
-    RSH_BHIP(launch_copy_many(tc, ntc, max_tab, aux));
-    RSH_BHIP(hipEventRecord(c->ev_tab, aux));
+    RSH_BHIP(launch_copy_many(tc, ntc, max_tab, st));  // stream order: after whatever produced them
+    RSH_BHIP(hipEventRecord(c->ev_tab, st));
     // (stream) the probe hashes and windows 0
     RSH_BHIP(hipMemsetAsync(S->slots.p, 0, (size_t)tns * 8, st));
     TableEnt* te = S->h_tabents.as<TableEnt>();
@@ -557,7 +560,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     // the batched aligned speculation (deferred; see scan_device in capi.cpp)
     const int gen = ++c->gen;
     CopyEnt* sc = S->h_ccopies.as<CopyEnt>() + NF;
-    auto launch_spec = [&]() -> int {
+    // K1 over the sources needs nothing but the sources; the chain flags need the received tables (ev_in)
+    bool k1_launched = false;
+    auto launch_spec_k1 = [&]() -> int {
+        k1_launched = true;
         if (!groups.empty())
             RSH_BHIP(hipMemcpyAsync(S->k1_groups.p, groups.data(), groups.size() * sizeof(K1Group),
                                     hipMemcpyHostToDevice, aux));
@@ -566,6 +572,14 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                                     aux));
         RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>(), (uint32_t)groups.size(), S->k1_lanes.as<K1Lane>(),
                                          (uint32_t)lanes.size(), lane_align, seed_word(seed), aux, c->abort_word, gen));
+        return RSH_OK;
+    };
+    auto launch_spec = [&]() -> int {
+        if (!k1_launched) {
+            const int r = launch_spec_k1();
+            if (r != RSH_OK) return r;
+        }
+        RSH_BHIP(hipStreamWaitEvent(aux, c->ev_in, 0));
         FlagEnt* fe = S->h_flagents.as<FlagEnt>();
         uint32_t max_nf = 0, nsc = 0;
         int64_t max_len = 0;
@@ -589,6 +603,18 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         return RSH_OK;
     };
 
+    // policy (A/B via RSH_BATCH_SPEC; the default, measured best on config 4, is head mode with the launch
+    // after kDeferRounds rounds): "early" = the speculation's K1 starts now, beside whatever the device is
+    // still doing (e.g. the Generator), resolvers in head mode until it lands; "wait" = as early, but the
+    // resolvers start only once it has landed; a number N = launch after N rounds
+    static const char* pol = getenv("RSH_BATCH_SPEC");
+    static const bool wait_spec = pol && strcmp(pol, "wait") == 0;
+    static const bool early_spec = pol && (strcmp(pol, "early") == 0 || wait_spec);
+    static const int defer_rounds = (pol && !early_spec) ? atoi(pol) : kDeferRounds;
+    if (early_spec) {
+        const int r = launch_spec_k1();
+        if (r != RSH_OK) return r;
+    }
     const double enq_ms = ms_since(t0);
     RSH_BHIP(hipEventSynchronize(c->ev_tab));
     RSH_BHIP(hipStreamSynchronize(st));
@@ -635,13 +661,13 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         F[f].aligned_weak = S->haw.as<int32_t>() + fs.off_na;
     }
 
-    // policy (A/B via RSH_BATCH_SPEC): "wait" = land the speculation before the resolvers start (no head
-    // mode), otherwise = head mode, speculation launched after that many rounds
-    static const char* pol = getenv("RSH_BATCH_SPEC");
-    static const bool wait_spec = pol && strcmp(pol, "wait") == 0;
-    static const int defer_rounds = (pol && !wait_spec) ? atoi(pol) : kDeferRounds;
     int spec_rc = RSH_OK;
     bool spec_launched = false;
+    if (early_spec && !wait_spec) {
+        spec_rc = launch_spec();  // the tail (flags, downloads) behind the K1 already running
+        if (spec_rc != RSH_OK) return spec_rc;
+        spec_launched = true;
+    }
     if (wait_spec) {
         spec_rc = launch_spec();
         if (spec_rc != RSH_OK) return spec_rc;

@@ -38,67 +38,24 @@ struct HostTrace {
 }  // namespace
 
 void ChunkTable::build() {
-    HostTrace tr("tab_sort", chunk_count, &host_times().sort_ms);
-    if (sorted_) return;
+    HostTrace tr("tab_index", chunk_count, &host_times().sort_ms);
+    if (indexed_) return;
     const auto t0 = std::chrono::steady_clock::now();
-    std::vector<uint32_t>& sorted_key = sorted_key_;
-    std::vector<int32_t>& sorted_idx = sorted_idx_;
     const int32_t n = chunk_count;
-    std::vector<uint32_t> k2(n);
-    std::vector<int32_t> i2(n);
-    sorted_key.resize(n);
-    sorted_idx.resize(n);
-    for (int32_t i = 0; i < n; ++i) {
-        sorted_key[i] = (uint32_t)weak[i];
-        sorted_idx[i] = i;
-    }
-    // LSD radix sort, three stable passes of 11/11/10 bits (cache-resident counters): ties keep
-    // ascending chunk index (Multimap insertion order, Multimap.java:27-61).
-    uint32_t cnt[2049];
-    std::vector<uint32_t>* ks = &sorted_key;
-    std::vector<int32_t>* is = &sorted_idx;
-    std::vector<uint32_t>* kd = &k2;
-    std::vector<int32_t>* id = &i2;
-    for (int pass = 0; pass < 3; ++pass) {
-        const int sh = 11 * pass;
-        const uint32_t mask = pass < 2 ? 0x7FFu : 0x3FFu;
-        std::fill(cnt, cnt + 2049, 0u);
-        const uint32_t* kp = ks->data();
-        for (int32_t i = 0; i < n; ++i) cnt[((kp[i] >> sh) & mask) + 1]++;
-        for (int d = 0; d < 2048; ++d) cnt[d + 1] += cnt[d];
-        const int32_t* ip = is->data();
-        uint32_t* kdp = kd->data();
-        int32_t* idp = id->data();
-        for (int32_t i = 0; i < n; ++i) {
-            const uint32_t dgt = (kp[i] >> sh) & mask;
-            const uint32_t at = cnt[dgt]++;
-            kdp[at] = kp[i];
-            idp[at] = ip[i];
-        }
-        std::swap(ks, kd);
-        std::swap(is, id);
-    }
-    if (ks != &sorted_key) {  // odd pass count: the result sits in the scratch pair
-        sorted_key.swap(*ks);
-        sorted_idx.swap(*is);
-    }
-    sorted_ = true;
-    sort_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-}
-
-void ChunkTable::build_filter() {
-    // the received table usually sits in pinned (uncached for the CPU) memory: take a cacheable copy first
-    weak_copy_.assign(weak, weak + chunk_count);
+    weak_copy_.assign(weak, weak + n);
     weak = weak_copy_.data();
-    uint32_t bits = 1u << 12;
-    while (bits < 32u * (uint32_t)chunk_count && bits < (1u << 26)) bits <<= 1;
-    filter_mask_ = bits - 1;
-    filter_.assign(bits / 64, 0ull);
-    for (int32_t i = 0; i < chunk_count; ++i) {
-        const uint32_t h = ((uint32_t)weak[i] * 0x9E3779B1u) >> 7;
-        filter_[(h & filter_mask_) >> 6] |= 1ull << (h & 63);
+    uint32_t slots = 1u << 10;
+    while (slots < 2u * (uint32_t)n && slots < (1u << 30)) slots <<= 1;
+    index_mask_ = slots - 1;
+    head_.assign(slots, -1);
+    next_.resize((size_t)n);
+    for (int32_t i = n - 1; i >= 0; --i) {  // prepend in descending order: chains ascend
+        const uint32_t h = ((uint32_t)weak[i] * 0x9E3779B1u >> 7) & index_mask_;
+        next_[(size_t)i] = head_[h];
+        head_[h] = i;
     }
-    has_filter_ = true;
+    indexed_ = true;
+    sort_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 const int32_t* ChunkTable::bucket(int32_t key, int32_t* size) {
@@ -106,24 +63,18 @@ const int32_t* ChunkTable::bucket(int32_t key, int32_t* size) {
         *size = (int32_t)primed_.size();
         return primed_.data();
     }
-    if (!has_filter_ && scan_lookups_ >= 2) build_filter();  // a scan that needs one or two lookups skips it
-    if (has_filter_ && !maybe_has(key)) {
-        *size = 0;
-        return nullptr;
-    }
     HostTrace tr("bucket", key, &host_times().bucket_ms);
-    if (!sorted_ && scan_lookups_ >= kScanLookups) build();
-    if (sorted_) {
-        const uint32_t k = (uint32_t)key;
-        auto a = std::lower_bound(sorted_key_.begin(), sorted_key_.end(), k);
-        auto b = std::upper_bound(a, sorted_key_.end(), k);
-        *size = (int32_t)(b - a);
-        return sorted_idx_.data() + (a - sorted_key_.begin());
+    if (!indexed_ && scan_lookups_ >= kScanLookups) build();
+    scratch_.clear();
+    if (indexed_) {
+        for (int32_t i = head_[((uint32_t)key * 0x9E3779B1u >> 7) & index_mask_]; i >= 0; i = next_[(size_t)i])
+            if (weak[i] == key) scratch_.push_back(i);
+        *size = (int32_t)scratch_.size();
+        return scratch_.data();
     }
     ++scan_lookups_;
     int32_t cnt = 0;  // counting pass (vectorises); most lookups find nothing
     for (int32_t i = 0; i < chunk_count; ++i) cnt += weak[i] == key;
-    scratch_.clear();
     if (cnt) {
         scratch_.reserve(cnt);
         for (int32_t i = 0; i < chunk_count; ++i)

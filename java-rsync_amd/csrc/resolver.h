@@ -38,12 +38,12 @@ struct ChunkTable {
     const uint8_t* strong = nullptr; // chunk_count * digest_length
 
     // Ascending chunk indices whose weak key is `key` (a Multimap bucket, in insertion order); valid
-    // until the next call.  The first kScanLookups lookups are linear scans of `weak`; after that the
-    // table is radix-sorted once and lookups binary-search it.  A scan that poisons early (quirk B)
-    // needs a handful of lookups and never pays for the sort.
+    // until the next call.  The first kScanLookups lookups are linear scans of `weak`; then the table is
+    // indexed once (a chained hash over a private copy of the keys, built in one pass) and lookups walk
+    // one chain.  A scan that poisons early (quirk B) needs a handful of lookups and never builds it.
     const int32_t* bucket(int32_t key, int32_t* size);
-    void build();  // sort now (radix sort of (weak, index))
-    bool sorted() const { return sorted_; }
+    void build();  // index now
+    bool indexed() const { return indexed_; }
     double sort_ms = 0;  // time spent in build()
     int32_t chunk_length(int32_t idx) const {  // Checksum.java:197-203
         return (idx == chunk_count - 1 && remainder > 0) ? remainder : block_length;
@@ -51,7 +51,7 @@ struct ChunkTable {
     // Distinct weak keys of the chunks whose digest equals d (the only ones a stale digest can match).
     void keys_with_digest(const uint8_t* d, std::vector<int32_t>* keys) const;
 
-    static constexpr int kScanLookups = 16;
+    static constexpr int kScanLookups = 2;
     // The bucket of `key` computed elsewhere (the device, in the round trip that found a probe hit):
     // idx ascending.  The next bucket(key) returns it without touching the table.
     void prime(int32_t key, const int32_t* idx, int32_t count) {
@@ -61,25 +61,16 @@ struct ChunkTable {
     }
 
   private:
-    // membership filter over the keys (one bit per hash slot, >= 32 slots per chunk): most lookups are
-    // for keys that are not in the table (the next aligned window after a match, in an edited file)
-    // and are answered by one bit test, without a scan and without counting towards the sort
-    bool has_filter_ = false;
-    uint32_t filter_mask_ = 0;
-    std::vector<uint64_t> filter_;
-    std::vector<int32_t> weak_copy_;
-    void build_filter();
-    bool maybe_has(int32_t key) const {
-        const uint32_t h = ((uint32_t)key * 0x9E3779B1u) >> 7;
-        return (filter_[(h & filter_mask_) >> 6] >> (h & 63)) & 1;
-    }
     bool primed_valid_ = false;
     int32_t primed_key_ = 0;
     std::vector<int32_t> primed_;
-    bool sorted_ = false;
+    bool indexed_ = false;
     int scan_lookups_ = 0;
-    std::vector<uint32_t> sorted_key_;  // bucket keys, sorted (stable: ascending chunk index per key)
-    std::vector<int32_t> sorted_idx_;
+    // chained hash index: head_[hash(key)] = smallest chunk index with that hash, next_[i] = the next
+    // larger one (chains ascend, so a bucket comes out in Multimap insertion order)
+    uint32_t index_mask_ = 0;
+    std::vector<int32_t> head_, next_;
+    std::vector<int32_t> weak_copy_;  // the received table usually sits in pinned host memory
     std::vector<int32_t> scratch_;
 };
 
