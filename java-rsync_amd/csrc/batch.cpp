@@ -117,7 +117,7 @@ class BatchBackend : public ScanBackend {
     uint8_t seed[4];
     ChunkTable* table = nullptr;
     std::vector<uint8_t> haw_ready;
-    int64_t win_pos = -1;  // the last probe's first hit: its window is in `hit`
+    int64_t win_pos[HIT_WINDOWS] = {-1};  // the last probe's hits whose windows are in `hit`
     int64_t t_pos = -1;    // the last hit returned: its weak sum t_val is known
     int32_t t_val = 0;
     HitCache cache;
@@ -228,8 +228,11 @@ void BatchBackend::md5_at(int64_t p, uint8_t out[16]) {
     const int64_t w = std::min<int64_t>(B, n - p);
     const uint8_t* src = nullptr;
     if (p == 0 && win0) src = win0;                 // copied to the host before the first round
-    else if (p == win_pos) src = hit + 16;          // came back with the probe result
     else {
+        for (int k = 0; k < HIT_WINDOWS; ++k)
+            if (p == win_pos[k]) src = hit + 16 + (int64_t)k * B;  // came back with the probe result
+    }
+    if (!src) {
         FileScan& fs = scan_of(b, f);
         fs.req = Req{};
         fs.req.kind = Req::WIN;
@@ -274,7 +277,8 @@ int64_t BatchBackend::first_hit(const ProbeInterval* iv, int64_t count, const st
     if (count == 1 && fs.req.out) cache.fill(iv[0], keys, *fs.req.out, n - B);
     else cache.valid = false;
     if (p < 0) return -1;
-    win_pos = t_pos = p;
+    window_slots(*fs.req.out, win_pos);
+    t_pos = p;
     t_val = *reinterpret_cast<const int32_t*>(hit);
     if (bucket[0] <= HIT_BUCKET_CAP) {  // ascending chunk order, as the Multimap keeps it
         std::vector<int32_t> idx(bucket + 2, bucket + 2 + bucket[0]);
@@ -486,7 +490,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         fs.off_as = tas, tas += fs.na * fs.dl;
         fs.off_nf = tnf, tnf += fs.nf;
         fs.off_ns = tns, tns += fs.ns;
-        fs.off_hit = thit, thit += pad16(16 + fs.B);
+        fs.off_hit = thit, thit += pad16(16 + HIT_WINDOWS * fs.B);
         fs.off_w0 = tw0, tw0 += pad16(std::min<int64_t>(fs.B, fs.n));
         maxC = std::max<int64_t>(maxC, fs.C);
     }

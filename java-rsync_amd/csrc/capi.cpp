@@ -106,9 +106,12 @@ class HipBackend : public rsh::ScanBackend {
             md5_0(out);
             return;
         }
-        if (p == win_pos_) {  // the window came back with the probe result
+        int slot = -1;
+        for (int k = 0; k < rsh::HIT_WINDOWS; ++k)
+            if (p == win_pos_[k]) slot = k;
+        if (slot >= 0) {  // the window came back with the probe result
             rsh::HostMd5 h;
-            h.update(c_->h_hit.as<uint8_t>() + 16, (size_t)w);
+            h.update(c_->h_hit.as<uint8_t>() + 16 + (int64_t)slot * B_, (size_t)w);
             h.update(seed_, 4);
             h.final(out);
             return;
@@ -160,7 +163,7 @@ class HipBackend : public rsh::ScanBackend {
         rsh::ProbeTile* ht = pin<rsh::ProbeTile>(c_->h_tiles, (int64_t)tiles_.size() + 1);
         rsh::PartialTile* hpt = pin<rsh::PartialTile>(c_->h_ptiles, (int64_t)ptiles_.size() + 1);
         rsh::ProbeOut* hf = pin<rsh::ProbeOut>(c_->h_first, 1);
-        uint8_t* hh = pin<uint8_t>(c_->h_hit, 16 + B_);
+        uint8_t* hh = pin<uint8_t>(c_->h_hit, 16 + rsh::HIT_WINDOWS * B_);
         int32_t* hb = pin<int32_t>(c_->h_bucket, 2 + rsh::HIT_BUCKET_CAP + 1);  // + the request list {0}
         rsh::ScanFile* F = file();
         ok(c_->partials.ensure((ptiles_.size() + 1) * sizeof(int4)));
@@ -217,7 +220,8 @@ class HipBackend : public rsh::ScanBackend {
         if (count == 1) cache_.fill(iv[0], keys, *hf, n_ - B_);
         else cache_.valid = false;
         if (hf->first == ~0ull) return -1;
-        win_pos_ = t_pos_ = (int64_t)hf->first;
+        rsh::window_slots(*hf, win_pos_);
+        t_pos_ = (int64_t)hf->first;
         t_val_ = *reinterpret_cast<const int32_t*>(hh);
         if (hb[0] <= rsh::HIT_BUCKET_CAP) {  // ascending chunk order, as the Multimap keeps it
             std::sort(hb + 2, hb + 2 + hb[0]);
@@ -261,7 +265,7 @@ class HipBackend : public rsh::ScanBackend {
         F->C = t_.chunk_count;
         return F;
     }
-    int64_t win_pos_ = -1;  // position of the last probe's first hit: its window is on the host (h_hit)
+    int64_t win_pos_[rsh::HIT_WINDOWS] = {-1};  // windows of the last probe's hits on the host (h_hit)
     int64_t t_pos_ = -1;    // position of the last hit returned: its weak sum t_val_ is known
     int32_t t_val_ = 0;
     HitCache cache_;

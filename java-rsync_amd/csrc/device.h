@@ -91,7 +91,8 @@ struct ScanFile {
     int32_t iv0, niv;                 // the file's intervals in the round's ProbeIv array
     int32_t pad;
     int32_t* bucket;                  // device: {count, key, idx[0 .. HIT_BUCKET_CAP)}
-    uint8_t* hit;                     // pinned host: T(p) in bytes 0..3, the window at p from byte 16
+    uint8_t* hit;                     // pinned host: T(p) in bytes 0..3, window k of the k-th smallest listed
+                                      // hit at 16 + k B (k < HIT_WINDOWS; k = 0: the first hit)
 };
 struct ProbeIv {
     int64_t a, b, anchor;

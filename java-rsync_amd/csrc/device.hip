@@ -1472,16 +1472,37 @@ __global__ __launch_bounds__(256) void hit_window_kernel(const ScanFile* __restr
         }
         return;
     }
-    uint8_t* __restrict__ h_win = F.hit + 16;
-    for (int64_t o = 16 * ((int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x); o < w;
-         o += 16 * (int64_t)(gridDim.x - 1) * blockDim.x) {
-        if (o + 16 <= w) {
+    // blocks 1 + 16 k .. 16 k + 16 copy window k: the k-th smallest listed hit (k = 0 is the first hit; the
+    // others only when the list is complete), so the resolver has the digest input of the next few
+    // events the hit list answers without another round trip
+    const int slot = (int)(blockIdx.x - 1) / 16, part = (int)(blockIdx.x - 1) % 16;
+    int64_t pw = p;
+    if (slot > 0) {
+        const unsigned long long cnt = F.out->count;
+        if (cnt > (unsigned long long)PROBE_HITS_CAP || (unsigned long long)slot >= cnt) return;
+        __shared__ long long sel;
+        if (threadIdx.x == 0) sel = -1;
+        __syncthreads();
+        if (threadIdx.x < (int)cnt) {  // rank of entry t among the listed positions (distinct)
+            const unsigned long long me = F.out->pos[threadIdx.x];
+            int rank = 0;
+            for (int j = 0; j < (int)cnt; ++j) rank += F.out->pos[j] < me;
+            if (rank == slot) sel = (long long)me;
+        }
+        __syncthreads();
+        pw = (int64_t)sel;
+        if (pw < 0) return;
+    }
+    const int64_t ww = (n - pw < B ? n - pw : B);
+    uint8_t* __restrict__ h_win = F.hit + 16 + (int64_t)slot * B;
+    for (int64_t o = 16 * ((int64_t)part * blockDim.x + threadIdx.x); o < ww; o += 16 * 16 * (int64_t)blockDim.x) {
+        if (o + 16 <= ww) {
             uint32_t q[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int i = 0; i < 16; ++i) q[i >> 2] |= (uint32_t)data[p + o + i] << (8 * (i & 3));
+            for (int i = 0; i < 16; ++i) q[i >> 2] |= (uint32_t)data[pw + o + i] << (8 * (i & 3));
             *reinterpret_cast<uint4*>(h_win + o) = make_uint4(q[0], q[1], q[2], q[3]);
         } else {
-            for (int64_t i = o; i < w; ++i) h_win[i] = data[p + i];
+            for (int64_t i = o; i < ww; ++i) h_win[i] = data[pw + i];
         }
     }
 }
@@ -1510,7 +1531,7 @@ __global__ __launch_bounds__(256) void hit_bucket_kernel(const ScanFile* __restr
 hipError_t launch_hit_window(const ScanFile* files, const ProbeIv* ivs, const int32_t* req, int32_t nreq, int32_t max_C,
                              hipStream_t s) {
     if (nreq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(hit_window_kernel, dim3(1 + 16, (uint32_t)nreq), dim3(256), 0, s, files, ivs, req);
+    hipLaunchKernelGGL(hit_window_kernel, dim3(1 + 16 * HIT_WINDOWS, (uint32_t)nreq), dim3(256), 0, s, files, ivs, req);
     if (max_C > 0)
         hipLaunchKernelGGL(hit_bucket_kernel, dim3((uint32_t)((max_C + 8 * 256 - 1) / (8 * 256)), (uint32_t)nreq),
                            dim3(256), 0, s, files, req);

@@ -21,6 +21,22 @@ struct ProbeOut {
     uint32_t key[PROBE_HITS_CAP];
 };
 
+// Windows the hit kernel returns with a probe: slot k holds the window at the k-th smallest listed hit
+// (slot 0: the first hit, always; slots >= 1 only when the list is complete).  More than one slot trades
+// D2H bytes and host digests for round trips; on config 4 (128 x 128 MiB) 4 slots cut the rounds from 26
+// to 18 but gave no faster step on 50%-modified bases and a slower one on identical bases (host digests
+// of windows the speculation would have supplied), so one slot it is.
+constexpr int HIT_WINDOWS = 1;
+inline void window_slots(const ProbeOut& o, int64_t (&slot)[HIT_WINDOWS]) {
+    for (int k = 0; k < HIT_WINDOWS; ++k) slot[k] = -1;
+    if (o.first == ~0ull) return;
+    slot[0] = (int64_t)o.first;
+    if (o.count > (unsigned long long)PROBE_HITS_CAP) return;
+    std::vector<int64_t> p(o.pos, o.pos + o.count);
+    std::sort(p.begin(), p.end());
+    for (int k = 1; k < HIT_WINDOWS && k < (int)p.size(); ++k) slot[k] = p[(size_t)k];
+}
+
 // The hits of the last single-interval range probe.  A later probe of [a', b') with the same key function
 // E and key set, starting inside the probed range, is answered from the list without a device round trip
 // when the list covers it, or is cut to the part beyond the probed range (the answer is the same: the
