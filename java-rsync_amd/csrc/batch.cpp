@@ -117,7 +117,7 @@ class BatchBackend : public ScanBackend {
     uint8_t seed[4];
     ChunkTable* table = nullptr;
     std::vector<uint8_t> haw_ready;
-    int64_t win_pos[HIT_WINDOWS] = {-1};  // the last probe's hits whose windows are in `hit`
+    int64_t win_pos[HIT_WINDOWS] = {-1, -1, -1, -1};  // the last probe's hits whose windows are in `hit`
     int64_t t_pos = -1;    // the last hit returned: its weak sum t_val is known
     int32_t t_val = 0;
     HitCache cache;
@@ -277,14 +277,10 @@ int64_t BatchBackend::first_hit(const ProbeInterval* iv, int64_t count, const st
     if (count == 1 && fs.req.out) cache.fill(iv[0], keys, *fs.req.out, n - B);
     else cache.valid = false;
     if (p < 0) return -1;
-    window_slots(*fs.req.out, win_pos);
+    window_slots(*fs.req.out, 1, win_pos);
     t_pos = p;
     t_val = *reinterpret_cast<const int32_t*>(hit);
-    if (bucket[0] <= HIT_BUCKET_CAP) {  // ascending chunk order, as the Multimap keeps it
-        std::vector<int32_t> idx(bucket + 2, bucket + 2 + bucket[0]);
-        std::sort(idx.begin(), idx.end());
-        table->prime(bucket[1], idx.data(), (int32_t)idx.size());
-    }
+    prime_from_probe(*table, *fs.req.out, bucket);
     return p;
 }
 
@@ -433,7 +429,7 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
         chk(launch_probe_first(A, (uint32_t)tiles.size(), hpt, (uint32_t)ptiles.size(), st));
         chk(launch_hit_window(F, hiv, hreq, (int32_t)preq.size(), max_C, st));
         chk(hipMemcpyAsync(S->h_first.p, S->first.p, files.size() * sizeof(ProbeOut), hipMemcpyDeviceToHost, st));
-        chk(hipMemcpyAsync(S->h_bucket.p, S->bucket.p, files.size() * (2 + HIT_BUCKET_CAP) * sizeof(int32_t),
+        chk(hipMemcpyAsync(S->h_bucket.p, S->bucket.p, files.size() * HIT_BUCKET_INTS * sizeof(int32_t),
                            hipMemcpyDeviceToHost, st));
     }
     chk(hipStreamSynchronize(st));
@@ -490,7 +486,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         fs.off_as = tas, tas += fs.na * fs.dl;
         fs.off_nf = tnf, tnf += fs.nf;
         fs.off_ns = tns, tns += fs.ns;
-        fs.off_hit = thit, thit += pad16(16 + HIT_WINDOWS * fs.B);
+        fs.off_hit = thit, thit += pad16(16 + fs.B);  // one window per file (ScanFile::nwin = 1)
         fs.off_w0 = tw0, tw0 += pad16(std::min<int64_t>(fs.B, fs.n));
         maxC = std::max<int64_t>(maxC, fs.C);
     }
@@ -510,8 +506,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     RSH_BHIP(S->h_win0.ensure((size_t)tw0));
     RSH_BHIP(S->first.ensure((size_t)NF * sizeof(ProbeOut)));
     RSH_BHIP(S->h_first.ensure((size_t)NF * sizeof(ProbeOut)));
-    RSH_BHIP(S->bucket.ensure((size_t)NF * (2 + HIT_BUCKET_CAP) * 4));
-    RSH_BHIP(S->h_bucket.ensure((size_t)NF * (2 + HIT_BUCKET_CAP) * 4));
+    RSH_BHIP(S->bucket.ensure((size_t)NF * HIT_BUCKET_INTS * 4));
+    RSH_BHIP(S->h_bucket.ensure((size_t)NF * HIT_BUCKET_INTS * 4));
     RSH_BHIP(S->h_copies.ensure((size_t)2 * NF * sizeof(CopyEnt)));
     RSH_BHIP(S->h_ccopies.ensure((size_t)NF * sizeof(CopyEnt) + (size_t)3 * NF * sizeof(CopyEnt)));
     RSH_BHIP(S->h_tabents.ensure((size_t)NF * sizeof(TableEnt)));
@@ -647,7 +643,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         be.win0 = S->h_win0.as<uint8_t>() + fs.off_w0;
         be.w0 = std::min<int64_t>(fs.B, fs.n);
         be.hit = S->h_hit.as<uint8_t>() + fs.off_hit;
-        be.bucket = S->h_bucket.as<int32_t>() + (int64_t)f * (2 + HIT_BUCKET_CAP);
+        be.bucket = S->h_bucket.as<int32_t>() + (int64_t)f * HIT_BUCKET_INTS;
         be.n = fs.n;
         be.B = fs.B;
         memcpy(be.seed, seed, 4);
@@ -660,8 +656,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         F[f].out = S->first.as<ProbeOut>() + f;
         F[f].table_weak = fs.d_weak;
         F[f].C = fs.C;
-        F[f].bucket = S->bucket.as<int32_t>() + (int64_t)f * (2 + HIT_BUCKET_CAP);
+        F[f].bucket = S->bucket.as<int32_t>() + (int64_t)f * HIT_BUCKET_INTS;
         F[f].hit = S->h_hit.as<uint8_t>() + fs.off_hit;
+        F[f].nwin = 1;
         F[f].aligned_weak = S->haw.as<int32_t>() + fs.off_na;
     }
 

@@ -24,9 +24,11 @@ namespace {
 // HIP implementation of the resolver's services.
 // ------------------------------------------------------------------------------------------------
 constexpr size_t kFirstSlots = 1024;
-// Head mode launches the aligned speculation after this many resolver steps or milliseconds.
-constexpr int64_t kDeferSteps = 2;
-constexpr double kDeferMs = 0.25;
+constexpr int kScanWindows = 2;  // hit windows per probe in the single-file scan (hit_cache.h)
+// Head mode launches the aligned speculation after this many resolver steps or milliseconds ...
+constexpr int64_t kChainSteps = 2;  // ... after this many steps when the last event is a run of matches
+constexpr int64_t kDeferSteps = 4;
+constexpr double kDeferMs = 0.5;
 
 // RSH_SCAN_TRACE=1: one stderr line per resolver round trip (diagnostics).
 struct CallTrace {
@@ -107,9 +109,14 @@ class HipBackend : public rsh::ScanBackend {
             return;
         }
         int slot = -1;
-        for (int k = 0; k < rsh::HIT_WINDOWS; ++k)
+        for (int k = 0; k < kScanWindows; ++k)
             if (p == win_pos_[k]) slot = k;
-        if (slot >= 0) {  // the window came back with the probe result
+        if (slot > 0) {  // digested on a host thread since the probe returned
+            if (win_md5_[slot].joinable()) win_md5_[slot].join();
+            memcpy(out, win_digest_[slot], 16);
+            return;
+        }
+        if (slot == 0) {  // the window came back with the probe result
             rsh::HostMd5 h;
             h.update(c_->h_hit.as<uint8_t>() + 16 + (int64_t)slot * B_, (size_t)w);
             h.update(seed_, 4);
@@ -163,11 +170,12 @@ class HipBackend : public rsh::ScanBackend {
         rsh::ProbeTile* ht = pin<rsh::ProbeTile>(c_->h_tiles, (int64_t)tiles_.size() + 1);
         rsh::PartialTile* hpt = pin<rsh::PartialTile>(c_->h_ptiles, (int64_t)ptiles_.size() + 1);
         rsh::ProbeOut* hf = pin<rsh::ProbeOut>(c_->h_first, 1);
-        uint8_t* hh = pin<uint8_t>(c_->h_hit, 16 + rsh::HIT_WINDOWS * B_);
-        int32_t* hb = pin<int32_t>(c_->h_bucket, 2 + rsh::HIT_BUCKET_CAP + 1);  // + the request list {0}
+        join_window_digests();  // h_hit is about to be overwritten
+        uint8_t* hh = pin<uint8_t>(c_->h_hit, 16 + kScanWindows * B_);
+        int32_t* hb = pin<int32_t>(c_->h_bucket, rsh::HIT_BUCKET_INTS + 1);  // + the request list {0}
         rsh::ScanFile* F = file();
         ok(c_->partials.ensure((ptiles_.size() + 1) * sizeof(int4)));
-        ok(c_->bucket.ensure((2 + rsh::HIT_BUCKET_CAP) * sizeof(int32_t)));
+        ok(c_->bucket.ensure(rsh::HIT_BUCKET_INTS * sizeof(int32_t)));
         // result records preset ("none") in batches: one reset launch per kFirstSlots probes
         ok(c_->first.ensure(kFirstSlots * sizeof(rsh::ProbeOut)));
         if (err != hipSuccess) return -1;
@@ -186,6 +194,7 @@ class HipBackend : public rsh::ScanBackend {
         F->niv = (int32_t)count;
         F->bucket = c_->bucket.as<int32_t>();
         F->hit = hh;
+        F->nwin = kScanWindows;
         if (head) {  // anchors T(kB) for the blocks these tiles sit in
             anchors_.clear();
             for (const rsh::ProbeTile& t : tiles_) {
@@ -210,23 +219,31 @@ class HipBackend : public rsh::ScanBackend {
         ok(rsh::launch_probe_first(A, (uint32_t)tiles_.size(), hpt, (uint32_t)ptiles_.size(), c_->stream));
         // the resolver's next questions at a hit are T(p), the bucket of the key that hit and (usually) the
         // MD5 of the window at p: answer them in this round trip
-        int32_t* req = hb + 2 + rsh::HIT_BUCKET_CAP;
+        int32_t* req = hb + rsh::HIT_BUCKET_INTS;
         *req = 0;
         ok(rsh::launch_hit_window(F, hiv, req, 1, t_.chunk_count, c_->stream));
         ok(hipMemcpyAsync(hf, d_first, sizeof(rsh::ProbeOut), hipMemcpyDeviceToHost, c_->stream));
-        ok(hipMemcpyAsync(hb, c_->bucket.p, (2 + rsh::HIT_BUCKET_CAP) * sizeof(int32_t), hipMemcpyDeviceToHost,
+        ok(hipMemcpyAsync(hb, c_->bucket.p, rsh::HIT_BUCKET_INTS * sizeof(int32_t), hipMemcpyDeviceToHost,
                           c_->stream));
         ok(hipStreamSynchronize(c_->stream));
         if (count == 1) cache_.fill(iv[0], keys, *hf, n_ - B_);
         else cache_.valid = false;
         if (hf->first == ~0ull) return -1;
-        rsh::window_slots(*hf, win_pos_);
+        rsh::window_slots(*hf, kScanWindows, win_pos_);
+        for (int k = 1; k < kScanWindows; ++k)
+            if (win_pos_[k] >= 0) {
+                const int64_t wk = std::min<int64_t>(B_, n_ - win_pos_[k]);
+                const uint8_t* src = hh + 16 + (int64_t)k * B_;
+                win_md5_[k] = std::thread([this, k, wk, src] {
+                    rsh::HostMd5 h;
+                    h.update(src, (size_t)wk);
+                    h.update(seed_, 4);
+                    h.final(win_digest_[k]);
+                });
+            }
         t_pos_ = (int64_t)hf->first;
         t_val_ = *reinterpret_cast<const int32_t*>(hh);
-        if (hb[0] <= rsh::HIT_BUCKET_CAP) {  // ascending chunk order, as the Multimap keeps it
-            std::sort(hb + 2, hb + 2 + hb[0]);
-            t_.prime(hb[1], hb + 2, hb[0]);
-        }
+        prime_from_probe(t_, *hf, hb);
         return t_pos_;
     }
 
@@ -265,7 +282,20 @@ class HipBackend : public rsh::ScanBackend {
         F->C = t_.chunk_count;
         return F;
     }
-    int64_t win_pos_[rsh::HIT_WINDOWS] = {-1};  // windows of the last probe's hits on the host (h_hit)
+    int64_t win_pos_[rsh::HIT_WINDOWS] = {-1, -1, -1, -1};  // windows of the last probe's hits on the host (h_hit)
+    // digests of the windows in slots 1 .. kScanWindows-1, started on host threads when the probe returns
+    // (the resolver handles the first hit meanwhile); joined before the next probe overwrites h_hit
+    std::thread win_md5_[rsh::HIT_WINDOWS];
+    uint8_t win_digest_[rsh::HIT_WINDOWS][16];
+    void join_window_digests() {
+        for (std::thread& t : win_md5_)
+            if (t.joinable()) t.join();
+    }
+
+  public:
+    ~HipBackend() { join_window_digests(); }
+
+  private:
     int64_t t_pos_ = -1;    // position of the last hit returned: its weak sum t_val_ is known
     int32_t t_val_ = 0;
     HitCache cache_;
@@ -411,7 +441,15 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         if (be.err != hipSuccess || !be.head) return true;
         CallTrace tr("ev_query", res->stats.head_steps);
         if (!spec_launched) {
-            if (res->stats.head_steps >= kDeferSteps || ms_since(t_head) >= kDeferMs) {
+            static const int64_t defer_steps = getenv("RSH_SCAN_DEFER_STEPS") ? atoll(getenv("RSH_SCAN_DEFER_STEPS"))
+                                                                            : kDeferSteps;  // A/B
+            static const double defer_ms = getenv("RSH_SCAN_DEFER_MS") ? atof(getenv("RSH_SCAN_DEFER_MS")) : kDeferMs;
+            // chain evidence: the scan just matched consecutive chunks, so long aligned runs are likely and
+            // the speculation pays; otherwise (e.g. a false weak hit that poisons the digest, after which
+            // the scan ends in closed form) it waits a little longer
+            const bool chain = !res->ev.empty() && res->ev.back().kind == RSH_EV_MATCH && res->ev.back().count >= 2;
+            if ((chain && res->stats.head_steps >= kChainSteps) || res->stats.head_steps >= defer_steps ||
+                ms_since(t_head) >= defer_ms) {
                 spec_rc = launch_spec();
                 spec_launched = true;
                 if (spec_rc != RSH_OK) return true;

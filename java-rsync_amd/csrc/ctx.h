@@ -194,4 +194,18 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                 rsh::ResolveResult* res);
 int emit_events(rsh_ctx* c, rsh::ResolveResult& r, rsh_event* ev, int64_t cap, int64_t* n_ev);
 
+// Primes the resolver's table with the buckets the device computed with a probe (device.h HIT_BUCKET_INTS
+// layout, copied to the host): the first hit's, and each listed hit's when it fits LISTED_IDX entries.
+inline void prime_from_probe(rsh::ChunkTable& t, const rsh::ProbeOut& o, const int32_t* b) {
+    t.prime_clear();
+    if (o.first == ~0ull) return;
+    if (b[0] <= rsh::HIT_BUCKET_CAP) t.prime(b[1], b + 2, b[0]);
+    if (o.count > (unsigned long long)rsh::PROBE_HITS_CAP) return;
+    const int32_t* lb = b + 2 + rsh::HIT_BUCKET_CAP;
+    for (unsigned long long j = 0; j < o.count; ++j) {
+        const int32_t* e = lb + (1 + rsh::LISTED_IDX) * j;
+        if (e[0] <= rsh::LISTED_IDX) t.prime((int32_t)o.key[j], e + 1, e[0]);
+    }
+}
+
 }  // namespace rshi

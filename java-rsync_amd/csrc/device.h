@@ -78,6 +78,7 @@ hipError_t launch_table_insert(unsigned long long* d_slots, uint32_t mask, const
 // every interval names its file, and a file's per-scan state is a ScanFile in device-readable memory.
 constexpr int PROBE_TILE = 4096;
 constexpr int HIT_BUCKET_CAP = 256;
+constexpr int HIT_BUCKET_INTS = 2 + HIT_BUCKET_CAP + PROBE_HITS_CAP * (1 + LISTED_IDX);
 struct ScanFile {
     const uint8_t* data;
     int64_t n;
@@ -89,8 +90,9 @@ struct ScanFile {
     const int32_t* table_weak;        // the received table's weak sums (device), C entries
     int32_t C;
     int32_t iv0, niv;                 // the file's intervals in the round's ProbeIv array
-    int32_t pad;
-    int32_t* bucket;                  // device: {count, key, idx[0 .. HIT_BUCKET_CAP)}
+    int32_t nwin;                     // hit windows wanted (1 .. HIT_WINDOWS)
+    int32_t* bucket;                  // device, HIT_BUCKET_INTS: {count, key, idx[0 .. HIT_BUCKET_CAP)} of the
+                                      // first hit, then per listed hit j {count, idx[LISTED_IDX]}
     uint8_t* hit;                     // pinned host: T(p) in bytes 0..3, window k of the k-th smallest listed
                                       // hit at 16 + k B (k < HIT_WINDOWS; k = 0: the first hit)
 };

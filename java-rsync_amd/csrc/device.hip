@@ -1470,12 +1470,14 @@ __global__ __launch_bounds__(256) void hit_window_kernel(const ScanFile* __restr
             F.bucket[0] = 0;
             F.bucket[1] = (int32_t)((((uint32_t)T + I.e_lo) & 0xFFFFu) | ((((uint32_t)T >> 16) + ehi) << 16));
         }
+        if (threadIdx.x < PROBE_HITS_CAP) F.bucket[2 + HIT_BUCKET_CAP + (1 + LISTED_IDX) * threadIdx.x] = 0;
         return;
     }
     // blocks 1 + 16 k .. 16 k + 16 copy window k: the k-th smallest listed hit (k = 0 is the first hit; the
     // others only when the list is complete), so the resolver has the digest input of the next few
     // events the hit list answers without another round trip
     const int slot = (int)(blockIdx.x - 1) / 16, part = (int)(blockIdx.x - 1) % 16;
+    if (slot >= F.nwin) return;
     int64_t pw = p;
     if (slot > 0) {
         const unsigned long long cnt = F.out->count;
@@ -1515,16 +1517,30 @@ __global__ __launch_bounds__(256) void hit_bucket_kernel(const ScanFile* __restr
     if (F.out->first == ~0ull) return;
     const int32_t C = F.C;
     const int32_t i0 = 8 * (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (i0 >= C) return;
     const int32_t key = F.bucket[1];
     const int32_t* __restrict__ weak = F.table_weak;
+    // the listed hits' keys too (complete lists only): their buckets spare the host a lookup per event
+    // the hit list answers
+    __shared__ int32_t lkey[PROBE_HITS_CAP];
+    const unsigned long long cnt = F.out->count;
+    const int nl = cnt <= (unsigned long long)PROBE_HITS_CAP ? (int)cnt : 0;
+    if (threadIdx.x < nl) lkey[threadIdx.x] = (int32_t)F.out->key[threadIdx.x];
+    __syncthreads();
+    int32_t* __restrict__ lb = F.bucket + 2 + HIT_BUCKET_CAP;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const int32_t i = i0 + k;
-        if (i < C && weak[i] == key) {
+        if (i >= C) break;
+        const int32_t wk = weak[i];
+        if (wk == key) {
             const int32_t at = atomicAdd(&F.bucket[0], 1);
             if (at < HIT_BUCKET_CAP) F.bucket[2 + at] = i;
         }
+        for (int j = 0; j < nl; ++j)
+            if (wk == lkey[j]) {
+                const int32_t at = atomicAdd(&lb[(1 + LISTED_IDX) * j], 1);
+                if (at < LISTED_IDX) lb[(1 + LISTED_IDX) * j + 1 + at] = i;
+            }
     }
 }
 

@@ -22,19 +22,24 @@ struct ProbeOut {
 };
 
 // Windows the hit kernel returns with a probe: slot k holds the window at the k-th smallest listed hit
-// (slot 0: the first hit, always; slots >= 1 only when the list is complete).  More than one slot trades
-// D2H bytes and host digests for round trips; on config 4 (128 x 128 MiB) 4 slots cut the rounds from 26
-// to 18 but gave no faster step on 50%-modified bases and a slower one on identical bases (host digests
-// of windows the speculation would have supplied), so one slot it is.
-constexpr int HIT_WINDOWS = 1;
-inline void window_slots(const ProbeOut& o, int64_t (&slot)[HIT_WINDOWS]) {
+// (slot 0: the first hit, always; slots >= 1 only when the list is complete), for k < the file's nwin
+// (ScanFile::nwin <= HIT_WINDOWS).  More slots trade D2H bytes and host digests for round trips: the
+// single-file scan asks for 2 (the second digest is computed on a host thread while the resolver handles
+// the first hit); the batched scan asks for 1 -- on config 4 (128 x 128 MiB) 4 slots cut the rounds from
+// 26 to 18 but gave no faster step on 50%-modified bases and a slower one on identical bases (host
+// digests of windows the speculation would have supplied).
+constexpr int HIT_WINDOWS = 4;
+// Buckets of the listed hits' keys computed with the probe (HitBuckets region of ScanFile::bucket): up
+// to LISTED_IDX chunk indices per listed key, in no particular order.
+constexpr int LISTED_IDX = 3;
+inline void window_slots(const ProbeOut& o, int nwin, int64_t (&slot)[HIT_WINDOWS]) {
     for (int k = 0; k < HIT_WINDOWS; ++k) slot[k] = -1;
     if (o.first == ~0ull) return;
     slot[0] = (int64_t)o.first;
     if (o.count > (unsigned long long)PROBE_HITS_CAP) return;
     std::vector<int64_t> p(o.pos, o.pos + o.count);
     std::sort(p.begin(), p.end());
-    for (int k = 1; k < HIT_WINDOWS && k < (int)p.size(); ++k) slot[k] = p[(size_t)k];
+    for (int k = 1; k < nwin && k < HIT_WINDOWS && k < (int)p.size(); ++k) slot[k] = p[(size_t)k];
 }
 
 // The hits of the last single-interval range probe.  A later probe of [a', b') with the same key function

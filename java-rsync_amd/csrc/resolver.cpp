@@ -59,10 +59,11 @@ void ChunkTable::build() {
 }
 
 const int32_t* ChunkTable::bucket(int32_t key, int32_t* size) {
-    if (primed_valid_ && key == primed_key_) {
-        *size = (int32_t)primed_.size();
-        return primed_.data();
-    }
+    for (int k = 0; k < primed_n_; ++k)
+        if (primed_[(size_t)k].key == key) {
+            *size = (int32_t)primed_[(size_t)k].idx.size();
+            return primed_[(size_t)k].idx.data();
+        }
     HostTrace tr("bucket", key, &host_times().bucket_ms);
     if (!indexed_ && scan_lookups_ >= kScanLookups) build();
     scratch_.clear();

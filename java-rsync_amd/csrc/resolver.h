@@ -15,6 +15,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <algorithm>
 #include <functional>
 #include <vector>
 
@@ -54,16 +55,24 @@ struct ChunkTable {
     static constexpr int kScanLookups = 2;
     // The bucket of `key` computed elsewhere (the device, in the round trip that found a probe hit):
     // idx ascending.  The next bucket(key) returns it without touching the table.
+    // The device computes buckets with each probe (the first hit's, and those of the listed hits): they
+    // stand in for lookups until the next probe (prime_clear).
+    void prime_clear() { primed_n_ = 0; }
     void prime(int32_t key, const int32_t* idx, int32_t count) {
-        primed_key_ = key;
-        primed_.assign(idx, idx + count);
-        primed_valid_ = true;
+        if (primed_n_ == (int)primed_.size()) primed_.emplace_back();
+        Primed& e = primed_[(size_t)primed_n_++];
+        e.key = key;
+        e.idx.assign(idx, idx + count);
+        std::sort(e.idx.begin(), e.idx.end());
     }
 
   private:
-    bool primed_valid_ = false;
-    int32_t primed_key_ = 0;
-    std::vector<int32_t> primed_;
+    struct Primed {
+        int32_t key;
+        std::vector<int32_t> idx;
+    };
+    std::vector<Primed> primed_;
+    int primed_n_ = 0;
     bool indexed_ = false;
     int scan_lookups_ = 0;
     // chained hash index: head_[hash(key)] = smallest chunk index with that hash, next_[i] = the next
