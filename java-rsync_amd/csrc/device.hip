@@ -1023,6 +1023,12 @@ void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Gr
     }
 }
 
+// RSH_K1_BATCH_PIN=1 (A/B): the batched Generator K1 with the 2-waves-per-SIMD occupancy pin
+static bool batch_pin() {
+    static const bool v = getenv("RSH_K1_BATCH_PIN") && atoi(getenv("RSH_K1_BATCH_PIN")) != 0;
+    return v;
+}
+
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
                                    int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag,
                                    int abort_gen) {
@@ -1031,6 +1037,9 @@ hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, co
         if (abort_flag)
             hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, false, 0, true>), dim3(ngroups), dim3(64), lb, s,
                                nullptr, 0u, 0u, seed_word, nullptr, nullptr, abort_flag, abort_gen, d_groups);
+        else if (batch_pin())
+            hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 0, true>), dim3(ngroups), dim3(64), lb, s,
+                               nullptr, 0u, 0u, seed_word, nullptr, nullptr, nullptr, 0, d_groups);
         else
             hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, false, 0, true>), dim3(ngroups), dim3(64), lb, s,
                                nullptr, 0u, 0u, seed_word, nullptr, nullptr, nullptr, 0, d_groups);
