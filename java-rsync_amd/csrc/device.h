@@ -77,6 +77,9 @@ hipError_t launch_table_insert(unsigned long long* d_slots, uint32_t mask, const
 // One launch serves a batch of files (a round of the batched Sender, or a single scan as a batch of one):
 // every interval names its file, and a file's per-scan state is a ScanFile in device-readable memory.
 constexpr int PROBE_TILE = 4096;
+// Tiles at most this far into their block take their block prefix by re-reading the tiles before them
+// (<= 2 x PROBE_INLINE_TILES x 4 KiB) instead of from pass 1; blocks of B <= 8 KiB then need no pass 1.
+constexpr int PROBE_INLINE_TILES = 1;
 constexpr int HIT_BUCKET_CAP = 256;
 constexpr int HIT_BUCKET_INTS = 2 + HIT_BUCKET_CAP + PROBE_HITS_CAP * (1 + LISTED_IDX);
 struct ScanFile {
@@ -105,7 +108,7 @@ struct ProbeIv {
 struct ProbeTile {
     int64_t q0;     // tile start (multiple of PROBE_TILE from its block start)
     int32_t iv;     // interval index
-    int32_t pbase;  // index of its block's tile-0 partial sums in ProbeArgs::partials (unused for tile 0)
+    int32_t pbase;  // index of its block's tile-0 partial sums in ProbeArgs::partials; -1: computed in-kernel
 };
 // Pass 1 of a probe: the four byte sums (x[j], (j - o) x[j] over the tile, and the same over the tile
 // shifted by B) of every tile of a block that lies before a probed tile of that block, so that pass 2

@@ -717,6 +717,14 @@ void allow_full_lds(K kernel) {
 
 // variant: -1 = production choice; 0..2 per-lane (NT PF4, plain PF4, NT PF8); 3..6 coalesced
 // (D=2 NT, D=3 NT, D=2 plain, D=4 NT).  Non-coalesced variants handle every chunk shape.
+// RSH_K1_PIN_ALL=0 (A/B): K1 launches of more than 2048 waves (single and batched) without the occupancy
+// pin -- the coalesced kernel for single files, the unpinned pipelined instantiation for batches
+static bool pin_all() {
+    static const bool v = !(getenv("RSH_K1_PIN_ALL") && atoi(getenv("RSH_K1_PIN_ALL")) == 0);
+    return v;
+}
+static bool batch_pin() { return pin_all(); }
+
 hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks,
                                      uint32_t dl, uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong,
                                      hipStream_t s, const int* abort_flag, int abort_gen) {
@@ -791,10 +799,13 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     }
                     break;
                 case 19:
-                    if (nst <= 1024 && nst >= 4 && abort_flag && waves <= 2 * 4 * kCUs) {
+                    // the pipelined K1 at any wave count (occupancy pinned to 2 waves/SIMD; beyond 2048 waves they
+                    // run in rounds): measured 3.19 vs 3.96 ms for 16 GiB at B = 64 KiB (4096 waves) against the
+                    // unpinned instantiation, and ahead of the coalesced kernel at every size
+                    if (nst <= 1024 && nst >= 4 && abort_flag && (waves <= 2 * 4 * kCUs || pin_all())) {
                         hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true>), dim3(waves), dim3(64), 2 * wave_lds,
                                            s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen);
-                    } else if (nst <= 1024 && nst >= 4 && waves <= 2 * 4 * kCUs) {
+                    } else if (nst <= 1024 && nst >= 4 && (waves <= 2 * 4 * kCUs || pin_all())) {
                         hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true>), dim3(waves), dim3(64), 2 * wave_lds,
                                            s, d_data, B, dl, seed_word, d_weak, d_strong);
                     } else if (nst <= 1024 && abort_flag && waves <= 2 * 4 * kCUs) {
@@ -1023,18 +1034,16 @@ void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Gr
     }
 }
 
-// RSH_K1_BATCH_PIN=1 (A/B): the batched Generator K1 with the 2-waves-per-SIMD occupancy pin
-static bool batch_pin() {
-    static const bool v = getenv("RSH_K1_BATCH_PIN") && atoi(getenv("RSH_K1_BATCH_PIN")) != 0;
-    return v;
-}
 
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
                                    int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag,
                                    int abort_gen) {
     const size_t lb = 2 * 64 * 9 * sizeof(uint4);
     if (ngroups > 0) {
-        if (abort_flag)
+        if (abort_flag && batch_pin())
+            hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true, 0, true>), dim3(ngroups), dim3(64), lb, s,
+                               nullptr, 0u, 0u, seed_word, nullptr, nullptr, abort_flag, abort_gen, d_groups);
+        else if (abort_flag)
             hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, false, 0, true>), dim3(ngroups), dim3(64), lb, s,
                                nullptr, 0u, 0u, seed_word, nullptr, nullptr, abort_flag, abort_gen, d_groups);
         else if (batch_pin())
@@ -1316,7 +1325,10 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A)
     int32_t head[4] = {0, 0, 0, 0};
     const int ti = (int)((q0 - o) / PROBE_TILE);
     if (ti > 0) {
-        if (threadIdx.x < ti) {
+        if (tile.pbase < 0) {  // near the block start: re-read the <= PROBE_INLINE_TILES tiles before it
+            range_sums(data, n, o, q0, o, head[0], head[1]);
+            range_sums(data, n, o + B, q0 + B, o, head[2], head[3]);
+        } else if (threadIdx.x < ti) {
             const int4 v = A.partials[tile.pbase + threadIdx.x];
             head[0] = v.x;
             head[1] = v.y;
@@ -1437,6 +1449,10 @@ void probe_partials(std::vector<ProbeTile>* tiles, size_t t0, int64_t B, int32_t
             cur_block = k;
             covered = 0;
             base = (int32_t)out->size();
+        }
+        if (ti <= PROBE_INLINE_TILES) {  // the kernel re-reads the few tiles before it (no pass 1)
+            t.pbase = -1;
+            continue;
         }
         for (; covered < ti; ++covered) out->push_back(PartialTile{k * B + covered * PROBE_TILE, file, 0});
         t.pbase = base;

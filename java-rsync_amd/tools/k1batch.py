@@ -1,3 +1,5 @@
+"""k1batch.py -- K1 launch times (HIP events, 5 launches averaged) for the batched and single-file entry points
+over 16 GiB at several (B, files) shapes.  Developer tool; prints one JSON line."""
 import ctypes, sys, os, time, json
 sys.path.insert(0, os.path.join(os.environ.get("GRAFT_REPO_ROOT", "/root/repo"), "java-rsync_amd"))
 import numpy as np, torch
@@ -26,6 +28,18 @@ for B, F in [(8192, 128), (131072, 1), (65536, 4)]:
     e1.record(stream); ctx.sync()
     ms = e0.elapsed_time(e1) / 5
     out[f"B{B}xF{F}"] = round(ms, 3)
+    hs = R.header_make(B, 3, n)
+    ws = torch.empty(hs.chunk_count, dtype=torch.int32, device="cuda")
+    ss = torch.empty(hs.chunk_count * 3, dtype=torch.uint8, device="cuda")
+    def single():
+        assert L.rsh_block_sums_device(ctx.handle, ctypes.c_void_p(basis.data_ptr()), n, ctypes.byref(hs),
+                                       seed.ctypes.data, ctypes.c_void_p(ws.data_ptr()), ctypes.c_void_p(ss.data_ptr())) == 0
+    single(); ctx.sync()
+    e0.record(stream)
+    for _ in range(5): single()
+    e1.record(stream); ctx.sync()
+    out[f"single_B{B}"] = round(e0.elapsed_time(e1) / 5, 3)
+    del ws, ss
     del basis, w, st
     torch.cuda.empty_cache()
 print(json.dumps(out))

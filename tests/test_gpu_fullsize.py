@@ -1,4 +1,5 @@
-"""Parity at BASELINE.json's full sizes (config 2: 4 GiB, B = 65536; config 5: 16 GiB, B = 131072).
+"""Parity at BASELINE.json's full sizes (config 2: 4 GiB, B = 65536; config 5: 16 GiB, B = 131072; config 4:
+128 x 128 MiB per GPU, B = 8192, through the batched entry points).
 
 The oracle cannot replay a 4-16 GiB Sender scan within a test's time limit (it walks every byte, ~0.05 GiB/s),
 so the full-size checks are the size-independent properties of the path:
@@ -180,5 +181,58 @@ def test_config5_16GiB(env, variant):
     if variant == "identical":
         assert len(ev) == 1 and ev[0]["count"] == h.chunk_count and lit == 0
     _check_delta(torch, ev, src, basis, h, lit, mat)
+    del src, basis
+    torch.cuda.empty_cache()
+
+
+def test_config4_segment_batch_equals_single(env):
+    """Config 4 per GPU: 128 files x 128 MiB (B = 8192 by the rule, dl = 3), every other block of each basis
+    replaced.  The batched entry points must give every file exactly what the single-file calls give
+    (which the parity suites tie to the oracle), and the Generator tables of a few files are checked
+    against the oracle directly."""
+    ctx, torch = env
+    F, S = 128, 128 << 20
+    B = R.block_length_for(S)
+    dl = R.digest_length_for(S, B)
+    assert (B, dl) == (8192, 3)
+    n = F * S
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _fill(ctx, src, KEY ^ 4)
+    basis = src.clone()
+    other = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _fill(ctx, other, KEY ^ 0x4ED1)
+    ctx.sync()
+    basis.view(-1, B)[1::2] = other.view(-1, B)[1::2]
+    del other
+    torch.cuda.synchronize()
+    h = R.header_make(B, dl, S)
+    C = h.chunk_count
+    w = torch.empty(F * C, dtype=torch.int32, device="cuda")
+    s = torch.empty(F * C * dl, dtype=torch.uint8, device="cuda")
+    bj = (R.BlockJob * F)()
+    for i in range(F):
+        bj[i].d_data, bj[i].n, bj[i].h = basis.data_ptr() + i * S, S, h
+        bj[i].d_weak, bj[i].d_strong = w.data_ptr() + 4 * i * C, s.data_ptr() + i * C * dl
+    assert R.lib().rsh_block_sums_batch_device(ctx.handle, bj, F, SEED_NP.ctypes.data) == 0
+    ctx.sync()
+    hw, hs = w.cpu().numpy(), s.cpu().numpy()
+    for i in (0, 77, F - 1):
+        ow, os_ = O.generator(basis[i * S:(i + 1) * S].cpu().numpy(), O.header(B, dl, S), SEED)
+        assert np.array_equal(hw[i * C:(i + 1) * C], ow) and np.array_equal(hs[i * C * dl:(i + 1) * C * dl], os_)
+    cap = C + S // B + 4096
+    evs = [np.zeros(cap, R.EVENT_DTYPE) for _ in range(F)]
+    sj = (R.ScanJob * F)()
+    for i in range(F):
+        sj[i].d_src, sj[i].n, sj[i].h = src.data_ptr() + i * S, S, h
+        sj[i].d_weak, sj[i].d_strong = bj[i].d_weak, bj[i].d_strong
+        sj[i].ev, sj[i].ev_cap = evs[i].ctypes.data, cap
+    assert R.lib().rsh_match_scan_batch_device(ctx.handle, sj, F, SEED_NP.ctypes.data, None) == 0
+    for i in range(F):
+        sub = src[i * S:(i + 1) * S]
+        ev, lit, mat, _ = _scan(ctx, torch, sub, h, w[i * C:(i + 1) * C], s[i * C * dl:(i + 1) * C * dl])
+        assert sj[i].status == 0 and (sj[i].literal, sj[i].matched) == (lit, mat)
+        assert R.events_as_tuples(evs[i][:sj[i].n_ev], B) == R.events_as_tuples(ev, B), f"file {i}"
+        if i % 32 == 0:
+            _check_delta(torch, ev, sub, basis[i * S:(i + 1) * S], h, lit, mat)
     del src, basis
     torch.cuda.empty_cache()
