@@ -448,8 +448,15 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 // resolver's range probe (104) to run beside the Sender's speculation launch in head mode.
 // MULTI (batched files, K1Group per wave): the wave's 64 chunks, B, dl and output slots come from
 // groups[blockIdx.x] instead of (data, B, dl, weak_out, strong_out) + blockIdx.x * 64 chunks.
+// K1_PIPE_ATTR (A/B at build time, -DRSH_K1_NUMVGPR=N): the register budget.  waves_per_eu(3) caps the
+// kernel at 168 VGPRs, which spills 12 of them to scratch (20 B/lane); num_vgpr(N) with N >= 184 does not.
+#ifdef RSH_K1_NUMVGPR
+#define K1_PIPE_ATTR __attribute__((amdgpu_num_vgpr(RSH_K1_NUMVGPR)))
+#else
+#define K1_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
+#endif
 template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void block_sums_pipe_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
+__global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
                                                              uint8_t* __restrict__ strong_out,
                                                              const int* abort_flag = nullptr, int abort_gen = 0,

@@ -19,7 +19,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "librsynchip.so")
+LIB_PATH = os.environ.get("RSH_LIB") or os.path.join(HERE, "lib", "librsynchip.so")  # RSH_LIB: A/B builds
 
 RSH_OK, RSH_E_INVAL, RSH_E_PROTOCOL, RSH_E_OVERFLOW, RSH_E_NOSPACE, RSH_E_DEVICE, RSH_E_NOMEM, RSH_E_BUSY = \
     0, -1, -2, -3, -4, -5, -6, -7
