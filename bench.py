@@ -46,8 +46,9 @@ def parse():
     ap.add_argument("--block", type=int, default=131072)
     ap.add_argument("--digest", type=int, default=4)
     ap.add_argument("--variant", choices=["half", "identical"], default="half")
-    ap.add_argument("--workload", choices=["file", "files"], default="file",
-                    help="file: config 5 (one 16 GiB pair per GPU); files: config 4 (many 128 MiB pairs per GPU)")
+    ap.add_argument("--workload", choices=["file", "files", "receiver"], default="file",
+                    help="file: config 5 (one 16 GiB pair per GPU); files: config 4 (many 128 MiB pairs per GPU); "
+                         "receiver: Receiver.combineDataToFile on the config-2 shape (4 GiB, B by the rule)")
     ap.add_argument("--files", type=int, default=128, help="files per GPU for --workload files")
     ap.add_argument("--file-mib", type=int, default=128)
     ap.add_argument("--threads", type=int, default=8, help="Sender scan contexts per GPU (--files-api single)")
@@ -64,6 +65,8 @@ def main():
     a = parse()
     if a.workload == "files":
         return main_files(a)
+    if a.workload == "receiver":
+        return main_receiver(a)
     import torch
     import torch.distributed as dist
 
@@ -334,16 +337,25 @@ def main_files(a):
         sjobs[i].ev = evbufs[i].ctypes.data
         sjobs[i].ev_cap = caps
     bst = R.ScanStats()
+    # the Generator's batched K1 (one launch over the segment) timed with HIP events on the context stream
+    stream = torch.cuda.ExternalStream(L.rsh_ctx_stream(ctx.handle))
+    gen_ev = []
 
-    def step_batch():
+    def step_batch(timed=False):
+        if timed:
+            gen_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+            gen_ev[-1][0].record(stream)
         assert L.rsh_block_sums_batch_device(ctx.handle, bjobs, F, seed.ctypes.data) == 0
+        if timed:
+            gen_ev[-1][1].record(stream)
         rc = L.rsh_match_scan_batch_device(ctx.handle, sjobs, F, seed.ctypes.data, ctypes.byref(bst))
         assert rc == 0, (rc, L.rsh_last_error().decode())
         for i in range(F):
             assert sjobs[i].literal + sjobs[i].matched == S
         return sum(sjobs[i].matched for i in range(F))
 
-    step = step_batch if a.files_api == "batch" else step_single
+    batch = a.files_api == "batch"
+    step = step_batch if batch else step_single
 
     for _ in range(a.warmup):
         step()
@@ -354,7 +366,8 @@ def main_files(a):
     t0 = time.perf_counter()
     matched = 0
     for _ in range(a.steps):
-        matched = step()
+        matched = step_batch(timed=True) if batch else step()
+    ctx.sync()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -373,6 +386,15 @@ def main_files(a):
         "scan": {"matched_bytes_per_step_per_gpu": int(matched),
                  "stats": bst.as_dict() if a.files_api == "batch" else None},
     }
+    if batch and gen_ev:
+        k_ms = sum(e0.elapsed_time(e1) for e0, e1 in gen_ev) / len(gen_ev)
+        ach = n / (k_ms * 1e-3) / 1e9
+        res["roofline"] = {"kernel": "block_sums_pipe_kernel (batched K1: the Generator over the segment)",
+                           "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(k_ms, 4),
+                           "algorithmic_bytes": n}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline_files(src, basis, S, F, B, dl, a.cpu_sample_mib << 20)
     if rank == 0:
         print(json.dumps(res), flush=True)
     ex.shutdown()
@@ -381,6 +403,93 @@ def main_files(a):
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def main_receiver(a):
+    """Receiver.combineDataToFile (Receiver.java:459-555) through rsh_receiver_combine_device: the token
+    stream the Sender produced for the pair (host memory, as it comes off the wire), the replica (the basis)
+    and the target in HBM.  One step = one call: the host token walk, the literal upload, the device block
+    gather and the Receiver's digest of the rebuilt file (one serial MD5 chain on the host, which bounds
+    the call).  Default shape: config 2 (4 GiB, B = 65536 by the rule, dl = 4).  1 GPU only."""
+    import torch
+    rank, world, local = shard.env_rank()
+    assert world == 1, "--workload receiver runs on one GPU"
+    torch.cuda.set_device(local)
+    if not os.path.exists(R.LIB_PATH):
+        R.build()
+    L = R.lib()
+    ctx = R.Context(local)
+    n = int((a.size_gib if a.size_gib != 16.0 else 4.0) * (1 << 30))
+    B = R.block_length_for(n)
+    dl = R.digest_length_for(n, B)
+    h = R.header_make(B, dl, n)
+    C = h.chunk_count
+    seed = np.frombuffer(bytes([1, 2, 3, 4]), np.uint8).copy()
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    basis = torch.empty(n, dtype=torch.uint8, device="cuda")
+    assert L.rsh_fill_splitmix_device(ctx.handle, src.data_ptr(), n, KEY_SRC, 0) == 0
+    assert L.rsh_fill_splitmix_device(ctx.handle, basis.data_ptr(), n, KEY_SRC, 0) == 0
+    if a.variant == "half":
+        other = torch.empty(n, dtype=torch.uint8, device="cuda")
+        assert L.rsh_fill_splitmix_device(ctx.handle, other.data_ptr(), n, KEY_EDIT, 0) == 0
+        ctx.sync()
+        full = (n // B) * B
+        basis[:full].view(-1, B)[1::2] = other[:full].view(-1, B)[1::2]
+        del other
+    ctx.sync()
+    torch.cuda.synchronize()
+    # the Sender's side, once: Generator + scan -> events -> the exact token stream (rsh_tokens_write)
+    d_weak = torch.empty(max(C, 1), dtype=torch.int32, device="cuda")
+    d_strong = torch.empty(max(C * dl, 1), dtype=torch.uint8, device="cuda")
+    assert L.rsh_block_sums_device(ctx.handle, ctypes.c_void_p(basis.data_ptr()), n, ctypes.byref(h),
+                                   seed.ctypes.data, ctypes.c_void_p(d_weak.data_ptr()),
+                                   ctypes.c_void_p(d_strong.data_ptr())) == 0
+    cap = C + (n // B) + 4096
+    ev = np.zeros(cap, R.EVENT_DTYPE)
+    n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    assert L.rsh_match_scan_device(ctx.handle, ctypes.c_void_p(src.data_ptr()), n, ctypes.byref(h),
+                                   ctypes.c_void_p(d_weak.data_ptr()), ctypes.c_void_p(d_strong.data_ptr()),
+                                   seed.ctypes.data, ev.ctypes.data, cap, ctypes.byref(n_ev), ctypes.byref(lit),
+                                   ctypes.byref(mat), None) == 0
+    src_host = src.cpu().numpy()
+    toks = np.frombuffer(R.tokens(src_host, ev[:n_ev.value], bytes(16)), np.uint8)
+    del src_host, d_weak, d_strong
+    target = torch.empty(n, dtype=torch.uint8, device="cuda")
+    out = R.CombineResult()
+    stream = torch.cuda.ExternalStream(L.rsh_ctx_stream(ctx.handle))
+
+    def step():
+        rc = L.rsh_receiver_combine_device(ctx.handle, toks.ctypes.data, toks.size, ctypes.byref(h),
+                                           ctypes.c_void_p(basis.data_ptr()), n, 0,
+                                           ctypes.c_void_p(target.data_ptr()), n, ctypes.byref(out))
+        assert rc == 0, (rc, L.rsh_last_error().decode())
+        assert out.target_len == n and out.literal + out.matched == n
+
+    for _ in range(a.warmup):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    with torch.cuda.stream(stream):
+        assert torch.equal(target, src), "rebuilt file differs from the source"
+    res = {
+        "metric": "GiB/s Receiver reconstruction (combineDataToFile: token walk, block gather, file digest)",
+        "value": round(a.steps * n / dt / (1 << 30), 4), "unit": "GiB/s", "n_gpus": 1, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64 on device)",
+        "config": {"workload": f"receiver: {n >> 30} GiB target from the Sender's tokens against a "
+                               f"{'50%-modified' if a.variant == 'half' else 'identical'} replica, B={B}, dl={dl}",
+                   "tokens_bytes": int(toks.size), "literal_bytes": int(out.literal),
+                   "matched_bytes": int(out.matched), "defer_write": 0,
+                   "bound": "the Receiver's serial whole-file MD5 on the host (Receiver.java:824-842)"},
+    }
+    print(json.dumps(res), flush=True)
+    ctx.close()
 
 
 def cfg_name(n, B):
@@ -429,6 +538,38 @@ def cpu_baseline(src, basis, B, dl, sample):
         "kind": "port",
         "sample": f"first {sample >> 20} MiB of the same source/basis pair (B={B}, dl={dl}): oracle Generator "
                   f"{(t1 - t0) * 1e3:.0f} ms + Sender scan incl. file MD5 {(t2 - t1) * 1e3:.0f} ms",
+    }
+
+
+def cpu_baseline_files(src, basis, S, F, B, dl, sample):
+    """Config 4 on the host: the oracle on K files at once, one file per host core (the
+    reference handles one file per Sender thread; independent invocations are its all-cores form).  Each
+    file contributes a bounded prefix of its pair; ctypes drops the GIL for the oracle calls."""
+    import concurrent.futures as cf
+    import oracle_ctypes as O
+    cores = max(1, min(16, len(os.sched_getaffinity(0)), F))
+    per = min(max(sample // cores, B), S)
+    per -= per % B
+    pairs = [(src[i * S:i * S + per].cpu().numpy(), basis[i * S:i * S + per].cpu().numpy()) for i in range(cores)]
+    seed = bytes([1, 2, 3, 4])
+    h = O.header(B, dl, per)
+
+    def one(pair):
+        s, b = pair
+        w, st = O.generator(b, h, seed)
+        O.sender(s, h, w, st, seed)
+
+    with cf.ThreadPoolExecutor(max_workers=cores) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(one, pairs))
+        dt = time.perf_counter() - t0
+    return {
+        "value": round(2 * per * cores / dt / (1 << 30), 4),
+        "unit": "GiB/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"{cores} files at once (one per core), the first {per >> 20} MiB of each source/basis pair "
+                  f"(B={B}, dl={dl}): oracle Generator + Sender scan incl. file MD5, {dt * 1e3:.0f} ms wall",
     }
 
 

@@ -1707,7 +1707,20 @@ __global__ __launch_bounds__(256) void gather_ops_kernel(const GatherOp* __restr
     const int64_t body = (op.len - head) & ~(int64_t)15;
     const uint8_t* __restrict__ s = op.src + head;
     uint8_t* __restrict__ o = op.dst + head;
-    if ((reinterpret_cast<uintptr_t>(s) & 3) == 0) {  // word-aligned source: four dword loads per store
+    if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) {  // 16-B aligned source: dwordx4 loads, 4 in flight
+        const int64_t step = 16 * (int64_t)blockDim.x;
+        int64_t k = 16 * (int64_t)t;
+        for (; k + 3 * step < body; k += 4 * step) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s + k + u * step));
+#pragma unroll
+            for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(o + k + u * step));
+        }
+        for (; k < body; k += step)
+            *reinterpret_cast<uint4*>(o + k) = *reinterpret_cast<const uint4*>(s + k);
+    } else if ((reinterpret_cast<uintptr_t>(s) & 3) == 0) {  // word-aligned source: four dword loads per store
         for (int64_t k = 16 * (int64_t)t; k < body; k += 16 * (int64_t)blockDim.x) {
             const uint32_t* w = reinterpret_cast<const uint32_t*>(s + k);
             *reinterpret_cast<uint4*>(o + k) = make_uint4(w[0], w[1], w[2], w[3]);
