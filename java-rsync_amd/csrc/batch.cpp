@@ -43,7 +43,24 @@ struct BatchState {
     // Sender batch: pinned host (read or written by the kernels directly)
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl, h_files, h_hit, h_win0, h_bucket, h_first, h_iv, h_tiles,
         h_ptiles, h_req, h_gw, h_gb, h_ow, h_ob, h_win, h_copies, h_tabents, h_flagents, h_dkeys, h_ccopies;
+    // device, uncached: one abort word per file of the batch; the speculation's groups of file f stop once
+    // file_abort[f] holds the scan's generation (written by the coordinator when f's resolver finishes)
+    int* file_abort = nullptr;
+    int64_t file_abort_cap = 0;
+    hipError_t ensure_file_abort(int64_t nf) {
+        if (nf <= file_abort_cap) return hipSuccess;
+        if (file_abort) (void)hipFree(file_abort);
+        file_abort = nullptr;
+        file_abort_cap = 0;
+        const int64_t cap = std::max<int64_t>(nf, 256);
+        hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&file_abort), (size_t)cap * 4,
+                                             hipDeviceMallocUncached);
+        if (e == hipSuccess) e = hipMemset(file_abort, 0, (size_t)cap * 4);  // generations start at 1
+        if (e == hipSuccess) file_abort_cap = cap;
+        return e;
+    }
     ~BatchState() {
+        if (file_abort) (void)hipFree(file_abort);
         for (DevBuf* b : {&g_groups, &g_lanes, &slots, &dslots, &src_weak, &src_strong, &flags, &haw, &partials, &bucket,
                           &first, &k1_groups, &k1_lanes})
             b->release();
@@ -121,6 +138,11 @@ class BatchBackend : public ScanBackend {
     int64_t t_pos = -1;    // the last hit returned: its weak sum t_val is known
     int32_t t_val = 0;
     HitCache cache;
+    // read-ahead of window requests: the bytes [pf_pos, pf_pos + pf.size()) of the source, copied with the
+    // last window request; a later digest inside them needs no round trip (in head mode the next match of
+    // a chain, or of every other block, is usually a window or two further on)
+    std::vector<uint8_t> pf;
+    int64_t pf_pos = -1;
 
     int64_t aligned_count() override { return head ? 0 : na; }
     int64_t max_batch() override { return head ? 4 : 4096; }
@@ -151,6 +173,7 @@ struct FileScan {
     bool pending = false;
     bool done = false;
     bool started = false;
+    bool cancelled = false;  // its speculation groups were dropped or told to stop (file_abort)
     int32_t worker = 0;
     ucontext_t uc;
     std::unique_ptr<char[]> stack;  // uninitialised: only the pages the fiber touches are committed
@@ -165,9 +188,12 @@ struct FileScan {
 struct Batch {
     std::mutex mu;
     std::condition_variable cv_coord, cv_work;
-    int32_t nworkers = 0, idle = 0;
-    uint64_t gen = 0;
-    bool quit = false;
+    int32_t nworkers = 0;
+    // written under mu (the condition variables' predicates); atomic so that a waiter can spin on them
+    // before it blocks (spin_wait)
+    std::atomic<int32_t> idle{0};
+    std::atomic<uint64_t> gen{0};
+    std::atomic<bool> quit{false};
     std::atomic<bool> landed{false};
     std::vector<FileScan>* files = nullptr;
     std::vector<ucontext_t> worker_uc;
@@ -182,6 +208,32 @@ struct Batch {
 };
 
 FileScan& scan_of(Batch* b, int32_t f) { return (*b->files)[(size_t)f]; }
+
+// Round hand-offs: a blocked thread takes ~50 us to wake from a condition variable, once per round per
+// side (coordinator -> workers, last worker -> coordinator).  Waiters spin up to RSH_BATCH_SPIN us
+// (default 200; 0 = block at once) on the predicate first, then block as before; the predicate is
+// re-checked under the mutex either way, so the hand-off protocol is unchanged.
+int spin_us() {
+    static const int v = [] {
+        const char* e = getenv("RSH_BATCH_SPIN");
+        return e ? std::max(0, atoi(e)) : 200;
+    }();
+    return v;
+}
+template <class Pred>
+void spin_wait(Pred pred) {
+    const int us = spin_us();
+    if (us <= 0 || pred()) return;
+    const auto end = std::chrono::steady_clock::now() + std::chrono::microseconds(us);
+    for (uint32_t i = 1;; ++i) {
+        __builtin_ia32_pause();
+        if (pred()) return;
+        if ((i & 63) == 0) {
+            if (std::chrono::steady_clock::now() >= end) return;
+            sched_yield();
+        }
+    }
+}
 
 // A resolver fiber: head mode until the batched speculation lands, then resume with it (resolve_run is
 // resumable); returning switches to uc_link (its worker).
@@ -224,6 +276,17 @@ void BatchBackend::bytes_many(const int64_t* pos, int64_t count, uint8_t* out) {
     b->post(fs);
 }
 
+// bytes copied per window request (A/B switch RSH_BATCH_READAHEAD; never less than the window).  Off by
+// default: on config 4 it cut the rounds from 23 to 18, but the head-mode rounds it removed were cheap
+// window copies and the probes left in their place wait behind the speculation K1
+int64_t readahead_bytes() {
+    static const int64_t v = [] {
+        const char* e = getenv("RSH_BATCH_READAHEAD");
+        return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)0;
+    }();
+    return v;
+}
+
 void BatchBackend::md5_at(int64_t p, uint8_t out[16]) {
     const int64_t w = std::min<int64_t>(B, n - p);
     const uint8_t* src = nullptr;
@@ -232,14 +295,21 @@ void BatchBackend::md5_at(int64_t p, uint8_t out[16]) {
         for (int k = 0; k < HIT_WINDOWS; ++k)
             if (p == win_pos[k]) src = hit + 16 + (int64_t)k * B;  // came back with the probe result
     }
+    if (!src && pf_pos >= 0 && p >= pf_pos && p + w <= pf_pos + (int64_t)pf.size()) src = pf.data() + (p - pf_pos);
     if (!src) {
         FileScan& fs = scan_of(b, f);
+        const int64_t ext = std::min<int64_t>(std::max<int64_t>(w, readahead_bytes()), n - p);
         fs.req = Req{};
         fs.req.kind = Req::WIN;
         fs.req.p = p;
-        fs.req.w = w;
+        fs.req.w = ext;
         b->post(fs);
         src = fs.req.win;
+        if (ext > w) {  // keep the read-ahead (the round's window buffer is reused by the next round)
+            pf.assign(src, src + ext);
+            pf_pos = p;
+            src = pf.data();
+        }
     }
     const auto t0 = std::chrono::steady_clock::now();
     HostMd5 h;  // one serial chain per window: on this file's host thread, beside the other files' work
@@ -522,6 +592,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     plan_block_sums_batch(k1.data(), NF, &groups, &lanes, &lane_align);
     RSH_BHIP(S->k1_groups.ensure((groups.size() + 1) * sizeof(K1Group)));
     RSH_BHIP(S->k1_lanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
+    RSH_BHIP(S->ensure_file_abort(NF));
+    for (K1Group& g : groups) g.abort = S->file_abort + g.file;
 
     hipStream_t st = c->stream, aux = c->aux;
     RSH_BHIP(hipEventRecord(c->ev_in, st));  // whatever produced the inputs on the context stream
@@ -564,6 +636,13 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     bool k1_launched = false;
     auto launch_spec_k1 = [&]() -> int {
         k1_launched = true;
+        // files already resolved (all workers idle here) need no speculation: their groups are dropped
+        size_t kept = 0;
+        for (const K1Group& g : groups)
+            if (!files[(size_t)g.file].done) groups[kept++] = g;
+        groups.resize(kept);
+        for (FileScan& fs : files)
+            if (fs.done) fs.cancelled = true;
         if (!groups.empty())
             RSH_BHIP(hipMemcpyAsync(S->k1_groups.p, groups.data(), groups.size() * sizeof(K1Group),
                                     hipMemcpyHostToDevice, aux));
@@ -682,7 +761,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     cpu_set_t cpus;
     int ncpu = 8;
     if (sched_getaffinity(0, sizeof(cpus), &cpus) == 0) ncpu = CPU_COUNT(&cpus);
-    const int32_t W = std::max<int32_t>(1, std::min<int32_t>({NF, (int32_t)ncpu, kMaxWorkers}));
+    // spinning waiters: one core stays free for the coordinator
+    const int32_t ncores = (spin_us() > 0 && ncpu > 2) ? ncpu - 1 : ncpu;
+    const int32_t W = std::max<int32_t>(1, std::min<int32_t>({NF, ncores, kMaxWorkers}));
     b.nworkers = W;
     b.worker_uc.resize((size_t)W);
     b.busy_ms.assign((size_t)W, 0.0);
@@ -696,8 +777,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             uint64_t seen = 0;
             for (;;) {
                 {
+                    auto go = [&] { return b.gen.load(std::memory_order_acquire) != seen || b.quit.load(); };
+                    spin_wait(go);
                     std::unique_lock<std::mutex> l(b.mu);
-                    b.cv_work.wait(l, [&] { return b.gen != seen || b.quit; });
+                    b.cv_work.wait(l, go);
                     if (b.quit) return;
                     seen = b.gen;
                 }
@@ -742,8 +825,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     auto t_round = std::chrono::steady_clock::now();
     for (;;) {
         {
+            auto all_idle = [&] { return b.idle.load(std::memory_order_acquire) == b.nworkers; };
+            spin_wait(all_idle);
             std::unique_lock<std::mutex> l(b.mu);
-            b.cv_coord.wait(l, [&] { return b.idle == b.nworkers; });
+            b.cv_coord.wait(l, all_idle);
             pend.clear();
             for (int32_t f = 0; f < NF; ++f)
                 if (!files[(size_t)f].done && files[(size_t)f].pending) pend.push_back(f);
@@ -759,6 +844,19 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         }
         if (spec_launched && spec_rc == RSH_OK && !b.landed.load() && hipEventQuery(c->ev_spec) == hipSuccess)
             b.landed.store(true, std::memory_order_release);
+        if (k1_launched && !b.landed.load()) {  // stop the speculation of files resolved since it started
+            for (int32_t f = 0; f < NF; ++f) {
+                FileScan& fs = files[(size_t)f];
+                if (fs.done && !fs.cancelled) {
+                    fs.cancelled = true;
+                    const hipError_t ew = hipStreamWriteValue32(st, S->file_abort + f, (uint32_t)gen, 0);
+                    if (ew != hipSuccess && err == hipSuccess) {  // a lost cancellation only costs time
+                        err = ew;
+                        note_error(ew, __LINE__, "batch.cpp");
+                    }
+                }
+            }
+        }
         const double wait_ms = ms_since(t_round);
         const auto t_serve = std::chrono::steady_clock::now();
         const hipError_t e = serve_round(c, S, files, pend);

@@ -38,6 +38,8 @@ struct K1Group {
     int32_t* weak;        // its output slots
     uint8_t* strong;
     uint32_t B, dl;
+    const int* abort = nullptr;  // abortable launches: this group's own abort word (nullptr: the launch's)
+    int32_t file = 0;            // index of its file in the planner's list (host bookkeeping only)
 };
 struct K1Lane {
     const uint8_t* data;  // the file

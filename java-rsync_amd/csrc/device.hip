@@ -476,6 +476,9 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
         weak_out = g.weak;
         strong_out = g.strong;
         c0 = 0;
+        if constexpr (ABORT) {
+            if (g.abort) abort_flag = g.abort;  // per-file cancellation (batched Sender speculation)
+        }
     }
     const uint32_t nst = B >> 7;  // host guarantees nst >= 4
     const int wr0 = (l >> 3) * ROW + (l & 7);
@@ -573,6 +576,11 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
 
     load(q[0], 0);
     load(q[1], 1);
+    if constexpr (ABORT && MULTI) {  // a group whose file was resolved before the wave started does nothing
+        int f0;
+        asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(f0) : "s"(abort_flag));
+        if (f0 == abort_gen) return;
+    }
     put(q[0], 0);
     load(q[0], 2);
     compiler_fence();
@@ -1031,7 +1039,8 @@ void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Gr
         if ((F.B % 128) == 0 && nst >= 4 && nst <= 1024 && (addr % 16) == 0) {  // the pipelined K1's shape
             const uint32_t nfullc = (uint32_t)std::min<int64_t>(F.n / F.B, F.nchunks);
             for (; c + 64 <= nfullc; c += 64)
-                groups->push_back(K1Group{F.data + (size_t)c * F.B, F.weak + c, F.strong + (size_t)c * F.dl, F.B, F.dl});
+                groups->push_back(
+                    K1Group{F.data + (size_t)c * F.B, F.weak + c, F.strong + (size_t)c * F.dl, F.B, F.dl, nullptr, f});
         }
         for (; c < F.nchunks; c += 64) {
             lanes->push_back(K1Lane{F.data, F.n, F.weak, F.strong, F.B, F.dl, c, F.nchunks});
