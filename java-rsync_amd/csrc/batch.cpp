@@ -641,8 +641,11 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         for (const K1Group& g : groups)
             if (!files[(size_t)g.file].done) groups[kept++] = g;
         groups.resize(kept);
+        int32_t dropped = 0;
         for (FileScan& fs : files)
-            if (fs.done) fs.cancelled = true;
+            if (fs.done) fs.cancelled = true, ++dropped;
+        if (getenv("RSH_SCAN_TRACE"))
+            fprintf(stderr, "[rsh-batch] speculation launched: %zu groups, %d resolved files dropped\n", groups.size(), dropped);
         if (!groups.empty())
             RSH_BHIP(hipMemcpyAsync(S->k1_groups.p, groups.data(), groups.size() * sizeof(K1Group),
                                     hipMemcpyHostToDevice, aux));
@@ -849,6 +852,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 FileScan& fs = files[(size_t)f];
                 if (fs.done && !fs.cancelled) {
                     fs.cancelled = true;
+                    if (trace) fprintf(stderr, "[rsh-batch] round %3d  file %d resolved: its speculation stops\n", rounds, f);
                     const hipError_t ew = hipStreamWriteValue32(st, S->file_abort + f, (uint32_t)gen, 0);
                     if (ew != hipSuccess && err == hipSuccess) {  // a lost cancellation only costs time
                         err = ew;

@@ -177,3 +177,85 @@ def test_batch_scan_nospace_is_per_file(ctx):
     assert sj[1].n_ev == len(full) and (sj[1].literal, sj[1].matched) == (lit, mat)
     want0, _, _, _, _ = ctx.match_scan(srcs[0], h, w, s, SEED)
     assert R.events_as_tuples(evs[0][:sj[0].n_ev], B) == R.events_as_tuples(want0, B)
+
+
+def test_batch_speculation_cancelled_per_file(ctx):
+    """Per-file cancellation of the batched speculation (batch.cpp: K1Group.abort, BatchState.file_abort).
+
+    Four 2 GiB identical files (generated on the device) need the speculation's aligned sums: a ~2 ms
+    launch.  Unrelated files resolve in the first rounds and are dropped from the launch; 50%-modified
+    files poison early (quirk B) and are told to stop while it runs.  A wrongly aimed abort word would
+    leave a live file with undefined aligned sums: the identical files must still give one MATCH per
+    chunk in order (Sender.java:1235-1327 with pref = i+1), the small ones must equal the oracle."""
+    B, dl = 8192, 3
+    rng = random.Random(77)
+    big_n, n_big = 2 << 30, 4
+    d_big = ctx.alloc(n_big * big_n)
+    h_big = R.header_make(B, dl, big_n)
+    C = h_big.chunk_count
+    d_bw, d_bs = ctx.alloc(4 * C * n_big), ctx.alloc(dl * C * n_big)
+    L = R.lib()
+    for k in range(n_big):
+        assert L.rsh_fill_splitmix_device(ctx.handle, d_big.ptr.value + k * big_n, big_n, 0xB16 + k, 0) == 0
+        assert L.rsh_block_sums_device(ctx.handle, d_big.ptr.value + k * big_n, big_n, ctypes.byref(h_big),
+                                       SEED_NP.ctypes.data, d_bw.ptr.value + 4 * C * k,
+                                       d_bs.ptr.value + dl * C * k) == 0
+    ctx.sync()
+    small = []
+    for i in range(16):
+        key = rng.randrange(1 << 62)
+        nb = 8 << 20
+        basis = O.splitmix(nb, key).tobytes()
+        if i % 2:                                            # every other block replaced: poisons early
+            other = O.splitmix(nb, key ^ 0xED17).tobytes()
+            src = b"".join(other[k:k + B] if (k // B) % 2 else basis[k:k + B] for k in range(0, nb, B))
+        else:
+            src = O.splitmix(nb, key ^ 0x5A5A).tobytes()    # unrelated: no hit at all
+        small.append((basis, src))
+    d_src, soffs = _pack(ctx, [f[1] for f in small], [0] * len(small))
+    nj = n_big + len(small)
+    sj = (R.ScanJob * nj)()
+    keep, expect, evs = [], [], []
+    for k in range(n_big):
+        ev = np.zeros(C + 64, R.EVENT_DTYPE)
+        evs.append(ev)
+        sj[k].d_src = d_big.ptr.value + k * big_n
+        sj[k].n = big_n
+        sj[k].h = h_big
+        sj[k].d_weak = d_bw.ptr.value + 4 * C * k
+        sj[k].d_strong = d_bs.ptr.value + dl * C * k
+        sj[k].ev = ev.ctypes.data
+        sj[k].ev_cap = C + 64
+        expect.append(None)
+    for i, (basis, src) in enumerate(small):
+        j = n_big + i
+        h = R.header_make(B, dl, len(basis))
+        w, s = ctx.block_sums(basis, h, SEED)
+        d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
+        d_w.upload(w)
+        d_s.upload(s)
+        cap = len(src) // (10 * B) + 2 * h.chunk_count + 64
+        ev = np.zeros(cap, R.EVENT_DTYPE)
+        keep += [d_w, d_s]
+        evs.append(ev)
+        sj[j].d_src = d_src.ptr.value + soffs[i]
+        sj[j].n = len(src)
+        sj[j].h = h
+        sj[j].d_weak = d_w.ptr.value
+        sj[j].d_strong = d_s.ptr.value
+        sj[j].ev = ev.ctypes.data
+        sj[j].ev_cap = cap
+        oev, _, olit, omat, _ = O.sender(src, O.header(B, dl, len(basis)), w, s, SEED)
+        expect.append(([tuple(e) for e in oev], olit, omat))
+    run = [(R.EV_MATCH, c * B, B, c) for c in range(C)]
+    for _ in range(2):  # the second call reuses the abort words (generations only grow)
+        rc = L.rsh_match_scan_batch_device(ctx.handle, sj, nj, SEED_NP.ctypes.data, None)
+        assert rc == 0, (rc, L.rsh_last_error())
+        for j in range(nj):
+            assert sj[j].status == 0
+            got = R.events_as_tuples(evs[j][:sj[j].n_ev], B)
+            if j < n_big:
+                assert got == run and (sj[j].literal, sj[j].matched) == (0, big_n), f"identical file {j}"
+            else:
+                oev, olit, omat = expect[j]
+                assert got == oev and (sj[j].literal, sj[j].matched) == (olit, omat), f"small file {j}"
