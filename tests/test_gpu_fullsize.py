@@ -1,5 +1,6 @@
-"""Parity at BASELINE.json's full sizes (config 2: 4 GiB, B = 65536; config 5: 16 GiB, B = 131072; config 4:
-128 x 128 MiB per GPU, B = 8192, through the batched entry points).
+"""Parity at BASELINE.json's full sizes (config 2: 4 GiB, B = 65536; config 3: 64 GiB, B = 262144 for the
+Generator and the B = 131072 override for the scan; config 5: 16 GiB, B = 131072; config 4: 128 x 128 MiB
+per GPU, B = 8192, through the batched entry points).
 
 The oracle cannot replay a 4-16 GiB Sender scan within a test's time limit (it walks every byte, ~0.05 GiB/s),
 so the full-size checks are the size-independent properties of the path:
@@ -150,6 +151,47 @@ def test_config2_4GiB_generator_and_scans(env):
     assert ev[0]["kind"] == R.EV_MATCH and ev[0]["index"] == 0 and ev[0]["count"] >= k
     _check_delta(torch, ev, src, basis, h, lit, mat)
     del src
+
+
+def test_config3_64GiB(env):
+    """Config 3: 64 GiB.  The README rule gives B = 262144, dl = 5: the Generator runs it (bit-exact against
+    the threaded oracle over all 262144 chunks), but the reference Sender rejects B > 2^17
+    (Checksum.java:81-82), so the scan runs under the explicit B = 131072 override (dl = 5) that bench.py's
+    config-3 line uses, over a source with two rewritten blocks (no shift, so every later match is an
+    aligned chain or, after a weak collision in the edited block, the rest is literal: quirk B)."""
+    ctx, torch = env
+    n = 64 << 30
+    B = R.block_length_for(n)
+    dl = R.digest_length_for(n, B)
+    assert (B, dl) == (262144, 5)
+    basis = torch.empty(n, dtype=torch.uint8, device="cuda")
+    _fill(ctx, basis, KEY ^ 3)
+    ctx.sync()
+    h = R.header_make(B, dl, n)
+    with pytest.raises(R.ProtocolError):
+        R.header_validate(h)
+    _gen_parity(ctx, torch, basis, B, dl)
+
+    B = 131072
+    h = R.header_make(B, dl, n)
+    R.header_validate(h)
+    d_w, d_s = _block_sums(ctx, torch, basis, h)
+    src = basis.clone()
+    k = (5 << 30) // B                                  # 5 GiB unchanged, then a reversed block
+    src[k * B:(k + 1) * B] = src[k * B:(k + 1) * B].flip(0)
+    j = (40 << 30) // B                                 # and a block of other bytes at 40 GiB
+    _fill(ctx, src[j * B:(j + 1) * B], KEY ^ 0x3E5)
+    ctx.sync()
+    ev, lit, mat, st = _scan(ctx, torch, src, h, d_w, d_s)
+    lead = 0  # the unchanged prefix: MATCH(0 .. k-1), and nothing further (chunk k was rewritten)
+    for e in ev:
+        if e["kind"] != R.EV_MATCH or int(e["index"]) != lead:
+            break
+        lead += int(e["count"])
+    assert lead == k
+    _check_delta(torch, ev, src, basis, h, lit, mat)
+    del src, basis
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("variant", ["identical", "half"])
