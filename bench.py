@@ -32,7 +32,8 @@ import shard  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 # production K1 instantiation (device.hip launch_block_sums_variant default); the committed PMC profile
 # for `traffic` is matched on this name so a stale profile of another kernel is never reported
-PROD_KERNEL = "block_sums_pipe_kernel<8, false, true, 0>"
+PROD_KERNEL = "block_sums_pipe_kernel<8, false, true, 0, false>"  # the Generator K1 (non-batched)
+BATCH_KERNEL = "block_sums_pipe_kernel<8, false, true, 0, true>"  # the Generator K1 over a segment
 KEY_SRC = 0x5EED5EED << 32
 KEY_EDIT = (0x5EED5EED << 32) | 0xED17
 
@@ -221,7 +222,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(os.path.join(ROOT, "profiles", "r1_pmc", "bench_fetch_size.csv"),
+            "traffic": pmc_traffic(os.path.join(ROOT, "profiles", "r1_v14_bench_fetch_size.csv"),
                                    PROD_KERNEL, n),
             "kernel_ms": round(gen_ms, 4),
             "algorithmic_bytes": n,
@@ -391,7 +392,10 @@ def main_files(a):
         ach = n / (k_ms * 1e-3) / 1e9
         res["roofline"] = {"kernel": "block_sums_pipe_kernel (batched K1: the Generator over the segment)",
                            "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(k_ms, 4),
+                           "frac": round(ach / HBM_PEAK_GBS, 4),
+                           "traffic": pmc_traffic(os.path.join(ROOT, "profiles", "r1_v14_files_fetch_size.csv"),
+                                                  BATCH_KERNEL, n),
+                           "kernel_ms": round(k_ms, 4),
                            "algorithmic_bytes": n}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_files(src, basis, S, F, B, dl, a.cpu_sample_mib << 20)

@@ -47,6 +47,15 @@ struct BatchState {
     // file_abort[f] holds the scan's generation (written by the coordinator when f's resolver finishes)
     int* file_abort = nullptr;
     int64_t file_abort_cap = 0;
+    // Generator batch: its launch descriptors, staged in pinned memory so that the upload is asynchronous
+    // (a pageable copy blocks the host while the device idles); ev_gcopy guards the staging buffers' reuse
+    PinnedBuf h_ggroups, h_glanes;
+    hipEvent_t ev_gcopy = nullptr;
+    bool gcopy_pending = false;
+    // the same for the Sender's speculation launch (uploaded on the aux stream from the coordinator thread)
+    PinnedBuf h_sgroups, h_slanes;
+    hipEvent_t ev_scopy = nullptr;
+    bool scopy_pending = false;
     hipError_t ensure_file_abort(int64_t nf) {
         if (nf <= file_abort_cap) return hipSuccess;
         if (file_abort) (void)hipFree(file_abort);
@@ -61,6 +70,18 @@ struct BatchState {
     }
     ~BatchState() {
         if (file_abort) (void)hipFree(file_abort);
+        if (ev_gcopy) {
+            if (gcopy_pending) (void)hipEventSynchronize(ev_gcopy);
+            (void)hipEventDestroy(ev_gcopy);
+        }
+        if (ev_scopy) {
+            if (scopy_pending) (void)hipEventSynchronize(ev_scopy);
+            (void)hipEventDestroy(ev_scopy);
+        }
+        h_ggroups.release();
+        h_glanes.release();
+        h_sgroups.release();
+        h_slanes.release();
         for (DevBuf* b : {&g_groups, &g_lanes, &slots, &dslots, &src_weak, &src_strong, &flags, &haw, &partials, &bucket,
                           &first, &k1_groups, &k1_lanes})
             b->release();
@@ -646,12 +667,23 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             if (fs.done) fs.cancelled = true, ++dropped;
         if (getenv("RSH_SCAN_TRACE"))
             fprintf(stderr, "[rsh-batch] speculation launched: %zu groups, %d resolved files dropped\n", groups.size(), dropped);
-        if (!groups.empty())
-            RSH_BHIP(hipMemcpyAsync(S->k1_groups.p, groups.data(), groups.size() * sizeof(K1Group),
+        if (!S->ev_scopy) RSH_BHIP(hipEventCreateWithFlags(&S->ev_scopy, hipEventDisableTiming));
+        if (S->scopy_pending) RSH_BHIP(hipEventSynchronize(S->ev_scopy));  // the previous scan's upload is done
+        S->scopy_pending = false;
+        RSH_BHIP(S->h_sgroups.ensure((groups.size() + 1) * sizeof(K1Group)));
+        RSH_BHIP(S->h_slanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
+        if (!groups.empty()) {  // pinned staging: the upload does not block the coordinator
+            memcpy(S->h_sgroups.p, groups.data(), groups.size() * sizeof(K1Group));
+            RSH_BHIP(hipMemcpyAsync(S->k1_groups.p, S->h_sgroups.p, groups.size() * sizeof(K1Group),
                                     hipMemcpyHostToDevice, aux));
-        if (!lanes.empty())
-            RSH_BHIP(hipMemcpyAsync(S->k1_lanes.p, lanes.data(), lanes.size() * sizeof(K1Lane), hipMemcpyHostToDevice,
+        }
+        if (!lanes.empty()) {
+            memcpy(S->h_slanes.p, lanes.data(), lanes.size() * sizeof(K1Lane));
+            RSH_BHIP(hipMemcpyAsync(S->k1_lanes.p, S->h_slanes.p, lanes.size() * sizeof(K1Lane), hipMemcpyHostToDevice,
                                     aux));
+        }
+        RSH_BHIP(hipEventRecord(S->ev_scopy, aux));
+        S->scopy_pending = true;
         RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>(), (uint32_t)groups.size(), S->k1_lanes.as<K1Lane>(),
                                          (uint32_t)lanes.size(), lane_align, seed_word(seed), aux, c->abort_word, gen));
         return RSH_OK;
@@ -980,13 +1012,23 @@ int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t
     plan_block_sums_batch(files.data(), (int32_t)files.size(), &groups, &lanes, &lane_align);
     RSH_BHIP(S->g_groups.ensure((groups.size() + 1) * sizeof(K1Group)));
     RSH_BHIP(S->g_lanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
-    // pageable sources: the copies are staged before hipMemcpyAsync returns, so the vectors may go
-    if (!groups.empty())
-        RSH_BHIP(hipMemcpyAsync(S->g_groups.p, groups.data(), groups.size() * sizeof(K1Group), hipMemcpyHostToDevice,
+    if (!S->ev_gcopy) RSH_BHIP(hipEventCreateWithFlags(&S->ev_gcopy, hipEventDisableTiming));
+    if (S->gcopy_pending) RSH_BHIP(hipEventSynchronize(S->ev_gcopy));  // the previous call's upload is done
+    S->gcopy_pending = false;
+    RSH_BHIP(S->h_ggroups.ensure((groups.size() + 1) * sizeof(K1Group)));
+    RSH_BHIP(S->h_glanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
+    if (!groups.empty()) {
+        memcpy(S->h_ggroups.p, groups.data(), groups.size() * sizeof(K1Group));
+        RSH_BHIP(hipMemcpyAsync(S->g_groups.p, S->h_ggroups.p, groups.size() * sizeof(K1Group), hipMemcpyHostToDevice,
                                 ctx->stream));
-    if (!lanes.empty())
-        RSH_BHIP(hipMemcpyAsync(S->g_lanes.p, lanes.data(), lanes.size() * sizeof(K1Lane), hipMemcpyHostToDevice,
+    }
+    if (!lanes.empty()) {
+        memcpy(S->h_glanes.p, lanes.data(), lanes.size() * sizeof(K1Lane));
+        RSH_BHIP(hipMemcpyAsync(S->g_lanes.p, S->h_glanes.p, lanes.size() * sizeof(K1Lane), hipMemcpyHostToDevice,
                                 ctx->stream));
+    }
+    RSH_BHIP(hipEventRecord(S->ev_gcopy, ctx->stream));
+    S->gcopy_pending = true;
     RSH_BHIP(launch_block_sums_batch(S->g_groups.as<K1Group>(), (uint32_t)groups.size(), S->g_lanes.as<K1Lane>(),
                                      (uint32_t)lanes.size(), lane_align, seed_word(seed), ctx->stream));
     return RSH_OK;
