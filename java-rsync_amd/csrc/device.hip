@@ -1,6 +1,9 @@
 // device.hip -- gfx950 (CDNA4) kernels for java-rsync's delta-transfer checksum path.
 //
-// Integer/byte work, HBM-bound: no MFMA.  Layout in HBM: the file is one flat byte array (caller's
+// Integer/byte work, HBM-bound (the MD5 chains are VALU work).  The one matrix-core use is the
+// production K1's weak sums: two v_mfma_i32_16x16x64_i8 per stage against a 0/1-and-index weight
+// matrix (exact int32, see block_sums_pipe_kernel), which takes them off the VALU that MD5 saturates.
+// No GEMM reshaping anywhere else.  Layout in HBM: the file is one flat byte array (caller's
 // buffer, 256-B aligned from hipMalloc); per-chunk outputs are struct-of-arrays (weak int32[C],
 // strong uint8[C*dl]).  See DESIGN.md for the roofline of each kernel.
 #include <hip/hip_runtime.h>
@@ -166,11 +169,7 @@ __device__ __forceinline__ void lane_chunk_sums(const uint8_t* __restrict__ data
 
     const int32_t s2 = (int32_t)(L * (uint32_t)s1 - (uint32_t)u);
     weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
-    uint8_t* o = strong_out + (size_t)c * dl;
-    for (uint32_t k = 0; k < dl; ++k) {
-        const uint32_t word = k < 4 ? st.a : k < 8 ? st.b : k < 12 ? st.c : st.d;
-        o[k] = (uint8_t)(word >> (8 * (k & 3)));
-    }
+    store_digest(strong_out + (size_t)c * dl, st, dl);
 }
 
 template <int ALIGN, int PF, bool NT = true>
@@ -417,11 +416,7 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
     if constexpr (MODE == 2) st.a ^= fold;
     const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
     weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
-    uint8_t* o = strong_out + (size_t)c * dl;
-    for (uint32_t k = 0; k < dl; ++k) {
-        const uint32_t word = k < 4 ? st.a : k < 8 ? st.b : k < 12 ? st.c : st.d;
-        o[k] = (uint8_t)(word >> (8 * (k & 3)));
-    }
+    store_digest(strong_out + (size_t)c * dl, st, dl);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -633,11 +628,7 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
     const uint32_t c = c0 + l;
     const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
     weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
-    uint8_t* o = strong_out + (size_t)c * dl;
-    for (uint32_t k = 0; k < dl; ++k) {
-        const uint32_t word = k < 4 ? st.a : k < 8 ? st.b : k < 12 ? st.c : st.d;
-        o[k] = (uint8_t)(word >> (8 * (k & 3)));
-    }
+    store_digest(strong_out + (size_t)c * dl, st, dl);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -710,11 +701,7 @@ __global__ __launch_bounds__(64) void block_sums_dma_kernel(const uint8_t* __res
     const uint32_t c = c0 + l;
     const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
     weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
-    uint8_t* o = strong_out + (size_t)c * dl;
-    for (uint32_t k = 0; k < dl; ++k) {
-        const uint32_t word = k < 4 ? st.a : k < 8 ? st.b : k < 12 ? st.c : st.d;
-        o[k] = (uint8_t)(word >> (8 * (k & 3)));
-    }
+    store_digest(strong_out + (size_t)c * dl, st, dl);
 }
 
 // MD5 step form of the production K1: 0 compiler, 1 one asm statement per step, 2 generated blocks

@@ -478,4 +478,13 @@ RSH_HD void md5_digest_bytes(const Md5State& st, uint8_t out[16]) {
         for (int j = 0; j < 4; j++) out[4 * i + j] = (uint8_t)(w[i] >> (8 * j));
 }
 
+// The first dl bytes of the digest as the Sender keeps them: Arrays.copyOf(digest, dl)
+// (Sender.java:1262) zero-pads past the 16 digest bytes when a peer's header asks for dl > 16.
+RSH_HD void store_digest(uint8_t* o, const Md5State& st, uint32_t dl) {
+    for (uint32_t k = 0; k < dl; ++k) {
+        const uint32_t word = k < 4 ? st.a : k < 8 ? st.b : k < 12 ? st.c : st.d;
+        o[k] = k < 16 ? (uint8_t)(word >> (8 * (k & 3))) : (uint8_t)0;
+    }
+}
+
 }  // namespace rsh

@@ -177,7 +177,8 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
     uint32_t& ehi = state->ehi;
     int64_t& anchor = state->anchor;
     bool& md5c_valid = state->md5c_valid;
-    uint8_t* md5c = state->md5c;
+    state->md5c.resize((size_t)dl);
+    uint8_t* md5c = state->md5c.data();
     std::vector<int32_t>& dkeys = state->dkeys;
     bool& dkeys_ready = state->dkeys_ready;
     int64_t& batch = state->batch;
@@ -317,7 +318,8 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
                         } else {
                             uint8_t full[16];
                             be.md5_at(p, full);
-                            memcpy(md5c, full, (size_t)dl);
+                            memcpy(md5c, full, (size_t)std::min(dl, 16));
+                            if (dl > 16) memset(md5c + 16, 0, (size_t)(dl - 16));
                             st.host_md5_windows++;
                         }
                         md5c_valid = true;

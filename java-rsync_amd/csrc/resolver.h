@@ -135,7 +135,7 @@ struct ResolveState {
     uint32_t elo = 0, ehi = 0;
     int64_t anchor = 0;
     bool md5c_valid = false;  // localChunkMd5sum != null (Sender.java:1248)
-    uint8_t md5c[16] = {};
+    std::vector<uint8_t> md5c;  // digest_length bytes: Arrays.copyOf(MD5, dl), zero past 16 (:1262)
     std::vector<int32_t> dkeys;  // weak keys of the chunks whose digest is md5c
     bool dkeys_ready = false;
     int64_t batch = 1;  // flush intervals speculated per batched probe

@@ -24,24 +24,57 @@ final class NativeChecksum implements AutoCloseable {
         }
     }
 
-    // one context per calling thread (Generator and Sender run on separate threads, RsyncClient.java:431)
-    private static final ThreadLocal<NativeChecksum> PER_THREAD = ThreadLocal.withInitial(() -> new NativeChecksum(
-            Integer.getInteger("rsync.hip.device", (int) (Thread.currentThread().getId() % Math.max(1,
-                    Integer.getInteger("rsync.hip.devices", 1))))));
+    // One context per calling thread (Generator and Sender run on separate threads, RsyncClient.java:431).
+    // Every context is registered so it is destroyed exactly once: by the owning task when it ends
+    // (releaseForThread() in the finally of Generator.call / Sender.call, RsyncTask) or, for threads that
+    // never release, by the shutdown hook.
+    private static final java.util.Set<NativeChecksum> LIVE = java.util.concurrent.ConcurrentHashMap.newKeySet();
+    private static final ThreadLocal<NativeChecksum> PER_THREAD = new ThreadLocal<>();
 
-    static NativeChecksum forThread() {
-        return PER_THREAD.get();
+    static {
+        if (ENABLED) {
+            Runtime.getRuntime().addShutdownHook(new Thread(() -> {
+                for (NativeChecksum c : LIVE) {
+                    c.close();
+                }
+            }, "rsync-hip-close"));
+        }
     }
 
-    private final long ctx;
+    static NativeChecksum forThread() {
+        NativeChecksum c = PER_THREAD.get();
+        if (c == null) {
+            int devices = Math.max(1, Integer.getInteger("rsync.hip.devices", 1));
+            c = new NativeChecksum(Integer.getInteger("rsync.hip.device",
+                    (int) (Thread.currentThread().getId() % devices)));
+            PER_THREAD.set(c);
+            LIVE.add(c);
+        }
+        return c;
+    }
+
+    /** Destroys the calling thread's context, if it has one (idempotent). */
+    static void releaseForThread() {
+        NativeChecksum c = PER_THREAD.get();
+        if (c != null) {
+            PER_THREAD.remove();
+            c.close();
+        }
+    }
+
+    private long ctx;
 
     private NativeChecksum(int device) {
         ctx = ctxCreate(device);
     }
 
     @Override
-    public void close() {
-        ctxDestroy(ctx);
+    public synchronized void close() {
+        if (ctx != 0) {
+            ctxDestroy(ctx);
+            ctx = 0;
+        }
+        LIVE.remove(this);
     }
 
     /** Generator.java:886-895: weak[i] and strong[i*dl .. i*dl+dl) for every chunk of the basis. */

@@ -63,6 +63,10 @@ def digest_length(n, blen):  # Generator.java:208-212 with Util.log2 (Util.java:
     return max(2, min(16, r))
 
 
+def copy_of(digest, dl):  # Arrays.copyOf (Sender.java:1262): truncate, or zero-pad past 16 bytes
+    return digest[:dl] + bytes(max(0, dl - len(digest)))
+
+
 def header(blen, dlen, n):  # Checksum.java:94-113
     if blen == 0:
         return dict(chunk_count=0, block_length=0, digest_length=0, remainder=0)
@@ -76,7 +80,7 @@ def generator(basis, hdr, seed):
     out = []
     for i in range(hdr["chunk_count"]):
         blk = basis[i * B:(i + 1) * B]
-        out.append((weak(blk), hashlib.md5(blk + seed).digest()[:dl]))
+        out.append((weak(blk), copy_of(hashlib.md5(blk + seed).digest(), dl)))
     return out
 
 
@@ -143,7 +147,7 @@ def sender(src, hdr, sums, seed):
         w = W(start)
         for c in candidates(roll, w, pref):
             if md5c is None:
-                md5c = hashlib.md5(src[start:start + w] + seed).digest()[:dl]
+                md5c = copy_of(hashlib.md5(src[start:start + w] + seed).digest(), dl)
             if md5c == sums[c][1]:
                 smatch += w
                 first = min(start, mark)

@@ -225,7 +225,10 @@ void orc_generator_sums(const uint8_t* basis, int64_t n, const orc_header* h, co
         orc_md5_update(&md, basis + off, (size_t)len);
         orc_md5_update(&md, seed, 4);
         orc_md5_final(&md, dig);
-        memcpy(strong_out + i * dl, dig, (size_t)dl);
+        /* the reference's rule never gives dl > 16 (and out.put(digest, 0, dl) would throw); a table
+         * with dl > 16 is only built here for Sender tests, padded as the Sender pads (:1262) */
+        memcpy(strong_out + i * dl, dig, (size_t)(dl < 16 ? dl : 16));
+        if (dl > 16) memset(strong_out + i * dl + 16, 0, (size_t)(dl - 16));
     }
 }
 
@@ -341,8 +344,13 @@ static int sender_match(const uint8_t* x, int64_t N, const orc_header* h, const 
     int32_t preferred = 0;
     int64_t size_literal = 0, size_match = 0;
     int md5c_valid = 0; /* localChunkMd5sum == null (:1248) */
-    uint8_t md5c[16];
+    /* Arrays.copyOf(digest, md5.length) (:1262): dl bytes, zero past the 16 digest bytes */
+    uint8_t* md5c = (uint8_t*)calloc((size_t)(dl > 0 ? dl : 1), 1);
     uint8_t dig[16];
+    if (!md5c) {
+        free(t.sorted);
+        return -1;
+    }
 
     while (wl(start, B, N) >= S) {
         int64_t w = wl(start, B, N);
@@ -371,7 +379,7 @@ static int sender_match(const uint8_t* x, int64_t N, const orc_header* h, const 
                     orc_md5_update(&chunk_digest, x + start, (size_t)w);
                     orc_md5_update(&chunk_digest, seed, 4);
                     orc_md5_final(&chunk_digest, dig);
-                    memcpy(md5c, dig, (size_t)dl);
+                    memcpy(md5c, dig, (size_t)(dl < 16 ? dl : 16));
                     md5c_valid = 1;
                     r->md5_windows++;
                 }
@@ -418,9 +426,11 @@ static int sender_match(const uint8_t* x, int64_t N, const orc_header* h, const 
     r->literal = size_literal;
     r->matched = size_match;
     free(t.sorted);
+    free(md5c);
     return 0;
 oom:
     free(t.sorted);
+    free(md5c);
     return -1;
 }
 

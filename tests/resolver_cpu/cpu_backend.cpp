@@ -33,7 +33,7 @@ class CpuBackend : public rsh::ScanBackend {
             aw_[k] = weak1(k * B_);
             uint8_t d[16];
             md5_at(k * B_, d);
-            memcpy(&as_[k * dl_], d, dl_);
+            memcpy(&as_[k * dl_], d, (size_t)std::min(dl_, 16));  // zero past 16 (Sender.java:1262)
         }
         const int64_t nf = na < t.chunk_count ? na : t.chunk_count;
         fl_.resize(nf > 0 ? nf : 1);

@@ -124,6 +124,33 @@ def test_sender_config_shapes(ctx, blen, dlen, mode):
     _sender_both(ctx, basis.tobytes(), src.tobytes(), blen, dlen)
 
 
+@pytest.mark.parametrize("pad", ["zero", "garbage"])
+def test_sender_digest_longer_than_md5(ctx, pad):
+    """digest_length 20 from the peer's header (accepted by Checksum.Header, Checksum.java:85-86): the Sender
+    compares Arrays.copyOf(MD5, 20) (Sender.java:1262), zero past byte 16, through the aligned speculation
+    (K1 writes zeros there) and the host window digests alike; the Generator refuses dl > 16 (its
+    out.put(digest, 0, dl) throws)."""
+    import ctypes
+    B, dl = 1024, 20
+    basis = O.splitmix(300 * B + 5, 4242).tobytes()
+    src = basis[:100 * B] + O.splitmix(333, 4343).tobytes() + basis[100 * B:]
+    h = O.header(B, dl, len(basis))
+    w, s = O.generator(basis, h, SEED)
+    s = s.copy()
+    if pad == "garbage":
+        s.reshape(-1, dl)[150:, 17] = 0xA5
+    oev, ofm, olit, omat, _ = O.sender(src, h, w, s, SEED)
+    rh = R.Header(**h.as_dict())
+    ev, fm, lit, mat, _ = ctx.match_scan(src, rh, w, s, SEED)
+    assert R.events_as_tuples(ev, B) == [tuple(e) for e in oev]
+    assert (fm, lit, mat) == (ofm, olit, omat) and omat >= 100 * B
+    a = np.frombuffer(basis, np.uint8)
+    ow, os_ = np.zeros(h.chunk_count, np.int32), np.zeros(h.chunk_count * dl, np.uint8)
+    seed = np.frombuffer(SEED, np.uint8).copy()
+    assert R.lib().rsh_block_sums(ctx.handle, a.ctypes.data, a.size, ctypes.byref(rh), seed.ctypes.data,
+                                  ow.ctypes.data, os_.ctypes.data) == R.RSH_E_INVAL
+
+
 def test_device_fill_matches_oracle(ctx):
     n = (1 << 20) + 13
     d = ctx.alloc(n)

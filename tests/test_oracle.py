@@ -154,7 +154,7 @@ def _fuzz_case(rng):
         src = blk * rng.randrange(0, 8) + O.splitmix(rng.randrange(0, B), key + 4).tobytes() + blk * 3
     else:
         src = bytes(rng.randrange(2) * 255 for _ in range(rng.randrange(0, 4 * B)))
-    dl = rng.choice([2, 2, 3, 16])
+    dl = rng.choice([2, 2, 3, 16, 20])  # 20: a peer header past the MD5 length (zero-padded, Sender.java:1262)
     return basis, src, B, dl
 
 

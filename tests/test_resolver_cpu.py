@@ -200,3 +200,26 @@ def test_resolver_hit_cache(seed_i):
     finally:
         L.rtest_hit_cache(0)
     assert answered > 0
+
+
+@pytest.mark.parametrize("pad", ["zero", "garbage"])
+def test_resolver_digest_longer_than_md5(pad):
+    """A peer header with digest_length > 16 (Checksum.Header accepts any dl >= 0, Checksum.java:85-86):
+    the Sender keeps Arrays.copyOf(MD5, dl) (Sender.java:1262), zero past byte 16.  Chunks whose received
+    digest is zero-padded match; chunks with other bytes there never do (and poison, quirk B)."""
+    B, dl = 512, 20
+    basis = O.splitmix(40 * B + 77, 4242).tobytes()
+    src = basis[:7 * B] + O.splitmix(300, 4343).tobytes() + basis[7 * B:]
+    h = O.header(B, dl, len(basis))
+    weak, strong = O.generator(basis, h, bytes([1, 2, 3, 4]))
+    strong = strong.copy()
+    assert not strong.reshape(-1, dl)[:, 16:].any()
+    if pad == "garbage":
+        strong.reshape(-1, dl)[20:, 18] = 0x5A
+    oev, _, olit, omat, _ = O.sender(src, h, weak, strong, bytes([1, 2, 3, 4]))
+    ev, lit, mat, _ = resolve(src, R.Header(**h.as_dict()), weak, strong, bytes([1, 2, 3, 4]))
+    assert R.events_as_tuples(ev, B) == [tuple(e) for e in oev]
+    assert (lit, mat) == (olit, omat)
+    assert omat >= 7 * B
+    if pad == "garbage":
+        assert omat < len(basis) - 20 * B
