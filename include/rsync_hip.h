@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RSH_ABI_VERSION 1
+#define RSH_ABI_VERSION 2
 
 /* Status codes (the JNI shim maps them onto the reference's exception types). */
 #define RSH_OK 0
@@ -79,6 +79,13 @@ typedef struct {
     int64_t head_steps;      /* resolver steps taken before the aligned speculation landed    */
     int64_t speculation_aborted; /* 1: the scan ended first and the speculation launch was stopped;
                                     2: the scan ended in head mode before the speculation was launched */
+    int64_t device_bytes;    /* source bytes the device work of this scan read: speculations that ran to
+                                completion (a stopped one counts 0), probed ranges (+ B - 1 per interval),
+                                weak-sum windows, gathered bytes and copied digest windows (ABI 2)  */
+    int64_t phase_launches;  /* phase-shifted speculations launched (chains at kB + delta, ABI 2)   */
+    int64_t phase_matches;   /* matches resolved from a phase-shifted speculation (ABI 2)           */
+    double spec_kernel_ms;   /* the aligned speculation's K1 alone (HIP events on its stream), when it ran
+                                to completion; 0 otherwise (ABI 2)                                   */
 } rsh_scan_stats;
 
 typedef struct rsh_ctx rsh_ctx;

@@ -277,6 +277,7 @@ void BatchBackend::weak_many(const int64_t* pos, int64_t count, int32_t* out) {
         out[0] = t_val;
         return;
     }
+    bytes_read += count * B;
     FileScan& fs = scan_of(b, f);
     fs.req = Req{};
     fs.req.kind = Req::WEAK;
@@ -288,6 +289,7 @@ void BatchBackend::weak_many(const int64_t* pos, int64_t count, int32_t* out) {
 
 void BatchBackend::bytes_many(const int64_t* pos, int64_t count, uint8_t* out) {
     if (count <= 0) return;
+    bytes_read += count;
     FileScan& fs = scan_of(b, f);
     fs.req = Req{};
     fs.req.kind = Req::BYTES;
@@ -324,6 +326,7 @@ void BatchBackend::md5_at(int64_t p, uint8_t out[16]) {
         fs.req.kind = Req::WIN;
         fs.req.p = p;
         fs.req.w = ext;
+        bytes_read += ext;
         b->post(fs);
         src = fs.req.win;
         if (ext > w) {  // keep the read-ahead (the round's window buffer is reused by the next round)
@@ -356,6 +359,7 @@ int64_t BatchBackend::first_hit(const ProbeInterval* iv, int64_t count, const st
         one.a = a2;
         iv = &one;
     }
+    bytes_read += probe_bytes(iv, count, B);
     FileScan& fs = scan_of(b, f);
     fs.req = Req{};
     fs.req.kind = Req::PROBE;
@@ -662,6 +666,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         for (const K1Group& g : groups)
             if (!files[(size_t)g.file].done) groups[kept++] = g;
         groups.resize(kept);
+        kept = 0;  // the tail lanes too (they have no abort word: they are short)
+        for (const K1Lane& ln : lanes)
+            if (!files[(size_t)ln.file].done) lanes[kept++] = ln;
+        lanes.resize(kept);
         int32_t dropped = 0;
         for (FileScan& fs : files)
             if (fs.done) fs.cancelled = true, ++dropped;
@@ -699,9 +707,12 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         int64_t max_len = 0;
         for (int32_t f = 0; f < NF; ++f) {
             FileScan& fs = files[(size_t)f];
+            // a file resolved before the launch has no speculation: no flags, no downloads
+            const uint32_t nflag = fs.cancelled ? 0u : (uint32_t)fs.nf;
             fe[f] = FlagEnt{S->src_weak.as<int32_t>() + fs.off_na, S->src_strong.as<uint8_t>() + fs.off_as, fs.d_weak,
-                            fs.d_strong, S->flags.as<uint8_t>() + fs.off_nf, (uint32_t)fs.nf, (uint32_t)fs.dl};
-            max_nf = std::max<uint32_t>(max_nf, (uint32_t)fs.nf);
+                            fs.d_strong, S->flags.as<uint8_t>() + fs.off_nf, nflag, (uint32_t)fs.dl};
+            max_nf = std::max<uint32_t>(max_nf, nflag);
+            if (fs.cancelled) continue;
             sc[nsc++] = CopyEnt{S->src_weak.as<uint8_t>() + 4 * fs.off_na, S->h_aw.as<uint8_t>() + 4 * fs.off_na,
                                 fs.na * 4};
             if (fs.dl > 0)
@@ -945,6 +956,15 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
 
     if (spec_launched) {
         if (hipEventQuery(c->ev_spec) == hipErrorNotReady) {  // every resolver finished first: stop it
+            // the batched K1's groups poll their own file's word (K1Group::abort), not the launch's: stop
+            // every file not cancelled yet (those resolved in the last round included)
+            for (int32_t f = 0; f < NF; ++f) {
+                FileScan& fs = files[(size_t)f];
+                if (fs.cancelled) continue;
+                fs.cancelled = true;
+                RSH_BHIP(hipStreamWriteValue32(st, S->file_abort + f, (uint32_t)gen, 0));
+            }
+            if (trace) fprintf(stderr, "[rsh-batch] scan done before the speculation landed: stopped\n");
             RSH_BHIP(hipStreamWriteValue32(st, c->abort_word, (uint32_t)gen, 0));
             RSH_BHIP(hipStreamWaitEvent(st, c->ev_spec, 0));
         }
@@ -970,6 +990,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             agg->host_md5_windows += s.host_md5_windows;
             agg->flushes += s.flushes;
             agg->table_ms += s.table_ms + fs.table.sort_ms;
+            agg->device_bytes += fs.be.bytes_read + ((spec_launched && b.landed.load() && !fs.cancelled) ? fs.n : 0);
+            agg->phase_matches += s.phase_matches;
         }
     }
     if (agg) {

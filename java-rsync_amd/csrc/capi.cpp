@@ -29,6 +29,8 @@ constexpr int kScanWindows = 2;  // hit windows per probe in the single-file sca
 constexpr int64_t kChainSteps = 2;  // ... after this many steps when the last event is a run of matches
 constexpr int64_t kDeferSteps = 4;
 constexpr double kDeferMs = 0.5;
+// ... or at once when the first kLeadWindows aligned source windows all carry chunk k's weak sum
+constexpr int64_t kLeadWindows = 32;
 
 // RSH_SCAN_TRACE=1: one stderr line per resolver round trip (diagnostics).
 struct CallTrace {
@@ -78,6 +80,7 @@ class HipBackend : public rsh::ScanBackend {
             return;
         }
         CallTrace tr("weak_many", count);
+        bytes_read += count * B_;
         rsh::GatherEnt* hp = pin<rsh::GatherEnt>(c_->h_pos, count);
         int32_t* ho = pin<int32_t>(c_->h_out, count);
         rsh::ScanFile* F = file();
@@ -90,6 +93,7 @@ class HipBackend : public rsh::ScanBackend {
     void bytes_many(const int64_t* pos, int64_t count, uint8_t* out) override {
         if (count <= 0) return;
         CallTrace tr("bytes_many", count);
+        bytes_read += count;
         rsh::GatherEnt* hp = pin<rsh::GatherEnt>(c_->h_pos, count);
         uint8_t* ho = pin<uint8_t>(c_->h_out, count);
         rsh::ScanFile* F = file();
@@ -125,6 +129,7 @@ class HipBackend : public rsh::ScanBackend {
         }
         uint8_t* hw = pin<uint8_t>(c_->h_win, w);
         if (err != hipSuccess) return;
+        bytes_read += w;
         ok(rsh::launch_copy_to_host(x_ + p, w, hw, c_->stream));
         ok(hipStreamSynchronize(c_->stream));
         rsh::HostMd5 h;
@@ -149,6 +154,7 @@ class HipBackend : public rsh::ScanBackend {
             iv = &one;
         }
         CallTrace tr("first_hit", count);
+        bytes_read += probe_bytes(iv, count, B_);
         rsh::ProbeTable tab = table;
         if (keys) {
             const uint32_t ns = pow2_at_least(2 * keys->size() + 2);
@@ -247,7 +253,71 @@ class HipBackend : public rsh::ScanBackend {
         return t_pos_;
     }
 
+    // ---- phase-shifted speculation (resolver.h ScanBackend::phase_hint / phase_sums): K1 over [s0, n) with
+    // the received header's B and dl, on the aux stream behind whatever runs there, one at a time ----
+    int64_t ph_launches = 0;
+    void phase_hint(int64_t s) override {
+        if (ph_s0_ >= 0 && s >= ph_s0_ && (s - ph_s0_) % B_ == 0) return;  // the current one covers s
+        const int64_t count = (n_ - s + B_ - 1) / B_;
+        if (count < kPhaseMinWindows || ph_launches >= kPhaseMaxLaunches || err != hipSuccess || !phase_on()) return;
+        phase_stop();  // one at another phase is dead work now
+        CallTrace tr("phase_spec", s);
+        ph_gen_ = ++c_->gen;
+        ok(hipStreamWaitEvent(c_->aux, c_->ev_in, 0));
+        ok(rsh::launch_block_sums(x_ + s, n_ - s, (uint32_t)B_, (uint32_t)count, (uint32_t)dl_, seed_word(seed_),
+                                  c_->ph_weak.as<int32_t>(), c_->ph_strong.as<uint8_t>(), c_->aux,
+                                  c_->abort_word + rsh_ctx::kPhaseWord, ph_gen_));
+        ok(hipMemcpyAsync(c_->h_pw.p, c_->ph_weak.p, (size_t)count * 4, hipMemcpyDeviceToHost, c_->aux));
+        if (dl_ > 0)
+            ok(hipMemcpyAsync(c_->h_ps.p, c_->ph_strong.p, (size_t)count * dl_, hipMemcpyDeviceToHost, c_->aux));
+        ok(hipEventRecord(c_->ev_phase, c_->aux));
+        if (err != hipSuccess) return;
+        ph_s0_ = s;
+        ph_count_ = count;
+        ph_landed_ = false;
+        ++ph_launches;
+    }
+    bool phase_sums(int64_t s, bool wait, rsh::PhaseView* v) override {
+        if (ph_s0_ < 0 || s < ph_s0_ || (s - ph_s0_) % B_ != 0 || err != hipSuccess) return false;
+        if (!ph_landed_) {
+            if (wait) {
+                CallTrace tr("phase_wait", s);
+                ok(hipEventSynchronize(c_->ev_phase));
+                ph_landed_ = err == hipSuccess;
+            } else {
+                ph_landed_ = hipEventQuery(c_->ev_phase) == hipSuccess;
+            }
+            if (!ph_landed_) return false;
+            bytes_read += n_ - ph_s0_;
+        }
+        v->s0 = ph_s0_;
+        v->count = ph_count_;
+        v->w = c_->h_pw.as<int32_t>();
+        v->st = c_->h_ps.as<uint8_t>();
+        return true;
+    }
+    // A phase speculation still running when the scan ends (or moves to another phase) is stopped; later
+    // work on the context stream waits until its waves have left.
+    void phase_stop() {
+        if (ph_s0_ >= 0 && !ph_landed_ && hipEventQuery(c_->ev_phase) == hipErrorNotReady) {
+            ok(hipStreamWriteValue32(c_->stream, c_->abort_word + rsh_ctx::kPhaseWord, (uint32_t)ph_gen_, 0));
+            ok(hipStreamWaitEvent(c_->stream, c_->ev_phase, 0));
+        }
+        ph_s0_ = -1;
+        ph_landed_ = false;
+    }
+    static bool phase_on() {  // A/B switch: RSH_SCAN_PHASE=0 turns the phase-shifted speculation off
+        static const bool v = !getenv("RSH_SCAN_PHASE") || atoi(getenv("RSH_SCAN_PHASE")) != 0;
+        return v;
+    }
+
   private:
+    static constexpr int64_t kPhaseMinWindows = 8;    // shorter remainders resolve faster on the generic path
+    static constexpr int64_t kPhaseMaxLaunches = 64;  // each covers the rest of the file
+    int64_t ph_s0_ = -1, ph_count_ = 0;
+    int ph_gen_ = 0;
+    bool ph_landed_ = false;
+
     template <class T>
     T* pin(PinnedBuf& b, int64_t count, int line = __builtin_LINE()) {
         ok(b.ensure((size_t)std::max<int64_t>(count, 1) * sizeof(T)), line);
@@ -340,6 +410,13 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     RSH_HIP(c->h_as.ensure((size_t)na * dl + 1));
     RSH_HIP(c->h_fl.ensure((size_t)nf + 1));
     RSH_HIP(c->haw.ensure((size_t)na * 4));
+    RSH_HIP(c->ph_weak.ensure((size_t)na * 4));
+    RSH_HIP(c->ph_strong.ensure((size_t)na * dl + 1));
+    RSH_HIP(c->h_pw.ensure((size_t)na * 4));
+    RSH_HIP(c->h_ps.ensure((size_t)na * dl + 1));
+    const int64_t nlead = std::min<int64_t>(kLeadWindows, nf);
+    const size_t lead_ents_at = ((size_t)(nlead + 1) * 4 + 63) & ~(size_t)63;
+    RSH_HIP(c->h_lead.ensure(lead_ents_at + (size_t)(nlead + 1) * sizeof(rsh::GatherEnt) + sizeof(rsh::ScanFile)));
 
     RSH_HIP(hipEventRecord(c->ev_in, c->stream));  // whatever produced the inputs on the caller's stream
     // (aux) the received table
@@ -362,9 +439,11 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     static const int diag = getenv("RSH_SCAN_DIAG") ? atoi(getenv("RSH_SCAN_DIAG")) : 0;  // A/B switches
     auto launch_spec = [&]() -> int {
         if (!download) RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
+        RSH_HIP(hipEventRecord(c->ev_k1a, c->aux));
         RSH_HIP(rsh::launch_block_sums(d_src, n, (uint32_t)B, (uint32_t)na, (uint32_t)dl, seed_word(seed),
                                        c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->aux,
                                        (diag & 2) ? nullptr : c->abort_word, gen));
+        RSH_HIP(hipEventRecord(c->ev_k1b, c->aux));
         RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
                                         (uint32_t)nf, (uint32_t)dl, c->flags.as<uint8_t>(), c->aux));
         RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)na * 4, hipMemcpyDeviceToHost, c->aux));
@@ -389,6 +468,20 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     const int64_t w0 = std::min<int64_t>(B, n);
     RSH_HIP(c->h_win0.ensure((size_t)w0 + 16));
     RSH_HIP(rsh::launch_copy_to_host(d_src, w0, c->h_win0.as<uint8_t>(), c->stream));
+    // (stream) T(kB) of the first nlead aligned windows: when all of them carry chunk k's weak sum the
+    // source very likely continues as an aligned run of matches (an unchanged or appended file), and the
+    // speculation is launched at once instead of after a few head-mode steps
+    int32_t* lead_w = c->h_lead.as<int32_t>();
+    if (head && nlead > 0) {
+        auto* ents = reinterpret_cast<rsh::GatherEnt*>(c->h_lead.as<uint8_t>() + lead_ents_at);
+        auto* lf = reinterpret_cast<rsh::ScanFile*>(ents + nlead + 1);
+        *lf = rsh::ScanFile{};
+        lf->data = d_src;
+        lf->n = n;
+        lf->B = (uint32_t)B;
+        for (int64_t k = 0; k < nlead; ++k) ents[k] = rsh::GatherEnt{k * B, 0, 0};
+        RSH_HIP(rsh::launch_window_weak(lf, ents, (uint32_t)nlead, lead_w, c->stream));
+    }
 
     // (host) sort the table
     rsh::ChunkTable table;
@@ -420,6 +513,20 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         }
     } joiner{md5_0_thread};
 
+    // the chain evidence of the first aligned windows (see above): launch the speculation now and let the
+    // resolver wait for it rather than take head-mode steps beside it
+    bool spec_wait = false;
+    static const bool wait_on = !getenv("RSH_SCAN_WAIT") || atoi(getenv("RSH_SCAN_WAIT")) != 0;  // A/B
+    if (head && !spec_launched && nlead > 0) {
+        int64_t lead = 0;
+        while (lead < nlead && lead_w[lead] == host_weak[lead]) ++lead;
+        if (lead == nlead && (nlead >= kLeadWindows || nlead == nf)) {
+            const int rc = launch_spec();
+            if (rc != RSH_OK) return rc;
+            spec_launched = true;
+            spec_wait = wait_on;
+        }
+    }
     HipBackend be(c, d_src, n, table, d_weak, seed);
     be.table.slots = c->slots.as<unsigned long long>();
     be.table.mask = ns - 1;
@@ -453,9 +560,17 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                 spec_rc = launch_spec();
                 spec_launched = true;
                 if (spec_rc != RSH_OK) return true;
+                spec_wait = wait_on && chain;  // a run of matches: the speculation will carry the scan
             }
-            res->stats.head_steps++;
-            return false;
+            if (!spec_wait) {
+                res->stats.head_steps++;
+                return false;
+            }
+        }
+        if (spec_wait) {  // head-mode steps beside the launch would only slow it down
+            CallTrace tw("spec_wait", res->stats.head_steps);
+            landed = hipEventSynchronize(c->ev_spec) == hipSuccess;
+            return true;
         }
         landed = hipEventQuery(c->ev_spec) != hipErrorNotReady;
         if (!landed) res->stats.head_steps++;
@@ -463,6 +578,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     });
     if (spec_rc != RSH_OK) return spec_rc;
     if (be.err != hipSuccess) return RSH_E_DEVICE;
+    bool spec_read = false;  // the aligned speculation ran to completion (its bytes count as read)
     if (done && !spec_launched) {
         res->stats.speculation_aborted = 2;  // the scan ended in head mode before the speculation was needed
         res->stats.device_ms += ms_since(t0);
@@ -477,13 +593,21 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     } else {
         RSH_HIP(hipEventSynchronize(c->ev_spec));
         res->stats.device_ms += ms_since(t0);
+        spec_read = true;
         if (!done) {
             be.head = false;
             rsh::resolve_run(n, table, be, &rs, res, nullptr);
         }
     }
+    be.phase_stop();
     if (be.err != hipSuccess) return RSH_E_DEVICE;
     res->stats.table_ms += table.sort_ms;  // 0 when the scan never needed the sorted table
+    res->stats.device_bytes += be.bytes_read + (spec_read ? n : 0);
+    if (spec_read) {
+        float k1ms = 0.f;
+        if (hipEventElapsedTime(&k1ms, c->ev_k1a, c->ev_k1b) == hipSuccess) res->stats.spec_kernel_ms = k1ms;
+    }
+    res->stats.phase_launches += be.ph_launches;
     return RSH_OK;
 }
 
@@ -547,6 +671,8 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
         hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_tab, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_phase, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreate(&c->ev_k1a) != hipSuccess || hipEventCreate(&c->ev_k1b) != hipSuccess ||
         hipExtMallocWithFlags(reinterpret_cast<void**>(&c->abort_word), 256, hipDeviceMallocUncached) != hipSuccess ||
         hipMemset(c->abort_word, 0, 256) != hipSuccess) {  // generations start at 1
         delete c;

@@ -98,10 +98,14 @@ struct rsh_ctx {
     hipStream_t stream = nullptr;
     DevBuf data, weak, strong;                   // host-input staging
     DevBuf src_weak, src_strong, flags;          // aligned speculation over the source
+    DevBuf ph_weak, ph_strong;                   // phase-shifted speculation over [s0, n) (chains at kB + delta)
     DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw, partials, bucket;
     hipStream_t aux = nullptr;                   // table download, then the aligned speculation
-    hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr;
+    hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr, ev_phase = nullptr;
+    hipEvent_t ev_k1a = nullptr, ev_k1b = nullptr;  // timing: the aligned speculation's K1 (stats)
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
+    PinnedBuf h_pw, h_ps;  // the phase-shifted speculation's sums (host copies)
+    PinnedBuf h_lead;      // T(kB) of the first aligned windows (the speculation launch decision)
     // resolver round trips: the small kernels read their inputs from and write their outputs to pinned
     // host memory directly (no staging copies); the probe result and digest windows come back by copy
     PinnedBuf h_pos, h_out, h_iv, h_tiles, h_keys, h_first, h_win, h_ptiles;
@@ -111,23 +115,30 @@ struct rsh_ctx {
     PinnedBuf h_files;   // the scan's rsh::ScanFile (a batch of one for the probe / gather kernels)
     PinnedBuf h_stage;   // file ingest ring (ingest.cpp); never shared with the scan's buffers
     uint64_t first_used = 0;    // probe result slots handed out (see HipBackend::first_hit)
-    int* abort_word = nullptr;  // device, uncached: the speculation launch of generation g stops once it reads g
+    // device, uncached, 256 B: the speculation launch of generation g stops once abort_word[0] holds g;
+    // a phase-shifted speculation polls abort_word[kPhaseWord] (its own 64-B line)
+    int* abort_word = nullptr;
+    static constexpr int kPhaseWord = 16;
     int gen = 0;
     std::vector<rsh_event> last_ev;  // kept when the caller's event buffer was too small
     std::atomic<bool> busy{false};   // the staging buffers and last_ev serve one call at a time
     rsh::BatchState* batch = nullptr;  // buffers of the batched (multi-file) entry points, on first use
     ~rsh_ctx() {
         if (batch) rsh::destroy_batch_state(batch);
-        for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &slots, &dslots, &dkeys, &pos, &out,
-                          &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket})
+        for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &ph_weak, &ph_strong, &slots, &dslots,
+                          &dkeys, &pos, &out, &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket})
             b->release();
-        for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pos, &h_out, &h_iv, &h_tiles, &h_keys, &h_first,
-                             &h_win, &h_ptiles, &h_hit, &h_win0, &h_bucket, &h_files, &h_stage})
+        for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pw, &h_ps, &h_lead, &h_pos, &h_out, &h_iv,
+                             &h_tiles, &h_keys, &h_first, &h_win, &h_ptiles, &h_hit, &h_win0, &h_bucket, &h_files,
+                             &h_stage})
             b->release();
         if (abort_word) (void)hipFree(abort_word);
         if (ev_in) (void)hipEventDestroy(ev_in);
         if (ev_tab) (void)hipEventDestroy(ev_tab);
         if (ev_spec) (void)hipEventDestroy(ev_spec);
+        if (ev_phase) (void)hipEventDestroy(ev_phase);
+        if (ev_k1a) (void)hipEventDestroy(ev_k1a);
+        if (ev_k1b) (void)hipEventDestroy(ev_k1b);
         if (aux) (void)hipStreamDestroy(aux);
         if (stream) (void)hipStreamDestroy(stream);
     }

@@ -47,6 +47,7 @@ struct K1Lane {
     int32_t* weak;        // the file's output arrays
     uint8_t* strong;
     uint32_t B, dl, c_first, nchunks;
+    int32_t file = 0;     // index of its file in the planner's list (host bookkeeping only)
 };
 void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Group>* groups,
                            std::vector<K1Lane>* lanes, int* lane_align);

@@ -737,7 +737,11 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
     const bool deep = variant == 4 || variant == 6 || variant == 7 || variant == 9 || variant == 10 ||
                       variant == 11 || variant == 12 || variant == 14 || variant == 15 || variant == 16 ||
                       variant == 18 || variant == 21 || variant >= 50;  // D >= 3 variants need nst >= 2D = 6 (8 for D = 4)
-    if (variant >= 3 && (B % 128) == 0 && (B >> 7) >= (deep ? 8u : 4u) && (addr % 16) == 0) {
+    // RSH_K1_UNALIGNED=1 (diagnostic A/B, read per launch): the pipelined K1 also at addresses that are not
+    // 16-B aligned (its buffer loads then straddle 16-B boundaries)
+    const char* ua = getenv("RSH_K1_UNALIGNED");
+    const bool unaligned_ok = ua && atoi(ua) != 0;
+    if (variant >= 3 && (B % 128) == 0 && (B >> 7) >= (deep ? 8u : 4u) && ((addr % 16) == 0 || unaligned_ok)) {
         const uint32_t nfullc = (uint32_t)std::min<int64_t>(n / B, nchunks);  // chunks with L == B
         const uint32_t waves = nfullc / 64;
         const uint32_t nst = B >> 7;
@@ -1030,7 +1034,7 @@ void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Gr
                     K1Group{F.data + (size_t)c * F.B, F.weak + c, F.strong + (size_t)c * F.dl, F.B, F.dl, nullptr, f});
         }
         for (; c < F.nchunks; c += 64) {
-            lanes->push_back(K1Lane{F.data, F.n, F.weak, F.strong, F.B, F.dl, c, F.nchunks});
+            lanes->push_back(K1Lane{F.data, F.n, F.weak, F.strong, F.B, F.dl, c, F.nchunks, f});
             const int a = ((F.B % 16) == 0 && (addr % 16) == 0) ? 16 : ((F.B % 4) == 0 && (addr % 4) == 0) ? 4 : 1;
             *lane_align = std::min(*lane_align, a);
         }

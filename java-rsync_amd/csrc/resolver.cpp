@@ -250,6 +250,42 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
                 continue;
             }
         }
+        // (1') chain at any other phase, or aligned with pref != k: the window at s is matched against chunk
+        // pref exactly when its sums are pref's (T(s) == weak[pref] puts pref in the bucket, so closeIndexOf
+        // makes it the first candidate, Checksum.java:206-213, and its digest then decides, Sender.java:1265),
+        // and the match jumps a whole window (:1282), so the next window is s + w against pref + 1.
+        if (!md5c_valid && synced && pref < table.chunk_count) {
+            PhaseView pv;
+            bool have = false;
+            if (s % B == 0 && s / B < nal) {
+                pv.s0 = 0, pv.count = nal, pv.w = aw, pv.st = as;
+                have = true;
+            } else if (s % B != 0) {
+                const bool chain = !ev.empty() && ev.back().kind == RSH_EV_MATCH && ev.back().count >= 2 &&
+                                   ev.back().offset + ev.back().length == s;
+                have = be.phase_sums(s, chain, &pv);
+            }
+            if (have) {
+                int64_t k = (s - pv.s0) / B, c = pref, p = s;
+                const int64_t C = table.chunk_count;
+                while (k < pv.count && c < C && p <= last && pv.w[k] == table.weak[c] &&
+                       (dl <= 0 || memcmp(pv.st + k * dl, table.strong + c * dl, (size_t)dl) == 0)) {
+                    p += wl(p);
+                    ++k;
+                    ++c;
+                }
+                if (c > pref) {
+                    emit_lit(m, s - m);
+                    emit_match(s, p - s, pref, (int32_t)(c - pref));
+                    st.phase_matches += c - pref;
+                    s = p;
+                    m = p;
+                    pref = (int32_t)c;
+                    anchor = s;
+                    continue;
+                }
+            }
+        }
         // (2) next candidate event in [s, stop]: the first flush point bounds the state's validity.
         const int64_t f = (m + 10 * B <= n) ? m + 9 * B : std::numeric_limits<int64_t>::max();
         const int64_t stop = std::min(f, last);
@@ -342,6 +378,7 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
                 anchor = s;
                 md5c_valid = false;
                 dkeys_ready = false;
+                if (s % B != 0 && s <= last) be.phase_hint(s);
                 continue;
             }
             if (p == f) flush(p, R);

@@ -90,10 +90,29 @@ struct ProbeInterval {
     uint32_t e_lo, e_hi;
 };
 
+// Speculated sums of the source windows at s0 + kB, k in [0, count) (a phase-shifted speculation: the
+// source's own block sums from s0 on, with the received header's B and dl).  w[k] = T(s0 + kB) over
+// min(B, n - s0 - kB) bytes, st + k * dl = that window's MD5 || seed, cut / zero-padded to dl bytes.
+struct PhaseView {
+    int64_t s0 = 0, count = 0;
+    const int32_t* w = nullptr;
+    const uint8_t* st = nullptr;
+};
+
 // Device (or test) services used by the resolver.  Positions are source file offsets.
 class ScanBackend {
   public:
     virtual ~ScanBackend() {}
+    // Shifted chains (Sender.java:1282-1287: after a match the scan jumps a whole window, so consecutive
+    // matches chain at any phase, not only at kB).  phase_hint(s): a match just left the scan synced at a
+    // non-aligned s; the backend may start a speculation over [s, n).  phase_sums(s, wait, v): sums of a
+    // speculation whose windows include s, if one has landed (wait: block until an in-flight one that
+    // covers s lands).  false = none; the resolver then takes the generic path (same answer).
+    virtual void phase_hint(int64_t s) { (void)s; }
+    virtual bool phase_sums(int64_t s, bool wait, PhaseView* v) {
+        (void)s, (void)wait, (void)v;
+        return false;
+    }
     // Aligned speculation over the source: window k = [kB, min(kB + B, n)), k < aligned_count().
     virtual int64_t aligned_count() = 0;
     virtual const int32_t* aligned_weak() = 0;
@@ -107,6 +126,13 @@ class ScanBackend {
     virtual int64_t first_hit(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) = 0;
     // Upper bound on the flush intervals one batched probe may cover.
     virtual int64_t max_batch() { return 4096; }
+    // Source bytes the backend's device work read for this scan (rsh_scan_stats::device_bytes).
+    int64_t bytes_read = 0;
+    static int64_t probe_bytes(const ProbeInterval* iv, int64_t count, int64_t B) {
+        int64_t b = 0;
+        for (int64_t i = 0; i < count; ++i) b += (iv[i].b - iv[i].a) + B - 1;
+        return b;
+    }
 
     int32_t weak_at(int64_t p) {
         int32_t r;

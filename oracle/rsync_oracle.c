@@ -334,6 +334,19 @@ static int sender_match(const uint8_t* x, int64_t N, const orc_header* h, const 
         t.sorted[i].idx = i;
     }
     qsort(t.sorted, (size_t)t.n, sizeof(kv), kv_cmp);
+    /* Lookup accelerator only (the Java HashMap lookup is O(1) as well): a filter of hashed keys; a clear bit proves the bucket empty, a set bit falls through to the exact binary search. */
+    int fbits = 12; /* >= 64 filter bits per key, at most 2^24 */
+    while (fbits < 24 && ((int64_t)1 << fbits) < 64 * (int64_t)t.n) fbits++;
+    const int fshift = 32 - fbits;
+    uint64_t* filt = (uint64_t*)calloc((size_t)1 << (fbits - 6), sizeof(uint64_t));
+    if (!filt) {
+        free(t.sorted);
+        return -1;
+    }
+    for (int32_t i = 0; i < t.n; i++) {
+        const uint32_t hk = ((uint32_t)weak[i] * 0x9E3779B1u) >> fshift;
+        filt[hk >> 6] |= 1ull << (hk & 63);
+    }
 
     orc_md5_ctx file_digest, chunk_digest;
     orc_md5_init(&file_digest);
@@ -349,13 +362,15 @@ static int sender_match(const uint8_t* x, int64_t N, const orc_header* h, const 
     uint8_t dig[16];
     if (!md5c) {
         free(t.sorted);
+        free(filt);
         return -1;
     }
 
     while (wl(start, B, N) >= S) {
         int64_t w = wl(start, B, N);
-        int32_t lo, hi;
-        bucket_of(&t, rolling, &lo, &hi);
+        int32_t lo = 0, hi = 0;
+        const uint32_t hk = ((uint32_t)rolling * 0x9E3779B1u) >> fshift;
+        if (filt[hk >> 6] >> (hk & 63) & 1) bucket_of(&t, rolling, &lo, &hi);
         int32_t size = hi - lo;
         if (size > 0) {
             const kv* bucket = t.sorted + lo;
@@ -427,10 +442,12 @@ static int sender_match(const uint8_t* x, int64_t N, const orc_header* h, const 
     r->matched = size_match;
     free(t.sorted);
     free(md5c);
+    free(filt);
     return 0;
 oom:
     free(t.sorted);
     free(md5c);
+    free(filt);
     return -1;
 }
 

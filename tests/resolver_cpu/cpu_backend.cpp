@@ -3,6 +3,7 @@
 // a GPU.  Never linked into librsynchip.so: the product's backend is the HIP one in capi.cpp.
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "hit_cache.h"
@@ -133,7 +134,45 @@ class CpuBackend : public rsh::ScanBackend {
         return -1;
     }
 
+    // Phase-shifted speculation (as the HIP backend's): phase_hint computes the sums of every window from
+    // s on; phase_sums reports them "in flight" for `phase_lag` non-waiting queries after each hint.
+    bool use_phase = false;
+    int64_t phase_lag = 0, phase_hints = 0, phase_answers = 0;
+    void phase_hint(int64_t s) override {
+        if (!use_phase) return;
+        if (ph_s0_ >= 0 && s >= ph_s0_ && (s - ph_s0_) % B_ == 0) return;
+        ++phase_hints;
+        ph_s0_ = s;
+        const int64_t count = (n_ - s + B_ - 1) / B_;
+        pw_.assign((size_t)count, 0);
+        ps_.assign((size_t)(count * dl_ + 1), 0);
+        for (int64_t k = 0; k < count; ++k) {
+            pw_[(size_t)k] = weak1(s + k * B_);
+            uint8_t d[16];
+            md5_at(s + k * B_, d);
+            memcpy(&ps_[(size_t)(k * dl_)], d, (size_t)std::min(dl_, 16));
+        }
+        ph_wait_ = phase_lag;
+    }
+    bool phase_sums(int64_t s, bool wait, rsh::PhaseView* v) override {
+        if (!use_phase || ph_s0_ < 0 || s < ph_s0_ || (s - ph_s0_) % B_ != 0) return false;
+        if (!wait && ph_wait_ > 0) {
+            --ph_wait_;
+            return false;
+        }
+        ph_wait_ = 0;
+        ++phase_answers;
+        v->s0 = ph_s0_;
+        v->count = (int64_t)pw_.size();
+        v->w = pw_.data();
+        v->st = ps_.data();
+        return true;
+    }
+
   private:
+    int64_t ph_s0_ = -1, ph_wait_ = 0;
+    std::vector<int32_t> pw_;
+    std::vector<uint8_t> ps_;
     int32_t last_key_ = 0;
     int64_t wl(int64_t p) const { return n_ - p < B_ ? n_ - p : B_; }
     const uint8_t* x_;
@@ -153,6 +192,15 @@ class CpuBackend : public rsh::ScanBackend {
 // aligned speculation (as while the device kernel is still running), then resumes with it.
 static int g_use_cache = 0;
 static int64_t g_cache_answers = 0;
+static int64_t g_phase = -1;  // < 0: no phase speculation; else its lag (non-waiting queries before it "lands")
+static int64_t g_phase_answers = 0;
+// Phase-shifted speculation mode; returns the number of resolver steps it answered since the last call.
+extern "C" int64_t rtest_phase(int64_t lag) {
+    g_phase = lag;
+    const int64_t a = g_phase_answers;
+    g_phase_answers = 0;
+    return a;
+}
 // 1: single-interval probes go through rsh::HitCache (as in the HIP backends); returns the number of
 // probes the cache answered since the last call.
 extern "C" int64_t rtest_hit_cache(int on) {
@@ -175,6 +223,8 @@ extern "C" int rtest_scan_staged(const uint8_t* src, int64_t n, const rsh_header
     if (head_steps < 0) t.build();  // staged runs leave the table lazy (linear-scan lookups first)
     CpuBackend be(src, n, t, seed);
     be.use_cache = g_use_cache != 0;
+    be.use_phase = g_phase >= 0;
+    be.phase_lag = g_phase < 0 ? 0 : g_phase;
     rsh::ResolveResult r;
     if (head_steps < 0) {
         rsh::resolve_scan(n, t, be, &r);
@@ -187,6 +237,7 @@ extern "C" int rtest_scan_staged(const uint8_t* src, int64_t n, const rsh_header
         if (!done) rsh::resolve_run(n, t, be, &st, &r, nullptr);
     }
     g_cache_answers += be.cache_answers;
+    g_phase_answers += be.phase_answers;
     *n_ev = (int64_t)r.ev.size();
     *lit = r.literal;
     *mat = r.matched;

@@ -29,7 +29,7 @@ def test_library_exports_every_symbol():
     L = ctypes.CDLL(R.LIB_PATH)
     for name in R.EXPORTS:
         assert hasattr(L, name), name
-    assert R.lib().rsh_abi_version() == 1
+    assert R.lib().rsh_abi_version() == 2
 
 
 @pytest.mark.parametrize("n", [1, 511, 512, 557, 1000, 64 << 20, 128 << 20, 4 << 30, 16 << 30, 64 << 30, (1 << 40) + 3])

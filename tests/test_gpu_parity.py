@@ -151,6 +151,43 @@ def test_sender_digest_longer_than_md5(ctx, pad):
                                   ow.ctypes.data, os_.ctypes.data) == R.RSH_E_INVAL
 
 
+@pytest.mark.parametrize("unaligned", ["0", "1"])
+def test_k1_unaligned_base(ctx, unaligned, monkeypatch):
+    """K1 over a basis that starts at every offset 0..15 from a 16-B boundary (the phase-shifted speculation
+    runs K1 over src + s for any s).  RSH_K1_UNALIGNED=1 (diagnostic) keeps the pipelined buffer-load kernel at
+    such addresses; by default they take the per-lane kernel.  Bit-exact against the oracle either way."""
+    import ctypes
+    monkeypatch.setenv("RSH_K1_UNALIGNED", unaligned)
+    B, dl = 2048, 4
+    n = 200 * B + 77
+    d = ctx.alloc(n + 64)
+    R.lib().rsh_fill_splitmix_device(ctx.handle, d.ptr, n + 64, 0xA11, 0)
+    ctx.sync()
+    host = d.download()
+    seed = np.frombuffer(SEED, np.uint8).copy()
+    for off in range(16):
+        h = R.header_make(B, dl, n)
+        d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
+        assert R.lib().rsh_block_sums_device(ctx.handle, ctypes.c_void_p(d.ptr.value + off), n, ctypes.byref(h), seed.ctypes.data,
+                                             d_w.ptr, d_s.ptr) == 0
+        ctx.sync()
+        ow, os_ = O.generator(host[off:off + n], O.header(B, dl, n), SEED)
+        assert np.array_equal(d_w.download(dtype=np.int32), ow), f"weak, offset {off}"
+        assert np.array_equal(d_s.download(), os_), f"strong, offset {off}"
+
+
+def test_sender_phase_shift_chains(ctx):
+    """Inserts and a delete of odd sizes in a 512 MiB source (B = 65536, 8192 chunks): after each the matches
+    continue at a new phase kB + delta (Sender.java:1282-1287).  The phase-shifted speculation carries them
+    (no host digest per match) and the events equal the oracle's."""
+    B, dl = 65536, 4
+    basis = O.splitmix(512 << 20, 0x5EED5EED000000F5)
+    a, b = 64 << 20, 300 << 20
+    src = np.concatenate([basis[:a], O.splitmix(1000, 1), basis[a:b], basis[b + 3:], O.splitmix(5, 2)])
+    st = _sender_both(ctx, basis.tobytes(), src.tobytes(), B, dl)
+    assert st["phase_launches"] >= 1 and st["phase_matches"] > 6000 and st["host_md5_windows"] < 100, st
+
+
 def test_device_fill_matches_oracle(ctx):
     n = (1 << 20) + 13
     d = ctx.alloc(n)

@@ -223,3 +223,39 @@ def test_resolver_digest_longer_than_md5(pad):
     assert omat >= 7 * B
     if pad == "garbage":
         assert omat < len(basis) - 20 * B
+
+
+@pytest.mark.parametrize("seed_i", range(6))
+def test_resolver_phase_chains(seed_i):
+    """Shifted chains (Sender.java:1282-1287: after a match the scan jumps a whole window, so runs of
+    matches continue at any phase): with a phase-shifted speculation over [s, n) after each non-aligned
+    match (ScanBackend::phase_hint / phase_sums, as the HIP backend launches it), inserts, deletes and
+    moved blocks give the oracle's events; the speculation answers while in flight or landed (lag)."""
+    L = rlib()
+    L.rtest_phase.argtypes = [ctypes.c_int64]
+    L.rtest_phase.restype = ctypes.c_int64
+    rng = random.Random(7000 + seed_i)
+    answered = 0
+    try:
+        for i in range(10):
+            L.rtest_phase(rng.choice([0, 1, 3]))
+            B = rng.choice([512, 576, 1024])
+            nb = rng.randrange(30 * B, 90 * B)
+            key = rng.randrange(1 << 62)
+            basis = O.splitmix(nb, key).tobytes()
+            src = basis
+            for _ in range(rng.randrange(1, 4)):  # a few shifts: inserts / deletes of odd sizes
+                a = rng.randrange(len(src))
+                if rng.random() < 0.5:
+                    src = src[:a] + O.splitmix(rng.randrange(1, 3 * B), key ^ a).tobytes() + src[a:]
+                else:
+                    src = src[:a] + src[a + rng.randrange(1, 2 * B):]
+            if i % 3 == 2:  # a block moved elsewhere (aligned chain with pref != k after it)
+                k = rng.randrange(1, nb // B - 2)
+                src = src[:B] + basis[k * B:(k + 4) * B] + src[B:]
+            check_case(basis, src, B, rng.choice([2, 3, 4, 16]), bytes([1, 2, 3, 4]),
+                       head_steps=rng.choice([-1, -1, 2, 9]))
+            answered += L.rtest_phase(-1)
+    finally:
+        L.rtest_phase(-1)
+    assert answered > 0
