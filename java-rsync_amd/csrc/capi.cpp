@@ -31,6 +31,8 @@ constexpr int64_t kDeferSteps = 4;
 constexpr double kDeferMs = 0.5;
 // ... or at once when the first kLeadWindows aligned source windows all carry chunk k's weak sum
 constexpr int64_t kLeadWindows = 32;
+// ... over the windows up to the last of kSampleWindows evenly spaced samples that still carries its chunk's sum
+constexpr int64_t kSampleWindows = 1024;
 
 // RSH_SCAN_TRACE=1: one stderr line per resolver round trip (diagnostics).
 struct CallTrace {
@@ -64,6 +66,9 @@ class HipBackend : public rsh::ScanBackend {
     // data, batched probes stay short, and the probe kernel's per-block anchors T(kB) come from c_->haw,
     // filled on demand for the blocks a probe touches.
     bool head = false;
+    // the speculation covers windows [0, na) only (a prefix of the source's na_all): the probe's block anchors
+    // beyond it come from c_->haw on demand, as in head mode
+    bool partial = false;
     std::vector<uint8_t> haw_ready;
     std::function<void(uint8_t*)> md5_0;  // digest of window 0 (joins its host thread)
 
@@ -192,7 +197,7 @@ class HipBackend : public rsh::ScanBackend {
             hiv[i] = rsh::ProbeIv{iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo & 0xFFFFu, iv[i].e_hi & 0xFFFFu, 0, 0};
         if (!tiles_.empty()) memcpy(ht, tiles_.data(), tiles_.size() * sizeof(rsh::ProbeTile));
         if (!ptiles_.empty()) memcpy(hpt, ptiles_.data(), ptiles_.size() * sizeof(rsh::PartialTile));
-        F->aligned_weak = head ? c_->haw.as<int32_t>() : c_->src_weak.as<int32_t>();
+        F->aligned_weak = (head || partial) ? c_->haw.as<int32_t>() : c_->src_weak.as<int32_t>();
         F->slots = tab.slots;
         F->mask = tab.mask;
         F->out = d_first;
@@ -201,7 +206,7 @@ class HipBackend : public rsh::ScanBackend {
         F->bucket = c_->bucket.as<int32_t>();
         F->hit = hh;
         F->nwin = kScanWindows;
-        if (head) {  // anchors T(kB) for the blocks these tiles sit in
+        if (head || partial) {  // anchors T(kB) for the blocks these tiles sit in
             anchors_.clear();
             for (const rsh::ProbeTile& t : tiles_) {
                 const int64_t k = t.q0 / B_;
@@ -347,7 +352,7 @@ class HipBackend : public rsh::ScanBackend {
         F->data = x_;
         F->n = n_;
         F->B = (uint32_t)B_;
-        F->aligned_weak = head ? c_->haw.as<int32_t>() : c_->src_weak.as<int32_t>();
+        F->aligned_weak = (head || partial) ? c_->haw.as<int32_t>() : c_->src_weak.as<int32_t>();
         F->table_weak = d_table_weak_;
         F->C = t_.chunk_count;
         return F;
@@ -414,9 +419,16 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     RSH_HIP(c->ph_strong.ensure((size_t)na * dl + 1));
     RSH_HIP(c->h_pw.ensure((size_t)na * 4));
     RSH_HIP(c->h_ps.ensure((size_t)na * dl + 1));
+    // sample windows for the launch decision: the first nlead, then one every `stride` windows
     const int64_t nlead = std::min<int64_t>(kLeadWindows, nf);
-    const size_t lead_ents_at = ((size_t)(nlead + 1) * 4 + 63) & ~(size_t)63;
-    RSH_HIP(c->h_lead.ensure(lead_ents_at + (size_t)(nlead + 1) * sizeof(rsh::GatherEnt) + sizeof(rsh::ScanFile)));
+    const int64_t stride = std::max<int64_t>(1, (nf + kSampleWindows - 1) / kSampleWindows);
+    std::vector<int64_t> samp;
+    for (int64_t k = 0; k < nlead; ++k) samp.push_back(k);
+    for (int64_t k = stride; k < nf; k += stride)
+        if (k >= nlead) samp.push_back(k);
+    const int64_t nsamp = (int64_t)samp.size();
+    const size_t lead_ents_at = ((size_t)(nsamp + 1) * 4 + 63) & ~(size_t)63;
+    RSH_HIP(c->h_lead.ensure(lead_ents_at + (size_t)(nsamp + 1) * sizeof(rsh::GatherEnt) + sizeof(rsh::ScanFile)));
 
     RSH_HIP(hipEventRecord(c->ev_in, c->stream));  // whatever produced the inputs on the caller's stream
     // (aux) the received table
@@ -437,19 +449,22 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // speculation takes ~0.16 ms instead of tens of microseconds).
     const int gen = ++c->gen;
     static const int diag = getenv("RSH_SCAN_DIAG") ? atoi(getenv("RSH_SCAN_DIAG")) : 0;  // A/B switches
+    int64_t spec_na = na;  // windows the speculation covers: all, or a prefix (sampled launch decision)
     auto launch_spec = [&]() -> int {
+        const int64_t sn = std::min<int64_t>(n, spec_na * B);  // bytes: whole windows, or to the end
+        const int64_t snf = std::min<int64_t>(spec_na, C);
         if (!download) RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
         RSH_HIP(hipEventRecord(c->ev_k1a, c->aux));
-        RSH_HIP(rsh::launch_block_sums(d_src, n, (uint32_t)B, (uint32_t)na, (uint32_t)dl, seed_word(seed),
+        RSH_HIP(rsh::launch_block_sums(d_src, sn, (uint32_t)B, (uint32_t)spec_na, (uint32_t)dl, seed_word(seed),
                                        c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->aux,
                                        (diag & 2) ? nullptr : c->abort_word, gen));
         RSH_HIP(hipEventRecord(c->ev_k1b, c->aux));
         RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
-                                        (uint32_t)nf, (uint32_t)dl, c->flags.as<uint8_t>(), c->aux));
-        RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)na * 4, hipMemcpyDeviceToHost, c->aux));
+                                        (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(), c->aux));
+        RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)spec_na * 4, hipMemcpyDeviceToHost, c->aux));
         if (dl > 0)
-            RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)na * dl, hipMemcpyDeviceToHost, c->aux));
-        if (nf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)nf, hipMemcpyDeviceToHost, c->aux));
+            RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)spec_na * dl, hipMemcpyDeviceToHost, c->aux));
+        if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, c->aux));
         RSH_HIP(hipEventRecord(c->ev_spec, c->aux));
         return RSH_OK;
     };
@@ -474,13 +489,13 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     int32_t* lead_w = c->h_lead.as<int32_t>();
     if (head && nlead > 0) {
         auto* ents = reinterpret_cast<rsh::GatherEnt*>(c->h_lead.as<uint8_t>() + lead_ents_at);
-        auto* lf = reinterpret_cast<rsh::ScanFile*>(ents + nlead + 1);
+        auto* lf = reinterpret_cast<rsh::ScanFile*>(ents + nsamp + 1);
         *lf = rsh::ScanFile{};
         lf->data = d_src;
         lf->n = n;
         lf->B = (uint32_t)B;
-        for (int64_t k = 0; k < nlead; ++k) ents[k] = rsh::GatherEnt{k * B, 0, 0};
-        RSH_HIP(rsh::launch_window_weak(lf, ents, (uint32_t)nlead, lead_w, c->stream));
+        for (int64_t i = 0; i < nsamp; ++i) ents[i] = rsh::GatherEnt{samp[(size_t)i] * B, 0, 0};
+        RSH_HIP(rsh::launch_window_weak(lf, ents, (uint32_t)nsamp, lead_w, c->stream));
     }
 
     // (host) sort the table
@@ -517,10 +532,19 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // resolver wait for it rather than take head-mode steps beside it
     bool spec_wait = false;
     static const bool wait_on = !getenv("RSH_SCAN_WAIT") || atoi(getenv("RSH_SCAN_WAIT")) != 0;  // A/B
+    static const bool sample_on = !getenv("RSH_SCAN_SAMPLE") || atoi(getenv("RSH_SCAN_SAMPLE")) != 0;  // A/B
     if (head && !spec_launched && nlead > 0) {
         int64_t lead = 0;
         while (lead < nlead && lead_w[lead] == host_weak[lead]) ++lead;
         if (lead == nlead && (nlead >= kLeadWindows || nlead == nf)) {
+            // the run may stop somewhere (an insert shifts everything after it to another phase, where the
+            // phase-shifted speculation takes over): cover only up to the last sample that still matches
+            // (plus one stride); a single K1 over the rest would compute sums nothing reads
+            int64_t lastk = nlead - 1;
+            for (int64_t i = nlead; i < nsamp; ++i)
+                if (lead_w[i] == host_weak[samp[(size_t)i]]) lastk = samp[(size_t)i];
+            const bool all = lastk + stride >= nf || !sample_on;
+            spec_na = all ? na : std::min<int64_t>(na, lastk + stride + 1);
             const int rc = launch_spec();
             if (rc != RSH_OK) return rc;
             spec_launched = true;
@@ -530,7 +554,8 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     HipBackend be(c, d_src, n, table, d_weak, seed);
     be.table.slots = c->slots.as<unsigned long long>();
     be.table.mask = ns - 1;
-    be.na = na;
+    be.na = spec_na;
+    be.partial = spec_na < na;
     be.aw = c->h_aw.as<int32_t>();
     be.as = c->h_as.as<uint8_t>();
     be.fl = c->h_fl.as<uint8_t>();
@@ -596,13 +621,17 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         spec_read = true;
         if (!done) {
             be.head = false;
+            if (be.partial) {  // the prefix's anchors from the speculation, the rest on demand
+                RSH_HIP(hipMemcpyAsync(c->haw.p, c->src_weak.p, (size_t)spec_na * 4, hipMemcpyDeviceToDevice, c->stream));
+                std::fill(be.haw_ready.begin(), be.haw_ready.begin() + spec_na, (uint8_t)1);
+            }
             rsh::resolve_run(n, table, be, &rs, res, nullptr);
         }
     }
     be.phase_stop();
     if (be.err != hipSuccess) return RSH_E_DEVICE;
     res->stats.table_ms += table.sort_ms;  // 0 when the scan never needed the sorted table
-    res->stats.device_bytes += be.bytes_read + (spec_read ? n : 0);
+    res->stats.device_bytes += be.bytes_read + (spec_read ? std::min<int64_t>(n, spec_na * B) : 0);
     if (spec_read) {
         float k1ms = 0.f;
         if (hipEventElapsedTime(&k1ms, c->ev_k1a, c->ev_k1b) == hipSuccess) res->stats.spec_kernel_ms = k1ms;

@@ -592,6 +592,9 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
         stage(std::integral_constant<int, 0>{}, s, true, true);
         stage(std::integral_constant<int, 1>{}, s + 1, true, true);
         if constexpr (ABORT) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(flag));
+        else if constexpr (MODE == 5) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // A/B: the drain alone
+        else if constexpr (MODE == 6) asm volatile("s_sleep 1" ::: "memory");            // A/B: a short sleep
+        else if constexpr (MODE == 7) asm volatile("s_sleep 4" ::: "memory");
     }
     if constexpr (ABORT) {
         if (flag == abort_gen) return;
@@ -737,10 +740,13 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
     const bool deep = variant == 4 || variant == 6 || variant == 7 || variant == 9 || variant == 10 ||
                       variant == 11 || variant == 12 || variant == 14 || variant == 15 || variant == 16 ||
                       variant == 18 || variant == 21 || variant >= 50;  // D >= 3 variants need nst >= 2D = 6 (8 for D = 4)
-    // RSH_K1_UNALIGNED=1 (diagnostic A/B, read per launch): the pipelined K1 also at addresses that are not
-    // 16-B aligned (its buffer loads then straddle 16-B boundaries)
+    // The pipelined K1 also runs at base addresses that are not 16-B aligned (the phase-shifted speculation
+    // starts at src + s for any s): its dwordx4 buffer loads then straddle 16-B boundaries, which gfx950
+    // serves in its unaligned access mode (bit-exact against the oracle at offsets 0..15,
+    // test_k1_unaligned_base).  RSH_K1_UNALIGNED=0 (A/B, read per launch) sends such bases to the per-lane
+    // kernel instead.
     const char* ua = getenv("RSH_K1_UNALIGNED");
-    const bool unaligned_ok = ua && atoi(ua) != 0;
+    const bool unaligned_ok = !ua || atoi(ua) != 0;
     if (variant >= 3 && (B % 128) == 0 && (B >> 7) >= (deep ? 8u : 4u) && ((addr % 16) == 0 || unaligned_ok)) {
         const uint32_t nfullc = (uint32_t)std::min<int64_t>(n / B, nchunks);  // chunks with L == B
         const uint32_t waves = nfullc / 64;
@@ -935,6 +941,18 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, false, 0>), dim3(waves), dim3(64), 2 * wave_lds, s,
                                        d_data, B, dl, seed_word, d_weak, d_strong);
                     break;
+                case 56:  // A/B: the plain kernel with s_sleep 1 / s_sleep 4 per 2 stages
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 6>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 57:
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 7>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 55:  // A/B: the plain kernel with the abortable kernel's lgkmcnt(0) drain per 2 stages
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 5>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
                 case 26:  // diagnostics (wrong results): synthetic data, no weak-sum MFMAs
                     hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 3, false, true, true, false, 2, true>),
                                        dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
@@ -1042,10 +1060,34 @@ void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Gr
 }
 
 
+// A word no launch ever writes: non-abortable K1 launches run the abortable instantiation polling it with
+// generation -1 (never stored).  Measured on the MI355X pool (round 2, kbench 16 GiB at B = 128 KiB, same
+// process, same buffer): the plain instantiation 4.07-4.57 ms, the abortable one 2.99-3.10 ms (the plain one
+// with only the abortable loop's lgkmcnt(0) drain: 4.38 ms); round 1's boxes ran both at ~3.0 ms.  The word
+// must be uncached device memory like the contexts' abort words: polling a __device__ global instead (L2,
+// one line for every wave) made the launch 27.9 ms.  RSH_K1_PLAIN=1 (A/B) launches the plain one.
+static const int* never_word() {
+    static int* ptr[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    if (!ptr[dev]) {  // one 256-B uncached word per device for the process's lifetime
+        int* p = nullptr;
+        if (hipExtMallocWithFlags(reinterpret_cast<void**>(&p), 256, hipDeviceMallocUncached) != hipSuccess) return nullptr;
+        if (hipMemset(p, 0, 256) != hipSuccess) return nullptr;
+        ptr[dev] = p;
+    }
+    return ptr[dev];
+}
+static bool plain_k1() {
+    static const bool v = getenv("RSH_K1_PLAIN") && atoi(getenv("RSH_K1_PLAIN")) != 0;
+    return v;
+}
+
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
                                    int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag,
                                    int abort_gen) {
     const size_t lb = 2 * 64 * 9 * sizeof(uint4);
+    if (!abort_flag && !plain_k1() && (abort_flag = never_word()) != nullptr) abort_gen = -1;  // see never_word
     if (ngroups > 0) {
         if (abort_flag && batch_pin())
             hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true, 0, true>), dim3(ngroups), dim3(64), lb, s,
@@ -1076,6 +1118,7 @@ hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint3
                              const int* abort_flag, int abort_gen) {
     // RSH_K1_VARIANT (diagnostic A/B, off by default) replaces the production variant for non-abortable launches
     static const int forced = getenv("RSH_K1_VARIANT") ? atoi(getenv("RSH_K1_VARIANT")) : -1;
+    if (!abort_flag && forced < 0 && !plain_k1() && (abort_flag = never_word()) != nullptr) abort_gen = -1;
     return launch_block_sums_variant(abort_flag ? -1 : forced, d_data, n, B, nchunks, dl, seed_word, d_weak, d_strong, s, abort_flag,
                                      abort_gen);
 }

@@ -117,12 +117,32 @@ def build(force=False):
     subprocess.run(cmd, check=True)
 
 
+def stale_sources():
+    """Sources that changed since librsynchip.so was built (the build's sha256 stamp, lib/librsynchip.srchash):
+    a stale library must never be the one a test or the bench measures.  [] when the stamp or the sources are
+    absent (a binary-only install)."""
+    import hashlib
+    stamp = os.path.join(HERE, "lib", "librsynchip.srchash")
+    if not os.path.exists(stamp):
+        return []
+    out = []
+    for line in open(stamp):
+        digest, _, rel = line.strip().partition("  ")
+        path = os.path.join(HERE, rel)
+        if os.path.exists(path) and hashlib.sha256(open(path, "rb").read()).hexdigest() != digest:
+            out.append(rel)
+    return out
+
+
 def lib():
     global _LIB
     if _LIB is not None:
         return _LIB
     if not os.path.exists(LIB_PATH):
         raise DeviceError(f"{LIB_PATH} missing: run rsync_hip.build() (or __graft_entry__.build())")
+    stale = stale_sources()
+    if stale:
+        raise DeviceError(f"{LIB_PATH} was built from other sources than {', '.join(stale)}: rebuild it")
     L = ctypes.CDLL(LIB_PATH)
     P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     HP = ctypes.POINTER(Header)

@@ -1,6 +1,8 @@
 // kbench -- developer micro-benchmark of the block-sum kernel variants (device.hip) on one GPU.
 // Times each variant with hipEvents on its stream and checks every variant's output against
 // variant 0 bit for bit.  usage: kbench <MiB> <B> <dl> <reps> <variant>...
+// variant 1000: the production abortable launch (the Sender's speculation: abort word never set);
+// variant 1001: the production entry launch_block_sums without an abort word (the Generator).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -33,7 +35,10 @@ int main(int argc, char** argv) {
     uint8_t* d;
     int32_t *w0, *w;
     uint8_t *s0, *sx;
-    CK(hipMalloc(&d, n));
+    // KBENCH_OFFSET=k: the data starts k bytes past a 256-B aligned allocation (unaligned-base A/B)
+    const int64_t off = getenv("KBENCH_OFFSET") ? atoll(getenv("KBENCH_OFFSET")) : 0;
+    CK(hipMalloc(&d, n + off + 64));
+    d += off;
     CK(hipMalloc(&w0, C * 4));
     CK(hipMalloc(&w, C * 4));
     CK(hipMalloc(&s0, (size_t)C * dl + 1));
@@ -45,13 +50,21 @@ int main(int argc, char** argv) {
     std::vector<uint8_t> hs0((size_t)C * dl), hs((size_t)C * dl);
     CK(hipMemcpy(hw0.data(), w0, C * 4, hipMemcpyDeviceToHost));
     CK(hipMemcpy(hs0.data(), s0, (size_t)C * dl, hipMemcpyDeviceToHost));
+    int* abort_word;
+    CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&abort_word), 256, hipDeviceMallocUncached));
+    CK(hipMemset(abort_word, 0, 256));
+    auto launch = [&](int v) {
+        if (v == 1000) return rsh::launch_block_sums_variant(-1, d, n, B, C, dl, 0x04030201u, w, sx, s, abort_word, 1);
+        if (v == 1001) return rsh::launch_block_sums(d, n, B, C, dl, 0x04030201u, w, sx, s);  // the production entry
+        return rsh::launch_block_sums_variant(v, d, n, B, C, dl, 0x04030201u, w, sx, s);
+    };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (int a = 5; a < argc; ++a) {
         const int v = atoi(argv[a]);
         CK(hipMemset(w, 0, C * 4));
-        CK(rsh::launch_block_sums_variant(v, d, n, B, C, dl, 0x04030201u, w, sx, s));
+        CK(launch(v));
         CK(hipStreamSynchronize(s));
         CK(hipMemcpy(hw.data(), w, C * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(hs.data(), sx, (size_t)C * dl, hipMemcpyDeviceToHost));
@@ -59,7 +72,7 @@ int main(int argc, char** argv) {
         float best = 1e30f, tot = 0;
         for (int r = 0; r < reps; ++r) {
             CK(hipEventRecord(e0, s));
-            CK(rsh::launch_block_sums_variant(v, d, n, B, C, dl, 0x04030201u, w, sx, s));
+            CK(launch(v));
             CK(hipEventRecord(e1, s));
             CK(hipEventSynchronize(e1));
             float ms;

@@ -32,6 +32,14 @@ def test_library_exports_every_symbol():
     assert R.lib().rsh_abi_version() == 2
 
 
+def test_library_built_from_these_sources():
+    """The build stamps librsynchip.so with its sources' sha256 (lib/librsynchip.srchash); rsync_hip.lib() refuses
+    a library whose sources changed since, so no test or bench run measures a stale binary."""
+    import os
+    assert os.path.exists(os.path.join(os.path.dirname(R.LIB_PATH), "librsynchip.srchash"))
+    assert R.stale_sources() == []
+
+
 @pytest.mark.parametrize("n", [1, 511, 512, 557, 1000, 64 << 20, 128 << 20, 4 << 30, 16 << 30, 64 << 30, (1 << 40) + 3])
 def test_sizing_matches_oracle(n):
     L = O.lib()

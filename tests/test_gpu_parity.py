@@ -154,8 +154,9 @@ def test_sender_digest_longer_than_md5(ctx, pad):
 @pytest.mark.parametrize("unaligned", ["0", "1"])
 def test_k1_unaligned_base(ctx, unaligned, monkeypatch):
     """K1 over a basis that starts at every offset 0..15 from a 16-B boundary (the phase-shifted speculation
-    runs K1 over src + s for any s).  RSH_K1_UNALIGNED=1 (diagnostic) keeps the pipelined buffer-load kernel at
-    such addresses; by default they take the per-lane kernel.  Bit-exact against the oracle either way."""
+    runs K1 over src + s for any s).  By default the pipelined buffer-load kernel runs at such addresses (its
+    dwordx4 loads straddle 16-B boundaries); RSH_K1_UNALIGNED=0 sends them to the per-lane kernel.  Bit-exact
+    against the oracle either way."""
     import ctypes
     monkeypatch.setenv("RSH_K1_UNALIGNED", unaligned)
     B, dl = 2048, 4
