@@ -32,15 +32,16 @@ import shard  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 # production K1 instantiation (device.hip launch_block_sums_variant default); the committed PMC profile
 # for `traffic` is matched on this name so a stale profile of another kernel is never reported
-PROD_KERNEL = "block_sums_pipe_kernel<8, false, true, 0, false>"  # the Generator K1 (non-batched)
-BATCH_KERNEL = "block_sums_pipe_kernel<8, false, true, 0, true>"  # the Generator K1 over a segment
+PROD_KERNEL = "block_sums_pipe_kernel<8, true, true, 0, false>"  # the Generator K1 (non-batched)
+BATCH_KERNEL = "block_sums_pipe_kernel<8, true, true, 0, true>"  # the Generator K1 over a segment
 KEY_SRC = 0x5EED5EED << 32
 KEY_EDIT = (0x5EED5EED << 32) | 0xED17
 # config 5 inputs = tests/fullsize_golden.py's: source key KEY ^ 5, edits KEY ^ 0xED17, inserted byte KEY ^ 0x1B
 KEY_CASE = KEY_SRC ^ 5
 KEY_INS = KEY_SRC ^ 0x1B
 SHIFT_AT = 155 * 131072 + 4096  # the "config5_shift1" insert position
-TRAFFIC_CSV = "r1_v14_bench_fetch_size.csv"
+TRAFFIC_CSV = "r2_v2_bench_fetch_size.csv"
+TRAFFIC_FILES_CSV = "r2_v2_files_fetch_size.csv"
 
 
 def parse():
@@ -449,8 +450,9 @@ def main_files(a):
         res["roofline"] = {"kernel": "block_sums_pipe_kernel (batched K1: the Generator over the segment)",
                            "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(ach / HBM_PEAK_GBS, 4),
-                           "traffic": pmc_traffic(os.path.join(ROOT, "profiles", "r1_v14_files_fetch_size.csv"),
+                           "traffic": pmc_traffic(os.path.join(ROOT, "profiles", TRAFFIC_FILES_CSV),
                                                   BATCH_KERNEL, n),
+                           "traffic_source": f"profiles/{TRAFFIC_FILES_CSV} (FETCH_SIZE x2, a prior run)",
                            "kernel_ms": round(k_ms, 4),
                            "algorithmic_bytes": n}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

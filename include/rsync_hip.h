@@ -78,7 +78,8 @@ typedef struct {
     double table_ms;         /* host index of the received table (chained hash, built lazily)  */
     int64_t head_steps;      /* resolver steps taken before the aligned speculation landed    */
     int64_t speculation_aborted; /* 1: the scan ended first and the speculation launch was stopped;
-                                    2: the scan ended in head mode before the speculation was launched */
+                                    2: the scan ended in head mode before the speculation was launched;
+                                    3: a tentative launch was stopped at once (the lead windows differ) */
     int64_t device_bytes;    /* source bytes the device work of this scan read: speculations that ran to
                                 completion (a stopped one counts 0), probed ranges (+ B - 1 per interval),
                                 weak-sum windows, gathered bytes and copied digest windows (ABI 2)  */

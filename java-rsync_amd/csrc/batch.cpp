@@ -42,7 +42,8 @@ struct BatchState {
     DevBuf slots, dslots, src_weak, src_strong, flags, haw, partials, bucket, first, k1_groups, k1_lanes;
     // Sender batch: pinned host (read or written by the kernels directly)
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl, h_files, h_hit, h_win0, h_bucket, h_first, h_iv, h_tiles,
-        h_ptiles, h_req, h_gw, h_gb, h_ow, h_ob, h_win, h_copies, h_tabents, h_flagents, h_dkeys, h_ccopies;
+        h_ptiles, h_req, h_gw, h_gb, h_ow, h_ob, h_win, h_copies, h_tabents, h_flagents, h_dkeys, h_ccopies,
+        h_lead;
     // device, uncached: one abort word per file of the batch; the speculation's groups of file f stop once
     // file_abort[f] holds the scan's generation (written by the coordinator when f's resolver finishes)
     int* file_abort = nullptr;
@@ -87,7 +88,7 @@ struct BatchState {
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_files, &h_hit, &h_win0, &h_bucket, &h_first,
                              &h_iv, &h_tiles, &h_ptiles, &h_req, &h_gw, &h_gb, &h_ow, &h_ob, &h_win, &h_copies,
-                             &h_tabents, &h_flagents, &h_dkeys, &h_ccopies})
+                             &h_tabents, &h_flagents, &h_dkeys, &h_ccopies, &h_lead})
             b->release();
     }
 };
@@ -121,7 +122,7 @@ hipError_t pin(PinnedBuf& b, int64_t count, T** out) {
 // Sender batch
 // ------------------------------------------------------------------------------------------------
 struct Req {
-    enum Kind { WEAK, BYTES, WIN, PROBE } kind = WEAK;
+    enum Kind { WEAK, BYTES, WIN, PROBE, WAIT } kind = WEAK;  // WAIT: until the speculation lands (no device work)
     const int64_t* pos = nullptr;  // WEAK / BYTES
     int64_t count = 0;
     int32_t* out_w = nullptr;
@@ -195,6 +196,7 @@ struct FileScan {
     bool done = false;
     bool started = false;
     bool cancelled = false;  // its speculation groups were dropped or told to stop (file_abort)
+    bool wait_spec = false;  // its lead windows carry their chunks' sums: wait for the speculation, no head mode
     int32_t worker = 0;
     ucontext_t uc;
     std::unique_ptr<char[]> stack;  // uninitialised: only the pages the fiber touches are committed
@@ -265,6 +267,12 @@ void fiber_main(uint32_t hi, uint32_t lo) {
     // small tables are sorted up front, here on the worker threads (in parallel across files): a segment's
     // resolvers would otherwise spend their first rounds in linear bucket scans before the lazy sort
     if (fs.C <= kEagerSortChunks) fs.table.build();
+    if (fs.wait_spec) {  // a run of aligned matches from the start: nothing to do until the speculation lands
+        fs.req = Req{};
+        fs.req.kind = Req::WAIT;
+        b.post(fs);
+        be.head = false;
+    }
     while (!resolve_run(fs.n, fs.table, be, &fs.rs, &fs.res,
                         [&] { return be.head && b.landed.load(std::memory_order_acquire); }))
         be.head = false;
@@ -620,6 +628,48 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     RSH_BHIP(S->ensure_file_abort(NF));
     for (K1Group& g : groups) g.abort = S->file_abort + g.file;
 
+    // per-file host state
+    ScanFile* F = S->h_files.as<ScanFile>();
+    Batch b;
+    b.files = &files;
+    for (int32_t f = 0; f < NF; ++f) {
+        FileScan& fs = files[(size_t)f];
+        const rsh_scan_job& j = jobs[fs.job];
+        fs.table.chunk_count = fs.C;
+        fs.table.block_length = (int32_t)fs.B;
+        fs.table.remainder = j.h.remainder;
+        fs.table.digest_length = fs.dl;
+        fs.table.weak = S->h_weak.as<int32_t>() + fs.off_tw;
+        fs.table.strong = S->h_strong.as<uint8_t>() + fs.off_ts;
+        BatchBackend& be = fs.be;
+        be.b = &b;
+        be.f = f;
+        be.na = fs.na;
+        be.aw = S->h_aw.as<int32_t>() + fs.off_na;
+        be.as = S->h_as.as<uint8_t>() + fs.off_as;
+        be.fl = S->h_fl.as<uint8_t>() + fs.off_nf;
+        be.win0 = S->h_win0.as<uint8_t>() + fs.off_w0;
+        be.w0 = std::min<int64_t>(fs.B, fs.n);
+        be.hit = S->h_hit.as<uint8_t>() + fs.off_hit;
+        be.bucket = S->h_bucket.as<int32_t>() + (int64_t)f * HIT_BUCKET_INTS;
+        be.n = fs.n;
+        be.B = fs.B;
+        memcpy(be.seed, seed, 4);
+        be.table = &fs.table;
+        be.haw_ready.assign((size_t)fs.na, 0);
+        F[f] = ScanFile{};
+        F[f].data = fs.d_src;
+        F[f].n = fs.n;
+        F[f].B = (uint32_t)fs.B;
+        F[f].out = S->first.as<ProbeOut>() + f;
+        F[f].table_weak = fs.d_weak;
+        F[f].C = fs.C;
+        F[f].bucket = S->bucket.as<int32_t>() + (int64_t)f * HIT_BUCKET_INTS;
+        F[f].hit = S->h_hit.as<uint8_t>() + fs.off_hit;
+        F[f].nwin = 1;
+        F[f].aligned_weak = S->haw.as<int32_t>() + fs.off_na;
+    }
+
     hipStream_t st = c->stream, aux = c->aux;
     RSH_BHIP(hipEventRecord(c->ev_in, st));  // whatever produced the inputs on the context stream
     // (stream) the received tables, to pinned host memory in one kernel
@@ -653,9 +703,24 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         max_w0 = std::max(max_w0, w0);
     }
     RSH_BHIP(launch_copy_many(wc, (uint32_t)NF, max_w0, st));
+    // (stream) T(kB) of each file's first lead windows (the launch decision below, as in scan_device)
+    std::vector<int64_t> lead_at((size_t)NF + 1, 0);
+    for (int32_t f = 0; f < NF; ++f)
+        lead_at[(size_t)f + 1] = lead_at[(size_t)f] + std::min<int64_t>(kLeadWindows, files[(size_t)f].nf);
+    const int64_t nlead_all = lead_at[(size_t)NF];
+    const size_t lead_ents_at = ((size_t)(nlead_all + 1) * 4 + 63) & ~(size_t)63;
+    RSH_BHIP(S->h_lead.ensure(lead_ents_at + (size_t)(nlead_all + 1) * sizeof(GatherEnt)));
+    int32_t* lead_w = S->h_lead.as<int32_t>();
+    if (nlead_all > 0) {
+        auto* ents = reinterpret_cast<GatherEnt*>(S->h_lead.as<uint8_t>() + lead_ents_at);
+        for (int32_t f = 0; f < NF; ++f)
+            for (int64_t k = 0; k < lead_at[(size_t)f + 1] - lead_at[(size_t)f]; ++k)
+                ents[lead_at[(size_t)f] + k] = GatherEnt{k * files[(size_t)f].B, f, 0};
+        RSH_BHIP(launch_window_weak(F, ents, (uint32_t)nlead_all, lead_w, st));
+    }
 
     // the batched aligned speculation (deferred; see scan_device in capi.cpp)
-    const int gen = ++c->gen;
+    int gen = ++c->gen;  // a stopped tentative launch's generation; a later launch takes a new one
     CopyEnt* sc = S->h_ccopies.as<CopyEnt>() + NF;
     // K1 over the sources needs nothing but the sources; the chain flags need the received tables (ev_in)
     bool k1_launched = false;
@@ -692,6 +757,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         }
         RSH_BHIP(hipEventRecord(S->ev_scopy, aux));
         S->scopy_pending = true;
+        RSH_BHIP(hipStreamWaitEvent(aux, c->ev_in, 0));  // the sources may come from work on the context stream
         RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>(), (uint32_t)groups.size(), S->k1_lanes.as<K1Lane>(),
                                          (uint32_t)lanes.size(), lane_align, seed_word(seed), aux, c->abort_word, gen));
         return RSH_OK;
@@ -736,7 +802,12 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     static const bool wait_spec = pol && strcmp(pol, "wait") == 0;
     static const bool early_spec = pol && (strcmp(pol, "early") == 0 || wait_spec);
     static const int defer_rounds = (pol && !early_spec) ? atoi(pol) : kDeferRounds;
-    if (early_spec) {
+    // launch-then-confirm (default policy): the speculation K1 is launched now, behind the Generator's work;
+    // the lead check below keeps it for the files whose first windows carry their chunks' sums (they wait for
+    // it instead of taking head-mode rounds) or stops it when no file qualifies
+    static const bool early_on = !getenv("RSH_SCAN_EARLY") || atoi(getenv("RSH_SCAN_EARLY")) != 0;  // A/B
+    const bool tentative = !pol && early_on && nlead_all > 0;
+    if (early_spec || tentative) {
         const int r = launch_spec_k1();
         if (r != RSH_OK) return r;
     }
@@ -745,50 +816,31 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     RSH_BHIP(hipStreamSynchronize(st));
     const double setup_ms = ms_since(t0);
 
-    // per-file host state
-    ScanFile* F = S->h_files.as<ScanFile>();
-    Batch b;
-    b.files = &files;
-    for (int32_t f = 0; f < NF; ++f) {
-        FileScan& fs = files[(size_t)f];
-        const rsh_scan_job& j = jobs[fs.job];
-        fs.table.chunk_count = fs.C;
-        fs.table.block_length = (int32_t)fs.B;
-        fs.table.remainder = j.h.remainder;
-        fs.table.digest_length = fs.dl;
-        fs.table.weak = S->h_weak.as<int32_t>() + fs.off_tw;
-        fs.table.strong = S->h_strong.as<uint8_t>() + fs.off_ts;
-        BatchBackend& be = fs.be;
-        be.b = &b;
-        be.f = f;
-        be.na = fs.na;
-        be.aw = S->h_aw.as<int32_t>() + fs.off_na;
-        be.as = S->h_as.as<uint8_t>() + fs.off_as;
-        be.fl = S->h_fl.as<uint8_t>() + fs.off_nf;
-        be.win0 = S->h_win0.as<uint8_t>() + fs.off_w0;
-        be.w0 = std::min<int64_t>(fs.B, fs.n);
-        be.hit = S->h_hit.as<uint8_t>() + fs.off_hit;
-        be.bucket = S->h_bucket.as<int32_t>() + (int64_t)f * HIT_BUCKET_INTS;
-        be.n = fs.n;
-        be.B = fs.B;
-        memcpy(be.seed, seed, 4);
-        be.table = &fs.table;
-        be.haw_ready.assign((size_t)fs.na, 0);
-        F[f] = ScanFile{};
-        F[f].data = fs.d_src;
-        F[f].n = fs.n;
-        F[f].B = (uint32_t)fs.B;
-        F[f].out = S->first.as<ProbeOut>() + f;
-        F[f].table_weak = fs.d_weak;
-        F[f].C = fs.C;
-        F[f].bucket = S->bucket.as<int32_t>() + (int64_t)f * HIT_BUCKET_INTS;
-        F[f].hit = S->h_hit.as<uint8_t>() + fs.off_hit;
-        F[f].nwin = 1;
-        F[f].aligned_weak = S->haw.as<int32_t>() + fs.off_na;
-    }
-
+    static const bool trace = getenv("RSH_SCAN_TRACE") != nullptr;
     int spec_rc = RSH_OK;
     bool spec_launched = false;
+    int32_t nwait = 0;
+    if (tentative) {
+        for (int32_t f = 0; f < NF; ++f) {
+            FileScan& fs = files[(size_t)f];
+            const int64_t a = lead_at[(size_t)f], nl = lead_at[(size_t)f + 1] - a;
+            int64_t lead = 0;
+            while (lead < nl && lead_w[a + lead] == fs.table.weak[lead]) ++lead;
+            fs.wait_spec = nl > 0 && lead == nl && (nl >= kLeadWindows || nl == fs.nf);
+            nwait += fs.wait_spec;
+        }
+        if (nwait > 0) {
+            spec_rc = launch_spec();
+            if (spec_rc != RSH_OK) return spec_rc;
+            spec_launched = true;
+        } else {  // no file qualifies: stop it (every group polls its file's word); the deferred launch stays
+            RSH_BHIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(S->file_abort), gen, (size_t)NF, st));
+            RSH_BHIP(hipStreamWaitEvent(st, S->ev_scopy, 0));
+            gen = ++c->gen;
+            k1_launched = false;
+        }
+        if (trace) fprintf(stderr, "[rsh-batch] lead check: %d of %d files wait for the speculation\n", nwait, NF);
+    }
     if (early_spec && !wait_spec) {
         spec_rc = launch_spec();  // the tail (flags, downloads) behind the K1 already running
         if (spec_rc != RSH_OK) return spec_rc;
@@ -833,6 +885,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 for (int32_t f = w; f < NF; f += W) {
                     FileScan& fs = files[(size_t)f];
                     if (fs.done) continue;
+                    if (fs.pending && fs.req.kind == Req::WAIT && !b.landed.load(std::memory_order_acquire)) continue;
                     fs.pending = false;
                     if (!fs.started) {
                         fs.started = true;
@@ -867,7 +920,6 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     hipError_t err = hipSuccess;
     int rounds = 0;
     std::vector<int32_t> pend;
-    static const bool trace = getenv("RSH_SCAN_TRACE") != nullptr;
     auto t_round = std::chrono::steady_clock::now();
     for (;;) {
         {
@@ -906,9 +958,19 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         }
         const double wait_ms = ms_since(t_round);
         const auto t_serve = std::chrono::steady_clock::now();
-        const hipError_t e = serve_round(c, S, files, pend);
+        std::vector<int32_t> work;  // requests with device work; WAITs are answered by the landing alone
+        for (int32_t f : pend)
+            if (files[(size_t)f].req.kind != Req::WAIT) work.push_back(f);
+        hipError_t e = hipSuccess;
+        if (!work.empty()) {
+            e = serve_round(c, S, files, work);
+        } else if (!b.landed.load()) {  // only waiting files: the speculation carries them
+            e = spec_launched ? hipEventSynchronize(c->ev_spec) : hipErrorInvalidValue;
+            if (e == hipSuccess) b.landed.store(true, std::memory_order_release);
+            if (trace) fprintf(stderr, "[rsh-batch] round %3d  waited for the speculation: %.3f ms\n", rounds, ms_since(t_serve));
+        }
         if (trace) {
-            int kinds[4] = {0, 0, 0, 0};
+            int kinds[5] = {0, 0, 0, 0, 0};
             for (int32_t f : pend) kinds[files[(size_t)f].req.kind]++;
             double bsum = 0, bmax = 0, fmax = 0;
             for (int32_t w = 0; w < b.nworkers; ++w) {

@@ -29,10 +29,12 @@ constexpr int kScanWindows = 2;  // hit windows per probe in the single-file sca
 constexpr int64_t kChainSteps = 2;  // ... after this many steps when the last event is a run of matches
 constexpr int64_t kDeferSteps = 4;
 constexpr double kDeferMs = 0.5;
-// ... or at once when the first kLeadWindows aligned source windows all carry chunk k's weak sum
-constexpr int64_t kLeadWindows = 32;
+// ... or at once when the first kLeadWindows (ctx.h) aligned source windows all carry chunk k's weak sum
 // ... over the windows up to the last of kSampleWindows evenly spaced samples that still carries its chunk's sum
 constexpr int64_t kSampleWindows = 1024;
+// windows one K1 launch digests in a single round of waves (2 waves/SIMD x 1024 SIMDs x 64 lanes): below this a
+// launch over fewer windows is no faster
+constexpr int64_t kRoundWindows = 131072;
 
 // RSH_SCAN_TRACE=1: one stderr line per resolver round trip (diagnostics).
 struct CallTrace {
@@ -447,7 +449,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // is launched only once the resolver has taken kDeferSteps steps or kDeferMs without finishing
     // (until then the resolver's round trips run on an otherwise idle device: a range probe beside the
     // speculation takes ~0.16 ms instead of tens of microseconds).
-    const int gen = ++c->gen;
+    int gen = ++c->gen;  // a stopped speculation's generation; a later launch takes a new one
     static const int diag = getenv("RSH_SCAN_DIAG") ? atoi(getenv("RSH_SCAN_DIAG")) : 0;  // A/B switches
     int64_t spec_na = na;  // windows the speculation covers: all, or a prefix (sampled launch decision)
     auto launch_spec = [&]() -> int {
@@ -498,6 +500,19 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         RSH_HIP(rsh::launch_window_weak(lf, ents, (uint32_t)nsamp, lead_w, c->stream));
     }
 
+    // Launch-then-confirm: when one K1 round covers every window (na <= kRoundWindows), the speculation that
+    // the lead decides on below is launched now, before the host knows the table, so it starts the moment the
+    // Generator's work ends on the device; the lead check then keeps it or stops it (its waves leave after
+    // their first two stages).  Larger sources wait for the samples (the launch may cover a prefix only).
+    static const bool early_on = !getenv("RSH_SCAN_EARLY") || atoi(getenv("RSH_SCAN_EARLY")) != 0;  // A/B
+    bool spec_tentative = false, tentative_stopped = false;
+    if (head && !spec_launched && nlead > 0 && early_on && na <= kRoundWindows &&
+        (nlead >= kLeadWindows || nlead == nf)) {
+        const int rc = launch_spec();
+        if (rc != RSH_OK) return rc;
+        spec_launched = spec_tentative = true;
+    }
+
     // (host) sort the table
     rsh::ChunkTable table;
     table.chunk_count = C;
@@ -533,18 +548,28 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     bool spec_wait = false;
     static const bool wait_on = !getenv("RSH_SCAN_WAIT") || atoi(getenv("RSH_SCAN_WAIT")) != 0;  // A/B
     static const bool sample_on = !getenv("RSH_SCAN_SAMPLE") || atoi(getenv("RSH_SCAN_SAMPLE")) != 0;  // A/B
-    if (head && !spec_launched && nlead > 0) {
+    if (head && nlead > 0 && (!spec_launched || spec_tentative)) {
         int64_t lead = 0;
         while (lead < nlead && lead_w[lead] == host_weak[lead]) ++lead;
-        if (lead == nlead && (nlead >= kLeadWindows || nlead == nf)) {
+        const bool eager = lead == nlead && (nlead >= kLeadWindows || nlead == nf);
+        if (spec_tentative && !eager) {  // stop the tentative launch; later launches take a new generation
+            RSH_HIP(hipStreamWriteValue32(c->stream, c->abort_word, (uint32_t)gen, 0));
+            gen = ++c->gen;
+            spec_launched = spec_tentative = false;
+            tentative_stopped = true;
+            res->stats.speculation_aborted = 3;  // overwritten below if a later launch lands or is stopped
+        } else if (spec_tentative) {
+            spec_wait = wait_on;
+        } else if (eager) {
             // the run may stop somewhere (an insert shifts everything after it to another phase, where the
             // phase-shifted speculation takes over): cover only up to the last sample that still matches
-            // (plus one stride); a single K1 over the rest would compute sums nothing reads
+            // (plus one stride) -- but never less than one K1 round of windows (kRoundWindows), since a K1
+            // over fewer chunks takes the same time (each lane digests its whole window serially)
             int64_t lastk = nlead - 1;
             for (int64_t i = nlead; i < nsamp; ++i)
                 if (lead_w[i] == host_weak[samp[(size_t)i]]) lastk = samp[(size_t)i];
             const bool all = lastk + stride >= nf || !sample_on;
-            spec_na = all ? na : std::min<int64_t>(na, lastk + stride + 1);
+            spec_na = all ? na : std::min<int64_t>(na, std::max<int64_t>(lastk + stride + 1, kRoundWindows));
             const int rc = launch_spec();
             if (rc != RSH_OK) return rc;
             spec_launched = true;
@@ -605,7 +630,10 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     if (be.err != hipSuccess) return RSH_E_DEVICE;
     bool spec_read = false;  // the aligned speculation ran to completion (its bytes count as read)
     if (done && !spec_launched) {
-        res->stats.speculation_aborted = 2;  // the scan ended in head mode before the speculation was needed
+        // the scan ended in head mode before the speculation was needed (3: a tentative launch was stopped)
+        if (res->stats.speculation_aborted != 3) res->stats.speculation_aborted = 2;
+        // the stopped launch's waves leave within two stages; later work on this context starts after them
+        if (tentative_stopped) RSH_HIP(hipStreamWaitEvent(c->stream, c->ev_spec, 0));
         res->stats.device_ms += ms_since(t0);
     } else if (done && !landed && hipEventQuery(c->ev_spec) == hipErrorNotReady) {
         RSH_HIP(hipStreamWriteValue32(c->stream, c->abort_word, (uint32_t)gen, 0));  // the rest is dead work
@@ -618,6 +646,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     } else {
         RSH_HIP(hipEventSynchronize(c->ev_spec));
         res->stats.device_ms += ms_since(t0);
+        res->stats.speculation_aborted = 0;
         spec_read = true;
         if (!done) {
             be.head = false;

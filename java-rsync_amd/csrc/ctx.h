@@ -27,6 +27,10 @@ namespace rshi {
 constexpr int64_t kChunkSize = 8192;        // Sender.java:230 CHUNK_SIZE
 constexpr int64_t kDefaultBlock = 8192;     // FileView.java:38 DEFAULT_BLOCK_SIZE
 constexpr int32_t kMaxBlockLength = 1 << 17;  // Checksum.java:151
+// Speculation launch decision (capi.cpp scan_device, batch.cpp scan_batch): when the first kLeadWindows
+// aligned source windows all carry their chunk's weak sum, a run of aligned matches is likely: the
+// speculation is launched at once and the resolver waits for it instead of taking head-mode steps.
+constexpr int64_t kLeadWindows = 32;
 
 struct DevBuf {
     void* p = nullptr;

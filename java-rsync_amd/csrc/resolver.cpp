@@ -138,13 +138,21 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
     const int64_t last = n - S;  // visited positions satisfy wl(s) >= S  <=>  s <= n - S
     const int64_t nB = n - B;
     // the speculation the backend has now (none while it is still in flight: every lookup below then
-    // takes the generic path, which gives the same answer)
-    const int64_t nal = be.aligned_count();
-    const int32_t* aw = be.aligned_weak();
-    const uint8_t* as = be.aligned_strong();
-    const uint8_t* fl = be.chain_flags();
-    const int64_t nflags = std::min<int64_t>(nal, table.chunk_count);
-    const int64_t max_batch = be.max_batch();
+    // takes the generic path, which gives the same answer); re-read every step, since a tiled backend
+    // extends it as its tiles land
+    int64_t nal = 0, nflags = 0, max_batch = 1;
+    const int32_t* aw = nullptr;
+    const uint8_t* as = nullptr;
+    const uint8_t* fl = nullptr;
+    auto refresh = [&] {
+        nal = be.aligned_count();
+        aw = be.aligned_weak();
+        as = be.aligned_strong();
+        fl = be.chain_flags();
+        nflags = std::min<int64_t>(nal, table.chunk_count);
+        max_batch = be.max_batch();
+    };
+    refresh();
     auto wl = [&](int64_t s) { return std::min<int64_t>(B, n - s); };  // FileView window length
     auto clampB = [&](int64_t p) { return std::min<int64_t>(p, nB); };
 
@@ -230,6 +238,7 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
             elapsed();
             return false;
         }
+        refresh();
         const bool synced = (elo == 0 && ehi == 0);
         // (1) aligned chain: preferred index == k and source window k carries chunk k's sums.
         if (!md5c_valid && synced && s % B == 0) {

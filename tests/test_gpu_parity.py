@@ -189,6 +189,19 @@ def test_sender_phase_shift_chains(ctx):
     assert st["phase_launches"] >= 1 and st["phase_matches"] > 6000 and st["host_md5_windows"] < 100, st
 
 
+def test_sender_partial_speculation(ctx):
+    """More windows than one K1 round (300000 > 131072 at B = 512) and a 7-byte insert after 1 MiB: the lead
+    windows match, the sampled windows past the insert do not, so the aligned speculation covers a prefix only
+    (the probe's block anchors past it are computed on demand) and the phase-shifted speculation carries the
+    rest.  Events equal the oracle's."""
+    B, dl = 512, 3
+    basis = O.splitmix(300000 * B, 0x5EED5EED000000A7)
+    src = np.concatenate([basis[:(1 << 20) + 5], O.splitmix(7, 3), basis[(1 << 20) + 5:]])
+    st = _sender_both(ctx, basis.tobytes(), src.tobytes(), B, dl)
+    assert st["phase_launches"] >= 1 and st["phase_matches"] > 290000, st
+    assert st["device_bytes"] < 2 * len(src), st
+
+
 def test_device_fill_matches_oracle(ctx):
     n = (1 << 20) + 13
     d = ctx.alloc(n)
