@@ -131,6 +131,16 @@ int rsh_match_scan_device(rsh_ctx* ctx, const void* d_src, int64_t n, const rsh_
                           const void* d_strong, const uint8_t seed[4], rsh_event* ev, int64_t ev_cap,
                           int64_t* n_ev, int64_t* literal, int64_t* matched, rsh_scan_stats* stats);
 
+/* Tiled form for sources larger than the device (BASELINE config 3; FileView streams any file through a
+ * 10*B window, FileView.java:235-278): the source stays in host memory and HBM holds one tile of tile_bytes
+ * (rounded to a multiple of B, at least 16*B; 0 = 4 GiB) plus a 16*B halo at a time, paged in as the scan
+ * advances; the aligned speculation runs tile by tile.  Events, literal and matched are those of
+ * rsh_match_scan.  file_md5 may be NULL (the serial whole-file digest is then skipped). */
+int rsh_match_scan_tiled(rsh_ctx* ctx, const uint8_t* src, int64_t n, const rsh_header* h, const int32_t* weak,
+                         const uint8_t* strong, const uint8_t seed[4], int64_t tile_bytes, rsh_event* ev,
+                         int64_t ev_cap, int64_t* n_ev, uint8_t file_md5[16], int64_t* literal, int64_t* matched,
+                         rsh_scan_stats* stats);
+
 /* After RSH_E_NOSPACE from rsh_match_scan[_device] the context keeps that scan's events: fetch them into
  * a buffer of at least *n_ev entries without recomputing (valid until the context's next scan). */
 int rsh_fetch_events(rsh_ctx* ctx, rsh_event* ev, int64_t ev_cap, int64_t* n_ev);

@@ -35,6 +35,8 @@ constexpr int64_t kSampleWindows = 1024;
 // windows one K1 launch digests in a single round of waves (2 waves/SIMD x 1024 SIMDs x 64 lanes): below this a
 // launch over fewer windows is no faster
 constexpr int64_t kRoundWindows = 131072;
+// rsh_match_scan_tiled: default tile (the device holds one tile + a 16 B halo of the source at a time)
+constexpr int64_t kDefaultTile = 4LL << 30;
 
 // RSH_SCAN_TRACE=1: one stderr line per resolver round trip (diagnostics).
 struct CallTrace {
@@ -74,8 +76,64 @@ class HipBackend : public rsh::ScanBackend {
     std::vector<uint8_t> haw_ready;
     std::function<void(uint8_t*)> md5_0;  // digest of window 0 (joins its host thread)
 
-    int64_t aligned_count() override { return head ? 0 : na; }
+    int64_t aligned_count() override { return tiled ? aligned_end : head ? 0 : na; }
     int64_t max_batch() override { return head ? 4 : 4096; }
+    int64_t max_batch_at(int64_t f) override {  // a batch's intervals, bytes and windows stay in the tile
+        if (!tiled) return max_batch();
+        ensure(f);
+        const int64_t hi = std::min(n_, tile_lo + tile_T + tile_H);
+        return std::max<int64_t>(1, std::min<int64_t>(max_batch(), (hi - f - B_ - 1) / (10 * B_)));
+    }
+
+    // ---- tiled source (rsh_match_scan_tiled): HBM holds [tile_lo, tile_lo + tile_T + tile_H) of the
+    // source, tile_T a multiple of B and tile_H >= 16 B.  Every device question starts at or after the
+    // scan position, which only grows, and reaches at most 10 B + 1 past it (a flush interval and its
+    // window); the batched flush chain is capped by max_batch_at.  So each question is answered from the
+    // tile that holds its first position, and tiles only advance.  Loading a tile copies it in (fill) and
+    // runs the aligned speculation over the windows that start in it. ----
+    bool tiled = false;
+    int64_t tile_T = 0, tile_H = 0, tile_lo = -1;
+    uint8_t* tile_buf = nullptr;
+    int64_t aligned_end = 0, tiles_loaded = 0;
+    std::function<hipError_t(uint8_t* dst, int64_t off, int64_t len)> fill;  // synchronous
+    const int32_t* d_table_strong = nullptr;
+    void ensure(int64_t a) {
+        if (!tiled || err != hipSuccess) return;
+        if (tile_lo >= 0 && a >= tile_lo && (a < tile_lo + tile_T || tile_lo + tile_T >= n_)) return;
+        load_tile(a / tile_T * tile_T);
+    }
+    void load_tile(int64_t lo) {
+        CallTrace tr("tile_load", lo);
+        if (ph_s0_ >= 0 && !ph_landed_) ok(hipEventSynchronize(c_->ev_phase));  // it reads the old tile
+        const int64_t hi = std::min(n_, lo + tile_T + tile_H);
+        ok(fill(tile_buf, lo, hi - lo));
+        if (err != hipSuccess) return;
+        tile_lo = lo;
+        x_ = tile_buf - lo;  // data[p] for p in [lo, hi)
+        ++tiles_loaded;
+        // the windows wholly inside the tile (the file's last window when the tile reaches the end)
+        const int64_t na_all = (n_ + B_ - 1) / B_;
+        const int64_t k0 = lo / B_, k1 = hi == n_ ? na_all : (hi - B_) / B_ + 1;
+        const int64_t C = t_.chunk_count, f1 = std::min(k1, C);
+        ok(rsh::launch_block_sums(x_ + k0 * B_, std::min(n_, k1 * B_) - k0 * B_, (uint32_t)B_, (uint32_t)(k1 - k0),
+                                  (uint32_t)dl_, seed_word(seed_), c_->src_weak.as<int32_t>() + k0,
+                                  c_->src_strong.as<uint8_t>() + k0 * dl_, c_->stream));
+        if (f1 > k0)
+            ok(rsh::launch_chain_flags(c_->src_weak.as<int32_t>() + k0, c_->src_strong.as<uint8_t>() + k0 * dl_,
+                                       d_table_weak_ + k0, reinterpret_cast<const uint8_t*>(d_table_strong) + k0 * dl_,
+                                       (uint32_t)(f1 - k0), (uint32_t)dl_, c_->flags.as<uint8_t>() + k0, c_->stream));
+        ok(hipMemcpyAsync(c_->h_aw.as<int32_t>() + k0, c_->src_weak.as<int32_t>() + k0, (size_t)(k1 - k0) * 4,
+                          hipMemcpyDeviceToHost, c_->stream));
+        if (dl_ > 0)
+            ok(hipMemcpyAsync(c_->h_as.as<uint8_t>() + k0 * dl_, c_->src_strong.as<uint8_t>() + k0 * dl_,
+                              (size_t)((k1 - k0) * dl_), hipMemcpyDeviceToHost, c_->stream));
+        if (f1 > k0)
+            ok(hipMemcpyAsync(c_->h_fl.as<uint8_t>() + k0, c_->flags.as<uint8_t>() + k0, (size_t)(f1 - k0),
+                              hipMemcpyDeviceToHost, c_->stream));
+        ok(hipStreamSynchronize(c_->stream));
+        bytes_read += std::min(n_, k1 * B_) - k0 * B_;
+        aligned_end = k1;
+    }
     const int32_t* aligned_weak() override { return aw; }
     const uint8_t* aligned_strong() override { return as; }
     const uint8_t* chain_flags() override { return fl; }
@@ -87,6 +145,7 @@ class HipBackend : public rsh::ScanBackend {
             return;
         }
         CallTrace tr("weak_many", count);
+        ensure(*std::min_element(pos, pos + count));
         bytes_read += count * B_;
         rsh::GatherEnt* hp = pin<rsh::GatherEnt>(c_->h_pos, count);
         int32_t* ho = pin<int32_t>(c_->h_out, count);
@@ -100,6 +159,7 @@ class HipBackend : public rsh::ScanBackend {
     void bytes_many(const int64_t* pos, int64_t count, uint8_t* out) override {
         if (count <= 0) return;
         CallTrace tr("bytes_many", count);
+        ensure(*std::min_element(pos, pos + count));
         bytes_read += count;
         rsh::GatherEnt* hp = pin<rsh::GatherEnt>(c_->h_pos, count);
         uint8_t* ho = pin<uint8_t>(c_->h_out, count);
@@ -134,6 +194,7 @@ class HipBackend : public rsh::ScanBackend {
             h.final(out);
             return;
         }
+        ensure(p);
         uint8_t* hw = pin<uint8_t>(c_->h_win, w);
         if (err != hipSuccess) return;
         bytes_read += w;
@@ -161,6 +222,7 @@ class HipBackend : public rsh::ScanBackend {
             iv = &one;
         }
         CallTrace tr("first_hit", count);
+        ensure(iv[0].a);
         bytes_read += probe_bytes(iv, count, B_);
         rsh::ProbeTable tab = table;
         if (keys) {
@@ -264,14 +326,18 @@ class HipBackend : public rsh::ScanBackend {
     // the received header's B and dl, on the aux stream behind whatever runs there, one at a time ----
     int64_t ph_launches = 0;
     void phase_hint(int64_t s) override {
-        if (ph_s0_ >= 0 && s >= ph_s0_ && (s - ph_s0_) % B_ == 0) return;  // the current one covers s
-        const int64_t count = (n_ - s + B_ - 1) / B_;
+        if (ph_s0_ >= 0 && s >= ph_s0_ && (s - ph_s0_) % B_ == 0 && s < ph_s0_ + ph_count_ * B_) return;  // covered
+        ensure(s);
+        // windows wholly in the data the device holds: the rest of the file, or of the tile
+        const int64_t hi = tiled ? std::min(n_, tile_lo + tile_T + tile_H) : n_;
+        const int64_t count = hi == n_ ? (n_ - s + B_ - 1) / B_ : (hi - s - B_) / B_ + 1;
         if (count < kPhaseMinWindows || ph_launches >= kPhaseMaxLaunches || err != hipSuccess || !phase_on()) return;
         phase_stop();  // one at another phase is dead work now
         CallTrace tr("phase_spec", s);
         ph_gen_ = ++c_->gen;
         ok(hipStreamWaitEvent(c_->aux, c_->ev_in, 0));
-        ok(rsh::launch_block_sums(x_ + s, n_ - s, (uint32_t)B_, (uint32_t)count, (uint32_t)dl_, seed_word(seed_),
+        ok(rsh::launch_block_sums(x_ + s, std::min(n_ - s, count * B_), (uint32_t)B_, (uint32_t)count, (uint32_t)dl_,
+                                  seed_word(seed_),
                                   c_->ph_weak.as<int32_t>(), c_->ph_strong.as<uint8_t>(), c_->aux,
                                   c_->abort_word + rsh_ctx::kPhaseWord, ph_gen_));
         ok(hipMemcpyAsync(c_->h_pw.p, c_->ph_weak.p, (size_t)count * 4, hipMemcpyDeviceToHost, c_->aux));
@@ -285,7 +351,8 @@ class HipBackend : public rsh::ScanBackend {
         ++ph_launches;
     }
     bool phase_sums(int64_t s, bool wait, rsh::PhaseView* v) override {
-        if (ph_s0_ < 0 || s < ph_s0_ || (s - ph_s0_) % B_ != 0 || err != hipSuccess) return false;
+        if (ph_s0_ < 0 || s < ph_s0_ || (s - ph_s0_) % B_ != 0 || s >= ph_s0_ + ph_count_ * B_ || err != hipSuccess)
+            return false;
         if (!ph_landed_) {
             if (wait) {
                 CallTrace tr("phase_wait", s);
@@ -295,7 +362,7 @@ class HipBackend : public rsh::ScanBackend {
                 ph_landed_ = hipEventQuery(c_->ev_phase) == hipSuccess;
             }
             if (!ph_landed_) return false;
-            bytes_read += n_ - ph_s0_;
+            bytes_read += std::min(n_ - ph_s0_, ph_count_ * B_);
         }
         v->s0 = ph_s0_;
         v->count = ph_count_;
@@ -669,6 +736,74 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     return RSH_OK;
 }
 
+// The Sender scan over a source that HBM holds a tile at a time (BASELINE config 3: files larger than the
+// device, FileView's sliding window over the file, FileView.java:235-278).  The table is on the device
+// (d_weak, d_strong) and on the host; `fill` copies source bytes [off, off + len) into HBM.  One resolver
+// over the whole file; its backend pages tiles of tile_T bytes (+ a 16 B halo) as the scan advances and
+// runs the aligned speculation tile by tile.  Identical events to scan_device.
+int scan_tiled(rsh_ctx* c, const std::function<hipError_t(uint8_t*, int64_t, int64_t)>& fill, int64_t n,
+               const rsh_header* h, const int32_t* d_weak, const uint8_t* d_strong, const int32_t* host_weak,
+               const uint8_t* host_strong, const uint8_t seed[4], int64_t tile_bytes, rsh::ResolveResult* res) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int64_t B = h->block_length;
+    const int32_t C = h->chunk_count;
+    const int32_t dl = h->digest_length;
+    const int64_t na = (n + B - 1) / B;
+    if (na > 2147483647LL) return RSH_E_OVERFLOW;
+    const uint32_t ns = pow2_at_least(2 * (uint64_t)C + 2);
+    const int64_t T = std::max<int64_t>(16 * B, tile_bytes / B * B), H = 16 * B;
+    const int64_t nf = std::min<int64_t>(na, C);
+    RSH_HIP(c->data.ensure((size_t)std::min(n, T + H)));
+    RSH_HIP(c->slots.ensure((size_t)ns * sizeof(unsigned long long)));
+    RSH_HIP(c->src_weak.ensure((size_t)na * 4));
+    RSH_HIP(c->src_strong.ensure((size_t)na * dl + 1));
+    RSH_HIP(c->flags.ensure((size_t)nf + 1));
+    RSH_HIP(c->h_aw.ensure((size_t)na * 4));
+    RSH_HIP(c->h_as.ensure((size_t)na * dl + 1));
+    RSH_HIP(c->h_fl.ensure((size_t)nf + 1));
+    RSH_HIP(c->haw.ensure((size_t)na * 4));
+    RSH_HIP(c->ph_weak.ensure((size_t)na * 4));
+    RSH_HIP(c->ph_strong.ensure((size_t)na * dl + 1));
+    RSH_HIP(c->h_pw.ensure((size_t)na * 4));
+    RSH_HIP(c->h_ps.ensure((size_t)na * dl + 1));
+    RSH_HIP(hipEventRecord(c->ev_in, c->stream));
+    RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, c->stream));
+    RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, c->stream));
+    RSH_HIP(hipStreamSynchronize(c->stream));
+    rsh::ChunkTable table;
+    table.chunk_count = C;
+    table.block_length = (int32_t)B;
+    table.remainder = h->remainder;
+    table.digest_length = dl;
+    table.weak = host_weak;
+    table.strong = host_strong;
+    HipBackend be(c, c->data.as<uint8_t>(), n, table, d_weak, seed);
+    be.table.slots = c->slots.as<unsigned long long>();
+    be.table.mask = ns - 1;
+    be.na = na;
+    be.aw = c->h_aw.as<int32_t>();
+    be.as = c->h_as.as<uint8_t>();
+    be.fl = c->h_fl.as<uint8_t>();
+    be.tiled = true;
+    be.tile_T = T;
+    be.tile_H = H;
+    be.tile_buf = c->data.as<uint8_t>();
+    be.fill = fill;
+    be.d_table_strong = reinterpret_cast<const int32_t*>(d_strong);
+    be.haw_ready.assign((size_t)na, 0);
+    be.ensure(0);
+    if (be.err != hipSuccess) return RSH_E_DEVICE;
+    rsh::resolve_scan(n, table, be, res);
+    be.phase_stop();
+    if (be.err != hipSuccess) return RSH_E_DEVICE;
+    res->stats.device_ms += ms_since(t0);
+    res->stats.table_ms += table.sort_ms;
+    res->stats.device_bytes += be.bytes_read;
+    res->stats.phase_launches += be.ph_launches;
+    res->stats.head_steps = be.tiles_loaded;  // tiled scans have no head mode: the count of tile loads
+    return RSH_OK;
+}
+
 int emit_events(rsh_ctx* c, rsh::ResolveResult& r, rsh_event* ev, int64_t cap, int64_t* n_ev) {
     *n_ev = (int64_t)r.ev.size();
     if ((int64_t)r.ev.size() > cap || (!ev && !r.ev.empty())) {
@@ -897,6 +1032,54 @@ int rsh_match_scan(rsh_ctx* ctx, const uint8_t* src, int64_t n, const rsh_header
         }
     }
     md5_thread.join();
+    if (rc != RSH_OK) return rc;
+    if (literal) *literal = r.literal;
+    if (matched) *matched = r.matched;
+    if (stats) *stats = r.stats;
+    return emit_events(ctx, r, ev, ev_cap, n_ev);
+}
+
+int rsh_match_scan_tiled(rsh_ctx* ctx, const uint8_t* src, int64_t n, const rsh_header* h, const int32_t* weak,
+                         const uint8_t* strong, const uint8_t seed[4], int64_t tile_bytes, rsh_event* ev,
+                         int64_t ev_cap, int64_t* n_ev, uint8_t file_md5[16], int64_t* literal, int64_t* matched,
+                         rsh_scan_stats* stats) {
+    if (!ctx || !h || !seed || !n_ev || n < 0 || tile_bytes < 0 || (n > 0 && !src)) return RSH_E_INVAL;
+    const int v = rsh_header_validate(h);
+    if (v != RSH_OK) return v;
+    RSH_CLAIM(ctx);
+    RSH_HIP(hipSetDevice(ctx->device));
+    std::thread md5_thread;
+    if (file_md5)
+        md5_thread = std::thread([&] {
+            rsh::HostMd5 m;
+            if (n > 0) m.update(src, (size_t)n);
+            m.final(file_md5);
+        });
+    rsh::ResolveResult r;
+    int rc = RSH_OK;
+    if (h->block_length == 0) {
+        skip_events(n, &r);
+    } else if (n > 0) {
+        const size_t C = (size_t)h->chunk_count, dl = (size_t)h->digest_length;
+        if (C > 0 && (!weak || (!strong && dl > 0))) rc = RSH_E_INVAL;
+        if (rc == RSH_OK && (ctx->weak.ensure(C * 4 + 4) != hipSuccess || ctx->strong.ensure(C * dl + 1) != hipSuccess))
+            rc = RSH_E_NOMEM;
+        if (rc == RSH_OK) {
+            bool okc = true;
+            if (C) okc = hipMemcpyAsync(ctx->weak.p, weak, C * 4, hipMemcpyHostToDevice, ctx->stream) == hipSuccess;
+            if (C && dl)
+                okc = okc && hipMemcpyAsync(ctx->strong.p, strong, C * dl, hipMemcpyHostToDevice, ctx->stream) == hipSuccess;
+            auto fill = [&](uint8_t* dst, int64_t off, int64_t len) -> hipError_t {
+                const hipError_t e = hipMemcpyAsync(dst, src + off, (size_t)len, hipMemcpyHostToDevice, ctx->stream);
+                return e != hipSuccess ? e : hipStreamSynchronize(ctx->stream);
+            };
+            const int64_t tb = tile_bytes > 0 ? tile_bytes : kDefaultTile;
+            rc = okc ? scan_tiled(ctx, fill, n, h, ctx->weak.as<int32_t>(), ctx->strong.as<uint8_t>(), weak, strong, seed,
+                                  tb, &r)
+                     : RSH_E_DEVICE;
+        }
+    }
+    if (md5_thread.joinable()) md5_thread.join();
     if (rc != RSH_OK) return rc;
     if (literal) *literal = r.literal;
     if (matched) *matched = r.matched;

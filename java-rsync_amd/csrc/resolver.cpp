@@ -402,7 +402,8 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
             // replace K round trips.  K doubles while no event turns up (wasted probing <= 2x).
             // flush i sits at f_i = f + 10B i and happens iff its mark m_i = f_i - 9B has m_i + 10B <= n
             int64_t K = 1;
-            while (K < std::min(batch, max_batch) && f + 10 * B * K + B <= n) ++K;
+            const int64_t kcap = std::min(max_batch, be.max_batch_at(f));
+            while (K < std::min(batch, kcap) && f + 10 * B * K + B <= n) ++K;
             std::vector<int64_t> tpos, bpos;
             for (int64_t i = 0; i < K; ++i) {
                 const int64_t fi = f + 10 * B * i;

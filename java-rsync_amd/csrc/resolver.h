@@ -124,8 +124,13 @@ class ScanBackend {
     // Smallest p over all intervals whose key is in the key set (keys == nullptr: the whole chunk
     // table); -1 if none.
     virtual int64_t first_hit(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) = 0;
-    // Upper bound on the flush intervals one batched probe may cover.
+    // Upper bound on the flush intervals one batched probe may cover (max_batch_at: for a batch whose first
+    // flush point is f -- a tiled backend keeps the batch inside its resident tile).
     virtual int64_t max_batch() { return 4096; }
+    virtual int64_t max_batch_at(int64_t f) {
+        (void)f;
+        return max_batch();
+    }
     // Source bytes the backend's device work read for this scan (rsh_scan_stats::device_bytes).
     int64_t bytes_read = 0;
     static int64_t probe_bytes(const ProbeInterval* iv, int64_t count, int64_t B) {

@@ -104,7 +104,7 @@ EVENT_DTYPE = np.dtype([("offset", "<i8"), ("length", "<i8"), ("kind", "<i4"), (
 EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_count", "rsh_ctx_create", "rsh_ctx_destroy",
            "rsh_ctx_stream", "rsh_block_length_for", "rsh_digest_length_for", "rsh_header_make",
            "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
-           "rsh_match_scan_device", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
+           "rsh_match_scan_device", "rsh_match_scan_tiled", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
            "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_receiver_combine",
            "rsh_receiver_combine_device", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 
@@ -165,6 +165,8 @@ def lib():
                             ctypes.POINTER(I64), ctypes.POINTER(ScanStats)], ctypes.c_int),
         "rsh_match_scan_device": ([P, P, I64, HP, P, P, P, P, I64, ctypes.POINTER(I64), ctypes.POINTER(I64),
                                    ctypes.POINTER(I64), ctypes.POINTER(ScanStats)], ctypes.c_int),
+        "rsh_match_scan_tiled": ([P, P, I64, HP, P, P, P, I64, P, I64, ctypes.POINTER(I64), P, ctypes.POINTER(I64),
+                                  ctypes.POINTER(I64), ctypes.POINTER(ScanStats)], ctypes.c_int),
         "rsh_fetch_events": ([P, P, I64, ctypes.POINTER(I64)], ctypes.c_int),
         "rsh_file_md5": ([P, I64, P], ctypes.c_int),
         "rsh_tokens_size": ([P, I64], I64),
@@ -350,6 +352,27 @@ class Context:
         _check(rc)
         return ev[:n_ev.value], fm.tobytes(), lit.value, mat.value, stats.as_dict()
 
+    def match_scan_tiled(self, src, h, weak, strong, seed, tile_bytes=0, digest=True, ev_cap=None):
+        """The scan with HBM holding one tile of the source at a time (rsh_match_scan_tiled): as match_scan;
+        file_md5 is None when digest is False."""
+        a = _u8(src)
+        s = np.frombuffer(bytes(seed), np.uint8).copy()
+        w = np.ascontiguousarray(weak, dtype=np.int32)
+        st = np.ascontiguousarray(strong, dtype=np.uint8)
+        cap = ev_cap if ev_cap is not None else int(a.size // max(10 * h.block_length, 1) + 2 * h.chunk_count + 64)
+        ev = np.zeros(max(cap, 1), EVENT_DTYPE)
+        n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        fm = np.zeros(16, np.uint8)
+        stats = ScanStats()
+        rc = lib().rsh_match_scan_tiled(self._p, _ptr(a), a.size, ctypes.byref(h), _ptr(w) if w.size else None,
+                                        _ptr(st) if st.size else None, _ptr(s), tile_bytes, _ptr(ev), cap,
+                                        ctypes.byref(n_ev), _ptr(fm) if digest else None, ctypes.byref(lit),
+                                        ctypes.byref(mat), ctypes.byref(stats))
+        if rc == RSH_E_NOSPACE and ev_cap is None:
+            ev = np.zeros(n_ev.value, EVENT_DTYPE)
+            rc = lib().rsh_fetch_events(self._p, _ptr(ev), n_ev.value, ctypes.byref(n_ev))
+        _check(rc)
+        return ev[:n_ev.value], (fm.tobytes() if digest else None), lit.value, mat.value, stats.as_dict()
 
     def block_sums_file(self, path, size, h, seed):
         """Generator pass over a file (FileView reads of `size` bytes): (weak, strong, read_error)."""

@@ -250,7 +250,16 @@ def test_config3_64GiB(env):
         lead += int(e["count"])
     assert lead == k
     _check_delta(torch, ev, src, basis, h, lit, mat)
-    del src, basis
+    # the same scan with the source in host memory and HBM holding 4 GiB tiles (+ a 16 B halo) at a time
+    # (rsh_match_scan_tiled: a file larger than the device): the identical event list
+    host = src.cpu().numpy()
+    del src
+    tev, _, tlit, tmat, tst = ctx.match_scan_tiled(host, h, d_w.cpu().numpy(), d_s.cpu().numpy(), SEED,
+                                                   tile_bytes=4 << 30, digest=False)
+    assert (tlit, tmat) == (lit, mat) and tst["head_steps"] >= 16, tst  # 16+ tile loads
+    assert np.array_equal(tev[["offset", "length", "kind", "index", "count"]], ev[["offset", "length", "kind", "index", "count"]])
+    del host
+    del basis
     torch.cuda.empty_cache()
 
 

@@ -202,6 +202,35 @@ def test_sender_partial_speculation(ctx):
     assert st["device_bytes"] < 2 * len(src), st
 
 
+@pytest.mark.parametrize("seed_i", range(3))
+def test_sender_tiled_matches_oracle(ctx, seed_i):
+    """rsh_match_scan_tiled (HBM holds one tile + a 16 B halo of the source at a time, BASELINE config 3's
+    regime) with tiles as small as 16 B: the events, literal/matched and file MD5 equal the oracle's over
+    inserts, deletes, rewritten blocks and >= 9 B literal runs (flushes across tile boundaries)."""
+    from test_resolver_cpu import _mutate
+    rng = random.Random(4400 + seed_i)
+    for i in range(8):
+        B = rng.choice([512, 1024, 2048])
+        nb = rng.randrange(100 * B, 400 * B)
+        key = rng.randrange(1 << 62)
+        basis = O.splitmix(nb, key).tobytes()
+        src = _mutate(rng, basis, B, key) or basis
+        if i % 4 == 3:  # a long literal run: flush intervals straddle tiles
+            a = rng.randrange(len(src))
+            src = src[:a] + O.splitmix(40 * B + 7, key ^ 9).tobytes() + src[a:]
+        dl = rng.choice([2, 3, 4])
+        h = O.header(B, dl, len(basis))
+        w, s = O.generator(basis, h, SEED)
+        oev, ofm, olit, omat, _ = O.sender(src, h, w, s, SEED)
+        rh = R.Header(**h.as_dict())
+        tile = rng.choice([16 * B, 16 * B + 100, 37 * B, 1 << 30])
+        ev, fm, lit, mat, st = ctx.match_scan_tiled(src, rh, w, s, SEED, tile_bytes=tile)
+        assert R.events_as_tuples(ev, B) == [tuple(e) for e in oev], (i, tile)
+        assert (fm, lit, mat) == (ofm, olit, omat)
+        if tile < len(src) // 2:
+            assert st["head_steps"] >= 2  # tile loads
+
+
 def test_device_fill_matches_oracle(ctx):
     n = (1 << 20) + 13
     d = ctx.alloc(n)
