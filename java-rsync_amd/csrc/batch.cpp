@@ -166,7 +166,8 @@ class BatchBackend : public ScanBackend {
     std::vector<uint8_t> pf;
     int64_t pf_pos = -1;
 
-    int64_t aligned_count() override { return head ? 0 : na; }
+    int64_t aligned_count() override;
+    int64_t flags_count() override { return head ? 0 : na; }
     int64_t max_batch() override { return head ? 4 : 4096; }
     const int32_t* aligned_weak() override { return aw; }
     const uint8_t* aligned_strong() override { return as; }
@@ -217,7 +218,8 @@ struct Batch {
     std::atomic<int32_t> idle{0};
     std::atomic<uint64_t> gen{0};
     std::atomic<bool> quit{false};
-    std::atomic<bool> landed{false};
+    std::atomic<bool> landed{false};   // the speculation's chain flags are on the host (resolvers leave head mode)
+    std::atomic<bool> aligned{false};  // ... and its aligned sums (aligned lookups)
     std::vector<FileScan>* files = nullptr;
     std::vector<ucontext_t> worker_uc;
     std::vector<double> busy_ms, max_fiber_ms;  // per worker, this round (trace)
@@ -231,6 +233,8 @@ struct Batch {
 };
 
 FileScan& scan_of(Batch* b, int32_t f) { return (*b->files)[(size_t)f]; }
+
+int64_t BatchBackend::aligned_count() { return (head || !b->aligned.load(std::memory_order_acquire)) ? 0 : na; }
 
 // Round hand-offs: a blocked thread takes ~50 us to wake from a condition variable, once per round per
 // side (coordinator -> workers, last worker -> coordinator).  Waiters spin up to RSH_BATCH_SPIN us
@@ -771,25 +775,33 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         FlagEnt* fe = S->h_flagents.as<FlagEnt>();
         uint32_t max_nf = 0, nsc = 0;
         int64_t max_len = 0;
-        for (int32_t f = 0; f < NF; ++f) {
+        int64_t max_fl = 0;
+        for (int32_t f = 0; f < NF; ++f) {  // the flags first (the chains need nothing else) ...
             FileScan& fs = files[(size_t)f];
             // a file resolved before the launch has no speculation: no flags, no downloads
             const uint32_t nflag = fs.cancelled ? 0u : (uint32_t)fs.nf;
             fe[f] = FlagEnt{S->src_weak.as<int32_t>() + fs.off_na, S->src_strong.as<uint8_t>() + fs.off_as, fs.d_weak,
                             fs.d_strong, S->flags.as<uint8_t>() + fs.off_nf, nflag, (uint32_t)fs.dl};
             max_nf = std::max<uint32_t>(max_nf, nflag);
+            if (fs.cancelled || fs.nf == 0) continue;
+            sc[nsc++] = CopyEnt{S->flags.as<uint8_t>() + fs.off_nf, S->h_fl.as<uint8_t>() + fs.off_nf, fs.nf};
+            max_fl = std::max<int64_t>(max_fl, fs.nf);
+        }
+        const uint32_t nfl = nsc;
+        for (int32_t f = 0; f < NF; ++f) {  // ... then the sums (aligned lookups off the chains)
+            FileScan& fs = files[(size_t)f];
             if (fs.cancelled) continue;
             sc[nsc++] = CopyEnt{S->src_weak.as<uint8_t>() + 4 * fs.off_na, S->h_aw.as<uint8_t>() + 4 * fs.off_na,
                                 fs.na * 4};
             if (fs.dl > 0)
                 sc[nsc++] = CopyEnt{S->src_strong.as<uint8_t>() + fs.off_as, S->h_as.as<uint8_t>() + fs.off_as,
                                     fs.na * fs.dl};
-            if (fs.nf > 0)
-                sc[nsc++] = CopyEnt{S->flags.as<uint8_t>() + fs.off_nf, S->h_fl.as<uint8_t>() + fs.off_nf, fs.nf};
             max_len = std::max<int64_t>(max_len, fs.na * 4);
         }
         RSH_BHIP(launch_chain_flags_many(fe, (uint32_t)NF, max_nf, aux));
-        RSH_BHIP(launch_copy_many(sc, nsc, max_len, aux));
+        RSH_BHIP(launch_copy_many(sc, nfl, max_fl, aux));
+        RSH_BHIP(hipEventRecord(c->ev_flags, aux));
+        RSH_BHIP(launch_copy_many(sc + nfl, nsc - nfl, max_len, aux));
         RSH_BHIP(hipEventRecord(c->ev_spec, aux));
         return RSH_OK;
     };
@@ -853,6 +865,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         RSH_BHIP(hipEventSynchronize(c->ev_spec));
         if (getenv("RSH_SCAN_TRACE")) fprintf(stderr, "[rsh-batch] speculation landed at %.3f ms\n", ms_since(t0));
         b.landed.store(true);
+        b.aligned.store(true);
         for (FileScan& fs : files) fs.be.head = false;
     }
 
@@ -940,8 +953,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             spec_rc = launch_spec();
             spec_launched = true;
         }
-        if (spec_launched && spec_rc == RSH_OK && !b.landed.load() && hipEventQuery(c->ev_spec) == hipSuccess)
+        if (spec_launched && spec_rc == RSH_OK && !b.landed.load() && hipEventQuery(c->ev_flags) == hipSuccess)
             b.landed.store(true, std::memory_order_release);
+        if (spec_launched && spec_rc == RSH_OK && !b.aligned.load() && hipEventQuery(c->ev_spec) == hipSuccess)
+            b.aligned.store(true, std::memory_order_release);
         if (k1_launched && !b.landed.load()) {  // stop the speculation of files resolved since it started
             for (int32_t f = 0; f < NF; ++f) {
                 FileScan& fs = files[(size_t)f];
@@ -965,8 +980,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         if (!work.empty()) {
             e = serve_round(c, S, files, work);
         } else if (!b.landed.load()) {  // only waiting files: the speculation carries them
-            e = spec_launched ? hipEventSynchronize(c->ev_spec) : hipErrorInvalidValue;
+            e = spec_launched ? hipEventSynchronize(c->ev_flags) : hipErrorInvalidValue;
             if (e == hipSuccess) b.landed.store(true, std::memory_order_release);
+            if (e == hipSuccess && hipEventQuery(c->ev_spec) == hipSuccess) b.aligned.store(true, std::memory_order_release);
             if (trace) fprintf(stderr, "[rsh-batch] round %3d  waited for the speculation: %.3f ms\n", rounds, ms_since(t_serve));
         }
         if (trace) {

@@ -325,6 +325,7 @@ class HipBackend : public rsh::ScanBackend {
     // ---- phase-shifted speculation (resolver.h ScanBackend::phase_hint / phase_sums): K1 over [s0, n) with
     // the received header's B and dl, on the aux stream behind whatever runs there, one at a time ----
     int64_t ph_launches = 0;
+    double phase_ms = 0;  // the K1s of the phase speculations that landed
     void phase_hint(int64_t s) override {
         if (ph_s0_ >= 0 && s >= ph_s0_ && (s - ph_s0_) % B_ == 0 && s < ph_s0_ + ph_count_ * B_) return;  // covered
         ensure(s);
@@ -336,10 +337,12 @@ class HipBackend : public rsh::ScanBackend {
         CallTrace tr("phase_spec", s);
         ph_gen_ = ++c_->gen;
         ok(hipStreamWaitEvent(c_->aux, c_->ev_in, 0));
+        ok(hipEventRecord(c_->ev_pha, c_->aux));
         ok(rsh::launch_block_sums(x_ + s, std::min(n_ - s, count * B_), (uint32_t)B_, (uint32_t)count, (uint32_t)dl_,
                                   seed_word(seed_),
                                   c_->ph_weak.as<int32_t>(), c_->ph_strong.as<uint8_t>(), c_->aux,
                                   c_->abort_word + rsh_ctx::kPhaseWord, ph_gen_));
+        ok(hipEventRecord(c_->ev_phb, c_->aux));
         ok(hipMemcpyAsync(c_->h_pw.p, c_->ph_weak.p, (size_t)count * 4, hipMemcpyDeviceToHost, c_->aux));
         if (dl_ > 0)
             ok(hipMemcpyAsync(c_->h_ps.p, c_->ph_strong.p, (size_t)count * dl_, hipMemcpyDeviceToHost, c_->aux));
@@ -363,6 +366,8 @@ class HipBackend : public rsh::ScanBackend {
             }
             if (!ph_landed_) return false;
             bytes_read += std::min(n_ - ph_s0_, ph_count_ * B_);
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, c_->ev_pha, c_->ev_phb) == hipSuccess) phase_ms += ms;
         }
         v->s0 = ph_s0_;
         v->count = ph_count_;
@@ -733,6 +738,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         if (hipEventElapsedTime(&k1ms, c->ev_k1a, c->ev_k1b) == hipSuccess) res->stats.spec_kernel_ms = k1ms;
     }
     res->stats.phase_launches += be.ph_launches;
+    res->stats.phase_kernel_ms += be.phase_ms;
     return RSH_OK;
 }
 
@@ -800,6 +806,7 @@ int scan_tiled(rsh_ctx* c, const std::function<hipError_t(uint8_t*, int64_t, int
     res->stats.table_ms += table.sort_ms;
     res->stats.device_bytes += be.bytes_read;
     res->stats.phase_launches += be.ph_launches;
+    res->stats.phase_kernel_ms += be.phase_ms;
     res->stats.head_steps = be.tiles_loaded;  // tiled scans have no head mode: the count of tile loads
     return RSH_OK;
 }
@@ -865,7 +872,9 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
         hipEventCreateWithFlags(&c->ev_tab, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_phase, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_flags, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev_k1a) != hipSuccess || hipEventCreate(&c->ev_k1b) != hipSuccess ||
+        hipEventCreate(&c->ev_pha) != hipSuccess || hipEventCreate(&c->ev_phb) != hipSuccess ||
         hipExtMallocWithFlags(reinterpret_cast<void**>(&c->abort_word), 256, hipDeviceMallocUncached) != hipSuccess ||
         hipMemset(c->abort_word, 0, 256) != hipSuccess) {  // generations start at 1
         delete c;

@@ -106,7 +106,9 @@ struct rsh_ctx {
     DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw, partials, bucket;
     hipStream_t aux = nullptr;                   // table download, then the aligned speculation
     hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr, ev_phase = nullptr;
+    hipEvent_t ev_flags = nullptr;  // batched speculation: its chain flags are on the host (before its sums)
     hipEvent_t ev_k1a = nullptr, ev_k1b = nullptr;  // timing: the aligned speculation's K1 (stats)
+    hipEvent_t ev_pha = nullptr, ev_phb = nullptr;  // timing: the phase-shifted speculation's K1 (stats)
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
     PinnedBuf h_pw, h_ps;  // the phase-shifted speculation's sums (host copies)
     PinnedBuf h_lead;      // T(kB) of the first aligned windows (the speculation launch decision)
@@ -141,8 +143,11 @@ struct rsh_ctx {
         if (ev_tab) (void)hipEventDestroy(ev_tab);
         if (ev_spec) (void)hipEventDestroy(ev_spec);
         if (ev_phase) (void)hipEventDestroy(ev_phase);
+        if (ev_flags) (void)hipEventDestroy(ev_flags);
         if (ev_k1a) (void)hipEventDestroy(ev_k1a);
         if (ev_k1b) (void)hipEventDestroy(ev_k1b);
+        if (ev_pha) (void)hipEventDestroy(ev_pha);
+        if (ev_phb) (void)hipEventDestroy(ev_phb);
         if (aux) (void)hipStreamDestroy(aux);
         if (stream) (void)hipStreamDestroy(stream);
     }

@@ -149,7 +149,7 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
         aw = be.aligned_weak();
         as = be.aligned_strong();
         fl = be.chain_flags();
-        nflags = std::min<int64_t>(nal, table.chunk_count);
+        nflags = std::min<int64_t>(be.flags_count(), table.chunk_count);
         max_batch = be.max_batch();
     };
     refresh();

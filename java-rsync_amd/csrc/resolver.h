@@ -115,6 +115,8 @@ class ScanBackend {
     }
     // Aligned speculation over the source: window k = [kB, min(kB + B, n)), k < aligned_count().
     virtual int64_t aligned_count() = 0;
+    // Windows whose chain flag is known (the flags may land before the aligned sums they are computed from).
+    virtual int64_t flags_count() { return aligned_count(); }
     virtual const int32_t* aligned_weak() = 0;
     virtual const uint8_t* aligned_strong() = 0;  // digest_length bytes per window
     virtual const uint8_t* chain_flags() = 0;     // min(aligned_count, chunk_count) entries

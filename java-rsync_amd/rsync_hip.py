@@ -70,7 +70,8 @@ class ScanStats(ctypes.Structure):
                 ("device_ms", ctypes.c_double), ("resolver_ms", ctypes.c_double), ("table_ms", ctypes.c_double),
                 ("head_steps", ctypes.c_int64), ("speculation_aborted", ctypes.c_int64),
                 ("device_bytes", ctypes.c_int64), ("phase_launches", ctypes.c_int64),
-                ("phase_matches", ctypes.c_int64), ("spec_kernel_ms", ctypes.c_double)]
+                ("phase_matches", ctypes.c_int64), ("spec_kernel_ms", ctypes.c_double),
+                ("phase_kernel_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
