@@ -634,7 +634,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
 
     // per-file host state
     ScanFile* F = S->h_files.as<ScanFile>();
-    Batch b;
+    // shared with the worker threads, which are detached once every resolver is done (they then only wake,
+    // see quit and return: joining them would keep the call waiting for their exit)
+    auto bp = std::make_shared<Batch>();
+    Batch& b = *bp;
     b.files = &files;
     for (int32_t f = 0; f < NF; ++f) {
         FileScan& fs = files[(size_t)f];
@@ -884,7 +887,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     std::vector<std::thread> th;
     th.reserve((size_t)W);
     for (int32_t w = 0; w < W; ++w) {
-        th.emplace_back([&b, &files, w, NF, W] {
+        th.emplace_back([bp, &files, w, NF, W] {
+            Batch& b = *bp;
             uint64_t seen = 0;
             for (;;) {
                 {
@@ -983,7 +987,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             e = spec_launched ? hipEventSynchronize(c->ev_flags) : hipErrorInvalidValue;
             if (e == hipSuccess) b.landed.store(true, std::memory_order_release);
             if (e == hipSuccess && hipEventQuery(c->ev_spec) == hipSuccess) b.aligned.store(true, std::memory_order_release);
-            if (trace) fprintf(stderr, "[rsh-batch] round %3d  waited for the speculation: %.3f ms\n", rounds, ms_since(t_serve));
+            if (trace)
+                fprintf(stderr, "[rsh-batch] round %3d  waited for the speculation: %.3f ms (landed at %.3f ms)\n", rounds,
+                        ms_since(t_serve), ms_since(t0));
         }
         if (trace) {
             int kinds[5] = {0, 0, 0, 0, 0};
@@ -995,9 +1001,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 fmax = std::max(fmax, b.max_fiber_ms[(size_t)w]);
             }
             fprintf(stderr, "[rsh-batch] round %3d  pending %3zu (weak %d bytes %d win %d probe %d)  wait %.3f ms "
-                    "(host work: sum %.3f, max worker %.3f, max fiber %.3f)  serve %.3f ms%s\n",
+                    "(host work: sum %.3f, max worker %.3f, max fiber %.3f)  serve %.3f ms%s  at %.3f ms\n",
                     rounds, pend.size(), kinds[0], kinds[1], kinds[2], kinds[3], wait_ms, bsum, bmax, fmax,
-                    ms_since(t_serve), b.landed.load() ? "  [aligned]" : "");
+                    ms_since(t_serve), b.landed.load() ? "  [aligned]" : "", ms_since(t0));
             std::fill(b.busy_ms.begin(), b.busy_ms.end(), 0.0);
             std::fill(b.max_fiber_ms.begin(), b.max_fiber_ms.end(), 0.0);
         }
@@ -1015,7 +1021,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     }
     b.cv_work.notify_all();  // quit
     const double rounds_end_ms = ms_since(t0);
-    for (std::thread& t : th) t.join();
+    // every resolver is done and every worker idle: after quit a worker touches nothing but *bp
+    for (std::thread& t : th) t.detach();
     const double resolve_ms = ms_since(t0) - setup_ms;
     if (trace) {
         HostTimes tt;
