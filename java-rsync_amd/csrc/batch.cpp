@@ -1040,7 +1040,11 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 NF, enq_ms, setup_ms, rounds_end_ms, ms_since(t0));
 
     if (spec_launched) {
-        if (hipEventQuery(c->ev_spec) == hipErrorNotReady) {  // every resolver finished first: stop it
+        // every resolver finished before the speculation's K1 did: stop it.  (Once its flags have landed the
+        // K1 is done; the sums' download may still run on the aux stream, which the next call's work on that
+        // stream follows anyway.)
+        if (!b.landed.load() && hipEventQuery(c->ev_flags) == hipSuccess) b.landed.store(true);
+        if (!b.landed.load()) {
             // the batched K1's groups poll their own file's word (K1Group::abort), not the launch's: stop
             // every file not cancelled yet (those resolved in the last round included)
             for (int32_t f = 0; f < NF; ++f) {

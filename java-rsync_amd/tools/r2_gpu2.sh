@@ -8,8 +8,9 @@ timeout -k 10 900 python -u -m pytest $R/tests -m gpu -x -v --timeout 300 --time
 tail -n 16 $O/gpu_tests.log
 timeout -k 10 400 python $R/bench.py > $O/bench_default.log 2>&1 || { tail -n 20 $O/bench_default.log; exit 1; }
 timeout -k 10 300 python $R/bench.py --workload files --steps 3 --warmup 1 > $O/bench_files.log 2>&1 || { tail -n 20 $O/bench_files.log; exit 1; }
+timeout -k 10 300 python $R/bench.py --workload files --variant half --steps 3 --warmup 1 --no-cpu-baseline > $O/bench_files_half.log 2>&1 || { tail -n 20 $O/bench_files_half.log; exit 1; }
 RSH_SCAN_TRACE=1 timeout -k 10 300 python $R/bench.py --workload files --steps 1 --warmup 1 --no-cpu-baseline > $O/trace_files.log 2>&1 || exit 1
-if [ -n "$SKIP_PROF" ]; then for f in $O/bench_default.log $O/bench_files.log; do tail -n 1 $f | cut -c 1-300; done; exit 0; fi
+if [ -n "$SKIP_PROF" ]; then for f in $O/bench_default.log $O/bench_files.log $O/bench_files_half.log; do tail -n 1 $f | cut -c 1-300; done; exit 0; fi
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_default -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-companions > $O/prof_default.log 2>&1 || exit 1
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/fetch_default -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-companions > $O/fetch_default.log 2>&1 || exit 1
