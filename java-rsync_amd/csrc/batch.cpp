@@ -122,9 +122,13 @@ hipError_t pin(PinnedBuf& b, int64_t count, T** out) {
 // Sender batch
 // ------------------------------------------------------------------------------------------------
 struct Req {
-    enum Kind { WEAK, BYTES, WIN, PROBE, WAIT } kind = WEAK;  // WAIT: until the speculation lands (no device work)
-    const int64_t* pos = nullptr;  // WEAK / BYTES
+    // WAIT: until the speculation lands (no device work); FLUSH: WEAK at pos + BYTES at pos2 (one round trip)
+    enum Kind { WEAK, BYTES, WIN, PROBE, WAIT, FLUSH } kind = WEAK;
+    const int64_t* pos = nullptr;  // WEAK / BYTES / FLUSH (weak sums)
     int64_t count = 0;
+    const int64_t* pos2 = nullptr;  // FLUSH: byte positions
+    int64_t count2 = 0;
+    uint8_t* out_b2 = nullptr;
     int32_t* out_w = nullptr;
     uint8_t* out_b = nullptr;
     int64_t p = 0, w = 0;          // WIN: window [p, p + w) lands at win
@@ -174,6 +178,8 @@ class BatchBackend : public ScanBackend {
     const uint8_t* chain_flags() override { return fl; }
     void weak_many(const int64_t* pos, int64_t count, int32_t* out) override;
     void bytes_many(const int64_t* pos, int64_t count, uint8_t* out) override;
+    void flush_gather(const int64_t* tpos, int64_t nt, int32_t* tv, const int64_t* bpos, int64_t nb,
+                      uint8_t* bv) override;
     void md5_at(int64_t p, uint8_t out[16]) override;
     int64_t first_hit(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) override;
 };
@@ -233,6 +239,29 @@ struct Batch {
 };
 
 FileScan& scan_of(Batch* b, int32_t f) { return (*b->files)[(size_t)f]; }
+
+// The cores this process may use: its affinity mask, capped by a cgroup CPU quota (cgroup v2 cpu.max,
+// "quota period"; containers often see every CPU of the machine in the mask but get a few cores' worth of
+// time).  More spinning workers than that get throttled by the scheduler for whole periods.
+int host_cores() {
+    static const int v = [] {
+        int n = 8;
+        cpu_set_t cpus;
+        if (sched_getaffinity(0, sizeof(cpus), &cpus) == 0) n = CPU_COUNT(&cpus);
+        if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {0};
+            long long period = 0;
+            if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+                const long long quota = atoll(q);
+                if (quota > 0) n = std::min<int>(n, (int)std::max<long long>(1, quota / period));
+            }
+            fclose(f);
+        }
+        if (const char* e = getenv("RSH_HOST_CORES")) n = std::max(1, atoi(e));  // explicit override
+        return n;
+    }();
+    return v;
+}
 
 int64_t BatchBackend::aligned_count() { return (head || !b->aligned.load(std::memory_order_acquire)) ? 0 : na; }
 
@@ -311,6 +340,25 @@ void BatchBackend::bytes_many(const int64_t* pos, int64_t count, uint8_t* out) {
     b->post(fs);
 }
 
+void BatchBackend::flush_gather(const int64_t* tpos, int64_t nt, int32_t* tv, const int64_t* bpos, int64_t nb,
+                                uint8_t* bv) {
+    if (nt <= 0 || nb <= 0) {
+        ScanBackend::flush_gather(tpos, nt, tv, bpos, nb, bv);
+        return;
+    }
+    bytes_read += nt * B + nb;
+    FileScan& fs = scan_of(b, f);
+    fs.req = Req{};
+    fs.req.kind = Req::FLUSH;
+    fs.req.pos = tpos;
+    fs.req.count = nt;
+    fs.req.out_w = tv;
+    fs.req.pos2 = bpos;
+    fs.req.count2 = nb;
+    fs.req.out_b2 = bv;
+    b->post(fs);
+}
+
 // bytes copied per window request (A/B switch RSH_BATCH_READAHEAD; never less than the window).  Off by
 // default: on config 4 it cut the rounds from 23 to 18, but the head-mode rounds it removed were cheap
 // window copies and the probes left in their place wait behind the speculation K1
@@ -382,6 +430,7 @@ int64_t BatchBackend::first_hit(const ProbeInterval* iv, int64_t count, const st
     b->post(fs);
     const int64_t p = fs.req.result;
     if (count == 1 && fs.req.out) cache.fill(iv[0], keys, *fs.req.out, n - B);
+    else if (fs.req.out) cache.fill_batch(iv, count, keys, *fs.req.out, n - B);
     else cache.valid = false;
     if (p < 0) return -1;
     window_slots(*fs.req.out, 1, win_pos);
@@ -424,6 +473,14 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
             case Req::BYTES:
                 gb_at[(size_t)f] = (int64_t)gb.size();
                 for (int64_t i = 0; i < r.count; ++i) gb.push_back(GatherEnt{r.pos[i], f, 0});
+                break;
+            case Req::FLUSH:
+                gw_at[(size_t)f] = (int64_t)gw.size();
+                for (int64_t i = 0; i < r.count; ++i) gw.push_back(GatherEnt{r.pos[i], f, 0});
+                gb_at[(size_t)f] = (int64_t)gb.size();
+                for (int64_t i = 0; i < r.count2; ++i) gb.push_back(GatherEnt{r.pos2[i], f, 0});
+                break;
+            case Req::WAIT:
                 break;
             case Req::WIN:
                 win_at[(size_t)f] = win_bytes;
@@ -552,6 +609,12 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
                 break;
             case Req::BYTES:
                 for (int64_t i = 0; i < r.count; ++i) r.out_b[i] = e == hipSuccess ? hob[gb_at[(size_t)f] + i] : 0;
+                break;
+            case Req::FLUSH:
+                for (int64_t i = 0; i < r.count; ++i) r.out_w[i] = e == hipSuccess ? how[gw_at[(size_t)f] + i] : 0;
+                for (int64_t i = 0; i < r.count2; ++i) r.out_b2[i] = e == hipSuccess ? hob[gb_at[(size_t)f] + i] : 0;
+                break;
+            case Req::WAIT:
                 break;
             case Req::WIN:
                 r.win = hwin + win_at[(size_t)f];
@@ -872,9 +935,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         for (FileScan& fs : files) fs.be.head = false;
     }
 
-    cpu_set_t cpus;
-    int ncpu = 8;
-    if (sched_getaffinity(0, sizeof(cpus), &cpus) == 0) ncpu = CPU_COUNT(&cpus);
+    const int ncpu = host_cores();
     // spinning waiters: one core stays free for the coordinator
     const int32_t ncores = (spin_us() > 0 && ncpu > 2) ? ncpu - 1 : ncpu;
     const int32_t W = std::max<int32_t>(1, std::min<int32_t>({NF, ncores, kMaxWorkers}));
@@ -992,7 +1053,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                         ms_since(t_serve), ms_since(t0));
         }
         if (trace) {
-            int kinds[5] = {0, 0, 0, 0, 0};
+            int kinds[6] = {0, 0, 0, 0, 0, 0};
             for (int32_t f : pend) kinds[files[(size_t)f].req.kind]++;
             double bsum = 0, bmax = 0, fmax = 0;
             for (int32_t w = 0; w < b.nworkers; ++w) {
@@ -1000,9 +1061,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 bmax = std::max(bmax, b.busy_ms[(size_t)w]);
                 fmax = std::max(fmax, b.max_fiber_ms[(size_t)w]);
             }
-            fprintf(stderr, "[rsh-batch] round %3d  pending %3zu (weak %d bytes %d win %d probe %d)  wait %.3f ms "
+            fprintf(stderr, "[rsh-batch] round %3d  pending %3zu (weak %d bytes %d win %d probe %d flush %d)  wait %.3f ms "
                     "(host work: sum %.3f, max worker %.3f, max fiber %.3f)  serve %.3f ms%s  at %.3f ms\n",
-                    rounds, pend.size(), kinds[0], kinds[1], kinds[2], kinds[3], wait_ms, bsum, bmax, fmax,
+                    rounds, pend.size(), kinds[0], kinds[1], kinds[2], kinds[3], kinds[5], wait_ms, bsum, bmax, fmax,
                     ms_since(t_serve), b.landed.load() ? "  [aligned]" : "", ms_since(t0));
             std::fill(b.busy_ms.begin(), b.busy_ms.end(), 0.0);
             std::fill(b.max_fiber_ms.begin(), b.max_fiber_ms.end(), 0.0);

@@ -170,6 +170,28 @@ class HipBackend : public rsh::ScanBackend {
         ok(hipStreamSynchronize(c_->stream));
         memcpy(out, ho, (size_t)count);
     }
+    void flush_gather(const int64_t* tpos, int64_t nt, int32_t* tv, const int64_t* bpos, int64_t nb,
+                      uint8_t* bv) override {
+        if (nt <= 0 || nb <= 0) {
+            ScanBackend::flush_gather(tpos, nt, tv, bpos, nb, bv);
+            return;
+        }
+        CallTrace tr("flush_gather", nt);
+        ensure(std::min(*std::min_element(tpos, tpos + nt), *std::min_element(bpos, bpos + nb)));
+        bytes_read += nt * B_ + nb;
+        rsh::GatherEnt* hp = pin<rsh::GatherEnt>(c_->h_pos, nt + nb);
+        int32_t* ho = pin<int32_t>(c_->h_out, nt + (nb + 3) / 4);
+        rsh::ScanFile* F = file();
+        if (err != hipSuccess) return;
+        for (int64_t i = 0; i < nt; ++i) hp[i] = rsh::GatherEnt{tpos[i], 0, 0};
+        for (int64_t i = 0; i < nb; ++i) hp[nt + i] = rsh::GatherEnt{bpos[i], 0, 0};
+        uint8_t* hb = reinterpret_cast<uint8_t*>(ho + nt);
+        ok(rsh::launch_window_weak(F, hp, (uint32_t)nt, ho, c_->stream));
+        ok(rsh::launch_gather_bytes(F, hp + nt, (uint32_t)nb, hb, c_->stream));
+        ok(hipStreamSynchronize(c_->stream));
+        memcpy(tv, ho, (size_t)nt * sizeof(int32_t));
+        memcpy(bv, hb, (size_t)nb);
+    }
     // A single window's digest is one serial MD5 chain: 64-wide waves give it nothing, so the rare
     // resolver misses (first table hit after a reset) are digested on the host from a D2H copy.
     void md5_at(int64_t p, uint8_t out[16]) override {
@@ -302,7 +324,7 @@ class HipBackend : public rsh::ScanBackend {
                           c_->stream));
         ok(hipStreamSynchronize(c_->stream));
         if (count == 1) cache_.fill(iv[0], keys, *hf, n_ - B_);
-        else cache_.valid = false;
+        else cache_.fill_batch(iv, count, keys, *hf, n_ - B_);
         if (hf->first == ~0ull) return -1;
         rsh::window_slots(*hf, kScanWindows, win_pos_);
         for (int k = 1; k < kScanWindows; ++k)

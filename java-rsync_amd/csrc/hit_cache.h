@@ -96,6 +96,30 @@ struct HitCache {
         *a2 = b;
         return 0;
     }
+    // After a probe over several intervals (the batched flush chain): the resolver's next question is the
+    // first hit inside the interval that holds the first hit, with that interval's key function -- keep
+    // that interval's hits (all of them when the list is complete, else the first).
+    void fill_batch(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* ks, const ProbeOut& o,
+                    int64_t n_minus_B) {
+        valid = false;
+        if (o.first == ~0ull) return;
+        const int64_t p = (int64_t)o.first;
+        for (int64_t j = 0; j < count; ++j) {
+            if (p < iv[j].a || p >= iv[j].b) continue;
+            ProbeOut one = o;  // the listed hits of interval j only (keys follow each interval's own E)
+            if (o.count <= (unsigned long long)PROBE_HITS_CAP) {
+                one.count = 0;
+                for (unsigned long long i = 0; i < o.count; ++i)
+                    if ((int64_t)o.pos[i] >= iv[j].a && (int64_t)o.pos[i] < iv[j].b) {
+                        one.pos[one.count] = o.pos[i];
+                        one.key[one.count] = o.key[i];
+                        ++one.count;
+                    }
+            }
+            fill(iv[j], ks, one, n_minus_B);
+            return;
+        }
+    }
     void fill(const ProbeInterval& iv, const std::vector<int32_t>* ks, const ProbeOut& o, int64_t n_minus_B) {
         nB = n_minus_B;
         valid = true;

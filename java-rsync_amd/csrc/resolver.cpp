@@ -414,8 +414,7 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
             }
             std::vector<int32_t> tv(tpos.size());
             std::vector<uint8_t> bv(bpos.size());
-            be.weak_many(tpos.data(), (int64_t)tpos.size(), tv.data());
-            be.bytes_many(bpos.data(), (int64_t)bpos.size(), bv.data());
+            be.flush_gather(tpos.data(), (int64_t)tpos.size(), tv.data(), bpos.data(), (int64_t)bpos.size(), bv.data());
             // host chain: state after each flush, the interval it opens
             struct Step {
                 int64_t s2;

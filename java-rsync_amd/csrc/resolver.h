@@ -141,6 +141,14 @@ class ScanBackend {
         return b;
     }
 
+    // The batched flush chain's gather: weak sums at tpos and bytes at bpos, in one device round trip where
+    // the backend can.
+    virtual void flush_gather(const int64_t* tpos, int64_t nt, int32_t* tv, const int64_t* bpos, int64_t nb,
+                              uint8_t* bv) {
+        weak_many(tpos, nt, tv);
+        bytes_many(bpos, nb, bv);
+    }
+
     int32_t weak_at(int64_t p) {
         int32_t r;
         weak_many(&p, 1, &r);

@@ -93,6 +93,25 @@ class CpuBackend : public rsh::ScanBackend {
             cache.fill(one, keys, o, n_ - B_);
             return o.first == ~0ull ? -1 : (int64_t)o.first;
         }
+        if (use_cache) {  // several intervals: list every hit as the kernel does, keep the first's interval
+            rsh::ProbeOut o;
+            o.first = ~0ull;
+            o.count = 0;
+            for (int64_t i = 0; i < count; ++i)
+                for (int64_t a = iv[i].a; a < iv[i].b;) {
+                    const int64_t p1 = first_hit1(a, iv[i].b, iv[i].anchor, iv[i].e_lo, iv[i].e_hi, keys);
+                    if (p1 < 0) break;
+                    if (o.first == ~0ull) o.first = (unsigned long long)p1;
+                    if (o.count < (unsigned long long)rsh::PROBE_HITS_CAP) {
+                        o.pos[o.count] = (unsigned long long)p1;
+                        o.key[o.count] = (uint32_t)last_key_;
+                    }
+                    ++o.count;
+                    a = p1 + 1;
+                }
+            cache.fill_batch(iv, count, keys, o, n_ - B_);
+            return o.first == ~0ull ? -1 : (int64_t)o.first;
+        }
         for (int64_t i = 0; i < count; ++i) {
             const int64_t p = first_hit1(iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo, iv[i].e_hi, keys);
             if (p >= 0) return p;  // intervals are in increasing position order
