@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <functional>
 #include <memory>
 #include <vector>
 
@@ -213,6 +214,10 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                 const uint8_t* d_strong, const int32_t* host_weak, const uint8_t* host_strong, const uint8_t seed[4],
                 rsh::ResolveResult* res);
 int emit_events(rsh_ctx* c, rsh::ResolveResult& r, rsh_event* ev, int64_t cap, int64_t* n_ev);
+// capi.cpp: the scan with HBM holding one tile of the source at a time (fill copies source bytes to HBM).
+int scan_tiled(rsh_ctx* c, const std::function<hipError_t(uint8_t*, int64_t, int64_t)>& fill, int64_t n,
+               const rsh_header* h, const int32_t* d_weak, const uint8_t* d_strong, const int32_t* host_weak,
+               const uint8_t* host_strong, const uint8_t seed[4], int64_t tile_bytes, rsh::ResolveResult* res);
 
 // Primes the resolver's table with the buckets the device computed with a probe (device.h HIT_BUCKET_INTS
 // layout, copied to the host): the first hit's, and each listed hit's when it fits LISTED_IDX entries.

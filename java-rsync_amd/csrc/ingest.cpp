@@ -8,6 +8,7 @@
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -67,6 +68,7 @@ class PieceReader {
         cv_.notify_all();
     }
     bool read_error() const { return error_at_ < size_; }
+    int fd() const { return fd_; }
 
   private:
     void run() {
@@ -186,6 +188,81 @@ int rsh_block_sums_file(rsh_ctx* ctx, const char* path, int64_t size, const rsh_
     return RSH_OK;
 }
 
+// Sources above this size are scanned tiled (scan_tiled): HBM then holds one kFileTile tile at a time.
+constexpr int64_t kFileTileAbove = 32LL << 30;
+constexpr int64_t kFileTile = 4LL << 30;
+
+namespace rsh {
+namespace {
+// The tiled file scan: the tiles are read with pread into a pinned buffer and copied to HBM; the whole-file
+// digest runs on its own thread over a second, sequential pass of the file (served by the page cache).  Both
+// apply FileView's rule: exactly `size` bytes, zero from the first short read or error on (read_error).
+int match_scan_file_tiled(rsh_ctx* ctx, int fd, const char* path, int64_t size, const rsh_header* h,
+                          const int32_t* weak, const uint8_t* strong, const uint8_t seed[4], rsh::ResolveResult* r,
+                          uint8_t file_md5[16], bool* read_error) {
+    const int64_t C = h->chunk_count, dl = h->digest_length;
+    std::atomic<int64_t> err_at{INT64_MAX};
+    auto read_at = [&](int rfd, uint8_t* dst, int64_t off, int64_t len) {
+        int64_t p = 0;
+        while (p < len && off + p < err_at.load()) {
+            const ssize_t k = pread(rfd, dst + p, (size_t)(len - p), (off_t)(off + p));
+            if (k < 0 && errno == EINTR) continue;
+            if (k <= 0) {
+                int64_t cur = err_at.load();
+                while (off + p < cur && !err_at.compare_exchange_weak(cur, off + p)) {
+                }
+                break;
+            }
+            p += k;
+        }
+        const int64_t z = std::max<int64_t>(0, std::min(len, err_at.load() - off));
+        if (z < len) memset(dst + z, 0, (size_t)(len - z));
+    };
+    std::thread md5_thread([&] {
+        const int mfd = ::open(path, O_RDONLY | O_CLOEXEC);
+        std::vector<uint8_t> buf((size_t)std::min<int64_t>(size, kScanPiece));
+        HostMd5 m;
+        for (int64_t off = 0; off < size; off += kScanPiece) {
+            const int64_t len = std::min<int64_t>(kScanPiece, size - off);
+            if (mfd >= 0) read_at(mfd, buf.data(), off, len);
+            else memset(buf.data(), 0, (size_t)len);
+            m.update(buf.data(), (size_t)len);
+        }
+        m.final(file_md5);
+        if (mfd >= 0) close(mfd);
+    });
+    int rc = RSH_OK;
+    hipError_t e = ctx->h_stage.ensure((size_t)kScanPiece);
+    if (e == hipSuccess) e = ctx->weak.ensure((size_t)C * 4 + 4);
+    if (e == hipSuccess) e = ctx->strong.ensure((size_t)(C * dl + 1));
+    if (e == hipSuccess && C > 0) e = hipMemcpyAsync(ctx->weak.p, weak, (size_t)C * 4, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess && C > 0 && dl > 0)
+        e = hipMemcpyAsync(ctx->strong.p, strong, (size_t)(C * dl), hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) {
+        note_error(e, __LINE__, "ingest.cpp");
+        rc = RSH_E_DEVICE;
+    } else {
+        auto fill = [&](uint8_t* dst, int64_t off, int64_t len) -> hipError_t {  // piece by piece, pinned
+            for (int64_t p = 0; p < len; p += kScanPiece) {
+                const int64_t l = std::min<int64_t>(kScanPiece, len - p);
+                read_at(fd, ctx->h_stage.as<uint8_t>(), off + p, l);
+                hipError_t e2 = hipMemcpyAsync(dst + p, ctx->h_stage.p, (size_t)l, hipMemcpyHostToDevice, ctx->stream);
+                if (e2 == hipSuccess) e2 = hipStreamSynchronize(ctx->stream);
+                if (e2 != hipSuccess) return e2;
+            }
+            return hipSuccess;
+        };
+        const int64_t tile = getenv("RSH_FILE_TILE") ? atoll(getenv("RSH_FILE_TILE")) : kFileTile;
+        rc = scan_tiled(ctx, fill, size, h, ctx->weak.as<int32_t>(), ctx->strong.as<uint8_t>(), weak, strong, seed,
+                        tile, r);
+    }
+    md5_thread.join();
+    *read_error = err_at.load() < size;
+    return rc;
+}
+}  // namespace
+}  // namespace rsh
+
 int rsh_match_scan_file(rsh_ctx* ctx, const char* path, int64_t size, const rsh_header* h, const int32_t* weak,
                         const uint8_t* strong, const uint8_t seed[4], rsh_event* ev, int64_t ev_cap, int64_t* n_ev,
                         uint8_t file_md5[16], int64_t* literal, int64_t* matched, rsh_scan_stats* stats,
@@ -201,6 +278,19 @@ int rsh_match_scan_file(rsh_ctx* ctx, const char* path, int64_t size, const rsh_
     if (h->block_length > 0 && C > 0 && (!weak || (!strong && dl > 0))) return RSH_E_INVAL;
     RSH_CLAIM(ctx);
     RSH_HIP(hipSetDevice(ctx->device));
+    // A/B and test switches (read per call): RSH_FILE_TILE_ABOVE (bytes) and RSH_FILE_TILE (tile bytes)
+    const int64_t tile_above = getenv("RSH_FILE_TILE_ABOVE") ? atoll(getenv("RSH_FILE_TILE_ABOVE")) : kFileTileAbove;
+    if (h->block_length > 0 && size > tile_above) {  // larger than we keep in HBM whole: tiled
+        rsh::ResolveResult r;
+        bool rerr = false;
+        const int rc = rsh::match_scan_file_tiled(ctx, rd.fd(), path, size, h, weak, strong, seed, &r, file_md5, &rerr);
+        if (rc != RSH_OK) return rc;
+        if (read_error) *read_error = rerr ? 1 : 0;
+        if (literal) *literal = r.literal;
+        if (matched) *matched = r.matched;
+        if (stats) *stats = r.stats;
+        return emit_events(ctx, r, ev, ev_cap, n_ev);
+    }
     const int64_t piece = kScanPiece;
     RSH_HIP(ctx->h_stage.ensure((size_t)(kBuffers * piece)));
     RSH_HIP(ctx->data.ensure((size_t)std::max<int64_t>(size, 1)));

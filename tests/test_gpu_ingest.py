@@ -86,3 +86,26 @@ def test_open_errors(ctx, tmp_path):
         os.chmod(p, 0)
         with pytest.raises(R.FileViewOpenFailed):
             ctx.block_sums_file(p, 1000, h, SEED)
+
+
+@pytest.mark.parametrize("short", [False, True])
+def test_file_scan_tiled(ctx, tmp_path, monkeypatch, short):
+    """Files above RSH_FILE_TILE_ABOVE (32 GiB by default; lowered here) are scanned with HBM holding one tile
+    at a time (scan_tiled), read piece by piece from the file, the whole-file digest on its own pass: same
+    events and digest as the oracle, FileView's zero fill and read_error included."""
+    monkeypatch.setenv("RSH_FILE_TILE_ABOVE", str(1 << 20))
+    monkeypatch.setenv("RSH_FILE_TILE", str(1 << 20))
+    B = 4096
+    n = (24 << 20) + 123
+    basis = O.splitmix(n, 0x7711).tobytes()
+    src = basis[:5 << 20] + O.splitmix(5000, 0x7712).tobytes() + basis[5 << 20:]
+    size = len(src) + (3 * B + 7 if short else 0)  # the FileInfo size; a short file is zero-filled
+    view = src + bytes(size - len(src))
+    p = _write(tmp_path, "big", src)
+    h = R.header_make(B, 3, n)
+    ow, os_ = O.generator(basis, O.header(B, 3, n), SEED)
+    ev, fm, lit, mat, st, err = ctx.match_scan_file(p, size, h, ow, os_, SEED)
+    oev, ofm, olit, omat, _ = O.sender(view, O.header(B, 3, n), ow, os_, SEED)
+    assert err == short
+    assert R.events_as_tuples(ev, B) == [tuple(e) for e in oev] and (fm, lit, mat) == (ofm, olit, omat)
+    assert st["head_steps"] >= 20  # tile loads

@@ -231,6 +231,35 @@ def test_sender_tiled_matches_oracle(ctx, seed_i):
             assert st["head_steps"] >= 2  # tile loads
 
 
+def test_contexts_per_thread_on_every_device():
+    """The JNI binding's design (NativeChecksum.forThread: one context per calling thread, device = thread id
+    mod rsync.hip.devices; RsyncClient.java:431 runs Generator and Sender on separate threads): 2 threads per
+    visible device, each creating its own context on its device, run a Generator pass and a scan there; every
+    result equals the oracle's.  On a one-GPU box all threads share device 0."""
+    import ctypes
+    import concurrent.futures as cf
+    cnt = ctypes.c_int()
+    assert R.lib().rsh_device_count(ctypes.byref(cnt)) == 0 and cnt.value >= 1
+    ndev = cnt.value
+    B, dl = 1024, 3
+
+    def work(t):
+        basis = O.splitmix(150 * B + 7 * t, 900 + t).tobytes()
+        src = basis[:40 * B] + O.splitmix(333 + t, 950 + t).tobytes() + basis[40 * B:]
+        h = O.header(B, dl, len(basis))
+        ow, os_ = O.generator(basis, h, SEED)
+        oev, ofm, olit, omat, _ = O.sender(src, h, ow, os_, SEED)
+        with R.Context(t % ndev) as c:
+            rh = R.Header(**h.as_dict())
+            gw, gs = c.block_sums(basis, rh, SEED)
+            ev, fm, lit, mat, _ = c.match_scan(src, rh, gw, gs, SEED)
+        return (np.array_equal(gw, ow) and np.array_equal(gs, os_) and
+                R.events_as_tuples(ev, B) == [tuple(e) for e in oev] and (fm, lit, mat) == (ofm, olit, omat))
+
+    with cf.ThreadPoolExecutor(2 * ndev) as ex:
+        assert all(ex.map(work, range(2 * ndev)))
+
+
 def test_device_fill_matches_oracle(ctx):
     n = (1 << 20) + 13
     d = ctx.alloc(n)
