@@ -76,7 +76,14 @@ class HipBackend : public rsh::ScanBackend {
     std::vector<uint8_t> haw_ready;
     std::function<void(uint8_t*)> md5_0;  // digest of window 0 (joins its host thread)
 
-    int64_t aligned_count() override { return tiled ? aligned_end : head ? 0 : na; }
+    int64_t aligned_count() override {  // the sums land after the flags (ev_spec after ev_flags)
+        if (tiled) return aligned_end;
+        if (head) return 0;
+        if (!sums_ready) sums_ready = hipEventQuery(c_->ev_spec) == hipSuccess;
+        return sums_ready ? na : 0;
+    }
+    int64_t flags_count() override { return tiled ? aligned_end : head ? 0 : na; }
+    bool sums_ready = false;
     int64_t max_batch() override { return head ? 4 : 4096; }
     int64_t max_batch_at(int64_t f) override {  // a batch's intervals, bytes and windows stay in the tile
         if (!tiled) return max_batch();
@@ -527,14 +534,14 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     RSH_HIP(c->h_lead.ensure(lead_ents_at + (size_t)(nsamp + 1) * sizeof(rsh::GatherEnt) + sizeof(rsh::ScanFile)));
 
     RSH_HIP(hipEventRecord(c->ev_in, c->stream));  // whatever produced the inputs on the caller's stream
-    // (aux) the received table
+    // (stream) the received table: on the context stream, so that the aux stream's speculation launch
+    // (below) does not queue behind the download
     if (download) {
-        RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
         if (C > 0) {
-            RSH_HIP(hipMemcpyAsync(c->h_weak.p, d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, c->aux));
-            if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_strong.p, d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, c->aux));
+            RSH_HIP(hipMemcpyAsync(c->h_weak.p, d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, c->stream));
+            if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_strong.p, d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, c->stream));
         }
-        RSH_HIP(hipEventRecord(c->ev_tab, c->aux));
+        RSH_HIP(hipEventRecord(c->ev_tab, c->stream));
         host_weak = c->h_weak.as<int32_t>();
         host_strong = c->h_strong.as<uint8_t>();
     }
@@ -549,7 +556,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     auto launch_spec = [&]() -> int {
         const int64_t sn = std::min<int64_t>(n, spec_na * B);  // bytes: whole windows, or to the end
         const int64_t snf = std::min<int64_t>(spec_na, C);
-        if (!download) RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
+        RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
         RSH_HIP(hipEventRecord(c->ev_k1a, c->aux));
         RSH_HIP(rsh::launch_block_sums(d_src, sn, (uint32_t)B, (uint32_t)spec_na, (uint32_t)dl, seed_word(seed),
                                        c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->aux,
@@ -557,10 +564,12 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         RSH_HIP(hipEventRecord(c->ev_k1b, c->aux));
         RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
                                         (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(), c->aux));
+        // the flags first (a run of matches needs nothing else), then the sums (aligned lookups off the run)
+        if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, c->aux));
+        RSH_HIP(hipEventRecord(c->ev_flags, c->aux));
         RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)spec_na * 4, hipMemcpyDeviceToHost, c->aux));
         if (dl > 0)
             RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)spec_na * dl, hipMemcpyDeviceToHost, c->aux));
-        if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, c->aux));
         RSH_HIP(hipEventRecord(c->ev_spec, c->aux));
         return RSH_OK;
     };
@@ -713,10 +722,10 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         }
         if (spec_wait) {  // head-mode steps beside the launch would only slow it down
             CallTrace tw("spec_wait", res->stats.head_steps);
-            landed = hipEventSynchronize(c->ev_spec) == hipSuccess;
+            landed = hipEventSynchronize(c->ev_flags) == hipSuccess;
             return true;
         }
-        landed = hipEventQuery(c->ev_spec) != hipErrorNotReady;
+        landed = hipEventQuery(c->ev_flags) != hipErrorNotReady;
         if (!landed) res->stats.head_steps++;
         return landed;
     });
@@ -729,7 +738,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         // the stopped launch's waves leave within two stages; later work on this context starts after them
         if (tentative_stopped) RSH_HIP(hipStreamWaitEvent(c->stream, c->ev_spec, 0));
         res->stats.device_ms += ms_since(t0);
-    } else if (done && !landed && hipEventQuery(c->ev_spec) == hipErrorNotReady) {
+    } else if (done && !landed && hipEventQuery(c->ev_flags) == hipErrorNotReady) {
         RSH_HIP(hipStreamWriteValue32(c->stream, c->abort_word, (uint32_t)gen, 0));  // the rest is dead work
         // Later work on this context starts only once the stopped launch has left the CUs: K1 fills every
         // wave slot of the chip exactly once (2 per SIMD at 16 GiB, B = 128 KiB), and a launch that finds
@@ -738,7 +747,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         res->stats.speculation_aborted = 1;
         res->stats.device_ms += ms_since(t0);
     } else {
-        RSH_HIP(hipEventSynchronize(c->ev_spec));
+        RSH_HIP(hipEventSynchronize(c->ev_flags));  // the sums follow on aux; aligned_count() polls ev_spec
         res->stats.device_ms += ms_since(t0);
         res->stats.speculation_aborted = 0;
         spec_read = true;
