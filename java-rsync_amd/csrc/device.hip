@@ -106,6 +106,21 @@ __device__ __forceinline__ void load_block(const uint8_t* p, uint4 (&q)[4]) {
         const uint32_t* v = reinterpret_cast<const uint32_t*>(p);
 #pragma unroll
         for (int i = 0; i < 4; ++i) q[i] = make_uint4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+    } else if constexpr (ALIGN == 0) {
+        // any alignment: the 16 or 17 aligned dwords that hold the 64 bytes, funnel-shifted (v_alignbyte_b32);
+        // the 17th is read only when the block is not dword aligned, so no byte past p + 63's dword is touched
+        const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
+        const uint32_t* v = reinterpret_cast<const uint32_t*>(pa & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(pa & 3);
+        uint32_t d[17];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) d[i] = v[i];
+        d[16] = sh ? v[16] : 0u;
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
     } else {
         uint32_t w[16];
 #pragma unroll
@@ -188,7 +203,9 @@ __global__ __launch_bounds__(64) void block_sums_lane_batch_kernel(const K1Lane*
     const K1Lane e = lanes[blockIdx.x];
     const uint32_t c = e.c_first + threadIdx.x;
     if (c >= e.nchunks) return;
-    lane_chunk_sums<ALIGN, ALIGN == 16 ? 4 : ALIGN == 4 ? 2 : 1>(e.data, e.n, e.B, c, e.dl, seed, e.weak, e.strong);
+    // byte-aligned files read through the funnel-shift form (ALIGN 0), 4 blocks ahead
+    lane_chunk_sums<ALIGN == 1 ? 0 : ALIGN, ALIGN == 16 ? 4 : ALIGN == 4 ? 2 : 4, ALIGN != 1>(e.data, e.n, e.B, c, e.dl,
+                                                                                          seed, e.weak, e.strong);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -634,6 +651,216 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
     store_digest(strong_out + (size_t)c * dl, st, dl);
 }
 
+#ifndef RSH_K1_SHIFT_VGPR
+#define RSH_K1_SHIFT_VGPR 256  // 2 waves/SIMD (the LDS ring and the MFMA tiles of the aligned kernel, plus the funnel)
+#endif
+// ------------------------------------------------------------------------------------------------
+// K1 at a base that is not 128-B aligned.  The Sender's phase-shifted speculation runs K1 over src + s0 for
+// any s0; the pipelined kernel's dwordx4 loads at such a base straddle 128-B lines (every 8-lane row touches
+// two) and ran at 0.6x of the aligned rate (kbench, 16 GiB at B = 128 KiB: 4.95 ms at offsets 1 and 8 against
+// 3.0 ms).  Here every load stays line-aligned: line u of a chunk is its bytes [128u - a, 128u - a + 128),
+// a = base % 128, read from base - a; a chunk spans lines 0..nst.
+//  * LDS: each chunk row is a two-line ring (16 slots + 1 pad slot), line u in half u & 1.
+//  * MD5 stage t (chunk bytes [128t, 128t + 128)) is ring bytes [(128t + a) mod 256, +128): lines t and t + 1,
+//    so MD5 runs one step behind the loads.  Step u writes line u + 1 only after reading stage u - 1's
+//    block-1 words (lines u - 1 and u; a wave's LDS operations execute in order).  A block's words come from
+//    5 slots at slot offset a >> 4 (mod 16) and are funnel-shifted by a & 15 bytes: dword offset
+//    W = (a >> 2) & 3 (template), byte shift a & 3 (v_alignbyte_b32).
+//  * Weak sums: the MFMAs sum whole lines 0..nst in the aligned kernel's operand layout; line 0's bytes before
+//    the chunk (a) and line nst's bytes after it (128 - a) are subtracted per lane (v_dot4 over its own row).
+//  * Tail waves (blockIdx >= main_waves): one lane per remaining chunk on the per-lane path (any alignment),
+//    dispatched with the main waves rather than as a second launch queued behind them.
+// ------------------------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGPR))) void block_sums_shift_kernel(
+    const uint8_t* __restrict__ data, int64_t n, uint32_t a, uint32_t B, uint32_t nchunks, uint32_t main_waves,
+    uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out, uint8_t* __restrict__ strong_out,
+    const int* abort_flag, int abort_gen) {
+    if (blockIdx.x >= main_waves) {
+        const uint32_t c = main_waves * 64u + (blockIdx.x - main_waves) * 64u + threadIdx.x;
+        if (c < nchunks) lane_chunk_sums<0, 4, false>(data, n, B, c, dl, seed, weak_out, strong_out);
+        return;
+    }
+    constexpr int ROW = 17;
+    extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // 64 rows of ROW slots
+    const int l = threadIdx.x;
+    const uint32_t c0 = blockIdx.x * 64u;
+    const uint8_t* gdata = data - a + (size_t)c0 * B;  // line-aligned; the host checked [gdata, +64 B + 128)
+    const uint32_t nst = B >> 7;                       // host guarantees 4 <= nst <= 1024
+    const uint32_t Q = a >> 4, r = a & 3;
+    const int wr0 = (l >> 3) * ROW + (l & 7);
+    const int row = l * ROW;
+
+    v4i32 wA[2];
+    v4i32 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    int32_t Racc[4] = {0, 0, 0, 0};
+    {
+        const int rw = l & 15, ks = l >> 4;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                uint32_t word = 0;
+                if (rw == 0) word = 0x01010101u;
+                else if (rw == 1)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) word |= (uint32_t)(16 * (4 * h + mfma_sigma(ks)) + 4 * w + b) << (8 * b);
+                wA[h][w] = (int)word;
+            }
+    }
+    const int rdB = mfma_pi(l & 15) * ROW + mfma_sigma(l >> 4);
+
+    uint4 q[2][8];  // line u + 1 and u + 2 in flight while step u computes
+    uint4 Wa[5];    // block 0 of the next MD5 stage
+    uint4 Wb[5];    // block 1 of the current MD5 stage
+    uint4 Bv[8];    // MFMA operands of the current line
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(gdata), 0, (int)(64 * B + 128), 0x00020000);
+    const uint32_t lane_off = (uint32_t)(l >> 3) * B + 16u * (uint32_t)(l & 7);
+    auto load = [&](uint4 (&dst)[8], uint32_t line) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_off + 128u * line, (int)(j * 8u * B), 2);
+            dst[j] = make_uint4(t.x, t.y, t.z, t.w);
+        }
+    };
+    auto put = [&](const uint4 (&src)[8], int half) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lds_all[wr0 + j * 8 * ROW + 8 * half] = src[j];
+    };
+    // the 5 slots holding block h of the MD5 stage with parity P (ring offset 128 P + a + 64 h)
+    auto get_words = [&](uint4 (&w)[5], int P, int h) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) w[k] = lds_all[row + ((8 * P + 4 * h + Q + k) & 15)];
+    };
+    auto get_mfma = [&](int half) __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) Bv[4 * h + g] = lds_all[16 * ROW * g + rdB + 8 * half + 4 * h];
+    };
+    Md5State st = md5_init();
+    auto md5_block = [&](const uint4 (&w)[5]) __attribute__((always_inline)) {
+        uint32_t d[20];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            d[4 * k] = w[k].x;
+            d[4 * k + 1] = w[k].y;
+            d[4 * k + 2] = w[k].z;
+            d[4 * k + 3] = w[k].w;
+        }
+        uint32_t m[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_alignbyte(d[W + i + 1], d[W + i], r);
+        md5_stream_block<8>(st, m);
+    };
+    auto weak_mfma = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) Racc[g] += acc[g][0];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const uint4 bv = Bv[4 * h + g];
+                const v4i32 b4 = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
+                acc[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wA[h], b4, acc[g], 0, 0, 0);
+            }
+    };
+    // signed-byte sums of the lane's own row, line in `half`, over the bytes j with (j < a) == BEFORE
+    auto edge_sums = [&](int half, bool before, int32_t& s, int32_t& u) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint4 v = lds_all[row + 8 * half + k];
+            const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int j0 = 16 * k + 4 * e;
+                const int nb = (int)a - j0;  // bytes of this dword before the chunk
+                const uint32_t lo = nb <= 0 ? 0u : nb >= 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
+                const uint32_t x = dw[e] & (before ? lo : ~lo);
+                s = __builtin_amdgcn_sdot4((int)x, 0x01010101, s, false);
+                u = __builtin_amdgcn_sdot4((int)x, j0 | ((j0 + 1) << 8) | ((j0 + 2) << 16) | ((j0 + 3) << 24), u, false);
+            }
+        }
+    };
+    // Step u: line u sits in half P = u & 1.  PREV: MD5 of stage u - 1; NEXT: write line u + 1 (half P ^ 1) and
+    // read the next stage's block 0; REFILL: load line u + 3 into the slot line u + 1 leaves.
+    auto step = [&](auto pc, uint32_t u, bool prev, bool next, bool refill) __attribute__((always_inline)) {
+        constexpr int P = decltype(pc)::value;
+        if (prev) get_words(Wb, P ^ 1, 1);  // lines u - 1 and u, before line u + 1 replaces line u - 1
+        compiler_fence();
+        if (next) {
+            put(q[P ^ 1], P ^ 1);
+            if (refill) load(q[P ^ 1], u + 3);
+        }
+        get_mfma(P);
+        if (prev) md5_block(Wa);
+        weak_mfma();
+        compiler_fence();
+        if (next) get_words(Wa, P, 0);  // lines u and u + 1
+        if (prev) md5_block(Wb);
+        compiler_fence();
+    };
+
+    load(q[0], 0);
+    load(q[1], 1);
+    put(q[0], 0);
+    load(q[0], 2);
+    compiler_fence();
+    int32_t hs = 0, hu = 0;  // line 0 before the chunk
+    edge_sums(0, true, hs, hu);
+    step(std::integral_constant<int, 0>{}, 0, false, true, true);
+    uint32_t u = 1;
+    [[maybe_unused]] int flag = 0;
+    // steady state: both steps write a line and refill (u + 4 <= nst); abort word polled as in the pipelined K1
+    for (; u + 4 <= nst && flag != abort_gen; u += 2) {
+        asm volatile("s_load_dword %0, %1, 0x0 glc" : "=s"(flag) : "s"(abort_flag));
+        step(std::integral_constant<int, 1>{}, u, true, true, true);
+        step(std::integral_constant<int, 0>{}, u + 1, true, true, true);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(flag));
+    }
+    if (flag == abort_gen) return;
+    for (; u <= nst; u += 2) {  // drain: steps up to nst (line nst; MD5 of stage nst - 1)
+        step(std::integral_constant<int, 1>{}, u, true, u < nst, u + 3 <= nst);
+        if (u + 1 <= nst) step(std::integral_constant<int, 0>{}, u + 1, true, u + 1 < nst, u + 4 <= nst);
+    }
+    int32_t ts = 0, tj = 0;  // line nst after the chunk
+    edge_sums((int)(nst & 1), false, ts, tj);
+    {
+        const uint64_t bits = ((uint64_t)B + 4) * 8;
+        uint32_t m[16] = {seed, 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, (uint32_t)bits, (uint32_t)(bits >> 32)};
+        md5_compress(st, m);
+    }
+    int32_t s1, uu;
+    {
+        const uint32_t nl = nst + 1;  // lines summed by the MFMAs
+        int32_t s1g[4], ug[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            Racc[g] += acc[g][0];
+            s1g[g] = acc[g][0];
+            ug[g] = (int32_t)(128u * (nl * (uint32_t)acc[g][0] - (uint32_t)Racc[g])) + acc[g][1];
+        }
+        const int src = mfma_pi_inv(l & 15);
+        int32_t t1[4], tu[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            t1[g] = __shfl(s1g[g], src, 64);
+            tu[g] = __shfl(ug[g], src, 64);
+        }
+        const int gs = l >> 4;
+        s1 = gs == 0 ? t1[0] : gs == 1 ? t1[1] : gs == 2 ? t1[2] : t1[3];
+        uu = gs == 0 ? tu[0] : gs == 1 ? tu[1] : gs == 2 ? tu[2] : tu[3];
+    }
+    // lines -> chunk: S = S_lines - head - tail; sum over the chunk of (i' - a) x' with i' the line-space index
+    const uint32_t S = (uint32_t)s1 - (uint32_t)hs - (uint32_t)ts;
+    const uint32_t Ui = (uint32_t)uu - (uint32_t)hu - (128u * nst * (uint32_t)ts + (uint32_t)tj) - a * S;
+    const uint32_t c = c0 + l;
+    const int32_t s2 = (int32_t)(B * S - Ui);
+    weak_out[c] = (int32_t)((S & 0xFFFFu) | ((uint32_t)s2 << 16));
+    store_digest(strong_out + (size_t)c * dl, st, dl);
+}
+
 // ------------------------------------------------------------------------------------------------
 // K1 (LDS-DMA): as the coalesced kernel, but each stage goes HBM -> LDS directly with
 // global_load_lds_dwordx4 (no VGPR staging, no ds_write).  LDS-DMA writes lane l's 16 B at slot
@@ -747,6 +974,47 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
     // kernel instead.
     const char* ua = getenv("RSH_K1_UNALIGNED");
     const bool unaligned_ok = !ua || atoi(ua) != 0;
+    // A base that is not 128-B aligned goes to the line-aligned shift kernel when the lines it reads around the
+    // data -- a bytes before it, up to 128 - a after the last full wave -- lie in the same allocation
+    // (RSH_K1_SHIFT=0, read per launch: the pipelined kernel at the unaligned base, A/B).
+    const char* sk = getenv("RSH_K1_SHIFT");
+    if (variant == 19 && (addr % 128) != 0 && (B % 128) == 0 && (B >> 7) >= 4 && (B >> 7) <= 1024 && abort_flag &&
+        !(sk && atoi(sk) == 0)) {
+        hipDeviceptr_t lo = nullptr;
+        size_t size = 0;
+        const uint32_t a = (uint32_t)(addr % 128);
+        if (hipMemGetAddressRange(&lo, &size, reinterpret_cast<hipDeviceptr_t>(const_cast<uint8_t*>(d_data))) ==
+                hipSuccess &&
+            addr - a >= reinterpret_cast<uintptr_t>(lo)) {
+            const int64_t avail = (int64_t)(reinterpret_cast<uintptr_t>(lo) + size - (addr - a));
+            const uint32_t nfullc = (uint32_t)std::min<int64_t>(n / B, nchunks);
+            const int64_t fit = avail >= 128 ? (avail - 128) / ((int64_t)64 * B) : 0;
+            const uint32_t mw = (uint32_t)std::min<int64_t>(nfullc / 64, fit);
+            if (mw > 0) {
+                const uint32_t tail_waves = (nchunks - 64 * mw + 63) / 64;
+                const dim3 grid(mw + tail_waves);
+                const size_t lb = 64 * 17 * sizeof(uint4);
+                switch ((a >> 2) & 3) {
+                    case 0:
+                        hipLaunchKernelGGL((block_sums_shift_kernel<0>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
+                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen);
+                        break;
+                    case 1:
+                        hipLaunchKernelGGL((block_sums_shift_kernel<1>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
+                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen);
+                        break;
+                    case 2:
+                        hipLaunchKernelGGL((block_sums_shift_kernel<2>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
+                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen);
+                        break;
+                    default:
+                        hipLaunchKernelGGL((block_sums_shift_kernel<3>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
+                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen);
+                }
+                return hipGetLastError();
+            }
+        }
+    }
     if (variant >= 3 && (B % 128) == 0 && (B >> 7) >= (deep ? 8u : 4u) && ((addr % 16) == 0 || unaligned_ok)) {
         const uint32_t nfullc = (uint32_t)std::min<int64_t>(n / B, nchunks);  // chunks with L == B
         const uint32_t waves = nfullc / 64;
@@ -1028,8 +1296,8 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
         hipLaunchKernelGGL((block_sums_kernel<4, 2>), grid, block, 0, s, d_data, n, B, nchunks, dl, seed_word, d_weak,
                            d_strong, c_first);
     } else {
-        hipLaunchKernelGGL((block_sums_kernel<1, 1>), grid, block, 0, s, d_data, n, B, nchunks, dl, seed_word, d_weak,
-                           d_strong, c_first);
+        hipLaunchKernelGGL((block_sums_kernel<0, 4, false>), grid, block, 0, s, d_data, n, B, nchunks, dl, seed_word,
+                           d_weak, d_strong, c_first);
     }
     return hipGetLastError();
 }

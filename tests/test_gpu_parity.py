@@ -151,26 +151,52 @@ def test_sender_digest_longer_than_md5(ctx, pad):
                                   ow.ctypes.data, os_.ctypes.data) == R.RSH_E_INVAL
 
 
-@pytest.mark.parametrize("unaligned", ["0", "1"])
-def test_k1_unaligned_base(ctx, unaligned, monkeypatch):
-    """K1 over a basis that starts at every offset 0..15 from a 16-B boundary (the phase-shifted speculation
-    runs K1 over src + s for any s).  By default the pipelined buffer-load kernel runs at such addresses (its
-    dwordx4 loads straddle 16-B boundaries); RSH_K1_UNALIGNED=0 sends them to the per-lane kernel.  Bit-exact
-    against the oracle either way."""
+@pytest.mark.parametrize("path", ["shift", "pipe", "lane"])
+def test_k1_unaligned_base(ctx, path, monkeypatch):
+    """K1 over a basis that starts at offsets 0..15 and beyond from a 128-B line (the phase-shifted speculation
+    runs K1 over src + s for any s).  By default such bases go to the line-aligned shift kernel (its loads stay
+    on 128-B lines; MD5 words funnel-shifted out of an LDS ring; the lines' bytes outside the chunk taken out of
+    the weak sums; tail chunks on per-lane waves of the same launch).  RSH_K1_SHIFT=0 runs the pipelined kernel
+    at the unaligned base; with RSH_K1_UNALIGNED=0 too, the per-lane kernel.  Bit-exact against the oracle."""
     import ctypes
-    monkeypatch.setenv("RSH_K1_UNALIGNED", unaligned)
+    monkeypatch.setenv("RSH_K1_SHIFT", "0" if path != "shift" else "1")
+    monkeypatch.setenv("RSH_K1_UNALIGNED", "0" if path == "lane" else "1")
     B, dl = 2048, 4
     n = 200 * B + 77
-    d = ctx.alloc(n + 64)
-    R.lib().rsh_fill_splitmix_device(ctx.handle, d.ptr, n + 64, 0xA11, 0)
+    d = ctx.alloc(n + 256)
+    R.lib().rsh_fill_splitmix_device(ctx.handle, d.ptr, n + 256, 0xA11, 0)
     ctx.sync()
     host = d.download()
     seed = np.frombuffer(SEED, np.uint8).copy()
-    for off in range(16):
+    offs = list(range(16)) + ([17, 36, 50, 64, 65, 100, 127, 130] if path != "lane" else [])
+    for off in offs:
         h = R.header_make(B, dl, n)
         d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
         assert R.lib().rsh_block_sums_device(ctx.handle, ctypes.c_void_p(d.ptr.value + off), n, ctypes.byref(h), seed.ctypes.data,
                                              d_w.ptr, d_s.ptr) == 0
+        ctx.sync()
+        ow, os_ = O.generator(host[off:off + n], O.header(B, dl, n), SEED)
+        assert np.array_equal(d_w.download(dtype=np.int32), ow), f"weak, offset {off}"
+        assert np.array_equal(d_s.download(), os_), f"strong, offset {off}"
+
+
+@pytest.mark.parametrize("nfull", [192, 256])
+def test_k1_shift_allocation_edge(ctx, nfull):
+    """The shift kernel reads whole lines around the data: a bytes before it and up to 128 - a past the last
+    full wave.  With the data ending exactly at the end of its allocation, the waves whose lines would leave it
+    run on the per-lane tail waves instead (no access outside the allocation; results bit-exact)."""
+    import ctypes
+    B, dl = 2048, 4
+    for off in (1, 77):
+        n = nfull * B
+        d = ctx.alloc(n + off)
+        R.lib().rsh_fill_splitmix_device(ctx.handle, d.ptr, n + off, 0xB22 + off, 0)
+        ctx.sync()
+        host = d.download()
+        h = R.header_make(B, dl, n)
+        d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
+        assert R.lib().rsh_block_sums_device(ctx.handle, ctypes.c_void_p(d.ptr.value + off), n, ctypes.byref(h),
+                                             np.frombuffer(SEED, np.uint8).ctypes.data, d_w.ptr, d_s.ptr) == 0
         ctx.sync()
         ow, os_ = O.generator(host[off:off + n], O.header(B, dl, n), SEED)
         assert np.array_equal(d_w.download(dtype=np.int32), ow), f"weak, offset {off}"
