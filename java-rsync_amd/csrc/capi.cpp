@@ -365,17 +365,17 @@ class HipBackend : public rsh::ScanBackend {
         phase_stop();  // one at another phase is dead work now
         CallTrace tr("phase_spec", s);
         ph_gen_ = ++c_->gen;
-        ok(hipStreamWaitEvent(c_->aux, c_->ev_in, 0));
-        ok(hipEventRecord(c_->ev_pha, c_->aux));
+        hipStream_t ps = c_->phase;  // its own stream: it does not queue behind a prefix speculation on aux
+        ok(hipStreamWaitEvent(ps, c_->ev_in, 0));
+        ok(hipEventRecord(c_->ev_pha, ps));
         ok(rsh::launch_block_sums(x_ + s, std::min(n_ - s, count * B_), (uint32_t)B_, (uint32_t)count, (uint32_t)dl_,
                                   seed_word(seed_),
-                                  c_->ph_weak.as<int32_t>(), c_->ph_strong.as<uint8_t>(), c_->aux,
+                                  c_->ph_weak.as<int32_t>(), c_->ph_strong.as<uint8_t>(), ps,
                                   c_->abort_word + rsh_ctx::kPhaseWord, ph_gen_));
-        ok(hipEventRecord(c_->ev_phb, c_->aux));
-        ok(hipMemcpyAsync(c_->h_pw.p, c_->ph_weak.p, (size_t)count * 4, hipMemcpyDeviceToHost, c_->aux));
-        if (dl_ > 0)
-            ok(hipMemcpyAsync(c_->h_ps.p, c_->ph_strong.p, (size_t)count * dl_, hipMemcpyDeviceToHost, c_->aux));
-        ok(hipEventRecord(c_->ev_phase, c_->aux));
+        ok(hipEventRecord(c_->ev_phb, ps));
+        ok(hipMemcpyAsync(c_->h_pw.p, c_->ph_weak.p, (size_t)count * 4, hipMemcpyDeviceToHost, ps));
+        if (dl_ > 0) ok(hipMemcpyAsync(c_->h_ps.p, c_->ph_strong.p, (size_t)count * dl_, hipMemcpyDeviceToHost, ps));
+        ok(hipEventRecord(c_->ev_phase, ps));
         if (err != hipSuccess) return;
         ph_s0_ = s;
         ph_count_ = count;
@@ -649,30 +649,41 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // the chain evidence of the first aligned windows (see above): launch the speculation now and let the
     // resolver wait for it rather than take head-mode steps beside it
     bool spec_wait = false;
+    int64_t run_last = -1, run_miss = -1;  // a sampled run's last matching window, the first sample past it
     static const bool wait_on = !getenv("RSH_SCAN_WAIT") || atoi(getenv("RSH_SCAN_WAIT")) != 0;  // A/B
     static const bool sample_on = !getenv("RSH_SCAN_SAMPLE") || atoi(getenv("RSH_SCAN_SAMPLE")) != 0;  // A/B
     if (head && nlead > 0 && (!spec_launched || spec_tentative)) {
         int64_t lead = 0;
         while (lead < nlead && lead_w[lead] == host_weak[lead]) ++lead;
         const bool eager = lead == nlead && (nlead >= kLeadWindows || nlead == nf);
-        if (spec_tentative && !eager) {  // stop the tentative launch; later launches take a new generation
+        // The run may stop somewhere (an insert shifts everything after it to another phase, where the
+        // phase-shifted speculation takes over): cover only up to the last sample that still matches, plus
+        // one stride.  A K1 over a few waves is not free -- each lane digests its whole window serially, 1.9 ms
+        // at B = 128 KiB -- but it lands well before a full launch (3.0-3.4 ms at 2 waves/SIMD), and the
+        // phase-shifted launch that follows gets the whole chip.
+        int64_t cover = na;
+        if (eager && sample_on) {
+            int64_t lastk = nlead - 1;
+            for (int64_t i = nlead; i < nsamp; ++i)
+                if (lead_w[i] == host_weak[samp[(size_t)i]]) lastk = samp[(size_t)i];
+            if (lastk + stride < nf) {
+                cover = std::min<int64_t>(na, (lastk + stride + 64) & ~(int64_t)63);  // whole waves
+                run_last = lastk;
+                for (int64_t i = 0; i < nsamp && run_miss < 0; ++i)
+                    if (samp[(size_t)i] > lastk) run_miss = samp[(size_t)i];
+            }
+        }
+        if (spec_tentative && (!eager || cover < na)) {  // stop the tentative launch; later ones take a new generation
             RSH_HIP(hipStreamWriteValue32(c->stream, c->abort_word, (uint32_t)gen, 0));
             gen = ++c->gen;
             spec_launched = spec_tentative = false;
             tentative_stopped = true;
             res->stats.speculation_aborted = 3;  // overwritten below if a later launch lands or is stopped
-        } else if (spec_tentative) {
+        }
+        if (spec_tentative) {
             spec_wait = wait_on;
         } else if (eager) {
-            // the run may stop somewhere (an insert shifts everything after it to another phase, where the
-            // phase-shifted speculation takes over): cover only up to the last sample that still matches
-            // (plus one stride) -- but never less than one K1 round of windows (kRoundWindows), since a K1
-            // over fewer chunks takes the same time (each lane digests its whole window serially)
-            int64_t lastk = nlead - 1;
-            for (int64_t i = nlead; i < nsamp; ++i)
-                if (lead_w[i] == host_weak[samp[(size_t)i]]) lastk = samp[(size_t)i];
-            const bool all = lastk + stride >= nf || !sample_on;
-            spec_na = all ? na : std::min<int64_t>(na, std::max<int64_t>(lastk + stride + 1, kRoundWindows));
+            spec_na = cover;
             const int rc = launch_spec();
             if (rc != RSH_OK) return rc;
             spec_launched = true;
@@ -693,6 +704,36 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         memcpy(out, md5_0, 16);
     };
     be.haw_ready.assign((size_t)na, 0);
+    // Phase guess.  When the samples show the aligned run stopping (only a prefix speculated), the source most
+    // likely goes on at another phase after an insert or delete (Sender.java:1282-1287: the scan then matches
+    // chunks at kB + delta).  Look for that phase now -- the first position in [mB, mB + B), m the first sample
+    // past the run, whose window and the next three carry four consecutive chunks' weak sums -- and start the
+    // phase-shifted speculation there (own stream, beside the prefix speculation) instead of once the resolver
+    // has walked the prefix.  Starting it a few windows early costs a few lanes; a wrong guess is stopped when
+    // the resolver hints another phase.  RSH_SCAN_PHASE_GUESS=0 (A/B) turns it off.
+    static const bool guess_on = !getenv("RSH_SCAN_PHASE_GUESS") || atoi(getenv("RSH_SCAN_PHASE_GUESS")) != 0;
+    if (guess_on && run_miss > 0 && spec_launched && HipBackend::phase_on() && C >= 4) {
+        CallTrace tr("phase_guess", run_miss);
+        int64_t a = run_miss * B;
+        const int64_t b = std::min<int64_t>(run_miss * B + B, n - 4 * B + 1);
+        for (int tries = 0; tries < 8 && a < b && be.err == hipSuccess; ++tries) {
+            const rsh::ProbeInterval iv{a, b, a, 0, 0};
+            const int64_t p = be.first_hit(&iv, 1, nullptr);
+            if (p < 0) break;
+            const int64_t pos[4] = {p, p + B, p + 2 * B, p + 3 * B};
+            int32_t w[4];
+            be.weak_many(pos, 4, w);
+            bool run = false;
+            for (int64_t j = 0; j + 3 < C && !run; ++j)
+                run = host_weak[j] == w[0] && host_weak[j + 1] == w[1] && host_weak[j + 2] == w[2] &&
+                      host_weak[j + 3] == w[3];
+            if (run) {
+                be.phase_hint(p - ((p - run_last * B) / B) * B);  // from the run's last sampled window on
+                break;
+            }
+            a = p + 1;
+        }
+    }
     rsh::ResolveState rs;
     bool landed = false;
     int spec_rc = RSH_OK;
@@ -899,6 +940,7 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
     c->abort_word = nullptr;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->phase, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_tab, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming) != hipSuccess ||

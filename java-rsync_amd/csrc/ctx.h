@@ -105,7 +105,8 @@ struct rsh_ctx {
     DevBuf src_weak, src_strong, flags;          // aligned speculation over the source
     DevBuf ph_weak, ph_strong;                   // phase-shifted speculation over [s0, n) (chains at kB + delta)
     DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw, partials, bucket;
-    hipStream_t aux = nullptr;                   // table download, then the aligned speculation
+    hipStream_t aux = nullptr;                   // the aligned speculation
+    hipStream_t phase = nullptr;                 // the phase-shifted speculation (beside a prefix speculation)
     hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr, ev_phase = nullptr;
     hipEvent_t ev_flags = nullptr;  // batched speculation: its chain flags are on the host (before its sums)
     hipEvent_t ev_k1a = nullptr, ev_k1b = nullptr;  // timing: the aligned speculation's K1 (stats)
@@ -150,6 +151,7 @@ struct rsh_ctx {
         if (ev_pha) (void)hipEventDestroy(ev_pha);
         if (ev_phb) (void)hipEventDestroy(ev_phb);
         if (aux) (void)hipStreamDestroy(aux);
+        if (phase) (void)hipStreamDestroy(phase);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };

@@ -462,6 +462,9 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 // groups[blockIdx.x] instead of (data, B, dl, weak_out, strong_out) + blockIdx.x * 64 chunks.
 // K1_PIPE_ATTR (A/B at build time, -DRSH_K1_NUMVGPR=N): the register budget.  waves_per_eu(3) caps the
 // kernel at 168 VGPRs, which spills 12 of them to scratch (20 B/lane); num_vgpr(N) with N >= 184 does not.
+#ifndef RSH_K1_TAIL_PF
+#define RSH_K1_TAIL_PF 2
+#endif
 #ifdef RSH_K1_NUMVGPR
 #define K1_PIPE_ATTR __attribute__((amdgpu_num_vgpr(RSH_K1_NUMVGPR)))
 #else
@@ -472,9 +475,27 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
                                                              uint8_t* __restrict__ strong_out,
                                                              const int* abort_flag = nullptr, int abort_gen = 0,
-                                                             const K1Group* __restrict__ groups = nullptr) {
+                                                             const K1Group* __restrict__ groups = nullptr,
+                                                             int64_t n = 0, uint32_t nchunks = 0,
+                                                             uint32_t main_waves = 0xFFFFFFFFu) {
     constexpr int ROW = 9;
     constexpr int BUF = 64 * ROW;  // uint4 slots per LDS buffer
+    constexpr int TAIL_PF = RSH_K1_TAIL_PF;
+    if constexpr (!MULTI) {
+        // tail waves (blockIdx >= main_waves): one lane per chunk left over (a partial last wave, the short last
+        // chunk), dispatched with the main waves rather than as a launch queued behind them (a lone wave takes
+        // as long as one lane's window: 1.9 ms at B = 128 KiB)
+        if (blockIdx.x >= main_waves) {
+            const uint32_t c = main_waves * 64u + (blockIdx.x - main_waves) * 64u + threadIdx.x;
+            if (c < nchunks) {
+                if ((reinterpret_cast<uintptr_t>(data) % 16) == 0)
+                    lane_chunk_sums<16, TAIL_PF>(data, n, B, c, dl, seed, weak_out, strong_out);
+                else
+                    lane_chunk_sums<0, TAIL_PF, false>(data, n, B, c, dl, seed, weak_out, strong_out);
+            }
+            return;
+        }
+    }
     if constexpr (PIN) asm volatile("; occupancy pin" ::: "v175");
     extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // 2 buffers (sized at launch)
     const int l = threadIdx.x;
@@ -1083,8 +1104,11 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     // run in rounds): measured 3.19 vs 3.96 ms for 16 GiB at B = 64 KiB (4096 waves) against the
                     // unpinned instantiation, and ahead of the coalesced kernel at every size
                     if (nst <= 1024 && nst >= 4 && abort_flag && (waves <= 2 * 4 * kCUs || pin_all())) {
-                        hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true>), dim3(waves), dim3(64), 2 * wave_lds,
-                                           s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen);
+                        const uint32_t tail_waves = (nchunks - 64 * waves + 63) / 64;  // in the same launch
+                        hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true>), dim3(waves + tail_waves), dim3(64),
+                                           2 * wave_lds, s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag,
+                                           abort_gen, nullptr, n, nchunks, waves);
+                        return hipGetLastError();
                     } else if (nst <= 1024 && nst >= 4 && (waves <= 2 * 4 * kCUs || pin_all())) {
                         hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true>), dim3(waves), dim3(64), 2 * wave_lds,
                                            s, d_data, B, dl, seed_word, d_weak, d_strong);
