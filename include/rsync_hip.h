@@ -88,6 +88,8 @@ typedef struct {
     double spec_kernel_ms;   /* the aligned speculation's K1 alone (HIP events on its stream), when it ran
                                 to completion; 0 otherwise (ABI 2)                                   */
     double phase_kernel_ms;  /* the phase-shifted speculations' K1s that ran to completion, summed (ABI 2) */
+    int64_t phase_guesses;   /* phase-shifted speculations started before the resolver, at the phase found
+                                past a sampled run's end (ABI 2)                                     */
 } rsh_scan_stats;
 
 typedef struct rsh_ctx rsh_ctx;

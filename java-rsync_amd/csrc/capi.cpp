@@ -706,7 +706,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     be.haw_ready.assign((size_t)na, 0);
     // Phase guess.  When the samples show the aligned run stopping (only a prefix speculated), the source most
     // likely goes on at another phase after an insert or delete (Sender.java:1282-1287: the scan then matches
-    // chunks at kB + delta).  Look for that phase now -- the first position in [mB, mB + B), m the first sample
+    // chunks at kB + delta).  Look for that phase now -- the first position in [mB, mB + 2B), m the first sample
     // past the run, whose window and the next three carry four consecutive chunks' weak sums -- and start the
     // phase-shifted speculation there (own stream, beside the prefix speculation) instead of once the resolver
     // has walked the prefix.  Starting it a few windows early costs a few lanes; a wrong guess is stopped when
@@ -715,7 +715,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     if (guess_on && run_miss > 0 && spec_launched && HipBackend::phase_on() && C >= 4) {
         CallTrace tr("phase_guess", run_miss);
         int64_t a = run_miss * B;
-        const int64_t b = std::min<int64_t>(run_miss * B + B, n - 4 * B + 1);
+        const int64_t b = std::min<int64_t>(run_miss * B + 2 * B, n - 4 * B + 1);  // the edit may sit in window m
         for (int tries = 0; tries < 8 && a < b && be.err == hipSuccess; ++tries) {
             const rsh::ProbeInterval iv{a, b, a, 0, 0};
             const int64_t p = be.first_hit(&iv, 1, nullptr);
@@ -728,7 +728,9 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                 run = host_weak[j] == w[0] && host_weak[j + 1] == w[1] && host_weak[j + 2] == w[2] &&
                       host_weak[j + 3] == w[3];
             if (run) {
+                const int64_t before = be.ph_launches;
                 be.phase_hint(p - ((p - run_last * B) / B) * B);  // from the run's last sampled window on
+                res->stats.phase_guesses += be.ph_launches - before;
                 break;
             }
             a = p + 1;

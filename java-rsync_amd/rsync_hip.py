@@ -71,7 +71,7 @@ class ScanStats(ctypes.Structure):
                 ("head_steps", ctypes.c_int64), ("speculation_aborted", ctypes.c_int64),
                 ("device_bytes", ctypes.c_int64), ("phase_launches", ctypes.c_int64),
                 ("phase_matches", ctypes.c_int64), ("spec_kernel_ms", ctypes.c_double),
-                ("phase_kernel_ms", ctypes.c_double)]
+                ("phase_kernel_ms", ctypes.c_double), ("phase_guesses", ctypes.c_int64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -215,6 +215,32 @@ def test_sender_phase_shift_chains(ctx):
     assert st["phase_launches"] >= 1 and st["phase_matches"] > 6000 and st["host_md5_windows"] < 100, st
 
 
+@pytest.mark.parametrize("edit", ["insert1", "delete3", "two_inserts", "insert_far"])
+def test_sender_phase_guess(ctx, edit):
+    """A source that follows the basis up to an edit and continues at another phase after it (4096 windows at
+    B = 65536, samples every 4): the speculation covers the sampled prefix only, and before the resolver starts
+    the backend finds the phase past the run (a range probe plus four consecutive chunk sums) and starts the
+    phase-shifted speculation there.  two_inserts: a second insert two windows after the first, so the guess
+    (past both) is not the phase the resolver meets first.  insert_far: the edit is past every sample but the
+    last.  Events equal the oracle's in every case."""
+    B, dl = 65536, 4
+    basis = O.splitmix(256 << 20, 0x5EED5EED000000C3)
+    x = 300 * B + 777
+    if edit == "insert1":
+        src = np.concatenate([basis[:x], O.splitmix(1, 7), basis[x:]])
+    elif edit == "delete3":
+        src = np.concatenate([basis[:x], basis[x + 3:]])
+    elif edit == "two_inserts":
+        y = 302 * B + 5
+        src = np.concatenate([basis[:x], O.splitmix(1, 7), basis[x:y], O.splitmix(2, 8), basis[y:]])
+    else:
+        z = 4090 * B + 11
+        src = np.concatenate([basis[:z], O.splitmix(9, 9), basis[z:]])
+    st = _sender_both(ctx, basis.tobytes(), src.tobytes(), B, dl)
+    if edit in ("insert1", "delete3"):  # (the others may poison the cached digest after the edits: quirk B)
+        assert st["phase_launches"] >= 1 and st["phase_guesses"] == 1 and st["host_md5_windows"] < 10, st
+
+
 def test_sender_partial_speculation(ctx):
     """More windows than one K1 round (300000 > 131072 at B = 512) and a 7-byte insert after 1 MiB: the lead
     windows match, the sampled windows past the insert do not, so the aligned speculation covers a prefix only
