@@ -404,6 +404,15 @@ class HipBackend : public rsh::ScanBackend {
         v->st = c_->h_ps.as<uint8_t>();
         return true;
     }
+    // A phase-shifted speculation the caller launched (the segmented prefix + phase launch, scan_device) over
+    // windows s0 + kB, k < count, generation gen, landing on ev_phase: from now on this backend's.
+    void phase_adopt(int64_t s0, int64_t count, int gen) {
+        ph_s0_ = s0;
+        ph_count_ = count;
+        ph_gen_ = gen;
+        ph_landed_ = false;
+        ++ph_launches;
+    }
     // A phase speculation still running when the scan ends (or moves to another phase) is stopped; later
     // work on the context stream waits until its waves have left.
     void phase_stop() {
@@ -520,6 +529,9 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     RSH_HIP(c->haw.ensure((size_t)na * 4));
     RSH_HIP(c->ph_weak.ensure((size_t)na * 4));
     RSH_HIP(c->ph_strong.ensure((size_t)na * dl + 1));
+    const size_t seg_bytes = ((size_t)na / 64 + 4) * sizeof(rsh::K1Seg) + 256 * sizeof(rsh::K1Tail);
+    RSH_HIP(c->segs.ensure(seg_bytes));
+    RSH_HIP(c->h_segs.ensure(seg_bytes));
     RSH_HIP(c->h_pw.ensure((size_t)na * 4));
     RSH_HIP(c->h_ps.ensure((size_t)na * dl + 1));
     // sample windows for the launch decision: the first nlead, then one every `stride` windows
@@ -650,6 +662,9 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // resolver wait for it rather than take head-mode steps beside it
     bool spec_wait = false;
     int64_t run_last = -1, run_miss = -1;  // a sampled run's last matching window, the first sample past it
+    bool defer_prefix = false;             // the prefix speculation waits for the phase guess (below)
+    static const bool guess_on = !getenv("RSH_SCAN_PHASE_GUESS") || atoi(getenv("RSH_SCAN_PHASE_GUESS")) != 0;
+    static const bool seg_on = !getenv("RSH_SCAN_SEGMENTED") || atoi(getenv("RSH_SCAN_SEGMENTED")) != 0;  // A/B
     static const bool wait_on = !getenv("RSH_SCAN_WAIT") || atoi(getenv("RSH_SCAN_WAIT")) != 0;  // A/B
     static const bool sample_on = !getenv("RSH_SCAN_SAMPLE") || atoi(getenv("RSH_SCAN_SAMPLE")) != 0;  // A/B
     if (head && nlead > 0 && (!spec_launched || spec_tentative)) {
@@ -684,17 +699,19 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             spec_wait = wait_on;
         } else if (eager) {
             spec_na = cover;
-            const int rc = launch_spec();
-            if (rc != RSH_OK) return rc;
-            spec_launched = true;
+            if (cover < na && run_miss > 0 && guess_on && HipBackend::phase_on() && C >= 4) {
+                defer_prefix = true;  // launched below, with the phase guess's speculation when there is one
+            } else {
+                const int rc = launch_spec();
+                if (rc != RSH_OK) return rc;
+                spec_launched = true;
+            }
             spec_wait = wait_on;
         }
     }
     HipBackend be(c, d_src, n, table, d_weak, seed);
     be.table.slots = c->slots.as<unsigned long long>();
     be.table.mask = ns - 1;
-    be.na = spec_na;
-    be.partial = spec_na < na;
     be.aw = c->h_aw.as<int32_t>();
     be.as = c->h_as.as<uint8_t>();
     be.fl = c->h_fl.as<uint8_t>();
@@ -708,11 +725,10 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // likely goes on at another phase after an insert or delete (Sender.java:1282-1287: the scan then matches
     // chunks at kB + delta).  Look for that phase now -- the first position in [mB, mB + 2B), m the first sample
     // past the run, whose window and the next three carry four consecutive chunks' weak sums -- and start the
-    // phase-shifted speculation there (own stream, beside the prefix speculation) instead of once the resolver
-    // has walked the prefix.  Starting it a few windows early costs a few lanes; a wrong guess is stopped when
-    // the resolver hints another phase.  RSH_SCAN_PHASE_GUESS=0 (A/B) turns it off.
-    static const bool guess_on = !getenv("RSH_SCAN_PHASE_GUESS") || atoi(getenv("RSH_SCAN_PHASE_GUESS")) != 0;
-    if (guess_on && run_miss > 0 && spec_launched && HipBackend::phase_on() && C >= 4) {
+    // phase-shifted speculation there instead of once the resolver has walked the prefix.  A wrong guess is
+    // stopped when the resolver hints another phase.  RSH_SCAN_PHASE_GUESS=0 (A/B) turns it off.
+    int64_t guess = -1;
+    if (guess_on && run_miss > 0 && (spec_launched || defer_prefix) && HipBackend::phase_on() && C >= 4) {
         CallTrace tr("phase_guess", run_miss);
         int64_t a = run_miss * B;
         const int64_t b = std::min<int64_t>(run_miss * B + 2 * B, n - 4 * B + 1);  // the edit may sit in window m
@@ -728,14 +744,115 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                 run = host_weak[j] == w[0] && host_weak[j + 1] == w[1] && host_weak[j + 2] == w[2] &&
                       host_weak[j + 3] == w[3];
             if (run) {
-                const int64_t before = be.ph_launches;
-                be.phase_hint(p - ((p - run_last * B) / B) * B);  // from the run's last sampled window on
-                res->stats.phase_guesses += be.ph_launches - before;
+                guess = p;
                 break;
             }
             a = p + 1;
         }
     }
+    // The prefix and the phase-shifted speculation in one segmented K1 launch: as two launches they need one
+    // wave more than the chip's wave slots (each has a partial last wave), and that wave starts only when
+    // another finishes (config 5's shift case: the phase launch landed after 5.4 ms instead of 3.9).  The
+    // prefix ends at the first aligned window past the run whose weak sum is not its chunk's (found with one
+    // gather); the phase windows start at the first window of the guessed phase at or after it; the two
+    // segments' leftover chunks share the per-lane tail waves.
+    bool seg_launched = false;
+    if (defer_prefix && guess >= 0 && seg_on && be.err == hipSuccess) {
+        CallTrace tr("seg_launch", guess);
+        const int64_t k_lo = run_last + 1, k_hi = std::min<int64_t>(run_miss, nf - 1);
+        const int64_t cnt = k_hi - k_lo + 1;
+        hipDeviceptr_t lo = nullptr;
+        size_t asize = 0;
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(d_src);
+        if (cnt > 0 && cnt <= 4096 && B % 128 == 0 && (B >> 7) >= 4 && (B >> 7) <= 1024 &&
+            hipMemGetAddressRange(&lo, &asize, reinterpret_cast<hipDeviceptr_t>(const_cast<uint8_t*>(d_src))) ==
+                hipSuccess) {
+            std::vector<int64_t> pos((size_t)cnt);
+            std::vector<int32_t> w((size_t)cnt);
+            for (int64_t i = 0; i < cnt; ++i) pos[(size_t)i] = (k_lo + i) * B;
+            be.weak_many(pos.data(), cnt, w.data());
+            int64_t P = run_miss;  // aligned windows [0, P): up to the first one whose weak sum is not its chunk's
+            for (int64_t i = 0; i < cnt; ++i)
+                if (w[(size_t)i] != host_weak[k_lo + i]) {
+                    P = k_lo + i;
+                    break;
+                }
+            const int64_t s0 = guess - ((guess - P * B) / B) * B;  // the first window at the guess's phase >= P B
+            const int64_t Q = (n - s0 + B - 1) / B;
+            const uintptr_t alo = reinterpret_cast<uintptr_t>(lo), ahi = alo + asize;
+            const uint32_t a0 = (uint32_t)(addr % 128), a1 = (uint32_t)((addr + (uintptr_t)s0) % 128);
+            if (P > 0 && Q >= 8 && addr - a0 >= alo && be.err == hipSuccess) {
+                auto* sg = reinterpret_cast<rsh::K1Seg*>(c->h_segs.p);
+                const int64_t wp = P / 64;
+                int64_t wq = ((n - s0) / B) / 64;  // full phase waves whose lines stay in the allocation
+                while (wq > 0 && addr + (uintptr_t)s0 - a1 + (uintptr_t)(wq * 64 * B) + 128 > ahi) --wq;
+                const int gph = ++c->gen;
+                uint32_t nseg = 0;
+                for (int64_t v = 0; v < wp; ++v)
+                    sg[nseg++] = rsh::K1Seg{d_src - a0 + v * 64 * B, c->src_weak.as<int32_t>() + v * 64,
+                                            c->src_strong.as<uint8_t>() + v * 64 * dl, c->abort_word, gen, a0};
+                for (int64_t v = 0; v < wq; ++v)
+                    sg[nseg++] = rsh::K1Seg{d_src + s0 - a1 + v * 64 * B, c->ph_weak.as<int32_t>() + v * 64,
+                                            c->ph_strong.as<uint8_t>() + v * 64 * dl,
+                                            c->abort_word + rsh_ctx::kPhaseWord, gph, a1};
+                auto* tl = reinterpret_cast<rsh::K1Tail*>(sg + nseg);
+                uint32_t ntail = 0;
+                for (int64_t k = wp * 64; k < P; ++k)
+                    tl[ntail++] = rsh::K1Tail{d_src, n, c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(),
+                                              (uint32_t)k};
+                for (int64_t k = wq * 64; k < Q; ++k)
+                    tl[ntail++] = rsh::K1Tail{d_src + s0, n - s0, c->ph_weak.as<int32_t>(), c->ph_strong.as<uint8_t>(),
+                                              (uint32_t)k};
+                const size_t bytes = nseg * sizeof(rsh::K1Seg) + ntail * sizeof(rsh::K1Tail);
+                if (ntail <= 256 && bytes <= seg_bytes) {
+                    spec_na = P;
+                    const int64_t snf = std::min<int64_t>(P, C);
+                    RSH_HIP(hipMemcpyAsync(c->segs.p, c->h_segs.p, bytes, hipMemcpyHostToDevice, c->aux));
+                    RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
+                    RSH_HIP(hipEventRecord(c->ev_k1a, c->aux));
+                    RSH_HIP(hipEventRecord(c->ev_pha, c->aux));
+                    RSH_HIP(rsh::launch_block_sums_segments(c->segs.as<rsh::K1Seg>(), nseg,
+                                                            reinterpret_cast<const rsh::K1Tail*>(
+                                                                c->segs.as<uint8_t>() + nseg * sizeof(rsh::K1Seg)),
+                                                            ntail, (uint32_t)B, (uint32_t)dl, seed_word(seed), c->aux));
+                    RSH_HIP(hipEventRecord(c->ev_k1b, c->aux));
+                    RSH_HIP(hipEventRecord(c->ev_phb, c->aux));
+                    RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak,
+                                                    d_strong, (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(),
+                                                    c->aux));
+                    if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, c->aux));
+                    RSH_HIP(hipEventRecord(c->ev_flags, c->aux));
+                    RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)P * 4, hipMemcpyDeviceToHost, c->aux));
+                    if (dl > 0)
+                        RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)P * dl, hipMemcpyDeviceToHost, c->aux));
+                    RSH_HIP(hipEventRecord(c->ev_spec, c->aux));
+                    RSH_HIP(hipMemcpyAsync(c->h_pw.p, c->ph_weak.p, (size_t)Q * 4, hipMemcpyDeviceToHost, c->aux));
+                    if (dl > 0)
+                        RSH_HIP(hipMemcpyAsync(c->h_ps.p, c->ph_strong.p, (size_t)Q * dl, hipMemcpyDeviceToHost, c->aux));
+                    RSH_HIP(hipEventRecord(c->ev_phase, c->aux));
+                    be.phase_adopt(s0, Q, gph);
+                    res->stats.phase_guesses++;
+                    spec_launched = seg_launched = true;
+                }
+            }
+        }
+    }
+    if (defer_prefix && !seg_launched) {  // the prefix alone, and the guess's speculation (if any) beside it
+        const int rc = launch_spec();
+        if (rc != RSH_OK) return rc;
+        spec_launched = true;
+        if (guess >= 0) {
+            const int64_t before = be.ph_launches;
+            be.phase_hint(guess - ((guess - run_last * B) / B) * B);  // from the run's last sampled window on
+            res->stats.phase_guesses += be.ph_launches - before;
+        }
+    } else if (!defer_prefix && guess >= 0) {
+        const int64_t before = be.ph_launches;
+        be.phase_hint(guess - ((guess - run_last * B) / B) * B);
+        res->stats.phase_guesses += be.ph_launches - before;
+    }
+    be.na = spec_na;
+    be.partial = spec_na < na;
     rsh::ResolveState rs;
     bool landed = false;
     int spec_rc = RSH_OK;

@@ -104,6 +104,7 @@ struct rsh_ctx {
     DevBuf data, weak, strong;                   // host-input staging
     DevBuf src_weak, src_strong, flags;          // aligned speculation over the source
     DevBuf ph_weak, ph_strong;                   // phase-shifted speculation over [s0, n) (chains at kB + delta)
+    DevBuf segs;                                 // segmented K1 descriptors (prefix + phase speculation)
     DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw, partials, bucket;
     hipStream_t aux = nullptr;                   // the aligned speculation
     hipStream_t phase = nullptr;                 // the phase-shifted speculation (beside a prefix speculation)
@@ -113,6 +114,7 @@ struct rsh_ctx {
     hipEvent_t ev_pha = nullptr, ev_phb = nullptr;  // timing: the phase-shifted speculation's K1 (stats)
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
     PinnedBuf h_pw, h_ps;  // the phase-shifted speculation's sums (host copies)
+    PinnedBuf h_segs;      // staging of the segmented K1 descriptors
     PinnedBuf h_lead;      // T(kB) of the first aligned windows (the speculation launch decision)
     // resolver round trips: the small kernels read their inputs from and write their outputs to pinned
     // host memory directly (no staging copies); the probe result and digest windows come back by copy

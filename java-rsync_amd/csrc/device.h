@@ -49,6 +49,26 @@ struct K1Lane {
     uint32_t B, dl, c_first, nchunks;
     int32_t file = 0;     // index of its file in the planner's list (host bookkeeping only)
 };
+// Segmented K1 (the Sender's prefix + phase-shifted speculation in one launch): K1Seg = one wave of 64 full
+// chunks of length B starting at lines + a (lines 128-B aligned, [lines, lines + 64 B + 128) readable), with
+// its own output slots and abort word; K1Tail = one leftover chunk (chunk c of the file (data, n)).
+struct K1Seg {
+    const uint8_t* lines;
+    int32_t* weak;
+    uint8_t* strong;
+    const int* abort;
+    int32_t abort_gen;
+    uint32_t a;
+};
+struct K1Tail {
+    const uint8_t* data;
+    int64_t n;
+    int32_t* weak;  // the file's output arrays (chunk c is written at weak[c], strong[c * dl])
+    uint8_t* strong;
+    uint32_t c;
+};
+hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const K1Tail* d_tails, uint32_t ntail,
+                                      uint32_t B, uint32_t dl, uint32_t seed_word, hipStream_t s);
 void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Group>* groups,
                            std::vector<K1Lane>* lanes, int* lane_align);
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,

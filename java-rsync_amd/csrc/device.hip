@@ -692,22 +692,18 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
 //  * Tail waves (blockIdx >= main_waves): one lane per remaining chunk on the per-lane path (any alignment),
 //    dispatched with the main waves rather than as a second launch queued behind them.
 // ------------------------------------------------------------------------------------------------
+// One wave of the shift kernel: 64 full chunks whose first byte is gdata + a (gdata 128-B aligned; the host
+// checked [gdata, gdata + 64 B + 128) lies in the data's allocation); weak_out / strong_out point at the
+// wave's chunk 0.
 template <int W>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGPR))) void block_sums_shift_kernel(
-    const uint8_t* __restrict__ data, int64_t n, uint32_t a, uint32_t B, uint32_t nchunks, uint32_t main_waves,
-    uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out, uint8_t* __restrict__ strong_out,
-    const int* abort_flag, int abort_gen) {
-    if (blockIdx.x >= main_waves) {
-        const uint32_t c = main_waves * 64u + (blockIdx.x - main_waves) * 64u + threadIdx.x;
-        if (c < nchunks) lane_chunk_sums<0, 4, false>(data, n, B, c, dl, seed, weak_out, strong_out);
-        return;
-    }
+__device__ __forceinline__ void shift_wave(const uint8_t* __restrict__ gdata, uint32_t a, uint32_t B, uint32_t dl,
+                                           uint32_t seed, int32_t* __restrict__ weak_out,
+                                           uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen) {
     constexpr int ROW = 17;
     extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // 64 rows of ROW slots
     const int l = threadIdx.x;
-    const uint32_t c0 = blockIdx.x * 64u;
-    const uint8_t* gdata = data - a + (size_t)c0 * B;  // line-aligned; the host checked [gdata, +64 B + 128)
-    const uint32_t nst = B >> 7;                       // host guarantees 4 <= nst <= 1024
+    const uint32_t c0 = 0;
+    const uint32_t nst = B >> 7;  // host guarantees 4 <= nst <= 1024
     const uint32_t Q = a >> 4, r = a & 3;
     const int wr0 = (l >> 3) * ROW + (l & 7);
     const int row = l * ROW;
@@ -880,6 +876,55 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGP
     const int32_t s2 = (int32_t)(B * S - Ui);
     weak_out[c] = (int32_t)((S & 0xFFFFu) | ((uint32_t)s2 << 16));
     store_digest(strong_out + (size_t)c * dl, st, dl);
+}
+
+template <int W>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGPR))) void block_sums_shift_kernel(
+    const uint8_t* __restrict__ data, int64_t n, uint32_t a, uint32_t B, uint32_t nchunks, uint32_t main_waves,
+    uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out, uint8_t* __restrict__ strong_out,
+    const int* abort_flag, int abort_gen) {
+    if (blockIdx.x >= main_waves) {
+        const uint32_t c = main_waves * 64u + (blockIdx.x - main_waves) * 64u + threadIdx.x;
+        if (c < nchunks) lane_chunk_sums<0, 4, false>(data, n, B, c, dl, seed, weak_out, strong_out);
+        return;
+    }
+    const uint32_t c0 = blockIdx.x * 64u;
+    shift_wave<W>(data - a + (size_t)c0 * B, a, B, dl, seed, weak_out + c0, strong_out + (size_t)c0 * dl, abort_flag,
+                  abort_gen);
+}
+
+// Segmented K1: the waves of several chunk sets at different bases in one launch (the Sender's prefix
+// speculation at phase 0 and its phase-shifted speculation after an edit: separate launches would need one
+// wave more than the chip's 2048 wave slots, and the last wave would start only when another finished).
+// Waves [0, nseg) take a K1Seg each (64 full chunks; the dword offset W of its base chosen per wave);
+// waves past them take one chunk per lane from the K1Tail list (the segments' leftover chunks, any shape).
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGPR))) void block_sums_seg_kernel(
+    const K1Seg* __restrict__ segs, uint32_t nseg, const K1Tail* __restrict__ tails, uint32_t ntail, uint32_t B,
+    uint32_t dl, uint32_t seed) {
+    if (blockIdx.x >= nseg) {
+        const uint32_t i = (blockIdx.x - nseg) * 64u + threadIdx.x;
+        if (i < ntail) {
+            const K1Tail t = tails[i];
+            lane_chunk_sums<0, 4, false>(t.data, t.n, B, t.c, dl, seed, t.weak, t.strong);
+        }
+        return;
+    }
+    const K1Seg g = segs[blockIdx.x];
+    switch ((g.a >> 2) & 3) {
+        case 0: shift_wave<0>(g.lines, g.a, B, dl, seed, g.weak, g.strong, g.abort, g.abort_gen); break;
+        case 1: shift_wave<1>(g.lines, g.a, B, dl, seed, g.weak, g.strong, g.abort, g.abort_gen); break;
+        case 2: shift_wave<2>(g.lines, g.a, B, dl, seed, g.weak, g.strong, g.abort, g.abort_gen); break;
+        default: shift_wave<3>(g.lines, g.a, B, dl, seed, g.weak, g.strong, g.abort, g.abort_gen);
+    }
+}
+
+hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const K1Tail* d_tails, uint32_t ntail,
+                                      uint32_t B, uint32_t dl, uint32_t seed_word, hipStream_t s) {
+    if (nseg + ntail == 0) return hipSuccess;
+    const uint32_t waves = nseg + (ntail + 63) / 64;
+    hipLaunchKernelGGL(block_sums_seg_kernel, dim3(waves), dim3(64), 64 * 17 * sizeof(uint4), s, d_segs, nseg, d_tails,
+                       ntail, B, dl, seed_word);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------------

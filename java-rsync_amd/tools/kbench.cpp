@@ -2,7 +2,9 @@
 // Times each variant with hipEvents on its stream and checks every variant's output against
 // variant 0 bit for bit.  usage: kbench <MiB> <B> <dl> <reps> <variant>...
 // variant 1000: the production abortable launch (the Sender's speculation: abort word never set);
-// variant 1001: the production entry launch_block_sums without an abort word (the Generator).
+// variant 1001: the production entry launch_block_sums without an abort word (the Generator);
+// variant 1002: the batched launch over KBENCH_FILES (128) equal files cut from the buffer (config 4's shape).
+// Its parity check holds when per is a multiple of B (then the files' chunks are the buffer's chunks).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -53,7 +55,28 @@ int main(int argc, char** argv) {
     int* abort_word;
     CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&abort_word), 256, hipDeviceMallocUncached));
     CK(hipMemset(abort_word, 0, 256));
+    // variant 1002: the batched launch (config 4's shape) over the same buffer cut into KBENCH_FILES files
+    const int nfiles = getenv("KBENCH_FILES") ? atoi(getenv("KBENCH_FILES")) : 128;
+    std::vector<rsh::K1File> kf;
+    const int64_t per = n / nfiles;
+    for (int f = 0; f < nfiles; ++f) {
+        const uint32_t cf = (uint32_t)((per + B - 1) / B), c0 = (uint32_t)((int64_t)f * per / B);
+        kf.push_back(rsh::K1File{d + (int64_t)f * per, per, B, dl, cf, w + c0, sx + (size_t)c0 * dl});
+    }
+    std::vector<rsh::K1Group> groups;
+    std::vector<rsh::K1Lane> lanes;
+    int lane_align = 16;
+    rsh::plan_block_sums_batch(kf.data(), nfiles, &groups, &lanes, &lane_align);
+    rsh::K1Group* d_groups;
+    rsh::K1Lane* d_lanes;
+    CK(hipMalloc(&d_groups, (groups.size() + 1) * sizeof(rsh::K1Group)));
+    CK(hipMalloc(&d_lanes, (lanes.size() + 1) * sizeof(rsh::K1Lane)));
+    CK(hipMemcpy(d_groups, groups.data(), groups.size() * sizeof(rsh::K1Group), hipMemcpyHostToDevice));
+    if (!lanes.empty()) CK(hipMemcpy(d_lanes, lanes.data(), lanes.size() * sizeof(rsh::K1Lane), hipMemcpyHostToDevice));
     auto launch = [&](int v) {
+        if (v == 1002)
+            return rsh::launch_block_sums_batch(d_groups, (uint32_t)groups.size(), d_lanes, (uint32_t)lanes.size(),
+                                                lane_align, 0x04030201u, s);
         if (v == 1000) return rsh::launch_block_sums_variant(-1, d, n, B, C, dl, 0x04030201u, w, sx, s, abort_word, 1);
         if (v == 1001) return rsh::launch_block_sums(d, n, B, C, dl, 0x04030201u, w, sx, s);  // the production entry
         return rsh::launch_block_sums_variant(v, d, n, B, C, dl, 0x04030201u, w, sx, s);
