@@ -663,8 +663,9 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     bool spec_wait = false;
     int64_t run_last = -1, run_miss = -1;  // a sampled run's last matching window, the first sample past it
     bool defer_prefix = false;             // the prefix speculation waits for the phase guess (below)
-    static const bool guess_on = !getenv("RSH_SCAN_PHASE_GUESS") || atoi(getenv("RSH_SCAN_PHASE_GUESS")) != 0;
-    static const bool seg_on = !getenv("RSH_SCAN_SEGMENTED") || atoi(getenv("RSH_SCAN_SEGMENTED")) != 0;  // A/B
+    // A/B switches, read per scan (tests flip them)
+    const bool guess_on = !getenv("RSH_SCAN_PHASE_GUESS") || atoi(getenv("RSH_SCAN_PHASE_GUESS")) != 0;
+    const bool seg_on = !getenv("RSH_SCAN_SEGMENTED") || atoi(getenv("RSH_SCAN_SEGMENTED")) != 0;
     static const bool wait_on = !getenv("RSH_SCAN_WAIT") || atoi(getenv("RSH_SCAN_WAIT")) != 0;  // A/B
     static const bool sample_on = !getenv("RSH_SCAN_SAMPLE") || atoi(getenv("RSH_SCAN_SAMPLE")) != 0;  // A/B
     if (head && nlead > 0 && (!spec_launched || spec_tentative)) {

@@ -215,14 +215,17 @@ def test_sender_phase_shift_chains(ctx):
     assert st["phase_launches"] >= 1 and st["phase_matches"] > 6000 and st["host_md5_windows"] < 100, st
 
 
+@pytest.mark.parametrize("segmented", ["1", "0"])
 @pytest.mark.parametrize("edit", ["insert1", "delete3", "two_inserts", "insert_far"])
-def test_sender_phase_guess(ctx, edit):
+def test_sender_phase_guess(ctx, edit, segmented, monkeypatch):
     """A source that follows the basis up to an edit and continues at another phase after it (4096 windows at
     B = 65536, samples every 4): the speculation covers the sampled prefix only, and before the resolver starts
     the backend finds the phase past the run (a range probe plus four consecutive chunk sums) and starts the
     phase-shifted speculation there.  two_inserts: a second insert two windows after the first, so the guess
     (past both) is not the phase the resolver meets first.  insert_far: the edit is past every sample but the
-    last.  Events equal the oracle's in every case."""
+    last.  segmented=1: the prefix and the guessed phase go out as one segmented K1 launch (per-wave bases,
+    shared per-lane tail waves); 0: two launches.  Events equal the oracle's in every case."""
+    monkeypatch.setenv("RSH_SCAN_SEGMENTED", segmented)
     B, dl = 65536, 4
     basis = O.splitmix(256 << 20, 0x5EED5EED000000C3)
     x = 300 * B + 777
