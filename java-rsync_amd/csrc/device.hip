@@ -106,6 +106,36 @@ __device__ __forceinline__ void load_block(const uint8_t* p, uint4 (&q)[4]) {
         const uint32_t* v = reinterpret_cast<const uint32_t*>(p);
 #pragma unroll
         for (int i = 0; i < 4; ++i) q[i] = make_uint4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+    } else if constexpr (ALIGN == 2) {
+        // any alignment, wide loads: the 4 or 5 aligned 16-B pieces that hold the 64 bytes, then a per-lane
+        // dword select (lanes of one wave may sit at different offsets) and a byte funnel shift; the fifth
+        // piece is read only when the block is not 16-B aligned (it holds byte p + 63 then)
+        const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
+        const u32x4* v = reinterpret_cast<const u32x4*>(pa & ~(uintptr_t)15);
+        const uint32_t o = (uint32_t)(pa & 15), wo = o >> 2, sh = o & 3;
+        uint32_t d[20];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4 t = v[i];
+            d[4 * i] = t.x;
+            d[4 * i + 1] = t.y;
+            d[4 * i + 2] = t.z;
+            d[4 * i + 3] = t.w;
+        }
+        u32x4 t4 = {0u, 0u, 0u, 0u};
+        if (o) t4 = v[4];
+        d[16] = t4.x;
+        d[17] = t4.y;
+        d[18] = t4.z;
+        d[19] = t4.w;
+        uint32_t e[17];
+#pragma unroll
+        for (int i = 0; i < 17; ++i) e[i] = wo == 0 ? d[i] : wo == 1 ? d[i + 1] : wo == 2 ? d[i + 2] : d[i + 3];
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_alignbyte(e[i + 1], e[i], sh);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
     } else if constexpr (ALIGN == 0) {
         // any alignment: the 16 or 17 aligned dwords that hold the 64 bytes, funnel-shifted (v_alignbyte_b32);
         // the 17th is read only when the block is not dword aligned, so no byte past p + 63's dword is touched
@@ -484,15 +514,13 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
     if constexpr (!MULTI) {
         // tail waves (blockIdx >= main_waves): one lane per chunk left over (a partial last wave, the short last
         // chunk), dispatched with the main waves rather than as a launch queued behind them (a lone wave takes
-        // as long as one lane's window: 1.9 ms at B = 128 KiB)
+        // as long as one lane's window: 1.9 ms at B = 128 KiB).  Plain dwordx4 loads at the lane's own address,
+        // 16-B aligned or not (gfx950 serves unaligned vector loads; bit-exact at every offset, tests): kbench,
+        // 16 GiB of per-lane waves at B = 128 KiB, 3.6 ms with plain loads against 7.7 ms non-temporal and
+        // 4.7 ms funnel-shifting 17 dword loads per block (one wave alone: 1.6 ms, the coalesced kernel 1.9).
         if (blockIdx.x >= main_waves) {
             const uint32_t c = main_waves * 64u + (blockIdx.x - main_waves) * 64u + threadIdx.x;
-            if (c < nchunks) {
-                if ((reinterpret_cast<uintptr_t>(data) % 16) == 0)
-                    lane_chunk_sums<16, TAIL_PF>(data, n, B, c, dl, seed, weak_out, strong_out);
-                else
-                    lane_chunk_sums<0, TAIL_PF, false>(data, n, B, c, dl, seed, weak_out, strong_out);
-            }
+            if (c < nchunks) lane_chunk_sums<16, TAIL_PF, false>(data, n, B, c, dl, seed, weak_out, strong_out);
             return;
         }
     }
@@ -885,7 +913,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGP
     const int* abort_flag, int abort_gen) {
     if (blockIdx.x >= main_waves) {
         const uint32_t c = main_waves * 64u + (blockIdx.x - main_waves) * 64u + threadIdx.x;
-        if (c < nchunks) lane_chunk_sums<0, 4, false>(data, n, B, c, dl, seed, weak_out, strong_out);
+        if (c < nchunks) lane_chunk_sums<16, 4, false>(data, n, B, c, dl, seed, weak_out, strong_out);
         return;
     }
     const uint32_t c0 = blockIdx.x * 64u;
@@ -898,6 +926,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGP
 // wave more than the chip's 2048 wave slots, and the last wave would start only when another finished).
 // Waves [0, nseg) take a K1Seg each (64 full chunks; the dword offset W of its base chosen per wave);
 // waves past them take one chunk per lane from the K1Tail list (the segments' leftover chunks, any shape).
+template <int TAIL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGPR))) void block_sums_seg_kernel(
     const K1Seg* __restrict__ segs, uint32_t nseg, const K1Tail* __restrict__ tails, uint32_t ntail, uint32_t B,
     uint32_t dl, uint32_t seed) {
@@ -905,7 +934,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGP
         const uint32_t i = (blockIdx.x - nseg) * 64u + threadIdx.x;
         if (i < ntail) {
             const K1Tail t = tails[i];
-            lane_chunk_sums<0, 4, false>(t.data, t.n, B, t.c, dl, seed, t.weak, t.strong);
+            if constexpr (TAIL == 0) lane_chunk_sums<2, 4, false>(t.data, t.n, B, t.c, dl, seed, t.weak, t.strong);
+            else if constexpr (TAIL == 1) lane_chunk_sums<0, 4, false>(t.data, t.n, B, t.c, dl, seed, t.weak, t.strong);
+            else lane_chunk_sums<16, 4, false>(t.data, t.n, B, t.c, dl, seed, t.weak, t.strong);
         }
         return;
     }
@@ -922,8 +953,21 @@ hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const 
                                       uint32_t B, uint32_t dl, uint32_t seed_word, hipStream_t s) {
     if (nseg + ntail == 0) return hipSuccess;
     const uint32_t waves = nseg + (ntail + 63) / 64;
-    hipLaunchKernelGGL(block_sums_seg_kernel, dim3(waves), dim3(64), 64 * 17 * sizeof(uint4), s, d_segs, nseg, d_tails,
-                       ntail, B, dl, seed_word);
+    // tail lanes (A/B, read per launch: RSH_K1_TAIL=1 (default) dword loads + funnel, 0 wide aligned loads + a
+    // per-lane select, 2 plain unaligned dwordx4).  kbench, 2047 coalesced waves + one tail wave of 64 chunks
+    // at offset 1: 3.70-3.75 / 4.13-4.19 / 4.19-4.28 ms (3.33 ms without the tail wave)
+    const char* tm = getenv("RSH_K1_TAIL");
+    const int mode = tm ? atoi(tm) : 1;
+    const size_t lb = 64 * 17 * sizeof(uint4);
+    if (mode == 1)
+        hipLaunchKernelGGL(block_sums_seg_kernel<1>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
+                           seed_word);
+    else if (mode == 2)
+        hipLaunchKernelGGL(block_sums_seg_kernel<2>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
+                           seed_word);
+    else
+        hipLaunchKernelGGL(block_sums_seg_kernel<0>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
+                           seed_word);
     return hipGetLastError();
 }
 
@@ -1029,6 +1073,18 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
     if (nchunks == 0) return hipSuccess;
     const uintptr_t addr = reinterpret_cast<uintptr_t>(d_data);
     if (variant < 0) variant = 19;  // coalesced, 2 stages in flight, weak sums on the matrix pipe
+    if (variant == 3000 || variant == 3001 || variant == 3002) {  // kbench A/B: the per-lane path at any base
+        if (variant == 3002)
+            hipLaunchKernelGGL((block_sums_kernel<2, 4, false>), dim3((nchunks + 63) / 64), dim3(64), 0, s, d_data, n,
+                               B, nchunks, dl, seed_word, d_weak, d_strong, 0u);
+        else if (variant == 3000)
+            hipLaunchKernelGGL((block_sums_kernel<16, 4, false>), dim3((nchunks + 63) / 64), dim3(64), 0, s, d_data, n,
+                               B, nchunks, dl, seed_word, d_weak, d_strong, 0u);
+        else
+            hipLaunchKernelGGL((block_sums_kernel<0, 4, false>), dim3((nchunks + 63) / 64), dim3(64), 0, s, d_data, n,
+                               B, nchunks, dl, seed_word, d_weak, d_strong, 0u);
+        return hipGetLastError();
+    }
     uint32_t c_first = 0;
     const bool deep = variant == 4 || variant == 6 || variant == 7 || variant == 9 || variant == 10 ||
                       variant == 11 || variant == 12 || variant == 14 || variant == 15 || variant == 16 ||

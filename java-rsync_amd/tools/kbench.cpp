@@ -5,6 +5,7 @@
 // variant 1001: the production entry launch_block_sums without an abort word (the Generator);
 // variant 1002: the batched launch over KBENCH_FILES (128) equal files cut from the buffer (config 4's shape).
 // Its parity check holds when per is a multiple of B (then the files' chunks are the buffer's chunks).
+// variant 1003: the segmented launch (the Sender's prefix + phase speculation kernel) over the buffer.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -28,7 +29,8 @@ int main(int argc, char** argv) {
         fprintf(stderr, "usage: kbench <MiB> <B> <dl> <reps> <variant>...\n");
         return 2;
     }
-    const int64_t n = (int64_t)atoll(argv[1]) << 20;
+    // KBENCH_TRIM=t: t bytes fewer than the MiB count (a short last chunk, a partial last wave)
+    const int64_t n = ((int64_t)atoll(argv[1]) << 20) - (getenv("KBENCH_TRIM") ? atoll(getenv("KBENCH_TRIM")) : 0);
     const uint32_t B = (uint32_t)atoi(argv[2]), dl = (uint32_t)atoi(argv[3]);
     const int reps = atoi(argv[4]);
     const uint32_t C = (uint32_t)((n + B - 1) / B);
@@ -39,6 +41,12 @@ int main(int argc, char** argv) {
     uint8_t *s0, *sx;
     // KBENCH_OFFSET=k: the data starts k bytes past a 256-B aligned allocation (unaligned-base A/B)
     const int64_t off = getenv("KBENCH_OFFSET") ? atoll(getenv("KBENCH_OFFSET")) : 0;
+    // KBENCH_PREALLOC=k: k buffers of the same size allocated (and filled) first, as the bench's other pairs are
+    for (int k = 0; k < (getenv("KBENCH_PREALLOC") ? atoi(getenv("KBENCH_PREALLOC")) : 0); ++k) {
+        uint8_t* pre;
+        CK(hipMalloc(&pre, n + 64));
+        CK(rsh::launch_fill_splitmix(pre, n, 0x1234 + k, 0, s));
+    }
     CK(hipMalloc(&d, n + off + 64));
     d += off;
     CK(hipMalloc(&w0, C * 4));
@@ -73,7 +81,27 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d_lanes, (lanes.size() + 1) * sizeof(rsh::K1Lane)));
     CK(hipMemcpy(d_groups, groups.data(), groups.size() * sizeof(rsh::K1Group), hipMemcpyHostToDevice));
     if (!lanes.empty()) CK(hipMemcpy(d_lanes, lanes.data(), lanes.size() * sizeof(rsh::K1Lane), hipMemcpyHostToDevice));
+    // variant 1003: the segmented launch (block_sums_seg_kernel) over the whole buffer as one segment; the
+    // buffer's base must be such that base - base % 128 is inside the allocation (KBENCH_OFFSET < 128)
+    const uint32_t a_off = (uint32_t)(reinterpret_cast<uintptr_t>(d) % 128);
+    const uint32_t nfull = (uint32_t)(n / B), nw = nfull / 64;
+    std::vector<rsh::K1Seg> segs;
+    std::vector<rsh::K1Tail> tails;
+    int* never;
+    CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&never), 256, hipDeviceMallocUncached));
+    CK(hipMemset(never, 0, 256));
+    for (uint32_t v = 0; v < nw; ++v)
+        segs.push_back(rsh::K1Seg{d - a_off + (size_t)v * 64 * B, w + v * 64, sx + (size_t)v * 64 * dl, never, -1, a_off});
+    for (uint32_t c = nw * 64; c < C; ++c) tails.push_back(rsh::K1Tail{d, n, w, sx, c});
+    rsh::K1Seg* d_segs;
+    CK(hipMalloc(&d_segs, segs.size() * sizeof(rsh::K1Seg) + tails.size() * sizeof(rsh::K1Tail) + 64));
+    CK(hipMemcpy(d_segs, segs.data(), segs.size() * sizeof(rsh::K1Seg), hipMemcpyHostToDevice));
+    rsh::K1Tail* d_tails = reinterpret_cast<rsh::K1Tail*>(d_segs + segs.size());
+    if (!tails.empty()) CK(hipMemcpy(d_tails, tails.data(), tails.size() * sizeof(rsh::K1Tail), hipMemcpyHostToDevice));
     auto launch = [&](int v) {
+        if (v == 1003)
+            return rsh::launch_block_sums_segments(d_segs, (uint32_t)segs.size(), d_tails, (uint32_t)tails.size(), B, dl,
+                                                   0x04030201u, s);
         if (v == 1002)
             return rsh::launch_block_sums_batch(d_groups, (uint32_t)groups.size(), d_lanes, (uint32_t)lanes.size(),
                                                 lane_align, 0x04030201u, s);
