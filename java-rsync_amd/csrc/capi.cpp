@@ -565,10 +565,16 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     int gen = ++c->gen;  // a stopped speculation's generation; a later launch takes a new one
     static const int diag = getenv("RSH_SCAN_DIAG") ? atoi(getenv("RSH_SCAN_DIAG")) : 0;  // A/B switches
     int64_t spec_na = na;  // windows the speculation covers: all, or a prefix (sampled launch decision)
+    // The speculation K1 starts after the table and sample work on the context stream (~0.1 ms of small kernels)
+    // rather than beside it: every K1 wave holds its SIMD for the whole launch, so the waves that share their
+    // SIMDs with those kernels set the launch's end (r2: 3.13 ms ordered against 3.40-3.49 ms beside them;
+    // the step 6.48-6.58 against 6.67 ms).  RSH_SCAN_SPEC_ORDER=0 (A/B, read per scan): beside them.
+    const bool spec_after_prep = !getenv("RSH_SCAN_SPEC_ORDER") || atoi(getenv("RSH_SCAN_SPEC_ORDER")) != 0;
+    bool prep_recorded = false;
     auto launch_spec = [&]() -> int {
         const int64_t sn = std::min<int64_t>(n, spec_na * B);  // bytes: whole windows, or to the end
         const int64_t snf = std::min<int64_t>(spec_na, C);
-        RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
+        RSH_HIP(hipStreamWaitEvent(c->aux, spec_after_prep && prep_recorded ? c->ev_prep : c->ev_in, 0));
         RSH_HIP(hipEventRecord(c->ev_k1a, c->aux));
         RSH_HIP(rsh::launch_block_sums(d_src, sn, (uint32_t)B, (uint32_t)spec_na, (uint32_t)dl, seed_word(seed),
                                        c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->aux,
@@ -613,6 +619,10 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         lf->B = (uint32_t)B;
         for (int64_t i = 0; i < nsamp; ++i) ents[i] = rsh::GatherEnt{samp[(size_t)i] * B, 0, 0};
         RSH_HIP(rsh::launch_window_weak(lf, ents, (uint32_t)nsamp, lead_w, c->stream));
+    }
+    if (spec_after_prep) {
+        RSH_HIP(hipEventRecord(c->ev_prep, c->stream));
+        prep_recorded = true;
     }
 
     // Launch-then-confirm: when one K1 round covers every window (na <= kRoundWindows), the speculation that
@@ -1066,6 +1076,7 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
         hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_phase, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_flags, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev_k1a) != hipSuccess || hipEventCreate(&c->ev_k1b) != hipSuccess ||
         hipEventCreate(&c->ev_pha) != hipSuccess || hipEventCreate(&c->ev_phb) != hipSuccess ||
         hipExtMallocWithFlags(reinterpret_cast<void**>(&c->abort_word), 256, hipDeviceMallocUncached) != hipSuccess ||

@@ -109,6 +109,7 @@ struct rsh_ctx {
     hipStream_t aux = nullptr;                   // the aligned speculation
     hipStream_t phase = nullptr;                 // the phase-shifted speculation (beside a prefix speculation)
     hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr, ev_phase = nullptr;
+    hipEvent_t ev_prep = nullptr;   // the scan's table and sample work on the context stream (A/B ordering)
     hipEvent_t ev_flags = nullptr;  // batched speculation: its chain flags are on the host (before its sums)
     hipEvent_t ev_k1a = nullptr, ev_k1b = nullptr;  // timing: the aligned speculation's K1 (stats)
     hipEvent_t ev_pha = nullptr, ev_phb = nullptr;  // timing: the phase-shifted speculation's K1 (stats)
@@ -148,6 +149,7 @@ struct rsh_ctx {
         if (ev_spec) (void)hipEventDestroy(ev_spec);
         if (ev_phase) (void)hipEventDestroy(ev_phase);
         if (ev_flags) (void)hipEventDestroy(ev_flags);
+        if (ev_prep) (void)hipEventDestroy(ev_prep);
         if (ev_k1a) (void)hipEventDestroy(ev_k1a);
         if (ev_k1b) (void)hipEventDestroy(ev_k1b);
         if (ev_pha) (void)hipEventDestroy(ev_pha);

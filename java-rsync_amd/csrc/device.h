@@ -71,6 +71,9 @@ hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const 
                                       uint32_t B, uint32_t dl, uint32_t seed_word, hipStream_t s);
 void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Group>* groups,
                            std::vector<K1Lane>* lanes, int* lane_align);
+// the same over groups only, at 4 waves per SIMD (block_sums_quad_kernel; A/B: RSH_K1_QUAD=1, kbench 1004)
+hipError_t launch_block_sums_batch_quad(const K1Group* d_groups, uint32_t ngroups, uint32_t seed_word, hipStream_t s,
+                                        const int* abort_flag = nullptr, int abort_gen = 0);
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
                                    int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag = nullptr,
                                    int abort_gen = 0);

@@ -700,6 +700,157 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
     store_digest(strong_out + (size_t)c * dl, st, dl);
 }
 
+// ------------------------------------------------------------------------------------------------
+// K1 at 4 waves per SIMD (batched groups, one K1Group per wave).  A wave issues at most one VALU
+// instruction per ~2.7 SIMD slots of a full-rate op, so two waves leave a SIMD's VALU a quarter idle and
+// the half-rate rotate half idle (tools/op_rate.hip: SIMD cost per wave-instruction v_add_u32 2.69 at 2
+// waves, 2.01 at 4; v_alignbit_b32 4.79 / 3.39).  The pipelined kernel needs 176 VGPRs and two 9 KiB LDS
+// buffers (2 waves/SIMD); this one keeps one buffer and one stage of loads in flight so that four waves
+// fit (<= 128 VGPRs, 9 KiB LDS): the reads of stage s are issued before stage s + 1 overwrites the buffer
+// (a wave's LDS operations execute in order), and the other waves hide the latency the shallower
+// pipeline exposes.  Same data path and outputs as block_sums_pipe_kernel<.., MULTI = true>.
+// ------------------------------------------------------------------------------------------------
+template <bool ABORT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void block_sums_quad_kernel(
+    const K1Group* __restrict__ groups, uint32_t seed, const int* abort_flag, int abort_gen) {
+    constexpr int ROW = 9;
+    extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // one buffer: 64 rows of ROW slots
+    const int l = threadIdx.x;
+    const K1Group g = groups[blockIdx.x];
+    const uint8_t* gdata = g.data;
+    const uint32_t B = g.B, dl = g.dl;
+    if constexpr (ABORT) {
+        if (g.abort) abort_flag = g.abort;
+    }
+    const uint32_t nst = B >> 7;  // host guarantees nst >= 2
+    const int wr0 = (l >> 3) * ROW + (l & 7);
+    const int rd0 = l * ROW;
+    v4i32 wA[2];
+    v4i32 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    int32_t Racc[4] = {0, 0, 0, 0};
+    {
+        const int row = l & 15, ks = l >> 4;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                uint32_t word = 0;
+                if (row == 0) word = 0x01010101u;
+                else if (row == 1)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) word |= (uint32_t)(16 * (4 * h + mfma_sigma(ks)) + 4 * w + b) << (8 * b);
+                wA[h][w] = (int)word;
+            }
+    }
+    const int rdB = mfma_pi(l & 15) * ROW + mfma_sigma(l >> 4);
+    uint4 q[8];
+    uint4 Wa[4], Wb[4];
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(gdata), 0, (int)(64 * B), 0x00020000);
+    const uint32_t lane_off = (uint32_t)(l >> 3) * B + 16u * (uint32_t)(l & 7);
+    auto load = [&](uint32_t stg) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_off + 128u * stg, (int)(j * 8u * B), 2);
+            q[j] = make_uint4(t.x, t.y, t.z, t.w);
+        }
+    };
+    auto put = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lds_all[wr0 + j * 8 * ROW] = q[j];
+    };
+    auto get_words = [&](uint4 (&w)[4], int h) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = lds_all[rd0 + 4 * h + k];
+    };
+    Md5State st = md5_init();
+    auto md5_block = [&](const uint4 (&w)[4]) __attribute__((always_inline)) {
+        uint32_t m[16];
+        unpack(w, m);
+        md5_stream_block<8>(st, m);
+    };
+    // the weak-sum MFMAs of the stage in the buffer, operands read half by half (16 VGPRs at a time)
+    auto weak_mfma = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) Racc[g4] += acc[g4][0];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint4 Bv[4];
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) Bv[g4] = lds_all[16 * ROW * g4 + rdB + 4 * h];
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const v4i32 b4 = {(int)Bv[g4].x, (int)Bv[g4].y, (int)Bv[g4].z, (int)Bv[g4].w};
+                acc[g4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wA[h], b4, acc[g4], 0, 0, 0);
+            }
+        }
+    };
+    load(0);
+    if constexpr (ABORT) {
+        int f0;
+        asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(f0) : "s"(abort_flag));
+        if (f0 == abort_gen) return;
+    }
+    put();
+    load(1);
+    compiler_fence();
+    get_words(Wa, 0);
+    [[maybe_unused]] int flag = 0;
+    for (uint32_t s = 0; s < nst; ++s) {
+        const bool has_next = s + 1 < nst;
+        if constexpr (ABORT) {
+            if ((s & 1) == 0) asm volatile("s_load_dword %0, %1, 0x0 glc" : "=s"(flag) : "s"(abort_flag));
+        }
+        get_words(Wb, 1);
+        weak_mfma();
+        compiler_fence();
+        if (has_next) {
+            put();  // stage s + 1 (its reads of stage s were issued above)
+            if (s + 2 < nst) load(s + 2);
+        }
+        compiler_fence();
+        md5_block(Wa);
+        compiler_fence();
+        if (has_next) get_words(Wa, 0);
+        md5_block(Wb);
+        compiler_fence();
+        if constexpr (ABORT) {
+            if (s & 1) {
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(flag));
+                if (flag == abort_gen) return;
+            }
+        }
+    }
+    {
+        const uint64_t bits = ((uint64_t)B + 4) * 8;
+        uint32_t m[16] = {seed, 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, (uint32_t)bits, (uint32_t)(bits >> 32)};
+        md5_compress(st, m);
+    }
+    int32_t s1, u;
+    {
+        int32_t s1g[4], ug[4];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            Racc[g4] += acc[g4][0];
+            s1g[g4] = acc[g4][0];
+            ug[g4] = (int32_t)(128u * (nst * (uint32_t)acc[g4][0] - (uint32_t)Racc[g4])) + acc[g4][1];
+        }
+        const int src = mfma_pi_inv(l & 15);
+        int32_t t1[4], tu[4];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            t1[g4] = __shfl(s1g[g4], src, 64);
+            tu[g4] = __shfl(ug[g4], src, 64);
+        }
+        const int gs = l >> 4;
+        s1 = gs == 0 ? t1[0] : gs == 1 ? t1[1] : gs == 2 ? t1[2] : t1[3];
+        u = gs == 0 ? tu[0] : gs == 1 ? tu[1] : gs == 2 ? tu[2] : tu[3];
+    }
+    const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
+    g.weak[l] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
+    store_digest(g.strong + (size_t)l * dl, st, dl);
+}
+
 #ifndef RSH_K1_SHIFT_VGPR
 #define RSH_K1_SHIFT_VGPR 256  // 2 waves/SIMD (the LDS ring and the MFMA tiles of the aligned kernel, plus the funnel)
 #endif
@@ -1476,11 +1627,30 @@ static bool plain_k1() {
     return v;
 }
 
+hipError_t launch_block_sums_batch_quad(const K1Group* d_groups, uint32_t ngroups, uint32_t seed_word, hipStream_t s,
+                                        const int* abort_flag, int abort_gen) {
+    if (ngroups == 0) return hipSuccess;
+    const size_t lb = 64 * 9 * sizeof(uint4);
+    if (!abort_flag && (abort_flag = never_word()) != nullptr) abort_gen = -1;
+    if (abort_flag)
+        hipLaunchKernelGGL((block_sums_quad_kernel<true>), dim3(ngroups), dim3(64), lb, s, d_groups, seed_word, abort_flag,
+                           abort_gen);
+    else
+        hipLaunchKernelGGL((block_sums_quad_kernel<false>), dim3(ngroups), dim3(64), lb, s, d_groups, seed_word, nullptr, 0);
+    return hipGetLastError();
+}
+
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
                                    int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag,
                                    int abort_gen) {
     const size_t lb = 2 * 64 * 9 * sizeof(uint4);
+    static const bool quad = getenv("RSH_K1_QUAD") && atoi(getenv("RSH_K1_QUAD")) != 0;  // A/B: 4 waves/SIMD
     if (!abort_flag && !plain_k1() && (abort_flag = never_word()) != nullptr) abort_gen = -1;  // see never_word
+    if (ngroups > 0 && quad) {
+        const hipError_t e = launch_block_sums_batch_quad(d_groups, ngroups, seed_word, s, abort_flag, abort_gen);
+        if (e != hipSuccess) return e;
+        ngroups = 0;
+    }
     if (ngroups > 0) {
         if (abort_flag && batch_pin())
             hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true, 0, true>), dim3(ngroups), dim3(64), lb, s,
