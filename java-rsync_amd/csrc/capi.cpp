@@ -546,17 +546,6 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     RSH_HIP(c->h_lead.ensure(lead_ents_at + (size_t)(nsamp + 1) * sizeof(rsh::GatherEnt) + sizeof(rsh::ScanFile)));
 
     RSH_HIP(hipEventRecord(c->ev_in, c->stream));  // whatever produced the inputs on the caller's stream
-    // (stream) the received table: on the context stream, so that the aux stream's speculation launch
-    // (below) does not queue behind the download
-    if (download) {
-        if (C > 0) {
-            RSH_HIP(hipMemcpyAsync(c->h_weak.p, d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, c->stream));
-            if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_strong.p, d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, c->stream));
-        }
-        RSH_HIP(hipEventRecord(c->ev_tab, c->stream));
-        host_weak = c->h_weak.as<int32_t>();
-        host_strong = c->h_strong.as<uint8_t>();
-    }
     // (aux) the aligned speculation: the source's own block sums with the basis header's B and dl,
     // the chain flags, and their download.  It is a bet on long runs of aligned matches; in head mode it
     // is launched only once the resolver has taken kDeferSteps steps or kDeferMs without finishing
@@ -565,10 +554,11 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     int gen = ++c->gen;  // a stopped speculation's generation; a later launch takes a new one
     static const int diag = getenv("RSH_SCAN_DIAG") ? atoi(getenv("RSH_SCAN_DIAG")) : 0;  // A/B switches
     int64_t spec_na = na;  // windows the speculation covers: all, or a prefix (sampled launch decision)
-    // The speculation K1 starts after the table and sample work on the context stream (~0.1 ms of small kernels)
-    // rather than beside it: every K1 wave holds its SIMD for the whole launch, so the waves that share their
-    // SIMDs with those kernels set the launch's end (r2: 3.13 ms ordered against 3.40-3.49 ms beside them;
-    // the step 6.48-6.58 against 6.67 ms).  RSH_SCAN_SPEC_ORDER=0 (A/B, read per scan): beside them.
+    // The speculation K1 starts after the sample kernels on the context stream (window 0's copy and the lead and
+    // sample weak sums, ~50 us) rather than beside them: every K1 wave holds its SIMD for the whole launch, so
+    // the waves that share their SIMDs with a VALU-heavy kernel set the launch's end (r2: 3.13 ms ordered
+    // against 3.40-3.49 ms beside them; the step 6.48-6.58 against 6.67 ms).  RSH_SCAN_SPEC_ORDER=0 (A/B, read
+    // per scan): beside them.
     const bool spec_after_prep = !getenv("RSH_SCAN_SPEC_ORDER") || atoi(getenv("RSH_SCAN_SPEC_ORDER")) != 0;
     bool prep_recorded = false;
     auto launch_spec = [&]() -> int {
@@ -598,9 +588,6 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         if (rc != RSH_OK) return rc;
         spec_launched = true;
     }
-    // (stream) the device probe hash
-    RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, c->stream));
-    RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, c->stream));
     // (stream + a host thread) the digest of window 0: the first event of a scan over a similar file is
     // at position 0, and its MD5 (one serial chain, ~0.13 ms for 128 KiB) then overlaps the first probe
     const int64_t w0 = std::min<int64_t>(B, n);
@@ -624,6 +611,20 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         RSH_HIP(hipEventRecord(c->ev_prep, c->stream));
         prep_recorded = true;
     }
+    // (stream) the received table to the host (the lead check and the resolver), after the sample work: the
+    // speculation waits for the samples only, and these copies and the hash build below run beside it
+    if (download) {
+        if (C > 0) {
+            RSH_HIP(hipMemcpyAsync(c->h_weak.p, d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, c->stream));
+            if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_strong.p, d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, c->stream));
+        }
+        RSH_HIP(hipEventRecord(c->ev_tab, c->stream));
+        host_weak = c->h_weak.as<int32_t>();
+        host_strong = c->h_strong.as<uint8_t>();
+    }
+    // (stream) the device probe hash
+    RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, c->stream));
+    RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, c->stream));
 
     // Launch-then-confirm: when one K1 round covers every window (na <= kRoundWindows), the speculation that
     // the lead decides on below is launched now, before the host knows the table, so it starts the moment the

@@ -71,6 +71,24 @@ hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const 
                                       uint32_t B, uint32_t dl, uint32_t seed_word, hipStream_t s);
 void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Group>* groups,
                            std::vector<K1Lane>* lanes, int* lane_align);
+// Device-side group expansion: the host plans per file (K1Plan: the file's first group index g0 and its
+// count of full 64-chunk groups) and one thread per group writes its K1Group (expand_groups_kernel), instead of
+// the host building and uploading ~40 B per 64 chunks (config 4: 32768 groups, 1.5 MB, ~0.14 ms of host time
+// per batched call).  Lanes (tails, odd shapes) stay host-planned: they are few.
+struct K1Plan {
+    const uint8_t* data;
+    int32_t* weak;
+    uint8_t* strong;
+    uint32_t B, dl;
+    uint32_t g0, ng;            // groups [g0, g0 + ng) of the launch are this file's chunks [0, 64 ng)
+    const int* abort = nullptr;  // K1Group::abort of its groups
+    int32_t file = 0;
+};
+// plans (one per file with full groups, ascending g0) and the host lanes; returns the total group count
+uint32_t plan_block_sums_files(const K1File* files, int32_t nfiles, std::vector<K1Plan>* plans,
+                               std::vector<K1Lane>* lanes, int* lane_align);
+hipError_t launch_expand_groups(const K1Plan* d_plans, uint32_t nplans, uint32_t ngroups, K1Group* d_groups,
+                                hipStream_t s);
 // the same over groups only, at 4 waves per SIMD (block_sums_quad_kernel; A/B: RSH_K1_QUAD=1, kbench 1004)
 hipError_t launch_block_sums_batch_quad(const K1Group* d_groups, uint32_t ngroups, uint32_t seed_word, hipStream_t s,
                                         const int* abort_flag = nullptr, int abort_gen = 0);
@@ -89,7 +107,11 @@ struct ProbeTable {
     const unsigned long long* slots;
     uint32_t mask;
 };
-hipError_t launch_table_clear(unsigned long long* d_slots, uint32_t nslots, hipStream_t s);
+// bg (background): priority 0 and at most kBackgroundGroups workgroups, for table work that runs beside a K1
+// launch (a high-priority kernel spread over every CU slows the K1 waves that share its SIMDs, and the slowest
+// wave ends the launch)
+constexpr uint32_t kBackgroundGroups = 256;
+hipError_t launch_table_clear(unsigned long long* d_slots, uint64_t nslots, hipStream_t s, bool bg = false);
 hipError_t launch_table_insert(unsigned long long* d_slots, uint32_t mask, const int32_t* d_keys, uint32_t nkeys,
                                hipStream_t s);
 
@@ -185,7 +207,7 @@ struct CopyEnt {
     uint8_t* dst;
     int64_t len;
 };
-hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hipStream_t s);
+hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hipStream_t s, bool bg = false);
 // n bytes of device memory into pinned host memory (h_dst 16-byte aligned), by a kernel.
 hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s);
 // Byte ranges between arbitrary (unaligned) device addresses: one op per workgroup, 16-byte stores to
@@ -203,7 +225,8 @@ struct TableEnt {
     uint32_t mask;
     int32_t nkeys;
 };
-hipError_t launch_table_insert_many(const TableEnt* ents, uint32_t n, int32_t max_keys, hipStream_t s);
+hipError_t launch_table_insert_many(const TableEnt* ents, uint32_t n, int32_t max_keys, hipStream_t s,
+                                    bool bg = false);
 // Chain flags of many files.
 struct FlagEnt {
     const int32_t* wsrc;

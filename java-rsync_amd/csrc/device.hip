@@ -1604,6 +1604,57 @@ void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Gr
 }
 
 
+uint32_t plan_block_sums_files(const K1File* files, int32_t nfiles, std::vector<K1Plan>* plans,
+                               std::vector<K1Lane>* lanes, int* lane_align) {
+    plans->clear();
+    lanes->clear();
+    *lane_align = 16;
+    uint32_t g = 0;
+    for (int32_t f = 0; f < nfiles; ++f) {  // the same cut as plan_block_sums_batch
+        const K1File& F = files[f];
+        if (F.nchunks == 0 || F.B == 0) continue;
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(F.data);
+        const uint32_t nst = F.B >> 7;
+        uint32_t c = 0;
+        if ((F.B % 128) == 0 && nst >= 4 && nst <= 1024 && (addr % 16) == 0) {
+            const uint32_t nfullc = (uint32_t)std::min<int64_t>(F.n / F.B, F.nchunks);
+            const uint32_t ng = nfullc / 64;
+            if (ng > 0) plans->push_back(K1Plan{F.data, F.weak, F.strong, F.B, F.dl, g, ng, nullptr, f});
+            g += ng;
+            c = 64 * ng;
+        }
+        for (; c < F.nchunks; c += 64) {
+            lanes->push_back(K1Lane{F.data, F.n, F.weak, F.strong, F.B, F.dl, c, F.nchunks, f});
+            const int a = ((F.B % 16) == 0 && (addr % 16) == 0) ? 16 : ((F.B % 4) == 0 && (addr % 4) == 0) ? 4 : 1;
+            *lane_align = std::min(*lane_align, a);
+        }
+    }
+    return g;
+}
+
+__global__ __launch_bounds__(256) void expand_groups_kernel(const K1Plan* __restrict__ plans, uint32_t nplans,
+                                                            uint32_t ngroups, K1Group* __restrict__ groups) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ngroups) return;
+    uint32_t lo = 0, hi = nplans;  // the last plan with g0 <= t
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (plans[mid].g0 <= t) lo = mid;
+        else hi = mid;
+    }
+    const K1Plan& P = plans[lo];
+    const uint32_t c = 64 * (t - P.g0);
+    groups[t] = K1Group{P.data + (size_t)c * P.B, P.weak + c, P.strong + (size_t)c * P.dl, P.B, P.dl, P.abort, P.file};
+}
+
+hipError_t launch_expand_groups(const K1Plan* d_plans, uint32_t nplans, uint32_t ngroups, K1Group* d_groups,
+                                hipStream_t s) {
+    if (ngroups == 0 || nplans == 0) return hipSuccess;
+    hipLaunchKernelGGL(expand_groups_kernel, dim3((ngroups + 255) / 256), dim3(256), 0, s, d_plans, nplans, ngroups,
+                       d_groups);
+    return hipGetLastError();
+}
+
 // A word no launch ever writes: non-abortable K1 launches run the abortable instantiation polling it with
 // generation -1 (never stored).  Measured on the MI355X pool (round 2, kbench 16 GiB at B = 128 KiB, same
 // process, same buffer): the plain instantiation 4.07-4.57 ms, the abortable one 2.99-3.10 ms (the plain one
@@ -1716,9 +1767,9 @@ __device__ __forceinline__ uint32_t slot_hash(uint32_t key) {
     return h ^ (h >> 15);
 }
 
-__global__ void table_clear_kernel(unsigned long long* slots, uint32_t nslots) {
-    __builtin_amdgcn_s_setprio(3);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += gridDim.x * blockDim.x) slots[i] = 0ull;
+__global__ void table_clear_kernel(unsigned long long* slots, uint64_t nslots, int hi) {
+    if (hi) __builtin_amdgcn_s_setprio(3);
+    for (uint64_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * blockDim.x) slots[i] = 0ull;
 }
 
 __global__ void table_insert_kernel(unsigned long long* slots, uint32_t mask, const int32_t* __restrict__ keys,
@@ -1736,9 +1787,10 @@ __global__ void table_insert_kernel(unsigned long long* slots, uint32_t mask, co
     }
 }
 
-hipError_t launch_table_clear(unsigned long long* d_slots, uint32_t nslots, hipStream_t s) {
-    hipLaunchKernelGGL(table_clear_kernel, dim3(std::min<uint32_t>((nslots + 255) / 256, 2048u)), dim3(256), 0, s,
-                       d_slots, nslots);
+hipError_t launch_table_clear(unsigned long long* d_slots, uint64_t nslots, hipStream_t s, bool bg) {
+    const uint64_t cap = bg ? kBackgroundGroups : 2048u;
+    hipLaunchKernelGGL(table_clear_kernel, dim3((uint32_t)std::min<uint64_t>((nslots + 255) / 256, cap)), dim3(256), 0, s,
+                       d_slots, nslots, bg ? 0 : 1);
     return hipGetLastError();
 }
 
@@ -2258,18 +2310,18 @@ hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, 
 }
 
 // grid (., n): entry blockIdx.y, 16 bytes per thread, grid-strided over the entry's length
-__global__ __launch_bounds__(256) void copy_many_kernel(const CopyEnt* __restrict__ ents) {
-    __builtin_amdgcn_s_setprio(3);
+__global__ __launch_bounds__(256) void copy_many_kernel(const CopyEnt* __restrict__ ents, int hi) {
+    if (hi) __builtin_amdgcn_s_setprio(3);
     const CopyEnt e = ents[blockIdx.y];
     for (int64_t o = 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); o < e.len;
          o += 16 * (int64_t)gridDim.x * blockDim.x)
         copy_piece(e.src, e.dst, e.len, o);
 }
 
-hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hipStream_t s) {
+hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hipStream_t s, bool bg) {
     if (n == 0 || max_len <= 0) return hipSuccess;
-    const int64_t blocks = std::min<int64_t>((max_len + 16 * 256 - 1) / (16 * 256), 64);
-    hipLaunchKernelGGL(copy_many_kernel, dim3((uint32_t)blocks, n), dim3(256), 0, s, ents);
+    const int64_t blocks = bg ? 1 : std::min<int64_t>((max_len + 16 * 256 - 1) / (16 * 256), 64);
+    hipLaunchKernelGGL(copy_many_kernel, dim3((uint32_t)blocks, n), dim3(256), 0, s, ents, bg ? 0 : 1);
     return hipGetLastError();
 }
 
@@ -2348,8 +2400,8 @@ hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s) {
     return hipGetLastError();
 }
 
-__global__ void table_insert_many_kernel(const TableEnt* __restrict__ ents) {
-    __builtin_amdgcn_s_setprio(3);
+__global__ void table_insert_many_kernel(const TableEnt* __restrict__ ents, int hi) {
+    if (hi) __builtin_amdgcn_s_setprio(3);
     const TableEnt e = ents[blockIdx.y];
     for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < e.nkeys; i += gridDim.x * blockDim.x) {
         const uint32_t key = (uint32_t)e.keys[i];
@@ -2363,10 +2415,10 @@ __global__ void table_insert_many_kernel(const TableEnt* __restrict__ ents) {
     }
 }
 
-hipError_t launch_table_insert_many(const TableEnt* ents, uint32_t n, int32_t max_keys, hipStream_t s) {
+hipError_t launch_table_insert_many(const TableEnt* ents, uint32_t n, int32_t max_keys, hipStream_t s, bool bg) {
     if (n == 0 || max_keys <= 0) return hipSuccess;
-    const uint32_t blocks = (uint32_t)std::min<int64_t>((max_keys + 255) / 256, 256);
-    hipLaunchKernelGGL(table_insert_many_kernel, dim3(blocks, n), dim3(256), 0, s, ents);
+    const uint32_t blocks = (uint32_t)std::min<int64_t>((max_keys + 255) / 256, bg ? std::max<uint32_t>(1, kBackgroundGroups / n) : 256);
+    hipLaunchKernelGGL(table_insert_many_kernel, dim3(blocks, n), dim3(256), 0, s, ents, bg ? 0 : 1);
     return hipGetLastError();
 }
 
