@@ -740,6 +740,22 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // phase-shifted speculation there instead of once the resolver has walked the prefix.  A wrong guess is
     // stopped when the resolver hints another phase.  RSH_SCAN_PHASE_GUESS=0 (A/B) turns it off.
     int64_t guess = -1;
+    // The prefix end (below) needs the weak sums of the aligned windows between the run's last matching sample
+    // and the first that does not: launched now, ahead of the guess's first probe, so that they land in its
+    // round trip instead of one of their own
+    const int64_t pe_lo = run_last + 1, pe_hi = std::min<int64_t>(run_miss, nf - 1), pe_cnt = pe_hi - pe_lo + 1;
+    int32_t* pe_w = nullptr;
+    if (defer_prefix && guess_on && seg_on && run_miss > 0 && pe_cnt > 0 && pe_cnt <= 4096 && be.err == hipSuccess) {
+        const size_t ents_at = ((size_t)pe_cnt * 4 + 63) & ~(size_t)63;
+        RSH_HIP(c->h_pend.ensure(ents_at + (size_t)pe_cnt * sizeof(rsh::GatherEnt)));
+        pe_w = c->h_pend.as<int32_t>();
+        auto* pents = reinterpret_cast<rsh::GatherEnt*>(c->h_pend.as<uint8_t>() + ents_at);
+        for (int64_t i = 0; i < pe_cnt; ++i) pents[i] = rsh::GatherEnt{(pe_lo + i) * B, 0, 0};
+        auto* lf = reinterpret_cast<rsh::ScanFile*>(reinterpret_cast<rsh::GatherEnt*>(c->h_lead.as<uint8_t>() + lead_ents_at) +
+                                                    nsamp + 1);
+        RSH_HIP(rsh::launch_window_weak(lf, pents, (uint32_t)pe_cnt, pe_w, c->stream));
+        be.bytes_read += pe_cnt * B;
+    }
     if (guess_on && run_miss > 0 && (spec_launched || defer_prefix) && HipBackend::phase_on() && C >= 4) {
         CallTrace tr("phase_guess", run_miss);
         int64_t a = run_miss * B;
@@ -779,10 +795,15 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         if (cnt > 0 && cnt <= 4096 && B % 128 == 0 && (B >> 7) >= 4 && (B >> 7) <= 1024 &&
             hipMemGetAddressRange(&lo, &asize, reinterpret_cast<hipDeviceptr_t>(const_cast<uint8_t*>(d_src))) ==
                 hipSuccess) {
-            std::vector<int64_t> pos((size_t)cnt);
             std::vector<int32_t> w((size_t)cnt);
-            for (int64_t i = 0; i < cnt; ++i) pos[(size_t)i] = (k_lo + i) * B;
-            be.weak_many(pos.data(), cnt, w.data());
+            if (pe_w && k_lo == pe_lo && cnt == pe_cnt) {  // launched with the guess (above); landed with its probes
+                RSH_HIP(hipStreamSynchronize(c->stream));
+                memcpy(w.data(), pe_w, (size_t)cnt * 4);
+            } else {
+                std::vector<int64_t> pos((size_t)cnt);
+                for (int64_t i = 0; i < cnt; ++i) pos[(size_t)i] = (k_lo + i) * B;
+                be.weak_many(pos.data(), cnt, w.data());
+            }
             int64_t P = run_miss;  // aligned windows [0, P): up to the first one whose weak sum is not its chunk's
             for (int64_t i = 0; i < cnt; ++i)
                 if (w[(size_t)i] != host_weak[k_lo + i]) {

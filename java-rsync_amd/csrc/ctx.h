@@ -122,6 +122,7 @@ struct rsh_ctx {
     PinnedBuf h_pos, h_out, h_iv, h_tiles, h_keys, h_first, h_win, h_ptiles;
     PinnedBuf h_hit;  // after a probe hit: T(p) (bytes 0..3) and the window at p (from byte 16)
     PinnedBuf h_win0;    // window 0 of the current scan (its digest is computed on a host thread)
+    PinnedBuf h_pend;    // the prefix end's window sums (launched with the phase guess's first probe)
     PinnedBuf h_bucket;  // after a probe hit: {count, key, chunk indices} of the key that hit
     PinnedBuf h_files;   // the scan's rsh::ScanFile (a batch of one for the probe / gather kernels)
     PinnedBuf h_stage;   // file ingest ring (ingest.cpp); never shared with the scan's buffers
@@ -140,7 +141,7 @@ struct rsh_ctx {
                           &dkeys, &pos, &out, &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pw, &h_ps, &h_lead, &h_pos, &h_out, &h_iv,
-                             &h_tiles, &h_keys, &h_first, &h_win, &h_ptiles, &h_hit, &h_win0, &h_bucket, &h_files,
+                             &h_tiles, &h_keys, &h_first, &h_win, &h_ptiles, &h_hit, &h_win0, &h_pend, &h_bucket, &h_files,
                              &h_stage})
             b->release();
         if (abort_word) (void)hipFree(abort_word);
