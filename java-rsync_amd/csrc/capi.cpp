@@ -340,7 +340,10 @@ class HipBackend : public rsh::ScanBackend {
                 const uint8_t* src = hh + 16 + (int64_t)k * B_;
                 win_md5_[k] = std::thread([this, k, wk, src] {
                     rsh::HostMd5 h;
-                    h.update(src, (size_t)wk);
+                    for (int64_t o = 0; o < wk; o += kDigestPiece) {  // stops early once nobody can ask for it
+                        if (win_cancel_.load(std::memory_order_relaxed)) return;
+                        h.update(src + o, (size_t)std::min<int64_t>(kDigestPiece, wk - o));
+                    }
                     h.update(seed_, 4);
                     h.final(win_digest_[k]);
                 });
@@ -474,13 +477,20 @@ class HipBackend : public rsh::ScanBackend {
     // (the resolver handles the first hit meanwhile); joined before the next probe overwrites h_hit
     std::thread win_md5_[rsh::HIT_WINDOWS];
     uint8_t win_digest_[rsh::HIT_WINDOWS][16];
+    // set when the scan ends: a window digest still running then is never read (the join at the end of the
+    // scan took ~0.09 ms for one 128 KiB window digested after the scan's last probe)
+    std::atomic<bool> win_cancel_{false};
+    static constexpr int64_t kDigestPiece = 8192;
     void join_window_digests() {
         for (std::thread& t : win_md5_)
             if (t.joinable()) t.join();
     }
 
   public:
-    ~HipBackend() { join_window_digests(); }
+    ~HipBackend() {
+        win_cancel_.store(true, std::memory_order_relaxed);
+        join_window_digests();
+    }
 
   private:
     int64_t t_pos_ = -1;    // position of the last hit returned: its weak sum t_val_ is known
@@ -950,6 +960,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                 RSH_HIP(hipMemcpyAsync(c->haw.p, c->src_weak.p, (size_t)spec_na * 4, hipMemcpyDeviceToDevice, c->stream));
                 std::fill(be.haw_ready.begin(), be.haw_ready.begin() + spec_na, (uint8_t)1);
             }
+            CallTrace tr("resolve_end", res->stats.events);
             rsh::resolve_run(n, table, be, &rs, res, nullptr);
         }
     }
@@ -963,6 +974,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     }
     res->stats.phase_launches += be.ph_launches;
     res->stats.phase_kernel_ms += be.phase_ms;
+    if (CallTrace::on()) fprintf(stderr, "[rsh] scan_body  %10lld %9.3f ms\n", (long long)n, ms_since(t0));
     return RSH_OK;
 }
 
@@ -1222,6 +1234,7 @@ int rsh_match_scan_device(rsh_ctx* ctx, const void* d_src, int64_t n, const rsh_
         skip_events(n, &r);
     } else if (n > 0) {
         if (!d_src || (h->chunk_count > 0 && (!d_weak || (!d_strong && h->digest_length > 0)))) return RSH_E_INVAL;
+        CallTrace tr("scan_call", n);  // with scan_device's teardown
         const int rc = scan_device(ctx, static_cast<const uint8_t*>(d_src), n, h, static_cast<const int32_t*>(d_weak),
                                    static_cast<const uint8_t*>(d_strong), nullptr, nullptr, seed, &r);
         if (rc != RSH_OK) return rc;
