@@ -40,8 +40,8 @@ KEY_EDIT = (0x5EED5EED << 32) | 0xED17
 KEY_CASE = KEY_SRC ^ 5
 KEY_INS = KEY_SRC ^ 0x1B
 SHIFT_AT = 155 * 131072 + 4096  # the "config5_shift1" insert position
-TRAFFIC_CSV = "r2_v11_bench_fetch_size.csv"
-TRAFFIC_FILES_CSV = "r2_v11_files_fetch_size.csv"
+TRAFFIC_CSV = "r2_v16_bench_fetch_size.csv"
+TRAFFIC_FILES_CSV = "r2_v16_files_fetch_size.csv"
 
 
 def parse():

@@ -31,7 +31,7 @@ constexpr int64_t kDeferSteps = 4;
 constexpr double kDeferMs = 0.5;
 // ... or at once when the first kLeadWindows (ctx.h) aligned source windows all carry chunk k's weak sum
 // ... over the windows up to the last of kSampleWindows evenly spaced samples that still carries its chunk's sum
-constexpr int64_t kSampleWindows = 1024;
+constexpr int64_t kSampleWindows = 256;  // (1024 until round 2: the same step time, r2_ab2; RSH_SCAN_SAMPLES A/B)
 // windows one K1 launch digests in a single round of waves (2 waves/SIMD x 1024 SIMDs x 64 lanes): below this a
 // launch over fewer windows is no faster
 constexpr int64_t kRoundWindows = 131072;
@@ -546,7 +546,9 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     RSH_HIP(c->h_ps.ensure((size_t)na * dl + 1));
     // sample windows for the launch decision: the first nlead, then one every `stride` windows
     const int64_t nlead = std::min<int64_t>(kLeadWindows, nf);
-    const int64_t stride = std::max<int64_t>(1, (nf + kSampleWindows - 1) / kSampleWindows);
+    static const int64_t nsamples = getenv("RSH_SCAN_SAMPLES") ? std::max(1, atoi(getenv("RSH_SCAN_SAMPLES")))
+                                                              : kSampleWindows;  // A/B
+    const int64_t stride = std::max<int64_t>(1, (nf + nsamples - 1) / nsamples);
     std::vector<int64_t> samp;
     for (int64_t k = 0; k < nlead; ++k) samp.push_back(k);
     for (int64_t k = stride; k < nf; k += stride)
@@ -582,7 +584,8 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         RSH_HIP(hipEventRecord(c->ev_k1b, c->aux));
         RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
                                         (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(), c->aux));
-        // the flags first (a run of matches needs nothing else), then the sums (aligned lookups off the run)
+        // the flags first (a run of matches needs nothing else), then the sums (aligned lookups off the run).
+        // (Written by the flags kernel straight into pinned host memory instead: no difference, r2_ab2.)
         if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, c->aux));
         RSH_HIP(hipEventRecord(c->ev_flags, c->aux));
         RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)spec_na * 4, hipMemcpyDeviceToHost, c->aux));
