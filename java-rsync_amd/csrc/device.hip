@@ -478,6 +478,21 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
 
+// MD5F == 9 (kbench A/B): the K constants in VGPRs, a + m + K as one v_add3_u32 (gfx950 VOP3 has no literal)
+__device__ __forceinline__ void md5_k3_init(uint32_t (&kv)[64]) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(__gfx950__)
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        kv[i] = RSH_MD5_KTAB[i];
+        asm volatile("" : "+v"(kv[i]));
+    }
+#endif
+}
+__device__ __forceinline__ void md5_k3_block(Md5State& st, const uint32_t (&m)[16], const uint32_t (&kv)[64]) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(__gfx950__)
+    md5_compress_k3_8(st, m, kv);
+#endif
+}
 template <int MD5F>
 __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&m)[16]) {
     if constexpr (MD5F == 8) md5_compress_rot16n(st, m);
@@ -501,7 +516,7 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 #define K1_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
 #endif
 template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false>
-__global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
+__device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
                                                              uint8_t* __restrict__ strong_out,
                                                              const int* abort_flag = nullptr, int abort_gen = 0,
@@ -599,10 +614,14 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
             for (int g = 0; g < 4; ++g) Bv[4 * h + g] = lds_all[buf * BUF + 16 * ROW * g + rdB + 4 * h];
     };
     Md5State st = md5_init();
+    // MD5F == 9 (kbench A/B): a + m + K as one v_add3_u32 per step, the 64 K constants held in VGPRs
+    [[maybe_unused]] uint32_t kv[64];
+    if constexpr (MD5F == 9) md5_k3_init(kv);
     auto md5_block = [&](const uint4 (&w)[4]) __attribute__((always_inline)) {
         uint32_t m[16];
         unpack(w, m);
-        md5_stream_block<MD5F>(st, m);
+        if constexpr (MD5F == 9) md5_k3_block(st, m, kv);
+        else md5_stream_block<MD5F>(st, m);
     };
     auto weak_mfma = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -698,6 +717,25 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
     const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
     weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
     store_digest(strong_out + (size_t)c * dl, st, dl);
+}
+
+template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false>
+__global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
+                                                             uint32_t seed, int32_t* __restrict__ weak_out,
+                                                             uint8_t* __restrict__ strong_out,
+                                                             const int* abort_flag = nullptr, int abort_gen = 0,
+                                                             const K1Group* __restrict__ groups = nullptr,
+                                                             int64_t n = 0, uint32_t nchunks = 0,
+                                                             uint32_t main_waves = 0xFFFFFFFFu) {
+    block_sums_pipe_body<MD5F, ABORT, PIN, MODE, MULTI>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
+                                                        groups, n, nchunks, main_waves);
+}
+// kbench A/B (variant 61): MD5F == 9 holds the 64 K constants in VGPRs (176 + 64 registers, still 2 waves/SIMD)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void block_sums_pipe_k3_kernel(
+    const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
+    uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen) {
+    block_sums_pipe_body<9, true, true, 0, false>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
+                                                  nullptr, 0, 0, 0xFFFFFFFFu);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1218,6 +1256,7 @@ static bool pin_all() {
 }
 static bool batch_pin() { return pin_all(); }
 
+static const int* never_word();
 hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks,
                                      uint32_t dl, uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong,
                                      hipStream_t s, const int* abort_flag, int abort_gen) {
@@ -1484,6 +1523,10 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                 case 54:
                     hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, false, 0>), dim3(waves), dim3(64), 2 * wave_lds, s,
                                        d_data, B, dl, seed_word, d_weak, d_strong);
+                    break;
+                case 61:  // A/B: MD5 steps with a + m + K as one v_add3_u32 (K in VGPRs), abortable form
+                    hipLaunchKernelGGL(block_sums_pipe_k3_kernel, dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
                     break;
                 case 56:  // A/B: the plain kernel with s_sleep 1 / s_sleep 4 per 2 stages
                     hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 6>), dim3(waves), dim3(64), 2 * wave_lds, s,
