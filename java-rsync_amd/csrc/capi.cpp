@@ -849,6 +849,10 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                 for (int64_t k = wq * 64; k < Q; ++k)
                     tl[ntail++] = rsh::K1Tail{d_src + s0, n - s0, c->ph_weak.as<int32_t>(), c->ph_strong.as<uint8_t>(),
                                               (uint32_t)k};
+                // full-length tails first (gathered into coalesced waves), the short last window after them
+                const uint32_t nfull = (uint32_t)(std::stable_partition(tl, tl + ntail, [&](const rsh::K1Tail& t) {
+                                                      return (int64_t)(t.c + 1) * B <= t.n;
+                                                  }) - tl);
                 const size_t bytes = nseg * sizeof(rsh::K1Seg) + ntail * sizeof(rsh::K1Tail);
                 if (ntail <= 256 && bytes <= seg_bytes) {
                     spec_na = P;
@@ -860,7 +864,8 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                     RSH_HIP(rsh::launch_block_sums_segments(c->segs.as<rsh::K1Seg>(), nseg,
                                                             reinterpret_cast<const rsh::K1Tail*>(
                                                                 c->segs.as<uint8_t>() + nseg * sizeof(rsh::K1Seg)),
-                                                            ntail, (uint32_t)B, (uint32_t)dl, seed_word(seed), c->aux));
+                                                            ntail, nfull, (uint32_t)B, (uint32_t)dl, seed_word(seed),
+                                                            c->aux));
                     RSH_HIP(hipEventRecord(c->ev_k1b, c->aux));
                     RSH_HIP(hipEventRecord(c->ev_phb, c->aux));
                     RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak,

@@ -67,8 +67,10 @@ struct K1Tail {
     uint8_t* strong;
     uint32_t c;
 };
+// d_tails[0, nfull): full-length chunks (gathered 64 to a coalesced wave when that adds no wave); the rest
+// (short chunks) one per lane
 hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const K1Tail* d_tails, uint32_t ntail,
-                                      uint32_t B, uint32_t dl, uint32_t seed_word, hipStream_t s);
+                                      uint32_t nfull, uint32_t B, uint32_t dl, uint32_t seed_word, hipStream_t s);
 void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Group>* groups,
                            std::vector<K1Lane>* lanes, int* lane_align);
 // Device-side group expansion: the host plans per file (K1Plan: the file's first group index g0 and its

@@ -89,6 +89,7 @@ __device__ __forceinline__ void unpack(const uint4 (&q)[4], uint32_t (&m)[16]) {
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+static const int* never_word();
 
 template <bool NT>
 __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
@@ -515,18 +516,23 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 #else
 #define K1_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
 #endif
-template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false>
+// GATHER (the segmented launch's leftover chunks): the wave's 64 chunks are full-length chunks at any base and
+// in any file (gt[0..gcnt), K1Tail), loaded with plain dwordx4 loads (16-B aligned or not) from one 64-bit
+// pointer per 8-chunk row instead of a buffer descriptor; lane l writes chunk gt[l]'s sums (l < gcnt).
+template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false, bool GATHER = false>
 __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
                                                              uint8_t* __restrict__ strong_out,
                                                              const int* abort_flag = nullptr, int abort_gen = 0,
                                                              const K1Group* __restrict__ groups = nullptr,
                                                              int64_t n = 0, uint32_t nchunks = 0,
-                                                             uint32_t main_waves = 0xFFFFFFFFu) {
+                                                             uint32_t main_waves = 0xFFFFFFFFu,
+                                                             const K1Tail* __restrict__ gt = nullptr,
+                                                             uint32_t gcnt = 0) {
     constexpr int ROW = 9;
     constexpr int BUF = 64 * ROW;  // uint4 slots per LDS buffer
     constexpr int TAIL_PF = RSH_K1_TAIL_PF;
-    if constexpr (!MULTI) {
+    if constexpr (!MULTI && !GATHER) {
         // tail waves (blockIdx >= main_waves): one lane per chunk left over (a partial last wave, the short last
         // chunk), dispatched with the main waves rather than as a launch queued behind them (a lone wave takes
         // as long as one lane's window: 1.9 ms at B = 128 KiB).  Plain dwordx4 loads at the lane's own address,
@@ -555,6 +561,16 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         if constexpr (ABORT) {
             if (g.abort) abort_flag = g.abort;  // per-file cancellation (batched Sender speculation)
         }
+    }
+    [[maybe_unused]] const uint8_t* rp[8];  // GATHER: row j's lane address (chunk (l >> 3) + 8 j, piece l & 7)
+    if constexpr (GATHER) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t ci = (uint32_t)(l >> 3) + 8u * (uint32_t)j;
+            const K1Tail t = gt[ci < gcnt ? ci : 0u];  // lanes past gcnt digest chunk 0 again (not stored)
+            rp[j] = t.data + (size_t)t.c * B + 16u * (uint32_t)(l & 7);
+        }
+        c0 = 0;
     }
     const uint32_t nst = B >> 7;  // host guarantees nst >= 4
     const int wr0 = (l >> 3) * ROW + (l & 7);
@@ -593,6 +609,8 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         for (int j = 0; j < 8; ++j) {
             if constexpr (MODE == 1) {
                 dst[j] = make_uint4(l + stg, j, c0, 7);
+            } else if constexpr (GATHER) {
+                dst[j] = ld16<false>(rp[j] + 128u * stg);
             } else {
                 const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_off + 128u * stg, (int)(j * 8u * B), 2);
                 dst[j] = make_uint4(t.x, t.y, t.z, t.w);
@@ -713,7 +731,14 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         s1 = gs == 0 ? t1[0] : gs == 1 ? t1[1] : gs == 2 ? t1[2] : t1[3];
         u = gs == 0 ? tu[0] : gs == 1 ? tu[1] : gs == 2 ? tu[2] : tu[3];
     }
-    const uint32_t c = c0 + l;
+    uint32_t c = c0 + l;
+    if constexpr (GATHER) {
+        if ((uint32_t)l >= gcnt) return;
+        const K1Tail t = gt[l];
+        weak_out = t.weak;
+        strong_out = t.strong;
+        c = t.c;
+    }
     const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
     weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
     store_digest(strong_out + (size_t)c * dl, st, dl);
@@ -1114,13 +1139,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGP
 // speculation at phase 0 and its phase-shifted speculation after an edit: separate launches would need one
 // wave more than the chip's 2048 wave slots, and the last wave would start only when another finished).
 // Waves [0, nseg) take a K1Seg each (64 full chunks; the dword offset W of its base chosen per wave);
-// waves past them take one chunk per lane from the K1Tail list (the segments' leftover chunks, any shape).
+// waves past them take the K1Tail list (the segments' leftover chunks): its first `ngf` entries (full-length
+// chunks at any base) 64 to a gathered coalesced wave (block_sums_pipe_body<.., GATHER>), the rest one chunk
+// per lane.  A per-lane wave runs ~20% slower than a coalesced one (its loads and v_dot4 weak sums), and as
+// the launch's last wave it set the launch's end: kbench, 2047 segment waves + one per-lane wave of 64
+// chunks 3.70-3.75 ms against 3.33 ms without it.
 template <int TAIL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGPR))) void block_sums_seg_kernel(
     const K1Seg* __restrict__ segs, uint32_t nseg, const K1Tail* __restrict__ tails, uint32_t ntail, uint32_t B,
-    uint32_t dl, uint32_t seed) {
+    uint32_t dl, uint32_t seed, uint32_t ngf, const int* never) {
     if (blockIdx.x >= nseg) {
-        const uint32_t i = (blockIdx.x - nseg) * 64u + threadIdx.x;
+        const uint32_t tw = blockIdx.x - nseg, ngw = (ngf + 63u) / 64u;
+        if (tw < ngw) {
+            block_sums_pipe_body<8, true, true, 0, false, true>(nullptr, B, dl, seed, nullptr, nullptr, never, -1,
+                                                               nullptr, 0, 0, 0xFFFFFFFFu, tails + 64u * tw,
+                                                               min(64u, ngf - 64u * tw));
+            return;
+        }
+        const uint32_t i = ngf + (tw - ngw) * 64u + threadIdx.x;
         if (i < ntail) {
             const K1Tail t = tails[i];
             if constexpr (TAIL == 0) lane_chunk_sums<2, 4, false>(t.data, t.n, B, t.c, dl, seed, t.weak, t.strong);
@@ -1139,24 +1175,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGP
 }
 
 hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const K1Tail* d_tails, uint32_t ntail,
-                                      uint32_t B, uint32_t dl, uint32_t seed_word, hipStream_t s) {
+                                      uint32_t nfull, uint32_t B, uint32_t dl, uint32_t seed_word, hipStream_t s) {
     if (nseg + ntail == 0) return hipSuccess;
-    const uint32_t waves = nseg + (ntail + 63) / 64;
+    // gathered waves for the full-length tails when that adds no wave (the launch fills the chip's 2048 wave
+    // slots exactly in the bench's shift case: one more wave would start only when another finished).
+    // RSH_K1_GATHER=0 (A/B, read per launch): every tail per lane.
+    const char* gm = getenv("RSH_K1_GATHER");
+    const bool gather_on = !gm || atoi(gm) != 0;
+    const int* never = never_word();
+    uint32_t ngf = 0;
+    if (gather_on && never && nfull > 0 && nfull <= ntail && (B % 128) == 0 && (B >> 7) >= 8 &&
+        (nfull + 63) / 64 + (ntail - nfull + 63) / 64 == (ntail + 63) / 64)
+        ngf = nfull;
+    const uint32_t waves = nseg + (ngf + 63) / 64 + (ntail - ngf + 63) / 64;
     // tail lanes (A/B, read per launch: RSH_K1_TAIL=1 (default) dword loads + funnel, 0 wide aligned loads + a
     // per-lane select, 2 plain unaligned dwordx4).  kbench, 2047 coalesced waves + one tail wave of 64 chunks
     // at offset 1: 3.70-3.75 / 4.13-4.19 / 4.19-4.28 ms (3.33 ms without the tail wave)
     const char* tm = getenv("RSH_K1_TAIL");
     const int mode = tm ? atoi(tm) : 1;
-    const size_t lb = 64 * 17 * sizeof(uint4);
+    // LDS: the shift wave's ring (64 rows of 17 slots); a gathered wave's two 9-slot buffers when there is one
+    const size_t lb = ngf > 0 ? 2 * 64 * 9 * sizeof(uint4) : 64 * 17 * sizeof(uint4);
     if (mode == 1)
         hipLaunchKernelGGL(block_sums_seg_kernel<1>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
-                           seed_word);
+                           seed_word, ngf, never);
     else if (mode == 2)
         hipLaunchKernelGGL(block_sums_seg_kernel<2>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
-                           seed_word);
+                           seed_word, ngf, never);
     else
         hipLaunchKernelGGL(block_sums_seg_kernel<0>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
-                           seed_word);
+                           seed_word, ngf, never);
     return hipGetLastError();
 }
 
@@ -1256,7 +1303,6 @@ static bool pin_all() {
 }
 static bool batch_pin() { return pin_all(); }
 
-static const int* never_word();
 hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks,
                                      uint32_t dl, uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong,
                                      hipStream_t s, const int* abort_flag, int abort_gen) {

@@ -12,6 +12,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "device.h"
@@ -85,7 +86,8 @@ int main(int argc, char** argv) {
     // variant 1003: the segmented launch (block_sums_seg_kernel) over the whole buffer as one segment; the
     // buffer's base must be such that base - base % 128 is inside the allocation (KBENCH_OFFSET < 128)
     const uint32_t a_off = (uint32_t)(reinterpret_cast<uintptr_t>(d) % 128);
-    const uint32_t nfull = (uint32_t)(n / B), nw = nfull / 64;
+    // KBENCH_SEGTAIL=1: the last full wave's 64 chunks go to the tail list instead (the shift case's tail wave)
+    const uint32_t nfull = (uint32_t)(n / B), nw = nfull / 64 - ((getenv("KBENCH_SEGTAIL") && nfull >= 64) ? 1 : 0);
     std::vector<rsh::K1Seg> segs;
     std::vector<rsh::K1Tail> tails;
     int* never;
@@ -101,8 +103,12 @@ int main(int argc, char** argv) {
     if (!tails.empty()) CK(hipMemcpy(d_tails, tails.data(), tails.size() * sizeof(rsh::K1Tail), hipMemcpyHostToDevice));
     auto launch = [&](int v) {
         if (v == 1003)
-            return rsh::launch_block_sums_segments(d_segs, (uint32_t)segs.size(), d_tails, (uint32_t)tails.size(), B, dl,
-                                                   0x04030201u, s);
+            return rsh::launch_block_sums_segments(d_segs, (uint32_t)segs.size(), d_tails, (uint32_t)tails.size(),
+                                                   (uint32_t)std::count_if(tails.begin(), tails.end(),
+                                                                           [&](const rsh::K1Tail& t) {
+                                                                               return (int64_t)(t.c + 1) * B <= t.n;
+                                                                           }),
+                                                   B, dl, 0x04030201u, s);
         if (v == 1002)
             return rsh::launch_block_sums_batch(d_groups, (uint32_t)groups.size(), d_lanes, (uint32_t)lanes.size(),
                                                 lane_align, 0x04030201u, s);

@@ -215,7 +215,7 @@ def test_sender_phase_shift_chains(ctx):
     assert st["phase_launches"] >= 1 and st["phase_matches"] > 6000 and st["host_md5_windows"] < 100, st
 
 
-@pytest.mark.parametrize("segmented", ["1", "0"])
+@pytest.mark.parametrize("segmented", ["1", "1-lane", "0"])
 @pytest.mark.parametrize("edit", ["insert1", "delete3", "two_inserts", "insert_far"])
 def test_sender_phase_guess(ctx, edit, segmented, monkeypatch):
     """A source that follows the basis up to an edit and continues at another phase after it (4096 windows at
@@ -223,9 +223,12 @@ def test_sender_phase_guess(ctx, edit, segmented, monkeypatch):
     the backend finds the phase past the run (a range probe plus four consecutive chunk sums) and starts the
     phase-shifted speculation there.  two_inserts: a second insert two windows after the first, so the guess
     (past both) is not the phase the resolver meets first.  insert_far: the edit is past every sample but the
-    last.  segmented=1: the prefix and the guessed phase go out as one segmented K1 launch (per-wave bases,
-    shared per-lane tail waves); 0: two launches.  Events equal the oracle's in every case."""
-    monkeypatch.setenv("RSH_SCAN_SEGMENTED", segmented)
+    last.  segmented=1: the prefix and the guessed phase go out as one segmented K1 launch (per-wave bases; the
+    two segments' leftover chunks -- 44 + 20 full ones for insert1, 44 + 19 for delete3 -- in one gathered
+    coalesced wave); 1-lane: the same launch with the leftovers one per lane (RSH_K1_GATHER=0); 0: two
+    launches.  Events equal the oracle's in every case."""
+    monkeypatch.setenv("RSH_SCAN_SEGMENTED", segmented[0])
+    monkeypatch.setenv("RSH_K1_GATHER", "0" if segmented == "1-lane" else "1")
     B, dl = 65536, 4
     basis = O.splitmix(256 << 20, 0x5EED5EED000000C3)
     x = 300 * B + 777
