@@ -516,9 +516,11 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 #else
 #define K1_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(3)))
 #endif
-// GATHER (the segmented launch's leftover chunks): the wave's 64 chunks are full-length chunks at any base and
-// in any file (gt[0..gcnt), K1Tail), loaded with plain dwordx4 loads (16-B aligned or not) from one 64-bit
-// pointer per 8-chunk row instead of a buffer descriptor; lane l writes chunk gt[l]'s sums (l < gcnt).
+// GATHER (leftover chunks of a launch): the wave's gcnt <= 64 chunks are full-length chunks at any base,
+// loaded with plain dwordx4 loads (16-B aligned or not) from one 64-bit pointer per 8-chunk row instead of a
+// buffer descriptor.  gt != nullptr: chunk i is gt[i] (K1Tail: any file; the segmented launch); else chunk i
+// is data + i B with outputs weak_out[i], strong_out[i dl] (a single launch's partial last wave).  Lanes past
+// gcnt digest chunk 0 again and store nothing.
 template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false, bool GATHER = false>
 __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
@@ -567,8 +569,13 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const uint32_t ci = (uint32_t)(l >> 3) + 8u * (uint32_t)j;
-            const K1Tail t = gt[ci < gcnt ? ci : 0u];  // lanes past gcnt digest chunk 0 again (not stored)
-            rp[j] = t.data + (size_t)t.c * B + 16u * (uint32_t)(l & 7);
+            const uint32_t cs = ci < gcnt ? ci : 0u;
+            if (gt) {
+                const K1Tail t = gt[cs];
+                rp[j] = t.data + (size_t)t.c * B + 16u * (uint32_t)(l & 7);
+            } else {
+                rp[j] = data + (size_t)cs * B + 16u * (uint32_t)(l & 7);
+            }
         }
         c0 = 0;
     }
@@ -734,10 +741,12 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     uint32_t c = c0 + l;
     if constexpr (GATHER) {
         if ((uint32_t)l >= gcnt) return;
-        const K1Tail t = gt[l];
-        weak_out = t.weak;
-        strong_out = t.strong;
-        c = t.c;
+        if (gt) {
+            const K1Tail t = gt[l];
+            weak_out = t.weak;
+            strong_out = t.strong;
+            c = t.c;
+        }
     }
     const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
     weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
@@ -754,6 +763,36 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
                                                              uint32_t main_waves = 0xFFFFFFFFu) {
     block_sums_pipe_body<MD5F, ABORT, PIN, MODE, MULTI>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
                                                         groups, n, nchunks, main_waves);
+}
+// The production K1 with the partial last wave's full-length chunks as a gathered coalesced wave (the tail
+// waves past main_waves: ceil(tail_full / 64) gathered ones, then the short last chunk, if any, per lane).  A
+// per-lane wave runs ~20% slower than a coalesced one and, when every wave runs in the first round, sets the
+// launch's end.  Used only for launches with such a tail: the exact-multiple launches keep
+// block_sums_pipe_kernel.  Its register budget is 256 (2 waves/SIMD): under K1_PIPE_ATTR the two bodies spill.
+template <bool ABORT>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void block_sums_pipe_tailg_kernel(
+    const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
+    uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen, int64_t n, uint32_t nchunks,
+    uint32_t main_waves, uint32_t tail_full) {
+    if (blockIdx.x >= main_waves) {
+        const uint32_t tw = blockIdx.x - main_waves, ngw = (tail_full + 63u) / 64u;
+        if (tw < ngw) {
+            const uint32_t first = main_waves * 64u + 64u * tw;
+            block_sums_pipe_body<8, ABORT, true, 0, false, true>(
+                data + (size_t)first * B, B, dl, seed, weak_out + first, strong_out + (size_t)first * dl, abort_flag,
+                abort_gen, nullptr, 0, 0, 0xFFFFFFFFu, nullptr, min(64u, tail_full - 64u * tw));
+            return;
+        }
+        const uint32_t c = main_waves * 64u + tail_full + (tw - ngw) * 64u + threadIdx.x;
+        if (c < nchunks) lane_chunk_sums<16, RSH_K1_TAIL_PF, false>(data, n, B, c, dl, seed, weak_out, strong_out);
+        return;
+    }
+    block_sums_pipe_body<8, ABORT, true, 0, false>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
+                                                   nullptr, n, nchunks, main_waves);
+}
+static bool tail_gather_on() {  // RSH_K1_GATHER=0 (A/B, read per launch): leftover chunks one per lane
+    const char* gm = getenv("RSH_K1_GATHER");
+    return !gm || atoi(gm) != 0;
 }
 // kbench A/B (variant 61): MD5F == 9 holds the 64 K constants in VGPRs (176 + 64 registers, still 2 waves/SIMD)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void block_sums_pipe_k3_kernel(
@@ -1180,11 +1219,10 @@ hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const 
     // gathered waves for the full-length tails when that adds no wave (the launch fills the chip's 2048 wave
     // slots exactly in the bench's shift case: one more wave would start only when another finished).
     // RSH_K1_GATHER=0 (A/B, read per launch): every tail per lane.
-    const char* gm = getenv("RSH_K1_GATHER");
-    const bool gather_on = !gm || atoi(gm) != 0;
+    const bool gather_on = tail_gather_on();
     const int* never = never_word();
     uint32_t ngf = 0;
-    if (gather_on && never && nfull > 0 && nfull <= ntail && (B % 128) == 0 && (B >> 7) >= 8 &&
+    if (gather_on && never && nfull > 0 && nfull <= ntail && (B % 128) == 0 && (B >> 7) >= 4 &&
         (nfull + 63) / 64 + (ntail - nfull + 63) / 64 == (ntail + 63) / 64)
         ngf = nfull;
     const uint32_t waves = nseg + (ngf + 63) / 64 + (ntail - ngf + 63) / 64;
@@ -1442,6 +1480,17 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     // unpinned instantiation, and ahead of the coalesced kernel at every size
                     if (nst <= 1024 && nst >= 4 && abort_flag && (waves <= 2 * 4 * kCUs || pin_all())) {
                         const uint32_t tail_waves = (nchunks - 64 * waves + 63) / 64;  // in the same launch
+                        // the partial last wave's full chunks gathered into a coalesced wave when that adds no
+                        // wave or every wave still fits the chip's slots (2 per SIMD)
+                        const uint32_t tail_full = nfullc - 64 * waves, tail_short = nchunks - nfullc;
+                        const uint32_t gwaves = (tail_full + 63) / 64 + (tail_short + 63) / 64;
+                        if (tail_full > 0 && tail_gather_on() &&
+                            (gwaves == tail_waves || waves + gwaves <= 2 * 4 * kCUs)) {
+                            hipLaunchKernelGGL((block_sums_pipe_tailg_kernel<true>), dim3(waves + gwaves), dim3(64),
+                                               2 * wave_lds, s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag,
+                                               abort_gen, n, nchunks, waves, tail_full);
+                            return hipGetLastError();
+                        }
                         hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true>), dim3(waves + tail_waves), dim3(64),
                                            2 * wave_lds, s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag,
                                            abort_gen, nullptr, n, nchunks, waves);

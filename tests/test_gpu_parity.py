@@ -203,6 +203,32 @@ def test_k1_shift_allocation_edge(ctx, nfull):
         assert np.array_equal(d_s.download(), os_), f"strong, offset {off}"
 
 
+@pytest.mark.parametrize("gather", ["1", "0"])
+def test_k1_partial_last_wave(ctx, gather, monkeypatch):
+    """A K1 launch whose last wave is partial: its full-length chunks run as a gathered coalesced wave (a 64-bit
+    pointer per 8-chunk row; lanes past the count store nothing), the short last chunk per lane (gather=1), or
+    every leftover chunk per lane (gather=0, RSH_K1_GATHER).  Sizes: 44 leftover full chunks; 63 + a short one;
+    1 leftover; a 16-B-unaligned base.  Bit-exact against the oracle (Generator.java:886-895)."""
+    import ctypes
+    monkeypatch.setenv("RSH_K1_GATHER", gather)
+    B, dl = 2048, 4
+    for nchunks, short, off in ((64 * 5 + 44, 0, 0), (64 * 3 + 64, 700, 0), (64 * 7 + 1, 0, 0), (64 * 2 + 17, 5, 9)):
+        n = (nchunks - (1 if short else 0)) * B + short
+        d = ctx.alloc(n + off + 256)
+        R.lib().rsh_fill_splitmix_device(ctx.handle, d.ptr, n + off, 0xC41 + nchunks, 0)
+        ctx.sync()
+        host = d.download()
+        h = R.header_make(B, dl, n)
+        assert h.chunk_count == nchunks
+        d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
+        assert R.lib().rsh_block_sums_device(ctx.handle, ctypes.c_void_p(d.ptr.value + off), n, ctypes.byref(h),
+                                             np.frombuffer(SEED, np.uint8).ctypes.data, d_w.ptr, d_s.ptr) == 0
+        ctx.sync()
+        ow, os_ = O.generator(host[off:off + n], O.header(B, dl, n), SEED)
+        assert np.array_equal(d_w.download(dtype=np.int32), ow), f"weak, {nchunks} chunks"
+        assert np.array_equal(d_s.download(), os_), f"strong, {nchunks} chunks"
+
+
 def test_sender_phase_shift_chains(ctx):
     """Inserts and a delete of odd sizes in a 512 MiB source (B = 65536, 8192 chunks): after each the matches
     continue at a new phase kB + delta (Sender.java:1282-1287).  The phase-shifted speculation carries them
