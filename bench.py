@@ -15,6 +15,7 @@ sharding, no collective on the data path); value = all ranks' bytes / max-over-r
 import argparse
 import ctypes
 import json
+import gc
 import os
 import queue
 import sys
@@ -40,8 +41,8 @@ KEY_EDIT = (0x5EED5EED << 32) | 0xED17
 KEY_CASE = KEY_SRC ^ 5
 KEY_INS = KEY_SRC ^ 0x1B
 SHIFT_AT = 155 * 131072 + 4096  # the "config5_shift1" insert position
-TRAFFIC_CSV = "r2_v16_bench_fetch_size.csv"
-TRAFFIC_FILES_CSV = "r2_v16_files_fetch_size.csv"
+TRAFFIC_CSV = "r2_v18_bench_fetch_size.csv"
+TRAFFIC_FILES_CSV = "r2_v18_files_fetch_size.csv"
 
 
 def parse():
@@ -169,18 +170,31 @@ def main():
         ctx.sync()
         barrier()
         torch.cuda.synchronize()
+        # the timed steps run with Python's cyclic GC paused (as timeit does): a collection inside a step
+        # stalled one 6.3 ms step to 18 ms (r2_steps); BENCH_GC=1 keeps it on (A/B)
+        gc.collect()
+        gc_off = os.environ.get("BENCH_GC", "0") != "1" and gc.isenabled()
+        if gc_off:
+            gc.disable()
         t0 = time.perf_counter()
+        t_step = []  # host time at each step's end (the scan call returns when its events are final)
         for i in range(steps):
             step(i)
+            t_step.append(time.perf_counter())
         ctx.sync()
         torch.cuda.synchronize()
         barrier()
         dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device="cuda")
-        gen_ms = float(np.mean([s0.elapsed_time(e0) for s0, e0 in gen_ev]))
+        if gc_off:
+            gc.enable()
+        step_ms = [round((b - a) * 1e3, 3) for a, b in zip([t0] + t_step[:-1], t_step)]
+        gen_steps = [s0.elapsed_time(e0) for s0, e0 in gen_ev]
+        gen_ms = float(np.mean(gen_steps))
         # bytes the timed region read: the Generator's basis pass + the source bytes the scan's device work
         # read (its speculation K1s when they ran to completion, probed ranges, digest windows)
         read_step = n + float(np.mean(dev_bytes))
-        out = {"ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
+        out = {"ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "step_ms": step_ms,
+               "step_kernel_ms": [[round(g, 3) for g in gen_steps], [round(x, 3) for x in spec_ms]],
                "bytes_read_per_step": int(read_step),
                "value_read": round(world * steps * read_step / dt / (1 << 30), 3),
                "generator_kernel_ms": round(gen_ms, 4),
@@ -213,6 +227,8 @@ def main():
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": head["ms_per_step"],
+        "step_ms": head["step_ms"],
+        "step_kernel_ms": head["step_kernel_ms"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
