@@ -41,6 +41,7 @@ KEY_EDIT = (0x5EED5EED << 32) | 0xED17
 KEY_CASE = KEY_SRC ^ 5
 KEY_INS = KEY_SRC ^ 0x1B
 SHIFT_AT = 155 * 131072 + 4096  # the "config5_shift1" insert position
+WARMUP_MIN_MS = 250.0  # untimed warmup of at least this long (and at least --warmup steps)
 TRAFFIC_CSV = "r2_v18_bench_fetch_size.csv"
 TRAFFIC_FILES_CSV = "r2_v18_files_fetch_size.csv"
 
@@ -48,7 +49,7 @@ TRAFFIC_FILES_CSV = "r2_v18_files_fetch_size.csv"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--size-gib", type=float, default=16.0)
     ap.add_argument("--block", type=int, default=131072)
@@ -165,14 +166,29 @@ def main():
                 spec_ms.append(st.spec_kernel_ms)
                 dev_bytes.append(st.device_bytes)
 
-        for _ in range(warmup):
-            step()
-        ctx.sync()
+        # W warmup steps, and at least WARMUP_MIN_MS of them (untimed; the line reports how long they ran)
+        tw = time.perf_counter()
+        done = 0
+        diag = int(os.environ.get("BENCH_DIAG", "0"))  # A/B: 1 warmup records the timing events too
+        while done < warmup or (time.perf_counter() - tw < WARMUP_MIN_MS / 1e3 and done < 200):
+            step(done % steps if diag & 1 else None)
+            done += 1
+        spec_ms.clear()
+        dev_bytes.clear()
+        for s0, e0 in gen_ev:  # the timing events exist before the clock starts (torch creates them lazily)
+            s0.record(stream)
+            e0.record(stream)
+        if not diag & 2:  # A/B: 2 = no sync between the warmup and the timed steps (diagnostic only)
+            ctx.sync()
+            torch.cuda.synchronize()
+        warmup_ms = (time.perf_counter() - tw) * 1e3
         barrier()
         torch.cuda.synchronize()
-        # the timed steps run with Python's cyclic GC paused (as timeit does): a collection inside a step
-        # stalled one 6.3 ms step to 18 ms (r2_steps); BENCH_GC=1 keeps it on (A/B)
-        gc.collect()
+        # the timed steps run with Python's cyclic GC paused (as timeit does); no gc.collect() first: the objects
+        # it frees release device memory, and the timed steps after it ramped from 7.9 to 6.3 ms over ~6 steps
+        # (r2_ramp); BENCH_GC=1 keeps the GC on (A/B), BENCH_DIAG=4 collects first (A/B)
+        if int(os.environ.get("BENCH_DIAG", "0")) & 4:
+            gc.collect()
         gc_off = os.environ.get("BENCH_GC", "0") != "1" and gc.isenabled()
         if gc_off:
             gc.disable()
@@ -194,6 +210,7 @@ def main():
         # read (its speculation K1s when they ran to completion, probed ranges, digest windows)
         read_step = n + float(np.mean(dev_bytes))
         out = {"ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "step_ms": step_ms,
+               "warmup_steps": done, "warmup_ms": round(warmup_ms, 1),
                "step_kernel_ms": [[round(g, 3) for g in gen_steps], [round(x, 3) for x in spec_ms]],
                "bytes_read_per_step": int(read_step),
                "value_read": round(world * steps * read_step / dt / (1 << 30), 3),
@@ -226,6 +243,8 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
+        "warmup_steps": head["warmup_steps"],
+        "warmup_ms": head["warmup_ms"],
         "ms_per_step": head["ms_per_step"],
         "step_ms": head["step_ms"],
         "step_kernel_ms": head["step_kernel_ms"],
@@ -446,6 +465,9 @@ def main_files(a):
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
+    gc_off = os.environ.get("BENCH_GC", "0") != "1" and gc.isenabled()  # as in run_variant (no collection first)
+    if gc_off:
+        gc.disable()
     t0 = time.perf_counter()
     matched = 0
     dev_bytes = []
@@ -457,6 +479,8 @@ def main_files(a):
     if world > 1:
         dist.barrier()
     dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device="cuda")
+    if gc_off:
+        gc.enable()
     if batch:
         matched = check_jobs()
     # bytes the timed region read: the Generator's pass over the bases + what the scans' device work read
