@@ -689,7 +689,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     std::vector<K1Plan> plans;
     std::vector<K1Lane> lanes;
     int lane_align = 16;
-    uint32_t ngroups = plan_block_sums_files(k1.data(), NF, &plans, &lanes, &lane_align);
+    bool partial = tail_gather_on() && !batch_quad();
+    uint32_t ngroups = plan_block_sums_files(k1.data(), NF, &plans, &lanes, &lane_align, &partial);
     RSH_BHIP(S->k1_groups.ensure(((size_t)ngroups + 1) * sizeof(K1Group)));
     RSH_BHIP(S->k1_plans.ensure((plans.size() + 1) * sizeof(K1Plan)));
     RSH_BHIP(S->k1_lanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
@@ -850,7 +851,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         // the sources may come from work on the context stream (and the lead sums go first, see above)
         RSH_BHIP(hipStreamWaitEvent(aux, spec_after_prep ? c->ev_prep : c->ev_in, 0));
         RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>(), ngroups, S->k1_lanes.as<K1Lane>(),
-                                         (uint32_t)lanes.size(), lane_align, seed_word(seed), aux, c->abort_word, gen));
+                                         (uint32_t)lanes.size(), lane_align, seed_word(seed), aux, c->abort_word, gen,
+                                         partial));
         return RSH_OK;
     };
     auto launch_spec = [&]() -> int {
@@ -1202,7 +1204,9 @@ int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t
     std::vector<K1Plan> plans;
     std::vector<K1Lane> lanes;
     int lane_align = 16;
-    const uint32_t ngroups = plan_block_sums_files(files.data(), (int32_t)files.size(), &plans, &lanes, &lane_align);
+    bool partial = tail_gather_on() && !batch_quad();
+    const uint32_t ngroups =
+        plan_block_sums_files(files.data(), (int32_t)files.size(), &plans, &lanes, &lane_align, &partial);
     RSH_BHIP(S->g_groups.ensure(((size_t)ngroups + 1) * sizeof(K1Group)));
     RSH_BHIP(S->g_plans.ensure((plans.size() + 1) * sizeof(K1Plan)));
     RSH_BHIP(S->g_lanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
@@ -1226,7 +1230,8 @@ int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t
     RSH_BHIP(launch_expand_groups(S->g_plans.as<K1Plan>(), (uint32_t)plans.size(), ngroups, S->g_groups.as<K1Group>(),
                                   ctx->stream));
     RSH_BHIP(launch_block_sums_batch(S->g_groups.as<K1Group>(), ngroups, S->g_lanes.as<K1Lane>(),
-                                     (uint32_t)lanes.size(), lane_align, seed_word(seed), ctx->stream));
+                                     (uint32_t)lanes.size(), lane_align, seed_word(seed), ctx->stream, nullptr, 0,
+                                     partial));
     return RSH_OK;
 }
 

@@ -40,6 +40,7 @@ struct K1Group {
     uint32_t B, dl;
     const int* abort = nullptr;  // abortable launches: this group's own abort word (nullptr: the launch's)
     int32_t file = 0;            // index of its file in the planner's list (host bookkeeping only)
+    uint32_t count = 64;         // its chunks (< 64: a file's partial last wave, run as a gathered wave)
 };
 struct K1Lane {
     const uint8_t* data;  // the file
@@ -82,21 +83,27 @@ struct K1Plan {
     int32_t* weak;
     uint8_t* strong;
     uint32_t B, dl;
-    uint32_t g0, ng;            // groups [g0, g0 + ng) of the launch are this file's chunks [0, 64 ng)
+    uint32_t g0, ng;            // groups [g0, g0 + ng) of the launch are this file's chunks [0, min(64 ng, nfull))
     const int* abort = nullptr;  // K1Group::abort of its groups
     int32_t file = 0;
+    uint32_t nfull = 0;          // its full-length chunks covered by groups (the last group may be partial)
 };
-// plans (one per file with full groups, ascending g0) and the host lanes; returns the total group count
+// plans (one per file with groups, ascending g0) and the host lanes; returns the total group count.  A file's
+// full-length chunks past its last full wave form a partial group (K1Group::count < 64) when *partial is set
+// on entry (RSH_K1_GATHER, not with the 4-waves kernel); on return *partial says whether any plan has one.
 uint32_t plan_block_sums_files(const K1File* files, int32_t nfiles, std::vector<K1Plan>* plans,
-                               std::vector<K1Lane>* lanes, int* lane_align);
+                               std::vector<K1Lane>* lanes, int* lane_align, bool* partial = nullptr);
 hipError_t launch_expand_groups(const K1Plan* d_plans, uint32_t nplans, uint32_t ngroups, K1Group* d_groups,
                                 hipStream_t s);
 // the same over groups only, at 4 waves per SIMD (block_sums_quad_kernel; A/B: RSH_K1_QUAD=1, kbench 1004)
 hipError_t launch_block_sums_batch_quad(const K1Group* d_groups, uint32_t ngroups, uint32_t seed_word, hipStream_t s,
                                         const int* abort_flag = nullptr, int abort_gen = 0);
+bool batch_quad();
+bool tail_gather_on();  // RSH_K1_GATHER=0 (A/B, read per call): leftover chunks one per lane, no gathered waves  // RSH_K1_QUAD=1 (A/B): the batched groups at 4 waves per SIMD
+// partial: some groups have count < 64 (plan_block_sums_files) -- they run as gathered waves of the same launch
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
                                    int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag = nullptr,
-                                   int abort_gen = 0);
+                                   int abort_gen = 0, bool partial = false);
 
 // Chain flags for the Sender fast path: flag[k] = 1 iff source window k (aligned, from the source's
 // own block sums) has the same weak key and the same dl-byte digest as basis chunk k.

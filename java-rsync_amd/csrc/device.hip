@@ -790,7 +790,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
     block_sums_pipe_body<8, ABORT, true, 0, false>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
                                                    nullptr, n, nchunks, main_waves);
 }
-static bool tail_gather_on() {  // RSH_K1_GATHER=0 (A/B, read per launch): leftover chunks one per lane
+bool tail_gather_on() {  // RSH_K1_GATHER=0 (A/B, read per launch): leftover chunks one per lane
     const char* gm = getenv("RSH_K1_GATHER");
     return !gm || atoi(gm) != 0;
 }
@@ -1743,10 +1743,35 @@ void plan_block_sums_batch(const K1File* files, int32_t nfiles, std::vector<K1Gr
 
 
 uint32_t plan_block_sums_files(const K1File* files, int32_t nfiles, std::vector<K1Plan>* plans,
-                               std::vector<K1Lane>* lanes, int* lane_align) {
+                               std::vector<K1Lane>* lanes, int* lane_align, bool* partial) {
     plans->clear();
     lanes->clear();
     *lane_align = 16;
+    bool want_partial = partial && *partial;
+    if (partial) *partial = false;
+    if (want_partial) {
+        // partial groups + one lane per short chunk, or (as without them) one lane wave per file tail: whichever
+        // needs fewer rounds of the chip's wave slots (a wave past the last full round waits for a free slot;
+        // the lanes run in the same launch, launch_block_sums_batch)
+        uint64_t full = 0, w_part = 0, shorts = 0, w_lane = 0;
+        for (int32_t f = 0; f < nfiles; ++f) {
+            const K1File& F = files[f];
+            if (F.nchunks == 0 || F.B == 0) continue;
+            const uint32_t nst = F.B >> 7;
+            const uintptr_t addr = reinterpret_cast<uintptr_t>(F.data);
+            uint32_t nfullc = 0;
+            if ((F.B % 128) == 0 && nst >= 4 && nst <= 1024 && (addr % 16) == 0)
+                nfullc = (uint32_t)std::min<int64_t>(F.n / F.B, F.nchunks);
+            full += nfullc / 64;
+            w_part += (nfullc % 64) ? 1 : 0;
+            shorts += F.nchunks - nfullc;
+            w_lane += (F.nchunks - 64 * (nfullc / 64) + 63) / 64;
+        }
+        const uint64_t slots = 2ull * 4 * kCUs;
+        const uint64_t r_part = (full + w_part + (shorts + 63) / 64 + slots - 1) / slots;
+        const uint64_t r_lane = (full + w_lane + slots - 1) / slots;
+        want_partial = w_part > 0 && r_part <= r_lane;
+    }
     uint32_t g = 0;
     for (int32_t f = 0; f < nfiles; ++f) {  // the same cut as plan_block_sums_batch
         const K1File& F = files[f];
@@ -1756,10 +1781,13 @@ uint32_t plan_block_sums_files(const K1File* files, int32_t nfiles, std::vector<
         uint32_t c = 0;
         if ((F.B % 128) == 0 && nst >= 4 && nst <= 1024 && (addr % 16) == 0) {
             const uint32_t nfullc = (uint32_t)std::min<int64_t>(F.n / F.B, F.nchunks);
-            const uint32_t ng = nfullc / 64;
-            if (ng > 0) plans->push_back(K1Plan{F.data, F.weak, F.strong, F.B, F.dl, g, ng, nullptr, f});
+            // the full chunks past the last full wave: a partial group (gathered wave) or lanes
+            const uint32_t ng = want_partial ? (nfullc + 63) / 64 : nfullc / 64;
+            const uint32_t cov = std::min(nfullc, 64 * ng);
+            if (ng > 0) plans->push_back(K1Plan{F.data, F.weak, F.strong, F.B, F.dl, g, ng, nullptr, f, cov});
+            if (cov % 64 != 0) *partial = true;
             g += ng;
-            c = 64 * ng;
+            c = cov;
         }
         for (; c < F.nchunks; c += 64) {
             lanes->push_back(K1Lane{F.data, F.n, F.weak, F.strong, F.B, F.dl, c, F.nchunks, f});
@@ -1782,7 +1810,8 @@ __global__ __launch_bounds__(256) void expand_groups_kernel(const K1Plan* __rest
     }
     const K1Plan& P = plans[lo];
     const uint32_t c = 64 * (t - P.g0);
-    groups[t] = K1Group{P.data + (size_t)c * P.B, P.weak + c, P.strong + (size_t)c * P.dl, P.B, P.dl, P.abort, P.file};
+    groups[t] = K1Group{P.data + (size_t)c * P.B, P.weak + c, P.strong + (size_t)c * P.dl, P.B, P.dl, P.abort, P.file,
+                        min(64u, P.nfull - c)};
 }
 
 hipError_t launch_expand_groups(const K1Plan* d_plans, uint32_t nplans, uint32_t ngroups, K1Group* d_groups,
@@ -1816,6 +1845,37 @@ static bool plain_k1() {
     return v;
 }
 
+// The batched K1 with its leftovers in the same launch: groups some of which are a file's partial last wave
+// (K1Group::count < 64: the gathered-wave path, one 64-bit pointer per 8-chunk row, lanes past the count store
+// nothing), then the lane waves (short chunks and odd shapes, one chunk per lane), instead of the per-lane
+// kernel queued behind the groups (a wave of it takes one chunk's serial time: ~2 ms at B = 128 KiB).
+// Register budget 256 as block_sums_pipe_tailg_kernel.
+template <int ALIGN>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void block_sums_pipe_multi_g_kernel(
+    const K1Group* __restrict__ groups, uint32_t ngroups, const K1Lane* __restrict__ lanes, uint32_t seed,
+    const int* abort_flag, int abort_gen) {
+    if (blockIdx.x >= ngroups) {  // the lane waves (short chunks, odd shapes) in the same launch
+        const K1Lane e = lanes[blockIdx.x - ngroups];
+        const uint32_t c = e.c_first + threadIdx.x;
+        if (c < e.nchunks)
+            lane_chunk_sums<ALIGN == 1 ? 0 : ALIGN, ALIGN == 16 ? 4 : ALIGN == 4 ? 2 : 4, ALIGN != 1>(
+                e.data, e.n, e.B, c, e.dl, seed, e.weak, e.strong);
+        return;
+    }
+    const K1Group g = groups[blockIdx.x];
+    if (g.count < 64) {
+        block_sums_pipe_body<8, true, true, 0, false, true>(g.data, g.B, g.dl, seed, g.weak, g.strong,
+                                                           g.abort ? g.abort : abort_flag, abort_gen, nullptr, 0, 0,
+                                                           0xFFFFFFFFu, nullptr, g.count);
+        return;
+    }
+    block_sums_pipe_body<8, true, true, 0, true>(nullptr, 0u, 0u, seed, nullptr, nullptr, abort_flag, abort_gen, groups);
+}
+bool batch_quad() {  // RSH_K1_QUAD=1 (A/B): the batched groups at 4 waves/SIMD
+    static const bool v = getenv("RSH_K1_QUAD") && atoi(getenv("RSH_K1_QUAD")) != 0;
+    return v;
+}
+
 hipError_t launch_block_sums_batch_quad(const K1Group* d_groups, uint32_t ngroups, uint32_t seed_word, hipStream_t s,
                                         const int* abort_flag, int abort_gen) {
     if (ngroups == 0) return hipSuccess;
@@ -1831,10 +1891,26 @@ hipError_t launch_block_sums_batch_quad(const K1Group* d_groups, uint32_t ngroup
 
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
                                    int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag,
-                                   int abort_gen) {
+                                   int abort_gen, bool partial) {
     const size_t lb = 2 * 64 * 9 * sizeof(uint4);
-    static const bool quad = getenv("RSH_K1_QUAD") && atoi(getenv("RSH_K1_QUAD")) != 0;  // A/B: 4 waves/SIMD
+    static const bool quad = batch_quad();
     if (!abort_flag && !plain_k1() && (abort_flag = never_word()) != nullptr) abort_gen = -1;  // see never_word
+    // partial groups, or lanes beside groups: one launch (RSH_K1_GATHER=0: the lanes as a second launch)
+    if (partial || (tail_gather_on() && !quad && nlanes > 0 && ngroups > 0)) {
+        if (!abort_flag && (abort_flag = never_word()) != nullptr) abort_gen = -1;
+        if (!abort_flag || quad) return hipErrorInvalidValue;  // the planner makes no partial group for these
+        const dim3 grid(ngroups + nlanes);
+        if (lane_align == 16)
+            hipLaunchKernelGGL((block_sums_pipe_multi_g_kernel<16>), grid, dim3(64), lb, s, d_groups, ngroups, d_lanes,
+                               seed_word, abort_flag, abort_gen);
+        else if (lane_align == 4)
+            hipLaunchKernelGGL((block_sums_pipe_multi_g_kernel<4>), grid, dim3(64), lb, s, d_groups, ngroups, d_lanes,
+                               seed_word, abort_flag, abort_gen);
+        else
+            hipLaunchKernelGGL((block_sums_pipe_multi_g_kernel<1>), grid, dim3(64), lb, s, d_groups, ngroups, d_lanes,
+                               seed_word, abort_flag, abort_gen);
+        return hipGetLastError();
+    }
     if (ngroups > 0 && quad) {
         const hipError_t e = launch_block_sums_batch_quad(d_groups, ngroups, seed_word, s, abort_flag, abort_gen);
         if (e != hipSuccess) return e;

@@ -83,6 +83,40 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d_lanes, (lanes.size() + 1) * sizeof(rsh::K1Lane)));
     CK(hipMemcpy(d_groups, groups.data(), groups.size() * sizeof(rsh::K1Group), hipMemcpyHostToDevice));
     if (!lanes.empty()) CK(hipMemcpy(d_lanes, lanes.data(), lanes.size() * sizeof(rsh::K1Lane), hipMemcpyHostToDevice));
+    // variant 1005: the production batch planner (plan_block_sums_files, groups expanded on the device) over
+    // KBENCH_FILES files of per - KBENCH_RAG bytes each (ragged: every file has a partial last wave and a short
+    // chunk); RSH_K1_GATHER picks gathered partial groups or per-lane leftovers.  Parity is not comparable to
+    // variant 0 when KBENCH_RAG > 0 (the files' chunk grids differ from the buffer's).
+    const int64_t rag = getenv("KBENCH_RAG") ? atoll(getenv("KBENCH_RAG")) : 0;
+    std::vector<rsh::K1File> kr;
+    for (int f = 0; f < nfiles; ++f) {
+        const int64_t len = per - rag;
+        const uint32_t c0 = (uint32_t)((int64_t)f * per / B);
+        kr.push_back(rsh::K1File{d + (int64_t)f * per, len, B, dl, (uint32_t)((len + B - 1) / B), w + c0,
+                                 sx + (size_t)c0 * dl});
+    }
+    auto launch_rag = [&]() -> hipError_t {
+        std::vector<rsh::K1Plan> plans;
+        std::vector<rsh::K1Lane> rl;
+        int ra = 16;
+        bool partial = rsh::tail_gather_on();
+        const uint32_t ng = rsh::plan_block_sums_files(kr.data(), nfiles, &plans, &rl, &ra, &partial);
+        static rsh::K1Plan* d_plans = nullptr;
+        static rsh::K1Group* d_rg = nullptr;
+        static rsh::K1Lane* d_rl = nullptr;
+        if (!d_plans) {
+            CK(hipMalloc(&d_plans, (size_t)(nfiles + 1) * sizeof(rsh::K1Plan)));
+            CK(hipMalloc(&d_rg, (size_t)(C / 64 + nfiles + 1) * sizeof(rsh::K1Group)));
+            CK(hipMalloc(&d_rl, (size_t)(2 * nfiles + 1) * sizeof(rsh::K1Lane)));
+            CK(hipMemcpy(d_plans, plans.data(), plans.size() * sizeof(rsh::K1Plan), hipMemcpyHostToDevice));
+            if (!rl.empty()) CK(hipMemcpy(d_rl, rl.data(), rl.size() * sizeof(rsh::K1Lane), hipMemcpyHostToDevice));
+            CK(rsh::launch_expand_groups(d_plans, (uint32_t)plans.size(), ng, d_rg, s));
+            CK(hipStreamSynchronize(s));
+            printf("variant 1005: %u groups (partial %d), %zu lane waves\n", ng, (int)partial, rl.size());
+        }
+        return rsh::launch_block_sums_batch(d_rg, ng, d_rl, (uint32_t)rl.size(), ra, 0x04030201u, s, nullptr, 0,
+                                            partial);
+    };
     // variant 1003: the segmented launch (block_sums_seg_kernel) over the whole buffer as one segment; the
     // buffer's base must be such that base - base % 128 is inside the allocation (KBENCH_OFFSET < 128)
     const uint32_t a_off = (uint32_t)(reinterpret_cast<uintptr_t>(d) % 128);
@@ -109,6 +143,7 @@ int main(int argc, char** argv) {
                                                                                return (int64_t)(t.c + 1) * B <= t.n;
                                                                            }),
                                                    B, dl, 0x04030201u, s);
+        if (v == 1005) return launch_rag();
         if (v == 1002)
             return rsh::launch_block_sums_batch(d_groups, (uint32_t)groups.size(), d_lanes, (uint32_t)lanes.size(),
                                                 lane_align, 0x04030201u, s);
