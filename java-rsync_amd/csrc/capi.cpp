@@ -389,7 +389,9 @@ class HipBackend : public rsh::ScanBackend {
         if (ph_s0_ < 0 || s < ph_s0_ || (s - ph_s0_) % B_ != 0 || s >= ph_s0_ + ph_count_ * B_ || err != hipSuccess)
             return false;
         if (!ph_landed_) {
-            if (wait) {
+            // a phase K1 that has finished leaves only its sums' download (~1 MB): waiting for it beats a host
+            // digest of the window (0.13 ms at B = 128 KiB), the resolver's alternative at a hit
+            if (wait || hipEventQuery(c_->ev_phb) == hipSuccess) {
                 CallTrace tr("phase_wait", s);
                 ok(hipEventSynchronize(c_->ev_phase));
                 ph_landed_ = err == hipSuccess;
@@ -884,6 +886,19 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                     be.phase_adopt(s0, Q, gph);
                     res->stats.phase_guesses++;
                     spec_launched = seg_launched = true;
+                    // The resolver's first question past the prefix chain: the first hit in [P B, P B + 9 B] (synced
+                    // state, the whole table; resolver.cpp step 2: window P is past the speculated windows, so
+                    // its own sum is not known and the probe starts there).  Asked now, beside the launch, its
+                    // answer and the window at the hit are in the backend's hit cache when the speculation
+                    // lands, instead of a round trip after it (0.17-0.19 ms on the shift case).  Unused (and
+                    // harmless) when the resolver asks elsewhere.  RSH_SCAN_PREPROBE=0 (A/B, per scan).
+                    const bool preprobe = !getenv("RSH_SCAN_PREPROBE") || atoi(getenv("RSH_SCAN_PREPROBE")) != 0;
+                    const int64_t last = n - (h->remainder > 0 ? h->remainder : B);
+                    const int64_t pa = P * B, pstop = std::min(P * B + 9 * B, last);
+                    if (preprobe && P * B + 10 * B <= n && pa <= pstop && be.err == hipSuccess) {
+                        const rsh::ProbeInterval iv{pa, pstop + 1, pa, 0, 0};
+                        (void)be.first_hit(&iv, 1, nullptr);
+                    }
                 }
             }
         }
