@@ -1163,9 +1163,18 @@ template <int W>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGPR))) void block_sums_shift_kernel(
     const uint8_t* __restrict__ data, int64_t n, uint32_t a, uint32_t B, uint32_t nchunks, uint32_t main_waves,
     uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out, uint8_t* __restrict__ strong_out,
-    const int* abort_flag, int abort_gen) {
+    const int* abort_flag, int abort_gen, uint32_t tail_full) {
     if (blockIdx.x >= main_waves) {
-        const uint32_t c = main_waves * 64u + (blockIdx.x - main_waves) * 64u + threadIdx.x;
+        // the first tail_full leftover chunks (full length) as gathered coalesced waves, the rest per lane
+        const uint32_t tw = blockIdx.x - main_waves, ngw = (tail_full + 63u) / 64u;
+        if (tw < ngw) {
+            const uint32_t first = main_waves * 64u + 64u * tw;
+            block_sums_pipe_body<8, true, true, 0, false, true>(
+                data + (size_t)first * B, B, dl, seed, weak_out + first, strong_out + (size_t)first * dl, abort_flag,
+                abort_gen, nullptr, 0, 0, 0xFFFFFFFFu, nullptr, min(64u, tail_full - 64u * tw));
+            return;
+        }
+        const uint32_t c = main_waves * 64u + tail_full + (tw - ngw) * 64u + threadIdx.x;
         if (c < nchunks) lane_chunk_sums<16, 4, false>(data, n, B, c, dl, seed, weak_out, strong_out);
         return;
     }
@@ -1387,25 +1396,33 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
             const int64_t fit = avail >= 128 ? (avail - 128) / ((int64_t)64 * B) : 0;
             const uint32_t mw = (uint32_t)std::min<int64_t>(nfullc / 64, fit);
             if (mw > 0) {
-                const uint32_t tail_waves = (nchunks - 64 * mw + 63) / 64;
+                uint32_t tail_waves = (nchunks - 64 * mw + 63) / 64;
+                // full-length leftovers gathered into coalesced waves when that adds no wave or every wave fits
+                // the chip's slots (as block_sums_pipe_tailg_kernel); LDS then for the gathered body's buffers
+                const uint32_t tail_full = nfullc - 64 * mw, tail_short = nchunks - nfullc;
+                const uint32_t gwaves = (tail_full + 63) / 64 + (tail_short + 63) / 64;
+                const bool gather = tail_full > 0 && tail_gather_on() &&
+                                    (gwaves == tail_waves || mw + gwaves <= 2 * 4 * kCUs);
+                const uint32_t tf = gather ? tail_full : 0u;
+                if (gather) tail_waves = gwaves;
                 const dim3 grid(mw + tail_waves);
-                const size_t lb = 64 * 17 * sizeof(uint4);
+                const size_t lb = gather ? 2 * 64 * 9 * sizeof(uint4) : 64 * 17 * sizeof(uint4);
                 switch ((a >> 2) & 3) {
                     case 0:
                         hipLaunchKernelGGL((block_sums_shift_kernel<0>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
-                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen);
+                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
                         break;
                     case 1:
                         hipLaunchKernelGGL((block_sums_shift_kernel<1>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
-                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen);
+                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
                         break;
                     case 2:
                         hipLaunchKernelGGL((block_sums_shift_kernel<2>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
-                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen);
+                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
                         break;
                     default:
                         hipLaunchKernelGGL((block_sums_shift_kernel<3>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
-                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen);
+                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
                 }
                 return hipGetLastError();
             }
