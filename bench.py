@@ -9,8 +9,11 @@ a 16 GiB source against a 50%-modified basis (every other block replaced), B = 1
 01 02 03 04, splitmix64 synthetic bytes generated on the device.  The serial whole-file MD5 runs on the
 host in the product (rsh_match_scan) and is excluded here (see DESIGN.md "Measurement").
 
-Multi-GPU: one process per GPU (torch.distributed.run), each rank scans its own file pair (file-parallel
-sharding, no collective on the data path); value = all ranks' bytes / max-over-ranks time.
+Multi-GPU: one process per GPU, each rank scans its own file pair (file-parallel sharding, no collective on the
+data path); value = all ranks' bytes / max-over-ranks time.  Under torch.distributed.run the ranks come from its
+environment; `python bench.py --gpus N` without a launcher starts the N rank processes itself (spawn_ranks) before
+anything touches a GPU.  `--dry-run` runs the rank plumbing (gloo barrier, max-over-ranks reduction, the JSON line)
+without a device.
 """
 import argparse
 import ctypes
@@ -18,6 +21,8 @@ import json
 import gc
 import os
 import queue
+import socket
+import subprocess
 import sys
 import time
 
@@ -69,11 +74,73 @@ def parse():
                          "per round for all files) or one rsh_match_scan_device per file on a context pool")
     ap.add_argument("--cpu-sample-mib", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank plumbing only (gloo on CPU, no device): the line reports n_gpus and no value")
     return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(a):
+    """`--gpus N` (N > 1) without an external launcher: start one child process per GPU with RANK, LOCAL_RANK,
+    WORLD_SIZE and a 127.0.0.1 rendezvous, as torch.distributed.run would, and return the worst exit code.  This
+    process touches no GPU (the children do), so starting them is safe.  A rank that fails stops the others
+    (they would wait in a barrier forever)."""
+    port = _free_port()
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def main_dry(a):
+    """The multi-rank plumbing without a device (CPU test of --gpus N): gloo process group, the barriers and
+    the max-over-ranks reduction of the timed region, rank 0's JSON line."""
+    rank, world, _ = shard.env_rank()
+    if world > 1:
+        shard.init_distributed("gloo")
+    t0 = time.perf_counter()
+    sizes = [a.file_mib << 20] * (a.files * world)
+    mine = shard.shard_files(sizes, world)[rank]
+    dt = shard.reduce_over_ranks(time.perf_counter() - t0 + 1e-6, "max")
+    files = int(shard.reduce_over_ranks(len(mine), "sum"))
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (no device)", "value": None, "unit": "GiB/s", "n_gpus": world,
+                          "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt * 1e3, 3),
+                          "higher_is_better": True, "scaling": "weak", "dry_run": True,
+                          "config": {"workload": a.workload, "files_total": files,
+                                     "parallelism": f"file-sharded x{world} (no collectives)"}}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def main():
     a = parse()
+    if a.gpus > 1 and "RANK" not in os.environ:  # no launcher: one process per GPU, started here
+        sys.exit(spawn_ranks(a))
+    if a.dry_run:
+        return main_dry(a)
     if a.workload == "files":
         return main_files(a)
     if a.workload == "receiver":

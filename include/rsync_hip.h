@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RSH_ABI_VERSION 2
+#define RSH_ABI_VERSION 3
 
 /* Status codes (the JNI shim maps them onto the reference's exception types). */
 #define RSH_OK 0
@@ -213,6 +213,24 @@ int rsh_match_scan_file(rsh_ctx* ctx, const char* path, int64_t size, const rsh_
                         const uint8_t* strong, const uint8_t seed[4], rsh_event* ev, int64_t ev_cap, int64_t* n_ev,
                         uint8_t file_md5[16], int64_t* literal, int64_t* matched, rsh_scan_stats* stats,
                         int32_t* read_error);
+
+/* ---- a file handed over as a list of host buffers ----
+ * A JVM cannot hold a file above 2^31 - 1 bytes in one direct ByteBuffer, while the reference streams any
+ * file size through FileView (FileView.java:51-80,235-278).  These forms take the file as pieces (each a
+ * caller-owned host buffer; the file is their concatenation, in order; a chunk or window may straddle
+ * two pieces) and return exactly what rsh_block_sums / rsh_match_scan return for the concatenated bytes.
+ * The Sender's literal events name file offsets; the binding replays each from the pieces
+ * (INTEGRATION.md).  Sources above 32 GiB are paged through HBM a tile at a time. */
+typedef struct {
+    const uint8_t* data;
+    int64_t len;
+} rsh_piece;
+int rsh_block_sums_pieces(rsh_ctx* ctx, const rsh_piece* pieces, int32_t npieces, const rsh_header* h,
+                          const uint8_t seed[4], int32_t* weak_out, uint8_t* strong_out);
+int rsh_match_scan_pieces(rsh_ctx* ctx, const rsh_piece* pieces, int32_t npieces, const rsh_header* h,
+                          const int32_t* weak, const uint8_t* strong, const uint8_t seed[4], rsh_event* ev,
+                          int64_t ev_cap, int64_t* n_ev, uint8_t file_md5[16], int64_t* literal, int64_t* matched,
+                          rsh_scan_stats* stats);
 
 /* ---- Receiver (Receiver.java:459-555 combineDataToFile, :557-578 copies, :204-209 blockSize) ----
  * Replays one file's de-multiplexed token stream -- putInt(len)+bytes, putInt(-(i+1)), putInt(0), exactly

@@ -111,7 +111,7 @@ class HipBackend : public rsh::ScanBackend {
     }
     void load_tile(int64_t lo) {
         CallTrace tr("tile_load", lo);
-        if (ph_s0_ >= 0 && !ph_landed_) ok(hipEventSynchronize(c_->ev_phase));  // it reads the old tile
+        if (ph_s0_ >= 0 && !ph_landed_) ok(hipEventSynchronize(c_->ev_phase[ph_set_]));  // it reads the old tile
         const int64_t hi = std::min(n_, lo + tile_T + tile_H);
         ok(fill(tile_buf, lo, hi - lo));
         if (err != hipSuccess) return;
@@ -369,16 +369,25 @@ class HipBackend : public rsh::ScanBackend {
         CallTrace tr("phase_spec", s);
         ph_gen_ = ++c_->gen;
         hipStream_t ps = c_->phase;  // its own stream: it does not queue behind a prefix speculation on aux
+        // The launch this one replaces may still be draining on another stream (the segmented launch on aux
+        // keeps its prefix waves and tail lanes running after the phase word stops its phase waves) and
+        // still write its sums and their host copies: this launch takes the other buffer set, after that
+        // set's previous launch and downloads.
+        const int set = 1 - c_->ph_set;
         ok(hipStreamWaitEvent(ps, c_->ev_in, 0));
-        ok(hipEventRecord(c_->ev_pha, ps));
+        ok(hipStreamWaitEvent(ps, c_->ev_phase[set], 0));
+        ok(hipEventRecord(c_->ev_pha[set], ps));
         ok(rsh::launch_block_sums(x_ + s, std::min(n_ - s, count * B_), (uint32_t)B_, (uint32_t)count, (uint32_t)dl_,
                                   seed_word(seed_),
-                                  c_->ph_weak.as<int32_t>(), c_->ph_strong.as<uint8_t>(), ps,
+                                  c_->ph_weak[set].as<int32_t>(), c_->ph_strong[set].as<uint8_t>(), ps,
                                   c_->abort_word + rsh_ctx::kPhaseWord, ph_gen_));
-        ok(hipEventRecord(c_->ev_phb, ps));
-        ok(hipMemcpyAsync(c_->h_pw.p, c_->ph_weak.p, (size_t)count * 4, hipMemcpyDeviceToHost, ps));
-        if (dl_ > 0) ok(hipMemcpyAsync(c_->h_ps.p, c_->ph_strong.p, (size_t)count * dl_, hipMemcpyDeviceToHost, ps));
-        ok(hipEventRecord(c_->ev_phase, ps));
+        ok(hipEventRecord(c_->ev_phb[set], ps));
+        ok(hipMemcpyAsync(c_->h_pw[set].p, c_->ph_weak[set].p, (size_t)count * 4, hipMemcpyDeviceToHost, ps));
+        if (dl_ > 0)
+            ok(hipMemcpyAsync(c_->h_ps[set].p, c_->ph_strong[set].p, (size_t)count * dl_, hipMemcpyDeviceToHost, ps));
+        ok(hipEventRecord(c_->ev_phase[set], ps));
+        c_->ph_set = set;
+        ph_set_ = set;
         if (err != hipSuccess) return;
         ph_s0_ = s;
         ph_count_ = count;
@@ -391,27 +400,29 @@ class HipBackend : public rsh::ScanBackend {
         if (!ph_landed_) {
             // a phase K1 that has finished leaves only its sums' download (~1 MB): waiting for it beats a host
             // digest of the window (0.13 ms at B = 128 KiB), the resolver's alternative at a hit
-            if (wait || hipEventQuery(c_->ev_phb) == hipSuccess) {
+            if (wait || hipEventQuery(c_->ev_phb[ph_set_]) == hipSuccess) {
                 CallTrace tr("phase_wait", s);
-                ok(hipEventSynchronize(c_->ev_phase));
+                ok(hipEventSynchronize(c_->ev_phase[ph_set_]));
                 ph_landed_ = err == hipSuccess;
             } else {
-                ph_landed_ = hipEventQuery(c_->ev_phase) == hipSuccess;
+                ph_landed_ = hipEventQuery(c_->ev_phase[ph_set_]) == hipSuccess;
             }
             if (!ph_landed_) return false;
             bytes_read += std::min(n_ - ph_s0_, ph_count_ * B_);
             float ms = 0.f;
-            if (hipEventElapsedTime(&ms, c_->ev_pha, c_->ev_phb) == hipSuccess) phase_ms += ms;
+            if (hipEventElapsedTime(&ms, c_->ev_pha[ph_set_], c_->ev_phb[ph_set_]) == hipSuccess) phase_ms += ms;
         }
         v->s0 = ph_s0_;
         v->count = ph_count_;
-        v->w = c_->h_pw.as<int32_t>();
-        v->st = c_->h_ps.as<uint8_t>();
+        v->w = c_->h_pw[ph_set_].as<int32_t>();
+        v->st = c_->h_ps[ph_set_].as<uint8_t>();
         return true;
     }
     // A phase-shifted speculation the caller launched (the segmented prefix + phase launch, scan_device) over
-    // windows s0 + kB, k < count, generation gen, landing on ev_phase: from now on this backend's.
-    void phase_adopt(int64_t s0, int64_t count, int gen) {
+    // windows s0 + kB, k < count, generation gen, into buffer set `set`, landing on ev_phase[set]: from now on
+    // this backend's.
+    void phase_adopt(int64_t s0, int64_t count, int gen, int set) {
+        ph_set_ = set;
         ph_s0_ = s0;
         ph_count_ = count;
         ph_gen_ = gen;
@@ -421,9 +432,9 @@ class HipBackend : public rsh::ScanBackend {
     // A phase speculation still running when the scan ends (or moves to another phase) is stopped; later
     // work on the context stream waits until its waves have left.
     void phase_stop() {
-        if (ph_s0_ >= 0 && !ph_landed_ && hipEventQuery(c_->ev_phase) == hipErrorNotReady) {
+        if (ph_s0_ >= 0 && !ph_landed_ && hipEventQuery(c_->ev_phase[ph_set_]) == hipErrorNotReady) {
             ok(hipStreamWriteValue32(c_->stream, c_->abort_word + rsh_ctx::kPhaseWord, (uint32_t)ph_gen_, 0));
-            ok(hipStreamWaitEvent(c_->stream, c_->ev_phase, 0));
+            ok(hipStreamWaitEvent(c_->stream, c_->ev_phase[ph_set_], 0));
         }
         ph_s0_ = -1;
         ph_landed_ = false;
@@ -438,6 +449,7 @@ class HipBackend : public rsh::ScanBackend {
     static constexpr int64_t kPhaseMaxLaunches = 64;  // each covers the rest of the file
     int64_t ph_s0_ = -1, ph_count_ = 0;
     int ph_gen_ = 0;
+    int ph_set_ = 0;  // the buffer set (rsh_ctx::ph_weak[i] ...) of the current phase launch
     bool ph_landed_ = false;
 
     template <class T>
@@ -539,13 +551,15 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     RSH_HIP(c->h_as.ensure((size_t)na * dl + 1));
     RSH_HIP(c->h_fl.ensure((size_t)nf + 1));
     RSH_HIP(c->haw.ensure((size_t)na * 4));
-    RSH_HIP(c->ph_weak.ensure((size_t)na * 4));
-    RSH_HIP(c->ph_strong.ensure((size_t)na * dl + 1));
+    for (int i = 0; i < 2; ++i) {
+        RSH_HIP(c->ph_weak[i].ensure((size_t)na * 4));
+        RSH_HIP(c->ph_strong[i].ensure((size_t)na * dl + 1));
+        RSH_HIP(c->h_pw[i].ensure((size_t)na * 4));
+        RSH_HIP(c->h_ps[i].ensure((size_t)na * dl + 1));
+    }
     const size_t seg_bytes = ((size_t)na / 64 + 4) * sizeof(rsh::K1Seg) + 256 * sizeof(rsh::K1Tail);
     RSH_HIP(c->segs.ensure(seg_bytes));
     RSH_HIP(c->h_segs.ensure(seg_bytes));
-    RSH_HIP(c->h_pw.ensure((size_t)na * 4));
-    RSH_HIP(c->h_ps.ensure((size_t)na * dl + 1));
     // sample windows for the launch decision: the first nlead, then one every `stride` windows
     const int64_t nlead = std::min<int64_t>(kLeadWindows, nf);
     static const int64_t nsamples = getenv("RSH_SCAN_SAMPLES") ? std::max(1, atoi(getenv("RSH_SCAN_SAMPLES")))
@@ -831,17 +845,19 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             const uint32_t a0 = (uint32_t)(addr % 128), a1 = (uint32_t)((addr + (uintptr_t)s0) % 128);
             if (P > 0 && Q >= 8 && addr - a0 >= alo && be.err == hipSuccess) {
                 auto* sg = reinterpret_cast<rsh::K1Seg*>(c->h_segs.p);
-                const int64_t wp = P / 64;
+                int64_t wp = P / 64;  // full prefix waves whose lines (64 B + 128 bytes from d_src - a0) stay in it
+                while (wp > 0 && addr - a0 + (uintptr_t)(wp * 64 * B) + 128 > ahi) --wp;
                 int64_t wq = ((n - s0) / B) / 64;  // full phase waves whose lines stay in the allocation
                 while (wq > 0 && addr + (uintptr_t)s0 - a1 + (uintptr_t)(wq * 64 * B) + 128 > ahi) --wq;
                 const int gph = ++c->gen;
+                const int pset = 1 - c->ph_set;  // the phase part's buffer set (HipBackend::phase_hint)
                 uint32_t nseg = 0;
                 for (int64_t v = 0; v < wp; ++v)
                     sg[nseg++] = rsh::K1Seg{d_src - a0 + v * 64 * B, c->src_weak.as<int32_t>() + v * 64,
                                             c->src_strong.as<uint8_t>() + v * 64 * dl, c->abort_word, gen, a0};
                 for (int64_t v = 0; v < wq; ++v)
-                    sg[nseg++] = rsh::K1Seg{d_src + s0 - a1 + v * 64 * B, c->ph_weak.as<int32_t>() + v * 64,
-                                            c->ph_strong.as<uint8_t>() + v * 64 * dl,
+                    sg[nseg++] = rsh::K1Seg{d_src + s0 - a1 + v * 64 * B, c->ph_weak[pset].as<int32_t>() + v * 64,
+                                            c->ph_strong[pset].as<uint8_t>() + v * 64 * dl,
                                             c->abort_word + rsh_ctx::kPhaseWord, gph, a1};
                 auto* tl = reinterpret_cast<rsh::K1Tail*>(sg + nseg);
                 uint32_t ntail = 0;
@@ -849,7 +865,8 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                     tl[ntail++] = rsh::K1Tail{d_src, n, c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(),
                                               (uint32_t)k};
                 for (int64_t k = wq * 64; k < Q; ++k)
-                    tl[ntail++] = rsh::K1Tail{d_src + s0, n - s0, c->ph_weak.as<int32_t>(), c->ph_strong.as<uint8_t>(),
+                    tl[ntail++] = rsh::K1Tail{d_src + s0, n - s0, c->ph_weak[pset].as<int32_t>(),
+                                              c->ph_strong[pset].as<uint8_t>(),
                                               (uint32_t)k};
                 // full-length tails first (gathered into coalesced waves), the short last window after them
                 const uint32_t nfull = (uint32_t)(std::stable_partition(tl, tl + ntail, [&](const rsh::K1Tail& t) {
@@ -861,15 +878,16 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                     const int64_t snf = std::min<int64_t>(P, C);
                     RSH_HIP(hipMemcpyAsync(c->segs.p, c->h_segs.p, bytes, hipMemcpyHostToDevice, c->aux));
                     RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
+                    RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_phase[pset], 0));
                     RSH_HIP(hipEventRecord(c->ev_k1a, c->aux));
-                    RSH_HIP(hipEventRecord(c->ev_pha, c->aux));
+                    RSH_HIP(hipEventRecord(c->ev_pha[pset], c->aux));
                     RSH_HIP(rsh::launch_block_sums_segments(c->segs.as<rsh::K1Seg>(), nseg,
                                                             reinterpret_cast<const rsh::K1Tail*>(
                                                                 c->segs.as<uint8_t>() + nseg * sizeof(rsh::K1Seg)),
                                                             ntail, nfull, (uint32_t)B, (uint32_t)dl, seed_word(seed),
                                                             c->aux));
                     RSH_HIP(hipEventRecord(c->ev_k1b, c->aux));
-                    RSH_HIP(hipEventRecord(c->ev_phb, c->aux));
+                    RSH_HIP(hipEventRecord(c->ev_phb[pset], c->aux));
                     RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak,
                                                     d_strong, (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(),
                                                     c->aux));
@@ -879,11 +897,14 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                     if (dl > 0)
                         RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)P * dl, hipMemcpyDeviceToHost, c->aux));
                     RSH_HIP(hipEventRecord(c->ev_spec, c->aux));
-                    RSH_HIP(hipMemcpyAsync(c->h_pw.p, c->ph_weak.p, (size_t)Q * 4, hipMemcpyDeviceToHost, c->aux));
+                    RSH_HIP(hipMemcpyAsync(c->h_pw[pset].p, c->ph_weak[pset].p, (size_t)Q * 4, hipMemcpyDeviceToHost,
+                                           c->aux));
                     if (dl > 0)
-                        RSH_HIP(hipMemcpyAsync(c->h_ps.p, c->ph_strong.p, (size_t)Q * dl, hipMemcpyDeviceToHost, c->aux));
-                    RSH_HIP(hipEventRecord(c->ev_phase, c->aux));
-                    be.phase_adopt(s0, Q, gph);
+                        RSH_HIP(hipMemcpyAsync(c->h_ps[pset].p, c->ph_strong[pset].p, (size_t)Q * dl,
+                                               hipMemcpyDeviceToHost, c->aux));
+                    RSH_HIP(hipEventRecord(c->ev_phase[pset], c->aux));
+                    c->ph_set = pset;
+                    be.phase_adopt(s0, Q, gph, pset);
                     res->stats.phase_guesses++;
                     spec_launched = seg_launched = true;
                     // The resolver's first question past the prefix chain: the first hit in [P B, P B + 9 B] (synced
@@ -1027,10 +1048,12 @@ int scan_tiled(rsh_ctx* c, const std::function<hipError_t(uint8_t*, int64_t, int
     RSH_HIP(c->h_as.ensure((size_t)na * dl + 1));
     RSH_HIP(c->h_fl.ensure((size_t)nf + 1));
     RSH_HIP(c->haw.ensure((size_t)na * 4));
-    RSH_HIP(c->ph_weak.ensure((size_t)na * 4));
-    RSH_HIP(c->ph_strong.ensure((size_t)na * dl + 1));
-    RSH_HIP(c->h_pw.ensure((size_t)na * 4));
-    RSH_HIP(c->h_ps.ensure((size_t)na * dl + 1));
+    for (int i = 0; i < 2; ++i) {
+        RSH_HIP(c->ph_weak[i].ensure((size_t)na * 4));
+        RSH_HIP(c->ph_strong[i].ensure((size_t)na * dl + 1));
+        RSH_HIP(c->h_pw[i].ensure((size_t)na * 4));
+        RSH_HIP(c->h_ps[i].ensure((size_t)na * dl + 1));
+    }
     RSH_HIP(hipEventRecord(c->ev_in, c->stream));
     RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, c->stream));
     RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, c->stream));
@@ -1131,13 +1154,17 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
         hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_tab, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_spec, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_phase, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_phase[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_phase[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_flags, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev_k1a) != hipSuccess || hipEventCreate(&c->ev_k1b) != hipSuccess ||
-        hipEventCreate(&c->ev_pha) != hipSuccess || hipEventCreate(&c->ev_phb) != hipSuccess ||
+        hipEventCreate(&c->ev_pha[0]) != hipSuccess || hipEventCreate(&c->ev_phb[0]) != hipSuccess ||
+        hipEventCreate(&c->ev_pha[1]) != hipSuccess || hipEventCreate(&c->ev_phb[1]) != hipSuccess ||
         hipExtMallocWithFlags(reinterpret_cast<void**>(&c->abort_word), 256, hipDeviceMallocUncached) != hipSuccess ||
-        hipMemset(c->abort_word, 0, 256) != hipSuccess) {  // generations start at 1
+        hipMemset(c->abort_word, 0, 256) != hipSuccess ||  // generations start at 1
+        // recorded once, so that a launch may always wait for its buffer set's previous launch
+        hipEventRecord(c->ev_phase[0], c->stream) != hipSuccess || hipEventRecord(c->ev_phase[1], c->stream) != hipSuccess) {
         delete c;
         return RSH_E_DEVICE;
     }

@@ -103,18 +103,22 @@ struct rsh_ctx {
     hipStream_t stream = nullptr;
     DevBuf data, weak, strong;                   // host-input staging
     DevBuf src_weak, src_strong, flags;          // aligned speculation over the source
-    DevBuf ph_weak, ph_strong;                   // phase-shifted speculation over [s0, n) (chains at kB + delta)
+    // phase-shifted speculation over [s0, n) (chains at kB + delta): two buffer sets used in turn, so that a
+    // launch never writes the sums (or their host copies) of the launch it replaces while that one drains
+    DevBuf ph_weak[2], ph_strong[2];
     DevBuf segs;                                 // segmented K1 descriptors (prefix + phase speculation)
     DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw, partials, bucket;
     hipStream_t aux = nullptr;                   // the aligned speculation
     hipStream_t phase = nullptr;                 // the phase-shifted speculation (beside a prefix speculation)
-    hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr, ev_phase = nullptr;
+    hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr;
+    hipEvent_t ev_phase[2] = {nullptr, nullptr};  // set i's last phase launch and its downloads are done
     hipEvent_t ev_prep = nullptr;   // the scan's table and sample work on the context stream (A/B ordering)
     hipEvent_t ev_flags = nullptr;  // batched speculation: its chain flags are on the host (before its sums)
     hipEvent_t ev_k1a = nullptr, ev_k1b = nullptr;  // timing: the aligned speculation's K1 (stats)
-    hipEvent_t ev_pha = nullptr, ev_phb = nullptr;  // timing: the phase-shifted speculation's K1 (stats)
+    hipEvent_t ev_pha[2] = {nullptr, nullptr}, ev_phb[2] = {nullptr, nullptr};  // timing: set i's phase K1 (stats)
+    int ph_set = 0;  // the buffer set of the latest phase launch
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
-    PinnedBuf h_pw, h_ps;  // the phase-shifted speculation's sums (host copies)
+    PinnedBuf h_pw[2], h_ps[2];  // the phase-shifted speculation's sums (host copies), per set
     PinnedBuf h_segs;      // staging of the segmented K1 descriptors
     PinnedBuf h_lead;      // T(kB) of the first aligned windows (the speculation launch decision)
     // resolver round trips: the small kernels read their inputs from and write their outputs to pinned
@@ -137,10 +141,11 @@ struct rsh_ctx {
     rsh::BatchState* batch = nullptr;  // buffers of the batched (multi-file) entry points, on first use
     ~rsh_ctx() {
         if (batch) rsh::destroy_batch_state(batch);
-        for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &ph_weak, &ph_strong, &slots, &dslots,
+        for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &ph_weak[0], &ph_strong[0],
+                          &ph_weak[1], &ph_strong[1], &slots, &dslots,
                           &dkeys, &pos, &out, &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket})
             b->release();
-        for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pw, &h_ps, &h_lead, &h_pos, &h_out, &h_iv,
+        for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pw[0], &h_ps[0], &h_pw[1], &h_ps[1], &h_lead, &h_pos, &h_out, &h_iv,
                              &h_tiles, &h_keys, &h_first, &h_win, &h_ptiles, &h_hit, &h_win0, &h_pend, &h_bucket, &h_files,
                              &h_stage})
             b->release();
@@ -148,13 +153,12 @@ struct rsh_ctx {
         if (ev_in) (void)hipEventDestroy(ev_in);
         if (ev_tab) (void)hipEventDestroy(ev_tab);
         if (ev_spec) (void)hipEventDestroy(ev_spec);
-        if (ev_phase) (void)hipEventDestroy(ev_phase);
+        for (hipEvent_t e : {ev_phase[0], ev_phase[1], ev_pha[0], ev_pha[1], ev_phb[0], ev_phb[1]})
+            if (e) (void)hipEventDestroy(e);
         if (ev_flags) (void)hipEventDestroy(ev_flags);
         if (ev_prep) (void)hipEventDestroy(ev_prep);
         if (ev_k1a) (void)hipEventDestroy(ev_k1a);
         if (ev_k1b) (void)hipEventDestroy(ev_k1b);
-        if (ev_pha) (void)hipEventDestroy(ev_pha);
-        if (ev_phb) (void)hipEventDestroy(ev_phb);
         if (aux) (void)hipStreamDestroy(aux);
         if (phase) (void)hipStreamDestroy(phase);
         if (stream) (void)hipStreamDestroy(stream);

@@ -12,6 +12,7 @@
 package com.github.java.rsync.internal.session;
 
 import java.nio.ByteBuffer;
+import java.util.concurrent.locks.ReentrantLock;
 
 final class NativeChecksum implements AutoCloseable {
     static final boolean ENABLED = Boolean.getBoolean("rsync.hip");
@@ -31,11 +32,20 @@ final class NativeChecksum implements AutoCloseable {
     private static final java.util.Set<NativeChecksum> LIVE = java.util.concurrent.ConcurrentHashMap.newKeySet();
     private static final ThreadLocal<NativeChecksum> PER_THREAD = new ThreadLocal<>();
 
+    // The hook destroys only contexts that no thread is using: a context whose owner is still inside a native
+    // call (System.exit or SIGINT during a transfer) is left to the process exit, which reclaims its device
+    // memory; destroying it under the running scan would free buffers and streams the scan still uses.
     static {
         if (ENABLED) {
             Runtime.getRuntime().addShutdownHook(new Thread(() -> {
                 for (NativeChecksum c : LIVE) {
-                    c.close();
+                    if (c.lock.tryLock()) {
+                        try {
+                            c.closeLocked();
+                        } finally {
+                            c.lock.unlock();
+                        }
+                    }
                 }
             }, "rsync-hip-close"));
         }
@@ -63,13 +73,25 @@ final class NativeChecksum implements AutoCloseable {
     }
 
     private long ctx;
+    // Held for every native call and by close(): a context is never destroyed under a running scan.  One
+    // thread uses a context, so the lock is uncontended except against close() and the shutdown hook.
+    private final ReentrantLock lock = new ReentrantLock();
 
     private NativeChecksum(int device) {
         ctx = ctxCreate(device);
     }
 
     @Override
-    public synchronized void close() {
+    public void close() {
+        lock.lock();
+        try {
+            closeLocked();
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    private void closeLocked() {
         if (ctx != 0) {
             ctxDestroy(ctx);
             ctx = 0;
@@ -77,9 +99,32 @@ final class NativeChecksum implements AutoCloseable {
         LIVE.remove(this);
     }
 
+    /** The live handle; the lock is held.  A closed context throws (the shim also rejects handle 0). */
+    private long handle() {
+        if (ctx == 0) {
+            throw new IllegalStateException("NativeChecksum context is closed");
+        }
+        return ctx;
+    }
+
     /** Generator.java:886-895: weak[i] and strong[i*dl .. i*dl+dl) for every chunk of the basis. */
     void blockSums(ByteBuffer basis, long size, Checksum.Header h, byte[] seed, int[] weak, byte[] strong) {
-        blockSums(ctx, basis, size, toArray(h), seed, weak, strong);
+        lock.lock();
+        try {
+            blockSums(handle(), basis, size, toArray(h), seed, weak, strong);
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    /** As blockSums for a basis of any size held in several direct buffers (FileView.readPieces()). */
+    void blockSums(ByteBuffer[] basis, long size, Checksum.Header h, byte[] seed, int[] weak, byte[] strong) {
+        lock.lock();
+        try {
+            blockSumsBuffers(handle(), basis, size, toArray(h), seed, weak, strong);
+        } finally {
+            lock.unlock();
+        }
     }
 
     /**
@@ -88,18 +133,44 @@ final class NativeChecksum implements AutoCloseable {
      */
     long[] matchScan(ByteBuffer source, long size, Checksum.Header h, int[] weak, byte[] strong, byte[] seed,
             byte[] fileMd5, long[] sizes) {
-        return matchScan(ctx, source, size, toArray(h), weak, strong, seed, fileMd5, sizes);
+        lock.lock();
+        try {
+            return matchScan(handle(), source, size, toArray(h), weak, strong, seed, fileMd5, sizes);
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    /** As matchScan for a source of any size held in several direct buffers (FileView.readPieces()). */
+    long[] matchScan(ByteBuffer[] source, long size, Checksum.Header h, int[] weak, byte[] strong, byte[] seed,
+            byte[] fileMd5, long[] sizes) {
+        lock.lock();
+        try {
+            return matchScanBuffers(handle(), source, size, toArray(h), weak, strong, seed, fileMd5, sizes);
+        } finally {
+            lock.unlock();
+        }
     }
 
     /** As blockSums, reading the file natively (FileView semantics); true = read error (FileViewException). */
     boolean blockSumsFile(String path, long size, Checksum.Header h, byte[] seed, int[] weak, byte[] strong) {
-        return blockSumsFile(ctx, path, size, toArray(h), seed, weak, strong);
+        lock.lock();
+        try {
+            return blockSumsFile(handle(), path, size, toArray(h), seed, weak, strong);
+        } finally {
+            lock.unlock();
+        }
     }
 
     /** As matchScan, reading the file natively; sizes = {sizeLiteral, sizeMatch, readError}. */
     long[] matchScanFile(String path, long size, Checksum.Header h, int[] weak, byte[] strong, byte[] seed,
             byte[] fileMd5, long[] sizes) {
-        return matchScanFile(ctx, path, size, toArray(h), weak, strong, seed, fileMd5, sizes);
+        lock.lock();
+        try {
+            return matchScanFile(handle(), path, size, toArray(h), weak, strong, seed, fileMd5, sizes);
+        } finally {
+            lock.unlock();
+        }
     }
 
     /**
@@ -108,8 +179,13 @@ final class NativeChecksum implements AutoCloseable {
      */
     boolean receiverCombine(ByteBuffer tokens, long tokensLen, Checksum.Header h, ByteBuffer replica, long replicaLen,
             boolean deferWrite, ByteBuffer target, long targetCap, long[] result, byte[] md5) {
-        return receiverCombine(ctx, tokens, tokensLen, toArray(h), replica, replicaLen, deferWrite, target, targetCap,
-                result, md5);
+        lock.lock();
+        try {
+            return receiverCombine(handle(), tokens, tokensLen, toArray(h), replica, replicaLen, deferWrite, target,
+                    targetCap, result, md5);
+        } finally {
+            lock.unlock();
+        }
     }
 
     private static int[] toArray(Checksum.Header h) {
@@ -129,6 +205,12 @@ final class NativeChecksum implements AutoCloseable {
 
     static native long[] matchScan(long ctx, ByteBuffer src, long n, int[] header, int[] weak, byte[] strong,
             byte[] seed, byte[] fileMd5Out, long[] sizesOut);
+
+    static native void blockSumsBuffers(long ctx, ByteBuffer[] data, long n, int[] header, byte[] seed,
+            int[] weakOut, byte[] strongOut);
+
+    static native long[] matchScanBuffers(long ctx, ByteBuffer[] src, long n, int[] header, int[] weak,
+            byte[] strong, byte[] seed, byte[] fileMd5Out, long[] sizesOut);
 
     static native boolean blockSumsFile(long ctx, String path, long size, int[] header, byte[] seed, int[] weakOut,
             byte[] strongOut);

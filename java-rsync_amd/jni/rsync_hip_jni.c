@@ -14,11 +14,17 @@
  *                     chose to; the library itself never falls back)
  *   RSH_E_NOTFOUND -> ...internal.io.FileViewNotFound                (FileView.java:74-75)
  *   RSH_E_OPEN     -> ...internal.io.FileViewOpenFailed              (FileView.java:76-78)
- * blockSums / matchScan take the file bytes from Java (FileView semantics incl. zero-fill after read
- * errors stay in Java, FileView.java:209-271); blockSumsFile / matchScanFile read the file natively with
- * the same semantics and report a read error as a flag (the FileViewException the Java code would get
- * at close()).  The Sender replays the returned events through its own sendDataFrom/putInt so channel
- * framing is untouched (Sender.java:794-809).
+ * A closed context (handle 0) is an IllegalStateException; a byte count larger than the direct buffer it
+ * names is an IllegalArgumentException -- the library is never handed memory the buffer does not own.
+ *
+ * Three ways to hand over the file bytes:
+ *   blockSums / matchScan              one direct ByteBuffer (files < 2 GiB: a buffer's capacity is an int);
+ *   blockSumsBuffers / matchScanBuffers  an array of direct ByteBuffers, the file being their concatenation
+ *                                      (any size; FileView streams any file, FileView.java:235-278);
+ *   blockSumsFile / matchScanFile      a path: the library reads the file with FileView's semantics and
+ *                                      reports a read error as a flag (the FileViewException of close()).
+ * The Sender replays the returned events through its own sendDataFrom/putInt so channel framing is
+ * untouched (Sender.java:794-809); INTEGRATION.md shows the replay for each form.
  *
  * Build (needs a JDK): make -C java-rsync_amd jni JAVA_HOME=/path/to/jdk
  */
@@ -28,6 +34,12 @@
 #include <string.h>
 
 #include "rsync_hip.h"
+
+static void throw_class(JNIEnv* env, const char* cls, const char* msg) {
+    jclass c = (*env)->FindClass(env, cls);
+    if (!c) return; /* NoClassDefFoundError already pending */
+    (*env)->ThrowNew(env, c, msg);
+}
 
 static void throw_status(JNIEnv* env, int rc) {
     const char* cls;
@@ -40,9 +52,71 @@ static void throw_status(JNIEnv* env, int rc) {
         case RSH_E_OPEN: cls = "com/github/java/rsync/internal/io/FileViewOpenFailed"; break;
         default: cls = "java/lang/IllegalStateException"; break;
     }
-    jclass c = (*env)->FindClass(env, cls);
-    if (!c) return; /* NoClassDefFoundError already pending */
-    (*env)->ThrowNew(env, c, rsh_strerror(rc));
+    throw_class(env, cls, rsh_strerror(rc));
+}
+
+/* The context of a live NativeChecksum; throws IllegalStateException for a closed one (handle 0). */
+static rsh_ctx* ctx_of(JNIEnv* env, jlong ctx) {
+    if (ctx == 0) throw_class(env, "java/lang/IllegalStateException", "NativeChecksum context is closed");
+    return (rsh_ctx*)(intptr_t)ctx;
+}
+
+/* The address of a direct buffer that holds at least `need` bytes; NULL (IllegalArgumentException thrown)
+ * for a heap buffer, a negative count or a count past the buffer's capacity. */
+static const uint8_t* direct_bytes(JNIEnv* env, jobject buf, jlong need) {
+    if (!buf || need < 0) {
+        throw_status(env, RSH_E_INVAL);
+        return NULL;
+    }
+    const uint8_t* p = (const uint8_t*)(*env)->GetDirectBufferAddress(env, buf);
+    const jlong cap = (*env)->GetDirectBufferCapacity(env, buf);
+    if (!p || cap < need) {
+        throw_class(env, "java/lang/IllegalArgumentException",
+                    p ? "byte count exceeds the direct buffer's capacity" : "not a direct ByteBuffer");
+        return NULL;
+    }
+    return p;
+}
+
+/* The pieces of a file handed over as ByteBuffer[]: every buffer's whole capacity in order, the last one
+ * cut at n.  Returns the piece count (0 for n == 0), or -1 with IllegalArgumentException thrown when a
+ * buffer is not direct or the buffers hold fewer than n bytes.  *out is malloc'd (free it). */
+static jint pieces_from(JNIEnv* env, jobjectArray bufs, jlong n, rsh_piece** out) {
+    *out = NULL;
+    const jsize nb = bufs ? (*env)->GetArrayLength(env, bufs) : 0;
+    if (n < 0 || (n > 0 && nb == 0)) {
+        throw_status(env, RSH_E_INVAL);
+        return -1;
+    }
+    rsh_piece* p = (rsh_piece*)malloc(sizeof(rsh_piece) * (size_t)(nb > 0 ? nb : 1));
+    if (!p) {
+        throw_status(env, RSH_E_NOMEM);
+        return -1;
+    }
+    jlong left = n;
+    jint k = 0;
+    for (jsize i = 0; i < nb && left > 0; ++i) {
+        jobject b = (*env)->GetObjectArrayElement(env, bufs, i);
+        const uint8_t* a = b ? (const uint8_t*)(*env)->GetDirectBufferAddress(env, b) : NULL;
+        const jlong cap = b ? (*env)->GetDirectBufferCapacity(env, b) : -1;
+        if (b) (*env)->DeleteLocalRef(env, b);
+        if (!a || cap < 0) {
+            free(p);
+            throw_class(env, "java/lang/IllegalArgumentException", "piece is not a direct ByteBuffer");
+            return -1;
+        }
+        p[k].data = a;
+        p[k].len = cap < left ? cap : left;
+        left -= p[k].len;
+        ++k;
+    }
+    if (left > 0) {
+        free(p);
+        throw_class(env, "java/lang/IllegalArgumentException", "the buffers hold fewer bytes than the file size");
+        return -1;
+    }
+    *out = p;
+    return k;
 }
 
 static int header_from(JNIEnv* env, jintArray hdr4, rsh_header* h) {
@@ -53,6 +127,117 @@ static int header_from(JNIEnv* env, jintArray hdr4, rsh_header* h) {
     h->block_length = v[1];
     h->digest_length = v[2];
     h->remainder = v[3];
+    return RSH_OK;
+}
+
+static int seed_from(JNIEnv* env, jbyteArray seed, jbyte s4[4]) {
+    if (!seed || (*env)->GetArrayLength(env, seed) != 4) return RSH_E_INVAL;
+    (*env)->GetByteArrayRegion(env, seed, 0, 4, s4);
+    return RSH_OK;
+}
+
+/* Generator outputs: weakOut[chunkCount], strongOut[chunkCount * digestLength]. */
+static int sums_out_ok(JNIEnv* env, const rsh_header* h, jintArray weakOut, jbyteArray strongOut) {
+    if (!weakOut || !strongOut || h->chunk_count < 0 || h->digest_length < 0) return RSH_E_INVAL;
+    if ((*env)->GetArrayLength(env, weakOut) < h->chunk_count ||
+        (*env)->GetArrayLength(env, strongOut) < (jlong)h->chunk_count * h->digest_length)
+        return RSH_E_INVAL;
+    return RSH_OK;
+}
+
+typedef int (*sums_fn)(rsh_ctx* c, const void* src, const rsh_header* h, const uint8_t* seed, int32_t* w,
+                       uint8_t* st, void* arg);
+
+/* Runs a Generator pass into native buffers (the call can run for seconds: no JNI critical region, which
+ * would stall the GC) and copies the sums into the Java arrays. */
+static void run_sums(JNIEnv* env, rsh_ctx* c, const void* src, const rsh_header* h, const jbyte* s4, jintArray weakOut,
+                     jbyteArray strongOut, sums_fn fn, void* arg) {
+    const size_t C = (size_t)h->chunk_count, dl = (size_t)h->digest_length;
+    int32_t* w = (int32_t*)malloc(C * 4 + 4);
+    uint8_t* st = (uint8_t*)malloc(C * dl + 1);
+    int rc = (w && st) ? fn(c, src, h, (const uint8_t*)s4, w, st, arg) : RSH_E_NOMEM;
+    if (rc == RSH_OK) {
+        (*env)->SetIntArrayRegion(env, weakOut, 0, (jsize)C, (const jint*)w);
+        (*env)->SetByteArrayRegion(env, strongOut, 0, (jsize)(C * dl), (const jbyte*)st);
+    }
+    free(st);
+    free(w);
+    if (rc != RSH_OK) throw_status(env, rc);
+}
+
+/* Events as a flat long[] of 4-tuples {kind, offset, length, index | (count << 32)}. */
+static jlongArray events_to_java(JNIEnv* env, const rsh_event* ev, int64_t n_ev) {
+    jlongArray out = (*env)->NewLongArray(env, (jsize)(4 * n_ev));
+    if (!out) return NULL;
+    jlong* o = (*env)->GetLongArrayElements(env, out, NULL);
+    if (!o) return NULL;
+    for (int64_t i = 0; i < n_ev; ++i) {
+        o[4 * i + 0] = ev[i].kind;
+        o[4 * i + 1] = ev[i].offset;
+        o[4 * i + 2] = ev[i].length;
+        o[4 * i + 3] = (jlong)(uint32_t)ev[i].index | ((jlong)ev[i].count << 32);
+    }
+    (*env)->ReleaseLongArrayElements(env, out, o, 0);
+    return out;
+}
+
+typedef int (*scan_fn)(rsh_ctx* c, const void* src, const rsh_header* h, const int32_t* w, const uint8_t* st,
+                       const uint8_t* seed, rsh_event* ev, int64_t cap, int64_t* n_ev, uint8_t md5[16], int64_t* lit,
+                       int64_t* mat, void* arg);
+
+/* Runs a Sender pass: copies the (small) received table out of the Java arrays (no critical region across
+ * a long scan), sizes the event buffer, fetches the events again on RSH_E_NOSPACE (the context kept them:
+ * not a rescan).  Returns the events, or NULL with an exception pending. */
+static jlongArray run_scan(JNIEnv* env, rsh_ctx* c, const void* src, jlong n, const rsh_header* h, jintArray weak,
+                           jbyteArray strong, const jbyte* s4, uint8_t md5[16], int64_t* lit, int64_t* mat, scan_fn fn,
+                           void* arg) {
+    /* one literal per flush interval plus a literal and a match run per chunk */
+    int64_t cap = (n / (10 * (int64_t)(h->block_length > 0 ? h->block_length : 8192))) +
+                  2 * (int64_t)(h->chunk_count > 0 ? h->chunk_count : 0) + 64;
+    int64_t n_ev = 0;
+    const jsize nw = weak ? (*env)->GetArrayLength(env, weak) : 0;
+    const jsize ns = strong ? (*env)->GetArrayLength(env, strong) : 0;
+    int rc = RSH_OK;
+    if (h->chunk_count > 0 && (nw < h->chunk_count || (jlong)ns < (jlong)h->chunk_count * h->digest_length))
+        rc = RSH_E_INVAL; /* received table shorter than its header says */
+    rsh_event* ev = (rsh_event*)malloc((size_t)cap * sizeof(rsh_event));
+    int32_t* w = (int32_t*)malloc((size_t)nw * 4 + 4);
+    uint8_t* st = (uint8_t*)malloc((size_t)ns + 1);
+    if (rc == RSH_OK && (!ev || !w || !st)) rc = RSH_E_NOMEM;
+    if (rc == RSH_OK) {
+        if (nw) (*env)->GetIntArrayRegion(env, weak, 0, nw, (jint*)w);
+        if (ns) (*env)->GetByteArrayRegion(env, strong, 0, ns, (jbyte*)st);
+        rc = fn(c, src, h, nw ? w : NULL, ns ? st : NULL, (const uint8_t*)s4, ev, cap, &n_ev, md5, lit, mat, arg);
+        if (rc == RSH_E_NOSPACE) {
+            rsh_event* grown = (rsh_event*)realloc(ev, (size_t)n_ev * sizeof(rsh_event));
+            if (!grown) rc = RSH_E_NOMEM;
+            else {
+                ev = grown;
+                rc = rsh_fetch_events(c, ev, n_ev, &n_ev);
+            }
+        }
+    }
+    free(st);
+    free(w);
+    jlongArray out = NULL;
+    if (rc == RSH_OK) out = events_to_java(env, ev, n_ev);
+    else throw_status(env, rc);
+    free(ev);
+    return out;
+}
+
+static void sizes_out(JNIEnv* env, jlongArray sizesOut, jbyteArray fileMd5Out, const uint8_t md5[16], jlong lit,
+                      jlong mat, int with_error, jlong read_error) {
+    jlong sizes[3] = {lit, mat, read_error};
+    (*env)->SetByteArrayRegion(env, fileMd5Out, 0, 16, (const jbyte*)md5);
+    (*env)->SetLongArrayRegion(env, sizesOut, 0, with_error ? 3 : 2, sizes);
+}
+
+static int scan_args_ok(JNIEnv* env, jintArray hdr4, rsh_header* h, jbyteArray seed, jbyte s4[4],
+                        jbyteArray fileMd5Out, jlongArray sizesOut, jsize nsizes) {
+    if (header_from(env, hdr4, h) != RSH_OK || seed_from(env, seed, s4) != RSH_OK || !fileMd5Out || !sizesOut ||
+        (*env)->GetArrayLength(env, fileMd5Out) != 16 || (*env)->GetArrayLength(env, sizesOut) < nsizes)
+        return RSH_E_INVAL;
     return RSH_OK;
 }
 
@@ -72,7 +257,7 @@ JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksu
                                                                                            jlong ctx) {
     (void)env;
     (void)cls;
-    rsh_ctx_destroy((rsh_ctx*)(intptr_t)ctx);
+    rsh_ctx_destroy((rsh_ctx*)(intptr_t)ctx); /* NULL is a no-op */
 }
 
 /* Generator.getBlockLengthFor / getDigestLength (Generator.java:198-212, :873). */
@@ -90,223 +275,187 @@ JNIEXPORT jint JNICALL Java_com_github_java_rsync_internal_session_NativeChecksu
     return rsh_digest_length_for(size, blen, min_dl);
 }
 
-/*
- * Generator.sendItemizeAndChecksums hot loop (Generator.java:886-895).
- * data: a direct ByteBuffer holding the whole basis file (n bytes).  weakOut[chunkCount],
- * strongOut[chunkCount * digestLength] are filled; Java then writes header + sums to the channel.
- */
+/* ---- Generator.sendItemizeAndChecksums hot loop (Generator.java:886-895) ---- */
+
+static int sums_buffer(rsh_ctx* c, const void* src, const rsh_header* h, const uint8_t* seed, int32_t* w, uint8_t* st,
+                       void* arg) {
+    return rsh_block_sums(c, (const uint8_t*)src, *(const jlong*)arg, h, seed, w, st);
+}
+
+/* data: a direct ByteBuffer holding the whole basis file (n <= its capacity). */
 JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_blockSums(
     JNIEnv* env, jclass cls, jlong ctx, jobject data, jlong n, jintArray hdr4, jbyteArray seed, jintArray weakOut,
     jbyteArray strongOut) {
     (void)cls;
+    rsh_ctx* c = ctx_of(env, ctx);
+    if (!c) return;
     rsh_header h;
-    int rc = header_from(env, hdr4, &h);
-    if (rc != RSH_OK) {
-        throw_status(env, rc);
-        return;
-    }
-    const uint8_t* p = (const uint8_t*)(*env)->GetDirectBufferAddress(env, data);
-    if ((!p && n > 0) || (*env)->GetArrayLength(env, seed) != 4 ||
-        (*env)->GetArrayLength(env, weakOut) < h.chunk_count ||
-        (*env)->GetArrayLength(env, strongOut) < (jlong)h.chunk_count * h.digest_length) {
+    jbyte s4[4];
+    if (header_from(env, hdr4, &h) != RSH_OK || seed_from(env, seed, s4) != RSH_OK ||
+        sums_out_ok(env, &h, weakOut, strongOut) != RSH_OK) {
         throw_status(env, RSH_E_INVAL);
         return;
     }
-    jbyte s4[4];
-    (*env)->GetByteArrayRegion(env, seed, 0, 4, s4);
-    /* the call can run for seconds: native buffers, not JNI critical regions (which would stall GC) */
-    const size_t C = (size_t)(h.chunk_count > 0 ? h.chunk_count : 0), dl = (size_t)(h.digest_length > 0 ? h.digest_length : 0);
-    int32_t* w = (int32_t*)malloc(C * 4 + 4);
-    uint8_t* st = (uint8_t*)malloc(C * dl + 1);
-    rc = (w && st) ? rsh_block_sums((rsh_ctx*)(intptr_t)ctx, p, n, &h, (const uint8_t*)s4, w, st) : RSH_E_NOMEM;
-    if (rc == RSH_OK) {
-        (*env)->SetIntArrayRegion(env, weakOut, 0, (jsize)C, (const jint*)w);
-        (*env)->SetByteArrayRegion(env, strongOut, 0, (jsize)(C * dl), (const jbyte*)st);
-    }
-    free(st);
-    free(w);
-    if (rc != RSH_OK) throw_status(env, rc);
+    const uint8_t* p = direct_bytes(env, data, n);
+    if (!p) return;
+    run_sums(env, c, p, &h, s4, weakOut, strongOut, sums_buffer, &n);
 }
 
-/*
- * Sender.sendMatchesAndData / skipMatchSendData (Sender.java:1235-1327, 1386-1399).
- * Returns the events as a flat long[] of 4-tuples {kind, offset, length, index | (count << 32)};
- * fileMd5Out[16] receives the whole-file digest and sizesOut[2] = {sizeLiteral, sizeMatch}.
- */
+static int sums_pieces(rsh_ctx* c, const void* src, const rsh_header* h, const uint8_t* seed, int32_t* w,
+                       uint8_t* st, void* arg) {
+    return rsh_block_sums_pieces(c, (const rsh_piece*)src, *(const jint*)arg, h, seed, w, st);
+}
+
+/* As blockSums over the concatenation of direct ByteBuffers (each full to its capacity but the last). */
+JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_blockSumsBuffers(
+    JNIEnv* env, jclass cls, jlong ctx, jobjectArray data, jlong n, jintArray hdr4, jbyteArray seed, jintArray weakOut,
+    jbyteArray strongOut) {
+    (void)cls;
+    rsh_ctx* c = ctx_of(env, ctx);
+    if (!c) return;
+    rsh_header h;
+    jbyte s4[4];
+    if (header_from(env, hdr4, &h) != RSH_OK || seed_from(env, seed, s4) != RSH_OK ||
+        sums_out_ok(env, &h, weakOut, strongOut) != RSH_OK) {
+        throw_status(env, RSH_E_INVAL);
+        return;
+    }
+    rsh_piece* pieces;
+    jint np = pieces_from(env, data, n, &pieces);
+    if (np < 0) return;
+    run_sums(env, c, pieces, &h, s4, weakOut, strongOut, sums_pieces, &np);
+    free(pieces);
+}
+
+/* ---- Sender.sendMatchesAndData / skipMatchSendData (Sender.java:1235-1327, 1386-1399) ----
+ * Return the events as {kind, offset, length, index | (count << 32)} quadruples; fileMd5Out[16] receives
+ * the whole-file digest and sizesOut = {sizeLiteral, sizeMatch[, readError]}. */
+
+static int scan_buffer(rsh_ctx* c, const void* src, const rsh_header* h, const int32_t* w, const uint8_t* st,
+                       const uint8_t* seed, rsh_event* ev, int64_t cap, int64_t* n_ev, uint8_t md5[16], int64_t* lit,
+                       int64_t* mat, void* arg) {
+    return rsh_match_scan(c, (const uint8_t*)src, *(const jlong*)arg, h, w, st, seed, ev, cap, n_ev, md5, lit, mat,
+                          NULL);
+}
+
 JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_matchScan(
     JNIEnv* env, jclass cls, jlong ctx, jobject src, jlong n, jintArray hdr4, jintArray weak, jbyteArray strong,
     jbyteArray seed, jbyteArray fileMd5Out, jlongArray sizesOut) {
     (void)cls;
+    rsh_ctx* c = ctx_of(env, ctx);
+    if (!c) return NULL;
     rsh_header h;
-    int rc = header_from(env, hdr4, &h);
-    if (rc != RSH_OK) {
-        throw_status(env, rc);
-        return NULL;
-    }
-    const uint8_t* p = (const uint8_t*)(*env)->GetDirectBufferAddress(env, src);
-    if ((!p && n > 0) || (*env)->GetArrayLength(env, seed) != 4 || (*env)->GetArrayLength(env, fileMd5Out) != 16 ||
-        (*env)->GetArrayLength(env, sizesOut) < 2) {
+    jbyte s4[4];
+    if (scan_args_ok(env, hdr4, &h, seed, s4, fileMd5Out, sizesOut, 2) != RSH_OK) {
         throw_status(env, RSH_E_INVAL);
         return NULL;
     }
-    jbyte s4[4];
-    (*env)->GetByteArrayRegion(env, seed, 0, 4, s4);
-    /* one literal per flush interval plus a literal and a match run per chunk; a short buffer is not
-       a rescan: the context keeps the events for rsh_fetch_events */
-    int64_t cap = (n / (10 * (int64_t)(h.block_length > 0 ? h.block_length : 8192))) + 2 * (int64_t)h.chunk_count + 64;
-    int64_t n_ev = 0, lit = 0, mat = 0;
-    rsh_event* ev = (rsh_event*)malloc((size_t)cap * sizeof(rsh_event));
+    const uint8_t* p = direct_bytes(env, src, n);
+    if (!p) return NULL;
     uint8_t md5[16];
-    if (!ev) {
-        rc = RSH_E_NOMEM;
-    } else {
-        /* copies of the (small) received table: no JNI critical region across a long scan */
-        const jsize nw = weak ? (*env)->GetArrayLength(env, weak) : 0;
-        const jsize ns = strong ? (*env)->GetArrayLength(env, strong) : 0;
-        int32_t* w = (int32_t*)malloc((size_t)nw * 4 + 4);
-        uint8_t* st = (uint8_t*)malloc((size_t)ns + 1);
-        if (!w || !st) {
-            rc = RSH_E_NOMEM;
-        } else if (h.chunk_count > 0 && (nw < h.chunk_count || (jlong)ns < (jlong)h.chunk_count * h.digest_length)) {
-            rc = RSH_E_INVAL; /* received table shorter than its header says */
-        } else {
-            if (nw) (*env)->GetIntArrayRegion(env, weak, 0, nw, (jint*)w);
-            if (ns) (*env)->GetByteArrayRegion(env, strong, 0, ns, (jbyte*)st);
-            rc = rsh_match_scan((rsh_ctx*)(intptr_t)ctx, p, n, &h, nw ? w : NULL, ns ? st : NULL, (const uint8_t*)s4,
-                                ev, cap, &n_ev, md5, &lit, &mat, NULL);
-        }
-        free(st);
-        free(w);
-        if (rc == RSH_E_NOSPACE) {
-            rsh_event* grown = (rsh_event*)realloc(ev, (size_t)n_ev * sizeof(rsh_event));
-            if (!grown) rc = RSH_E_NOMEM;
-            else {
-                ev = grown;
-                rc = rsh_fetch_events((rsh_ctx*)(intptr_t)ctx, ev, n_ev, &n_ev);
-            }
-        }
-    }
-    if (rc != RSH_OK) {
-        free(ev);
-        throw_status(env, rc);
+    int64_t lit = 0, mat = 0;
+    jlongArray out = run_scan(env, c, p, n, &h, weak, strong, s4, md5, &lit, &mat, scan_buffer, &n);
+    if (out) sizes_out(env, sizesOut, fileMd5Out, md5, lit, mat, 0, 0);
+    return out;
+}
+
+static int scan_pieces(rsh_ctx* c, const void* src, const rsh_header* h, const int32_t* w, const uint8_t* st,
+                       const uint8_t* seed, rsh_event* ev, int64_t cap, int64_t* n_ev, uint8_t md5[16], int64_t* lit,
+                       int64_t* mat, void* arg) {
+    return rsh_match_scan_pieces(c, (const rsh_piece*)src, *(const jint*)arg, h, w, st, seed, ev, cap, n_ev, md5, lit,
+                                 mat, NULL);
+}
+
+/* As matchScan over the concatenation of direct ByteBuffers: the source of any size.  The caller replays a
+ * LIT(offset, length) event from the same buffers (sendDataFrom over ByteBuffer[]). */
+JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_matchScanBuffers(
+    JNIEnv* env, jclass cls, jlong ctx, jobjectArray src, jlong n, jintArray hdr4, jintArray weak, jbyteArray strong,
+    jbyteArray seed, jbyteArray fileMd5Out, jlongArray sizesOut) {
+    (void)cls;
+    rsh_ctx* c = ctx_of(env, ctx);
+    if (!c) return NULL;
+    rsh_header h;
+    jbyte s4[4];
+    if (scan_args_ok(env, hdr4, &h, seed, s4, fileMd5Out, sizesOut, 2) != RSH_OK) {
+        throw_status(env, RSH_E_INVAL);
         return NULL;
     }
-    jlongArray out = (*env)->NewLongArray(env, (jsize)(4 * n_ev));
-    if (out) {
-        jlong* o = (*env)->GetLongArrayElements(env, out, NULL);
-        for (int64_t i = 0; i < n_ev; ++i) {
-            o[4 * i + 0] = ev[i].kind;
-            o[4 * i + 1] = ev[i].offset;
-            o[4 * i + 2] = ev[i].length;
-            o[4 * i + 3] = (jlong)(uint32_t)ev[i].index | ((jlong)ev[i].count << 32);
-        }
-        (*env)->ReleaseLongArrayElements(env, out, o, 0);
-        (*env)->SetByteArrayRegion(env, fileMd5Out, 0, 16, (const jbyte*)md5);
-        jlong sizes[2] = {lit, mat};
-        (*env)->SetLongArrayRegion(env, sizesOut, 0, 2, sizes);
-    }
-    free(ev);
+    rsh_piece* pieces;
+    jint np = pieces_from(env, src, n, &pieces);
+    if (np < 0) return NULL;
+    uint8_t md5[16];
+    int64_t lit = 0, mat = 0;
+    jlongArray out = run_scan(env, c, pieces, n, &h, weak, strong, s4, md5, &lit, &mat, scan_pieces, &np);
+    free(pieces);
+    if (out) sizes_out(env, sizesOut, fileMd5Out, md5, lit, mat, 0, 0);
     return out;
 }
 
 /* ---- the same passes reading the file natively (rsh_*_file: FileView.java:51-80,187-278 semantics) ---- */
+
+typedef struct {
+    jlong size;
+    int32_t read_error;
+} file_arg;
+
+static int sums_file(rsh_ctx* c, const void* src, const rsh_header* h, const uint8_t* seed, int32_t* w, uint8_t* st,
+                     void* arg) {
+    file_arg* a = (file_arg*)arg;
+    return rsh_block_sums_file(c, (const char*)src, a->size, h, seed, w, st, &a->read_error);
+}
 
 /* Returns true when the file could not be read to `size` (zero-filled from there: FileViewException). */
 JNIEXPORT jboolean JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_blockSumsFile(
     JNIEnv* env, jclass cls, jlong ctx, jstring path, jlong size, jintArray hdr4, jbyteArray seed, jintArray weakOut,
     jbyteArray strongOut) {
     (void)cls;
+    rsh_ctx* c = ctx_of(env, ctx);
+    if (!c) return JNI_FALSE;
     rsh_header h;
-    int rc = header_from(env, hdr4, &h);
-    if (rc != RSH_OK || !path || (*env)->GetArrayLength(env, seed) != 4 ||
-        (*env)->GetArrayLength(env, weakOut) < h.chunk_count ||
-        (*env)->GetArrayLength(env, strongOut) < (jlong)h.chunk_count * h.digest_length) {
-        throw_status(env, rc != RSH_OK ? rc : RSH_E_INVAL);
+    jbyte s4[4];
+    if (!path || header_from(env, hdr4, &h) != RSH_OK || seed_from(env, seed, s4) != RSH_OK ||
+        sums_out_ok(env, &h, weakOut, strongOut) != RSH_OK) {
+        throw_status(env, RSH_E_INVAL);
         return JNI_FALSE;
     }
-    jbyte s4[4];
-    (*env)->GetByteArrayRegion(env, seed, 0, 4, s4);
-    const size_t C = (size_t)(h.chunk_count > 0 ? h.chunk_count : 0), dl = (size_t)(h.digest_length > 0 ? h.digest_length : 0);
-    int32_t* w = (int32_t*)malloc(C * 4 + 4);
-    uint8_t* st = (uint8_t*)malloc(C * dl + 1);
     const char* cpath = (*env)->GetStringUTFChars(env, path, NULL);
-    int32_t read_error = 0;
-    rc = (w && st && cpath) ? rsh_block_sums_file((rsh_ctx*)(intptr_t)ctx, cpath, size, &h, (const uint8_t*)s4, w, st,
-                                                  &read_error)
-                            : RSH_E_NOMEM;
-    if (cpath) (*env)->ReleaseStringUTFChars(env, path, cpath);
-    if (rc == RSH_OK) {
-        (*env)->SetIntArrayRegion(env, weakOut, 0, (jsize)C, (const jint*)w);
-        (*env)->SetByteArrayRegion(env, strongOut, 0, (jsize)(C * dl), (const jbyte*)st);
-    }
-    free(st);
-    free(w);
-    if (rc != RSH_OK) throw_status(env, rc);
-    return read_error ? JNI_TRUE : JNI_FALSE;
+    if (!cpath) return JNI_FALSE; /* OutOfMemoryError pending */
+    file_arg a = {size, 0};
+    run_sums(env, c, cpath, &h, s4, weakOut, strongOut, sums_file, &a);
+    (*env)->ReleaseStringUTFChars(env, path, cpath);
+    return a.read_error ? JNI_TRUE : JNI_FALSE;
 }
 
-/* As matchScan, reading the source natively; sizesOut[3] = {sizeLiteral, sizeMatch, readError}. */
+static int scan_file(rsh_ctx* c, const void* src, const rsh_header* h, const int32_t* w, const uint8_t* st,
+                     const uint8_t* seed, rsh_event* ev, int64_t cap, int64_t* n_ev, uint8_t md5[16], int64_t* lit,
+                     int64_t* mat, void* arg) {
+    file_arg* a = (file_arg*)arg;
+    return rsh_match_scan_file(c, (const char*)src, a->size, h, w, st, seed, ev, cap, n_ev, md5, lit, mat, NULL,
+                               &a->read_error);
+}
+
+/* As matchScan, reading the source natively; sizesOut[3] = {sizeLiteral, sizeMatch, readError}.  The caller
+ * replays a LIT(offset, length) event with positional reads of the same file. */
 JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_matchScanFile(
     JNIEnv* env, jclass cls, jlong ctx, jstring path, jlong size, jintArray hdr4, jintArray weak, jbyteArray strong,
     jbyteArray seed, jbyteArray fileMd5Out, jlongArray sizesOut) {
     (void)cls;
+    rsh_ctx* c = ctx_of(env, ctx);
+    if (!c) return NULL;
     rsh_header h;
-    int rc = header_from(env, hdr4, &h);
-    if (rc != RSH_OK || !path || (*env)->GetArrayLength(env, seed) != 4 ||
-        (*env)->GetArrayLength(env, fileMd5Out) != 16 || (*env)->GetArrayLength(env, sizesOut) < 3) {
-        throw_status(env, rc != RSH_OK ? rc : RSH_E_INVAL);
+    jbyte s4[4];
+    if (!path || scan_args_ok(env, hdr4, &h, seed, s4, fileMd5Out, sizesOut, 3) != RSH_OK) {
+        throw_status(env, RSH_E_INVAL);
         return NULL;
     }
-    jbyte s4[4];
-    (*env)->GetByteArrayRegion(env, seed, 0, 4, s4);
-    int64_t cap = (size / (10 * (int64_t)(h.block_length > 0 ? h.block_length : 8192))) + 2 * (int64_t)h.chunk_count + 64;
-    int64_t n_ev = 0, lit = 0, mat = 0;
-    int32_t read_error = 0;
-    rsh_event* ev = (rsh_event*)malloc((size_t)cap * sizeof(rsh_event));
-    const jsize nw = weak ? (*env)->GetArrayLength(env, weak) : 0;
-    const jsize ns = strong ? (*env)->GetArrayLength(env, strong) : 0;
-    int32_t* w = (int32_t*)malloc((size_t)nw * 4 + 4);
-    uint8_t* st = (uint8_t*)malloc((size_t)ns + 1);
     const char* cpath = (*env)->GetStringUTFChars(env, path, NULL);
+    if (!cpath) return NULL;
     uint8_t md5[16];
-    if (!ev || !w || !st || !cpath) {
-        rc = RSH_E_NOMEM;
-    } else if (h.chunk_count > 0 && (nw < h.chunk_count || (jlong)ns < (jlong)h.chunk_count * h.digest_length)) {
-        rc = RSH_E_INVAL;
-    } else {
-        if (nw) (*env)->GetIntArrayRegion(env, weak, 0, nw, (jint*)w);
-        if (ns) (*env)->GetByteArrayRegion(env, strong, 0, ns, (jbyte*)st);
-        rc = rsh_match_scan_file((rsh_ctx*)(intptr_t)ctx, cpath, size, &h, nw ? w : NULL, ns ? st : NULL,
-                                 (const uint8_t*)s4, ev, cap, &n_ev, md5, &lit, &mat, NULL, &read_error);
-        if (rc == RSH_E_NOSPACE) {
-            rsh_event* grown = (rsh_event*)realloc(ev, (size_t)n_ev * sizeof(rsh_event));
-            if (!grown) rc = RSH_E_NOMEM;
-            else {
-                ev = grown;
-                rc = rsh_fetch_events((rsh_ctx*)(intptr_t)ctx, ev, n_ev, &n_ev);
-            }
-        }
-    }
-    if (cpath) (*env)->ReleaseStringUTFChars(env, path, cpath);
-    free(st);
-    free(w);
-    jlongArray out = NULL;
-    if (rc == RSH_OK) out = (*env)->NewLongArray(env, (jsize)(4 * n_ev));
-    if (out) {
-        jlong* o = (*env)->GetLongArrayElements(env, out, NULL);
-        for (int64_t i = 0; i < n_ev; ++i) {
-            o[4 * i + 0] = ev[i].kind;
-            o[4 * i + 1] = ev[i].offset;
-            o[4 * i + 2] = ev[i].length;
-            o[4 * i + 3] = (jlong)(uint32_t)ev[i].index | ((jlong)ev[i].count << 32);
-        }
-        (*env)->ReleaseLongArrayElements(env, out, o, 0);
-        (*env)->SetByteArrayRegion(env, fileMd5Out, 0, 16, (const jbyte*)md5);
-        jlong sizes[3] = {lit, mat, read_error};
-        (*env)->SetLongArrayRegion(env, sizesOut, 0, 3, sizes);
-    }
-    free(ev);
-    if (rc != RSH_OK) throw_status(env, rc);
+    int64_t lit = 0, mat = 0;
+    file_arg a = {size, 0};
+    jlongArray out = run_scan(env, c, cpath, size, &h, weak, strong, s4, md5, &lit, &mat, scan_file, &a);
+    (*env)->ReleaseStringUTFChars(env, path, cpath);
+    if (out) sizes_out(env, sizesOut, fileMd5Out, md5, lit, mat, 1, a.read_error);
     return out;
 }
 
@@ -318,19 +467,23 @@ JNIEXPORT jboolean JNICALL Java_com_github_java_rsync_internal_session_NativeChe
     JNIEnv* env, jclass cls, jlong ctx, jobject tokens, jlong tokensLen, jintArray hdr4, jobject replica,
     jlong replicaLen, jboolean deferWrite, jobject target, jlong targetCap, jlongArray resultOut, jbyteArray md5Out) {
     (void)cls;
+    rsh_ctx* c = ctx_of(env, ctx);
+    if (!c) return JNI_FALSE;
     rsh_header h;
-    int rc = header_from(env, hdr4, &h);
-    const uint8_t* t = tokens ? (const uint8_t*)(*env)->GetDirectBufferAddress(env, tokens) : NULL;
-    const uint8_t* r = replica ? (const uint8_t*)(*env)->GetDirectBufferAddress(env, replica) : NULL;
-    uint8_t* o = target ? (uint8_t*)(*env)->GetDirectBufferAddress(env, target) : NULL;
-    if (rc != RSH_OK || !t || (replica && !r) || (*env)->GetArrayLength(env, resultOut) < 4 ||
+    if (header_from(env, hdr4, &h) != RSH_OK || !resultOut || !md5Out || (*env)->GetArrayLength(env, resultOut) < 4 ||
         (*env)->GetArrayLength(env, md5Out) != 16) {
-        throw_status(env, rc != RSH_OK ? rc : RSH_E_INVAL);
+        throw_status(env, RSH_E_INVAL);
         return JNI_FALSE;
     }
+    const uint8_t* t = direct_bytes(env, tokens, tokensLen);
+    if (!t) return JNI_FALSE;
+    const uint8_t* r = NULL;
+    if (replica && !(r = direct_bytes(env, replica, replicaLen))) return JNI_FALSE;
+    uint8_t* o = NULL;
+    if (target && !(o = (uint8_t*)direct_bytes(env, target, targetCap))) return JNI_FALSE;
     rsh_combine_result res;
-    rc = rsh_receiver_combine((rsh_ctx*)(intptr_t)ctx, t, tokensLen, &h, r, r ? replicaLen : 0, deferWrite ? 1 : 0, o,
-                              o ? targetCap : 0, &res);
+    int rc = rsh_receiver_combine(c, t, tokensLen, &h, r, r ? replicaLen : 0, deferWrite ? 1 : 0, o, o ? targetCap : 0,
+                                  &res);
     if (rc != RSH_OK) {
         throw_status(env, rc);
         return JNI_FALSE;

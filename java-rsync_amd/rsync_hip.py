@@ -7,6 +7,7 @@ Mirrors the reference's hot-path surface (paths relative to core/src/main/java/c
   Generator.sendItemizeAndChecksums (hot loop)    session/Generator.java:866-909  -> Context.block_sums
   Sender.sendMatchesAndData / skipMatchSendData   session/Sender.java:1235-1399   -> Context.match_scan
   Sender channel bytes (sendDataFrom / putInt)    session/Sender.java:794-809     -> tokens
+  a file larger than one JVM buffer (FileView)    io/FileView.java:235-278        -> Context.*_pieces
 
 Errors raise the Python analogue of the reference's exception (ValueError ~ IllegalArgumentException,
 ProtocolError ~ RsyncProtocolException, OverflowError ~ Checksum.ChunkOverflow).  There is no CPU
@@ -98,6 +99,11 @@ class CombineResult(ctypes.Structure):
                 ("md5", ctypes.c_uint8 * 16)]
 
 
+class Piece(ctypes.Structure):
+    """rsh_piece: one host buffer of a file handed over in pieces (rsh_*_pieces)."""
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_int64)]
+
+
 EVENT_DTYPE = np.dtype([("offset", "<i8"), ("length", "<i8"), ("kind", "<i4"), ("index", "<i4"),
                         ("count", "<i4"), ("reserved", "<i4")])
 
@@ -107,7 +113,7 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_coun
            "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
            "rsh_match_scan_device", "rsh_match_scan_tiled", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
            "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_receiver_combine",
-           "rsh_receiver_combine_device", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
+           "rsh_receiver_combine_device", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 
 _LIB = None
 
@@ -183,6 +189,9 @@ def lib():
         "rsh_match_scan_file": ([P, ctypes.c_char_p, I64, HP, P, P, P, P, I64, ctypes.POINTER(I64), P,
                                  ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(ScanStats),
                                  ctypes.POINTER(I32)], ctypes.c_int),
+        "rsh_block_sums_pieces": ([P, ctypes.POINTER(Piece), I32, HP, P, P, P], ctypes.c_int),
+        "rsh_match_scan_pieces": ([P, ctypes.POINTER(Piece), I32, HP, P, P, P, P, I64, ctypes.POINTER(I64), P,
+                                   ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(ScanStats)], ctypes.c_int),
         "rsh_dev_alloc": ([P, I64, ctypes.POINTER(P)], ctypes.c_int),
         "rsh_dev_free": ([P, P], ctypes.c_int),
         "rsh_memcpy_h2d": ([P, P, P, I64], ctypes.c_int),
@@ -374,6 +383,43 @@ class Context:
             rc = lib().rsh_fetch_events(self._p, _ptr(ev), n_ev.value, ctypes.byref(n_ev))
         _check(rc)
         return ev[:n_ev.value], (fm.tobytes() if digest else None), lit.value, mat.value, stats.as_dict()
+
+    @staticmethod
+    def _pieces(pieces):
+        arrs = [_u8(p) for p in pieces]
+        pl = (Piece * max(len(arrs), 1))()
+        for i, a in enumerate(arrs):
+            pl[i].data, pl[i].len = (a.ctypes.data if a.size else None), a.size
+        return arrs, pl, sum(a.size for a in arrs)
+
+    def block_sums_pieces(self, pieces, h, seed):
+        """As block_sums over the concatenation of `pieces` (host buffers; rsh_block_sums_pieces)."""
+        arrs, pl, _ = self._pieces(pieces)
+        s = np.frombuffer(bytes(seed), np.uint8).copy()
+        weak = np.zeros(max(h.chunk_count, 1), np.int32)
+        strong = np.zeros(max(h.chunk_count * h.digest_length, 1), np.uint8)
+        _check(lib().rsh_block_sums_pieces(self._p, pl, len(arrs), ctypes.byref(h), _ptr(s), _ptr(weak), _ptr(strong)))
+        return weak[:h.chunk_count], strong[:h.chunk_count * h.digest_length]
+
+    def match_scan_pieces(self, pieces, h, weak, strong, seed):
+        """As match_scan over the concatenation of `pieces` (rsh_match_scan_pieces)."""
+        arrs, pl, n = self._pieces(pieces)
+        s = np.frombuffer(bytes(seed), np.uint8).copy()
+        w = np.ascontiguousarray(weak, dtype=np.int32)
+        st = np.ascontiguousarray(strong, dtype=np.uint8)
+        cap = int(n // max(10 * h.block_length, 1) + 2 * h.chunk_count + 64) if h.block_length else n // 8192 + 2
+        ev = np.zeros(max(cap, 1), EVENT_DTYPE)
+        n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        fm = np.zeros(16, np.uint8)
+        stats = ScanStats()
+        rc = lib().rsh_match_scan_pieces(self._p, pl, len(arrs), ctypes.byref(h), _ptr(w) if w.size else None,
+                                         _ptr(st) if st.size else None, _ptr(s), _ptr(ev), cap, ctypes.byref(n_ev),
+                                         _ptr(fm), ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(stats))
+        if rc == RSH_E_NOSPACE:
+            ev = np.zeros(n_ev.value, EVENT_DTYPE)
+            rc = lib().rsh_fetch_events(self._p, _ptr(ev), n_ev.value, ctypes.byref(n_ev))
+        _check(rc)
+        return ev[:n_ev.value], fm.tobytes(), lit.value, mat.value, stats.as_dict()
 
     def block_sums_file(self, path, size, h, seed):
         """Generator pass over a file (FileView reads of `size` bytes): (weak, strong, read_error)."""

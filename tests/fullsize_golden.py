@@ -36,8 +36,25 @@ CASES = {
     # one byte inserted at 155 * B + 4096, the first block >= 64 whose insert the scan rolls past without a
     # weak hit (make_fullsize.py --find-clean-insert): every later match is at phase kB + 1
     "config5_shift1": (16 << 30, 131072, 4, "insert1_at:20320256"),
+    # BASELINE config 3: 64 GiB basis KEY ^ 3 scanned under the B = 131072 override (the rule's 2^18 is rejected
+    # by the Sender, Checksum.java:81-82), dl = 5; the source is the basis with the block at 5 GiB reversed and
+    # the block at 40 GiB rewritten from splitmix(B, KEY ^ 0x3E5) (test_gpu_fullsize.py::test_config3_64GiB).
+    # Too large to hold twice in the build container: make_fullsize.py streams it through a file.
+    "config3_edit": (64 << 30, 131072, 5, "rev5g_fill40g"),
 }
-BASIS_KEY = {"config2": KEY ^ 2, "config5": KEY ^ 5}
+BASIS_KEY = {"config2": KEY ^ 2, "config3": KEY ^ 3, "config5": KEY ^ 5}
+CONFIG3_FILL_KEY = KEY ^ 0x3E5
+
+# BASELINE config 4: a list of 128 MiB files (1024 over 8 GPUs), B = 8192 by the rule, dl = 3, each file its own
+# splitmix stream (bench.py --workload files builds exactly these).  "half": every other block of each file's
+# basis replaced from the stream KEY_EDIT ^ key(i); "identical": the basis is the source.
+CONFIG4_FILES, CONFIG4_FILE_BYTES, CONFIG4_B, CONFIG4_DL = 1024, 128 << 20, 8192, 3
+KEY_EDIT = KEY | 0xED17
+
+
+def config4_key(i):
+    """Source stream of file i of the config-4 list (bench.py main_files)."""
+    return KEY ^ (i << 20) ^ 0x4F11E5
 
 
 def records_from_oracle(events):

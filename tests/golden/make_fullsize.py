@@ -6,6 +6,9 @@ chunk-aligned slices on a thread pool (chunks are independent), its Sender scan 
 and the basis in memory (32 GiB).
 
     python tests/golden/make_fullsize.py [case ...]        # default: every case in fullsize_golden.CASES
+    python tests/golden/make_fullsize.py --config4         # tests/golden/fullsize_config4.json (1024 files)
+
+config3_edit (64 GiB) streams its source through a file (RSH_C3_TMP, default /tmp; 64 GiB of disk).
 """
 import concurrent.futures as cf
 import json
@@ -85,13 +88,50 @@ def generator_threaded(basis, B, dl, workers=8):
     return np.concatenate([w for w, _ in res]), np.concatenate([s for _, s in res])
 
 
+def config3_inputs(name, path):
+    """Config 3 (64 GiB) without holding the basis and the source at once: the source is written to `path` a
+    GiB at a time (the basis stream with its two edited blocks) and memory-mapped for the oracle's scan; the
+    Generator runs over basis slices regenerated on the fly (splitmix64 is counter-based), 8 threads."""
+    n, B, dl, _ = G.CASES[name]
+    key = G.BASIS_KEY["config3"]
+    k5, k40 = (5 << 30) // B, (40 << 30) // B
+    piece = 1 << 30
+    with open(path, "wb") as f:
+        for off in range(0, n, piece):
+            a = O.splitmix(min(piece, n - off), key, off)
+            for blk, how in ((k5, "rev"), (k40, "fill")):
+                lo, hi = blk * B, (blk + 1) * B
+                if lo >= off and hi <= off + a.size:
+                    seg = a[lo - off:hi - off]
+                    seg[:] = seg[::-1].copy() if how == "rev" else O.splitmix(B, G.CONFIG3_FILL_KEY)
+            f.write(a.tobytes())
+            del a
+    C = n // B
+    per = piece // B
+    ws, ss = [], []
+    with cf.ThreadPoolExecutor(8) as ex:
+        def run(k0):
+            sl = O.splitmix(min(per, C - k0) * B, key, k0 * B)
+            return O.generator(sl, O.header(B, dl, sl.size), SEED)
+        for k in range(0, C, 8 * per):
+            for w, s in ex.map(run, range(k, min(C, k + 8 * per), per)):
+                ws.append(w)
+                ss.append(s)
+    return np.concatenate(ws), np.concatenate(ss), np.memmap(path, np.uint8, "r", shape=(n,))
+
+
 def run_case(name):
     n, B, dl, recipe = G.CASES[name]
     t0 = time.time()
-    basis, src = build_inputs(name)
-    h = O.header(B, dl, basis.size)
-    w, s = generator_threaded(basis, B, dl)
-    del basis
+    if recipe == "rev5g_fill40g":
+        path = os.environ.get("RSH_C3_TMP", "/tmp/rsh_config3_src.bin")
+        w, s, src = config3_inputs(name, path)
+        h = O.header(B, dl, n)
+    else:
+        basis, src = build_inputs(name)
+        h = O.header(B, dl, basis.size)
+        w, s = generator_threaded(basis, B, dl)
+        del basis
     t1 = time.time()
     ev, fm, lit, mat, md5_windows = O.sender(src, h, w, s, SEED)
     t2 = time.time()
@@ -105,12 +145,52 @@ def run_case(name):
         "oracle_seconds": {"generator": round(t1 - t0, 1), "sender": round(t2 - t1, 1)},
     }
     print(name, json.dumps(out), flush=True)
+    if recipe == "rev5g_fill40g":
+        del src
+        os.unlink(path)
     return out
+
+
+def run_config4(out_path=os.path.join(HERE, "fullsize_config4.json"), workers=8):
+    """Config 4: every file of the 1024-file list, both basis forms, one oracle Generator + Sender per file
+    (files are independent: a thread pool, ctypes drops the GIL).  Per file: event count, literal/matched,
+    SHA-256 of the event list at the oracle's granularity and the file MD5."""
+    F, S, B, dl = G.CONFIG4_FILES, G.CONFIG4_FILE_BYTES, G.CONFIG4_B, G.CONFIG4_DL
+    h = O.header(B, dl, S)
+
+    def one(i):
+        key = G.config4_key(i)
+        src = O.splitmix(S, key)
+        res = {}
+        for form in ("identical", "half"):
+            basis = src
+            if form == "half":
+                basis = src.copy()
+                basis.reshape(-1, B)[1::2] = O.splitmix(S, G.KEY_EDIT ^ key).reshape(-1, B)[1::2]
+            w, s = O.generator(basis, h, SEED)
+            ev, fm, lit, mat, _ = O.sender(src, h, w, s, SEED)
+            rec = G.records_from_oracle(ev)
+            res[form] = [int(rec.size), int(lit), int(mat), G.events_sha(rec), fm.hex()]
+        return res
+
+    t0 = time.time()
+    with cf.ThreadPoolExecutor(workers) as ex:
+        files = list(ex.map(one, range(F)))
+    data = {"files": F, "file_bytes": S, "block_length": B, "digest_length": dl,
+            "record": ["n_events", "literal", "matched", "events_sha256", "file_md5"],
+            "identical": [f["identical"] for f in files], "half": [f["half"] for f in files],
+            "oracle_seconds": round(time.time() - t0, 1)}
+    with open(out_path, "w") as f:
+        json.dump(data, f)
+    print("config4", data["oracle_seconds"], "s", flush=True)
 
 
 def main():
     if sys.argv[1:2] == ["--find-clean-insert"]:
         print(find_clean_insert())
+        return
+    if sys.argv[1:2] == ["--config4"]:
+        run_config4()
         return
     names = sys.argv[1:] or list(G.CASES)
     data = json.load(open(OUT)) if os.path.exists(OUT) else {}

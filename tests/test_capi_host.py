@@ -29,7 +29,7 @@ def test_library_exports_every_symbol():
     L = ctypes.CDLL(R.LIB_PATH)
     for name in R.EXPORTS:
         assert hasattr(L, name), name
-    assert R.lib().rsh_abi_version() == 2
+    assert R.lib().rsh_abi_version() == 3
 
 
 def test_library_built_from_these_sources():

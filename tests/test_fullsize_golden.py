@@ -50,3 +50,29 @@ def test_committed_fullsize_digests():
         assert c["literal"] + c["matched"] == c["n_src"]  # Sender.java:1325
     ident = d["config5_identical"]
     assert ident["matched"] == 16 << 30 and ident["n_events"] == ident["chunk_count"] == 131072
+
+
+def test_committed_config4_digests():
+    """tests/golden/fullsize_config4.json: every file of the 1024-file list, both basis forms.  Identical bases
+    scan as one match per chunk (Sender.java:1282-1287); every record satisfies literal + matched = size
+    (Sender.java:1325).  Two files are re-run through the oracle here (a 128 MiB pair takes ~2 s) to pin
+    the committed digests to the recipe (per-file keys, every other block replaced)."""
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize_config4.json")))
+    F, S, B, dl = G.CONFIG4_FILES, G.CONFIG4_FILE_BYTES, G.CONFIG4_B, G.CONFIG4_DL
+    assert (d["files"], d["file_bytes"], d["block_length"], d["digest_length"]) == (F, S, B, dl)
+    assert len(d["identical"]) == len(d["half"]) == F
+    for form in ("identical", "half"):
+        for n_ev, lit, mat, sha, fmd5 in d[form]:
+            assert lit + mat == S and len(sha) == 64 and len(fmd5) == 32
+    assert all(r[:3] == [S // B, 0, S] for r in d["identical"])
+    assert len({r[4] for r in d["half"]}) == F  # distinct sources: per-file keys
+    h = O.header(B, dl, S)
+    for i in (3, 1000):
+        key = G.config4_key(i)
+        src = O.splitmix(S, key)
+        basis = src.copy()
+        basis.reshape(-1, B)[1::2] = O.splitmix(S, G.KEY_EDIT ^ key).reshape(-1, B)[1::2]
+        w, s = O.generator(basis, h, SEED)
+        ev, fm, lit, mat, _ = O.sender(src, h, w, s, SEED)
+        rec = G.records_from_oracle(ev)
+        assert [int(rec.size), lit, mat, G.events_sha(rec), fm.hex()] == d["half"][i]

@@ -9,9 +9,9 @@ per GPU, B = 8192, through the batched entry points).
     SHA-256 of the event list at the oracle's granularity, event count, literal/matched, and -- where the
     channel bytes are small enough to hash here -- the file MD5 and SHA-256 of rsh_tokens_write's bytes).
     Every scan's event list must also decode back to the source (contiguous tiling, MATCH bytes equal to the
-    basis chunks they name, literal + matched == n: Sender.java:1325).  Config 3's scan (64 GiB, no oracle
-    digest: the source does not fit the build container's memory twice) is checked by those properties and
-    its structurally known prefix.
+    basis chunks they name, literal + matched == n: Sender.java:1325).  Config 3's 64 GiB scan (resident and
+    tiled) is compared with the oracle's digest too (make_fullsize.py streams that pair through a file), and
+    config 4's 128-file segments with per-file oracle digests (tests/golden/fullsize_config4.json).
 
 Inputs are splitmix64 bytes generated on the device (the same generator the oracle restates), built by the
 recipes tests/fullsize_golden.py names."""
@@ -213,6 +213,45 @@ def test_config2_4GiB_generator_and_scans(env):
     del src
 
 
+def _cut(a, sizes):
+    """Host pieces of `a` with the given lengths (the last takes the rest)."""
+    out, off = [], 0
+    for ln in sizes:
+        out.append(a[off:off + ln])
+        off += ln
+    out.append(a[off:])
+    return out
+
+
+def test_config2_pieces_4GiB(env):
+    """A file larger than one JVM direct ByteBuffer (capacity <= 2^31 - 1) handed over as pieces
+    (rsh_block_sums_pieces / rsh_match_scan_pieces, the binding's path for any file size: FileView streams
+    files of any size, FileView.java:235-278).  Config 2's insert pair, basis and source cut into pieces of at
+    most 2^31 - 1 bytes at offsets that are not multiples of B (chunks and windows straddle pieces): the table
+    equals the device Generator's, and the scan equals the oracle's digest of the same inputs, file MD5 and
+    channel bytes included."""
+    ctx, torch = env
+    basis_d, src_d = _build(ctx, torch, "config2_insert")
+    n, B, dl, _ = G.CASES["config2_insert"]
+    h = R.header_make(B, dl, n)
+    d_w, d_s = _block_sums(ctx, torch, basis_d, h)
+    basis, src = basis_d.cpu().numpy(), src_d.cpu().numpy()
+    del basis_d, src_d
+    torch.cuda.empty_cache()
+    big = (1 << 31) - 1
+    w, s = ctx.block_sums_pieces(_cut(basis, [big, 12345, big - 99999]), h, SEED)
+    assert np.array_equal(w, d_w.cpu().numpy()) and np.array_equal(s, d_s.cpu().numpy())
+    del basis
+    pieces = _cut(src, [big, 1, 777777, big - 5])
+    assert max(p.size for p in pieces) <= big and len(pieces) == 4
+    ev, fm, lit, mat, st = ctx.match_scan_pieces(pieces, h, w, s, SEED)
+    g = _fullsize("config2_insert")
+    rec = G.records_from_runs(ev, B)
+    assert (int(rec.size), lit, mat) == (g["n_events"], g["literal"], g["matched"])
+    assert G.events_sha(rec) == g["events_sha256"] and fm.hex() == g["file_md5"]
+    assert hashlib.sha256(R.tokens(src, ev, fm)).hexdigest() == g["tokens_sha256"]
+
+
 def test_config3_64GiB(env):
     """Config 3: 64 GiB.  The README rule gives B = 262144, dl = 5: the Generator runs it (bit-exact against
     the threaded oracle over all 262144 chunks), but the reference Sender rejects B > 2^17
@@ -243,6 +282,8 @@ def test_config3_64GiB(env):
     _fill(ctx, src[j * B:(j + 1) * B], KEY ^ 0x3E5)
     ctx.sync()
     ev, lit, mat, st = _scan(ctx, torch, src, h, d_w, d_s)
+    # the oracle's scan of the same 64 GiB pair (make_fullsize.py config3_edit streams it through a file)
+    _check_golden(torch, "config3_edit", ev, lit, mat, src, tokens=False)
     lead = 0  # the unchanged prefix: MATCH(0 .. k-1), and nothing further (chunk k was rewritten)
     for e in ev:
         if e["kind"] != R.EV_MATCH or int(e["index"]) != lead:
@@ -258,8 +299,8 @@ def test_config3_64GiB(env):
                                                    tile_bytes=4 << 30, digest=False)
     # tile loads: the prefix chain crosses one boundary; after the rewritten block the stale digest (quirk B)
     # leaves only closed-form flushes, which need no source bytes
-    assert (tlit, tmat) == (lit, mat) and tst["head_steps"] >= 2, tst
-    assert np.array_equal(tev[["offset", "length", "kind", "index", "count"]], ev[["offset", "length", "kind", "index", "count"]])
+    assert tst["head_steps"] >= 2, tst
+    _check_golden(torch, "config3_edit", tev, tlit, tmat, None, tokens=False)
     del host
     del basis
     torch.cuda.empty_cache()
@@ -294,54 +335,75 @@ def test_config5_16GiB(env, name):
     torch.cuda.empty_cache()
 
 
-def test_config4_segment_batch_equals_single(env):
-    """Config 4 per GPU: 128 files x 128 MiB (B = 8192 by the rule, dl = 3), every other block of each basis
-    replaced.  The batched entry points must give every file exactly what the single-file calls give
-    (which the parity suites tie to the oracle), and the Generator tables of a few files are checked
-    against the oracle directly."""
+_C4 = None
+
+
+def _config4_golden():
+    global _C4
+    if _C4 is None:
+        _C4 = json.load(open(os.path.join(ROOT, "tests", "golden", "fullsize_config4.json")))
+    return _C4
+
+
+@pytest.mark.parametrize("form,shard", [("half", "gpu1"), ("half", "rank5of8"), ("identical", "rank5of8")])
+def test_config4_segment_vs_oracle(env, form, shard):
+    """Config 4 per GPU: 128 files x 128 MiB (B = 8192 by the rule, dl = 3), each file its own splitmix stream
+    (bench.py --workload files builds exactly these): the files of the 1-GPU job (0..127) or those
+    shard.shard_files gives rank 5 of an 8-GPU job over the 1024-file list.  half: every other block of each
+    basis replaced.  The batched entry points (one K1 launch for the segment's Generator, one resolver per
+    file with gathered round trips) must give every file the oracle's event list (tests/golden/
+    fullsize_config4.json: make_fullsize.py --config4 ran the oracle over all 1024 files, both forms), and
+    a few files' Generator tables and whole-file MD5s are checked against the oracle directly."""
+    import shard as SH
     ctx, torch = env
-    F, S = 128, 128 << 20
-    B = R.block_length_for(S)
-    dl = R.digest_length_for(S, B)
-    assert (B, dl) == (8192, 3)
+    g = _config4_golden()
+    S, B, dl = G.CONFIG4_FILE_BYTES, G.CONFIG4_B, G.CONFIG4_DL
+    assert (R.block_length_for(S), R.digest_length_for(S, R.block_length_for(S))) == (B, dl)
+    files = list(range(128)) if shard == "gpu1" else SH.shard_files([S] * G.CONFIG4_FILES, 8)[5]
+    F = len(files)
+    assert F == 128
     n = F * S
     src = torch.empty(n, dtype=torch.uint8, device="cuda")
-    _fill(ctx, src, KEY ^ 4)
-    basis = src.clone()
-    other = torch.empty(n, dtype=torch.uint8, device="cuda")
-    _fill(ctx, other, KEY ^ 0x4ED1)
+    basis = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for j, i in enumerate(files):
+        _fill(ctx, src[j * S:(j + 1) * S], G.config4_key(i))
+        if form == "half":
+            _fill(ctx, basis[j * S:(j + 1) * S], G.KEY_EDIT ^ G.config4_key(i))
     ctx.sync()
-    basis.view(-1, B)[1::2] = other.view(-1, B)[1::2]
-    del other
+    if form == "half":
+        basis.view(-1, B)[::2] = src.view(-1, B)[::2]
+    else:
+        basis.copy_(src)
     torch.cuda.synchronize()
     h = R.header_make(B, dl, S)
     C = h.chunk_count
     w = torch.empty(F * C, dtype=torch.int32, device="cuda")
     s = torch.empty(F * C * dl, dtype=torch.uint8, device="cuda")
     bj = (R.BlockJob * F)()
-    for i in range(F):
-        bj[i].d_data, bj[i].n, bj[i].h = basis.data_ptr() + i * S, S, h
-        bj[i].d_weak, bj[i].d_strong = w.data_ptr() + 4 * i * C, s.data_ptr() + i * C * dl
+    for j in range(F):
+        bj[j].d_data, bj[j].n, bj[j].h = basis.data_ptr() + j * S, S, h
+        bj[j].d_weak, bj[j].d_strong = w.data_ptr() + 4 * j * C, s.data_ptr() + j * C * dl
     assert R.lib().rsh_block_sums_batch_device(ctx.handle, bj, F, SEED_NP.ctypes.data) == 0
     ctx.sync()
     hw, hs = w.cpu().numpy(), s.cpu().numpy()
-    for i in (0, 77, F - 1):
-        ow, os_ = O.generator(basis[i * S:(i + 1) * S].cpu().numpy(), O.header(B, dl, S), SEED)
-        assert np.array_equal(hw[i * C:(i + 1) * C], ow) and np.array_equal(hs[i * C * dl:(i + 1) * C * dl], os_)
+    for j in (0, 77, F - 1):
+        ow, os_ = O.generator(basis[j * S:(j + 1) * S].cpu().numpy(), O.header(B, dl, S), SEED)
+        assert np.array_equal(hw[j * C:(j + 1) * C], ow) and np.array_equal(hs[j * C * dl:(j + 1) * C * dl], os_)
     cap = C + S // B + 4096
     evs = [np.zeros(cap, R.EVENT_DTYPE) for _ in range(F)]
     sj = (R.ScanJob * F)()
-    for i in range(F):
-        sj[i].d_src, sj[i].n, sj[i].h = src.data_ptr() + i * S, S, h
-        sj[i].d_weak, sj[i].d_strong = bj[i].d_weak, bj[i].d_strong
-        sj[i].ev, sj[i].ev_cap = evs[i].ctypes.data, cap
+    for j in range(F):
+        sj[j].d_src, sj[j].n, sj[j].h = src.data_ptr() + j * S, S, h
+        sj[j].d_weak, sj[j].d_strong = bj[j].d_weak, bj[j].d_strong
+        sj[j].ev, sj[j].ev_cap = evs[j].ctypes.data, cap
     assert R.lib().rsh_match_scan_batch_device(ctx.handle, sj, F, SEED_NP.ctypes.data, None) == 0
-    for i in range(F):
-        sub = src[i * S:(i + 1) * S]
-        ev, lit, mat, _ = _scan(ctx, torch, sub, h, w[i * C:(i + 1) * C], s[i * C * dl:(i + 1) * C * dl])
-        assert sj[i].status == 0 and (sj[i].literal, sj[i].matched) == (lit, mat)
-        assert R.events_as_tuples(evs[i][:sj[i].n_ev], B) == R.events_as_tuples(ev, B), f"file {i}"
-        if i % 32 == 0:
-            _check_delta(torch, ev, sub, basis[i * S:(i + 1) * S], h, lit, mat)
+    for j, i in enumerate(files):
+        n_ev, lit, mat, sha, fmd5 = g[form][i]
+        rec = G.records_from_runs(evs[j][:sj[j].n_ev], B)
+        assert sj[j].status == 0 and (int(rec.size), sj[j].literal, sj[j].matched) == (n_ev, lit, mat), f"file {i}"
+        assert G.events_sha(rec) == sha, f"file {i}: match list differs from the oracle's"
+        if j % 40 == 0:
+            assert hashlib.md5(memoryview(src[j * S:(j + 1) * S].cpu().numpy())).hexdigest() == fmd5
+            _check_delta(torch, evs[j][:sj[j].n_ev], src[j * S:(j + 1) * S], basis[j * S:(j + 1) * S], h, lit, mat)
     del src, basis
     torch.cuda.empty_cache()

@@ -468,3 +468,31 @@ def test_concurrent_contexts_and_busy(ctx):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.parametrize("cuts", [[], [0], [1], [511, 0, 1], [7, 13, 1000, 4096, 65535], [200000, 3]],
+                         ids=lambda c: "-".join(map(str, c)) or "whole")
+def test_pieces_match_oracle(ctx, cuts):
+    """rsh_block_sums_pieces / rsh_match_scan_pieces over the same bytes cut into pieces of every shape (empty
+    pieces, single bytes, windows and chunks straddling pieces): exactly the oracle's table and events."""
+    basis = O.splitmix(300000, 0x91ECE5)
+    src = np.concatenate([basis[:70000], O.splitmix(5000, 0x1A5E), basis[70000:200000], basis[:9000]])
+    for blen, dlen in ((512, 2), (4096, 3), (0, 0)):
+        h = O.header(blen, dlen, basis.size)
+        rh = R.Header(**h.as_dict())
+
+        def pieces(a):
+            out, off = [], 0
+            for c in cuts:
+                out.append(a[off:off + c])
+                off += c
+            return out + [a[off:]]
+        if blen:
+            ow, os_ = O.generator(basis, h, SEED)
+            w, s = ctx.block_sums_pieces(pieces(basis), rh, SEED)
+            assert np.array_equal(w, ow) and np.array_equal(s, os_)
+        else:
+            ow, os_ = np.zeros(0, np.int32), np.zeros(0, np.uint8)
+        oev, ofm, olit, omat, _ = O.sender(src, h, ow, os_, SEED)
+        ev, fm, lit, mat, _ = ctx.match_scan_pieces(pieces(src), rh, ow, os_, SEED)
+        assert R.events_as_tuples(ev, blen) == [tuple(e) for e in oev] and (fm, lit, mat) == (ofm, olit, omat)

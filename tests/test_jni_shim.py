@@ -1,0 +1,177 @@
+"""The JNI shim (java-rsync_amd/jni/rsync_hip_jni.c) without a JVM: no JDK exists here or on the GPU box, so
+the shim is compiled against a test double of <jni.h> and driven through the fake JNIEnv of
+tests/jni/harness.c (libjniharness.so, ctypes).
+
+CPU tests: every entry point rejects a closed context (handle 0: IllegalStateException) and any byte count
+past the direct buffer it names (IllegalArgumentException) before the library is called -- the harness hands
+the shim a bogus non-zero context, so a call that reached the library would crash the test.  GPU tests: the
+shim's Generator and Sender over real contexts (one direct buffer, several buffers) equal the oracle, and the
+events it packs into long[] decode to the oracle's event list (Sender.java:1235-1327)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as O
+import rsync_hip as R
+from conftest import ROOT
+
+HARNESS = os.path.join(ROOT, "java-rsync_amd", "lib", "libjniharness.so")
+SEED = bytes([1, 2, 3, 4])
+BOGUS = 0x10  # a non-zero context that must never reach the library
+IAE, ISE = "java/lang/IllegalArgumentException", "java/lang/IllegalStateException"
+
+
+@pytest.fixture(scope="module")
+def H():
+    R.build()
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "java-rsync_amd"), "jni-harness"], check=True)
+    L = ctypes.CDLL(HARNESS)
+    L.jh_exception.restype = ctypes.c_char_p
+    L.jh_exception_message.restype = ctypes.c_char_p
+    L.jh_ctx_create.restype = ctypes.c_int64
+    for fn in ("jh_match_scan", "jh_match_scan_buffers"):
+        getattr(L, fn).restype = ctypes.c_int64
+    return L
+
+
+def _p(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def exc(H):
+    return H.jh_exception().decode()
+
+
+def _hdr(h):
+    return np.array([h.chunk_count, h.block_length, h.digest_length, h.remainder], np.int32)
+
+
+def block_sums(H, ctx, buf, cap, n, h, weak, strong, seed=SEED):
+    s = np.frombuffer(seed, np.uint8).copy()
+    H.jh_block_sums(ctypes.c_int64(ctx), _p(buf), ctypes.c_int64(cap), ctypes.c_int64(n), _p(_hdr(h)), _p(s),
+                    ctypes.c_int64(s.size), _p(weak), ctypes.c_int64(weak.size), _p(strong),
+                    ctypes.c_int64(strong.size))
+    return exc(H)
+
+
+def _bufs(pieces, caps=None):
+    arr = (ctypes.c_void_p * max(len(pieces), 1))(*[p.ctypes.data if p is not None else None for p in pieces])
+    cp = np.array(caps if caps is not None else [p.size for p in pieces], np.int64)
+    return arr, cp
+
+
+def block_sums_buffers(H, ctx, pieces, n, h, weak, strong, caps=None):
+    s = np.frombuffer(SEED, np.uint8).copy()
+    arr, cp = _bufs(pieces, caps)
+    H.jh_block_sums_buffers(ctypes.c_int64(ctx), arr, _p(cp), len(pieces), ctypes.c_int64(n), _p(_hdr(h)), _p(s),
+                            ctypes.c_int64(4), _p(weak), ctypes.c_int64(weak.size), _p(strong),
+                            ctypes.c_int64(strong.size))
+    return exc(H)
+
+
+def match_scan(H, ctx, src, cap, n, h, w, st, pieces=None, caps=None, md5_len=16, sizes_len=2):
+    s = np.frombuffer(SEED, np.uint8).copy()
+    md5 = np.zeros(max(md5_len, 1), np.uint8)
+    sizes = np.zeros(max(sizes_len, 1), np.int64)
+    evcap = 4 * (n // max(10 * h.block_length, 1) + 2 * h.chunk_count + 64) + 64
+    ev = np.zeros(evcap, np.int64)
+    common = (_p(_hdr(h)), _p(w), ctypes.c_int64(w.size), _p(st), ctypes.c_int64(st.size), _p(s), ctypes.c_int64(4),
+              _p(md5), ctypes.c_int64(md5_len), _p(sizes), ctypes.c_int64(sizes_len), _p(ev), ctypes.c_int64(evcap))
+    if pieces is None:
+        k = H.jh_match_scan(ctypes.c_int64(ctx), _p(src), ctypes.c_int64(cap), ctypes.c_int64(n), *common)
+    else:
+        arr, cp = _bufs(pieces, caps)
+        k = H.jh_match_scan_buffers(ctypes.c_int64(ctx), arr, _p(cp), len(pieces), ctypes.c_int64(n), *common)
+    return exc(H), (ev[:k] if k >= 0 else None), md5.tobytes(), sizes
+
+
+def test_closed_context_is_illegal_state(H):
+    """NativeChecksum after close() passes handle 0: the shim throws instead of casting it to a context."""
+    h = O.header(512, 2, 4096)
+    data = np.zeros(4096, np.uint8)
+    w, st = np.zeros(8, np.int32), np.zeros(16, np.uint8)
+    assert block_sums(H, 0, data, data.size, data.size, h, w, st) == ISE
+    assert block_sums_buffers(H, 0, [data], data.size, h, w, st) == ISE
+    assert match_scan(H, 0, data, data.size, data.size, h, w, st)[0] == ISE
+    assert match_scan(H, 0, data, data.size, data.size, h, w, st, pieces=[data])[0] == ISE
+    res, md5 = np.zeros(4, np.int64), np.zeros(16, np.uint8)
+    H.jh_receiver_combine(ctypes.c_int64(0), _p(data), ctypes.c_int64(16), ctypes.c_int64(16), _p(_hdr(h)), None,
+                          ctypes.c_int64(-1), ctypes.c_int64(0), 0, None, ctypes.c_int64(-1), ctypes.c_int64(0), _p(res),
+                          _p(md5))
+    assert exc(H) == ISE
+
+
+def test_byte_count_past_buffer_capacity_is_rejected(H):
+    """The memory-safety hole of round 2: n (the FileInfo size) larger than the direct buffer it names.  The
+    shim compares it with GetDirectBufferCapacity and throws before the library can read past the buffer."""
+    n = 8192
+    data = np.zeros(n, np.uint8)
+    h = O.header(512, 2, n)
+    w, st = np.zeros(16, np.int32), np.zeros(32, np.uint8)
+    assert block_sums(H, BOGUS, data, n - 1, n, h, w, st) == IAE
+    assert match_scan(H, BOGUS, data, n - 1, n, h, w, st)[0] == IAE
+    assert block_sums(H, BOGUS, data, -1, n, h, w, st) == IAE          # a heap ByteBuffer: no address
+    assert match_scan(H, BOGUS, data, n, -5, h, w, st)[0] == IAE        # a negative size
+    # several buffers holding fewer bytes than n, or one of them not direct
+    half = data[:n // 2]
+    assert block_sums_buffers(H, BOGUS, [half, half], n + 1, h, w, st) == IAE
+    assert match_scan(H, BOGUS, None, 0, n + 1, h, w, st, pieces=[half, half])[0] == IAE
+    assert match_scan(H, BOGUS, None, 0, n, h, w, st, pieces=[half, half], caps=[n // 2, -1])[0] == IAE
+    assert block_sums_buffers(H, BOGUS, [], n, h, w, st) == IAE
+    # the Receiver's three buffers
+    res, md5 = np.zeros(4, np.int64), np.zeros(16, np.uint8)
+    for tcap, rcap, ocap in ((15, n, n), (16, n - 1, n), (16, n, n - 1)):
+        H.jh_receiver_combine(ctypes.c_int64(BOGUS), _p(data), ctypes.c_int64(tcap), ctypes.c_int64(16), _p(_hdr(h)),
+                              _p(data), ctypes.c_int64(rcap), ctypes.c_int64(n), 0, _p(data), ctypes.c_int64(ocap),
+                              ctypes.c_int64(n), _p(res), _p(md5))
+        assert exc(H) == IAE, (tcap, rcap, ocap)
+
+
+def test_short_java_arrays_are_rejected(H):
+    """Output and table arrays shorter than the header says, a seed that is not 4 bytes, a short md5/sizes
+    array: IllegalArgumentException, nothing written past a Java array (the harness bounds-checks regions)."""
+    n = 4096
+    data = np.zeros(n, np.uint8)
+    h = O.header(512, 2, n)  # 8 chunks, 16 digest bytes
+    assert block_sums(H, BOGUS, data, n, n, h, np.zeros(7, np.int32), np.zeros(16, np.uint8)) == IAE
+    assert block_sums(H, BOGUS, data, n, n, h, np.zeros(8, np.int32), np.zeros(15, np.uint8)) == IAE
+    assert block_sums(H, BOGUS, data, n, n, h, np.zeros(8, np.int32), np.zeros(16, np.uint8), seed=b"\0" * 3) == IAE
+    w, st = np.zeros(8, np.int32), np.zeros(16, np.uint8)
+    assert match_scan(H, BOGUS, data, n, n, h, w, st, md5_len=15)[0] == IAE
+    assert match_scan(H, BOGUS, data, n, n, h, w, st, sizes_len=1)[0] == IAE
+
+
+@pytest.mark.gpu
+def test_shim_scans_match_oracle(H):
+    """Real contexts through the shim: blockSums / blockSumsBuffers and matchScan / matchScanBuffers equal the
+    oracle (table, events decoded from the long[] quadruples, file MD5, literal/matched)."""
+    ctx = H.jh_ctx_create(0)
+    assert ctx and exc(H) == "", exc(H)
+    try:
+        for n, blen, dl in ((100000, 512, 2), (3 << 20, 8192, 3), (1300, 512, 2)):
+            basis = O.splitmix(n, 0xB0 ^ n)
+            src = np.concatenate([basis[:n // 3], O.splitmix(777, 0xED), basis[n // 3 + 100:]])
+            h = O.header(blen, dl, n)
+            ow, os_ = O.generator(basis, h, SEED)
+            w, st = np.zeros(h.chunk_count, np.int32), np.zeros(h.chunk_count * dl, np.uint8)
+            assert block_sums(H, ctx, basis, basis.size, n, h, w, st) == ""
+            assert np.array_equal(w, ow) and np.array_equal(st, os_)
+            w2, st2 = np.zeros_like(w), np.zeros_like(st)
+            cut = [basis[:blen + 7], basis[blen + 7:blen + 8], basis[blen + 8:]]
+            assert block_sums_buffers(H, ctx, cut, n, h, w2, st2) == ""
+            assert np.array_equal(w2, ow) and np.array_equal(st2, os_)
+            oev, ofm, olit, omat, _ = O.sender(src, h, ow, os_, SEED)
+            for pieces in (None, [src[:5], src[5:blen * 3 + 1], src[blen * 3 + 1:]]):
+                e, ev, fm, sizes = match_scan(H, ctx, src, src.size, src.size, h, ow, os_, pieces=pieces)
+                assert e == "" and ev is not None, e
+                q = ev.reshape(-1, 4)
+                arr = np.zeros(q.shape[0], R.EVENT_DTYPE)  # {kind, offset, length, index | count << 32}
+                arr["kind"], arr["offset"], arr["length"] = q[:, 0], q[:, 1], q[:, 2]
+                arr["index"], arr["count"] = q[:, 3] & 0xFFFFFFFF, q[:, 3] >> 32
+                assert R.events_as_tuples(arr, blen) == [tuple(x) for x in oev]
+                assert fm == ofm and (sizes[0], sizes[1]) == (olit, omat)
+    finally:
+        H.jh_ctx_destroy(ctypes.c_int64(ctx))

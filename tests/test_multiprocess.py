@@ -71,3 +71,21 @@ def test_gloo_world2_file_sharding():
         mat += m
     assert out[0][:3] == out[1][:3] == (lit, mat, 2.0)
     assert out[0][3] + out[1][3] == len(sizes)
+
+
+def test_bench_gpus2_dry_run_spawns_ranks():
+    """`python bench.py --gpus 2` without a launcher starts the two rank processes itself (bench.spawn_ranks);
+    --dry-run keeps them off the device (gloo).  The line must come from rank 0 and report both ranks, with
+    the 256-file list (128 per GPU) sharded over them."""
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run",
+                          "--workload", "files"], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["dry_run"] and rec["config"]["files_total"] == 256
