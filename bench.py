@@ -74,9 +74,18 @@ def parse():
                          "per round for all files) or one rsh_match_scan_device per file on a context pool")
     ap.add_argument("--cpu-sample-mib", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="library option for an A/B run (include/rsync_hip_debug.h; reported in the line)")
     ap.add_argument("--dry-run", action="store_true",
                     help="rank plumbing only (gloo on CPU, no device): the line reports n_gpus and no value")
     return ap.parse_args()
+
+
+def apply_opts(a):
+    """--opt NAME=VALUE: the library's A/B switches (defaults otherwise; never read from the environment)."""
+    for kv in a.opt:
+        name, _, val = kv.partition("=")
+        R.set_option(name, int(val))
 
 
 def _free_port():
@@ -160,6 +169,7 @@ def main():
     if not os.path.exists(R.LIB_PATH):
         R.build()
     L = R.lib()
+    apply_opts(a)
     ctx = R.Context(local)
     stream = torch.cuda.ExternalStream(L.rsh_ctx_stream(ctx.handle))
 
@@ -352,6 +362,8 @@ def main():
         b0, s0 = pairs[a.variant]
         res["cpu_baseline"] = cpu_baseline(s0, b0, B, dl, a.cpu_sample_mib << 20)
     if rank == 0:
+        if a.opt:
+            res["config"]["options"] = a.opt
         print(json.dumps(res), flush=True)
     ctx.close()
     if world > 1:
@@ -413,6 +425,7 @@ def main_files(a):
     if not os.path.exists(R.LIB_PATH):
         R.build()
     L = R.lib()
+    apply_opts(a)
     S = a.file_mib << 20
     # the job's file list (BASELINE config 4: 1024 files at 8 GPUs; a.files per GPU) sharded over the ranks by
     # the production LPT helper; this rank lays its files end to end in HBM
@@ -582,6 +595,8 @@ def main_files(a):
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline_files(src, basis, S, F, B, dl, a.cpu_sample_mib << 20)
     if rank == 0:
+        if a.opt:
+            res["config"]["options"] = a.opt
         print(json.dumps(res), flush=True)
     ex.shutdown()
     for c in pool_ctx:
@@ -604,6 +619,7 @@ def main_receiver(a):
     if not os.path.exists(R.LIB_PATH):
         R.build()
     L = R.lib()
+    apply_opts(a)
     ctx = R.Context(local)
     n = int((a.size_gib if a.size_gib != 16.0 else 4.0) * (1 << 30))
     B = R.block_length_for(n)
@@ -674,6 +690,8 @@ def main_receiver(a):
                    "matched_bytes": int(out.matched), "defer_write": 0,
                    "bound": "the Receiver's serial whole-file MD5 on the host (Receiver.java:824-842)"},
     }
+    if a.opt:
+        res["config"]["options"] = a.opt
     print(json.dumps(res), flush=True)
     ctx.close()
 

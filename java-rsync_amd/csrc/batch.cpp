@@ -19,6 +19,7 @@
 #include <thread>
 
 #include "ctx.h"
+#include "options.h"
 #include "host_md5.h"
 #include "resolver.h"
 
@@ -244,6 +245,7 @@ FileScan& scan_of(Batch* b, int32_t f) { return (*b->files)[(size_t)f]; }
 // "quota period"; containers often see every CPU of the machine in the mask but get a few cores' worth of
 // time).  More spinning workers than that get throttled by the scheduler for whole periods.
 int host_cores() {
+    if (const int64_t o = opt(OPT_HOST_CORES); o > 0) return (int)o;  // explicit override (options.h)
     static const int v = [] {
         int n = 8;
         cpu_set_t cpus;
@@ -257,7 +259,6 @@ int host_cores() {
             }
             fclose(f);
         }
-        if (const char* e = getenv("RSH_HOST_CORES")) n = std::max(1, atoi(e));  // explicit override
         return n;
     }();
     return v;
@@ -267,15 +268,9 @@ int64_t BatchBackend::aligned_count() { return (head || !b->aligned.load(std::me
 
 // Round hand-offs: a blocked thread takes ~50 us to wake from a condition variable, once per round per
 // side (coordinator -> workers, last worker -> coordinator).  Waiters spin up to RSH_BATCH_SPIN us
-// (default 200; 0 = block at once) on the predicate first, then block as before; the predicate is
-// re-checked under the mutex either way, so the hand-off protocol is unchanged.
-int spin_us() {
-    static const int v = [] {
-        const char* e = getenv("RSH_BATCH_SPIN");
-        return e ? std::max(0, atoi(e)) : 200;
-    }();
-    return v;
-}
+// (option batch_spin_us, default 200; 0 = block at once) on the predicate first, then block as before; the
+// predicate is re-checked under the mutex either way, so the hand-off protocol is unchanged.
+int spin_us() { return (int)std::max<int64_t>(0, opt(OPT_BATCH_SPIN_US)); }
 template <class Pred>
 void spin_wait(Pred pred) {
     const int us = spin_us();
@@ -359,16 +354,10 @@ void BatchBackend::flush_gather(const int64_t* tpos, int64_t nt, int32_t* tv, co
     b->post(fs);
 }
 
-// bytes copied per window request (A/B switch RSH_BATCH_READAHEAD; never less than the window).  Off by
+// bytes copied per window request (A/B option batch_readahead; never less than the window).  Off by
 // default: on config 4 it cut the rounds from 23 to 18, but the head-mode rounds it removed were cheap
 // window copies and the probes left in their place wait behind the speculation K1
-int64_t readahead_bytes() {
-    static const int64_t v = [] {
-        const char* e = getenv("RSH_BATCH_READAHEAD");
-        return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)0;
-    }();
-    return v;
-}
+int64_t readahead_bytes() { return std::max<int64_t>(0, opt(OPT_BATCH_READAHEAD)); }
 
 void BatchBackend::md5_at(int64_t p, uint8_t out[16]) {
     const int64_t w = std::min<int64_t>(B, n - p);
@@ -689,7 +678,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     std::vector<K1Plan> plans;
     std::vector<K1Lane> lanes;
     int lane_align = 16;
-    bool partial = tail_gather_on() && !batch_quad();
+    bool partial = tail_gather_on();
     uint32_t ngroups = plan_block_sums_files(k1.data(), NF, &plans, &lanes, &lane_align, &partial);
     RSH_BHIP(S->k1_groups.ensure(((size_t)ngroups + 1) * sizeof(K1Group)));
     RSH_BHIP(S->k1_plans.ensure((plans.size() + 1) * sizeof(K1Plan)));
@@ -771,8 +760,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     }
     // the speculation K1 waits for the lead sums only (a VALU-heavy kernel beside it slows the waves that share
     // its SIMDs, and the slowest wave ends the launch); the tables' download and the probe hashes follow it on
-    // the context stream and run beside the speculation (RSH_SCAN_SPEC_ORDER=0, A/B: all of it beside)
-    static const bool spec_after_prep = !getenv("RSH_SCAN_SPEC_ORDER") || atoi(getenv("RSH_SCAN_SPEC_ORDER")) != 0;
+    // the context stream and run beside the speculation (option scan_spec_order = 0, A/B: all of it beside)
+    const bool spec_after_prep = opt(OPT_SCAN_SPEC_ORDER) != 0;
     if (spec_after_prep) RSH_BHIP(hipEventRecord(c->ev_prep, st));
     // (stream) the received tables, to pinned host memory in one kernel
     CopyEnt* tc = S->h_copies.as<CopyEnt>();
@@ -787,9 +776,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         max_tab = std::max<int64_t>(max_tab, (int64_t)fs.C * 4);
     }
     // with the speculation after the lead sums, the table work below runs beside its K1: background launches
-    // (priority 0, a few hundred workgroups; the download is PCIe-bound anyway).  RSH_BATCH_PREP=all (A/B): the
-    // speculation after all of it, full-width launches.
-    static const bool prep_all = getenv("RSH_BATCH_PREP") && strcmp(getenv("RSH_BATCH_PREP"), "all") == 0;
+    // (priority 0, a few hundred workgroups; the download is PCIe-bound anyway).  Option batch_prep_all = 1
+    // (A/B): the speculation after all of it, full-width launches.
+    const bool prep_all = opt(OPT_BATCH_PREP_ALL) != 0;
     const bool bg = spec_after_prep && !prep_all;
     RSH_BHIP(launch_copy_many(tc, ntc, max_tab, st, bg));  // stream order: after whatever produced them
     RSH_BHIP(hipEventRecord(c->ev_tab, st));
@@ -827,7 +816,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         int32_t dropped = 0;
         for (FileScan& fs : files)
             if (fs.done) fs.cancelled = true, ++dropped;
-        if (getenv("RSH_SCAN_TRACE"))
+        if (opt(OPT_SCAN_TRACE))
             fprintf(stderr, "[rsh-batch] speculation launched: %u groups, %d resolved files dropped\n", ngroups, dropped);
         if (!S->ev_scopy) RSH_BHIP(hipEventCreateWithFlags(&S->ev_scopy, hipEventDisableTiming));
         if (S->scopy_pending) RSH_BHIP(hipEventSynchronize(S->ev_scopy));  // the previous scan's upload is done
@@ -895,18 +884,19 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         return RSH_OK;
     };
 
-    // policy (A/B via RSH_BATCH_SPEC; the default, measured best on config 4, is head mode with the launch
-    // after kDeferRounds rounds): "early" = the speculation's K1 starts now, beside whatever the device is
-    // still doing (e.g. the Generator), resolvers in head mode until it lands; "wait" = as early, but the
-    // resolvers start only once it has landed; a number N = launch after N rounds
-    static const char* pol = getenv("RSH_BATCH_SPEC");
-    static const bool wait_spec = pol && strcmp(pol, "wait") == 0;
-    static const bool early_spec = pol && (strcmp(pol, "early") == 0 || wait_spec);
-    static const int defer_rounds = (pol && !early_spec) ? atoi(pol) : kDeferRounds;
+    // policy (A/B via option batch_spec; the default (-1), measured best on config 4, is head mode with the
+    // launch after kDeferRounds rounds): -2 "early" = the speculation's K1 starts now, beside whatever the
+    // device is still doing (e.g. the Generator), resolvers in head mode until it lands; -3 "wait" = as
+    // early, but the resolvers start only once it has landed; N >= 0 = launch after N rounds
+    const int64_t pol_v = opt(OPT_BATCH_SPEC);
+    const bool pol = pol_v != -1;
+    const bool wait_spec = pol_v == -3;
+    const bool early_spec = pol_v == -2 || wait_spec;
+    const int defer_rounds = (pol && !early_spec) ? (int)std::max<int64_t>(0, pol_v) : kDeferRounds;
     // launch-then-confirm (default policy): the speculation K1 is launched now, behind the Generator's work;
     // the lead check below keeps it for the files whose first windows carry their chunks' sums (they wait for
     // it instead of taking head-mode rounds) or stops it when no file qualifies
-    static const bool early_on = !getenv("RSH_SCAN_EARLY") || atoi(getenv("RSH_SCAN_EARLY")) != 0;  // A/B
+    const bool early_on = opt(OPT_SCAN_EARLY) != 0;  // A/B
     const bool tentative = !pol && early_on && nlead_all > 0;
     if (early_spec || tentative) {
         const int r = launch_spec_k1();
@@ -917,7 +907,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     RSH_BHIP(hipStreamSynchronize(st));
     const double setup_ms = ms_since(t0);
 
-    static const bool trace = getenv("RSH_SCAN_TRACE") != nullptr;
+    const bool trace = opt(OPT_SCAN_TRACE) != 0;
     int spec_rc = RSH_OK;
     bool spec_launched = false;
     int32_t nwait = 0;
@@ -952,7 +942,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         if (spec_rc != RSH_OK) return spec_rc;
         spec_launched = true;
         RSH_BHIP(hipEventSynchronize(c->ev_spec));
-        if (getenv("RSH_SCAN_TRACE")) fprintf(stderr, "[rsh-batch] speculation landed at %.3f ms\n", ms_since(t0));
+        if (trace) fprintf(stderr, "[rsh-batch] speculation landed at %.3f ms\n", ms_since(t0));
         b.landed.store(true);
         b.aligned.store(true);
         for (FileScan& fs : files) fs.be.head = false;
@@ -1204,7 +1194,7 @@ int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t
     std::vector<K1Plan> plans;
     std::vector<K1Lane> lanes;
     int lane_align = 16;
-    bool partial = tail_gather_on() && !batch_quad();
+    bool partial = tail_gather_on();
     const uint32_t ngroups =
         plan_block_sums_files(files.data(), (int32_t)files.size(), &plans, &lanes, &lane_align, &partial);
     RSH_BHIP(S->g_groups.ensure(((size_t)ngroups + 1) * sizeof(K1Group)));

@@ -18,6 +18,8 @@
 #include "rsync_hip.h"
 
 #include "ctx.h"
+#include "options.h"
+#include "rsync_hip_debug.h"
 
 namespace {
 // ------------------------------------------------------------------------------------------------
@@ -25,28 +27,24 @@ namespace {
 // ------------------------------------------------------------------------------------------------
 constexpr size_t kFirstSlots = 1024;
 constexpr int kScanWindows = 2;  // hit windows per probe in the single-file scan (hit_cache.h)
-// Head mode launches the aligned speculation after this many resolver steps or milliseconds ...
+// Head mode launches the aligned speculation after scan_defer_steps (4) resolver steps or scan_defer_us (500 us;
+// options.h) ...
 constexpr int64_t kChainSteps = 2;  // ... after this many steps when the last event is a run of matches
-constexpr int64_t kDeferSteps = 4;
-constexpr double kDeferMs = 0.5;
 // ... or at once when the first kLeadWindows (ctx.h) aligned source windows all carry chunk k's weak sum
-// ... over the windows up to the last of kSampleWindows evenly spaced samples that still carries its chunk's sum
-constexpr int64_t kSampleWindows = 256;  // (1024 until round 2: the same step time, r2_ab2; RSH_SCAN_SAMPLES A/B)
+// ... over the windows up to the last of scan_samples (256; 1024 until round 2: the same step time, r2_ab2)
+// evenly spaced samples that still carries its chunk's sum
 // windows one K1 launch digests in a single round of waves (2 waves/SIMD x 1024 SIMDs x 64 lanes): below this a
 // launch over fewer windows is no faster
 constexpr int64_t kRoundWindows = 131072;
 // rsh_match_scan_tiled: default tile (the device holds one tile + a 16 B halo of the source at a time)
 constexpr int64_t kDefaultTile = 4LL << 30;
 
-// RSH_SCAN_TRACE=1: one stderr line per resolver round trip (diagnostics).
+// Option scan_trace = 1: one stderr line per resolver round trip (diagnostics).
 struct CallTrace {
     const char* what;
     int64_t arg;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-    static bool on() {
-        static const bool v = getenv("RSH_SCAN_TRACE") != nullptr;
-        return v;
-    }
+    static bool on() { return rsh::opt(rsh::OPT_SCAN_TRACE) != 0; }
     CallTrace(const char* w, int64_t a) : what(w), arg(a) {}
     ~CallTrace() {
         if (on()) fprintf(stderr, "[rsh] %-10s %10lld %9.3f ms\n", what, (long long)arg, ms_since(t0));
@@ -439,10 +437,7 @@ class HipBackend : public rsh::ScanBackend {
         ph_s0_ = -1;
         ph_landed_ = false;
     }
-    static bool phase_on() {  // A/B switch: RSH_SCAN_PHASE=0 turns the phase-shifted speculation off
-        static const bool v = !getenv("RSH_SCAN_PHASE") || atoi(getenv("RSH_SCAN_PHASE")) != 0;
-        return v;
-    }
+    static bool phase_on() { return rsh::opt(rsh::OPT_SCAN_PHASE) != 0; }  // A/B: 0 = no phase speculation
 
   private:
     static constexpr int64_t kPhaseMinWindows = 8;    // shorter remainders resolve faster on the generic path
@@ -562,8 +557,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     RSH_HIP(c->h_segs.ensure(seg_bytes));
     // sample windows for the launch decision: the first nlead, then one every `stride` windows
     const int64_t nlead = std::min<int64_t>(kLeadWindows, nf);
-    static const int64_t nsamples = getenv("RSH_SCAN_SAMPLES") ? std::max(1, atoi(getenv("RSH_SCAN_SAMPLES")))
-                                                              : kSampleWindows;  // A/B
+    const int64_t nsamples = std::max<int64_t>(1, rsh::opt(rsh::OPT_SCAN_SAMPLES));
     const int64_t stride = std::max<int64_t>(1, (nf + nsamples - 1) / nsamples);
     std::vector<int64_t> samp;
     for (int64_t k = 0; k < nlead; ++k) samp.push_back(k);
@@ -576,18 +570,18 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     RSH_HIP(hipEventRecord(c->ev_in, c->stream));  // whatever produced the inputs on the caller's stream
     // (aux) the aligned speculation: the source's own block sums with the basis header's B and dl,
     // the chain flags, and their download.  It is a bet on long runs of aligned matches; in head mode it
-    // is launched only once the resolver has taken kDeferSteps steps or kDeferMs without finishing
+    // is launched only once the resolver has taken scan_defer_steps steps or scan_defer_us without finishing
     // (until then the resolver's round trips run on an otherwise idle device: a range probe beside the
     // speculation takes ~0.16 ms instead of tens of microseconds).
     int gen = ++c->gen;  // a stopped speculation's generation; a later launch takes a new one
-    static const int diag = getenv("RSH_SCAN_DIAG") ? atoi(getenv("RSH_SCAN_DIAG")) : 0;  // A/B switches
+    const int diag = (int)rsh::opt(rsh::OPT_SCAN_DIAG);  // diagnostics (options.h)
     int64_t spec_na = na;  // windows the speculation covers: all, or a prefix (sampled launch decision)
     // The speculation K1 starts after the sample kernels on the context stream (window 0's copy and the lead and
     // sample weak sums, ~50 us) rather than beside them: every K1 wave holds its SIMD for the whole launch, so
     // the waves that share their SIMDs with a VALU-heavy kernel set the launch's end (r2: 3.13 ms ordered
-    // against 3.40-3.49 ms beside them; the step 6.48-6.58 against 6.67 ms).  RSH_SCAN_SPEC_ORDER=0 (A/B, read
-    // per scan): beside them.
-    const bool spec_after_prep = !getenv("RSH_SCAN_SPEC_ORDER") || atoi(getenv("RSH_SCAN_SPEC_ORDER")) != 0;
+    // against 3.40-3.49 ms beside them; the step 6.48-6.58 against 6.67 ms).  Option scan_spec_order = 0 (A/B):
+    // beside them.
+    const bool spec_after_prep = rsh::opt(rsh::OPT_SCAN_SPEC_ORDER) != 0;
     bool prep_recorded = false;
     auto launch_spec = [&]() -> int {
         const int64_t sn = std::min<int64_t>(n, spec_na * B);  // bytes: whole windows, or to the end
@@ -612,7 +606,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     };
     const bool head = !(diag & 1);
     bool spec_launched = false;
-    if (!head || (diag & 4)) {  // RSH_SCAN_DIAG bit 2: launch at once even in head mode (A/B)
+    if (!head || (diag & 4)) {  // scan_diag bit 2: launch at once even in head mode (A/B)
         const int rc = launch_spec();
         if (rc != RSH_OK) return rc;
         spec_launched = true;
@@ -659,7 +653,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // the lead decides on below is launched now, before the host knows the table, so it starts the moment the
     // Generator's work ends on the device; the lead check then keeps it or stops it (its waves leave after
     // their first two stages).  Larger sources wait for the samples (the launch may cover a prefix only).
-    static const bool early_on = !getenv("RSH_SCAN_EARLY") || atoi(getenv("RSH_SCAN_EARLY")) != 0;  // A/B
+    const bool early_on = rsh::opt(rsh::OPT_SCAN_EARLY) != 0;  // A/B
     bool spec_tentative = false, tentative_stopped = false;
     if (head && !spec_launched && nlead > 0 && early_on && na <= kRoundWindows &&
         (nlead >= kLeadWindows || nlead == nf)) {
@@ -703,11 +697,11 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     bool spec_wait = false;
     int64_t run_last = -1, run_miss = -1;  // a sampled run's last matching window, the first sample past it
     bool defer_prefix = false;             // the prefix speculation waits for the phase guess (below)
-    // A/B switches, read per scan (tests flip them)
-    const bool guess_on = !getenv("RSH_SCAN_PHASE_GUESS") || atoi(getenv("RSH_SCAN_PHASE_GUESS")) != 0;
-    const bool seg_on = !getenv("RSH_SCAN_SEGMENTED") || atoi(getenv("RSH_SCAN_SEGMENTED")) != 0;
-    static const bool wait_on = !getenv("RSH_SCAN_WAIT") || atoi(getenv("RSH_SCAN_WAIT")) != 0;  // A/B
-    static const bool sample_on = !getenv("RSH_SCAN_SAMPLE") || atoi(getenv("RSH_SCAN_SAMPLE")) != 0;  // A/B
+    // A/B switches (options.h; tests flip some of them)
+    const bool guess_on = rsh::opt(rsh::OPT_SCAN_PHASE_GUESS) != 0;
+    const bool seg_on = rsh::opt(rsh::OPT_SCAN_SEGMENTED) != 0;
+    const bool wait_on = rsh::opt(rsh::OPT_SCAN_WAIT) != 0;
+    const bool sample_on = rsh::opt(rsh::OPT_SCAN_SAMPLE) != 0;
     if (head && nlead > 0 && (!spec_launched || spec_tentative)) {
         int64_t lead = 0;
         while (lead < nlead && lead_w[lead] == host_weak[lead]) ++lead;
@@ -912,8 +906,8 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                     // its own sum is not known and the probe starts there).  Asked now, beside the launch, its
                     // answer and the window at the hit are in the backend's hit cache when the speculation
                     // lands, instead of a round trip after it (0.17-0.19 ms on the shift case).  Unused (and
-                    // harmless) when the resolver asks elsewhere.  RSH_SCAN_PREPROBE=0 (A/B, per scan).
-                    const bool preprobe = !getenv("RSH_SCAN_PREPROBE") || atoi(getenv("RSH_SCAN_PREPROBE")) != 0;
+                    // harmless) when the resolver asks elsewhere.  Option scan_preprobe = 0 (A/B).
+                    const bool preprobe = rsh::opt(rsh::OPT_SCAN_PREPROBE) != 0;
                     const int64_t last = n - (h->remainder > 0 ? h->remainder : B);
                     const int64_t pa = P * B, pstop = std::min(P * B + 9 * B, last);
                     if (preprobe && P * B + 10 * B <= n && pa <= pstop && be.err == hipSuccess) {
@@ -948,9 +942,8 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         if (be.err != hipSuccess || !be.head) return true;
         CallTrace tr("ev_query", res->stats.head_steps);
         if (!spec_launched) {
-            static const int64_t defer_steps = getenv("RSH_SCAN_DEFER_STEPS") ? atoll(getenv("RSH_SCAN_DEFER_STEPS"))
-                                                                            : kDeferSteps;  // A/B
-            static const double defer_ms = getenv("RSH_SCAN_DEFER_MS") ? atof(getenv("RSH_SCAN_DEFER_MS")) : kDeferMs;
+            const int64_t defer_steps = rsh::opt(rsh::OPT_SCAN_DEFER_STEPS);
+            const double defer_ms = (double)rsh::opt(rsh::OPT_SCAN_DEFER_US) / 1e3;
             // chain evidence: the scan just matched consecutive chunks, so long aligned runs are likely and
             // the speculation pays; otherwise (e.g. a false weak hit that poisons the digest, after which
             // the scan ends in closed form) it waits a little longer
@@ -1485,6 +1478,24 @@ int rsh_memcpy_d2h(rsh_ctx* ctx, void* dst, const void* src, int64_t bytes) {
     RSH_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, ctx->stream));
     RSH_HIP(hipStreamSynchronize(ctx->stream));
     return RSH_OK;
+}
+
+int rsh_debug_set_option(const char* name, int64_t value) {
+    const int i = rsh::opt_index(name);
+    if (i < 0) return RSH_E_INVAL;
+    rsh::opt_table()[i].store(value, std::memory_order_relaxed);
+    return RSH_OK;
+}
+
+int rsh_debug_get_option(const char* name, int64_t* value) {
+    const int i = rsh::opt_index(name);
+    if (i < 0 || !value) return RSH_E_INVAL;
+    *value = rsh::opt((rsh::Opt)i);
+    return RSH_OK;
+}
+
+void rsh_debug_reset_options(void) {
+    for (int i = 0; i < rsh::OPT_COUNT; ++i) rsh::opt_table()[i].store(rsh::opt_info()[i].def, std::memory_order_relaxed);
 }
 
 int rsh_fill_splitmix_device(rsh_ctx* ctx, void* d_out, int64_t n, uint64_t key, int64_t byte_offset) {

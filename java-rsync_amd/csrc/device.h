@@ -17,9 +17,13 @@ hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint3
                              uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s,
                              const int* abort_flag = nullptr, int abort_gen = 0);
 
+#ifdef RSH_KBENCH
+// kbench only (tools/kbench.cpp, built with -DRSH_KBENCH): the K1 instantiations measured against the production
+// one (variant -1 = production; the numbers are kbench's).  librsynchip.so contains the production kernels only.
 hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks,
                                      uint32_t dl, uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong,
                                      hipStream_t s, const int* abort_flag = nullptr, int abort_gen = 0);
+#endif
 
 // Batched files (a segment's files in one launch; Generator.java:558-614 / Sender.sendFiles :1098-1148).
 // K1File: one file's chunk set.  plan_block_sums_batch cuts every file into waves of 64 chunks: the
@@ -90,16 +94,17 @@ struct K1Plan {
 };
 // plans (one per file with groups, ascending g0) and the host lanes; returns the total group count.  A file's
 // full-length chunks past its last full wave form a partial group (K1Group::count < 64) when *partial is set
-// on entry (RSH_K1_GATHER, not with the 4-waves kernel); on return *partial says whether any plan has one.
+// on entry (option k1_gather); on return *partial says whether any plan has one.
 uint32_t plan_block_sums_files(const K1File* files, int32_t nfiles, std::vector<K1Plan>* plans,
                                std::vector<K1Lane>* lanes, int* lane_align, bool* partial = nullptr);
 hipError_t launch_expand_groups(const K1Plan* d_plans, uint32_t nplans, uint32_t ngroups, K1Group* d_groups,
                                 hipStream_t s);
-// the same over groups only, at 4 waves per SIMD (block_sums_quad_kernel; A/B: RSH_K1_QUAD=1, kbench 1004)
+#ifdef RSH_KBENCH
+// the same over groups only, at 4 waves per SIMD (block_sums_quad_kernel; kbench 1004: not adopted)
 hipError_t launch_block_sums_batch_quad(const K1Group* d_groups, uint32_t ngroups, uint32_t seed_word, hipStream_t s,
                                         const int* abort_flag = nullptr, int abort_gen = 0);
-bool batch_quad();
-bool tail_gather_on();  // RSH_K1_GATHER=0 (A/B, read per call): leftover chunks one per lane, no gathered waves  // RSH_K1_QUAD=1 (A/B): the batched groups at 4 waves per SIMD
+#endif
+bool tail_gather_on();  // option k1_gather = 0: leftover chunks one per lane, no gathered waves
 // partial: some groups have count < 64 (plan_block_sums_files) -- they run as gathered waves of the same launch
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
                                    int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag = nullptr,

@@ -10,6 +10,7 @@
 
 #include "device.h"
 #include "md5_core.h"
+#include "options.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -790,10 +791,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
     block_sums_pipe_body<8, ABORT, true, 0, false>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
                                                    nullptr, n, nchunks, main_waves);
 }
-bool tail_gather_on() {  // RSH_K1_GATHER=0 (A/B, read per launch): leftover chunks one per lane
-    const char* gm = getenv("RSH_K1_GATHER");
-    return !gm || atoi(gm) != 0;
-}
+bool tail_gather_on() { return opt(OPT_K1_GATHER) != 0; }  // 0: leftover chunks one per lane (options.h)
+#ifdef RSH_KBENCH
 // kbench A/B (variant 61): MD5F == 9 holds the 64 K constants in VGPRs (176 + 64 registers, still 2 waves/SIMD)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void block_sums_pipe_k3_kernel(
     const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
@@ -801,7 +800,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
     block_sums_pipe_body<9, true, true, 0, false>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
                                                   nullptr, 0, 0, 0xFFFFFFFFu);
 }
+#endif
 
+#ifdef RSH_KBENCH  // not adopted: kbench only
 // ------------------------------------------------------------------------------------------------
 // K1 at 4 waves per SIMD (batched groups, one K1Group per wave).  A wave issues at most one VALU
 // instruction per ~2.7 SIMD slots of a full-rate op, so two waves leave a SIMD's VALU a quarter idle and
@@ -952,6 +953,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     g.weak[l] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
     store_digest(g.strong + (size_t)l * dl, st, dl);
 }
+
+#endif  // RSH_KBENCH
 
 #ifndef RSH_K1_SHIFT_VGPR
 #define RSH_K1_SHIFT_VGPR 256  // 2 waves/SIMD (the LDS ring and the MFMA tiles of the aligned kernel, plus the funnel)
@@ -1227,7 +1230,7 @@ hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const 
     if (nseg + ntail == 0) return hipSuccess;
     // gathered waves for the full-length tails when that adds no wave (the launch fills the chip's 2048 wave
     // slots exactly in the bench's shift case: one more wave would start only when another finished).
-    // RSH_K1_GATHER=0 (A/B, read per launch): every tail per lane.
+    // Option k1_gather = 0: every tail per lane.
     const bool gather_on = tail_gather_on();
     const int* never = never_word();
     uint32_t ngf = 0;
@@ -1235,25 +1238,31 @@ hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const 
         (nfull + 63) / 64 + (ntail - nfull + 63) / 64 == (ntail + 63) / 64)
         ngf = nfull;
     const uint32_t waves = nseg + (ngf + 63) / 64 + (ntail - ngf + 63) / 64;
-    // tail lanes (A/B, read per launch: RSH_K1_TAIL=1 (default) dword loads + funnel, 0 wide aligned loads + a
-    // per-lane select, 2 plain unaligned dwordx4).  kbench, 2047 coalesced waves + one tail wave of 64 chunks
-    // at offset 1: 3.70-3.75 / 4.13-4.19 / 4.19-4.28 ms (3.33 ms without the tail wave)
-    const char* tm = getenv("RSH_K1_TAIL");
-    const int mode = tm ? atoi(tm) : 1;
     // LDS: the shift wave's ring (64 rows of 17 slots); a gathered wave's two 9-slot buffers when there is one
     const size_t lb = ngf > 0 ? 2 * 64 * 9 * sizeof(uint4) : 64 * 17 * sizeof(uint4);
-    if (mode == 1)
-        hipLaunchKernelGGL(block_sums_seg_kernel<1>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
-                           seed_word, ngf, never);
-    else if (mode == 2)
+#ifdef RSH_KBENCH
+    // tail lanes (kbench A/B: RSH_K1_TAIL=1 (production) dword loads + funnel, 0 wide aligned loads + a per-lane
+    // select, 2 plain unaligned dwordx4).  2047 coalesced waves + one tail wave of 64 chunks at offset 1:
+    // 3.70-3.75 / 4.13-4.19 / 4.19-4.28 ms (3.33 ms without the tail wave)
+    const char* tm = getenv("RSH_K1_TAIL");
+    const int mode = tm ? atoi(tm) : 1;
+    if (mode == 2) {
         hipLaunchKernelGGL(block_sums_seg_kernel<2>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
                            seed_word, ngf, never);
-    else
+        return hipGetLastError();
+    }
+    if (mode == 0) {
         hipLaunchKernelGGL(block_sums_seg_kernel<0>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
                            seed_word, ngf, never);
+        return hipGetLastError();
+    }
+#endif
+    hipLaunchKernelGGL(block_sums_seg_kernel<1>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
+                       seed_word, ngf, never);
     return hipGetLastError();
 }
 
+#ifdef RSH_KBENCH  // not adopted: kbench only
 // ------------------------------------------------------------------------------------------------
 // K1 (LDS-DMA): as the coalesced kernel, but each stage goes HBM -> LDS directly with
 // global_load_lds_dwordx4 (no VGPR staging, no ds_write).  LDS-DMA writes lane l's 16 B at slot
@@ -1327,6 +1336,8 @@ __global__ __launch_bounds__(64) void block_sums_dma_kernel(const uint8_t* __res
     store_digest(strong_out + (size_t)c * dl, st, dl);
 }
 
+#endif  // RSH_KBENCH
+
 // MD5 step form of the production K1: 0 compiler, 1 one asm statement per step, 2 generated blocks
 // (tools/gen_md5_asm.py)
 constexpr int kMd5Form = 2;
@@ -1340,22 +1351,32 @@ void allow_full_lds(K kernel) {
                               (int)kLdsPerCU);
 }
 
-// variant: -1 = production choice; 0..2 per-lane (NT PF4, plain PF4, NT PF8); 3..6 coalesced
-// (D=2 NT, D=3 NT, D=2 plain, D=4 NT).  Non-coalesced variants handle every chunk shape.
-// RSH_K1_PIN_ALL=0 (A/B): K1 launches of more than 2048 waves (single and batched) without the occupancy
+// variant: -1 = production choice (19: the pipelined K1 with its tail and shift forms, the coalesced kernel above
+// B = 128 KiB, the per-lane kernel for other shapes).  The other variants exist in the kbench build only
+// (RSH_KBENCH): 0..2 per-lane (NT PF4, plain PF4, NT PF8); 3..6 coalesced (D=2 NT, D=3 NT, D=2 plain, D=4 NT),
+// and the numbered A/Bs below.  Non-coalesced variants handle every chunk shape.
+#ifdef RSH_KBENCH
+// RSH_K1_PIN_ALL=0 (kbench A/B): K1 launches of more than 2048 waves (single and batched) without the occupancy
 // pin -- the coalesced kernel for single files, the unpinned pipelined instantiation for batches
 static bool pin_all() {
     static const bool v = !(getenv("RSH_K1_PIN_ALL") && atoi(getenv("RSH_K1_PIN_ALL")) == 0);
     return v;
 }
 static bool batch_pin() { return pin_all(); }
+#else
+static bool pin_all() { return true; }
+#endif
 
+#ifndef RSH_KBENCH
+static
+#endif
 hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks,
                                      uint32_t dl, uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong,
                                      hipStream_t s, const int* abort_flag, int abort_gen) {
     if (nchunks == 0) return hipSuccess;
     const uintptr_t addr = reinterpret_cast<uintptr_t>(d_data);
     if (variant < 0) variant = 19;  // coalesced, 2 stages in flight, weak sums on the matrix pipe
+#ifdef RSH_KBENCH
     if (variant == 3000 || variant == 3001 || variant == 3002) {  // kbench A/B: the per-lane path at any base
         if (variant == 3002)
             hipLaunchKernelGGL((block_sums_kernel<2, 4, false>), dim3((nchunks + 63) / 64), dim3(64), 0, s, d_data, n,
@@ -1368,6 +1389,7 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                                B, nchunks, dl, seed_word, d_weak, d_strong, 0u);
         return hipGetLastError();
     }
+#endif
     uint32_t c_first = 0;
     const bool deep = variant == 4 || variant == 6 || variant == 7 || variant == 9 || variant == 10 ||
                       variant == 11 || variant == 12 || variant == 14 || variant == 15 || variant == 16 ||
@@ -1375,16 +1397,13 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
     // The pipelined K1 also runs at base addresses that are not 16-B aligned (the phase-shifted speculation
     // starts at src + s for any s): its dwordx4 buffer loads then straddle 16-B boundaries, which gfx950
     // serves in its unaligned access mode (bit-exact against the oracle at offsets 0..15,
-    // test_k1_unaligned_base).  RSH_K1_UNALIGNED=0 (A/B, read per launch) sends such bases to the per-lane
-    // kernel instead.
-    const char* ua = getenv("RSH_K1_UNALIGNED");
-    const bool unaligned_ok = !ua || atoi(ua) != 0;
+    // test_k1_unaligned_base).  Option k1_unaligned = 0 (test) sends such bases to the per-lane kernel instead.
+    const bool unaligned_ok = opt(OPT_K1_UNALIGNED) != 0;
     // A base that is not 128-B aligned goes to the line-aligned shift kernel when the lines it reads around the
-    // data -- a bytes before it, up to 128 - a after the last full wave -- lie in the same allocation
-    // (RSH_K1_SHIFT=0, read per launch: the pipelined kernel at the unaligned base, A/B).
-    const char* sk = getenv("RSH_K1_SHIFT");
+    // data -- a bytes before it, up to 128 - a after the last full wave -- lie in the same allocation (option
+    // k1_shift = 0, test: the pipelined kernel at the unaligned base, its path when the lines do not fit).
     if (variant == 19 && (addr % 128) != 0 && (B % 128) == 0 && (B >> 7) >= 4 && (B >> 7) <= 1024 && abort_flag &&
-        !(sk && atoi(sk) == 0)) {
+        opt(OPT_K1_SHIFT) != 0) {
         hipDeviceptr_t lo = nullptr;
         size_t size = 0;
         const uint32_t a = (uint32_t)(addr % 128);
@@ -1433,6 +1452,7 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
         const uint32_t waves = nfullc / 64;
         const uint32_t nst = B >> 7;
         const size_t wave_lds = 64 * 9 * sizeof(uint4);
+#ifdef RSH_KBENCH
         // LDS per workgroup chosen so that the dispatcher can place at most ceil(groups / CUs) groups
         // on a CU: every SIMD then holds the same number of equal-work waves (no stacking imbalance).
         auto lds_for = [&](uint32_t groups, uint32_t waves_per_group) -> size_t {
@@ -1455,7 +1475,10 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
             }
             c_first = groups * 256;
             variant = 0;
-        } else if (waves > 0) {
+        } else
+#endif
+        if (waves > 0) {
+#ifdef RSH_KBENCH
             const size_t lb = variant == 9 ? lds_for(waves, 1) : wave_lds;
             switch (variant) {
                 case 3:
@@ -1492,6 +1515,9 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     }
                     break;
                 case 19:
+#else
+            const size_t lb = wave_lds;
+#endif
                     // the pipelined K1 at any wave count (occupancy pinned to 2 waves/SIMD; beyond 2048 waves they
                     // run in rounds): measured 3.19 vs 3.96 ms for 16 GiB at B = 64 KiB (4096 waves) against the
                     // unpinned instantiation, and ahead of the coalesced kernel at every size
@@ -1512,7 +1538,9 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                                            2 * wave_lds, s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag,
                                            abort_gen, nullptr, n, nchunks, waves);
                         return hipGetLastError();
-                    } else if (nst <= 1024 && nst >= 4 && (waves <= 2 * 4 * kCUs || pin_all())) {
+                    }
+#ifdef RSH_KBENCH
+                    else if (nst <= 1024 && nst >= 4 && (waves <= 2 * 4 * kCUs || pin_all())) {
                         hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true>), dim3(waves), dim3(64), 2 * wave_lds,
                                            s, d_data, B, dl, seed_word, d_weak, d_strong);
                     } else if (nst <= 1024 && abort_flag && waves <= 2 * 4 * kCUs) {
@@ -1531,10 +1559,13 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     } else if (nst <= 1024) {
                         hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true>), dim3(waves), dim3(64),
                                            lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    } else {
+                    }
+#endif
+                    else {  // B > 128 KiB (the Generator of a file above 2^34 bytes, config 3): the coalesced K1
                         hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true>), dim3(waves), dim3(64), lb, s, d_data,
                                            B, dl, seed_word, d_weak, d_strong);
                     }
+#ifdef RSH_KBENCH
                     break;
                 case 20:
                     hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, false>), dim3(waves),
@@ -1705,6 +1736,7 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true>), dim3(waves), dim3(64), lb, s, d_data, B,
                                        dl, seed_word, d_weak, d_strong);
             }
+#endif
             c_first = waves * 64;
         }
         variant = 0;
@@ -1714,6 +1746,7 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
     const dim3 block(64);
     const dim3 grid((rest + 63) / 64);
     if ((B % 16) == 0 && (addr % 16) == 0) {
+#ifdef RSH_KBENCH
         if (variant == 1)
             hipLaunchKernelGGL((block_sums_kernel<16, 4, false>), grid, block, 0, s, d_data, n, B, nchunks, dl,
                                seed_word, d_weak, d_strong, c_first);
@@ -1721,6 +1754,7 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
             hipLaunchKernelGGL((block_sums_kernel<16, 8, true>), grid, block, 0, s, d_data, n, B, nchunks, dl,
                                seed_word, d_weak, d_strong, c_first);
         else
+#endif
             hipLaunchKernelGGL((block_sums_kernel<16, 4, true>), grid, block, 0, s, d_data, n, B, nchunks, dl,
                                seed_word, d_weak, d_strong, c_first);
     } else if ((B % 4) == 0 && (addr % 4) == 0) {
@@ -1844,7 +1878,7 @@ hipError_t launch_expand_groups(const K1Plan* d_plans, uint32_t nplans, uint32_t
 // process, same buffer): the plain instantiation 4.07-4.57 ms, the abortable one 2.99-3.10 ms (the plain one
 // with only the abortable loop's lgkmcnt(0) drain: 4.38 ms); round 1's boxes ran both at ~3.0 ms.  The word
 // must be uncached device memory like the contexts' abort words: polling a __device__ global instead (L2,
-// one line for every wave) made the launch 27.9 ms.  RSH_K1_PLAIN=1 (A/B) launches the plain one.
+// one line for every wave) made the launch 27.9 ms.  RSH_K1_PLAIN=1 (kbench A/B) launches the plain one.
 static const int* never_word() {
     static int* ptr[64] = {};
     int dev = 0;
@@ -1857,10 +1891,14 @@ static const int* never_word() {
     }
     return ptr[dev];
 }
+#ifdef RSH_KBENCH
 static bool plain_k1() {
     static const bool v = getenv("RSH_K1_PLAIN") && atoi(getenv("RSH_K1_PLAIN")) != 0;
     return v;
 }
+#else
+static bool plain_k1() { return false; }
+#endif
 
 // The batched K1 with its leftovers in the same launch: groups some of which are a file's partial last wave
 // (K1Group::count < 64: the gathered-wave path, one 64-bit pointer per 8-chunk row, lanes past the count store
@@ -1888,7 +1926,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
     }
     block_sums_pipe_body<8, true, true, 0, true>(nullptr, 0u, 0u, seed, nullptr, nullptr, abort_flag, abort_gen, groups);
 }
-bool batch_quad() {  // RSH_K1_QUAD=1 (A/B): the batched groups at 4 waves/SIMD
+#ifdef RSH_KBENCH
+bool batch_quad() {  // RSH_K1_QUAD=1 (kbench A/B): the batched groups at 4 waves/SIMD
     static const bool v = getenv("RSH_K1_QUAD") && atoi(getenv("RSH_K1_QUAD")) != 0;
     return v;
 }
@@ -1905,6 +1944,9 @@ hipError_t launch_block_sums_batch_quad(const K1Group* d_groups, uint32_t ngroup
         hipLaunchKernelGGL((block_sums_quad_kernel<false>), dim3(ngroups), dim3(64), lb, s, d_groups, seed_word, nullptr, 0);
     return hipGetLastError();
 }
+#else
+static bool batch_quad() { return false; }
+#endif
 
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
                                    int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag,
@@ -1928,12 +1970,15 @@ hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, co
                                seed_word, abort_flag, abort_gen);
         return hipGetLastError();
     }
+#ifdef RSH_KBENCH
     if (ngroups > 0 && quad) {
         const hipError_t e = launch_block_sums_batch_quad(d_groups, ngroups, seed_word, s, abort_flag, abort_gen);
         if (e != hipSuccess) return e;
         ngroups = 0;
     }
+#endif
     if (ngroups > 0) {
+#ifdef RSH_KBENCH
         if (abort_flag && batch_pin())
             hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true, 0, true>), dim3(ngroups), dim3(64), lb, s,
                                nullptr, 0u, 0u, seed_word, nullptr, nullptr, abort_flag, abort_gen, d_groups);
@@ -1946,6 +1991,11 @@ hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, co
         else
             hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, false, 0, true>), dim3(ngroups), dim3(64), lb, s,
                                nullptr, 0u, 0u, seed_word, nullptr, nullptr, nullptr, 0, d_groups);
+#else
+        if (!abort_flag) return hipErrorOutOfMemory;  // never_word() failed: no uncached word for the pinned K1
+        hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true, 0, true>), dim3(ngroups), dim3(64), lb, s, nullptr,
+                           0u, 0u, seed_word, nullptr, nullptr, abort_flag, abort_gen, d_groups);
+#endif
     }
     if (nlanes > 0) {
         if (lane_align == 16)
@@ -1961,8 +2011,12 @@ hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, co
 hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks, uint32_t dl,
                              uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s,
                              const int* abort_flag, int abort_gen) {
-    // RSH_K1_VARIANT (diagnostic A/B, off by default) replaces the production variant for non-abortable launches
+#ifdef RSH_KBENCH
+    // RSH_K1_VARIANT (kbench A/B) replaces the production variant for non-abortable launches
     static const int forced = getenv("RSH_K1_VARIANT") ? atoi(getenv("RSH_K1_VARIANT")) : -1;
+#else
+    constexpr int forced = -1;
+#endif
     if (!abort_flag && forced < 0 && !plain_k1() && (abort_flag = never_word()) != nullptr) abort_gen = -1;
     return launch_block_sums_variant(abort_flag ? -1 : forced, d_data, n, B, nchunks, dl, seed_word, d_weak, d_strong, s, abort_flag,
                                      abort_gen);

@@ -15,6 +15,7 @@
 
 #include "ctx.h"
 #include "host_md5.h"
+#include "options.h"
 
 namespace rsh {
 namespace {
@@ -188,9 +189,8 @@ int rsh_block_sums_file(rsh_ctx* ctx, const char* path, int64_t size, const rsh_
     return RSH_OK;
 }
 
-// Sources above this size are scanned tiled (scan_tiled): HBM then holds one kFileTile tile at a time.
-constexpr int64_t kFileTileAbove = 32LL << 30;
-constexpr int64_t kFileTile = 4LL << 30;
+// Sources above file_tile_above (options.h: 32 GiB) are scanned tiled (scan_tiled): HBM then holds one tile of
+// file_tile (4 GiB) at a time.
 
 namespace rsh {
 namespace {
@@ -252,7 +252,7 @@ int match_scan_file_tiled(rsh_ctx* ctx, int fd, const char* path, int64_t size, 
             }
             return hipSuccess;
         };
-        const int64_t tile = getenv("RSH_FILE_TILE") ? atoll(getenv("RSH_FILE_TILE")) : kFileTile;
+        const int64_t tile = opt(OPT_FILE_TILE);
         rc = scan_tiled(ctx, fill, size, h, ctx->weak.as<int32_t>(), ctx->strong.as<uint8_t>(), weak, strong, seed,
                         tile, r);
     }
@@ -278,8 +278,8 @@ int rsh_match_scan_file(rsh_ctx* ctx, const char* path, int64_t size, const rsh_
     if (h->block_length > 0 && C > 0 && (!weak || (!strong && dl > 0))) return RSH_E_INVAL;
     RSH_CLAIM(ctx);
     RSH_HIP(hipSetDevice(ctx->device));
-    // A/B and test switches (read per call): RSH_FILE_TILE_ABOVE (bytes) and RSH_FILE_TILE (tile bytes)
-    const int64_t tile_above = getenv("RSH_FILE_TILE_ABOVE") ? atoll(getenv("RSH_FILE_TILE_ABOVE")) : kFileTileAbove;
+    // test switches (options.h): file_tile_above and file_tile (bytes)
+    const int64_t tile_above = opt(OPT_FILE_TILE_ABOVE);
     if (h->block_length > 0 && size > tile_above) {  // larger than we keep in HBM whole: tiled
         rsh::ResolveResult r;
         bool rerr = false;

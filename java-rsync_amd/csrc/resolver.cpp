@@ -3,6 +3,8 @@
 // io/FileView.java:143-185,235-278 (window, mark, isFull), util/Rolling.java:25-60 (add/subtract).
 #include "resolver.h"
 
+#include "options.h"
+
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -20,7 +22,7 @@ HostTimes& host_times() {
 }
 
 namespace {
-// RSH_SCAN_TRACE=1: one stderr line per host-side table operation (=2: totals only, see host_times)
+// Option scan_trace = 1: one stderr line per host-side table operation (=2: totals only, see host_times)
 struct HostTrace {
     const char* what;
     int64_t arg;
@@ -28,7 +30,7 @@ struct HostTrace {
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     HostTrace(const char* w, int64_t a, double* total) : what(w), arg(a), acc(total) {}
     ~HostTrace() {
-        static const int on = getenv("RSH_SCAN_TRACE") ? atoi(getenv("RSH_SCAN_TRACE")) : 0;
+        const int on = (int)opt(OPT_SCAN_TRACE);
         if (!on) return;
         const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         *acc += ms;

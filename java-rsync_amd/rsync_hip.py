@@ -114,6 +114,8 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_coun
            "rsh_match_scan_device", "rsh_match_scan_tiled", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
            "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_receiver_combine",
            "rsh_receiver_combine_device", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
+# include/rsync_hip_debug.h (testing / diagnostics ABI)
+DEBUG_EXPORTS = ["rsh_debug_set_option", "rsh_debug_get_option", "rsh_debug_reset_options"]
 
 _LIB = None
 
@@ -197,6 +199,9 @@ def lib():
         "rsh_memcpy_h2d": ([P, P, P, I64], ctypes.c_int),
         "rsh_memcpy_d2h": ([P, P, P, I64], ctypes.c_int),
         "rsh_fill_splitmix_device": ([P, P, I64, ctypes.c_uint64, I64], ctypes.c_int),
+        "rsh_debug_set_option": ([ctypes.c_char_p, I64], ctypes.c_int),
+        "rsh_debug_get_option": ([ctypes.c_char_p, ctypes.POINTER(I64)], ctypes.c_int),
+        "rsh_debug_reset_options": ([], None),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -289,6 +294,36 @@ def tokens(src, ev, file_md5_bytes):
     fm = np.frombuffer(file_md5_bytes, np.uint8).copy()
     _check(lib().rsh_tokens_write(_ptr(a), _ptr(ev) if n else None, n, _ptr(fm), _ptr(out), size))
     return out.tobytes()
+
+
+def set_option(name, value):
+    """A library tunable or diagnostic switch (include/rsync_hip_debug.h; tests and A/B runs only)."""
+    _check(lib().rsh_debug_set_option(name.encode(), int(value)))
+
+
+def get_option(name):
+    v = ctypes.c_int64()
+    _check(lib().rsh_debug_get_option(name.encode(), ctypes.byref(v)))
+    return v.value
+
+
+def reset_options():
+    lib().rsh_debug_reset_options()
+
+
+class option:
+    """Context manager: `with option("k1_gather", 0): ...` sets a switch and restores its previous value."""
+
+    def __init__(self, name, value):
+        self.name, self.value = name, value
+
+    def __enter__(self):
+        self.old = get_option(self.name)
+        set_option(self.name, self.value)
+        return self
+
+    def __exit__(self, *a):
+        set_option(self.name, self.old)
 
 
 def device_count():

@@ -55,3 +55,16 @@ def pytest_collection_finish(session):
             torch.cuda.init()
     except Exception:  # no usable GPU: the gpu tests report it themselves
         pass
+
+
+@pytest.fixture
+def rsh_opt():
+    """Sets librsynchip options (include/rsync_hip_debug.h) for one test: rsh_opt("k1_gather", 0).  Every option
+    is back at its default afterwards."""
+    import rsync_hip as R
+
+    def setter(name, value):
+        R.set_option(name, int(value))
+
+    yield setter
+    R.reset_options()

@@ -25,11 +25,46 @@ def test_header_declares_exports():
     assert declared == set(R.EXPORTS)
 
 
+def test_debug_header_declares_exports():
+    text = open(os.path.join(ROOT, "include", "rsync_hip_debug.h")).read()
+    declared = set(re.findall(r"\b(rsh_[a-z0-9_]+)\s*\(", text))
+    assert declared == set(R.DEBUG_EXPORTS)
+
+
 def test_library_exports_every_symbol():
     L = ctypes.CDLL(R.LIB_PATH)
-    for name in R.EXPORTS:
+    for name in R.EXPORTS + R.DEBUG_EXPORTS:
         assert hasattr(L, name), name
     assert R.lib().rsh_abi_version() == 3
+
+
+def test_options_have_defaults_and_no_environment():
+    """Tunables and diagnostic switches (include/rsync_hip_debug.h) change only through the debug ABI: an
+    environment variable of the old A/B form is ignored, an unknown name is rejected, reset restores defaults."""
+    assert R.get_option("k1_gather") == 1 and R.get_option("file_tile_above") == 32 << 30
+    with R.option("k1_gather", 0):
+        assert R.get_option("k1_gather") == 0
+    assert R.get_option("k1_gather") == 1
+    with pytest.raises(ValueError):
+        R.set_option("no_such_option", 1)
+    R.set_option("scan_samples", 17)
+    R.reset_options()
+    assert R.get_option("scan_samples") == 256
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import rsync_hip as R; print(R.get_option('k1_gather'))"
+            % os.path.join(ROOT, "java-rsync_amd"))
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, RSH_K1_GATHER="0"), capture_output=True,
+                         text=True, check=True)
+    assert out.stdout.strip() == "1"
+
+
+def test_product_library_has_no_ab_scaffolding():
+    """The kbench-only K1 variants (RSH_KBENCH) and the old getenv switches are not in librsynchip.so."""
+    blob = open(R.LIB_PATH, "rb").read()
+    for s in (b"RSH_K1_", b"RSH_SCAN_", b"RSH_BATCH_", b"RSH_FILE_", b"block_sums_quad_kernel", b"block_sums_dma_kernel",
+              b"block_sums_pipe_k3_kernel"):
+        assert s not in blob, s
 
 
 def test_library_built_from_these_sources():

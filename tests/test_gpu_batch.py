@@ -75,10 +75,10 @@ def _pack(ctx, blobs, misalign):
 
 
 @pytest.mark.parametrize("gather", ["1", "0"])
-def test_batch_generator_and_scan_match_oracle(ctx, gather, monkeypatch):
+def test_batch_generator_and_scan_match_oracle(ctx, gather, rsh_opt):
     # gather=1: each file's full chunks past its last full wave run as a gathered wave of the batched launch
-    # (K1Group::count < 64); 0: one per lane in the lane kernel (RSH_K1_GATHER)
-    monkeypatch.setenv("RSH_K1_GATHER", gather)
+    # (K1Group::count < 64); 0: one per lane in the lane kernel (option k1_gather)
+    rsh_opt("k1_gather", int(gather))
     rng = random.Random(2024)
     files = _segment(rng, 48)
     mis = [0 if rng.random() < 0.8 else rng.choice([1, 3, 4, 8]) for _ in files]

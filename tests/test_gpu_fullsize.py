@@ -242,7 +242,7 @@ def test_config2_pieces_4GiB(env):
     w, s = ctx.block_sums_pieces(_cut(basis, [big, 12345, big - 99999]), h, SEED)
     assert np.array_equal(w, d_w.cpu().numpy()) and np.array_equal(s, d_s.cpu().numpy())
     del basis
-    pieces = _cut(src, [big, 1, 777777, big - 5])
+    pieces = _cut(src, [big, 1, 777777])  # the last piece: 2146706904 bytes
     assert max(p.size for p in pieces) <= big and len(pieces) == 4
     ev, fm, lit, mat, st = ctx.match_scan_pieces(pieces, h, w, s, SEED)
     g = _fullsize("config2_insert")

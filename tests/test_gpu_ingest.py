@@ -89,12 +89,12 @@ def test_open_errors(ctx, tmp_path):
 
 
 @pytest.mark.parametrize("short", [False, True])
-def test_file_scan_tiled(ctx, tmp_path, monkeypatch, short):
-    """Files above RSH_FILE_TILE_ABOVE (32 GiB by default; lowered here) are scanned with HBM holding one tile
+def test_file_scan_tiled(ctx, tmp_path, rsh_opt, short):
+    """Files above file_tile_above (32 GiB by default; lowered here) are scanned with HBM holding one tile
     at a time (scan_tiled), read piece by piece from the file, the whole-file digest on its own pass: same
     events and digest as the oracle, FileView's zero fill and read_error included."""
-    monkeypatch.setenv("RSH_FILE_TILE_ABOVE", str(1 << 20))
-    monkeypatch.setenv("RSH_FILE_TILE", str(1 << 20))
+    rsh_opt("file_tile_above", 1 << 20)
+    rsh_opt("file_tile", 1 << 20)
     B = 4096
     n = (24 << 20) + 123
     basis = O.splitmix(n, 0x7711).tobytes()

@@ -152,15 +152,15 @@ def test_sender_digest_longer_than_md5(ctx, pad):
 
 
 @pytest.mark.parametrize("path", ["shift", "pipe", "lane"])
-def test_k1_unaligned_base(ctx, path, monkeypatch):
+def test_k1_unaligned_base(ctx, path, rsh_opt):
     """K1 over a basis that starts at offsets 0..15 and beyond from a 128-B line (the phase-shifted speculation
     runs K1 over src + s for any s).  By default such bases go to the line-aligned shift kernel (its loads stay
     on 128-B lines; MD5 words funnel-shifted out of an LDS ring; the lines' bytes outside the chunk taken out of
-    the weak sums; tail chunks on per-lane waves of the same launch).  RSH_K1_SHIFT=0 runs the pipelined kernel
-    at the unaligned base; with RSH_K1_UNALIGNED=0 too, the per-lane kernel.  Bit-exact against the oracle."""
+    the weak sums; tail chunks on per-lane waves of the same launch).  Option k1_shift = 0 runs the pipelined kernel
+    at the unaligned base; with k1_unaligned = 0 too, the per-lane kernel.  Bit-exact against the oracle."""
     import ctypes
-    monkeypatch.setenv("RSH_K1_SHIFT", "0" if path != "shift" else "1")
-    monkeypatch.setenv("RSH_K1_UNALIGNED", "0" if path == "lane" else "1")
+    rsh_opt("k1_shift", 0 if path != "shift" else 1)
+    rsh_opt("k1_unaligned", 0 if path == "lane" else 1)
     B, dl = 2048, 4
     n = 200 * B + 77
     d = ctx.alloc(n + 256)
@@ -204,13 +204,13 @@ def test_k1_shift_allocation_edge(ctx, nfull):
 
 
 @pytest.mark.parametrize("gather", ["1", "0"])
-def test_k1_partial_last_wave(ctx, gather, monkeypatch):
+def test_k1_partial_last_wave(ctx, gather, rsh_opt):
     """A K1 launch whose last wave is partial: its full-length chunks run as a gathered coalesced wave (a 64-bit
     pointer per 8-chunk row; lanes past the count store nothing), the short last chunk per lane (gather=1), or
-    every leftover chunk per lane (gather=0, RSH_K1_GATHER).  Sizes: 44 leftover full chunks; 63 + a short one;
+    every leftover chunk per lane (gather=0, option k1_gather).  Sizes: 44 leftover full chunks; 63 + a short one;
     1 leftover; a 16-B-unaligned base.  Bit-exact against the oracle (Generator.java:886-895)."""
     import ctypes
-    monkeypatch.setenv("RSH_K1_GATHER", gather)
+    rsh_opt("k1_gather", int(gather))
     B, dl = 2048, 4
     for nchunks, short, off in ((64 * 5 + 44, 0, 0), (64 * 3 + 64, 700, 0), (64 * 7 + 1, 0, 0), (64 * 2 + 17, 5, 9)):
         n = (nchunks - (1 if short else 0)) * B + short
@@ -243,7 +243,7 @@ def test_sender_phase_shift_chains(ctx):
 
 @pytest.mark.parametrize("segmented", ["1", "1-lane", "0"])
 @pytest.mark.parametrize("edit", ["insert1", "delete3", "two_inserts", "insert_far"])
-def test_sender_phase_guess(ctx, edit, segmented, monkeypatch):
+def test_sender_phase_guess(ctx, edit, segmented, rsh_opt):
     """A source that follows the basis up to an edit and continues at another phase after it (4096 windows at
     B = 65536, samples every 4): the speculation covers the sampled prefix only, and before the resolver starts
     the backend finds the phase past the run (a range probe plus four consecutive chunk sums) and starts the
@@ -251,10 +251,10 @@ def test_sender_phase_guess(ctx, edit, segmented, monkeypatch):
     (past both) is not the phase the resolver meets first.  insert_far: the edit is past every sample but the
     last.  segmented=1: the prefix and the guessed phase go out as one segmented K1 launch (per-wave bases; the
     two segments' leftover chunks -- 44 + 20 full ones for insert1, 44 + 19 for delete3 -- in one gathered
-    coalesced wave); 1-lane: the same launch with the leftovers one per lane (RSH_K1_GATHER=0); 0: two
+    coalesced wave); 1-lane: the same launch with the leftovers one per lane (option k1_gather = 0); 0: two
     launches.  Events equal the oracle's in every case."""
-    monkeypatch.setenv("RSH_SCAN_SEGMENTED", segmented[0])
-    monkeypatch.setenv("RSH_K1_GATHER", "0" if segmented == "1-lane" else "1")
+    rsh_opt("scan_segmented", int(segmented[0]))
+    rsh_opt("k1_gather", 0 if segmented == "1-lane" else 1)
     B, dl = 65536, 4
     basis = O.splitmix(256 << 20, 0x5EED5EED000000C3)
     x = 300 * B + 777
