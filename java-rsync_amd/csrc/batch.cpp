@@ -32,6 +32,7 @@ constexpr int32_t kMaxWorkers = 32;   // host threads running the resolvers
 constexpr size_t kFiberStack = 512 * 1024;
 constexpr int32_t kEagerSortChunks = 1 << 16;  // tables up to this size are sorted before the first round
 constexpr int64_t kPad = 16;
+constexpr int32_t kChainEvents = 1024;  // events one file's chain walk may emit before it hands over
 
 int64_t pad16(int64_t v) { return (v + kPad - 1) / kPad * kPad; }
 }  // namespace
@@ -58,6 +59,11 @@ struct BatchState {
     PinnedBuf h_sgroups, h_slanes;
     hipEvent_t ev_scopy = nullptr;
     bool scopy_pending = false;
+    // the chain walk (options.h batch_chain): chunk indexes, descriptors, results and events (pinned), and the
+    // speculation's flags kernel done on the aux stream (the walk reads the device flags and sums)
+    DevBuf kslots;
+    PinnedBuf h_kents, h_chain, h_chain_out, h_chain_ev;
+    hipEvent_t ev_fk = nullptr;
     hipError_t ensure_file_abort(int64_t nf) {
         if (nf <= file_abort_cap) return hipSuccess;
         if (file_abort) (void)hipFree(file_abort);
@@ -80,6 +86,9 @@ struct BatchState {
             if (scopy_pending) (void)hipEventSynchronize(ev_scopy);
             (void)hipEventDestroy(ev_scopy);
         }
+        if (ev_fk) (void)hipEventDestroy(ev_fk);
+        kslots.release();
+        for (PinnedBuf* b : {&h_kents, &h_chain, &h_chain_out, &h_chain_ev}) b->release();
         h_ggroups.release();
         h_glanes.release();
         h_sgroups.release();
@@ -790,6 +799,27 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         te[f] = TableEnt{S->slots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
     }
     RSH_BHIP(launch_table_insert_many(te, (uint32_t)NF, (int32_t)maxC, st, bg));
+    // The chain walk (option batch_chain, with the default speculation policy): the speculation runs at once for
+    // every file, and one launch walks each file's Sender state machine on the device from its start for as long
+    // as the state stays synced and unpoisoned and every digest it needs is speculated (device.hip
+    // chain_advance_kernel).  The resolvers start where the walks stopped -- files whose walk reached the end
+    // need none -- instead of taking one device round trip per event from the start.  Its chunk indexes go here.
+    const bool chain_on = opt(OPT_BATCH_CHAIN) != 0 && opt(OPT_BATCH_SPEC) == -1;
+    if (chain_on) {
+        RSH_BHIP(S->kslots.ensure((size_t)tns * 8));
+        RSH_BHIP(S->h_kents.ensure((size_t)NF * sizeof(TableEnt)));
+        RSH_BHIP(S->h_chain.ensure((size_t)NF * sizeof(ChainFile)));
+        RSH_BHIP(S->h_chain_out.ensure((size_t)NF * sizeof(ChainOut)));
+        RSH_BHIP(S->h_chain_ev.ensure((size_t)NF * kChainEvents * sizeof(rsh_event)));
+        if (!S->ev_fk) RSH_BHIP(hipEventCreateWithFlags(&S->ev_fk, hipEventDisableTiming));
+        RSH_BHIP(launch_table_clear(S->kslots.as<unsigned long long>(), (uint64_t)tns, st, bg));
+        TableEnt* ke = S->h_kents.as<TableEnt>();
+        for (int32_t f = 0; f < NF; ++f) {
+            FileScan& fs = files[(size_t)f];
+            ke[f] = TableEnt{S->kslots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
+        }
+        RSH_BHIP(launch_chunk_index(ke, (uint32_t)NF, (int32_t)maxC, st, bg));
+    }
     if (spec_after_prep && prep_all) RSH_BHIP(hipEventRecord(c->ev_prep, st));
 
     // the batched aligned speculation (deferred; see scan_device in capi.cpp)
@@ -877,6 +907,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             max_len = std::max<int64_t>(max_len, fs.na * 4);
         }
         RSH_BHIP(launch_chain_flags_many(fe, (uint32_t)NF, max_nf, aux));
+        if (chain_on) RSH_BHIP(hipEventRecord(S->ev_fk, aux));
         RSH_BHIP(launch_copy_many(sc, nfl, max_fl, aux));
         RSH_BHIP(hipEventRecord(c->ev_flags, aux));
         RSH_BHIP(launch_copy_many(sc + nfl, nsc - nfl, max_len, aux));
@@ -897,10 +928,31 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     // the lead check below keeps it for the files whose first windows carry their chunks' sums (they wait for
     // it instead of taking head-mode rounds) or stops it when no file qualifies
     const bool early_on = opt(OPT_SCAN_EARLY) != 0;  // A/B
-    const bool tentative = !pol && early_on && nlead_all > 0;
+    const bool tentative = !pol && early_on && nlead_all > 0 && !chain_on;
     if (early_spec || tentative) {
         const int r = launch_spec_k1();
         if (r != RSH_OK) return r;
+    }
+    bool spec_launched = false;
+    if (chain_on) {  // the speculation, then the walks on the context stream (beside the sums' download on aux)
+        const int r = launch_spec();
+        if (r != RSH_OK) return r;
+        spec_launched = true;
+        ChainFile* cf = S->h_chain.as<ChainFile>();
+        ChainOut* co = S->h_chain_out.as<ChainOut>();
+        rsh_event* ce = S->h_chain_ev.as<rsh_event>();
+        for (int32_t f = 0; f < NF; ++f) {
+            FileScan& fs = files[(size_t)f];
+            co[f] = ChainOut{};
+            cf[f] = ChainFile{fs.d_src, fs.n, (uint32_t)fs.B, fs.C, fs.dl, jobs[fs.job].h.remainder,
+                              S->slots.as<unsigned long long>() + fs.off_ns, fs.ns - 1, fs.ns - 1,
+                              S->kslots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.d_strong,
+                              S->src_weak.as<int32_t>() + fs.off_na, S->src_strong.as<uint8_t>() + fs.off_as,
+                              S->flags.as<uint8_t>() + fs.off_nf, fs.na, ce + (int64_t)f * kChainEvents, kChainEvents,
+                              0, co + f};
+        }
+        RSH_BHIP(hipStreamWaitEvent(st, S->ev_fk, 0));
+        RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st));
     }
     const double enq_ms = ms_since(t0);
     RSH_BHIP(hipEventSynchronize(c->ev_tab));
@@ -909,8 +961,36 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
 
     const bool trace = opt(OPT_SCAN_TRACE) != 0;
     int spec_rc = RSH_OK;
-    bool spec_launched = false;
     int32_t nwait = 0;
+    if (chain_on) {  // the walks have ended (the stream sync above): each resolver resumes where its walk stopped
+        const ChainOut* co = S->h_chain_out.as<ChainOut>();
+        const rsh_event* ce = S->h_chain_ev.as<rsh_event>();
+        int32_t left = 0;
+        for (int32_t f = 0; f < NF; ++f) {
+            FileScan& fs = files[(size_t)f];
+            const ChainOut& o = co[f];
+            fs.res.ev.assign(ce + (int64_t)f * kChainEvents, ce + (int64_t)f * kChainEvents + o.n_ev);
+            fs.res.literal = o.literal;
+            fs.res.matched = o.matched;
+            fs.res.stats.chain_matches += o.chain_matches;
+            fs.res.stats.events += o.events;
+            fs.rs.s = o.s;
+            fs.rs.m = o.m;
+            fs.rs.pref = o.pref;
+            fs.rs.anchor = o.s;
+            if (o.status == CHAIN_DONE) fs.rs.done = fs.done = true;
+            else ++left;
+        }
+        b.landed.store(true);  // the walks ran after the speculation's K1 and flags
+        if (left > 0) {        // the host resolvers use the speculation's host copies
+            RSH_BHIP(hipEventSynchronize(c->ev_spec));
+            b.aligned.store(true);
+            for (FileScan& fs : files) fs.be.head = false;
+        }
+        if (trace)
+            fprintf(stderr, "[rsh-batch] chain walks done at %.3f ms: %d of %d files left to the resolvers\n", ms_since(t0),
+                    left, NF);
+    }
     if (tentative) {
         for (int32_t f = 0; f < NF; ++f) {
             FileScan& fs = files[(size_t)f];

@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "hit_cache.h"
+#include "rsync_hip.h"
 
 namespace rsh {
 
@@ -256,6 +257,41 @@ inline uint32_t slot_hash_host(uint32_t key) {
     const uint32_t h = key * 0x9E3779B1u;
     return h ^ (h >> 15);
 }
+
+// Chain advance of a batched Sender scan (device.hip chain_advance_kernel, batch.cpp): one workgroup per file
+// walks Sender.sendMatchesAndData on the device while the state stays synced and unpoisoned and every digest
+// comes from the aligned speculation; it stops before any other step, which the host resolver then takes.
+// ChainOut holds the state on entry (s, m, pref) and on return; events go to ev (device-readable, ev_cap).
+enum { CHAIN_STOP = 0, CHAIN_DONE = 1 };
+constexpr int CHAIN_BUCKET_CAP = 64;
+struct ChainOut {
+    int64_t s, m;
+    int32_t pref, status;
+    int32_t n_ev, pad;
+    int64_t literal, matched, chain_matches, events;
+};
+struct ChainFile {
+    const uint8_t* data;
+    int64_t n;
+    uint32_t B;
+    int32_t C, dl, rem;
+    const unsigned long long* slots;   // the probe hash of the table's distinct keys
+    uint32_t mask;
+    uint32_t kmask;
+    const unsigned long long* kslots;  // the chunk index: (key << 32) | (i + 1) per chunk i (launch_chunk_index)
+    const int32_t* table_weak;
+    const uint8_t* table_strong;
+    const int32_t* aw;                 // the aligned speculation over windows [0, na): weak, digests, chain flags
+    const uint8_t* as;
+    const uint8_t* flags;
+    int64_t na;
+    rsh_event* ev;
+    int32_t ev_cap, pad;
+    ChainOut* out;
+};
+hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s);
+// The chunk indexes of many files (slots cleared by the caller; TableEnt as for the probe hashes).
+hipError_t launch_chunk_index(const TableEnt* ents, uint32_t nfiles, int32_t max_keys, hipStream_t s, bool bg = false);
 
 // splitmix64 counter stream (bench input): byte i = byte (i % 8) of mix(key + (i / 8 + 1) * golden).
 hipError_t launch_fill_splitmix(uint8_t* d_out, int64_t n, uint64_t key, int64_t byte_offset, hipStream_t s);

@@ -1338,9 +1338,11 @@ __global__ __launch_bounds__(64) void block_sums_dma_kernel(const uint8_t* __res
 
 #endif  // RSH_KBENCH
 
-// MD5 step form of the production K1: 0 compiler, 1 one asm statement per step, 2 generated blocks
-// (tools/gen_md5_asm.py)
+#ifdef RSH_KBENCH
+// MD5 step form of the coalesced K1 A/Bs: 0 compiler, 1 one asm statement per step, 2 generated blocks
+// (tools/gen_md5_asm.py; the production pipelined K1 uses 2)
 constexpr int kMd5Form = 2;
+#endif
 constexpr uint32_t kCUs = 256;            // MI355X compute units
 constexpr uint32_t kLdsPerCU = 160 * 1024; // bytes
 
@@ -2546,6 +2548,319 @@ hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const Part
     if (nptiles > 0)
         hipLaunchKernelGGL(probe_partials_kernel, dim3(nptiles), dim3(256), 0, s, args.files, ptiles, args.partials);
     hipLaunchKernelGGL(probe_first_kernel, dim3(ntiles), dim3(PROBE_THREADS), 0, s, args);
+    return hipGetLastError();
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// Chain advance (batched Sender scan, batch.cpp): one workgroup per file walks Sender.sendMatchesAndData
+// (Sender.java:1235-1327) on the device for as long as the state stays synced (no FileView flush since the last
+// match, so R = T) and unpoisoned (localChunkMd5sum == null, :1248) and every candidate digest comes from the
+// aligned speculation -- the resolver's steps (1), (1') at aligned positions and (2) (resolver.cpp), with the
+// candidate order of Checksum.getCandidateChunks (:206-276).  Anything else (a flush, a hit at an unaligned
+// position, a digest mismatch that poisons the cached digest, a bucket longer than CHAIN_BUCKET_CAP, the
+// shrinking windows at the end of a file with a remainder, a full event buffer) stops the walk before that step:
+// the host resolver resumes from the returned state and takes the step itself.  So the device emits exactly
+// the events the resolver would, in the same order.  In config 4's 50%-modified form (every other block
+// replaced) a file's run of MATCH / LIT pairs until its first false weak hit cost one device round trip per
+// pair on the host path; here the whole run is one launch for every file of the segment.
+//
+// All lanes keep the same copy of the state (s, mark, pref) and take the same decisions (every value they
+// branch on is read from global memory or LDS by all of them); lane 0 writes the events.
+// ------------------------------------------------------------------------------------------------
+constexpr int CHAIN_THREADS = PROBE_THREADS;
+
+__device__ __forceinline__ bool chain_digest_eq(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int dl) {
+    for (int j = 0; j < dl; ++j)
+        if (a[j] != b[j]) return false;
+    return true;
+}
+
+__global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const ChainFile* __restrict__ files) {
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ int32_t sh[4 * CHAIN_THREADS / 64];
+    __shared__ int32_t s_hit;                  // first hit in a tile (offset from the tile start), or INT_MAX
+    __shared__ uint32_t s_key;                 // its key
+    __shared__ int32_t s_bk[CHAIN_BUCKET_CAP];  // bucket of the key (ascending chunk index)
+    __shared__ int32_t s_nbk;
+    __shared__ int64_t s_zero;                 // first unset chain flag
+    const ChainFile& F = files[blockIdx.x];
+    ChainOut* out = F.out;
+    const int t = threadIdx.x;
+    const int64_t n = F.n, B = F.B, C = F.C;
+    const int dl = F.dl;
+    const int64_t S = F.rem > 0 ? F.rem : B;  // Checksum.java:131-137
+    const int64_t last = n - S, nB = n - B;
+    const int64_t na = F.na, nflags = F.na < C ? F.na : C;
+    const ProbeTable table{F.slots, F.mask};
+    int64_t s = out->s, m = out->m;
+    int32_t pref = out->pref;
+    int32_t nev = 0, status = CHAIN_STOP;
+    int64_t lit = 0, mat = 0, chain_matches = 0, events = 0;
+    rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
+    bool have = false;
+    auto flush_pend = [&]() {
+        if (have && t == 0) F.ev[nev] = pend;
+        if (have) ++nev;
+        have = false;
+    };
+    auto emit_lit = [&](int64_t off, int64_t len) {  // Sender.sendDataFrom; zero-length calls write nothing
+        if (len <= 0) return;
+        flush_pend();
+        pend = rsh_event{off, len, RSH_EV_LITERAL, 0, 0, 0};
+        have = true;
+        lit += len;
+    };
+    auto emit_match = [&](int64_t off, int64_t len, int32_t idx, int32_t cnt) {
+        mat += len;
+        if (have && pend.kind == RSH_EV_MATCH && pend.index + pend.count == idx && pend.offset + pend.length == off) {
+            pend.count += cnt;
+            pend.length += len;
+            return;
+        }
+        flush_pend();
+        pend = rsh_event{off, len, RSH_EV_MATCH, idx, cnt, 0};
+        have = true;
+    };
+
+    for (;;) {
+        if (nev + 3 > F.ev_cap) break;  // room for a pending event, a literal and a match
+        if (s > last) {                 // the loop ends (Sender.java:1313-1316)
+            emit_lit(m, n - m);
+            status = CHAIN_DONE;
+            break;
+        }
+        if (s % B != 0) break;  // phase-shifted windows: the host's phase speculation
+        const int64_t k = s / B;
+        // (1) aligned chain: preferred index == k and source window k carries chunk k's sums
+        if (k == pref && k < nflags && F.flags[k]) {
+            if (t == 0) s_zero = nflags;
+            __syncthreads();
+            for (int64_t j0 = k; j0 < nflags; j0 += CHAIN_THREADS) {
+                const int64_t j = j0 + t;
+                if (j < nflags && !F.flags[j]) atomicMin((unsigned long long*)&s_zero, (unsigned long long)j);
+                __syncthreads();
+                if (s_zero < nflags) break;
+            }
+            const int64_t j_end = s_zero;
+            __syncthreads();
+            const int64_t t_max = (last - s) / B + 1;
+            const int64_t tt = (j_end - k < t_max) ? j_end - k : t_max;
+            const int64_t j = k + tt, p = (s + tt * B < n) ? s + tt * B : n;
+            emit_lit(m, s - m);
+            emit_match(s, p - s, (int32_t)k, (int32_t)(j - k));
+            chain_matches += j - k;
+            s = m = p;
+            pref = (int32_t)j;
+            continue;
+        }
+        // (1') the window at s against chunk pref while both sums agree (windows s + iB, chunks pref + i)
+        if (pref < C && k < na) {
+            int64_t lim = na - k;
+            if (C - pref < lim) lim = C - pref;
+            if ((last - s) / B + 1 < lim) lim = (last - s) / B + 1;
+            int64_t tt = 0;
+            while (tt < lim && F.aw[k + tt] == F.table_weak[pref + tt] &&
+                   chain_digest_eq(F.as + (k + tt) * dl, F.table_strong + (pref + tt) * dl, dl))
+                ++tt;
+            if (tt > 0) {
+                const int64_t p = (s + tt * B < n) ? s + tt * B : n;
+                emit_lit(m, s - m);
+                emit_match(s, p - s, pref, (int32_t)tt);
+                s = m = p;
+                pref += (int32_t)tt;
+                continue;
+            }
+        }
+        // (2) the next candidate event in [s, stop]
+        const int64_t f = (m + 10 * B <= n) ? m + 9 * B : INT64_MAX;
+        const int64_t stop = f < last ? f : last;
+        if (stop > nB) break;  // shrinking windows near the end: the host
+        int64_t p = -1;
+        uint32_t key = 0;
+        int64_t a = s;
+        if (k < na) {
+            key = (uint32_t)F.aw[k];
+            if (table_has(table, key)) p = s;
+            else a = s + 1;
+        }
+        // tiles of PROBE_TILE positions in block coordinates, from a's tile on, until the first hit
+        bool cut = false;  // the search reached windows past the speculation (no anchor T(o))
+        for (int64_t q0 = (a / B) * B + ((a % B) / PROBE_TILE) * PROBE_TILE; p < 0 && q0 <= stop;) {
+            const int64_t kb = q0 / B, o = kb * B;
+            if (kb >= na) {
+                cut = true;
+                break;
+            }
+            int64_t qend = q0 + PROBE_TILE;
+            if (qend > o + B) qend = o + B;
+            int32_t head[4] = {0, 0, 0, 0};
+            if (q0 > o) {  // prefix of both streams from the block origin up to the tile
+                range_sums(F.data, n, o, q0, o, head[0], head[1]);
+                range_sums(F.data, n, o + B, q0 + B, o, head[2], head[3]);
+                block_reduce<4>(head, sh);
+            }
+            const int64_t p0 = q0 + (int64_t)t * PROBE_PPT;
+            uint32_t xa[4], xb[4];
+            load16(F.data, n, p0, xa);
+            load16(F.data, n, p0 + B, xb);
+            int32_t part[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < PROBE_PPT; ++i) {
+                const int32_t va = sbyte_of(xa, i), vb = sbyte_of(xb, i);
+                part[0] += va;
+                part[1] += (int32_t)((uint32_t)(p0 + i - o) * (uint32_t)va);
+                part[2] += vb;
+                part[3] += (int32_t)((uint32_t)(p0 + B + i - o) * (uint32_t)vb);
+            }
+            int32_t pre[4] = {part[0], part[1], part[2], part[3]};
+            block_exscan<4>(pre, sh);
+            if (t == 0) s_hit = 0x7FFFFFFF;
+            __syncthreads();
+            uint32_t keys[PROBE_PPT];
+            if (p0 < qend && p0 <= stop && p0 + PROBE_PPT > a) {
+                const uint32_t pa = (uint32_t)(head[0] + pre[0]), pa2 = (uint32_t)(head[1] + pre[1]);
+                const uint32_t pb = (uint32_t)(head[2] + pre[2]), pb2 = (uint32_t)(head[3] + pre[3]);
+                const int32_t To = F.aw[kb];
+                const uint32_t s1o = (uint32_t)To & 0xFFFFu, s2o = (uint32_t)To >> 16;
+                const uint32_t P1e = s1o + pb;
+                const uint32_t P2e = (uint32_t)B * s1o - s2o + pb2;  // windows inside [o, nB]: e0 = o + B
+                const uint32_t s1 = P1e - pa;
+                const uint32_t s2 = (uint32_t)B * s1 - (P2e - pa2);
+                int32_t R = (int32_t)((s1 & 0xFFFFu) | (s2 << 16));  // synced: the key is the true weak sum
+#pragma unroll
+                for (int i = 0; i < PROBE_PPT; ++i) {
+                    keys[i] = (uint32_t)R;
+                    R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(xa, i)), sbyte_of(xb, i));
+                }
+#pragma unroll
+                for (int i = 0; i < PROBE_PPT; ++i) {
+                    const int64_t pp = p0 + i;
+                    if (pp < a || pp > stop || pp >= qend) continue;
+                    if (table_has(table, keys[i])) {
+                        atomicMin(&s_hit, (int32_t)(pp - q0));
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            if (s_hit != 0x7FFFFFFF && (s_hit >> 4) == t) s_key = keys[s_hit & 15];
+            __syncthreads();
+            if (s_hit != 0x7FFFFFFF) {
+                p = q0 + s_hit;
+                key = s_key;
+            }
+            __syncthreads();
+            q0 = qend;
+        }
+        if (p < 0) {
+            if (cut || f <= last) break;  // past the speculation, or a flush (quirk A): the host
+            emit_lit(m, n - m);           // no candidate before the end
+            status = CHAIN_DONE;
+            s = n;
+            break;
+        }
+        // the event at p: its bucket (Multimap order), the candidates of Checksum.getCandidateChunks
+        ++events;
+        const int64_t kp = p / B;
+        if (p % B != 0 || kp >= na) break;  // the window's digest is not speculated: the host digests it
+        if (t == 0) {
+            int32_t cnt = 0;
+            const unsigned long long* ks = F.kslots;
+            uint32_t h = slot_hash(key) & F.kmask;
+            for (;;) {  // every chunk with this key lies on the probe path before the first empty slot
+                const unsigned long long v = ks[h];
+                if (v == 0ull) break;
+                if ((uint32_t)(v >> 32) == key) {
+                    if (cnt < CHAIN_BUCKET_CAP) s_bk[cnt] = (int32_t)((uint32_t)v - 1u);
+                    ++cnt;
+                }
+                h = (h + 1) & F.kmask;
+            }
+            for (int i = 1; i < cnt && i < CHAIN_BUCKET_CAP; ++i)  // ascending chunk index (insertion order)
+                for (int j = i; j > 0 && s_bk[j - 1] > s_bk[j]; --j) {
+                    const int32_t x = s_bk[j];
+                    s_bk[j] = s_bk[j - 1];
+                    s_bk[j - 1] = x;
+                }
+            s_nbk = cnt;
+        }
+        __syncthreads();
+        const int32_t size = s_nbk;
+        if (size == 0 || size > CHAIN_BUCKET_CAP) break;
+        // closeIndexOf(bucket, pref) (Checksum.java:175-213): pref's position, else the first index above it,
+        // else the last; not length-filtered.  Then the others in ascending order with length == window.
+        int32_t l = 0, r = size - 1, init = -1;
+        while (l <= r) {
+            const int32_t mid = l + (r - l) / 2;
+            if (s_bk[mid] == pref) {
+                init = mid;
+                break;
+            }
+            if (s_bk[mid] < pref) l = mid + 1;
+            else r = mid - 1;
+        }
+        if (init < 0) init = l < size - 1 ? l : size - 1;
+        const int64_t w = B;  // p <= nB
+        const uint8_t* md5c = F.as + kp * dl;  // Sender.java:1259-1263: the window's digest
+        int32_t hit = -1;
+        for (int32_t it = -1; it < size && hit < 0; ++it) {
+            int32_t pos;
+            if (it < 0) {
+                pos = init;
+            } else {
+                const int32_t c = s_bk[it];
+                const int64_t clen = (c == C - 1 && F.rem > 0) ? F.rem : B;  // Checksum.java:197-203
+                if (it == init || clen != w) continue;
+                pos = it;
+            }
+            const int32_t c = s_bk[pos];
+            if (chain_digest_eq(md5c, F.table_strong + (int64_t)c * dl, dl)) hit = c;
+        }
+        __syncthreads();
+        if (hit < 0) break;  // the cached digest is stale from here on (quirk B): the host
+        emit_lit(m, p - m);  // Sender.java:1265-1288
+        emit_match(p, w, hit, 1);
+        pref = hit + 1;
+        s = m = p + w;
+    }
+    flush_pend();
+    if (t == 0) {
+        out->s = s;
+        out->m = m;
+        out->pref = pref;
+        out->status = status;
+        out->n_ev = nev;
+        out->literal = lit;
+        out->matched = mat;
+        out->chain_matches = chain_matches;
+        out->events = events;
+    }
+}
+
+hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s) {
+    if (nfiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(chain_advance_kernel, dim3(nfiles), dim3(CHAIN_THREADS), 0, s, files);
+    return hipGetLastError();
+}
+
+// The chunk index of the chain walk: every chunk i of a file as (key << 32) | (i + 1) in an open-addressing table
+// (0 = empty); the chunks with one key all lie on that key's probe path before its first empty slot.
+__global__ void chunk_index_kernel(const TableEnt* __restrict__ ents, uint32_t nfiles) {
+    const TableEnt e = ents[blockIdx.y];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < e.nkeys; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t key = (uint32_t)e.keys[i];
+        const unsigned long long v = ((unsigned long long)key << 32) | (uint32_t)(i + 1);
+        uint32_t h = slot_hash(key) & e.mask;
+        while (atomicCAS(&e.slots[h], 0ull, v) != 0ull) h = (h + 1) & e.mask;
+    }
+    (void)nfiles;
+}
+
+hipError_t launch_chunk_index(const TableEnt* ents, uint32_t nfiles, int32_t max_keys, hipStream_t s, bool bg) {
+    if (nfiles == 0 || max_keys <= 0) return hipSuccess;
+    const uint32_t gx = (uint32_t)std::min<int64_t>((max_keys + 255) / 256, bg ? 2 : 64);
+    hipLaunchKernelGGL(chunk_index_kernel, dim3(gx, nfiles), dim3(256), 0, s, ents, nfiles);
     return hipGetLastError();
 }
 
