@@ -1673,6 +1673,11 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     hipLaunchKernelGGL(block_sums_pipe_k3_kernel, dim3(waves), dim3(64), 2 * wave_lds, s,
                                        d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
                     break;
+                case 58:  // diagnostics (wrong results): the production abortable K1 on synthetic stage data, no
+                          // global loads -- its s_waitcnt time is the LDS / abort-word share (PMC attribution)
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true, 1>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
+                    break;
                 case 56:  // A/B: the plain kernel with s_sleep 1 / s_sleep 4 per 2 stages
                     hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 6>), dim3(waves), dim3(64), 2 * wave_lds, s,
                                        d_data, B, dl, seed_word, d_weak, d_strong);
@@ -2726,7 +2731,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 const uint32_t P1e = s1o + pb;
                 const uint32_t P2e = (uint32_t)B * s1o - s2o + pb2;  // windows inside [o, nB]: e0 = o + B
                 const uint32_t s1 = P1e - pa;
-                const uint32_t s2 = (uint32_t)B * s1 - (P2e - pa2);
+                const uint32_t s2 = (uint32_t)(p0 + B - o) * s1 - (P2e - pa2);  // (p0 + B - o) s1 - sum (j - o) x_j
                 int32_t R = (int32_t)((s1 & 0xFFFFu) | (s2 << 16));  // synced: the key is the true weak sum
 #pragma unroll
                 for (int i = 0; i < PROBE_PPT; ++i) {
