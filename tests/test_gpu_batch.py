@@ -266,3 +266,54 @@ def test_batch_speculation_cancelled_per_file(ctx):
             else:
                 oev, olit, omat = expect[j]
                 assert got == oev and (sj[j].literal, sj[j].matched) == (olit, omat), f"small file {j}"
+
+
+@pytest.mark.parametrize("alphabet", [2, 4, 16])
+def test_batch_chain_low_entropy(ctx, alphabet):
+    """The device chain walk against the oracle where weak-sum collisions are everywhere: bytes from a small
+    alphabet, so the first table hit after a modified block is usually a false one at an unaligned position
+    (the walk must find exactly that position, hand the poisoning step to the host -- quirk B -- and never
+    match a later aligned block the Java scan no longer reaches).  Forms: every other block replaced, an
+    insert, unrelated; B from 512 to 8192."""
+    rng = random.Random(77 + alphabet)
+    files = []
+    for i in range(24):
+        B = rng.choice([512, 1024, 4096, 8192])
+        nb = rng.randrange(40 * B, 200 * B)
+        basis = (np.frombuffer(O.splitmix(nb, 900 + i).tobytes(), np.uint8) % alphabet).astype(np.uint8)
+        other = (np.frombuffer(O.splitmix(nb, 1900 + i).tobytes(), np.uint8) % alphabet).astype(np.uint8)
+        form = i % 3
+        if form == 0:
+            src = basis.copy()
+            src.reshape(-1)[:nb // B * B].reshape(-1, B)[1::2] = other[:nb // B * B].reshape(-1, B)[1::2]
+        elif form == 1:
+            x = rng.randrange(1, nb - 1)
+            src = np.concatenate([basis[:x], other[:rng.randrange(1, 3 * B)], basis[x:]])
+        else:
+            src = other
+        files.append((basis.tobytes(), src.tobytes(), B, rng.choice([2, 3, 4])))
+    d_basis, boffs = _pack(ctx, [f[0] for f in files], [0] * len(files))
+    d_src, soffs = _pack(ctx, [f[1] for f in files], [0] * len(files))
+    sj = (R.ScanJob * len(files))()
+    evs, keep, expect = [], [], []
+    for i, (basis, src, B, dl) in enumerate(files):
+        h = R.header_make(B, dl, len(basis))
+        w, s = ctx.block_sums(basis, h, SEED)
+        d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
+        d_w.upload(w)
+        d_s.upload(s)
+        keep += [d_w, d_s]
+        cap = len(src) // (10 * B) + 2 * h.chunk_count + 64
+        ev = np.zeros(cap, R.EVENT_DTYPE)
+        evs.append(ev)
+        sj[i].d_src, sj[i].n, sj[i].h = d_src.ptr.value + soffs[i], len(src), h
+        sj[i].d_weak, sj[i].d_strong = d_w.ptr.value, d_s.ptr.value
+        sj[i].ev, sj[i].ev_cap = ev.ctypes.data, cap
+        oev, _, olit, omat, _ = O.sender(src, O.header(B, dl, len(basis)), w, s, SEED)
+        expect.append(([tuple(e) for e in oev], olit, omat))
+    assert R.lib().rsh_match_scan_batch_device(ctx.handle, sj, len(files), SEED_NP.ctypes.data, None) == 0
+    for i, (basis, src, B, dl) in enumerate(files):
+        oev, olit, omat = expect[i]
+        assert sj[i].status == 0
+        assert R.events_as_tuples(evs[i][:sj[i].n_ev], B) == oev, f"file {i}: B={B} form={i % 3}"
+        assert (sj[i].literal, sj[i].matched) == (olit, omat)
