@@ -347,6 +347,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
+            # the whole step (both K1s, the scan's host work and the gaps between them): bytes read / step / peak
+            "step_frac": round(bytes_step / (head["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic(os.path.join(ROOT, "profiles", TRAFFIC_CSV), PROD_KERNEL, n),
             "traffic_source": f"profiles/{TRAFFIC_CSV} (rocprofv3 --pmc FETCH_SIZE pass of this kernel, x2 gfx950 "
                               f"correction; a prior run, not this one)",
@@ -411,10 +413,13 @@ def check_golden(g, ev, lit, mat, B):
 
 
 def main_files(a):
-    """BASELINE config 4: F files x S MiB per GPU (1024 x 128 MiB over 8 GPUs).  Every file is a multiple of
-    B, so the F basis files laid end to end form one array whose chunk table is the per-file tables back
-    to back: the Generator is one launch.  The F Sender scans (one per file, each with its own table) run
-    on a pool of contexts, one stream each, so their speculation kernels and resolvers overlap."""
+    """BASELINE config 4: F files x S MiB per GPU (1024 x 128 MiB over 8 GPUs), each file its own splitmix stream
+    (the inputs of tests/golden/fullsize_config4.json).  One step = the batched Generator over the F basis
+    files (rsh_block_sums_batch_device: one K1 launch) + the batched Sender over the F sources
+    (rsh_match_scan_batch_device).  The headline basis form (--variant, identical by default) is timed for
+    --steps; the other form (50%-modified: every other block replaced) runs as a companion under `variants`, so
+    both are always measured.  Every file's last timed scan is checked against the oracle's per-file digest.
+    --files-api single: one rsh_match_scan_device per file on a pool of contexts instead (comparison)."""
     import concurrent.futures as cf
 
     import torch
@@ -439,171 +444,176 @@ def main_files(a):
     assert S % B == 0
     n = F * S
     seed = np.frombuffer(bytes([1, 2, 3, 4]), np.uint8).copy()
-    hall = R.header_make(B, dl, n)
     ctx = R.Context(local)
-    pool_ctx = [R.Context(local) for _ in range(a.threads)]
     assert a.variant in ("identical", "half"), "--workload files: identical or half"
     src = torch.empty(n, dtype=torch.uint8, device="cuda")
-    basis = torch.empty(n, dtype=torch.uint8, device="cuda")
+    half = torch.empty(n, dtype=torch.uint8, device="cuda")
     for j, i in enumerate(mine):  # file i of the global list: its own splitmix stream
         key = KEY_SRC ^ (i << 20) ^ 0x4F11E5
         assert L.rsh_fill_splitmix_device(ctx.handle, src.data_ptr() + j * S, S, key, 0) == 0
-        if a.variant == "half":
-            assert L.rsh_fill_splitmix_device(ctx.handle, basis.data_ptr() + j * S, S, KEY_EDIT ^ key, 0) == 0
+        assert L.rsh_fill_splitmix_device(ctx.handle, half.data_ptr() + j * S, S, KEY_EDIT ^ key, 0) == 0
     ctx.sync()
-    if a.variant == "half":
-        other = basis
-        basis = src.clone()
-        basis.view(-1, B)[1::2] = other.view(-1, B)[1::2]
-        del other
-    else:
-        basis.copy_(src)
+    half.view(-1, B)[::2] = src.view(-1, B)[::2]  # the even blocks of every file from the source
     torch.cuda.synchronize()
     ctx.sync()
+    bases = {"identical": src, "half": half}  # the identical basis is the source's own buffer
+    golden = files_golden(mine, S, B, dl)
     d_weak = torch.empty(F * C1, dtype=torch.int32, device="cuda")
     d_strong = torch.empty(F * C1 * dl, dtype=torch.uint8, device="cuda")
     caps = C1 + S // B + 4096
-
+    stream = torch.cuda.ExternalStream(L.rsh_ctx_stream(ctx.handle))
+    evbufs = [np.zeros(caps, R.EVENT_DTYPE) for _ in range(F)]
+    sjobs = (R.ScanJob * F)()
+    bjobs = (R.BlockJob * F)()
+    for i in range(F):
+        bjobs[i].n, bjobs[i].h = S, h1
+        bjobs[i].d_weak = d_weak.data_ptr() + 4 * i * C1
+        bjobs[i].d_strong = d_strong.data_ptr() + i * C1 * dl
+        sjobs[i].d_src, sjobs[i].n, sjobs[i].h = src.data_ptr() + i * S, S, h1
+        sjobs[i].d_weak, sjobs[i].d_strong = bjobs[i].d_weak, bjobs[i].d_strong
+        sjobs[i].ev, sjobs[i].ev_cap = evbufs[i].ctypes.data, caps
+    bst = R.ScanStats()
+    pool_ctx, ex = [], None
+    if a.files_api == "single":
+        pool_ctx = [R.Context(local) for _ in range(a.threads)]
+        ex = cf.ThreadPoolExecutor(max_workers=a.threads)
     free_ctx = queue.SimpleQueue()  # a context serves one call at a time (rsync_hip.h)
     for c in pool_ctx:
         free_ctx.put(c)
 
-    def scan(i):
+    def scan_single(i):
         c = free_ctx.get()
         try:
-            return scan_on(i, c)
+            n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+            rc = L.rsh_match_scan_device(c.handle, ctypes.c_void_p(src.data_ptr() + i * S), S, ctypes.byref(h1),
+                                         ctypes.c_void_p(d_weak.data_ptr() + 4 * i * C1),
+                                         ctypes.c_void_p(d_strong.data_ptr() + i * C1 * dl), seed.ctypes.data,
+                                         evbufs[i].ctypes.data, caps, ctypes.byref(n_ev), ctypes.byref(lit),
+                                         ctypes.byref(mat), None)
+            assert rc == 0, (rc, L.rsh_last_error().decode())
+            sjobs[i].n_ev, sjobs[i].literal, sjobs[i].matched = n_ev.value, lit.value, mat.value
         finally:
             free_ctx.put(c)
 
-    def scan_on(i, c):
-        ev = np.zeros(caps, R.EVENT_DTYPE)
-        n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-        rc = L.rsh_match_scan_device(c.handle, ctypes.c_void_p(src.data_ptr() + i * S), S, ctypes.byref(h1),
-                                     ctypes.c_void_p(d_weak.data_ptr() + 4 * i * C1),
-                                     ctypes.c_void_p(d_strong.data_ptr() + i * C1 * dl), seed.ctypes.data,
-                                     ev.ctypes.data, caps, ctypes.byref(n_ev), ctypes.byref(lit), ctypes.byref(mat),
-                                     None)
-        assert rc == 0, (rc, L.rsh_last_error().decode())
-        assert lit.value + mat.value == S
-        return mat.value
-
-    ex = cf.ThreadPoolExecutor(max_workers=a.threads)
-
-    def step_single():
-        rc = L.rsh_block_sums_device(ctx.handle, ctypes.c_void_p(basis.data_ptr()), n, ctypes.byref(hall),
-                                     seed.ctypes.data, ctypes.c_void_p(d_weak.data_ptr()),
-                                     ctypes.c_void_p(d_strong.data_ptr()))
-        assert rc == 0
-        ctx.sync()  # tables ready before the scans (other streams)
-        futs = [ex.submit(scan, i) for i in range(F)]
-        return sum(f.result() for f in futs)
-
-    # batched: F basis files -> one rsh_block_sums_batch_device; F sources -> one rsh_match_scan_batch_device
-    bjobs = (R.BlockJob * F)()
-    sjobs = (R.ScanJob * F)()
-    evbufs = [np.zeros(caps, R.EVENT_DTYPE) for _ in range(F)]
-    for i in range(F):
-        bjobs[i].d_data = basis.data_ptr() + i * S
-        bjobs[i].n = S
-        bjobs[i].h = h1
-        bjobs[i].d_weak = d_weak.data_ptr() + 4 * i * C1
-        bjobs[i].d_strong = d_strong.data_ptr() + i * C1 * dl
-        sjobs[i].d_src = src.data_ptr() + i * S
-        sjobs[i].n = S
-        sjobs[i].h = h1
-        sjobs[i].d_weak = bjobs[i].d_weak
-        sjobs[i].d_strong = bjobs[i].d_strong
-        sjobs[i].ev = evbufs[i].ctypes.data
-        sjobs[i].ev_cap = caps
-    bst = R.ScanStats()
-    # the Generator's batched K1 (one launch over the segment) timed with HIP events on the context stream
-    stream = torch.cuda.ExternalStream(L.rsh_ctx_stream(ctx.handle))
-    gen_ev = []
-
-    def step_batch(timed=False):
-        if timed:
-            gen_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
-            gen_ev[-1][0].record(stream)
-        assert L.rsh_block_sums_batch_device(ctx.handle, bjobs, F, seed.ctypes.data) == 0
-        if timed:
-            gen_ev[-1][1].record(stream)
-        rc = L.rsh_match_scan_batch_device(ctx.handle, sjobs, F, seed.ctypes.data, ctypes.byref(bst))
-        assert rc == 0, (rc, L.rsh_last_error().decode())
-        return None if timed else check_jobs()  # timed steps: the last one is checked after the clock stops
-
-    def check_jobs():  # Sender.java:1325 for every file of the batch; the matched bytes
+    def run_files_variant(v, steps, warmup):
+        basis = bases[v]
         for i in range(F):
+            bjobs[i].d_data = basis.data_ptr() + i * S
+        gen_ev = []
+
+        def step(timed):
+            if timed:
+                gen_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                gen_ev[-1][0].record(stream)
+            assert L.rsh_block_sums_batch_device(ctx.handle, bjobs, F, seed.ctypes.data) == 0
+            if timed:
+                gen_ev[-1][1].record(stream)
+            if a.files_api == "batch":
+                rc = L.rsh_match_scan_batch_device(ctx.handle, sjobs, F, seed.ctypes.data, ctypes.byref(bst))
+                assert rc == 0, (rc, L.rsh_last_error().decode())
+            else:
+                ctx.sync()  # tables ready before the scans (other streams)
+                list(ex.map(scan_single, range(F)))
+
+        for _ in range(warmup):
+            step(False)
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+        gc_off = os.environ.get("BENCH_GC", "0") != "1" and gc.isenabled()  # as in run_variant
+        if gc_off:
+            gc.disable()
+        t0 = time.perf_counter()
+        dev_bytes, t_step = [], []
+        for _ in range(steps):
+            step(True)
+            t_step.append(time.perf_counter())
+            dev_bytes.append(bst.device_bytes if a.files_api == "batch" else n)
+        ctx.sync()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device="cuda")
+        if gc_off:
+            gc.enable()
+        for i in range(F):  # Sender.java:1325 for every file of the last timed step
             assert sjobs[i].literal + sjobs[i].matched == S
-        return sum(sjobs[i].matched for i in range(F))
+        # bytes the timed region read: the Generator's pass over the bases + what the scans' device work read
+        read_step = n + float(np.mean(dev_bytes))
+        assert read_step / (dt / steps) / 1e9 <= HBM_PEAK_GBS, "bytes read exceed the HBM peak: accounting error"
+        k_ms = sum(e0.elapsed_time(e1) for e0, e1 in gen_ev) / len(gen_ev)
+        return {"ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
+                "step_ms": [round((b - a_) * 1e3, 3) for a_, b in zip([t0] + t_step[:-1], t_step)],
+                "bytes_read_per_step": int(read_step),
+                "value_read": round(world * steps * read_step / dt / (1 << 30), 3),
+                "generator_kernel_ms": round(k_ms, 4),
+                "scan": {"matched_bytes_per_step_per_gpu": int(sum(sjobs[i].matched for i in range(F))),
+                         "stats": bst.as_dict() if a.files_api == "batch" else None},
+                "parity": check_files_golden(golden, v, sjobs, evbufs, B)}, dt, read_step, k_ms
 
-    batch = a.files_api == "batch"
-    step = step_batch if batch else step_single
-
-    for _ in range(a.warmup):
-        step()
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    torch.cuda.synchronize()
-    gc_off = os.environ.get("BENCH_GC", "0") != "1" and gc.isenabled()  # as in run_variant (no collection first)
-    if gc_off:
-        gc.disable()
-    t0 = time.perf_counter()
-    matched = 0
-    dev_bytes = []
-    for _ in range(a.steps):
-        matched = step_batch(timed=True) if batch else step()
-        dev_bytes.append(bst.device_bytes if batch else n)
-    ctx.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device="cuda")
-    if gc_off:
-        gc.enable()
-    if batch:
-        matched = check_jobs()
-    # bytes the timed region read: the Generator's pass over the bases + what the scans' device work read
-    # (the batched speculation over every source that ran to completion, probes, windows)
-    read_step = n + float(np.mean(dev_bytes))
-    value = world * a.steps * read_step / dt / (1 << 30)
-    assert read_step / (dt / a.steps) / 1e9 <= HBM_PEAK_GBS, "bytes read exceed the HBM peak: accounting error"
+    other = "half" if a.variant == "identical" else "identical"
+    head, dt, read_step, k_ms = run_files_variant(a.variant, a.steps, a.warmup)
+    comp = {} if a.no_companions else {other: run_files_variant(other, max(2, min(a.steps, 3)), 1)[0]}
+    ach = n / (k_ms * 1e-3) / 1e9
     res = {
         "metric": "GiB/s device-resident rolling+MD5 scan (Generator block sums + Sender match scan; bytes read)",
-        "value": round(value, 3), "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": round(dt / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64 on device)",
+        "value": head["value_read"], "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": head["ms_per_step"], "step_ms": head["step_ms"], "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64 on device; tests/golden/fullsize_config4.json)",
         "config": {"workload": f"config4: {F} files x {a.file_mib} MiB per GPU of a {len(sizes)}-file list "
-                               f"({'50%-modified' if a.variant == 'half' else 'identical'} bases), B={B}, dl={dl}",
+                               f"({VARIANT_TEXT[a.variant]} bases), B={B}, dl={dl}",
                    "bytes_per_step_per_gpu": int(read_step), "files_per_gpu": F, "block_length": B, "digest_length": dl,
                    "parallelism": f"file-sharded x{world} (no collectives), " + (
                        "batched entry points" if a.files_api == "batch" else f"{a.threads} scan contexts per GPU")},
-        "scan": {"matched_bytes_per_step_per_gpu": int(matched),
-                 "stats": bst.as_dict() if a.files_api == "batch" else None},
+        "roofline": {"kernel": "block_sums_pipe_kernel (batched K1: the Generator over the segment)", "bound": "hbm",
+                     "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                     "step_frac": round(read_step / (head["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": pmc_traffic(os.path.join(ROOT, "profiles", TRAFFIC_FILES_CSV), BATCH_KERNEL, n),
+                     "traffic_source": f"profiles/{TRAFFIC_FILES_CSV} (FETCH_SIZE x2, a prior run)",
+                     "kernel_ms": round(k_ms, 4), "algorithmic_bytes": n},
+        "scan": head["scan"], "parity": head["parity"], "variants": comp,
     }
-    if batch and gen_ev:
-        k_ms = sum(e0.elapsed_time(e1) for e0, e1 in gen_ev) / len(gen_ev)
-        ach = n / (k_ms * 1e-3) / 1e9
-        res["roofline"] = {"kernel": "block_sums_pipe_kernel (batched K1: the Generator over the segment)",
-                           "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(ach / HBM_PEAK_GBS, 4),
-                           "traffic": pmc_traffic(os.path.join(ROOT, "profiles", TRAFFIC_FILES_CSV),
-                                                  BATCH_KERNEL, n),
-                           "traffic_source": f"profiles/{TRAFFIC_FILES_CSV} (FETCH_SIZE x2, a prior run)",
-                           "kernel_ms": round(k_ms, 4),
-                           "algorithmic_bytes": n}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline_files(src, basis, S, F, B, dl, a.cpu_sample_mib << 20)
+        res["cpu_baseline"] = cpu_baseline_files(src, bases[a.variant], S, F, B, dl, a.cpu_sample_mib << 20)
     if rank == 0:
         if a.opt:
             res["config"]["options"] = a.opt
         print(json.dumps(res), flush=True)
-    ex.shutdown()
+    if ex:
+        ex.shutdown()
     for c in pool_ctx:
         c.close()
     ctx.close()
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def files_golden(mine, S, B, dl):
+    """The oracle's per-file digests of config 4's list (tests/golden/fullsize_config4.json), for this rank's
+    files, when the bench runs that shape."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "fullsize_config4.json")) as f:
+            d = json.load(f)
+    except OSError:
+        return None
+    if (d["file_bytes"], d["block_length"], d["digest_length"]) != (S, B, dl) or max(mine) >= d["files"]:
+        return None
+    return {v: [d[v][i] for i in mine] for v in ("identical", "half")}
+
+
+def check_files_golden(golden, v, sjobs, evbufs, B):
+    """Every file's events of the last timed step against the oracle's digest of that file (not timed)."""
+    if not golden:
+        return "unchecked (no committed oracle digest for this shape)"
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import fullsize_golden as G
+    for j, (n_ev, lit, mat, sha, _) in enumerate(golden[v]):
+        rec = G.records_from_runs(evbufs[j][:sjobs[j].n_ev], B)
+        ok = (int(rec.size), sjobs[j].literal, sjobs[j].matched) == (n_ev, lit, mat) and G.events_sha(rec) == sha
+        assert ok, f"file {j}: the scan's match list differs from the oracle's digest of the same inputs"
+    return f"every file's events identical to the oracle ({len(golden[v])} per-file digests)"
 
 
 def main_receiver(a):
