@@ -228,10 +228,10 @@ struct FileScan {
 struct Batch {
     std::mutex mu;
     std::condition_variable cv_coord, cv_work;
-    int32_t nworkers = 0;
     // written under mu (the condition variables' predicates); atomic so that a waiter can spin on them
     // before it blocks (spin_wait)
     std::atomic<int32_t> idle{0};
+    std::atomic<int32_t> nworkers{0};  // workers with a live file (a worker leaves once all of its files are done)
     std::atomic<uint64_t> gen{0};
     std::atomic<bool> quit{false};
     std::atomic<bool> landed{false};   // the speculation's chain flags are on the host (resolvers leave head mode)
@@ -1031,17 +1031,23 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     const int ncpu = host_cores();
     // spinning waiters: one core stays free for the coordinator
     const int32_t ncores = (spin_us() > 0 && ncpu > 2) ? ncpu - 1 : ncpu;
-    const int32_t W = std::max<int32_t>(1, std::min<int32_t>({NF, ncores, kMaxWorkers}));
+    // only the files still live get a worker: after the chain walks (or a leading speculation) most files are
+    // done, and a worker per core spinning for one live file's rounds only eats the CPU quota
+    std::vector<int32_t> live;
+    for (int32_t f = 0; f < NF; ++f)
+        if (!files[(size_t)f].done) live.push_back(f);
+    const int32_t NL = (int32_t)live.size();
+    const int32_t W = std::min<int32_t>({NL, ncores, kMaxWorkers});
     b.nworkers = W;
     b.worker_uc.resize((size_t)W);
     b.busy_ms.assign((size_t)W, 0.0);
     b.times.assign((size_t)W, HostTimes{});
     b.max_fiber_ms.assign((size_t)W, 0.0);
-    for (int32_t f = 0; f < NF; ++f) files[(size_t)f].worker = f % W;
+    for (int32_t i = 0; i < NL; ++i) files[(size_t)live[(size_t)i]].worker = i % W;
     std::vector<std::thread> th;
     th.reserve((size_t)W);
     for (int32_t w = 0; w < W; ++w) {
-        th.emplace_back([bp, &files, w, NF, W] {
+        th.emplace_back([bp, &files, &live, w, NL, W] {
             Batch& b = *bp;
             uint64_t seen = 0;
             for (;;) {
@@ -1053,8 +1059,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                     if (b.quit) return;
                     seen = b.gen;
                 }
-                for (int32_t f = w; f < NF; f += W) {
-                    FileScan& fs = files[(size_t)f];
+                bool any = false;
+                for (int32_t i = w; i < NL; i += W) {
+                    FileScan& fs = files[(size_t)live[(size_t)i]];
                     if (fs.done) continue;
                     if (fs.pending && fs.req.kind == Req::WAIT && !b.landed.load(std::memory_order_acquire)) continue;
                     fs.pending = false;
@@ -1074,9 +1081,14 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                     const double dt = ms_since(tf);
                     b.busy_ms[(size_t)w] += dt;
                     b.max_fiber_ms[(size_t)w] = std::max(b.max_fiber_ms[(size_t)w], dt);
+                    any = any || !fs.done;
                 }
                 std::lock_guard<std::mutex> l(b.mu);
                 b.times[(size_t)w] = host_times();
+                if (!any) {  // all of its files are done: leave (the coordinator's rounds no longer count it)
+                    if (b.idle == --b.nworkers) b.cv_coord.notify_one();
+                    return;
+                }
                 if (++b.idle == b.nworkers) b.cv_coord.notify_one();
             }
         });
@@ -1149,7 +1161,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             int kinds[6] = {0, 0, 0, 0, 0, 0};
             for (int32_t f : pend) kinds[files[(size_t)f].req.kind]++;
             double bsum = 0, bmax = 0, fmax = 0;
-            for (int32_t w = 0; w < b.nworkers; ++w) {
+            for (int32_t w = 0; w < W; ++w) {
                 bsum += b.busy_ms[(size_t)w];
                 bmax = std::max(bmax, b.busy_ms[(size_t)w]);
                 fmax = std::max(fmax, b.max_fiber_ms[(size_t)w]);

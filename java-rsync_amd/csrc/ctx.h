@@ -62,10 +62,13 @@ struct PinnedBuf {
     size_t cap = 0;
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
+        // small buffers grow geometrically: a round-trip buffer that creeps up by a few entries per call
+        // would otherwise pay a pinned allocation (~0.1-1 ms) every time
+        if (n < (64u << 20)) n = std::max<size_t>({n, std::min<size_t>(2 * cap, 64u << 20), 64u << 10});
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
-        hipError_t e = hipHostMalloc(&p, n ? n : 1, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
         if (e == hipSuccess) cap = n;
         return e;
     }

@@ -2738,11 +2738,18 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     keys[i] = (uint32_t)R;
                     R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(xa, i)), sbyte_of(xb, i));
                 }
+                // the 16 keys' first hash slots in one burst of independent loads (as probe_first_kernel): most
+                // keys are decided by their first slot, so a lane waits for about one L2 round trip, not 16
+                unsigned long long sl[PROBE_PPT];
+#pragma unroll
+                for (int i = 0; i < PROBE_PPT; ++i) sl[i] = table.slots[slot_hash(keys[i]) & table.mask];
 #pragma unroll
                 for (int i = 0; i < PROBE_PPT; ++i) {
                     const int64_t pp = p0 + i;
                     if (pp < a || pp > stop || pp >= qend) continue;
-                    if (table_has(table, keys[i])) {
+                    bool hit = sl[i] == ((1ull << 32) | keys[i]);
+                    if (!hit && sl[i] != 0ull) hit = table_has(table, keys[i]);
+                    if (hit) {
                         atomicMin(&s_hit, (int32_t)(pp - q0));
                         break;
                     }

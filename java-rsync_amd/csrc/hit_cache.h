@@ -98,11 +98,16 @@ struct HitCache {
     }
     // After a probe over several intervals (the batched flush chain): the resolver's next question is the
     // first hit inside the interval that holds the first hit, with that interval's key function -- keep
-    // that interval's hits (all of them when the list is complete, else the first).
+    // that interval's hits (all of them when the list is complete, else the first).  Without a hit every
+    // flush is committed and the next question is the last interval itself: keep it, proven hit-free.
     void fill_batch(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* ks, const ProbeOut& o,
                     int64_t n_minus_B) {
         valid = false;
-        if (o.first == ~0ull) return;
+        if (count <= 0) return;
+        if (o.first == ~0ull) {
+            fill(iv[count - 1], ks, o, n_minus_B);
+            return;
+        }
         const int64_t p = (int64_t)o.first;
         for (int64_t j = 0; j < count; ++j) {
             if (p < iv[j].a || p >= iv[j].b) continue;

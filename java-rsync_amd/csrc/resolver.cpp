@@ -426,6 +426,14 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
             // the flush, so one batched gather, a host chain and one probe over all K intervals
             // replace K round trips.  K doubles while no event turns up (wasted probing <= 2x).
             // flush i sits at f_i = f + 10B i and happens iff its mark m_i = f_i - 9B has m_i + 10B <= n
+            // The doubling starts higher when candidates are rare: a stale digest carried by few chunks leaves
+            // about |keys| 10B / 2^32 candidate positions per interval (x4 for the weak sums' uneven spread), so a
+            // poisoned state with a handful of keys probes thousands of intervals at once instead of climbing
+            // from one through a dozen round trips.  The batch size only decides how much is speculated per
+            // probe, never the result.
+            const int64_t nkeys = keys ? (int64_t)keys->size() : (int64_t)table.chunk_count;
+            const int64_t floor_k = std::clamp<int64_t>((int64_t)((1ull << 32) / ((uint64_t)(40 * B) * (uint64_t)std::max<int64_t>(nkeys, 1))), 1, 4096);
+            batch = std::max(batch, floor_k);
             int64_t K = 1;
             const int64_t kcap = std::min(max_batch, be.max_batch_at(f));
             while (K < std::min(batch, kcap) && f + 10 * B * K + B <= n) ++K;
