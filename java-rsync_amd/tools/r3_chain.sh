@@ -10,3 +10,4 @@ for v in half identical; do
   timeout -k 10 300 python bench.py --workload files --variant $v --steps 5 --warmup 2 --no-cpu-baseline --opt batch_chain=0 > $O/files_${v}_nochain.json 2> $O/files_${v}_nochain.err || exit 1
 done
 timeout -k 10 300 python bench.py --workload files --variant half --steps 1 --warmup 1 --no-cpu-baseline --opt scan_trace=2 > $O/files_half_trace.json 2> $O/files_half_trace.err || exit 1
+timeout -k 10 300 python bench.py --workload files --variant identical --steps 1 --warmup 1 --no-cpu-baseline --opt scan_trace=2 > $O/files_identical_trace.json 2> $O/files_identical_trace.err || exit 1
