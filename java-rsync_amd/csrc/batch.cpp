@@ -64,6 +64,7 @@ struct BatchState {
     DevBuf kslots;
     PinnedBuf h_kents, h_chain, h_chain_out, h_chain_ev;
     hipEvent_t ev_fk = nullptr;
+    hipEvent_t ev_ch0 = nullptr, ev_ch1 = nullptr;  // around the walk (trace)
     hipError_t ensure_file_abort(int64_t nf) {
         if (nf <= file_abort_cap) return hipSuccess;
         if (file_abort) (void)hipFree(file_abort);
@@ -86,7 +87,8 @@ struct BatchState {
             if (scopy_pending) (void)hipEventSynchronize(ev_scopy);
             (void)hipEventDestroy(ev_scopy);
         }
-        if (ev_fk) (void)hipEventDestroy(ev_fk);
+        for (hipEvent_t e : {ev_fk, ev_ch0, ev_ch1})
+            if (e) (void)hipEventDestroy(e);
         kslots.release();
         for (PinnedBuf* b : {&h_kents, &h_chain, &h_chain_out, &h_chain_ev}) b->release();
         h_ggroups.release();
@@ -952,7 +954,13 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                               0, co + f};
         }
         RSH_BHIP(hipStreamWaitEvent(st, S->ev_fk, 0));
+        if (opt(OPT_SCAN_TRACE) != 0) {  // the walk's own duration (trace only)
+            for (hipEvent_t* e : {&S->ev_ch0, &S->ev_ch1})
+                if (!*e) RSH_BHIP(hipEventCreate(e));
+            RSH_BHIP(hipEventRecord(S->ev_ch0, st));
+        }
         RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st));
+        if (opt(OPT_SCAN_TRACE) != 0) RSH_BHIP(hipEventRecord(S->ev_ch1, st));
     }
     const double enq_ms = ms_since(t0);
     RSH_BHIP(hipEventSynchronize(c->ev_tab));
@@ -987,9 +995,21 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             b.aligned.store(true);
             for (FileScan& fs : files) fs.be.head = false;
         }
-        if (trace)
-            fprintf(stderr, "[rsh-batch] chain walks done at %.3f ms: %d of %d files left to the resolvers\n", ms_since(t0),
-                    left, NF);
+        if (trace) {
+            float kms = 0.f;
+            if (S->ev_ch0 && S->ev_ch1) (void)hipEventElapsedTime(&kms, S->ev_ch0, S->ev_ch1);
+            int64_t tsum = 0, esum = 0;
+            int32_t tmax = 0, emax = 0;
+            for (int32_t f = 0; f < NF; ++f) {
+                tsum += co[f].tiles;
+                tmax = std::max(tmax, co[f].tiles);
+                esum += co[f].events;
+                emax = std::max<int32_t>(emax, (int32_t)co[f].events);
+            }
+            fprintf(stderr, "[rsh-batch] chain walks done at %.3f ms (kernel %.3f ms; tiles %lld, max %d per file; events "
+                    "%lld, max %d): %d of %d files left to the resolvers\n", ms_since(t0), kms, (long long)tsum, tmax,
+                    (long long)esum, emax, left, NF);
+        }
     }
     if (tentative) {
         for (int32_t f = 0; f < NF; ++f) {

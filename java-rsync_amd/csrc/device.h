@@ -267,7 +267,7 @@ constexpr int CHAIN_BUCKET_CAP = 64;
 struct ChainOut {
     int64_t s, m;
     int32_t pref, status;
-    int32_t n_ev, pad;
+    int32_t n_ev, tiles;  // tiles: probe tiles the walk searched (trace)
     int64_t literal, matched, chain_matches, events;
 };
 struct ChainFile {

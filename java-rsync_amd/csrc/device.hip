@@ -2589,7 +2589,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_bk[CHAIN_BUCKET_CAP];  // bucket of the key (ascending chunk index)
     __shared__ int32_t s_nbk;
     __shared__ int64_t s_zero;                 // first unset chain flag
-    const ChainFile& F = files[blockIdx.x];
+    // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
+    // fields across the loop (the event stores may alias it) -- a PCIe round trip each
+    const ChainFile F = files[blockIdx.x];
     ChainOut* out = F.out;
     const int t = threadIdx.x;
     const int64_t n = F.n, B = F.B, C = F.C;
@@ -2602,6 +2604,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     int32_t pref = out->pref;
     int32_t nev = 0, status = CHAIN_STOP;
     int64_t lit = 0, mat = 0, chain_matches = 0, events = 0;
+    int32_t tiles = 0;
     rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
     bool have = false;
     auto flush_pend = [&]() {
@@ -2699,6 +2702,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             }
             int64_t qend = q0 + PROBE_TILE;
             if (qend > o + B) qend = o + B;
+            ++tiles;
             int32_t head[4] = {0, 0, 0, 0};
             if (q0 > o) {  // prefix of both streams from the block origin up to the tile
                 range_sums(F.data, n, o, q0, o, head[0], head[1]);
@@ -2843,6 +2847,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->pref = pref;
         out->status = status;
         out->n_ev = nev;
+        out->tiles = tiles;
         out->literal = lit;
         out->matched = mat;
         out->chain_matches = chain_matches;
