@@ -101,6 +101,9 @@ uint32_t plan_block_sums_files(const K1File* files, int32_t nfiles, std::vector<
 hipError_t launch_expand_groups(const K1Plan* d_plans, uint32_t nplans, uint32_t ngroups, K1Group* d_groups,
                                 hipStream_t s);
 #ifdef RSH_KBENCH
+// the batched launch as persistent waves (kbench 1006)
+hipError_t launch_block_sums_batch_persist(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes,
+                                           uint32_t nlanes, int lane_align, uint32_t seed_word, hipStream_t s);
 // the same over groups only, at 4 waves per SIMD (block_sums_quad_kernel; kbench 1004: not adopted)
 hipError_t launch_block_sums_batch_quad(const K1Group* d_groups, uint32_t ngroups, uint32_t seed_word, hipStream_t s,
                                         const int* abort_flag = nullptr, int abort_gen = 0);

@@ -531,7 +531,7 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
                                                              int64_t n = 0, uint32_t nchunks = 0,
                                                              uint32_t main_waves = 0xFFFFFFFFu,
                                                              const K1Tail* __restrict__ gt = nullptr,
-                                                             uint32_t gcnt = 0) {
+                                                             uint32_t gcnt = 0, uint32_t gsel = 0xFFFFFFFFu) {
     constexpr int ROW = 9;
     constexpr int BUF = 64 * ROW;  // uint4 slots per LDS buffer
     constexpr int TAIL_PF = RSH_K1_TAIL_PF;
@@ -554,7 +554,7 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     uint32_t c0 = blockIdx.x * 64u;
     const uint8_t* gdata = data + (size_t)c0 * B;
     if constexpr (MULTI) {
-        const K1Group g = groups[blockIdx.x];
+        const K1Group g = groups[gsel == 0xFFFFFFFFu ? blockIdx.x : gsel];  // gsel: a persistent wave's group
         gdata = g.data;
         B = g.B;
         dl = g.dl;
@@ -1934,6 +1934,54 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
     block_sums_pipe_body<8, true, true, 0, true>(nullptr, 0u, 0u, seed, nullptr, nullptr, abort_flag, abort_gen, groups);
 }
 #ifdef RSH_KBENCH
+// kbench A/B (variant 1006): the batched launch as persistent waves -- a grid of (CUs x 8) waves, each taking
+// groups i, i + grid, ... (then the lane waves) one after the other, instead of one dispatched workgroup per group.
+template <int ALIGN>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void block_sums_pipe_persist_kernel(
+    const K1Group* __restrict__ groups, uint32_t ngroups, const K1Lane* __restrict__ lanes, uint32_t nlanes,
+    uint32_t seed, const int* abort_flag, int abort_gen) {
+    for (uint32_t i = blockIdx.x; i < ngroups + nlanes; i += gridDim.x) {
+        if (i >= ngroups) {
+            const K1Lane e = lanes[i - ngroups];
+            const uint32_t c = e.c_first + threadIdx.x;
+            if (c < e.nchunks)
+                lane_chunk_sums<ALIGN == 1 ? 0 : ALIGN, ALIGN == 16 ? 4 : ALIGN == 4 ? 2 : 4, ALIGN != 1>(
+                    e.data, e.n, e.B, c, e.dl, seed, e.weak, e.strong);
+            continue;
+        }
+        const K1Group g = groups[i];
+        if (g.count < 64) {
+            block_sums_pipe_body<8, true, true, 0, false, true>(g.data, g.B, g.dl, seed, g.weak, g.strong,
+                                                               g.abort ? g.abort : abort_flag, abort_gen, nullptr, 0, 0,
+                                                               0xFFFFFFFFu, nullptr, g.count);
+            continue;
+        }
+        block_sums_pipe_body<8, true, true, 0, true>(nullptr, 0u, 0u, seed, nullptr, nullptr, abort_flag, abort_gen,
+                                                     groups, 0, 0, 0xFFFFFFFFu, nullptr, 0, i);
+    }
+}
+hipError_t launch_block_sums_batch_persist(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes,
+                                           uint32_t nlanes, int lane_align, uint32_t seed_word, hipStream_t s) {
+    const size_t lb = 2 * 64 * 9 * sizeof(uint4);
+    const int* abort_flag = never_word();
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    uint32_t waves = (uint32_t)cus * 8u;
+    if (const char* e = getenv("KBENCH_PERSIST_WAVES")) waves = (uint32_t)atoi(e);
+    const uint32_t total = ngroups + nlanes;
+    const dim3 grid(std::min(total, std::max(1u, waves)));
+    if (lane_align == 16)
+        hipLaunchKernelGGL((block_sums_pipe_persist_kernel<16>), grid, dim3(64), lb, s, d_groups, ngroups, d_lanes, nlanes,
+                           seed_word, abort_flag, -1);
+    else if (lane_align == 4)
+        hipLaunchKernelGGL((block_sums_pipe_persist_kernel<4>), grid, dim3(64), lb, s, d_groups, ngroups, d_lanes, nlanes,
+                           seed_word, abort_flag, -1);
+    else
+        hipLaunchKernelGGL((block_sums_pipe_persist_kernel<1>), grid, dim3(64), lb, s, d_groups, ngroups, d_lanes, nlanes,
+                           seed_word, abort_flag, -1);
+    return hipGetLastError();
+}
+
 bool batch_quad() {  // RSH_K1_QUAD=1 (kbench A/B): the batched groups at 4 waves/SIMD
     static const bool v = getenv("RSH_K1_QUAD") && atoi(getenv("RSH_K1_QUAD")) != 0;
     return v;

@@ -144,6 +144,9 @@ int main(int argc, char** argv) {
                                                                            }),
                                                    B, dl, 0x04030201u, s);
         if (v == 1005) return launch_rag();
+        if (v == 1006)
+            return rsh::launch_block_sums_batch_persist(d_groups, (uint32_t)groups.size(), d_lanes, (uint32_t)lanes.size(),
+                                                        lane_align, 0x04030201u, s);
         if (v == 1002)
             return rsh::launch_block_sums_batch(d_groups, (uint32_t)groups.size(), d_lanes, (uint32_t)lanes.size(),
                                                 lane_align, 0x04030201u, s);
