@@ -951,7 +951,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                               S->kslots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.d_strong,
                               S->src_weak.as<int32_t>() + fs.off_na, S->src_strong.as<uint8_t>() + fs.off_as,
                               S->flags.as<uint8_t>() + fs.off_nf, fs.na, ce + (int64_t)f * kChainEvents, kChainEvents,
-                              0, co + f};
+                              seed_word(seed), co + f};
         }
         RSH_BHIP(hipStreamWaitEvent(st, S->ev_fk, 0));
         if (opt(OPT_SCAN_TRACE) != 0) {  // the walk's own duration (trace only)
@@ -986,6 +986,11 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             fs.rs.m = o.m;
             fs.rs.pref = o.pref;
             fs.rs.anchor = o.s;
+            if (o.md5c_valid) {  // poisoned at an unaligned hit: the resolver goes on with the stale digest
+                fs.rs.md5c.assign(o.md5c, o.md5c + fs.dl);
+                fs.rs.md5c_valid = true;
+                fs.rs.dkeys_ready = false;
+            }
             if (o.status == CHAIN_DONE) fs.rs.done = fs.done = true;
             else ++left;
         }
@@ -998,17 +1003,19 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         if (trace) {
             float kms = 0.f;
             if (S->ev_ch0 && S->ev_ch1) (void)hipEventElapsedTime(&kms, S->ev_ch0, S->ev_ch1);
-            int64_t tsum = 0, esum = 0;
+            int64_t tsum = 0, esum = 0, dsum = 0, psum = 0;
             int32_t tmax = 0, emax = 0;
             for (int32_t f = 0; f < NF; ++f) {
                 tsum += co[f].tiles;
                 tmax = std::max(tmax, co[f].tiles);
                 esum += co[f].events;
+                dsum += co[f].digests;
+                psum += co[f].md5c_valid;
                 emax = std::max<int32_t>(emax, (int32_t)co[f].events);
             }
             fprintf(stderr, "[rsh-batch] chain walks done at %.3f ms (kernel %.3f ms; tiles %lld, max %d per file; events "
-                    "%lld, max %d): %d of %d files left to the resolvers\n", ms_since(t0), kms, (long long)tsum, tmax,
-                    (long long)esum, emax, left, NF);
+                    "%lld, max %d; %lld windows digested, %lld files poisoned): %d of %d files left to the resolvers\n",
+                    ms_since(t0), kms, (long long)tsum, tmax, (long long)esum, emax, (long long)dsum, (long long)psum, left, NF);
         }
     }
     if (tentative) {

@@ -272,6 +272,9 @@ struct ChainOut {
     int32_t pref, status;
     int32_t n_ev, tiles;  // tiles: probe tiles the walk searched (trace)
     int64_t literal, matched, chain_matches, events;
+    // stopped on a poisoned state (quirk B): the stale cached digest, the window's at the hit (md5c_valid = 1)
+    uint8_t md5c[16];
+    int32_t md5c_valid, digests;  // digests: windows the walk digested itself (unaligned hits)
 };
 struct ChainFile {
     const uint8_t* data;
@@ -289,7 +292,8 @@ struct ChainFile {
     const uint8_t* flags;
     int64_t na;
     rsh_event* ev;
-    int32_t ev_cap, pad;
+    int32_t ev_cap;
+    uint32_t seed;                     // the checksum seed (a window's digest at an unaligned hit)
     ChainOut* out;
 };
 hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s);

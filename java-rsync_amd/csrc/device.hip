@@ -2637,6 +2637,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_bk[CHAIN_BUCKET_CAP];  // bucket of the key (ascending chunk index)
     __shared__ int32_t s_nbk;
     __shared__ int64_t s_zero;                 // first unset chain flag
+    __shared__ int32_t s_wtmp;                 // an unaligned window's sums (its digest: s_dig)
+    __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
     // fields across the loop (the event stores may alias it) -- a PCIe round trip each
     const ChainFile F = files[blockIdx.x];
@@ -2652,7 +2654,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     int32_t pref = out->pref;
     int32_t nev = 0, status = CHAIN_STOP;
     int64_t lit = 0, mat = 0, chain_matches = 0, events = 0;
-    int32_t tiles = 0;
+    int32_t tiles = 0, digests = 0, poisoned = 0;
+    const uint8_t* stale = nullptr;  // poisoned: the cached digest
     rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
     bool have = false;
     auto flush_pend = [&]() {
@@ -2827,7 +2830,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         // the event at p: its bucket (Multimap order), the candidates of Checksum.getCandidateChunks
         ++events;
         const int64_t kp = p / B;
-        if (p % B != 0 || kp >= na) break;  // the window's digest is not speculated: the host digests it
+        const bool spec_digest = p % B == 0 && kp < na;
         if (t == 0) {
             int32_t cnt = 0;
             const unsigned long long* ks = F.kslots;
@@ -2866,7 +2869,15 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         }
         if (init < 0) init = l < size - 1 ? l : size - 1;
         const int64_t w = B;  // p <= nB
-        const uint8_t* md5c = F.as + kp * dl;  // Sender.java:1259-1263: the window's digest
+        // Sender.java:1259-1263: the window's digest -- the speculation's at aligned positions, else one lane digests
+        // the window here (lane_chunk_sums over the B bytes at p, the seed appended), the host path's md5_at
+        const uint8_t* md5c = F.as + kp * dl;
+        if (!spec_digest) {
+            if (t == 0) lane_chunk_sums<0, 2, false>(F.data + p, n - p, (uint32_t)B, 0u, (uint32_t)dl, F.seed, &s_wtmp, s_dig);
+            __syncthreads();
+            md5c = s_dig;
+            ++digests;
+        }
         int32_t hit = -1;
         for (int32_t it = -1; it < size && hit < 0; ++it) {
             int32_t pos;
@@ -2882,7 +2893,16 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             if (chain_digest_eq(md5c, F.table_strong + (int64_t)c * dl, dl)) hit = c;
         }
         __syncthreads();
-        if (hit < 0) break;  // the cached digest is stale from here on (quirk B): the host
+        if (hit < 0) {
+            // the cached digest is stale from here on (quirk B): the host goes on with it from p + 1 (a hit at the
+            // flush point itself flushes there: the host retakes that step from s)
+            if (p < f) {
+                s = p + 1;
+                poisoned = 1;
+                stale = md5c;
+            }
+            break;
+        }
         emit_lit(m, p - m);  // Sender.java:1265-1288
         emit_match(p, w, hit, 1);
         pref = hit + 1;
@@ -2896,6 +2916,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->status = status;
         out->n_ev = nev;
         out->tiles = tiles;
+        out->digests = digests;
+        out->md5c_valid = poisoned;
+        if (poisoned)
+            for (int j = 0; j < dl && j < 16; ++j) out->md5c[j] = stale[j];
         out->literal = lit;
         out->matched = mat;
         out->chain_matches = chain_matches;
