@@ -32,6 +32,7 @@ constexpr int32_t kMaxWorkers = 32;   // host threads running the resolvers
 constexpr size_t kFiberStack = 512 * 1024;
 constexpr int32_t kEagerSortChunks = 1 << 16;  // tables up to this size are sorted before the first round
 constexpr int64_t kPad = 16;
+constexpr int64_t kWaveSlots = 2 * 4 * 256;  // the chip's K1 wave slots (2 waves per SIMD, 4 SIMDs, 256 CUs)
 constexpr int32_t kChainEvents = 1024;  // events one file's chain walk may emit before it hands over
 
 int64_t pad16(int64_t v) { return (v + kPad - 1) / kPad * kPad; }
@@ -44,7 +45,7 @@ struct BatchState {
     DevBuf slots, dslots, src_weak, src_strong, flags, haw, partials, bucket, first, k1_groups, k1_lanes;
     // Sender batch: pinned host (read or written by the kernels directly)
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl, h_files, h_hit, h_win0, h_bucket, h_first, h_iv, h_tiles,
-        h_ptiles, h_req, h_gw, h_gb, h_ow, h_ob, h_win, h_copies, h_tabents, h_flagents, h_dkeys, h_ccopies,
+        h_ptiles, h_req, h_gw, h_gb, h_ow, h_ob, h_win, h_copies, h_tabents, h_flagents, h_flagents_a, h_dkeys, h_ccopies,
         h_lead;
     // device, uncached: one abort word per file of the batch; the speculation's groups of file f stop once
     // file_abort[f] holds the scan's generation (written by the coordinator when f's resolver finishes)
@@ -65,6 +66,7 @@ struct BatchState {
     PinnedBuf h_kents, h_chain, h_chain_out, h_chain_ev;
     hipEvent_t ev_fk = nullptr;
     hipEvent_t ev_ch0 = nullptr, ev_ch1 = nullptr;  // around the walk (trace)
+    hipEvent_t ev_fa = nullptr, ev_wa = nullptr;    // two-phase walk: prefix flags done, phase-0 walk done
     hipError_t ensure_file_abort(int64_t nf) {
         if (nf <= file_abort_cap) return hipSuccess;
         if (file_abort) (void)hipFree(file_abort);
@@ -87,7 +89,7 @@ struct BatchState {
             if (scopy_pending) (void)hipEventSynchronize(ev_scopy);
             (void)hipEventDestroy(ev_scopy);
         }
-        for (hipEvent_t e : {ev_fk, ev_ch0, ev_ch1})
+        for (hipEvent_t e : {ev_fk, ev_ch0, ev_ch1, ev_fa, ev_wa})
             if (e) (void)hipEventDestroy(e);
         kslots.release();
         for (PinnedBuf* b : {&h_kents, &h_chain, &h_chain_out, &h_chain_ev}) b->release();
@@ -100,7 +102,7 @@ struct BatchState {
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_files, &h_hit, &h_win0, &h_bucket, &h_first,
                              &h_iv, &h_tiles, &h_ptiles, &h_req, &h_gw, &h_gb, &h_ow, &h_ob, &h_win, &h_copies,
-                             &h_tabents, &h_flagents, &h_dkeys, &h_ccopies, &h_lead})
+                             &h_tabents, &h_flagents, &h_flagents_a, &h_dkeys, &h_ccopies, &h_lead})
             b->release();
     }
 };
@@ -202,6 +204,7 @@ struct FileScan {
     const int32_t* d_weak = nullptr;
     const uint8_t* d_strong = nullptr;
     int64_t n = 0, B = 0, na = 0, nf = 0;
+    int64_t na_a = 0;  // two-phase chain walk: the windows of its prefix speculation (na: one phase)
     int32_t C = 0, dl = 0;
     uint32_t ns = 0;
     int64_t off_tw = 0, off_ts = 0, off_na = 0, off_as = 0, off_nf = 0, off_ns = 0, off_hit = 0, off_w0 = 0;
@@ -682,6 +685,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     RSH_BHIP(S->h_ccopies.ensure((size_t)NF * sizeof(CopyEnt) + (size_t)3 * NF * sizeof(CopyEnt)));
     RSH_BHIP(S->h_tabents.ensure((size_t)NF * sizeof(TableEnt)));
     RSH_BHIP(S->h_flagents.ensure((size_t)NF * sizeof(FlagEnt)));
+    RSH_BHIP(S->h_flagents_a.ensure((size_t)NF * sizeof(FlagEnt)));
     std::vector<K1File> k1;
     for (FileScan& fs : files)
         k1.push_back(K1File{fs.d_src, fs.n, (uint32_t)fs.B, (uint32_t)fs.dl, (uint32_t)fs.na,
@@ -691,11 +695,50 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     int lane_align = 16;
     bool partial = tail_gather_on();
     uint32_t ngroups = plan_block_sums_files(k1.data(), NF, &plans, &lanes, &lane_align, &partial);
-    RSH_BHIP(S->k1_groups.ensure(((size_t)ngroups + 1) * sizeof(K1Group)));
-    RSH_BHIP(S->k1_plans.ensure((plans.size() + 1) * sizeof(K1Plan)));
-    RSH_BHIP(S->k1_lanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
     RSH_BHIP(S->ensure_file_abort(NF));
     for (K1Plan& pl : plans) pl.abort = S->file_abort + pl.file;
+    // The chain walk (option batch_chain, with the default speculation policy) runs after the speculation.  Two
+    // phases (option batch_chain_prefix): the speculation over each file's first na_a windows -- about one round of
+    // the chip's wave slots over the whole batch -- and a walk over them; then the rest of the speculation for the
+    // files whose walk reached the prefix's end (the others' groups stop at once: the walk wrote their abort words)
+    // and a second walk.  A file that leaves the synced state early (an edit) costs its prefix, not its whole length.
+    const bool chain_on = opt(OPT_BATCH_CHAIN) != 0 && opt(OPT_BATCH_SPEC) == -1;
+    bool two_phase = false;
+    std::vector<K1Plan> plans_a, plans_b;
+    std::vector<K1Lane> lanes_a, lanes_b;
+    int align_a = 16, align_b = 16;
+    bool partial_a = tail_gather_on(), partial_b = tail_gather_on();
+    uint32_t ng_a = 0, ng_b = 0;
+    for (FileScan& fs : files) fs.na_a = fs.na;
+    if (const int64_t pre = opt(OPT_BATCH_CHAIN_PREFIX); chain_on && pre != 0) {
+        const int64_t P = pre > 0 ? pre : 64 * std::max<int64_t>(1, kWaveSlots / std::max<int32_t>(NF, 1));
+        for (FileScan& fs : files) {
+            fs.na_a = std::min(fs.na, P);
+            two_phase = two_phase || fs.na_a < fs.na;
+        }
+    }
+    if (two_phase) {
+        std::vector<K1File> ka, kb;
+        std::vector<int32_t> b_file;
+        for (int32_t f = 0; f < NF; ++f) {
+            FileScan& fs = files[(size_t)f];
+            ka.push_back(K1File{fs.d_src, std::min<int64_t>(fs.n, fs.na_a * fs.B), (uint32_t)fs.B, (uint32_t)fs.dl,
+                                (uint32_t)fs.na_a, S->src_weak.as<int32_t>() + fs.off_na,
+                                S->src_strong.as<uint8_t>() + fs.off_as});
+            if (fs.na_a == fs.na) continue;
+            kb.push_back(K1File{fs.d_src + fs.na_a * fs.B, fs.n - fs.na_a * fs.B, (uint32_t)fs.B, (uint32_t)fs.dl,
+                                (uint32_t)(fs.na - fs.na_a), S->src_weak.as<int32_t>() + fs.off_na + fs.na_a,
+                                S->src_strong.as<uint8_t>() + fs.off_as + fs.na_a * fs.dl});
+            b_file.push_back(f);
+        }
+        ng_a = plan_block_sums_files(ka.data(), (int32_t)ka.size(), &plans_a, &lanes_a, &align_a, &partial_a);
+        ng_b = plan_block_sums_files(kb.data(), (int32_t)kb.size(), &plans_b, &lanes_b, &align_b, &partial_b);
+        for (K1Plan& pl : plans_a) pl.abort = nullptr;  // the launch's word
+        for (K1Plan& pl : plans_b) pl.abort = S->file_abort + b_file[(size_t)pl.file];
+    }
+    RSH_BHIP(S->k1_groups.ensure(((size_t)std::max(ngroups, ng_a + ng_b) + 1) * sizeof(K1Group)));
+    RSH_BHIP(S->k1_plans.ensure((std::max(plans.size(), plans_a.size() + plans_b.size()) + 1) * sizeof(K1Plan)));
+    RSH_BHIP(S->k1_lanes.ensure((std::max(lanes.size(), lanes_a.size() + lanes_b.size()) + 1) * sizeof(K1Lane)));
 
     // per-file host state
     ScanFile* F = S->h_files.as<ScanFile>();
@@ -801,12 +844,11 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         te[f] = TableEnt{S->slots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
     }
     RSH_BHIP(launch_table_insert_many(te, (uint32_t)NF, (int32_t)maxC, st, bg));
-    // The chain walk (option batch_chain, with the default speculation policy): the speculation runs at once for
-    // every file, and one launch walks each file's Sender state machine on the device from its start for as long
-    // as the state stays synced and unpoisoned and every digest it needs is speculated (device.hip
-    // chain_advance_kernel).  The resolvers start where the walks stopped -- files whose walk reached the end
-    // need none -- instead of taking one device round trip per event from the start.  Its chunk indexes go here.
-    const bool chain_on = opt(OPT_BATCH_CHAIN) != 0 && opt(OPT_BATCH_SPEC) == -1;
+    // The chain walk: the speculation runs at once for every file, and one launch walks each file's Sender state
+    // machine on the device from its start for as long as the state stays synced and unpoisoned and every digest
+    // it needs is speculated (device.hip chain_advance_kernel; two phases: see above).  The resolvers start where
+    // the walks stopped -- files whose walk reached the end need none -- instead of taking one device round trip
+    // per event from the start.  Its chunk indexes go here.
     if (chain_on) {
         RSH_BHIP(S->kslots.ensure((size_t)tns * 8));
         RSH_BHIP(S->h_kents.ensure((size_t)NF * sizeof(TableEnt)));
@@ -937,9 +979,6 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     }
     bool spec_launched = false;
     if (chain_on) {  // the speculation, then the walks on the context stream (beside the sums' download on aux)
-        const int r = launch_spec();
-        if (r != RSH_OK) return r;
-        spec_launched = true;
         ChainFile* cf = S->h_chain.as<ChainFile>();
         ChainOut* co = S->h_chain_out.as<ChainOut>();
         rsh_event* ce = S->h_chain_ev.as<rsh_event>();
@@ -950,17 +989,77 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                               S->slots.as<unsigned long long>() + fs.off_ns, fs.ns - 1, fs.ns - 1,
                               S->kslots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.d_strong,
                               S->src_weak.as<int32_t>() + fs.off_na, S->src_strong.as<uint8_t>() + fs.off_as,
-                              S->flags.as<uint8_t>() + fs.off_nf, fs.na, ce + (int64_t)f * kChainEvents, kChainEvents,
+                              S->flags.as<uint8_t>() + fs.off_nf, fs.na, fs.na_a,
+                              two_phase ? S->file_abort + f : nullptr, ce + (int64_t)f * kChainEvents, kChainEvents,
                               seed_word(seed), co + f};
         }
-        RSH_BHIP(hipStreamWaitEvent(st, S->ev_fk, 0));
-        if (opt(OPT_SCAN_TRACE) != 0) {  // the walk's own duration (trace only)
+        const bool tr = opt(OPT_SCAN_TRACE) != 0;
+        if (tr) {  // the walks' own duration (trace only)
             for (hipEvent_t* e : {&S->ev_ch0, &S->ev_ch1})
                 if (!*e) RSH_BHIP(hipEventCreate(e));
-            RSH_BHIP(hipEventRecord(S->ev_ch0, st));
         }
-        RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st));
-        if (opt(OPT_SCAN_TRACE) != 0) RSH_BHIP(hipEventRecord(S->ev_ch1, st));
+        if (two_phase) {
+            // phase 0: the prefix speculation (groups and lanes of both phases staged in one upload), its flags, the
+            // walks over it; phase 1's K1 follows the walks, which stop the groups of the files they finished
+            for (hipEvent_t* e : {&S->ev_fa, &S->ev_wa})
+                if (!*e) RSH_BHIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+            if (!S->ev_scopy) RSH_BHIP(hipEventCreateWithFlags(&S->ev_scopy, hipEventDisableTiming));
+            if (S->scopy_pending) RSH_BHIP(hipEventSynchronize(S->ev_scopy));  // the previous scan's upload is done
+            S->scopy_pending = false;
+            const size_t npa = plans_a.size(), npb = plans_b.size(), nla = lanes_a.size(), nlb = lanes_b.size();
+            RSH_BHIP(S->h_sgroups.ensure((npa + npb + 1) * sizeof(K1Plan)));
+            RSH_BHIP(S->h_slanes.ensure((nla + nlb + 1) * sizeof(K1Lane)));
+            K1Plan* hp = S->h_sgroups.as<K1Plan>();
+            std::copy(plans_a.begin(), plans_a.end(), hp);
+            std::copy(plans_b.begin(), plans_b.end(), hp + npa);
+            K1Lane* hl = S->h_slanes.as<K1Lane>();
+            std::copy(lanes_a.begin(), lanes_a.end(), hl);
+            std::copy(lanes_b.begin(), lanes_b.end(), hl + nla);
+            if (npa + npb > 0)
+                RSH_BHIP(hipMemcpyAsync(S->k1_plans.p, hp, (npa + npb) * sizeof(K1Plan), hipMemcpyHostToDevice, aux));
+            if (npa > 0)
+                RSH_BHIP(launch_expand_groups(S->k1_plans.as<K1Plan>(), (uint32_t)npa, ng_a, S->k1_groups.as<K1Group>(), aux));
+            if (npb > 0)
+                RSH_BHIP(launch_expand_groups(S->k1_plans.as<K1Plan>() + npa, (uint32_t)npb, ng_b,
+                                              S->k1_groups.as<K1Group>() + ng_a, aux));
+            if (nla + nlb > 0)
+                RSH_BHIP(hipMemcpyAsync(S->k1_lanes.p, hl, (nla + nlb) * sizeof(K1Lane), hipMemcpyHostToDevice, aux));
+            RSH_BHIP(hipEventRecord(S->ev_scopy, aux));
+            S->scopy_pending = true;
+            RSH_BHIP(hipStreamWaitEvent(aux, spec_after_prep ? c->ev_prep : c->ev_in, 0));
+            RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>(), ng_a, S->k1_lanes.as<K1Lane>(), (uint32_t)nla,
+                                             align_a, seed_word(seed), aux, c->abort_word, gen, partial_a));
+            RSH_BHIP(hipStreamWaitEvent(aux, c->ev_in, 0));  // the flags need the received tables
+            FlagEnt* fa = S->h_flagents_a.as<FlagEnt>();
+            uint32_t max_na = 0;
+            for (int32_t f = 0; f < NF; ++f) {
+                FileScan& fs = files[(size_t)f];
+                const uint32_t nflag = (uint32_t)std::min(fs.na_a, fs.nf);
+                fa[f] = FlagEnt{S->src_weak.as<int32_t>() + fs.off_na, S->src_strong.as<uint8_t>() + fs.off_as, fs.d_weak,
+                                fs.d_strong, S->flags.as<uint8_t>() + fs.off_nf, nflag, (uint32_t)fs.dl};
+                max_na = std::max(max_na, nflag);
+            }
+            RSH_BHIP(launch_chain_flags_many(fa, (uint32_t)NF, max_na, aux));
+            RSH_BHIP(hipEventRecord(S->ev_fa, aux));
+            RSH_BHIP(hipStreamWaitEvent(st, S->ev_fa, 0));
+            const int gen_b = ++c->gen;
+            if (tr) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
+            RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, 0, gen_b));
+            RSH_BHIP(hipEventRecord(S->ev_wa, st));
+            RSH_BHIP(hipStreamWaitEvent(aux, S->ev_wa, 0));
+            RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>() + ng_a, ng_b, S->k1_lanes.as<K1Lane>() + nla,
+                                             (uint32_t)nlb, align_b, seed_word(seed), aux, c->abort_word, gen_b, partial_b));
+            k1_launched = true;
+            if (opt(OPT_SCAN_TRACE))
+                fprintf(stderr, "[rsh-batch] two-phase speculation: prefix %u groups, rest %u groups\n", ng_a, ng_b);
+        }
+        const int r = launch_spec();  // (two phases: the flags of whole files and the downloads)
+        if (r != RSH_OK) return r;
+        spec_launched = true;
+        RSH_BHIP(hipStreamWaitEvent(st, S->ev_fk, 0));
+        if (tr && !two_phase) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
+        RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, two_phase ? 1 : 0, 0));
+        if (tr) RSH_BHIP(hipEventRecord(S->ev_ch1, st));
     }
     const double enq_ms = ms_since(t0);
     RSH_BHIP(hipEventSynchronize(c->ev_tab));
@@ -986,6 +1085,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             fs.rs.m = o.m;
             fs.rs.pref = o.pref;
             fs.rs.anchor = o.s;
+            // a walk that stopped inside the prefix leaves only the prefix speculated (its file's other groups
+            // stopped): the resolver's aligned lookups end there
+            fs.be.na = o.aborted ? fs.na_a : fs.na;
             if (o.md5c_valid) {  // poisoned at an unaligned hit: the resolver goes on with the stale digest
                 fs.rs.md5c.assign(o.md5c, o.md5c + fs.dl);
                 fs.rs.md5c_valid = true;
@@ -1003,7 +1105,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         if (trace) {
             float kms = 0.f;
             if (S->ev_ch0 && S->ev_ch1) (void)hipEventElapsedTime(&kms, S->ev_ch0, S->ev_ch1);
-            int64_t tsum = 0, esum = 0, dsum = 0, psum = 0;
+            int64_t tsum = 0, esum = 0, dsum = 0, psum = 0, asum = 0;
             int32_t tmax = 0, emax = 0;
             for (int32_t f = 0; f < NF; ++f) {
                 tsum += co[f].tiles;
@@ -1011,11 +1113,13 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 esum += co[f].events;
                 dsum += co[f].digests;
                 psum += co[f].md5c_valid;
+                asum += co[f].aborted;
                 emax = std::max<int32_t>(emax, (int32_t)co[f].events);
             }
             fprintf(stderr, "[rsh-batch] chain walks done at %.3f ms (kernel %.3f ms; tiles %lld, max %d per file; events "
-                    "%lld, max %d; %lld windows digested, %lld files poisoned): %d of %d files left to the resolvers\n",
-                    ms_since(t0), kms, (long long)tsum, tmax, (long long)esum, emax, (long long)dsum, (long long)psum, left, NF);
+                    "%lld, max %d; %lld windows digested, %lld files poisoned, %lld speculations stopped at the prefix): %d of %d "
+                    "files left to the resolvers\n", ms_since(t0), kms, (long long)tsum, tmax, (long long)esum, emax,
+                    (long long)dsum, (long long)psum, (long long)asum, left, NF);
         }
     }
     if (tentative) {
@@ -1272,7 +1376,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             agg->host_md5_windows += s.host_md5_windows;
             agg->flushes += s.flushes;
             agg->table_ms += s.table_ms + fs.table.sort_ms;
-            agg->device_bytes += fs.be.bytes_read + ((spec_launched && b.landed.load() && !fs.cancelled) ? fs.n : 0);
+            int64_t spec_bytes = (spec_launched && b.landed.load() && !fs.cancelled) ? fs.n : 0;
+            if (spec_bytes > 0 && fs.be.na < fs.na)  // a two-phase file that stopped in its prefix (+ a short last chunk)
+                spec_bytes = std::min<int64_t>(fs.n, fs.be.na * fs.B) + fs.n % fs.B;
+            agg->device_bytes += fs.be.bytes_read + spec_bytes;
             agg->phase_matches += s.phase_matches;
         }
     }

@@ -265,7 +265,8 @@ inline uint32_t slot_hash_host(uint32_t key) {
 // walks Sender.sendMatchesAndData on the device while the state stays synced and unpoisoned and every digest
 // comes from the aligned speculation; it stops before any other step, which the host resolver then takes.
 // ChainOut holds the state on entry (s, m, pref) and on return; events go to ev (device-readable, ev_cap).
-enum { CHAIN_STOP = 0, CHAIN_DONE = 1 };
+// CHAIN_MORE: the walk reached the end of a prefix speculation (phase 0); phase 1 resumes it over the whole file
+enum { CHAIN_STOP = 0, CHAIN_DONE = 1, CHAIN_MORE = 2 };
 constexpr int CHAIN_BUCKET_CAP = 64;
 struct ChainOut {
     int64_t s, m;
@@ -275,6 +276,8 @@ struct ChainOut {
     // stopped on a poisoned state (quirk B): the stale cached digest, the window's at the hit (md5c_valid = 1)
     uint8_t md5c[16];
     int32_t md5c_valid, digests;  // digests: windows the walk digested itself (unaligned hits)
+    int32_t spec_full;            // phase 1 walked it
+    int32_t aborted;              // phase 0 stopped its phase-1 K1 groups: only the prefix is speculated
 };
 struct ChainFile {
     const uint8_t* data;
@@ -291,12 +294,16 @@ struct ChainFile {
     const uint8_t* as;
     const uint8_t* flags;
     int64_t na;
+    int64_t na_a;                      // phase 0: the speculated prefix's windows (<= na)
+    int* abort;                        // phase 0 writes abort_gen here when the file needs no more speculation: done,
+                                       // or poisoned by a digest no chunk carries (its phase-1 K1 groups stop)
     rsh_event* ev;
     int32_t ev_cap;
     uint32_t seed;                     // the checksum seed (a window's digest at an unaligned hit)
     ChainOut* out;
 };
-hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s);
+hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s, int phase = 1,
+                                int abort_gen = 0);
 // The chunk indexes of many files (slots cleared by the caller; TableEnt as for the probe hashes).
 hipError_t launch_chunk_index(const TableEnt* ents, uint32_t nfiles, int32_t max_keys, hipStream_t s, bool bg = false);
 

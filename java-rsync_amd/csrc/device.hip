@@ -2629,7 +2629,8 @@ __device__ __forceinline__ bool chain_digest_eq(const uint8_t* __restrict__ a, c
     return true;
 }
 
-__global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const ChainFile* __restrict__ files) {
+__global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const ChainFile* __restrict__ files, int phase,
+                                                                      int abort_gen) {
     __builtin_amdgcn_s_setprio(3);
     __shared__ int32_t sh[4 * CHAIN_THREADS / 64];
     __shared__ int32_t s_hit;                  // first hit in a tile (offset from the tile start), or INT_MAX
@@ -2638,26 +2639,34 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_nbk;
     __shared__ int64_t s_zero;                 // first unset chain flag
     __shared__ int32_t s_wtmp;                 // an unaligned window's sums (its digest: s_dig)
+    __shared__ int32_t s_any;                  // some chunk carries the stale digest
     __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
     // fields across the loop (the event stores may alias it) -- a PCIe round trip each
     const ChainFile F = files[blockIdx.x];
     ChainOut* out = F.out;
+    // phase 0 walks over the prefix speculation [0, na_a); phase 1 resumes the walks that reached its end
+    if (phase == 1 && out->status != CHAIN_MORE) return;
     const int t = threadIdx.x;
     const int64_t n = F.n, B = F.B, C = F.C;
     const int dl = F.dl;
     const int64_t S = F.rem > 0 ? F.rem : B;  // Checksum.java:131-137
     const int64_t last = n - S, nB = n - B;
-    const int64_t na = F.na, nflags = F.na < C ? F.na : C;
+    const int64_t na = phase == 0 ? F.na_a : F.na, nflags = na < C ? na : C;
     const ProbeTable table{F.slots, F.mask};
     int64_t s = out->s, m = out->m;
     int32_t pref = out->pref;
-    int32_t nev = 0, status = CHAIN_STOP;
-    int64_t lit = 0, mat = 0, chain_matches = 0, events = 0;
-    int32_t tiles = 0, digests = 0, poisoned = 0;
+    int32_t nev = out->n_ev, status = CHAIN_STOP;
+    int64_t lit = out->literal, mat = out->matched, chain_matches = out->chain_matches, events = out->events;
+    int32_t tiles = out->tiles, digests = out->digests, poisoned = 0, dead = 0;
     const uint8_t* stale = nullptr;  // poisoned: the cached digest
     rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
     bool have = false;
+    if (nev > 0) {  // phase 1: the last event stays open (a MATCH run may go on across the prefix's end)
+        pend = F.ev[nev - 1];
+        have = true;
+        --nev;
+    }
     auto flush_pend = [&]() {
         if (have && t == 0) F.ev[nev] = pend;
         if (have) ++nev;
@@ -2821,7 +2830,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             q0 = qend;
         }
         if (p < 0) {
-            if (cut || f <= last) break;  // past the speculation, or a flush (quirk A): the host
+            if (cut) {  // past the speculation: the rest of it (phase 1), or the host
+                if (na < F.na) status = CHAIN_MORE;
+                break;
+            }
+            if (f <= last) break;  // a flush (quirk A): the host
             emit_lit(m, n - m);           // no candidate before the end
             status = CHAIN_DONE;
             s = n;
@@ -2900,6 +2913,14 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 s = p + 1;
                 poisoned = 1;
                 stale = md5c;
+                // no chunk carries the stale digest: nothing can match again (the host's closed form), so the
+                // file needs no more speculation
+                if (t == 0) s_any = 0;
+                __syncthreads();
+                for (int64_t c = t; c < C; c += CHAIN_THREADS)
+                    if (chain_digest_eq(F.table_strong + c * dl, stale, dl)) s_any = 1;
+                __syncthreads();
+                dead = s_any == 0;
             }
             break;
         }
@@ -2917,6 +2938,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->n_ev = nev;
         out->tiles = tiles;
         out->digests = digests;
+        out->spec_full = phase == 1;
+        // a file that needs no more speculation stops its phase-1 K1 groups (they poll this word); any other stop
+        // keeps them (the resolver's aligned lookups past the prefix use them)
+        const bool stop_spec = phase == 0 && F.abort && (status == CHAIN_DONE || dead);
+        out->aborted = stop_spec;
+        if (stop_spec) *(volatile int*)F.abort = abort_gen;
         out->md5c_valid = poisoned;
         if (poisoned)
             for (int j = 0; j < dl && j < 16; ++j) out->md5c[j] = stale[j];
@@ -2927,9 +2954,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     }
 }
 
-hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s) {
+hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s, int phase, int abort_gen) {
     if (nfiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(chain_advance_kernel, dim3(nfiles), dim3(CHAIN_THREADS), 0, s, files);
+    hipLaunchKernelGGL(chain_advance_kernel, dim3(nfiles), dim3(CHAIN_THREADS), 0, s, files, phase, abort_gen);
     return hipGetLastError();
 }
 
