@@ -74,14 +74,17 @@ def _pack(ctx, blobs, misalign):
     return d, offs
 
 
-@pytest.mark.parametrize("gather,chain", [("1", "1"), ("0", "1"), ("1", "0")])
-def test_batch_generator_and_scan_match_oracle(ctx, gather, chain, rsh_opt):
+@pytest.mark.parametrize("gather,chain,prefix", [("1", "1", -1), ("0", "1", -1), ("1", "0", -1), ("1", "1", 3),
+                                                  ("0", "1", 64)])
+def test_batch_generator_and_scan_match_oracle(ctx, gather, chain, prefix, rsh_opt):
     # gather=1: each file's full chunks past its last full wave run as a gathered wave of the batched launch
     # (K1Group::count < 64); 0: one per lane in the lane kernel (option k1_gather).  chain=1 (default): the
     # device walks each file's state machine until a step it leaves to the host resolver (device.hip
-    # chain_advance_kernel); 0: the resolvers from the start (option batch_chain)
+    # chain_advance_kernel); 0: the resolvers from the start (option batch_chain).  prefix: the two-phase walk's
+    # prefix in windows (option batch_chain_prefix; -1 = auto, which these small files fit whole: one phase)
     rsh_opt("k1_gather", int(gather))
     rsh_opt("batch_chain", int(chain))
+    rsh_opt("batch_chain_prefix", prefix)
     rng = random.Random(2024)
     files = _segment(rng, 48)
     mis = [0 if rng.random() < 0.8 else rng.choice([1, 3, 4, 8]) for _ in files]
@@ -268,13 +271,14 @@ def test_batch_speculation_cancelled_per_file(ctx):
                 assert got == oev and (sj[j].literal, sj[j].matched) == (olit, omat), f"small file {j}"
 
 
-@pytest.mark.parametrize("alphabet", [2, 4, 16])
-def test_batch_chain_low_entropy(ctx, alphabet):
+@pytest.mark.parametrize("alphabet,prefix", [(2, -1), (4, -1), (16, -1), (2, 5), (16, 7)])
+def test_batch_chain_low_entropy(ctx, alphabet, prefix, rsh_opt):
     """The device chain walk against the oracle where weak-sum collisions are everywhere: bytes from a small
     alphabet, so the first table hit after a modified block is usually a false one at an unaligned position
     (the walk must find exactly that position, hand the poisoning step to the host -- quirk B -- and never
     match a later aligned block the Java scan no longer reaches).  Forms: every other block replaced, an
     insert, unrelated; B from 512 to 8192."""
+    rsh_opt("batch_chain_prefix", prefix)  # > 0: the two-phase walk (prefix speculation, then the rest)
     rng = random.Random(77 + alphabet)
     files = []
     for i in range(24):
