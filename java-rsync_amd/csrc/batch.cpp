@@ -1001,8 +1001,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         if (two_phase) {
             // phase 0: the prefix speculation (groups and lanes of both phases staged in one upload), its flags, the
             // walks over it; phase 1's K1 follows the walks, which stop the groups of the files they finished
-            for (hipEvent_t* e : {&S->ev_fa, &S->ev_wa})
-                if (!*e) RSH_BHIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+            if (!S->ev_fa) RSH_BHIP(hipEventCreateWithFlags(&S->ev_fa, hipEventDisableTiming));
+            if (!S->ev_wa) RSH_BHIP(hipEventCreate(&S->ev_wa));  // timed: the trace reports phase 0's walk
             if (!S->ev_scopy) RSH_BHIP(hipEventCreateWithFlags(&S->ev_scopy, hipEventDisableTiming));
             if (S->scopy_pending) RSH_BHIP(hipEventSynchronize(S->ev_scopy));  // the previous scan's upload is done
             S->scopy_pending = false;
@@ -1046,7 +1046,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             if (tr) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
             RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, 0, gen_b));
             RSH_BHIP(hipEventRecord(S->ev_wa, st));
-            RSH_BHIP(hipStreamWaitEvent(aux, S->ev_wa, 0));
+            // the rest of the speculation after the walks (the groups of files they finished stop at once), or
+            // (option batch_chain_overlap) beside them: no gap after the prefix's K1, but the walks share the chip
+            if (opt(OPT_BATCH_CHAIN_OVERLAP) == 0) RSH_BHIP(hipStreamWaitEvent(aux, S->ev_wa, 0));
             RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>() + ng_a, ng_b, S->k1_lanes.as<K1Lane>() + nla,
                                              (uint32_t)nlb, align_b, seed_word(seed), aux, c->abort_word, gen_b, partial_b));
             k1_launched = true;
@@ -1103,8 +1105,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             for (FileScan& fs : files) fs.be.head = false;
         }
         if (trace) {
-            float kms = 0.f;
+            float kms = 0.f, wams = 0.f;
             if (S->ev_ch0 && S->ev_ch1) (void)hipEventElapsedTime(&kms, S->ev_ch0, S->ev_ch1);
+            if (two_phase && S->ev_ch0 && S->ev_wa) (void)hipEventElapsedTime(&wams, S->ev_ch0, S->ev_wa);
             int64_t tsum = 0, esum = 0, dsum = 0, psum = 0, asum = 0;
             int32_t tmax = 0, emax = 0;
             for (int32_t f = 0; f < NF; ++f) {
@@ -1116,9 +1119,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 asum += co[f].aborted;
                 emax = std::max<int32_t>(emax, (int32_t)co[f].events);
             }
-            fprintf(stderr, "[rsh-batch] chain walks done at %.3f ms (kernel %.3f ms; tiles %lld, max %d per file; events "
+            fprintf(stderr, "[rsh-batch] chain walks done at %.3f ms (walks %.3f ms, phase 0 %.3f ms; tiles %lld, max %d per file; events "
                     "%lld, max %d; %lld windows digested, %lld files poisoned, %lld speculations stopped at the prefix): %d of %d "
-                    "files left to the resolvers\n", ms_since(t0), kms, (long long)tsum, tmax, (long long)esum, emax,
+                    "files left to the resolvers\n", ms_since(t0), kms, wams, (long long)tsum, tmax, (long long)esum, emax,
                     (long long)dsum, (long long)psum, (long long)asum, left, NF);
         }
     }

@@ -2621,7 +2621,45 @@ hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const Part
 // All lanes keep the same copy of the state (s, mark, pref) and take the same decisions (every value they
 // branch on is read from global memory or LDS by all of them); lane 0 writes the events.
 // ------------------------------------------------------------------------------------------------
-constexpr int CHAIN_THREADS = PROBE_THREADS;
+constexpr int CHAIN_THREADS = 512;                      // 8 waves (2 per SIMD: 256 VGPRs each)
+constexpr int64_t CHAIN_TILE = (int64_t)CHAIN_THREADS * PROBE_PPT;
+constexpr int CHAIN_SEGS = 64;                           // blocks a tile may start (B >= 512 when wide)
+
+// The first of a lane's 16 keys (bit i of valid: position i is in the search) that the table holds, or -1: the 16
+// first hash slots in one burst of independent loads (as probe_first_kernel: most keys are decided by their first
+// slot, so a lane waits for about one L2 round trip, not 16), then the full lookup only for keys whose first slot
+// holds another key, in order and only before the first certain hit (one out-of-line lookup loop, few registers)
+__device__ __forceinline__ int chain_first_hit16(const ProbeTable& table, const uint32_t (&keys)[PROBE_PPT], uint32_t valid) {
+    uint32_t hit = 0, need = 0;
+    {
+        unsigned long long sl[PROBE_PPT];
+#pragma unroll
+        for (int i = 0; i < PROBE_PPT; ++i) sl[i] = table.slots[slot_hash(keys[i]) & table.mask];
+#pragma unroll
+        for (int i = 0; i < PROBE_PPT; ++i) {
+            if (sl[i] == ((1ull << 32) | keys[i])) hit |= 1u << i;
+            else if (sl[i] != 0ull) need |= 1u << i;
+        }
+    }
+    hit &= valid;
+    need &= valid & (hit ? (hit & (0u - hit)) - 1u : 0xFFFFFFFFu);
+    while (need) {
+        const int i = __builtin_ctz(need);
+        uint32_t kk = 0;
+#pragma unroll
+        for (int j = 0; j < PROBE_PPT; ++j)
+            if (j == i) kk = keys[j];
+        if (table_has(table, kk)) return i;
+        need &= need - 1u;
+    }
+    return hit ? __builtin_ctz(hit) : -1;
+}
+
+// one lane digests an unaligned hit's window: out of line, so that the walk's tile search keeps its registers
+__device__ __attribute__((noinline)) void chain_window_digest(const uint8_t* x, int64_t n, uint32_t B, uint32_t dl,
+                                                              uint32_t seed, int32_t* w, uint8_t* dig) {
+    lane_chunk_sums<0, 2, false>(x, n, B, 0u, dl, seed, w, dig);
+}
 
 __device__ __forceinline__ bool chain_digest_eq(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int dl) {
     for (int j = 0; j < dl; ++j)
@@ -2640,6 +2678,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int64_t s_zero;                 // first unset chain flag
     __shared__ int32_t s_wtmp;                 // an unaligned window's sums (its digest: s_dig)
     __shared__ int32_t s_any;                  // some chunk carries the stale digest
+    __shared__ int32_t s_seg[CHAIN_SEGS][4];   // wide tiles: the exscan at each block's first lane
     __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
     // fields across the loop (the event stores may alias it) -- a PCIe round trip each
@@ -2654,6 +2693,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const int64_t last = n - S, nB = n - B;
     const int64_t na = phase == 0 ? F.na_a : F.na, nflags = na < C ? na : C;
     const ProbeTable table{F.slots, F.mask};
+    const bool wide = (B % 16) == 0 && B >= 512 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
     int64_t s = out->s, m = out->m;
     int32_t pref = out->pref;
     int32_t nev = out->n_ev, status = CHAIN_STOP;
@@ -2752,9 +2792,101 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             if (table_has(table, key)) p = s;
             else a = s + 1;
         }
-        // tiles of PROBE_TILE positions in block coordinates, from a's tile on, until the first hit
         bool cut = false;  // the search reached windows past the speculation (no anchor T(o))
-        for (int64_t q0 = (a / B) * B + ((a % B) / PROBE_TILE) * PROBE_TILE; p < 0 && q0 <= stop;) {
+        if (wide) {
+            // tiles of CHAIN_TILE positions from a (lane-aligned), across block boundaries: each lane anchors its
+            // 16 positions on its own block's T(o); the prefix sums from o come from one exscan over the tile
+            // with weights relative to the tile start, rebased at each block's first lane (a segmented scan), and
+            // the head of the block the tile starts in (range_sums from o to the tile)
+            const int64_t lim_spec = na * B - 1;  // windows with an anchor: blocks < na
+            const int64_t qlast = stop < lim_spec ? stop : lim_spec;
+            for (int64_t q0 = a & ~(int64_t)15; p < 0 && q0 <= qlast;) {
+                ++tiles;
+                const int64_t kb0 = q0 / B, o0 = kb0 * B;
+                int32_t head[4] = {0, 0, 0, 0};
+                if (q0 > o0) {
+                    range_sums(F.data, n, o0, q0, o0, head[0], head[1]);
+                    range_sums(F.data, n, o0 + B, q0 + B, o0, head[2], head[3]);
+                    block_reduce<4>(head, sh);
+                }
+                const int64_t p0 = q0 + (int64_t)t * PROBE_PPT;
+                const int64_t kb = p0 / B, o = kb * B;
+                uint32_t xa[4], xb[4];
+                load16(F.data, n, p0, xa);
+                load16(F.data, n, p0 + B, xb);
+                const bool live = p0 <= stop && p0 <= lim_spec && p0 + PROBE_PPT > a;
+                const int32_t To = live ? F.aw[kb] : 0;
+                int32_t pre[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int i = 0; i < PROBE_PPT; ++i) {
+                    const int32_t va = sbyte_of(xa, i), vb = sbyte_of(xb, i);
+                    pre[0] += va;
+                    pre[1] += (int32_t)((uint32_t)(p0 + i - q0) * (uint32_t)va);
+                    pre[2] += vb;
+                    pre[3] += (int32_t)((uint32_t)(p0 + B + i - q0) * (uint32_t)vb);
+                }
+                block_exscan<4>(pre, sh);  // sums over [q0, p0) and [q0 + B, p0 + B), weights j - q0
+                if (p0 == o) {              // a block's first lane: its rebasing point
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) s_seg[kb - kb0][v] = pre[v];
+                }
+                if (t == 0) s_hit = 0x7FFFFFFF;
+                __syncthreads();
+                uint32_t keys[PROBE_PPT];
+                if (live) {
+                    uint32_t pa, pa2, pb, pb2;  // sums over [o, p0) and [o + B, p0 + B), weights j - o
+                    if (o < q0) {               // the tile's first block: its head + the tile's part
+                        const uint32_t d = (uint32_t)(q0 - o);
+                        pa = (uint32_t)head[0] + (uint32_t)pre[0];
+                        pa2 = (uint32_t)head[1] + (uint32_t)pre[1] + d * (uint32_t)pre[0];
+                        pb = (uint32_t)head[2] + (uint32_t)pre[2];
+                        pb2 = (uint32_t)head[3] + (uint32_t)pre[3] + d * (uint32_t)pre[2];
+                    } else {                    // rebased at the block's first lane
+                        const int32_t* L = s_seg[kb - kb0];
+                        const uint32_t d = (uint32_t)(o - q0);
+                        pa = (uint32_t)(pre[0] - L[0]);
+                        pa2 = (uint32_t)(pre[1] - L[1]) - d * pa;
+                        pb = (uint32_t)(pre[2] - L[2]);
+                        pb2 = (uint32_t)(pre[3] - L[3]) - d * pb;
+                    }
+                    const uint32_t s1o = (uint32_t)To & 0xFFFFu, s2o = (uint32_t)To >> 16;
+                    const uint32_t P1e = s1o + pb;
+                    const uint32_t P2e = (uint32_t)B * s1o - s2o + pb2;
+                    const uint32_t s1 = P1e - pa;
+                    const uint32_t s2 = (uint32_t)(p0 + B - o) * s1 - (P2e - pa2);
+                    int32_t R = (int32_t)((s1 & 0xFFFFu) | (s2 << 16));
+#pragma unroll
+                    for (int i = 0; i < PROBE_PPT; ++i) {
+                        keys[i] = (uint32_t)R;
+                        R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(xa, i)), sbyte_of(xb, i));
+                    }
+                    uint32_t valid = 0;
+#pragma unroll
+                    for (int i = 0; i < PROBE_PPT; ++i) {
+                        const int64_t pp = p0 + i;
+                        if (pp >= a && pp <= stop && pp <= lim_spec) valid |= 1u << i;
+                    }
+                    const int h = chain_first_hit16(table, keys, valid);
+                    if (h >= 0) atomicMin(&s_hit, (int32_t)(p0 + h - q0));
+                }
+                __syncthreads();
+                if (s_hit != 0x7FFFFFFF && (s_hit >> 4) == t) {
+#pragma unroll
+                    for (int i = 0; i < PROBE_PPT; ++i)  // (a static index: keys stays in registers)
+                        if (i == (s_hit & 15)) s_key = keys[i];
+                }
+                __syncthreads();
+                if (s_hit != 0x7FFFFFFF) {
+                    p = q0 + s_hit;
+                    key = s_key;
+                }
+                __syncthreads();
+                q0 += CHAIN_TILE;
+            }
+            cut = p < 0 && stop > lim_spec;  // (lim_spec, stop] has no anchors: not searched
+        }
+        // narrow blocks (B not a multiple of 16, or < 512): tiles of PROBE_TILE positions in block coordinates
+        for (int64_t q0 = (a / B) * B + ((a % B) / PROBE_TILE) * PROBE_TILE; !wide && p < 0 && q0 <= stop;) {
             const int64_t kb = q0 / B, o = kb * B;
             if (kb >= na) {
                 cut = true;
@@ -2787,7 +2919,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             if (t == 0) s_hit = 0x7FFFFFFF;
             __syncthreads();
             uint32_t keys[PROBE_PPT];
-            if (p0 < qend && p0 <= stop && p0 + PROBE_PPT > a) {
+            if (t < PROBE_THREADS && p0 < qend && p0 <= stop && p0 + PROBE_PPT > a) {
                 const uint32_t pa = (uint32_t)(head[0] + pre[0]), pa2 = (uint32_t)(head[1] + pre[1]);
                 const uint32_t pb = (uint32_t)(head[2] + pre[2]), pb2 = (uint32_t)(head[3] + pre[3]);
                 const int32_t To = F.aw[kb];
@@ -2802,25 +2934,21 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     keys[i] = (uint32_t)R;
                     R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(xa, i)), sbyte_of(xb, i));
                 }
-                // the 16 keys' first hash slots in one burst of independent loads (as probe_first_kernel): most
-                // keys are decided by their first slot, so a lane waits for about one L2 round trip, not 16
-                unsigned long long sl[PROBE_PPT];
-#pragma unroll
-                for (int i = 0; i < PROBE_PPT; ++i) sl[i] = table.slots[slot_hash(keys[i]) & table.mask];
+                uint32_t valid = 0;
 #pragma unroll
                 for (int i = 0; i < PROBE_PPT; ++i) {
                     const int64_t pp = p0 + i;
-                    if (pp < a || pp > stop || pp >= qend) continue;
-                    bool hit = sl[i] == ((1ull << 32) | keys[i]);
-                    if (!hit && sl[i] != 0ull) hit = table_has(table, keys[i]);
-                    if (hit) {
-                        atomicMin(&s_hit, (int32_t)(pp - q0));
-                        break;
-                    }
+                    if (pp >= a && pp <= stop && pp < qend) valid |= 1u << i;
                 }
+                const int h = chain_first_hit16(table, keys, valid);
+                if (h >= 0) atomicMin(&s_hit, (int32_t)(p0 + h - q0));
             }
             __syncthreads();
-            if (s_hit != 0x7FFFFFFF && (s_hit >> 4) == t) s_key = keys[s_hit & 15];
+            if (s_hit != 0x7FFFFFFF && (s_hit >> 4) == t) {
+#pragma unroll
+                    for (int i = 0; i < PROBE_PPT; ++i)  // (a static index: keys stays in registers)
+                        if (i == (s_hit & 15)) s_key = keys[i];
+                }
             __syncthreads();
             if (s_hit != 0x7FFFFFFF) {
                 p = q0 + s_hit;
@@ -2886,7 +3014,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         // the window here (lane_chunk_sums over the B bytes at p, the seed appended), the host path's md5_at
         const uint8_t* md5c = F.as + kp * dl;
         if (!spec_digest) {
-            if (t == 0) lane_chunk_sums<0, 2, false>(F.data + p, n - p, (uint32_t)B, 0u, (uint32_t)dl, F.seed, &s_wtmp, s_dig);
+            if (t == 0) chain_window_digest(F.data + p, n - p, (uint32_t)B, (uint32_t)dl, F.seed, &s_wtmp, s_dig);
             __syncthreads();
             md5c = s_dig;
             ++digests;

@@ -38,6 +38,7 @@ enum Opt : int {
     OPT_BATCH_PREP_ALL,    // 1: the batched speculation after all the table work (full-width launches)
     OPT_BATCH_CHAIN,       // 1: the device-side chain advance of the batched scan (batch.cpp)
     OPT_BATCH_CHAIN_PREFIX,  // chain walk over a speculated prefix first (windows per file; -1 auto, 0 off)
+    OPT_BATCH_CHAIN_OVERLAP, // 1: the rest of the speculation starts beside the prefix walk (0: after it)
     OPT_HOST_CORES,        // resolver worker threads (0: the process's cores, cgroup quota included)
     OPT_FILE_TILE,         // rsh_match_scan_file: tile bytes above OPT_FILE_TILE_ABOVE
     OPT_FILE_TILE_ABOVE,   // rsh_match_scan_file: sources above this size are scanned tiled
@@ -56,7 +57,8 @@ inline const OptInfo* opt_info() {
         {"scan_preprobe", 1},      {"scan_samples", 256},     {"scan_sample", 1},      {"scan_spec_order", 1},
         {"scan_early", 1},         {"scan_wait", 1},          {"scan_defer_steps", 4}, {"scan_defer_us", 500},
         {"batch_spec", -1},        {"batch_spin_us", 200},    {"batch_readahead", 0},  {"batch_prep_all", 0},
-        {"batch_chain", 1},        {"batch_chain_prefix", -1}, {"host_cores", 0},         {"file_tile", 4LL << 30}, {"file_tile_above", 32LL << 30},
+        {"batch_chain", 1},        {"batch_chain_prefix", -1}, {"batch_chain_overlap", 0},
+        {"host_cores", 0},         {"file_tile", 4LL << 30}, {"file_tile_above", 32LL << 30},
     };
     return t;
 }
