@@ -1109,10 +1109,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             if (S->ev_ch0 && S->ev_ch1) (void)hipEventElapsedTime(&kms, S->ev_ch0, S->ev_ch1);
             if (two_phase && S->ev_ch0 && S->ev_wa) (void)hipEventElapsedTime(&wams, S->ev_ch0, S->ev_wa);
             int64_t tsum = 0, esum = 0, dsum = 0, psum = 0, asum = 0;
-            int32_t tmax = 0, emax = 0;
+            int32_t tmax = 0, emax = 0, fmax = 0;
             for (int32_t f = 0; f < NF; ++f) {
                 tsum += co[f].tiles;
-                tmax = std::max(tmax, co[f].tiles);
+                if (co[f].tiles > tmax) tmax = co[f].tiles, fmax = f;
                 esum += co[f].events;
                 dsum += co[f].digests;
                 psum += co[f].md5c_valid;
@@ -1123,6 +1123,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                     "%lld, max %d; %lld windows digested, %lld files poisoned, %lld speculations stopped at the prefix): %d of %d "
                     "files left to the resolvers\n", ms_since(t0), kms, wams, (long long)tsum, tmax, (long long)esum, emax,
                     (long long)dsum, (long long)psum, (long long)asum, left, NF);
+            const ChainOut& x = co[fmax];  // the walk with the most tiles: where its time went (10 ns ticks)
+            fprintf(stderr, "[rsh-batch]   file %d: walk %.1f us = tiles %.1f (table checks %.1f) + events %.1f (digests %.1f)"
+                    " + other\n", fmax, x.t_total / 100.0, x.t_tiles / 100.0, x.t_check / 100.0, x.t_event / 100.0,
+                    x.t_digest / 100.0);
         }
     }
     if (tentative) {

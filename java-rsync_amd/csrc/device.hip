@@ -2699,6 +2699,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     int32_t nev = out->n_ev, status = CHAIN_STOP;
     int64_t lit = out->literal, mat = out->matched, chain_matches = out->chain_matches, events = out->events;
     int32_t tiles = out->tiles, digests = out->digests, poisoned = 0, dead = 0;
+    const int64_t tk0 = (int64_t)wall_clock64();
+    int64_t t_tiles = 0, t_check = 0, t_event = 0, t_digest = 0;
     const uint8_t* stale = nullptr;  // poisoned: the cached digest
     rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
     bool have = false;
@@ -2802,6 +2804,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             const int64_t qlast = stop < lim_spec ? stop : lim_spec;
             for (int64_t q0 = a & ~(int64_t)15; p < 0 && q0 <= qlast;) {
                 ++tiles;
+                const int64_t tt0 = (int64_t)wall_clock64();
                 const int64_t kb0 = q0 / B, o0 = kb0 * B;
                 int32_t head[4] = {0, 0, 0, 0};
                 if (q0 > o0) {
@@ -2832,6 +2835,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 }
                 if (t == 0) s_hit = 0x7FFFFFFF;
                 __syncthreads();
+                const int64_t tc0 = (int64_t)wall_clock64();
                 uint32_t keys[PROBE_PPT];
                 if (live) {
                     uint32_t pa, pa2, pb, pb2;  // sums over [o, p0) and [o + B, p0 + B), weights j - o
@@ -2870,6 +2874,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     if (h >= 0) atomicMin(&s_hit, (int32_t)(p0 + h - q0));
                 }
                 __syncthreads();
+                t_check += (int64_t)wall_clock64() - tc0;
                 if (s_hit != 0x7FFFFFFF && (s_hit >> 4) == t) {
 #pragma unroll
                     for (int i = 0; i < PROBE_PPT; ++i)  // (a static index: keys stays in registers)
@@ -2882,6 +2887,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 }
                 __syncthreads();
                 q0 += CHAIN_TILE;
+                t_tiles += (int64_t)wall_clock64() - tt0;
             }
             cut = p < 0 && stop > lim_spec;  // (lim_spec, stop] has no anchors: not searched
         }
@@ -2969,6 +2975,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             break;
         }
         // the event at p: its bucket (Multimap order), the candidates of Checksum.getCandidateChunks
+        const int64_t te0 = (int64_t)wall_clock64();
         ++events;
         const int64_t kp = p / B;
         const bool spec_digest = p % B == 0 && kp < na;
@@ -3014,10 +3021,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         // the window here (lane_chunk_sums over the B bytes at p, the seed appended), the host path's md5_at
         const uint8_t* md5c = F.as + kp * dl;
         if (!spec_digest) {
+            const int64_t td0 = (int64_t)wall_clock64();
             if (t == 0) chain_window_digest(F.data + p, n - p, (uint32_t)B, (uint32_t)dl, F.seed, &s_wtmp, s_dig);
             __syncthreads();
             md5c = s_dig;
             ++digests;
+            t_digest += (int64_t)wall_clock64() - td0;
         }
         int32_t hit = -1;
         for (int32_t it = -1; it < size && hit < 0; ++it) {
@@ -3034,6 +3043,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             if (chain_digest_eq(md5c, F.table_strong + (int64_t)c * dl, dl)) hit = c;
         }
         __syncthreads();
+        t_event += (int64_t)wall_clock64() - te0;
         if (hit < 0) {
             // the cached digest is stale from here on (quirk B): the host goes on with it from p + 1 (a hit at the
             // flush point itself flushes there: the host retakes that step from s)
@@ -3066,6 +3076,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->n_ev = nev;
         out->tiles = tiles;
         out->digests = digests;
+        out->t_total += (int64_t)wall_clock64() - tk0;
+        out->t_tiles += t_tiles;
+        out->t_check += t_check;
+        out->t_event += t_event;
+        out->t_digest += t_digest;
         out->spec_full = phase == 1;
         // a file that needs no more speculation stops its phase-1 K1 groups (they poll this word); any other stop
         // keeps them (the resolver's aligned lookups past the prefix use them)
