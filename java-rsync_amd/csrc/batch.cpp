@@ -33,7 +33,7 @@ constexpr size_t kFiberStack = 512 * 1024;
 constexpr int32_t kEagerSortChunks = 1 << 16;  // tables up to this size are sorted before the first round
 constexpr int64_t kPad = 16;
 constexpr int64_t kWaveSlots = 2 * 4 * 256;  // the chip's K1 wave slots (2 waves per SIMD, 4 SIMDs, 256 CUs)
-constexpr int32_t kChainEvents = 1024;  // events one file's chain walk may emit before it hands over
+constexpr int32_t kChainEvents = 4096;  // events one file's chain walk may emit before it hands over
 
 int64_t pad16(int64_t v) { return (v + kPad - 1) / kPad * kPad; }
 }  // namespace
@@ -952,9 +952,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         }
         RSH_BHIP(launch_chain_flags_many(fe, (uint32_t)NF, max_nf, aux));
         if (chain_on) RSH_BHIP(hipEventRecord(S->ev_fk, aux));
-        RSH_BHIP(launch_copy_many(sc, nfl, max_fl, aux));
+        // (chain walks: the host copies follow the walks, for the files they leave to the resolvers only)
+        if (!chain_on) RSH_BHIP(launch_copy_many(sc, nfl, max_fl, aux));
         RSH_BHIP(hipEventRecord(c->ev_flags, aux));
-        RSH_BHIP(launch_copy_many(sc + nfl, nsc - nfl, max_len, aux));
+        if (!chain_on) RSH_BHIP(launch_copy_many(sc + nfl, nsc - nfl, max_len, aux));
         RSH_BHIP(hipEventRecord(c->ev_spec, aux));
         return RSH_OK;
     };
@@ -1083,6 +1084,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             fs.res.matched = o.matched;
             fs.res.stats.chain_matches += o.chain_matches;
             fs.res.stats.events += o.events;
+            fs.res.stats.flushes += o.flushes;
             fs.rs.s = o.s;
             fs.rs.m = o.m;
             fs.rs.pref = o.pref;
@@ -1099,8 +1101,23 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             else ++left;
         }
         b.landed.store(true);  // the walks ran after the speculation's K1 and flags
-        if (left > 0) {        // the host resolvers use the speculation's host copies
-            RSH_BHIP(hipEventSynchronize(c->ev_spec));
+        if (left > 0) {  // the host resolvers use the speculation's host copies: the left files' flags and sums
+            CopyEnt* lc = S->h_ccopies.as<CopyEnt>() + NF;
+            uint32_t nl = 0;
+            int64_t mx = 0;
+            for (FileScan& fs : files) {
+                if (fs.done) continue;
+                const int64_t nal = fs.be.na, nfl = std::min(fs.nf, nal);
+                if (nfl > 0) lc[nl++] = CopyEnt{S->flags.as<uint8_t>() + fs.off_nf, S->h_fl.as<uint8_t>() + fs.off_nf, nfl};
+                lc[nl++] = CopyEnt{S->src_weak.as<uint8_t>() + 4 * fs.off_na, S->h_aw.as<uint8_t>() + 4 * fs.off_na, nal * 4};
+                if (fs.dl > 0)
+                    lc[nl++] = CopyEnt{S->src_strong.as<uint8_t>() + fs.off_as, S->h_as.as<uint8_t>() + fs.off_as,
+                                       nal * fs.dl};
+                mx = std::max(mx, nal * 4);
+            }
+            RSH_BHIP(hipStreamWaitEvent(st, c->ev_spec, 0));
+            RSH_BHIP(launch_copy_many(lc, nl, mx, st));
+            RSH_BHIP(hipStreamSynchronize(st));
             b.aligned.store(true);
             for (FileScan& fs : files) fs.be.head = false;
         }

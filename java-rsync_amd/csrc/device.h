@@ -276,6 +276,7 @@ struct ChainOut {
     // stopped on a poisoned state (quirk B): the stale cached digest, the window's at the hit (md5c_valid = 1)
     uint8_t md5c[16];
     int32_t md5c_valid, digests;  // digests: windows the walk digested itself (unaligned hits)
+    int64_t flushes;              // FileView flushes of the closed form (a dead poisoned state)
     int64_t t_total, t_tiles, t_check, t_event, t_digest;  // wall-clock ticks (10 ns) of the walk's parts (trace)
     int32_t spec_full;            // phase 1 walked it
     int32_t aborted;              // phase 0 stopped its phase-1 K1 groups: only the prefix is speculated

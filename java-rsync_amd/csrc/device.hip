@@ -2699,6 +2699,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     int32_t nev = out->n_ev, status = CHAIN_STOP;
     int64_t lit = out->literal, mat = out->matched, chain_matches = out->chain_matches, events = out->events;
     int32_t tiles = out->tiles, digests = out->digests, poisoned = 0, dead = 0;
+    int64_t flushes = out->flushes;
     const int64_t tk0 = (int64_t)wall_clock64();
     int64_t t_tiles = 0, t_check = 0, t_event = 0, t_digest = 0;
     const uint8_t* stale = nullptr;  // poisoned: the cached digest
@@ -3059,6 +3060,20 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     if (chain_digest_eq(F.table_strong + c * dl, stale, dl)) s_any = 1;
                 __syncthreads();
                 dead = s_any == 0;
+                // dead: the host's closed form (resolver.cpp), here when its literals fit the event buffer -- the
+                // flushes at mark + 9B (one 10B literal each), then the rest (Sender.java:1313-1316)
+                if (dead) {
+                    const int64_t nfl = s <= last ? (n - m) / (10 * B) : 0;  // (the loop has ended: no flushes)
+                    if (nev + nfl + 3 <= F.ev_cap) {
+                        for (int64_t i = 0; i < nfl; ++i) emit_lit(m + 10 * B * i, 10 * B);
+                        m += 10 * B * nfl;
+                        flushes += nfl;
+                        emit_lit(m, n - m);
+                        s = n;
+                        status = CHAIN_DONE;
+                        poisoned = 0;
+                    }
+                }
             }
             break;
         }
@@ -3076,6 +3091,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->n_ev = nev;
         out->tiles = tiles;
         out->digests = digests;
+        out->flushes = flushes;
         out->t_total += (int64_t)wall_clock64() - tk0;
         out->t_tiles += t_tiles;
         out->t_check += t_check;
