@@ -834,16 +834,20 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     // (A/B): the speculation after all of it, full-width launches.
     const bool prep_all = opt(OPT_BATCH_PREP_ALL) != 0;
     const bool bg = spec_after_prep && !prep_all;
-    RSH_BHIP(launch_copy_many(tc, ntc, max_tab, st, bg));  // stream order: after whatever produced them
+    // (chain walks: the host tables and the probe hashes serve the resolvers only -- built after the walks, for
+    // the files they leave)
+    if (!chain_on) RSH_BHIP(launch_copy_many(tc, ntc, max_tab, st, bg));  // stream order: after whatever produced them
     RSH_BHIP(hipEventRecord(c->ev_tab, st));
     // (stream) the probe hashes
-    RSH_BHIP(launch_table_clear(S->slots.as<unsigned long long>(), (uint64_t)tns, st, bg));
     TableEnt* te = S->h_tabents.as<TableEnt>();
-    for (int32_t f = 0; f < NF; ++f) {
-        FileScan& fs = files[(size_t)f];
-        te[f] = TableEnt{S->slots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
+    if (!chain_on) {
+        RSH_BHIP(launch_table_clear(S->slots.as<unsigned long long>(), (uint64_t)tns, st, bg));
+        for (int32_t f = 0; f < NF; ++f) {
+            FileScan& fs = files[(size_t)f];
+            te[f] = TableEnt{S->slots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
+        }
+        RSH_BHIP(launch_table_insert_many(te, (uint32_t)NF, (int32_t)maxC, st, bg));
     }
-    RSH_BHIP(launch_table_insert_many(te, (uint32_t)NF, (int32_t)maxC, st, bg));
     // The chain walk: the speculation runs at once for every file, and one launch walks each file's Sender state
     // machine on the device from its start for as long as the state stays synced and unpoisoned and every digest
     // it needs is speculated (device.hip chain_advance_kernel; two phases: see above).  The resolvers start where
@@ -912,7 +916,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         RSH_BHIP(hipEventRecord(S->ev_scopy, aux));
         S->scopy_pending = true;
         // the sources may come from work on the context stream (and the lead sums go first, see above)
-        RSH_BHIP(hipStreamWaitEvent(aux, spec_after_prep ? c->ev_prep : c->ev_in, 0));
+        RSH_BHIP(hipStreamWaitEvent(aux, (spec_after_prep && !chain_on) ? c->ev_prep : c->ev_in, 0));
         RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>(), ngroups, S->k1_lanes.as<K1Lane>(),
                                          (uint32_t)lanes.size(), lane_align, seed_word(seed), aux, c->abort_word, gen,
                                          partial));
@@ -987,8 +991,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             FileScan& fs = files[(size_t)f];
             co[f] = ChainOut{};
             cf[f] = ChainFile{fs.d_src, fs.n, (uint32_t)fs.B, fs.C, fs.dl, jobs[fs.job].h.remainder,
-                              S->slots.as<unsigned long long>() + fs.off_ns, fs.ns - 1, fs.ns - 1,
-                              S->kslots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.d_strong,
+                              fs.ns - 1, S->kslots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.d_strong,
                               S->src_weak.as<int32_t>() + fs.off_na, S->src_strong.as<uint8_t>() + fs.off_as,
                               S->flags.as<uint8_t>() + fs.off_nf, fs.na, fs.na_a,
                               two_phase ? S->file_abort + f : nullptr, ce + (int64_t)f * kChainEvents, kChainEvents,
@@ -1027,7 +1030,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 RSH_BHIP(hipMemcpyAsync(S->k1_lanes.p, hl, (nla + nlb) * sizeof(K1Lane), hipMemcpyHostToDevice, aux));
             RSH_BHIP(hipEventRecord(S->ev_scopy, aux));
             S->scopy_pending = true;
-            RSH_BHIP(hipStreamWaitEvent(aux, spec_after_prep ? c->ev_prep : c->ev_in, 0));
+            RSH_BHIP(hipStreamWaitEvent(aux, c->ev_in, 0));  // the sources only (no lead check in chain mode)
             RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>(), ng_a, S->k1_lanes.as<K1Lane>(), (uint32_t)nla,
                                              align_a, seed_word(seed), aux, c->abort_word, gen, partial_a));
             RSH_BHIP(hipStreamWaitEvent(aux, c->ev_in, 0));  // the flags need the received tables
@@ -1102,6 +1105,20 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         }
         b.landed.store(true);  // the walks ran after the speculation's K1 and flags
         if (left > 0) {  // the host resolvers use the speculation's host copies: the left files' flags and sums
+            // the left files' received tables (host) and probe hashes (device) first
+            uint32_t nt = 0, ntl = 0;
+            int64_t mt = 0;
+            for (FileScan& fs : files) {
+                if (fs.done || fs.C == 0) continue;
+                tc[nt++] = CopyEnt{reinterpret_cast<const uint8_t*>(fs.d_weak), S->h_weak.as<uint8_t>() + 4 * fs.off_tw,
+                                   (int64_t)fs.C * 4};
+                if (fs.dl > 0) tc[nt++] = CopyEnt{fs.d_strong, S->h_strong.as<uint8_t>() + fs.off_ts, (int64_t)fs.C * fs.dl};
+                mt = std::max<int64_t>(mt, (int64_t)fs.C * 4);
+                te[ntl++] = TableEnt{S->slots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
+            }
+            RSH_BHIP(launch_copy_many(tc, nt, mt, st));
+            RSH_BHIP(launch_table_clear(S->slots.as<unsigned long long>(), (uint64_t)tns, st));
+            RSH_BHIP(launch_table_insert_many(te, ntl, (int32_t)maxC, st));
             CopyEnt* lc = S->h_ccopies.as<CopyEnt>() + NF;
             uint32_t nl = 0;
             int64_t mx = 0;

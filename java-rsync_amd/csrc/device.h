@@ -286,10 +286,9 @@ struct ChainFile {
     int64_t n;
     uint32_t B;
     int32_t C, dl, rem;
-    const unsigned long long* slots;   // the probe hash of the table's distinct keys
-    uint32_t mask;
     uint32_t kmask;
-    const unsigned long long* kslots;  // the chunk index: (key << 32) | (i + 1) per chunk i (launch_chunk_index)
+    const unsigned long long* kslots;  // the chunk index: (key << 32) | (i + 1) per chunk i (launch_chunk_index);
+                                       // key presence and buckets both come from it
     const int32_t* table_weak;
     const uint8_t* table_strong;
     const int32_t* aw;                 // the aligned speculation over windows [0, na): weak, digests, chain flags

@@ -2625,20 +2625,52 @@ constexpr int CHAIN_THREADS = 512;                      // 8 waves (2 per SIMD: 
 constexpr int64_t CHAIN_TILE = (int64_t)CHAIN_THREADS * PROBE_PPT;
 constexpr int CHAIN_SEGS = 64;                           // blocks a tile may start (B >= 512 when wide)
 
+// A key's presence in a chunk index (launch_chunk_index: (key << 32) | (i + 1) per chunk, 0 = empty): every chunk
+// with the key lies on the key's probe path before its first empty slot
+__device__ __forceinline__ bool kslots_has(const unsigned long long* __restrict__ ks, uint32_t mask, uint32_t key) {
+    uint32_t h = slot_hash(key) & mask;
+    for (;;) {
+        const unsigned long long v = ks[h];
+        if (v == 0ull) return false;
+        if ((uint32_t)(v >> 32) == key) return true;
+        h = (h + 1) & mask;
+    }
+}
+
+// The chain walk's key filter: 2^20 bits in LDS (128 KiB), two bits per key from two multiplicative hashes
+constexpr int CHAIN_BLOOM_LOG = 20;
+constexpr int CHAIN_BLOOM_WORDS = 1 << (CHAIN_BLOOM_LOG - 5);
+__device__ __forceinline__ uint32_t chain_bloom_h1(uint32_t k) { return (k * 0x9E3779B1u) >> (32 - CHAIN_BLOOM_LOG); }
+__device__ __forceinline__ uint32_t chain_bloom_h2(uint32_t k) {
+    return ((k ^ (k >> 15)) * 0x85EBCA77u) >> (32 - CHAIN_BLOOM_LOG);
+}
+__device__ __forceinline__ bool chain_bloom_has(const uint32_t* bm, uint32_t k) {
+    const uint32_t a = chain_bloom_h1(k), b = chain_bloom_h2(k);
+    return ((bm[a >> 5] >> (a & 31)) & (bm[b >> 5] >> (b & 31)) & 1u) != 0;
+}
+
 // The first of a lane's 16 keys (bit i of valid: position i is in the search) that the table holds, or -1: the 16
 // first hash slots in one burst of independent loads (as probe_first_kernel: most keys are decided by their first
 // slot, so a lane waits for about one L2 round trip, not 16), then the full lookup only for keys whose first slot
 // holds another key, in order and only before the first certain hit (one out-of-line lookup loop, few registers)
-__device__ __forceinline__ int chain_first_hit16(const ProbeTable& table, const uint32_t (&keys)[PROBE_PPT], uint32_t valid) {
+__device__ __forceinline__ int chain_first_hit16(const unsigned long long* __restrict__ ks, uint32_t kmask,
+                                                 const uint32_t* bloom, const uint32_t (&keys)[PROBE_PPT], uint32_t valid) {
+    // the file's key filter in LDS first: a clear bit proves the key absent, so the table (global memory) sees only
+    // the few keys whose two filter bits are set -- the table's keys and ~0.1 % false positives
+#pragma unroll
+    for (int i = 0; i < PROBE_PPT; ++i)
+        if (!chain_bloom_has(bloom, keys[i])) valid &= ~(1u << i);
+    if (valid == 0) return -1;
     uint32_t hit = 0, need = 0;
     {
         unsigned long long sl[PROBE_PPT];
 #pragma unroll
-        for (int i = 0; i < PROBE_PPT; ++i) sl[i] = table.slots[slot_hash(keys[i]) & table.mask];
+        for (int i = 0; i < PROBE_PPT; ++i) sl[i] = (valid >> i) & 1u ? ks[slot_hash(keys[i]) & kmask] : 0ull;
 #pragma unroll
         for (int i = 0; i < PROBE_PPT; ++i) {
-            if (sl[i] == ((1ull << 32) | keys[i])) hit |= 1u << i;
-            else if (sl[i] != 0ull) need |= 1u << i;
+            if (sl[i] == 0ull) continue;
+            if ((uint32_t)(sl[i] >> 32) == keys[i]) hit |= 1u << i;
+            else need |= 1u << i;
         }
     }
     hit &= valid;
@@ -2649,7 +2681,7 @@ __device__ __forceinline__ int chain_first_hit16(const ProbeTable& table, const 
 #pragma unroll
         for (int j = 0; j < PROBE_PPT; ++j)
             if (j == i) kk = keys[j];
-        if (table_has(table, kk)) return i;
+        if (kslots_has(ks, kmask, kk)) return i;
         need &= need - 1u;
     }
     return hit ? __builtin_ctz(hit) : -1;
@@ -2679,6 +2711,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_wtmp;                 // an unaligned window's sums (its digest: s_dig)
     __shared__ int32_t s_any;                  // some chunk carries the stale digest
     __shared__ int32_t s_seg[CHAIN_SEGS][4];   // wide tiles: the exscan at each block's first lane
+    __shared__ uint32_t s_bloom[CHAIN_BLOOM_WORDS];  // the table's keys (chain_first_hit16)
     __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
     // fields across the loop (the event stores may alias it) -- a PCIe round trip each
@@ -2692,8 +2725,15 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const int64_t S = F.rem > 0 ? F.rem : B;  // Checksum.java:131-137
     const int64_t last = n - S, nB = n - B;
     const int64_t na = phase == 0 ? F.na_a : F.na, nflags = na < C ? na : C;
-    const ProbeTable table{F.slots, F.mask};
     const bool wide = (B % 16) == 0 && B >= 512 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
+    for (int i = t; i < CHAIN_BLOOM_WORDS; i += CHAIN_THREADS) s_bloom[i] = 0u;
+    __syncthreads();
+    for (int64_t c = t; c < C; c += CHAIN_THREADS) {
+        const uint32_t k = (uint32_t)F.table_weak[c], h1 = chain_bloom_h1(k), h2 = chain_bloom_h2(k);
+        atomicOr(&s_bloom[h1 >> 5], 1u << (h1 & 31));
+        atomicOr(&s_bloom[h2 >> 5], 1u << (h2 & 31));
+    }
+    __syncthreads();
     int64_t s = out->s, m = out->m;
     int32_t pref = out->pref;
     int32_t nev = out->n_ev, status = CHAIN_STOP;
@@ -2792,7 +2832,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         int64_t a = s;
         if (k < na) {
             key = (uint32_t)F.aw[k];
-            if (table_has(table, key)) p = s;
+            if (chain_bloom_has(s_bloom, key) && kslots_has(F.kslots, F.kmask, key)) p = s;
             else a = s + 1;
         }
         bool cut = false;  // the search reached windows past the speculation (no anchor T(o))
@@ -2871,7 +2911,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                         const int64_t pp = p0 + i;
                         if (pp >= a && pp <= stop && pp <= lim_spec) valid |= 1u << i;
                     }
-                    const int h = chain_first_hit16(table, keys, valid);
+                    const int h = chain_first_hit16(F.kslots, F.kmask, s_bloom, keys, valid);
                     if (h >= 0) atomicMin(&s_hit, (int32_t)(p0 + h - q0));
                 }
                 __syncthreads();
@@ -2947,7 +2987,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     const int64_t pp = p0 + i;
                     if (pp >= a && pp <= stop && pp < qend) valid |= 1u << i;
                 }
-                const int h = chain_first_hit16(table, keys, valid);
+                const int h = chain_first_hit16(F.kslots, F.kmask, s_bloom, keys, valid);
                 if (h >= 0) atomicMin(&s_hit, (int32_t)(p0 + h - q0));
             }
             __syncthreads();
@@ -3065,7 +3105,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 if (dead) {
                     const int64_t nfl = s <= last ? (n - m) / (10 * B) : 0;  // (the loop has ended: no flushes)
                     if (nev + nfl + 3 <= F.ev_cap) {
-                        for (int64_t i = 0; i < nfl; ++i) emit_lit(m + 10 * B * i, 10 * B);
+                        flush_pend();  // the literals themselves: one per thread (writes to pinned host memory)
+                        for (int64_t i = t; i < nfl; i += CHAIN_THREADS)
+                            F.ev[nev + i] = rsh_event{m + 10 * B * i, 10 * B, RSH_EV_LITERAL, 0, 0, 0};
+                        nev += (int32_t)nfl;
+                        lit += 10 * B * nfl;
                         m += 10 * B * nfl;
                         flushes += nfl;
                         emit_lit(m, n - m);
