@@ -57,7 +57,7 @@ inline const OptInfo* opt_info() {
         {"scan_preprobe", 1},      {"scan_samples", 256},     {"scan_sample", 1},      {"scan_spec_order", 1},
         {"scan_early", 1},         {"scan_wait", 1},          {"scan_defer_steps", 4}, {"scan_defer_us", 500},
         {"batch_spec", -1},        {"batch_spin_us", 200},    {"batch_readahead", 0},  {"batch_prep_all", 0},
-        {"batch_chain", 1},        {"batch_chain_prefix", -1}, {"batch_chain_overlap", 1},
+        {"batch_chain", 1},        {"batch_chain_prefix", -1}, {"batch_chain_overlap", 0},
         {"host_cores", 0},         {"file_tile", 4LL << 30}, {"file_tile_above", 32LL << 30},
     };
     return t;
