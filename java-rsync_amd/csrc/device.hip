@@ -2622,7 +2622,8 @@ hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const Part
 // branch on is read from global memory or LDS by all of them); lane 0 writes the events.
 // ------------------------------------------------------------------------------------------------
 constexpr int CHAIN_THREADS = 512;                      // 8 waves (2 per SIMD: 256 VGPRs each)
-constexpr int64_t CHAIN_TILE = (int64_t)CHAIN_THREADS * PROBE_PPT;
+constexpr int CHAIN_PPT = 32;                            // wide tiles: positions per lane (two halves of 16)
+constexpr int64_t CHAIN_TILE = (int64_t)CHAIN_THREADS * CHAIN_PPT;
 constexpr int CHAIN_SEGS = 64;                           // blocks a tile may start (B >= 512 when wide)
 
 // A key's presence in a chunk index (launch_chunk_index: (key << 32) | (i + 1) per chunk, 0 = empty): every chunk
@@ -2637,16 +2638,21 @@ __device__ __forceinline__ bool kslots_has(const unsigned long long* __restrict_
     }
 }
 
-// The chain walk's key filter: 2^20 bits in LDS (128 KiB), two bits per key from two multiplicative hashes
-constexpr int CHAIN_BLOOM_LOG = 20;
-constexpr int CHAIN_BLOOM_WORDS = 1 << (CHAIN_BLOOM_LOG - 5);
-__device__ __forceinline__ uint32_t chain_bloom_h1(uint32_t k) { return (k * 0x9E3779B1u) >> (32 - CHAIN_BLOOM_LOG); }
-__device__ __forceinline__ uint32_t chain_bloom_h2(uint32_t k) {
-    return ((k ^ (k >> 15)) * 0x85EBCA77u) >> (32 - CHAIN_BLOOM_LOG);
+// The chain walk's key filter: a blocked Bloom filter in LDS, 2^14 words of 64 bits (128 KiB); a key sets 6 bits of
+// one word (one ds_read_b64 per lookup).  At 16384 keys (config 4's tables) about 2 in 10^5 absent keys pass.
+constexpr int CHAIN_BLOOM_LOG = 14;
+constexpr int CHAIN_BLOOM_WORDS = 1 << CHAIN_BLOOM_LOG;
+__device__ __forceinline__ uint32_t chain_bloom_word(uint32_t k) { return (k * 0x9E3779B1u) >> (32 - CHAIN_BLOOM_LOG); }
+__device__ __forceinline__ unsigned long long chain_bloom_mask(uint32_t k) {
+    const unsigned long long h = (unsigned long long)(k ^ (k >> 16)) * 0x9E3779B97F4A7C15ull;
+    unsigned long long m = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) m |= 1ull << ((h >> (28 + 6 * i)) & 63);
+    return m;
 }
-__device__ __forceinline__ bool chain_bloom_has(const uint32_t* bm, uint32_t k) {
-    const uint32_t a = chain_bloom_h1(k), b = chain_bloom_h2(k);
-    return ((bm[a >> 5] >> (a & 31)) & (bm[b >> 5] >> (b & 31)) & 1u) != 0;
+__device__ __forceinline__ bool chain_bloom_has(const unsigned long long* bm, uint32_t k) {
+    const unsigned long long m = chain_bloom_mask(k);
+    return (bm[chain_bloom_word(k)] & m) == m;
 }
 
 // The first of a lane's 16 keys (bit i of valid: position i is in the search) that the table holds, or -1: the 16
@@ -2654,7 +2660,8 @@ __device__ __forceinline__ bool chain_bloom_has(const uint32_t* bm, uint32_t k) 
 // slot, so a lane waits for about one L2 round trip, not 16), then the full lookup only for keys whose first slot
 // holds another key, in order and only before the first certain hit (one out-of-line lookup loop, few registers)
 __device__ __forceinline__ int chain_first_hit16(const unsigned long long* __restrict__ ks, uint32_t kmask,
-                                                 const uint32_t* bloom, const uint32_t (&keys)[PROBE_PPT], uint32_t valid) {
+                                                 const unsigned long long* bloom, const uint32_t (&keys)[PROBE_PPT],
+                                                 uint32_t valid) {
     // the file's key filter in LDS first: a clear bit proves the key absent, so the table (global memory) sees only
     // the few keys whose two filter bits are set -- the table's keys and ~0.1 % false positives
 #pragma unroll
@@ -2711,7 +2718,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_wtmp;                 // an unaligned window's sums (its digest: s_dig)
     __shared__ int32_t s_any;                  // some chunk carries the stale digest
     __shared__ int32_t s_seg[CHAIN_SEGS][4];   // wide tiles: the exscan at each block's first lane
-    __shared__ uint32_t s_bloom[CHAIN_BLOOM_WORDS];  // the table's keys (chain_first_hit16)
+    __shared__ unsigned long long s_bloom[CHAIN_BLOOM_WORDS];  // the table's keys (chain_first_hit16)
     __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
     // fields across the loop (the event stores may alias it) -- a PCIe round trip each
@@ -2725,13 +2732,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const int64_t S = F.rem > 0 ? F.rem : B;  // Checksum.java:131-137
     const int64_t last = n - S, nB = n - B;
     const int64_t na = phase == 0 ? F.na_a : F.na, nflags = na < C ? na : C;
-    const bool wide = (B % 16) == 0 && B >= 512 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
-    for (int i = t; i < CHAIN_BLOOM_WORDS; i += CHAIN_THREADS) s_bloom[i] = 0u;
+    const bool wide = (B % CHAIN_PPT) == 0 && B >= 512 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
+    for (int i = t; i < CHAIN_BLOOM_WORDS; i += CHAIN_THREADS) s_bloom[i] = 0ull;
     __syncthreads();
     for (int64_t c = t; c < C; c += CHAIN_THREADS) {
-        const uint32_t k = (uint32_t)F.table_weak[c], h1 = chain_bloom_h1(k), h2 = chain_bloom_h2(k);
-        atomicOr(&s_bloom[h1 >> 5], 1u << (h1 & 31));
-        atomicOr(&s_bloom[h2 >> 5], 1u << (h2 & 31));
+        const uint32_t k = (uint32_t)F.table_weak[c];
+        atomicOr(&s_bloom[chain_bloom_word(k)], chain_bloom_mask(k));
     }
     __syncthreads();
     int64_t s = out->s, m = out->m;
@@ -2843,7 +2849,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             // the head of the block the tile starts in (range_sums from o to the tile)
             const int64_t lim_spec = na * B - 1;  // windows with an anchor: blocks < na
             const int64_t qlast = stop < lim_spec ? stop : lim_spec;
-            for (int64_t q0 = a & ~(int64_t)15; p < 0 && q0 <= qlast;) {
+            for (int64_t q0 = a & ~(int64_t)(CHAIN_PPT - 1); p < 0 && q0 <= qlast;) {
                 ++tiles;
                 const int64_t tt0 = (int64_t)wall_clock64();
                 const int64_t kb0 = q0 / B, o0 = kb0 * B;
@@ -2853,22 +2859,27 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     range_sums(F.data, n, o0 + B, q0 + B, o0, head[2], head[3]);
                     block_reduce<4>(head, sh);
                 }
-                const int64_t p0 = q0 + (int64_t)t * PROBE_PPT;
+                const int64_t p0 = q0 + (int64_t)t * CHAIN_PPT;
                 const int64_t kb = p0 / B, o = kb * B;
-                uint32_t xa[4], xb[4];
-                load16(F.data, n, p0, xa);
-                load16(F.data, n, p0 + B, xb);
-                const bool live = p0 <= stop && p0 <= lim_spec && p0 + PROBE_PPT > a;
+                uint32_t xa[2][4], xb[2][4];
+                load16(F.data, n, p0, xa[0]);
+                load16(F.data, n, p0 + 16, xa[1]);
+                load16(F.data, n, p0 + B, xb[0]);
+                load16(F.data, n, p0 + B + 16, xb[1]);
+                const bool live = p0 <= stop && p0 <= lim_spec && p0 + CHAIN_PPT > a;
                 const int32_t To = live ? F.aw[kb] : 0;
                 int32_t pre[4] = {0, 0, 0, 0};
 #pragma unroll
-                for (int i = 0; i < PROBE_PPT; ++i) {
-                    const int32_t va = sbyte_of(xa, i), vb = sbyte_of(xb, i);
-                    pre[0] += va;
-                    pre[1] += (int32_t)((uint32_t)(p0 + i - q0) * (uint32_t)va);
-                    pre[2] += vb;
-                    pre[3] += (int32_t)((uint32_t)(p0 + B + i - q0) * (uint32_t)vb);
-                }
+                for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int32_t va = sbyte_of(xa[hh], i), vb = sbyte_of(xb[hh], i);
+                        const uint32_t r = (uint32_t)(p0 + 16 * hh + i - q0);
+                        pre[0] += va;
+                        pre[1] += (int32_t)(r * (uint32_t)va);
+                        pre[2] += vb;
+                        pre[3] += (int32_t)((r + (uint32_t)B) * (uint32_t)vb);
+                    }
                 block_exscan<4>(pre, sh);  // sums over [q0, p0) and [q0 + B, p0 + B), weights j - q0
                 if (p0 == o) {              // a block's first lane: its rebasing point
 #pragma unroll
@@ -2877,7 +2888,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 if (t == 0) s_hit = 0x7FFFFFFF;
                 __syncthreads();
                 const int64_t tc0 = (int64_t)wall_clock64();
-                uint32_t keys[PROBE_PPT];
+                int32_t my_hit = 0x7FFFFFFF;
+                uint32_t my_key = 0;
                 if (live) {
                     uint32_t pa, pa2, pb, pb2;  // sums over [o, p0) and [o + B, p0 + B), weights j - o
                     if (o < q0) {               // the tile's first block: its head + the tile's part
@@ -2900,27 +2912,36 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     const uint32_t s1 = P1e - pa;
                     const uint32_t s2 = (uint32_t)(p0 + B - o) * s1 - (P2e - pa2);
                     int32_t R = (int32_t)((s1 & 0xFFFFu) | (s2 << 16));
+                    // the lane's 32 positions as two halves of 16 (the first hit of the first half wins)
 #pragma unroll
-                    for (int i = 0; i < PROBE_PPT; ++i) {
-                        keys[i] = (uint32_t)R;
-                        R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(xa, i)), sbyte_of(xb, i));
-                    }
-                    uint32_t valid = 0;
+                    for (int hh = 0; hh < 2; ++hh) {
+                        uint32_t keys[16];
 #pragma unroll
-                    for (int i = 0; i < PROBE_PPT; ++i) {
-                        const int64_t pp = p0 + i;
-                        if (pp >= a && pp <= stop && pp <= lim_spec) valid |= 1u << i;
+                        for (int i = 0; i < 16; ++i) {
+                            keys[i] = (uint32_t)R;
+                            R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(xa[hh], i)), sbyte_of(xb[hh], i));
+                        }
+                        uint32_t valid = 0;
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const int64_t pp = p0 + 16 * hh + i;
+                            if (pp >= a && pp <= stop && pp <= lim_spec) valid |= 1u << i;
+                        }
+                        if (my_hit == 0x7FFFFFFF) {
+                            const int h = chain_first_hit16(F.kslots, F.kmask, s_bloom, keys, valid);
+                            if (h >= 0) {
+                                my_hit = (int32_t)(p0 + 16 * hh + h - q0);
+#pragma unroll
+                                for (int i = 0; i < 16; ++i)  // (a static index: keys stays in registers)
+                                    if (i == h) my_key = keys[i];
+                            }
+                        }
                     }
-                    const int h = chain_first_hit16(F.kslots, F.kmask, s_bloom, keys, valid);
-                    if (h >= 0) atomicMin(&s_hit, (int32_t)(p0 + h - q0));
+                    if (my_hit != 0x7FFFFFFF) atomicMin(&s_hit, my_hit);
                 }
                 __syncthreads();
                 t_check += (int64_t)wall_clock64() - tc0;
-                if (s_hit != 0x7FFFFFFF && (s_hit >> 4) == t) {
-#pragma unroll
-                    for (int i = 0; i < PROBE_PPT; ++i)  // (a static index: keys stays in registers)
-                        if (i == (s_hit & 15)) s_key = keys[i];
-                }
+                if (my_hit != 0x7FFFFFFF && my_hit == s_hit) s_key = my_key;
                 __syncthreads();
                 if (s_hit != 0x7FFFFFFF) {
                     p = q0 + s_hit;
