@@ -2638,21 +2638,46 @@ __device__ __forceinline__ bool kslots_has(const unsigned long long* __restrict_
     }
 }
 
-// The chain walk's key filter: a blocked Bloom filter in LDS, 2^14 words of 64 bits (128 KiB); a key sets 6 bits of
-// one word (one ds_read_b64 per lookup).  At 16384 keys (config 4's tables) about 2 in 10^5 absent keys pass.
-constexpr int CHAIN_BLOOM_LOG = 14;
-constexpr int CHAIN_BLOOM_WORDS = 1 << CHAIN_BLOOM_LOG;
-__device__ __forceinline__ uint32_t chain_bloom_word(uint32_t k) { return (k * 0x9E3779B1u) >> (32 - CHAIN_BLOOM_LOG); }
-__device__ __forceinline__ unsigned long long chain_bloom_mask(uint32_t k) {
-    const unsigned long long h = (unsigned long long)(k ^ (k >> 16)) * 0x9E3779B97F4A7C15ull;
-    unsigned long long m = 0;
+// The chain walk's key set: the table's distinct weak sums in LDS as a bucketed cuckoo set -- 2 x 4096 buckets of 4
+// keys (128 KiB), a key in bucket h1(k) of the first half or h2(k) of the second, 0 = empty (key 0 has its own
+// flag).  A lookup is two 16-byte LDS reads and eight compares, exact.  Config 4's 16384 keys fill half of it; a
+// key still displaced after the insertion's bound (tables near or above 32768 distinct keys) marks the set
+// incomplete, and the walk then confirms every key in the chunk index instead.
+constexpr int CHAIN_CK_BUCKETS = 4096;
+__device__ __forceinline__ uint32_t chain_ck_h1(uint32_t k) { return (k * 0x9E3779B1u) >> 20; }
+__device__ __forceinline__ uint32_t chain_ck_h2(uint32_t k) { return CHAIN_CK_BUCKETS + (((k ^ (k >> 15)) * 0x85EBCA77u) >> 20); }
+struct ChainKeySet {
+    uint4* b;      // 2 * CHAIN_CK_BUCKETS buckets
+    int32_t* has0;  // key 0 present
+    int32_t* full;  // some key found no slot: lookups are not exact
+};
+__device__ __forceinline__ void chain_ck_insert(const ChainKeySet& ks, uint32_t k) {
+    if (k == 0u) {
+        *ks.has0 = 1;
+        return;
+    }
+    // cuckoo insertion: a free slot of the key's bucket in table w, else displace one of that bucket's keys and
+    // carry it to its bucket in the other table (every key lives in its own h1 or h2 bucket)
+    uint32_t cur = k;
+    int w = 0;
+    for (int it = 0; it < 96; ++it) {
+        uint32_t* slot = reinterpret_cast<uint32_t*>(&ks.b[w == 0 ? chain_ck_h1(cur) : chain_ck_h2(cur)]);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) m |= 1ull << ((h >> (28 + 6 * i)) & 63);
-    return m;
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t old = atomicCAS(slot + j, 0u, cur);
+            if (old == 0u || old == cur) return;
+        }
+        const uint32_t old = atomicExch(slot + (it & 3), cur);
+        if (old == 0u || old == cur) return;
+        cur = old;
+        w ^= 1;
+    }
+    *ks.full = 1;  // a key is left over: the set is not exact
 }
-__device__ __forceinline__ bool chain_bloom_has(const unsigned long long* bm, uint32_t k) {
-    const unsigned long long m = chain_bloom_mask(k);
-    return (bm[chain_bloom_word(k)] & m) == m;
+__device__ __forceinline__ bool chain_ck_has(const ChainKeySet& ks, uint32_t k) {
+    if (k == 0u) return *ks.has0 != 0;
+    const uint4 a = ks.b[chain_ck_h1(k)], c = ks.b[chain_ck_h2(k)];
+    return a.x == k || a.y == k || a.z == k || a.w == k || c.x == k || c.y == k || c.z == k || c.w == k;
 }
 
 // The first of a lane's 16 keys (bit i of valid: position i is in the search) that the table holds, or -1: the 16
@@ -2660,14 +2685,15 @@ __device__ __forceinline__ bool chain_bloom_has(const unsigned long long* bm, ui
 // slot, so a lane waits for about one L2 round trip, not 16), then the full lookup only for keys whose first slot
 // holds another key, in order and only before the first certain hit (one out-of-line lookup loop, few registers)
 __device__ __forceinline__ int chain_first_hit16(const unsigned long long* __restrict__ ks, uint32_t kmask,
-                                                 const unsigned long long* bloom, const uint32_t (&keys)[PROBE_PPT],
+                                                 const ChainKeySet& set, const uint32_t (&keys)[PROBE_PPT],
                                                  uint32_t valid) {
-    // the file's key filter in LDS first: a clear bit proves the key absent, so the table (global memory) sees only
-    // the few keys whose two filter bits are set -- the table's keys and ~0.1 % false positives
+    // the key set in LDS: exact (the usual case), so the table in global memory is not touched at all
+    if (*set.full == 0) {
 #pragma unroll
-    for (int i = 0; i < PROBE_PPT; ++i)
-        if (!chain_bloom_has(bloom, keys[i])) valid &= ~(1u << i);
-    if (valid == 0) return -1;
+        for (int i = 0; i < PROBE_PPT; ++i)
+            if (!chain_ck_has(set, keys[i])) valid &= ~(1u << i);
+        return valid ? __builtin_ctz(valid) : -1;
+    }
     uint32_t hit = 0, need = 0;
     {
         unsigned long long sl[PROBE_PPT];
@@ -2718,7 +2744,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_wtmp;                 // an unaligned window's sums (its digest: s_dig)
     __shared__ int32_t s_any;                  // some chunk carries the stale digest
     __shared__ int32_t s_seg[CHAIN_SEGS][4];   // wide tiles: the exscan at each block's first lane
-    __shared__ unsigned long long s_bloom[CHAIN_BLOOM_WORDS];  // the table's keys (chain_first_hit16)
+    __shared__ uint4 s_ck[2 * CHAIN_CK_BUCKETS];  // the table's keys (ChainKeySet)
+    __shared__ int32_t s_ck_has0, s_ck_full;
     __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
     // fields across the loop (the event stores may alias it) -- a PCIe round trip each
@@ -2733,12 +2760,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const int64_t last = n - S, nB = n - B;
     const int64_t na = phase == 0 ? F.na_a : F.na, nflags = na < C ? na : C;
     const bool wide = (B % CHAIN_PPT) == 0 && B >= 512 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
-    for (int i = t; i < CHAIN_BLOOM_WORDS; i += CHAIN_THREADS) s_bloom[i] = 0ull;
+    const ChainKeySet kset{s_ck, &s_ck_has0, &s_ck_full};
+    for (int i = t; i < 2 * CHAIN_CK_BUCKETS; i += CHAIN_THREADS) s_ck[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (t == 0) s_ck_has0 = s_ck_full = 0;
     __syncthreads();
-    for (int64_t c = t; c < C; c += CHAIN_THREADS) {
-        const uint32_t k = (uint32_t)F.table_weak[c];
-        atomicOr(&s_bloom[chain_bloom_word(k)], chain_bloom_mask(k));
-    }
+    for (int64_t c = t; c < C; c += CHAIN_THREADS) chain_ck_insert(kset, (uint32_t)F.table_weak[c]);
     __syncthreads();
     int64_t s = out->s, m = out->m;
     int32_t pref = out->pref;
@@ -2838,7 +2864,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         int64_t a = s;
         if (k < na) {
             key = (uint32_t)F.aw[k];
-            if (chain_bloom_has(s_bloom, key) && kslots_has(F.kslots, F.kmask, key)) p = s;
+            if (s_ck_full ? kslots_has(F.kslots, F.kmask, key) : chain_ck_has(kset, key)) p = s;
             else a = s + 1;
         }
         bool cut = false;  // the search reached windows past the speculation (no anchor T(o))
@@ -2911,24 +2937,29 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     const uint32_t P2e = (uint32_t)B * s1o - s2o + pb2;
                     const uint32_t s1 = P1e - pa;
                     const uint32_t s2 = (uint32_t)(p0 + B - o) * s1 - (P2e - pa2);
-                    int32_t R = (int32_t)((s1 & 0xFFFFu) | (s2 << 16));
-                    // the lane's 32 positions as two halves of 16 (the first hit of the first half wins)
+                    // the lane's 32 positions as two halves of 16 (the first hit of the first half wins).  The two
+                    // 16-bit halves of the rolling value are kept apart (u1, u2: each exact mod 2^16, the Java
+                    // subtract-then-add of Rolling.java:25-60 in two adds each), packed into the key per position
+                    uint32_t u1 = s1, u2 = s2;
+                    const int64_t lim_p = stop < lim_spec ? stop : lim_spec;
 #pragma unroll
                     for (int hh = 0; hh < 2; ++hh) {
                         uint32_t keys[16];
 #pragma unroll
                         for (int i = 0; i < 16; ++i) {
-                            keys[i] = (uint32_t)R;
-                            R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(xa[hh], i)), sbyte_of(xb[hh], i));
+                            keys[i] = (u1 & 0xFFFFu) | (u2 << 16);
+                            const int32_t xo = sbyte_of(xa[hh], i), xi = sbyte_of(xb[hh], i);
+                            u1 += (uint32_t)(xi - xo);
+                            u2 += u1 - (uint32_t)B * (uint32_t)xo;
                         }
+                        // positions base + i with a <= position <= lim_p, as a bit range
+                        const int64_t base = p0 + 16 * hh;
+                        const int64_t lo = a > base ? a - base : 0, hi = lim_p - base;
                         uint32_t valid = 0;
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            const int64_t pp = p0 + 16 * hh + i;
-                            if (pp >= a && pp <= stop && pp <= lim_spec) valid |= 1u << i;
-                        }
+                        if (lo <= 15 && hi >= 0 && hi >= lo)
+                            valid = (0xFFFFu >> (15 - (hi < 15 ? hi : 15))) & (0xFFFFu << lo);
                         if (my_hit == 0x7FFFFFFF) {
-                            const int h = chain_first_hit16(F.kslots, F.kmask, s_bloom, keys, valid);
+                            const int h = chain_first_hit16(F.kslots, F.kmask, kset, keys, valid);
                             if (h >= 0) {
                                 my_hit = (int32_t)(p0 + 16 * hh + h - q0);
 #pragma unroll
@@ -3008,7 +3039,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     const int64_t pp = p0 + i;
                     if (pp >= a && pp <= stop && pp < qend) valid |= 1u << i;
                 }
-                const int h = chain_first_hit16(F.kslots, F.kmask, s_bloom, keys, valid);
+                const int h = chain_first_hit16(F.kslots, F.kmask, kset, keys, valid);
                 if (h >= 0) atomicMin(&s_hit, (int32_t)(p0 + h - q0));
             }
             __syncthreads();
