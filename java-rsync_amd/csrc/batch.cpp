@@ -32,7 +32,8 @@ constexpr int32_t kMaxWorkers = 32;   // host threads running the resolvers
 constexpr size_t kFiberStack = 512 * 1024;
 constexpr int32_t kEagerSortChunks = 1 << 16;  // tables up to this size are sorted before the first round
 constexpr int64_t kPad = 16;
-constexpr int64_t kWaveSlots = 2 * 4 * 256;  // the chip's K1 wave slots (2 waves per SIMD, 4 SIMDs, 256 CUs)
+constexpr int64_t kWaveSlots = 2 * 4 * 256;
+constexpr size_t kProbeUpload = 2048;  // probes with more tiles read their descriptors from device memory  // the chip's K1 wave slots (2 waves per SIMD, 4 SIMDs, 256 CUs)
 constexpr int32_t kChainEvents = 4096;  // events one file's chain walk may emit before it hands over
 
 int64_t pad16(int64_t v) { return (v + kPad - 1) / kPad * kPad; }
@@ -43,6 +44,7 @@ struct BatchState {
     DevBuf g_groups, g_lanes, g_plans, k1_plans;  // K1 groups are expanded on the device from per-file plans
     // Sender batch: device
     DevBuf slots, dslots, src_weak, src_strong, flags, haw, partials, bucket, first, k1_groups, k1_lanes;
+    DevBuf d_probe;  // a large probe's descriptors (files, intervals, tiles, partial tiles) in device memory
     // Sender batch: pinned host (read or written by the kernels directly)
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl, h_files, h_hit, h_win0, h_bucket, h_first, h_iv, h_tiles,
         h_ptiles, h_req, h_gw, h_gb, h_ow, h_ob, h_win, h_copies, h_tabents, h_flagents, h_flagents_a, h_dkeys, h_ccopies,
@@ -97,7 +99,7 @@ struct BatchState {
         h_glanes.release();
         h_sgroups.release();
         h_slanes.release();
-        for (DevBuf* b : {&g_groups, &g_lanes, &g_plans, &k1_plans, &slots, &dslots, &src_weak, &src_strong, &flags, &haw, &partials, &bucket,
+        for (DevBuf* b : {&d_probe, &g_groups, &g_lanes, &g_plans, &k1_plans, &slots, &dslots, &src_weak, &src_strong, &flags, &haw, &partials, &bucket,
                           &first, &k1_groups, &k1_lanes})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_files, &h_hit, &h_win0, &h_bucket, &h_first,
@@ -588,12 +590,35 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
     chk(launch_gather_bytes(F, hgb, (uint32_t)gb.size(), hob, st));
     chk(launch_copy_many(hcp, (uint32_t)copies.size(), max_win, st));
     if (!preq.empty()) {
+        // The kernels read their descriptors where they are: pinned host memory, one PCIe round trip per workgroup,
+        // which is nothing for a round's few tiles but the whole cost of a probe over a file's rest (a batched flush
+        // chain of ~1600 intervals: ~30K tiles, 0.9 ms).  Above kProbeUpload tiles they go to device memory first.
+        const ScanFile* dF = F;
+        const ProbeIv* div = hiv;
+        const ProbeTile* dt = ht;
+        const PartialTile* dpt = hpt;
+        if (tiles.size() > kProbeUpload) {
+            const size_t bf = pad16(files.size() * sizeof(ScanFile)), bi = pad16(ivs.size() * sizeof(ProbeIv)),
+                         bt = pad16(tiles.size() * sizeof(ProbeTile)), bp = pad16(ptiles.size() * sizeof(PartialTile));
+            chk(S->d_probe.ensure(bf + bi + bt + bp + 16));
+            if (e != hipSuccess) return e;
+            uint8_t* d = S->d_probe.as<uint8_t>();
+            chk(hipMemcpyAsync(d, F, files.size() * sizeof(ScanFile), hipMemcpyHostToDevice, st));
+            chk(hipMemcpyAsync(d + bf, hiv, ivs.size() * sizeof(ProbeIv), hipMemcpyHostToDevice, st));
+            chk(hipMemcpyAsync(d + bf + bi, ht, tiles.size() * sizeof(ProbeTile), hipMemcpyHostToDevice, st));
+            if (!ptiles.empty())
+                chk(hipMemcpyAsync(d + bf + bi + bt, hpt, ptiles.size() * sizeof(PartialTile), hipMemcpyHostToDevice, st));
+            dF = reinterpret_cast<const ScanFile*>(d);
+            div = reinterpret_cast<const ProbeIv*>(d + bf);
+            dt = reinterpret_cast<const ProbeTile*>(d + bf + bi);
+            dpt = reinterpret_cast<const PartialTile*>(d + bf + bi + bt);
+        }
         ProbeArgs A;
-        A.files = F;
-        A.ivs = hiv;
-        A.tiles = ht;
+        A.files = dF;
+        A.ivs = div;
+        A.tiles = dt;
         A.partials = S->partials.as<int4>();
-        chk(launch_probe_first(A, (uint32_t)tiles.size(), hpt, (uint32_t)ptiles.size(), st));
+        chk(launch_probe_first(A, (uint32_t)tiles.size(), dpt, (uint32_t)ptiles.size(), st));
         chk(launch_hit_window(F, hiv, hreq, (int32_t)preq.size(), max_C, st));
         chk(hipMemcpyAsync(S->h_first.p, S->first.p, files.size() * sizeof(ProbeOut), hipMemcpyDeviceToHost, st));
         chk(hipMemcpyAsync(S->h_bucket.p, S->bucket.p, files.size() * HIT_BUCKET_INTS * sizeof(int32_t),
