@@ -1,0 +1,72 @@
+# gpu_steps.sh -- the GPU-box measurement steps, one script (developer tool; the steps DESIGN.md cites).
+#
+# usage (from the repo root, on the GPU box):  TAG=name bash java-rsync_amd/tools/gpu_steps.sh STEP [STEP ...]
+# Outputs go to gpurun_out/$TAG/.  Every step runs under its own time limit; the first step that fails (a test
+# failure, a fault, an abort or a time limit) ends the call, so nothing else touches the GPU after it.
+#
+#   tests        the whole GPU suite (pytest -m gpu)
+#   tests-batch  the batched-scan suite and the config-4 oracle checks
+#   smoke        __graft_entry__.smoke()
+#   bench        the default bench line (config 5, with companions)
+#   files        the config-4 line, both basis forms (FILES_STEPS steps)
+#   files-trace  one traced config-4 step (VARIANT, default half): the chain walk's breakdown (scan_trace = 2)
+#   prof         rocprofv3 kernel trace + stats of the default line (the summary committed under profiles/)
+#   timeline     rocprofv3 kernel + copy timeline of the config-4 line (VARIANT)
+#   pmc-k1       one PMC pass over kbench: the production K1 against the same kernel without global loads
+#   kbench-k1    kbench: the K1 at B = 128 KiB and 8 KiB, the batched forms (1002, 1005, 1006)
+#   e2e          java-rsync_amd/tools/e2e.py at config 5 (16 GiB from host memory)
+#   ab           AB_OPTS ("name=value ...") against the default, alternating, REPS times (AB_ARGS: bench args)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+O=$R/gpurun_out/${TAG:-steps}
+mkdir -p "$O"
+cd "$R"
+K=$R/java-rsync_amd/lib/kbench
+VARIANT=${VARIANT:-half}
+
+run() {  # run LIMIT cmd... : the step's own time limit; any failure ends the call
+    local lim=$1
+    shift
+    timeout -k 10 "$lim" "$@" || { echo "step failed ($?): $*"; exit 1; }
+}
+
+for step in "$@"; do
+    echo "[gpu_steps] $step"
+    case $step in
+        tests) run 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > "$O/gpu_tests.log" 2>&1 ;;
+        tests-batch) run 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_batch.py \
+            tests/test_gpu_fullsize.py -k "batch or config4" > "$O/batch_tests.log" 2>&1 ;;
+        smoke) run 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.log" 2>&1 ;;
+        bench) run 300 python bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
+        files)
+            for v in half identical; do
+                run 300 python bench.py --workload files --variant $v --steps "${FILES_STEPS:-8}" --warmup 2 \
+                    --no-cpu-baseline --no-companions > "$O/files_$v.json" 2> "$O/files_$v.err"
+            done ;;
+        files-trace) run 300 python bench.py --workload files --variant "$VARIANT" --steps 1 --warmup 1 --no-cpu-baseline \
+            --no-companions --opt scan_trace=2 > "$O/files_${VARIANT}_trace.json" 2> "$O/files_${VARIANT}_trace.err" ;;
+        prof) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run \
+            --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline \
+            > "$O/prof_bench.json" 2> "$O/prof_bench.err") || exit 1 ;;
+        timeline) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --kernel-trace --memory-copy-trace --stats \
+            -d "$O/timeline" -o run --output-format csv -- python3 "$R/bench.py" --workload files --variant "$VARIANT" \
+            --steps 3 --warmup 1 --no-cpu-baseline --no-companions > "$O/timeline.json" 2> "$O/timeline.err") || exit 1 ;;
+        pmc-k1)
+            C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
+            run 120 "$K" 16384 131072 4 5 1000 58 > "$O/pmc_kbench.log" 2>&1
+            (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d "$O/pmc" -o run \
+                --output-format csv -- "$K" 16384 131072 4 3 1000 58 > "$O/pmc.log" 2>&1) || exit 1 ;;
+        kbench-k1)
+            run 120 "$K" 16384 131072 4 8 1000 > "$O/kbench_128k.log" 2>&1
+            run 120 "$K" 16384 8192 3 8 1000 1002 1005 1006 > "$O/kbench_8k.log" 2>&1 ;;
+        e2e) run 400 python java-rsync_amd/tools/e2e.py --gib 16 > "$O/e2e_16GiB.json" 2> "$O/e2e.err" ;;
+        ab)
+            OPTS=""
+            for o in $AB_OPTS; do OPTS="$OPTS --opt $o"; done
+            for r in $(seq 1 "${REPS:-3}"); do
+                run 300 python bench.py $AB_ARGS --steps 20 --warmup 5 --no-cpu-baseline --no-companions > "$O/a_$r.json" 2> "$O/a_$r.err"
+                run 300 python bench.py $AB_ARGS --steps 20 --warmup 5 --no-cpu-baseline --no-companions $OPTS > "$O/b_$r.json" 2> "$O/b_$r.err"
+            done ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
