@@ -34,7 +34,10 @@ constexpr int32_t kEagerSortChunks = 1 << 16;  // tables up to this size are sor
 constexpr int64_t kPad = 16;
 constexpr int64_t kWaveSlots = 2 * 4 * 256;
 constexpr size_t kProbeUpload = 2048;  // probes with more tiles read their descriptors from device memory  // the chip's K1 wave slots (2 waves per SIMD, 4 SIMDs, 256 CUs)
-constexpr int32_t kChainEvents = 4096;  // events one file's chain walk may emit before it hands over
+// events one file's chain walk may emit before it hands over: 4096 (config 4's closed forms fit), fewer for
+// batches of more than 512 files so that the pinned event buffer stays within 64 MiB
+constexpr int32_t kChainEventsMax = 4096;
+constexpr int64_t kChainEventBytes = 64ll << 20;
 
 int64_t pad16(int64_t v) { return (v + kPad - 1) / kPad * kPad; }
 }  // namespace
@@ -728,6 +731,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     // files whose walk reached the prefix's end (the others' groups stop at once: the walk wrote their abort words)
     // and a second walk.  A file that leaves the synced state early (an edit) costs its prefix, not its whole length.
     const bool chain_on = opt(OPT_BATCH_CHAIN) != 0 && opt(OPT_BATCH_SPEC) == -1;
+    const int32_t kChainEvents = (int32_t)std::clamp<int64_t>(
+        kChainEventBytes / ((int64_t)std::max<int32_t>(NF, 1) * (int64_t)sizeof(rsh_event)), 256, kChainEventsMax);
     bool two_phase = false;
     std::vector<K1Plan> plans_a, plans_b;
     std::vector<K1Lane> lanes_a, lanes_b;
@@ -883,7 +888,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         RSH_BHIP(S->h_kents.ensure((size_t)NF * sizeof(TableEnt)));
         RSH_BHIP(S->h_chain.ensure((size_t)NF * sizeof(ChainFile)));
         RSH_BHIP(S->h_chain_out.ensure((size_t)NF * sizeof(ChainOut)));
-        RSH_BHIP(S->h_chain_ev.ensure((size_t)NF * kChainEvents * sizeof(rsh_event)));
+        RSH_BHIP(S->h_chain_ev.ensure((size_t)NF * kChainEvents * sizeof(rsh_event)));  // (kChainEvents: see above)
         if (!S->ev_fk) RSH_BHIP(hipEventCreateWithFlags(&S->ev_fk, hipEventDisableTiming));
         RSH_BHIP(launch_table_clear(S->kslots.as<unsigned long long>(), (uint64_t)tns, st, bg));
         TableEnt* ke = S->h_kents.as<TableEnt>();
