@@ -503,7 +503,11 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
                 F[f].aligned_weak = r.head ? S->haw.as<int32_t>() + fs.off_na : S->src_weak.as<int32_t>() + fs.off_na;
                 F[f].slots = S->slots.as<unsigned long long>() + fs.off_ns;
                 F[f].mask = fs.ns - 1;
-                if (r.keys) {  // stale digest: only its chunks' keys (a handful), hashed here
+                F[f].nsmall = 0;
+                if (r.keys && !r.keys->empty() && r.keys->size() <= (size_t)PROBE_SMALL_KEYS) {  // compared in registers
+                    F[f].nsmall = (int32_t)r.keys->size();
+                    for (size_t j = 0; j < r.keys->size(); ++j) F[f].small[j] = (uint32_t)(*r.keys)[j];
+                } else if (r.keys) {  // stale digest: only its chunks' keys (a handful), hashed here
                     const uint32_t nsl = pow2_at_least(2 * r.keys->size() + 2);
                     const int64_t off = (int64_t)dkeys.size();
                     dkeys.resize(dkeys.size() + nsl, 0ull);

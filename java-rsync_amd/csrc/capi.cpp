@@ -479,6 +479,7 @@ class HipBackend : public rsh::ScanBackend {
         F->aligned_weak = (head || partial) ? c_->haw.as<int32_t>() : c_->src_weak.as<int32_t>();
         F->table_weak = d_table_weak_;
         F->C = t_.chunk_count;
+        F->nsmall = 0;  // key sets as probe hashes (tab.slots)
         return F;
     }
     int64_t win_pos_[rsh::HIT_WINDOWS] = {-1, -1, -1, -1};  // windows of the last probe's hits on the host (h_hit)

@@ -148,6 +148,7 @@ constexpr int PROBE_TILE = 4096;
 constexpr int PROBE_INLINE_TILES = 1;
 constexpr int HIT_BUCKET_CAP = 256;
 constexpr int HIT_BUCKET_INTS = 2 + HIT_BUCKET_CAP + PROBE_HITS_CAP * (1 + LISTED_IDX);
+constexpr int PROBE_SMALL_KEYS = 8;
 struct ScanFile {
     const uint8_t* data;
     int64_t n;
@@ -164,6 +165,8 @@ struct ScanFile {
                                       // first hit, then per listed hit j {count, idx[LISTED_IDX]}
     uint8_t* hit;                     // pinned host: T(p) in bytes 0..3, window k of the k-th smallest listed
                                       // hit at 16 + k B (k < HIT_WINDOWS; k = 0: the first hit)
+    int32_t nsmall;                   // > 0: the round's key set is these few keys (a stale digest's chunks),
+    uint32_t small[PROBE_SMALL_KEYS]; // compared in registers instead of looked up in slots
 };
 struct ProbeIv {
     int64_t a, b, anchor;

@@ -2388,17 +2388,30 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A)
         R = roll_sub(R, (int32_t)w, sbyte_of(xa, i));
         if (n - (p + 1) >= B) R = roll_add(R, sbyte_of(xb, i));
     }
-    unsigned long long sl[PROBE_PPT];
+    // a stale digest's few keys (the batched flush chain's probes over a file's rest): compared in registers
+    const int nsmall = F.nsmall;
+    uint32_t small[PROBE_SMALL_KEYS];
 #pragma unroll
-    for (int i = 0; i < PROBE_PPT; ++i) sl[i] = table.slots[slot_hash(key[i]) & table.mask];
+    for (int j = 0; j < PROBE_SMALL_KEYS; ++j) small[j] = F.small[j];
+    unsigned long long sl[PROBE_PPT];
+    if (nsmall == 0) {
+#pragma unroll
+        for (int i = 0; i < PROBE_PPT; ++i) sl[i] = table.slots[slot_hash(key[i]) & table.mask];
+    }
 #pragma unroll
     for (int i = 0; i < PROBE_PPT; ++i) {
         const int64_t p = p0 + i;
         if (p >= I.b || p >= qend) break;
         if (p < I.a) continue;
-        const unsigned long long v = (1ull << 32) | key[i];
-        bool hit = sl[i] == v;
-        if (!hit && sl[i] != 0ull) hit = table_has(table, key[i]);
+        bool hit = false;
+        if (nsmall > 0) {
+#pragma unroll
+            for (int j = 0; j < PROBE_SMALL_KEYS; ++j) hit = hit || (j < nsmall && small[j] == key[i]);
+        } else {
+            const unsigned long long v = (1ull << 32) | key[i];
+            hit = sl[i] == v;
+            if (!hit && sl[i] != 0ull) hit = table_has(table, key[i]);
+        }
         if (hit) {
             atomicMin(&F.out->first, (unsigned long long)p);
             const unsigned long long at = atomicAdd(&F.out->count, 1ull);
