@@ -2659,24 +2659,12 @@ __device__ __forceinline__ bool kslots_has(const unsigned long long* __restrict_
 constexpr int CHAIN_CK_BUCKETS = 4096;
 __device__ __forceinline__ uint32_t chain_ck_h1(uint32_t k) { return (k * 0x9E3779B1u) >> 20; }
 __device__ __forceinline__ uint32_t chain_ck_h2(uint32_t k) { return CHAIN_CK_BUCKETS + (((k ^ (k >> 15)) * 0x85EBCA77u) >> 20); }
-// In front of it, a two-bit filter of the same keys in the rest of the LDS (3072 64-bit words, 24 KiB: ~3 % of
-// absent keys pass at 16384 keys), so most lookups read 8 bytes instead of 32.
-constexpr int CHAIN_PRE_WORDS = 3072;
-__device__ __forceinline__ uint32_t chain_pre_word(uint32_t k) {
-    return (uint32_t)(((unsigned long long)(k * 0x2545F491u) * CHAIN_PRE_WORDS) >> 32);
-}
-__device__ __forceinline__ unsigned long long chain_pre_mask(uint32_t k) {
-    const uint32_t h = (k ^ (k >> 13)) * 0x5BD1E995u;
-    return (1ull << (h >> 26)) | (1ull << ((h >> 20) & 63u));
-}
 struct ChainKeySet {
     uint4* b;      // 2 * CHAIN_CK_BUCKETS buckets
     int32_t* has0;  // key 0 present
     int32_t* full;  // some key found no slot: lookups are not exact
-    unsigned long long* pre;  // the filter (CHAIN_PRE_WORDS)
 };
 __device__ __forceinline__ void chain_ck_insert(const ChainKeySet& ks, uint32_t k) {
-    atomicOr(&ks.pre[chain_pre_word(k)], chain_pre_mask(k));
     if (k == 0u) {
         *ks.has0 = 1;
         return;
@@ -2700,8 +2688,6 @@ __device__ __forceinline__ void chain_ck_insert(const ChainKeySet& ks, uint32_t 
     *ks.full = 1;  // a key is left over: the set is not exact
 }
 __device__ __forceinline__ bool chain_ck_has(const ChainKeySet& ks, uint32_t k) {
-    const unsigned long long m = chain_pre_mask(k);
-    if ((ks.pre[chain_pre_word(k)] & m) != m) return false;
     if (k == 0u) return *ks.has0 != 0;
     const uint4 a = ks.b[chain_ck_h1(k)], c = ks.b[chain_ck_h2(k)];
     return a.x == k || a.y == k || a.z == k || a.w == k || c.x == k || c.y == k || c.z == k || c.w == k;
@@ -2773,7 +2759,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_seg[CHAIN_SEGS][4];   // wide tiles: the exscan at each block's first lane
     __shared__ uint4 s_ck[2 * CHAIN_CK_BUCKETS];  // the table's keys (ChainKeySet)
     __shared__ int32_t s_ck_has0, s_ck_full;
-    __shared__ unsigned long long s_pre[CHAIN_PRE_WORDS];
     __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
     // fields across the loop (the event stores may alias it) -- a PCIe round trip each
@@ -2788,9 +2773,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const int64_t last = n - S, nB = n - B;
     const int64_t na = phase == 0 ? F.na_a : F.na, nflags = na < C ? na : C;
     const bool wide = (B % CHAIN_PPT) == 0 && B >= 512 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
-    const ChainKeySet kset{s_ck, &s_ck_has0, &s_ck_full, s_pre};
+    const ChainKeySet kset{s_ck, &s_ck_has0, &s_ck_full};
     for (int i = t; i < 2 * CHAIN_CK_BUCKETS; i += CHAIN_THREADS) s_ck[i] = make_uint4(0u, 0u, 0u, 0u);
-    for (int i = t; i < CHAIN_PRE_WORDS; i += CHAIN_THREADS) s_pre[i] = 0ull;
     if (t == 0) s_ck_has0 = s_ck_full = 0;
     __syncthreads();
     for (int64_t c = t; c < C; c += CHAIN_THREADS) chain_ck_insert(kset, (uint32_t)F.table_weak[c]);
