@@ -2700,12 +2700,22 @@ __device__ __forceinline__ bool chain_ck_has(const ChainKeySet& ks, uint32_t k) 
 __device__ __forceinline__ int chain_first_hit16(const unsigned long long* __restrict__ ks, uint32_t kmask,
                                                  const ChainKeySet& set, const uint32_t (&keys)[PROBE_PPT],
                                                  uint32_t valid) {
-    // the key set in LDS: exact (the usual case), so the table in global memory is not touched at all
+    // the key set in LDS: exact (the usual case), so the table in global memory is not touched at all.  Branch
+    // free: two 16-byte reads and eight compares per key (a wave's lanes would take every branch anyway)
     if (*set.full == 0) {
+        const bool has0 = *set.has0 != 0;
+        uint32_t m = 0;
 #pragma unroll
-        for (int i = 0; i < PROBE_PPT; ++i)
-            if (!chain_ck_has(set, keys[i])) valid &= ~(1u << i);
-        return valid ? __builtin_ctz(valid) : -1;
+        for (int i = 0; i < PROBE_PPT; ++i) {
+            const uint32_t k = keys[i];
+            const uint4 x = set.b[chain_ck_h1(k)], y = set.b[chain_ck_h2(k)];
+            const bool in = (x.x == k) | (x.y == k) | (x.z == k) | (x.w == k) | (y.x == k) | (y.y == k) | (y.z == k) |
+                            (y.w == k);
+            m |= (uint32_t)(k != 0u ? in : has0) << i;
+            if ((i & 3) == 3) asm volatile("" ::: "memory");  // 4 keys' reads in flight at a time (registers)
+        }
+        m &= valid;
+        return m ? __builtin_ctz(m) : -1;
     }
     uint32_t hit = 0, need = 0;
     {
@@ -2955,13 +2965,19 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     // subtract-then-add of Rolling.java:25-60 in two adds each), packed into the key per position
                     uint32_t u1 = s1, u2 = s2;
                     const int64_t lim_p = stop < lim_spec ? stop : lim_spec;
+#pragma unroll 1
+                    for (int hh = 0; hh < 2; ++hh) {  // (not unrolled: one half's keys in registers at a time)
+                        uint32_t wa[4], wb[4];
 #pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
+                        for (int j = 0; j < 4; ++j) {
+                            wa[j] = hh ? xa[1][j] : xa[0][j];
+                            wb[j] = hh ? xb[1][j] : xb[0][j];
+                        }
                         uint32_t keys[16];
 #pragma unroll
                         for (int i = 0; i < 16; ++i) {
                             keys[i] = (u1 & 0xFFFFu) | (u2 << 16);
-                            const int32_t xo = sbyte_of(xa[hh], i), xi = sbyte_of(xb[hh], i);
+                            const int32_t xo = sbyte_of(wa, i), xi = sbyte_of(wb, i);
                             u1 += (uint32_t)(xi - xo);
                             u2 += u1 - (uint32_t)B * (uint32_t)xo;
                         }
