@@ -121,6 +121,21 @@ def spawn_ranks(a):
     return rc
 
 
+SHARED_NOTE = "; REHEARSAL: more ranks than GPUs, ranks share GPUs round-robin (gloo barrier), not a scaling point"
+
+
+def setup_rank():
+    """This rank's GPU and process group (one process per GPU; the collectives are only the contract's barrier and
+    the max-over-ranks time).  Returns (rank, world, device, device of the time reduction, shared)."""
+    import torch
+    rank, world, local = shard.env_rank()
+    dev, backend, shared = shard.rank_device(local, world, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    if world > 1:
+        shard.init_distributed(backend, torch.device("cuda", dev) if backend == "nccl" else None)
+    return rank, world, dev, ("cuda" if backend == "nccl" else "cpu"), shared
+
+
 def main_dry(a):
     """The multi-rank plumbing without a device (CPU test of --gpus N): gloo process group, the barriers and
     the max-over-ranks reduction of the timed region, rank 0's JSON line."""
@@ -157,10 +172,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    rank, world, local = shard.env_rank()
-    torch.cuda.set_device(local)
-    if world > 1:  # one process per GPU; RCCL only for the barrier and the max-over-ranks time
-        shard.init_distributed("nccl", torch.device("cuda", local))
+    rank, world, local, red_dev, shared = setup_rank()
 
     def barrier():
         if world > 1:
@@ -277,7 +289,7 @@ def main():
         ctx.sync()
         torch.cuda.synchronize()
         barrier()
-        dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device="cuda")
+        dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device=red_dev)
         if gc_off:
             gc.enable()
         step_ms = [round((b - a) * 1e3, 3) for a, b in zip([t0] + t_step[:-1], t_step)]
@@ -337,7 +349,7 @@ def main():
             "block_length": B,
             "digest_length": dl,
             "chunks": C,
-            "parallelism": f"file-sharded x{world} (no collectives)",
+            "parallelism": f"file-sharded x{world} (no collectives)" + SHARED_NOTE * shared,
         },
         "roofline": {
             "kernel": "block_sums_pipe_kernel (K1: the Generator's launch; the Sender's aligned speculation is the "
@@ -423,10 +435,7 @@ def main_files(a):
     import concurrent.futures as cf
 
     import torch
-    rank, world, local = shard.env_rank()
-    torch.cuda.set_device(local)
-    if world > 1:
-        shard.init_distributed("nccl", torch.device("cuda", local))
+    rank, world, local, red_dev, shared = setup_rank()
     if not os.path.exists(R.LIB_PATH):
         R.build()
     L = R.lib()
@@ -534,7 +543,7 @@ def main_files(a):
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device="cuda")
+        dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device=red_dev)
         if gc_off:
             gc.enable()
         for i in range(F):  # Sender.java:1325 for every file of the last timed step
@@ -565,7 +574,8 @@ def main_files(a):
                                f"({VARIANT_TEXT[a.variant]} bases), B={B}, dl={dl}",
                    "bytes_per_step_per_gpu": int(read_step), "files_per_gpu": F, "block_length": B, "digest_length": dl,
                    "parallelism": f"file-sharded x{world} (no collectives), " + (
-                       "batched entry points" if a.files_api == "batch" else f"{a.threads} scan contexts per GPU")},
+                       "batched entry points" if a.files_api == "batch" else f"{a.threads} scan contexts per GPU")
+                   + SHARED_NOTE * shared},
         "roofline": {"kernel": "block_sums_pipe_kernel (batched K1: the Generator over the segment)", "bound": "hbm",
                      "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "step_frac": round(read_step / (head["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -27,6 +27,19 @@ def env_rank():
     return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def rank_device(local, world, ngpu):
+    """(device, backend, shared) for a rank: its own GPU LOCAL_RANK and RCCL for the barrier and the time
+    reduction when the node has a GPU per local rank; otherwise (a rehearsal of N ranks on a box with fewer GPUs)
+    ranks share GPUs round-robin and the collectives run on gloo, since RCCL refuses two ranks on one device.
+    The choice depends only on (LOCAL_WORLD_SIZE, ngpu), so every rank picks the same backend."""
+    if ngpu < 1:
+        raise RuntimeError("no GPU visible to this rank")
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if local_world <= ngpu:
+        return local, "nccl", False
+    return local % ngpu, "gloo", True
+
+
 def init_distributed(backend, device=None):
     """torch.distributed over 127.0.0.1 (the container hostname may not resolve)."""
     import torch.distributed as dist

@@ -15,6 +15,8 @@
 #   pmc-k1       one PMC pass over kbench: the production K1 against the same kernel without global loads
 #   kbench-k1    kbench: the K1 at B = 128 KiB and 8 KiB, the batched forms (1002, 1005, 1006)
 #   e2e          java-rsync_amd/tools/e2e.py at config 5 (16 GiB from host memory)
+#   multi        bench.py --gpus 2 without a launcher (its own rank processes) on a one-GPU box: the N-rank path,
+#                ranks sharing the GPU (a rehearsal, not a scaling point); config 5 and config 4
 #   ab           AB_OPTS ("name=value ...") against the default, alternating, REPS times (AB_ARGS: bench args)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
@@ -59,6 +61,11 @@ for step in "$@"; do
         kbench-k1)
             run 120 "$K" 16384 131072 4 8 1000 > "$O/kbench_128k.log" 2>&1
             run 120 "$K" 16384 8192 3 8 1000 1002 1005 1006 > "$O/kbench_8k.log" 2>&1 ;;
+        multi)
+            run 300 python bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline --no-companions \
+                > "$O/multi_file.json" 2> "$O/multi_file.err"
+            run 300 python bench.py --gpus 2 --workload files --steps 5 --warmup 2 --no-cpu-baseline --no-companions \
+                > "$O/multi_files.json" 2> "$O/multi_files.err" ;;
         e2e) run 400 python java-rsync_amd/tools/e2e.py --gib 16 > "$O/e2e_16GiB.json" 2> "$O/e2e.err" ;;
         ab)
             OPTS=""

@@ -89,3 +89,17 @@ def test_bench_gpus2_dry_run_spawns_ranks():
     assert len(lines) == 1, out.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["dry_run"] and rec["config"]["files_total"] == 256
+
+
+def test_rank_device_plan(monkeypatch):
+    """One GPU per local rank: RCCL on the rank's own device.  More local ranks than GPUs (a rehearsal of the
+    N-rank launch on a smaller box): round-robin devices and gloo, chosen identically by every rank."""
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert [shard.rank_device(r, 8, 8) for r in range(8)] == [(r, "nccl", False) for r in range(8)]
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert [shard.rank_device(r, 2, 1) for r in range(2)] == [(0, "gloo", True), (0, "gloo", True)]
+    monkeypatch.delenv("LOCAL_WORLD_SIZE")
+    assert [shard.rank_device(r, 4, 2) for r in range(4)] == [(0, "gloo", True), (1, "gloo", True),
+                                                              (0, "gloo", True), (1, "gloo", True)]
+    with pytest.raises(RuntimeError):
+        shard.rank_device(0, 1, 0)
