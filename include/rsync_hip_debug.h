@@ -8,7 +8,8 @@
  * applies to calls that start after the change.  Names: k1_gather, k1_shift, k1_unaligned, scan_trace,
  * scan_diag, scan_phase, scan_phase_guess, scan_segmented, scan_preprobe, scan_samples, scan_sample,
  * scan_spec_order, scan_early, scan_wait, scan_defer_steps, scan_defer_us, batch_spec, batch_spin_us,
- * batch_readahead, batch_prep_all, batch_chain, host_cores, file_tile, file_tile_above.
+ * batch_readahead, batch_prep_all, batch_chain, batch_chain_prefix, batch_chain_overlap, host_cores, file_tile,
+ * file_tile_above, probe_long.
  */
 #ifndef RSYNC_HIP_DEBUG_H
 #define RSYNC_HIP_DEBUG_H

@@ -49,7 +49,7 @@ struct BatchState {
     DevBuf slots, dslots, src_weak, src_strong, flags, haw, partials, bucket, first, k1_groups, k1_lanes;
     DevBuf d_probe;  // a large probe's descriptors (files, intervals, tiles, partial tiles) in device memory
     // Sender batch: pinned host (read or written by the kernels directly)
-    PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl, h_files, h_hit, h_win0, h_bucket, h_first, h_iv, h_tiles,
+    PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl, h_files, h_hit, h_win0, h_bucket, h_first, h_iv, h_tiles, h_segs,
         h_ptiles, h_req, h_gw, h_gb, h_ow, h_ob, h_win, h_copies, h_tabents, h_flagents, h_flagents_a, h_dkeys, h_ccopies,
         h_lead;
     // device, uncached: one abort word per file of the batch; the speculation's groups of file f stop once
@@ -106,7 +106,7 @@ struct BatchState {
                           &first, &k1_groups, &k1_lanes})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_files, &h_hit, &h_win0, &h_bucket, &h_first,
-                             &h_iv, &h_tiles, &h_ptiles, &h_req, &h_gw, &h_gb, &h_ow, &h_ob, &h_win, &h_copies,
+                             &h_iv, &h_tiles, &h_segs, &h_ptiles, &h_req, &h_gw, &h_gb, &h_ow, &h_ob, &h_win, &h_copies,
                              &h_tabents, &h_flagents, &h_flagents_a, &h_dkeys, &h_ccopies, &h_lead})
             b->release();
     }
@@ -458,6 +458,7 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
     std::vector<CopyEnt> copies;
     std::vector<ProbeIv> ivs;
     std::vector<ProbeTile> tiles;
+    std::vector<ProbeSeg> segs;
     std::vector<PartialTile> ptiles;
     std::vector<int32_t> preq;
     std::vector<int64_t> gw_at(files.size(), -1), gb_at(files.size(), -1), win_at(files.size(), -1);
@@ -522,10 +523,13 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
                 F[f].iv0 = (int32_t)ivs.size();
                 F[f].niv = (int32_t)r.niv;
                 const size_t t0 = tiles.size();
+                int64_t full = 0;
+                for (int64_t i = 0; i < r.niv; ++i) full += probe_full_positions(r.iv[i].a, r.iv[i].b, fs.n, fs.B);
+                const int64_t seg_len = probe_seg_len(full, fs.B);
                 for (int64_t i = 0; i < r.niv; ++i) {
                     const ProbeInterval& v = r.iv[i];
                     ivs.push_back(ProbeIv{v.a, v.b, v.anchor, v.e_lo & 0xFFFFu, v.e_hi & 0xFFFFu, f, 0});
-                    probe_tiles(v.a, v.b, fs.B, (int32_t)(ivs.size() - 1), &tiles);
+                    probe_plan(v.a, v.b, fs.n, fs.B, (int32_t)(ivs.size() - 1), seg_len, &tiles, &segs);
                 }
                 probe_partials(&tiles, t0, fs.B, f, &ptiles);
                 if (r.head) {  // anchors T(kB) of the blocks these tiles sit in
@@ -550,6 +554,7 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
     CopyEnt* hcp;
     ProbeIv* hiv;
     ProbeTile* ht;
+    ProbeSeg* hsg;
     PartialTile* hpt;
     unsigned long long* hdk;
     hipError_t e = hipSuccess;
@@ -564,6 +569,7 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
     chk(pin(S->h_copies, (int64_t)copies.size(), &hcp));
     chk(pin(S->h_iv, (int64_t)ivs.size(), &hiv));
     chk(pin(S->h_tiles, (int64_t)tiles.size(), &ht));
+    chk(pin(S->h_segs, (int64_t)segs.size(), &hsg));
     chk(pin(S->h_ptiles, (int64_t)ptiles.size(), &hpt));
     chk(pin(S->h_req, (int64_t)preq.size(), &hreq));
     chk(pin(S->h_dkeys, (int64_t)dkeys.size(), &hdk));
@@ -582,6 +588,7 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
     if (!copies.empty()) memcpy(hcp, copies.data(), copies.size() * sizeof(CopyEnt));
     if (!ivs.empty()) memcpy(hiv, ivs.data(), ivs.size() * sizeof(ProbeIv));
     if (!tiles.empty()) memcpy(ht, tiles.data(), tiles.size() * sizeof(ProbeTile));
+    if (!segs.empty()) memcpy(hsg, segs.data(), segs.size() * sizeof(ProbeSeg));
     if (!ptiles.empty()) memcpy(hpt, ptiles.data(), ptiles.size() * sizeof(PartialTile));
     if (!preq.empty()) memcpy(hreq, preq.data(), preq.size() * sizeof(int32_t));
     if (!dkeys.empty()) memcpy(hdk, dkeys.data(), dkeys.size() * sizeof(uint64_t));
@@ -606,10 +613,12 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
         const ProbeIv* div = hiv;
         const ProbeTile* dt = ht;
         const PartialTile* dpt = hpt;
-        if (tiles.size() > kProbeUpload) {
+        const ProbeSeg* dsg = hsg;
+        if (tiles.size() + segs.size() > kProbeUpload) {
             const size_t bf = pad16(files.size() * sizeof(ScanFile)), bi = pad16(ivs.size() * sizeof(ProbeIv)),
-                         bt = pad16(tiles.size() * sizeof(ProbeTile)), bp = pad16(ptiles.size() * sizeof(PartialTile));
-            chk(S->d_probe.ensure(bf + bi + bt + bp + 16));
+                         bt = pad16(tiles.size() * sizeof(ProbeTile)), bp = pad16(ptiles.size() * sizeof(PartialTile)),
+                         bs = pad16(segs.size() * sizeof(ProbeSeg));
+            chk(S->d_probe.ensure(bf + bi + bt + bp + bs + 16));
             if (e != hipSuccess) return e;
             uint8_t* d = S->d_probe.as<uint8_t>();
             chk(hipMemcpyAsync(d, F, files.size() * sizeof(ScanFile), hipMemcpyHostToDevice, st));
@@ -621,6 +630,9 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
             div = reinterpret_cast<const ProbeIv*>(d + bf);
             dt = reinterpret_cast<const ProbeTile*>(d + bf + bi);
             dpt = reinterpret_cast<const PartialTile*>(d + bf + bi + bt);
+            if (!segs.empty())
+                chk(hipMemcpyAsync(d + bf + bi + bt + bp, hsg, segs.size() * sizeof(ProbeSeg), hipMemcpyHostToDevice, st));
+            dsg = reinterpret_cast<const ProbeSeg*>(d + bf + bi + bt + bp);
         }
         ProbeArgs A;
         A.files = dF;
@@ -628,6 +640,7 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
         A.tiles = dt;
         A.partials = S->partials.as<int4>();
         chk(launch_probe_first(A, (uint32_t)tiles.size(), dpt, (uint32_t)ptiles.size(), st));
+        chk(launch_probe_long(A, dsg, (uint32_t)segs.size(), st));
         chk(launch_hit_window(F, hiv, hreq, (int32_t)preq.size(), max_C, st));
         chk(hipMemcpyAsync(S->h_first.p, S->first.p, files.size() * sizeof(ProbeOut), hipMemcpyDeviceToHost, st));
         chk(hipMemcpyAsync(S->h_bucket.p, S->bucket.p, files.size() * HIT_BUCKET_INTS * sizeof(int32_t),
@@ -896,7 +909,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         RSH_BHIP(S->h_chain_out.ensure((size_t)NF * sizeof(ChainOut)));
         RSH_BHIP(S->h_chain_ev.ensure((size_t)NF * kChainEvents * sizeof(rsh_event)));  // (kChainEvents: see above)
         if (!S->ev_fk) RSH_BHIP(hipEventCreateWithFlags(&S->ev_fk, hipEventDisableTiming));
-        RSH_BHIP(launch_table_clear(S->kslots.as<unsigned long long>(), (uint64_t)tns, st, bg));
+        // the chunk indexes must be ready when the prefix K1 ends (the phase-0 walks wait for both): the runtime's
+        // fill, then the index with several CASes in flight per thread; beside the prefix K1 (which holds every
+        // wave slot) both end with it in config 4 (r3s: fill 0.06 ms + index 0.20 ms inside the K1's 0.29 ms)
+        RSH_BHIP(hipMemsetAsync(S->kslots.p, 0, (size_t)tns * 8, st));
         TableEnt* ke = S->h_kents.as<TableEnt>();
         for (int32_t f = 0; f < NF; ++f) {
             FileScan& fs = files[(size_t)f];

@@ -265,12 +265,17 @@ class HipBackend : public rsh::ScanBackend {
             tab.mask = ns - 1;
         }
         tiles_.clear();
+        segs_.clear();
         ptiles_.clear();
-        for (int64_t i = 0; i < count; ++i) rsh::probe_tiles(iv[i].a, iv[i].b, B_, (int32_t)i, &tiles_);
+        int64_t full = 0;
+        for (int64_t i = 0; i < count; ++i) full += rsh::probe_full_positions(iv[i].a, iv[i].b, n_, B_);
+        const int64_t seg_len = tiled ? 0 : rsh::probe_seg_len(full, B_);  // (tiled: one tile of the source in HBM)
+        for (int64_t i = 0; i < count; ++i) rsh::probe_plan(iv[i].a, iv[i].b, n_, B_, (int32_t)i, seg_len, &tiles_, &segs_);
         rsh::probe_partials(&tiles_, 0, B_, 0, &ptiles_);
         rsh::ProbeIv* hiv = pin<rsh::ProbeIv>(c_->h_iv, count + 1);
         rsh::ProbeTile* ht = pin<rsh::ProbeTile>(c_->h_tiles, (int64_t)tiles_.size() + 1);
         rsh::PartialTile* hpt = pin<rsh::PartialTile>(c_->h_ptiles, (int64_t)ptiles_.size() + 1);
+        rsh::ProbeSeg* hsg = pin<rsh::ProbeSeg>(c_->h_psegs, (int64_t)segs_.size() + 1);
         rsh::ProbeOut* hf = pin<rsh::ProbeOut>(c_->h_first, 1);
         join_window_digests();  // h_hit is about to be overwritten
         uint8_t* hh = pin<uint8_t>(c_->h_hit, 16 + kScanWindows * B_);
@@ -288,6 +293,7 @@ class HipBackend : public rsh::ScanBackend {
             hiv[i] = rsh::ProbeIv{iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo & 0xFFFFu, iv[i].e_hi & 0xFFFFu, 0, 0};
         if (!tiles_.empty()) memcpy(ht, tiles_.data(), tiles_.size() * sizeof(rsh::ProbeTile));
         if (!ptiles_.empty()) memcpy(hpt, ptiles_.data(), ptiles_.size() * sizeof(rsh::PartialTile));
+        if (!segs_.empty()) memcpy(hsg, segs_.data(), segs_.size() * sizeof(rsh::ProbeSeg));
         F->aligned_weak = (head || partial) ? c_->haw.as<int32_t>() : c_->src_weak.as<int32_t>();
         F->slots = tab.slots;
         F->mask = tab.mask;
@@ -319,6 +325,7 @@ class HipBackend : public rsh::ScanBackend {
         A.tiles = ht;
         A.partials = c_->partials.as<int4>();
         ok(rsh::launch_probe_first(A, (uint32_t)tiles_.size(), hpt, (uint32_t)ptiles_.size(), c_->stream));
+        ok(rsh::launch_probe_long(A, hsg, (uint32_t)segs_.size(), c_->stream));
         // the resolver's next questions at a hit are T(p), the bucket of the key that hit and (usually) the
         // MD5 of the window at p: answer them in this round trip
         int32_t* req = hb + rsh::HIT_BUCKET_INTS;
@@ -468,6 +475,7 @@ class HipBackend : public rsh::ScanBackend {
     uint8_t seed_[4];
     std::vector<rsh::ProbeTile> tiles_;
     std::vector<rsh::PartialTile> ptiles_;
+    std::vector<rsh::ProbeSeg> segs_;
     std::vector<rsh::GatherEnt> anchors_;
     // the scan as a batch of one file for the probe / gather kernels (pinned, device-readable)
     rsh::ScanFile* file() {

@@ -126,7 +126,7 @@ struct rsh_ctx {
     PinnedBuf h_lead;      // T(kB) of the first aligned windows (the speculation launch decision)
     // resolver round trips: the small kernels read their inputs from and write their outputs to pinned
     // host memory directly (no staging copies); the probe result and digest windows come back by copy
-    PinnedBuf h_pos, h_out, h_iv, h_tiles, h_keys, h_first, h_win, h_ptiles;
+    PinnedBuf h_pos, h_out, h_iv, h_tiles, h_keys, h_first, h_win, h_ptiles, h_psegs;
     PinnedBuf h_hit;  // after a probe hit: T(p) (bytes 0..3) and the window at p (from byte 16)
     PinnedBuf h_win0;    // window 0 of the current scan (its digest is computed on a host thread)
     PinnedBuf h_pend;    // the prefix end's window sums (launched with the phase guess's first probe)
@@ -149,7 +149,7 @@ struct rsh_ctx {
                           &dkeys, &pos, &out, &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pw[0], &h_ps[0], &h_pw[1], &h_ps[1], &h_lead, &h_pos, &h_out, &h_iv,
-                             &h_tiles, &h_keys, &h_first, &h_win, &h_ptiles, &h_hit, &h_win0, &h_pend, &h_bucket, &h_files,
+                             &h_tiles, &h_keys, &h_first, &h_win, &h_ptiles, &h_psegs, &h_hit, &h_win0, &h_pend, &h_bucket, &h_files,
                              &h_stage})
             b->release();
         if (abort_word) (void)hipFree(abort_word);

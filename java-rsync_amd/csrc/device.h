@@ -193,8 +193,31 @@ struct ProbeArgs {
     const ProbeTile* tiles;
     int4* partials;  // written by pass 1
 };
+// Long intervals (a batched flush chain over a file's rest: ~1600 intervals of 9B + 1 positions) as segments of up
+// to PROBE_LONG_PASSES x PROBE_LONG_SUB positions, one workgroup each, PROBE_LONG_PPL consecutive positions per lane: the workgroup
+// digests its own anchor T(q0) (the window at its first position) instead of taking it from an aligned block's
+// sums, so segments ignore block boundaries and need no pass 1.  Only positions whose window is full (p <= n - B).
+constexpr int PROBE_LONG_PPL = 64;
+constexpr int64_t PROBE_LONG_SUB = 256 * PROBE_LONG_PPL;  // positions per pass of a workgroup's lanes
+constexpr int64_t PROBE_LONG_PASSES = 8;                  // at most this many passes per workgroup (one anchor)
+constexpr int64_t PROBE_LONG_MIN = 2 * PROBE_LONG_SUB;    // shorter full-window parts stay in tiles
+constexpr int64_t PROBE_LONG_BIG = 256 * PROBE_LONG_SUB;  // smaller probes stay in tiles (parallelism, latency)
+constexpr int64_t PROBE_LONG_MAX_B = 16384;               // larger blocks stay in tiles (the anchor reads B bytes)
+struct ProbeSeg {
+    int64_t q0;   // first position (16-aligned; positions below the interval's a are skipped)
+    int32_t iv;   // interval index
+    int32_t len;  // positions [q0, q0 + len), every one <= n - B
+};
 // Appends the tiles covering [a, b) for interval `iv` (host side).
 void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeTile>* out);
+// The segment length for a probe whose intervals hold `full_positions` full-window positions in all (0: tiles only).
+int64_t probe_seg_len(int64_t full_positions, int64_t B);
+int64_t probe_full_positions(int64_t a, int64_t b, int64_t n, int64_t B);
+// As probe_tiles, with the full-window part of a long interval as segments of seg_len positions (host side).
+void probe_plan(int64_t a, int64_t b, int64_t n, int64_t B, int32_t iv, int64_t seg_len, std::vector<ProbeTile>* tiles,
+                std::vector<ProbeSeg>* segs);
+// The segments' launch (writes the same ProbeOut records as the tiles' launch; either order).
+hipError_t launch_probe_long(const ProbeArgs& args, const ProbeSeg* segs, uint32_t nsegs, hipStream_t s);
 // Assigns ProbeTile::pbase for tiles[t0 ..] (one file's tiles, ascending) and appends the partial tiles
 // pass 1 computes for them (host side).
 void probe_partials(std::vector<ProbeTile>* tiles, size_t t0, int64_t B, int32_t file, std::vector<PartialTile>* out);

@@ -2608,6 +2608,144 @@ void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeT
     }
 }
 
+int64_t probe_seg_len(int64_t full_positions, int64_t B) {
+    // segments pay off for big probes (a flush chain over a file's rest) at block lengths whose anchor (B bytes per
+    // workgroup) is small against the segment; a few long intervals keep the tiles' parallelism instead (a probe
+    // beside the speculation K1 sits on the resolver's latency path: 128 KiB blocks as 8-pass segments were 1 ms
+    // slower per config-5 step than as tiles)
+    if (opt(OPT_PROBE_LONG) == 0 || B > PROBE_LONG_MAX_B || full_positions < PROBE_LONG_BIG) return 0;
+    const int64_t passes = full_positions / (1024 * PROBE_LONG_SUB);  // ~1024 workgroups, then longer ones
+    return (passes < 1 ? 1 : passes > PROBE_LONG_PASSES ? PROBE_LONG_PASSES : passes) * PROBE_LONG_SUB;
+}
+
+int64_t probe_full_positions(int64_t a, int64_t b, int64_t n, int64_t B) {
+    const int64_t e = b < n - B + 1 ? b : n - B + 1;
+    return e > a ? e - a : 0;
+}
+
+void probe_plan(int64_t a, int64_t b, int64_t n, int64_t B, int32_t iv, int64_t seg_len, std::vector<ProbeTile>* tiles,
+                std::vector<ProbeSeg>* segs) {
+    const int64_t full_end = b < n - B + 1 ? b : n - B + 1;  // positions below it have a full window
+    if (seg_len <= 0 || full_end - a < PROBE_LONG_MIN) {
+        probe_tiles(a, b, B, iv, tiles);
+        return;
+    }
+    for (int64_t q = a & ~(int64_t)15; q < full_end; q += seg_len)
+        segs->push_back(ProbeSeg{q, iv, (int32_t)(full_end - q < seg_len ? full_end - q : seg_len)});
+    probe_tiles(full_end, b, B, iv, tiles);  // the shrinking windows near the end, if the interval reaches them
+}
+
+// Pass-free probe over long segments (see ProbeSeg): T(q0) digested by the workgroup once, then sub-segments of
+// PROBE_LONG_SUB positions in order: the lanes' start values from one exscan of their 64 positions' byte sums (both
+// streams, weights relative to the sub-segment's start), each lane rolls its 64 positions with the exact Java updates
+// on R = T + E and checks every key as probe_first_kernel does per tile, and the last lane's rolled value (less E)
+// anchors the next sub-segment.  One anchor and one launch slot per segment (up to PROBE_LONG_PASSES passes).
+__global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void probe_long_kernel(ProbeArgs A, const ProbeSeg* __restrict__ segs) {
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ int32_t sh[4 * PROBE_THREADS / 64];
+    __shared__ int32_t s_next;  // T at the next sub-segment's start (packed halves)
+    const ProbeSeg g = segs[blockIdx.x];
+    const ProbeIv I = A.ivs[g.iv];
+    const ScanFile& F = A.files[I.file];
+    const int64_t n = F.n, B = F.B;
+    const uint8_t* __restrict__ data = F.data;
+    const int64_t q0 = g.q0, q1 = q0 + g.len;  // every window full: q1 - 1 <= n - B
+    const int64_t nb = n - B;
+    auto clampB = [&](int64_t p) { return p < nb ? p : nb; };
+    // the anchor: T(q0) = (sum x, sum (B - i) x_{q0 + i}) over the window [q0, q0 + B) (full: q0 <= n - B)
+    int32_t h[2] = {0, 0};
+    range_sums(data, n, q0, q0 + B, q0, h[0], h[1]);
+    block_reduce<2>(h, sh);
+    uint32_t s1o = (uint32_t)h[0], s2o = (uint32_t)B * (uint32_t)h[0] - (uint32_t)h[1];
+    const ProbeTable table{F.slots, F.mask};
+    const int nsmall = F.nsmall;
+    uint32_t small[PROBE_SMALL_KEYS];
+#pragma unroll
+    for (int j = 0; j < PROBE_SMALL_KEYS; ++j) small[j] = F.small[j];
+    const int t = threadIdx.x;
+    for (int64_t base = q0; base < q1; base += PROBE_LONG_SUB) {
+        const int64_t p0 = base + (int64_t)t * PROBE_LONG_PPL;
+        int32_t pre[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < PROBE_LONG_PPL / 16; ++k) {  // the lane's bytes at p0 and at p0 + B: its sums
+            uint32_t wa[4], wb[4];
+            load16(data, n, p0 + 16 * k, wa);
+            load16(data, n, p0 + B + 16 * k, wb);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                dword_sums(wa[j], (uint32_t)(p0 + 16 * k + 4 * j - base), pre[0], pre[1]);
+                dword_sums(wb[j], (uint32_t)(p0 + B + 16 * k + 4 * j - base), pre[2], pre[3]);
+            }
+        }
+        block_exscan<4>(pre, sh);  // sums over [base, p0) and [base + B, p0 + B), weights j - base
+        const bool live = p0 < q1;
+        if (live) {
+            const uint32_t P1e = s1o + (uint32_t)pre[2];
+            const uint32_t P2e = (uint32_t)B * s1o - s2o + (uint32_t)pre[3];
+            const uint32_t s1 = P1e - (uint32_t)pre[0];
+            const uint32_t s2 = (uint32_t)(p0 + B - base) * s1 - (P2e - (uint32_t)pre[1]);
+            const uint32_t ehi = I.e_hi + I.e_lo * (uint32_t)(clampB(p0) - clampB(I.anchor));
+            int32_t R = (int32_t)(((s1 + I.e_lo) & 0xFFFFu) | ((s2 + ehi) << 16));
+#pragma unroll 1
+            for (int grp = 0; grp < PROBE_LONG_PPL / 16; ++grp) {  // 16 positions at a time (bytes re-read: L1)
+                uint32_t wa[4], wb[4];
+                load16(data, n, p0 + 16 * grp, wa);
+                load16(data, n, p0 + B + 16 * grp, wb);
+                uint32_t key[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {  // full windows throughout: w = B, the add always follows
+                    key[i] = (uint32_t)R;
+                    R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(wa, i)), sbyte_of(wb, i));
+                }
+                if (p0 + 16 * grp + 15 < I.a || p0 + 16 * grp >= q1) continue;  // (a group wholly below a)
+                unsigned long long sl[16];
+                if (nsmall == 0) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) sl[i] = table.slots[slot_hash(key[i]) & table.mask];
+                }
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int64_t p = p0 + 16 * grp + i;
+                    if (p >= q1 || p >= I.b) break;
+                    if (p < I.a) continue;
+                    bool hit = false;
+                    if (nsmall > 0) {
+#pragma unroll
+                        for (int j = 0; j < PROBE_SMALL_KEYS; ++j) hit = hit || (j < nsmall && small[j] == key[i]);
+                    } else {
+                        hit = sl[i] == ((1ull << 32) | key[i]);
+                        if (!hit && sl[i] != 0ull) hit = table_has(table, key[i]);
+                    }
+                    if (hit) {
+                        atomicMin(&F.out->first, (unsigned long long)p);
+                        const unsigned long long at = atomicAdd(&F.out->count, 1ull);
+                        if (at < (unsigned long long)PROBE_HITS_CAP) {
+                            F.out->pos[at] = (unsigned long long)p;
+                            F.out->key[at] = key[i];
+                        }
+                    }
+                }
+            }
+            if (t == PROBE_THREADS - 1) {  // R(p0 + 64) less E there: the next sub-segment's anchor T
+                const int64_t pn = p0 + PROBE_LONG_PPL;
+                const uint32_t en = I.e_hi + I.e_lo * (uint32_t)(clampB(pn) - clampB(I.anchor));
+                const uint32_t r = (uint32_t)R;
+                s_next = (int32_t)((((r & 0xFFFFu) - I.e_lo) & 0xFFFFu) | (((r >> 16) - en) << 16));
+            }
+        }
+        __syncthreads();
+        s1o = (uint32_t)s_next & 0xFFFFu;
+        s2o = (uint32_t)s_next >> 16;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_probe_long(const ProbeArgs& args, const ProbeSeg* segs, uint32_t nsegs, hipStream_t s) {
+    if (nsegs == 0) return hipSuccess;
+    hipLaunchKernelGGL(probe_long_kernel, dim3(nsegs), dim3(PROBE_THREADS), 0, s, args, segs);
+    return hipGetLastError();
+}
+
 hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const PartialTile* ptiles, uint32_t nptiles,
                               hipStream_t s) {
     if (ntiles == 0) return hipSuccess;
@@ -2842,9 +2980,29 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         if (k == pref && k < nflags && F.flags[k]) {
             if (t == 0) s_zero = nflags;
             __syncthreads();
-            for (int64_t j0 = k; j0 < nflags; j0 += CHAIN_THREADS) {
-                const int64_t j = j0 + t;
-                if (j < nflags && !F.flags[j]) atomicMin((unsigned long long*)&s_zero, (unsigned long long)j);
+            // one aligned 16-byte line of flags per lane per pass: an identical file's 16384 flags in two passes
+            // instead of 32 load-and-barrier rounds.  A line may start before flag k (or before the file's flags,
+            // inside the batch's flag buffer) and is masked to [k, nflags); a line past the end is read bytewise.
+            const uintptr_t fa = reinterpret_cast<uintptr_t>(F.flags);
+            for (uintptr_t l0 = (fa + (uintptr_t)k) & ~(uintptr_t)15; l0 < fa + (uintptr_t)nflags;
+                 l0 += 16u * CHAIN_THREADS) {
+                const uintptr_t la = l0 + 16u * (uintptr_t)t;
+                const int64_t jb = (int64_t)la - (int64_t)fa;  // flag index of the line's first byte
+                int64_t z = -1;
+                if (la < fa + (uintptr_t)nflags) {
+                    uint32_t w[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
+                    if (la + 16 <= fa + (uintptr_t)nflags) {
+                        const uint4 q = *reinterpret_cast<const uint4*>(la);
+                        w[0] = q.x, w[1] = q.y, w[2] = q.z, w[3] = q.w;
+                    } else {
+                        for (int i = 0; i < 16; ++i)
+                            if (jb + i >= 0 && jb + i < nflags && F.flags[jb + i] == 0) w[i >> 2] &= ~(0xFFu << (8 * (i & 3)));
+                    }
+#pragma unroll
+                    for (int i = 15; i >= 0; --i)
+                        if (jb + i >= k && jb + i < nflags && ((w[i >> 2] >> (8 * (i & 3))) & 0xFFu) == 0u) z = jb + i;
+                }
+                if (z >= 0) atomicMin((unsigned long long*)&s_zero, (unsigned long long)z);
                 __syncthreads();
                 if (s_zero < nflags) break;
             }
@@ -3246,13 +3404,33 @@ hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStre
 
 // The chunk index of the chain walk: every chunk i of a file as (key << 32) | (i + 1) in an open-addressing table
 // (0 = empty); the chunks with one key all lie on that key's probe path before its first empty slot.
+// A thread's keys go in groups of CHUNK_INDEX_MLP: the group's first-slot CASes are issued back to back (independent
+// atomics, all in flight at once), and only a CAS that found its slot taken walks the probe path (a serial
+// CAS-then-next loop keeps one atomic round trip in flight per thread).  Config 4's 2 M chunks on the background
+// grid beside the prefix K1: the index now ends inside that launch instead of 0.03 ms after it.
+constexpr int CHUNK_INDEX_MLP = 8;
 __global__ void chunk_index_kernel(const TableEnt* __restrict__ ents, uint32_t nfiles) {
     const TableEnt e = ents[blockIdx.y];
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < e.nkeys; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t key = (uint32_t)e.keys[i];
-        const unsigned long long v = ((unsigned long long)key << 32) | (uint32_t)(i + 1);
-        uint32_t h = slot_hash(key) & e.mask;
-        while (atomicCAS(&e.slots[h], 0ull, v) != 0ull) h = (h + 1) & e.mask;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < e.nkeys; i0 += CHUNK_INDEX_MLP * stride) {
+        unsigned long long v[CHUNK_INDEX_MLP], got[CHUNK_INDEX_MLP];
+        uint32_t h[CHUNK_INDEX_MLP];
+#pragma unroll
+        for (int j = 0; j < CHUNK_INDEX_MLP; ++j) {
+            const int64_t i = i0 + j * stride;
+            const uint32_t key = i < e.nkeys ? (uint32_t)e.keys[i] : 0u;
+            v[j] = ((unsigned long long)key << 32) | (uint32_t)(i + 1);
+            h[j] = slot_hash(key) & e.mask;
+        }
+#pragma unroll
+        for (int j = 0; j < CHUNK_INDEX_MLP; ++j)
+            got[j] = i0 + j * stride < e.nkeys ? atomicCAS(&e.slots[h[j]], 0ull, v[j]) : 0ull;
+#pragma unroll
+        for (int j = 0; j < CHUNK_INDEX_MLP; ++j) {
+            if (got[j] == 0ull) continue;
+            uint32_t hh = (h[j] + 1) & e.mask;
+            while (atomicCAS(&e.slots[hh], 0ull, v[j]) != 0ull) hh = (hh + 1) & e.mask;
+        }
     }
     (void)nfiles;
 }

@@ -42,6 +42,7 @@ enum Opt : int {
     OPT_HOST_CORES,        // resolver worker threads (0: the process's cores, cgroup quota included)
     OPT_FILE_TILE,         // rsh_match_scan_file: tile bytes above OPT_FILE_TILE_ABOVE
     OPT_FILE_TILE_ABOVE,   // rsh_match_scan_file: sources above this size are scanned tiled
+    OPT_PROBE_LONG,        // 1: long probe intervals as pass-free segments (probe_long_kernel); 0: tiles only
     OPT_COUNT
 };
 
@@ -59,6 +60,7 @@ inline const OptInfo* opt_info() {
         {"batch_spec", -1},        {"batch_spin_us", 200},    {"batch_readahead", 0},  {"batch_prep_all", 0},
         {"batch_chain", 1},        {"batch_chain_prefix", -1}, {"batch_chain_overlap", 0},
         {"host_cores", 0},         {"file_tile", 4LL << 30}, {"file_tile_above", 32LL << 30},
+        {"probe_long", 1},
     };
     return t;
 }

@@ -6,12 +6,15 @@
 #
 #   tests        the whole GPU suite (pytest -m gpu)
 #   tests-batch  the batched-scan suite and the config-4 oracle checks
+#   pytest       the GPU tests named in PYTEST_ARGS (files / -k expressions)
 #   smoke        __graft_entry__.smoke()
 #   bench        the default bench line (config 5, with companions)
 #   files        the config-4 line, both basis forms (FILES_STEPS steps)
 #   files-trace  one traced config-4 step (VARIANT, default half): the chain walk's breakdown (scan_trace = 2)
 #   prof         rocprofv3 kernel trace + stats of the default line (the summary committed under profiles/)
 #   timeline     rocprofv3 kernel + copy timeline of the config-4 line (VARIANT)
+#   fetch        rocprofv3 --pmc FETCH_SIZE passes (counters only, kernel trace) of the default line and the config-4
+#                line: the HBM bytes per K1 launch that bench.py reports as roofline.traffic
 #   pmc-k1       one PMC pass over kbench: the production K1 against the same kernel without global loads
 #   kbench-k1    kbench: the K1 at B = 128 KiB and 8 KiB, the batched forms (1002, 1005, 1006)
 #   e2e          java-rsync_amd/tools/e2e.py at config 5 (16 GiB from host memory)
@@ -38,6 +41,8 @@ for step in "$@"; do
         tests) run 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > "$O/gpu_tests.log" 2>&1 ;;
         tests-batch) run 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread tests/test_gpu_batch.py \
             tests/test_gpu_fullsize.py -k "batch or config4" > "$O/batch_tests.log" 2>&1 ;;
+        pytest) run 900 python -u -m pytest -m gpu -x -v --timeout 400 --timeout-method thread $PYTEST_ARGS \
+            > "$O/pytest.log" 2>&1 ;;
         smoke) run 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.log" 2>&1 ;;
         bench) run 300 python bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
         files)
@@ -53,6 +58,13 @@ for step in "$@"; do
         timeline) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --kernel-trace --memory-copy-trace --stats \
             -d "$O/timeline" -o run --output-format csv -- python3 "$R/bench.py" --workload files --variant "$VARIANT" \
             --steps 3 --warmup 1 --no-cpu-baseline --no-companions > "$O/timeline.json" 2> "$O/timeline.err") || exit 1 ;;
+        fetch)
+            (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch" -o run \
+                --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-companions \
+                > "$O/fetch_bench.json" 2> "$O/fetch_bench.err") || exit 1
+            (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch_files" -o run \
+                --output-format csv -- python3 "$R/bench.py" --workload files --steps 2 --warmup 1 --no-cpu-baseline \
+                --no-companions > "$O/fetch_files.json" 2> "$O/fetch_files.err") || exit 1 ;;
         pmc-k1)
             C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"
             run 120 "$K" 16384 131072 4 5 1000 58 > "$O/pmc_kbench.log" 2>&1

@@ -271,7 +271,7 @@ def test_batch_speculation_cancelled_per_file(ctx):
                 assert got == oev and (sj[j].literal, sj[j].matched) == (olit, omat), f"small file {j}"
 
 
-@pytest.mark.parametrize("alphabet,prefix", [(2, -1), (4, -1), (16, -1), (2, 5), (16, 7)])
+@pytest.mark.parametrize("alphabet,prefix", [(2, -1), (4, -1), (16, -1), (2, 5), (16, 7), (4, 64)])
 def test_batch_chain_low_entropy(ctx, alphabet, prefix, rsh_opt):
     """The device chain walk against the oracle where weak-sum collisions are everywhere: bytes from a small
     alphabet, so the first table hit after a modified block is usually a false one at an unaligned position
