@@ -47,8 +47,8 @@ KEY_CASE = KEY_SRC ^ 5
 KEY_INS = KEY_SRC ^ 0x1B
 SHIFT_AT = 155 * 131072 + 4096  # the "config5_shift1" insert position
 WARMUP_MIN_MS = 250.0  # untimed warmup of at least this long (and at least --warmup steps)
-TRAFFIC_CSV = "r2_v22_bench_fetch_size.csv"
-TRAFFIC_FILES_CSV = "r2_v22_files_fetch_size.csv"
+TRAFFIC_CSV = "r3/r3x_bench_fetch_size.csv"
+TRAFFIC_FILES_CSV = "r3/r3x_files_fetch_size.csv"
 
 
 def parse():
@@ -580,7 +580,7 @@ def main_files(a):
                      "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                      "step_frac": round(read_step / (head["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": pmc_traffic(os.path.join(ROOT, "profiles", TRAFFIC_FILES_CSV), BATCH_KERNEL, n),
-                     "traffic_source": f"profiles/{TRAFFIC_FILES_CSV} (FETCH_SIZE x2, a prior run)",
+                     "traffic_source": f"profiles/{TRAFFIC_FILES_CSV} (FETCH_SIZE x2 of the 16 GiB launches, a prior run)",
                      "kernel_ms": round(k_ms, 4), "algorithmic_bytes": n},
         "scan": head["scan"], "parity": head["parity"], "variants": comp,
     }
@@ -739,7 +739,10 @@ def pmc_traffic(path, kernel_substr, n):
     per = {}
     for r in rows:
         per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    return round(sum(per.values()) / len(per) * 1024 * 2)
+    # launches over the whole 16 GiB only (the Generator's, a full speculation's): the batched scan's prefix
+    # speculation (1 GiB), the rest of it (15 GiB) and stopped launches run the same kernel over less
+    full = [v * 1024 * 2 for v in per.values() if v * 1024 * 2 >= 0.98 * n]
+    return round(sum(full) / len(full)) if full else None
 
 
 def cpu_baseline(src, basis, B, dl, sample):
