@@ -2922,12 +2922,48 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const int64_t na = phase == 0 ? F.na_a : F.na, nflags = na < C ? na : C;
     const bool wide = (B % CHAIN_PPT) == 0 && B >= 512 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
     const ChainKeySet kset{s_ck, &s_ck_has0, &s_ck_full};
-    for (int i = t; i < 2 * CHAIN_CK_BUCKETS; i += CHAIN_THREADS) s_ck[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (t == 0) s_ck_has0 = s_ck_full = 0;
-    __syncthreads();
-    for (int64_t c = t; c < C; c += CHAIN_THREADS) chain_ck_insert(kset, (uint32_t)F.table_weak[c]);
-    __syncthreads();
     int64_t s = out->s, m = out->m;
+    // The key set (~C LDS inserts, tens of microseconds) only if the walk may search: a walk that starts aligned on
+    // an unbroken run of chain flags up to the last window with a chunk (an identical file, or its rest after the
+    // prefix) follows the chain and never looks a key up; should it need one after all, it stops there (the host).
+    bool kset_built = true;
+    if (s % B == 0 && nflags >= na) {
+        if (t == 0) s_zero = nflags;
+        __syncthreads();
+        // one 16-byte line of flags per lane per pass (as in step (1) below), masked to [s / B, nflags)
+        const int64_t k = s / B;
+        const uintptr_t fa = reinterpret_cast<uintptr_t>(F.flags);
+        for (uintptr_t l0 = (fa + (uintptr_t)k) & ~(uintptr_t)15; l0 < fa + (uintptr_t)nflags;
+             l0 += 16u * CHAIN_THREADS) {
+            const uintptr_t la = l0 + 16u * (uintptr_t)t;
+            const int64_t jb = (int64_t)la - (int64_t)fa;
+            if (la < fa + (uintptr_t)nflags) {
+                uint32_t w[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
+                if (la + 16 <= fa + (uintptr_t)nflags) {
+                    const uint4 q = *reinterpret_cast<const uint4*>(la);
+                    w[0] = q.x, w[1] = q.y, w[2] = q.z, w[3] = q.w;
+                } else {
+                    for (int i = 0; i < 16; ++i)
+                        if (jb + i >= 0 && jb + i < nflags && F.flags[jb + i] == 0) w[i >> 2] &= ~(0xFFu << (8 * (i & 3)));
+                }
+                int64_t z = -1;
+#pragma unroll
+                for (int i = 15; i >= 0; --i)
+                    if (jb + i >= k && jb + i < nflags && ((w[i >> 2] >> (8 * (i & 3))) & 0xFFu) == 0u) z = jb + i;
+                if (z >= 0) atomicMin((unsigned long long*)&s_zero, (unsigned long long)z);
+            }
+        }
+        __syncthreads();
+        kset_built = s_zero < nflags;  // (uniform) a break in the chain: the walk will search
+        __syncthreads();
+    }
+    if (kset_built) {
+        for (int i = t; i < 2 * CHAIN_CK_BUCKETS; i += CHAIN_THREADS) s_ck[i] = make_uint4(0u, 0u, 0u, 0u);
+        if (t == 0) s_ck_has0 = s_ck_full = 0;
+        __syncthreads();
+        for (int64_t c = t; c < C; c += CHAIN_THREADS) chain_ck_insert(kset, (uint32_t)F.table_weak[c]);
+        __syncthreads();
+    }
     int32_t pref = out->pref;
     int32_t nev = out->n_ev, status = CHAIN_STOP;
     int64_t lit = out->literal, mat = out->matched, chain_matches = out->chain_matches, events = out->events;
@@ -3040,6 +3076,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const int64_t f = (m + 10 * B <= n) ? m + 9 * B : INT64_MAX;
         const int64_t stop = f < last ? f : last;
         if (stop > nB) break;  // shrinking windows near the end: the host
+        // (see above: an unbroken chain needed no key set; should this step look a key up after all, the host takes
+        // it -- at the prefix's end the search is empty and the walk goes on to its cut, as with a key set)
+        if (!kset_built && (s / B < na || s <= (stop < na * B - 1 ? stop : na * B - 1))) break;
         int64_t p = -1;
         uint32_t key = 0;
         int64_t a = s;
