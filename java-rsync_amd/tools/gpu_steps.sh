@@ -18,6 +18,8 @@
 #   pmc-k1       one PMC pass over kbench: the production K1 against the same kernel without global loads
 #   kbench-k1    kbench: the K1 at B = 128 KiB and 8 KiB, the batched forms (1002, 1005, 1006)
 #   e2e          java-rsync_amd/tools/e2e.py at config 5 (16 GiB from host memory)
+#   config3      the config-3 line: a 64 GiB identical pair resident in HBM, B = 131072 (the Sender's limit), dl = 5
+#   receiver     the Receiver line (combineDataToFile on the config-2 shape)
 #   multi        bench.py --gpus 2 without a launcher (its own rank processes) on a one-GPU box: the N-rank path,
 #                ranks sharing the GPU (a rehearsal, not a scaling point); config 5 and config 4
 #   ab           AB_OPTS ("name=value ...") against the default, alternating, REPS times (AB_ARGS: bench args)
@@ -78,6 +80,9 @@ for step in "$@"; do
                 > "$O/multi_file.json" 2> "$O/multi_file.err"
             run 300 python bench.py --gpus 2 --workload files --steps 5 --warmup 2 --no-cpu-baseline --no-companions \
                 > "$O/multi_files.json" 2> "$O/multi_files.err" ;;
+        config3) run 300 python bench.py --size-gib 64 --digest 5 --steps 3 --warmup 1 --no-companions --no-cpu-baseline \
+            > "$O/config3.json" 2> "$O/config3.err" ;;
+        receiver) run 300 python bench.py --workload receiver --steps 2 --warmup 1 > "$O/receiver.json" 2> "$O/receiver.err" ;;
         e2e) run 400 python java-rsync_amd/tools/e2e.py --gib 16 > "$O/e2e_16GiB.json" 2> "$O/e2e.err" ;;
         ab)
             OPTS=""
