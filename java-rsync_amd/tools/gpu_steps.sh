@@ -16,6 +16,8 @@
 #   fetch        rocprofv3 --pmc FETCH_SIZE passes (counters only, kernel trace) of the default line and the config-4
 #                line: the HBM bytes per K1 launch that bench.py reports as roofline.traffic
 #   pmc-k1       one PMC pass over kbench: the production K1 against the same kernel without global loads
+#   pmc-walk     two PMC passes (SQ issue/wait/LDS counters) over one config-4 step (VARIANT): the chain walk's
+#                instruction mix and LDS bank conflicts
 #   kbench-k1    kbench: the K1 at B = 128 KiB and 8 KiB, the batched forms (1002, 1005, 1006)
 #   e2e          java-rsync_amd/tools/e2e.py at config 5 (16 GiB from host memory)
 #   config3      the config-3 line: a 64 GiB identical pair resident in HBM, B = 131072 (the Sender's limit), dl = 5
@@ -72,6 +74,16 @@ for step in "$@"; do
             run 120 "$K" 16384 131072 4 5 1000 58 > "$O/pmc_kbench.log" 2>&1
             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d "$O/pmc" -o run \
                 --output-format csv -- "$K" 16384 131072 4 3 1000 58 > "$O/pmc.log" 2>&1) || exit 1 ;;
+        pmc-walk)
+            # two PMC passes over one config-4 step (every kernel; the chain walk is chain_advance_kernel)
+            CA="SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"
+            CB="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES"
+            (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $CA --kernel-trace -d "$O/pmc_walk_a" -o run \
+                --output-format csv -- python3 "$R/bench.py" --workload files --variant "$VARIANT" --steps 1 --warmup 1 \
+                --no-cpu-baseline --no-companions > "$O/pmc_walk_a.json" 2> "$O/pmc_walk_a.err") || exit 1
+            (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $CB --kernel-trace -d "$O/pmc_walk_b" -o run \
+                --output-format csv -- python3 "$R/bench.py" --workload files --variant "$VARIANT" --steps 1 --warmup 1 \
+                --no-cpu-baseline --no-companions > "$O/pmc_walk_b.json" 2> "$O/pmc_walk_b.err") || exit 1 ;;
         kbench-k1)
             run 120 "$K" 16384 131072 4 8 1000 > "$O/kbench_128k.log" 2>&1
             run 120 "$K" 16384 8192 3 8 1000 1002 1005 1006 > "$O/kbench_8k.log" 2>&1 ;;
