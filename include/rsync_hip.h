@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RSH_ABI_VERSION 3
+#define RSH_ABI_VERSION 4
 
 /* Status codes (the JNI shim maps them onto the reference's exception types). */
 #define RSH_OK 0
@@ -231,6 +231,56 @@ int rsh_match_scan_pieces(rsh_ctx* ctx, const rsh_piece* pieces, int32_t npieces
                           const int32_t* weak, const uint8_t* strong, const uint8_t seed[4], rsh_event* ev,
                           int64_t ev_cap, int64_t* n_ev, uint8_t file_md5[16], int64_t* literal, int64_t* matched,
                           rsh_scan_stats* stats);
+
+/* ---- a segment's files from host memory (ABI 4) ----
+ * What a Java Generator / Sender holding a file-list segment in JVM buffers calls: Generator.itemizeSegment
+ * (Generator.java:558-614) sends every file's header + table (sendItemizeAndChecksums :866-909 per file), and
+ * Sender.sendFiles (Sender.java:1098-1148) answers each file in turn with sendMatchesAndData (:1235-1327), whose
+ * last 16 bytes are the whole-file MD5 (:1241,1326).  These forms take the whole segment in one call: each file
+ * is a list of caller-owned host pieces (as rsh_*_pieces), the bytes are copied to HBM (up to a budget of about
+ * 16 GiB per pass; a file larger than that goes through the tiled single-file path), every file's sums or scan
+ * run in the batched device forms above, and -- for the Sender -- every file's MD5 runs on the host's cores
+ * beside the copies and the scan, several files per core (rsh_file_md5_batch).  Per-file results equal the
+ * single-file calls'.  Returns RSH_OK, or the first failing job's status; every job's own status is in it
+ * (RSH_E_NOSPACE: ev_cap was short, n_ev holds the count needed and the file's events are not kept). */
+typedef struct {
+    const rsh_piece* pieces; /* the basis file: the concatenation of its pieces (npieces 0: an empty file) */
+    int32_t npieces;
+    int32_t status;          /* out */
+    rsh_header h;            /* 3-arg Checksum.Header of the file (as for rsh_block_sums) */
+    int32_t* weak_out;       /* host: chunk_count weak sums */
+    uint8_t* strong_out;     /* host: chunk_count * digest_length digest bytes */
+} rsh_block_batch_job;
+int rsh_block_sums_batch(rsh_ctx* ctx, rsh_block_batch_job* jobs, int32_t njobs, const uint8_t seed[4]);
+
+typedef struct {
+    const rsh_piece* pieces; /* the source file */
+    int32_t npieces;
+    int32_t status;          /* out */
+    rsh_header h;            /* the received header (validated as by rsh_match_scan) */
+    const int32_t* weak;     /* host: the received table */
+    const uint8_t* strong;
+    rsh_event* ev;           /* host, caller-owned: ev_cap entries */
+    int64_t ev_cap;
+    int64_t n_ev;            /* out */
+    int64_t literal;         /* out: sizeLiteral */
+    int64_t matched;         /* out: sizeMatch */
+    uint8_t file_md5[16];    /* out: MD5 of the whole source (Sender.java:1241,1326) */
+} rsh_scan_batch_job;
+/* stats (optional): summed over the files, as rsh_match_scan_batch_device's. */
+int rsh_match_scan_batch(rsh_ctx* ctx, rsh_scan_batch_job* jobs, int32_t njobs, const uint8_t seed[4],
+                         rsh_scan_stats* stats);
+
+/* Whole-file MD5s of many files (pure host; no context): md5[16] of each job = MD5 of its pieces'
+ * concatenation.  Independent files run side by side, up to 16 per core (AVX-512; 8 with AVX2), on `threads`
+ * threads (0 = the process's cores, cgroup quota included). */
+typedef struct {
+    const rsh_piece* pieces;
+    int32_t npieces;
+    int32_t reserved;
+    uint8_t md5[16];         /* out */
+} rsh_md5_job;
+int rsh_file_md5_batch(rsh_md5_job* jobs, int32_t njobs, int32_t threads);
 
 /* ---- Receiver (Receiver.java:459-555 combineDataToFile, :557-578 copies, :204-209 blockSize) ----
  * Replays one file's de-multiplexed token stream -- putInt(len)+bytes, putInt(-(i+1)), putInt(0), exactly

@@ -25,6 +25,29 @@
 
 namespace rsh {
 
+// The cores this process may use: its affinity mask, capped by a cgroup CPU quota (cgroup v2 cpu.max,
+// "quota period"; containers often see every CPU of the machine in the mask but get a few cores' worth of
+// time).  More spinning workers than that get throttled by the scheduler for whole periods.
+int host_cores() {
+    if (const int64_t o = opt(OPT_HOST_CORES); o > 0) return (int)o;  // explicit override (options.h)
+    static const int v = [] {
+        int n = 8;
+        cpu_set_t cpus;
+        if (sched_getaffinity(0, sizeof(cpus), &cpus) == 0) n = CPU_COUNT(&cpus);
+        if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+            char q[32] = {0};
+            long long period = 0;
+            if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+                const long long quota = atoll(q);
+                if (quota > 0) n = std::min<int>(n, (int)std::max<long long>(1, quota / period));
+            }
+            fclose(f);
+        }
+        return n;
+    }();
+    return v;
+}
+
 namespace {
 constexpr int32_t kMaxLive = 256;     // files resolved concurrently (one host thread each)
 constexpr int kDeferRounds = 2;       // rounds in head mode before the speculation is launched
@@ -210,6 +233,7 @@ struct FileScan {
     const uint8_t* d_strong = nullptr;
     int64_t n = 0, B = 0, na = 0, nf = 0;
     int64_t na_a = 0;  // two-phase chain walk: the windows of its prefix speculation (na: one phase)
+    int64_t lane_b_bytes = 0;  // bytes of its phase-1 lane chunks (they poll no abort word: they always run)
     const rsh_event* dev_ev = nullptr;  // a file the chain walk finished: its events, in the walk's pinned buffer
     int64_t dev_n = 0;
     int32_t C = 0, dl = 0;
@@ -261,29 +285,6 @@ struct Batch {
 };
 
 FileScan& scan_of(Batch* b, int32_t f) { return (*b->files)[(size_t)f]; }
-
-// The cores this process may use: its affinity mask, capped by a cgroup CPU quota (cgroup v2 cpu.max,
-// "quota period"; containers often see every CPU of the machine in the mask but get a few cores' worth of
-// time).  More spinning workers than that get throttled by the scheduler for whole periods.
-int host_cores() {
-    if (const int64_t o = opt(OPT_HOST_CORES); o > 0) return (int)o;  // explicit override (options.h)
-    static const int v = [] {
-        int n = 8;
-        cpu_set_t cpus;
-        if (sched_getaffinity(0, sizeof(cpus), &cpus) == 0) n = CPU_COUNT(&cpus);
-        if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
-            char q[32] = {0};
-            long long period = 0;
-            if (fscanf(f, "%31s %lld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
-                const long long quota = atoll(q);
-                if (quota > 0) n = std::min<int>(n, (int)std::max<long long>(1, quota / period));
-            }
-            fclose(f);
-        }
-        return n;
-    }();
-    return v;
-}
 
 int64_t BatchBackend::aligned_count() { return (head || !b->aligned.load(std::memory_order_acquire)) ? 0 : na; }
 
@@ -784,6 +785,12 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         ng_b = plan_block_sums_files(kb.data(), (int32_t)kb.size(), &plans_b, &lanes_b, &align_b, &partial_b);
         for (K1Plan& pl : plans_a) pl.abort = nullptr;  // the launch's word
         for (K1Plan& pl : plans_b) pl.abort = S->file_abort + b_file[(size_t)pl.file];
+        // phase 1's lane chunks have no abort word: they read their bytes even for a file whose walk ended in the
+        // prefix (the device-bytes stat counts them)
+        for (const K1Lane& ln : lanes_b) {
+            const int64_t lo = (int64_t)ln.c_first * ln.B, hi = std::min<int64_t>(ln.n, lo + (int64_t)ln.nchunks * ln.B);
+            files[(size_t)b_file[(size_t)ln.file]].lane_b_bytes += std::max<int64_t>(0, hi - lo);
+        }
     }
     RSH_BHIP(S->k1_groups.ensure(((size_t)std::max(ngroups, ng_a + ng_b) + 1) * sizeof(K1Group)));
     RSH_BHIP(S->k1_plans.ensure((std::max(plans.size(), plans_a.size() + plans_b.size()) + 1) * sizeof(K1Plan)));
@@ -1310,8 +1317,11 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                     const double dt = ms_since(tf);
                     b.busy_ms[(size_t)w] += dt;
                     b.max_fiber_ms[(size_t)w] = std::max(b.max_fiber_ms[(size_t)w], dt);
-                    any = any || !fs.done;
                 }
+                // the worker stays while any file it owns is not done -- including files parked on WAIT, which
+                // resume in a later round once the speculation lands (a worker whose live files all
+                // waited used to leave for good, and the coordinator spun on their pending requests)
+                for (int32_t i = w; i < NL && !any; i += W) any = !files[(size_t)live[(size_t)i]].done;
                 std::lock_guard<std::mutex> l(b.mu);
                 b.times[(size_t)w] = host_times();
                 if (!any) {  // all of its files are done: leave (the coordinator's rounds no longer count it)
@@ -1503,8 +1513,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             agg->flushes += s.flushes;
             agg->table_ms += s.table_ms + fs.table.sort_ms;
             int64_t spec_bytes = (spec_launched && b.landed.load() && !fs.cancelled) ? fs.n : 0;
-            if (spec_bytes > 0 && fs.be.na < fs.na)  // a two-phase file that stopped in its prefix (+ a short last chunk)
-                spec_bytes = std::min<int64_t>(fs.n, fs.be.na * fs.B) + fs.n % fs.B;
+            if (spec_bytes > 0 && fs.be.na < fs.na)  // a two-phase file that stopped in its prefix: the prefix K1,
+                spec_bytes = std::min<int64_t>(fs.n, fs.be.na * fs.B) + fs.lane_b_bytes;  // + phase 1's lane chunks
             agg->device_bytes += fs.be.bytes_read + spec_bytes;
             agg->phase_matches += s.phase_matches;
         }
@@ -1523,9 +1533,11 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
 
 using namespace rsh;
 
-extern "C" {
+namespace rsh {
 
-int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t njobs, const uint8_t seed[4]) {
+// rsh_block_sums_batch_device with the context already claimed by the caller (segment.cpp builds the host forms
+// on it).
+int block_sums_batch_claimed(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t njobs, const uint8_t seed[4]) {
     if (!ctx || !seed || njobs < 0 || (njobs > 0 && !jobs)) return RSH_E_INVAL;
     std::vector<K1File> files;
     for (int32_t i = 0; i < njobs; ++i) {
@@ -1539,7 +1551,6 @@ int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t
                                static_cast<uint8_t*>(j.d_strong)});
     }
     if (files.empty()) return RSH_OK;
-    RSH_CLAIM(ctx);
     BatchState* S = state_of(ctx);
     if (!S) return RSH_E_NOMEM;
     RSH_BHIP(hipSetDevice(ctx->device));
@@ -1577,8 +1588,9 @@ int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t
     return RSH_OK;
 }
 
-int rsh_match_scan_batch_device(rsh_ctx* ctx, rsh_scan_job* jobs, int32_t njobs, const uint8_t seed[4],
-                                rsh_scan_stats* stats) {
+// rsh_match_scan_batch_device with the context already claimed by the caller.
+int match_scan_batch_claimed(rsh_ctx* ctx, rsh_scan_job* jobs, int32_t njobs, const uint8_t seed[4],
+                             rsh_scan_stats* stats) {
     if (!ctx || !seed || njobs < 0 || (njobs > 0 && !jobs)) return RSH_E_INVAL;
     if (stats) *stats = rsh_scan_stats{};
     std::vector<int32_t> scan;
@@ -1615,7 +1627,6 @@ int rsh_match_scan_batch_device(rsh_ctx* ctx, rsh_scan_job* jobs, int32_t njobs,
         scan.push_back(i);
     }
     if (!scan.empty()) {
-        RSH_CLAIM(ctx);
         RSH_BHIP(hipSetDevice(ctx->device));
         for (size_t k = 0; k < scan.size(); k += kMaxLive) {
             const std::vector<int32_t> part(scan.begin() + (ptrdiff_t)k,
@@ -1630,6 +1641,23 @@ int rsh_match_scan_batch_device(rsh_ctx* ctx, rsh_scan_job* jobs, int32_t njobs,
     for (int32_t i = 0; i < njobs; ++i)
         if (jobs[i].status != RSH_OK) return jobs[i].status;
     return RSH_OK;
+}
+
+}  // namespace rsh
+
+extern "C" {
+
+int rsh_block_sums_batch_device(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t njobs, const uint8_t seed[4]) {
+    if (!ctx) return RSH_E_INVAL;
+    RSH_CLAIM(ctx);
+    return rsh::block_sums_batch_claimed(ctx, jobs, njobs, seed);
+}
+
+int rsh_match_scan_batch_device(rsh_ctx* ctx, rsh_scan_job* jobs, int32_t njobs, const uint8_t seed[4],
+                                rsh_scan_stats* stats) {
+    if (!ctx) return RSH_E_INVAL;
+    RSH_CLAIM(ctx);
+    return rsh::match_scan_batch_claimed(ctx, jobs, njobs, seed, stats);
 }
 
 }  // extern "C"

@@ -21,6 +21,13 @@
 namespace rsh {
 struct BatchState;  // batch.cpp
 void destroy_batch_state(BatchState* b);
+// batch.cpp: the cores this process may use (affinity mask, cgroup quota; option host_cores overrides)
+int host_cores();
+// batch.cpp: rsh_block_sums_batch_device / rsh_match_scan_batch_device for a caller that holds the context's
+// claim (segment.cpp's host-memory forms)
+int block_sums_batch_claimed(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t njobs, const uint8_t seed[4]);
+int match_scan_batch_claimed(rsh_ctx* ctx, rsh_scan_job* jobs, int32_t njobs, const uint8_t seed[4],
+                             rsh_scan_stats* stats);
 }  // namespace rsh
 
 namespace rshi {
@@ -111,6 +118,7 @@ struct rsh_ctx {
     DevBuf ph_weak[2], ph_strong[2];
     DevBuf segs;                                 // segmented K1 descriptors (prefix + phase speculation)
     DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw, partials, bucket;
+    DevBuf seg_data, seg_tab;                    // rsh_*_batch (segment.cpp): a pass's files and tables / sums
     hipStream_t aux = nullptr;                   // the aligned speculation
     hipStream_t phase = nullptr;                 // the phase-shifted speculation (beside a prefix speculation)
     hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr;
@@ -146,7 +154,7 @@ struct rsh_ctx {
         if (batch) rsh::destroy_batch_state(batch);
         for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &ph_weak[0], &ph_strong[0],
                           &ph_weak[1], &ph_strong[1], &slots, &dslots,
-                          &dkeys, &pos, &out, &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket})
+                          &dkeys, &pos, &out, &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket, &seg_data, &seg_tab})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pw[0], &h_ps[0], &h_pw[1], &h_ps[1], &h_lead, &h_pos, &h_out, &h_iv,
                              &h_tiles, &h_keys, &h_first, &h_win, &h_ptiles, &h_psegs, &h_hit, &h_win0, &h_pend, &h_bucket, &h_files,

@@ -43,6 +43,8 @@ enum Opt : int {
     OPT_FILE_TILE,         // rsh_match_scan_file: tile bytes above OPT_FILE_TILE_ABOVE
     OPT_FILE_TILE_ABOVE,   // rsh_match_scan_file: sources above this size are scanned tiled
     OPT_PROBE_LONG,        // 1: long probe intervals as pass-free segments (probe_long_kernel); 0: tiles only
+    OPT_SEGMENT_BYTES,     // rsh_*_batch (host memory): bytes of a segment's files copied to HBM per pass
+    OPT_MD5_WIDTH,         // rsh_file_md5_batch / rsh_match_scan_batch: 0 = widest multi-buffer MD5, 1/8/16 = forced
     OPT_COUNT
 };
 
@@ -60,7 +62,7 @@ inline const OptInfo* opt_info() {
         {"batch_spec", -1},        {"batch_spin_us", 200},    {"batch_readahead", 0},  {"batch_prep_all", 0},
         {"batch_chain", 1},        {"batch_chain_prefix", -1}, {"batch_chain_overlap", 0},
         {"host_cores", 0},         {"file_tile", 4LL << 30}, {"file_tile_above", 32LL << 30},
-        {"probe_long", 1},
+        {"probe_long", 1},         {"segment_bytes", 16LL << 30}, {"md5_width", 0},
     };
     return t;
 }

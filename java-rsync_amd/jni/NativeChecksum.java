@@ -174,6 +174,93 @@ final class NativeChecksum implements AutoCloseable {
     }
 
     /**
+     * A segment's Generator pass in one call (Generator.itemizeSegment, Generator.java:558-614): basis[f] holds
+     * file f's bytes in one or more direct buffers, headers[f] its 3-arg Checksum.Header; weak[f] / strong[f]
+     * receive its sums.  One device launch covers every file of the segment.
+     */
+    void blockSumsSegment(ByteBuffer[][] basis, long[] sizes, Checksum.Header[] headers, byte[] seed, int[][] weak,
+            byte[][] strong) {
+        Segment s = new Segment(basis, headers);
+        lock.lock();
+        try {
+            blockSumsBatch(handle(), s.buffers, s.filePieces, sizes, s.headers, seed, weak, strong);
+        } finally {
+            lock.unlock();
+        }
+    }
+
+    /**
+     * A segment's Sender pass in one call (Sender.sendFiles, Sender.java:1098-1148): returns, per file, its
+     * events as {kind, offset, length, index | count << 32} quadruples (the caller replays each file's as
+     * matchScan's, Sender.java:794-809 / 1274 / 1316); fileMd5[f] and sizes[f] = {sizeLiteral, sizeMatch}.
+     * The files' MD5s run on the host's cores beside the device work.
+     */
+    long[][] matchScanSegment(ByteBuffer[][] source, long[] fileSizes, Checksum.Header[] headers, int[][] weak,
+            byte[][] strong, byte[] seed, byte[][] fileMd5, long[][] sizes) {
+        Segment s = new Segment(source, headers);
+        int nf = headers.length;
+        byte[] md5 = new byte[16 * nf];
+        long[] per = new long[3 * nf];
+        long[] flat;
+        lock.lock();
+        try {
+            flat = matchScanBatch(handle(), s.buffers, s.filePieces, fileSizes, s.headers, weak, strong, seed, md5,
+                    per);
+        } finally {
+            lock.unlock();
+        }
+        long[][] events = new long[nf][];
+        int at = 0;
+        for (int f = 0; f < nf; f++) {
+            int len = (int) (4 * per[3 * f]);
+            events[f] = java.util.Arrays.copyOfRange(flat, at, at + len);
+            at += len;
+            System.arraycopy(md5, 16 * f, fileMd5[f], 0, 16);
+            sizes[f][0] = per[3 * f + 1];
+            sizes[f][1] = per[3 * f + 2];
+        }
+        return events;
+    }
+
+    /** One file's precomputed table (the Generator's segment hook, INTEGRATION.md). */
+    static final class Sums {
+        final Checksum.Header header;
+        final int[] weak;
+        final byte[] strong;
+
+        Sums(Checksum.Header header, int[] weak, byte[] strong) {
+            this.header = header;
+            this.weak = weak;
+            this.strong = strong;
+        }
+    }
+
+    /** The flat argument form of a segment: every file's buffers in order, the count per file, 4 ints per header. */
+    private static final class Segment {
+        final ByteBuffer[] buffers;
+        final int[] filePieces;
+        final int[] headers;
+
+        Segment(ByteBuffer[][] files, Checksum.Header[] hs) {
+            int total = 0;
+            for (ByteBuffer[] f : files) {
+                total += f.length;
+            }
+            buffers = new ByteBuffer[total];
+            filePieces = new int[files.length];
+            headers = new int[4 * hs.length];
+            int b = 0;
+            for (int f = 0; f < files.length; f++) {
+                filePieces[f] = files[f].length;
+                for (ByteBuffer x : files[f]) {
+                    buffers[b++] = x;
+                }
+                System.arraycopy(toArray(hs[f]), 0, headers, 4 * f, 4);
+            }
+        }
+    }
+
+    /**
      * Receiver.combineDataToFile (Receiver.java:459-555): result = {tokensUsed, targetLength, sizeLiteral,
      * sizeMatch}; returns true when the deferred write left the replica as the file.
      */
@@ -217,6 +304,12 @@ final class NativeChecksum implements AutoCloseable {
 
     static native long[] matchScanFile(long ctx, String path, long size, int[] header, int[] weak, byte[] strong,
             byte[] seed, byte[] fileMd5Out, long[] sizesOut);
+
+    static native void blockSumsBatch(long ctx, ByteBuffer[] data, int[] filePieces, long[] sizes, int[] headers,
+            byte[] seed, int[][] weakOut, byte[][] strongOut);
+
+    static native long[] matchScanBatch(long ctx, ByteBuffer[] src, int[] filePieces, long[] sizes, int[] headers,
+            int[][] weak, byte[][] strong, byte[] seed, byte[] fileMd5Out, long[] perFileOut);
 
     static native boolean receiverCombine(long ctx, ByteBuffer tokens, long tokensLen, int[] header,
             ByteBuffer replica, long replicaLen, boolean deferWrite, ByteBuffer target, long targetCap,

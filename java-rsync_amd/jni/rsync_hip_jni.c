@@ -22,7 +22,9 @@
  *   blockSumsBuffers / matchScanBuffers  an array of direct ByteBuffers, the file being their concatenation
  *                                      (any size; FileView streams any file, FileView.java:235-278);
  *   blockSumsFile / matchScanFile      a path: the library reads the file with FileView's semantics and
- *                                      reports a read error as a flag (the FileViewException of close()).
+ *                                      reports a read error as a flag (the FileViewException of close());
+ *   blockSumsBatch / matchScanBatch    a whole file-list segment in one call (Generator.itemizeSegment,
+ *                                      Sender.sendFiles): every file's pieces, header and table at once.
  * The Sender replays the returned events through its own sendDataFrom/putInt so channel framing is
  * untouched (Sender.java:794-809); INTEGRATION.md shows the replay for each form.
  *
@@ -31,6 +33,7 @@
 #include <jni.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 
 #include "rsync_hip.h"
@@ -456,6 +459,283 @@ JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeC
     jlongArray out = run_scan(env, c, cpath, size, &h, weak, strong, s4, md5, &lit, &mat, scan_file, &a);
     (*env)->ReleaseStringUTFChars(env, path, cpath);
     if (out) sizes_out(env, sizesOut, fileMd5Out, md5, lit, mat, 1, a.read_error);
+    return out;
+}
+
+/* ---- a segment's files in one call (rsh_block_sums_batch / rsh_match_scan_batch) ----
+ * Generator.itemizeSegment (Generator.java:558-614) and Sender.sendFiles (Sender.java:1098-1148) walk a
+ * segment's files one by one; these natives take them all: data holds every file's direct buffers in file order,
+ * filePieces[f] of them for file f (each full to its capacity but the file's last, which is cut at sizes[f]),
+ * hdrs four ints per file in Connection.sendChecksumHeader order.  A failing file throws its exception, naming
+ * the file; the reference would have thrown it from that file's call. */
+
+typedef struct {
+    rsh_piece* pieces; /* all files' pieces */
+    int32_t* first;    /* file f: pieces[first[f] .. first[f] + count[f]) */
+    int32_t* count;
+    rsh_header* h;
+    jint nf;
+} segment_args;
+
+static void segment_free(segment_args* a) {
+    free(a->pieces);
+    free(a->first);
+    free(a->count);
+    free(a->h);
+}
+
+/* Splits `bufs` into the files' piece lists and reads their headers; RSH_OK, or an exception thrown. */
+static int segment_from(JNIEnv* env, jobjectArray bufs, jintArray filePieces, jlongArray sizes, jintArray hdrs,
+                        segment_args* a) {
+    memset(a, 0, sizeof(*a));
+    const jsize nb = bufs ? (*env)->GetArrayLength(env, bufs) : 0;
+    const jint nf = filePieces ? (*env)->GetArrayLength(env, filePieces) : -1;
+    if (nf < 0 || !sizes || !hdrs || (*env)->GetArrayLength(env, sizes) < nf ||
+        (*env)->GetArrayLength(env, hdrs) < 4 * (jlong)nf) {
+        throw_status(env, RSH_E_INVAL);
+        return RSH_E_INVAL;
+    }
+    a->nf = nf;
+    a->pieces = (rsh_piece*)malloc(sizeof(rsh_piece) * (size_t)(nb + 1));
+    a->first = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nf + 1));
+    a->count = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nf + 1));
+    a->h = (rsh_header*)malloc(sizeof(rsh_header) * (size_t)(nf + 1));
+    jint* fp = (jint*)malloc(sizeof(jint) * (size_t)(nf + 1));
+    jlong* sz = (jlong*)malloc(sizeof(jlong) * (size_t)(nf + 1));
+    jint* hv = (jint*)malloc(sizeof(jint) * (size_t)(4 * nf + 1));
+    int rc = (a->pieces && a->first && a->count && a->h && fp && sz && hv) ? RSH_OK : RSH_E_NOMEM;
+    if (rc == RSH_OK && nf > 0) {
+        (*env)->GetIntArrayRegion(env, filePieces, 0, nf, fp);
+        (*env)->GetLongArrayRegion(env, sizes, 0, nf, sz);
+        (*env)->GetIntArrayRegion(env, hdrs, 0, 4 * nf, hv);
+    }
+    const char* why = NULL;
+    jsize b = 0;
+    for (jint f = 0; rc == RSH_OK && f < nf; ++f) {
+        a->h[f].chunk_count = hv[4 * f];
+        a->h[f].block_length = hv[4 * f + 1];
+        a->h[f].digest_length = hv[4 * f + 2];
+        a->h[f].remainder = hv[4 * f + 3];
+        if (fp[f] < 0 || sz[f] < 0 || (jlong)b + fp[f] > nb) {
+            rc = RSH_E_INVAL;
+            why = "file piece counts or sizes do not match the buffers";
+            break;
+        }
+        a->first[f] = (int32_t)b;
+        a->count[f] = 0;
+        jlong left = sz[f];
+        for (jint k = 0; k < fp[f]; ++k, ++b) {
+            jobject o = (*env)->GetObjectArrayElement(env, bufs, b);
+            const uint8_t* p = o ? (const uint8_t*)(*env)->GetDirectBufferAddress(env, o) : NULL;
+            const jlong cap = o ? (*env)->GetDirectBufferCapacity(env, o) : -1;
+            if (o) (*env)->DeleteLocalRef(env, o);
+            if (!p || cap < 0) {
+                rc = RSH_E_INVAL;
+                why = "piece is not a direct ByteBuffer";
+                break;
+            }
+            rsh_piece* pc = &a->pieces[a->first[f] + a->count[f]++];
+            pc->data = p;
+            pc->len = cap < left ? cap : left;
+            left -= pc->len;
+        }
+        if (rc == RSH_OK && left > 0) {
+            rc = RSH_E_INVAL;
+            why = "a file's buffers hold fewer bytes than its size";
+        }
+    }
+    free(fp);
+    free(sz);
+    free(hv);
+    if (rc != RSH_OK) {
+        segment_free(a);
+        if (why) throw_class(env, "java/lang/IllegalArgumentException", why);
+        else throw_status(env, rc);
+    }
+    return rc;
+}
+
+/* The exception of file f's status, the message naming the file. */
+static void throw_file_status(JNIEnv* env, jint f, int rc) {
+    char msg[160];
+    snprintf(msg, sizeof(msg), "segment file %d: %s", (int)f, rsh_strerror(rc));
+    const char* cls;
+    switch (rc) {
+        case RSH_E_PROTOCOL: cls = "com/github/java/rsync/RsyncProtocolException"; break;
+        case RSH_E_OVERFLOW: cls = "com/github/java/rsync/internal/session/Checksum$ChunkOverflow"; break;
+        case RSH_E_INVAL: cls = "java/lang/IllegalArgumentException"; break;
+        case RSH_E_NOMEM: cls = "java/lang/OutOfMemoryError"; break;
+        default: cls = "java/lang/IllegalStateException"; break;
+    }
+    throw_class(env, cls, msg);
+}
+
+/* weakOut[f] (int[chunkCount]) and strongOut[f] (byte[chunkCount * digestLength]) receive file f's sums. */
+JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_blockSumsBatch(
+    JNIEnv* env, jclass cls, jlong ctx, jobjectArray data, jintArray filePieces, jlongArray sizes, jintArray hdrs,
+    jbyteArray seed, jobjectArray weakOut, jobjectArray strongOut) {
+    (void)cls;
+    rsh_ctx* c = ctx_of(env, ctx);
+    if (!c) return;
+    jbyte s4[4];
+    if (seed_from(env, seed, s4) != RSH_OK) {
+        throw_status(env, RSH_E_INVAL);
+        return;
+    }
+    segment_args a;
+    if (segment_from(env, data, filePieces, sizes, hdrs, &a) != RSH_OK) return;
+    const jint nf = a.nf;
+    int rc = RSH_OK;
+    if (!weakOut || !strongOut || (*env)->GetArrayLength(env, weakOut) < nf ||
+        (*env)->GetArrayLength(env, strongOut) < nf)
+        rc = RSH_E_INVAL;
+    rsh_block_batch_job* jobs = (rsh_block_batch_job*)calloc((size_t)nf + 1, sizeof(rsh_block_batch_job));
+    jobject* wo = (jobject*)calloc((size_t)nf + 1, sizeof(jobject));
+    jobject* so = (jobject*)calloc((size_t)nf + 1, sizeof(jobject));
+    if (rc == RSH_OK && (!jobs || !wo || !so)) rc = RSH_E_NOMEM;
+    for (jint f = 0; rc == RSH_OK && f < nf; ++f) {
+        wo[f] = (*env)->GetObjectArrayElement(env, weakOut, f);
+        so[f] = (*env)->GetObjectArrayElement(env, strongOut, f);
+        if (sums_out_ok(env, &a.h[f], (jintArray)wo[f], (jbyteArray)so[f]) != RSH_OK) {
+            rc = RSH_E_INVAL;
+            break;
+        }
+        const size_t C = (size_t)a.h[f].chunk_count, dl = (size_t)a.h[f].digest_length;
+        jobs[f].pieces = a.pieces + a.first[f];
+        jobs[f].npieces = a.count[f];
+        jobs[f].h = a.h[f];
+        jobs[f].weak_out = (int32_t*)malloc(C * 4 + 4);
+        jobs[f].strong_out = (uint8_t*)malloc(C * dl + 1);
+        if (!jobs[f].weak_out || !jobs[f].strong_out) rc = RSH_E_NOMEM;
+    }
+    if (rc == RSH_OK) {
+        rc = rsh_block_sums_batch(c, jobs, nf, (const uint8_t*)s4);
+        if (rc != RSH_OK) {
+            for (jint f = 0; f < nf; ++f)
+                if (jobs[f].status != RSH_OK) {
+                    throw_file_status(env, f, jobs[f].status);
+                    break;
+                }
+        } else {
+            for (jint f = 0; f < nf; ++f) {
+                const jsize C = a.h[f].chunk_count;
+                (*env)->SetIntArrayRegion(env, (jintArray)wo[f], 0, C, (const jint*)jobs[f].weak_out);
+                (*env)->SetByteArrayRegion(env, (jbyteArray)so[f], 0, (jsize)((jlong)C * a.h[f].digest_length),
+                                           (const jbyte*)jobs[f].strong_out);
+            }
+        }
+    } else {
+        throw_status(env, rc);
+    }
+    for (jint f = 0; jobs && f < nf; ++f) {
+        free(jobs[f].weak_out);
+        free(jobs[f].strong_out);
+        if (wo && wo[f]) (*env)->DeleteLocalRef(env, wo[f]);
+        if (so && so[f]) (*env)->DeleteLocalRef(env, so[f]);
+    }
+    free(jobs);
+    free(wo);
+    free(so);
+    segment_free(&a);
+}
+
+/* An event buffer no scan of n bytes overflows: each MATCH but the last consumes a full window, each LITERAL
+ * precedes a MATCH or ends a 10*B flush interval (Sender.java:1251-1316). */
+static int64_t event_bound(int64_t n, const rsh_header* h) {
+    if (h->block_length <= 0) return n / 8192 + 2;
+    return 2 * (n / h->block_length + 1) + n / (10 * (int64_t)h->block_length) + 4;
+}
+
+/* Returns every file's events, file after file, as {kind, offset, length, index | (count << 32)} quadruples;
+ * perFileOut[3f..3f+2] = {event count, sizeLiteral, sizeMatch}, fileMd5Out[16f..16f+15] = file f's MD5. */
+JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_matchScanBatch(
+    JNIEnv* env, jclass cls, jlong ctx, jobjectArray src, jintArray filePieces, jlongArray sizes, jintArray hdrs,
+    jobjectArray weak, jobjectArray strong, jbyteArray seed, jbyteArray fileMd5Out, jlongArray perFileOut) {
+    (void)cls;
+    rsh_ctx* c = ctx_of(env, ctx);
+    if (!c) return NULL;
+    jbyte s4[4];
+    if (seed_from(env, seed, s4) != RSH_OK) {
+        throw_status(env, RSH_E_INVAL);
+        return NULL;
+    }
+    segment_args a;
+    if (segment_from(env, src, filePieces, sizes, hdrs, &a) != RSH_OK) return NULL;
+    const jint nf = a.nf;
+    int rc = RSH_OK;
+    if (!weak || !strong || !fileMd5Out || !perFileOut || (*env)->GetArrayLength(env, weak) < nf ||
+        (*env)->GetArrayLength(env, strong) < nf || (*env)->GetArrayLength(env, fileMd5Out) < 16 * (jlong)nf ||
+        (*env)->GetArrayLength(env, perFileOut) < 3 * (jlong)nf)
+        rc = RSH_E_INVAL;
+    rsh_scan_batch_job* jobs = (rsh_scan_batch_job*)calloc((size_t)nf + 1, sizeof(rsh_scan_batch_job));
+    if (rc == RSH_OK && !jobs) rc = RSH_E_NOMEM;
+    for (jint f = 0; rc == RSH_OK && f < nf; ++f) {
+        jobject wa = (*env)->GetObjectArrayElement(env, weak, f);
+        jobject sa = (*env)->GetObjectArrayElement(env, strong, f);
+        const jsize nw = wa ? (*env)->GetArrayLength(env, wa) : 0, ns = sa ? (*env)->GetArrayLength(env, sa) : 0;
+        const rsh_header* h = &a.h[f];
+        if (h->chunk_count > 0 && (nw < h->chunk_count || (jlong)ns < (jlong)h->chunk_count * h->digest_length))
+            rc = RSH_E_INVAL; /* received table shorter than its header says */
+        int64_t n = 0;
+        for (int32_t k = 0; k < a.count[f]; ++k) n += a.pieces[a.first[f] + k].len;
+        jobs[f].pieces = a.pieces + a.first[f];
+        jobs[f].npieces = a.count[f];
+        jobs[f].h = *h;
+        jobs[f].ev_cap = event_bound(n, h);
+        jobs[f].ev = (rsh_event*)malloc((size_t)jobs[f].ev_cap * sizeof(rsh_event));
+        int32_t* w = (int32_t*)malloc((size_t)nw * 4 + 4);
+        uint8_t* st = (uint8_t*)malloc((size_t)ns + 1);
+        jobs[f].weak = w;
+        jobs[f].strong = st;
+        if (rc == RSH_OK && (!jobs[f].ev || !w || !st)) rc = RSH_E_NOMEM;
+        if (rc == RSH_OK && nw) (*env)->GetIntArrayRegion(env, wa, 0, nw, (jint*)w);
+        if (rc == RSH_OK && ns) (*env)->GetByteArrayRegion(env, sa, 0, ns, (jbyte*)st);
+        if (wa) (*env)->DeleteLocalRef(env, wa);
+        if (sa) (*env)->DeleteLocalRef(env, sa);
+    }
+    jlongArray out = NULL;
+    if (rc == RSH_OK) {
+        rc = rsh_match_scan_batch(c, jobs, nf, (const uint8_t*)s4, NULL);
+        if (rc != RSH_OK) {
+            for (jint f = 0; f < nf; ++f)
+                if (jobs[f].status != RSH_OK) {
+                    throw_file_status(env, f, jobs[f].status);
+                    break;
+                }
+        } else {
+            int64_t total = 0;
+            for (jint f = 0; f < nf; ++f) total += jobs[f].n_ev;
+            out = (*env)->NewLongArray(env, (jsize)(4 * total));
+            jlong* o = out ? (*env)->GetLongArrayElements(env, out, NULL) : NULL;
+            if (o) {
+                int64_t q = 0;
+                for (jint f = 0; f < nf; ++f) {
+                    const rsh_event* ev = jobs[f].ev;
+                    for (int64_t i = 0; i < jobs[f].n_ev; ++i, ++q) {
+                        o[4 * q + 0] = ev[i].kind;
+                        o[4 * q + 1] = ev[i].offset;
+                        o[4 * q + 2] = ev[i].length;
+                        o[4 * q + 3] = (jlong)(uint32_t)ev[i].index | ((jlong)ev[i].count << 32);
+                    }
+                    const jlong per[3] = {jobs[f].n_ev, jobs[f].literal, jobs[f].matched};
+                    (*env)->SetLongArrayRegion(env, perFileOut, 3 * f, 3, per);
+                    (*env)->SetByteArrayRegion(env, fileMd5Out, 16 * f, 16, (const jbyte*)jobs[f].file_md5);
+                }
+                (*env)->ReleaseLongArrayElements(env, out, o, 0);
+            } else {
+                out = NULL; /* OutOfMemoryError pending */
+            }
+        }
+    } else {
+        throw_status(env, rc);
+    }
+    for (jint f = 0; jobs && f < nf; ++f) {
+        free(jobs[f].ev);
+        free((void*)jobs[f].weak);
+        free((void*)jobs[f].strong);
+    }
+    free(jobs);
+    segment_free(&a);
     return out;
 }
 

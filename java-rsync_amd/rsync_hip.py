@@ -104,6 +104,26 @@ class Piece(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_int64)]
 
 
+class BlockBatchJob(ctypes.Structure):
+    """rsh_block_batch_job: one basis file of a segment's Generator pass from host memory (rsh_block_sums_batch)."""
+    _fields_ = [("pieces", ctypes.POINTER(Piece)), ("npieces", ctypes.c_int32), ("status", ctypes.c_int32),
+                ("h", Header), ("weak_out", ctypes.c_void_p), ("strong_out", ctypes.c_void_p)]
+
+
+class ScanBatchJob(ctypes.Structure):
+    """rsh_scan_batch_job: one source file of a segment's Sender pass from host memory (rsh_match_scan_batch)."""
+    _fields_ = [("pieces", ctypes.POINTER(Piece)), ("npieces", ctypes.c_int32), ("status", ctypes.c_int32),
+                ("h", Header), ("weak", ctypes.c_void_p), ("strong", ctypes.c_void_p), ("ev", ctypes.c_void_p),
+                ("ev_cap", ctypes.c_int64), ("n_ev", ctypes.c_int64), ("literal", ctypes.c_int64),
+                ("matched", ctypes.c_int64), ("file_md5", ctypes.c_uint8 * 16)]
+
+
+class Md5Job(ctypes.Structure):
+    """rsh_md5_job: one file of rsh_file_md5_batch."""
+    _fields_ = [("pieces", ctypes.POINTER(Piece)), ("npieces", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("md5", ctypes.c_uint8 * 16)]
+
+
 EVENT_DTYPE = np.dtype([("offset", "<i8"), ("length", "<i8"), ("kind", "<i4"), ("index", "<i4"),
                         ("count", "<i4"), ("reserved", "<i4")])
 
@@ -113,7 +133,7 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_coun
            "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
            "rsh_match_scan_device", "rsh_match_scan_tiled", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
            "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_receiver_combine",
-           "rsh_receiver_combine_device", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
+           "rsh_receiver_combine_device", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_block_sums_batch", "rsh_match_scan_batch", "rsh_file_md5_batch", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 # include/rsync_hip_debug.h (testing / diagnostics ABI)
 DEBUG_EXPORTS = ["rsh_debug_set_option", "rsh_debug_get_option", "rsh_debug_reset_options"]
 
@@ -194,6 +214,9 @@ def lib():
         "rsh_block_sums_pieces": ([P, ctypes.POINTER(Piece), I32, HP, P, P, P], ctypes.c_int),
         "rsh_match_scan_pieces": ([P, ctypes.POINTER(Piece), I32, HP, P, P, P, P, I64, ctypes.POINTER(I64), P,
                                    ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(ScanStats)], ctypes.c_int),
+        "rsh_block_sums_batch": ([P, ctypes.POINTER(BlockBatchJob), I32, P], ctypes.c_int),
+        "rsh_match_scan_batch": ([P, ctypes.POINTER(ScanBatchJob), I32, P, ctypes.POINTER(ScanStats)], ctypes.c_int),
+        "rsh_file_md5_batch": ([ctypes.POINTER(Md5Job), I32, I32], ctypes.c_int),
         "rsh_dev_alloc": ([P, I64, ctypes.POINTER(P)], ctypes.c_int),
         "rsh_dev_free": ([P, P], ctypes.c_int),
         "rsh_memcpy_h2d": ([P, P, P, I64], ctypes.c_int),
@@ -266,6 +289,33 @@ def file_md5(data):
     out = np.zeros(16, np.uint8)
     _check(lib().rsh_file_md5(_ptr(a), a.size, _ptr(out)))
     return out.tobytes()
+
+
+def _piece_list(pieces):
+    arrs = [_u8(p) for p in pieces]
+    pl = (Piece * max(len(arrs), 1))()
+    for i, a in enumerate(arrs):
+        pl[i].data, pl[i].len = (a.ctypes.data if a.size else None), a.size
+    return arrs, pl, sum(a.size for a in arrs)
+
+
+def file_md5_batch(files, threads=0):
+    """Whole-file MD5 of each file (a list of pieces each; rsh_file_md5_batch): several files per core."""
+    keep, jobs = [], (Md5Job * max(len(files), 1))()
+    for i, pieces in enumerate(files):
+        arrs, pl, _ = _piece_list(pieces)
+        keep.append((arrs, pl))
+        jobs[i].pieces, jobs[i].npieces = ctypes.cast(pl, ctypes.POINTER(Piece)), len(arrs)
+    _check(lib().rsh_file_md5_batch(jobs, len(files), threads))
+    return [bytes(jobs[i].md5) for i in range(len(files))]
+
+
+def scan_event_cap(n, h):
+    """An event buffer no scan of n source bytes can overflow: every MATCH consumes a window of B bytes but
+    possibly the last, every LITERAL but the last precedes a MATCH or ends a 10*B flush interval."""
+    if h.block_length <= 0:
+        return n // 8192 + 2
+    return 2 * (n // h.block_length + 1) + n // (10 * h.block_length) + 4
 
 
 def events_as_tuples(ev, block_length):
@@ -421,11 +471,54 @@ class Context:
 
     @staticmethod
     def _pieces(pieces):
-        arrs = [_u8(p) for p in pieces]
-        pl = (Piece * max(len(arrs), 1))()
-        for i, a in enumerate(arrs):
-            pl[i].data, pl[i].len = (a.ctypes.data if a.size else None), a.size
-        return arrs, pl, sum(a.size for a in arrs)
+        return _piece_list(pieces)
+
+    def block_sums_batch(self, files, seed):
+        """A segment's Generator pass from host memory (rsh_block_sums_batch; Generator.itemizeSegment):
+        files = [(pieces, Header)] -> [(weak, strong)] per file."""
+        s = np.frombuffer(bytes(seed), np.uint8).copy()
+        jobs = (BlockBatchJob * max(len(files), 1))()
+        keep, outs = [], []
+        for i, (pieces, h) in enumerate(files):
+            arrs, pl, _ = _piece_list(pieces)
+            w = np.zeros(max(h.chunk_count, 1), np.int32)
+            st = np.zeros(max(h.chunk_count * h.digest_length, 1), np.uint8)
+            keep.append((arrs, pl))
+            outs.append((w, st, h))
+            jobs[i].pieces, jobs[i].npieces, jobs[i].h = ctypes.cast(pl, ctypes.POINTER(Piece)), len(arrs), h
+            jobs[i].weak_out, jobs[i].strong_out = w.ctypes.data, st.ctypes.data
+        _check(lib().rsh_block_sums_batch(self._p, jobs, len(files), _ptr(s)))
+        return [(w[:h.chunk_count], st[:h.chunk_count * h.digest_length]) for w, st, h in outs]
+
+    def match_scan_batch(self, files, seed, ev_caps=None):
+        """A segment's Sender pass from host memory (rsh_match_scan_batch; Sender.sendFiles):
+        files = [(pieces, Header, weak, strong)] -> ([(events, file_md5, literal, matched, status)], stats).
+        A file's status is RSH_E_NOSPACE when its ev_caps entry was short (its events are then not kept)."""
+        s = np.frombuffer(bytes(seed), np.uint8).copy()
+        jobs = (ScanBatchJob * max(len(files), 1))()
+        keep, evs = [], []
+        for i, (pieces, h, weak, strong) in enumerate(files):
+            arrs, pl, n = _piece_list(pieces)
+            w = np.ascontiguousarray(weak, dtype=np.int32)
+            st = np.ascontiguousarray(strong, dtype=np.uint8)
+            cap = ev_caps[i] if ev_caps is not None else scan_event_cap(n, h)
+            ev = np.zeros(max(cap, 1), EVENT_DTYPE)
+            keep.append((arrs, pl, w, st))
+            evs.append(ev)
+            j = jobs[i]
+            j.pieces, j.npieces, j.h = ctypes.cast(pl, ctypes.POINTER(Piece)), len(arrs), h
+            j.weak, j.strong = (w.ctypes.data if w.size else None), (st.ctypes.data if st.size else None)
+            j.ev, j.ev_cap = ev.ctypes.data, cap
+        stats = ScanStats()
+        rc = lib().rsh_match_scan_batch(self._p, jobs, len(files), _ptr(s), ctypes.byref(stats))
+        if rc != RSH_E_NOSPACE:
+            _check(rc)
+        out = []
+        for i in range(len(files)):
+            j = jobs[i]
+            ev = evs[i][:j.n_ev] if j.status == RSH_OK else evs[i][:0]
+            out.append((ev, bytes(j.file_md5), j.literal, j.matched, j.status))
+        return out, stats.as_dict()
 
     def block_sums_pieces(self, pieces, h, seed):
         """As block_sums over the concatenation of `pieces` (host buffers; rsh_block_sums_pieces)."""

@@ -90,6 +90,10 @@ static void f_SetLongArrayRegion(JNIEnv* env, jlongArray a, jsize s, jsize l, co
     (void)env;
     if (in_bounds(a, s, l)) memcpy((jlong*)a->data + s, buf, (size_t)l * 8);
 }
+static void f_GetLongArrayRegion(JNIEnv* env, jlongArray a, jsize s, jsize l, jlong* buf) {
+    (void)env;
+    if (in_bounds(a, s, l)) memcpy(buf, (jlong*)a->data + s, (size_t)l * 8);
+}
 static jlongArray f_NewLongArray(JNIEnv* env, jsize len) {
     (void)env;
     fobj* o = (fobj*)calloc(1, sizeof(fobj));
@@ -124,7 +128,7 @@ static const struct JNINativeInterface_ g_fns = {
     f_FindClass, f_ThrowNew, f_DeleteLocalRef, f_GetDirectBufferAddress, f_GetDirectBufferCapacity, f_GetArrayLength,
     f_GetObjectArrayElement, f_GetIntArrayRegion, f_SetIntArrayRegion, f_GetByteArrayRegion, f_SetByteArrayRegion,
     f_SetLongArrayRegion, f_NewLongArray, f_GetLongArrayElements, f_ReleaseLongArrayElements, f_GetStringUTFChars,
-    f_ReleaseStringUTFChars,
+    f_ReleaseStringUTFChars, f_GetLongArrayRegion,
 };
 static JNIEnv g_env = &g_fns;
 
@@ -138,6 +142,10 @@ jlongArray NC(matchScan)(JNIEnv*, jclass, jlong, jobject, jlong, jintArray, jint
                          jbyteArray, jlongArray);
 jlongArray NC(matchScanBuffers)(JNIEnv*, jclass, jlong, jobjectArray, jlong, jintArray, jintArray, jbyteArray,
                                 jbyteArray, jbyteArray, jlongArray);
+void NC(blockSumsBatch)(JNIEnv*, jclass, jlong, jobjectArray, jintArray, jlongArray, jintArray, jbyteArray,
+                        jobjectArray, jobjectArray);
+jlongArray NC(matchScanBatch)(JNIEnv*, jclass, jlong, jobjectArray, jintArray, jlongArray, jintArray, jobjectArray,
+                              jobjectArray, jbyteArray, jbyteArray, jlongArray);
 jboolean NC(receiverCombine)(JNIEnv*, jclass, jlong, jobject, jlong, jintArray, jobject, jlong, jboolean, jobject, jlong,
                              jlongArray, jbyteArray);
 
@@ -261,4 +269,77 @@ JNIEXPORT int jh_receiver_combine(jlong ctx, void* tokens, jlong tok_cap, jlong 
     OBJ(m, K_BYTE, md5, 16);
     return NC(receiverCombine)(&g_env, NULL, ctx, t, tokens_len, h, r, replica_len, (jboolean)defer, o, target_cap,
                                res, m);
+}
+
+/* A segment (blockSumsBatch / matchScanBatch): nb buffers, nf files of file_pieces[f] buffers each; the per-file
+ * Java arrays (int[][] / byte[][]) are arrs[f] with lens[f] elements (lens[f] < 0 with a NULL pointer: a Java
+ * null element). */
+static jobjectArray objs_of(fobj* store, jobject* refs, int kind, void** arrs, const jlong* lens, int n) {
+    for (int i = 0; i < n; ++i) {
+        store[i].kind = kind;
+        store[i].data = arrs[i];
+        store[i].len = lens[i];
+        refs[i] = (lens[i] < 0 && !arrs[i]) ? NULL : &store[i];
+    }
+    return NULL;
+}
+
+JNIEXPORT void jh_block_sums_batch(jlong ctx, void** bufs, const jlong* caps, int nb, int32_t* file_pieces, int nf,
+                                   jlong* sizes, int32_t* hdrs, uint8_t* seed, void** weak, const jlong* weak_lens,
+                                   void** strong, const jlong* strong_lens) {
+    reset();
+    fobj* store = (fobj*)calloc((size_t)nb + 1, sizeof(fobj));
+    jobject* refs = (jobject*)calloc((size_t)nb + 1, sizeof(jobject));
+    buffers(store, refs, bufs, caps, nb);
+    fobj arr = {K_OBJS, refs, nb};
+    fobj* ws = (fobj*)calloc((size_t)nf + 1, sizeof(fobj));
+    jobject* wr = (jobject*)calloc((size_t)nf + 1, sizeof(jobject));
+    fobj* ss = (fobj*)calloc((size_t)nf + 1, sizeof(fobj));
+    jobject* sr = (jobject*)calloc((size_t)nf + 1, sizeof(jobject));
+    objs_of(ws, wr, K_INT, weak, weak_lens, nf);
+    objs_of(ss, sr, K_BYTE, strong, strong_lens, nf);
+    fobj wa = {K_OBJS, wr, nf}, sa = {K_OBJS, sr, nf};
+    OBJ(fp, K_INT, file_pieces, nf);
+    OBJ(sz, K_LONG, sizes, nf);
+    OBJ(h, K_INT, hdrs, 4 * nf);
+    OBJ(s, K_BYTE, seed, 4);
+    NC(blockSumsBatch)(&g_env, NULL, ctx, &arr, fp, sz, h, s, &wa, &sa);
+    free(refs);
+    free(store);
+    free(ws);
+    free(wr);
+    free(ss);
+    free(sr);
+}
+
+JNIEXPORT jlong jh_match_scan_batch(jlong ctx, void** bufs, const jlong* caps, int nb, int32_t* file_pieces, int nf,
+                                    jlong* sizes, int32_t* hdrs, void** weak, const jlong* weak_lens, void** strong,
+                                    const jlong* strong_lens, uint8_t* seed, uint8_t* md5, jlong md5_len,
+                                    jlong* per_file, jlong per_len, jlong* ev_out, jlong ev_cap) {
+    reset();
+    fobj* store = (fobj*)calloc((size_t)nb + 1, sizeof(fobj));
+    jobject* refs = (jobject*)calloc((size_t)nb + 1, sizeof(jobject));
+    buffers(store, refs, bufs, caps, nb);
+    fobj arr = {K_OBJS, refs, nb};
+    fobj* ws = (fobj*)calloc((size_t)nf + 1, sizeof(fobj));
+    jobject* wr = (jobject*)calloc((size_t)nf + 1, sizeof(jobject));
+    fobj* ss = (fobj*)calloc((size_t)nf + 1, sizeof(fobj));
+    jobject* sr = (jobject*)calloc((size_t)nf + 1, sizeof(jobject));
+    objs_of(ws, wr, K_INT, weak, weak_lens, nf);
+    objs_of(ss, sr, K_BYTE, strong, strong_lens, nf);
+    fobj wa = {K_OBJS, wr, nf}, sa = {K_OBJS, sr, nf};
+    OBJ(fp, K_INT, file_pieces, nf);
+    OBJ(sz, K_LONG, sizes, nf);
+    OBJ(h, K_INT, hdrs, 4 * nf);
+    OBJ(s, K_BYTE, seed, 4);
+    OBJ(m, K_BYTE, md5, md5_len);
+    OBJ(pf, K_LONG, per_file, per_len);
+    jlong r = events_back(NC(matchScanBatch)(&g_env, NULL, ctx, &arr, fp, sz, h, &wa, &sa, s, m, pf), ev_out, ev_cap);
+    free(refs);
+    free(store);
+    free(ws);
+    free(wr);
+    free(ss);
+    free(sr);
+    return r;
 }

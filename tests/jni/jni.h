@@ -52,6 +52,7 @@ struct JNINativeInterface_ {
     void (*ReleaseLongArrayElements)(JNIEnv* env, jlongArray array, jlong* elems, jint mode);
     const char* (*GetStringUTFChars)(JNIEnv* env, jstring str, jboolean* isCopy);
     void (*ReleaseStringUTFChars)(JNIEnv* env, jstring str, const char* chars);
+    void (*GetLongArrayRegion)(JNIEnv* env, jlongArray array, jsize start, jsize len, jlong* buf);
 };
 
 #endif

@@ -35,7 +35,7 @@ def test_library_exports_every_symbol():
     L = ctypes.CDLL(R.LIB_PATH)
     for name in R.EXPORTS + R.DEBUG_EXPORTS:
         assert hasattr(L, name), name
-    assert R.lib().rsh_abi_version() == 3
+    assert R.lib().rsh_abi_version() == 4
 
 
 def test_options_have_defaults_and_no_environment():
@@ -160,3 +160,30 @@ def test_status_strings_and_last_error():
     assert isinstance(L.rsh_last_error(), bytes)  # "" until a HIP call of this thread fails
     with pytest.raises(R.ContextBusyError):
         R._check(R.RSH_E_BUSY)
+
+
+@pytest.mark.parametrize("width", [0, 1, 8, 16])
+def test_file_md5_batch_matches_hashlib(width):
+    """rsh_file_md5_batch (md5_mb.cpp, the Sender's whole-file MD5s of a segment, Sender.java:1241,1326): every
+    file's digest is hashlib's, whatever its length (every padding case around 55/56/64/119/120 bytes), its
+    pieces (empty ones, blocks straddling pieces) and the lane it ran on.  width: the multi-buffer form (0 = the
+    widest this CPU has, 1 scalar, 8 AVX2, 16 AVX-512; capped at what the CPU runs), several thread counts."""
+    import random
+    rng = random.Random(77 + width)
+    sizes = [0, 1, 55, 56, 57, 63, 64, 65, 119, 120, 121, 127, 128, 129, 1000, 4096, 70000]
+    sizes += [rng.randrange(0, 300000) for _ in range(40)] + [1 << 20, 3 << 20]
+    files = []
+    for k, n in enumerate(sizes):
+        a = O.splitmix(n, 0xABC + k) if n else np.zeros(0, np.uint8)
+        cuts = sorted(rng.randrange(0, n + 1) for _ in range(rng.randrange(0, 5)))
+        pieces, prev = [], 0
+        for c in cuts + [n]:
+            pieces.append(a[prev:c])
+            prev = c
+        files.append((a, pieces))
+    with R.option("md5_width", width):
+        for threads in (1, 3, 0):
+            got = R.file_md5_batch([p for _, p in files], threads=threads)
+            for (a, _), d in zip(files, got):
+                assert d == hashlib.md5(a.tobytes()).digest(), (a.size, threads)
+    assert R.file_md5_batch([]) == []

@@ -321,3 +321,73 @@ def test_batch_chain_low_entropy(ctx, alphabet, prefix, rsh_opt):
         assert sj[i].status == 0
         assert R.events_as_tuples(evs[i][:sj[i].n_ev], B) == oev, f"file {i}: B={B} form={i % 3}"
         assert (sj[i].literal, sj[i].matched) == (olit, omat)
+
+
+def test_batch_waiting_files_keep_their_worker(ctx, rsh_opt):
+    """with the device chain walk off (batch_chain = 0) the lead check parks files whose first
+    aligned windows all match on a WAIT request, and they resume only once the speculation lands.  Two
+    workers (host_cores 3: one core stays with the coordinator) own the even and the odd files; the even files
+    are identical 512 MiB copies (they wait for a ~0.5 ms speculation), the odd ones low-entropy edits that
+    need many head-mode rounds.  The worker that owns only waiting files must stay for them: before the fix it
+    left in the second round and the coordinator spun forever on their pending requests."""
+    rsh_opt("batch_chain", 0)
+    rsh_opt("host_cores", 3)
+    B, dl = 8192, 3
+    L = R.lib()
+    big_n, n_big = 512 << 20, 4
+    h_big = R.header_make(B, dl, big_n)
+    C = h_big.chunk_count
+    d_big = ctx.alloc(n_big * big_n)
+    d_bw, d_bs = ctx.alloc(4 * C * n_big), ctx.alloc(dl * C * n_big)
+    for k in range(n_big):
+        assert L.rsh_fill_splitmix_device(ctx.handle, d_big.ptr.value + k * big_n, big_n, 0xA11 + k, 0) == 0
+        assert L.rsh_block_sums_device(ctx.handle, d_big.ptr.value + k * big_n, big_n, ctypes.byref(h_big),
+                                       SEED_NP.ctypes.data, d_bw.ptr.value + 4 * C * k,
+                                       d_bs.ptr.value + dl * C * k) == 0
+    ctx.sync()
+    rng = random.Random(5)
+    small = []
+    for i in range(n_big):
+        nb = rng.randrange(60 * B, 120 * B)
+        basis = (np.frombuffer(O.splitmix(nb, 700 + i).tobytes(), np.uint8) % 4).astype(np.uint8)
+        other = (np.frombuffer(O.splitmix(nb, 1700 + i).tobytes(), np.uint8) % 4).astype(np.uint8)
+        src = basis.copy()
+        src[:nb // B * B].reshape(-1, B)[1::2] = other[:nb // B * B].reshape(-1, B)[1::2]
+        small.append((basis.tobytes(), src.tobytes()))
+    d_src, soffs = _pack(ctx, [f[1] for f in small], [0] * n_big)
+    sj = (R.ScanJob * (2 * n_big))()
+    evs, keep, expect = [], [], []
+    for k in range(n_big):
+        j = 2 * k                                          # even: identical, waits for the speculation
+        ev = np.zeros(C + 64, R.EVENT_DTYPE)
+        evs.append(ev)
+        sj[j].d_src, sj[j].n, sj[j].h = d_big.ptr.value + k * big_n, big_n, h_big
+        sj[j].d_weak, sj[j].d_strong = d_bw.ptr.value + 4 * C * k, d_bs.ptr.value + dl * C * k
+        sj[j].ev, sj[j].ev_cap = ev.ctypes.data, C + 64
+        expect.append(None)
+        basis, src = small[k]                              # odd: head-mode rounds
+        j += 1
+        h = R.header_make(B, dl, len(basis))
+        w, s = ctx.block_sums(basis, h, SEED)
+        d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
+        d_w.upload(w)
+        d_s.upload(s)
+        keep += [d_w, d_s]
+        cap = len(src) // (10 * B) + 2 * h.chunk_count + 64
+        ev = np.zeros(cap, R.EVENT_DTYPE)
+        evs.append(ev)
+        sj[j].d_src, sj[j].n, sj[j].h = d_src.ptr.value + soffs[k], len(src), h
+        sj[j].d_weak, sj[j].d_strong = d_w.ptr.value, d_s.ptr.value
+        sj[j].ev, sj[j].ev_cap = ev.ctypes.data, cap
+        oev, _, olit, omat, _ = O.sender(src, O.header(B, dl, len(basis)), w, s, SEED)
+        expect.append(([tuple(e) for e in oev], olit, omat))
+    run = [(R.EV_MATCH, c * B, B, c) for c in range(C)]
+    assert L.rsh_match_scan_batch_device(ctx.handle, sj, 2 * n_big, SEED_NP.ctypes.data, None) == 0
+    for j in range(2 * n_big):
+        assert sj[j].status == 0
+        got = R.events_as_tuples(evs[j][:sj[j].n_ev], B)
+        if j % 2 == 0:
+            assert got == run and (sj[j].literal, sj[j].matched) == (0, big_n), f"identical file {j}"
+        else:
+            oev, olit, omat = expect[j]
+            assert got == oev and (sj[j].literal, sj[j].matched) == (olit, omat), f"edited file {j}"

@@ -496,3 +496,30 @@ def test_pieces_match_oracle(ctx, cuts):
         oev, ofm, olit, omat, _ = O.sender(src, h, ow, os_, SEED)
         ev, fm, lit, mat, _ = ctx.match_scan_pieces(pieces(src), rh, ow, os_, SEED)
         assert R.events_as_tuples(ev, blen) == [tuple(e) for e in oev] and (fm, lit, mat) == (ofm, olit, omat)
+
+
+@pytest.mark.parametrize("cuts", [[7, 13, 1000, 4096, 65535], [200000, 3]], ids=lambda c: "-".join(map(str, c)))
+def test_pieces_tiled_match_oracle(ctx, cuts, rsh_opt):
+    """The pieces forms' tiled paths at a small size: file_tile_above and file_tile lowered to 64 KiB
+    so that rsh_match_scan_pieces pages the source through HBM a tile at a time (scan_tiled, chunks and windows
+    straddling both pieces and tiles) and rsh_block_sums_pieces runs its double-buffered multi-tile loop."""
+    rsh_opt("file_tile_above", 1 << 16)
+    rsh_opt("file_tile", 1 << 16)
+    basis = O.splitmix(300000, 0x91ECE6)
+    src = np.concatenate([basis[:70000], O.splitmix(5000, 0x1A5F), basis[70000:200000], basis[:9000]])
+    for blen, dlen in ((512, 2), (4096, 3), (1000, 4)):
+        h = O.header(blen, dlen, basis.size)
+        rh = R.Header(**h.as_dict())
+
+        def pieces(a):
+            out, off = [], 0
+            for c in cuts:
+                out.append(a[off:off + c])
+                off += c
+            return out + [a[off:]]
+        ow, os_ = O.generator(basis, h, SEED)
+        w, s = ctx.block_sums_pieces(pieces(basis), rh, SEED)
+        assert np.array_equal(w, ow) and np.array_equal(s, os_), blen
+        oev, ofm, olit, omat, _ = O.sender(src, h, ow, os_, SEED)
+        ev, fm, lit, mat, st = ctx.match_scan_pieces(pieces(src), rh, ow, os_, SEED)
+        assert R.events_as_tuples(ev, blen) == [tuple(e) for e in oev] and (fm, lit, mat) == (ofm, olit, omat), blen

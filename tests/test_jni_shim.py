@@ -32,7 +32,7 @@ def H():
     L.jh_exception.restype = ctypes.c_char_p
     L.jh_exception_message.restype = ctypes.c_char_p
     L.jh_ctx_create.restype = ctypes.c_int64
-    for fn in ("jh_match_scan", "jh_match_scan_buffers"):
+    for fn in ("jh_match_scan", "jh_match_scan_buffers", "jh_match_scan_batch"):
         getattr(L, fn).restype = ctypes.c_int64
     return L
 
@@ -173,5 +173,116 @@ def test_shim_scans_match_oracle(H):
                 arr["index"], arr["count"] = q[:, 3] & 0xFFFFFFFF, q[:, 3] >> 32
                 assert R.events_as_tuples(arr, blen) == [tuple(x) for x in oev]
                 assert fm == ofm and (sizes[0], sizes[1]) == (olit, omat)
+    finally:
+        H.jh_ctx_destroy(ctypes.c_int64(ctx))
+
+
+def _objs(arrs):
+    """per-file Java arrays: (pointer array, length array); None = a Java null element."""
+    ptrs = (ctypes.c_void_p * max(len(arrs), 1))(*[a.ctypes.data if a is not None else None for a in arrs])
+    lens = np.array([a.size if a is not None else -1 for a in arrs] or [0], np.int64)
+    return ptrs, lens
+
+
+def _segment_args(files, caps=None):
+    """files = [(pieces, n, h)] -> the flat buffer list and per-file arrays of the batch natives."""
+    bufs = [p for pieces, _, _ in files for p in pieces]
+    arr, cp = _bufs(bufs, caps)
+    fp = np.array([len(pieces) for pieces, _, _ in files] or [0], np.int32)
+    sz = np.array([n for _, n, _ in files] or [0], np.int64)
+    hd = np.concatenate([_hdr(h) for _, _, h in files]) if files else np.zeros(4, np.int32)
+    return arr, cp, len(bufs), fp, sz, hd
+
+
+def block_sums_batch(H, ctx, files, weak, strong, caps=None, nf=None):
+    arr, cp, nb, fp, sz, hd = _segment_args(files, caps)
+    s = np.frombuffer(SEED, np.uint8).copy()
+    wp, wl = _objs(weak)
+    sp, sl = _objs(strong)
+    H.jh_block_sums_batch(ctypes.c_int64(ctx), arr, _p(cp), nb, _p(fp), len(files) if nf is None else nf, _p(sz),
+                          _p(hd), _p(s), wp, _p(wl), sp, _p(sl))
+    return exc(H)
+
+
+def match_scan_batch(H, ctx, files, weak, strong, caps=None, md5_len=None, per_len=None):
+    arr, cp, nb, fp, sz, hd = _segment_args(files, caps)
+    s = np.frombuffer(SEED, np.uint8).copy()
+    wp, wl = _objs(weak)
+    sp, sl = _objs(strong)
+    F = len(files)
+    md5 = np.zeros(max(16 * F if md5_len is None else md5_len, 1), np.uint8)
+    per = np.zeros(max(3 * F if per_len is None else per_len, 1), np.int64)
+    evcap = sum(4 * R.scan_event_cap(n, h) for _, n, h in files) + 64
+    ev = np.zeros(evcap, np.int64)
+    k = H.jh_match_scan_batch(ctypes.c_int64(ctx), arr, _p(cp), nb, _p(fp), F, _p(sz), _p(hd), wp, _p(wl), sp, _p(sl),
+                              _p(s), _p(md5), ctypes.c_int64(md5.size if md5_len is None else md5_len), _p(per),
+                              ctypes.c_int64(per.size if per_len is None else per_len), _p(ev), ctypes.c_int64(evcap))
+    return exc(H), (ev[:k] if k >= 0 else None), md5, per
+
+
+def test_segment_natives_reject_before_the_library(H):
+    """blockSumsBatch / matchScanBatch: a closed context, a file whose buffers hold fewer bytes than its size,
+    piece counts that run past the buffer array, a heap buffer, a short weakOut array or null element, and short
+    md5 / per-file output arrays are rejected in the shim (the harness's bogus context would crash the library)."""
+    n, B = 4096, 512
+    data = np.zeros(n, np.uint8)
+    h = O.header(B, 2, n)
+    w, st = np.zeros(8, np.int32), np.zeros(16, np.uint8)
+    ok = [([data[:1000], data[1000:]], n, h)]
+    assert block_sums_batch(H, 0, ok, [w], [st]) == ISE
+    assert match_scan_batch(H, 0, ok, [w], [st])[0] == ISE
+    assert block_sums_batch(H, BOGUS, [([data[:1000], data[1000:]], n + 1, h)], [w], [st]) == IAE
+    assert match_scan_batch(H, BOGUS, [([data[:1000], data[1000:]], n + 1, h)], [w], [st])[0] == IAE
+    assert block_sums_batch(H, BOGUS, ok, [w], [st], caps=[1000, -1]) == IAE      # a heap buffer
+    assert match_scan_batch(H, BOGUS, ok, [w], [st], caps=[-1, n - 1000])[0] == IAE
+    assert block_sums_batch(H, BOGUS, ok, [np.zeros(7, np.int32)], [st]) == IAE   # weakOut[0] too short
+    assert block_sums_batch(H, BOGUS, ok, [None], [st]) == IAE
+    assert block_sums_batch(H, BOGUS, ok, [w], [st], nf=2) == IAE                 # sizes / hdrs shorter than nf
+    assert match_scan_batch(H, BOGUS, ok, [np.zeros(7, np.int32)], [st])[0] == IAE  # received table short
+    assert match_scan_batch(H, BOGUS, ok, [w], [st], md5_len=15)[0] == IAE
+    assert match_scan_batch(H, BOGUS, ok, [w], [st], per_len=2)[0] == IAE
+
+
+@pytest.mark.gpu
+def test_segment_natives_match_oracle(H):
+    """A segment through blockSumsBatch / matchScanBatch on a real context: every file's tables, events (the flat
+    long[] split by perFileOut's counts), sizes and file MD5 equal the oracle's; files are cut into several
+    direct buffers; a new file (B = 0) rides along."""
+    ctx = H.jh_ctx_create(0)
+    assert ctx and exc(H) == "", exc(H)
+    try:
+        files, tables, heads, srcs = [], [], [], []
+        for k, (n, blen, dl) in enumerate(((100000, 512, 2), (3 << 20, 8192, 3), (1300, 512, 2), (70000, 1024, 4))):
+            basis = O.splitmix(n, 0xC0 ^ n)
+            src = np.concatenate([basis[:n // 3], O.splitmix(777 + k, 0xEE), basis[n // 3 + 100:]])
+            h = O.header(blen, dl, n)
+            heads.append(h)
+            srcs.append(src)
+            files.append(([basis[:blen + 7], basis[blen + 7:blen + 8], basis[blen + 8:]], n, h))
+            tables.append((np.zeros(h.chunk_count, np.int32), np.zeros(h.chunk_count * dl, np.uint8)))
+        assert block_sums_batch(H, ctx, files, [t[0] for t in tables], [t[1] for t in tables]) == ""
+        for (pieces, n, h), (w, st) in zip(files, tables):
+            ow, os_ = O.generator(np.concatenate(pieces), h, SEED)
+            assert np.array_equal(w, ow) and np.array_equal(st, os_)
+        sf = [([src[:5], src[5:]], src.size, h) for src, h in zip(srcs, heads)]
+        sf.append(([srcs[0]], srcs[0].size, O.header(0, 0, 0)))
+        ws = [t[0] for t in tables] + [np.zeros(0, np.int32)]
+        ss = [t[1] for t in tables] + [np.zeros(0, np.uint8)]
+        e, ev, md5, per = match_scan_batch(H, ctx, sf, ws, ss)
+        assert e == "" and ev is not None, e
+        q = ev.reshape(-1, 4)
+        at = 0
+        for f, (src, h) in enumerate(zip(srcs + [srcs[0]], heads + [O.header(0, 0, 0)])):
+            w, st = (ws[f], ss[f])
+            oev, ofm, olit, omat, _ = O.sender(src, h, w, st, SEED)
+            cnt = int(per[3 * f])
+            part = q[at:at + cnt]
+            at += cnt
+            arr = np.zeros(cnt, R.EVENT_DTYPE)
+            arr["kind"], arr["offset"], arr["length"] = part[:, 0], part[:, 1], part[:, 2]
+            arr["index"], arr["count"] = part[:, 3] & 0xFFFFFFFF, part[:, 3] >> 32
+            assert R.events_as_tuples(arr, h.block_length or 1) == [tuple(x) for x in oev], f"file {f}"
+            assert md5[16 * f:16 * f + 16].tobytes() == ofm and (per[3 * f + 1], per[3 * f + 2]) == (olit, omat)
+        assert at == q.shape[0]
     finally:
         H.jh_ctx_destroy(ctypes.c_int64(ctx))
