@@ -4,13 +4,17 @@
 One step = the hot path over one file pair already resident in HBM:
   Generator block sums over the basis  (Generator.sendItemizeAndChecksums, Generator.java:886-895)
   + Sender match scan over the source  (Sender.sendMatchesAndData, Sender.java:1235-1327)
-through the C-ABI (rsh_block_sums_device + rsh_match_scan_device).  Workload (BASELINE.json config 5):
-a 16 GiB source against a 50%-modified basis (every other block replaced), B = 131072, dl = 4, seed
-01 02 03 04, splitmix64 synthetic bytes generated on the device.  The serial whole-file MD5 runs on the
-host in the product (rsh_match_scan) and is excluded here (see DESIGN.md "Measurement").
+through the C-ABI (rsh_block_sums_device + rsh_match_scan_device).  Headline workload (BASELINE.json config 5):
+a 16 GiB source against an identical basis (every source block digested: the MD5-heavy case; --variant), B =
+131072, dl = 4, seed 01 02 03 04, splitmix64 synthetic bytes generated on the device; the 50%-modified basis and a
+1-byte shift run as companions under `variants`.  The serial whole-file MD5 runs on the host in the product
+(rsh_match_scan) and is excluded here (see DESIGN.md "Measurement").  The line also carries a `files` block:
+BASELINE config 4 (128 x 128 MiB per GPU, the job's 128*N-file list sharded over the N ranks) through the
+batched entry points.
 
 Multi-GPU: one process per GPU, each rank scans its own file pair (file-parallel sharding, no collective on the
-data path); value = all ranks' bytes / max-over-ranks time.  Under torch.distributed.run the ranks come from its
+data path); value = all ranks' bytes / max-over-ranks time; the `files` block is config 4's 1024-file list at 8
+GPUs (its own value, files_total and per-rank times).  Under torch.distributed.run the ranks come from its
 environment; `python bench.py --gpus N` without a launcher starts the N rank processes itself (spawn_ranks) before
 anything touches a GPU.  `--dry-run` runs the rank plumbing (gloo barrier, max-over-ranks reduction, the JSON line)
 without a device.
@@ -63,6 +67,8 @@ def parse():
                     help="the headline pair (config 5): identical basis (every source block digested), 50%%-modified "
                          "basis, or an identical basis with one byte inserted into the source after 155 blocks")
     ap.add_argument("--no-companions", action="store_true", help="skip the other two variants")
+    ap.add_argument("--no-files", action="store_true",
+                    help="--workload file: skip the config-4 `files` block (128 files per GPU, sharded list)")
     ap.add_argument("--workload", choices=["file", "files", "receiver"], default="file",
                     help="file: config 5 (one 16 GiB pair per GPU); files: config 4 (many 128 MiB pairs per GPU); "
                          "receiver: Receiver.combineDataToFile on the config-2 shape (4 GiB, B by the rule)")
@@ -152,7 +158,10 @@ def main_dry(a):
                           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt * 1e3, 3),
                           "higher_is_better": True, "scaling": "weak", "dry_run": True,
                           "config": {"workload": a.workload, "files_total": files,
-                                     "parallelism": f"file-sharded x{world} (no collectives)"}}), flush=True)
+                                     "parallelism": f"file-sharded x{world} (no collectives)"},
+                          "files": {"files_total": files, "files_per_gpu": len(mine),
+                                    "world_size_seen": world_size_seen()}}),
+              flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
@@ -289,7 +298,8 @@ def main():
         ctx.sync()
         torch.cuda.synchronize()
         barrier()
-        dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device=red_dev)
+        per_rank = shard.gather_over_ranks(time.perf_counter() - t0, device=red_dev)
+        dt = max(per_rank)
         if gc_off:
             gc.enable()
         step_ms = [round((b - a) * 1e3, 3) for a, b in zip([t0] + t_step[:-1], t_step)]
@@ -299,6 +309,7 @@ def main():
         # read (its speculation K1s when they ran to completion, probed ranges, digest windows)
         read_step = n + float(np.mean(dev_bytes))
         out = {"ms_per_step": round(dt / steps * 1e3, 3), "steps": steps, "step_ms": step_ms,
+               "per_rank_ms_per_step": [round(x / steps * 1e3, 3) for x in per_rank],
                "warmup_steps": done, "warmup_ms": round(warmup_ms, 1),
                "step_kernel_ms": [[round(g, 3) for g in gen_steps], [round(x, 3) for x in spec_ms]],
                "bytes_read_per_step": int(read_step),
@@ -336,6 +347,7 @@ def main():
         "warmup_ms": head["warmup_ms"],
         "ms_per_step": head["ms_per_step"],
         "step_ms": head["step_ms"],
+        "per_rank_ms_per_step": head["per_rank_ms_per_step"],
         "step_kernel_ms": head["step_kernel_ms"],
         "higher_is_better": True,
         "scaling": "weak",
@@ -350,6 +362,7 @@ def main():
             "digest_length": dl,
             "chunks": C,
             "parallelism": f"file-sharded x{world} (no collectives)" + SHARED_NOTE * shared,
+            "world_size_seen": world_size_seen(),
         },
         "roofline": {
             "kernel": "block_sums_pipe_kernel (K1: the Generator's launch; the Sender's aligned speculation is the "
@@ -375,6 +388,23 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         b0, s0 = pairs[a.variant]
         res["cpu_baseline"] = cpu_baseline(s0, b0, B, dl, a.cpu_sample_mib << 20)
+    if not a.no_files and cfg_name(n, B) == "config5":
+        # BASELINE config 4 beside the headline: this rank's shard of the job's 128*N-file list (1024 files at 8
+        # GPUs), the same batched entry points and per-file oracle checks as --workload files
+        del pairs, src, d_weak, d_strong
+        torch.cuda.empty_cache()
+        f = run_files(a, ctx, rank, world, red_dev, shared, "identical", a.steps, a.warmup, not a.no_companions,
+                      cpu=False)
+        res["files"] = {"value": f["value"], "unit": "GiB/s", "ms_per_step": f["ms_per_step"],
+                        "per_rank_ms_per_step": f["per_rank_ms_per_step"], "steps": f["steps"],
+                        "workload": f["config"]["workload"], "files_total": f["config"]["files_total"],
+                        "files_per_gpu": f["config"]["files_per_gpu"],
+                        "bytes_per_step_per_gpu": f["config"]["bytes_per_step_per_gpu"],
+                        "world_size_seen": f["config"]["world_size_seen"],
+                        "roofline": {k: f["roofline"][k] for k in ("frac", "step_frac", "kernel_ms", "traffic")},
+                        "parity": f["parity"],
+                        "variants": {v: {k: r[k] for k in ("value_read", "ms_per_step", "per_rank_ms_per_step",
+                                                          "parity")} for v, r in f["variants"].items()}}
     if rank == 0:
         if a.opt:
             res["config"]["options"] = a.opt
@@ -432,14 +462,31 @@ def main_files(a):
     --steps; the other form (50%-modified: every other block replaced) runs as a companion under `variants`, so
     both are always measured.  Every file's last timed scan is checked against the oracle's per-file digest.
     --files-api single: one rsh_match_scan_device per file on a pool of contexts instead (comparison)."""
-    import concurrent.futures as cf
-
-    import torch
     rank, world, local, red_dev, shared = setup_rank()
     if not os.path.exists(R.LIB_PATH):
         R.build()
-    L = R.lib()
     apply_opts(a)
+    ctx = R.Context(local)
+    res = run_files(a, ctx, rank, world, red_dev, shared, a.variant, a.steps, a.warmup, not a.no_companions,
+                    cpu=not a.no_cpu_baseline)
+    if rank == 0:
+        if a.opt:
+            res["config"]["options"] = a.opt
+        print(json.dumps(res), flush=True)
+    ctx.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def run_files(a, ctx, rank, world, red_dev, shared, variant, steps, warmup, companions, cpu):
+    """Config 4 on this rank's shard of the job's file list (main_files' line; the `files` block of the default
+    line): returns the line's dict."""
+    import concurrent.futures as cf
+
+    import torch
+    L = R.lib()
+    local = torch.cuda.current_device()
     S = a.file_mib << 20
     # the job's file list (BASELINE config 4: 1024 files at 8 GPUs; a.files per GPU) sharded over the ranks by
     # the production LPT helper; this rank lays its files end to end in HBM
@@ -453,8 +500,7 @@ def main_files(a):
     assert S % B == 0
     n = F * S
     seed = np.frombuffer(bytes([1, 2, 3, 4]), np.uint8).copy()
-    ctx = R.Context(local)
-    assert a.variant in ("identical", "half"), "--workload files: identical or half"
+    assert variant in ("identical", "half"), "--workload files: identical or half"
     src = torch.empty(n, dtype=torch.uint8, device="cuda")
     half = torch.empty(n, dtype=torch.uint8, device="cuda")
     for j, i in enumerate(mine):  # file i of the global list: its own splitmix stream
@@ -543,7 +589,8 @@ def main_files(a):
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        dt = shard.reduce_over_ranks(time.perf_counter() - t0, "max", device=red_dev)
+        per_rank = shard.gather_over_ranks(time.perf_counter() - t0, device=red_dev)
+        dt = max(per_rank)
         if gc_off:
             gc.enable()
         for i in range(F):  # Sender.java:1325 for every file of the last timed step
@@ -553,6 +600,7 @@ def main_files(a):
         assert read_step / (dt / steps) / 1e9 <= HBM_PEAK_GBS, "bytes read exceed the HBM peak: accounting error"
         k_ms = sum(e0.elapsed_time(e1) for e0, e1 in gen_ev) / len(gen_ev)
         return {"ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
+                "per_rank_ms_per_step": [round(x / steps * 1e3, 3) for x in per_rank],
                 "step_ms": [round((b - a_) * 1e3, 3) for a_, b in zip([t0] + t_step[:-1], t_step)],
                 "bytes_read_per_step": int(read_step),
                 "value_read": round(world * steps * read_step / dt / (1 << 30), 3),
@@ -561,18 +609,20 @@ def main_files(a):
                          "stats": bst.as_dict() if a.files_api == "batch" else None},
                 "parity": check_files_golden(golden, v, sjobs, evbufs, B)}, dt, read_step, k_ms
 
-    other = "half" if a.variant == "identical" else "identical"
-    head, dt, read_step, k_ms = run_files_variant(a.variant, a.steps, a.warmup)
-    comp = {} if a.no_companions else {other: run_files_variant(other, max(2, min(a.steps, 3)), 1)[0]}
+    other = "half" if variant == "identical" else "identical"
+    head, dt, read_step, k_ms = run_files_variant(variant, steps, warmup)
+    comp = {other: run_files_variant(other, max(2, min(steps, 3)), 1)[0]} if companions else {}
     ach = n / (k_ms * 1e-3) / 1e9
     res = {
         "metric": "GiB/s device-resident rolling+MD5 scan (Generator block sums + Sender match scan; bytes read)",
-        "value": head["value_read"], "unit": "GiB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": head["ms_per_step"], "step_ms": head["step_ms"], "higher_is_better": True, "scaling": "weak",
+        "value": head["value_read"], "unit": "GiB/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": head["ms_per_step"], "step_ms": head["step_ms"],
+        "per_rank_ms_per_step": head["per_rank_ms_per_step"], "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic (splitmix64 on device; tests/golden/fullsize_config4.json)",
         "config": {"workload": f"config4: {F} files x {a.file_mib} MiB per GPU of a {len(sizes)}-file list "
-                               f"({VARIANT_TEXT[a.variant]} bases), B={B}, dl={dl}",
-                   "bytes_per_step_per_gpu": int(read_step), "files_per_gpu": F, "block_length": B, "digest_length": dl,
+                               f"({VARIANT_TEXT[variant]} bases), B={B}, dl={dl}",
+                   "bytes_per_step_per_gpu": int(read_step), "files_per_gpu": F, "files_total": len(sizes),
+                   "world_size_seen": world_size_seen(), "block_length": B, "digest_length": dl,
                    "parallelism": f"file-sharded x{world} (no collectives), " + (
                        "batched entry points" if a.files_api == "batch" else f"{a.threads} scan contexts per GPU")
                    + SHARED_NOTE * shared},
@@ -584,20 +634,21 @@ def main_files(a):
                      "kernel_ms": round(k_ms, 4), "algorithmic_bytes": n},
         "scan": head["scan"], "parity": head["parity"], "variants": comp,
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline_files(src, bases[a.variant], S, F, B, dl, a.cpu_sample_mib << 20)
-    if rank == 0:
-        if a.opt:
-            res["config"]["options"] = a.opt
-        print(json.dumps(res), flush=True)
+    if rank == 0 and world == 1 and cpu:
+        res["cpu_baseline"] = cpu_baseline_files(src, bases[variant], S, F, B, dl, a.cpu_sample_mib << 20)
     if ex:
         ex.shutdown()
     for c in pool_ctx:
         c.close()
-    ctx.close()
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    del src, half, bases, d_weak, d_strong
+    torch.cuda.empty_cache()
+    return res
+
+
+def world_size_seen():
+    """The size of the process group this rank joined (1 without one)."""
+    import torch.distributed as dist
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
 def files_golden(mine, S, B, dl):

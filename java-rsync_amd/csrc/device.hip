@@ -522,6 +522,8 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 // buffer descriptor.  gt != nullptr: chunk i is gt[i] (K1Tail: any file; the segmented launch); else chunk i
 // is data + i B with outputs weak_out[i], strong_out[i dl] (a single launch's partial last wave).  Lanes past
 // gcnt digest chunk 0 again and store nothing.
+// MODE != 0 (A/B and diagnostic forms: synthetic stage data, per-iteration drains or sleeps) exists in the kbench
+// build only (RSH_KBENCH); the product library instantiates MODE 0.
 template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false, bool GATHER = false>
 __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
@@ -535,6 +537,9 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     constexpr int ROW = 9;
     constexpr int BUF = 64 * ROW;  // uint4 slots per LDS buffer
     constexpr int TAIL_PF = RSH_K1_TAIL_PF;
+#ifndef RSH_KBENCH
+    static_assert(MODE == 0 && MD5F == 8, "the product library runs the production K1 only");
+#endif
     if constexpr (!MULTI && !GATHER) {
         // tail waves (blockIdx >= main_waves): one lane per chunk left over (a partial last wave, the short last
         // chunk), dispatched with the main waves rather than as a launch queued behind them (a lone wave takes
@@ -615,9 +620,13 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     auto load = [&](uint4 (&dst)[8], uint32_t stg) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            if constexpr (MODE == 1) {
+#ifdef RSH_KBENCH
+            if constexpr (MODE == 1) {  // diagnostics: synthetic stage data, no global loads
                 dst[j] = make_uint4(l + stg, j, c0, 7);
-            } else if constexpr (GATHER) {
+                continue;
+            }
+#endif
+            if constexpr (GATHER) {
                 dst[j] = ld16<false>(rp[j] + 128u * stg);
             } else {
                 const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_off + 128u * stg, (int)(j * 8u * B), 2);
@@ -703,9 +712,11 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         stage(std::integral_constant<int, 0>{}, s, true, true);
         stage(std::integral_constant<int, 1>{}, s + 1, true, true);
         if constexpr (ABORT) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(flag));
+#ifdef RSH_KBENCH
         else if constexpr (MODE == 5) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // A/B: the drain alone
         else if constexpr (MODE == 6) asm volatile("s_sleep 1" ::: "memory");            // A/B: a short sleep
         else if constexpr (MODE == 7) asm volatile("s_sleep 4" ::: "memory");
+#endif
     }
     if constexpr (ABORT) {
         if (flag == abort_gen) return;

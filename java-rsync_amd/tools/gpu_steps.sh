@@ -20,6 +20,8 @@
 #                instruction mix and LDS bank conflicts
 #   kbench-k1    kbench: the K1 at B = 128 KiB and 8 KiB, the batched forms (1002, 1005, 1006)
 #   e2e          java-rsync_amd/tools/e2e.py at config 5 (16 GiB from host memory)
+#   e2e4         java-rsync_amd/tools/e2e_config4.py: config 4's shard (128 x 128 MiB) from host memory, the segment
+#                entry points against 128 single-file calls
 #   config3      the config-3 line: a 64 GiB identical pair resident in HBM, B = 131072 (the Sender's limit), dl = 5
 #   receiver     the Receiver line (combineDataToFile on the config-2 shape)
 #   multi        bench.py --gpus 2 without a launcher (its own rank processes) on a one-GPU box: the N-rank path,
@@ -47,6 +49,7 @@ for step in "$@"; do
             tests/test_gpu_fullsize.py -k "batch or config4" > "$O/batch_tests.log" 2>&1 ;;
         pytest) run 900 python -u -m pytest -m gpu -x -v --timeout 400 --timeout-method thread $PYTEST_ARGS \
             > "$O/pytest.log" 2>&1 ;;
+        e2e4) run 900 python java-rsync_amd/tools/e2e_config4.py > "$O/e2e_config4.json" 2> "$O/e2e_config4.err" ;;
         smoke) run 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.log" 2>&1 ;;
         bench) run 300 python bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
         files)

@@ -91,6 +91,24 @@ def test_bench_gpus2_dry_run_spawns_ranks():
     assert rec["n_gpus"] == 2 and rec["dry_run"] and rec["config"]["files_total"] == 256
 
 
+def test_bench_gpus8_dry_run_reports_config4_list():
+    """The driver's 8-GPU line (`python bench.py --gpus 8`, default workload) carries BASELINE config 4's files
+    block: the 1024-file list sharded 128 per rank over a process group of 8 (gloo here, RCCL on the node)."""
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--dry-run"],
+                         capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 8 and rec["files"]["files_total"] == 1024
+    assert rec["files"]["files_per_gpu"] == 128 and rec["files"]["world_size_seen"] == 8
+
+
 def test_rank_device_plan(monkeypatch):
     """One GPU per local rank: RCCL on the rank's own device.  More local ranks than GPUs (a rehearsal of the
     N-rank launch on a smaller box): round-robin devices and gloo, chosen identically by every rank."""
