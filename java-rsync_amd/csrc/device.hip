@@ -386,6 +386,10 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
                 for (int k = 0; k < 16; ++k) fold ^= m[k];
             } else if constexpr (MFMAW) {
                 if constexpr (MD5F == 8) md5_compress_rot16n(st, m);
+#ifdef RSH_KBENCH
+    else if constexpr (MD5F == 10) md5_compress_k3s_8(st, m);   // A/B: a + m + K in one v_add3_u32, K from an SGPR
+    else if constexpr (MD5F == 11) md5_compress_k3s_16(st, m);
+#endif
                 else if constexpr (MD5F == 7) md5_compress_rot4n(st, m);
                 else if constexpr (MD5F == 6) md5_compress_rot16(st, m);
                 else if constexpr (MD5F == 5) md5_compress_rot4(st, m);
@@ -498,6 +502,10 @@ __device__ __forceinline__ void md5_k3_block(Md5State& st, const uint32_t (&m)[1
 template <int MD5F>
 __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&m)[16]) {
     if constexpr (MD5F == 8) md5_compress_rot16n(st, m);
+#ifdef RSH_KBENCH
+    else if constexpr (MD5F == 10) md5_compress_k3s_8(st, m);   // A/B: a + m + K in one v_add3_u32, K from an SGPR
+    else if constexpr (MD5F == 11) md5_compress_k3s_16(st, m);
+#endif
     else if constexpr (MD5F == 7) md5_compress_rot4n(st, m);
     else if constexpr (MD5F == 1) md5_compress_lit(st, m);
     else md5_compress(st, m);
@@ -1684,6 +1692,14 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     hipLaunchKernelGGL(block_sums_pipe_k3_kernel, dim3(waves), dim3(64), 2 * wave_lds, s,
                                        d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
                     break;
+                case 62:  // A/B: MD5 steps with a + m + K as one v_add3_u32, K from an SGPR (s_mov per step), abortable
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<10, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
+                    break;
+                case 63:  // ... 16 steps per asm statement
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<11, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
+                    break;
                 case 58:  // diagnostics (wrong results): the production abortable K1 on synthetic stage data, no
                           // global loads -- its s_waitcnt time is the LDS / abort-word share (PMC attribution)
                     hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true, 1>), dim3(waves), dim3(64), 2 * wave_lds, s,
@@ -2806,10 +2822,18 @@ __device__ __forceinline__ bool kslots_has(const unsigned long long* __restrict_
 // key still displaced after the insertion's bound (tables near or above 32768 distinct keys) marks the set
 // incomplete, and the walk then confirms every key in the chunk index instead.
 constexpr int CHAIN_CK_BUCKETS = 4096;
-__device__ __forceinline__ uint32_t chain_ck_h1(uint32_t k) { return (k * 0x9E3779B1u) >> 20; }
+// In front of it, a one-read bit filter: word (k * phi) >> 20 of 4096 (16 KiB, the word index is the key's first cuckoo
+// bucket) with two bits of the same product set per key.  Config 4's 16384 keys leave ~5 % of absent keys passing it,
+// so a tile's lookups cost one 4-byte LDS read per position and the two 16-byte cuckoo reads only for survivors
+// (r3ze: the cuckoo reads' bank conflicts were half the walk's LDS cycles).
+constexpr int CHAIN_BF_WORDS = 4096;
+__device__ __forceinline__ uint32_t chain_ck_mix(uint32_t k) { return k * 0x9E3779B1u; }
+__device__ __forceinline__ uint32_t chain_bf_mask(uint32_t x) { return (1u << ((x >> 15) & 31u)) | (1u << ((x >> 10) & 31u)); }
+__device__ __forceinline__ uint32_t chain_ck_h1(uint32_t k) { return chain_ck_mix(k) >> 20; }
 __device__ __forceinline__ uint32_t chain_ck_h2(uint32_t k) { return CHAIN_CK_BUCKETS + (((k ^ (k >> 15)) * 0x85EBCA77u) >> 20); }
 struct ChainKeySet {
     uint4* b;      // 2 * CHAIN_CK_BUCKETS buckets
+    uint32_t* bf;  // CHAIN_BF_WORDS filter words
     int32_t* has0;  // key 0 present
     int32_t* full;  // some key found no slot: lookups are not exact
 };
@@ -2818,6 +2842,8 @@ __device__ __forceinline__ void chain_ck_insert(const ChainKeySet& ks, uint32_t 
         *ks.has0 = 1;
         return;
     }
+    const uint32_t x = chain_ck_mix(k);
+    atomicOr(ks.bf + (x >> 20), chain_bf_mask(x));
     // cuckoo insertion: a free slot of the key's bucket in table w, else displace one of that bucket's keys and
     // carry it to its bucket in the other table (every key lives in its own h1 or h2 bucket)
     uint32_t cur = k;
@@ -2853,15 +2879,38 @@ __device__ __forceinline__ int chain_first_hit16(const unsigned long long* __res
     // free: two 16-byte reads and eight compares per key (a wave's lanes would take every branch anyway)
     if (*set.full == 0) {
         const bool has0 = *set.has0 != 0;
-        uint32_t m = 0;
+        // the bit filter: one 4-byte read per key, the 16 reads in flight together
+        uint32_t w[PROBE_PPT];
+#pragma unroll
+        for (int i = 0; i < PROBE_PPT; ++i) w[i] = set.bf[chain_ck_mix(keys[i]) >> 20];
+        uint32_t pass = 0, m = 0;
 #pragma unroll
         for (int i = 0; i < PROBE_PPT; ++i) {
-            const uint32_t k = keys[i];
-            const uint4 x = set.b[chain_ck_h1(k)], y = set.b[chain_ck_h2(k)];
-            const bool in = (x.x == k) | (x.y == k) | (x.z == k) | (x.w == k) | (y.x == k) | (y.y == k) | (y.z == k) |
-                            (y.w == k);
-            m |= (uint32_t)(k != 0u ? in : has0) << i;
-            if ((i & 3) == 3) asm volatile("" ::: "memory");  // 4 keys' reads in flight at a time (registers)
+            const uint32_t k = keys[i], bm = chain_bf_mask(chain_ck_mix(k));
+            if (k != 0u) pass |= (uint32_t)((w[i] & bm) == bm) << i;
+            else m |= (uint32_t)has0 << i;  // key 0 has its own flag (exact)
+        }
+        pass &= valid;
+        // the exact lookup for the survivors only (a lane with none reads nothing), 4 keys' reads in flight at a time
+#pragma unroll
+        for (int g = 0; g < PROBE_PPT; g += 4) {
+            if (((pass >> g) & 15u) == 0u) continue;
+            uint4 x[4], y[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                x[j] = y[j] = make_uint4(0u, 0u, 0u, 0u);
+                if ((pass >> (g + j)) & 1u) {
+                    x[j] = set.b[chain_ck_h1(keys[g + j])];
+                    y[j] = set.b[chain_ck_h2(keys[g + j])];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = keys[g + j];
+                const bool in = (x[j].x == k) | (x[j].y == k) | (x[j].z == k) | (x[j].w == k) | (y[j].x == k) |
+                                (y[j].y == k) | (y[j].z == k) | (y[j].w == k);
+                m |= (uint32_t)(in && ((pass >> (g + j)) & 1u)) << (g + j);
+            }
         }
         m &= valid;
         return m ? __builtin_ctz(m) : -1;
@@ -2917,6 +2966,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_any;                  // some chunk carries the stale digest
     __shared__ int32_t s_seg[CHAIN_SEGS][4];   // wide tiles: the exscan at each block's first lane
     __shared__ uint4 s_ck[2 * CHAIN_CK_BUCKETS];  // the table's keys (ChainKeySet)
+    __shared__ uint32_t s_bf[CHAIN_BF_WORDS];     // ... and their bit filter
     __shared__ int32_t s_ck_has0, s_ck_full;
     __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
@@ -2932,7 +2982,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const int64_t last = n - S, nB = n - B;
     const int64_t na = phase == 0 ? F.na_a : F.na, nflags = na < C ? na : C;
     const bool wide = (B % CHAIN_PPT) == 0 && B >= 512 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
-    const ChainKeySet kset{s_ck, &s_ck_has0, &s_ck_full};
+    const ChainKeySet kset{s_ck, s_bf, &s_ck_has0, &s_ck_full};
     int64_t s = out->s, m = out->m;
     // The key set (~C LDS inserts, tens of microseconds) only if the walk may search: a walk that starts aligned on
     // an unbroken run of chain flags up to the last window with a chunk (an identical file, or its rest after the
@@ -2970,6 +3020,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     }
     if (kset_built) {
         for (int i = t; i < 2 * CHAIN_CK_BUCKETS; i += CHAIN_THREADS) s_ck[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (int i = t; i < CHAIN_BF_WORDS; i += CHAIN_THREADS) s_bf[i] = 0u;
         if (t == 0) s_ck_has0 = s_ck_full = 0;
         __syncthreads();
         for (int64_t c = t; c < C; c += CHAIN_THREADS) chain_ck_insert(kset, (uint32_t)F.table_weak[c]);
@@ -3110,12 +3161,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 ++tiles;
                 const int64_t tt0 = (int64_t)wall_clock64();
                 const int64_t kb0 = q0 / B, o0 = kb0 * B;
-                int32_t head[4] = {0, 0, 0, 0};
-                if (q0 > o0) {
-                    range_sums(F.data, n, o0, q0, o0, head[0], head[1]);
-                    range_sums(F.data, n, o0 + B, q0 + B, o0, head[2], head[3]);
-                    block_reduce<4>(head, sh);
-                }
+                // the lane's bytes and anchor first: their loads are in flight while the block's head is reduced
+                // (one global round trip per tile instead of two)
                 const int64_t p0 = q0 + (int64_t)t * CHAIN_PPT;
                 const int64_t kb = p0 / B, o = kb * B;
                 uint32_t xa[2][4], xb[2][4];
@@ -3125,6 +3172,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 load16(F.data, n, p0 + B + 16, xb[1]);
                 const bool live = p0 <= stop && p0 <= lim_spec && p0 + CHAIN_PPT > a;
                 const int32_t To = live ? F.aw[kb] : 0;
+                int32_t head[4] = {0, 0, 0, 0};
+                if (q0 > o0) {
+                    range_sums(F.data, n, o0, q0, o0, head[0], head[1]);
+                    range_sums(F.data, n, o0 + B, q0 + B, o0, head[2], head[3]);
+                    block_reduce<4>(head, sh);
+                }
                 int32_t pre[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh)
@@ -3309,26 +3362,34 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         ++events;
         const int64_t kp = p / B;
         const bool spec_digest = p % B == 0 && kp < na;
-        if (t == 0) {
+        if (t < 64) {
+            // every chunk with this key lies on the probe path before the first empty slot: wave 0 reads 64 slots of
+            // it per round trip (one, nearly always) instead of one dependent load per slot
             int32_t cnt = 0;
             const unsigned long long* ks = F.kslots;
             uint32_t h = slot_hash(key) & F.kmask;
-            for (;;) {  // every chunk with this key lies on the probe path before the first empty slot
-                const unsigned long long v = ks[h];
-                if (v == 0ull) break;
-                if ((uint32_t)(v >> 32) == key) {
-                    if (cnt < CHAIN_BUCKET_CAP) s_bk[cnt] = (int32_t)((uint32_t)v - 1u);
-                    ++cnt;
-                }
-                h = (h + 1) & F.kmask;
+            for (bool more = true; more; h = (h + 64u) & F.kmask) {
+                const unsigned long long v = ks[(h + (uint32_t)t) & F.kmask];
+                const unsigned long long empty = __ballot(v == 0ull);
+                const int lim = empty ? __builtin_ctzll(empty) : 64;  // slots before the first empty one
+                const bool mine = t < lim && (uint32_t)(v >> 32) == key;
+                const unsigned long long hits = __ballot(mine);
+                const int at = cnt + __popcll(hits & ((1ull << t) - 1ull));
+                if (mine && at < CHAIN_BUCKET_CAP) s_bk[at] = (int32_t)((uint32_t)v - 1u);
+                cnt += __popcll(hits);
+                more = empty == 0ull;
             }
+            if (t == 0) s_nbk = cnt;
+        }
+        __syncthreads();
+        if (t == 0) {
+            const int32_t cnt = s_nbk;
             for (int i = 1; i < cnt && i < CHAIN_BUCKET_CAP; ++i)  // ascending chunk index (insertion order)
                 for (int j = i; j > 0 && s_bk[j - 1] > s_bk[j]; --j) {
                     const int32_t x = s_bk[j];
                     s_bk[j] = s_bk[j - 1];
                     s_bk[j - 1] = x;
                 }
-            s_nbk = cnt;
         }
         __syncthreads();
         const int32_t size = s_nbk;

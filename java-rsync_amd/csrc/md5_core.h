@@ -343,6 +343,8 @@ RSH_HD void md5_compress_rot4n(Md5State& st, const uint32_t (&m)[16]) { md5_comp
 RSH_HD void md5_compress_rot16n(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
 RSH_HD void md5_compress_asm4(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
 RSH_HD void md5_compress_asm16(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+RSH_HD void md5_compress_k3s_8(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+RSH_HD void md5_compress_k3s_16(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
 #endif
 
 #if defined(__HIP__)

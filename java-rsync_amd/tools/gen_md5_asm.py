@@ -163,6 +163,38 @@ def main_k3(steps_per_block, nt):
     print("\n".join(out))
 
 
+def k3s_block(lo, hi, nt):
+    """k3 with K from an SGPR operand (VOP3 takes one SGPR): a + m + K in one v_add3_u32 without the 64 VGPRs of
+    constants; the compiler materialises each K with an s_mov_b32 (SALU, beside the other wave's VALU).  kbench A/B."""
+    lines = []
+    words = sorted({msg_index(i) for i in range(lo, hi)})
+    for i in range(lo, hi):
+        a, b, c, d = ROLES[i % 4]
+        t, f = f"%[t{i % nt}]", f"%[f{i % nt}]"
+        lines += [f"v_add3_u32 {t}, %[m{msg_index(i)}], %[{a}], %[k{i - lo}]",
+                  f"v_bitop3_b32 {f}, %[{b}], %[{c}], %[{d}] bitop3:{bop(i)}",
+                  f"v_add_u32 {t}, {t}, {f}",
+                  f"v_alignbit_b32 {t}, {t}, {t}, {32 - S[i]}",
+                  f"v_add_u32 %[{a}], {t}, %[{b}]",
+                  "s_nop 0"]
+    body = "\\n\\t".join(lines)
+    ins = ", ".join([f'[m{w}] "v"(m[{w}])' for w in words] + [f'[k{i - lo}] "s"(0x{K[i]:08x}u)' for i in range(lo, hi)])
+    tmps = ", ".join(f'[t{k}] "=&v"(t{k}), [f{k}] "=&v"(f{k})' for k in range(nt))
+    return (f'    asm("{body}"\n'
+            f'        : [a] "+v"(a), [b] "+v"(b), [c] "+v"(c), [d] "+v"(d), {tmps}\n'
+            f'        : {ins});')
+
+
+def main_k3s(steps_per_block, nt):
+    out = [f"__device__ __forceinline__ void md5_compress_k3s_{steps_per_block}(Md5State& st, const uint32_t (&m)[16]) {{",
+           "    uint32_t a = st.a, b = st.b, c = st.c, d = st.d;",
+           "    uint32_t " + ", ".join(f"t{k}, f{k}" for k in range(nt)) + ";"]
+    for lo in range(0, 64, steps_per_block):
+        out.append(k3s_block(lo, lo + steps_per_block, nt))
+    out += ["    st.a += a;", "    st.b += b;", "    st.c += c;", "    st.d += d;", "}"]
+    print("\n".join(out))
+
+
 def main():
     out = ["// Generated by tools/gen_md5_asm.py -- do not edit.  See that script for the design.",
            "__device__ __forceinline__ void md5_compress_asm(Md5State& st, const uint32_t (&m)[16]) {",
@@ -179,6 +211,8 @@ def main():
     main_rot(4, 4, True)
     main_rot(16, 4, True)
     main_k3(8, 4)
+    main_k3s(8, 4)
+    main_k3s(16, 4)
 
 
 if __name__ == "__main__":
