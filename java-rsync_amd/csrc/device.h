@@ -262,6 +262,9 @@ struct GatherOp {
     int64_t len;
 };
 hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s);
+#ifdef RSH_KBENCH
+hipError_t launch_gather_ops_variant(int v, const GatherOp* ops, uint32_t n, hipStream_t s);  // A/Bs (kbench)
+#endif
 // Probe hashes of many files (slots cleared by the caller): keys[i] into slots/mask.
 struct TableEnt {
     unsigned long long* slots;

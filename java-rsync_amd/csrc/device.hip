@@ -389,6 +389,8 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
 #ifdef RSH_KBENCH
     else if constexpr (MD5F == 10) md5_compress_k3s_8(st, m);   // A/B: a + m + K in one v_add3_u32, K from an SGPR
     else if constexpr (MD5F == 11) md5_compress_k3s_16(st, m);
+    else if constexpr (MD5F == 12) md5_compress_k3s_16_nonop(st, m);
+    else if constexpr (MD5F == 13) md5_compress_k3s_16_nop2(st, m);
 #endif
                 else if constexpr (MD5F == 7) md5_compress_rot4n(st, m);
                 else if constexpr (MD5F == 6) md5_compress_rot16(st, m);
@@ -505,6 +507,8 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 #ifdef RSH_KBENCH
     else if constexpr (MD5F == 10) md5_compress_k3s_8(st, m);   // A/B: a + m + K in one v_add3_u32, K from an SGPR
     else if constexpr (MD5F == 11) md5_compress_k3s_16(st, m);
+    else if constexpr (MD5F == 12) md5_compress_k3s_16_nonop(st, m);
+    else if constexpr (MD5F == 13) md5_compress_k3s_16_nop2(st, m);
 #endif
     else if constexpr (MD5F == 7) md5_compress_rot4n(st, m);
     else if constexpr (MD5F == 1) md5_compress_lit(st, m);
@@ -1694,6 +1698,14 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     break;
                 case 62:  // A/B: MD5 steps with a + m + K as one v_add3_u32, K from an SGPR (s_mov per step), abortable
                     hipLaunchKernelGGL((block_sums_pipe_kernel<10, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
+                    break;
+                case 64:  // ... without the s_nop after each step
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<12, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
+                    break;
+                case 65:  // ... an s_nop after every other step
+                    hipLaunchKernelGGL((block_sums_pipe_kernel<13, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
                                        d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
                     break;
                 case 63:  // ... 16 steps per asm statement
@@ -3644,7 +3656,10 @@ hipError_t launch_window_weak(const ScanFile* files, const GatherEnt* ents, uint
     return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void gather_ops_kernel(const GatherOp* __restrict__ ops) {
+// D dwordx4 loads in flight per thread before their stores; NTL / NTS: non-temporal loads / stores.  The production
+// form is <256, 4, true, true>; the others are kbench A/Bs (KBENCH_GATHER).
+template <int T, int D, bool NTL, bool NTS>
+__global__ __launch_bounds__(T) void gather_ops_kernel_t(const GatherOp* __restrict__ ops) {
     const GatherOp op = ops[blockIdx.x];
     const uintptr_t d = reinterpret_cast<uintptr_t>(op.dst);
     int64_t head = (int64_t)((16 - (d & 15)) & 15);
@@ -3655,15 +3670,23 @@ __global__ __launch_bounds__(256) void gather_ops_kernel(const GatherOp* __restr
     const uint8_t* __restrict__ s = op.src + head;
     uint8_t* __restrict__ o = op.dst + head;
     if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) {  // 16-B aligned source: dwordx4 loads, 4 in flight
-        const int64_t step = 16 * (int64_t)blockDim.x;
+        const int64_t step = 16 * (int64_t)T;
         int64_t k = 16 * (int64_t)t;
-        for (; k + 3 * step < body; k += 4 * step) {
+        for (; k + (D - 1) * step < body; k += D * step) {
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 v[4];
+            u32x4 v[D];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s + k + u * step));
+            for (int u = 0; u < D; ++u) {
+                const u32x4* a = reinterpret_cast<const u32x4*>(s + k + u * step);
+                if constexpr (NTL) v[u] = __builtin_nontemporal_load(a);
+                else v[u] = *a;
+            }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], reinterpret_cast<u32x4*>(o + k + u * step));
+            for (int u = 0; u < D; ++u) {
+                u32x4* a = reinterpret_cast<u32x4*>(o + k + u * step);
+                if constexpr (NTS) __builtin_nontemporal_store(v[u], a);
+                else *a = v[u];
+            }
         }
         for (; k < body; k += step)
             *reinterpret_cast<uint4*>(o + k) = *reinterpret_cast<const uint4*>(s + k);
@@ -3685,9 +3708,24 @@ __global__ __launch_bounds__(256) void gather_ops_kernel(const GatherOp* __restr
 
 hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(gather_ops_kernel, dim3(n), dim3(256), 0, s, ops);
+    hipLaunchKernelGGL((gather_ops_kernel_t<256, 4, true, true>), dim3(n), dim3(256), 0, s, ops);
     return hipGetLastError();
 }
+#ifdef RSH_KBENCH
+hipError_t launch_gather_ops_variant(int v, const GatherOp* ops, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    switch (v) {
+        case 1: hipLaunchKernelGGL((gather_ops_kernel_t<256, 8, true, true>), dim3(n), dim3(256), 0, s, ops); break;
+        case 2: hipLaunchKernelGGL((gather_ops_kernel_t<512, 4, true, true>), dim3(n), dim3(512), 0, s, ops); break;
+        case 3: hipLaunchKernelGGL((gather_ops_kernel_t<256, 4, false, true>), dim3(n), dim3(256), 0, s, ops); break;
+        case 4: hipLaunchKernelGGL((gather_ops_kernel_t<256, 4, false, false>), dim3(n), dim3(256), 0, s, ops); break;
+        case 5: hipLaunchKernelGGL((gather_ops_kernel_t<512, 8, true, true>), dim3(n), dim3(512), 0, s, ops); break;
+        case 6: hipLaunchKernelGGL((gather_ops_kernel_t<1024, 4, true, true>), dim3(n), dim3(1024), 0, s, ops); break;
+        default: hipLaunchKernelGGL((gather_ops_kernel_t<256, 4, true, true>), dim3(n), dim3(256), 0, s, ops); break;
+    }
+    return hipGetLastError();
+}
+#endif
 
 __global__ void table_insert_many_kernel(const TableEnt* __restrict__ ents, int hi) {
     if (hi) __builtin_amdgcn_s_setprio(3);

@@ -345,6 +345,8 @@ RSH_HD void md5_compress_asm4(Md5State& st, const uint32_t (&m)[16]) { md5_compr
 RSH_HD void md5_compress_asm16(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
 RSH_HD void md5_compress_k3s_8(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
 RSH_HD void md5_compress_k3s_16(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+RSH_HD void md5_compress_k3s_16_nonop(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
+RSH_HD void md5_compress_k3s_16_nop2(Md5State& st, const uint32_t (&m)[16]) { md5_compress(st, m); }
 #endif
 
 #if defined(__HIP__)

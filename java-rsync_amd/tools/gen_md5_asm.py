@@ -163,7 +163,7 @@ def main_k3(steps_per_block, nt):
     print("\n".join(out))
 
 
-def k3s_block(lo, hi, nt):
+def k3s_block(lo, hi, nt, nop_every=1):
     """k3 with K from an SGPR operand (VOP3 takes one SGPR): a + m + K in one v_add3_u32 without the 64 VGPRs of
     constants; the compiler materialises each K with an s_mov_b32 (SALU, beside the other wave's VALU).  kbench A/B."""
     lines = []
@@ -175,8 +175,9 @@ def k3s_block(lo, hi, nt):
                   f"v_bitop3_b32 {f}, %[{b}], %[{c}], %[{d}] bitop3:{bop(i)}",
                   f"v_add_u32 {t}, {t}, {f}",
                   f"v_alignbit_b32 {t}, {t}, {t}, {32 - S[i]}",
-                  f"v_add_u32 %[{a}], {t}, %[{b}]",
-                  "s_nop 0"]
+                  f"v_add_u32 %[{a}], {t}, %[{b}]"]
+        if nop_every and (i + 1) % nop_every == 0:
+            lines.append("s_nop 0")
     body = "\\n\\t".join(lines)
     ins = ", ".join([f'[m{w}] "v"(m[{w}])' for w in words] + [f'[k{i - lo}] "s"(0x{K[i]:08x}u)' for i in range(lo, hi)])
     tmps = ", ".join(f'[t{k}] "=&v"(t{k}), [f{k}] "=&v"(f{k})' for k in range(nt))
@@ -185,12 +186,12 @@ def k3s_block(lo, hi, nt):
             f'        : {ins});')
 
 
-def main_k3s(steps_per_block, nt):
-    out = [f"__device__ __forceinline__ void md5_compress_k3s_{steps_per_block}(Md5State& st, const uint32_t (&m)[16]) {{",
+def main_k3s(steps_per_block, nt, nop_every=1, suffix=""):
+    out = [f"__device__ __forceinline__ void md5_compress_k3s_{steps_per_block}{suffix}(Md5State& st, const uint32_t (&m)[16]) {{",
            "    uint32_t a = st.a, b = st.b, c = st.c, d = st.d;",
            "    uint32_t " + ", ".join(f"t{k}, f{k}" for k in range(nt)) + ";"]
     for lo in range(0, 64, steps_per_block):
-        out.append(k3s_block(lo, lo + steps_per_block, nt))
+        out.append(k3s_block(lo, lo + steps_per_block, nt, nop_every))
     out += ["    st.a += a;", "    st.b += b;", "    st.c += c;", "    st.d += d;", "}"]
     print("\n".join(out))
 
@@ -213,6 +214,8 @@ def main():
     main_k3(8, 4)
     main_k3s(8, 4)
     main_k3s(16, 4)
+    main_k3s(16, 4, 0, "_nonop")
+    main_k3s(16, 4, 2, "_nop2")
 
 
 if __name__ == "__main__":

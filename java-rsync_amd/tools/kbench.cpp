@@ -26,7 +26,61 @@
         }                                                                       \
     } while (0)
 
+// KBENCH_GATHER=<op bytes>: the Receiver's block gather (gather_ops_kernel) A/Bs instead: <MiB> copied from one buffer
+// to another as ops of that many bytes (shuffled order, as matched blocks arrive), variants of launch_gather_ops_variant;
+// GB/s counts the bytes read and written.
+static int gather_main(int argc, char** argv) {
+    const int64_t n = (int64_t)atoll(argv[1]) << 20;
+    const int64_t op = atoll(getenv("KBENCH_GATHER"));
+    const int reps = atoi(argv[4]);
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    uint8_t *src, *dst;
+    CK(hipMalloc(&src, n));
+    CK(hipMalloc(&dst, n));
+    CK(rsh::launch_fill_splitmix(src, n, 0x5EED, 0, s));
+    std::vector<rsh::GatherOp> ops;
+    for (int64_t o = 0; o < n; o += op) ops.push_back(rsh::GatherOp{src + o, dst + o, std::min(op, n - o)});
+    for (size_t i = ops.size(); i > 1; --i) std::swap(ops[i - 1], ops[(i * 2654435761u) % i]);
+    rsh::GatherOp* d_ops;
+    CK(hipMalloc(&d_ops, ops.size() * sizeof(rsh::GatherOp)));
+    CK(hipMemcpy(d_ops, ops.data(), ops.size() * sizeof(rsh::GatherOp), hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<uint64_t> a(1024), b(1024);
+    for (int k = 5; k < argc; ++k) {
+        const int v = atoi(argv[k]);
+        CK(hipMemset(dst, 0, n));
+        CK(rsh::launch_gather_ops_variant(v, d_ops, (uint32_t)ops.size(), s));
+        CK(hipStreamSynchronize(s));
+        bool same = true;
+        for (int64_t off : {(int64_t)0, n / 3, n - 8192}) {
+            CK(hipMemcpy(a.data(), src + off, 8192, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(b.data(), dst + off, 8192, hipMemcpyDeviceToHost));
+            same = same && a == b;
+        }
+        float best = 1e30f, tot = 0;
+        for (int r = 0; r < reps; ++r) {
+            CK(hipEventRecord(e0, s));
+            CK(rsh::launch_gather_ops_variant(v, d_ops, (uint32_t)ops.size(), s));
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            best = ms < best ? ms : best;
+            tot += ms;
+        }
+        printf("gather variant %d  n=%lld op=%lld  avg %.3f ms  best %.3f ms  %.1f GB/s (read+write; %.3f of 8 TB/s)  copy=%s\n",
+               v, (long long)n, (long long)op, tot / reps, best, 2.0 * n / (tot / reps / 1e3) / 1e9,
+               2.0 * n / (tot / reps / 1e3) / 8e12, same ? "ok" : "MISMATCH");
+        fflush(stdout);
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc >= 6 && getenv("KBENCH_GATHER")) return gather_main(argc, argv);
     if (argc < 6) {
         fprintf(stderr, "usage: kbench <MiB> <B> <dl> <reps> <variant>...\n");
         return 2;
