@@ -536,7 +536,12 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 // gcnt digest chunk 0 again and store nothing.
 // MODE != 0 (A/B and diagnostic forms: synthetic stage data, per-iteration drains or sleeps) exists in the kbench
 // build only (RSH_KBENCH); the product library instantiates MODE 0.
-template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false, bool GATHER = false>
+// WEAKW (kbench A/B): the weak sums from the MD5 message words already in registers instead of a second read of
+// the stage from LDS in the MFMA operand layout: per 64-B block, four v_mfma_i32_16x16x64_i8 with B = the lane's
+// own 16-byte quarter w of its block and A = rows that select one lane group each (row m reads lane group m & 3:
+// type m >> 2 = 0 ones, 1 the byte's offset 16 w + i in the block), all into one accumulator -- chunk n + 16 q's
+// block sum lands in lane n (element q), its weighted sum in lane n + 16.  Saves the 8 ds_read_b128 per stage.
+template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false, bool GATHER = false, bool WEAKW = false>
 __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
                                                              uint8_t* __restrict__ strong_out,
@@ -550,7 +555,7 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     constexpr int BUF = 64 * ROW;  // uint4 slots per LDS buffer
     constexpr int TAIL_PF = RSH_K1_TAIL_PF;
 #ifndef RSH_KBENCH
-    static_assert(MODE == 0 && MD5F == 8, "the product library runs the production K1 only");
+    static_assert(MODE == 0 && MD5F == 8 && !WEAKW, "the product library runs the production K1 only");
 #endif
     if constexpr (!MULTI && !GATHER) {
         // tail waves (blockIdx >= main_waves): one lane per chunk left over (a partial last wave, the short last
@@ -619,6 +624,22 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
             }
     }
     const int rdB = mfma_pi(l & 15) * ROW + mfma_sigma(l >> 4);
+    [[maybe_unused]] v4i32 wW[4];  // WEAKW: the A operand for block quarter w
+    [[maybe_unused]] v4i32 accW = {0, 0, 0, 0}, RW = {0, 0, 0, 0};
+    if constexpr (WEAKW) {
+        const int m = l & 15, q = l >> 4, type = m >> 2;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                uint32_t word = 0;
+                if (q == (m & 3) && type == 0) word = 0x01010101u;
+                else if (q == (m & 3) && type == 1)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) word |= (uint32_t)(16 * w + 4 * d + b) << (8 * b);
+                wW[w][d] = (int)word;
+            }
+    }
 
     uint4 q[2][8];  // load slots: stage s+1 and s+2 in flight while stage s computes
     uint4 Wa[4];    // words of the current stage's block 0 (then: the next stage's block 0)
@@ -670,6 +691,15 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         if constexpr (MD5F == 9) md5_k3_block(st, m, kv);
         else md5_stream_block<MD5F>(st, m);
     };
+    auto weak_words = [&](const uint4 (&w)[4]) __attribute__((always_inline)) {  // WEAKW: one 64-B block
+#pragma unroll
+        for (int e = 0; e < 4; ++e) RW[e] += accW[e];  // R += P_{b-1}
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const v4i32 b4 = {(int)w[k].x, (int)w[k].y, (int)w[k].z, (int)w[k].w};
+            accW = __builtin_amdgcn_mfma_i32_16x16x64_i8(wW[k], b4, accW, 0, 0, 0);
+        }
+    };
     auto weak_mfma = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) Racc[g] += acc[g][0];  // R += P_{s-1}
@@ -692,12 +722,14 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
             if (refill) load(q[P ^ 1], si + 3);
         }
         get_words(Wb, P, 1);
-        get_mfma(P);
+        if constexpr (!WEAKW) get_mfma(P);
         md5_block(Wa);
-        weak_mfma();
+        if constexpr (WEAKW) weak_words(Wa);
+        else weak_mfma();
         compiler_fence();
         if (has_next) get_words(Wa, P ^ 1, 0);
         md5_block(Wb);
+        if constexpr (WEAKW) weak_words(Wb);
         compiler_fence();
     };
 
@@ -743,7 +775,23 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         md5_compress(st, m);
     }
     int32_t s1, u;
-    {
+    if constexpr (WEAKW) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) RW[e] += accW[e];
+        const int n = l & 15, q = l >> 4;
+        int32_t tS[4], tR[4], tW[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            tS[e] = __shfl(accW[e], n, 64);
+            tR[e] = __shfl(RW[e], n, 64);
+            tW[e] = __shfl(accW[e], n + 16, 64);
+        }
+        const int32_t S = q == 0 ? tS[0] : q == 1 ? tS[1] : q == 2 ? tS[2] : tS[3];
+        const int32_t Rq = q == 0 ? tR[0] : q == 1 ? tR[1] : q == 2 ? tR[2] : tR[3];
+        const int32_t Wq = q == 0 ? tW[0] : q == 1 ? tW[1] : q == 2 ? tW[2] : tW[3];
+        s1 = S;
+        u = (int32_t)(64u * (2u * nst * (uint32_t)S - (uint32_t)Rq)) + Wq;
+    } else {
         int32_t s1g[4], ug[4];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
@@ -816,6 +864,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
 }
 bool tail_gather_on() { return opt(OPT_K1_GATHER) != 0; }  // 0: leftover chunks one per lane (options.h)
 #ifdef RSH_KBENCH
+// kbench A/B (variant 66): the weak sums from the MD5 words in registers (WEAKW)
+__global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_weakw_kernel(
+    const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
+    uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen) {
+    block_sums_pipe_body<8, true, true, 0, false, false, true>(data, B, dl, seed, weak_out, strong_out, abort_flag,
+                                                               abort_gen, nullptr, 0, 0, 0xFFFFFFFFu);
+}
 // kbench A/B (variant 61): MD5F == 9 holds the 64 K constants in VGPRs (176 + 64 registers, still 2 waves/SIMD)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void block_sums_pipe_k3_kernel(
     const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
@@ -825,159 +880,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
 }
 #endif
 
-#ifdef RSH_KBENCH  // not adopted: kbench only
-// ------------------------------------------------------------------------------------------------
-// K1 at 4 waves per SIMD (batched groups, one K1Group per wave).  A wave issues at most one VALU
-// instruction per ~2.7 SIMD slots of a full-rate op, so two waves leave a SIMD's VALU a quarter idle and
-// the half-rate rotate half idle (tools/op_rate.hip: SIMD cost per wave-instruction v_add_u32 2.69 at 2
-// waves, 2.01 at 4; v_alignbit_b32 4.79 / 3.39).  The pipelined kernel needs 176 VGPRs and two 9 KiB LDS
-// buffers (2 waves/SIMD); this one keeps one buffer and one stage of loads in flight so that four waves
-// fit (<= 128 VGPRs, 9 KiB LDS): the reads of stage s are issued before stage s + 1 overwrites the buffer
-// (a wave's LDS operations execute in order), and the other waves hide the latency the shallower
-// pipeline exposes.  Same data path and outputs as block_sums_pipe_kernel<.., MULTI = true>.
-// ------------------------------------------------------------------------------------------------
-template <bool ABORT>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) void block_sums_quad_kernel(
-    const K1Group* __restrict__ groups, uint32_t seed, const int* abort_flag, int abort_gen) {
-    constexpr int ROW = 9;
-    extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // one buffer: 64 rows of ROW slots
-    const int l = threadIdx.x;
-    const K1Group g = groups[blockIdx.x];
-    const uint8_t* gdata = g.data;
-    const uint32_t B = g.B, dl = g.dl;
-    if constexpr (ABORT) {
-        if (g.abort) abort_flag = g.abort;
-    }
-    const uint32_t nst = B >> 7;  // host guarantees nst >= 2
-    const int wr0 = (l >> 3) * ROW + (l & 7);
-    const int rd0 = l * ROW;
-    v4i32 wA[2];
-    v4i32 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-    int32_t Racc[4] = {0, 0, 0, 0};
-    {
-        const int row = l & 15, ks = l >> 4;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                uint32_t word = 0;
-                if (row == 0) word = 0x01010101u;
-                else if (row == 1)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) word |= (uint32_t)(16 * (4 * h + mfma_sigma(ks)) + 4 * w + b) << (8 * b);
-                wA[h][w] = (int)word;
-            }
-    }
-    const int rdB = mfma_pi(l & 15) * ROW + mfma_sigma(l >> 4);
-    uint4 q[8];
-    uint4 Wa[4], Wb[4];
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(gdata), 0, (int)(64 * B), 0x00020000);
-    const uint32_t lane_off = (uint32_t)(l >> 3) * B + 16u * (uint32_t)(l & 7);
-    auto load = [&](uint32_t stg) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const u32x4 t = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane_off + 128u * stg, (int)(j * 8u * B), 2);
-            q[j] = make_uint4(t.x, t.y, t.z, t.w);
-        }
-    };
-    auto put = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) lds_all[wr0 + j * 8 * ROW] = q[j];
-    };
-    auto get_words = [&](uint4 (&w)[4], int h) __attribute__((always_inline)) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w[k] = lds_all[rd0 + 4 * h + k];
-    };
-    Md5State st = md5_init();
-    auto md5_block = [&](const uint4 (&w)[4]) __attribute__((always_inline)) {
-        uint32_t m[16];
-        unpack(w, m);
-        md5_stream_block<8>(st, m);
-    };
-    // the weak-sum MFMAs of the stage in the buffer, operands read half by half (16 VGPRs at a time)
-    auto weak_mfma = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) Racc[g4] += acc[g4][0];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            uint4 Bv[4];
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) Bv[g4] = lds_all[16 * ROW * g4 + rdB + 4 * h];
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const v4i32 b4 = {(int)Bv[g4].x, (int)Bv[g4].y, (int)Bv[g4].z, (int)Bv[g4].w};
-                acc[g4] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wA[h], b4, acc[g4], 0, 0, 0);
-            }
-        }
-    };
-    load(0);
-    if constexpr (ABORT) {
-        int f0;
-        asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(f0) : "s"(abort_flag));
-        if (f0 == abort_gen) return;
-    }
-    put();
-    load(1);
-    compiler_fence();
-    get_words(Wa, 0);
-    [[maybe_unused]] int flag = 0;
-    for (uint32_t s = 0; s < nst; ++s) {
-        const bool has_next = s + 1 < nst;
-        if constexpr (ABORT) {
-            if ((s & 1) == 0) asm volatile("s_load_dword %0, %1, 0x0 glc" : "=s"(flag) : "s"(abort_flag));
-        }
-        get_words(Wb, 1);
-        weak_mfma();
-        compiler_fence();
-        if (has_next) {
-            put();  // stage s + 1 (its reads of stage s were issued above)
-            if (s + 2 < nst) load(s + 2);
-        }
-        compiler_fence();
-        md5_block(Wa);
-        compiler_fence();
-        if (has_next) get_words(Wa, 0);
-        md5_block(Wb);
-        compiler_fence();
-        if constexpr (ABORT) {
-            if (s & 1) {
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(flag));
-                if (flag == abort_gen) return;
-            }
-        }
-    }
-    {
-        const uint64_t bits = ((uint64_t)B + 4) * 8;
-        uint32_t m[16] = {seed, 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, (uint32_t)bits, (uint32_t)(bits >> 32)};
-        md5_compress(st, m);
-    }
-    int32_t s1, u;
-    {
-        int32_t s1g[4], ug[4];
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-            Racc[g4] += acc[g4][0];
-            s1g[g4] = acc[g4][0];
-            ug[g4] = (int32_t)(128u * (nst * (uint32_t)acc[g4][0] - (uint32_t)Racc[g4])) + acc[g4][1];
-        }
-        const int src = mfma_pi_inv(l & 15);
-        int32_t t1[4], tu[4];
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-            t1[g4] = __shfl(s1g[g4], src, 64);
-            tu[g4] = __shfl(ug[g4], src, 64);
-        }
-        const int gs = l >> 4;
-        s1 = gs == 0 ? t1[0] : gs == 1 ? t1[1] : gs == 2 ? t1[2] : t1[3];
-        u = gs == 0 ? tu[0] : gs == 1 ? tu[1] : gs == 2 ? tu[2] : tu[3];
-    }
-    const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
-    g.weak[l] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
-    store_digest(g.strong + (size_t)l * dl, st, dl);
-}
-
-#endif  // RSH_KBENCH
 
 #ifndef RSH_K1_SHIFT_VGPR
 #define RSH_K1_SHIFT_VGPR 256  // 2 waves/SIMD (the LDS ring and the MFMA tiles of the aligned kernel, plus the funnel)
@@ -1285,83 +1187,11 @@ hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const 
     return hipGetLastError();
 }
 
-#ifdef RSH_KBENCH  // not adopted: kbench only
-// ------------------------------------------------------------------------------------------------
-// K1 (LDS-DMA): as the coalesced kernel, but each stage goes HBM -> LDS directly with
-// global_load_lds_dwordx4 (no VGPR staging, no ds_write).  LDS-DMA writes lane l's 16 B at slot
-// base + l, so the lane -> (chunk, piece) mapping of each DMA instruction fixes the layout: in
-// instruction j lane l fetches chunk c = 8j + (l >> 3), piece q = (l & 7) ^ ((c >> 1) & 7), which puts
-// (c, q) at slot 8c + (q ^ ((c >> 1) & 7)): the transposed ds_read_b128 (lane c, piece k) then hits 16
-// distinct bank quads in every 16-lane group.  S stages of 8 KiB ring per wave.
-// ------------------------------------------------------------------------------------------------
-typedef __attribute__((address_space(3))) void lds_void_t;
-
-template <int S>
-__global__ __launch_bounds__(64) void block_sums_dma_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
-                                                            uint32_t seed, int32_t* __restrict__ weak_out,
-                                                            uint8_t* __restrict__ strong_out) {
-    extern __shared__ __attribute__((aligned(16))) uint4 lds_ring[];  // S * 512 slots
-    const int l = threadIdx.x;
-    const uint32_t c0 = blockIdx.x * 64u;
-    const uint32_t nst = B >> 7;
-    const uint8_t* wbase = data + (size_t)c0 * B;
-    // per-lane byte offsets for even / odd DMA instructions (the swizzle depends on j & 1 only)
-    const uint32_t row = (uint32_t)(l >> 3) * B;
-    const uint32_t voff0 = row + 16u * ((uint32_t)(l & 7) ^ (uint32_t)((l >> 4) & 7));
-    const uint32_t voff1 = row + 16u * ((uint32_t)(l & 7) ^ (uint32_t)((4 + (l >> 4)) & 7));
-    const size_t jstride = (size_t)8 * B;
-    auto issue = [&](uint32_t st) {
-        uint4* ring = lds_ring + (st % S) * 512;
-        const uint8_t* g = wbase + 128 * (size_t)st;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            __builtin_amdgcn_global_load_lds(g + j * jstride + ((j & 1) ? voff1 : voff0),
-                                             (lds_void_t*)(ring + 64 * j), 16, 0, 0);
-    };
-    const int sw = (l >> 1) & 7;
-#pragma unroll
-    for (int d = 0; d < S; ++d)
-        if ((uint32_t)d < nst) issue(d);
-
-    Md5State st = md5_init();
-    int32_t s1 = 0, u = 0;
-    for (uint32_t s = 0; s < nst; ++s) {
-        // stage s landed once at most (S - 1) later stages (8 DMA instructions each) are outstanding
-        const uint32_t ahead = nst - 1 - s < (uint32_t)(S - 1) ? nst - 1 - s : (uint32_t)(S - 1);
-        switch (ahead) {
-            case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-            case 1: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-            case 2: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-            default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-        }
-        const uint4* ring = lds_ring + (s % S) * 512 + 8 * l;
-        uint4 r[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) r[k] = ring[k ^ sw];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot free before it is refilled
-        if (s + S < nst) issue(s + S);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            uint32_t m[16];
-            unpack(*reinterpret_cast<const uint4(*)[4]>(&r[4 * h]), m);
-            weak_block(m, s1, u, 128 * s + 64 * h);
-            md5_compress(st, m);
-        }
-    }
-    {
-        const uint64_t bits = ((uint64_t)B + 4) * 8;
-        uint32_t m[16] = {seed, 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, (uint32_t)bits, (uint32_t)(bits >> 32)};
-        md5_compress(st, m);
-    }
-    const uint32_t c = c0 + l;
-    const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
-    weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
-    store_digest(strong_out + (size_t)c * dl, st, dl);
-}
-
-#endif  // RSH_KBENCH
 
 #ifdef RSH_KBENCH
+template <int S>
+__global__ void block_sums_dma_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed,
+                                      int32_t* __restrict__ weak_out, uint8_t* __restrict__ strong_out);  // device_kbench.inc
 // MD5 step form of the coalesced K1 A/Bs: 0 compiler, 1 one asm statement per step, 2 generated blocks
 // (tools/gen_md5_asm.py; the production pipelined K1 uses 2)
 constexpr int kMd5Form = 2;
@@ -1700,6 +1530,10 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     hipLaunchKernelGGL((block_sums_pipe_kernel<10, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
                                        d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
                     break;
+                case 66:  // A/B: weak sums from the MD5 words in registers (no MFMA-operand LDS reads), abortable
+                    hipLaunchKernelGGL((block_sums_pipe_weakw_kernel), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
+                    break;
                 case 64:  // ... without the s_nop after each step
                     hipLaunchKernelGGL((block_sums_pipe_kernel<12, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
                                        d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
@@ -1973,71 +1807,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
     block_sums_pipe_body<8, true, true, 0, true>(nullptr, 0u, 0u, seed, nullptr, nullptr, abort_flag, abort_gen, groups);
 }
 #ifdef RSH_KBENCH
-// kbench A/B (variant 1006): the batched launch as persistent waves -- a grid of (CUs x 8) waves, each taking
-// groups i, i + grid, ... (then the lane waves) one after the other, instead of one dispatched workgroup per group.
-template <int ALIGN>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void block_sums_pipe_persist_kernel(
-    const K1Group* __restrict__ groups, uint32_t ngroups, const K1Lane* __restrict__ lanes, uint32_t nlanes,
-    uint32_t seed, const int* abort_flag, int abort_gen) {
-    for (uint32_t i = blockIdx.x; i < ngroups + nlanes; i += gridDim.x) {
-        if (i >= ngroups) {
-            const K1Lane e = lanes[i - ngroups];
-            const uint32_t c = e.c_first + threadIdx.x;
-            if (c < e.nchunks)
-                lane_chunk_sums<ALIGN == 1 ? 0 : ALIGN, ALIGN == 16 ? 4 : ALIGN == 4 ? 2 : 4, ALIGN != 1>(
-                    e.data, e.n, e.B, c, e.dl, seed, e.weak, e.strong);
-            continue;
-        }
-        const K1Group g = groups[i];
-        if (g.count < 64) {
-            block_sums_pipe_body<8, true, true, 0, false, true>(g.data, g.B, g.dl, seed, g.weak, g.strong,
-                                                               g.abort ? g.abort : abort_flag, abort_gen, nullptr, 0, 0,
-                                                               0xFFFFFFFFu, nullptr, g.count);
-            continue;
-        }
-        block_sums_pipe_body<8, true, true, 0, true>(nullptr, 0u, 0u, seed, nullptr, nullptr, abort_flag, abort_gen,
-                                                     groups, 0, 0, 0xFFFFFFFFu, nullptr, 0, i);
-    }
-}
-hipError_t launch_block_sums_batch_persist(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes,
-                                           uint32_t nlanes, int lane_align, uint32_t seed_word, hipStream_t s) {
-    const size_t lb = 2 * 64 * 9 * sizeof(uint4);
-    const int* abort_flag = never_word();
-    int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-    uint32_t waves = (uint32_t)cus * 8u;
-    if (const char* e = getenv("KBENCH_PERSIST_WAVES")) waves = (uint32_t)atoi(e);
-    const uint32_t total = ngroups + nlanes;
-    const dim3 grid(std::min(total, std::max(1u, waves)));
-    if (lane_align == 16)
-        hipLaunchKernelGGL((block_sums_pipe_persist_kernel<16>), grid, dim3(64), lb, s, d_groups, ngroups, d_lanes, nlanes,
-                           seed_word, abort_flag, -1);
-    else if (lane_align == 4)
-        hipLaunchKernelGGL((block_sums_pipe_persist_kernel<4>), grid, dim3(64), lb, s, d_groups, ngroups, d_lanes, nlanes,
-                           seed_word, abort_flag, -1);
-    else
-        hipLaunchKernelGGL((block_sums_pipe_persist_kernel<1>), grid, dim3(64), lb, s, d_groups, ngroups, d_lanes, nlanes,
-                           seed_word, abort_flag, -1);
-    return hipGetLastError();
-}
-
-bool batch_quad() {  // RSH_K1_QUAD=1 (kbench A/B): the batched groups at 4 waves/SIMD
-    static const bool v = getenv("RSH_K1_QUAD") && atoi(getenv("RSH_K1_QUAD")) != 0;
-    return v;
-}
-
-hipError_t launch_block_sums_batch_quad(const K1Group* d_groups, uint32_t ngroups, uint32_t seed_word, hipStream_t s,
-                                        const int* abort_flag, int abort_gen) {
-    if (ngroups == 0) return hipSuccess;
-    const size_t lb = 64 * 9 * sizeof(uint4);
-    if (!abort_flag && (abort_flag = never_word()) != nullptr) abort_gen = -1;
-    if (abort_flag)
-        hipLaunchKernelGGL((block_sums_quad_kernel<true>), dim3(ngroups), dim3(64), lb, s, d_groups, seed_word, abort_flag,
-                           abort_gen);
-    else
-        hipLaunchKernelGGL((block_sums_quad_kernel<false>), dim3(ngroups), dim3(64), lb, s, d_groups, seed_word, nullptr, 0);
-    return hipGetLastError();
-}
+#include "device_kbench.inc"
 #else
 static bool batch_quad() { return false; }
 #endif

@@ -20,6 +20,9 @@
 #                instruction mix and LDS bank conflicts
 #   kbench-k1    kbench: the K1 at B = 128 KiB and 8 KiB, the batched forms (1002, 1005, 1006)
 #   e2e          java-rsync_amd/tools/e2e.py at config 5 (16 GiB from host memory)
+#   kb-ab        kbench A/Bs of KB_VARIANTS (default: production 1000 against the round-4 K1 forms) at the headline
+#                shape, interleaved, then one clock pass (GRBM_GUI_ACTIVE) over the same variants
+#   kb-gather    kbench's Receiver block-gather A/Bs (KBENCH_GATHER: 4 GiB as 1 MiB ops)
 #   e2e4         java-rsync_amd/tools/e2e_config4.py: config 4's shard (128 x 128 MiB) from host memory, the segment
 #                entry points against 128 single-file calls
 #   config3      the config-3 line: a 64 GiB identical pair resident in HBM, B = 131072 (the Sender's limit), dl = 5
@@ -49,6 +52,14 @@ for step in "$@"; do
             tests/test_gpu_fullsize.py -k "batch or config4" > "$O/batch_tests.log" 2>&1 ;;
         pytest) run 900 python -u -m pytest -m gpu -x -v --timeout 400 --timeout-method thread $PYTEST_ARGS \
             > "$O/pytest.log" 2>&1 ;;
+        kb-ab)
+            V=${KB_VARIANTS:-"1000 66 64 65"}
+            run 240 "$K" 16384 131072 4 6 $V $V $V > "$O/kb_ab.log" 2>&1
+            (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace \
+                -d "$O/kb_ab_clock" -o run --output-format csv -- "$K" 16384 131072 4 5 $V > "$O/kb_ab_clock.log" 2>&1) \
+                || exit 1
+            python3 java-rsync_amd/tools/clock_summary.py "$O/kb_ab_clock" > "$O/kb_ab_clock.txt" 2>&1 ;;
+        kb-gather) KBENCH_GATHER=1048576 run 180 "$K" 4096 0 0 5 0 1 2 3 4 5 6 0 1 2 3 4 5 6 > "$O/kb_gather.log" 2>&1 ;;
         e2e4) run 900 python java-rsync_amd/tools/e2e_config4.py > "$O/e2e_config4.json" 2> "$O/e2e_config4.err" ;;
         smoke) run 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.log" 2>&1 ;;
         bench) run 300 python bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
