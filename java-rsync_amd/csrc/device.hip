@@ -536,12 +536,13 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 // gcnt digest chunk 0 again and store nothing.
 // MODE != 0 (A/B and diagnostic forms: synthetic stage data, per-iteration drains or sleeps) exists in the kbench
 // build only (RSH_KBENCH); the product library instantiates MODE 0.
-// WEAKW (kbench A/B): the weak sums from the MD5 message words already in registers instead of a second read of
+// WEAKW (production since round 4): the weak sums from the MD5 message words already in registers instead of a second read of
 // the stage from LDS in the MFMA operand layout: per 64-B block, four v_mfma_i32_16x16x64_i8 with B = the lane's
 // own 16-byte quarter w of its block and A = rows that select one lane group each (row m reads lane group m & 3:
 // type m >> 2 = 0 ones, 1 the byte's offset 16 w + i in the block), all into one accumulator -- chunk n + 16 q's
-// block sum lands in lane n (element q), its weighted sum in lane n + 16.  Saves the 8 ds_read_b128 per stage.
-template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false, bool GATHER = false, bool WEAKW = false>
+// block sum lands in lane n (element q), its weighted sum in lane n + 16.  Saves the 8 ds_read_b128 per stage: the
+// same cycles at a higher clock, 2.5 % less time (kbench 66 vs 67, profiles/r4/r4e_kbench_weakw_k3s*).
+template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false, bool GATHER = false, bool WEAKW = true>
 __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
                                                              uint8_t* __restrict__ strong_out,
@@ -555,7 +556,7 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     constexpr int BUF = 64 * ROW;  // uint4 slots per LDS buffer
     constexpr int TAIL_PF = RSH_K1_TAIL_PF;
 #ifndef RSH_KBENCH
-    static_assert(MODE == 0 && MD5F == 8 && !WEAKW, "the product library runs the production K1 only");
+    static_assert(MODE == 0 && MD5F == 8 && WEAKW, "the product library runs the production K1 only");
 #endif
     if constexpr (!MULTI && !GATHER) {
         // tail waves (blockIdx >= main_waves): one lane per chunk left over (a partial last wave, the short last
@@ -864,7 +865,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
 }
 bool tail_gather_on() { return opt(OPT_K1_GATHER) != 0; }  // 0: leftover chunks one per lane (options.h)
 #ifdef RSH_KBENCH
-// kbench A/B (variant 66): the weak sums from the MD5 words in registers (WEAKW)
+// kbench A/B (variant 67): round 3's production form, the weak-sum MFMA operands read from LDS (WEAKW = false)
+__global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_ldsw_kernel(
+    const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
+    uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen) {
+    block_sums_pipe_body<8, true, true, 0, false, false, false>(data, B, dl, seed, weak_out, strong_out, abort_flag,
+                                                                abort_gen, nullptr, 0, 0, 0xFFFFFFFFu);
+}
+// kbench A/B (variant 66): the weak sums from the MD5 words in registers (WEAKW; the production form since round 4)
 __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_weakw_kernel(
     const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
     uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen) {
@@ -1532,6 +1540,10 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                     break;
                 case 66:  // A/B: weak sums from the MD5 words in registers (no MFMA-operand LDS reads), abortable
                     hipLaunchKernelGGL((block_sums_pipe_weakw_kernel), dim3(waves), dim3(64), 2 * wave_lds, s,
+                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
+                    break;
+                case 67:  // A/B: round 3's production K1 (weak-sum MFMA operands from LDS), abortable
+                    hipLaunchKernelGGL((block_sums_pipe_ldsw_kernel), dim3(waves), dim3(64), 2 * wave_lds, s,
                                        d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
                     break;
                 case 64:  // ... without the s_nop after each step
@@ -2604,18 +2616,10 @@ __device__ __forceinline__ bool kslots_has(const unsigned long long* __restrict_
 // key still displaced after the insertion's bound (tables near or above 32768 distinct keys) marks the set
 // incomplete, and the walk then confirms every key in the chunk index instead.
 constexpr int CHAIN_CK_BUCKETS = 4096;
-// In front of it, a one-read bit filter: word (k * phi) >> 20 of 4096 (16 KiB, the word index is the key's first cuckoo
-// bucket) with two bits of the same product set per key.  Config 4's 16384 keys leave ~5 % of absent keys passing it,
-// so a tile's lookups cost one 4-byte LDS read per position and the two 16-byte cuckoo reads only for survivors
-// (r3ze: the cuckoo reads' bank conflicts were half the walk's LDS cycles).
-constexpr int CHAIN_BF_WORDS = 4096;
-__device__ __forceinline__ uint32_t chain_ck_mix(uint32_t k) { return k * 0x9E3779B1u; }
-__device__ __forceinline__ uint32_t chain_bf_mask(uint32_t x) { return (1u << ((x >> 15) & 31u)) | (1u << ((x >> 10) & 31u)); }
-__device__ __forceinline__ uint32_t chain_ck_h1(uint32_t k) { return chain_ck_mix(k) >> 20; }
+__device__ __forceinline__ uint32_t chain_ck_h1(uint32_t k) { return (k * 0x9E3779B1u) >> 20; }
 __device__ __forceinline__ uint32_t chain_ck_h2(uint32_t k) { return CHAIN_CK_BUCKETS + (((k ^ (k >> 15)) * 0x85EBCA77u) >> 20); }
 struct ChainKeySet {
     uint4* b;      // 2 * CHAIN_CK_BUCKETS buckets
-    uint32_t* bf;  // CHAIN_BF_WORDS filter words
     int32_t* has0;  // key 0 present
     int32_t* full;  // some key found no slot: lookups are not exact
 };
@@ -2624,8 +2628,6 @@ __device__ __forceinline__ void chain_ck_insert(const ChainKeySet& ks, uint32_t 
         *ks.has0 = 1;
         return;
     }
-    const uint32_t x = chain_ck_mix(k);
-    atomicOr(ks.bf + (x >> 20), chain_bf_mask(x));
     // cuckoo insertion: a free slot of the key's bucket in table w, else displace one of that bucket's keys and
     // carry it to its bucket in the other table (every key lives in its own h1 or h2 bucket)
     uint32_t cur = k;
@@ -2661,38 +2663,15 @@ __device__ __forceinline__ int chain_first_hit16(const unsigned long long* __res
     // free: two 16-byte reads and eight compares per key (a wave's lanes would take every branch anyway)
     if (*set.full == 0) {
         const bool has0 = *set.has0 != 0;
-        // the bit filter: one 4-byte read per key, the 16 reads in flight together
-        uint32_t w[PROBE_PPT];
-#pragma unroll
-        for (int i = 0; i < PROBE_PPT; ++i) w[i] = set.bf[chain_ck_mix(keys[i]) >> 20];
-        uint32_t pass = 0, m = 0;
+        uint32_t m = 0;
 #pragma unroll
         for (int i = 0; i < PROBE_PPT; ++i) {
-            const uint32_t k = keys[i], bm = chain_bf_mask(chain_ck_mix(k));
-            if (k != 0u) pass |= (uint32_t)((w[i] & bm) == bm) << i;
-            else m |= (uint32_t)has0 << i;  // key 0 has its own flag (exact)
-        }
-        pass &= valid;
-        // the exact lookup for the survivors only (a lane with none reads nothing), 4 keys' reads in flight at a time
-#pragma unroll
-        for (int g = 0; g < PROBE_PPT; g += 4) {
-            if (((pass >> g) & 15u) == 0u) continue;
-            uint4 x[4], y[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                x[j] = y[j] = make_uint4(0u, 0u, 0u, 0u);
-                if ((pass >> (g + j)) & 1u) {
-                    x[j] = set.b[chain_ck_h1(keys[g + j])];
-                    y[j] = set.b[chain_ck_h2(keys[g + j])];
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t k = keys[g + j];
-                const bool in = (x[j].x == k) | (x[j].y == k) | (x[j].z == k) | (x[j].w == k) | (y[j].x == k) |
-                                (y[j].y == k) | (y[j].z == k) | (y[j].w == k);
-                m |= (uint32_t)(in && ((pass >> (g + j)) & 1u)) << (g + j);
-            }
+            const uint32_t k = keys[i];
+            const uint4 x = set.b[chain_ck_h1(k)], y = set.b[chain_ck_h2(k)];
+            const bool in = (x.x == k) | (x.y == k) | (x.z == k) | (x.w == k) | (y.x == k) | (y.y == k) | (y.z == k) |
+                            (y.w == k);
+            m |= (uint32_t)(k != 0u ? in : has0) << i;
+            if ((i & 3) == 3) asm volatile("" ::: "memory");  // 4 keys' reads in flight at a time (registers)
         }
         m &= valid;
         return m ? __builtin_ctz(m) : -1;
@@ -2748,7 +2727,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_any;                  // some chunk carries the stale digest
     __shared__ int32_t s_seg[CHAIN_SEGS][4];   // wide tiles: the exscan at each block's first lane
     __shared__ uint4 s_ck[2 * CHAIN_CK_BUCKETS];  // the table's keys (ChainKeySet)
-    __shared__ uint32_t s_bf[CHAIN_BF_WORDS];     // ... and their bit filter
     __shared__ int32_t s_ck_has0, s_ck_full;
     __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
@@ -2764,7 +2742,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const int64_t last = n - S, nB = n - B;
     const int64_t na = phase == 0 ? F.na_a : F.na, nflags = na < C ? na : C;
     const bool wide = (B % CHAIN_PPT) == 0 && B >= 512 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
-    const ChainKeySet kset{s_ck, s_bf, &s_ck_has0, &s_ck_full};
+    const ChainKeySet kset{s_ck, &s_ck_has0, &s_ck_full};
     int64_t s = out->s, m = out->m;
     // The key set (~C LDS inserts, tens of microseconds) only if the walk may search: a walk that starts aligned on
     // an unbroken run of chain flags up to the last window with a chunk (an identical file, or its rest after the
@@ -2802,7 +2780,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     }
     if (kset_built) {
         for (int i = t; i < 2 * CHAIN_CK_BUCKETS; i += CHAIN_THREADS) s_ck[i] = make_uint4(0u, 0u, 0u, 0u);
-        for (int i = t; i < CHAIN_BF_WORDS; i += CHAIN_THREADS) s_bf[i] = 0u;
         if (t == 0) s_ck_has0 = s_ck_full = 0;
         __syncthreads();
         for (int64_t c = t; c < C; c += CHAIN_THREADS) chain_ck_insert(kset, (uint32_t)F.table_weak[c]);
@@ -2951,8 +2928,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 ++tiles;
                 const int64_t tt0 = (int64_t)wall_clock64();
                 const int64_t kb0 = q0 / B, o0 = kb0 * B;
-                // the lane's bytes and anchor first: their loads are in flight while the block's head is reduced
-                // (one global round trip per tile instead of two)
+                int32_t head[4] = {0, 0, 0, 0};
+                if (q0 > o0) {
+                    range_sums(F.data, n, o0, q0, o0, head[0], head[1]);
+                    range_sums(F.data, n, o0 + B, q0 + B, o0, head[2], head[3]);
+                    block_reduce<4>(head, sh);
+                }
                 const int64_t p0 = q0 + (int64_t)t * CHAIN_PPT;
                 const int64_t kb = p0 / B, o = kb * B;
                 uint32_t xa[2][4], xb[2][4];
@@ -2962,12 +2943,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 load16(F.data, n, p0 + B + 16, xb[1]);
                 const bool live = p0 <= stop && p0 <= lim_spec && p0 + CHAIN_PPT > a;
                 const int32_t To = live ? F.aw[kb] : 0;
-                int32_t head[4] = {0, 0, 0, 0};
-                if (q0 > o0) {
-                    range_sums(F.data, n, o0, q0, o0, head[0], head[1]);
-                    range_sums(F.data, n, o0 + B, q0 + B, o0, head[2], head[3]);
-                    block_reduce<4>(head, sh);
-                }
                 int32_t pre[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh)
@@ -3435,7 +3410,7 @@ hipError_t launch_window_weak(const ScanFile* files, const GatherEnt* ents, uint
 }
 
 // D dwordx4 loads in flight per thread before their stores; NTL / NTS: non-temporal loads / stores.  The production
-// form is <256, 4, true, true>; the others are kbench A/Bs (KBENCH_GATHER).
+// form is <1024, 4, true, true>; the others are kbench A/Bs (KBENCH_GATHER).
 template <int T, int D, bool NTL, bool NTS>
 __global__ __launch_bounds__(T) void gather_ops_kernel_t(const GatherOp* __restrict__ ops) {
     const GatherOp op = ops[blockIdx.x];
@@ -3486,7 +3461,9 @@ __global__ __launch_bounds__(T) void gather_ops_kernel_t(const GatherOp* __restr
 
 hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL((gather_ops_kernel_t<256, 4, true, true>), dim3(n), dim3(256), 0, s, ops);
+    // 1024 threads per 1 MiB op (16 waves per CU in flight): 0.754 of the 8 TB/s peak (read + write) against 0.680 for
+    // 256 threads, kbench KBENCH_GATHER (profiles/r4/r4e_kbench_gather.log)
+    hipLaunchKernelGGL((gather_ops_kernel_t<1024, 4, true, true>), dim3(n), dim3(1024), 0, s, ops);
     return hipGetLastError();
 }
 #ifdef RSH_KBENCH
