@@ -1197,6 +1197,9 @@ hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const 
 
 
 #ifdef RSH_KBENCH
+__global__ void block_sums_direct_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed,
+                                         int32_t* __restrict__ weak_out, uint8_t* __restrict__ strong_out,
+                                         const int* abort_flag, int abort_gen);  // device_kbench.inc
 template <int S>
 __global__ void block_sums_dma_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed,
                                       int32_t* __restrict__ weak_out, uint8_t* __restrict__ strong_out);  // device_kbench.inc
@@ -1545,6 +1548,10 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                 case 67:  // A/B: round 3's production K1 (weak-sum MFMA operands from LDS), abortable
                     hipLaunchKernelGGL((block_sums_pipe_ldsw_kernel), dim3(waves), dim3(64), 2 * wave_lds, s,
                                        d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
+                    break;
+                case 68:  // A/B: no LDS -- per-lane loads into registers, weak sums from the MD5 words
+                    hipLaunchKernelGGL(block_sums_direct_kernel, dim3(waves), dim3(64), 0, s, d_data, B, dl, seed_word,
+                                       d_weak, d_strong, never_word(), -1);
                     break;
                 case 64:  // ... without the s_nop after each step
                     hipLaunchKernelGGL((block_sums_pipe_kernel<12, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
