@@ -92,6 +92,10 @@ struct BatchState {
     // speculation's flags kernel done on the aux stream (the walk reads the device flags and sums)
     DevBuf kslots;
     PinnedBuf h_kents, h_chain, h_chain_out, h_chain_ev;
+    // the phase-0 hit map (device.h ChainHelp): the files' shared map state (reset from pinned staging before each
+    // launch) and the map words (generation-tagged: zeroed once when allocated, never cleared between scans)
+    DevBuf chain_help, chain_map;
+    PinnedBuf h_chain_help;
     hipEvent_t ev_fk = nullptr;
     hipEvent_t ev_ch0 = nullptr, ev_ch1 = nullptr;  // around the walk (trace)
     hipEvent_t ev_fa = nullptr, ev_wa = nullptr;    // two-phase walk: prefix flags done, phase-0 walk done
@@ -120,7 +124,9 @@ struct BatchState {
         for (hipEvent_t e : {ev_fk, ev_ch0, ev_ch1, ev_fa, ev_wa})
             if (e) (void)hipEventDestroy(e);
         kslots.release();
-        for (PinnedBuf* b : {&h_kents, &h_chain, &h_chain_out, &h_chain_ev}) b->release();
+        for (PinnedBuf* b : {&h_kents, &h_chain, &h_chain_out, &h_chain_ev, &h_chain_help}) b->release();
+        chain_help.release();
+        chain_map.release();
         h_ggroups.release();
         h_glanes.release();
         h_sgroups.release();
@@ -1046,16 +1052,45 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         ChainFile* cf = S->h_chain.as<ChainFile>();
         ChainOut* co = S->h_chain_out.as<ChainOut>();
         rsh_event* ce = S->h_chain_ev.as<rsh_event>();
+        // the phase-0 hit map: each file whose walk may search tile by tile (wide tiles: B a multiple of 32, >= 512)
+        // gets words for the positions [0, hend) its phase-0 searches may reach, if they all fit the budget
+        std::vector<int64_t> map_off((size_t)NF + 1, 0);
+        const int64_t helpers_opt = opt(OPT_CHAIN_HELPERS);
+        bool map_on = two_phase && helpers_opt != 0;
+        for (int32_t f = 0; map_on && f < NF; ++f) {
+            const FileScan& fs = files[(size_t)f];
+            const bool wide = fs.B >= 512 && fs.B % 32 == 0 && CHAIN_TILE / fs.B + 2 <= CHAIN_SEGS;
+            const int64_t hend = std::min<int64_t>(fs.na_a * fs.B, fs.n - fs.B + 1);
+            map_off[(size_t)f + 1] = map_off[(size_t)f] + (wide && fs.C > 0 && hend > 0 ? (hend + 31) / 32 : 0);
+        }
+        map_on = map_on && map_off[(size_t)NF] > 0 && map_off[(size_t)NF] * 8 <= opt(OPT_CHAIN_MAP_BYTES);
+        if (map_on) {
+            const size_t words = (size_t)map_off[(size_t)NF];
+            if (words * 8 > S->chain_map.cap) {
+                RSH_BHIP(S->chain_map.ensure(words * 8));
+                RSH_BHIP(hipMemsetAsync(S->chain_map.p, 0, S->chain_map.cap, st));  // no stale generation
+            }
+            RSH_BHIP(S->chain_help.ensure((size_t)NF * sizeof(ChainHelp)));
+            RSH_BHIP(S->h_chain_help.ensure((size_t)NF * sizeof(ChainHelp)));
+        }
+        ChainHelp* chh = map_on ? S->h_chain_help.as<ChainHelp>() : nullptr;
         for (int32_t f = 0; f < NF; ++f) {
             FileScan& fs = files[(size_t)f];
             co[f] = ChainOut{};
+            const int64_t mw = map_on ? map_off[(size_t)f + 1] - map_off[(size_t)f] : 0;
+            const int64_t hend = mw > 0 ? std::min<int64_t>(fs.na_a * fs.B, fs.n - fs.B + 1) : 0;
             cf[f] = ChainFile{fs.d_src, fs.n, (uint32_t)fs.B, fs.C, fs.dl, jobs[fs.job].h.remainder,
                               fs.ns - 1, S->kslots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.d_strong,
                               S->src_weak.as<int32_t>() + fs.off_na, S->src_strong.as<uint8_t>() + fs.off_as,
                               S->flags.as<uint8_t>() + fs.off_nf, fs.na, fs.na_a,
                               two_phase ? S->file_abort + f : nullptr, ce + (int64_t)f * kChainEvents, kChainEvents,
-                              seed_word(seed), co + f};
+                              seed_word(seed), co + f,
+                              mw > 0 ? S->chain_map.as<unsigned long long>() + map_off[(size_t)f] : nullptr, hend};
+            if (chh) chh[f] = ChainHelp{(int32_t)((hend + CHAIN_MAP_SEG - 1) / CHAIN_MAP_SEG), 0, 1, 0, 0, 0, 0, 0, INT64_MAX};
         }
+        const uint32_t n_help = !map_on ? 0u
+                                : helpers_opt > 0 ? (uint32_t)helpers_opt
+                                                  : (uint32_t)std::max<int64_t>(0, (int64_t)c->n_cu - NF);
         const bool tr = opt(OPT_SCAN_TRACE) != 0;
         if (tr) {  // the walks' own duration (trace only)
             for (hipEvent_t* e : {&S->ev_ch0, &S->ev_ch1})
@@ -1107,7 +1142,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             RSH_BHIP(hipStreamWaitEvent(st, S->ev_fa, 0));
             const int gen_b = ++c->gen;
             if (tr) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
-            RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, 0, gen_b));
+            if (map_on)
+                RSH_BHIP(hipMemcpyAsync(S->chain_help.p, chh, (size_t)NF * sizeof(ChainHelp), hipMemcpyHostToDevice, st));
+            RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, 0, gen_b, map_on ? S->chain_help.as<ChainHelp>() : nullptr,
+                                          n_help));
             RSH_BHIP(hipEventRecord(S->ev_wa, st));
             // the rest of the speculation after the walks (the groups of files they finished stop at once), or
             // (option batch_chain_overlap) beside them: no gap after the prefix's K1, but the walks share the chip
@@ -1206,10 +1244,11 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             float kms = 0.f, wams = 0.f;
             if (S->ev_ch0 && S->ev_ch1) (void)hipEventElapsedTime(&kms, S->ev_ch0, S->ev_ch1);
             if (two_phase && S->ev_ch0 && S->ev_wa) (void)hipEventElapsedTime(&wams, S->ev_ch0, S->ev_wa);
-            int64_t tsum = 0, esum = 0, dsum = 0, psum = 0, asum = 0;
+            int64_t tsum = 0, esum = 0, dsum = 0, psum = 0, asum = 0, msum = 0;
             int32_t tmax = 0, emax = 0, fmax = 0;
             for (int32_t f = 0; f < NF; ++f) {
                 tsum += co[f].tiles;
+                msum += co[f].mapped;
                 if (co[f].tiles > tmax) tmax = co[f].tiles, fmax = f;
                 esum += co[f].events;
                 dsum += co[f].digests;
@@ -1217,14 +1256,32 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 asum += co[f].aborted;
                 emax = std::max<int32_t>(emax, (int32_t)co[f].events);
             }
-            fprintf(stderr, "[rsh-batch] chain walks done at %.3f ms (walks %.3f ms, phase 0 %.3f ms; tiles %lld, max %d per file; events "
-                    "%lld, max %d; %lld windows digested, %lld files poisoned, %lld speculations stopped at the prefix): %d of %d "
-                    "files left to the resolvers\n", ms_since(t0), kms, wams, (long long)tsum, tmax, (long long)esum, emax,
+            fprintf(stderr, "[rsh-batch] chain walks done at %.3f ms (walks %.3f ms, phase 0 %.3f ms; tiles %lld (%lld from the hit "
+                    "map), max %d per file; events %lld, max %d; %lld windows digested, %lld files poisoned, %lld speculations "
+                    "stopped at the prefix): %d of %d files left to the resolvers\n", ms_since(t0), kms, wams, (long long)tsum,
+                    (long long)msum, tmax, (long long)esum, emax,
                     (long long)dsum, (long long)psum, (long long)asum, left, NF);
             const ChainOut& x = co[fmax];  // the walk with the most tiles: where its time went (10 ns ticks)
-            fprintf(stderr, "[rsh-batch]   file %d: walk %.1f us = tiles %.1f (table checks %.1f) + events %.1f (digests %.1f)"
-                    " + other\n", fmax, x.t_total / 100.0, x.t_tiles / 100.0, x.t_check / 100.0, x.t_event / 100.0,
+            fprintf(stderr, "[rsh-batch]   file %d: walk %.1f us = tiles %.1f (table checks %.1f; %d of %d tiles from the hit map,"
+                    " the first at tile %d) + events %.1f (digests %.1f) + other\n", fmax, x.t_total / 100.0,
+                    x.t_tiles / 100.0, x.t_check / 100.0, x.mapped, x.tiles, x.first_mapped, x.t_event / 100.0,
                     x.t_digest / 100.0);
+            if (S->chain_help.p && two_phase) {  // the map's helpers (device state of the last phase-0 launch)
+                std::vector<ChainHelp> hh((size_t)NF);
+                if (hipMemcpy(hh.data(), S->chain_help.p, (size_t)NF * sizeof(ChainHelp), hipMemcpyDeviceToHost) == hipSuccess) {
+                    int64_t segs = 0, joins = 0, files_helped = 0;
+                    for (const ChainHelp& q : hh) {
+                        segs += q.mapped;
+                        joins += q.joins;
+                        files_helped += q.joins > 0;
+                    }
+                    const ChainHelp& q = hh[(size_t)fmax];
+                    fprintf(stderr, "[rsh-batch]   hit map: %lld segments mapped over %lld files (%lld key sets built); file %d: %d "
+                            "segments, %d key sets, claims %d of %d, first segment %.1f us after the walk's start\n",
+                            (long long)segs, (long long)files_helped, (long long)joins, fmax, q.mapped, q.joins, q.claim,
+                            q.nseg, q.t_first == INT64_MAX ? -1.0 : (q.t_first - q.t_start) / 100.0);
+                }
+            }
         }
     }
     if (tentative) {

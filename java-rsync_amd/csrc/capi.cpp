@@ -1149,6 +1149,7 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
     rsh_ctx* c = new (std::nothrow) rsh_ctx();
     if (!c) return RSH_E_NOMEM;
     c->device = device;
+    c->n_cu = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     c->abort_word = nullptr;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||

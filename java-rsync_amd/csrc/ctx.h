@@ -110,6 +110,7 @@ using rsh::HitCache;
 
 struct rsh_ctx {
     int device = 0;
+    int n_cu = 256;  // compute units (the chain walk's helper workgroups fill the ones its files leave idle)
     hipStream_t stream = nullptr;
     DevBuf data, weak, strong;                   // host-input staging
     DevBuf src_weak, src_strong, flags;          // aligned speculation over the source

@@ -309,7 +309,30 @@ struct ChainOut {
     int64_t t_total, t_tiles, t_check, t_event, t_digest;  // wall-clock ticks (10 ns) of the walk's parts (trace)
     int32_t spec_full;            // phase 1 walked it
     int32_t aborted;              // phase 0 stopped its phase-1 K1 groups: only the prefix is speculated
+    int32_t mapped, first_mapped; // tiles answered from the hit map; the walk's tile count at the first (trace)
 };
+// The phase-0 hit map (chain_help): while one file's walk searches tile after tile on its CU, the workgroups whose
+// own walks have ended (and the launch's extra ones) map that file's prefix ahead of it -- in the synced state the
+// key at p is the true weak sum T(p), whatever the walk does.  One 64-bit word per 32 positions: the map's
+// generation (high half) and bit i = "T(32 w + i) is in the table" (low half), written in one store, so that a
+// word either carries this launch's generation and its bits or is ignored.  ChainHelp is the file's shared state,
+// in device memory, reset by the host before each phase-0 launch.
+struct ChainHelp {
+    int32_t nseg;    // map segments of CHAIN_MAP_SEG positions over [0, hend) (0: not mapped)
+    int32_t claim;   // next segment a helper takes (atomic)
+    int32_t live;    // 1 while the file's walk runs (the walk clears it)
+    int32_t tiles;   // tiles the walk has searched so far (helpers join files that searched at least twice)
+    int64_t pos;     // the walk's current search start (helpers skip segments behind it)
+    int32_t mapped;  // segments mapped (trace)
+    int32_t joins;   // helpers that built this file's key set (trace)
+    int64_t t_start, t_first;  // wall clock: the walk's start, the first segment mapped ahead of it (trace)
+};
+constexpr int CHAIN_THREADS = 512;                      // 8 waves (2 per SIMD: 256 VGPRs each)
+constexpr int CHAIN_PPT = 32;                            // wide tiles: positions per lane (two halves of 16)
+constexpr int64_t CHAIN_TILE = (int64_t)CHAIN_THREADS * CHAIN_PPT;
+constexpr int CHAIN_SEGS = 64;                           // blocks a tile may start (B >= 512 when wide)
+constexpr int64_t CHAIN_MAP_SEG = 2 * CHAIN_TILE;        // positions per helper claim
+
 struct ChainFile {
     const uint8_t* data;
     int64_t n;
@@ -331,9 +354,13 @@ struct ChainFile {
     int32_t ev_cap;
     uint32_t seed;                     // the checksum seed (a window's digest at an unaligned hit)
     ChainOut* out;
+    unsigned long long* hmap;          // its map words, positions [0, hend) (null: not mapped)
+    int64_t hend;                      // min(na_a B, n - B + 1): the positions a phase-0 search may reach
 };
+// help (phase 0): the files' ChainHelp array, or null (no map); helpers: extra workgroups beyond nfiles that only
+// map; finished walks map too.  abort_gen is also the map's generation.
 hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s, int phase = 1,
-                                int abort_gen = 0);
+                                int abort_gen = 0, ChainHelp* help = nullptr, uint32_t helpers = 0);
 // The chunk indexes of many files (slots cleared by the caller; TableEnt as for the probe hashes).
 hipError_t launch_chunk_index(const TableEnt* ents, uint32_t nfiles, int32_t max_keys, hipStream_t s, bool bg = false);
 

@@ -2600,10 +2600,7 @@ hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const Part
 // All lanes keep the same copy of the state (s, mark, pref) and take the same decisions (every value they
 // branch on is read from global memory or LDS by all of them); lane 0 writes the events.
 // ------------------------------------------------------------------------------------------------
-constexpr int CHAIN_THREADS = 512;                      // 8 waves (2 per SIMD: 256 VGPRs each)
-constexpr int CHAIN_PPT = 32;                            // wide tiles: positions per lane (two halves of 16)
-constexpr int64_t CHAIN_TILE = (int64_t)CHAIN_THREADS * CHAIN_PPT;
-constexpr int CHAIN_SEGS = 64;                           // blocks a tile may start (B >= 512 when wide)
+// CHAIN_THREADS, CHAIN_PPT, CHAIN_TILE, CHAIN_SEGS: device.h (the host sizes the hit map with them)
 
 // A key's presence in a chunk index (launch_chunk_index: (key << 32) | (i + 1) per chunk, 0 = empty): every chunk
 // with the key lies on the key's probe path before its first empty slot
@@ -2617,46 +2614,68 @@ __device__ __forceinline__ bool kslots_has(const unsigned long long* __restrict_
     }
 }
 
-// The chain walk's key set: the table's distinct weak sums in LDS as a bucketed cuckoo set -- 2 x 4096 buckets of 4
-// keys (128 KiB), a key in bucket h1(k) of the first half or h2(k) of the second, 0 = empty (key 0 has its own
-// flag).  A lookup is two 16-byte LDS reads and eight compares, exact.  Config 4's 16384 keys fill half of it; a
-// key still displaced after the insertion's bound (tables near or above 32768 distinct keys) marks the set
-// incomplete, and the walk then confirms every key in the chunk index instead.
-constexpr int CHAIN_CK_BUCKETS = 4096;
-__device__ __forceinline__ uint32_t chain_ck_h1(uint32_t k) { return (k * 0x9E3779B1u) >> 20; }
-__device__ __forceinline__ uint32_t chain_ck_h2(uint32_t k) { return CHAIN_CK_BUCKETS + (((k ^ (k >> 15)) * 0x85EBCA77u) >> 20); }
+// The chain walk's key set: the table's distinct weak sums in LDS as a bucketed cuckoo set -- 2 x 8192 buckets of 2
+// keys (128 KiB), a key in bucket h1(k) of the first half or h2(k) of the second.  A bucket's free slots hold its own
+// empty value, a key that can never live in that bucket (its hashes point elsewhere), so every 32-bit key -- 0
+// included -- is stored as itself, and a lookup is two 8-byte LDS reads and four compares, exact.  The hashes
+// multiply 24-bit folds of the key by 24-bit constants (full-rate v_mul_u32_u24; a 32-bit multiply issues at quarter
+// rate), a different fold per table, so that keys sharing one fold still part in the other table.  Config 4's 16384
+// keys fill half of it; a key still displaced after the insertion's bound (tables near or above 32768 distinct keys,
+// or keys crowding a few buckets) marks the set incomplete, and the walk then confirms every key in the chunk index.
+constexpr int CHAIN_CK_BUCKETS = 8192;
+__host__ __device__ constexpr uint32_t chain_ck_h1(uint32_t k) {
+    return (((k ^ (k >> 15)) & 0xFFFFFFu) * 0x9E3779u) >> 19;
+}
+__host__ __device__ constexpr uint32_t chain_ck_h2(uint32_t k) {
+    return CHAIN_CK_BUCKETS + ((((k ^ (k >> 8)) & 0xFFFFFFu) * 0x85EBCBu) >> 19);
+}
+// bucket i's empty value: 0, except in the two buckets key 0 hashes to, which use 1 (whose own buckets differ)
+__host__ __device__ constexpr uint32_t chain_ck_empty(uint32_t i) {
+    return (i == chain_ck_h1(0u) || i == chain_ck_h2(0u)) ? 1u : 0u;
+}
+static_assert(chain_ck_h1(1u) != chain_ck_h1(0u) && chain_ck_h2(1u) != chain_ck_h2(0u), "empty values");
 struct ChainKeySet {
-    uint4* b;      // 2 * CHAIN_CK_BUCKETS buckets
-    int32_t* has0;  // key 0 present
+    uint2* b;       // 2 * CHAIN_CK_BUCKETS buckets
     int32_t* full;  // some key found no slot: lookups are not exact
 };
 __device__ __forceinline__ void chain_ck_insert(const ChainKeySet& ks, uint32_t k) {
-    if (k == 0u) {
-        *ks.has0 = 1;
-        return;
-    }
     // cuckoo insertion: a free slot of the key's bucket in table w, else displace one of that bucket's keys and
-    // carry it to its bucket in the other table (every key lives in its own h1 or h2 bucket)
+    // carry it to its bucket in the other table (every key lives in its own h1 or h2 bucket; slots only ever go
+    // from empty to a key)
     uint32_t cur = k;
     int w = 0;
-    for (int it = 0; it < 96; ++it) {
-        uint32_t* slot = reinterpret_cast<uint32_t*>(&ks.b[w == 0 ? chain_ck_h1(cur) : chain_ck_h2(cur)]);
+    for (int it = 0; it < 128; ++it) {
+        const uint32_t bi = w == 0 ? chain_ck_h1(cur) : chain_ck_h2(cur), e = chain_ck_empty(bi);
+        uint32_t* slot = reinterpret_cast<uint32_t*>(&ks.b[bi]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t old = atomicCAS(slot + j, 0u, cur);
-            if (old == 0u || old == cur) return;
+        for (int j = 0; j < 2; ++j) {
+            const uint32_t old = atomicCAS(slot + j, e, cur);
+            if (old == e || old == cur) return;
         }
-        const uint32_t old = atomicExch(slot + (it & 3), cur);
-        if (old == 0u || old == cur) return;
+        const uint32_t old = atomicExch(slot + (it & 1), cur);
+        if (old == cur) return;
         cur = old;
         w ^= 1;
     }
     *ks.full = 1;  // a key is left over: the set is not exact
 }
 __device__ __forceinline__ bool chain_ck_has(const ChainKeySet& ks, uint32_t k) {
-    if (k == 0u) return *ks.has0 != 0;
-    const uint4 a = ks.b[chain_ck_h1(k)], c = ks.b[chain_ck_h2(k)];
-    return a.x == k || a.y == k || a.z == k || a.w == k || c.x == k || c.y == k || c.z == k || c.w == k;
+    const uint2 a = ks.b[chain_ck_h1(k)], c = ks.b[chain_ck_h2(k)];
+    return a.x == k || a.y == k || c.x == k || c.y == k;
+}
+
+// bit i: keys[i] is in the key set (exact sets only).  Branch free: two 8-byte reads and four compares per key (a
+// wave's lanes would take every branch anyway)
+__device__ __forceinline__ uint32_t chain_mask16(const ChainKeySet& set, const uint32_t (&keys)[16]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t k = keys[i];
+        const uint2 x = set.b[chain_ck_h1(k)], y = set.b[chain_ck_h2(k)];
+        m |= (uint32_t)((x.x == k) | (x.y == k) | (y.x == k) | (y.y == k)) << i;
+        if ((i & 3) == 3) asm volatile("" ::: "memory");  // 4 keys' reads in flight at a time (registers)
+    }
+    return m;
 }
 
 // The first of a lane's 16 keys (bit i of valid: position i is in the search) that the table holds, or -1: the 16
@@ -2666,21 +2685,9 @@ __device__ __forceinline__ bool chain_ck_has(const ChainKeySet& ks, uint32_t k) 
 __device__ __forceinline__ int chain_first_hit16(const unsigned long long* __restrict__ ks, uint32_t kmask,
                                                  const ChainKeySet& set, const uint32_t (&keys)[PROBE_PPT],
                                                  uint32_t valid) {
-    // the key set in LDS: exact (the usual case), so the table in global memory is not touched at all.  Branch
-    // free: two 16-byte reads and eight compares per key (a wave's lanes would take every branch anyway)
+    // the key set in LDS: exact (the usual case), so the table in global memory is not touched at all
     if (*set.full == 0) {
-        const bool has0 = *set.has0 != 0;
-        uint32_t m = 0;
-#pragma unroll
-        for (int i = 0; i < PROBE_PPT; ++i) {
-            const uint32_t k = keys[i];
-            const uint4 x = set.b[chain_ck_h1(k)], y = set.b[chain_ck_h2(k)];
-            const bool in = (x.x == k) | (x.y == k) | (x.z == k) | (x.w == k) | (y.x == k) | (y.y == k) | (y.z == k) |
-                            (y.w == k);
-            m |= (uint32_t)(k != 0u ? in : has0) << i;
-            if ((i & 3) == 3) asm volatile("" ::: "memory");  // 4 keys' reads in flight at a time (registers)
-        }
-        m &= valid;
+        const uint32_t m = chain_mask16(set, keys) & valid;
         return m ? __builtin_ctz(m) : -1;
     }
     uint32_t hit = 0, need = 0;
@@ -2716,13 +2723,242 @@ __device__ __attribute__((noinline)) void chain_window_digest(const uint8_t* x, 
 }
 
 __device__ __forceinline__ bool chain_digest_eq(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int dl) {
-    for (int j = 0; j < dl; ++j)
-        if (a[j] != b[j]) return false;
-    return true;
+    // every byte's loads issued before any compare (one round trip, not dl): indices past dl re-read the last byte
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int jj = j < dl ? j : dl - 1;
+        diff |= j < dl ? (uint32_t)(a[jj] ^ b[jj]) : 0u;
+    }
+    return diff == 0u;
+}
+// the same against a digest already in registers (a's bytes packed four to a word)
+__device__ __forceinline__ bool chain_digest_eq_reg(const uint32_t (&a)[4], const uint8_t* __restrict__ b, int dl) {
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int jj = j < dl ? j : dl - 1;
+        diff |= j < dl ? (((a[j >> 2] >> (8 * (j & 3))) ^ (uint32_t)b[jj]) & 0xFFu) : 0u;
+    }
+    return diff == 0u;
+}
+// dl (<= 16) digest bytes at a, packed four to a word (all loads issued at once)
+__device__ __forceinline__ void chain_digest_load(const uint8_t* __restrict__ a, int dl, uint32_t (&w)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j >> 2] |= (uint32_t)a[j < dl ? j : dl - 1] << (8 * (j & 3));
+}
+
+// A wide tile lane's sums over its 32 positions' bytes x at p0 and y at p0 + B, weights relative to the tile start
+// (base = p0 - q0): (sum x, sum (base + j) x, sum y, sum (base + B + j) y), j = 0..31 -- four bytes per v_dot4_i32_i8
+// against the byte weights j (signed bytes, as Java's)
+__device__ __forceinline__ void chain_lane_sums(const uint32_t (&xa)[2][4], const uint32_t (&xb)[2][4], uint32_t base,
+                                                uint32_t B, int32_t (&pre)[4]) {
+    int32_t sa = 0, ja = 0, sb = 0, jb = 0;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            const int wt = 0x03020100 + 0x04040404 * d + 0x10101010 * hh;  // bytes 16 hh + 4 d + 0..3
+            sa = __builtin_amdgcn_sdot4((int)xa[hh][d], 0x01010101, sa, false);
+            ja = __builtin_amdgcn_sdot4((int)xa[hh][d], wt, ja, false);
+            sb = __builtin_amdgcn_sdot4((int)xb[hh][d], 0x01010101, sb, false);
+            jb = __builtin_amdgcn_sdot4((int)xb[hh][d], wt, jb, false);
+        }
+    pre[0] = sa;
+    pre[1] = (int32_t)(base * (uint32_t)sa) + ja;
+    pre[2] = sb;
+    pre[3] = (int32_t)((base + B) * (uint32_t)sb) + jb;
+}
+
+// the table's distinct weak sums into the workgroup's key set
+__device__ __forceinline__ void chain_kset_build(const ChainKeySet& ks, const int32_t* __restrict__ weak, int64_t C) {
+    const int t = threadIdx.x;
+    for (int i = t; i < 2 * CHAIN_CK_BUCKETS; i += CHAIN_THREADS) {
+        const uint32_t e = chain_ck_empty((uint32_t)i);
+        ks.b[i] = make_uint2(e, e);
+    }
+    if (t == 0) *ks.full = 0;
+    __syncthreads();
+    for (int64_t c = t; c < C; c += CHAIN_THREADS) chain_ck_insert(ks, (uint32_t)weak[c]);
+    __syncthreads();
+}
+
+// the map's shared words: relaxed atomics at agent scope (the workgroups sit on different XCDs, whose L2s are not
+// coherent with each other); vector memory operations throughout
+__device__ __forceinline__ int32_t chain_ld(const int32_t* p) {
+    return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int64_t chain_ld64(const int64_t* p) {
+    return __hip_atomic_load(const_cast<int64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void chain_st(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void chain_st64(int64_t* p, int64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One tile of a file's hit map: positions [q0, q0 + CHAIN_TILE) below hend, q0 a multiple of CHAIN_TILE.  The keys
+// are the walk's wide-tile keys in the synced state (each lane anchored on its block's aligned sum T(o), the prefix
+// sums from one exscan rebased at each block's first lane, the head of the block the tile starts in); bit i of
+// lane t's word = position q0 + 32 t + i hits the key set.  Stored as (gen << 32) | bits, one 8-byte store.
+__device__ void chain_map_tile(const ChainFile& F, int64_t q0, uint32_t gen, const ChainKeySet& kset, int32_t* sh,
+                               int32_t (*s_seg)[4]) {
+    const int t = threadIdx.x;
+    const int64_t n = F.n, B = F.B, hend = F.hend;
+    const int64_t kb0 = q0 / B, o0 = kb0 * B;
+    int32_t head[4] = {0, 0, 0, 0};
+    if (q0 > o0) {
+        range_sums(F.data, n, o0, q0, o0, head[0], head[1]);
+        range_sums(F.data, n, o0 + B, q0 + B, o0, head[2], head[3]);
+        block_reduce<4>(head, sh);
+    }
+    const int64_t p0 = q0 + (int64_t)t * CHAIN_PPT;
+    const int64_t kb = p0 / B, o = kb * B;
+    uint32_t xa[2][4], xb[2][4];
+    load16(F.data, n, p0, xa[0]);
+    load16(F.data, n, p0 + 16, xa[1]);
+    load16(F.data, n, p0 + B, xb[0]);
+    load16(F.data, n, p0 + B + 16, xb[1]);
+    const bool live = p0 < hend;
+    const int32_t To = live ? F.aw[kb] : 0;
+    int32_t pre[4];
+    chain_lane_sums(xa, xb, (uint32_t)(p0 - q0), (uint32_t)B, pre);
+    block_exscan<4>(pre, sh);
+    if (p0 == o) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) s_seg[kb - kb0][v] = pre[v];
+    }
+    __syncthreads();
+    if (live) {
+        uint32_t pa, pa2, pb, pb2;
+        if (o < q0) {
+            const uint32_t d = (uint32_t)(q0 - o);
+            pa = (uint32_t)head[0] + (uint32_t)pre[0];
+            pa2 = (uint32_t)head[1] + (uint32_t)pre[1] + d * (uint32_t)pre[0];
+            pb = (uint32_t)head[2] + (uint32_t)pre[2];
+            pb2 = (uint32_t)head[3] + (uint32_t)pre[3] + d * (uint32_t)pre[2];
+        } else {
+            const int32_t* L = s_seg[kb - kb0];
+            const uint32_t d = (uint32_t)(o - q0);
+            pa = (uint32_t)(pre[0] - L[0]);
+            pa2 = (uint32_t)(pre[1] - L[1]) - d * pa;
+            pb = (uint32_t)(pre[2] - L[2]);
+            pb2 = (uint32_t)(pre[3] - L[3]) - d * pb;
+        }
+        const uint32_t s1o = (uint32_t)To & 0xFFFFu, s2o = (uint32_t)To >> 16;
+        const uint32_t P1e = s1o + pb;
+        const uint32_t P2e = (uint32_t)B * s1o - s2o + pb2;
+        uint32_t u1 = P1e - pa;
+        uint32_t u2 = (uint32_t)(p0 + B - o) * u1 - (P2e - pa2);
+        uint32_t bits = 0;
+#pragma unroll 1
+        for (int hh = 0; hh < 2; ++hh) {
+            uint32_t wa[4], wb[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                wa[j] = hh ? xa[1][j] : xa[0][j];
+                wb[j] = hh ? xb[1][j] : xb[0][j];
+            }
+            uint32_t keys[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                keys[i] = (u1 & 0xFFFFu) | (u2 << 16);
+                const int32_t xo = sbyte_of(wa, i), xi = sbyte_of(wb, i);
+                u1 += (uint32_t)(xi - xo);
+                u2 += u1 - (uint32_t)__mul24((int)B, xo);  // (B <= 2^17: a full-rate 24-bit multiply)
+            }
+            bits |= chain_mask16(kset, keys) << (16 * hh);
+        }
+        if (hend - p0 < 32) bits &= (1u << (uint32_t)(hend - p0)) - 1u;  // windows past hend: not searched
+        __hip_atomic_store(&F.hmap[p0 >> 5], ((unsigned long long)gen << 32) | bits, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();  // (s_seg and sh: the next tile)
+}
+
+// A helper workgroup: while some walk that has searched at least two tiles is still running, take the next unmapped
+// segment of the one with the most segments left (its own current file first: the key set is built per file) and
+// map it tile by tile, stopping when the walk ends or has passed the tile.  No workgroup ever waits for another: a
+// walk reads a map word only when it carries this launch's generation, and searches the tile itself otherwise.
+__device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict__ files, int nfiles, uint32_t gen,
+                                                     ChainHelp* help, uint2* ck, int32_t* ck_full,
+                                                     int32_t* sh, int32_t (*s_seg)[4], unsigned long long* s_best,
+                                                     int32_t* s_word) {
+    const int t = threadIdx.x;
+    const ChainKeySet kset{ck, ck_full};
+    int cur = -1;
+    ChainFile F = files[0];
+    for (;;) {
+        if (t == 0) *s_best = 0ull;
+        __syncthreads();
+        for (int f = t; f < nfiles; f += CHAIN_THREADS) {
+            ChainHelp* h = help + f;
+            const int32_t nseg = h->nseg;  // (written by the host before the launch)
+            if (nseg == 0) continue;
+            // one round trip for the file's shared words
+            const int32_t live = chain_ld(&h->live), tiles = chain_ld(&h->tiles), claim = chain_ld(&h->claim);
+            const int64_t pos = chain_ld64(&h->pos);
+            if (live == 0 || tiles < 2 || claim >= nseg) continue;
+            // the most urgent file: the map's frontier least far ahead of its walk (the current file while its
+            // frontier is within 8 segments of the walk: its key set is built)
+            const int64_t lead = (int64_t)claim - pos / CHAIN_MAP_SEG;
+            const uint32_t urg = (uint32_t)(lead < -1000 ? 2000 : lead > 999 ? 1 : 1000 - lead);
+            const uint32_t tie = (((uint32_t)f * 0x9E3779B1u) ^ ((uint32_t)blockIdx.x * 0x85EBCA77u)) >> 20;
+            const unsigned long long key = ((unsigned long long)(f == cur && lead < 8) << 63) |
+                                           ((unsigned long long)urg << 32) | ((unsigned long long)tie << 20) |
+                                           (uint32_t)f;
+            atomicMax(s_best, key);
+        }
+        __syncthreads();
+        const unsigned long long best = *s_best;
+        if (best == 0ull) return;
+        const int f = (int)(best & 0xFFFFFull);
+        ChainHelp* h = help + f;
+        if (t == 0) {  // the segments behind the walk are skipped, not claimed one by one
+            atomicMax(&h->claim, (int32_t)(chain_ld64(&h->pos) / CHAIN_MAP_SEG));
+            *s_word = atomicAdd(&h->claim, 1);
+        }
+        __syncthreads();
+        const int32_t seg = *s_word;
+        __syncthreads();
+        if (seg >= h->nseg) continue;
+        if (f != cur) {
+            F = files[f];
+            chain_kset_build(kset, F.table_weak, F.C);
+            if (*kset.full) {  // not exact: the walk confirms keys in the chunk index; no map for this file
+                if (t == 0) atomicMax(&h->claim, h->nseg);
+                cur = -1;
+                __syncthreads();
+                continue;
+            }
+            cur = f;
+            if (t == 0) atomicAdd(&h->joins, 1);
+        }
+        const int64_t lo = (int64_t)seg * CHAIN_MAP_SEG, hi = lo + CHAIN_MAP_SEG < F.hend ? lo + CHAIN_MAP_SEG : F.hend;
+        bool whole = true;
+        for (int64_t q0 = lo; q0 < hi; q0 += CHAIN_TILE) {
+            if (t == 0) *s_word = chain_ld(&h->live) != 0 && chain_ld64(&h->pos) < q0 + CHAIN_TILE;
+            __syncthreads();
+            const bool go = *s_word != 0;
+            __syncthreads();
+            if (!go) {
+                whole = false;
+                break;
+            }
+            chain_map_tile(F, q0, gen, kset, sh, s_seg);
+        }
+        if (t == 0) {
+            atomicAdd(&h->mapped, 1);
+            if (whole) atomicMin((unsigned long long*)&h->t_first, (unsigned long long)wall_clock64());
+        }
+    }
 }
 
 __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const ChainFile* __restrict__ files, int phase,
-                                                                      int abort_gen) {
+                                                                      int abort_gen, ChainHelp* help, int nfiles) {
     __builtin_amdgcn_s_setprio(3);
     __shared__ int32_t sh[4 * CHAIN_THREADS / 64];
     __shared__ int32_t s_hit;                  // first hit in a tile (offset from the tile start), or INT_MAX
@@ -2733,12 +2969,22 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_wtmp;                 // an unaligned window's sums (its digest: s_dig)
     __shared__ int32_t s_any;                  // some chunk carries the stale digest
     __shared__ int32_t s_seg[CHAIN_SEGS][4];   // wide tiles: the exscan at each block's first lane
-    __shared__ uint4 s_ck[2 * CHAIN_CK_BUCKETS];  // the table's keys (ChainKeySet)
-    __shared__ int32_t s_ck_has0, s_ck_full;
+    __shared__ uint2 s_ck[2 * CHAIN_CK_BUCKETS];  // the table's keys (ChainKeySet)
+    __shared__ int32_t s_ck_full;
     __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
+    __shared__ unsigned long long s_best;      // helpers: the file to map next
+    __shared__ int32_t s_word;
+    const ChainKeySet kset{s_ck, &s_ck_full};
+    if ((int)blockIdx.x >= nfiles) {  // a helper workgroup (phase 0): it only maps
+        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word);
+        return;
+    }
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
     // fields across the loop (the event stores may alias it) -- a PCIe round trip each
     const ChainFile F = files[blockIdx.x];
+    ChainHelp* const H = (phase == 0 && help != nullptr) ? help + blockIdx.x : nullptr;
+    if (H != nullptr && threadIdx.x == 0) chain_st64(&H->t_start, (int64_t)wall_clock64());
+    const uint32_t map_gen = (H != nullptr && F.hmap != nullptr) ? (uint32_t)abort_gen : 0u;  // 0: no map
     ChainOut* out = F.out;
     // phase 0 walks over the prefix speculation [0, na_a); phase 1 resumes the walks that reached its end
     if (phase == 1 && out->status != CHAIN_MORE) return;
@@ -2749,7 +2995,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const int64_t last = n - S, nB = n - B;
     const int64_t na = phase == 0 ? F.na_a : F.na, nflags = na < C ? na : C;
     const bool wide = (B % CHAIN_PPT) == 0 && B >= 512 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
-    const ChainKeySet kset{s_ck, &s_ck_has0, &s_ck_full};
     int64_t s = out->s, m = out->m;
     // The key set (~C LDS inserts, tens of microseconds) only if the walk may search: a walk that starts aligned on
     // an unbroken run of chain flags up to the last window with a chunk (an identical file, or its rest after the
@@ -2785,17 +3030,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         kset_built = s_zero < nflags;  // (uniform) a break in the chain: the walk will search
         __syncthreads();
     }
-    if (kset_built) {
-        for (int i = t; i < 2 * CHAIN_CK_BUCKETS; i += CHAIN_THREADS) s_ck[i] = make_uint4(0u, 0u, 0u, 0u);
-        if (t == 0) s_ck_has0 = s_ck_full = 0;
-        __syncthreads();
-        for (int64_t c = t; c < C; c += CHAIN_THREADS) chain_ck_insert(kset, (uint32_t)F.table_weak[c]);
-        __syncthreads();
-    }
+    if (kset_built) chain_kset_build(kset, F.table_weak, C);
     int32_t pref = out->pref;
     int32_t nev = out->n_ev, status = CHAIN_STOP;
     int64_t lit = out->literal, mat = out->matched, chain_matches = out->chain_matches, events = out->events;
-    int32_t tiles = out->tiles, digests = out->digests, poisoned = 0, dead = 0;
+    int32_t tiles = out->tiles, digests = out->digests, poisoned = 0, dead = 0, mapped = out->mapped;
+    int32_t first_mapped = out->first_mapped;
     int64_t flushes = out->flushes;
     const int64_t tk0 = (int64_t)wall_clock64();
     int64_t t_tiles = 0, t_check = 0, t_event = 0, t_digest = 0;
@@ -2931,9 +3171,49 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             // the head of the block the tile starts in (range_sums from o to the tile)
             const int64_t lim_spec = na * B - 1;  // windows with an anchor: blocks < na
             const int64_t qlast = stop < lim_spec ? stop : lim_spec;
+            if (H != nullptr && t == 0) {  // for the helpers: where this search starts, how many tiles so far
+                chain_st64(&H->pos, a);
+                chain_st(&H->tiles, tiles);
+            }
             for (int64_t q0 = a & ~(int64_t)(CHAIN_PPT - 1); p < 0 && q0 <= qlast;) {
                 ++tiles;
                 const int64_t tt0 = (int64_t)wall_clock64();
+                if (map_gen != 0u) {
+                    // the tile from the hit map when every word it needs carries this launch's generation: lane t's
+                    // word holds positions [q0 + 32 t, + 32), masked to [a, qlast] (qlast < hend)
+                    const int64_t pm = q0 + (int64_t)t * CHAIN_PPT;
+                    const int64_t lo = a > pm ? a - pm : 0, hi = qlast - pm;
+                    const bool need = lo <= 31 && hi >= lo;
+                    unsigned long long wv = 0ull;
+                    if (need) wv = __hip_atomic_load(&F.hmap[pm >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (t == 0) s_hit = 0x7FFFFFFF;
+                    if (__syncthreads_and(!need || (uint32_t)(wv >> 32) == map_gen)) {
+                        if (need) {
+                            const uint32_t bits = (uint32_t)wv & (0xFFFFFFFFu >> (31 - (hi < 31 ? hi : 31))) &
+                                                  (0xFFFFFFFFu << lo);
+                            if (bits) atomicMin(&s_hit, (int32_t)(pm - q0) + __builtin_ctz(bits));
+                        }
+                        __syncthreads();
+                        const int32_t hoff = s_hit;
+                        __syncthreads();
+                        if (hoff != 0x7FFFFFFF) {  // the key: the window's true weak sum (synced)
+                            p = q0 + hoff;
+                            if (p % B == 0) {      // an aligned window: the speculation's sum (p / B < na here)
+                                key = (uint32_t)F.aw[p / B];
+                            } else {               // else one reduction over its B bytes
+                                int32_t w2[2] = {0, 0};
+                                range_sums(F.data, n, p, p + B, p, w2[0], w2[1]);
+                                block_reduce<2>(w2, sh);
+                                const uint32_t S1 = (uint32_t)w2[0], S2 = (uint32_t)B * S1 - (uint32_t)w2[1];
+                                key = (S1 & 0xFFFFu) | (S2 << 16);
+                            }
+                        }
+                        if (mapped++ == 0) first_mapped = tiles;
+                        q0 += CHAIN_TILE;
+                        t_tiles += (int64_t)wall_clock64() - tt0;
+                        continue;
+                    }
+                }
                 const int64_t kb0 = q0 / B, o0 = kb0 * B;
                 int32_t head[4] = {0, 0, 0, 0};
                 if (q0 > o0) {
@@ -2950,18 +3230,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 load16(F.data, n, p0 + B + 16, xb[1]);
                 const bool live = p0 <= stop && p0 <= lim_spec && p0 + CHAIN_PPT > a;
                 const int32_t To = live ? F.aw[kb] : 0;
-                int32_t pre[4] = {0, 0, 0, 0};
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int32_t va = sbyte_of(xa[hh], i), vb = sbyte_of(xb[hh], i);
-                        const uint32_t r = (uint32_t)(p0 + 16 * hh + i - q0);
-                        pre[0] += va;
-                        pre[1] += (int32_t)(r * (uint32_t)va);
-                        pre[2] += vb;
-                        pre[3] += (int32_t)((r + (uint32_t)B) * (uint32_t)vb);
-                    }
+                int32_t pre[4];
+                chain_lane_sums(xa, xb, (uint32_t)(p0 - q0), (uint32_t)B, pre);
                 block_exscan<4>(pre, sh);  // sums over [q0, p0) and [q0 + B, p0 + B), weights j - q0
                 if (p0 == o) {              // a block's first lane: its rebasing point
 #pragma unroll
@@ -3012,7 +3282,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                             keys[i] = (u1 & 0xFFFFu) | (u2 << 16);
                             const int32_t xo = sbyte_of(wa, i), xi = sbyte_of(wb, i);
                             u1 += (uint32_t)(xi - xo);
-                            u2 += u1 - (uint32_t)B * (uint32_t)xo;
+                            u2 += u1 - (uint32_t)__mul24((int)B, xo);  // (B <= 2^17: a full-rate 24-bit multiply)
                         }
                         // positions base + i with a <= position <= lim_p, as a bit range
                         const int64_t base = p0 + 16 * hh;
@@ -3134,6 +3404,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         ++events;
         const int64_t kp = p / B;
         const bool spec_digest = p % B == 0 && kp < na;
+        // the speculation's digest of an aligned window, loaded beside the bucket's slots (it depends only on p)
+        uint32_t dg[4] = {0u, 0u, 0u, 0u};
+        if (spec_digest) chain_digest_load(F.as + kp * dl, dl, dg);
         if (t < 64) {
             // every chunk with this key lies on the probe path before the first empty slot: wave 0 reads 64 slots of
             // it per round trip (one, nearly always) instead of one dependent load per slot
@@ -3188,6 +3461,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             if (t == 0) chain_window_digest(F.data + p, n - p, (uint32_t)B, (uint32_t)dl, F.seed, &s_wtmp, s_dig);
             __syncthreads();
             md5c = s_dig;
+            chain_digest_load(s_dig, dl, dg);
             ++digests;
             t_digest += (int64_t)wall_clock64() - td0;
         }
@@ -3203,7 +3477,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 pos = it;
             }
             const int32_t c = s_bk[pos];
-            if (chain_digest_eq(md5c, F.table_strong + (int64_t)c * dl, dl)) hit = c;
+            if (chain_digest_eq_reg(dg, F.table_strong + (int64_t)c * dl, dl)) hit = c;
         }
         __syncthreads();
         t_event += (int64_t)wall_clock64() - te0;
@@ -3264,6 +3538,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->t_event += t_event;
         out->t_digest += t_digest;
         out->spec_full = phase == 1;
+        out->mapped = mapped;
+        out->first_mapped = first_mapped;
         // a file that needs no more speculation stops its phase-1 K1 groups (they poll this word); any other stop
         // keeps them (the resolver's aligned lookups past the prefix use them)
         const bool stop_spec = phase == 0 && F.abort && (status == CHAIN_DONE || dead);
@@ -3277,11 +3553,22 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->chain_matches = chain_matches;
         out->events = events;
     }
+    if (H != nullptr) {  // this walk is over: its helpers stop, and the workgroup helps the walks still searching
+        if (t == 0) chain_st(&H->live, 0);
+        __syncthreads();
+        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word);
+    }
 }
 
-hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s, int phase, int abort_gen) {
+hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s, int phase, int abort_gen,
+                                ChainHelp* help, uint32_t helpers) {
     if (nfiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(chain_advance_kernel, dim3(nfiles), dim3(CHAIN_THREADS), 0, s, files, phase, abort_gen);
+    if (phase != 0 || help == nullptr || nfiles >= (1u << 20)) {  // (helpers pick files by a 20-bit index)
+        help = nullptr;
+        helpers = 0;
+    }
+    hipLaunchKernelGGL(chain_advance_kernel, dim3(nfiles + helpers), dim3(CHAIN_THREADS), 0, s, files, phase,
+                       abort_gen, help, (int)nfiles);
     return hipGetLastError();
 }
 

@@ -391,3 +391,63 @@ def test_batch_waiting_files_keep_their_worker(ctx, rsh_opt):
         else:
             oev, olit, omat = expect[j]
             assert got == oev and (sj[j].literal, sj[j].matched) == (olit, omat), f"edited file {j}"
+
+
+@pytest.mark.parametrize("helpers", [-1, 0, 3])
+def test_batch_chain_hit_map(ctx, helpers, rsh_opt, capfd):
+    """The phase-0 walk with its hit map (device.hip chain_help / chain_map_tile): while a walk searches tile after
+    tile, workgroups whose walks have ended (and, helpers = -1 / 3, extra ones) map its prefix ahead of it, and the
+    walk takes a tile from the map when every word carries the launch's generation.  Files whose walks search
+    hundreds of times before any false hit (random bytes, few keys, every other block replaced), low-entropy ones
+    whose first hits are false and unaligned, and identical ones, against the oracle; helpers = 0: no map at all.
+    The walk must give exactly the events of the tile search either way."""
+    rsh_opt("batch_chain_prefix", 1024)  # two phases: the map covers each file's first 1024 windows
+    rsh_opt("chain_helpers", helpers)
+    rsh_opt("scan_trace", 2)
+    rng = random.Random(4242)
+    files = []
+    for i in range(10):
+        B = [1024, 2048, 512, 4096][i % 4]
+        nb = rng.randrange(1500 * B, 2500 * B) if B < 4096 else 700 * B
+        basis = np.frombuffer(O.splitmix(nb, 7100 + i).tobytes(), np.uint8)
+        other = np.frombuffer(O.splitmix(nb, 8100 + i).tobytes(), np.uint8)
+        if i in (6, 7):  # low entropy: false weak hits at unaligned positions
+            basis, other = basis % 4, other % 4
+        src = basis.copy()
+        if i != 9:  # (file 9: identical)
+            src[:nb // B * B].reshape(-1, B)[1::2] = other[:nb // B * B].reshape(-1, B)[1::2]
+        files.append((basis.astype(np.uint8).tobytes(), src.astype(np.uint8).tobytes(), B, 3))
+    d_src, soffs = _pack(ctx, [f[1] for f in files], [0] * len(files))
+    sj = (R.ScanJob * len(files))()
+    evs, keep, expect = [], [], []
+    for i, (basis, src, B, dl) in enumerate(files):
+        h = R.header_make(B, dl, len(basis))
+        w, s = ctx.block_sums(basis, h, SEED)
+        d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
+        d_w.upload(w)
+        d_s.upload(s)
+        keep += [d_w, d_s]
+        cap = len(src) // (10 * B) + 2 * h.chunk_count + 64
+        ev = np.zeros(cap, R.EVENT_DTYPE)
+        evs.append(ev)
+        sj[i].d_src, sj[i].n, sj[i].h = d_src.ptr.value + soffs[i], len(src), h
+        sj[i].d_weak, sj[i].d_strong = d_w.ptr.value, d_s.ptr.value
+        sj[i].ev, sj[i].ev_cap = ev.ctypes.data, cap
+        oev, _, olit, omat, _ = O.sender(src, O.header(B, dl, len(basis)), w, s, SEED)
+        expect.append(([tuple(e) for e in oev], olit, omat))
+    capfd.readouterr()
+    for rep in range(2):  # the second scan reuses the map words (generations only grow)
+        assert R.lib().rsh_match_scan_batch_device(ctx.handle, sj, len(files), SEED_NP.ctypes.data, None) == 0
+        for i, (basis, src, B, dl) in enumerate(files):
+            oev, olit, omat = expect[i]
+            assert sj[i].status == 0
+            assert R.events_as_tuples(evs[i][:sj[i].n_ev], B) == oev, f"file {i}: B={B} (scan {rep})"
+            assert (sj[i].literal, sj[i].matched) == (olit, omat)
+    err = capfd.readouterr().err
+    import re
+    mapped = [int(m) for m in re.findall(r"\((\d+) from the hit map\)", err)]
+    assert len(mapped) == 2, err[-2000:]
+    if helpers == 0:
+        assert mapped == [0, 0]
+    else:  # the long walks search ~1000 tiles each in phase 0: the helpers get ahead of them
+        assert min(mapped) > 0, err[-2000:]
