@@ -2109,7 +2109,7 @@ static_assert(PROBE_TILE == PROBE_THREADS * PROBE_PPT, "tile = threads x positio
 
 __device__ __forceinline__ int32_t roll_sub(int32_t cs, int32_t w, int32_t x) {  // Rolling.java:56-60
     const uint32_t lo = ((uint32_t)cs & 0xFFFFu) - (uint32_t)x;
-    const uint32_t hi = ((uint32_t)cs >> 16) - (uint32_t)w * (uint32_t)x;
+    const uint32_t hi = ((uint32_t)cs >> 16) - (uint32_t)__mul24(w, x);  // (w <= B <= 2^17: a full-rate 24-bit multiply)
     return (int32_t)((lo & 0xFFFFu) | (hi << 16));
 }
 __device__ __forceinline__ int32_t roll_add(int32_t cs, int32_t x) {  // Rolling.java:25-29
@@ -2136,6 +2136,68 @@ __device__ __forceinline__ void load16(const uint8_t* __restrict__ x, int64_t n,
 }
 __device__ __forceinline__ int32_t sbyte_of(const uint32_t (&w)[4], int i) {
     return (int32_t)(int8_t)(uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+}
+
+// A lane's 16 keys at positions base + i (bit i of valid: in the interval): every hit goes to the file's hit list
+// (the first position by atomicMin, up to PROBE_HITS_CAP of them listed).  The stale digest's few keys (the batched
+// flush chain's probes over a file's rest) are compared against each key in turn; otherwise the 16 first hash slots
+// go out in one burst of independent loads -- most keys are decided by their first slot (load factor <= 1/2), so a
+// lane waits for about one L2 round trip -- and only keys whose first slot holds another key walk the probe path.
+// Branch free but for those walks and the (rare) hits.
+__device__ __forceinline__ void probe_check16(const ScanFile& F, const ProbeTable& table, int nsmall,
+                                              const uint32_t (&key)[16], uint32_t valid, int64_t base) {
+    uint32_t m = 0;
+    if (nsmall > 0) {
+        for (int j = 0; j < nsmall; ++j) {
+            const uint32_t kj = F.small[j];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) m |= (uint32_t)(key[i] == kj) << i;
+        }
+    } else {
+        unsigned long long sl[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sl[i] = (valid >> i) & 1u ? table.slots[slot_hash(key[i]) & table.mask] : 0ull;
+        uint32_t need = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if (sl[i] == ((1ull << 32) | key[i])) m |= 1u << i;
+            else if (sl[i] != 0ull) need |= 1u << i;
+        }
+        need &= valid;
+        while (need) {
+            const int i = __builtin_ctz(need);
+            uint32_t kk = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (j == i) kk = key[j];
+            if (table_has(table, kk)) m |= 1u << i;
+            need &= need - 1u;
+        }
+    }
+    m &= valid;
+    while (m) {
+        const int i = __builtin_ctz(m);
+        uint32_t kk = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+            if (j == i) kk = key[j];
+        const int64_t p = base + i;
+        atomicMin(&F.out->first, (unsigned long long)p);
+        const unsigned long long at = atomicAdd(&F.out->count, 1ull);
+        if (at < (unsigned long long)PROBE_HITS_CAP) {
+            F.out->pos[at] = (unsigned long long)p;
+            F.out->key[at] = kk;
+        }
+        m &= m - 1u;
+    }
+}
+
+// bit i set for positions base + i in [lo, hi), i < 16
+__device__ __forceinline__ uint32_t probe_valid16(int64_t base, int64_t lo, int64_t hi) {
+    const int64_t a = lo - base, b = hi - base;
+    if (b <= 0 || a >= 16 || b <= a) return 0u;
+    const int ia = a < 0 ? 0 : (int)a, ib = b > 16 ? 16 : (int)b;
+    return (0xFFFFu >> (16 - ib)) & (0xFFFFu << ia);
 }
 
 __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A) {
@@ -2216,39 +2278,7 @@ __global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A)
         R = roll_sub(R, (int32_t)w, sbyte_of(xa, i));
         if (n - (p + 1) >= B) R = roll_add(R, sbyte_of(xb, i));
     }
-    // a stale digest's few keys (the batched flush chain's probes over a file's rest): compared in registers
-    const int nsmall = F.nsmall;
-    uint32_t small[PROBE_SMALL_KEYS];
-#pragma unroll
-    for (int j = 0; j < PROBE_SMALL_KEYS; ++j) small[j] = F.small[j];
-    unsigned long long sl[PROBE_PPT];
-    if (nsmall == 0) {
-#pragma unroll
-        for (int i = 0; i < PROBE_PPT; ++i) sl[i] = table.slots[slot_hash(key[i]) & table.mask];
-    }
-#pragma unroll
-    for (int i = 0; i < PROBE_PPT; ++i) {
-        const int64_t p = p0 + i;
-        if (p >= I.b || p >= qend) break;
-        if (p < I.a) continue;
-        bool hit = false;
-        if (nsmall > 0) {
-#pragma unroll
-            for (int j = 0; j < PROBE_SMALL_KEYS; ++j) hit = hit || (j < nsmall && small[j] == key[i]);
-        } else {
-            const unsigned long long v = (1ull << 32) | key[i];
-            hit = sl[i] == v;
-            if (!hit && sl[i] != 0ull) hit = table_has(table, key[i]);
-        }
-        if (hit) {
-            atomicMin(&F.out->first, (unsigned long long)p);
-            const unsigned long long at = atomicAdd(&F.out->count, 1ull);
-            if (at < (unsigned long long)PROBE_HITS_CAP) {
-                F.out->pos[at] = (unsigned long long)p;
-                F.out->key[at] = key[i];
-            }
-        }
-    }
+    probe_check16(F, table, F.nsmall, key, probe_valid16(p0, I.a, I.b < qend ? I.b : qend), p0);
 }
 
 __global__ void probe_out_reset_kernel(ProbeOut* out, uint32_t n) {
@@ -2487,9 +2517,6 @@ __global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(4
     uint32_t s1o = (uint32_t)h[0], s2o = (uint32_t)B * (uint32_t)h[0] - (uint32_t)h[1];
     const ProbeTable table{F.slots, F.mask};
     const int nsmall = F.nsmall;
-    uint32_t small[PROBE_SMALL_KEYS];
-#pragma unroll
-    for (int j = 0; j < PROBE_SMALL_KEYS; ++j) small[j] = F.small[j];
     const int t = threadIdx.x;
     for (int64_t base = q0; base < q1; base += PROBE_LONG_SUB) {
         const int64_t p0 = base + (int64_t)t * PROBE_LONG_PPL;
@@ -2525,34 +2552,8 @@ __global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(4
                     key[i] = (uint32_t)R;
                     R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(wa, i)), sbyte_of(wb, i));
                 }
-                if (p0 + 16 * grp + 15 < I.a || p0 + 16 * grp >= q1) continue;  // (a group wholly below a)
-                unsigned long long sl[16];
-                if (nsmall == 0) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) sl[i] = table.slots[slot_hash(key[i]) & table.mask];
-                }
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int64_t p = p0 + 16 * grp + i;
-                    if (p >= q1 || p >= I.b) break;
-                    if (p < I.a) continue;
-                    bool hit = false;
-                    if (nsmall > 0) {
-#pragma unroll
-                        for (int j = 0; j < PROBE_SMALL_KEYS; ++j) hit = hit || (j < nsmall && small[j] == key[i]);
-                    } else {
-                        hit = sl[i] == ((1ull << 32) | key[i]);
-                        if (!hit && sl[i] != 0ull) hit = table_has(table, key[i]);
-                    }
-                    if (hit) {
-                        atomicMin(&F.out->first, (unsigned long long)p);
-                        const unsigned long long at = atomicAdd(&F.out->count, 1ull);
-                        if (at < (unsigned long long)PROBE_HITS_CAP) {
-                            F.out->pos[at] = (unsigned long long)p;
-                            F.out->key[at] = key[i];
-                        }
-                    }
-                }
+                const uint32_t valid = probe_valid16(p0 + 16 * grp, I.a, I.b < q1 ? I.b : q1);
+                if (valid) probe_check16(F, table, nsmall, key, valid, p0 + 16 * grp);
             }
             if (t == PROBE_THREADS - 1) {  // R(p0 + 64) less E there: the next sub-segment's anchor T
                 const int64_t pn = p0 + PROBE_LONG_PPL;
