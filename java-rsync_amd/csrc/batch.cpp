@@ -1077,6 +1077,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         for (int32_t f = 0; f < NF; ++f) {
             FileScan& fs = files[(size_t)f];
             co[f] = ChainOut{};
+            co[f].clear_to = -1;
             const int64_t mw = map_on ? map_off[(size_t)f + 1] - map_off[(size_t)f] : 0;
             const int64_t hend = mw > 0 ? std::min<int64_t>(fs.na_a * fs.B, fs.n - fs.B + 1) : 0;
             cf[f] = ChainFile{fs.d_src, fs.n, (uint32_t)fs.B, fs.C, fs.dl, jobs[fs.job].h.remainder,
@@ -1086,7 +1087,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                               two_phase ? S->file_abort + f : nullptr, ce + (int64_t)f * kChainEvents, kChainEvents,
                               seed_word(seed), co + f,
                               mw > 0 ? S->chain_map.as<unsigned long long>() + map_off[(size_t)f] : nullptr, hend};
-            if (chh) chh[f] = ChainHelp{(int32_t)((hend + CHAIN_MAP_SEG - 1) / CHAIN_MAP_SEG), 0, 1, 0, 0, 0, 0, 0, INT64_MAX};
+            if (chh) chh[f] = ChainHelp{(int32_t)((hend + CHAIN_MAP_SEG - 1) / CHAIN_MAP_SEG), 0, 1, 0, 0, 0, 0, 0, INT64_MAX, 0, 0, 0};
         }
         const uint32_t n_help = !map_on ? 0u
                                 : helpers_opt > 0 ? (uint32_t)helpers_opt
@@ -1194,6 +1195,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             fs.rs.m = o.m;
             fs.rs.pref = o.pref;
             fs.rs.anchor = o.s;
+            fs.rs.clear_from = o.clear_to >= 0 ? o.s : -1;  // the walk searched up to the flush point
+            fs.rs.clear_to = o.clear_to;
             // a walk that stopped inside the prefix leaves only the prefix speculated (its file's other groups
             // stopped): the resolver's aligned lookups end there
             fs.be.na = o.aborted ? fs.na_a : fs.na;
@@ -1277,9 +1280,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                     }
                     const ChainHelp& q = hh[(size_t)fmax];
                     fprintf(stderr, "[rsh-batch]   hit map: %lld segments mapped over %lld files (%lld key sets built); file %d: %d "
-                            "segments, %d key sets, claims %d of %d, first segment %.1f us after the walk's start\n",
-                            (long long)segs, (long long)files_helped, (long long)joins, fmax, q.mapped, q.joins, q.claim,
-                            q.nseg, q.t_first == INT64_MAX ? -1.0 : (q.t_first - q.t_start) / 100.0);
+                            "segments (%d whole), %d key sets (%.1f us each), claims %d of %d, first whole segment %.1f us after "
+                            "the walk's start\n", (long long)segs, (long long)files_helped, (long long)joins, fmax, q.mapped,
+                            q.whole, q.joins, q.joins ? q.t_kset / 100.0 / q.joins : 0.0, q.claim, q.nseg,
+                            q.t_first == INT64_MAX ? -1.0 : (q.t_first - q.t_start) / 100.0);
                 }
             }
         }

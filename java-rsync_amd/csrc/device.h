@@ -310,6 +310,7 @@ struct ChainOut {
     int32_t spec_full;            // phase 1 walked it
     int32_t aborted;              // phase 0 stopped its phase-1 K1 groups: only the prefix is speculated
     int32_t mapped, first_mapped; // tiles answered from the hit map; the walk's tile count at the first (trace)
+    int64_t clear_to;             // stopped before a flush: no candidate in [s, clear_to] (else -1)
 };
 // The phase-0 hit map (chain_help): while one file's walk searches tile after tile on its CU, the workgroups whose
 // own walks have ended (and the launch's extra ones) map that file's prefix ahead of it -- in the synced state the
@@ -326,6 +327,8 @@ struct ChainHelp {
     int32_t mapped;  // segments mapped (trace)
     int32_t joins;   // helpers that built this file's key set (trace)
     int64_t t_start, t_first;  // wall clock: the walk's start, the first segment mapped ahead of it (trace)
+    int64_t t_kset;            // wall-clock ticks spent building this file's key set in helpers (trace)
+    int32_t whole, pad2;       // segments mapped whole, before the walk reached them (trace)
 };
 constexpr int CHAIN_THREADS = 512;                      // 8 waves (2 per SIMD: 256 VGPRs each)
 constexpr int CHAIN_PPT = 32;                            // wide tiles: positions per lane (two halves of 16)

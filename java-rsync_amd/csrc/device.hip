@@ -2880,10 +2880,13 @@ __device__ void chain_map_tile(const ChainFile& F, int64_t q0, uint32_t gen, con
     __syncthreads();  // (s_seg and sh: the next tile)
 }
 
-// A helper workgroup: while some walk that has searched at least two tiles is still running, take the next unmapped
-// segment of the one with the most segments left (its own current file first: the key set is built per file) and
-// map it tile by tile, stopping when the walk ends or has passed the tile.  No workgroup ever waits for another: a
-// walk reads a map word only when it carries this launch's generation, and searches the tile itself otherwise.
+constexpr int CHAIN_HELP_TILES = 4;   // a walk gets helpers once it has searched this many tiles
+constexpr int CHAIN_HELP_LEAD = 64;   // a helper stays with its file while the map leads the walk by fewer segments
+// A helper workgroup: while some walk that has searched CHAIN_HELP_TILES tiles is still running, take the next
+// unmapped segment of the one whose map leads it least (its own current file while the lead is short: the key set is
+// built per file) -- never the segment the walk is in, which it will finish first -- and map it tile by tile,
+// stopping when the walk ends or has passed the tile.  No workgroup ever waits for another: a walk reads a map word
+// only when it carries this launch's generation, and searches the tile itself otherwise.
 __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict__ files, int nfiles, uint32_t gen,
                                                      ChainHelp* help, uint2* ck, int32_t* ck_full,
                                                      int32_t* sh, int32_t (*s_seg)[4], unsigned long long* s_best,
@@ -2902,13 +2905,13 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
             // one round trip for the file's shared words
             const int32_t live = chain_ld(&h->live), tiles = chain_ld(&h->tiles), claim = chain_ld(&h->claim);
             const int64_t pos = chain_ld64(&h->pos);
-            if (live == 0 || tiles < 2 || claim >= nseg) continue;
+            if (live == 0 || tiles < CHAIN_HELP_TILES || claim >= nseg) continue;
             // the most urgent file: the map's frontier least far ahead of its walk (the current file while its
-            // frontier is within 8 segments of the walk: its key set is built)
+            // frontier is within CHAIN_HELP_LEAD segments of the walk: its key set is built)
             const int64_t lead = (int64_t)claim - pos / CHAIN_MAP_SEG;
             const uint32_t urg = (uint32_t)(lead < -1000 ? 2000 : lead > 999 ? 1 : 1000 - lead);
             const uint32_t tie = (((uint32_t)f * 0x9E3779B1u) ^ ((uint32_t)blockIdx.x * 0x85EBCA77u)) >> 20;
-            const unsigned long long key = ((unsigned long long)(f == cur && lead < 8) << 63) |
+            const unsigned long long key = ((unsigned long long)(f == cur && lead < CHAIN_HELP_LEAD) << 63) |
                                            ((unsigned long long)urg << 32) | ((unsigned long long)tie << 20) |
                                            (uint32_t)f;
             atomicMax(s_best, key);
@@ -2918,8 +2921,8 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
         if (best == 0ull) return;
         const int f = (int)(best & 0xFFFFFull);
         ChainHelp* h = help + f;
-        if (t == 0) {  // the segments behind the walk are skipped, not claimed one by one
-            atomicMax(&h->claim, (int32_t)(chain_ld64(&h->pos) / CHAIN_MAP_SEG));
+        if (t == 0) {  // the segment the walk is in and those behind it are skipped, not claimed one by one
+            atomicMax(&h->claim, (int32_t)(chain_ld64(&h->pos) / CHAIN_MAP_SEG) + 1);
             *s_word = atomicAdd(&h->claim, 1);
         }
         __syncthreads();
@@ -2927,8 +2930,10 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
         __syncthreads();
         if (seg >= h->nseg) continue;
         if (f != cur) {
+            const int64_t tb = (int64_t)wall_clock64();
             F = files[f];
             chain_kset_build(kset, F.table_weak, F.C);
+            if (t == 0) atomicAdd((unsigned long long*)&h->t_kset, (unsigned long long)((int64_t)wall_clock64() - tb));
             if (*kset.full) {  // not exact: the walk confirms keys in the chunk index; no map for this file
                 if (t == 0) atomicMax(&h->claim, h->nseg);
                 cur = -1;
@@ -2953,7 +2958,10 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
         }
         if (t == 0) {
             atomicAdd(&h->mapped, 1);
-            if (whole) atomicMin((unsigned long long*)&h->t_first, (unsigned long long)wall_clock64());
+            if (whole) {
+                atomicAdd(&h->whole, 1);
+                atomicMin((unsigned long long*)&h->t_first, (unsigned long long)wall_clock64());
+            }
         }
     }
 }
@@ -3041,6 +3049,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const int64_t tk0 = (int64_t)wall_clock64();
     int64_t t_tiles = 0, t_check = 0, t_event = 0, t_digest = 0;
     const uint8_t* stale = nullptr;  // poisoned: the cached digest
+    uint32_t dg[4] = {0u, 0u, 0u, 0u};  // the window's digest at the current event (poisoned: the stale one)
+    int64_t clear_to = -1;            // stopped at a flush point: no candidate in [s, clear_to]
     rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
     bool have = false;
     if (nev > 0) {  // phase 1: the last event stays open (a MATCH run may go on across the prefix's end)
@@ -3079,13 +3089,16 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             status = CHAIN_DONE;
             break;
         }
-        if (s % B != 0) break;  // phase-shifted windows: the host's phase speculation
+        // phase-shifted windows: the host's phase speculation.  A poisoned walk (a stale cached digest, quirk B) goes
+        // on from any position: only step (2) applies to it, and every candidate is compared with the stale digest
+        if (s % B != 0 && !poisoned) break;
         const int64_t k = s / B;
+        const bool al = s % B == 0;
         // the words steps (1), (1') and (2) look at first, loaded together: one global round trip per step instead of
         // three in sequence (a desynced walk takes these steps once per event)
-        const uint8_t flag_k = (k == pref && k < nflags) ? F.flags[k] : (uint8_t)0;
-        const int32_t aw_k = k < na ? F.aw[k] : 0;
-        const int32_t tw_pref = (pref < C && k < na) ? F.table_weak[pref] : 0;
+        const uint8_t flag_k = (!poisoned && k == pref && k < nflags) ? F.flags[k] : (uint8_t)0;
+        const int32_t aw_k = (al && k < na) ? F.aw[k] : 0;
+        const int32_t tw_pref = (!poisoned && pref < C && k < na) ? F.table_weak[pref] : 0;
         // (1) aligned chain: preferred index == k and source window k carries chunk k's sums
         if (flag_k) {
             if (t == 0) s_zero = nflags;
@@ -3129,7 +3142,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             continue;
         }
         // (1') the window at s against chunk pref while both sums agree (windows s + iB, chunks pref + i)
-        if (pref < C && k < na) {
+        if (!poisoned && pref < C && k < na) {
             int64_t lim = na - k;
             if (C - pref < lim) lim = C - pref;
             if ((last - s) / B + 1 < lim) lim = (last - s) / B + 1;
@@ -3159,7 +3172,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         int64_t p = -1;
         uint32_t key = 0;
         int64_t a = s;
-        if (k < na) {
+        if (al && k < na) {
             key = (uint32_t)aw_k;
             if (s_ck_full ? kslots_has(F.kslots, F.kmask, key) : chain_ck_has(kset, key)) p = s;
             else a = s + 1;
@@ -3394,7 +3407,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 if (na < F.na) status = CHAIN_MORE;
                 break;
             }
-            if (f <= last) break;  // a flush (quirk A): the host
+            if (f <= last) {  // a flush (quirk A): the host, which need not search [s, stop] again
+                clear_to = stop;
+                break;
+            }
             emit_lit(m, n - m);           // no candidate before the end
             status = CHAIN_DONE;
             s = n;
@@ -3404,9 +3420,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const int64_t te0 = (int64_t)wall_clock64();
         ++events;
         const int64_t kp = p / B;
-        const bool spec_digest = p % B == 0 && kp < na;
+        const bool spec_digest = !poisoned && p % B == 0 && kp < na;
         // the speculation's digest of an aligned window, loaded beside the bucket's slots (it depends only on p)
-        uint32_t dg[4] = {0u, 0u, 0u, 0u};
         if (spec_digest) chain_digest_load(F.as + kp * dl, dl, dg);
         if (t < 64) {
             // every chunk with this key lies on the probe path before the first empty slot: wave 0 reads 64 slots of
@@ -3456,8 +3471,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const int64_t w = B;  // p <= nB
         // Sender.java:1259-1263: the window's digest -- the speculation's at aligned positions, else one lane digests
         // the window here (lane_chunk_sums over the B bytes at p, the seed appended), the host path's md5_at
-        const uint8_t* md5c = F.as + kp * dl;
-        if (!spec_digest) {
+        const uint8_t* md5c = poisoned ? stale : F.as + kp * dl;
+        if (!spec_digest && !poisoned) {
             const int64_t td0 = (int64_t)wall_clock64();
             if (t == 0) chain_window_digest(F.data + p, n - p, (uint32_t)B, (uint32_t)dl, F.seed, &s_wtmp, s_dig);
             __syncthreads();
@@ -3483,10 +3498,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         __syncthreads();
         t_event += (int64_t)wall_clock64() - te0;
         if (hit < 0) {
-            // the cached digest is stale from here on (quirk B): the host goes on with it from p + 1 (a hit at the
-            // flush point itself flushes there: the host retakes that step from s)
+            // the cached digest is stale from here on (quirk B): the walk goes on with it from p + 1, comparing every
+            // later candidate with it, up to the next flush point (a hit at the flush point itself flushes there: the
+            // host retakes that step from s)
             if (p < f) {
                 s = p + 1;
+                if (poisoned) continue;  // (already stale: nothing changes)
                 poisoned = 1;
                 stale = md5c;
                 // no chunk carries the stale digest: nothing can match again (the host's closed form), so the
@@ -3515,6 +3532,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                         poisoned = 0;
                     }
                 }
+                if (!dead) continue;  // some chunk carries it: the search goes on from p + 1
             }
             break;
         }
@@ -3522,6 +3540,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         emit_match(p, w, hit, 1);
         pref = hit + 1;
         s = m = p + w;
+        poisoned = 0;  // a match clears the cached digest (Sender.java:1287)
     }
     flush_pend();
     if (t == 0) {
@@ -3540,6 +3559,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->t_digest += t_digest;
         out->spec_full = phase == 1;
         out->mapped = mapped;
+        out->clear_to = clear_to;
         out->first_mapped = first_mapped;
         // a file that needs no more speculation stops its phase-1 K1 groups (they poll this word); any other stop
         // keeps them (the resolver's aligned lookups past the prefix use them)

@@ -350,7 +350,8 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
                 if (size > 0) p = s;
                 else a = s + 1;
             }
-            if (p < 0 && a <= stop) {
+            const bool clear = state->clear_from == s && state->clear_to >= stop;  // the walk searched it
+            if (p < 0 && a <= stop && !clear) {
                 uint32_t el, eh;
                 E_at(a, &el, &eh);
                 const ProbeInterval one{a, stop + 1, a, el, eh};
@@ -358,6 +359,7 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
                 st.probe_launches++;
             }
         }
+        state->clear_from = state->clear_to = -1;
         if (p >= 0) {
             uint32_t el, eh;
             E_at(p, &el, &eh);

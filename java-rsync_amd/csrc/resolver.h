@@ -181,6 +181,9 @@ struct ResolveState {
     bool dkeys_ready = false;
     int64_t batch = 1;  // flush intervals speculated per batched probe
     bool done = false;
+    // handed over by the device chain walk: no candidate event in [clear_from, clear_to] -- its search reached the
+    // flush point -- so the first step (2) from s == clear_from needs no probe (consumed by that step)
+    int64_t clear_from = -1, clear_to = -1;
 };
 
 // n > 0 and h->block_length > 0 (skipMatchSendData / empty sources are handled by the caller).
