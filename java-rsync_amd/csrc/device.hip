@@ -3403,8 +3403,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             q0 = qend;
         }
         if (p < 0) {
-            if (cut) {  // past the speculation: the rest of it (phase 1), or the host
-                if (na < F.na) status = CHAIN_MORE;
+            if (cut) {  // past the speculation: the rest of it (phase 1), or the host -- which also takes a
+                // poisoned walk (phase 1 starts from the unpoisoned state)
+                if (na < F.na && !poisoned) status = CHAIN_MORE;
                 break;
             }
             if (f <= last) {  // a flush (quirk A): the host, which need not search [s, stop] again

@@ -451,3 +451,62 @@ def test_batch_chain_hit_map(ctx, helpers, rsh_opt, capfd):
         assert mapped == [0, 0]
     else:  # the long walks search ~1000 tiles each in phase 0: the helpers get ahead of them
         assert min(mapped) > 0, err[-2000:]
+
+
+@pytest.mark.parametrize("prefix,helpers", [(-1, -1), (64, -1), (64, 0), (8, -1)])
+def test_batch_poisoned_walk(ctx, prefix, helpers, rsh_opt):
+    """The walk past a poisoning (quirk B): a weak twin of chunk 5 poisons the state with a digest another chunk (the
+    carrier) carries, and the walk goes on with the stale digest -- every later candidate compared with it -- up to
+    the flush point, then hands the searched range to the resolver.  Forms: nothing more before the flush (the
+    resolver's flush chain follows without a probe of its own); the carrier's own bytes later in the interval,
+    aligned or not (the stale digest matches: a MATCH in the poisoned state, which clears it); a second twin after
+    the first (a candidate compared with the stale digest, no match).  prefix 8: the two-phase walk's prefix (8
+    windows) ends before the flush point, so the poisoned search runs past it and must stop for the resolver (phase 1
+    would resume unpoisoned).  Each file against the oracle."""
+    from test_gpu_probe_long import weak_twin_carrier
+    rsh_opt("batch_chain_prefix", prefix)
+    rsh_opt("chain_helpers", helpers)
+    B, dl, n = 4096, 2, 4 << 20
+    files = []
+    for form in range(5):
+        basis = O.splitmix(n, 0x5EED0000 + form)
+        twin, carrier = weak_twin_carrier(basis, B, dl)
+        src = O.splitmix(n, 0x5EED1000 + form).copy()
+        src[1000:1000 + B] = np.frombuffer(twin, np.uint8)
+        cb = basis[carrier * B:(carrier + 1) * B]
+        if form == 1:    # the carrier's bytes at an unaligned position before the flush point
+            src[3 * B + 77:4 * B + 77] = cb
+        elif form == 2:  # ... at an aligned one
+            src[5 * B:6 * B] = cb
+        elif form == 3:  # a second twin, then the carrier
+            src[2 * B + 500:3 * B + 500] = np.frombuffer(twin, np.uint8)
+            src[7 * B:8 * B] = cb
+        elif form == 4:  # the carrier, then identical blocks from the basis
+            src[4 * B:5 * B] = cb
+            src[6 * B:] = basis[6 * B:]
+        files.append((basis.tobytes(), src.tobytes(), B, dl))
+    d_src, soffs = _pack(ctx, [f[1] for f in files], [0] * len(files))
+    sj = (R.ScanJob * len(files))()
+    evs, keep, expect = [], [], []
+    for i, (basis, src, B, dl) in enumerate(files):
+        h = R.header_make(B, dl, len(basis))
+        w, s = ctx.block_sums(basis, h, SEED)
+        d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
+        d_w.upload(w)
+        d_s.upload(s)
+        keep += [d_w, d_s]
+        cap = len(src) // (10 * B) + 2 * h.chunk_count + 64
+        ev = np.zeros(cap, R.EVENT_DTYPE)
+        evs.append(ev)
+        sj[i].d_src, sj[i].n, sj[i].h = d_src.ptr.value + soffs[i], len(src), h
+        sj[i].d_weak, sj[i].d_strong = d_w.ptr.value, d_s.ptr.value
+        sj[i].ev, sj[i].ev_cap = ev.ctypes.data, cap
+        oev, _, olit, omat, _ = O.sender(src, O.header(B, dl, len(basis)), w, s, SEED)
+        expect.append(([tuple(e) for e in oev], olit, omat))
+    assert R.lib().rsh_match_scan_batch_device(ctx.handle, sj, len(files), SEED_NP.ctypes.data, None) == 0
+    for i, (basis, src, B, dl) in enumerate(files):
+        oev, olit, omat = expect[i]
+        assert sj[i].status == 0
+        assert R.events_as_tuples(evs[i][:sj[i].n_ev], B) == oev, f"form {i}"
+        assert (sj[i].literal, sj[i].matched) == (olit, omat)
+    assert any(e[0] == R.EV_MATCH for e in expect[1][0]), "form 1: the stale digest must match the carrier"
