@@ -328,7 +328,8 @@ struct ChainHelp {
     int32_t joins;   // helpers that built this file's key set (trace)
     int64_t t_start, t_first;  // wall clock: the walk's start, the first segment mapped ahead of it (trace)
     int64_t t_kset;            // wall-clock ticks spent building this file's key set in helpers (trace)
-    int32_t whole, pad2;       // segments mapped whole, before the walk reached them (trace)
+    int32_t whole;             // segments mapped whole, before the walk reached them (trace)
+    int32_t nhelp;             // helpers currently on this file
 };
 constexpr int CHAIN_THREADS = 512;                      // 8 waves (2 per SIMD: 256 VGPRs each)
 constexpr int CHAIN_PPT = 32;                            // wide tiles: positions per lane (two halves of 16)

@@ -2885,18 +2885,23 @@ constexpr int CHAIN_HELP_LEAD = 64;   // a helper stays with its file while the 
 // A helper workgroup: while some walk that has searched CHAIN_HELP_TILES tiles is still running, take the next
 // unmapped segment of the one whose map leads it least (its own current file while the lead is short: the key set is
 // built per file) -- never the segment the walk is in, which it will finish first -- and map it tile by tile,
-// stopping when the walk ends or has passed the tile.  No workgroup ever waits for another: a walk reads a map word
-// only when it carries this launch's generation, and searches the tile itself otherwise.
+// stopping when the walk ends or has passed the tile.  While walks are running that have not searched that far yet it
+// sleeps and looks again; once no mappable walk is running it leaves.  No walk ever waits for a helper: a walk reads
+// a map word only when it carries this launch's generation, and searches the tile itself otherwise.  (A helper waits
+// only for walks of its own launch, whose workgroups precede it in dispatch order.)
 __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict__ files, int nfiles, uint32_t gen,
                                                      ChainHelp* help, uint2* ck, int32_t* ck_full,
                                                      int32_t* sh, int32_t (*s_seg)[4], unsigned long long* s_best,
-                                                     int32_t* s_word) {
+                                                     int32_t* s_word, int32_t* s_live) {
     const int t = threadIdx.x;
     const ChainKeySet kset{ck, ck_full};
     int cur = -1;
     ChainFile F = files[0];
     for (;;) {
-        if (t == 0) *s_best = 0ull;
+        if (t == 0) {
+            *s_best = 0ull;
+            *s_live = 0;
+        }
         __syncthreads();
         for (int f = t; f < nfiles; f += CHAIN_THREADS) {
             ChainHelp* h = help + f;
@@ -2904,21 +2909,32 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
             if (nseg == 0) continue;
             // one round trip for the file's shared words
             const int32_t live = chain_ld(&h->live), tiles = chain_ld(&h->tiles), claim = chain_ld(&h->claim);
+            const int32_t nhelp = chain_ld(&h->nhelp);
             const int64_t pos = chain_ld64(&h->pos);
-            if (live == 0 || tiles < CHAIN_HELP_TILES || claim >= nseg) continue;
-            // the most urgent file: the map's frontier least far ahead of its walk (the current file while its
-            // frontier is within CHAIN_HELP_LEAD segments of the walk: its key set is built)
+            if (live == 0 || claim >= nseg) continue;
+            *s_live = 1;  // a walk that may still search: wait for it rather than leave
+            if (tiles < CHAIN_HELP_TILES) continue;
+            // the most urgent files first -- the map's frontier least far ahead of the walk, in four levels -- then
+            // the fewest helpers, then a hash that spreads the helpers; the current file while the map leads its
+            // walk by fewer than CHAIN_HELP_LEAD segments (its key set is built)
             const int64_t lead = (int64_t)claim - pos / CHAIN_MAP_SEG;
-            const uint32_t urg = (uint32_t)(lead < -1000 ? 2000 : lead > 999 ? 1 : 1000 - lead);
-            const uint32_t tie = (((uint32_t)f * 0x9E3779B1u) ^ ((uint32_t)blockIdx.x * 0x85EBCA77u)) >> 20;
+            const uint32_t level = lead <= 0 ? 3u : lead <= 4 ? 2u : lead <= 16 ? 1u : 0u;
+            const uint32_t few = 255u - (uint32_t)(nhelp < 0 ? 0 : nhelp > 255 ? 255 : nhelp);
+            const uint32_t tie = ((uint32_t)f * 0x9E3779B1u) ^ ((uint32_t)blockIdx.x * 0x85EBCA77u);
             const unsigned long long key = ((unsigned long long)(f == cur && lead < CHAIN_HELP_LEAD) << 63) |
-                                           ((unsigned long long)urg << 32) | ((unsigned long long)tie << 20) |
-                                           (uint32_t)f;
+                                           ((unsigned long long)level << 61) | ((unsigned long long)few << 53) |
+                                           ((unsigned long long)(tie >> 1) << 21) | (uint32_t)f;
             atomicMax(s_best, key);
         }
         __syncthreads();
         const unsigned long long best = *s_best;
-        if (best == 0ull) return;
+        const bool any_live = *s_live != 0;
+        __syncthreads();
+        if (best == 0ull) {
+            if (!any_live) break;  // every mappable walk has ended: nothing will come
+            __builtin_amdgcn_s_sleep(64);  // walks still short of CHAIN_HELP_TILES tiles: look again shortly
+            continue;
+        }
         const int f = (int)(best & 0xFFFFFull);
         ChainHelp* h = help + f;
         if (t == 0) {  // the segment the walk is in and those behind it are skipped, not claimed one by one
@@ -2930,18 +2946,23 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
         __syncthreads();
         if (seg >= h->nseg) continue;
         if (f != cur) {
+            if (t == 0) {
+                if (cur >= 0) atomicSub(&help[cur].nhelp, 1);
+                atomicAdd(&h->nhelp, 1);
+            }
+            cur = f;
             const int64_t tb = (int64_t)wall_clock64();
             F = files[f];
             chain_kset_build(kset, F.table_weak, F.C);
-            if (t == 0) atomicAdd((unsigned long long*)&h->t_kset, (unsigned long long)((int64_t)wall_clock64() - tb));
+            if (t == 0) {
+                atomicAdd((unsigned long long*)&h->t_kset, (unsigned long long)((int64_t)wall_clock64() - tb));
+                atomicAdd(&h->joins, 1);
+            }
             if (*kset.full) {  // not exact: the walk confirms keys in the chunk index; no map for this file
                 if (t == 0) atomicMax(&h->claim, h->nseg);
-                cur = -1;
                 __syncthreads();
                 continue;
             }
-            cur = f;
-            if (t == 0) atomicAdd(&h->joins, 1);
         }
         const int64_t lo = (int64_t)seg * CHAIN_MAP_SEG, hi = lo + CHAIN_MAP_SEG < F.hend ? lo + CHAIN_MAP_SEG : F.hend;
         bool whole = true;
@@ -2964,6 +2985,7 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
             }
         }
     }
+    if (t == 0 && cur >= 0) atomicSub(&help[cur].nhelp, 1);
 }
 
 __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const ChainFile* __restrict__ files, int phase,
@@ -2982,10 +3004,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_ck_full;
     __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
     __shared__ unsigned long long s_best;      // helpers: the file to map next
-    __shared__ int32_t s_word;
+    __shared__ int32_t s_word, s_live;
     const ChainKeySet kset{s_ck, &s_ck_full};
     if ((int)blockIdx.x >= nfiles) {  // a helper workgroup (phase 0): it only maps
-        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word);
+        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live);
         return;
     }
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
@@ -3578,7 +3600,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     if (H != nullptr) {  // this walk is over: its helpers stop, and the workgroup helps the walks still searching
         if (t == 0) chain_st(&H->live, 0);
         __syncthreads();
-        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word);
+        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live);
     }
 }
 
