@@ -2717,10 +2717,51 @@ __device__ __forceinline__ int chain_first_hit16(const unsigned long long* __res
     return hit ? __builtin_ctz(hit) : -1;
 }
 
-// one lane digests an unaligned hit's window: out of line, so that the walk's tile search keeps its registers
-__device__ __attribute__((noinline)) void chain_window_digest(const uint8_t* x, int64_t n, uint32_t B, uint32_t dl,
-                                                              uint32_t seed, int32_t* w, uint8_t* dig) {
-    lane_chunk_sums<0, 2, false>(x, n, B, 0u, dl, seed, w, dig);
+// An unaligned hit's window digest (MD5 of its L bytes, the seed appended, dl bytes kept), by the whole workgroup: the
+// bytes staged through LDS in pieces of CHAIN_WIN_BUF (each thread one 16-byte aligned load of the source per granule,
+// the source's misalignment taken out by the byte stores), lane 0 compressing each piece from LDS.  The compression is
+// one dependent chain (~90 us for 8 KiB on one lane); staging takes the global-load latency off it (a lane loading two
+// blocks ahead spent ~150 us).  Out of line, so that the walk's tile search keeps its registers.
+constexpr int CHAIN_WIN_BUF = 16384;
+__device__ __attribute__((noinline)) void chain_window_digest(const uint8_t* x, uint32_t L, uint32_t dl, uint32_t seed,
+                                                              uint8_t* buf, uint8_t* dig) {
+    const int t = threadIdx.x;
+    Md5State st = md5_init();
+    for (uint32_t c0 = 0; c0 < L; c0 += CHAIN_WIN_BUF) {
+        const uint32_t len = L - c0 < (uint32_t)CHAIN_WIN_BUF ? L - c0 : (uint32_t)CHAIN_WIN_BUF;
+        const uintptr_t xa = reinterpret_cast<uintptr_t>(x) + c0, a0 = xa & ~(uintptr_t)15;
+        const int32_t shift = (int32_t)(xa - a0);
+        // every granule overlaps [xa, xa + len), so it lies in a page the source occupies
+        for (int32_t g = 16 * t; g < shift + (int32_t)len; g += 16 * CHAIN_THREADS) {
+            const uint4 q = *reinterpret_cast<const uint4*>(a0 + (uintptr_t)g);
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int32_t o = g + k - shift;
+                if (o >= 0 && o < (int32_t)len) buf[o] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+            }
+        }
+        __syncthreads();
+        if (t == 0) {
+            const uint32_t nfull = len >> 6;
+            for (uint32_t b = 0; b < nfull; ++b) {
+                uint32_t m[16];
+                const uint4* q = reinterpret_cast<const uint4*>(buf + 64 * b);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint4 v = q[i];
+                    m[4 * i] = v.x, m[4 * i + 1] = v.y, m[4 * i + 2] = v.z, m[4 * i + 3] = v.w;
+                }
+                md5_compress(st, m);
+            }
+            if (c0 + len == L) {  // the last piece: its remainder, the seed, the padding
+                int32_t s1 = 0, u = 0;
+                md5_tail(st, buf + 64 * nfull, len & 63u, seed, (uint64_t)L + 4, s1, u, 0u);
+                store_digest(dig, st, dl);
+            }
+        }
+        __syncthreads();
+    }
 }
 
 __device__ __forceinline__ bool chain_digest_eq(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int dl) {
@@ -2997,7 +3038,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_bk[CHAIN_BUCKET_CAP];  // bucket of the key (ascending chunk index)
     __shared__ int32_t s_nbk;
     __shared__ int64_t s_zero;                 // first unset chain flag
-    __shared__ int32_t s_wtmp;                 // an unaligned window's sums (its digest: s_dig)
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[CHAIN_WIN_BUF];  // an unaligned window's bytes (its digest: s_dig)
     __shared__ int32_t s_any;                  // some chunk carries the stale digest
     __shared__ int32_t s_seg[CHAIN_SEGS][4];   // wide tiles: the exscan at each block's first lane
     __shared__ uint2 s_ck[2 * CHAIN_CK_BUCKETS];  // the table's keys (ChainKeySet)
@@ -3497,8 +3538,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const uint8_t* md5c = poisoned ? stale : F.as + kp * dl;
         if (!spec_digest && !poisoned) {
             const int64_t td0 = (int64_t)wall_clock64();
-            if (t == 0) chain_window_digest(F.data + p, n - p, (uint32_t)B, (uint32_t)dl, F.seed, &s_wtmp, s_dig);
-            __syncthreads();
+            chain_window_digest(F.data + p, (uint32_t)B, (uint32_t)dl, F.seed, s_win, s_dig);  // (ends with a barrier)
             md5c = s_dig;
             chain_digest_load(s_dig, dl, dg);
             ++digests;
