@@ -229,6 +229,11 @@ extern "C" int64_t rtest_hit_cache(int on) {
     return a;
 }
 
+// >= 0: the scan starts as the device chain walk hands a file over (batch.cpp): no candidate in [0, clear_to], so
+// the first step (2) from s = 0 needs no probe when clear_to reaches its stop
+static int64_t g_clear_to = -1;
+extern "C" void rtest_clear(int64_t clear_to) { g_clear_to = clear_to; }
+
 extern "C" int rtest_scan_staged(const uint8_t* src, int64_t n, const rsh_header* h, const int32_t* weak,
                                  const uint8_t* strong, const uint8_t seed[4], rsh_event* ev, int64_t cap,
                                  int64_t* n_ev, int64_t* lit, int64_t* mat, rsh_scan_stats* stats, int64_t head_steps) {
@@ -245,7 +250,12 @@ extern "C" int rtest_scan_staged(const uint8_t* src, int64_t n, const rsh_header
     be.use_phase = g_phase >= 0;
     be.phase_lag = g_phase < 0 ? 0 : g_phase;
     rsh::ResolveResult r;
-    if (head_steps < 0) {
+    if (head_steps < 0 && g_clear_to >= 0) {
+        rsh::ResolveState st;
+        st.clear_from = 0;
+        st.clear_to = g_clear_to;
+        rsh::resolve_run(n, t, be, &st, &r, nullptr);
+    } else if (head_steps < 0) {
         rsh::resolve_scan(n, t, be, &r);
     } else {
         rsh::ResolveState st;

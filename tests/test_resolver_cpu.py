@@ -259,3 +259,32 @@ def test_resolver_phase_chains(seed_i):
     finally:
         L.rtest_phase(-1)
     assert answered > 0
+
+
+def test_resolver_walk_handoff_clear_range():
+    """The chain walk's handoff (ResolveState.clear_from / clear_to, batch.cpp): a walk that searched up to the flush
+    point without a candidate tells the resolver so, and its first step (2) goes to the batched flush chain without a
+    probe of its own.  An unrelated source (no candidate before the first flush point): the same events as the
+    oracle, one probe fewer; a range short of the stop changes nothing."""
+    L = rlib()
+    L.rtest_clear.argtypes = [ctypes.c_int64]
+    B, dl = 1024, 2
+    basis = O.splitmix(64 * B, 0xC1EA)
+    src = O.splitmix(200 * B, 0xC1EB)
+    h = O.header(B, dl, len(basis))
+    seed = bytes([1, 2, 3, 4])
+    w, s = O.generator(basis, h, seed)
+    oev, _, olit, omat, _ = O.sender(src, h, w, s, seed)
+    assert all(e[0] == R.EV_LITERAL for e in oev), "the source must have no candidate at all"
+    rh = R.Header(**h.as_dict())
+    runs = {}
+    for clear in (-1, 9 * B, 9 * B - 1):
+        L.rtest_clear(clear)
+        try:
+            ev, lit, mat, st = resolve(src, rh, w, s, seed)
+        finally:
+            L.rtest_clear(-1)
+        assert R.events_as_tuples(ev, B) == [tuple(e) for e in oev]
+        assert (lit, mat) == (olit, omat)
+        runs[clear] = st["probe_launches"]
+    assert runs[9 * B] == runs[-1] - 1 and runs[9 * B - 1] == runs[-1]
