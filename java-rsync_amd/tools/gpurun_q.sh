@@ -6,7 +6,7 @@
 log=$1
 lim=$2
 cmd=$3
-for i in $(seq 1 12); do
+for i in $(seq 1 40); do
     /usr/local/graft/bin/gpurun --timeout "$lim" -- "$cmd" > "$log" 2>&1
     rc=$?
     [ $rc -ne 3 ] && break
