@@ -3486,7 +3486,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const int64_t kp = p / B;
         const bool spec_digest = !poisoned && p % B == 0 && kp < na;
         // the speculation's digest of an aligned window, loaded beside the bucket's slots (it depends only on p)
+        // ... and chunk kp's own digest beside it: the candidate of a window that sits where its chunk sat (identical
+        // stretches, edited blocks in place) is decided without another round trip
+        uint32_t dgk[4] = {0u, 0u, 0u, 0u};
+        const bool diag = spec_digest && kp < C;
         if (spec_digest) chain_digest_load(F.as + kp * dl, dl, dg);
+        if (diag) chain_digest_load(F.table_strong + kp * dl, dl, dgk);
         if (t < 64) {
             // every chunk with this key lies on the probe path before the first empty slot: wave 0 reads 64 slots of
             // it per round trip (one, nearly always) instead of one dependent load per slot
@@ -3556,7 +3561,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 pos = it;
             }
             const int32_t c = s_bk[pos];
-            if (chain_digest_eq_reg(dg, F.table_strong + (int64_t)c * dl, dl)) hit = c;
+            const bool eq = (diag && c == kp) ? ((dg[0] ^ dgk[0]) | (dg[1] ^ dgk[1]) | (dg[2] ^ dgk[2]) | (dg[3] ^ dgk[3])) == 0u
+                                              : chain_digest_eq_reg(dg, F.table_strong + (int64_t)c * dl, dl);
+            if (eq) hit = c;
         }
         __syncthreads();
         t_event += (int64_t)wall_clock64() - te0;
