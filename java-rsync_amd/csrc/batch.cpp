@@ -1265,8 +1265,11 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                     (long long)msum, tmax, (long long)esum, emax,
                     (long long)dsum, (long long)psum, (long long)asum, left, NF);
             const ChainOut& x = co[fmax];  // the walk with the most tiles: where its time went (10 ns ticks)
-            fprintf(stderr, "[rsh-batch]   file %d: stopped at s %lld (status %d, poisoned %d, searched to %lld, phase 1 %d)\n",
-                    fmax, (long long)x.s, x.status, x.md5c_valid, (long long)x.clear_to, x.spec_full);
+            for (int32_t f = 0; f < NF; ++f)  // the walks that left their files to the resolvers: where and why
+                if (co[f].status != CHAIN_DONE)
+                    fprintf(stderr, "[rsh-batch]   file %d: left at s %lld (events %lld, tiles %d, poisoned %d, searched to %lld, "
+                            "phase 1 %d, walk %.1f us)\n", f, (long long)co[f].s, (long long)co[f].events, co[f].tiles,
+                            co[f].md5c_valid, (long long)co[f].clear_to, co[f].spec_full, co[f].t_total / 100.0);
             fprintf(stderr, "[rsh-batch]   file %d: walk %.1f us = tiles %.1f (table checks %.1f; %d of %d tiles from the hit map,"
                     " the first at tile %d) + events %.1f (digests %.1f) + other\n", fmax, x.t_total / 100.0,
                     x.t_tiles / 100.0, x.t_check / 100.0, x.mapped, x.tiles, x.first_mapped, x.t_event / 100.0,

@@ -2717,18 +2717,108 @@ __device__ __forceinline__ int chain_first_hit16(const unsigned long long* __res
     return hit ? __builtin_ctz(hit) : -1;
 }
 
+// One MD5 compression on the scalar unit: every value wave-uniform (SGPRs), the round functions and adds as SALU
+// instructions, the rotates as SALU shift pairs (the backend would otherwise form v_alignbit and move the chain to the
+// VALU).  A single message is one dependent chain: on the VALU each dependent instruction waits out the wave64
+// pipeline (~8 cycles), on the SALU ~1-2.
+__device__ __forceinline__ uint32_t md5s_rotl(uint32_t x, uint32_t s, uint32_t r) {  // s + r = 32, both immediate
+    uint32_t y, z;
+    asm("s_lshl_b32 %0, %2, %3\n\ts_lshr_b32 %1, %2, %4\n\ts_or_b32 %0, %0, %1"
+        : "=&s"(y), "=&s"(z)
+        : "s"(x), "n"(s), "n"(r)
+        : "scc");
+    return y;
+}
+#define RSH_MD5S_STEP(f, a, b, c, d, m, k, s) (a) = (b) + md5s_rotl((a) + f((b), (c), (d)) + (m) + (k), (s), 32 - (s))
+__device__ __forceinline__ void md5_compress_scalar(Md5State& st, const uint32_t (&m)[16]) {
+    uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
+    RSH_MD5S_STEP(RSH_MD5_F, a, b, c, d, m[0], 0xd76aa478u, 7);
+    RSH_MD5S_STEP(RSH_MD5_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
+    RSH_MD5S_STEP(RSH_MD5_F, c, d, a, b, m[2], 0x242070dbu, 17);
+    RSH_MD5S_STEP(RSH_MD5_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
+    RSH_MD5S_STEP(RSH_MD5_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
+    RSH_MD5S_STEP(RSH_MD5_F, d, a, b, c, m[5], 0x4787c62au, 12);
+    RSH_MD5S_STEP(RSH_MD5_F, c, d, a, b, m[6], 0xa8304613u, 17);
+    RSH_MD5S_STEP(RSH_MD5_F, b, c, d, a, m[7], 0xfd469501u, 22);
+    RSH_MD5S_STEP(RSH_MD5_F, a, b, c, d, m[8], 0x698098d8u, 7);
+    RSH_MD5S_STEP(RSH_MD5_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
+    RSH_MD5S_STEP(RSH_MD5_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
+    RSH_MD5S_STEP(RSH_MD5_F, b, c, d, a, m[11], 0x895cd7beu, 22);
+    RSH_MD5S_STEP(RSH_MD5_F, a, b, c, d, m[12], 0x6b901122u, 7);
+    RSH_MD5S_STEP(RSH_MD5_F, d, a, b, c, m[13], 0xfd987193u, 12);
+    RSH_MD5S_STEP(RSH_MD5_F, c, d, a, b, m[14], 0xa679438eu, 17);
+    RSH_MD5S_STEP(RSH_MD5_F, b, c, d, a, m[15], 0x49b40821u, 22);
+    RSH_MD5S_STEP(RSH_MD5_G, a, b, c, d, m[1], 0xf61e2562u, 5);
+    RSH_MD5S_STEP(RSH_MD5_G, d, a, b, c, m[6], 0xc040b340u, 9);
+    RSH_MD5S_STEP(RSH_MD5_G, c, d, a, b, m[11], 0x265e5a51u, 14);
+    RSH_MD5S_STEP(RSH_MD5_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
+    RSH_MD5S_STEP(RSH_MD5_G, a, b, c, d, m[5], 0xd62f105du, 5);
+    RSH_MD5S_STEP(RSH_MD5_G, d, a, b, c, m[10], 0x02441453u, 9);
+    RSH_MD5S_STEP(RSH_MD5_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
+    RSH_MD5S_STEP(RSH_MD5_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+    RSH_MD5S_STEP(RSH_MD5_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
+    RSH_MD5S_STEP(RSH_MD5_G, d, a, b, c, m[14], 0xc33707d6u, 9);
+    RSH_MD5S_STEP(RSH_MD5_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
+    RSH_MD5S_STEP(RSH_MD5_G, b, c, d, a, m[8], 0x455a14edu, 20);
+    RSH_MD5S_STEP(RSH_MD5_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
+    RSH_MD5S_STEP(RSH_MD5_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
+    RSH_MD5S_STEP(RSH_MD5_G, c, d, a, b, m[7], 0x676f02d9u, 14);
+    RSH_MD5S_STEP(RSH_MD5_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
+    RSH_MD5S_STEP(RSH_MD5_H, a, b, c, d, m[5], 0xfffa3942u, 4);
+    RSH_MD5S_STEP(RSH_MD5_H, d, a, b, c, m[8], 0x8771f681u, 11);
+    RSH_MD5S_STEP(RSH_MD5_H, c, d, a, b, m[11], 0x6d9d6122u, 16);
+    RSH_MD5S_STEP(RSH_MD5_H, b, c, d, a, m[14], 0xfde5380cu, 23);
+    RSH_MD5S_STEP(RSH_MD5_H, a, b, c, d, m[1], 0xa4beea44u, 4);
+    RSH_MD5S_STEP(RSH_MD5_H, d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    RSH_MD5S_STEP(RSH_MD5_H, c, d, a, b, m[7], 0xf6bb4b60u, 16);
+    RSH_MD5S_STEP(RSH_MD5_H, b, c, d, a, m[10], 0xbebfbc70u, 23);
+    RSH_MD5S_STEP(RSH_MD5_H, a, b, c, d, m[13], 0x289b7ec6u, 4);
+    RSH_MD5S_STEP(RSH_MD5_H, d, a, b, c, m[0], 0xeaa127fau, 11);
+    RSH_MD5S_STEP(RSH_MD5_H, c, d, a, b, m[3], 0xd4ef3085u, 16);
+    RSH_MD5S_STEP(RSH_MD5_H, b, c, d, a, m[6], 0x04881d05u, 23);
+    RSH_MD5S_STEP(RSH_MD5_H, a, b, c, d, m[9], 0xd9d4d039u, 4);
+    RSH_MD5S_STEP(RSH_MD5_H, d, a, b, c, m[12], 0xe6db99e5u, 11);
+    RSH_MD5S_STEP(RSH_MD5_H, c, d, a, b, m[15], 0x1fa27cf8u, 16);
+    RSH_MD5S_STEP(RSH_MD5_H, b, c, d, a, m[2], 0xc4ac5665u, 23);
+    RSH_MD5S_STEP(RSH_MD5_I, a, b, c, d, m[0], 0xf4292244u, 6);
+    RSH_MD5S_STEP(RSH_MD5_I, d, a, b, c, m[7], 0x432aff97u, 10);
+    RSH_MD5S_STEP(RSH_MD5_I, c, d, a, b, m[14], 0xab9423a7u, 15);
+    RSH_MD5S_STEP(RSH_MD5_I, b, c, d, a, m[5], 0xfc93a039u, 21);
+    RSH_MD5S_STEP(RSH_MD5_I, a, b, c, d, m[12], 0x655b59c3u, 6);
+    RSH_MD5S_STEP(RSH_MD5_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
+    RSH_MD5S_STEP(RSH_MD5_I, c, d, a, b, m[10], 0xffeff47du, 15);
+    RSH_MD5S_STEP(RSH_MD5_I, b, c, d, a, m[1], 0x85845dd1u, 21);
+    RSH_MD5S_STEP(RSH_MD5_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
+    RSH_MD5S_STEP(RSH_MD5_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+    RSH_MD5S_STEP(RSH_MD5_I, c, d, a, b, m[6], 0xa3014314u, 15);
+    RSH_MD5S_STEP(RSH_MD5_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
+    RSH_MD5S_STEP(RSH_MD5_I, a, b, c, d, m[4], 0xf7537e82u, 6);
+    RSH_MD5S_STEP(RSH_MD5_I, d, a, b, c, m[11], 0xbd3af235u, 10);
+    RSH_MD5S_STEP(RSH_MD5_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+    RSH_MD5S_STEP(RSH_MD5_I, b, c, d, a, m[9], 0xeb86d391u, 21);
+    st.a += a;
+    st.b += b;
+    st.c += c;
+    st.d += d;
+}
+
 // An unaligned hit's window digest (MD5 of its L bytes, the seed appended, dl bytes kept), by the whole workgroup: the
 // bytes staged through LDS in pieces of CHAIN_WIN_BUF (each thread one 16-byte aligned load of the source per granule,
-// the source's misalignment taken out by the byte stores), lane 0 compressing each piece from LDS.  The compression is
-// one dependent chain (~90 us for 8 KiB on one lane); staging takes the global-load latency off it (a lane loading two
-// blocks ahead spent ~150 us).  Out of line, so that the walk's tile search keeps its registers.
+// the source's misalignment taken out by the byte stores; the last piece also gets the seed and the padding), wave 0
+// compressing each piece on the scalar unit (md5_compress_scalar, the words read from LDS and made uniform).  A lane
+// compressing on the VALU with loads two blocks ahead spent ~170 us on an 8 KiB window.  Out of line, so that the
+// walk's tile search keeps its registers.
 constexpr int CHAIN_WIN_BUF = 16384;
 __device__ __attribute__((noinline)) void chain_window_digest(const uint8_t* x, uint32_t L, uint32_t dl, uint32_t seed,
-                                                              uint8_t* buf, uint8_t* dig) {
+                                                              uint8_t* buf /* CHAIN_WIN_BUF + 128 */, uint8_t* dig) {
     const int t = threadIdx.x;
+    // (a callee's arguments arrive in VGPRs: made uniform, so that the loops and the state stay scalar)
+    L = __builtin_amdgcn_readfirstlane(L);
+    seed = __builtin_amdgcn_readfirstlane(seed);
     Md5State st = md5_init();
     for (uint32_t c0 = 0; c0 < L; c0 += CHAIN_WIN_BUF) {
         const uint32_t len = L - c0 < (uint32_t)CHAIN_WIN_BUF ? L - c0 : (uint32_t)CHAIN_WIN_BUF;
+        const bool last = c0 + len == L;
         const uintptr_t xa = reinterpret_cast<uintptr_t>(x) + c0, a0 = xa & ~(uintptr_t)15;
         const int32_t shift = (int32_t)(xa - a0);
         // every granule overlaps [xa, xa + len), so it lies in a page the source occupies
@@ -2741,27 +2831,31 @@ __device__ __attribute__((noinline)) void chain_window_digest(const uint8_t* x, 
                 if (o >= 0 && o < (int32_t)len) buf[o] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
             }
         }
+        // the last piece: the seed, 0x80, zeros, the message's bit length (L + 4 bytes), to a whole block
+        const uint32_t plen = last ? ((len + 4 + 1 + 8 + 63) & ~63u) : len;
+        if (last && (uint32_t)t < plen - len) {
+            const uint32_t i = len + (uint32_t)t;
+            const uint64_t bits = ((uint64_t)L + 4) * 8;
+            uint32_t v = 0;
+            if (t < 4) v = (seed >> (8 * t)) & 0xFFu;
+            else if (t == 4) v = 0x80u;
+            else if (i >= plen - 8) v = (uint32_t)(bits >> (8 * (i - (plen - 8)))) & 0xFFu;
+            buf[i] = (uint8_t)v;
+        }
         __syncthreads();
-        if (t == 0) {
-            const uint32_t nfull = len >> 6;
-            for (uint32_t b = 0; b < nfull; ++b) {
+        if (__builtin_amdgcn_readfirstlane(t >> 6) == 0) {  // wave 0 (a wave-uniform test: the state stays in SGPRs)
+            const uint32_t* bw = reinterpret_cast<const uint32_t*>(buf);
+            for (uint32_t b = 0; b < plen / 64; ++b) {
                 uint32_t m[16];
-                const uint4* q = reinterpret_cast<const uint4*>(buf + 64 * b);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint4 v = q[i];
-                    m[4 * i] = v.x, m[4 * i + 1] = v.y, m[4 * i + 2] = v.z, m[4 * i + 3] = v.w;
-                }
-                md5_compress(st, m);
-            }
-            if (c0 + len == L) {  // the last piece: its remainder, the seed, the padding
-                int32_t s1 = 0, u = 0;
-                md5_tail(st, buf + 64 * nfull, len & 63u, seed, (uint64_t)L + 4, s1, u, 0u);
-                store_digest(dig, st, dl);
+                for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_readfirstlane(bw[16 * b + i]);
+                md5_compress_scalar(st, m);
             }
         }
         __syncthreads();
     }
+    if (t == 0) store_digest(dig, st, dl);
+    __syncthreads();
 }
 
 __device__ __forceinline__ bool chain_digest_eq(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int dl) {
@@ -3038,7 +3132,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_bk[CHAIN_BUCKET_CAP];  // bucket of the key (ascending chunk index)
     __shared__ int32_t s_nbk;
     __shared__ int64_t s_zero;                 // first unset chain flag
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[CHAIN_WIN_BUF];  // an unaligned window's bytes (its digest: s_dig)
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[CHAIN_WIN_BUF + 128];  // an unaligned window's bytes (its digest: s_dig)
     __shared__ int32_t s_any;                  // some chunk carries the stale digest
     __shared__ int32_t s_seg[CHAIN_SEGS][4];   // wide tiles: the exscan at each block's first lane
     __shared__ uint2 s_ck[2 * CHAIN_CK_BUCKETS];  // the table's keys (ChainKeySet)
