@@ -1048,6 +1048,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         if (r != RSH_OK) return r;
     }
     bool spec_launched = false;
+    bool skip_rest = false;  // two phases, and phase 0 finished or handed over every file: no rest speculated
     if (chain_on) {  // the speculation, then the walks on the context stream (beside the sums' download on aux)
         ChainFile* cf = S->h_chain.as<ChainFile>();
         ChainOut* co = S->h_chain_out.as<ChainOut>();
@@ -1148,21 +1149,42 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, 0, gen_b, map_on ? S->chain_help.as<ChainHelp>() : nullptr,
                                           n_help));
             RSH_BHIP(hipEventRecord(S->ev_wa, st));
-            // the rest of the speculation after the walks (the groups of files they finished stop at once), or
-            // (option batch_chain_overlap) beside them: no gap after the prefix's K1, but the walks share the chip
-            if (opt(OPT_BATCH_CHAIN_OVERLAP) == 0) RSH_BHIP(hipStreamWaitEvent(aux, S->ev_wa, 0));
-            RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>() + ng_a, ng_b, S->k1_lanes.as<K1Lane>() + nla,
-                                             (uint32_t)nlb, align_b, seed_word(seed), aux, c->abort_word, gen_b, partial_b));
-            k1_launched = true;
+            // (option batch_skip_rest) once phase 0 has ended, the rest of the speculation only if some walk reached
+            // the prefix's end (CHAIN_MORE): otherwise every file is done, or left to its resolver with the prefix
+            // speculated, and the rest's launch -- all its groups stopping at once, ~0.17 ms of dispatch for config 4's
+            // 30720 -- its flags and phase 1 are skipped.  The host waits for phase 0 either way (a few us more before
+            // the rest's launch when it is needed).
+            if (opt(OPT_BATCH_SKIP_REST) != 0 && opt(OPT_BATCH_CHAIN_OVERLAP) == 0) {
+                RSH_BHIP(hipEventSynchronize(S->ev_wa));
+                skip_rest = true;
+                for (int32_t f = 0; f < NF && skip_rest; ++f) skip_rest = co[f].status != CHAIN_MORE;
+            }
+            if (!skip_rest) {
+                // the rest of the speculation after the walks (the groups of files they finished stop at once), or
+                // (option batch_chain_overlap) beside them: no gap after the prefix's K1, but the walks share the chip
+                if (opt(OPT_BATCH_CHAIN_OVERLAP) == 0) RSH_BHIP(hipStreamWaitEvent(aux, S->ev_wa, 0));
+                RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>() + ng_a, ng_b, S->k1_lanes.as<K1Lane>() + nla,
+                                                 (uint32_t)nlb, align_b, seed_word(seed), aux, c->abort_word, gen_b,
+                                                 partial_b));
+                k1_launched = true;
+            }
             if (opt(OPT_SCAN_TRACE))
-                fprintf(stderr, "[rsh-batch] two-phase speculation: prefix %u groups, rest %u groups\n", ng_a, ng_b);
+                fprintf(stderr, "[rsh-batch] two-phase speculation: prefix %u groups, rest %u groups%s\n", ng_a, ng_b,
+                        skip_rest ? " (skipped: no walk reached the prefix's end)" : "");
         }
-        const int r = launch_spec();  // (two phases: the flags of whole files and the downloads)
-        if (r != RSH_OK) return r;
-        spec_launched = true;
-        RSH_BHIP(hipStreamWaitEvent(st, S->ev_fk, 0));
-        if (tr && !two_phase) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
-        RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, two_phase ? 1 : 0, 0));
+        if (!skip_rest) {
+            const int r = launch_spec();  // (two phases: the flags of whole files and the downloads)
+            if (r != RSH_OK) return r;
+            spec_launched = true;
+            RSH_BHIP(hipStreamWaitEvent(st, S->ev_fk, 0));
+            if (tr && !two_phase) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
+            RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, two_phase ? 1 : 0, 0));
+        } else {  // what waits on the speculation's events below finds them complete (phase 0 is)
+            RSH_BHIP(hipEventRecord(c->ev_flags, st));
+            RSH_BHIP(hipEventRecord(c->ev_spec, st));
+            RSH_BHIP(hipEventRecord(S->ev_fk, st));
+            spec_launched = true;
+        }
         if (tr) RSH_BHIP(hipEventRecord(S->ev_ch1, st));
     }
     const double enq_ms = ms_since(t0);
@@ -1199,7 +1221,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             fs.rs.clear_to = o.clear_to;
             // a walk that stopped inside the prefix leaves only the prefix speculated (its file's other groups
             // stopped): the resolver's aligned lookups end there
-            fs.be.na = o.aborted ? fs.na_a : fs.na;
+            fs.be.na = (o.aborted || skip_rest) ? fs.na_a : fs.na;
             if (o.md5c_valid) {  // poisoned at an unaligned hit: the resolver goes on with the stale digest
                 fs.rs.md5c.assign(o.md5c, o.md5c + fs.dl);
                 fs.rs.md5c_valid = true;
@@ -1267,9 +1289,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             const ChainOut& x = co[fmax];  // the walk with the most tiles: where its time went (10 ns ticks)
             for (int32_t f = 0; f < NF; ++f)  // the walks that left their files to the resolvers: where and why
                 if (co[f].status != CHAIN_DONE)
-                    fprintf(stderr, "[rsh-batch]   file %d: left at s %lld (events %lld, tiles %d, poisoned %d, searched to %lld, "
-                            "phase 1 %d, walk %.1f us)\n", f, (long long)co[f].s, (long long)co[f].events, co[f].tiles,
-                            co[f].md5c_valid, (long long)co[f].clear_to, co[f].spec_full, co[f].t_total / 100.0);
+                    fprintf(stderr, "[rsh-batch]   file %d: left at s %lld (why %d, events %lld, tiles %d, poisoned %d, searched to "
+                            "%lld, phase 1 %d, walk %.1f us)\n", f, (long long)co[f].s, co[f].why, (long long)co[f].events,
+                            co[f].tiles, co[f].md5c_valid, (long long)co[f].clear_to, co[f].spec_full, co[f].t_total / 100.0);
             fprintf(stderr, "[rsh-batch]   file %d: walk %.1f us = tiles %.1f (table checks %.1f; %d of %d tiles from the hit map,"
                     " the first at tile %d) + events %.1f (digests %.1f) + other\n", fmax, x.t_total / 100.0,
                     x.t_tiles / 100.0, x.t_check / 100.0, x.mapped, x.tiles, x.first_mapped, x.t_event / 100.0,
@@ -1580,7 +1602,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             agg->table_ms += s.table_ms + fs.table.sort_ms;
             int64_t spec_bytes = (spec_launched && b.landed.load() && !fs.cancelled) ? fs.n : 0;
             if (spec_bytes > 0 && fs.be.na < fs.na)  // a two-phase file that stopped in its prefix: the prefix K1,
-                spec_bytes = std::min<int64_t>(fs.n, fs.be.na * fs.B) + fs.lane_b_bytes;  // + phase 1's lane chunks
+                spec_bytes = std::min<int64_t>(fs.n, fs.be.na * fs.B) + (skip_rest ? 0 : fs.lane_b_bytes);  // + phase 1's lane chunks
             agg->device_bytes += fs.be.bytes_read + spec_bytes;
             agg->phase_matches += s.phase_matches;
         }

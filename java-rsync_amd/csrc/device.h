@@ -311,7 +311,10 @@ struct ChainOut {
     int32_t aborted;              // phase 0 stopped its phase-1 K1 groups: only the prefix is speculated
     int32_t mapped, first_mapped; // tiles answered from the hit map; the walk's tile count at the first (trace)
     int64_t clear_to;             // stopped before a flush: no candidate in [s, clear_to] (else -1)
+    int32_t why, pad2;            // why the walk stopped (CHAIN_WHY_*, trace)
 };
+enum { CHAIN_WHY_NONE = 0, CHAIN_WHY_EVCAP, CHAIN_WHY_END, CHAIN_WHY_PHASE, CHAIN_WHY_TAIL, CHAIN_WHY_NOKSET,
+       CHAIN_WHY_CUT, CHAIN_WHY_FLUSH, CHAIN_WHY_BUCKET, CHAIN_WHY_FLUSHHIT, CHAIN_WHY_DEADCAP, CHAIN_WHY_CLOSED };
 // The phase-0 hit map (chain_help): while one file's walk searches tile after tile on its CU, the workgroups whose
 // own walks have ended (and the launch's extra ones) map that file's prefix ahead of it -- in the synced state the
 // key at p is the true weak sum T(p), whatever the walk does.  One 64-bit word per 32 positions: the map's

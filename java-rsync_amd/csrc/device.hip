@@ -2858,32 +2858,33 @@ __device__ __attribute__((noinline)) void chain_window_digest(const uint8_t* x, 
     __syncthreads();
 }
 
-__device__ __forceinline__ bool chain_digest_eq(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int dl) {
-    // every byte's loads issued before any compare (one round trip, not dl): indices past dl re-read the last byte
-    uint32_t diff = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int jj = j < dl ? j : dl - 1;
-        diff |= j < dl ? (uint32_t)(a[jj] ^ b[jj]) : 0u;
-    }
-    return diff == 0u;
-}
-// the same against a digest already in registers (a's bytes packed four to a word)
-__device__ __forceinline__ bool chain_digest_eq_reg(const uint32_t (&a)[4], const uint8_t* __restrict__ b, int dl) {
-    uint32_t diff = 0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const int jj = j < dl ? j : dl - 1;
-        diff |= j < dl ? (((a[j >> 2] >> (8 * (j & 3))) ^ (uint32_t)b[jj]) & 0xFFu) : 0u;
-    }
-    return diff == 0u;
-}
-// dl (<= 16) digest bytes at a, packed four to a word (all loads issued at once)
-__device__ __forceinline__ void chain_digest_load(const uint8_t* __restrict__ a, int dl, uint32_t (&w)[4]) {
+// dl (1..16) digest bytes at a, packed four to a word, zero past dl: every byte's load issued before any use (one
+// round trip, not dl), in as few loads as dl needs (4, 8 or 16; indices past dl re-read the last byte)
+template <int NB>
+__device__ __forceinline__ void chain_digest_load_n(const uint8_t* __restrict__ a, int dl, uint32_t (&w)[4]) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) w[k] = 0u;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) w[j >> 2] |= (uint32_t)a[j < dl ? j : dl - 1] << (8 * (j & 3));
+    for (int j = 0; j < NB; ++j) {
+        const uint32_t v = a[j < dl ? j : dl - 1];  // (unconditional: all NB loads go out together)
+        w[j >> 2] |= (j < dl ? v : 0u) << (8 * (j & 3));
+    }
+}
+__device__ __forceinline__ void chain_digest_load(const uint8_t* __restrict__ a, int dl, uint32_t (&w)[4]) {
+    if (dl <= 4) chain_digest_load_n<4>(a, dl, w);
+    else if (dl <= 8) chain_digest_load_n<8>(a, dl, w);
+    else chain_digest_load_n<16>(a, dl, w);
+}
+// a digest already in registers (bytes packed four to a word, zero past dl) against dl bytes at b
+__device__ __forceinline__ bool chain_digest_eq_reg(const uint32_t (&a)[4], const uint8_t* __restrict__ b, int dl) {
+    uint32_t w[4];
+    chain_digest_load(b, dl, w);
+    return ((a[0] ^ w[0]) | (a[1] ^ w[1]) | (a[2] ^ w[2]) | (a[3] ^ w[3])) == 0u;
+}
+__device__ __forceinline__ bool chain_digest_eq(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int dl) {
+    uint32_t w[4];
+    chain_digest_load(a, dl, w);
+    return chain_digest_eq_reg(w, b, dl);
 }
 
 // A wide tile lane's sums over its 32 positions' bytes x at p0 and y at p0 + B, weights relative to the tile start
@@ -3208,6 +3209,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const uint8_t* stale = nullptr;  // poisoned: the cached digest
     uint32_t dg[4] = {0u, 0u, 0u, 0u};  // the window's digest at the current event (poisoned: the stale one)
     int64_t clear_to = -1;            // stopped at a flush point: no candidate in [s, clear_to]
+    int32_t why = CHAIN_WHY_NONE;
     rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
     bool have = false;
     if (nev > 0) {  // phase 1: the last event stays open (a MATCH run may go on across the prefix's end)
@@ -3240,15 +3242,22 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     };
 
     for (;;) {
-        if (nev + 3 > F.ev_cap) break;  // room for a pending event, a literal and a match
-        if (s > last) {                 // the loop ends (Sender.java:1313-1316)
+        if (nev + 3 > F.ev_cap) {  // room for a pending event, a literal and a match
+            why = CHAIN_WHY_EVCAP;
+            break;
+        }
+        if (s > last) {  // the loop ends (Sender.java:1313-1316)
             emit_lit(m, n - m);
             status = CHAIN_DONE;
+            why = CHAIN_WHY_END;
             break;
         }
         // phase-shifted windows: the host's phase speculation.  A poisoned walk (a stale cached digest, quirk B) goes
         // on from any position: only step (2) applies to it, and every candidate is compared with the stale digest
-        if (s % B != 0 && !poisoned) break;
+        if (s % B != 0 && !poisoned) {
+            why = CHAIN_WHY_PHASE;
+            break;
+        }
         const int64_t k = s / B;
         const bool al = s % B == 0;
         // the words steps (1), (1') and (2) look at first, loaded together: one global round trip per step instead of
@@ -3322,10 +3331,16 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         // (2) the next candidate event in [s, stop]
         const int64_t f = (m + 10 * B <= n) ? m + 9 * B : INT64_MAX;
         const int64_t stop = f < last ? f : last;
-        if (stop > nB) break;  // shrinking windows near the end: the host
+        if (stop > nB) {  // shrinking windows near the end: the host
+            why = CHAIN_WHY_TAIL;
+            break;
+        }
         // (see above: an unbroken chain needed no key set; should this step look a key up after all, the host takes
         // it -- at the prefix's end the search is empty and the walk goes on to its cut, as with a key set)
-        if (!kset_built && (s / B < na || s <= (stop < na * B - 1 ? stop : na * B - 1))) break;
+        if (!kset_built && (s / B < na || s <= (stop < na * B - 1 ? stop : na * B - 1))) {
+            why = CHAIN_WHY_NOKSET;
+            break;
+        }
         int64_t p = -1;
         uint32_t key = 0;
         int64_t a = s;
@@ -3563,15 +3578,18 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             if (cut) {  // past the speculation: the rest of it (phase 1), or the host -- which also takes a
                 // poisoned walk (phase 1 starts from the unpoisoned state)
                 if (na < F.na && !poisoned) status = CHAIN_MORE;
+                why = CHAIN_WHY_CUT;
                 break;
             }
             if (f <= last) {  // a flush (quirk A): the host, which need not search [s, stop] again
                 clear_to = stop;
+                why = CHAIN_WHY_FLUSH;
                 break;
             }
             emit_lit(m, n - m);           // no candidate before the end
             status = CHAIN_DONE;
             s = n;
+            why = CHAIN_WHY_END;
             break;
         }
         // the event at p: its bucket (Multimap order), the candidates of Checksum.getCandidateChunks
@@ -3617,7 +3635,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         }
         __syncthreads();
         const int32_t size = s_nbk;
-        if (size == 0 || size > CHAIN_BUCKET_CAP) break;
+        if (size == 0 || size > CHAIN_BUCKET_CAP) {
+            why = CHAIN_WHY_BUCKET;
+            break;
+        }
         // closeIndexOf(bucket, pref) (Checksum.java:175-213): pref's position, else the first index above it,
         // else the last; not length-filtered.  Then the others in ascending order with length == window.
         int32_t l = 0, r = size - 1, init = -1;
@@ -3674,8 +3695,17 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 // file needs no more speculation
                 if (t == 0) s_any = 0;
                 __syncthreads();
-                for (int64_t c = t; c < C; c += CHAIN_THREADS)
-                    if (chain_digest_eq(F.table_strong + c * dl, stale, dl)) s_any = 1;
+                {  // the stale digest is in dg: four chunks' digests per thread in flight at a time
+                    bool any = false;
+                    for (int64_t c0 = t; c0 < C; c0 += 4 * CHAIN_THREADS) {
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int64_t c = c0 + u * CHAIN_THREADS;
+                            any |= c < C && chain_digest_eq_reg(dg, F.table_strong + (c < C ? c : 0) * dl, dl);
+                        }
+                    }
+                    if (any) s_any = 1;
+                }
                 __syncthreads();
                 dead = s_any == 0;
                 // dead: the host's closed form (resolver.cpp), here when its literals fit the event buffer -- the
@@ -3697,6 +3727,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     }
                 }
                 if (!dead) continue;  // some chunk carries it: the search goes on from p + 1
+                why = status == CHAIN_DONE ? CHAIN_WHY_CLOSED : CHAIN_WHY_DEADCAP;
+            } else {
+                why = CHAIN_WHY_FLUSHHIT;
             }
             break;
         }
@@ -3724,6 +3757,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->spec_full = phase == 1;
         out->mapped = mapped;
         out->clear_to = clear_to;
+        out->why = why;
         out->first_mapped = first_mapped;
         // a file that needs no more speculation stops its phase-1 K1 groups (they poll this word); any other stop
         // keeps them (the resolver's aligned lookups past the prefix use them)

@@ -47,6 +47,7 @@ enum Opt : int {
     OPT_MD5_WIDTH,         // rsh_file_md5_batch / rsh_match_scan_batch: 0 = widest multi-buffer MD5, 1/8/16 = forced
     OPT_CHAIN_HELPERS,     // phase-0 walk: extra workgroups mapping searching files' prefixes (-1: CUs - files; 0: no map)
     OPT_CHAIN_MAP_BYTES,   // ... the map's HBM budget (bytes; above it the walks search tile by tile)
+    OPT_BATCH_SKIP_REST,   // 1: the rest of a two-phase speculation only if some phase-0 walk reached the prefix's end
     OPT_COUNT
 };
 
@@ -65,7 +66,7 @@ inline const OptInfo* opt_info() {
         {"batch_chain", 1},        {"batch_chain_prefix", -1}, {"batch_chain_overlap", 0},
         {"host_cores", 0},         {"file_tile", 4LL << 30}, {"file_tile_above", 32LL << 30},
         {"probe_long", 1},         {"segment_bytes", 16LL << 30}, {"md5_width", 0},
-        {"chain_helpers", -1},     {"chain_map_bytes", 1LL << 30},
+        {"chain_helpers", -1},     {"chain_map_bytes", 1LL << 30}, {"batch_skip_rest", 1},
     };
     return t;
 }
