@@ -385,6 +385,15 @@ def main():
         "parity": head["parity"],
         "variants": {v: r for v, r in res_v.items() if v != a.variant},
     }
+    # the clock the chip held under K1: a diagnostic instantiation of the same body with per-wave
+    # s_memtime / s_memrealtime stamps, three launches over the resident source after the timed steps; the
+    # production kernels never stamp (MI355X_MICROARCH.md, "DVFS give-back" item 6)
+    ghz = ctypes.c_double(0.0)
+    if L.rsh_debug_k1_clock(ctx.handle, ctypes.c_void_p(src.data_ptr()), n, B, 3, ctypes.byref(ghz)) == 0:
+        res["roofline"]["k1_clock_ghz"] = round(ghz.value, 3)
+        res["roofline"]["k1_clock_source"] = ("3 launches of a stamped diagnostic instantiation of the Generator's K1 "
+                                              "body over the same resident source, after the timed steps "
+                                              "(rsh_debug_k1_clock; sum of s_memtime ticks / sum of 100 MHz ticks)")
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         b0, s0 = pairs[a.variant]
         res["cpu_baseline"] = cpu_baseline(s0, b0, B, dl, a.cpu_sample_mib << 20)

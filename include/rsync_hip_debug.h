@@ -9,12 +9,14 @@
  * scan_diag, scan_phase, scan_phase_guess, scan_segmented, scan_preprobe, scan_samples, scan_sample,
  * scan_spec_order, scan_early, scan_wait, scan_defer_steps, scan_defer_us, batch_spec, batch_spin_us,
  * batch_readahead, batch_prep_all, batch_chain, batch_chain_prefix, batch_chain_overlap, host_cores, file_tile,
- * file_tile_above, probe_long.
+ * file_tile_above, probe_long, segment_bytes, md5_width, chain_helpers, chain_map_bytes, batch_skip_rest.
  */
 #ifndef RSYNC_HIP_DEBUG_H
 #define RSYNC_HIP_DEBUG_H
 
 #include <stdint.h>
+
+#include "rsync_hip.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -25,6 +27,14 @@ int rsh_debug_set_option(const char* name, int64_t value);
 int rsh_debug_get_option(const char* name, int64_t* value);
 /* Every option back to its compiled-in default. */
 void rsh_debug_reset_options(void);
+
+/* The clock the chip holds under the Generator's K1 (MI355X_MICROARCH.md, "DVFS give-back" item 6): reps launches of
+ * a diagnostic instantiation of the production K1 body over the device bytes [d_data, d_data + n) (n a multiple of
+ * 64 * block_length, block_length a multiple of 128) with each wave's s_memtime / s_memrealtime ticks stamped around
+ * it; *clock_ghz = sum of shader ticks / sum of 100 MHz ticks x 0.1.  The production kernels never stamp.  bench.py
+ * reports it beside the headline (k1_clock_ghz). */
+int rsh_debug_k1_clock(rsh_ctx* ctx, const void* d_data, int64_t n, int32_t block_length, int32_t reps,
+                       double* clock_ghz);
 
 #ifdef __cplusplus
 }

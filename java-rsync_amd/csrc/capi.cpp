@@ -1508,6 +1508,32 @@ void rsh_debug_reset_options(void) {
     for (int i = 0; i < rsh::OPT_COUNT; ++i) rsh::opt_table()[i].store(rsh::opt_info()[i].def, std::memory_order_relaxed);
 }
 
+int rsh_debug_k1_clock(rsh_ctx* ctx, const void* d_data, int64_t n, int32_t block_length, int32_t reps,
+                       double* clock_ghz) {
+    if (!ctx || !d_data || !clock_ghz || reps <= 0 || block_length <= 0 || n <= 0 || block_length % 128 != 0 ||
+        n % (64 * (int64_t)block_length) != 0)
+        return RSH_E_INVAL;
+    RSH_HIP(hipSetDevice(ctx->device));
+    const int64_t C = n / block_length;
+    void *w = nullptr, *st = nullptr, *clk = nullptr;
+    hipError_t e = hipMalloc(&w, (size_t)C * 4);
+    if (e == hipSuccess) e = hipMalloc(&st, (size_t)C * 16);
+    if (e == hipSuccess) e = hipMalloc(&clk, 16);
+    if (e == hipSuccess) e = hipMemsetAsync(clk, 0, 16, ctx->stream);
+    for (int32_t r = 0; e == hipSuccess && r < reps; ++r)
+        e = rsh::launch_k1_clock(static_cast<const uint8_t*>(d_data), n, (uint32_t)block_length, 16, 0x04030201u,
+                                 static_cast<int32_t*>(w), static_cast<uint8_t*>(st),
+                                 static_cast<unsigned long long*>(clk), ctx->stream);
+    unsigned long long h[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpyAsync(h, clk, 16, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    for (void* p : {w, st, clk})
+        if (p) (void)hipFree(p);
+    RSH_HIP(e);
+    *clock_ghz = h[1] ? 0.1 * (double)h[0] / (double)h[1] : 0.0;  // ticks / (ticks of 10 ns) / 10 ns -> GHz
+    return RSH_OK;
+}
+
 int rsh_fill_splitmix_device(rsh_ctx* ctx, void* d_out, int64_t n, uint64_t key, int64_t byte_offset) {
     if (!ctx || (n > 0 && !d_out) || n < 0 || byte_offset < 0) return RSH_E_INVAL;
     RSH_HIP(hipSetDevice(ctx->device));

@@ -364,6 +364,10 @@ struct ChainFile {
     unsigned long long* hmap;          // its map words, positions [0, hend) (null: not mapped)
     int64_t hend;                      // min(na_a B, n - B + 1): the positions a phase-0 search may reach
 };
+// Diagnostic: the Generator's K1 over n = 64 k B bytes with per-wave clock stamps summed into d_clk[0] (shader clock
+// ticks) and d_clk[1] (100 MHz ticks); the production kernels never stamp.
+hipError_t launch_k1_clock(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t dl, uint32_t seed_word,
+                           int32_t* d_weak, uint8_t* d_strong, unsigned long long* d_clk, hipStream_t s);
 // help (phase 0): the files' ChainHelp array, or null (no map); helpers: extra workgroups beyond nfiles that only
 // map; finished walks map too.  abort_gen is also the map's generation.
 hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s, int phase = 1,

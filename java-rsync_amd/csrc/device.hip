@@ -864,6 +864,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
                                                    nullptr, n, nchunks, main_waves);
 }
 bool tail_gather_on() { return opt(OPT_K1_GATHER) != 0; }  // 0: leftover chunks one per lane (options.h)
+
+// Diagnostic (rsh_debug_k1_clock, MI355X_MICROARCH.md "DVFS give-back" item 6): the Generator's production K1 body
+// with each wave's shader-clock (s_memtime) and 100 MHz (s_memrealtime) ticks stamped around it and summed over the
+// launch; their quotient x 100 MHz is the clock the chip held under this load.  Only this instantiation stamps: the
+// production kernels never execute a stamp.  Whole coalesced waves only (n = 64 k B, B % 128 == 0).
+__global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_clock_kernel(
+    const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
+    uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen, int64_t n, uint32_t nchunks,
+    unsigned long long* __restrict__ clk) {
+    const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    block_sums_pipe_body<8, true, true, 0, false>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
+                                                   nullptr, n, nchunks, 0xFFFFFFFFu);
+    const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        atomicAdd(&clk[0], (unsigned long long)(c1 - c0));
+        atomicAdd(&clk[1], (unsigned long long)(r1 - r0));
+    }
+}
+
+hipError_t launch_k1_clock(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t dl, uint32_t seed_word,
+                           int32_t* d_weak, uint8_t* d_strong, unsigned long long* d_clk, hipStream_t s) {
+    if (B == 0 || B % 128 != 0 || n <= 0 || n % (64 * (int64_t)B) != 0 || dl > 16) return hipErrorInvalidValue;
+    const uint32_t nchunks = (uint32_t)(n / B), waves = nchunks / 64;
+    const size_t wave_lds = 64 * 9 * sizeof(uint4);
+    hipLaunchKernelGGL(block_sums_pipe_clock_kernel, dim3(waves), dim3(64), 2 * wave_lds, s, d_data, B, dl, seed_word,
+                       d_weak, d_strong, never_word(), -1, n, nchunks, d_clk);
+    return hipGetLastError();
+}
 #ifdef RSH_KBENCH
 // kbench A/B (variant 67): round 3's production form, the weak-sum MFMA operands read from LDS (WEAKW = false)
 __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_ldsw_kernel(
