@@ -1087,7 +1087,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                               S->flags.as<uint8_t>() + fs.off_nf, fs.na, fs.na_a,
                               two_phase ? S->file_abort + f : nullptr, ce + (int64_t)f * kChainEvents, kChainEvents,
                               seed_word(seed), co + f,
-                              mw > 0 ? S->chain_map.as<unsigned long long>() + map_off[(size_t)f] : nullptr, hend};
+                              mw > 0 ? S->chain_map.as<unsigned long long>() + map_off[(size_t)f] : nullptr, hend,
+                              (int32_t)opt(OPT_CHAIN_DIGEST_SCALAR)};
             if (chh) chh[f] = ChainHelp{(int32_t)((hend + CHAIN_MAP_SEG - 1) / CHAIN_MAP_SEG), 0, 1, 0, 0, 0, 0, 0, INT64_MAX, 0, 0, 0};
         }
         const uint32_t n_help = !map_on ? 0u
@@ -1293,9 +1294,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                             "%lld, phase 1 %d, walk %.1f us)\n", f, (long long)co[f].s, co[f].why, (long long)co[f].events,
                             co[f].tiles, co[f].md5c_valid, (long long)co[f].clear_to, co[f].spec_full, co[f].t_total / 100.0);
             fprintf(stderr, "[rsh-batch]   file %d: walk %.1f us = tiles %.1f (table checks %.1f; %d of %d tiles from the hit map,"
-                    " the first at tile %d) + events %.1f (digests %.1f) + other\n", fmax, x.t_total / 100.0,
+                    " the first at tile %d) + events %.1f (%d digests: %.1f) + other\n", fmax, x.t_total / 100.0,
                     x.t_tiles / 100.0, x.t_check / 100.0, x.mapped, x.tiles, x.first_mapped, x.t_event / 100.0,
-                    x.t_digest / 100.0);
+                    x.digests, x.t_digest / 100.0);
             if (S->chain_help.p && two_phase) {  // the map's helpers (device state of the last phase-0 launch)
                 std::vector<ChainHelp> hh((size_t)NF);
                 if (hipMemcpy(hh.data(), S->chain_help.p, (size_t)NF * sizeof(ChainHelp), hipMemcpyDeviceToHost) == hipSuccess) {

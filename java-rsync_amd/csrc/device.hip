@@ -2831,53 +2831,85 @@ __device__ __forceinline__ void md5_compress_scalar(Md5State& st, const uint32_t
 }
 
 // An unaligned hit's window digest (MD5 of its L bytes, the seed appended, dl bytes kept), by the whole workgroup: the
-// bytes staged through LDS in pieces of CHAIN_WIN_BUF (each thread one 16-byte aligned load of the source per granule,
-// the source's misalignment taken out by the byte stores; the last piece also gets the seed and the padding), wave 0
-// compressing each piece on the scalar unit (md5_compress_scalar, the words read from LDS and made uniform).  A lane
-// compressing on the VALU with loads two blocks ahead spent ~170 us on an 8 KiB window.  Out of line, so that the
-// walk's tile search keeps its registers.
+// bytes staged through LDS in pieces of CHAIN_WIN_BUF, then compressed by one lane on the VALU (the default) or by wave
+// 0 on the scalar unit (option chain_digest_scalar).  One message is one dependent chain either way: a lane loading
+// two blocks ahead spent 120-180 us on an 8 KiB window.  Out of line, so that the walk's tile search keeps its
+// registers.
 constexpr int CHAIN_WIN_BUF = 16384;
-__device__ __attribute__((noinline)) void chain_window_digest(const uint8_t* x, uint32_t L, uint32_t dl, uint32_t seed,
-                                                              uint8_t* buf /* CHAIN_WIN_BUF + 128 */, uint8_t* dig) {
+// Stage piece [c0, c0 + len) of the window at x into buf (16-byte aligned source loads, byte stores that take the
+// misalignment out; every granule overlaps the piece, so it lies in a page the source occupies) and, for the last
+// piece, the seed, 0x80, zeros and the message's bit length (L + 4 bytes) to a whole block.  Returns the padded length.
+__device__ __forceinline__ uint32_t chain_window_stage(const uint8_t* x, uint32_t L, uint32_t seed, uint8_t* buf,
+                                                       uint32_t c0) {
+    const int t = threadIdx.x;
+    const uint32_t len = L - c0 < (uint32_t)CHAIN_WIN_BUF ? L - c0 : (uint32_t)CHAIN_WIN_BUF;
+    const bool last = c0 + len == L;
+    const uintptr_t xa = reinterpret_cast<uintptr_t>(x) + c0, a0 = xa & ~(uintptr_t)15;
+    const int32_t shift = (int32_t)(xa - a0);
+    for (int32_t g = 16 * t; g < shift + (int32_t)len; g += 16 * CHAIN_THREADS) {
+        const uint4 q = *reinterpret_cast<const uint4*>(a0 + (uintptr_t)g);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int32_t o = g + k - shift;
+            if (o >= 0 && o < (int32_t)len) buf[o] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+    const uint32_t plen = last ? ((len + 4 + 1 + 8 + 63) & ~63u) : len;
+    if (last && (uint32_t)t < plen - len) {
+        const uint32_t i = len + (uint32_t)t;
+        const uint64_t bits = ((uint64_t)L + 4) * 8;
+        uint32_t v = 0;
+        if (t < 4) v = (seed >> (8 * t)) & 0xFFu;
+        else if (t == 4) v = 0x80u;
+        else if (i >= plen - 8) v = (uint32_t)(bits >> (8 * (i - (plen - 8)))) & 0xFFu;
+        buf[i] = (uint8_t)v;
+    }
+    __syncthreads();
+    return plen;
+}
+// ... wave 0 compressing each staged piece on the scalar unit (md5_compress_scalar: the words read from LDS and
+// made uniform, the state in SGPRs)
+__device__ __attribute__((noinline)) void chain_window_digest_scalar(const uint8_t* x, uint32_t L, uint32_t dl,
+                                                                     uint32_t seed, uint8_t* buf, uint8_t* dig) {
     const int t = threadIdx.x;
     // (a callee's arguments arrive in VGPRs: made uniform, so that the loops and the state stay scalar)
     L = __builtin_amdgcn_readfirstlane(L);
     seed = __builtin_amdgcn_readfirstlane(seed);
     Md5State st = md5_init();
     for (uint32_t c0 = 0; c0 < L; c0 += CHAIN_WIN_BUF) {
-        const uint32_t len = L - c0 < (uint32_t)CHAIN_WIN_BUF ? L - c0 : (uint32_t)CHAIN_WIN_BUF;
-        const bool last = c0 + len == L;
-        const uintptr_t xa = reinterpret_cast<uintptr_t>(x) + c0, a0 = xa & ~(uintptr_t)15;
-        const int32_t shift = (int32_t)(xa - a0);
-        // every granule overlaps [xa, xa + len), so it lies in a page the source occupies
-        for (int32_t g = 16 * t; g < shift + (int32_t)len; g += 16 * CHAIN_THREADS) {
-            const uint4 q = *reinterpret_cast<const uint4*>(a0 + (uintptr_t)g);
-            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int32_t o = g + k - shift;
-                if (o >= 0 && o < (int32_t)len) buf[o] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-            }
-        }
-        // the last piece: the seed, 0x80, zeros, the message's bit length (L + 4 bytes), to a whole block
-        const uint32_t plen = last ? ((len + 4 + 1 + 8 + 63) & ~63u) : len;
-        if (last && (uint32_t)t < plen - len) {
-            const uint32_t i = len + (uint32_t)t;
-            const uint64_t bits = ((uint64_t)L + 4) * 8;
-            uint32_t v = 0;
-            if (t < 4) v = (seed >> (8 * t)) & 0xFFu;
-            else if (t == 4) v = 0x80u;
-            else if (i >= plen - 8) v = (uint32_t)(bits >> (8 * (i - (plen - 8)))) & 0xFFu;
-            buf[i] = (uint8_t)v;
-        }
-        __syncthreads();
-        if (__builtin_amdgcn_readfirstlane(t >> 6) == 0) {  // wave 0 (a wave-uniform test: the state stays in SGPRs)
+        const uint32_t plen = __builtin_amdgcn_readfirstlane(chain_window_stage(x, L, seed, buf, c0));
+        if (__builtin_amdgcn_readfirstlane(t >> 6) == 0) {  // wave 0 (a wave-uniform test)
             const uint32_t* bw = reinterpret_cast<const uint32_t*>(buf);
             for (uint32_t b = 0; b < plen / 64; ++b) {
                 uint32_t m[16];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_readfirstlane(bw[16 * b + i]);
                 md5_compress_scalar(st, m);
+            }
+        }
+        __syncthreads();
+    }
+    if (t == 0) store_digest(dig, st, dl);
+    __syncthreads();
+}
+// ... or lane 0 compressing them on the VALU (md5_compress: v_bitop3 round functions), the words from LDS
+__device__ __attribute__((noinline)) void chain_window_digest(const uint8_t* x, uint32_t L, uint32_t dl, uint32_t seed,
+                                                              uint8_t* buf, uint8_t* dig) {
+    const int t = threadIdx.x;
+    Md5State st = md5_init();
+    for (uint32_t c0 = 0; c0 < L; c0 += CHAIN_WIN_BUF) {
+        const uint32_t plen = chain_window_stage(x, L, seed, buf, c0);
+        if (t == 0) {
+            const uint4* bq = reinterpret_cast<const uint4*>(buf);
+            for (uint32_t b = 0; b < plen / 64; ++b) {
+                uint32_t m[16];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint4 v = bq[4 * b + i];
+                    m[4 * i] = v.x, m[4 * i + 1] = v.y, m[4 * i + 2] = v.z, m[4 * i + 3] = v.w;
+                }
+                md5_compress(st, m);
             }
         }
         __syncthreads();
@@ -3686,7 +3718,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const uint8_t* md5c = poisoned ? stale : F.as + kp * dl;
         if (!spec_digest && !poisoned) {
             const int64_t td0 = (int64_t)wall_clock64();
-            chain_window_digest(F.data + p, (uint32_t)B, (uint32_t)dl, F.seed, s_win, s_dig);  // (ends with a barrier)
+            if (F.digest_scalar)  // (both end with a barrier)
+                chain_window_digest_scalar(F.data + p, (uint32_t)B, (uint32_t)dl, F.seed, s_win, s_dig);
+            else
+                chain_window_digest(F.data + p, (uint32_t)B, (uint32_t)dl, F.seed, s_win, s_dig);
             md5c = s_dig;
             chain_digest_load(s_dig, dl, dg);
             ++digests;
