@@ -2630,6 +2630,7 @@ hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const Part
 // branch on is read from global memory or LDS by all of them); lane 0 writes the events.
 // ------------------------------------------------------------------------------------------------
 // CHAIN_THREADS, CHAIN_PPT, CHAIN_TILE, CHAIN_SEGS: device.h (the host sizes the hit map with them)
+constexpr int CHAIN_EV_LDS = 64;  // events a walk holds in LDS before writing them out
 
 // A key's presence in a chunk index (launch_chunk_index: (key << 32) | (i + 1) per chunk, 0 = empty): every chunk
 // with the key lies on the key's probe path before its first empty slot
@@ -2745,96 +2746,10 @@ __device__ __forceinline__ int chain_first_hit16(const unsigned long long* __res
     return hit ? __builtin_ctz(hit) : -1;
 }
 
-// One MD5 compression on the scalar unit: every value wave-uniform (SGPRs), the round functions and adds as SALU
-// instructions, the rotates as SALU shift pairs (the backend would otherwise form v_alignbit and move the chain to the
-// VALU).  A single message is one dependent chain: on the VALU each dependent instruction waits out the wave64
-// pipeline (~8 cycles), on the SALU ~1-2.
-__device__ __forceinline__ uint32_t md5s_rotl(uint32_t x, uint32_t s, uint32_t r) {  // s + r = 32, both immediate
-    uint32_t y, z;
-    asm("s_lshl_b32 %0, %2, %3\n\ts_lshr_b32 %1, %2, %4\n\ts_or_b32 %0, %0, %1"
-        : "=&s"(y), "=&s"(z)
-        : "s"(x), "n"(s), "n"(r)
-        : "scc");
-    return y;
-}
-#define RSH_MD5S_STEP(f, a, b, c, d, m, k, s) (a) = (b) + md5s_rotl((a) + f((b), (c), (d)) + (m) + (k), (s), 32 - (s))
-__device__ __forceinline__ void md5_compress_scalar(Md5State& st, const uint32_t (&m)[16]) {
-    uint32_t a = st.a, b = st.b, c = st.c, d = st.d;
-    RSH_MD5S_STEP(RSH_MD5_F, a, b, c, d, m[0], 0xd76aa478u, 7);
-    RSH_MD5S_STEP(RSH_MD5_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
-    RSH_MD5S_STEP(RSH_MD5_F, c, d, a, b, m[2], 0x242070dbu, 17);
-    RSH_MD5S_STEP(RSH_MD5_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
-    RSH_MD5S_STEP(RSH_MD5_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
-    RSH_MD5S_STEP(RSH_MD5_F, d, a, b, c, m[5], 0x4787c62au, 12);
-    RSH_MD5S_STEP(RSH_MD5_F, c, d, a, b, m[6], 0xa8304613u, 17);
-    RSH_MD5S_STEP(RSH_MD5_F, b, c, d, a, m[7], 0xfd469501u, 22);
-    RSH_MD5S_STEP(RSH_MD5_F, a, b, c, d, m[8], 0x698098d8u, 7);
-    RSH_MD5S_STEP(RSH_MD5_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
-    RSH_MD5S_STEP(RSH_MD5_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
-    RSH_MD5S_STEP(RSH_MD5_F, b, c, d, a, m[11], 0x895cd7beu, 22);
-    RSH_MD5S_STEP(RSH_MD5_F, a, b, c, d, m[12], 0x6b901122u, 7);
-    RSH_MD5S_STEP(RSH_MD5_F, d, a, b, c, m[13], 0xfd987193u, 12);
-    RSH_MD5S_STEP(RSH_MD5_F, c, d, a, b, m[14], 0xa679438eu, 17);
-    RSH_MD5S_STEP(RSH_MD5_F, b, c, d, a, m[15], 0x49b40821u, 22);
-    RSH_MD5S_STEP(RSH_MD5_G, a, b, c, d, m[1], 0xf61e2562u, 5);
-    RSH_MD5S_STEP(RSH_MD5_G, d, a, b, c, m[6], 0xc040b340u, 9);
-    RSH_MD5S_STEP(RSH_MD5_G, c, d, a, b, m[11], 0x265e5a51u, 14);
-    RSH_MD5S_STEP(RSH_MD5_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
-    RSH_MD5S_STEP(RSH_MD5_G, a, b, c, d, m[5], 0xd62f105du, 5);
-    RSH_MD5S_STEP(RSH_MD5_G, d, a, b, c, m[10], 0x02441453u, 9);
-    RSH_MD5S_STEP(RSH_MD5_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
-    RSH_MD5S_STEP(RSH_MD5_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
-    RSH_MD5S_STEP(RSH_MD5_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
-    RSH_MD5S_STEP(RSH_MD5_G, d, a, b, c, m[14], 0xc33707d6u, 9);
-    RSH_MD5S_STEP(RSH_MD5_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
-    RSH_MD5S_STEP(RSH_MD5_G, b, c, d, a, m[8], 0x455a14edu, 20);
-    RSH_MD5S_STEP(RSH_MD5_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
-    RSH_MD5S_STEP(RSH_MD5_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
-    RSH_MD5S_STEP(RSH_MD5_G, c, d, a, b, m[7], 0x676f02d9u, 14);
-    RSH_MD5S_STEP(RSH_MD5_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
-    RSH_MD5S_STEP(RSH_MD5_H, a, b, c, d, m[5], 0xfffa3942u, 4);
-    RSH_MD5S_STEP(RSH_MD5_H, d, a, b, c, m[8], 0x8771f681u, 11);
-    RSH_MD5S_STEP(RSH_MD5_H, c, d, a, b, m[11], 0x6d9d6122u, 16);
-    RSH_MD5S_STEP(RSH_MD5_H, b, c, d, a, m[14], 0xfde5380cu, 23);
-    RSH_MD5S_STEP(RSH_MD5_H, a, b, c, d, m[1], 0xa4beea44u, 4);
-    RSH_MD5S_STEP(RSH_MD5_H, d, a, b, c, m[4], 0x4bdecfa9u, 11);
-    RSH_MD5S_STEP(RSH_MD5_H, c, d, a, b, m[7], 0xf6bb4b60u, 16);
-    RSH_MD5S_STEP(RSH_MD5_H, b, c, d, a, m[10], 0xbebfbc70u, 23);
-    RSH_MD5S_STEP(RSH_MD5_H, a, b, c, d, m[13], 0x289b7ec6u, 4);
-    RSH_MD5S_STEP(RSH_MD5_H, d, a, b, c, m[0], 0xeaa127fau, 11);
-    RSH_MD5S_STEP(RSH_MD5_H, c, d, a, b, m[3], 0xd4ef3085u, 16);
-    RSH_MD5S_STEP(RSH_MD5_H, b, c, d, a, m[6], 0x04881d05u, 23);
-    RSH_MD5S_STEP(RSH_MD5_H, a, b, c, d, m[9], 0xd9d4d039u, 4);
-    RSH_MD5S_STEP(RSH_MD5_H, d, a, b, c, m[12], 0xe6db99e5u, 11);
-    RSH_MD5S_STEP(RSH_MD5_H, c, d, a, b, m[15], 0x1fa27cf8u, 16);
-    RSH_MD5S_STEP(RSH_MD5_H, b, c, d, a, m[2], 0xc4ac5665u, 23);
-    RSH_MD5S_STEP(RSH_MD5_I, a, b, c, d, m[0], 0xf4292244u, 6);
-    RSH_MD5S_STEP(RSH_MD5_I, d, a, b, c, m[7], 0x432aff97u, 10);
-    RSH_MD5S_STEP(RSH_MD5_I, c, d, a, b, m[14], 0xab9423a7u, 15);
-    RSH_MD5S_STEP(RSH_MD5_I, b, c, d, a, m[5], 0xfc93a039u, 21);
-    RSH_MD5S_STEP(RSH_MD5_I, a, b, c, d, m[12], 0x655b59c3u, 6);
-    RSH_MD5S_STEP(RSH_MD5_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
-    RSH_MD5S_STEP(RSH_MD5_I, c, d, a, b, m[10], 0xffeff47du, 15);
-    RSH_MD5S_STEP(RSH_MD5_I, b, c, d, a, m[1], 0x85845dd1u, 21);
-    RSH_MD5S_STEP(RSH_MD5_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
-    RSH_MD5S_STEP(RSH_MD5_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
-    RSH_MD5S_STEP(RSH_MD5_I, c, d, a, b, m[6], 0xa3014314u, 15);
-    RSH_MD5S_STEP(RSH_MD5_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
-    RSH_MD5S_STEP(RSH_MD5_I, a, b, c, d, m[4], 0xf7537e82u, 6);
-    RSH_MD5S_STEP(RSH_MD5_I, d, a, b, c, m[11], 0xbd3af235u, 10);
-    RSH_MD5S_STEP(RSH_MD5_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
-    RSH_MD5S_STEP(RSH_MD5_I, b, c, d, a, m[9], 0xeb86d391u, 21);
-    st.a += a;
-    st.b += b;
-    st.c += c;
-    st.d += d;
-}
-
 // An unaligned hit's window digest (MD5 of its L bytes, the seed appended, dl bytes kept), by the whole workgroup: the
-// bytes staged through LDS in pieces of CHAIN_WIN_BUF, then compressed by one lane on the VALU (the default) or by wave
-// 0 on the scalar unit (option chain_digest_scalar).  One message is one dependent chain either way: a lane loading
-// two blocks ahead spent 120-180 us on an 8 KiB window.  Out of line, so that the walk's tile search keeps its
-// registers.
+// bytes staged through LDS in pieces of CHAIN_WIN_BUF, then compressed by one lane on the VALU.  One message is one
+// dependent chain (~160 us for an 8 KiB window; a scalar-unit form measured slower: DESIGN.md section 5a).  Out of
+// line, so that the walk's tile search keeps its registers.
 constexpr int CHAIN_WIN_BUF = 16384;
 // Stage piece [c0, c0 + len) of the window at x into buf (16-byte aligned source loads, byte stores that take the
 // misalignment out; every granule overlaps the piece, so it lies in a page the source occupies) and, for the last
@@ -2868,32 +2783,7 @@ __device__ __forceinline__ uint32_t chain_window_stage(const uint8_t* x, uint32_
     __syncthreads();
     return plen;
 }
-// ... wave 0 compressing each staged piece on the scalar unit (md5_compress_scalar: the words read from LDS and
-// made uniform, the state in SGPRs)
-__device__ __attribute__((noinline)) void chain_window_digest_scalar(const uint8_t* x, uint32_t L, uint32_t dl,
-                                                                     uint32_t seed, uint8_t* buf, uint8_t* dig) {
-    const int t = threadIdx.x;
-    // (a callee's arguments arrive in VGPRs: made uniform, so that the loops and the state stay scalar)
-    L = __builtin_amdgcn_readfirstlane(L);
-    seed = __builtin_amdgcn_readfirstlane(seed);
-    Md5State st = md5_init();
-    for (uint32_t c0 = 0; c0 < L; c0 += CHAIN_WIN_BUF) {
-        const uint32_t plen = __builtin_amdgcn_readfirstlane(chain_window_stage(x, L, seed, buf, c0));
-        if (__builtin_amdgcn_readfirstlane(t >> 6) == 0) {  // wave 0 (a wave-uniform test)
-            const uint32_t* bw = reinterpret_cast<const uint32_t*>(buf);
-            for (uint32_t b = 0; b < plen / 64; ++b) {
-                uint32_t m[16];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_readfirstlane(bw[16 * b + i]);
-                md5_compress_scalar(st, m);
-            }
-        }
-        __syncthreads();
-    }
-    if (t == 0) store_digest(dig, st, dl);
-    __syncthreads();
-}
-// ... or lane 0 compressing them on the VALU (md5_compress: v_bitop3 round functions), the words from LDS
+// ... lane 0 compressing them on the VALU (md5_compress: v_bitop3 round functions), the words from LDS
 __device__ __attribute__((noinline)) void chain_window_digest(const uint8_t* x, uint32_t L, uint32_t dl, uint32_t seed,
                                                               uint8_t* buf, uint8_t* dig) {
     const int t = threadIdx.x;
@@ -3199,6 +3089,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ uint2 s_ck[2 * CHAIN_CK_BUCKETS];  // the table's keys (ChainKeySet)
     __shared__ int32_t s_ck_full;
     __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
+    __shared__ rsh_event s_ev[CHAIN_EV_LDS];   // finished events not yet in F.ev
     __shared__ unsigned long long s_best;      // helpers: the file to map next
     __shared__ int32_t s_word, s_live;
     const ChainKeySet kset{s_ck, &s_ck_full};
@@ -3277,9 +3168,21 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         have = true;
         --nev;
     }
-    auto flush_pend = [&]() {
-        if (have && t == 0) F.ev[nev] = pend;
-        if (have) ++nev;
+    // Finished events collect in LDS and go to the event buffer (pinned host memory) CHAIN_EV_LDS at a time, one per
+    // thread: a store to host memory is a PCIe write whose completion the next vmcnt wait of its wave waits for (on
+    // gfx9 the counter covers stores too), so lane 0 writing each event itself held the walk ~1-2 us per event.
+    int32_t nev_w = nev;  // events already in F.ev
+    auto drain_ev = [&]() {  // (all threads)
+        __syncthreads();
+        for (int32_t i = t; i < nev - nev_w; i += CHAIN_THREADS) F.ev[nev_w + i] = s_ev[i];
+        nev_w = nev;
+        __syncthreads();
+    };
+    auto flush_pend = [&]() {  // (the loop drains at its top while fewer than CHAIN_EV_LDS - 8 are held)
+        if (have) {
+            if (t == 0) s_ev[nev - nev_w] = pend;
+            ++nev;
+        }
         have = false;
     };
     auto emit_lit = [&](int64_t off, int64_t len) {  // Sender.sendDataFrom; zero-length calls write nothing
@@ -3302,6 +3205,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     };
 
     for (;;) {
+        if (nev - nev_w >= CHAIN_EV_LDS - 8) drain_ev();  // (a step adds at most three)
         if (nev + 3 > F.ev_cap) {  // room for a pending event, a literal and a match
             why = CHAIN_WHY_EVCAP;
             break;
@@ -3718,10 +3622,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const uint8_t* md5c = poisoned ? stale : F.as + kp * dl;
         if (!spec_digest && !poisoned) {
             const int64_t td0 = (int64_t)wall_clock64();
-            if (F.digest_scalar)  // (both end with a barrier)
-                chain_window_digest_scalar(F.data + p, (uint32_t)B, (uint32_t)dl, F.seed, s_win, s_dig);
-            else
-                chain_window_digest(F.data + p, (uint32_t)B, (uint32_t)dl, F.seed, s_win, s_dig);
+            chain_window_digest(F.data + p, (uint32_t)B, (uint32_t)dl, F.seed, s_win, s_dig);  // (ends with a barrier)
             md5c = s_dig;
             chain_digest_load(s_dig, dl, dg);
             ++digests;
@@ -3758,14 +3659,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 // file needs no more speculation
                 if (t == 0) s_any = 0;
                 __syncthreads();
-                {  // the stale digest is in dg: four chunks' digests per thread in flight at a time
+                {  // the stale digest is in dg; two chunks' digests per thread in flight at a time
                     bool any = false;
-                    for (int64_t c0 = t; c0 < C; c0 += 4 * CHAIN_THREADS) {
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int64_t c = c0 + u * CHAIN_THREADS;
-                            any |= c < C && chain_digest_eq_reg(dg, F.table_strong + (c < C ? c : 0) * dl, dl);
-                        }
+                    for (int64_t c = t; c < C; c += 2 * CHAIN_THREADS) {
+                        const int64_t c2 = c + CHAIN_THREADS < C ? c + CHAIN_THREADS : c;
+                        any |= chain_digest_eq_reg(dg, F.table_strong + c * dl, dl) |
+                               chain_digest_eq_reg(dg, F.table_strong + c2 * dl, dl);
                     }
                     if (any) s_any = 1;
                 }
@@ -3777,9 +3676,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     const int64_t nfl = s <= last ? (n - m) / (10 * B) : 0;  // (the loop has ended: no flushes)
                     if (nev + nfl + 3 <= F.ev_cap) {
                         flush_pend();  // the literals themselves: one per thread (writes to pinned host memory)
+                        drain_ev();
                         for (int64_t i = t; i < nfl; i += CHAIN_THREADS)
                             F.ev[nev + i] = rsh_event{m + 10 * B * i, 10 * B, RSH_EV_LITERAL, 0, 0, 0};
                         nev += (int32_t)nfl;
+                        nev_w = nev;
                         lit += 10 * B * nfl;
                         m += 10 * B * nfl;
                         flushes += nfl;
@@ -3803,6 +3704,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         poisoned = 0;  // a match clears the cached digest (Sender.java:1287)
     }
     flush_pend();
+    drain_ev();
     if (t == 0) {
         out->s = s;
         out->m = m;
