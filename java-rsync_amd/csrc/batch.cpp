@@ -18,6 +18,8 @@
 #include <mutex>
 #include <thread>
 
+#include <immintrin.h>
+
 #include "ctx.h"
 #include "options.h"
 #include "host_md5.h"
@@ -97,6 +99,7 @@ struct BatchState {
     DevBuf chain_help, chain_map;
     PinnedBuf h_chain_help;
     hipEvent_t ev_fk = nullptr;
+    hipEvent_t ev_sync = nullptr;  // spin_sync: the latency-path waits poll an event instead of blocking
     hipEvent_t ev_ch0 = nullptr, ev_ch1 = nullptr;  // around the walk (trace)
     hipEvent_t ev_fa = nullptr, ev_wa = nullptr;    // two-phase walk: prefix flags done, phase-0 walk done
     hipError_t ensure_file_abort(int64_t nf) {
@@ -121,7 +124,7 @@ struct BatchState {
             if (scopy_pending) (void)hipEventSynchronize(ev_scopy);
             (void)hipEventDestroy(ev_scopy);
         }
-        for (hipEvent_t e : {ev_fk, ev_ch0, ev_ch1, ev_fa, ev_wa})
+        for (hipEvent_t e : {ev_fk, ev_ch0, ev_ch1, ev_fa, ev_wa, ev_sync})
             if (e) (void)hipEventDestroy(e);
         kslots.release();
         for (PinnedBuf* b : {&h_kents, &h_chain, &h_chain_out, &h_chain_ev, &h_chain_help}) b->release();
@@ -459,6 +462,25 @@ int64_t BatchBackend::first_hit(const ProbeInterval* iv, int64_t count, const st
 
 // One round: answer every pending request of the batch.  Returns a HIP error (then every request is
 // answered with "nothing": the resolvers run to completion on garbage and the batch reports the error).
+// Wait for an event by polling it: the resolver rounds sit on this latency path, and a blocking wait can sleep past
+// the completion (the runtime's yield) -- each round's hand-off back to the host is ~10-50 us of the step otherwise.
+hipError_t spin_event(hipEvent_t ev) {
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        _mm_pause();
+    }
+}
+// ... and for everything enqueued on st so far
+hipError_t spin_sync(BatchState* S, hipStream_t st) {
+    if (!S->ev_sync) {
+        const hipError_t e = hipEventCreateWithFlags(&S->ev_sync, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    const hipError_t e = hipEventRecord(S->ev_sync, st);
+    return e != hipSuccess ? e : spin_event(S->ev_sync);
+}
+
 hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, const std::vector<int32_t>& pend) {
     hipStream_t st = c->stream;
     std::vector<GatherEnt> gw, gb;
@@ -653,7 +675,7 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
         chk(hipMemcpyAsync(S->h_bucket.p, S->bucket.p, files.size() * HIT_BUCKET_INTS * sizeof(int32_t),
                            hipMemcpyDeviceToHost, st));
     }
-    chk(hipStreamSynchronize(st));
+    chk(spin_sync(S, st));
 
     // answers
     const ProbeOut* hf = S->h_first.as<ProbeOut>();
@@ -1155,7 +1177,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             // 30720 -- its flags and phase 1 are skipped.  The host waits for phase 0 either way (a few us more before
             // the rest's launch when it is needed).
             if (opt(OPT_BATCH_SKIP_REST) != 0 && opt(OPT_BATCH_CHAIN_OVERLAP) == 0) {
-                RSH_BHIP(hipEventSynchronize(S->ev_wa));
+                RSH_BHIP(spin_event(S->ev_wa));
                 skip_rest = true;
                 for (int32_t f = 0; f < NF && skip_rest; ++f) skip_rest = co[f].status != CHAIN_MORE;
             }
@@ -1189,7 +1211,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     }
     const double enq_ms = ms_since(t0);
     RSH_BHIP(hipEventSynchronize(c->ev_tab));
-    RSH_BHIP(hipStreamSynchronize(st));
+    RSH_BHIP(spin_sync(S, st));
     const double setup_ms = ms_since(t0);
 
     const bool trace = opt(OPT_SCAN_TRACE) != 0;
@@ -1261,7 +1283,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             }
             RSH_BHIP(hipStreamWaitEvent(st, c->ev_spec, 0));
             RSH_BHIP(launch_copy_many(lc, nl, mx, st));
-            RSH_BHIP(hipStreamSynchronize(st));
+            RSH_BHIP(spin_sync(S, st));
             b.aligned.store(true);
             for (FileScan& fs : files) fs.be.head = false;
         }
