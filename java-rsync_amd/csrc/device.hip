@@ -3159,6 +3159,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     int64_t t_tiles = 0, t_check = 0, t_event = 0, t_digest = 0;
     const uint8_t* stale = nullptr;  // poisoned: the cached digest
     uint32_t dg[4] = {0u, 0u, 0u, 0u};  // the window's digest at the current event (poisoned: the stale one)
+    int64_t pf_k = -1;                  // the next step's words, loaded by an aligned event (pf_k: their window)
+    uint8_t pf_flag = 0;
+    int32_t pf_aw = 0, pf_tw = 0;
     int64_t clear_to = -1;            // stopped at a flush point: no candidate in [s, clear_to]
     int32_t why = CHAIN_WHY_NONE;
     rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
@@ -3226,9 +3229,18 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const bool al = s % B == 0;
         // the words steps (1), (1') and (2) look at first, loaded together: one global round trip per step instead of
         // three in sequence (a desynced walk takes these steps once per event)
-        const uint8_t flag_k = (!poisoned && k == pref && k < nflags) ? F.flags[k] : (uint8_t)0;
-        const int32_t aw_k = (al && k < na) ? F.aw[k] : 0;
-        const int32_t tw_pref = (!poisoned && pref < C && k < na) ? F.table_weak[pref] : 0;
+        uint8_t flag_k;
+        int32_t aw_k, tw_pref;
+        if (pf_k == k && pref == k && al && !poisoned) {  // prefetched by the event that led here (its own chunk)
+            flag_k = pf_flag;
+            aw_k = pf_aw;
+            tw_pref = pf_tw;
+        } else {
+            flag_k = (!poisoned && k == pref && k < nflags) ? F.flags[k] : (uint8_t)0;
+            aw_k = (al && k < na) ? F.aw[k] : 0;
+            tw_pref = (!poisoned && pref < C && k < na) ? F.table_weak[pref] : 0;
+        }
+        pf_k = -1;
         // (1) aligned chain: preferred index == k and source window k carries chunk k's sums
         if (flag_k) {
             if (t == 0) s_zero = nflags;
@@ -3336,6 +3348,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     const bool need = lo <= 31 && hi >= lo;
                     unsigned long long wv = 0ull;
                     if (need) wv = __hip_atomic_load(&F.hmap[pm >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // beside it, the speculation's sum of an aligned window in the lane's range: a hit there needs
+                    // no second round trip for its key
+                    const bool al_lane = need && pm % B == 0;  // (pm <= qlast < na B)
+                    const int32_t awl = al_lane ? F.aw[pm / B] : 0;
                     if (t == 0) s_hit = 0x7FFFFFFF;
                     if (__syncthreads_and(!need || (uint32_t)(wv >> 32) == map_gen)) {
                         if (need) {
@@ -3345,11 +3361,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                         }
                         __syncthreads();
                         const int32_t hoff = s_hit;
+                        if (hoff != 0x7FFFFFFF && al_lane && pm == q0 + hoff) s_key = (uint32_t)awl;
                         __syncthreads();
                         if (hoff != 0x7FFFFFFF) {  // the key: the window's true weak sum (synced)
                             p = q0 + hoff;
-                            if (p % B == 0) {      // an aligned window: the speculation's sum (p / B < na here)
-                                key = (uint32_t)F.aw[p / B];
+                            if (p % B == 0) {      // an aligned window: the speculation's sum, loaded above
+                                key = s_key;
                             } else {               // else one reduction over its B bytes
                                 int32_t w2[2] = {0, 0};
                                 range_sums(F.data, n, p, p + B, p, w2[0], w2[1]);
@@ -3567,7 +3584,15 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         uint32_t dgk[4] = {0u, 0u, 0u, 0u};
         const bool diag = spec_digest && kp < C;
         if (spec_digest) chain_digest_load(F.as + kp * dl, dl, dg);
-        if (diag) chain_digest_load(F.table_strong + kp * dl, dl, dgk);
+        if (diag) {
+            chain_digest_load(F.table_strong + kp * dl, dl, dgk);
+            // and, should it match, the words the next step (at kp + 1, preferring chunk kp + 1) looks at first
+            const int64_t kn = kp + 1;
+            pf_k = kn;
+            pf_flag = kn < nflags ? F.flags[kn] : (uint8_t)0;
+            pf_aw = kn < na ? F.aw[kn] : 0;
+            pf_tw = (kn < C && kn < na) ? F.table_weak[kn] : 0;
+        }
         if (t < 64) {
             // every chunk with this key lies on the probe path before the first empty slot: wave 0 reads 64 slots of
             // it per round trip (one, nearly always) instead of one dependent load per slot
