@@ -3160,6 +3160,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     const uint8_t* stale = nullptr;  // poisoned: the cached digest
     uint32_t dg[4] = {0u, 0u, 0u, 0u};  // the window's digest at the current event (poisoned: the stale one)
     int64_t pf_k = -1;                  // the next step's words, loaded by an aligned event (pf_k: their window)
+    int64_t pf_q0 = -1;                 // ... and the map words of a tile starting there (lane t's in pf_wv)
+    unsigned long long pf_wv = 0ull;
     uint8_t pf_flag = 0;
     int32_t pf_aw = 0, pf_tw = 0;
     int64_t clear_to = -1;            // stopped at a flush point: no candidate in [s, clear_to]
@@ -3347,7 +3349,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     const int64_t lo = a > pm ? a - pm : 0, hi = qlast - pm;
                     const bool need = lo <= 31 && hi >= lo;
                     unsigned long long wv = 0ull;
-                    if (need) wv = __hip_atomic_load(&F.hmap[pm >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (need) {  // (the event before may have loaded this tile's words already)
+                        wv = (q0 == pf_q0 && (uint32_t)(pf_wv >> 32) == map_gen)
+                                 ? pf_wv
+                                 : __hip_atomic_load(&F.hmap[pm >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    pf_q0 = -1;
                     // beside it, the speculation's sum of an aligned window in the lane's range: a hit there needs
                     // no second round trip for its key
                     const bool al_lane = need && pm % B == 0;  // (pm <= qlast < na B)
@@ -3586,6 +3593,13 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         if (spec_digest) chain_digest_load(F.as + kp * dl, dl, dg);
         if (diag) {
             chain_digest_load(F.table_strong + kp * dl, dl, dgk);
+            // the next search's map words too, should it start a block on (after a match here)
+            if (map_gen != 0u && p + B < F.hend) {
+                pf_q0 = p + B;
+                const int64_t pmn = pf_q0 + (int64_t)t * CHAIN_PPT;
+                pf_wv = pmn < F.hend ? __hip_atomic_load(&F.hmap[pmn >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0ull;
+            }
             // and, should it match, the words the next step (at kp + 1, preferring chunk kp + 1) looks at first
             const int64_t kn = kp + 1;
             pf_k = kn;
