@@ -3591,8 +3591,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         uint32_t dgk[4] = {0u, 0u, 0u, 0u};
         const bool diag = spec_digest && kp < C;
         if (spec_digest) chain_digest_load(F.as + kp * dl, dl, dg);
-        if (diag) {
-            chain_digest_load(F.table_strong + kp * dl, dl, dgk);
+        if (diag) chain_digest_load(F.table_strong + kp * dl, dl, dgk);
+        if (diag && F.prefetch) {
             // the next search's map words too, should it start a block on (after a match here)
             if (map_gen != 0u && p + B < F.hend) {
                 pf_q0 = p + B;
@@ -3603,9 +3603,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             // and, should it match, the words the next step (at kp + 1, preferring chunk kp + 1) looks at first
             const int64_t kn = kp + 1;
             pf_k = kn;
-            pf_flag = kn < nflags ? F.flags[kn] : (uint8_t)0;
-            pf_aw = kn < na ? F.aw[kn] : 0;
-            pf_tw = (kn < C && kn < na) ? F.table_weak[kn] : 0;
+            // (vector loads: a scalar load here would hold the event's LDS reads, which wait on the same counter)
+            pf_flag = kn < nflags ? __builtin_nontemporal_load(&F.flags[kn]) : (uint8_t)0;
+            pf_aw = kn < na ? __builtin_nontemporal_load(&F.aw[kn]) : 0;
+            pf_tw = (kn < C && kn < na) ? __builtin_nontemporal_load(&F.table_weak[kn]) : 0;
         }
         if (t < 64) {
             // every chunk with this key lies on the probe path before the first empty slot: wave 0 reads 64 slots of
