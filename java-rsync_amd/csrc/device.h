@@ -363,7 +363,6 @@ struct ChainFile {
     ChainOut* out;
     unsigned long long* hmap;          // its map words, positions [0, hend) (null: not mapped)
     int64_t hend;                      // min(na_a B, n - B + 1): the positions a phase-0 search may reach
-    int32_t prefetch;                  // an aligned event prefetches the next step's words (option chain_prefetch)
 };
 // Diagnostic: the Generator's K1 over n = 64 k B bytes with per-wave clock stamps summed into d_clk[0] (shader clock
 // ticks) and d_clk[1] (100 MHz ticks); the production kernels never stamp.

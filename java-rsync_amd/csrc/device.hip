@@ -3159,11 +3159,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     int64_t t_tiles = 0, t_check = 0, t_event = 0, t_digest = 0;
     const uint8_t* stale = nullptr;  // poisoned: the cached digest
     uint32_t dg[4] = {0u, 0u, 0u, 0u};  // the window's digest at the current event (poisoned: the stale one)
-    int64_t pf_k = -1;                  // the next step's words, loaded by an aligned event (pf_k: their window)
-    int64_t pf_q0 = -1;                 // ... and the map words of a tile starting there (lane t's in pf_wv)
-    unsigned long long pf_wv = 0ull;
-    uint8_t pf_flag = 0;
-    int32_t pf_aw = 0, pf_tw = 0;
     int64_t clear_to = -1;            // stopped at a flush point: no candidate in [s, clear_to]
     int32_t why = CHAIN_WHY_NONE;
     rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
@@ -3231,18 +3226,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const bool al = s % B == 0;
         // the words steps (1), (1') and (2) look at first, loaded together: one global round trip per step instead of
         // three in sequence (a desynced walk takes these steps once per event)
-        uint8_t flag_k;
-        int32_t aw_k, tw_pref;
-        if (pf_k == k && pref == k && al && !poisoned) {  // prefetched by the event that led here (its own chunk)
-            flag_k = pf_flag;
-            aw_k = pf_aw;
-            tw_pref = pf_tw;
-        } else {
-            flag_k = (!poisoned && k == pref && k < nflags) ? F.flags[k] : (uint8_t)0;
-            aw_k = (al && k < na) ? F.aw[k] : 0;
-            tw_pref = (!poisoned && pref < C && k < na) ? F.table_weak[pref] : 0;
-        }
-        pf_k = -1;
+        const uint8_t flag_k = (!poisoned && k == pref && k < nflags) ? F.flags[k] : (uint8_t)0;
+        const int32_t aw_k = (al && k < na) ? F.aw[k] : 0;
+        const int32_t tw_pref = (!poisoned && pref < C && k < na) ? F.table_weak[pref] : 0;
         // (1) aligned chain: preferred index == k and source window k carries chunk k's sums
         if (flag_k) {
             if (t == 0) s_zero = nflags;
@@ -3349,12 +3335,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     const int64_t lo = a > pm ? a - pm : 0, hi = qlast - pm;
                     const bool need = lo <= 31 && hi >= lo;
                     unsigned long long wv = 0ull;
-                    if (need) {  // (the event before may have loaded this tile's words already)
-                        wv = (q0 == pf_q0 && (uint32_t)(pf_wv >> 32) == map_gen)
-                                 ? pf_wv
-                                 : __hip_atomic_load(&F.hmap[pm >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    pf_q0 = -1;
+                    if (need) wv = __hip_atomic_load(&F.hmap[pm >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     // beside it, the speculation's sum of an aligned window in the lane's range: a hit there needs
                     // no second round trip for its key
                     const bool al_lane = need && pm % B == 0;  // (pm <= qlast < na B)
@@ -3592,22 +3573,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const bool diag = spec_digest && kp < C;
         if (spec_digest) chain_digest_load(F.as + kp * dl, dl, dg);
         if (diag) chain_digest_load(F.table_strong + kp * dl, dl, dgk);
-        if (diag && F.prefetch) {
-            // the next search's map words too, should it start a block on (after a match here)
-            if (map_gen != 0u && p + B < F.hend) {
-                pf_q0 = p + B;
-                const int64_t pmn = pf_q0 + (int64_t)t * CHAIN_PPT;
-                pf_wv = pmn < F.hend ? __hip_atomic_load(&F.hmap[pmn >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                     : 0ull;
-            }
-            // and, should it match, the words the next step (at kp + 1, preferring chunk kp + 1) looks at first
-            const int64_t kn = kp + 1;
-            pf_k = kn;
-            // (vector loads: a scalar load here would hold the event's LDS reads, which wait on the same counter)
-            pf_flag = kn < nflags ? __builtin_nontemporal_load(&F.flags[kn]) : (uint8_t)0;
-            pf_aw = kn < na ? __builtin_nontemporal_load(&F.aw[kn]) : 0;
-            pf_tw = (kn < C && kn < na) ? __builtin_nontemporal_load(&F.table_weak[kn]) : 0;
-        }
         if (t < 64) {
             // every chunk with this key lies on the probe path before the first empty slot: wave 0 reads 64 slots of
             // it per round trip (one, nearly always) instead of one dependent load per slot
