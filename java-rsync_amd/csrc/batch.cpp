@@ -98,6 +98,7 @@ struct BatchState {
     // launch) and the map words (generation-tagged: zeroed once when allocated, never cleared between scans)
     DevBuf chain_help, chain_map;
     PinnedBuf h_chain_help;
+    std::vector<std::unique_ptr<char[]>> fiber_stacks;  // the resolver fibers' stacks (batch.cpp workers)
     hipEvent_t ev_fk = nullptr;
     hipEvent_t ev_sync = nullptr;  // spin_sync: the latency-path waits poll an event instead of blocking
     hipEvent_t ev_ch0 = nullptr, ev_ch1 = nullptr;  // around the walk (trace)
@@ -261,7 +262,7 @@ struct FileScan {
     bool wait_spec = false;  // its lead windows carry their chunks' sums: wait for the speculation, no head mode
     int32_t worker = 0;
     ucontext_t uc;
-    std::unique_ptr<char[]> stack;  // uninitialised: only the pages the fiber touches are committed
+    char* stack = nullptr;  // BatchState::fiber_stacks[i] for the i-th live file (reused across scans)
 };
 
 // Rounds: W worker threads (one per host core of the process, at most kMaxWorkers) each own a share of
@@ -1390,10 +1391,19 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     b.times.assign((size_t)W, HostTimes{});
     b.max_fiber_ms.assign((size_t)W, 0.0);
     for (int32_t i = 0; i < NL; ++i) files[(size_t)live[(size_t)i]].worker = i % W;
+    // the fibers' stacks, kept across scans: a fresh 512 KiB allocation per file and scan is an mmap, page faults as
+    // the fiber first runs, and a munmap, all on the resolvers' latency path (uninitialised: only touched pages commit)
+    if (S->fiber_stacks.size() < (size_t)NL) S->fiber_stacks.resize((size_t)NL);
+    std::vector<char*> stack_of((size_t)NL);
+    for (int32_t i = 0; i < NL; ++i) {
+        if (!S->fiber_stacks[(size_t)i]) S->fiber_stacks[(size_t)i].reset(new char[kFiberStack]);
+        stack_of[(size_t)i] = S->fiber_stacks[(size_t)i].get();
+    }
+    char* const* stacks = stack_of.data();
     std::vector<std::thread> th;
     th.reserve((size_t)W);
     for (int32_t w = 0; w < W; ++w) {
-        th.emplace_back([bp, &files, &live, w, NL, W] {
+        th.emplace_back([bp, &files, &live, w, NL, W, stacks] {
             Batch& b = *bp;
             uint64_t seen = 0;
             for (;;) {
@@ -1413,9 +1423,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                     fs.pending = false;
                     if (!fs.started) {
                         fs.started = true;
-                        fs.stack.reset(new char[kFiberStack]);
+                        fs.stack = stacks[i];
                         getcontext(&fs.uc);
-                        fs.uc.uc_stack.ss_sp = fs.stack.get();
+                        fs.uc.uc_stack.ss_sp = fs.stack;
                         fs.uc.uc_stack.ss_size = kFiberStack;
                         fs.uc.uc_link = &b.worker_uc[(size_t)w];
                         const uintptr_t a = reinterpret_cast<uintptr_t>(&fs);
