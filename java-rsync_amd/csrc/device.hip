@@ -2500,7 +2500,8 @@ int64_t probe_seg_len(int64_t full_positions, int64_t B) {
     // beside the speculation K1 sits on the resolver's latency path: 128 KiB blocks as 8-pass segments were 1 ms
     // slower per config-5 step than as tiles)
     if (opt(OPT_PROBE_LONG) == 0 || B > PROBE_LONG_MAX_B || full_positions < PROBE_LONG_BIG) return 0;
-    const int64_t passes = full_positions / (1024 * PROBE_LONG_SUB);  // ~1024 workgroups, then longer ones
+    // ~1024 workgroups per unit of the option (one residency wave at 4 waves per SIMD), then longer ones
+    const int64_t passes = full_positions / (1024 * opt(OPT_PROBE_LONG) * PROBE_LONG_SUB);
     return (passes < 1 ? 1 : passes > PROBE_LONG_PASSES ? PROBE_LONG_PASSES : passes) * PROBE_LONG_SUB;
 }
 

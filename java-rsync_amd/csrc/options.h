@@ -42,7 +42,7 @@ enum Opt : int {
     OPT_HOST_CORES,        // resolver worker threads (0: the process's cores, cgroup quota included)
     OPT_FILE_TILE,         // rsh_match_scan_file: tile bytes above OPT_FILE_TILE_ABOVE
     OPT_FILE_TILE_ABOVE,   // rsh_match_scan_file: sources above this size are scanned tiled
-    OPT_PROBE_LONG,        // 1: long probe intervals as pass-free segments (probe_long_kernel); 0: tiles only
+    OPT_PROBE_LONG,        // k > 0: long probe intervals as pass-free segments over ~1024 k workgroups; 0: tiles only
     OPT_SEGMENT_BYTES,     // rsh_*_batch (host memory): bytes of a segment's files copied to HBM per pass
     OPT_MD5_WIDTH,         // rsh_file_md5_batch / rsh_match_scan_batch: 0 = widest multi-buffer MD5, 1/8/16 = forced
     OPT_CHAIN_HELPERS,     // phase-0 walk: extra workgroups mapping searching files' prefixes (-1: CUs - files; 0: no map)
