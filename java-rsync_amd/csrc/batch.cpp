@@ -1747,15 +1747,18 @@ int match_scan_batch_claimed(rsh_ctx* ctx, rsh_scan_job* jobs, int32_t njobs, co
         scan.push_back(i);
     }
     if (!scan.empty()) {
-        RSH_BHIP(hipSetDevice(ctx->device));
+        // a failing call leaves no file it did not finish at RSH_OK: that file and every later one carry its code
+        // (a caller that trusts per-file statuses must never read zeros as results)
+        auto fail_from = [&](size_t k, int rc) {
+            for (size_t q = k; q < scan.size(); ++q) jobs[scan[q]].status = rc;
+            return rc;
+        };
+        if (hipSetDevice(ctx->device) != hipSuccess) return fail_from(0, RSH_E_DEVICE);
         for (size_t k = 0; k < scan.size(); k += kMaxLive) {
             const std::vector<int32_t> part(scan.begin() + (ptrdiff_t)k,
                                             scan.begin() + (ptrdiff_t)std::min(scan.size(), k + kMaxLive));
             const int rc = scan_batch(ctx, jobs, part, seed, stats);
-            if (rc != RSH_OK) {
-                for (int32_t i : part) jobs[i].status = rc;
-                return rc;
-            }
+            if (rc != RSH_OK) return fail_from(k, rc);
         }
     }
     for (int32_t i = 0; i < njobs; ++i)

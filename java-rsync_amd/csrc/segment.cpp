@@ -54,6 +54,11 @@ hipError_t copy_pieces(const rsh_piece* p, int32_t np, uint8_t* dst, hipStream_t
 
 int64_t budget() { return std::max<int64_t>(kAlign, rsh::opt(rsh::OPT_SEGMENT_BYTES)); }
 
+// Fault injection (option fault_inject, tests only): the failure paths of a segment call must leave every
+// unfinished file with a failing status.
+bool fail_alloc() { return (rsh::opt(rsh::OPT_FAULT_INJECT) & 1) != 0; }
+hipError_t fail_copy(hipError_t e) { return e == hipSuccess && (rsh::opt(rsh::OPT_FAULT_INJECT) & 2) ? hipErrorInvalidValue : e; }
+
 // Passes over the files `idx` (in order): consecutive runs whose aligned sizes fit the budget; a file larger
 // than the budget gets a pass of its own marked `alone`.
 struct Pass {
@@ -100,6 +105,59 @@ void add_stats(rsh_scan_stats* to, const rsh_scan_stats& s) {
     to->phase_guesses += s.phase_guesses;
 }
 
+// rsh_block_sums_batch's device work: the passes over `run` (validated files with chunks); done[f] once file f's
+// sums are on the host.  Any early return is the call's status (the caller marks the unfinished files).
+int block_sums_passes(rsh_ctx* ctx, rsh_block_batch_job* jobs, const std::vector<int32_t>& run,
+                      const std::vector<int64_t>& n, const uint8_t seed[4], std::vector<char>& done) {
+    RSH_CLAIM(ctx);
+    RSH_HIP(hipSetDevice(ctx->device));
+    for (const Pass& pass : plan_passes(run, n)) {
+        if (pass.alone) {  // larger than a pass: tile by tile (pieces.cpp)
+            rsh_block_batch_job& j = jobs[pass.files[0]];
+            j.status = rsh::block_sums_pieces_claimed(ctx, j.pieces, j.npieces, n[(size_t)pass.files[0]], &j.h, seed,
+                                                      j.weak_out, j.strong_out);
+            done[(size_t)pass.files[0]] = 1;
+            if (j.status != RSH_OK) return j.status;
+            continue;
+        }
+        int64_t data_bytes = 0, sum_bytes = 0;
+        for (int32_t f : pass.files) {
+            data_bytes += align_up(n[(size_t)f]);
+            sum_bytes += align_up(4 * (int64_t)jobs[f].h.chunk_count) +
+                         align_up((int64_t)jobs[f].h.chunk_count * jobs[f].h.digest_length);
+        }
+        if (fail_alloc() || ctx->seg_data.ensure((size_t)data_bytes + kAlign) != hipSuccess ||
+            ctx->seg_tab.ensure((size_t)sum_bytes + kAlign) != hipSuccess) {
+            snprintf(g_last_err, sizeof(g_last_err), "segment pass of %lld bytes: device memory (segment.cpp)",
+                     (long long)(data_bytes + sum_bytes));
+            return RSH_E_NOMEM;
+        }
+        std::vector<rsh_block_job> bj;
+        int64_t doff = 0, soff = 0;
+        for (int32_t f : pass.files) {
+            const rsh_block_batch_job& j = jobs[f];
+            uint8_t* d = ctx->seg_data.as<uint8_t>() + doff;
+            uint8_t* w = ctx->seg_tab.as<uint8_t>() + soff;
+            uint8_t* s = w + align_up(4 * (int64_t)j.h.chunk_count);
+            RSH_HIP(fail_copy(copy_pieces(j.pieces, j.npieces, d, ctx->stream)));
+            bj.push_back(rsh_block_job{d, n[(size_t)f], j.h, w, s});
+            doff += align_up(n[(size_t)f]);
+            soff += align_up(4 * (int64_t)j.h.chunk_count) + align_up((int64_t)j.h.chunk_count * j.h.digest_length);
+        }
+        const int rc = rsh::block_sums_batch_claimed(ctx, bj.data(), (int32_t)bj.size(), seed);
+        if (rc != RSH_OK) return rc;
+        for (size_t k = 0; k < bj.size(); ++k) {
+            rsh_block_batch_job& j = jobs[pass.files[k]];
+            const size_t C = (size_t)j.h.chunk_count, dl = (size_t)j.h.digest_length;
+            RSH_HIP(hipMemcpyAsync(j.weak_out, bj[k].d_weak, C * 4, hipMemcpyDeviceToHost, ctx->stream));
+            if (dl) RSH_HIP(hipMemcpyAsync(j.strong_out, bj[k].d_strong, C * dl, hipMemcpyDeviceToHost, ctx->stream));
+        }
+        RSH_HIP(hipStreamSynchronize(ctx->stream));
+        for (int32_t f : pass.files) done[(size_t)f] = 1;
+    }
+    return RSH_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -139,48 +197,15 @@ int rsh_block_sums_batch(rsh_ctx* ctx, rsh_block_batch_job* jobs, int32_t njobs,
         run.push_back(i);
     }
     if (!run.empty()) {
-        RSH_CLAIM(ctx);
-        RSH_HIP(hipSetDevice(ctx->device));
-        for (const Pass& pass : plan_passes(run, n)) {
-            if (pass.alone) {  // larger than a pass: tile by tile (pieces.cpp)
-                rsh_block_batch_job& j = jobs[pass.files[0]];
-                j.status = rsh::block_sums_pieces_claimed(ctx, j.pieces, j.npieces, n[(size_t)pass.files[0]], &j.h, seed,
-                                                          j.weak_out, j.strong_out);
-                if (j.status != RSH_OK) return j.status;
-                continue;
-            }
-            int64_t data_bytes = 0, sum_bytes = 0;
-            for (int32_t f : pass.files) {
-                data_bytes += align_up(n[(size_t)f]);
-                sum_bytes += align_up(4 * (int64_t)jobs[f].h.chunk_count) +
-                             align_up((int64_t)jobs[f].h.chunk_count * jobs[f].h.digest_length);
-            }
-            RSH_HIP(ctx->seg_data.ensure((size_t)data_bytes + kAlign));
-            RSH_HIP(ctx->seg_tab.ensure((size_t)sum_bytes + kAlign));
-            std::vector<rsh_block_job> bj;
-            int64_t doff = 0, soff = 0;
-            for (int32_t f : pass.files) {
-                const rsh_block_batch_job& j = jobs[f];
-                uint8_t* d = ctx->seg_data.as<uint8_t>() + doff;
-                uint8_t* w = ctx->seg_tab.as<uint8_t>() + soff;
-                uint8_t* s = w + align_up(4 * (int64_t)j.h.chunk_count);
-                RSH_HIP(copy_pieces(j.pieces, j.npieces, d, ctx->stream));
-                bj.push_back(rsh_block_job{d, n[(size_t)f], j.h, w, s});
-                doff += align_up(n[(size_t)f]);
-                soff += align_up(4 * (int64_t)j.h.chunk_count) + align_up((int64_t)j.h.chunk_count * j.h.digest_length);
-            }
-            const int rc = rsh::block_sums_batch_claimed(ctx, bj.data(), (int32_t)bj.size(), seed);
-            if (rc != RSH_OK) {
-                for (int32_t f : pass.files) jobs[f].status = rc;
-                return rc;
-            }
-            for (size_t k = 0; k < bj.size(); ++k) {
-                rsh_block_batch_job& j = jobs[pass.files[k]];
-                const size_t C = (size_t)j.h.chunk_count, dl = (size_t)j.h.digest_length;
-                RSH_HIP(hipMemcpyAsync(j.weak_out, bj[k].d_weak, C * 4, hipMemcpyDeviceToHost, ctx->stream));
-                if (dl) RSH_HIP(hipMemcpyAsync(j.strong_out, bj[k].d_strong, C * dl, hipMemcpyDeviceToHost, ctx->stream));
-            }
-            RSH_HIP(hipStreamSynchronize(ctx->stream));
+        // every file of `run` is finished (its sums on the host) once its flag is set; a failure leaves the others
+        // carrying the call's code, never RSH_OK with unwritten sums
+        std::vector<char> done((size_t)njobs, 0);
+        const int rc = block_sums_passes(ctx, jobs, run, n, seed, done);
+        if (rc != RSH_OK) {
+            (void)hipStreamSynchronize(ctx->stream);  // no copy from the caller's buffers outlives the call
+            for (int32_t i : run)
+                if (!done[(size_t)i] && jobs[i].status == RSH_OK) jobs[i].status = rc;
+            return rc;
         }
     }
     for (int32_t i = 0; i < njobs; ++i)
@@ -223,8 +248,23 @@ int rsh_match_scan_batch(rsh_ctx* ctx, rsh_scan_batch_job* jobs, int32_t njobs, 
             if (jobs[i].status != RSH_OK) return jobs[i].status;
         return RSH_OK;
     }
-    RSH_CLAIM(ctx);
-    RSH_HIP(hipSetDevice(ctx->device));
+    // A failure leaves no file it did not finish at RSH_OK (zero counts must never read as a result):
+    // every such file carries the call's code.
+    std::vector<char> done((size_t)njobs, 0);
+    auto fail_unfinished = [&](int code) {
+        for (int32_t i : ok)
+            if (!done[(size_t)i] && jobs[i].status == RSH_OK) jobs[i].status = code;
+        return code;
+    };
+    CtxClaim claim_(ctx);
+    if (!claim_.held) {
+        snprintf(g_last_err, sizeof(g_last_err), "context in use by another thread");
+        return fail_unfinished(RSH_E_BUSY);
+    }
+    if (const hipError_t e = hipSetDevice(ctx->device); e != hipSuccess) {
+        note_error(e, __LINE__, "segment.cpp");
+        return fail_unfinished(RSH_E_DEVICE);
+    }
     // every file's MD5 beside the copies and the scans (one core stays with the copies and the coordinator)
     std::vector<rsh::Md5File> mf;
     for (int32_t i : ok) mf.push_back(rsh::Md5File{jobs[i].pieces, jobs[i].npieces});
@@ -253,6 +293,7 @@ int rsh_match_scan_batch(rsh_ctx* ctx, rsh_scan_batch_job* jobs, int32_t njobs, 
             j.n_ev = sj[k].n_ev;
             j.literal = sj[k].literal;
             j.matched = sj[k].matched;
+            if (rc == RSH_OK || rc == RSH_E_NOSPACE) done[(size_t)host[k]] = 1;
         }
         if (rc == RSH_E_NOSPACE) rc = RSH_OK;  // per file
     }
@@ -269,6 +310,7 @@ int rsh_match_scan_batch(rsh_ctx* ctx, rsh_scan_batch_job* jobs, int32_t njobs, 
                 if (stats) add_stats(stats, r.stats);
                 j.status = emit_events(ctx, r, j.ev, j.ev_cap, &j.n_ev);
             }
+            done[(size_t)pass.files[0]] = 1;
             if (j.status != RSH_OK && j.status != RSH_E_NOSPACE) rc = j.status;
             continue;
         }
@@ -278,8 +320,10 @@ int rsh_match_scan_batch(rsh_ctx* ctx, rsh_scan_batch_job* jobs, int32_t njobs, 
             tab_bytes += align_up(4 * (int64_t)jobs[f].h.chunk_count) +
                          align_up((int64_t)jobs[f].h.chunk_count * jobs[f].h.digest_length);
         }
-        if (ctx->seg_data.ensure((size_t)data_bytes + kAlign) != hipSuccess ||
+        if (fail_alloc() || ctx->seg_data.ensure((size_t)data_bytes + kAlign) != hipSuccess ||
             ctx->seg_tab.ensure((size_t)tab_bytes + kAlign) != hipSuccess) {
+            snprintf(g_last_err, sizeof(g_last_err), "segment pass of %lld bytes: device memory (segment.cpp)",
+                     (long long)(data_bytes + tab_bytes));
             rc = RSH_E_NOMEM;
             break;
         }
@@ -292,7 +336,7 @@ int rsh_match_scan_batch(rsh_ctx* ctx, rsh_scan_batch_job* jobs, int32_t njobs, 
             uint8_t* d = ctx->seg_data.as<uint8_t>() + doff;
             uint8_t* w = ctx->seg_tab.as<uint8_t>() + toff;
             uint8_t* s = w + align_up(4 * (int64_t)C);
-            if (e == hipSuccess) e = copy_pieces(j.pieces, j.npieces, d, ctx->stream);
+            if (e == hipSuccess) e = fail_copy(copy_pieces(j.pieces, j.npieces, d, ctx->stream));
             if (e == hipSuccess && C) e = hipMemcpyAsync(w, j.weak, C * 4, hipMemcpyHostToDevice, ctx->stream);
             if (e == hipSuccess && C && dl) e = hipMemcpyAsync(s, j.strong, C * dl, hipMemcpyHostToDevice, ctx->stream);
             rsh_scan_job x{};
@@ -320,13 +364,15 @@ int rsh_match_scan_batch(rsh_ctx* ctx, rsh_scan_batch_job* jobs, int32_t njobs, 
             j.n_ev = sj[k].n_ev;
             j.literal = sj[k].literal;
             j.matched = sj[k].matched;
+            if (prc == RSH_OK || prc == RSH_E_NOSPACE) done[(size_t)pass.files[k]] = 1;
         }
         if (stats) add_stats(stats, ps);
         if (prc != RSH_OK && prc != RSH_E_NOSPACE) rc = prc;
     }
     md5_thread.join();
+    if (rc != RSH_OK) (void)hipStreamSynchronize(ctx->stream);  // no copy from the caller's buffers outlives the call
     for (size_t k = 0; k < ok.size(); ++k) memcpy(jobs[ok[k]].file_md5, md5.data() + 16 * k, 16);
-    if (rc != RSH_OK) return rc;
+    if (rc != RSH_OK) return fail_unfinished(rc);
     for (int32_t i = 0; i < njobs; ++i)
         if (jobs[i].status != RSH_OK) return jobs[i].status;
     return RSH_OK;

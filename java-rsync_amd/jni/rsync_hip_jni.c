@@ -611,11 +611,10 @@ JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksu
     if (rc == RSH_OK) {
         rc = rsh_block_sums_batch(c, jobs, nf, (const uint8_t*)s4);
         if (rc != RSH_OK) {
-            for (jint f = 0; f < nf; ++f)
-                if (jobs[f].status != RSH_OK) {
-                    throw_file_status(env, f, jobs[f].status);
-                    break;
-                }
+            jint f = 0;
+            while (f < nf && jobs[f].status == RSH_OK) ++f;
+            if (f < nf) throw_file_status(env, f, jobs[f].status);
+            else throw_status(env, rc); /* the call failed before any file did: never zero sums as results */
         } else {
             for (jint f = 0; f < nf; ++f) {
                 const jsize C = a.h[f].chunk_count;
@@ -639,11 +638,33 @@ JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksu
     segment_free(&a);
 }
 
-/* An event buffer no scan of n bytes overflows: each MATCH but the last consumes a full window, each LITERAL
- * precedes a MATCH or ends a 10*B flush interval (Sender.java:1251-1316). */
+/* An event buffer no scan of n bytes overflows (Sender.java:1251-1316):
+ *  - a MATCH consumes its window, w = min(B, n - start) bytes (:1279-1287); w < B only when the window reaches the
+ *    file's end, and then the match ends the scan, so M <= n / B + 1 (runs of consecutive matches are one event);
+ *  - a flush (isFull, :1294-1302) emits exactly 10*B literal bytes and moves the mark past them: F <= n / (10 B);
+ *  - every other LITERAL precedes a MATCH (:1270) or is the final one (:1313), and empty literals are not emitted.
+ * So events <= 2 M + F + 1 <= 2 (n / B + 1) + n / (10 B) + 1 (tests/test_oracle.py::test_event_bound_adversarial
+ * checks the bound on alternating match / literal / flush sources at small B). */
 static int64_t event_bound(int64_t n, const rsh_header* h) {
     if (h->block_length <= 0) return n / 8192 + 2;
     return 2 * (n / h->block_length + 1) + n / (10 * (int64_t)h->block_length) + 4;
+}
+
+/* A file whose events outran event_bound (it cannot, by the argument above; this keeps the segment correct should
+ * the bound ever be wrong) is scanned again alone into a buffer of the event count the first scan reported. */
+static int rescan_nospace(rsh_ctx* c, rsh_scan_batch_job* jobs, jint nf, const uint8_t* seed) {
+    int rc = RSH_OK;
+    for (jint f = 0; f < nf; ++f) {
+        if (jobs[f].status == RSH_OK) continue;
+        if (jobs[f].status != RSH_E_NOSPACE) return jobs[f].status;
+        rsh_event* ev = (rsh_event*)realloc(jobs[f].ev, (size_t)jobs[f].n_ev * sizeof(rsh_event) + sizeof(rsh_event));
+        if (!ev) return RSH_E_NOMEM;
+        jobs[f].ev = ev;
+        jobs[f].ev_cap = jobs[f].n_ev;
+        rc = rsh_match_scan_batch(c, &jobs[f], 1, seed, NULL);
+        if (rc != RSH_OK) return rc;
+    }
+    return rc;
 }
 
 /* Returns every file's events, file after file, as {kind, offset, length, index | (count << 32)} quadruples;
@@ -696,12 +717,12 @@ JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeC
     jlongArray out = NULL;
     if (rc == RSH_OK) {
         rc = rsh_match_scan_batch(c, jobs, nf, (const uint8_t*)s4, NULL);
+        if (rc == RSH_E_NOSPACE) rc = rescan_nospace(c, jobs, nf, (const uint8_t*)s4);
         if (rc != RSH_OK) {
-            for (jint f = 0; f < nf; ++f)
-                if (jobs[f].status != RSH_OK) {
-                    throw_file_status(env, f, jobs[f].status);
-                    break;
-                }
+            jint f = 0;
+            while (f < nf && jobs[f].status == RSH_OK) ++f;
+            if (f < nf) throw_file_status(env, f, jobs[f].status);
+            else throw_status(env, rc); /* the call failed before any file did */
         } else {
             int64_t total = 0;
             for (jint f = 0; f < nf; ++f) total += jobs[f].n_ev;

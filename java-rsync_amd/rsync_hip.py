@@ -474,9 +474,10 @@ class Context:
     def _pieces(pieces):
         return _piece_list(pieces)
 
-    def block_sums_batch(self, files, seed):
+    def block_sums_batch(self, files, seed, statuses=None):
         """A segment's Generator pass from host memory (rsh_block_sums_batch; Generator.itemizeSegment):
-        files = [(pieces, Header)] -> [(weak, strong)] per file."""
+        files = [(pieces, Header)] -> [(weak, strong)] per file.  statuses (a list): receives the call's code and
+        every file's status instead of raising (tests of the failure paths)."""
         s = np.frombuffer(bytes(seed), np.uint8).copy()
         jobs = (BlockBatchJob * max(len(files), 1))()
         keep, outs = [], []
@@ -488,13 +489,18 @@ class Context:
             outs.append((w, st, h))
             jobs[i].pieces, jobs[i].npieces, jobs[i].h = ctypes.cast(pl, ctypes.POINTER(Piece)), len(arrs), h
             jobs[i].weak_out, jobs[i].strong_out = w.ctypes.data, st.ctypes.data
-        _check(lib().rsh_block_sums_batch(self._p, jobs, len(files), _ptr(s)))
+        rc = lib().rsh_block_sums_batch(self._p, jobs, len(files), _ptr(s))
+        if statuses is not None:
+            statuses[:] = [rc] + [jobs[i].status for i in range(len(files))]
+        else:
+            _check(rc)
         return [(w[:h.chunk_count], st[:h.chunk_count * h.digest_length]) for w, st, h in outs]
 
-    def match_scan_batch(self, files, seed, ev_caps=None):
+    def match_scan_batch(self, files, seed, ev_caps=None, statuses=None):
         """A segment's Sender pass from host memory (rsh_match_scan_batch; Sender.sendFiles):
         files = [(pieces, Header, weak, strong)] -> ([(events, file_md5, literal, matched, status)], stats).
-        A file's status is RSH_E_NOSPACE when its ev_caps entry was short (its events are then not kept)."""
+        A file's status is RSH_E_NOSPACE when its ev_caps entry was short (its events are then not kept).
+        statuses (a list): receives the call's code instead of raising."""
         s = np.frombuffer(bytes(seed), np.uint8).copy()
         jobs = (ScanBatchJob * max(len(files), 1))()
         keep, evs = [], []
@@ -512,7 +518,9 @@ class Context:
             j.ev, j.ev_cap = ev.ctypes.data, cap
         stats = ScanStats()
         rc = lib().rsh_match_scan_batch(self._p, jobs, len(files), _ptr(s), ctypes.byref(stats))
-        if rc != RSH_E_NOSPACE:
+        if statuses is not None:
+            statuses[:] = [rc]
+        elif rc != RSH_E_NOSPACE:
             _check(rc)
         out = []
         for i in range(len(files)):

@@ -13,6 +13,8 @@
 #   files-trace  one traced config-4 step (VARIANT, default half): the chain walk's breakdown (scan_trace = 2)
 #   prof         rocprofv3 kernel trace + stats of the default line (the summary committed under profiles/)
 #   timeline     rocprofv3 kernel + copy timeline of the config-4 line (VARIANT)
+#   hl           the config-5 headline alone (no companions, no config 4), 20 steps
+#   hl-trace     rocprofv3 kernel + copy trace of the headline alone, and its per-step gaps (tools/step_gaps.py)
 #   fetch        rocprofv3 --pmc FETCH_SIZE passes (counters only, kernel trace) of the default line and the config-4
 #                line: the HBM bytes per K1 launch that bench.py reports as roofline.traffic
 #   pmc-k1       one PMC pass over kbench: the production K1 against the same kernel without global loads
@@ -63,6 +65,12 @@ for step in "$@"; do
         e2e4) run 900 python java-rsync_amd/tools/e2e_config4.py > "$O/e2e_config4.json" 2> "$O/e2e_config4.err" ;;
         smoke) run 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.log" 2>&1 ;;
         bench) run 300 python bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
+        hl) run 240 python bench.py --no-companions --no-files --no-cpu-baseline --steps 20 --warmup 5 $HL_ARGS \
+            > "$O/hl.json" 2> "$O/hl.err" ;;
+        hl-trace) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --kernel-trace --memory-copy-trace -d "$O/hl_trace" \
+            -o run --output-format csv -- python3 "$R/bench.py" --no-companions --no-files --no-cpu-baseline --steps 10 \
+            --warmup 3 $HL_ARGS > "$O/hl_trace.json" 2> "$O/hl_trace.err") || exit 1
+            python3 java-rsync_amd/tools/step_gaps.py "$O/hl_trace" > "$O/hl_gaps.txt" 2>&1 ;;
         files)
             for v in half identical; do
                 run 300 python bench.py --workload files --variant $v --steps "${FILES_STEPS:-8}" --warmup 2 \

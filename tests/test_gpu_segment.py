@@ -155,3 +155,27 @@ def test_config4_shard_from_host_memory(ctx):
         assert status == 0 and (int(rec.size), l2, m2) == (n_ev, lit, mat), f"file {i}"
         assert G.events_sha(rec) == sha, f"file {i}: match list differs from the oracle's"
         assert fm.hex() == fmd5, f"file {i}: file MD5"
+
+
+@pytest.mark.parametrize("fault", [1, 2])
+def test_segment_failure_marks_every_unfinished_file(ctx, rsh_opt, fault):
+    """a segment call that fails (fault 1: a pass's HBM allocation, RSH_E_NOMEM; fault 2: its
+    copies, RSH_E_DEVICE) leaves no file it did not finish at RSH_OK, so a caller trusting per-file statuses
+    never sends zero-filled sums or an empty event list as a result.  Two passes (a lowered budget): every file
+    fails.  The context works again once the fault is gone."""
+    B, dl = 512, 2
+    files = [O.splitmix(40 * B + 9 * k, 77 + k) for k in range(5)]
+    heads = [R.header_make(B, dl, f.size) for f in files]
+    rsh_opt("segment_bytes", 3 * 40 * B)
+    rsh_opt("fault_inject", fault)
+    want = R.RSH_E_NOMEM if fault == 1 else R.RSH_E_DEVICE
+    st = []
+    ctx.block_sums_batch([([f], h) for f, h in zip(files, heads)], SEED, statuses=st)
+    assert st[0] == want and st[1:] == [want] * len(files), st
+    tabs = [O.generator(f, O.header(B, dl, f.size), SEED) for f in files]
+    st = []
+    out, _ = ctx.match_scan_batch([([f], h, w, s) for f, h, (w, s) in zip(files, heads, tabs)], SEED, statuses=st)
+    assert st == [want] and [o[4] for o in out] == [want] * len(files), (st, [o[4] for o in out])
+    rsh_opt("fault_inject", 0)
+    sums = ctx.block_sums_batch([([f], h) for f, h in zip(files, heads)], SEED)
+    assert all(np.array_equal(w, ow) and np.array_equal(s, os_) for (w, s), (ow, os_) in zip(sums, tabs))

@@ -286,3 +286,28 @@ def test_segment_natives_match_oracle(H):
         assert at == q.shape[0]
     finally:
         H.jh_ctx_destroy(ctypes.c_int64(ctx))
+
+
+@pytest.mark.gpu
+def test_segment_natives_throw_when_the_call_fails(H):
+    """a segment call that fails before any file has a status of its own (here an injected HBM
+    allocation failure, option fault_inject) throws -- blockSumsBatch no longer returns zero-filled sums and
+    matchScanBatch no longer returns null with no exception pending."""
+    ctx = H.jh_ctx_create(0)
+    assert ctx and exc(H) == "", exc(H)
+    try:
+        n, B = 100000, 512
+        data = O.splitmix(n, 0xF00D)
+        h = O.header(B, 2, n)
+        w, st = np.zeros(h.chunk_count, np.int32), np.zeros(h.chunk_count * 2, np.uint8)
+        R.set_option("fault_inject", 1)
+        assert block_sums_batch(H, ctx, [([data], n, h)], [w], [st]) == "java/lang/OutOfMemoryError"
+        e, ev, _, _ = match_scan_batch(H, ctx, [([data], n, h)], [w], [st])
+        assert e == "java/lang/OutOfMemoryError" and ev is None
+        R.set_option("fault_inject", 0)
+        assert block_sums_batch(H, ctx, [([data], n, h)], [w], [st]) == ""
+        ow, os_ = O.generator(data, h, SEED)
+        assert np.array_equal(w, ow) and np.array_equal(st, os_)
+    finally:
+        R.reset_options()
+        H.jh_ctx_destroy(ctypes.c_int64(ctx))

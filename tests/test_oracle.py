@@ -230,3 +230,39 @@ def test_receiver_combine_deferred_and_errors():
     assert O.receiver_combine(bad, h, basis)[0] == -1
     assert O.receiver_combine(mixed, O.header(0, 0, 0), basis)[0] == -1
     assert O.receiver_combine(tok[:5], h, basis)[0] == -2
+
+
+def _event_bound(n, B):
+    """rsync_hip_jni.c event_bound (the per-file event buffer of matchScanBatch)."""
+    return n // 8192 + 2 if B <= 0 else 2 * (n // B + 1) + n // (10 * B) + 4
+
+
+@pytest.mark.parametrize("B", [1, 2, 3, 8, 17])
+def test_event_bound_adversarial(B):
+    """the segment JNI sizes each file's event buffer by event_bound.  Sources built to
+    maximise events -- a match, one literal byte, a match ... ; runs of >= 10 B literal bytes (flushes) between
+    matches; a short last chunk matched at the end -- never exceed it (the oracle does not merge match runs, so
+    its count bounds the device's)."""
+    rng = random.Random(B)
+    seed = bytes([1, 2, 3, 4])
+    for trial in range(12):
+        C = rng.randrange(4, 40)
+        basis = bytes(rng.randrange(256) for _ in range(C * B + rng.randrange(0, B)))
+        blocks = [basis[k * B:(k + 1) * B] for k in range((len(basis) + B - 1) // B)]
+        out = bytearray()
+        for k in range(rng.randrange(20, 80)):
+            out += blocks[rng.randrange(len(blocks) - 1)]
+            mode = trial % 3
+            if mode == 0:
+                out += bytes([rng.randrange(256)])  # one literal byte between matches
+            elif mode == 1:
+                out += bytes(rng.randrange(256) for _ in range(10 * B + rng.randrange(0, 3)))  # a flush first
+            else:
+                out += bytes(rng.randrange(256) for _ in range(rng.randrange(0, 2 * B)))
+        out += blocks[-1]  # the short last chunk (when there is one) at the very end
+        src = np.frombuffer(bytes(out), np.uint8).copy()
+        h = O.header(B, 2, len(basis))
+        w, s = O.generator(np.frombuffer(basis, np.uint8).copy(), h, seed)
+        ev = O.sender(src, h, w, s, seed)[0]
+        assert len(ev) <= _event_bound(src.size, B), (B, trial, len(ev), _event_bound(src.size, B))
+        assert any(e[0] == 2 for e in ev)  # the construction really matches
