@@ -313,6 +313,31 @@ int rsh_receiver_combine_device(rsh_ctx* ctx, const uint8_t* tokens, int64_t tok
                                 const void* d_replica, int64_t replica_len, int32_t defer_write, void* d_target,
                                 int64_t target_cap, rsh_combine_result* out);
 
+/* ---- a segment's Receiver from host memory (Receiver.receiveFiles, Receiver.java:1145-1263: combineDataToFile
+ * :459-556 and isRemoteAndLocalFileIdentical :824-842 for each file in turn) ----
+ * One job per file: its de-multiplexed token stream, its replica as host pieces (nreplica 0: no replica), the
+ * target buffer.  Each job gets rsh_receiver_combine's result and its own status (RSH_E_PROTOCOL / RSH_E_INVAL /
+ * RSH_E_NOSPACE as there); a call that fails as a whole leaves every file it did not finish with its code.  The
+ * rebuilt files are gathered on the device (the token streams and the replica ranges they name go up, every file's
+ * blocks and literals are one gather launch, the targets come back) in passes of at most option segment_bytes,
+ * overlapped; the verify digests -- one serial MD5 chain per file -- run on the host's cores beside the copies,
+ * up to 16 files per core (md5_mb.cpp), over the replica ranges and literal bytes the tokens name, which are
+ * exactly the rebuilt file's bytes. */
+typedef struct {
+    const uint8_t* tokens;    /* host: the file's token stream, ending with putInt(0) */
+    int64_t tokens_len;
+    rsh_header h;             /* the file's checksum header (as sent by the Generator) */
+    const rsh_piece* replica; /* host: the replica as pieces (their concatenation); NULL / 0 pieces: none */
+    int32_t nreplica;
+    int32_t defer_write;
+    uint8_t* target;          /* host, caller-owned: target_cap bytes (nothing written when intact) */
+    int64_t target_cap;
+    int32_t status;           /* out */
+    int32_t reserved;
+    rsh_combine_result res;   /* out */
+} rsh_combine_job;
+int rsh_receiver_combine_batch(rsh_ctx* ctx, rsh_combine_job* jobs, int32_t njobs);
+
 /* ---- device buffers for the *_device entry points (callers without their own allocator, e.g. JNI) ---- */
 int rsh_dev_alloc(rsh_ctx* ctx, int64_t bytes, void** out);
 int rsh_dev_free(rsh_ctx* ctx, void* p);

@@ -120,6 +120,7 @@ struct rsh_ctx {
     DevBuf segs;                                 // segmented K1 descriptors (prefix + phase speculation)
     DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw, partials, bucket;
     DevBuf seg_data, seg_tab;                    // rsh_*_batch (segment.cpp): a pass's files and tables / sums
+    DevBuf rcv[2], rcv_ops[2];                   // rsh_receiver_combine_batch: two pass buffers and their gather ops
     hipStream_t aux = nullptr;                   // the aligned speculation
     hipStream_t phase = nullptr;                 // the phase-shifted speculation (beside a prefix speculation)
     hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr;
@@ -142,6 +143,7 @@ struct rsh_ctx {
     PinnedBuf h_bucket;  // after a probe hit: {count, key, chunk indices} of the key that hit
     PinnedBuf h_files;   // the scan's rsh::ScanFile (a batch of one for the probe / gather kernels)
     PinnedBuf h_stage;   // file ingest ring (ingest.cpp); never shared with the scan's buffers
+    PinnedBuf h_rcv_ops[2];  // rsh_receiver_combine_batch: the gather ops of a pass, staged
     uint64_t first_used = 0;    // probe result slots handed out (see HipBackend::first_hit)
     // device, uncached, 256 B: the speculation launch of generation g stops once abort_word[0] holds g;
     // a phase-shifted speculation polls abort_word[kPhaseWord] (its own 64-B line)
@@ -155,11 +157,12 @@ struct rsh_ctx {
         if (batch) rsh::destroy_batch_state(batch);
         for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &ph_weak[0], &ph_strong[0],
                           &ph_weak[1], &ph_strong[1], &slots, &dslots,
-                          &dkeys, &pos, &out, &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket, &seg_data, &seg_tab})
+                          &dkeys, &pos, &out, &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket, &seg_data, &seg_tab,
+                          &rcv[0], &rcv[1], &rcv_ops[0], &rcv_ops[1]})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pw[0], &h_ps[0], &h_pw[1], &h_ps[1], &h_lead, &h_pos, &h_out, &h_iv,
                              &h_tiles, &h_keys, &h_first, &h_win, &h_ptiles, &h_psegs, &h_hit, &h_win0, &h_pend, &h_bucket, &h_files,
-                             &h_stage})
+                             &h_stage, &h_rcv_ops[0], &h_rcv_ops[1]})
             b->release();
         if (abort_word) (void)hipFree(abort_word);
         if (ev_in) (void)hipEventDestroy(ev_in);

@@ -261,7 +261,8 @@ struct GatherOp {
     uint8_t* dst;
     int64_t len;
 };
-hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s);
+// avg_len (optional): the ops' average length; below 64 KiB a 256-thread form (four short ops per CU slot of one)
+hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s, int64_t avg_len = 1 << 20);
 #ifdef RSH_KBENCH
 hipError_t launch_gather_ops_variant(int v, const GatherOp* ops, uint32_t n, hipStream_t s);  // A/Bs (kbench)
 #endif

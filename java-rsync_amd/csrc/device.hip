@@ -3943,8 +3943,12 @@ __global__ __launch_bounds__(T) void gather_ops_kernel_t(const GatherOp* __restr
     for (int64_t k = head + body + t; k < op.len; k += blockDim.x) op.dst[k] = op.src[k];
 }
 
-hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s) {
+hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s, int64_t avg_len) {
     if (n == 0) return hipSuccess;
+    if (avg_len < (64 << 10)) {  // short ops (a segment's 8 KiB literal tokens and blocks): 256 threads each
+        hipLaunchKernelGGL((gather_ops_kernel_t<256, 2, true, true>), dim3(n), dim3(256), 0, s, ops);
+        return hipGetLastError();
+    }
     // 1024 threads per 1 MiB op (16 waves per CU in flight): 0.754 of the 8 TB/s peak (read + write) against 0.680 for
     // 256 threads, kbench KBENCH_GATHER (profiles/r4/r4e_kbench_gather.log)
     hipLaunchKernelGGL((gather_ops_kernel_t<1024, 4, true, true>), dim3(n), dim3(1024), 0, s, ops);

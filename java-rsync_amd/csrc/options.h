@@ -48,7 +48,7 @@ enum Opt : int {
     OPT_CHAIN_HELPERS,     // phase-0 walk: extra workgroups mapping searching files' prefixes (-1: CUs - files; 0: no map)
     OPT_CHAIN_MAP_BYTES,   // ... the map's HBM budget (bytes; above it the walks search tile by tile)
     OPT_BATCH_SKIP_REST,   // 1: the rest of a two-phase speculation only if some phase-0 walk reached the prefix's end
-    OPT_FAULT_INJECT,      // tests only: bit 0 a segment pass's HBM allocation fails, bit 1 its copies report a device error
+    OPT_FAULT_INJECT,      // tests only: bit 0 a segment / Receiver pass's HBM allocation fails, bit 1 a segment's copies fail
     OPT_COUNT
 };
 

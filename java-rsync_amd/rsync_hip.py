@@ -104,6 +104,14 @@ class Piece(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_int64)]
 
 
+class CombineJob(ctypes.Structure):
+    """rsh_combine_job: one file of a segment's Receiver pass (rsh_receiver_combine_batch)."""
+    _fields_ = [("tokens", ctypes.c_void_p), ("tokens_len", ctypes.c_int64), ("h", Header),
+                ("replica", ctypes.POINTER(Piece)), ("nreplica", ctypes.c_int32), ("defer_write", ctypes.c_int32),
+                ("target", ctypes.c_void_p), ("target_cap", ctypes.c_int64), ("status", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("res", CombineResult)]
+
+
 class BlockBatchJob(ctypes.Structure):
     """rsh_block_batch_job: one basis file of a segment's Generator pass from host memory (rsh_block_sums_batch)."""
     _fields_ = [("pieces", ctypes.POINTER(Piece)), ("npieces", ctypes.c_int32), ("status", ctypes.c_int32),
@@ -133,7 +141,7 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_coun
            "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
            "rsh_match_scan_device", "rsh_match_scan_tiled", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
            "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_receiver_combine",
-           "rsh_receiver_combine_device", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_block_sums_batch", "rsh_match_scan_batch", "rsh_file_md5_batch", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
+           "rsh_receiver_combine_device", "rsh_receiver_combine_batch", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_block_sums_batch", "rsh_match_scan_batch", "rsh_file_md5_batch", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 # include/rsync_hip_debug.h (testing / diagnostics ABI)
 DEBUG_EXPORTS = ["rsh_debug_set_option", "rsh_debug_get_option", "rsh_debug_reset_options", "rsh_debug_k1_clock"]
 
@@ -205,6 +213,7 @@ def lib():
         "rsh_match_scan_batch_device": ([P, ctypes.POINTER(ScanJob), I32, P, ctypes.POINTER(ScanStats)],
                                         ctypes.c_int),
         "rsh_receiver_combine": ([P, P, I64, HP, P, I64, I32, P, I64, ctypes.POINTER(CombineResult)], ctypes.c_int),
+        "rsh_receiver_combine_batch": ([P, ctypes.POINTER(CombineJob), I32], ctypes.c_int),
         "rsh_receiver_combine_device": ([P, P, I64, HP, P, I64, I32, P, I64, ctypes.POINTER(CombineResult)],
                                         ctypes.c_int),
         "rsh_block_sums_file": ([P, ctypes.c_char_p, I64, HP, P, P, P, ctypes.POINTER(I32)], ctypes.c_int),
@@ -588,6 +597,38 @@ class Context:
             rc = lib().rsh_fetch_events(self._p, _ptr(ev), n_ev.value, ctypes.byref(n_ev))
         _check(rc)
         return ev[:n_ev.value], fm.tobytes(), lit.value, mat.value, stats.as_dict(), bool(err.value)
+
+    def receiver_combine_batch(self, files, statuses=None):
+        """A segment's Receiver from host memory (rsh_receiver_combine_batch; Receiver.receiveFiles):
+        files = [(tokens, Header, replica pieces or None, defer_write, target_cap or None)] ->
+        [(status, target bytes, CombineResult)].  statuses (a list): receives the call's code instead of raising."""
+        jobs = (CombineJob * max(len(files), 1))()
+        keep, tgts = [], []
+        for i, (tokens, h, replica, defer, cap) in enumerate(files):
+            t = _u8(tokens)
+            arrs, pl, rn = _piece_list(replica) if replica is not None else ([], None, 0)
+            if cap is None:
+                cap = t.size + (t.size // 4) * max(h.block_length, 1) + 16
+            tgt = np.zeros(max(cap, 1), np.uint8)
+            keep.append((t, arrs, pl))
+            tgts.append(tgt)
+            j = jobs[i]
+            j.tokens, j.tokens_len, j.h = (t.ctypes.data if t.size else None), t.size, h
+            if replica is not None:
+                j.replica, j.nreplica = ctypes.cast(pl, ctypes.POINTER(Piece)), len(arrs)
+            j.defer_write, j.target, j.target_cap = int(bool(defer)), tgt.ctypes.data, cap
+        rc = lib().rsh_receiver_combine_batch(self._p, jobs, len(files))
+        if statuses is not None:
+            statuses[:] = [rc]
+        elif rc not in (RSH_OK, RSH_E_NOSPACE, RSH_E_PROTOCOL, RSH_E_INVAL):
+            _check(rc)
+        out = []
+        for i in range(len(files)):
+            j = jobs[i]
+            r = CombineResult.from_buffer_copy(j.res)
+            n = r.target_len if j.status == RSH_OK else 0
+            out.append((j.status, tgts[i][:n].tobytes(), r))
+        return out
 
     def receiver_combine(self, tokens, h, replica, defer_write=False, target_cap=None):
         """Receiver.combineDataToFile (Receiver.java:459-555): (target bytes, CombineResult).  The target is

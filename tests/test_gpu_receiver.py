@@ -120,3 +120,73 @@ def test_receiver_1GiB_from_device_scan(ctx):
     assert rc == 0 and r.target_len == n and (r.literal, r.matched) == (lit, mat)
     assert bytes(r.md5) == fm
     assert np.array_equal(d_src.download(), src)
+
+
+def _cut(rng, b):
+    """bytes -> 1-3 host pieces cut anywhere (empty pieces included)."""
+    a = np.frombuffer(b, np.uint8)
+    pts = sorted(rng.randrange(0, len(a) + 1) for _ in range(rng.randrange(0, 3)))
+    out, prev = [], 0
+    for p in pts + [len(a)]:
+        out.append(a[prev:p])
+        prev = p
+    return out
+
+
+@pytest.mark.parametrize("budget", [0, 1 << 16])
+def test_receiver_batch_matches_oracle(ctx, rsh_opt, budget):
+    """A segment's Receiver in one call (rsh_receiver_combine_batch; Receiver.receiveFiles, Receiver.java:1145-1263):
+    40 files of every edit shape, replicas cut into host pieces, some without a replica, some with deferred writes
+    (intact files), one stream with a block index out of range (RsyncProtocolException, that file only), one target
+    too small (RSH_E_NOSPACE, that file only).  Every file's rebuilt bytes, sizes, intact flag and digest equal
+    orc_receiver_combine's (budget: the pass size, lowered so that files go through many overlapped passes)."""
+    from test_resolver_cpu import _mutate
+    if budget:
+        rsh_opt("segment_bytes", budget)
+    rng = random.Random(7 + budget)
+    jobs, want = [], []
+    for i in range(40):
+        B = rng.choice([512, 700, 1024, 2048, 8192])
+        nb = rng.randrange(1, 60 * B)
+        key = rng.randrange(1 << 62)
+        basis = O.splitmix(nb, key).tobytes()
+        src = basis if i % 7 == 0 else (_mutate(rng, basis, B, key) or basis)
+        dl = rng.choice([2, 3, 16])
+        h, tok, fm = _stream(basis, src, B, dl)
+        defer = i % 3 == 0
+        replica = None if i % 11 == 5 else basis
+        cap = None
+        if i == 17:  # a block index past the table
+            tok = int.to_bytes((-(h.chunk_count + 1)) & 0xFFFFFFFF, 4, "little") + bytes(4)
+        if i == 23:
+            cap = 10
+        jobs.append((tok, h, None if replica is None else _cut(rng, replica), defer, cap))
+        want.append(O.receiver_combine(tok, O.header(B, dl, nb), replica, defer,
+                                       target_cap=cap if cap is not None else len(tok) + len(src) + 64))
+    out = ctx.receiver_combine_batch(jobs)
+    for i, ((status, tgt, r), (orc, otgt, olit, omat, ointact, omd5)) in enumerate(zip(out, want)):
+        if i == 17:
+            assert orc == -1 and status == R.RSH_E_PROTOCOL, (i, status)
+            continue
+        if i == 23:
+            assert orc == -3 and status == R.RSH_E_NOSPACE and r.target_len > 10, (i, status)
+            continue
+        assert status == 0, (i, status)
+        assert (tgt, r.literal, r.matched, r.intact, bytes(r.md5), r.tokens_used) == \
+            (otgt, olit, omat, ointact, omd5, orc), f"file {i}"
+
+
+def test_receiver_batch_failure_marks_every_file(ctx, rsh_opt):
+    """A pass that cannot get its HBM (fault injection) fails every file it did not finish (no file left at RSH_OK
+    with an unwritten target); the intact files, which need no device pass, keep their results."""
+    B = 1024
+    basis = O.splitmix(30 * B, 5).tobytes()
+    src = basis[:7 * B] + b"x" * 100 + basis[7 * B:]
+    h, tok, _ = _stream(basis, src, B, 2)
+    hi, toki, fmi = _stream(basis, basis, B, 2)
+    rsh_opt("fault_inject", 1)
+    st = []
+    out = ctx.receiver_combine_batch([(tok, h, [np.frombuffer(basis, np.uint8)], False, None),
+                                      (toki, hi, [np.frombuffer(basis, np.uint8)], True, None)], statuses=st)
+    assert st == [R.RSH_E_NOMEM] and out[0][0] == R.RSH_E_NOMEM
+    assert out[1][0] == 0 and out[1][2].intact == 1 and bytes(out[1][2].md5) == fmi
