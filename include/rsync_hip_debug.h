@@ -9,7 +9,8 @@
  * scan_diag, scan_phase, scan_phase_guess, scan_segmented, scan_preprobe, scan_samples, scan_sample,
  * scan_spec_order, scan_early, scan_wait, scan_defer_steps, scan_defer_us, batch_spec, batch_spin_us,
  * batch_readahead, batch_prep_all, batch_chain, batch_chain_prefix, batch_chain_overlap, host_cores, file_tile,
- * file_tile_above, probe_long, segment_bytes, md5_width, chain_helpers, chain_map_bytes, batch_skip_rest.
+ * file_tile_above, probe_long, segment_bytes, md5_width, chain_helpers, chain_map_bytes, batch_skip_rest,
+ * fault_inject.
  */
 #ifndef RSYNC_HIP_DEBUG_H
 #define RSYNC_HIP_DEBUG_H
@@ -27,6 +28,10 @@ int rsh_debug_set_option(const char* name, int64_t value);
 int rsh_debug_get_option(const char* name, int64_t* value);
 /* Every option back to its compiled-in default. */
 void rsh_debug_reset_options(void);
+
+/* Which of the context's streams still have work queued or running (hipStreamQuery): bit 0 the context stream,
+ * bit 1 aux (the aligned speculation), bit 2 phase (the phase-shifted speculation).  After rsh_ctx_sync it is 0. */
+int rsh_debug_streams_busy(rsh_ctx* ctx, int32_t* mask);
 
 /* The clock the chip holds under the Generator's K1 (MI355X_MICROARCH.md, "DVFS give-back" item 6): reps launches of
  * a diagnostic instantiation of the production K1 body over the device bytes [d_data, d_data + n) (n a multiple of

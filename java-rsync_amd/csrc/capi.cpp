@@ -1178,7 +1178,7 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
 void rsh_ctx_destroy(rsh_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    for (hipStream_t st : {ctx->stream, ctx->aux})
+    for (hipStream_t st : {ctx->stream, ctx->aux, ctx->phase})  // nothing may still read or write its buffers
         if (st) (void)hipStreamSynchronize(st);
     delete ctx;
 }
@@ -1189,7 +1189,8 @@ int rsh_ctx_sync(rsh_ctx* ctx) {
     if (!ctx) return RSH_E_INVAL;
     RSH_HIP(hipSetDevice(ctx->device));
     RSH_HIP(hipStreamSynchronize(ctx->stream));
-    RSH_HIP(hipStreamSynchronize(ctx->aux));  // includes a cancelled speculation draining
+    RSH_HIP(hipStreamSynchronize(ctx->aux));    // includes a cancelled speculation draining
+    RSH_HIP(hipStreamSynchronize(ctx->phase));  // a stopped phase-shifted speculation and its downloads
     return RSH_OK;
 }
 
@@ -1506,6 +1507,19 @@ int rsh_debug_get_option(const char* name, int64_t* value) {
 
 void rsh_debug_reset_options(void) {
     for (int i = 0; i < rsh::OPT_COUNT; ++i) rsh::opt_table()[i].store(rsh::opt_info()[i].def, std::memory_order_relaxed);
+}
+
+int rsh_debug_streams_busy(rsh_ctx* ctx, int32_t* mask) {
+    if (!ctx || !mask) return RSH_E_INVAL;
+    RSH_HIP(hipSetDevice(ctx->device));
+    *mask = 0;
+    const hipStream_t st[3] = {ctx->stream, ctx->aux, ctx->phase};
+    for (int i = 0; i < 3; ++i) {
+        const hipError_t e = hipStreamQuery(st[i]);
+        if (e == hipErrorNotReady) *mask |= 1 << i;
+        else if (e != hipSuccess) RSH_HIP(e);
+    }
+    return RSH_OK;
 }
 
 int rsh_debug_k1_clock(rsh_ctx* ctx, const void* d_data, int64_t n, int32_t block_length, int32_t reps,

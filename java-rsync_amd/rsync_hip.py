@@ -143,7 +143,8 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_coun
            "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_receiver_combine",
            "rsh_receiver_combine_device", "rsh_receiver_combine_batch", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_block_sums_batch", "rsh_match_scan_batch", "rsh_file_md5_batch", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 # include/rsync_hip_debug.h (testing / diagnostics ABI)
-DEBUG_EXPORTS = ["rsh_debug_set_option", "rsh_debug_get_option", "rsh_debug_reset_options", "rsh_debug_k1_clock"]
+DEBUG_EXPORTS = ["rsh_debug_set_option", "rsh_debug_get_option", "rsh_debug_reset_options", "rsh_debug_k1_clock",
+                 "rsh_debug_streams_busy"]
 
 _LIB = None
 
@@ -235,6 +236,7 @@ def lib():
         "rsh_debug_get_option": ([ctypes.c_char_p, ctypes.POINTER(I64)], ctypes.c_int),
         "rsh_debug_reset_options": ([], None),
         "rsh_debug_k1_clock": ([P, P, I64, I32, I32, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+        "rsh_debug_streams_busy": ([P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -419,6 +421,12 @@ class Context:
     @property
     def handle(self):
         return self._p
+
+    def streams_busy(self):
+        """Bit mask of the context's streams with work still queued (rsh_debug_streams_busy)."""
+        m = ctypes.c_int32(-1)
+        _check(lib().rsh_debug_streams_busy(self._p, ctypes.byref(m)))
+        return m.value
 
     def sync(self):
         _check(lib().rsh_ctx_sync(self._p))

@@ -397,6 +397,9 @@ def test_config4_segment_vs_oracle(env, form, shard):
         sj[j].d_weak, sj[j].d_strong = bj[j].d_weak, bj[j].d_strong
         sj[j].ev, sj[j].ev_cap = evs[j].ctypes.data, cap
     assert R.lib().rsh_match_scan_batch_device(ctx.handle, sj, F, SEED_NP.ctypes.data, None) == 0
+    # nothing the scan enqueued outlives rsh_ctx_sync (stream, aux and phase all idle)
+    ctx.sync()
+    assert ctx.streams_busy() == 0
     for j, i in enumerate(files):
         n_ev, lit, mat, sha, fmd5 = g[form][i]
         rec = G.records_from_runs(evs[j][:sj[j].n_ev], B)
