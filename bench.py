@@ -242,17 +242,22 @@ def main():
         ns = source.numel()
         n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         st = R.ScanStats()
+        # The Generator K1's duration per timed step: HIP events the launch itself records on the context stream
+        # (rsh_debug_kernel_ms: hipExtLaunchKernelGGL start / stop, the kernel's dispatch timestamps).  Round 4 bracketed
+        # the call with torch events instead; their marker packets sat between the step's kernels (BENCH_DIAG=8: A/B).
+        torch_ev = bool(int(os.environ.get("BENCH_DIAG", "0")) & 8)
         gen_ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        gen_k1 = []
         spec_ms, dev_bytes = [], []
 
         def step(i=None):
-            if i is not None:
+            if i is not None and torch_ev:
                 gen_ev[i][0].record(stream)
             rc = L.rsh_block_sums_device(ctx.handle, ctypes.c_void_p(basis.data_ptr()), n, ctypes.byref(h),
                                          seed.ctypes.data, ctypes.c_void_p(d_weak.data_ptr()),
                                          ctypes.c_void_p(d_strong.data_ptr()))
             assert rc == 0, rc
-            if i is not None:
+            if i is not None and torch_ev:
                 gen_ev[i][1].record(stream)
             rc = L.rsh_match_scan_device(ctx.handle, ctypes.c_void_p(source.data_ptr()), ns, ctypes.byref(h),
                                          ctypes.c_void_p(d_weak.data_ptr()), ctypes.c_void_p(d_strong.data_ptr()),
@@ -263,6 +268,8 @@ def main():
             if i is not None:
                 spec_ms.append(st.spec_kernel_ms)
                 dev_bytes.append(st.device_bytes)
+                if not torch_ev:
+                    gen_k1.append(ctx.kernel_ms(0))
 
         # W warmup steps, and at least WARMUP_MIN_MS of them (untimed; the line reports how long they ran)
         tw = time.perf_counter()
@@ -273,9 +280,11 @@ def main():
             done += 1
         spec_ms.clear()
         dev_bytes.clear()
-        for s0, e0 in gen_ev:  # the timing events exist before the clock starts (torch creates them lazily)
-            s0.record(stream)
-            e0.record(stream)
+        gen_k1.clear()
+        if torch_ev:
+            for s0, e0 in gen_ev:  # the timing events exist before the clock starts (torch creates them lazily)
+                s0.record(stream)
+                e0.record(stream)
         if not diag & 2:  # A/B: 2 = no sync between the warmup and the timed steps (diagnostic only)
             ctx.sync()
             torch.cuda.synchronize()
@@ -303,7 +312,8 @@ def main():
         if gc_off:
             gc.enable()
         step_ms = [round((b - a) * 1e3, 3) for a, b in zip([t0] + t_step[:-1], t_step)]
-        gen_steps = [s0.elapsed_time(e0) for s0, e0 in gen_ev]
+        gen_steps = [s0.elapsed_time(e0) for s0, e0 in gen_ev] if torch_ev else list(gen_k1)
+        assert all(g > 0 for g in gen_steps), "the Generator K1 was not timed"
         gen_ms = float(np.mean(gen_steps))
         # bytes the timed region read: the Generator's basis pass + the source bytes the scan's device work
         # read (its speculation K1s when they ran to completion, probed ranges, digest windows)

@@ -10,7 +10,7 @@
  * scan_spec_order, scan_early, scan_wait, scan_defer_steps, scan_defer_us, batch_spec, batch_spin_us,
  * batch_readahead, batch_prep_all, batch_chain, batch_chain_prefix, batch_chain_overlap, host_cores, file_tile,
  * file_tile_above, probe_long, segment_bytes, md5_width, chain_helpers, chain_map_bytes, batch_skip_rest,
- * fault_inject.
+ * scan_spec_queue, fault_inject.
  */
 #ifndef RSYNC_HIP_DEBUG_H
 #define RSYNC_HIP_DEBUG_H
@@ -28,6 +28,11 @@ int rsh_debug_set_option(const char* name, int64_t value);
 int rsh_debug_get_option(const char* name, int64_t* value);
 /* Every option back to its compiled-in default. */
 void rsh_debug_reset_options(void);
+
+/* The duration of a K1 from its own dispatch timestamps (HIP events recorded by the launch, hipExtLaunchKernelGGL):
+ * which 0 = the last rsh_block_sums_device's K1 (the Generator), 1 = the last single-file scan's aligned speculation
+ * when it ran to completion.  *ms = -1 when that launch was not timed (a shape whose kernel takes no events). */
+int rsh_debug_kernel_ms(rsh_ctx* ctx, int32_t which, double* ms);
 
 /* Which of the context's streams still have work queued or running (hipStreamQuery): bit 0 the context stream,
  * bit 1 aux (the aligned speculation), bit 2 phase (the phase-shifted speculation).  After rsh_ctx_sync it is 0. */

@@ -55,10 +55,14 @@ class HipBackend : public rsh::ScanBackend {
   public:
     HipBackend(rsh_ctx* c, const uint8_t* d_src, int64_t n, rsh::ChunkTable& t, const int32_t* d_table_weak,
                const uint8_t seed[4])
-        : c_(c), x_(d_src), n_(n), t_(t), d_table_weak_(d_table_weak), B_(t.block_length), dl_(t.digest_length) {
+        : rs_(c->stream), c_(c), x_(d_src), n_(n), t_(t), d_table_weak_(d_table_weak), B_(t.block_length),
+          dl_(t.digest_length) {
         memcpy(seed_, seed, 4);
     }
     hipError_t err = hipSuccess;
+    // the queue of the round trips (and of the tiled scan's loads): the context stream, or aux when the
+    // speculation runs on the context stream (option scan_spec_queue, scan_device)
+    hipStream_t rs_;
     int64_t na = 0;
     const int32_t* aw = nullptr;  // pinned host copies of the aligned speculation
     const uint8_t* as = nullptr;
@@ -77,9 +81,20 @@ class HipBackend : public rsh::ScanBackend {
     int64_t aligned_count() override {  // the sums land after the flags (ev_spec after ev_flags)
         if (tiled) return aligned_end;
         if (head) return 0;
-        if (!sums_ready) sums_ready = hipEventQuery(c_->ev_spec) == hipSuccess;
+        if (!sums_ready) {
+            if (lazy_na >= 0) {  // scan_spec_queue: the first request downloads them (on rs_; the flags have landed)
+                ok(hipStreamWaitEvent(rs_, c_->ev_flags, 0));
+                ok(hipMemcpyAsync(c_->h_aw.p, c_->src_weak.p, (size_t)lazy_na * 4, hipMemcpyDeviceToHost, rs_));
+                if (dl_ > 0)
+                    ok(hipMemcpyAsync(c_->h_as.p, c_->src_strong.p, (size_t)lazy_na * dl_, hipMemcpyDeviceToHost, rs_));
+                ok(hipEventRecord(c_->ev_spec, rs_));
+                lazy_na = -1;
+            }
+            sums_ready = err == hipSuccess && hipEventQuery(c_->ev_spec) == hipSuccess;
+        }
         return sums_ready ? na : 0;
     }
+    int64_t lazy_na = -1;  // >= 0: the speculation's sums (this many windows) are still on the device
     int64_t flags_count() override { return tiled ? aligned_end : head ? 0 : na; }
     bool sums_ready = false;
     int64_t max_batch() override { return head ? 4 : 4096; }
@@ -122,20 +137,20 @@ class HipBackend : public rsh::ScanBackend {
         const int64_t C = t_.chunk_count, f1 = std::min(k1, C);
         ok(rsh::launch_block_sums(x_ + k0 * B_, std::min(n_, k1 * B_) - k0 * B_, (uint32_t)B_, (uint32_t)(k1 - k0),
                                   (uint32_t)dl_, seed_word(seed_), c_->src_weak.as<int32_t>() + k0,
-                                  c_->src_strong.as<uint8_t>() + k0 * dl_, c_->stream));
+                                  c_->src_strong.as<uint8_t>() + k0 * dl_, rs_));
         if (f1 > k0)
             ok(rsh::launch_chain_flags(c_->src_weak.as<int32_t>() + k0, c_->src_strong.as<uint8_t>() + k0 * dl_,
                                        d_table_weak_ + k0, reinterpret_cast<const uint8_t*>(d_table_strong) + k0 * dl_,
-                                       (uint32_t)(f1 - k0), (uint32_t)dl_, c_->flags.as<uint8_t>() + k0, c_->stream));
+                                       (uint32_t)(f1 - k0), (uint32_t)dl_, c_->flags.as<uint8_t>() + k0, rs_));
         ok(hipMemcpyAsync(c_->h_aw.as<int32_t>() + k0, c_->src_weak.as<int32_t>() + k0, (size_t)(k1 - k0) * 4,
-                          hipMemcpyDeviceToHost, c_->stream));
+                          hipMemcpyDeviceToHost, rs_));
         if (dl_ > 0)
             ok(hipMemcpyAsync(c_->h_as.as<uint8_t>() + k0 * dl_, c_->src_strong.as<uint8_t>() + k0 * dl_,
-                              (size_t)((k1 - k0) * dl_), hipMemcpyDeviceToHost, c_->stream));
+                              (size_t)((k1 - k0) * dl_), hipMemcpyDeviceToHost, rs_));
         if (f1 > k0)
             ok(hipMemcpyAsync(c_->h_fl.as<uint8_t>() + k0, c_->flags.as<uint8_t>() + k0, (size_t)(f1 - k0),
-                              hipMemcpyDeviceToHost, c_->stream));
-        ok(hipStreamSynchronize(c_->stream));
+                              hipMemcpyDeviceToHost, rs_));
+        ok(hipStreamSynchronize(rs_));
         bytes_read += std::min(n_, k1 * B_) - k0 * B_;
         aligned_end = k1;
     }
@@ -157,8 +172,8 @@ class HipBackend : public rsh::ScanBackend {
         rsh::ScanFile* F = file();
         if (err != hipSuccess) return;
         for (int64_t i = 0; i < count; ++i) hp[i] = rsh::GatherEnt{pos[i], 0, 0};
-        ok(rsh::launch_window_weak(F, hp, (uint32_t)count, ho, c_->stream));
-        ok(hipStreamSynchronize(c_->stream));
+        ok(rsh::launch_window_weak(F, hp, (uint32_t)count, ho, rs_));
+        ok(hipStreamSynchronize(rs_));
         memcpy(out, ho, (size_t)count * sizeof(int32_t));
     }
     void bytes_many(const int64_t* pos, int64_t count, uint8_t* out) override {
@@ -171,8 +186,8 @@ class HipBackend : public rsh::ScanBackend {
         rsh::ScanFile* F = file();
         if (err != hipSuccess) return;
         for (int64_t i = 0; i < count; ++i) hp[i] = rsh::GatherEnt{pos[i], 0, 0};
-        ok(rsh::launch_gather_bytes(F, hp, (uint32_t)count, ho, c_->stream));
-        ok(hipStreamSynchronize(c_->stream));
+        ok(rsh::launch_gather_bytes(F, hp, (uint32_t)count, ho, rs_));
+        ok(hipStreamSynchronize(rs_));
         memcpy(out, ho, (size_t)count);
     }
     void flush_gather(const int64_t* tpos, int64_t nt, int32_t* tv, const int64_t* bpos, int64_t nb,
@@ -191,9 +206,9 @@ class HipBackend : public rsh::ScanBackend {
         for (int64_t i = 0; i < nt; ++i) hp[i] = rsh::GatherEnt{tpos[i], 0, 0};
         for (int64_t i = 0; i < nb; ++i) hp[nt + i] = rsh::GatherEnt{bpos[i], 0, 0};
         uint8_t* hb = reinterpret_cast<uint8_t*>(ho + nt);
-        ok(rsh::launch_window_weak(F, hp, (uint32_t)nt, ho, c_->stream));
-        ok(rsh::launch_gather_bytes(F, hp + nt, (uint32_t)nb, hb, c_->stream));
-        ok(hipStreamSynchronize(c_->stream));
+        ok(rsh::launch_window_weak(F, hp, (uint32_t)nt, ho, rs_));
+        ok(rsh::launch_gather_bytes(F, hp + nt, (uint32_t)nb, hb, rs_));
+        ok(hipStreamSynchronize(rs_));
         memcpy(tv, ho, (size_t)nt * sizeof(int32_t));
         memcpy(bv, hb, (size_t)nb);
     }
@@ -225,8 +240,8 @@ class HipBackend : public rsh::ScanBackend {
         uint8_t* hw = pin<uint8_t>(c_->h_win, w);
         if (err != hipSuccess) return;
         bytes_read += w;
-        ok(rsh::launch_copy_to_host(x_ + p, w, hw, c_->stream));
-        ok(hipStreamSynchronize(c_->stream));
+        ok(rsh::launch_copy_to_host(x_ + p, w, hw, rs_));
+        ok(hipStreamSynchronize(rs_));
         rsh::HostMd5 h;
         h.update(hw, (size_t)w);
         h.update(seed_, 4);
@@ -258,9 +273,9 @@ class HipBackend : public rsh::ScanBackend {
             int32_t* hk = pin<int32_t>(c_->h_keys, (int64_t)keys->size() + 1);
             if (err != hipSuccess) return -1;
             if (!keys->empty()) memcpy(hk, keys->data(), keys->size() * sizeof(int32_t));
-            ok(rsh::launch_table_clear(c_->dslots.as<unsigned long long>(), ns, c_->stream));
+            ok(rsh::launch_table_clear(c_->dslots.as<unsigned long long>(), ns, rs_));
             ok(rsh::launch_table_insert(c_->dslots.as<unsigned long long>(), ns - 1, hk, (uint32_t)keys->size(),
-                                        c_->stream));
+                                        rs_));
             tab.slots = c_->dslots.as<unsigned long long>();
             tab.mask = ns - 1;
         }
@@ -287,7 +302,7 @@ class HipBackend : public rsh::ScanBackend {
         ok(c_->first.ensure(kFirstSlots * sizeof(rsh::ProbeOut)));
         if (err != hipSuccess) return -1;
         if (c_->first_used % kFirstSlots == 0)
-            ok(rsh::launch_probe_out_reset(c_->first.as<rsh::ProbeOut>(), (uint32_t)kFirstSlots, c_->stream));
+            ok(rsh::launch_probe_out_reset(c_->first.as<rsh::ProbeOut>(), (uint32_t)kFirstSlots, rs_));
         rsh::ProbeOut* d_first = c_->first.as<rsh::ProbeOut>() + c_->first_used++ % kFirstSlots;
         for (int64_t i = 0; i < count; ++i)
             hiv[i] = rsh::ProbeIv{iv[i].a, iv[i].b, iv[i].anchor, iv[i].e_lo & 0xFFFFu, iv[i].e_hi & 0xFFFFu, 0, 0};
@@ -316,7 +331,7 @@ class HipBackend : public rsh::ScanBackend {
                 rsh::GatherEnt* hp = pin<rsh::GatherEnt>(c_->h_pos, (int64_t)anchors_.size());
                 if (err != hipSuccess) return -1;
                 memcpy(hp, anchors_.data(), anchors_.size() * sizeof(rsh::GatherEnt));
-                ok(rsh::launch_window_weak(F, hp, (uint32_t)anchors_.size(), nullptr, c_->stream));
+                ok(rsh::launch_window_weak(F, hp, (uint32_t)anchors_.size(), nullptr, rs_));
             }
         }
         rsh::ProbeArgs A;
@@ -324,17 +339,17 @@ class HipBackend : public rsh::ScanBackend {
         A.ivs = hiv;
         A.tiles = ht;
         A.partials = c_->partials.as<int4>();
-        ok(rsh::launch_probe_first(A, (uint32_t)tiles_.size(), hpt, (uint32_t)ptiles_.size(), c_->stream));
-        ok(rsh::launch_probe_long(A, hsg, (uint32_t)segs_.size(), c_->stream));
+        ok(rsh::launch_probe_first(A, (uint32_t)tiles_.size(), hpt, (uint32_t)ptiles_.size(), rs_));
+        ok(rsh::launch_probe_long(A, hsg, (uint32_t)segs_.size(), rs_));
         // the resolver's next questions at a hit are T(p), the bucket of the key that hit and (usually) the
         // MD5 of the window at p: answer them in this round trip
         int32_t* req = hb + rsh::HIT_BUCKET_INTS;
         *req = 0;
-        ok(rsh::launch_hit_window(F, hiv, req, 1, t_.chunk_count, c_->stream));
-        ok(hipMemcpyAsync(hf, d_first, sizeof(rsh::ProbeOut), hipMemcpyDeviceToHost, c_->stream));
+        ok(rsh::launch_hit_window(F, hiv, req, 1, t_.chunk_count, rs_));
+        ok(hipMemcpyAsync(hf, d_first, sizeof(rsh::ProbeOut), hipMemcpyDeviceToHost, rs_));
         ok(hipMemcpyAsync(hb, c_->bucket.p, rsh::HIT_BUCKET_INTS * sizeof(int32_t), hipMemcpyDeviceToHost,
-                          c_->stream));
-        ok(hipStreamSynchronize(c_->stream));
+                          rs_));
+        ok(hipStreamSynchronize(rs_));
         if (count == 1) cache_.fill(iv[0], keys, *hf, n_ - B_);
         else cache_.fill_batch(iv, count, keys, *hf, n_ - B_);
         if (hf->first == ~0ull) return -1;
@@ -438,8 +453,10 @@ class HipBackend : public rsh::ScanBackend {
     // work on the context stream waits until its waves have left.
     void phase_stop() {
         if (ph_s0_ >= 0 && !ph_landed_ && hipEventQuery(c_->ev_phase[ph_set_]) == hipErrorNotReady) {
-            ok(hipStreamWriteValue32(c_->stream, c_->abort_word + rsh_ctx::kPhaseWord, (uint32_t)ph_gen_, 0));
-            ok(hipStreamWaitEvent(c_->stream, c_->ev_phase[ph_set_], 0));
+            ok(hipStreamWriteValue32(rs_, c_->abort_word + rsh_ctx::kPhaseWord, (uint32_t)ph_gen_, 0));
+            ok(hipStreamWaitEvent(rs_, c_->ev_phase[ph_set_], 0));
+            // the caller's later work on the context stream (it may rewrite the source) after the draining waves
+            if (rs_ != c_->stream) ok(hipStreamWaitEvent(c_->stream, c_->ev_phase[ph_set_], 0));
         }
         ph_s0_ = -1;
         ph_landed_ = false;
@@ -519,6 +536,18 @@ class HipBackend : public rsh::ScanBackend {
 }  // namespace
 
 namespace rshi {
+// Under scan_spec_queue the aligned speculation's sums come down on aux after the scan has moved on (or returned):
+// a K1 that rewrites src_weak / src_strong on the context stream first waits for that download, when it is still
+// running (a host-side query: no wait packet in the common case).
+hipError_t spec_buffers_free(rsh_ctx* c) {
+    if (!c->spec_dl_pending) return hipSuccess;
+    c->spec_dl_pending = false;
+    const hipError_t q = hipEventQuery(c->ev_rs_tail);
+    if (q == hipSuccess) return hipSuccess;
+    if (q != hipErrorNotReady) return q;
+    return hipStreamWaitEvent(c->stream, c->ev_rs_tail, 0);
+}
+
 // The device-resident Sender scan (everything but the whole-file MD5).  h validated by the caller;
 // n > 0, block_length > 0.  host_weak/host_strong may be null (then copied back from the device).
 //
@@ -576,7 +605,15 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     const size_t lead_ents_at = ((size_t)(nsamp + 1) * 4 + 63) & ~(size_t)63;
     RSH_HIP(c->h_lead.ensure(lead_ents_at + (size_t)(nsamp + 1) * sizeof(rsh::GatherEnt) + sizeof(rsh::ScanFile)));
 
+    // Queues (option scan_spec_queue, default 1).  1: the speculation runs on the context stream itself, queued
+    // right behind whatever produced the inputs there (the Generator's K1 in the bench: no cross-queue hand-off
+    // and no sample kernels between the two K1s), and the round trips -- window 0, the samples, the table, the
+    // resolver -- on aux beside it.  0: round 4's layout, the speculation on aux after the sample kernels.
+    const bool on_ctx = rsh::opt(rsh::OPT_SCAN_SPEC_QUEUE) != 0;
+    hipStream_t ss = on_ctx ? c->stream : c->aux;  // the speculation
+    hipStream_t rs = on_ctx ? c->aux : c->stream;  // the round trips
     RSH_HIP(hipEventRecord(c->ev_in, c->stream));  // whatever produced the inputs on the caller's stream
+    if (on_ctx) RSH_HIP(hipStreamWaitEvent(rs, c->ev_in, 0));
     // (aux) the aligned speculation: the source's own block sums with the basis header's B and dl,
     // the chain flags, and their download.  It is a bet on long runs of aligned matches; in head mode it
     // is launched only once the resolver has taken scan_defer_steps steps or scan_defer_us without finishing
@@ -592,21 +629,39 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // beside them.
     const bool spec_after_prep = rsh::opt(rsh::OPT_SCAN_SPEC_ORDER) != 0;
     bool prep_recorded = false;
+    bool k1_timed = false;  // the speculation's K1 recorded ev_k1a / ev_k1b with its dispatch (no marker packets)
+    int64_t spec_sums_na = -1;  // scan_spec_queue: windows of the launched speculation whose sums are still on the device
     auto launch_spec = [&]() -> int {
         const int64_t sn = std::min<int64_t>(n, spec_na * B);  // bytes: whole windows, or to the end
         const int64_t snf = std::min<int64_t>(spec_na, C);
-        RSH_HIP(hipStreamWaitEvent(c->aux, spec_after_prep && prep_recorded ? c->ev_prep : c->ev_in, 0));
-        RSH_HIP(hipEventRecord(c->ev_k1a, c->aux));
-        RSH_HIP(rsh::launch_block_sums(d_src, sn, (uint32_t)B, (uint32_t)spec_na, (uint32_t)dl, seed_word(seed),
-                                       c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), c->aux,
-                                       (diag & 2) ? nullptr : c->abort_word, gen));
-        RSH_HIP(hipEventRecord(c->ev_k1b, c->aux));
+        if (on_ctx) {
+            RSH_HIP(spec_buffers_free(c));  // the previous scan's downloads of these buffers (aux) are done
+            rsh::k1_timing_next(c->ev_k1a, c->ev_k1b);
+        } else {
+            RSH_HIP(hipStreamWaitEvent(c->aux, spec_after_prep && prep_recorded ? c->ev_prep : c->ev_in, 0));
+            RSH_HIP(hipEventRecord(c->ev_k1a, c->aux));
+        }
+        const hipError_t e = rsh::launch_block_sums(d_src, sn, (uint32_t)B, (uint32_t)spec_na, (uint32_t)dl,
+                                                    seed_word(seed), c->src_weak.as<int32_t>(),
+                                                    c->src_strong.as<uint8_t>(), ss,
+                                                    (diag & 2) ? nullptr : c->abort_word, gen);
+        k1_timed = on_ctx && rsh::k1_timing_taken();
+        if (on_ctx) rsh::k1_timing_next(nullptr, nullptr);
+        RSH_HIP(e);
+        if (!on_ctx) RSH_HIP(hipEventRecord(c->ev_k1b, c->aux));
         RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
-                                        (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(), c->aux));
+                                        (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(), ss));
         // the flags first (a run of matches needs nothing else), then the sums (aligned lookups off the run).
         // (Written by the flags kernel straight into pinned host memory instead: no difference, r2_ab2.)
-        if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, c->aux));
-        RSH_HIP(hipEventRecord(c->ev_flags, c->aux));
+        if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, ss));
+        RSH_HIP(hipEventRecord(c->ev_flags, ss));
+        if (on_ctx) {
+            // the sums come down on aux once the resolver first asks for them (HipBackend::aligned_count): on the
+            // context stream they would hold up the caller's next launch (the next Generator K1), and an identical
+            // file resolves from the flags alone
+            spec_sums_na = spec_na;
+            return RSH_OK;
+        }
         RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)spec_na * 4, hipMemcpyDeviceToHost, c->aux));
         if (dl > 0)
             RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)spec_na * dl, hipMemcpyDeviceToHost, c->aux));
@@ -624,7 +679,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // at position 0, and its MD5 (one serial chain, ~0.13 ms for 128 KiB) then overlaps the first probe
     const int64_t w0 = std::min<int64_t>(B, n);
     RSH_HIP(c->h_win0.ensure((size_t)w0 + 16));
-    RSH_HIP(rsh::launch_copy_to_host(d_src, w0, c->h_win0.as<uint8_t>(), c->stream));
+    RSH_HIP(rsh::launch_copy_to_host(d_src, w0, c->h_win0.as<uint8_t>(), rs));
     // (stream) T(kB) of the first nlead aligned windows: when all of them carry chunk k's weak sum the
     // source very likely continues as an aligned run of matches (an unchanged or appended file), and the
     // speculation is launched at once instead of after a few head-mode steps
@@ -637,26 +692,26 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         lf->n = n;
         lf->B = (uint32_t)B;
         for (int64_t i = 0; i < nsamp; ++i) ents[i] = rsh::GatherEnt{samp[(size_t)i] * B, 0, 0};
-        RSH_HIP(rsh::launch_window_weak(lf, ents, (uint32_t)nsamp, lead_w, c->stream));
+        RSH_HIP(rsh::launch_window_weak(lf, ents, (uint32_t)nsamp, lead_w, rs));
     }
     if (spec_after_prep) {
-        RSH_HIP(hipEventRecord(c->ev_prep, c->stream));
+        RSH_HIP(hipEventRecord(c->ev_prep, rs));
         prep_recorded = true;
     }
     // (stream) the received table to the host (the lead check and the resolver), after the sample work: the
     // speculation waits for the samples only, and these copies and the hash build below run beside it
     if (download) {
         if (C > 0) {
-            RSH_HIP(hipMemcpyAsync(c->h_weak.p, d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, c->stream));
-            if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_strong.p, d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, c->stream));
+            RSH_HIP(hipMemcpyAsync(c->h_weak.p, d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, rs));
+            if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_strong.p, d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, rs));
         }
-        RSH_HIP(hipEventRecord(c->ev_tab, c->stream));
+        RSH_HIP(hipEventRecord(c->ev_tab, rs));
         host_weak = c->h_weak.as<int32_t>();
         host_strong = c->h_strong.as<uint8_t>();
     }
     // (stream) the device probe hash
-    RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, c->stream));
-    RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, c->stream));
+    RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, rs));
+    RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, rs));
 
     // Launch-then-confirm: when one K1 round covers every window (na <= kRoundWindows), the speculation that
     // the lead decides on below is launched now, before the host knows the table, so it starts the moment the
@@ -685,7 +740,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     }
     {
         CallTrace tr("hash_sync", ns);
-        RSH_HIP(hipStreamSynchronize(c->stream));
+        RSH_HIP(hipStreamSynchronize(rs));
     }
     uint8_t md5_0[16];
     std::thread md5_0_thread([&] {
@@ -733,7 +788,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             }
         }
         if (spec_tentative && (!eager || cover < na)) {  // stop the tentative launch; later ones take a new generation
-            RSH_HIP(hipStreamWriteValue32(c->stream, c->abort_word, (uint32_t)gen, 0));
+            RSH_HIP(hipStreamWriteValue32(rs, c->abort_word, (uint32_t)gen, 0));
             gen = ++c->gen;
             spec_launched = spec_tentative = false;
             tentative_stopped = true;
@@ -754,6 +809,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         }
     }
     HipBackend be(c, d_src, n, table, d_weak, seed);
+    be.rs_ = rs;
     be.table.slots = c->slots.as<unsigned long long>();
     be.table.mask = ns - 1;
     be.aw = c->h_aw.as<int32_t>();
@@ -785,7 +841,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         for (int64_t i = 0; i < pe_cnt; ++i) pents[i] = rsh::GatherEnt{(pe_lo + i) * B, 0, 0};
         auto* lf = reinterpret_cast<rsh::ScanFile*>(reinterpret_cast<rsh::GatherEnt*>(c->h_lead.as<uint8_t>() + lead_ents_at) +
                                                     nsamp + 1);
-        RSH_HIP(rsh::launch_window_weak(lf, pents, (uint32_t)pe_cnt, pe_w, c->stream));
+        RSH_HIP(rsh::launch_window_weak(lf, pents, (uint32_t)pe_cnt, pe_w, rs));
         be.bytes_read += pe_cnt * B;
     }
     if (guess_on && run_miss > 0 && (spec_launched || defer_prefix) && HipBackend::phase_on() && C >= 4) {
@@ -829,7 +885,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                 hipSuccess) {
             std::vector<int32_t> w((size_t)cnt);
             if (pe_w && k_lo == pe_lo && cnt == pe_cnt) {  // launched with the guess (above); landed with its probes
-                RSH_HIP(hipStreamSynchronize(c->stream));
+                RSH_HIP(hipStreamSynchronize(rs));
                 memcpy(w.data(), pe_w, (size_t)cnt * 4);
             } else {
                 std::vector<int64_t> pos((size_t)cnt);
@@ -879,34 +935,36 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                 if (ntail <= 256 && bytes <= seg_bytes) {
                     spec_na = P;
                     const int64_t snf = std::min<int64_t>(P, C);
-                    RSH_HIP(hipMemcpyAsync(c->segs.p, c->h_segs.p, bytes, hipMemcpyHostToDevice, c->aux));
-                    RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_in, 0));
-                    RSH_HIP(hipStreamWaitEvent(c->aux, c->ev_phase[pset], 0));
-                    RSH_HIP(hipEventRecord(c->ev_k1a, c->aux));
-                    RSH_HIP(hipEventRecord(c->ev_pha[pset], c->aux));
+                    RSH_HIP(hipMemcpyAsync(c->segs.p, c->h_segs.p, bytes, hipMemcpyHostToDevice, ss));
+                    if (on_ctx) RSH_HIP(spec_buffers_free(c));
+                    else RSH_HIP(hipStreamWaitEvent(ss, c->ev_in, 0));
+                    RSH_HIP(hipStreamWaitEvent(ss, c->ev_phase[pset], 0));
+                    RSH_HIP(hipEventRecord(c->ev_k1a, ss));
+                    RSH_HIP(hipEventRecord(c->ev_pha[pset], ss));
                     RSH_HIP(rsh::launch_block_sums_segments(c->segs.as<rsh::K1Seg>(), nseg,
                                                             reinterpret_cast<const rsh::K1Tail*>(
                                                                 c->segs.as<uint8_t>() + nseg * sizeof(rsh::K1Seg)),
                                                             ntail, nfull, (uint32_t)B, (uint32_t)dl, seed_word(seed),
-                                                            c->aux));
-                    RSH_HIP(hipEventRecord(c->ev_k1b, c->aux));
-                    RSH_HIP(hipEventRecord(c->ev_phb[pset], c->aux));
+                                                            ss));
+                    RSH_HIP(hipEventRecord(c->ev_k1b, ss));
+                    RSH_HIP(hipEventRecord(c->ev_phb[pset], ss));
                     RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak,
                                                     d_strong, (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(),
-                                                    c->aux));
-                    if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, c->aux));
-                    RSH_HIP(hipEventRecord(c->ev_flags, c->aux));
-                    RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)P * 4, hipMemcpyDeviceToHost, c->aux));
+                                                    ss));
+                    if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, ss));
+                    RSH_HIP(hipEventRecord(c->ev_flags, ss));
+                    RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)P * 4, hipMemcpyDeviceToHost, ss));
                     if (dl > 0)
-                        RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)P * dl, hipMemcpyDeviceToHost, c->aux));
-                    RSH_HIP(hipEventRecord(c->ev_spec, c->aux));
+                        RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)P * dl, hipMemcpyDeviceToHost, ss));
+                    RSH_HIP(hipEventRecord(c->ev_spec, ss));
                     RSH_HIP(hipMemcpyAsync(c->h_pw[pset].p, c->ph_weak[pset].p, (size_t)Q * 4, hipMemcpyDeviceToHost,
-                                           c->aux));
+                                           ss));
                     if (dl > 0)
                         RSH_HIP(hipMemcpyAsync(c->h_ps[pset].p, c->ph_strong[pset].p, (size_t)Q * dl,
-                                               hipMemcpyDeviceToHost, c->aux));
-                    RSH_HIP(hipEventRecord(c->ev_phase[pset], c->aux));
+                                               hipMemcpyDeviceToHost, ss));
+                    RSH_HIP(hipEventRecord(c->ev_phase[pset], ss));
                     c->ph_set = pset;
+                    k1_timed = true;  // (the event records around it)
                     be.phase_adopt(s0, Q, gph, pset);
                     res->stats.phase_guesses++;
                     spec_launched = seg_launched = true;
@@ -943,11 +1001,11 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     }
     be.na = spec_na;
     be.partial = spec_na < na;
-    rsh::ResolveState rs;
+    rsh::ResolveState rstate;
     bool landed = false;
     int spec_rc = RSH_OK;
     const auto t_head = std::chrono::steady_clock::now();
-    const bool done = rsh::resolve_run(n, table, be, &rs, res, [&] {
+    const bool done = rsh::resolve_run(n, table, be, &rstate, res, [&] {
         if (be.err != hipSuccess || !be.head) return true;
         CallTrace tr("ev_query", res->stats.head_steps);
         if (!spec_launched) {
@@ -985,14 +1043,14 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         // the scan ended in head mode before the speculation was needed (3: a tentative launch was stopped)
         if (res->stats.speculation_aborted != 3) res->stats.speculation_aborted = 2;
         // the stopped launch's waves leave within two stages; later work on this context starts after them
-        if (tentative_stopped) RSH_HIP(hipStreamWaitEvent(c->stream, c->ev_spec, 0));
+        if (tentative_stopped) RSH_HIP(hipStreamWaitEvent(rs, on_ctx ? c->ev_flags : c->ev_spec, 0));
         res->stats.device_ms += ms_since(t0);
     } else if (done && !landed && hipEventQuery(c->ev_flags) == hipErrorNotReady) {
-        RSH_HIP(hipStreamWriteValue32(c->stream, c->abort_word, (uint32_t)gen, 0));  // the rest is dead work
+        RSH_HIP(hipStreamWriteValue32(rs, c->abort_word, (uint32_t)gen, 0));  // the rest is dead work
         // Later work on this context starts only once the stopped launch has left the CUs: K1 fills every
         // wave slot of the chip exactly once (2 per SIMD at 16 GiB, B = 128 KiB), and a launch that finds
         // slots still held by the draining waves (or their LDS fragmented) runs a second round of waves.
-        RSH_HIP(hipStreamWaitEvent(c->stream, c->ev_spec, 0));
+        if (!on_ctx) RSH_HIP(hipStreamWaitEvent(c->stream, c->ev_spec, 0));  // (on_ctx: it runs on the context stream)
         res->stats.speculation_aborted = 1;
         res->stats.device_ms += ms_since(t0);
     } else {
@@ -1002,19 +1060,25 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         spec_read = true;
         if (!done) {
             be.head = false;
+            if (on_ctx && spec_sums_na >= 0) be.lazy_na = spec_sums_na;
             if (be.partial) {  // the prefix's anchors from the speculation, the rest on demand
-                RSH_HIP(hipMemcpyAsync(c->haw.p, c->src_weak.p, (size_t)spec_na * 4, hipMemcpyDeviceToDevice, c->stream));
+                RSH_HIP(hipMemcpyAsync(c->haw.p, c->src_weak.p, (size_t)spec_na * 4, hipMemcpyDeviceToDevice, rs));
                 std::fill(be.haw_ready.begin(), be.haw_ready.begin() + spec_na, (uint8_t)1);
             }
             CallTrace tr("resolve_end", res->stats.events);
-            rsh::resolve_run(n, table, be, &rs, res, nullptr);
+            rsh::resolve_run(n, table, be, &rstate, res, nullptr);
         }
     }
     be.phase_stop();
     if (be.err != hipSuccess) return RSH_E_DEVICE;
+    if (on_ctx) {  // the next K1 over src_weak / src_strong on the context stream waits for what aux still does
+        RSH_HIP(hipEventRecord(c->ev_rs_tail, rs));
+        c->spec_dl_pending = true;
+    }
     res->stats.table_ms += table.sort_ms;  // 0 when the scan never needed the sorted table
     res->stats.device_bytes += be.bytes_read + (spec_read ? std::min<int64_t>(n, spec_na * B) : 0);
-    if (spec_read) {
+    c->spec_timed = spec_read && (!on_ctx || k1_timed);
+    if (c->spec_timed) {
         float k1ms = 0.f;
         if (hipEventElapsedTime(&k1ms, c->ev_k1a, c->ev_k1b) == hipSuccess) res->stats.spec_kernel_ms = k1ms;
     }
@@ -1056,6 +1120,7 @@ int scan_tiled(rsh_ctx* c, const std::function<hipError_t(uint8_t*, int64_t, int
         RSH_HIP(c->h_pw[i].ensure((size_t)na * 4));
         RSH_HIP(c->h_ps[i].ensure((size_t)na * dl + 1));
     }
+    RSH_HIP(spec_buffers_free(c));  // its tiles' K1s rewrite src_weak / src_strong on the context stream
     RSH_HIP(hipEventRecord(c->ev_in, c->stream));
     RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, c->stream));
     RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, c->stream));
@@ -1162,6 +1227,8 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
         hipEventCreateWithFlags(&c->ev_flags, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_prep, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev_k1a) != hipSuccess || hipEventCreate(&c->ev_k1b) != hipSuccess ||
+        hipEventCreate(&c->ev_gen_a) != hipSuccess || hipEventCreate(&c->ev_gen_b) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_rs_tail, hipEventDisableTiming) != hipSuccess ||
         hipEventCreate(&c->ev_pha[0]) != hipSuccess || hipEventCreate(&c->ev_phb[0]) != hipSuccess ||
         hipEventCreate(&c->ev_pha[1]) != hipSuccess || hipEventCreate(&c->ev_phb[1]) != hipSuccess ||
         hipExtMallocWithFlags(reinterpret_cast<void**>(&c->abort_word), 256, hipDeviceMallocUncached) != hipSuccess ||
@@ -1247,9 +1314,15 @@ int rsh_block_sums_device(rsh_ctx* ctx, const void* d_data, int64_t n, const rsh
     if (h->chunk_count == 0) return RSH_OK;
     if (!d_data || !d_weak || (!d_strong && h->digest_length > 0)) return RSH_E_INVAL;
     RSH_HIP(hipSetDevice(ctx->device));
-    RSH_HIP(rsh::launch_block_sums(static_cast<const uint8_t*>(d_data), n, (uint32_t)h->block_length,
-                                   (uint32_t)h->chunk_count, (uint32_t)h->digest_length, seed_word(seed),
-                                   static_cast<int32_t*>(d_weak), static_cast<uint8_t*>(d_strong), ctx->stream));
+    // the K1's own start / stop timestamps (rsh_debug_kernel_ms; no marker packets around it)
+    rsh::k1_timing_next(ctx->ev_gen_a, ctx->ev_gen_b);
+    const hipError_t e = rsh::launch_block_sums(static_cast<const uint8_t*>(d_data), n, (uint32_t)h->block_length,
+                                                (uint32_t)h->chunk_count, (uint32_t)h->digest_length, seed_word(seed),
+                                                static_cast<int32_t*>(d_weak), static_cast<uint8_t*>(d_strong),
+                                                ctx->stream);
+    ctx->gen_timed = rsh::k1_timing_taken();
+    rsh::k1_timing_next(nullptr, nullptr);
+    RSH_HIP(e);
     return RSH_OK;
 }
 
@@ -1507,6 +1580,19 @@ int rsh_debug_get_option(const char* name, int64_t* value) {
 
 void rsh_debug_reset_options(void) {
     for (int i = 0; i < rsh::OPT_COUNT; ++i) rsh::opt_table()[i].store(rsh::opt_info()[i].def, std::memory_order_relaxed);
+}
+
+int rsh_debug_kernel_ms(rsh_ctx* ctx, int32_t which, double* ms) {
+    if (!ctx || !ms || which < 0 || which > 1) return RSH_E_INVAL;
+    *ms = -1.0;
+    const bool timed = which == 0 ? ctx->gen_timed : ctx->spec_timed;
+    if (!timed) return RSH_OK;
+    RSH_HIP(hipSetDevice(ctx->device));
+    RSH_HIP(hipEventSynchronize(which == 0 ? ctx->ev_gen_b : ctx->ev_k1b));
+    float f = 0.f;
+    RSH_HIP(hipEventElapsedTime(&f, which == 0 ? ctx->ev_gen_a : ctx->ev_k1a, which == 0 ? ctx->ev_gen_b : ctx->ev_k1b));
+    *ms = f;
+    return RSH_OK;
 }
 
 int rsh_debug_streams_busy(rsh_ctx* ctx, int32_t* mask) {

@@ -128,6 +128,10 @@ struct rsh_ctx {
     hipEvent_t ev_prep = nullptr;   // the scan's table and sample work on the context stream (A/B ordering)
     hipEvent_t ev_flags = nullptr;  // batched speculation: its chain flags are on the host (before its sums)
     hipEvent_t ev_k1a = nullptr, ev_k1b = nullptr;  // timing: the aligned speculation's K1 (stats)
+    hipEvent_t ev_gen_a = nullptr, ev_gen_b = nullptr;  // timing: rsh_block_sums_device's K1 (rsh_debug_kernel_ms)
+    bool gen_timed = false;                             // ... recorded by the last rsh_block_sums_device
+    bool spec_timed = false;                            // ev_k1a / ev_k1b belong to the last scan's speculation
+    hipEvent_t ev_rs_tail = nullptr;  // scan_spec_queue: the end of a scan's work on aux (see spec_buffers_free)
     hipEvent_t ev_pha[2] = {nullptr, nullptr}, ev_phb[2] = {nullptr, nullptr};  // timing: set i's phase K1 (stats)
     int ph_set = 0;  // the buffer set of the latest phase launch
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl;
@@ -150,6 +154,7 @@ struct rsh_ctx {
     int* abort_word = nullptr;
     static constexpr int kPhaseWord = 16;
     int gen = 0;
+    bool spec_dl_pending = false;  // the last speculation's sums download (aux) may still read src_weak / src_strong
     std::vector<rsh_event> last_ev;  // kept when the caller's event buffer was too small
     std::atomic<bool> busy{false};   // the staging buffers and last_ev serve one call at a time
     rsh::BatchState* batch = nullptr;  // buffers of the batched (multi-file) entry points, on first use
@@ -172,8 +177,8 @@ struct rsh_ctx {
             if (e) (void)hipEventDestroy(e);
         if (ev_flags) (void)hipEventDestroy(ev_flags);
         if (ev_prep) (void)hipEventDestroy(ev_prep);
-        if (ev_k1a) (void)hipEventDestroy(ev_k1a);
-        if (ev_k1b) (void)hipEventDestroy(ev_k1b);
+        for (hipEvent_t e : {ev_k1a, ev_k1b, ev_gen_a, ev_gen_b, ev_rs_tail})
+            if (e) (void)hipEventDestroy(e);
         if (aux) (void)hipStreamDestroy(aux);
         if (phase) (void)hipStreamDestroy(phase);
         if (stream) (void)hipStreamDestroy(stream);

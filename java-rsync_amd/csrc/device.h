@@ -17,6 +17,12 @@ namespace rsh {
 hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks, uint32_t dl,
                              uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s,
                              const int* abort_flag = nullptr, int abort_gen = 0);
+// Timing of the next K1 launch_block_sums makes on this thread: its dispatch records start / stop in these events
+// (hipExtLaunchKernelGGL: the kernel's own timestamps, no marker packets in the stream and so no bubble before or
+// after the kernel).  k1_timing_taken() says whether that launch took them (the pipelined and the shift kernels do;
+// the rare per-lane and coalesced shapes do not, and the events then stay unrecorded).
+void k1_timing_next(hipEvent_t start, hipEvent_t stop);
+bool k1_timing_taken();
 
 #ifdef RSH_KBENCH
 // kbench only (tools/kbench.cpp, built with -DRSH_KBENCH): the K1 instantiations measured against the production

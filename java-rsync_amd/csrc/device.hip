@@ -6,6 +6,7 @@
 // No GEMM reshaping anywhere else.  Layout in HBM: the file is one flat byte array (caller's
 // buffer, 256-B aligned from hipMalloc); per-chunk outputs are struct-of-arrays (weak int32[C],
 // strong uint8[C*dl]).  See DESIGN.md for the roofline of each kernel.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "device.h"
@@ -1261,6 +1262,30 @@ static bool batch_pin() { return pin_all(); }
 static bool pin_all() { return true; }
 #endif
 
+// K1 timing (k1_timing_next): the events the next production K1 launch on this thread records with its dispatch.
+namespace {
+thread_local hipEvent_t t_k1_start = nullptr, t_k1_stop = nullptr;
+thread_local bool t_k1_taken = false;
+}  // namespace
+void k1_timing_next(hipEvent_t start, hipEvent_t stop) {
+    t_k1_start = start;
+    t_k1_stop = stop;
+    t_k1_taken = false;
+}
+bool k1_timing_taken() { return t_k1_taken; }
+// A production K1 launch: with the pending timing events through hipExtLaunchKernelGGL (they are consumed), else
+// a plain launch.
+template <typename... KArgs, typename... Args>
+static void k1_launch(void (*kernel)(KArgs...), dim3 grid, dim3 block, uint32_t lds, hipStream_t s, Args... args) {
+    if (t_k1_start) {
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, s, t_k1_start, t_k1_stop, 0u, static_cast<KArgs>(args)...);
+        t_k1_start = t_k1_stop = nullptr;
+        t_k1_taken = true;
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, static_cast<KArgs>(args)...);
+    }
+}
+
 #ifndef RSH_KBENCH
 static
 #endif
@@ -1322,20 +1347,20 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                 const size_t lb = gather ? 2 * 64 * 9 * sizeof(uint4) : 64 * 17 * sizeof(uint4);
                 switch ((a >> 2) & 3) {
                     case 0:
-                        hipLaunchKernelGGL((block_sums_shift_kernel<0>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
-                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
+                        k1_launch(block_sums_shift_kernel<0>, grid, dim3(64), (uint32_t)lb, s, d_data, n, a, B, nchunks,
+                                  mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
                         break;
                     case 1:
-                        hipLaunchKernelGGL((block_sums_shift_kernel<1>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
-                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
+                        k1_launch(block_sums_shift_kernel<1>, grid, dim3(64), (uint32_t)lb, s, d_data, n, a, B, nchunks,
+                                  mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
                         break;
                     case 2:
-                        hipLaunchKernelGGL((block_sums_shift_kernel<2>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
-                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
+                        k1_launch(block_sums_shift_kernel<2>, grid, dim3(64), (uint32_t)lb, s, d_data, n, a, B, nchunks,
+                                  mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
                         break;
                     default:
-                        hipLaunchKernelGGL((block_sums_shift_kernel<3>), grid, dim3(64), lb, s, d_data, n, a, B, nchunks,
-                                           mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
+                        k1_launch(block_sums_shift_kernel<3>, grid, dim3(64), (uint32_t)lb, s, d_data, n, a, B, nchunks,
+                                  mw, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, tf);
                 }
                 return hipGetLastError();
             }
@@ -1423,14 +1448,14 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                         const uint32_t gwaves = (tail_full + 63) / 64 + (tail_short + 63) / 64;
                         if (tail_full > 0 && tail_gather_on() &&
                             (gwaves == tail_waves || waves + gwaves <= 2 * 4 * kCUs)) {
-                            hipLaunchKernelGGL((block_sums_pipe_tailg_kernel<true>), dim3(waves + gwaves), dim3(64),
-                                               2 * wave_lds, s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag,
-                                               abort_gen, n, nchunks, waves, tail_full);
+                            k1_launch(block_sums_pipe_tailg_kernel<true>, dim3(waves + gwaves), dim3(64),
+                                      (uint32_t)(2 * wave_lds), s, d_data, B, dl, seed_word, d_weak, d_strong,
+                                      abort_flag, abort_gen, n, nchunks, waves, tail_full);
                             return hipGetLastError();
                         }
-                        hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true>), dim3(waves + tail_waves), dim3(64),
-                                           2 * wave_lds, s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag,
-                                           abort_gen, nullptr, n, nchunks, waves);
+                        k1_launch(block_sums_pipe_kernel<8, true, true>, dim3(waves + tail_waves), dim3(64),
+                                  (uint32_t)(2 * wave_lds), s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag,
+                                  abort_gen, nullptr, n, nchunks, waves);
                         return hipGetLastError();
                     }
 #ifdef RSH_KBENCH

@@ -48,6 +48,7 @@ enum Opt : int {
     OPT_CHAIN_HELPERS,     // phase-0 walk: extra workgroups mapping searching files' prefixes (-1: CUs - files; 0: no map)
     OPT_CHAIN_MAP_BYTES,   // ... the map's HBM budget (bytes; above it the walks search tile by tile)
     OPT_BATCH_SKIP_REST,   // 1: the rest of a two-phase speculation only if some phase-0 walk reached the prefix's end
+    OPT_SCAN_SPEC_QUEUE,   // 1: the single-file speculation on the context stream, round trips on aux; 0: round 4's layout
     OPT_FAULT_INJECT,      // tests only: bit 0 a segment / Receiver pass's HBM allocation fails, bit 1 a segment's copies fail
     OPT_COUNT
 };
@@ -68,7 +69,7 @@ inline const OptInfo* opt_info() {
         {"host_cores", 0},         {"file_tile", 4LL << 30}, {"file_tile_above", 32LL << 30},
         {"probe_long", 1},         {"segment_bytes", 16LL << 30}, {"md5_width", 0},
         {"chain_helpers", -1},     {"chain_map_bytes", 1LL << 30}, {"batch_skip_rest", 1},
-        {"fault_inject", 0},
+        {"scan_spec_queue", 1},    {"fault_inject", 0},
     };
     return t;
 }

@@ -144,7 +144,7 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_coun
            "rsh_receiver_combine_device", "rsh_receiver_combine_batch", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_block_sums_batch", "rsh_match_scan_batch", "rsh_file_md5_batch", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 # include/rsync_hip_debug.h (testing / diagnostics ABI)
 DEBUG_EXPORTS = ["rsh_debug_set_option", "rsh_debug_get_option", "rsh_debug_reset_options", "rsh_debug_k1_clock",
-                 "rsh_debug_streams_busy"]
+                 "rsh_debug_streams_busy", "rsh_debug_kernel_ms"]
 
 _LIB = None
 
@@ -237,6 +237,7 @@ def lib():
         "rsh_debug_reset_options": ([], None),
         "rsh_debug_k1_clock": ([P, P, I64, I32, I32, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "rsh_debug_streams_busy": ([P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+        "rsh_debug_kernel_ms": ([P, I32, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -421,6 +422,12 @@ class Context:
     @property
     def handle(self):
         return self._p
+
+    def kernel_ms(self, which):
+        """The last Generator (0) or speculation (1) K1's duration from its own dispatch events (-1: not timed)."""
+        ms = ctypes.c_double(-1.0)
+        _check(lib().rsh_debug_kernel_ms(self._p, which, ctypes.byref(ms)))
+        return ms.value
 
     def streams_busy(self):
         """Bit mask of the context's streams with work still queued (rsh_debug_streams_busy)."""
