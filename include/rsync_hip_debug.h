@@ -10,7 +10,7 @@
  * scan_spec_order, scan_early, scan_wait, scan_defer_steps, scan_defer_us, batch_spec, batch_spin_us,
  * batch_readahead, batch_prep_all, batch_chain, batch_chain_prefix, batch_chain_overlap, host_cores, file_tile,
  * file_tile_above, probe_long, segment_bytes, md5_width, chain_helpers, chain_map_bytes, batch_skip_rest,
- * scan_spec_queue, fault_inject.
+ * scan_spec_queue, scan_flags_host, time_spec, time_gen, fault_inject.
  */
 #ifndef RSYNC_HIP_DEBUG_H
 #define RSYNC_HIP_DEBUG_H

@@ -1,6 +1,7 @@
 // capi.cpp -- the C-ABI of include/rsync_hip.h: contexts, device memory, the HIP scan backend and the
 // host-side glue that mirrors Generator.sendItemizeAndChecksums / Sender.sendFiles per-file handling.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -539,6 +540,46 @@ namespace rshi {
 // Under scan_spec_queue the aligned speculation's sums come down on aux after the scan has moved on (or returned):
 // a K1 that rewrites src_weak / src_strong on the context stream first waits for that download, when it is still
 // running (a host-side query: no wait packet in the common case).
+// The stamped launches' device counters and pinned stamps (scan_device under scan_spec_queue): slot 0 the prep
+// launch, slot 1 the chain flags.  prep_dev: the two counters (one 64-B line each), then the prep's scratch sums;
+// zero when allocated, and every stamped launch leaves them zero.
+hipError_t prep_ensure(rsh_ctx* c, int64_t nsamp) {
+    const size_t need = 256 + (size_t)(2 * nsamp + 2) * 4;
+    if (c->prep_dev.cap < need) {
+        hipError_t e = c->prep_dev.ensure(std::max<size_t>(need, 4096));
+        if (e == hipSuccess) e = hipMemset(c->prep_dev.p, 0, c->prep_dev.cap);
+        if (e != hipSuccess) return e;
+    }
+    if (!c->h_stamps.p) {
+        const hipError_t e = c->h_stamps.ensure(4096);
+        if (e != hipSuccess) return e;
+        memset(c->h_stamps.p, 0, c->h_stamps.cap);
+    }
+    return hipSuccess;
+}
+uint32_t* prep_counter(rsh_ctx* c, int slot) { return reinterpret_cast<uint32_t*>(c->prep_dev.as<uint8_t>() + 64 * slot); }
+int* prep_stamp(rsh_ctx* c, int slot) { return reinterpret_cast<int*>(c->h_stamps.as<uint8_t>() + 64 * slot); }
+
+// Spins until a stamped launch has written `gen` into its stamp.  A launch that fails never writes it: after 10 s
+// the stream is synchronised, which reports the failure.
+hipError_t wait_stamp(const int* stamp, int gen, hipStream_t s) {
+    const volatile int* v = stamp;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; ++i) {
+        if (*v == gen) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            return hipSuccess;
+        }
+        _mm_pause();
+        if ((i & 0x3FF) == 0 && ms_since(t0) > 0.2) std::this_thread::yield();  // a K1 takes milliseconds
+        if ((i & 0xFFFF) == 0 && ms_since(t0) > 10000.0) {
+            const hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+            return *v == gen ? hipSuccess : hipErrorLaunchFailure;
+        }
+    }
+}
+
 hipError_t spec_buffers_free(rsh_ctx* c) {
     if (!c->spec_dl_pending) return hipSuccess;
     c->spec_dl_pending = false;
@@ -612,8 +653,11 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     const bool on_ctx = rsh::opt(rsh::OPT_SCAN_SPEC_QUEUE) != 0;
     hipStream_t ss = on_ctx ? c->stream : c->aux;  // the speculation
     hipStream_t rs = on_ctx ? c->aux : c->stream;  // the round trips
-    RSH_HIP(hipEventRecord(c->ev_in, c->stream));  // whatever produced the inputs on the caller's stream
-    if (on_ctx) RSH_HIP(hipStreamWaitEvent(rs, c->ev_in, 0));
+    if (on_ctx) RSH_HIP(prep_ensure(c, nsamp));     // the stamped launches' counters and stamps
+    // (old layout) whatever produced the inputs on the caller's stream.  scan_spec_queue: no marker between the
+    // producer and the speculation -- the prep launch's stamp (below) tells the host the inputs are complete, and
+    // ev_in is recorded on aux once it has seen it.
+    if (!on_ctx) RSH_HIP(hipEventRecord(c->ev_in, c->stream));
     // (aux) the aligned speculation: the source's own block sums with the basis header's B and dl,
     // the chain flags, and their download.  It is a bet on long runs of aligned matches; in head mode it
     // is launched only once the resolver has taken scan_defer_steps steps or scan_defer_us without finishing
@@ -631,12 +675,22 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     bool prep_recorded = false;
     bool k1_timed = false;  // the speculation's K1 recorded ev_k1a / ev_k1b with its dispatch (no marker packets)
     int64_t spec_sums_na = -1;  // scan_spec_queue: windows of the launched speculation whose sums are still on the device
+    int flags_gen = 0;          // > 0: the last launch's flags are stamped with this value (prep_stamp(c, 1))
+    // the last launch's flags on the host: its stamp, or its ev_flags
+    auto flags_landed = [&]() -> bool {
+        if (flags_gen > 0) return *static_cast<volatile int*>(prep_stamp(c, 1)) == flags_gen;
+        return hipEventQuery(c->ev_flags) != hipErrorNotReady;
+    };
+    auto wait_flags = [&]() -> hipError_t {
+        return flags_gen > 0 ? wait_stamp(prep_stamp(c, 1), flags_gen, c->stream) : hipEventSynchronize(c->ev_flags);
+    };
     auto launch_spec = [&]() -> int {
         const int64_t sn = std::min<int64_t>(n, spec_na * B);  // bytes: whole windows, or to the end
         const int64_t snf = std::min<int64_t>(spec_na, C);
         if (on_ctx) {
             RSH_HIP(spec_buffers_free(c));  // the previous scan's downloads of these buffers (aux) are done
-            rsh::k1_timing_next(c->ev_k1a, c->ev_k1b);
+            // (option time_spec) its own dispatch events: each costs the queue ~4.5 us after the kernel
+            if (rsh::opt(rsh::OPT_TIME_SPEC) != 0) rsh::k1_timing_next(c->ev_k1a, c->ev_k1b);
         } else {
             RSH_HIP(hipStreamWaitEvent(c->aux, spec_after_prep && prep_recorded ? c->ev_prep : c->ev_in, 0));
             RSH_HIP(hipEventRecord(c->ev_k1a, c->aux));
@@ -649,11 +703,22 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         if (on_ctx) rsh::k1_timing_next(nullptr, nullptr);
         RSH_HIP(e);
         if (!on_ctx) RSH_HIP(hipEventRecord(c->ev_k1b, c->aux));
-        RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
-                                        (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(), ss));
-        // the flags first (a run of matches needs nothing else), then the sums (aligned lookups off the run).
-        // (Written by the flags kernel straight into pinned host memory instead: no difference, r2_ab2.)
-        if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, ss));
+        // the flags first (a run of matches needs nothing else), then the sums (aligned lookups off the run).  Under
+        // scan_spec_queue the flags kernel writes them into pinned host memory itself (option scan_flags_host): a
+        // D2H copy between two kernels on one queue left it idle 20-100 us (tools/queue_lat.hip case 8); round 2
+        // measured no difference in the old layout (r2_ab2), where the copy was off the critical path.
+        const bool flags_host = on_ctx && rsh::opt(rsh::OPT_SCAN_FLAGS_HOST) != 0;
+        if (flags_host) {  // stamped: the host polls the stamp instead of waiting for an event
+            flags_gen = ++c->stamp_seq;
+            RSH_HIP(rsh::launch_chain_flags_stamped(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak,
+                                                    d_strong, (uint32_t)snf, (uint32_t)dl, c->h_fl.as<uint8_t>(),
+                                                    rsh::Stamp{prep_counter(c, 1), prep_stamp(c, 1), flags_gen}, ss));
+        } else {
+            flags_gen = 0;
+            RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
+                                            (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(), ss));
+            if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, ss));
+        }
         RSH_HIP(hipEventRecord(c->ev_flags, ss));
         if (on_ctx) {
             // the sums come down on aux once the resolver first asks for them (HipBackend::aligned_count): on the
@@ -670,6 +735,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     };
     const bool head = !(diag & 1);
     bool spec_launched = false;
+    bool spec_tentative = false, tentative_stopped = false;
     if (!head || (diag & 4)) {  // scan_diag bit 2: launch at once even in head mode (A/B)
         const int rc = launch_spec();
         if (rc != RSH_OK) return rc;
@@ -679,12 +745,54 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // at position 0, and its MD5 (one serial chain, ~0.13 ms for 128 KiB) then overlaps the first probe
     const int64_t w0 = std::min<int64_t>(B, n);
     RSH_HIP(c->h_win0.ensure((size_t)w0 + 16));
-    RSH_HIP(rsh::launch_copy_to_host(d_src, w0, c->h_win0.as<uint8_t>(), rs));
+    int32_t* lead_w = c->h_lead.as<int32_t>();
+    const int32_t* lead_tw = nullptr;  // scan_spec_queue: the table's weak sums at the sampled chunks (prep launch)
+    if (on_ctx) {
+        // (context stream) window 0, the lead and sample sums and the table's sums at those chunks in one stamped
+        // launch right behind the inputs' producer, then (launch-then-confirm, below) the speculation right behind
+        // it: the two K1s are apart by this launch only, and nothing runs beside the speculation's start (the sample
+        // kernels on aux beside it cost it ~90 us, r5c/r5e traces)
+        const size_t wins_at = 128, tw_at = wins_at + (((size_t)nsamp * 8 + 63) & ~(size_t)63);
+        RSH_HIP(c->h_prep.ensure(tw_at + (size_t)(nsamp + 1) * 4 + 64));
+        auto* wins = reinterpret_cast<int64_t*>(c->h_prep.as<uint8_t>() + wins_at);
+        for (int64_t i = 0; i < nsamp; ++i) wins[i] = samp[(size_t)i];
+        int32_t* tw = reinterpret_cast<int32_t*>(c->h_prep.as<uint8_t>() + tw_at);
+        const int prep_gen = ++c->stamp_seq;
+        rsh::ScanPrep P{};
+        P.data = d_src;
+        P.n = n;
+        P.B = (uint32_t)B;
+        P.nsamp = head ? (uint32_t)nsamp : 0u;
+        P.pieces = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(8, (B + 16383) / 16384));
+        P.wins = wins;
+        P.table_weak = d_weak;
+        P.C = C;
+        P.out_t = lead_w;
+        P.out_w = tw;
+        P.w0 = c->h_win0.as<uint8_t>();
+        P.w0_len = w0;
+        P.scratch = reinterpret_cast<int32_t*>(c->prep_dev.as<uint8_t>() + 256);
+        P.st = rsh::Stamp{prep_counter(c, 0), prep_stamp(c, 0), prep_gen};
+        RSH_HIP(rsh::launch_scan_prep(P, ss));
+        if (head && !spec_launched && nlead > 0 && rsh::opt(rsh::OPT_SCAN_EARLY) != 0 && na <= kRoundWindows &&
+            (nlead >= kLeadWindows || nlead == nf)) {  // launch-then-confirm (below), right behind the prep launch
+            const int rc = launch_spec();
+            if (rc != RSH_OK) return rc;
+            spec_launched = spec_tentative = true;
+        }
+        {
+            CallTrace tr("prep_stamp", nsamp);
+            RSH_HIP(wait_stamp(prep_stamp(c, 0), prep_gen, ss));
+        }
+        RSH_HIP(hipEventRecord(c->ev_in, rs));  // the inputs are complete (the host saw the stamp)
+        lead_tw = tw;
+    } else {
+        RSH_HIP(rsh::launch_copy_to_host(d_src, w0, c->h_win0.as<uint8_t>(), rs));
+    }
     // (stream) T(kB) of the first nlead aligned windows: when all of them carry chunk k's weak sum the
     // source very likely continues as an aligned run of matches (an unchanged or appended file), and the
     // speculation is launched at once instead of after a few head-mode steps
-    int32_t* lead_w = c->h_lead.as<int32_t>();
-    if (head && nlead > 0) {
+    if (!on_ctx && head && nlead > 0) {
         auto* ents = reinterpret_cast<rsh::GatherEnt*>(c->h_lead.as<uint8_t>() + lead_ents_at);
         auto* lf = reinterpret_cast<rsh::ScanFile*>(ents + nsamp + 1);
         *lf = rsh::ScanFile{};
@@ -694,32 +802,54 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         for (int64_t i = 0; i < nsamp; ++i) ents[i] = rsh::GatherEnt{samp[(size_t)i] * B, 0, 0};
         RSH_HIP(rsh::launch_window_weak(lf, ents, (uint32_t)nsamp, lead_w, rs));
     }
-    if (spec_after_prep) {
+    if (!on_ctx && spec_after_prep) {
         RSH_HIP(hipEventRecord(c->ev_prep, rs));
         prep_recorded = true;
     }
     // (stream) the received table to the host (the lead check and the resolver), after the sample work: the
-    // speculation waits for the samples only, and these copies and the hash build below run beside it
-    if (download) {
-        if (C > 0) {
-            RSH_HIP(hipMemcpyAsync(c->h_weak.p, d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, rs));
-            if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_strong.p, d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, rs));
+    // speculation waits for the samples only, and these copies and the hash build below run beside it.
+    // (scan_spec_queue: after the lead check, which takes the table's sums at the samples from the prep launch,
+    // so that a stopped tentative launch's abort does not queue behind these copies)
+    auto table_work = [&]() -> int {
+        if (download) {
+            if (C > 0) {
+                RSH_HIP(hipMemcpyAsync(c->h_weak.p, d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, rs));
+                if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_strong.p, d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, rs));
+            }
+            RSH_HIP(hipEventRecord(c->ev_tab, rs));
         }
-        RSH_HIP(hipEventRecord(c->ev_tab, rs));
+        // (stream) the device probe hash
+        RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, rs));
+        RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, rs));
+        return RSH_OK;
+    };
+    auto table_wait = [&]() -> int {
+        {
+            CallTrace tr("table_dl", C);
+            if (download) RSH_HIP(hipEventSynchronize(c->ev_tab));
+        }
+        {
+            CallTrace tr("hash_sync", ns);
+            RSH_HIP(hipStreamSynchronize(rs));
+        }
+        return RSH_OK;
+    };
+    if (download) {
         host_weak = c->h_weak.as<int32_t>();
         host_strong = c->h_strong.as<uint8_t>();
     }
-    // (stream) the device probe hash
-    RSH_HIP(rsh::launch_table_clear(c->slots.as<unsigned long long>(), ns, rs));
-    RSH_HIP(rsh::launch_table_insert(c->slots.as<unsigned long long>(), ns - 1, d_weak, (uint32_t)C, rs));
+    if (!on_ctx) {
+        const int rc = table_work();
+        if (rc != RSH_OK) return rc;
+    }
 
     // Launch-then-confirm: when one K1 round covers every window (na <= kRoundWindows), the speculation that
     // the lead decides on below is launched now, before the host knows the table, so it starts the moment the
     // Generator's work ends on the device; the lead check then keeps it or stops it (its waves leave after
     // their first two stages).  Larger sources wait for the samples (the launch may cover a prefix only).
+    // (scan_spec_queue: launched above, right behind the prep launch.)
     const bool early_on = rsh::opt(rsh::OPT_SCAN_EARLY) != 0;  // A/B
-    bool spec_tentative = false, tentative_stopped = false;
-    if (head && !spec_launched && nlead > 0 && early_on && na <= kRoundWindows &&
+    if (!on_ctx && head && !spec_launched && nlead > 0 && early_on && na <= kRoundWindows &&
         (nlead >= kLeadWindows || nlead == nf)) {
         const int rc = launch_spec();
         if (rc != RSH_OK) return rc;
@@ -734,13 +864,9 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     table.digest_length = dl;
     table.weak = host_weak;
     table.strong = host_strong;
-    {
-        CallTrace tr("table_dl", C);
-        if (download) RSH_HIP(hipEventSynchronize(c->ev_tab));
-    }
-    {
-        CallTrace tr("hash_sync", ns);
-        RSH_HIP(hipStreamSynchronize(rs));
+    if (!on_ctx) {
+        const int rc = table_wait();
+        if (rc != RSH_OK) return rc;
     }
     uint8_t md5_0[16];
     std::thread md5_0_thread([&] {
@@ -767,8 +893,10 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     const bool wait_on = rsh::opt(rsh::OPT_SCAN_WAIT) != 0;
     const bool sample_on = rsh::opt(rsh::OPT_SCAN_SAMPLE) != 0;
     if (head && nlead > 0 && (!spec_launched || spec_tentative)) {
+        // the table's weak sum at sample i: from the prep launch (scan_spec_queue) or the downloaded table
+        auto tw_at = [&](int64_t i) { return lead_tw ? lead_tw[i] : host_weak[samp[(size_t)i]]; };
         int64_t lead = 0;
-        while (lead < nlead && lead_w[lead] == host_weak[lead]) ++lead;
+        while (lead < nlead && lead_w[lead] == tw_at(lead)) ++lead;
         const bool eager = lead == nlead && (nlead >= kLeadWindows || nlead == nf);
         // The run may stop somewhere (an insert shifts everything after it to another phase, where the
         // phase-shifted speculation takes over): cover only up to the last sample that still matches, plus
@@ -779,7 +907,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         if (eager && sample_on) {
             int64_t lastk = nlead - 1;
             for (int64_t i = nlead; i < nsamp; ++i)
-                if (lead_w[i] == host_weak[samp[(size_t)i]]) lastk = samp[(size_t)i];
+                if (lead_w[i] == tw_at(i)) lastk = samp[(size_t)i];
             if (lastk + stride < nf) {
                 cover = std::min<int64_t>(na, (lastk + stride + 64) & ~(int64_t)63);  // whole waves
                 run_last = lastk;
@@ -807,6 +935,11 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             }
             spec_wait = wait_on;
         }
+    }
+    if (on_ctx) {  // (aux) the table and the probe hash, after a tentative launch's abort (above)
+        int rc = table_work();
+        if (rc == RSH_OK) rc = table_wait();
+        if (rc != RSH_OK) return rc;
     }
     HipBackend be(c, d_src, n, table, d_weak, seed);
     be.rs_ = rs;
@@ -1029,10 +1162,10 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         }
         if (spec_wait) {  // head-mode steps beside the launch would only slow it down
             CallTrace tw("spec_wait", res->stats.head_steps);
-            landed = hipEventSynchronize(c->ev_flags) == hipSuccess;
+            landed = wait_flags() == hipSuccess;
             return true;
         }
-        landed = hipEventQuery(c->ev_flags) != hipErrorNotReady;
+        landed = flags_landed();
         if (!landed) res->stats.head_steps++;
         return landed;
     });
@@ -1045,7 +1178,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         // the stopped launch's waves leave within two stages; later work on this context starts after them
         if (tentative_stopped) RSH_HIP(hipStreamWaitEvent(rs, on_ctx ? c->ev_flags : c->ev_spec, 0));
         res->stats.device_ms += ms_since(t0);
-    } else if (done && !landed && hipEventQuery(c->ev_flags) == hipErrorNotReady) {
+    } else if (done && !landed && !flags_landed()) {
         RSH_HIP(hipStreamWriteValue32(rs, c->abort_word, (uint32_t)gen, 0));  // the rest is dead work
         // Later work on this context starts only once the stopped launch has left the CUs: K1 fills every
         // wave slot of the chip exactly once (2 per SIMD at 16 GiB, B = 128 KiB), and a launch that finds
@@ -1054,7 +1187,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         res->stats.speculation_aborted = 1;
         res->stats.device_ms += ms_since(t0);
     } else {
-        RSH_HIP(hipEventSynchronize(c->ev_flags));  // the sums follow on aux; aligned_count() polls ev_spec
+        RSH_HIP(wait_flags());  // the sums follow on aux; aligned_count() polls ev_spec
         res->stats.device_ms += ms_since(t0);
         res->stats.speculation_aborted = 0;
         spec_read = true;
@@ -1314,8 +1447,8 @@ int rsh_block_sums_device(rsh_ctx* ctx, const void* d_data, int64_t n, const rsh
     if (h->chunk_count == 0) return RSH_OK;
     if (!d_data || !d_weak || (!d_strong && h->digest_length > 0)) return RSH_E_INVAL;
     RSH_HIP(hipSetDevice(ctx->device));
-    // the K1's own start / stop timestamps (rsh_debug_kernel_ms; no marker packets around it)
-    rsh::k1_timing_next(ctx->ev_gen_a, ctx->ev_gen_b);
+    // the K1's own start / stop timestamps (rsh_debug_kernel_ms; no marker packets around it; option time_gen)
+    if (rsh::opt(rsh::OPT_TIME_GEN) != 0) rsh::k1_timing_next(ctx->ev_gen_a, ctx->ev_gen_b);
     const hipError_t e = rsh::launch_block_sums(static_cast<const uint8_t*>(d_data), n, (uint32_t)h->block_length,
                                                 (uint32_t)h->chunk_count, (uint32_t)h->digest_length, seed_word(seed),
                                                 static_cast<int32_t*>(d_weak), static_cast<uint8_t*>(d_strong),

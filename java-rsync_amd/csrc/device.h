@@ -125,6 +125,38 @@ hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, co
 hipError_t launch_chain_flags(const int32_t* d_wsrc, const uint8_t* d_ssrc, const int32_t* d_wbas,
                               const uint8_t* d_sbas, uint32_t count, uint32_t dl, uint8_t* d_flags,
                               hipStream_t s);
+// Completion without a marker packet: the launch's last workgroup to finish writes `gen` into *stamp (pinned host
+// memory, system-scope release after every workgroup's stores), which the host polls.  counter: device memory,
+// zero before the launch (the last workgroup zeroes it again).
+struct Stamp {
+    uint32_t* counter;
+    int* stamp;
+    int gen;
+};
+// The chain flags of the single-file scan into pinned host memory, stamped.
+hipError_t launch_chain_flags_stamped(const int32_t* d_wsrc, const uint8_t* d_ssrc, const int32_t* d_wbas,
+                                      const uint8_t* d_sbas, uint32_t count, uint32_t dl, uint8_t* h_flags,
+                                      Stamp st, hipStream_t s);
+// The single-file scan's launch decision in one launch on the speculation's queue, ahead of it (scan_device,
+// scan_spec_queue): the weak sums T(kB) of the sampled windows wins[i] (each window split over `pieces` workgroups,
+// partial sums added with device atomics into scratch, 2 ints per sample, zero before the launch), the received
+// table's weak sums at the same chunks, and window 0's bytes, all into pinned host memory, then the stamp.
+struct ScanPrep {
+    const uint8_t* data;
+    int64_t n;
+    uint32_t B;
+    uint32_t nsamp, pieces;
+    const int64_t* wins;        // pinned host: the sampled window indices
+    const int32_t* table_weak;  // device: the received table's weak sums
+    int32_t C;
+    int32_t* out_t;             // pinned host: T(wins[i] B)
+    int32_t* out_w;             // pinned host: table_weak[wins[i]] (0 past the table)
+    uint8_t* w0;                // pinned host: window 0 (w0_len bytes)
+    int64_t w0_len;
+    int32_t* scratch;           // device: 2 nsamp ints
+    Stamp st;
+};
+hipError_t launch_scan_prep(const ScanPrep& P, hipStream_t s);
 
 // Probe table: open-addressing hash of the distinct weak keys (key -> 1).  slots = power of two.
 struct ProbeTable {

@@ -3872,6 +3872,89 @@ hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, 
     return hipGetLastError();
 }
 
+// The last workgroup of a stamped launch: every thread's stores are fenced at system scope before its workgroup
+// counts itself done, and the workgroup that completes the count writes the stamp after another system fence (the
+// host polls the stamp, then reads what the launch wrote).  Returns true in the last workgroup (after its barrier).
+__device__ __forceinline__ bool stamp_arrive(const Stamp& st, bool* sh_last) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) *sh_last = atomicAdd(st.counter, 1u) == gridDim.x * gridDim.y - 1;
+    __syncthreads();
+    return *sh_last;
+}
+__device__ __forceinline__ void stamp_write(const Stamp& st) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicExch(st.counter, 0u);
+        __threadfence_system();
+        __hip_atomic_store(st.stamp, st.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ __launch_bounds__(256) void chain_flags_stamped_kernel(const int32_t* __restrict__ wsrc,
+                                                                  const uint8_t* __restrict__ ssrc,
+                                                                  const int32_t* __restrict__ wbas,
+                                                                  const uint8_t* __restrict__ sbas, uint32_t count,
+                                                                  uint32_t dl, uint8_t* __restrict__ flags, Stamp st) {
+    __shared__ bool last;
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < count) {
+        bool eq = wsrc[k] == wbas[k];
+        for (uint32_t j = 0; j < dl; ++j) eq &= ssrc[(size_t)k * dl + j] == sbas[(size_t)k * dl + j];
+        flags[k] = eq ? 1 : 0;
+    }
+    if (stamp_arrive(st, &last)) stamp_write(st);
+}
+
+hipError_t launch_chain_flags_stamped(const int32_t* d_wsrc, const uint8_t* d_ssrc, const int32_t* d_wbas,
+                                      const uint8_t* d_sbas, uint32_t count, uint32_t dl, uint8_t* h_flags,
+                                      Stamp st, hipStream_t s) {
+    hipLaunchKernelGGL(chain_flags_stamped_kernel, dim3(count ? (count + 255) / 256 : 1), dim3(256), 0, s, d_wsrc,
+                       d_ssrc, d_wbas, d_sbas, count, dl, h_flags, st);
+    return hipGetLastError();
+}
+
+// blockIdx.x < nsamp * pieces: piece (blockIdx.x % pieces) of sample window blockIdx.x / pieces; the blocks past them
+// copy window 0 to the host, 4 KiB each.
+__global__ __launch_bounds__(256) void scan_prep_kernel(ScanPrep P) {
+    __shared__ int32_t sh[2 * 4];
+    __shared__ bool last;
+    const uint32_t b = blockIdx.x, nsum = P.nsamp * P.pieces;
+    if (b < nsum) {
+        const uint32_t i = b / P.pieces, q = b % P.pieces;
+        const int64_t p = P.wins[i] * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
+        const int64_t plen = ((w + P.pieces - 1) / P.pieces + 15) & ~(int64_t)15;
+        const int64_t lo = p + (int64_t)q * plen, hi = lo + plen < p + w ? lo + plen : p + w;
+        int32_t v[2] = {0, 0};
+        range_sums(P.data, P.n, lo, hi, p, v[0], v[1]);
+        block_reduce<2>(v, sh);
+        if (threadIdx.x == 0) {
+            atomicAdd(&P.scratch[2 * i], v[0]);
+            atomicAdd(&P.scratch[2 * i + 1], v[1]);
+        }
+    } else {
+        const int64_t o = 16 * ((int64_t)(b - nsum) * blockDim.x + threadIdx.x);
+        if (o < P.w0_len) copy_piece(P.data, P.w0, P.w0_len, o);
+    }
+    if (!stamp_arrive(P.st, &last)) return;
+    for (uint32_t i = threadIdx.x; i < P.nsamp; i += blockDim.x) {
+        const int64_t k = P.wins[i], p = k * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
+        const uint32_t S1 = (uint32_t)atomicExch(&P.scratch[2 * i], 0);
+        const uint32_t U = (uint32_t)atomicExch(&P.scratch[2 * i + 1], 0);
+        const uint32_t S2 = (uint32_t)w * S1 - U;
+        P.out_t[i] = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
+        P.out_w[i] = k < P.C ? P.table_weak[k] : 0;
+    }
+    stamp_write(P.st);
+}
+
+hipError_t launch_scan_prep(const ScanPrep& P, hipStream_t s) {
+    const uint32_t copy_blocks = (uint32_t)((P.w0_len + 16 * 256 - 1) / (16 * 256));
+    hipLaunchKernelGGL(scan_prep_kernel, dim3(P.nsamp * P.pieces + copy_blocks), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
 // grid (., n): entry blockIdx.y, 16 bytes per thread, grid-strided over the entry's length
 __global__ __launch_bounds__(256) void copy_many_kernel(const CopyEnt* __restrict__ ents, int hi) {
     if (hi) __builtin_amdgcn_s_setprio(3);

@@ -159,14 +159,22 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
     // the speculation the backend has now (none while it is still in flight: every lookup below then
     // takes the generic path, which gives the same answer); re-read every step, since a tiled backend
     // extends it as its tiles land
-    int64_t nal = 0, nflags = 0, max_batch = 1;
+    // The aligned sums are asked for only when a step needs them (NAL()): an aligned run of matches resolves from
+    // the chain flags alone, and a backend may bring the sums to the host only on request (HipBackend).
+    int64_t nal_step = -1, nflags = 0, max_batch = 1;
     const int32_t* aw = nullptr;
     const uint8_t* as = nullptr;
     const uint8_t* fl = nullptr;
+    auto NAL = [&]() -> int64_t {
+        if (nal_step < 0) {
+            nal_step = be.aligned_count();
+            aw = be.aligned_weak();
+            as = be.aligned_strong();
+        }
+        return nal_step;
+    };
     auto refresh = [&] {
-        nal = be.aligned_count();
-        aw = be.aligned_weak();
-        as = be.aligned_strong();
+        nal_step = -1;
         fl = be.chain_flags();
         nflags = std::min<int64_t>(be.flags_count(), table.chunk_count);
         max_batch = be.max_batch();
@@ -216,7 +224,7 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
         *hi = ehi + elo * (uint32_t)(clampB(p) - clampB(anchor));
     };
     auto T_at = [&](int64_t p) -> int32_t {
-        if (p % B == 0 && p / B < nal) return aw[p / B];
+        if (p % B == 0 && p / B < NAL()) return aw[p / B];
         return be.weak_at(p);
     };
     // Flush bookkeeping shared by the single and the batched path: from the rolling value R at the
@@ -288,8 +296,8 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
         if (!md5c_valid && synced && pref < table.chunk_count) {
             PhaseView pv;
             bool have = false;
-            if (s % B == 0 && s / B < nal) {
-                pv.s0 = 0, pv.count = nal, pv.w = aw, pv.st = as;
+            if (s % B == 0 && s / B < NAL()) {
+                pv.s0 = 0, pv.count = NAL(), pv.w = aw, pv.st = as;
                 have = true;
             } else if (s % B != 0) {
                 const bool chain = !ev.empty() && ev.back().kind == RSH_EV_MATCH && ev.back().count >= 2 &&
@@ -344,7 +352,7 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
         int64_t p = -1;
         if (!none) {
             int64_t a = s;
-            if (!md5c_valid && synced && s % B == 0 && s / B < nal) {  // key known from aligned sums
+            if (!md5c_valid && synced && s % B == 0 && s / B < NAL()) {  // key known from aligned sums
                 int32_t size;
                 table.bucket(aw[s / B], &size);
                 if (size > 0) p = s;
@@ -383,7 +391,7 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
                     const int32_t c = bk[pos];
                     if (!md5c_valid) {  // Sender.java:1259-1263
                         PhaseView pd;
-                        if (p % B == 0 && p / B < nal) {
+                        if (p % B == 0 && p / B < NAL()) {
                             memcpy(md5c, as + (p / B) * dl, (size_t)dl);
                         } else if (p % B != 0 && be.phase_sums(p, false, &pd)) {  // a landed phase speculation's
                             memcpy(md5c, pd.st + ((p - pd.s0) / B) * dl, (size_t)dl);  // digest of this window

@@ -13,6 +13,10 @@
 //   8  busy, a D2H hipMemcpyAsync of 128 KiB into pinned memory, tiny
 //   9  busy, tiny writes 128 KiB straight into pinned host memory, then another tiny
 //  10  busy, hipStreamWaitEvent on an event that completed long ago, tiny
+//  11  busy through hipExtLaunchKernelGGL with a start event only, then tiny
+//  12  busy through hipExtLaunchKernelGGL with a stop event only, then tiny
+//  13  busy, then a 128 KiB D2H hipMemcpyAsync into pinned memory: the host time the call itself takes (printed)
+//  14  busy on stream 1, event, stream 2 waits, a 128 KiB D2H on stream 2: the host time of the copy call (printed)
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -62,10 +66,15 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s1));
     const dim3 G(256), T(64);
     for (int r = 0; r < reps; ++r) {
-        for (int c = 1; c <= 10; ++c) {
+        for (int c = 1; c <= 14; ++c) {
             const auto t0 = std::chrono::steady_clock::now();
+            double call_us = -1;
             if (c == 4) {
                 hipExtLaunchKernelGGL(busy, G, T, 0, s1, ea, eb, 0, d, iters, c);
+            } else if (c == 11) {
+                hipExtLaunchKernelGGL(busy, G, T, 0, s1, ea, nullptr, 0, d, iters, c);
+            } else if (c == 12) {
+                hipExtLaunchKernelGGL(busy, G, T, 0, s1, nullptr, eb, 0, d, iters, c);
             } else {
                 hipLaunchKernelGGL(busy, G, T, 0, s1, d, iters, c);
             }
@@ -90,6 +99,20 @@ int main(int argc, char** argv) {
                 case 8: CK(hipMemcpyAsync(hp, dp, 1 << 17, hipMemcpyDeviceToHost, s1)); break;
                 case 9: hipLaunchKernelGGL(tiny_host, dim3(32), dim3(256), 0, s1, hp, 1 << 17, c); break;
                 case 10: CK(hipStreamWaitEvent(s1, old, 0)); break;
+                case 13: {
+                    const auto c0 = std::chrono::steady_clock::now();
+                    CK(hipMemcpyAsync(hp, dp, 1 << 17, hipMemcpyDeviceToHost, s1));
+                    call_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c0).count();
+                    break;
+                }
+                case 14: {
+                    CK(hipEventRecord(en, s1));
+                    const auto c0 = std::chrono::steady_clock::now();
+                    CK(hipStreamWaitEvent(s2, en, 0));
+                    CK(hipMemcpyAsync(hp, dp, 1 << 17, hipMemcpyDeviceToHost, s2));
+                    call_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c0).count();
+                    break;
+                }
                 default: break;
             }
             hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, ts, d, c);
@@ -100,6 +123,8 @@ int main(int argc, char** argv) {
                 float k = 0;
                 CK(hipEventElapsedTime(&k, ea, eb));
                 printf("rep %d case %d host %.3f ms (busy by ext events %.3f ms)\n", r, c, ms, k);
+            } else if (call_us >= 0) {
+                printf("rep %d case %d host %.3f ms (the copy call took %.1f us)\n", r, c, ms, call_us);
             } else {
                 printf("rep %d case %d host %.3f ms\n", r, c, ms);
             }

@@ -1,5 +1,5 @@
 """Gaps of tools/queue_lat.hip's cases from its rocprofv3 kernel trace: for each `busy` launch, the idle time until
-the next kernel starts (case = launch index mod 10 + 1).  Usage: python queue_lat_gaps.py <trace dir>"""
+the next kernel starts (case = launch index mod 14 + 1).  Usage: python queue_lat_gaps.py <trace dir>"""
 import collections
 import csv
 import glob
@@ -13,7 +13,7 @@ gaps = collections.defaultdict(list)
 nb = 0
 for i, (a, b, name) in enumerate(k):
     if name.startswith("busy") and i + 1 < len(k):
-        gaps[nb % 10 + 1].append((k[i + 1][0] - b) / 1e3)
+        gaps[nb % 14 + 1].append((k[i + 1][0] - b) / 1e3)
         nb += 1
 for c in sorted(gaps):
     g = gaps[c][1:] or gaps[c]
