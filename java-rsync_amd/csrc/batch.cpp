@@ -1375,7 +1375,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         for (FileScan& fs : files) fs.be.head = false;
     }
 
-    const int ncpu = host_cores();
+    const int ncpu = WorkerCap::value() > 0 ? std::min(host_cores(), WorkerCap::value()) : host_cores();
     // spinning waiters: one core stays free for the coordinator
     const int32_t ncores = (spin_us() > 0 && ncpu > 2) ? ncpu - 1 : ncpu;
     // only the files still live get a worker: after the chain walks (or a leading speculation) most files are

@@ -83,12 +83,16 @@ class HipBackend : public rsh::ScanBackend {
         if (tiled) return aligned_end;
         if (head) return 0;
         if (!sums_ready) {
-            if (lazy_na >= 0) {  // scan_spec_queue: the first request downloads them (on rs_; the flags have landed)
+            if (lazy_na >= 0) {
+                // scan_spec_queue: the first step that needs them downloads them (on rs_; the flags have landed) and
+                // waits: the copy is tens of microseconds, the generic path's probe and host digest as long or longer
+                CallTrace tr("sums_dl", lazy_na);
                 ok(hipStreamWaitEvent(rs_, c_->ev_flags, 0));
                 ok(hipMemcpyAsync(c_->h_aw.p, c_->src_weak.p, (size_t)lazy_na * 4, hipMemcpyDeviceToHost, rs_));
                 if (dl_ > 0)
                     ok(hipMemcpyAsync(c_->h_as.p, c_->src_strong.p, (size_t)lazy_na * dl_, hipMemcpyDeviceToHost, rs_));
                 ok(hipEventRecord(c_->ev_spec, rs_));
+                ok(hipEventSynchronize(c_->ev_spec));
                 lazy_na = -1;
             }
             sums_ready = err == hipSuccess && hipEventQuery(c_->ev_spec) == hipSuccess;
@@ -757,13 +761,22 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         auto* wins = reinterpret_cast<int64_t*>(c->h_prep.as<uint8_t>() + wins_at);
         for (int64_t i = 0; i < nsamp; ++i) wins[i] = samp[(size_t)i];
         int32_t* tw = reinterpret_cast<int32_t*>(c->h_prep.as<uint8_t>() + tw_at);
+        {  // the scan as a batch of one for later gathers (the prefix end's window sums)
+            auto* ents = reinterpret_cast<rsh::GatherEnt*>(c->h_lead.as<uint8_t>() + lead_ents_at);
+            auto* lf = reinterpret_cast<rsh::ScanFile*>(ents + nsamp + 1);
+            *lf = rsh::ScanFile{};
+            lf->data = d_src;
+            lf->n = n;
+            lf->B = (uint32_t)B;
+        }
         const int prep_gen = ++c->stamp_seq;
         rsh::ScanPrep P{};
         P.data = d_src;
         P.n = n;
         P.B = (uint32_t)B;
         P.nsamp = head ? (uint32_t)nsamp : 0u;
-        P.pieces = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(8, (B + 16383) / 16384));
+        const int64_t pieces_opt = rsh::opt(rsh::OPT_SCAN_PREP_PIECES);
+        P.pieces = (uint32_t)std::max<int64_t>(1, pieces_opt > 0 ? pieces_opt : std::min<int64_t>(8, (B + 16383) / 16384));
         P.wins = wins;
         P.table_weak = d_weak;
         P.C = C;
@@ -1097,7 +1110,9 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                                                hipMemcpyDeviceToHost, ss));
                     RSH_HIP(hipEventRecord(c->ev_phase[pset], ss));
                     c->ph_set = pset;
-                    k1_timed = true;  // (the event records around it)
+                    k1_timed = true;     // (the event records around it)
+                    spec_sums_na = -1;   // its sums come down with it (above), not on request
+                    flags_gen = 0;       // ... and its flags land with ev_flags (a stopped launch's stamp says nothing)
                     be.phase_adopt(s0, Q, gph, pset);
                     res->stats.phase_guesses++;
                     spec_launched = seg_launched = true;

@@ -23,6 +23,18 @@ struct BatchState;  // batch.cpp
 void destroy_batch_state(BatchState* b);
 // batch.cpp: the cores this process may use (affinity mask, cgroup quota; option host_cores overrides)
 int host_cores();
+// The batched scan's resolver threads on this thread's calls: at most this many cores (0: host_cores()).  A segment
+// call that digests its files on the other cores meanwhile (segment.cpp) sets it, so that the spinning resolver
+// workers and the MD5 pool together stay within the cores (a cgroup quota throttles the whole process past it).
+struct WorkerCap {
+    static int& value() {
+        static thread_local int v = 0;
+        return v;
+    }
+    int saved;
+    explicit WorkerCap(int cap) : saved(value()) { value() = cap; }
+    ~WorkerCap() { value() = saved; }
+};
 // batch.cpp: rsh_block_sums_batch_device / rsh_match_scan_batch_device for a caller that holds the context's
 // claim (segment.cpp's host-memory forms)
 int block_sums_batch_claimed(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t njobs, const uint8_t seed[4]);

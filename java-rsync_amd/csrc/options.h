@@ -50,6 +50,7 @@ enum Opt : int {
     OPT_BATCH_SKIP_REST,   // 1: the rest of a two-phase speculation only if some phase-0 walk reached the prefix's end
     OPT_SCAN_SPEC_QUEUE,   // 1: the single-file speculation on the context stream, round trips on aux; 0: round 4's layout
     OPT_SCAN_FLAGS_HOST,   // 1: (scan_spec_queue) the chain flags kernel writes pinned host memory (no D2H copy)
+    OPT_SCAN_PREP_PIECES,  // (scan_spec_queue) workgroups per sampled window in the prep launch (0: auto, <= 8)
     OPT_TIME_SPEC,         // 1: the single-file speculation's K1 records timing events (stats spec_kernel_ms)
     OPT_TIME_GEN,          // 1: rsh_block_sums_device's K1 records timing events (rsh_debug_kernel_ms)
     OPT_FAULT_INJECT,      // tests only: bit 0 a segment / Receiver pass's HBM allocation fails, bit 1 a segment's copies fail
@@ -72,7 +73,7 @@ inline const OptInfo* opt_info() {
         {"host_cores", 0},         {"file_tile", 4LL << 30}, {"file_tile_above", 32LL << 30},
         {"probe_long", 1},         {"segment_bytes", 16LL << 30}, {"md5_width", 0},
         {"chain_helpers", -1},     {"chain_map_bytes", 1LL << 30}, {"batch_skip_rest", 1},
-        {"scan_spec_queue", 1},    {"scan_flags_host", 1},   {"time_spec", 0},        {"time_gen", 1},
+        {"scan_spec_queue", 1},    {"scan_flags_host", 1},   {"scan_prep_pieces", 0},   {"time_spec", 0},        {"time_gen", 1},
         {"fault_inject", 0},
     };
     return t;

@@ -265,13 +265,19 @@ int rsh_match_scan_batch(rsh_ctx* ctx, rsh_scan_batch_job* jobs, int32_t njobs, 
         note_error(e, __LINE__, "segment.cpp");
         return fail_unfinished(RSH_E_DEVICE);
     }
-    // every file's MD5 beside the copies and the scans (one core stays with the copies and the coordinator)
+    // every file's MD5 beside the copies and the scans.  The cores are split: the MD5 pool takes all but
+    // kScanCores, the batched scan's coordinator and resolver workers those (after the chain walks a segment
+    // leaves a file or two to the host resolvers); together they stay within the process's cores.
+    constexpr int kScanCores = 3;
+    const int cores = rsh::host_cores();
+    const int md5_threads = std::max(1, cores - kScanCores);
+    rsh::WorkerCap cap(std::max(1, cores - md5_threads));
     std::vector<rsh::Md5File> mf;
     for (int32_t i : ok) mf.push_back(rsh::Md5File{jobs[i].pieces, jobs[i].npieces});
     std::vector<uint8_t> md5((size_t)ok.size() * 16 + 16);
     std::thread md5_thread([&] {
-        rsh::md5_files(mf.data(), (int32_t)mf.size(), reinterpret_cast<uint8_t(*)[16]>(md5.data()),
-                       std::max(1, rsh::host_cores() - 1), (int)rsh::opt(rsh::OPT_MD5_WIDTH));
+        rsh::md5_files(mf.data(), (int32_t)mf.size(), reinterpret_cast<uint8_t(*)[16]>(md5.data()), md5_threads,
+                       (int)rsh::opt(rsh::OPT_MD5_WIDTH));
     });
     int rc = RSH_OK;
     // new files (skipMatchSendData) and empty sources: no bytes to copy

@@ -48,13 +48,18 @@ def main():
     ev = np.zeros(C + n // B + 4096, R.EVENT_DTYPE)
     n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     st = R.ScanStats()
-    out = {k: {"gen_call_ms": [], "scan_call_ms": [], "query_ms": [], "step_ms": [], "gen_k1_ms": []} for k in sets}
+    out = {k: {"gen_call_ms": [], "scan_call_ms": [], "query_ms": [], "step_ms": [], "gen_k1_ms": [], "spec_k1_ms": []}
+           for k in sets}
     for rep in range(a.reps):
         for cfg in sets:
             R.reset_options()
+            sleep_s = 0.0
             for kv in filter(None, cfg.split(",")):
                 k, _, v = kv.partition("=")
-                R.set_option(k, int(v))
+                if k == "sleep_us":  # host idle time after each step (not a library option): a power A/B
+                    sleep_s = int(v) / 1e6
+                else:
+                    R.set_option(k, int(v))
             rows = []
             for i in range(a.steps + 3):
                 t0 = time.perf_counter()
@@ -68,14 +73,19 @@ def main():
                                                ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(st)) == 0
                 t2 = time.perf_counter()
                 k = ctx.kernel_ms(0) if a.query else -1
+                if sleep_s:
+                    t_end = time.perf_counter() + sleep_s
+                    while time.perf_counter() < t_end:
+                        pass
                 t3 = time.perf_counter()
                 assert (lit.value, mat.value, n_ev.value) == (0, n, 1)
                 if i >= 3:
-                    rows.append((t1 - t0, t2 - t1, t3 - t2, t3 - t0, k))
+                    rows.append((t1 - t0, t2 - t1, t3 - t2, t3 - t0, k, st.spec_kernel_ms))
             o = out[cfg]
             for j, key in enumerate(("gen_call_ms", "scan_call_ms", "query_ms", "step_ms")):
                 o[key].append(round(statistics.median(r[j] for r in rows) * 1e3, 4))
             o["gen_k1_ms"].append(round(statistics.median(r[4] for r in rows), 4))
+            o["spec_k1_ms"].append(round(statistics.median(r[5] for r in rows), 4))
     R.reset_options()
     print(json.dumps({"steps": a.steps, "reps": a.reps, "sets": out, "streams_busy_after": ctx.streams_busy()}))
     ctx.close()
