@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "device.h"
+#include "device_common.h"
 #include "md5_core.h"
 #include "options.h"
 
@@ -36,7 +37,6 @@ __device__ __forceinline__ void weak_block(const uint32_t (&m)[16], int32_t& s1,
     u += (int32_t)(off * (uint32_t)a) + b;
 }
 
-__device__ __forceinline__ int32_t sbyte(uint8_t v) { return (int32_t)(int8_t)v; }
 
 // MD5 of one 64-byte block plus its weak-sum contribution at chunk offset `off`.
 __device__ __forceinline__ void md5_weak_block(Md5State& st, const uint32_t (&m)[16], int32_t& s1, int32_t& u,
@@ -1977,2183 +1977,6 @@ hipError_t launch_chain_flags(const int32_t* d_wsrc, const uint8_t* d_ssrc, cons
     if (count == 0) return hipSuccess;
     hipLaunchKernelGGL(chain_flags_kernel, dim3((count + 255) / 256), dim3(256), 0, s, d_wsrc, d_ssrc, d_wbas,
                        d_sbas, count, dl, d_flags);
-    return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------------
-// Probe table (distinct weak keys).  Slot = (1 << 32) | key; 0 = empty.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t slot_hash(uint32_t key) {
-    uint32_t h = key * 0x9E3779B1u;
-    return h ^ (h >> 15);
-}
-
-__global__ void table_clear_kernel(unsigned long long* slots, uint64_t nslots, int hi) {
-    if (hi) __builtin_amdgcn_s_setprio(3);
-    for (uint64_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nslots; i += (uint64_t)gridDim.x * blockDim.x) slots[i] = 0ull;
-}
-
-__global__ void table_insert_kernel(unsigned long long* slots, uint32_t mask, const int32_t* __restrict__ keys,
-                                    uint32_t nkeys) {
-    __builtin_amdgcn_s_setprio(3);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nkeys) return;
-    const uint32_t key = (uint32_t)keys[i];
-    const unsigned long long v = (1ull << 32) | key;
-    uint32_t h = slot_hash(key) & mask;
-    for (uint32_t probes = 0; probes <= mask; ++probes) {
-        const unsigned long long prev = atomicCAS(&slots[h], 0ull, v);
-        if (prev == 0ull || prev == v) return;
-        h = (h + 1) & mask;
-    }
-}
-
-hipError_t launch_table_clear(unsigned long long* d_slots, uint64_t nslots, hipStream_t s, bool bg) {
-    const uint64_t cap = bg ? kBackgroundGroups : 2048u;
-    hipLaunchKernelGGL(table_clear_kernel, dim3((uint32_t)std::min<uint64_t>((nslots + 255) / 256, cap)), dim3(256), 0, s,
-                       d_slots, nslots, bg ? 0 : 1);
-    return hipGetLastError();
-}
-
-hipError_t launch_table_insert(unsigned long long* d_slots, uint32_t mask, const int32_t* d_keys, uint32_t nkeys,
-                               hipStream_t s) {
-    if (nkeys == 0) return hipSuccess;
-    hipLaunchKernelGGL(table_insert_kernel, dim3((nkeys + 255) / 256), dim3(256), 0, s, d_slots, mask, d_keys,
-                       nkeys);
-    return hipGetLastError();
-}
-
-__device__ __forceinline__ bool table_has(const ProbeTable& t, uint32_t key) {
-    const unsigned long long v = (1ull << 32) | key;
-    uint32_t h = slot_hash(key) & t.mask;
-    for (;;) {
-        const unsigned long long sl = t.slots[h];
-        if (sl == v) return true;
-        if (sl == 0ull) return false;
-        h = (h + 1) & t.mask;
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Weighted byte sums over a range: S1 = sum x_j, S2 = sum (j - org) * x_j (signed bytes, mod 2^32),
-// accumulated by one workgroup with 16-byte loads where the range is 16-aligned.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void dword_sums(uint32_t w, uint32_t rel, int32_t& s1, int32_t& s2) {
-    const int32_t a = __builtin_amdgcn_sdot4((int)w, 0x01010101, 0, false);
-    s1 += a;
-    s2 += (int32_t)(rel * (uint32_t)a) + __builtin_amdgcn_sdot4((int)w, 0x03020100, 0, false);
-}
-
-// Sums of bytes [lo, hi) (clipped to [0, n)) relative to origin org, over all threads of the block.
-// Returns this thread's partial; the caller reduces.
-__device__ __forceinline__ void range_sums(const uint8_t* __restrict__ x, int64_t n, int64_t lo, int64_t hi, int64_t org,
-                                           int32_t& s1, int32_t& s2) {
-    if (hi > n) hi = n;
-    if (lo >= hi) return;
-    const int t = threadIdx.x, T = blockDim.x;
-    int64_t a16 = (lo + 15) & ~(int64_t)15;
-    if (a16 > hi) a16 = hi;
-    const int64_t b16 = a16 + ((hi - a16) & ~(int64_t)15);
-    for (int64_t j = lo + t; j < a16; j += T) {  // unaligned head
-        const int32_t v = sbyte(x[j]);
-        s1 += v;
-        s2 += (int32_t)((uint32_t)(j - org) * (uint32_t)v);
-    }
-    // 64-B pieces per lane, eight 16-B loads in flight before any use (a 128 KiB window in a few round
-    // trips instead of one per 4 KiB: these single-workgroup reductions sit on the resolver's latency path)
-    int64_t j = a16 + 64 * (int64_t)t;
-    for (; j + 64 * (int64_t)T + 64 <= b16; j += 128 * (int64_t)T) {
-        uint4 v[8];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = *reinterpret_cast<const uint4*>(x + j + 16 * k);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[4 + k] = *reinterpret_cast<const uint4*>(x + j + 64 * (int64_t)T + 16 * k);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t rel = (uint32_t)(j + (k >= 4 ? 64 * (int64_t)T : 0) + 16 * (k & 3) - org);
-            dword_sums(v[k].x, rel, s1, s2);
-            dword_sums(v[k].y, rel + 4, s1, s2);
-            dword_sums(v[k].z, rel + 8, s1, s2);
-            dword_sums(v[k].w, rel + 12, s1, s2);
-        }
-    }
-    for (; j < b16; j += 64 * (int64_t)T) {  // remaining 64-B pieces (the last may be 16..48 B)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (j + 16 * k >= b16) break;
-            const uint4 v = *reinterpret_cast<const uint4*>(x + j + 16 * k);
-            const uint32_t rel = (uint32_t)(j + 16 * k - org);
-            dword_sums(v.x, rel, s1, s2);
-            dword_sums(v.y, rel + 4, s1, s2);
-            dword_sums(v.z, rel + 8, s1, s2);
-            dword_sums(v.w, rel + 12, s1, s2);
-        }
-    }
-    for (int64_t j = b16 + t; j < hi; j += T) {  // tail
-        const int32_t v = sbyte(x[j]);
-        s1 += v;
-        s2 += (int32_t)((uint32_t)(j - org) * (uint32_t)v);
-    }
-}
-
-template <int NV>
-__device__ __forceinline__ void block_reduce(int32_t (&v)[NV], int32_t* sh /* NV * blockDim / 64 */) {
-    const int t = threadIdx.x, nw = blockDim.x >> 6;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        int32_t x = v[i];
-        for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
-        v[i] = x;
-    }
-    __syncthreads();
-    if ((t & 63) == 0)
-#pragma unroll
-        for (int i = 0; i < NV; ++i) sh[i * nw + (t >> 6)] = v[i];
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        int32_t x = 0;
-        for (int w = 0; w < nw; ++w) x += sh[i * nw + w];
-        v[i] = x;
-    }
-    __syncthreads();
-}
-
-// exclusive scan over the block's threads (thread order), NV values at once
-template <int NV>
-__device__ __forceinline__ void block_exscan(int32_t (&v)[NV], int32_t* sh /* NV * blockDim / 64 */) {
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, nw = blockDim.x >> 6;
-    int32_t incl[NV];
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        int32_t x = v[i];
-        for (int d = 1; d < 64; d <<= 1) {
-            const int32_t y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        incl[i] = x;
-    }
-    __syncthreads();
-    if (lane == 63)
-#pragma unroll
-        for (int i = 0; i < NV; ++i) sh[i * nw + wv] = incl[i];
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        int32_t base = 0;
-        for (int w = 0; w < wv; ++w) base += sh[i * nw + w];
-        v[i] = base + incl[i] - v[i];
-    }
-    __syncthreads();
-}
-
-// ------------------------------------------------------------------------------------------------
-// Probe: first position in [a, b) whose Sender rolling key hits the table.  Positions are tiled in
-// aligned-block coordinates (block k = [kB, kB + B), tile = 4096 positions); one 256-lane workgroup per
-// tile, 16 positions per lane.  With o = kB and P1/P2 the prefix sums of x and (j - o) x from o:
-//   T(p) = (s1, s2),  s1 = P1(e) - P1(p),  s2 = (e - o) s1 - (P2(e) - P2(p)),  e = min(p + B, n),
-// and P1(o + B) = s1(o), P2(o + B) = B s1(o) - s2(o) from the source's own aligned sum T(o).  Lane start
-// values come from the workgroup's prefix of both streams (x[p] and x[p + B]); each lane then rolls its
-// 16 positions with the exact Java updates (Rolling.java:25-60) on R = T + E.
-// ------------------------------------------------------------------------------------------------
-constexpr int PROBE_THREADS = 256;
-constexpr int PROBE_PPT = 16;
-static_assert(PROBE_TILE == PROBE_THREADS * PROBE_PPT, "tile = threads x positions per thread");
-
-__device__ __forceinline__ int32_t roll_sub(int32_t cs, int32_t w, int32_t x) {  // Rolling.java:56-60
-    const uint32_t lo = ((uint32_t)cs & 0xFFFFu) - (uint32_t)x;
-    const uint32_t hi = ((uint32_t)cs >> 16) - (uint32_t)__mul24(w, x);  // (w <= B <= 2^17: a full-rate 24-bit multiply)
-    return (int32_t)((lo & 0xFFFFu) | (hi << 16));
-}
-__device__ __forceinline__ int32_t roll_add(int32_t cs, int32_t x) {  // Rolling.java:25-29
-    const uint32_t lo = ((uint32_t)cs & 0xFFFFu) + (uint32_t)x;
-    const uint32_t hi = ((uint32_t)cs >> 16) + lo;
-    return (int32_t)((lo & 0xFFFFu) | (hi << 16));
-}
-
-// 16 bytes at p (zero outside [0, n)) as 4 little-endian words: bytes stay packed in 4 VGPRs
-__device__ __forceinline__ void load16(const uint8_t* __restrict__ x, int64_t n, int64_t p, uint32_t (&w)[4]) {
-    if (p >= 0 && p + 16 <= n && ((reinterpret_cast<uintptr_t>(x + p) & 15) == 0)) {
-        const uint4 q = *reinterpret_cast<const uint4*>(x + p);
-        w[0] = q.x;
-        w[1] = q.y;
-        w[2] = q.z;
-        w[3] = q.w;
-    } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w[k] = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-            if (p + i < n && p + i >= 0) w[i >> 2] |= (uint32_t)x[p + i] << (8 * (i & 3));
-    }
-}
-__device__ __forceinline__ int32_t sbyte_of(const uint32_t (&w)[4], int i) {
-    return (int32_t)(int8_t)(uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-}
-
-// A lane's 16 keys at positions base + i (bit i of valid: in the interval): every hit goes to the file's hit list
-// (the first position by atomicMin, up to PROBE_HITS_CAP of them listed).  The stale digest's few keys (the batched
-// flush chain's probes over a file's rest) are compared against each key in turn; otherwise the 16 first hash slots
-// go out in one burst of independent loads -- most keys are decided by their first slot (load factor <= 1/2), so a
-// lane waits for about one L2 round trip -- and only keys whose first slot holds another key walk the probe path.
-// Branch free but for those walks and the (rare) hits.
-__device__ __forceinline__ void probe_check16(const ScanFile& F, const ProbeTable& table, int nsmall,
-                                              const uint32_t (&key)[16], uint32_t valid, int64_t base) {
-    uint32_t m = 0;
-    if (nsmall > 0) {
-        for (int j = 0; j < nsmall; ++j) {
-            const uint32_t kj = F.small[j];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) m |= (uint32_t)(key[i] == kj) << i;
-        }
-    } else {
-        unsigned long long sl[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sl[i] = (valid >> i) & 1u ? table.slots[slot_hash(key[i]) & table.mask] : 0ull;
-        uint32_t need = 0;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            if (sl[i] == ((1ull << 32) | key[i])) m |= 1u << i;
-            else if (sl[i] != 0ull) need |= 1u << i;
-        }
-        need &= valid;
-        while (need) {
-            const int i = __builtin_ctz(need);
-            uint32_t kk = 0;
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                if (j == i) kk = key[j];
-            if (table_has(table, kk)) m |= 1u << i;
-            need &= need - 1u;
-        }
-    }
-    m &= valid;
-    while (m) {
-        const int i = __builtin_ctz(m);
-        uint32_t kk = 0;
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-            if (j == i) kk = key[j];
-        const int64_t p = base + i;
-        atomicMin(&F.out->first, (unsigned long long)p);
-        const unsigned long long at = atomicAdd(&F.out->count, 1ull);
-        if (at < (unsigned long long)PROBE_HITS_CAP) {
-            F.out->pos[at] = (unsigned long long)p;
-            F.out->key[at] = kk;
-        }
-        m &= m - 1u;
-    }
-}
-
-// bit i set for positions base + i in [lo, hi), i < 16
-__device__ __forceinline__ uint32_t probe_valid16(int64_t base, int64_t lo, int64_t hi) {
-    const int64_t a = lo - base, b = hi - base;
-    if (b <= 0 || a >= 16 || b <= a) return 0u;
-    const int ia = a < 0 ? 0 : (int)a, ib = b > 16 ? 16 : (int)b;
-    return (0xFFFFu >> (16 - ib)) & (0xFFFFu << ia);
-}
-
-__global__ __launch_bounds__(PROBE_THREADS) void probe_first_kernel(ProbeArgs A) {
-    __builtin_amdgcn_s_setprio(3);  // resolver latency path: ahead of a co-running speculation launch
-    __shared__ int32_t sh[4 * PROBE_THREADS / 64];
-    const ProbeTile tile = A.tiles[blockIdx.x];
-    const ProbeIv I = A.ivs[tile.iv];
-    const ScanFile& F = A.files[I.file];
-    const int64_t n = F.n, B = F.B;
-    const uint8_t* __restrict__ data = F.data;
-    const ProbeTable table{F.slots, F.mask};
-    const int64_t k = tile.q0 / B;
-    const int64_t o = k * B;
-    const int64_t q0 = tile.q0;
-    int64_t qend = q0 + PROBE_TILE;
-    if (qend > o + B) qend = o + B;
-    if (q0 >= I.b || qend <= I.a || q0 >= n) return;  // uniform over the workgroup
-
-    // prefix of both streams from the block origin up to the tile: the partial sums of the tiles before it
-    int32_t head[4] = {0, 0, 0, 0};
-    const int ti = (int)((q0 - o) / PROBE_TILE);
-    if (ti > 0) {
-        if (tile.pbase < 0) {  // near the block start: re-read the <= PROBE_INLINE_TILES tiles before it
-            range_sums(data, n, o, q0, o, head[0], head[1]);
-            range_sums(data, n, o + B, q0 + B, o, head[2], head[3]);
-        } else if (threadIdx.x < ti) {
-            const int4 v = A.partials[tile.pbase + threadIdx.x];
-            head[0] = v.x;
-            head[1] = v.y;
-            head[2] = v.z;
-            head[3] = v.w;
-        }
-        block_reduce<4>(head, sh);
-    }
-
-    const int t = threadIdx.x;
-    const int64_t p0 = q0 + (int64_t)t * PROBE_PPT;
-    uint32_t xa[4], xb[4];
-    load16(data, n, p0, xa);
-    load16(data, n, p0 + B, xb);
-    int32_t part[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int32_t va = (p0 + i < n) ? sbyte_of(xa, i) : 0;
-        const int32_t vb = (p0 + B + i < n) ? sbyte_of(xb, i) : 0;
-        part[0] += va;
-        part[1] += (int32_t)((uint32_t)(p0 + i - o) * (uint32_t)va);
-        part[2] += vb;
-        part[3] += (int32_t)((uint32_t)(p0 + B + i - o) * (uint32_t)vb);
-    }
-    int32_t pre[4] = {part[0], part[1], part[2], part[3]};
-    block_exscan<4>(pre, sh);
-    if (p0 >= qend || p0 >= I.b || p0 + PROBE_PPT <= I.a) return;
-
-    const uint32_t pa = (uint32_t)(head[0] + pre[0]), pa2 = (uint32_t)(head[1] + pre[1]);  // P1(p0), P2(p0)
-    const uint32_t pb = (uint32_t)(head[2] + pre[2]), pb2 = (uint32_t)(head[3] + pre[3]);  // sums over [o+B, p0+B)
-    const int32_t To = F.aligned_weak[k];
-    const int64_t e0 = (o + B < n ? o + B : n);
-    const uint32_t s1o = (uint32_t)To & 0xFFFFu, s2o = (uint32_t)To >> 16;
-    const uint32_t P1e = s1o + pb;
-    const uint32_t P2e = (uint32_t)(e0 - o) * s1o - s2o + pb2;
-    const int64_t endq = (p0 + B < n ? p0 + B : n);
-    const uint32_t s1 = P1e - pa;
-    const uint32_t s2 = (uint32_t)(endq - o) * s1 - (P2e - pa2);
-    const int64_t nb = n - B;
-    auto clampB = [&](int64_t p) { return p < nb ? p : nb; };
-    const uint32_t ehi = I.e_hi + I.e_lo * (uint32_t)(clampB(p0) - clampB(I.anchor));
-    int32_t R = (int32_t)(((s1 + I.e_lo) & 0xFFFFu) | ((s2 + ehi) << 16));
-    // keys of all 16 positions first (ALU only), then their first hash slots in one burst of independent
-    // loads: a hit/miss is decided by the first slot for most keys (load factor <= 1/2), so a lane waits
-    // for about one L2 round trip instead of 16 serial ones
-    uint32_t key[PROBE_PPT];
-#pragma unroll
-    for (int i = 0; i < PROBE_PPT; ++i) {
-        key[i] = (uint32_t)R;
-        const int64_t p = p0 + i;
-        const int64_t w = (n - p < B ? n - p : B);
-        R = roll_sub(R, (int32_t)w, sbyte_of(xa, i));
-        if (n - (p + 1) >= B) R = roll_add(R, sbyte_of(xb, i));
-    }
-    probe_check16(F, table, F.nsmall, key, probe_valid16(p0, I.a, I.b < qend ? I.b : qend), p0);
-}
-
-__global__ void probe_out_reset_kernel(ProbeOut* out, uint32_t n) {
-    __builtin_amdgcn_s_setprio(3);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        out[i].first = ~0ull;
-        out[i].count = 0ull;
-    }
-}
-
-hipError_t launch_probe_out_reset(ProbeOut* d_out, uint32_t n, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(probe_out_reset_kernel, dim3((n + 255) / 256), dim3(256), 0, s, d_out, n);
-    return hipGetLastError();
-}
-
-// Pass 1: one workgroup per partial tile [q0, min(q0 + PROBE_TILE, o + B)), o = its block start.
-__global__ __launch_bounds__(256) void probe_partials_kernel(const ScanFile* __restrict__ files,
-                                                             const PartialTile* __restrict__ pt,
-                                                             int4* __restrict__ out) {
-    __builtin_amdgcn_s_setprio(3);
-    __shared__ int32_t sh[4 * 256 / 64];
-    const PartialTile t = pt[blockIdx.x];
-    const ScanFile& F = files[t.file];
-    const int64_t B = F.B, q0 = t.q0;
-    const int64_t o = q0 / B * B;
-    const int64_t qe = q0 + PROBE_TILE < o + B ? q0 + PROBE_TILE : o + B;
-    int32_t v[4] = {0, 0, 0, 0};
-    range_sums(F.data, F.n, q0, qe, o, v[0], v[1]);
-    range_sums(F.data, F.n, q0 + B, qe + B, o, v[2], v[3]);
-    block_reduce<4>(v, sh);
-    if (threadIdx.x == 0) out[blockIdx.x] = make_int4(v[0], v[1], v[2], v[3]);
-}
-
-void probe_partials(std::vector<ProbeTile>* tiles, size_t t0, int64_t B, int32_t file, std::vector<PartialTile>* out) {
-    int64_t cur_block = -1, covered = 0;  // tiles of cur_block already listed: [0, covered)
-    int32_t base = 0;
-    for (size_t i = t0; i < tiles->size(); ++i) {
-        ProbeTile& t = (*tiles)[i];
-        const int64_t k = t.q0 / B;
-        const int64_t ti = (t.q0 - k * B) / PROBE_TILE;
-        if (k != cur_block) {  // one file's tiles arrive in increasing position order
-            cur_block = k;
-            covered = 0;
-            base = (int32_t)out->size();
-        }
-        if (ti <= PROBE_INLINE_TILES) {  // the kernel re-reads the few tiles before it (no pass 1)
-            t.pbase = -1;
-            continue;
-        }
-        for (; covered < ti; ++covered) out->push_back(PartialTile{k * B + covered * PROBE_TILE, file, 0});
-        t.pbase = base;
-    }
-}
-
-// grid (1 + 16, nreq): block 0 computes T(p) and the key, blocks 1..16 copy the window.
-__global__ __launch_bounds__(256) void hit_window_kernel(const ScanFile* __restrict__ files,
-                                                         const ProbeIv* __restrict__ ivs,
-                                                         const int32_t* __restrict__ req) {
-    __builtin_amdgcn_s_setprio(3);
-    __shared__ int32_t sh[2 * 256 / 64];
-    const ScanFile& F = files[req[blockIdx.y]];
-    const unsigned long long f = F.out->first;
-    if (f == ~0ull) return;
-    const int64_t n = F.n, B = F.B;
-    const uint8_t* __restrict__ data = F.data;
-    const int64_t p = (int64_t)f;
-    const int64_t w = (n - p < B ? n - p : B);
-    if (blockIdx.x == 0) {
-        int32_t v[2] = {0, 0};
-        range_sums(data, n, p, p + w, p, v[0], v[1]);
-        block_reduce<2>(v, sh);
-        if (threadIdx.x == 0) {
-            const uint32_t S1 = (uint32_t)v[0];
-            const uint32_t S2 = (uint32_t)w * S1 - (uint32_t)v[1];
-            const int32_t T = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
-            *reinterpret_cast<int32_t*>(F.hit) = T;
-            // the file's interval holding p (disjoint, ascending) gives E(p); R = T + E is the key that hit
-            int32_t lo = F.iv0, hi = F.iv0 + F.niv - 1;
-            while (lo < hi) {
-                const int32_t mid = (lo + hi + 1) / 2;
-                if (ivs[mid].a <= p) lo = mid;
-                else hi = mid - 1;
-            }
-            const ProbeIv I = ivs[lo];
-            const int64_t nb = n - B;
-            const int64_t cp = p < nb ? p : nb, ca = I.anchor < nb ? I.anchor : nb;
-            const uint32_t ehi = I.e_hi + I.e_lo * (uint32_t)(cp - ca);
-            F.bucket[0] = 0;
-            F.bucket[1] = (int32_t)((((uint32_t)T + I.e_lo) & 0xFFFFu) | ((((uint32_t)T >> 16) + ehi) << 16));
-        }
-        if (threadIdx.x < PROBE_HITS_CAP) F.bucket[2 + HIT_BUCKET_CAP + (1 + LISTED_IDX) * threadIdx.x] = 0;
-        return;
-    }
-    // blocks 1 + 16 k .. 16 k + 16 copy window k: the k-th smallest listed hit (k = 0 is the first hit; the
-    // others only when the list is complete), so the resolver has the digest input of the next few
-    // events the hit list answers without another round trip
-    const int slot = (int)(blockIdx.x - 1) / 16, part = (int)(blockIdx.x - 1) % 16;
-    if (slot >= F.nwin) return;
-    int64_t pw = p;
-    if (slot > 0) {
-        const unsigned long long cnt = F.out->count;
-        if (cnt > (unsigned long long)PROBE_HITS_CAP || (unsigned long long)slot >= cnt) return;
-        __shared__ long long sel;
-        if (threadIdx.x == 0) sel = -1;
-        __syncthreads();
-        if (threadIdx.x < (int)cnt) {  // rank of entry t among the listed positions (distinct)
-            const unsigned long long me = F.out->pos[threadIdx.x];
-            int rank = 0;
-            for (int j = 0; j < (int)cnt; ++j) rank += F.out->pos[j] < me;
-            if (rank == slot) sel = (long long)me;
-        }
-        __syncthreads();
-        pw = (int64_t)sel;
-        if (pw < 0) return;
-    }
-    const int64_t ww = (n - pw < B ? n - pw : B);
-    uint8_t* __restrict__ h_win = F.hit + 16 + (int64_t)slot * B;
-    for (int64_t o = 16 * ((int64_t)part * blockDim.x + threadIdx.x); o < ww; o += 16 * 16 * (int64_t)blockDim.x) {
-        if (o + 16 <= ww) {
-            uint32_t q[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int i = 0; i < 16; ++i) q[i >> 2] |= (uint32_t)data[pw + o + i] << (8 * (i & 3));
-            *reinterpret_cast<uint4*>(h_win + o) = make_uint4(q[0], q[1], q[2], q[3]);
-        } else {
-            for (int64_t i = o; i < ww; ++i) h_win[i] = data[pw + i];
-        }
-    }
-}
-
-// The bucket of the hit key: chunk indices i with weak[i] == key (8 per lane); grid (., nreq).
-__global__ __launch_bounds__(256) void hit_bucket_kernel(const ScanFile* __restrict__ files,
-                                                         const int32_t* __restrict__ req) {
-    __builtin_amdgcn_s_setprio(3);
-    const ScanFile& F = files[req[blockIdx.y]];
-    if (F.out->first == ~0ull) return;
-    const int32_t C = F.C;
-    const int32_t i0 = 8 * (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
-    const int32_t key = F.bucket[1];
-    const int32_t* __restrict__ weak = F.table_weak;
-    // the listed hits' keys too (complete lists only): their buckets spare the host a lookup per event
-    // the hit list answers
-    __shared__ int32_t lkey[PROBE_HITS_CAP];
-    const unsigned long long cnt = F.out->count;
-    const int nl = cnt <= (unsigned long long)PROBE_HITS_CAP ? (int)cnt : 0;
-    if (threadIdx.x < nl) lkey[threadIdx.x] = (int32_t)F.out->key[threadIdx.x];
-    __syncthreads();
-    int32_t* __restrict__ lb = F.bucket + 2 + HIT_BUCKET_CAP;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int32_t i = i0 + k;
-        if (i >= C) break;
-        const int32_t wk = weak[i];
-        if (wk == key) {
-            const int32_t at = atomicAdd(&F.bucket[0], 1);
-            if (at < HIT_BUCKET_CAP) F.bucket[2 + at] = i;
-        }
-        for (int j = 0; j < nl; ++j)
-            if (wk == lkey[j]) {
-                const int32_t at = atomicAdd(&lb[(1 + LISTED_IDX) * j], 1);
-                if (at < LISTED_IDX) lb[(1 + LISTED_IDX) * j + 1 + at] = i;
-            }
-    }
-}
-
-hipError_t launch_hit_window(const ScanFile* files, const ProbeIv* ivs, const int32_t* req, int32_t nreq, int32_t max_C,
-                             hipStream_t s) {
-    if (nreq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(hit_window_kernel, dim3(1 + 16 * HIT_WINDOWS, (uint32_t)nreq), dim3(256), 0, s, files, ivs, req);
-    if (max_C > 0)
-        hipLaunchKernelGGL(hit_bucket_kernel, dim3((uint32_t)((max_C + 8 * 256 - 1) / (8 * 256)), (uint32_t)nreq),
-                           dim3(256), 0, s, files, req);
-    return hipGetLastError();
-}
-
-void probe_tiles(int64_t a, int64_t b, int64_t B, int32_t iv, std::vector<ProbeTile>* out) {
-    if (a >= b) return;
-    for (int64_t k = a / B; k <= (b - 1) / B; ++k) {
-        const int64_t o = k * B;
-        const int64_t lo = a > o ? a : o;
-        const int64_t hi = b < o + B ? b : o + B;
-        for (int64_t t = (lo - o) / PROBE_TILE; t <= (hi - 1 - o) / PROBE_TILE; ++t)
-            out->push_back(ProbeTile{o + t * PROBE_TILE, iv, -1});
-    }
-}
-
-int64_t probe_seg_len(int64_t full_positions, int64_t B) {
-    // segments pay off for big probes (a flush chain over a file's rest) at block lengths whose anchor (B bytes per
-    // workgroup) is small against the segment; a few long intervals keep the tiles' parallelism instead (a probe
-    // beside the speculation K1 sits on the resolver's latency path: 128 KiB blocks as 8-pass segments were 1 ms
-    // slower per config-5 step than as tiles)
-    if (opt(OPT_PROBE_LONG) == 0 || B > PROBE_LONG_MAX_B || full_positions < PROBE_LONG_BIG) return 0;
-    // ~1024 workgroups per unit of the option (one residency wave at 4 waves per SIMD), then longer ones
-    const int64_t passes = full_positions / (1024 * opt(OPT_PROBE_LONG) * PROBE_LONG_SUB);
-    return (passes < 1 ? 1 : passes > PROBE_LONG_PASSES ? PROBE_LONG_PASSES : passes) * PROBE_LONG_SUB;
-}
-
-int64_t probe_full_positions(int64_t a, int64_t b, int64_t n, int64_t B) {
-    const int64_t e = b < n - B + 1 ? b : n - B + 1;
-    return e > a ? e - a : 0;
-}
-
-void probe_plan(int64_t a, int64_t b, int64_t n, int64_t B, int32_t iv, int64_t seg_len, std::vector<ProbeTile>* tiles,
-                std::vector<ProbeSeg>* segs) {
-    const int64_t full_end = b < n - B + 1 ? b : n - B + 1;  // positions below it have a full window
-    if (seg_len <= 0 || full_end - a < PROBE_LONG_MIN) {
-        probe_tiles(a, b, B, iv, tiles);
-        return;
-    }
-    for (int64_t q = a & ~(int64_t)15; q < full_end; q += seg_len)
-        segs->push_back(ProbeSeg{q, iv, (int32_t)(full_end - q < seg_len ? full_end - q : seg_len)});
-    probe_tiles(full_end, b, B, iv, tiles);  // the shrinking windows near the end, if the interval reaches them
-}
-
-// Pass-free probe over long segments (see ProbeSeg): T(q0) digested by the workgroup once, then sub-segments of
-// PROBE_LONG_SUB positions in order: the lanes' start values from one exscan of their 64 positions' byte sums (both
-// streams, weights relative to the sub-segment's start), each lane rolls its 64 positions with the exact Java updates
-// on R = T + E and checks every key as probe_first_kernel does per tile, and the last lane's rolled value (less E)
-// anchors the next sub-segment.  One anchor and one launch slot per segment (up to PROBE_LONG_PASSES passes).
-__global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void probe_long_kernel(ProbeArgs A, const ProbeSeg* __restrict__ segs) {
-    __builtin_amdgcn_s_setprio(3);
-    __shared__ int32_t sh[4 * PROBE_THREADS / 64];
-    __shared__ int32_t s_next;  // T at the next sub-segment's start (packed halves)
-    const ProbeSeg g = segs[blockIdx.x];
-    const ProbeIv I = A.ivs[g.iv];
-    const ScanFile& F = A.files[I.file];
-    const int64_t n = F.n, B = F.B;
-    const uint8_t* __restrict__ data = F.data;
-    const int64_t q0 = g.q0, q1 = q0 + g.len;  // every window full: q1 - 1 <= n - B
-    const int64_t nb = n - B;
-    auto clampB = [&](int64_t p) { return p < nb ? p : nb; };
-    // the anchor: T(q0) = (sum x, sum (B - i) x_{q0 + i}) over the window [q0, q0 + B) (full: q0 <= n - B)
-    int32_t h[2] = {0, 0};
-    range_sums(data, n, q0, q0 + B, q0, h[0], h[1]);
-    block_reduce<2>(h, sh);
-    uint32_t s1o = (uint32_t)h[0], s2o = (uint32_t)B * (uint32_t)h[0] - (uint32_t)h[1];
-    const ProbeTable table{F.slots, F.mask};
-    const int nsmall = F.nsmall;
-    const int t = threadIdx.x;
-    for (int64_t base = q0; base < q1; base += PROBE_LONG_SUB) {
-        const int64_t p0 = base + (int64_t)t * PROBE_LONG_PPL;
-        int32_t pre[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int k = 0; k < PROBE_LONG_PPL / 16; ++k) {  // the lane's bytes at p0 and at p0 + B: its sums
-            uint32_t wa[4], wb[4];
-            load16(data, n, p0 + 16 * k, wa);
-            load16(data, n, p0 + B + 16 * k, wb);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                dword_sums(wa[j], (uint32_t)(p0 + 16 * k + 4 * j - base), pre[0], pre[1]);
-                dword_sums(wb[j], (uint32_t)(p0 + B + 16 * k + 4 * j - base), pre[2], pre[3]);
-            }
-        }
-        block_exscan<4>(pre, sh);  // sums over [base, p0) and [base + B, p0 + B), weights j - base
-        const bool live = p0 < q1;
-        if (live) {
-            const uint32_t P1e = s1o + (uint32_t)pre[2];
-            const uint32_t P2e = (uint32_t)B * s1o - s2o + (uint32_t)pre[3];
-            const uint32_t s1 = P1e - (uint32_t)pre[0];
-            const uint32_t s2 = (uint32_t)(p0 + B - base) * s1 - (P2e - (uint32_t)pre[1]);
-            const uint32_t ehi = I.e_hi + I.e_lo * (uint32_t)(clampB(p0) - clampB(I.anchor));
-            int32_t R = (int32_t)(((s1 + I.e_lo) & 0xFFFFu) | ((s2 + ehi) << 16));
-#pragma unroll 1
-            for (int grp = 0; grp < PROBE_LONG_PPL / 16; ++grp) {  // 16 positions at a time (bytes re-read: L1)
-                uint32_t wa[4], wb[4];
-                load16(data, n, p0 + 16 * grp, wa);
-                load16(data, n, p0 + B + 16 * grp, wb);
-                uint32_t key[16];
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {  // full windows throughout: w = B, the add always follows
-                    key[i] = (uint32_t)R;
-                    R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(wa, i)), sbyte_of(wb, i));
-                }
-                const uint32_t valid = probe_valid16(p0 + 16 * grp, I.a, I.b < q1 ? I.b : q1);
-                if (valid) probe_check16(F, table, nsmall, key, valid, p0 + 16 * grp);
-            }
-            if (t == PROBE_THREADS - 1) {  // R(p0 + 64) less E there: the next sub-segment's anchor T
-                const int64_t pn = p0 + PROBE_LONG_PPL;
-                const uint32_t en = I.e_hi + I.e_lo * (uint32_t)(clampB(pn) - clampB(I.anchor));
-                const uint32_t r = (uint32_t)R;
-                s_next = (int32_t)((((r & 0xFFFFu) - I.e_lo) & 0xFFFFu) | (((r >> 16) - en) << 16));
-            }
-        }
-        __syncthreads();
-        s1o = (uint32_t)s_next & 0xFFFFu;
-        s2o = (uint32_t)s_next >> 16;
-        __syncthreads();
-    }
-}
-
-hipError_t launch_probe_long(const ProbeArgs& args, const ProbeSeg* segs, uint32_t nsegs, hipStream_t s) {
-    if (nsegs == 0) return hipSuccess;
-    hipLaunchKernelGGL(probe_long_kernel, dim3(nsegs), dim3(PROBE_THREADS), 0, s, args, segs);
-    return hipGetLastError();
-}
-
-hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const PartialTile* ptiles, uint32_t nptiles,
-                              hipStream_t s) {
-    if (ntiles == 0) return hipSuccess;
-    if (nptiles > 0)
-        hipLaunchKernelGGL(probe_partials_kernel, dim3(nptiles), dim3(256), 0, s, args.files, ptiles, args.partials);
-    hipLaunchKernelGGL(probe_first_kernel, dim3(ntiles), dim3(PROBE_THREADS), 0, s, args);
-    return hipGetLastError();
-}
-
-
-// ------------------------------------------------------------------------------------------------
-// Chain advance (batched Sender scan, batch.cpp): one workgroup per file walks Sender.sendMatchesAndData
-// (Sender.java:1235-1327) on the device for as long as the state stays synced (no FileView flush since the last
-// match, so R = T) and unpoisoned (localChunkMd5sum == null, :1248) and every candidate digest comes from the
-// aligned speculation -- the resolver's steps (1), (1') at aligned positions and (2) (resolver.cpp), with the
-// candidate order of Checksum.getCandidateChunks (:206-276).  Anything else (a flush, a hit at an unaligned
-// position, a digest mismatch that poisons the cached digest, a bucket longer than CHAIN_BUCKET_CAP, the
-// shrinking windows at the end of a file with a remainder, a full event buffer) stops the walk before that step:
-// the host resolver resumes from the returned state and takes the step itself.  So the device emits exactly
-// the events the resolver would, in the same order.  In config 4's 50%-modified form (every other block
-// replaced) a file's run of MATCH / LIT pairs until its first false weak hit cost one device round trip per
-// pair on the host path; here the whole run is one launch for every file of the segment.
-//
-// All lanes keep the same copy of the state (s, mark, pref) and take the same decisions (every value they
-// branch on is read from global memory or LDS by all of them); lane 0 writes the events.
-// ------------------------------------------------------------------------------------------------
-// CHAIN_THREADS, CHAIN_PPT, CHAIN_TILE, CHAIN_SEGS: device.h (the host sizes the hit map with them)
-constexpr int CHAIN_EV_LDS = 64;  // events a walk holds in LDS before writing them out
-
-// A key's presence in a chunk index (launch_chunk_index: (key << 32) | (i + 1) per chunk, 0 = empty): every chunk
-// with the key lies on the key's probe path before its first empty slot
-__device__ __forceinline__ bool kslots_has(const unsigned long long* __restrict__ ks, uint32_t mask, uint32_t key) {
-    uint32_t h = slot_hash(key) & mask;
-    for (;;) {
-        const unsigned long long v = ks[h];
-        if (v == 0ull) return false;
-        if ((uint32_t)(v >> 32) == key) return true;
-        h = (h + 1) & mask;
-    }
-}
-
-// The chain walk's key set: the table's distinct weak sums in LDS as a bucketed cuckoo set -- 2 x 8192 buckets of 2
-// keys (128 KiB), a key in bucket h1(k) of the first half or h2(k) of the second.  A bucket's free slots hold its own
-// empty value, a key that can never live in that bucket (its hashes point elsewhere), so every 32-bit key -- 0
-// included -- is stored as itself, and a lookup is two 8-byte LDS reads and four compares, exact.  The hashes
-// multiply 24-bit folds of the key by 24-bit constants (full-rate v_mul_u32_u24; a 32-bit multiply issues at quarter
-// rate), a different fold per table, so that keys sharing one fold still part in the other table.  Config 4's 16384
-// keys fill half of it; a key still displaced after the insertion's bound (tables near or above 32768 distinct keys,
-// or keys crowding a few buckets) marks the set incomplete, and the walk then confirms every key in the chunk index.
-constexpr int CHAIN_CK_BUCKETS = 8192;
-__host__ __device__ constexpr uint32_t chain_ck_h1(uint32_t k) {
-    return (((k ^ (k >> 15)) & 0xFFFFFFu) * 0x9E3779u) >> 19;
-}
-__host__ __device__ constexpr uint32_t chain_ck_h2(uint32_t k) {
-    return CHAIN_CK_BUCKETS + ((((k ^ (k >> 8)) & 0xFFFFFFu) * 0x85EBCBu) >> 19);
-}
-// bucket i's empty value: 0, except in the two buckets key 0 hashes to, which use 1 (whose own buckets differ)
-__host__ __device__ constexpr uint32_t chain_ck_empty(uint32_t i) {
-    return (i == chain_ck_h1(0u) || i == chain_ck_h2(0u)) ? 1u : 0u;
-}
-static_assert(chain_ck_h1(1u) != chain_ck_h1(0u) && chain_ck_h2(1u) != chain_ck_h2(0u), "empty values");
-struct ChainKeySet {
-    uint2* b;       // 2 * CHAIN_CK_BUCKETS buckets
-    int32_t* full;  // some key found no slot: lookups are not exact
-};
-__device__ __forceinline__ void chain_ck_insert(const ChainKeySet& ks, uint32_t k) {
-    // cuckoo insertion: a free slot of the key's bucket in table w, else displace one of that bucket's keys and
-    // carry it to its bucket in the other table (every key lives in its own h1 or h2 bucket; slots only ever go
-    // from empty to a key)
-    uint32_t cur = k;
-    int w = 0;
-    for (int it = 0; it < 128; ++it) {
-        const uint32_t bi = w == 0 ? chain_ck_h1(cur) : chain_ck_h2(cur), e = chain_ck_empty(bi);
-        uint32_t* slot = reinterpret_cast<uint32_t*>(&ks.b[bi]);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const uint32_t old = atomicCAS(slot + j, e, cur);
-            if (old == e || old == cur) return;
-        }
-        const uint32_t old = atomicExch(slot + (it & 1), cur);
-        if (old == cur) return;
-        cur = old;
-        w ^= 1;
-    }
-    *ks.full = 1;  // a key is left over: the set is not exact
-}
-__device__ __forceinline__ bool chain_ck_has(const ChainKeySet& ks, uint32_t k) {
-    const uint2 a = ks.b[chain_ck_h1(k)], c = ks.b[chain_ck_h2(k)];
-    return a.x == k || a.y == k || c.x == k || c.y == k;
-}
-
-// bit i: keys[i] is in the key set (exact sets only).  Branch free: two 8-byte reads and four compares per key (a
-// wave's lanes would take every branch anyway)
-__device__ __forceinline__ uint32_t chain_mask16(const ChainKeySet& set, const uint32_t (&keys)[16]) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint32_t k = keys[i];
-        const uint2 x = set.b[chain_ck_h1(k)], y = set.b[chain_ck_h2(k)];
-        m |= (uint32_t)((x.x == k) | (x.y == k) | (y.x == k) | (y.y == k)) << i;
-        if ((i & 3) == 3) asm volatile("" ::: "memory");  // 4 keys' reads in flight at a time (registers)
-    }
-    return m;
-}
-
-// The first of a lane's 16 keys (bit i of valid: position i is in the search) that the table holds, or -1: the 16
-// first hash slots in one burst of independent loads (as probe_first_kernel: most keys are decided by their first
-// slot, so a lane waits for about one L2 round trip, not 16), then the full lookup only for keys whose first slot
-// holds another key, in order and only before the first certain hit (one out-of-line lookup loop, few registers)
-__device__ __forceinline__ int chain_first_hit16(const unsigned long long* __restrict__ ks, uint32_t kmask,
-                                                 const ChainKeySet& set, const uint32_t (&keys)[PROBE_PPT],
-                                                 uint32_t valid) {
-    // the key set in LDS: exact (the usual case), so the table in global memory is not touched at all
-    if (*set.full == 0) {
-        const uint32_t m = chain_mask16(set, keys) & valid;
-        return m ? __builtin_ctz(m) : -1;
-    }
-    uint32_t hit = 0, need = 0;
-    {
-        unsigned long long sl[PROBE_PPT];
-#pragma unroll
-        for (int i = 0; i < PROBE_PPT; ++i) sl[i] = (valid >> i) & 1u ? ks[slot_hash(keys[i]) & kmask] : 0ull;
-#pragma unroll
-        for (int i = 0; i < PROBE_PPT; ++i) {
-            if (sl[i] == 0ull) continue;
-            if ((uint32_t)(sl[i] >> 32) == keys[i]) hit |= 1u << i;
-            else need |= 1u << i;
-        }
-    }
-    hit &= valid;
-    need &= valid & (hit ? (hit & (0u - hit)) - 1u : 0xFFFFFFFFu);
-    while (need) {
-        const int i = __builtin_ctz(need);
-        uint32_t kk = 0;
-#pragma unroll
-        for (int j = 0; j < PROBE_PPT; ++j)
-            if (j == i) kk = keys[j];
-        if (kslots_has(ks, kmask, kk)) return i;
-        need &= need - 1u;
-    }
-    return hit ? __builtin_ctz(hit) : -1;
-}
-
-// An unaligned hit's window digest (MD5 of its L bytes, the seed appended, dl bytes kept), by the whole workgroup: the
-// bytes staged through LDS in pieces of CHAIN_WIN_BUF, then compressed by one lane on the VALU.  One message is one
-// dependent chain (~160 us for an 8 KiB window; a scalar-unit form measured slower: DESIGN.md section 5a).  Out of
-// line, so that the walk's tile search keeps its registers.
-constexpr int CHAIN_WIN_BUF = 16384;
-// Stage piece [c0, c0 + len) of the window at x into buf (16-byte aligned source loads, byte stores that take the
-// misalignment out; every granule overlaps the piece, so it lies in a page the source occupies) and, for the last
-// piece, the seed, 0x80, zeros and the message's bit length (L + 4 bytes) to a whole block.  Returns the padded length.
-__device__ __forceinline__ uint32_t chain_window_stage(const uint8_t* x, uint32_t L, uint32_t seed, uint8_t* buf,
-                                                       uint32_t c0) {
-    const int t = threadIdx.x;
-    const uint32_t len = L - c0 < (uint32_t)CHAIN_WIN_BUF ? L - c0 : (uint32_t)CHAIN_WIN_BUF;
-    const bool last = c0 + len == L;
-    const uintptr_t xa = reinterpret_cast<uintptr_t>(x) + c0, a0 = xa & ~(uintptr_t)15;
-    const int32_t shift = (int32_t)(xa - a0);
-    for (int32_t g = 16 * t; g < shift + (int32_t)len; g += 16 * CHAIN_THREADS) {
-        const uint4 q = *reinterpret_cast<const uint4*>(a0 + (uintptr_t)g);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int32_t o = g + k - shift;
-            if (o >= 0 && o < (int32_t)len) buf[o] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
-        }
-    }
-    const uint32_t plen = last ? ((len + 4 + 1 + 8 + 63) & ~63u) : len;
-    if (last && (uint32_t)t < plen - len) {
-        const uint32_t i = len + (uint32_t)t;
-        const uint64_t bits = ((uint64_t)L + 4) * 8;
-        uint32_t v = 0;
-        if (t < 4) v = (seed >> (8 * t)) & 0xFFu;
-        else if (t == 4) v = 0x80u;
-        else if (i >= plen - 8) v = (uint32_t)(bits >> (8 * (i - (plen - 8)))) & 0xFFu;
-        buf[i] = (uint8_t)v;
-    }
-    __syncthreads();
-    return plen;
-}
-// ... lane 0 compressing them on the VALU (md5_compress: v_bitop3 round functions), the words from LDS
-__device__ __attribute__((noinline)) void chain_window_digest(const uint8_t* x, uint32_t L, uint32_t dl, uint32_t seed,
-                                                              uint8_t* buf, uint8_t* dig) {
-    const int t = threadIdx.x;
-    Md5State st = md5_init();
-    for (uint32_t c0 = 0; c0 < L; c0 += CHAIN_WIN_BUF) {
-        const uint32_t plen = chain_window_stage(x, L, seed, buf, c0);
-        if (t == 0) {
-            const uint4* bq = reinterpret_cast<const uint4*>(buf);
-            for (uint32_t b = 0; b < plen / 64; ++b) {
-                uint32_t m[16];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint4 v = bq[4 * b + i];
-                    m[4 * i] = v.x, m[4 * i + 1] = v.y, m[4 * i + 2] = v.z, m[4 * i + 3] = v.w;
-                }
-                md5_compress(st, m);
-            }
-        }
-        __syncthreads();
-    }
-    if (t == 0) store_digest(dig, st, dl);
-    __syncthreads();
-}
-
-// dl (1..16) digest bytes at a, packed four to a word, zero past dl: every byte's load issued before any use (one
-// round trip, not dl), in as few loads as dl needs (4, 8 or 16; indices past dl re-read the last byte)
-template <int NB>
-__device__ __forceinline__ void chain_digest_load_n(const uint8_t* __restrict__ a, int dl, uint32_t (&w)[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) w[k] = 0u;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-        const uint32_t v = a[j < dl ? j : dl - 1];  // (unconditional: all NB loads go out together)
-        w[j >> 2] |= (j < dl ? v : 0u) << (8 * (j & 3));
-    }
-}
-__device__ __forceinline__ void chain_digest_load(const uint8_t* __restrict__ a, int dl, uint32_t (&w)[4]) {
-    if (dl <= 4) chain_digest_load_n<4>(a, dl, w);
-    else if (dl <= 8) chain_digest_load_n<8>(a, dl, w);
-    else chain_digest_load_n<16>(a, dl, w);
-}
-// a digest already in registers (bytes packed four to a word, zero past dl) against dl bytes at b
-__device__ __forceinline__ bool chain_digest_eq_reg(const uint32_t (&a)[4], const uint8_t* __restrict__ b, int dl) {
-    uint32_t w[4];
-    chain_digest_load(b, dl, w);
-    return ((a[0] ^ w[0]) | (a[1] ^ w[1]) | (a[2] ^ w[2]) | (a[3] ^ w[3])) == 0u;
-}
-__device__ __forceinline__ bool chain_digest_eq(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, int dl) {
-    uint32_t w[4];
-    chain_digest_load(a, dl, w);
-    return chain_digest_eq_reg(w, b, dl);
-}
-
-// A wide tile lane's sums over its 32 positions' bytes x at p0 and y at p0 + B, weights relative to the tile start
-// (base = p0 - q0): (sum x, sum (base + j) x, sum y, sum (base + B + j) y), j = 0..31 -- four bytes per v_dot4_i32_i8
-// against the byte weights j (signed bytes, as Java's)
-__device__ __forceinline__ void chain_lane_sums(const uint32_t (&xa)[2][4], const uint32_t (&xb)[2][4], uint32_t base,
-                                                uint32_t B, int32_t (&pre)[4]) {
-    int32_t sa = 0, ja = 0, sb = 0, jb = 0;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            const int wt = 0x03020100 + 0x04040404 * d + 0x10101010 * hh;  // bytes 16 hh + 4 d + 0..3
-            sa = __builtin_amdgcn_sdot4((int)xa[hh][d], 0x01010101, sa, false);
-            ja = __builtin_amdgcn_sdot4((int)xa[hh][d], wt, ja, false);
-            sb = __builtin_amdgcn_sdot4((int)xb[hh][d], 0x01010101, sb, false);
-            jb = __builtin_amdgcn_sdot4((int)xb[hh][d], wt, jb, false);
-        }
-    pre[0] = sa;
-    pre[1] = (int32_t)(base * (uint32_t)sa) + ja;
-    pre[2] = sb;
-    pre[3] = (int32_t)((base + B) * (uint32_t)sb) + jb;
-}
-
-// the table's distinct weak sums into the workgroup's key set
-__device__ __forceinline__ void chain_kset_build(const ChainKeySet& ks, const int32_t* __restrict__ weak, int64_t C) {
-    const int t = threadIdx.x;
-    for (int i = t; i < 2 * CHAIN_CK_BUCKETS; i += CHAIN_THREADS) {
-        const uint32_t e = chain_ck_empty((uint32_t)i);
-        ks.b[i] = make_uint2(e, e);
-    }
-    if (t == 0) *ks.full = 0;
-    __syncthreads();
-    for (int64_t c = t; c < C; c += CHAIN_THREADS) chain_ck_insert(ks, (uint32_t)weak[c]);
-    __syncthreads();
-}
-
-// the map's shared words: relaxed atomics at agent scope (the workgroups sit on different XCDs, whose L2s are not
-// coherent with each other); vector memory operations throughout
-__device__ __forceinline__ int32_t chain_ld(const int32_t* p) {
-    return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int64_t chain_ld64(const int64_t* p) {
-    return __hip_atomic_load(const_cast<int64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void chain_st(int32_t* p, int32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void chain_st64(int64_t* p, int64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// One tile of a file's hit map: positions [q0, q0 + CHAIN_TILE) below hend, q0 a multiple of CHAIN_TILE.  The keys
-// are the walk's wide-tile keys in the synced state (each lane anchored on its block's aligned sum T(o), the prefix
-// sums from one exscan rebased at each block's first lane, the head of the block the tile starts in); bit i of
-// lane t's word = position q0 + 32 t + i hits the key set.  Stored as (gen << 32) | bits, one 8-byte store.
-__device__ void chain_map_tile(const ChainFile& F, int64_t q0, uint32_t gen, const ChainKeySet& kset, int32_t* sh,
-                               int32_t (*s_seg)[4]) {
-    const int t = threadIdx.x;
-    const int64_t n = F.n, B = F.B, hend = F.hend;
-    const int64_t kb0 = q0 / B, o0 = kb0 * B;
-    int32_t head[4] = {0, 0, 0, 0};
-    if (q0 > o0) {
-        range_sums(F.data, n, o0, q0, o0, head[0], head[1]);
-        range_sums(F.data, n, o0 + B, q0 + B, o0, head[2], head[3]);
-        block_reduce<4>(head, sh);
-    }
-    const int64_t p0 = q0 + (int64_t)t * CHAIN_PPT;
-    const int64_t kb = p0 / B, o = kb * B;
-    uint32_t xa[2][4], xb[2][4];
-    load16(F.data, n, p0, xa[0]);
-    load16(F.data, n, p0 + 16, xa[1]);
-    load16(F.data, n, p0 + B, xb[0]);
-    load16(F.data, n, p0 + B + 16, xb[1]);
-    const bool live = p0 < hend;
-    const int32_t To = live ? F.aw[kb] : 0;
-    int32_t pre[4];
-    chain_lane_sums(xa, xb, (uint32_t)(p0 - q0), (uint32_t)B, pre);
-    block_exscan<4>(pre, sh);
-    if (p0 == o) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) s_seg[kb - kb0][v] = pre[v];
-    }
-    __syncthreads();
-    if (live) {
-        uint32_t pa, pa2, pb, pb2;
-        if (o < q0) {
-            const uint32_t d = (uint32_t)(q0 - o);
-            pa = (uint32_t)head[0] + (uint32_t)pre[0];
-            pa2 = (uint32_t)head[1] + (uint32_t)pre[1] + d * (uint32_t)pre[0];
-            pb = (uint32_t)head[2] + (uint32_t)pre[2];
-            pb2 = (uint32_t)head[3] + (uint32_t)pre[3] + d * (uint32_t)pre[2];
-        } else {
-            const int32_t* L = s_seg[kb - kb0];
-            const uint32_t d = (uint32_t)(o - q0);
-            pa = (uint32_t)(pre[0] - L[0]);
-            pa2 = (uint32_t)(pre[1] - L[1]) - d * pa;
-            pb = (uint32_t)(pre[2] - L[2]);
-            pb2 = (uint32_t)(pre[3] - L[3]) - d * pb;
-        }
-        const uint32_t s1o = (uint32_t)To & 0xFFFFu, s2o = (uint32_t)To >> 16;
-        const uint32_t P1e = s1o + pb;
-        const uint32_t P2e = (uint32_t)B * s1o - s2o + pb2;
-        uint32_t u1 = P1e - pa;
-        uint32_t u2 = (uint32_t)(p0 + B - o) * u1 - (P2e - pa2);
-        uint32_t bits = 0;
-#pragma unroll 1
-        for (int hh = 0; hh < 2; ++hh) {
-            uint32_t wa[4], wb[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                wa[j] = hh ? xa[1][j] : xa[0][j];
-                wb[j] = hh ? xb[1][j] : xb[0][j];
-            }
-            uint32_t keys[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                keys[i] = (u1 & 0xFFFFu) | (u2 << 16);
-                const int32_t xo = sbyte_of(wa, i), xi = sbyte_of(wb, i);
-                u1 += (uint32_t)(xi - xo);
-                u2 += u1 - (uint32_t)__mul24((int)B, xo);  // (B <= 2^17: a full-rate 24-bit multiply)
-            }
-            bits |= chain_mask16(kset, keys) << (16 * hh);
-        }
-        if (hend - p0 < 32) bits &= (1u << (uint32_t)(hend - p0)) - 1u;  // windows past hend: not searched
-        __hip_atomic_store(&F.hmap[p0 >> 5], ((unsigned long long)gen << 32) | bits, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();  // (s_seg and sh: the next tile)
-}
-
-constexpr int CHAIN_HELP_TILES = 4;   // a walk gets helpers once it has searched this many tiles
-constexpr int CHAIN_HELP_LEAD = 64;   // a helper stays with its file while the map leads the walk by fewer segments
-// A helper workgroup: while some walk that has searched CHAIN_HELP_TILES tiles is still running, take the next
-// unmapped segment of the one whose map leads it least (its own current file while the lead is short: the key set is
-// built per file) -- never the segment the walk is in, which it will finish first -- and map it tile by tile,
-// stopping when the walk ends or has passed the tile.  While walks are running that have not searched that far yet it
-// sleeps and looks again; once no mappable walk is running it leaves.  No walk ever waits for a helper: a walk reads
-// a map word only when it carries this launch's generation, and searches the tile itself otherwise.  (A helper waits
-// only for walks of its own launch, whose workgroups precede it in dispatch order.)
-__device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict__ files, int nfiles, uint32_t gen,
-                                                     ChainHelp* help, uint2* ck, int32_t* ck_full,
-                                                     int32_t* sh, int32_t (*s_seg)[4], unsigned long long* s_best,
-                                                     int32_t* s_word, int32_t* s_live) {
-    const int t = threadIdx.x;
-    const ChainKeySet kset{ck, ck_full};
-    int cur = -1;
-    ChainFile F = files[0];
-    for (;;) {
-        if (t == 0) {
-            *s_best = 0ull;
-            *s_live = 0;
-        }
-        __syncthreads();
-        for (int f = t; f < nfiles; f += CHAIN_THREADS) {
-            ChainHelp* h = help + f;
-            const int32_t nseg = h->nseg;  // (written by the host before the launch)
-            if (nseg == 0) continue;
-            // one round trip for the file's shared words
-            const int32_t live = chain_ld(&h->live), tiles = chain_ld(&h->tiles), claim = chain_ld(&h->claim);
-            const int32_t nhelp = chain_ld(&h->nhelp);
-            const int64_t pos = chain_ld64(&h->pos);
-            if (live == 0 || claim >= nseg) continue;
-            *s_live = 1;  // a walk that may still search: wait for it rather than leave
-            if (tiles < CHAIN_HELP_TILES) continue;
-            // the most urgent files first -- the map's frontier least far ahead of the walk, in four levels -- then
-            // the fewest helpers, then a hash that spreads the helpers; the current file while the map leads its
-            // walk by fewer than CHAIN_HELP_LEAD segments (its key set is built)
-            const int64_t lead = (int64_t)claim - pos / CHAIN_MAP_SEG;
-            const uint32_t level = lead <= 0 ? 3u : lead <= 4 ? 2u : lead <= 16 ? 1u : 0u;
-            const uint32_t few = 255u - (uint32_t)(nhelp < 0 ? 0 : nhelp > 255 ? 255 : nhelp);
-            const uint32_t tie = ((uint32_t)f * 0x9E3779B1u) ^ ((uint32_t)blockIdx.x * 0x85EBCA77u);
-            const unsigned long long key = ((unsigned long long)(f == cur && lead < CHAIN_HELP_LEAD) << 63) |
-                                           ((unsigned long long)level << 61) | ((unsigned long long)few << 53) |
-                                           ((unsigned long long)(tie >> 1) << 21) | (uint32_t)f;
-            atomicMax(s_best, key);
-        }
-        __syncthreads();
-        const unsigned long long best = *s_best;
-        const bool any_live = *s_live != 0;
-        __syncthreads();
-        if (best == 0ull) {
-            if (!any_live) break;  // every mappable walk has ended: nothing will come
-            __builtin_amdgcn_s_sleep(64);  // walks still short of CHAIN_HELP_TILES tiles: look again shortly
-            continue;
-        }
-        const int f = (int)(best & 0xFFFFFull);
-        ChainHelp* h = help + f;
-        if (t == 0) {  // the segment the walk is in and those behind it are skipped, not claimed one by one
-            atomicMax(&h->claim, (int32_t)(chain_ld64(&h->pos) / CHAIN_MAP_SEG) + 1);
-            *s_word = atomicAdd(&h->claim, 1);
-        }
-        __syncthreads();
-        const int32_t seg = *s_word;
-        __syncthreads();
-        if (seg >= h->nseg) continue;
-        if (f != cur) {
-            if (t == 0) {
-                if (cur >= 0) atomicSub(&help[cur].nhelp, 1);
-                atomicAdd(&h->nhelp, 1);
-            }
-            cur = f;
-            const int64_t tb = (int64_t)wall_clock64();
-            F = files[f];
-            chain_kset_build(kset, F.table_weak, F.C);
-            if (t == 0) {
-                atomicAdd((unsigned long long*)&h->t_kset, (unsigned long long)((int64_t)wall_clock64() - tb));
-                atomicAdd(&h->joins, 1);
-            }
-            if (*kset.full) {  // not exact: the walk confirms keys in the chunk index; no map for this file
-                if (t == 0) atomicMax(&h->claim, h->nseg);
-                __syncthreads();
-                continue;
-            }
-        }
-        const int64_t lo = (int64_t)seg * CHAIN_MAP_SEG, hi = lo + CHAIN_MAP_SEG < F.hend ? lo + CHAIN_MAP_SEG : F.hend;
-        bool whole = true;
-        for (int64_t q0 = lo; q0 < hi; q0 += CHAIN_TILE) {
-            if (t == 0) *s_word = chain_ld(&h->live) != 0 && chain_ld64(&h->pos) < q0 + CHAIN_TILE;
-            __syncthreads();
-            const bool go = *s_word != 0;
-            __syncthreads();
-            if (!go) {
-                whole = false;
-                break;
-            }
-            chain_map_tile(F, q0, gen, kset, sh, s_seg);
-        }
-        if (t == 0) {
-            atomicAdd(&h->mapped, 1);
-            if (whole) {
-                atomicAdd(&h->whole, 1);
-                atomicMin((unsigned long long*)&h->t_first, (unsigned long long)wall_clock64());
-            }
-        }
-    }
-    if (t == 0 && cur >= 0) atomicSub(&help[cur].nhelp, 1);
-}
-
-__global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const ChainFile* __restrict__ files, int phase,
-                                                                      int abort_gen, ChainHelp* help, int nfiles) {
-    __builtin_amdgcn_s_setprio(3);
-    __shared__ int32_t sh[4 * CHAIN_THREADS / 64];
-    __shared__ int32_t s_hit;                  // first hit in a tile (offset from the tile start), or INT_MAX
-    __shared__ uint32_t s_key;                 // its key
-    __shared__ int32_t s_bk[CHAIN_BUCKET_CAP];  // bucket of the key (ascending chunk index)
-    __shared__ int32_t s_nbk;
-    __shared__ int64_t s_zero;                 // first unset chain flag
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[CHAIN_WIN_BUF + 128];  // an unaligned window's bytes (its digest: s_dig)
-    __shared__ int32_t s_any;                  // some chunk carries the stale digest
-    __shared__ int32_t s_seg[CHAIN_SEGS][4];   // wide tiles: the exscan at each block's first lane
-    __shared__ uint2 s_ck[2 * CHAIN_CK_BUCKETS];  // the table's keys (ChainKeySet)
-    __shared__ int32_t s_ck_full;
-    __shared__ __attribute__((aligned(16))) uint8_t s_dig[16];
-    __shared__ rsh_event s_ev[CHAIN_EV_LDS];   // finished events not yet in F.ev
-    __shared__ unsigned long long s_best;      // helpers: the file to map next
-    __shared__ int32_t s_word, s_live;
-    const ChainKeySet kset{s_ck, &s_ck_full};
-    if ((int)blockIdx.x >= nfiles) {  // a helper workgroup (phase 0): it only maps
-        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live);
-        return;
-    }
-    // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
-    // fields across the loop (the event stores may alias it) -- a PCIe round trip each
-    const ChainFile F = files[blockIdx.x];
-    ChainHelp* const H = (phase == 0 && help != nullptr) ? help + blockIdx.x : nullptr;
-    if (H != nullptr && threadIdx.x == 0) chain_st64(&H->t_start, (int64_t)wall_clock64());
-    const uint32_t map_gen = (H != nullptr && F.hmap != nullptr) ? (uint32_t)abort_gen : 0u;  // 0: no map
-    ChainOut* out = F.out;
-    // phase 0 walks over the prefix speculation [0, na_a); phase 1 resumes the walks that reached its end
-    if (phase == 1 && out->status != CHAIN_MORE) return;
-    const int t = threadIdx.x;
-    const int64_t n = F.n, B = F.B, C = F.C;
-    const int dl = F.dl;
-    const int64_t S = F.rem > 0 ? F.rem : B;  // Checksum.java:131-137
-    const int64_t last = n - S, nB = n - B;
-    const int64_t na = phase == 0 ? F.na_a : F.na, nflags = na < C ? na : C;
-    const bool wide = (B % CHAIN_PPT) == 0 && B >= 512 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
-    int64_t s = out->s, m = out->m;
-    // The key set (~C LDS inserts, tens of microseconds) only if the walk may search: a walk that starts aligned on
-    // an unbroken run of chain flags up to the last window with a chunk (an identical file, or its rest after the
-    // prefix) follows the chain and never looks a key up; should it need one after all, it stops there (the host).
-    bool kset_built = true;
-    if (s % B == 0 && nflags >= na) {
-        if (t == 0) s_zero = nflags;
-        __syncthreads();
-        // one 16-byte line of flags per lane per pass (as in step (1) below), masked to [s / B, nflags)
-        const int64_t k = s / B;
-        const uintptr_t fa = reinterpret_cast<uintptr_t>(F.flags);
-        for (uintptr_t l0 = (fa + (uintptr_t)k) & ~(uintptr_t)15; l0 < fa + (uintptr_t)nflags;
-             l0 += 16u * CHAIN_THREADS) {
-            const uintptr_t la = l0 + 16u * (uintptr_t)t;
-            const int64_t jb = (int64_t)la - (int64_t)fa;
-            if (la < fa + (uintptr_t)nflags) {
-                uint32_t w[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
-                if (la + 16 <= fa + (uintptr_t)nflags) {
-                    const uint4 q = *reinterpret_cast<const uint4*>(la);
-                    w[0] = q.x, w[1] = q.y, w[2] = q.z, w[3] = q.w;
-                } else {
-                    for (int i = 0; i < 16; ++i)
-                        if (jb + i >= 0 && jb + i < nflags && F.flags[jb + i] == 0) w[i >> 2] &= ~(0xFFu << (8 * (i & 3)));
-                }
-                int64_t z = -1;
-#pragma unroll
-                for (int i = 15; i >= 0; --i)
-                    if (jb + i >= k && jb + i < nflags && ((w[i >> 2] >> (8 * (i & 3))) & 0xFFu) == 0u) z = jb + i;
-                if (z >= 0) atomicMin((unsigned long long*)&s_zero, (unsigned long long)z);
-            }
-        }
-        __syncthreads();
-        kset_built = s_zero < nflags;  // (uniform) a break in the chain: the walk will search
-        __syncthreads();
-    }
-    if (kset_built) chain_kset_build(kset, F.table_weak, C);
-    int32_t pref = out->pref;
-    int32_t nev = out->n_ev, status = CHAIN_STOP;
-    int64_t lit = out->literal, mat = out->matched, chain_matches = out->chain_matches, events = out->events;
-    int32_t tiles = out->tiles, digests = out->digests, poisoned = 0, dead = 0, mapped = out->mapped;
-    int32_t first_mapped = out->first_mapped;
-    int64_t flushes = out->flushes;
-    const int64_t tk0 = (int64_t)wall_clock64();
-    int64_t t_tiles = 0, t_check = 0, t_event = 0, t_digest = 0;
-    const uint8_t* stale = nullptr;  // poisoned: the cached digest
-    uint32_t dg[4] = {0u, 0u, 0u, 0u};  // the window's digest at the current event (poisoned: the stale one)
-    int64_t clear_to = -1;            // stopped at a flush point: no candidate in [s, clear_to]
-    int32_t why = CHAIN_WHY_NONE;
-    rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
-    bool have = false;
-    if (nev > 0) {  // phase 1: the last event stays open (a MATCH run may go on across the prefix's end)
-        pend = F.ev[nev - 1];
-        have = true;
-        --nev;
-    }
-    // Finished events collect in LDS and go to the event buffer (pinned host memory) CHAIN_EV_LDS at a time, one per
-    // thread: a store to host memory is a PCIe write whose completion the next vmcnt wait of its wave waits for (on
-    // gfx9 the counter covers stores too), so lane 0 writing each event itself held the walk ~1-2 us per event.
-    int32_t nev_w = nev;  // events already in F.ev
-    auto drain_ev = [&]() {  // (all threads)
-        __syncthreads();
-        for (int32_t i = t; i < nev - nev_w; i += CHAIN_THREADS) F.ev[nev_w + i] = s_ev[i];
-        nev_w = nev;
-        __syncthreads();
-    };
-    auto flush_pend = [&]() {  // (the loop drains at its top while fewer than CHAIN_EV_LDS - 8 are held)
-        if (have) {
-            if (t == 0) s_ev[nev - nev_w] = pend;
-            ++nev;
-        }
-        have = false;
-    };
-    auto emit_lit = [&](int64_t off, int64_t len) {  // Sender.sendDataFrom; zero-length calls write nothing
-        if (len <= 0) return;
-        flush_pend();
-        pend = rsh_event{off, len, RSH_EV_LITERAL, 0, 0, 0};
-        have = true;
-        lit += len;
-    };
-    auto emit_match = [&](int64_t off, int64_t len, int32_t idx, int32_t cnt) {
-        mat += len;
-        if (have && pend.kind == RSH_EV_MATCH && pend.index + pend.count == idx && pend.offset + pend.length == off) {
-            pend.count += cnt;
-            pend.length += len;
-            return;
-        }
-        flush_pend();
-        pend = rsh_event{off, len, RSH_EV_MATCH, idx, cnt, 0};
-        have = true;
-    };
-
-    for (;;) {
-        if (nev - nev_w >= CHAIN_EV_LDS - 8) drain_ev();  // (a step adds at most three)
-        if (nev + 3 > F.ev_cap) {  // room for a pending event, a literal and a match
-            why = CHAIN_WHY_EVCAP;
-            break;
-        }
-        if (s > last) {  // the loop ends (Sender.java:1313-1316)
-            emit_lit(m, n - m);
-            status = CHAIN_DONE;
-            why = CHAIN_WHY_END;
-            break;
-        }
-        // phase-shifted windows: the host's phase speculation.  A poisoned walk (a stale cached digest, quirk B) goes
-        // on from any position: only step (2) applies to it, and every candidate is compared with the stale digest
-        if (s % B != 0 && !poisoned) {
-            why = CHAIN_WHY_PHASE;
-            break;
-        }
-        const int64_t k = s / B;
-        const bool al = s % B == 0;
-        // the words steps (1), (1') and (2) look at first, loaded together: one global round trip per step instead of
-        // three in sequence (a desynced walk takes these steps once per event)
-        const uint8_t flag_k = (!poisoned && k == pref && k < nflags) ? F.flags[k] : (uint8_t)0;
-        const int32_t aw_k = (al && k < na) ? F.aw[k] : 0;
-        const int32_t tw_pref = (!poisoned && pref < C && k < na) ? F.table_weak[pref] : 0;
-        // (1) aligned chain: preferred index == k and source window k carries chunk k's sums
-        if (flag_k) {
-            if (t == 0) s_zero = nflags;
-            __syncthreads();
-            // one aligned 16-byte line of flags per lane per pass: an identical file's 16384 flags in two passes
-            // instead of 32 load-and-barrier rounds.  A line may start before flag k (or before the file's flags,
-            // inside the batch's flag buffer) and is masked to [k, nflags); a line past the end is read bytewise.
-            const uintptr_t fa = reinterpret_cast<uintptr_t>(F.flags);
-            for (uintptr_t l0 = (fa + (uintptr_t)k) & ~(uintptr_t)15; l0 < fa + (uintptr_t)nflags;
-                 l0 += 16u * CHAIN_THREADS) {
-                const uintptr_t la = l0 + 16u * (uintptr_t)t;
-                const int64_t jb = (int64_t)la - (int64_t)fa;  // flag index of the line's first byte
-                int64_t z = -1;
-                if (la < fa + (uintptr_t)nflags) {
-                    uint32_t w[4] = {0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
-                    if (la + 16 <= fa + (uintptr_t)nflags) {
-                        const uint4 q = *reinterpret_cast<const uint4*>(la);
-                        w[0] = q.x, w[1] = q.y, w[2] = q.z, w[3] = q.w;
-                    } else {
-                        for (int i = 0; i < 16; ++i)
-                            if (jb + i >= 0 && jb + i < nflags && F.flags[jb + i] == 0) w[i >> 2] &= ~(0xFFu << (8 * (i & 3)));
-                    }
-#pragma unroll
-                    for (int i = 15; i >= 0; --i)
-                        if (jb + i >= k && jb + i < nflags && ((w[i >> 2] >> (8 * (i & 3))) & 0xFFu) == 0u) z = jb + i;
-                }
-                if (z >= 0) atomicMin((unsigned long long*)&s_zero, (unsigned long long)z);
-                __syncthreads();
-                if (s_zero < nflags) break;
-            }
-            const int64_t j_end = s_zero;
-            __syncthreads();
-            const int64_t t_max = (last - s) / B + 1;
-            const int64_t tt = (j_end - k < t_max) ? j_end - k : t_max;
-            const int64_t j = k + tt, p = (s + tt * B < n) ? s + tt * B : n;
-            emit_lit(m, s - m);
-            emit_match(s, p - s, (int32_t)k, (int32_t)(j - k));
-            chain_matches += j - k;
-            s = m = p;
-            pref = (int32_t)j;
-            continue;
-        }
-        // (1') the window at s against chunk pref while both sums agree (windows s + iB, chunks pref + i)
-        if (!poisoned && pref < C && k < na) {
-            int64_t lim = na - k;
-            if (C - pref < lim) lim = C - pref;
-            if ((last - s) / B + 1 < lim) lim = (last - s) / B + 1;
-            int64_t tt = 0;
-            if (lim > 0 && aw_k == tw_pref && chain_digest_eq(F.as + k * dl, F.table_strong + (int64_t)pref * dl, dl)) {
-                tt = 1;
-                while (tt < lim && F.aw[k + tt] == F.table_weak[pref + tt] &&
-                       chain_digest_eq(F.as + (k + tt) * dl, F.table_strong + (pref + tt) * dl, dl))
-                    ++tt;
-            }
-            if (tt > 0) {
-                const int64_t p = (s + tt * B < n) ? s + tt * B : n;
-                emit_lit(m, s - m);
-                emit_match(s, p - s, pref, (int32_t)tt);
-                s = m = p;
-                pref += (int32_t)tt;
-                continue;
-            }
-        }
-        // (2) the next candidate event in [s, stop]
-        const int64_t f = (m + 10 * B <= n) ? m + 9 * B : INT64_MAX;
-        const int64_t stop = f < last ? f : last;
-        if (stop > nB) {  // shrinking windows near the end: the host
-            why = CHAIN_WHY_TAIL;
-            break;
-        }
-        // (see above: an unbroken chain needed no key set; should this step look a key up after all, the host takes
-        // it -- at the prefix's end the search is empty and the walk goes on to its cut, as with a key set)
-        if (!kset_built && (s / B < na || s <= (stop < na * B - 1 ? stop : na * B - 1))) {
-            why = CHAIN_WHY_NOKSET;
-            break;
-        }
-        int64_t p = -1;
-        uint32_t key = 0;
-        int64_t a = s;
-        if (al && k < na) {
-            key = (uint32_t)aw_k;
-            if (s_ck_full ? kslots_has(F.kslots, F.kmask, key) : chain_ck_has(kset, key)) p = s;
-            else a = s + 1;
-        }
-        bool cut = false;  // the search reached windows past the speculation (no anchor T(o))
-        if (wide) {
-            // tiles of CHAIN_TILE positions from a (lane-aligned), across block boundaries: each lane anchors its
-            // 16 positions on its own block's T(o); the prefix sums from o come from one exscan over the tile
-            // with weights relative to the tile start, rebased at each block's first lane (a segmented scan), and
-            // the head of the block the tile starts in (range_sums from o to the tile)
-            const int64_t lim_spec = na * B - 1;  // windows with an anchor: blocks < na
-            const int64_t qlast = stop < lim_spec ? stop : lim_spec;
-            if (H != nullptr && t == 0) {  // for the helpers: where this search starts, how many tiles so far
-                chain_st64(&H->pos, a);
-                chain_st(&H->tiles, tiles);
-            }
-            for (int64_t q0 = a & ~(int64_t)(CHAIN_PPT - 1); p < 0 && q0 <= qlast;) {
-                ++tiles;
-                const int64_t tt0 = (int64_t)wall_clock64();
-                if (map_gen != 0u) {
-                    // the tile from the hit map when every word it needs carries this launch's generation: lane t's
-                    // word holds positions [q0 + 32 t, + 32), masked to [a, qlast] (qlast < hend)
-                    const int64_t pm = q0 + (int64_t)t * CHAIN_PPT;
-                    const int64_t lo = a > pm ? a - pm : 0, hi = qlast - pm;
-                    const bool need = lo <= 31 && hi >= lo;
-                    unsigned long long wv = 0ull;
-                    if (need) wv = __hip_atomic_load(&F.hmap[pm >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    // beside it, the speculation's sum of an aligned window in the lane's range: a hit there needs
-                    // no second round trip for its key
-                    const bool al_lane = need && pm % B == 0;  // (pm <= qlast < na B)
-                    const int32_t awl = al_lane ? F.aw[pm / B] : 0;
-                    if (t == 0) s_hit = 0x7FFFFFFF;
-                    if (__syncthreads_and(!need || (uint32_t)(wv >> 32) == map_gen)) {
-                        if (need) {
-                            const uint32_t bits = (uint32_t)wv & (0xFFFFFFFFu >> (31 - (hi < 31 ? hi : 31))) &
-                                                  (0xFFFFFFFFu << lo);
-                            if (bits) atomicMin(&s_hit, (int32_t)(pm - q0) + __builtin_ctz(bits));
-                        }
-                        __syncthreads();
-                        const int32_t hoff = s_hit;
-                        if (hoff != 0x7FFFFFFF && al_lane && pm == q0 + hoff) s_key = (uint32_t)awl;
-                        __syncthreads();
-                        if (hoff != 0x7FFFFFFF) {  // the key: the window's true weak sum (synced)
-                            p = q0 + hoff;
-                            if (p % B == 0) {      // an aligned window: the speculation's sum, loaded above
-                                key = s_key;
-                            } else {               // else one reduction over its B bytes
-                                int32_t w2[2] = {0, 0};
-                                range_sums(F.data, n, p, p + B, p, w2[0], w2[1]);
-                                block_reduce<2>(w2, sh);
-                                const uint32_t S1 = (uint32_t)w2[0], S2 = (uint32_t)B * S1 - (uint32_t)w2[1];
-                                key = (S1 & 0xFFFFu) | (S2 << 16);
-                            }
-                        }
-                        if (mapped++ == 0) first_mapped = tiles;
-                        q0 += CHAIN_TILE;
-                        t_tiles += (int64_t)wall_clock64() - tt0;
-                        continue;
-                    }
-                }
-                const int64_t kb0 = q0 / B, o0 = kb0 * B;
-                int32_t head[4] = {0, 0, 0, 0};
-                if (q0 > o0) {
-                    range_sums(F.data, n, o0, q0, o0, head[0], head[1]);
-                    range_sums(F.data, n, o0 + B, q0 + B, o0, head[2], head[3]);
-                    block_reduce<4>(head, sh);
-                }
-                const int64_t p0 = q0 + (int64_t)t * CHAIN_PPT;
-                const int64_t kb = p0 / B, o = kb * B;
-                uint32_t xa[2][4], xb[2][4];
-                load16(F.data, n, p0, xa[0]);
-                load16(F.data, n, p0 + 16, xa[1]);
-                load16(F.data, n, p0 + B, xb[0]);
-                load16(F.data, n, p0 + B + 16, xb[1]);
-                const bool live = p0 <= stop && p0 <= lim_spec && p0 + CHAIN_PPT > a;
-                const int32_t To = live ? F.aw[kb] : 0;
-                int32_t pre[4];
-                chain_lane_sums(xa, xb, (uint32_t)(p0 - q0), (uint32_t)B, pre);
-                block_exscan<4>(pre, sh);  // sums over [q0, p0) and [q0 + B, p0 + B), weights j - q0
-                if (p0 == o) {              // a block's first lane: its rebasing point
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) s_seg[kb - kb0][v] = pre[v];
-                }
-                if (t == 0) s_hit = 0x7FFFFFFF;
-                __syncthreads();
-                const int64_t tc0 = (int64_t)wall_clock64();
-                int32_t my_hit = 0x7FFFFFFF;
-                uint32_t my_key = 0;
-                if (live) {
-                    uint32_t pa, pa2, pb, pb2;  // sums over [o, p0) and [o + B, p0 + B), weights j - o
-                    if (o < q0) {               // the tile's first block: its head + the tile's part
-                        const uint32_t d = (uint32_t)(q0 - o);
-                        pa = (uint32_t)head[0] + (uint32_t)pre[0];
-                        pa2 = (uint32_t)head[1] + (uint32_t)pre[1] + d * (uint32_t)pre[0];
-                        pb = (uint32_t)head[2] + (uint32_t)pre[2];
-                        pb2 = (uint32_t)head[3] + (uint32_t)pre[3] + d * (uint32_t)pre[2];
-                    } else {                    // rebased at the block's first lane
-                        const int32_t* L = s_seg[kb - kb0];
-                        const uint32_t d = (uint32_t)(o - q0);
-                        pa = (uint32_t)(pre[0] - L[0]);
-                        pa2 = (uint32_t)(pre[1] - L[1]) - d * pa;
-                        pb = (uint32_t)(pre[2] - L[2]);
-                        pb2 = (uint32_t)(pre[3] - L[3]) - d * pb;
-                    }
-                    const uint32_t s1o = (uint32_t)To & 0xFFFFu, s2o = (uint32_t)To >> 16;
-                    const uint32_t P1e = s1o + pb;
-                    const uint32_t P2e = (uint32_t)B * s1o - s2o + pb2;
-                    const uint32_t s1 = P1e - pa;
-                    const uint32_t s2 = (uint32_t)(p0 + B - o) * s1 - (P2e - pa2);
-                    // the lane's 32 positions as two halves of 16 (the first hit of the first half wins).  The two
-                    // 16-bit halves of the rolling value are kept apart (u1, u2: each exact mod 2^16, the Java
-                    // subtract-then-add of Rolling.java:25-60 in two adds each), packed into the key per position
-                    uint32_t u1 = s1, u2 = s2;
-                    const int64_t lim_p = stop < lim_spec ? stop : lim_spec;
-#pragma unroll 1
-                    for (int hh = 0; hh < 2; ++hh) {  // (not unrolled: one half's keys in registers at a time)
-                        uint32_t wa[4], wb[4];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            wa[j] = hh ? xa[1][j] : xa[0][j];
-                            wb[j] = hh ? xb[1][j] : xb[0][j];
-                        }
-                        uint32_t keys[16];
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            keys[i] = (u1 & 0xFFFFu) | (u2 << 16);
-                            const int32_t xo = sbyte_of(wa, i), xi = sbyte_of(wb, i);
-                            u1 += (uint32_t)(xi - xo);
-                            u2 += u1 - (uint32_t)__mul24((int)B, xo);  // (B <= 2^17: a full-rate 24-bit multiply)
-                        }
-                        // positions base + i with a <= position <= lim_p, as a bit range
-                        const int64_t base = p0 + 16 * hh;
-                        const int64_t lo = a > base ? a - base : 0, hi = lim_p - base;
-                        uint32_t valid = 0;
-                        if (lo <= 15 && hi >= 0 && hi >= lo)
-                            valid = (0xFFFFu >> (15 - (hi < 15 ? hi : 15))) & (0xFFFFu << lo);
-                        if (my_hit == 0x7FFFFFFF) {
-                            const int h = chain_first_hit16(F.kslots, F.kmask, kset, keys, valid);
-                            if (h >= 0) {
-                                my_hit = (int32_t)(p0 + 16 * hh + h - q0);
-#pragma unroll
-                                for (int i = 0; i < 16; ++i)  // (a static index: keys stays in registers)
-                                    if (i == h) my_key = keys[i];
-                            }
-                        }
-                    }
-                    if (my_hit != 0x7FFFFFFF) atomicMin(&s_hit, my_hit);
-                }
-                __syncthreads();
-                t_check += (int64_t)wall_clock64() - tc0;
-                if (my_hit != 0x7FFFFFFF && my_hit == s_hit) s_key = my_key;
-                __syncthreads();
-                if (s_hit != 0x7FFFFFFF) {
-                    p = q0 + s_hit;
-                    key = s_key;
-                }
-                __syncthreads();
-                q0 += CHAIN_TILE;
-                t_tiles += (int64_t)wall_clock64() - tt0;
-            }
-            cut = p < 0 && stop > lim_spec;  // (lim_spec, stop] has no anchors: not searched
-        }
-        // narrow blocks (B not a multiple of 16, or < 512): tiles of PROBE_TILE positions in block coordinates
-        for (int64_t q0 = (a / B) * B + ((a % B) / PROBE_TILE) * PROBE_TILE; !wide && p < 0 && q0 <= stop;) {
-            const int64_t kb = q0 / B, o = kb * B;
-            if (kb >= na) {
-                cut = true;
-                break;
-            }
-            int64_t qend = q0 + PROBE_TILE;
-            if (qend > o + B) qend = o + B;
-            ++tiles;
-            int32_t head[4] = {0, 0, 0, 0};
-            if (q0 > o) {  // prefix of both streams from the block origin up to the tile
-                range_sums(F.data, n, o, q0, o, head[0], head[1]);
-                range_sums(F.data, n, o + B, q0 + B, o, head[2], head[3]);
-                block_reduce<4>(head, sh);
-            }
-            const int64_t p0 = q0 + (int64_t)t * PROBE_PPT;
-            uint32_t xa[4], xb[4];
-            load16(F.data, n, p0, xa);
-            load16(F.data, n, p0 + B, xb);
-            int32_t part[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int i = 0; i < PROBE_PPT; ++i) {
-                const int32_t va = sbyte_of(xa, i), vb = sbyte_of(xb, i);
-                part[0] += va;
-                part[1] += (int32_t)((uint32_t)(p0 + i - o) * (uint32_t)va);
-                part[2] += vb;
-                part[3] += (int32_t)((uint32_t)(p0 + B + i - o) * (uint32_t)vb);
-            }
-            int32_t pre[4] = {part[0], part[1], part[2], part[3]};
-            block_exscan<4>(pre, sh);
-            if (t == 0) s_hit = 0x7FFFFFFF;
-            __syncthreads();
-            uint32_t keys[PROBE_PPT];
-            if (t < PROBE_THREADS && p0 < qend && p0 <= stop && p0 + PROBE_PPT > a) {
-                const uint32_t pa = (uint32_t)(head[0] + pre[0]), pa2 = (uint32_t)(head[1] + pre[1]);
-                const uint32_t pb = (uint32_t)(head[2] + pre[2]), pb2 = (uint32_t)(head[3] + pre[3]);
-                const int32_t To = F.aw[kb];
-                const uint32_t s1o = (uint32_t)To & 0xFFFFu, s2o = (uint32_t)To >> 16;
-                const uint32_t P1e = s1o + pb;
-                const uint32_t P2e = (uint32_t)B * s1o - s2o + pb2;  // windows inside [o, nB]: e0 = o + B
-                const uint32_t s1 = P1e - pa;
-                const uint32_t s2 = (uint32_t)(p0 + B - o) * s1 - (P2e - pa2);  // (p0 + B - o) s1 - sum (j - o) x_j
-                int32_t R = (int32_t)((s1 & 0xFFFFu) | (s2 << 16));  // synced: the key is the true weak sum
-#pragma unroll
-                for (int i = 0; i < PROBE_PPT; ++i) {
-                    keys[i] = (uint32_t)R;
-                    R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(xa, i)), sbyte_of(xb, i));
-                }
-                uint32_t valid = 0;
-#pragma unroll
-                for (int i = 0; i < PROBE_PPT; ++i) {
-                    const int64_t pp = p0 + i;
-                    if (pp >= a && pp <= stop && pp < qend) valid |= 1u << i;
-                }
-                const int h = chain_first_hit16(F.kslots, F.kmask, kset, keys, valid);
-                if (h >= 0) atomicMin(&s_hit, (int32_t)(p0 + h - q0));
-            }
-            __syncthreads();
-            if (s_hit != 0x7FFFFFFF && (s_hit >> 4) == t) {
-#pragma unroll
-                    for (int i = 0; i < PROBE_PPT; ++i)  // (a static index: keys stays in registers)
-                        if (i == (s_hit & 15)) s_key = keys[i];
-                }
-            __syncthreads();
-            if (s_hit != 0x7FFFFFFF) {
-                p = q0 + s_hit;
-                key = s_key;
-            }
-            __syncthreads();
-            q0 = qend;
-        }
-        if (p < 0) {
-            if (cut) {  // past the speculation: the rest of it (phase 1), or the host -- which also takes a
-                // poisoned walk (phase 1 starts from the unpoisoned state)
-                if (na < F.na && !poisoned) status = CHAIN_MORE;
-                why = CHAIN_WHY_CUT;
-                break;
-            }
-            if (f <= last) {  // a flush (quirk A): the host, which need not search [s, stop] again
-                clear_to = stop;
-                why = CHAIN_WHY_FLUSH;
-                break;
-            }
-            emit_lit(m, n - m);           // no candidate before the end
-            status = CHAIN_DONE;
-            s = n;
-            why = CHAIN_WHY_END;
-            break;
-        }
-        // the event at p: its bucket (Multimap order), the candidates of Checksum.getCandidateChunks
-        const int64_t te0 = (int64_t)wall_clock64();
-        ++events;
-        const int64_t kp = p / B;
-        const bool spec_digest = !poisoned && p % B == 0 && kp < na;
-        // the speculation's digest of an aligned window, loaded beside the bucket's slots (it depends only on p)
-        // ... and chunk kp's own digest beside it: the candidate of a window that sits where its chunk sat (identical
-        // stretches, edited blocks in place) is decided without another round trip
-        uint32_t dgk[4] = {0u, 0u, 0u, 0u};
-        const bool diag = spec_digest && kp < C;
-        if (spec_digest) chain_digest_load(F.as + kp * dl, dl, dg);
-        if (diag) chain_digest_load(F.table_strong + kp * dl, dl, dgk);
-        if (t < 64) {
-            // every chunk with this key lies on the probe path before the first empty slot: wave 0 reads 64 slots of
-            // it per round trip (one, nearly always) instead of one dependent load per slot
-            int32_t cnt = 0;
-            const unsigned long long* ks = F.kslots;
-            uint32_t h = slot_hash(key) & F.kmask;
-            for (bool more = true; more; h = (h + 64u) & F.kmask) {
-                const unsigned long long v = ks[(h + (uint32_t)t) & F.kmask];
-                const unsigned long long empty = __ballot(v == 0ull);
-                const int lim = empty ? __builtin_ctzll(empty) : 64;  // slots before the first empty one
-                const bool mine = t < lim && (uint32_t)(v >> 32) == key;
-                const unsigned long long hits = __ballot(mine);
-                const int at = cnt + __popcll(hits & ((1ull << t) - 1ull));
-                if (mine && at < CHAIN_BUCKET_CAP) s_bk[at] = (int32_t)((uint32_t)v - 1u);
-                cnt += __popcll(hits);
-                more = empty == 0ull;
-            }
-            if (t == 0) s_nbk = cnt;
-        }
-        __syncthreads();
-        if (t == 0) {
-            const int32_t cnt = s_nbk;
-            for (int i = 1; i < cnt && i < CHAIN_BUCKET_CAP; ++i)  // ascending chunk index (insertion order)
-                for (int j = i; j > 0 && s_bk[j - 1] > s_bk[j]; --j) {
-                    const int32_t x = s_bk[j];
-                    s_bk[j] = s_bk[j - 1];
-                    s_bk[j - 1] = x;
-                }
-        }
-        __syncthreads();
-        const int32_t size = s_nbk;
-        if (size == 0 || size > CHAIN_BUCKET_CAP) {
-            why = CHAIN_WHY_BUCKET;
-            break;
-        }
-        // closeIndexOf(bucket, pref) (Checksum.java:175-213): pref's position, else the first index above it,
-        // else the last; not length-filtered.  Then the others in ascending order with length == window.
-        int32_t l = 0, r = size - 1, init = -1;
-        while (l <= r) {
-            const int32_t mid = l + (r - l) / 2;
-            if (s_bk[mid] == pref) {
-                init = mid;
-                break;
-            }
-            if (s_bk[mid] < pref) l = mid + 1;
-            else r = mid - 1;
-        }
-        if (init < 0) init = l < size - 1 ? l : size - 1;
-        const int64_t w = B;  // p <= nB
-        // Sender.java:1259-1263: the window's digest -- the speculation's at aligned positions, else one lane digests
-        // the window here (lane_chunk_sums over the B bytes at p, the seed appended), the host path's md5_at
-        const uint8_t* md5c = poisoned ? stale : F.as + kp * dl;
-        if (!spec_digest && !poisoned) {
-            const int64_t td0 = (int64_t)wall_clock64();
-            chain_window_digest(F.data + p, (uint32_t)B, (uint32_t)dl, F.seed, s_win, s_dig);  // (ends with a barrier)
-            md5c = s_dig;
-            chain_digest_load(s_dig, dl, dg);
-            ++digests;
-            t_digest += (int64_t)wall_clock64() - td0;
-        }
-        int32_t hit = -1;
-        for (int32_t it = -1; it < size && hit < 0; ++it) {
-            int32_t pos;
-            if (it < 0) {
-                pos = init;
-            } else {
-                const int32_t c = s_bk[it];
-                const int64_t clen = (c == C - 1 && F.rem > 0) ? F.rem : B;  // Checksum.java:197-203
-                if (it == init || clen != w) continue;
-                pos = it;
-            }
-            const int32_t c = s_bk[pos];
-            const bool eq = (diag && c == kp) ? ((dg[0] ^ dgk[0]) | (dg[1] ^ dgk[1]) | (dg[2] ^ dgk[2]) | (dg[3] ^ dgk[3])) == 0u
-                                              : chain_digest_eq_reg(dg, F.table_strong + (int64_t)c * dl, dl);
-            if (eq) hit = c;
-        }
-        __syncthreads();
-        t_event += (int64_t)wall_clock64() - te0;
-        if (hit < 0) {
-            // the cached digest is stale from here on (quirk B): the walk goes on with it from p + 1, comparing every
-            // later candidate with it, up to the next flush point (a hit at the flush point itself flushes there: the
-            // host retakes that step from s)
-            if (p < f) {
-                s = p + 1;
-                if (poisoned) continue;  // (already stale: nothing changes)
-                poisoned = 1;
-                stale = md5c;
-                // no chunk carries the stale digest: nothing can match again (the host's closed form), so the
-                // file needs no more speculation
-                if (t == 0) s_any = 0;
-                __syncthreads();
-                {  // the stale digest is in dg; two chunks' digests per thread in flight at a time
-                    bool any = false;
-                    for (int64_t c = t; c < C; c += 2 * CHAIN_THREADS) {
-                        const int64_t c2 = c + CHAIN_THREADS < C ? c + CHAIN_THREADS : c;
-                        any |= chain_digest_eq_reg(dg, F.table_strong + c * dl, dl) |
-                               chain_digest_eq_reg(dg, F.table_strong + c2 * dl, dl);
-                    }
-                    if (any) s_any = 1;
-                }
-                __syncthreads();
-                dead = s_any == 0;
-                // dead: the host's closed form (resolver.cpp), here when its literals fit the event buffer -- the
-                // flushes at mark + 9B (one 10B literal each), then the rest (Sender.java:1313-1316)
-                if (dead) {
-                    const int64_t nfl = s <= last ? (n - m) / (10 * B) : 0;  // (the loop has ended: no flushes)
-                    if (nev + nfl + 3 <= F.ev_cap) {
-                        flush_pend();  // the literals themselves: one per thread (writes to pinned host memory)
-                        drain_ev();
-                        for (int64_t i = t; i < nfl; i += CHAIN_THREADS)
-                            F.ev[nev + i] = rsh_event{m + 10 * B * i, 10 * B, RSH_EV_LITERAL, 0, 0, 0};
-                        nev += (int32_t)nfl;
-                        nev_w = nev;
-                        lit += 10 * B * nfl;
-                        m += 10 * B * nfl;
-                        flushes += nfl;
-                        emit_lit(m, n - m);
-                        s = n;
-                        status = CHAIN_DONE;
-                        poisoned = 0;
-                    }
-                }
-                if (!dead) continue;  // some chunk carries it: the search goes on from p + 1
-                why = status == CHAIN_DONE ? CHAIN_WHY_CLOSED : CHAIN_WHY_DEADCAP;
-            } else {
-                why = CHAIN_WHY_FLUSHHIT;
-            }
-            break;
-        }
-        emit_lit(m, p - m);  // Sender.java:1265-1288
-        emit_match(p, w, hit, 1);
-        pref = hit + 1;
-        s = m = p + w;
-        poisoned = 0;  // a match clears the cached digest (Sender.java:1287)
-    }
-    flush_pend();
-    drain_ev();
-    if (t == 0) {
-        out->s = s;
-        out->m = m;
-        out->pref = pref;
-        out->status = status;
-        out->n_ev = nev;
-        out->tiles = tiles;
-        out->digests = digests;
-        out->flushes = flushes;
-        out->t_total += (int64_t)wall_clock64() - tk0;
-        out->t_tiles += t_tiles;
-        out->t_check += t_check;
-        out->t_event += t_event;
-        out->t_digest += t_digest;
-        out->spec_full = phase == 1;
-        out->mapped = mapped;
-        out->clear_to = clear_to;
-        out->why = why;
-        out->first_mapped = first_mapped;
-        // a file that needs no more speculation stops its phase-1 K1 groups (they poll this word); any other stop
-        // keeps them (the resolver's aligned lookups past the prefix use them)
-        const bool stop_spec = phase == 0 && F.abort && (status == CHAIN_DONE || dead);
-        out->aborted = stop_spec;
-        if (stop_spec) *(volatile int*)F.abort = abort_gen;
-        out->md5c_valid = poisoned;
-        if (poisoned)
-            for (int j = 0; j < dl && j < 16; ++j) out->md5c[j] = stale[j];
-        out->literal = lit;
-        out->matched = mat;
-        out->chain_matches = chain_matches;
-        out->events = events;
-    }
-    if (H != nullptr) {  // this walk is over: its helpers stop, and the workgroup helps the walks still searching
-        if (t == 0) chain_st(&H->live, 0);
-        __syncthreads();
-        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live);
-    }
-}
-
-hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s, int phase, int abort_gen,
-                                ChainHelp* help, uint32_t helpers) {
-    if (nfiles == 0) return hipSuccess;
-    if (phase != 0 || help == nullptr || nfiles >= (1u << 20)) {  // (helpers pick files by a 20-bit index)
-        help = nullptr;
-        helpers = 0;
-    }
-    hipLaunchKernelGGL(chain_advance_kernel, dim3(nfiles + helpers), dim3(CHAIN_THREADS), 0, s, files, phase,
-                       abort_gen, help, (int)nfiles);
-    return hipGetLastError();
-}
-
-// The chunk index of the chain walk: every chunk i of a file as (key << 32) | (i + 1) in an open-addressing table
-// (0 = empty); the chunks with one key all lie on that key's probe path before its first empty slot.
-// A thread's keys go in groups of CHUNK_INDEX_MLP: the group's first-slot CASes are issued back to back (independent
-// atomics, all in flight at once), and only a CAS that found its slot taken walks the probe path (a serial
-// CAS-then-next loop keeps one atomic round trip in flight per thread).  Config 4's 2 M chunks on the background
-// grid beside the prefix K1: the index now ends inside that launch instead of 0.03 ms after it.
-constexpr int CHUNK_INDEX_MLP = 8;
-__global__ void chunk_index_kernel(const TableEnt* __restrict__ ents, uint32_t nfiles) {
-    const TableEnt e = ents[blockIdx.y];
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < e.nkeys; i0 += CHUNK_INDEX_MLP * stride) {
-        unsigned long long v[CHUNK_INDEX_MLP], got[CHUNK_INDEX_MLP];
-        uint32_t h[CHUNK_INDEX_MLP];
-#pragma unroll
-        for (int j = 0; j < CHUNK_INDEX_MLP; ++j) {
-            const int64_t i = i0 + j * stride;
-            const uint32_t key = i < e.nkeys ? (uint32_t)e.keys[i] : 0u;
-            v[j] = ((unsigned long long)key << 32) | (uint32_t)(i + 1);
-            h[j] = slot_hash(key) & e.mask;
-        }
-#pragma unroll
-        for (int j = 0; j < CHUNK_INDEX_MLP; ++j)
-            got[j] = i0 + j * stride < e.nkeys ? atomicCAS(&e.slots[h[j]], 0ull, v[j]) : 0ull;
-#pragma unroll
-        for (int j = 0; j < CHUNK_INDEX_MLP; ++j) {
-            if (got[j] == 0ull) continue;
-            uint32_t hh = (h[j] + 1) & e.mask;
-            while (atomicCAS(&e.slots[hh], 0ull, v[j]) != 0ull) hh = (hh + 1) & e.mask;
-        }
-    }
-    (void)nfiles;
-}
-
-hipError_t launch_chunk_index(const TableEnt* ents, uint32_t nfiles, int32_t max_keys, hipStream_t s, bool bg) {
-    if (nfiles == 0 || max_keys <= 0) return hipSuccess;
-    const uint32_t gx = (uint32_t)std::min<int64_t>((max_keys + 255) / 256, bg ? 2 : 64);
-    hipLaunchKernelGGL(chunk_index_kernel, dim3(gx, nfiles), dim3(256), 0, s, ents, nfiles);
-    return hipGetLastError();
-}
-
-__global__ void gather_bytes_kernel(const ScanFile* __restrict__ files, const GatherEnt* __restrict__ ents, uint32_t n,
-                                    uint8_t* __restrict__ out) {
-    __builtin_amdgcn_s_setprio(3);
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        const GatherEnt e = ents[i];
-        out[i] = files[e.file].data[e.p];
-    }
-}
-
-hipError_t launch_gather_bytes(const ScanFile* files, const GatherEnt* ents, uint32_t n, uint8_t* out, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(gather_bytes_kernel, dim3((n + 255) / 256), dim3(256), 0, s, files, ents, n, out);
-    return hipGetLastError();
-}
-
-// Device bytes -> pinned host memory, as a kernel: the runtime's copy path can queue behind a
-// co-running speculation launch, a high-priority kernel does not.  Thread t assembles bytes
-// [16t, 16t + 16) and writes them with one 16-byte store (dst 16-byte aligned).
-__device__ __forceinline__ void copy_piece(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int64_t n,
-                                           int64_t o) {
-    if (o + 16 <= n) {
-        uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i >> 2] |= (uint32_t)src[o + i] << (8 * (i & 3));
-        *reinterpret_cast<uint4*>(dst + o) = make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-        for (int64_t i = o; i < n; ++i) dst[i] = src[i];
-    }
-}
-
-__global__ __launch_bounds__(256) void copy_to_host_kernel(const uint8_t* __restrict__ src, int64_t n,
-                                                           uint8_t* __restrict__ dst) {
-    __builtin_amdgcn_s_setprio(3);
-    const int64_t o = 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-    if (o < n) copy_piece(src, dst, n, o);
-}
-
-hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    const int64_t threads = (n + 15) / 16;
-    hipLaunchKernelGGL(copy_to_host_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, d_src, n, h_dst);
-    return hipGetLastError();
-}
-
-// The last workgroup of a stamped launch.  No fence per workgroup: on this chip a fence at agent scope writes the
-// XCD's L2 back (its L2s are not coherent with each other), and one per workgroup cost the first version ~230 us for
-// 2304 workgroups (r5j trace).  Instead every thread waits for its own memory operations (vmcnt also counts stores and
-// atomics here), then one thread per workgroup counts the workgroup done with a device atomic; the workgroup that
-// completes the count -- its reads of the others' results are device atomics too -- releases at system scope once and
-// writes the stamp, which the host polls before it reads what the launch wrote to host memory.
-__device__ __forceinline__ bool stamp_arrive(const Stamp& st, bool* sh_last) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) *sh_last = atomicAdd(st.counter, 1u) == gridDim.x * gridDim.y - 1;
-    __syncthreads();
-    return *sh_last;
-}
-__device__ __forceinline__ void stamp_write(const Stamp& st) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        atomicExch(st.counter, 0u);
-        __threadfence_system();
-        __hip_atomic_store(st.stamp, st.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-__global__ __launch_bounds__(256) void chain_flags_stamped_kernel(const int32_t* __restrict__ wsrc,
-                                                                  const uint8_t* __restrict__ ssrc,
-                                                                  const int32_t* __restrict__ wbas,
-                                                                  const uint8_t* __restrict__ sbas, uint32_t count,
-                                                                  uint32_t dl, uint8_t* __restrict__ flags, Stamp st) {
-    __shared__ bool last;
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < count) {
-        bool eq = wsrc[k] == wbas[k];
-        for (uint32_t j = 0; j < dl; ++j) eq &= ssrc[(size_t)k * dl + j] == sbas[(size_t)k * dl + j];
-        flags[k] = eq ? 1 : 0;
-    }
-    if (stamp_arrive(st, &last)) stamp_write(st);
-}
-
-hipError_t launch_chain_flags_stamped(const int32_t* d_wsrc, const uint8_t* d_ssrc, const int32_t* d_wbas,
-                                      const uint8_t* d_sbas, uint32_t count, uint32_t dl, uint8_t* h_flags,
-                                      Stamp st, hipStream_t s) {
-    hipLaunchKernelGGL(chain_flags_stamped_kernel, dim3(count ? (count + 255) / 256 : 1), dim3(256), 0, s, d_wsrc,
-                       d_ssrc, d_wbas, d_sbas, count, dl, h_flags, st);
-    return hipGetLastError();
-}
-
-// blockIdx.x < nsamp * pieces: piece (blockIdx.x % pieces) of sample window blockIdx.x / pieces; the blocks past them
-// copy window 0 to the host, 4 KiB each.
-__global__ __launch_bounds__(256) void scan_prep_kernel(ScanPrep P) {
-    __shared__ int32_t sh[2 * 4];
-    __shared__ bool last;
-    const uint32_t b = blockIdx.x, nsum = P.nsamp * P.pieces;
-    if (b < nsum) {
-        const uint32_t i = b / P.pieces, q = b % P.pieces;
-        const int64_t p = P.wins[i] * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
-        const int64_t plen = ((w + P.pieces - 1) / P.pieces + 15) & ~(int64_t)15;
-        const int64_t lo = p + (int64_t)q * plen, hi = lo + plen < p + w ? lo + plen : p + w;
-        int32_t v[2] = {0, 0};
-        range_sums(P.data, P.n, lo, hi, p, v[0], v[1]);
-        block_reduce<2>(v, sh);
-        if (threadIdx.x == 0) {
-            atomicAdd(&P.scratch[2 * i], v[0]);
-            atomicAdd(&P.scratch[2 * i + 1], v[1]);
-        }
-    } else {
-        const int64_t o = 16 * ((int64_t)(b - nsum) * blockDim.x + threadIdx.x);
-        if (o < P.w0_len) copy_piece(P.data, P.w0, P.w0_len, o);
-    }
-    if (!stamp_arrive(P.st, &last)) return;
-    for (uint32_t i = threadIdx.x; i < P.nsamp; i += blockDim.x) {
-        const int64_t k = P.wins[i], p = k * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
-        const uint32_t S1 = (uint32_t)atomicExch(&P.scratch[2 * i], 0);
-        const uint32_t U = (uint32_t)atomicExch(&P.scratch[2 * i + 1], 0);
-        const uint32_t S2 = (uint32_t)w * S1 - U;
-        P.out_t[i] = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
-        P.out_w[i] = k < P.C ? P.table_weak[k] : 0;
-    }
-    stamp_write(P.st);
-}
-
-hipError_t launch_scan_prep(const ScanPrep& P, hipStream_t s) {
-    const uint32_t copy_blocks = (uint32_t)((P.w0_len + 16 * 256 - 1) / (16 * 256));
-    hipLaunchKernelGGL(scan_prep_kernel, dim3(P.nsamp * P.pieces + copy_blocks), dim3(256), 0, s, P);
-    return hipGetLastError();
-}
-
-// grid (., n): entry blockIdx.y, 16 bytes per thread, grid-strided over the entry's length
-__global__ __launch_bounds__(256) void copy_many_kernel(const CopyEnt* __restrict__ ents, int hi) {
-    if (hi) __builtin_amdgcn_s_setprio(3);
-    const CopyEnt e = ents[blockIdx.y];
-    for (int64_t o = 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); o < e.len;
-         o += 16 * (int64_t)gridDim.x * blockDim.x)
-        copy_piece(e.src, e.dst, e.len, o);
-}
-
-hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hipStream_t s, bool bg) {
-    if (n == 0 || max_len <= 0) return hipSuccess;
-    const int64_t blocks = bg ? 1 : std::min<int64_t>((max_len + 16 * 256 - 1) / (16 * 256), 64);
-    hipLaunchKernelGGL(copy_many_kernel, dim3((uint32_t)blocks, n), dim3(256), 0, s, ents, bg ? 0 : 1);
-    return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------------
-// True weak sums at arbitrary positions (one workgroup per position).
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void window_weak_kernel(const ScanFile* __restrict__ files,
-                                                          const GatherEnt* __restrict__ ents,
-                                                          int32_t* __restrict__ out) {
-    __builtin_amdgcn_s_setprio(3);
-    __shared__ int32_t sh[2 * 256 / 64];
-    const GatherEnt e = ents[blockIdx.x];
-    const ScanFile& F = files[e.file];
-    const int64_t p = e.p, n = F.n, B = F.B;
-    const int64_t w = (n - p < B ? n - p : B);
-    int32_t v[2] = {0, 0};
-    range_sums(F.data, n, p, p + w, p, v[0], v[1]);
-    block_reduce<2>(v, sh);
-    if (threadIdx.x == 0) {
-        const uint32_t S1 = (uint32_t)v[0];
-        const uint32_t S2 = (uint32_t)w * S1 - (uint32_t)v[1];
-        const int32_t T = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
-        if (e.by_block) F.aligned_weak[p / B] = T;
-        else out[blockIdx.x] = T;
-    }
-}
-
-hipError_t launch_window_weak(const ScanFile* files, const GatherEnt* ents, uint32_t n, int32_t* out, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(window_weak_kernel, dim3(n), dim3(256), 0, s, files, ents, out);
-    return hipGetLastError();
-}
-
-// D dwordx4 loads in flight per thread before their stores; NTL / NTS: non-temporal loads / stores.  The production
-// form is <1024, 4, true, true>; the others are kbench A/Bs (KBENCH_GATHER).
-template <int T, int D, bool NTL, bool NTS>
-__global__ __launch_bounds__(T) void gather_ops_kernel_t(const GatherOp* __restrict__ ops) {
-    const GatherOp op = ops[blockIdx.x];
-    const uintptr_t d = reinterpret_cast<uintptr_t>(op.dst);
-    int64_t head = (int64_t)((16 - (d & 15)) & 15);
-    if (head > op.len) head = op.len;
-    const int t = threadIdx.x;
-    if (t < head) op.dst[t] = op.src[t];
-    const int64_t body = (op.len - head) & ~(int64_t)15;
-    const uint8_t* __restrict__ s = op.src + head;
-    uint8_t* __restrict__ o = op.dst + head;
-    if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) {  // 16-B aligned source: dwordx4 loads, 4 in flight
-        const int64_t step = 16 * (int64_t)T;
-        int64_t k = 16 * (int64_t)t;
-        for (; k + (D - 1) * step < body; k += D * step) {
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 v[D];
-#pragma unroll
-            for (int u = 0; u < D; ++u) {
-                const u32x4* a = reinterpret_cast<const u32x4*>(s + k + u * step);
-                if constexpr (NTL) v[u] = __builtin_nontemporal_load(a);
-                else v[u] = *a;
-            }
-#pragma unroll
-            for (int u = 0; u < D; ++u) {
-                u32x4* a = reinterpret_cast<u32x4*>(o + k + u * step);
-                if constexpr (NTS) __builtin_nontemporal_store(v[u], a);
-                else *a = v[u];
-            }
-        }
-        for (; k < body; k += step)
-            *reinterpret_cast<uint4*>(o + k) = *reinterpret_cast<const uint4*>(s + k);
-    } else if ((reinterpret_cast<uintptr_t>(s) & 3) == 0) {  // word-aligned source: four dword loads per store
-        for (int64_t k = 16 * (int64_t)t; k < body; k += 16 * (int64_t)blockDim.x) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(s + k);
-            *reinterpret_cast<uint4*>(o + k) = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-    } else {
-        for (int64_t k = 16 * (int64_t)t; k < body; k += 16 * (int64_t)blockDim.x) {
-            uint32_t q[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int i = 0; i < 16; ++i) q[i >> 2] |= (uint32_t)s[k + i] << (8 * (i & 3));
-            *reinterpret_cast<uint4*>(o + k) = make_uint4(q[0], q[1], q[2], q[3]);
-        }
-    }
-    for (int64_t k = head + body + t; k < op.len; k += blockDim.x) op.dst[k] = op.src[k];
-}
-
-hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s, int64_t avg_len) {
-    if (n == 0) return hipSuccess;
-    if (avg_len < (64 << 10)) {  // short ops (a segment's 8 KiB literal tokens and blocks): 256 threads each
-        hipLaunchKernelGGL((gather_ops_kernel_t<256, 2, true, true>), dim3(n), dim3(256), 0, s, ops);
-        return hipGetLastError();
-    }
-    // 1024 threads per 1 MiB op (16 waves per CU in flight): 0.754 of the 8 TB/s peak (read + write) against 0.680 for
-    // 256 threads, kbench KBENCH_GATHER (profiles/r4/r4e_kbench_gather.log)
-    hipLaunchKernelGGL((gather_ops_kernel_t<1024, 4, true, true>), dim3(n), dim3(1024), 0, s, ops);
-    return hipGetLastError();
-}
-#ifdef RSH_KBENCH
-hipError_t launch_gather_ops_variant(int v, const GatherOp* ops, uint32_t n, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    switch (v) {
-        case 1: hipLaunchKernelGGL((gather_ops_kernel_t<256, 8, true, true>), dim3(n), dim3(256), 0, s, ops); break;
-        case 2: hipLaunchKernelGGL((gather_ops_kernel_t<512, 4, true, true>), dim3(n), dim3(512), 0, s, ops); break;
-        case 3: hipLaunchKernelGGL((gather_ops_kernel_t<256, 4, false, true>), dim3(n), dim3(256), 0, s, ops); break;
-        case 4: hipLaunchKernelGGL((gather_ops_kernel_t<256, 4, false, false>), dim3(n), dim3(256), 0, s, ops); break;
-        case 5: hipLaunchKernelGGL((gather_ops_kernel_t<512, 8, true, true>), dim3(n), dim3(512), 0, s, ops); break;
-        case 6: hipLaunchKernelGGL((gather_ops_kernel_t<1024, 4, true, true>), dim3(n), dim3(1024), 0, s, ops); break;
-        default: hipLaunchKernelGGL((gather_ops_kernel_t<256, 4, true, true>), dim3(n), dim3(256), 0, s, ops); break;
-    }
-    return hipGetLastError();
-}
-#endif
-
-__global__ void table_insert_many_kernel(const TableEnt* __restrict__ ents, int hi) {
-    if (hi) __builtin_amdgcn_s_setprio(3);
-    const TableEnt e = ents[blockIdx.y];
-    for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < e.nkeys; i += gridDim.x * blockDim.x) {
-        const uint32_t key = (uint32_t)e.keys[i];
-        const unsigned long long v = (1ull << 32) | key;
-        uint32_t h = slot_hash(key) & e.mask;
-        for (uint32_t probes = 0; probes <= e.mask; ++probes) {
-            const unsigned long long prev = atomicCAS(&e.slots[h], 0ull, v);
-            if (prev == 0ull || prev == v) break;
-            h = (h + 1) & e.mask;
-        }
-    }
-}
-
-hipError_t launch_table_insert_many(const TableEnt* ents, uint32_t n, int32_t max_keys, hipStream_t s, bool bg) {
-    if (n == 0 || max_keys <= 0) return hipSuccess;
-    const uint32_t blocks = (uint32_t)std::min<int64_t>((max_keys + 255) / 256, bg ? std::max<uint32_t>(1, kBackgroundGroups / n) : 256);
-    hipLaunchKernelGGL(table_insert_many_kernel, dim3(blocks, n), dim3(256), 0, s, ents, bg ? 0 : 1);
-    return hipGetLastError();
-}
-
-__global__ void chain_flags_many_kernel(const FlagEnt* __restrict__ ents) {
-    const FlagEnt e = ents[blockIdx.y];
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < e.count; k += gridDim.x * blockDim.x) {
-        bool eq = e.wsrc[k] == e.wbas[k];
-        for (uint32_t j = 0; j < e.dl; ++j) eq &= e.ssrc[(size_t)k * e.dl + j] == e.sbas[(size_t)k * e.dl + j];
-        e.flags[k] = eq ? 1 : 0;
-    }
-}
-
-hipError_t launch_chain_flags_many(const FlagEnt* ents, uint32_t n, uint32_t max_count, hipStream_t s) {
-    if (n == 0 || max_count == 0) return hipSuccess;
-    const uint32_t blocks = std::min<uint32_t>((max_count + 255) / 256, 256);
-    hipLaunchKernelGGL(chain_flags_many_kernel, dim3(blocks, n), dim3(256), 0, s, ents);
-    return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------------
-// splitmix64 counter stream.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t splitmix_mix(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-__global__ void fill_words_kernel(uint64_t* __restrict__ out, int64_t nwords, uint64_t key, int64_t word0) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords; i += (int64_t)gridDim.x * blockDim.x)
-        out[i] = splitmix_mix(key + (uint64_t)(word0 + i + 1) * 0x9E3779B97F4A7C15ull);
-}
-
-__global__ void fill_bytes_kernel(uint8_t* __restrict__ out, int64_t n, uint64_t key, int64_t off) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t pos = (uint64_t)(off + i);
-        out[i] = (uint8_t)(splitmix_mix(key + (pos / 8 + 1) * 0x9E3779B97F4A7C15ull) >> (8 * (pos % 8)));
-    }
-}
-
-hipError_t launch_fill_splitmix(uint8_t* d_out, int64_t n, uint64_t key, int64_t byte_offset, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    if (byte_offset % 8 == 0 && reinterpret_cast<uintptr_t>(d_out) % 8 == 0) {
-        const int64_t nw = n / 8;
-        if (nw > 0)
-            hipLaunchKernelGGL(fill_words_kernel, dim3(4096), dim3(256), 0, s, reinterpret_cast<uint64_t*>(d_out), nw,
-                               key, byte_offset / 8);
-        const int64_t done = nw * 8;
-        if (done < n)
-            hipLaunchKernelGGL(fill_bytes_kernel, dim3(1), dim3(64), 0, s, d_out + done, n - done, key,
-                               byte_offset + done);
-    } else {
-        hipLaunchKernelGGL(fill_bytes_kernel, dim3(4096), dim3(256), 0, s, d_out, n, key, byte_offset);
-    }
     return hipGetLastError();
 }
 

@@ -1,0 +1,344 @@
+// device_io.hip -- gfx950 kernels that move bytes for the scan and the Receiver: copies into pinned host memory,
+// window sums at arbitrary positions, the Receiver's block gather, the batched table inserts and flags, the
+// stamped launches (the single-file scan's prep launch and host-side chain flags) and the synthetic fills.
+#include <hip/hip_runtime.h>
+
+#include "device.h"
+#include "device_common.h"
+#include "options.h"
+
+#include <algorithm>
+
+namespace rsh {
+
+__global__ void gather_bytes_kernel(const ScanFile* __restrict__ files, const GatherEnt* __restrict__ ents, uint32_t n,
+                                    uint8_t* __restrict__ out) {
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const GatherEnt e = ents[i];
+        out[i] = files[e.file].data[e.p];
+    }
+}
+
+hipError_t launch_gather_bytes(const ScanFile* files, const GatherEnt* ents, uint32_t n, uint8_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_bytes_kernel, dim3((n + 255) / 256), dim3(256), 0, s, files, ents, n, out);
+    return hipGetLastError();
+}
+
+// Device bytes -> pinned host memory, as a kernel: the runtime's copy path can queue behind a
+// co-running speculation launch, a high-priority kernel does not.  Thread t assembles bytes
+// [16t, 16t + 16) and writes them with one 16-byte store (dst 16-byte aligned).
+__device__ __forceinline__ void copy_piece(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int64_t n,
+                                           int64_t o) {
+    if (o + 16 <= n) {
+        uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i >> 2] |= (uint32_t)src[o + i] << (8 * (i & 3));
+        *reinterpret_cast<uint4*>(dst + o) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+        for (int64_t i = o; i < n; ++i) dst[i] = src[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void copy_to_host_kernel(const uint8_t* __restrict__ src, int64_t n,
+                                                           uint8_t* __restrict__ dst) {
+    __builtin_amdgcn_s_setprio(3);
+    const int64_t o = 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+    if (o < n) copy_piece(src, dst, n, o);
+}
+
+hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int64_t threads = (n + 15) / 16;
+    hipLaunchKernelGGL(copy_to_host_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, s, d_src, n, h_dst);
+    return hipGetLastError();
+}
+
+// The last workgroup of a stamped launch.  No fence per workgroup: on this chip a fence at agent scope writes the
+// XCD's L2 back (its L2s are not coherent with each other), and one per workgroup cost the first version ~230 us for
+// 2304 workgroups (r5j trace).  Instead every thread waits for its own memory operations (vmcnt also counts stores and
+// atomics here), then one thread per workgroup counts the workgroup done with a device atomic; the workgroup that
+// completes the count -- its reads of the others' results are device atomics too -- releases at system scope once and
+// writes the stamp, which the host polls before it reads what the launch wrote to host memory.
+__device__ __forceinline__ bool stamp_arrive(const Stamp& st, bool* sh_last) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) *sh_last = atomicAdd(st.counter, 1u) == gridDim.x * gridDim.y - 1;
+    __syncthreads();
+    return *sh_last;
+}
+__device__ __forceinline__ void stamp_write(const Stamp& st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        atomicExch(st.counter, 0u);
+        __threadfence_system();
+        __hip_atomic_store(st.stamp, st.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ __launch_bounds__(256) void chain_flags_stamped_kernel(const int32_t* __restrict__ wsrc,
+                                                                  const uint8_t* __restrict__ ssrc,
+                                                                  const int32_t* __restrict__ wbas,
+                                                                  const uint8_t* __restrict__ sbas, uint32_t count,
+                                                                  uint32_t dl, uint8_t* __restrict__ flags, Stamp st) {
+    __shared__ bool last;
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < count) {
+        bool eq = wsrc[k] == wbas[k];
+        for (uint32_t j = 0; j < dl; ++j) eq &= ssrc[(size_t)k * dl + j] == sbas[(size_t)k * dl + j];
+        flags[k] = eq ? 1 : 0;
+    }
+    if (stamp_arrive(st, &last)) stamp_write(st);
+}
+
+hipError_t launch_chain_flags_stamped(const int32_t* d_wsrc, const uint8_t* d_ssrc, const int32_t* d_wbas,
+                                      const uint8_t* d_sbas, uint32_t count, uint32_t dl, uint8_t* h_flags,
+                                      Stamp st, hipStream_t s) {
+    hipLaunchKernelGGL(chain_flags_stamped_kernel, dim3(count ? (count + 255) / 256 : 1), dim3(256), 0, s, d_wsrc,
+                       d_ssrc, d_wbas, d_sbas, count, dl, h_flags, st);
+    return hipGetLastError();
+}
+
+// blockIdx.x < nsamp * pieces: piece (blockIdx.x % pieces) of sample window blockIdx.x / pieces; the blocks past them
+// copy window 0 to the host, 4 KiB each.
+__global__ __launch_bounds__(256) void scan_prep_kernel(ScanPrep P) {
+    __shared__ int32_t sh[2 * 4];
+    __shared__ bool last;
+    const uint32_t b = blockIdx.x, nsum = P.nsamp * P.pieces;
+    if (b < nsum) {
+        const uint32_t i = b / P.pieces, q = b % P.pieces;
+        const int64_t p = P.wins[i] * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
+        const int64_t plen = ((w + P.pieces - 1) / P.pieces + 15) & ~(int64_t)15;
+        const int64_t lo = p + (int64_t)q * plen, hi = lo + plen < p + w ? lo + plen : p + w;
+        int32_t v[2] = {0, 0};
+        range_sums(P.data, P.n, lo, hi, p, v[0], v[1]);
+        block_reduce<2>(v, sh);
+        if (threadIdx.x == 0) {
+            atomicAdd(&P.scratch[2 * i], v[0]);
+            atomicAdd(&P.scratch[2 * i + 1], v[1]);
+        }
+    } else {
+        const int64_t o = 16 * ((int64_t)(b - nsum) * blockDim.x + threadIdx.x);
+        if (o < P.w0_len) copy_piece(P.data, P.w0, P.w0_len, o);
+    }
+    if (!stamp_arrive(P.st, &last)) return;
+    for (uint32_t i = threadIdx.x; i < P.nsamp; i += blockDim.x) {
+        const int64_t k = P.wins[i], p = k * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
+        const uint32_t S1 = (uint32_t)atomicExch(&P.scratch[2 * i], 0);
+        const uint32_t U = (uint32_t)atomicExch(&P.scratch[2 * i + 1], 0);
+        const uint32_t S2 = (uint32_t)w * S1 - U;
+        P.out_t[i] = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
+        P.out_w[i] = k < P.C ? P.table_weak[k] : 0;
+    }
+    stamp_write(P.st);
+}
+
+hipError_t launch_scan_prep(const ScanPrep& P, hipStream_t s) {
+    const uint32_t copy_blocks = (uint32_t)((P.w0_len + 16 * 256 - 1) / (16 * 256));
+    hipLaunchKernelGGL(scan_prep_kernel, dim3(P.nsamp * P.pieces + copy_blocks), dim3(256), 0, s, P);
+    return hipGetLastError();
+}
+
+// grid (., n): entry blockIdx.y, 16 bytes per thread, grid-strided over the entry's length
+__global__ __launch_bounds__(256) void copy_many_kernel(const CopyEnt* __restrict__ ents, int hi) {
+    if (hi) __builtin_amdgcn_s_setprio(3);
+    const CopyEnt e = ents[blockIdx.y];
+    for (int64_t o = 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); o < e.len;
+         o += 16 * (int64_t)gridDim.x * blockDim.x)
+        copy_piece(e.src, e.dst, e.len, o);
+}
+
+hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hipStream_t s, bool bg) {
+    if (n == 0 || max_len <= 0) return hipSuccess;
+    const int64_t blocks = bg ? 1 : std::min<int64_t>((max_len + 16 * 256 - 1) / (16 * 256), 64);
+    hipLaunchKernelGGL(copy_many_kernel, dim3((uint32_t)blocks, n), dim3(256), 0, s, ents, bg ? 0 : 1);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// True weak sums at arbitrary positions (one workgroup per position).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void window_weak_kernel(const ScanFile* __restrict__ files,
+                                                          const GatherEnt* __restrict__ ents,
+                                                          int32_t* __restrict__ out) {
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ int32_t sh[2 * 256 / 64];
+    const GatherEnt e = ents[blockIdx.x];
+    const ScanFile& F = files[e.file];
+    const int64_t p = e.p, n = F.n, B = F.B;
+    const int64_t w = (n - p < B ? n - p : B);
+    int32_t v[2] = {0, 0};
+    range_sums(F.data, n, p, p + w, p, v[0], v[1]);
+    block_reduce<2>(v, sh);
+    if (threadIdx.x == 0) {
+        const uint32_t S1 = (uint32_t)v[0];
+        const uint32_t S2 = (uint32_t)w * S1 - (uint32_t)v[1];
+        const int32_t T = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
+        if (e.by_block) F.aligned_weak[p / B] = T;
+        else out[blockIdx.x] = T;
+    }
+}
+
+hipError_t launch_window_weak(const ScanFile* files, const GatherEnt* ents, uint32_t n, int32_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(window_weak_kernel, dim3(n), dim3(256), 0, s, files, ents, out);
+    return hipGetLastError();
+}
+
+// D dwordx4 loads in flight per thread before their stores; NTL / NTS: non-temporal loads / stores.  The production
+// form is <1024, 4, true, true>; the others are kbench A/Bs (KBENCH_GATHER).
+template <int T, int D, bool NTL, bool NTS>
+__global__ __launch_bounds__(T) void gather_ops_kernel_t(const GatherOp* __restrict__ ops) {
+    const GatherOp op = ops[blockIdx.x];
+    const uintptr_t d = reinterpret_cast<uintptr_t>(op.dst);
+    int64_t head = (int64_t)((16 - (d & 15)) & 15);
+    if (head > op.len) head = op.len;
+    const int t = threadIdx.x;
+    if (t < head) op.dst[t] = op.src[t];
+    const int64_t body = (op.len - head) & ~(int64_t)15;
+    const uint8_t* __restrict__ s = op.src + head;
+    uint8_t* __restrict__ o = op.dst + head;
+    if ((reinterpret_cast<uintptr_t>(s) & 15) == 0) {  // 16-B aligned source: dwordx4 loads, 4 in flight
+        const int64_t step = 16 * (int64_t)T;
+        int64_t k = 16 * (int64_t)t;
+        for (; k + (D - 1) * step < body; k += D * step) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 v[D];
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+                const u32x4* a = reinterpret_cast<const u32x4*>(s + k + u * step);
+                if constexpr (NTL) v[u] = __builtin_nontemporal_load(a);
+                else v[u] = *a;
+            }
+#pragma unroll
+            for (int u = 0; u < D; ++u) {
+                u32x4* a = reinterpret_cast<u32x4*>(o + k + u * step);
+                if constexpr (NTS) __builtin_nontemporal_store(v[u], a);
+                else *a = v[u];
+            }
+        }
+        for (; k < body; k += step)
+            *reinterpret_cast<uint4*>(o + k) = *reinterpret_cast<const uint4*>(s + k);
+    } else if ((reinterpret_cast<uintptr_t>(s) & 3) == 0) {  // word-aligned source: four dword loads per store
+        for (int64_t k = 16 * (int64_t)t; k < body; k += 16 * (int64_t)blockDim.x) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(s + k);
+            *reinterpret_cast<uint4*>(o + k) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    } else {
+        for (int64_t k = 16 * (int64_t)t; k < body; k += 16 * (int64_t)blockDim.x) {
+            uint32_t q[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < 16; ++i) q[i >> 2] |= (uint32_t)s[k + i] << (8 * (i & 3));
+            *reinterpret_cast<uint4*>(o + k) = make_uint4(q[0], q[1], q[2], q[3]);
+        }
+    }
+    for (int64_t k = head + body + t; k < op.len; k += blockDim.x) op.dst[k] = op.src[k];
+}
+
+hipError_t launch_gather_ops(const GatherOp* ops, uint32_t n, hipStream_t s, int64_t avg_len) {
+    if (n == 0) return hipSuccess;
+    if (avg_len < (64 << 10)) {  // short ops (a segment's 8 KiB literal tokens and blocks): 256 threads each
+        hipLaunchKernelGGL((gather_ops_kernel_t<256, 2, true, true>), dim3(n), dim3(256), 0, s, ops);
+        return hipGetLastError();
+    }
+    // 1024 threads per 1 MiB op (16 waves per CU in flight): 0.754 of the 8 TB/s peak (read + write) against 0.680 for
+    // 256 threads, kbench KBENCH_GATHER (profiles/r4/r4e_kbench_gather.log)
+    hipLaunchKernelGGL((gather_ops_kernel_t<1024, 4, true, true>), dim3(n), dim3(1024), 0, s, ops);
+    return hipGetLastError();
+}
+#ifdef RSH_KBENCH
+hipError_t launch_gather_ops_variant(int v, const GatherOp* ops, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    switch (v) {
+        case 1: hipLaunchKernelGGL((gather_ops_kernel_t<256, 8, true, true>), dim3(n), dim3(256), 0, s, ops); break;
+        case 2: hipLaunchKernelGGL((gather_ops_kernel_t<512, 4, true, true>), dim3(n), dim3(512), 0, s, ops); break;
+        case 3: hipLaunchKernelGGL((gather_ops_kernel_t<256, 4, false, true>), dim3(n), dim3(256), 0, s, ops); break;
+        case 4: hipLaunchKernelGGL((gather_ops_kernel_t<256, 4, false, false>), dim3(n), dim3(256), 0, s, ops); break;
+        case 5: hipLaunchKernelGGL((gather_ops_kernel_t<512, 8, true, true>), dim3(n), dim3(512), 0, s, ops); break;
+        case 6: hipLaunchKernelGGL((gather_ops_kernel_t<1024, 4, true, true>), dim3(n), dim3(1024), 0, s, ops); break;
+        default: hipLaunchKernelGGL((gather_ops_kernel_t<256, 4, true, true>), dim3(n), dim3(256), 0, s, ops); break;
+    }
+    return hipGetLastError();
+}
+#endif
+
+__global__ void table_insert_many_kernel(const TableEnt* __restrict__ ents, int hi) {
+    if (hi) __builtin_amdgcn_s_setprio(3);
+    const TableEnt e = ents[blockIdx.y];
+    for (int32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < e.nkeys; i += gridDim.x * blockDim.x) {
+        const uint32_t key = (uint32_t)e.keys[i];
+        const unsigned long long v = (1ull << 32) | key;
+        uint32_t h = slot_hash(key) & e.mask;
+        for (uint32_t probes = 0; probes <= e.mask; ++probes) {
+            const unsigned long long prev = atomicCAS(&e.slots[h], 0ull, v);
+            if (prev == 0ull || prev == v) break;
+            h = (h + 1) & e.mask;
+        }
+    }
+}
+
+hipError_t launch_table_insert_many(const TableEnt* ents, uint32_t n, int32_t max_keys, hipStream_t s, bool bg) {
+    if (n == 0 || max_keys <= 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)std::min<int64_t>((max_keys + 255) / 256, bg ? std::max<uint32_t>(1, kBackgroundGroups / n) : 256);
+    hipLaunchKernelGGL(table_insert_many_kernel, dim3(blocks, n), dim3(256), 0, s, ents, bg ? 0 : 1);
+    return hipGetLastError();
+}
+
+__global__ void chain_flags_many_kernel(const FlagEnt* __restrict__ ents) {
+    const FlagEnt e = ents[blockIdx.y];
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < e.count; k += gridDim.x * blockDim.x) {
+        bool eq = e.wsrc[k] == e.wbas[k];
+        for (uint32_t j = 0; j < e.dl; ++j) eq &= e.ssrc[(size_t)k * e.dl + j] == e.sbas[(size_t)k * e.dl + j];
+        e.flags[k] = eq ? 1 : 0;
+    }
+}
+
+hipError_t launch_chain_flags_many(const FlagEnt* ents, uint32_t n, uint32_t max_count, hipStream_t s) {
+    if (n == 0 || max_count == 0) return hipSuccess;
+    const uint32_t blocks = std::min<uint32_t>((max_count + 255) / 256, 256);
+    hipLaunchKernelGGL(chain_flags_many_kernel, dim3(blocks, n), dim3(256), 0, s, ents);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// splitmix64 counter stream.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix_mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void fill_words_kernel(uint64_t* __restrict__ out, int64_t nwords, uint64_t key, int64_t word0) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nwords; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = splitmix_mix(key + (uint64_t)(word0 + i + 1) * 0x9E3779B97F4A7C15ull);
+}
+
+__global__ void fill_bytes_kernel(uint8_t* __restrict__ out, int64_t n, uint64_t key, int64_t off) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t pos = (uint64_t)(off + i);
+        out[i] = (uint8_t)(splitmix_mix(key + (pos / 8 + 1) * 0x9E3779B97F4A7C15ull) >> (8 * (pos % 8)));
+    }
+}
+
+hipError_t launch_fill_splitmix(uint8_t* d_out, int64_t n, uint64_t key, int64_t byte_offset, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (byte_offset % 8 == 0 && reinterpret_cast<uintptr_t>(d_out) % 8 == 0) {
+        const int64_t nw = n / 8;
+        if (nw > 0)
+            hipLaunchKernelGGL(fill_words_kernel, dim3(4096), dim3(256), 0, s, reinterpret_cast<uint64_t*>(d_out), nw,
+                               key, byte_offset / 8);
+        const int64_t done = nw * 8;
+        if (done < n)
+            hipLaunchKernelGGL(fill_bytes_kernel, dim3(1), dim3(64), 0, s, d_out + done, n - done, key,
+                               byte_offset + done);
+    } else {
+        hipLaunchKernelGGL(fill_bytes_kernel, dim3(4096), dim3(256), 0, s, d_out, n, key, byte_offset);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace rsh
