@@ -3,14 +3,16 @@
  * rsync_hip.h; a Java binding never calls it).
  *
  * The library's tunables and diagnostic switches (java-rsync_amd/csrc/options.h) have compiled-in defaults and
- * are never read from the environment.  Tests set them to force paths the default policy takes only on rare
- * shapes; bench.py --opt NAME=VALUE and the tools use them for A/B runs.  The table is per process and
- * applies to calls that start after the change.  Names: k1_gather, k1_shift, k1_unaligned, scan_trace,
- * scan_diag, scan_phase, scan_phase_guess, scan_segmented, scan_preprobe, scan_samples, scan_sample,
- * scan_spec_order, scan_early, scan_wait, scan_defer_steps, scan_defer_us, batch_spec, batch_spin_us,
- * batch_readahead, batch_prep_all, batch_chain, batch_chain_prefix, batch_chain_overlap, host_cores, file_tile,
- * file_tile_above, probe_long, segment_bytes, md5_width, chain_helpers, chain_map_bytes, batch_skip_rest,
- * scan_spec_queue, scan_flags_host, time_spec, time_gen, fault_inject.
+ * are never read from the environment.  The table is per process and applies to calls that start after a change.
+ *  - settable in every build (tests force rare paths with them; a few are tunables): k1_gather, k1_shift,
+ *    k1_unaligned, scan_trace, scan_segmented, scan_samples, batch_chain, batch_chain_prefix, host_cores,
+ *    file_tile, file_tile_above, probe_long, segment_bytes, md5_width, chain_helpers, chain_map_bytes, time_gen,
+ *    fault_inject;
+ *  - A/B switches, settable only in the diagnostics build (make diag: lib/diag/librsynchip.so, loaded by the
+ *    tools through RSH_LIB); the product library answers RSH_E_INVAL and runs their defaults: scan_diag,
+ *    scan_phase, scan_phase_guess, scan_preprobe, scan_sample, scan_spec_order, scan_early, scan_wait,
+ *    scan_defer_steps, scan_defer_us, scan_spec_queue, scan_flags_host, scan_prep_pieces, time_spec, batch_spec,
+ *    batch_spin_us, batch_readahead, batch_prep_all, batch_chain_overlap, batch_skip_rest.
  */
 #ifndef RSYNC_HIP_DEBUG_H
 #define RSYNC_HIP_DEBUG_H
@@ -23,7 +25,7 @@
 extern "C" {
 #endif
 
-/* RSH_OK, or RSH_E_INVAL for an unknown name. */
+/* RSH_OK, or RSH_E_INVAL for an unknown name or an A/B switch in the product build. */
 int rsh_debug_set_option(const char* name, int64_t value);
 int rsh_debug_get_option(const char* name, int64_t* value);
 /* Every option back to its compiled-in default. */

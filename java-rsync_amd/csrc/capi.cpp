@@ -1714,7 +1714,7 @@ int rsh_memcpy_d2h(rsh_ctx* ctx, void* dst, const void* src, int64_t bytes) {
 
 int rsh_debug_set_option(const char* name, int64_t value) {
     const int i = rsh::opt_index(name);
-    if (i < 0) return RSH_E_INVAL;
+    if (!rsh::opt_settable(i)) return RSH_E_INVAL;  // unknown, or an A/B switch outside the diagnostics build
     rsh::opt_table()[i].store(value, std::memory_order_relaxed);
     return RSH_OK;
 }

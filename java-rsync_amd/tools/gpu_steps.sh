@@ -118,7 +118,8 @@ for step in "$@"; do
             > "$O/config3.json" 2> "$O/config3.err" ;;
         receiver) run 300 python bench.py --workload receiver --steps 2 --warmup 1 > "$O/receiver.json" 2> "$O/receiver.err" ;;
         e2e) run 400 python java-rsync_amd/tools/e2e.py --gib 16 > "$O/e2e_16GiB.json" 2> "$O/e2e.err" ;;
-        ab)
+        ab)  # the A/B switches are settable in the diagnostics build only: both arms load it
+            export RSH_LIB="$R/java-rsync_amd/lib/diag/librsynchip.so"
             OPTS=""
             for o in $AB_OPTS; do OPTS="$OPTS --opt $o"; done
             for r in $(seq 1 "${REPS:-3}"); do

@@ -59,6 +59,19 @@ def test_options_have_defaults_and_no_environment():
     assert out.stdout.strip() == "1"
 
 
+def test_ab_switches_only_in_the_diagnostics_build():
+    """options.h: the A/B switches (rejected alternatives, policy knobs) are compiled-in constants of the product
+    library -- rsh_debug_set_option refuses them and their value is the default -- and settable only in the
+    diagnostics build (make diag, lib/diag/librsynchip.so) that the A/B tools load."""
+    if os.environ.get("RSH_LIB"):
+        pytest.skip("a non-product library is loaded")
+    for name, default in (("scan_spec_queue", 1), ("batch_spin_us", 200), ("scan_phase", 1), ("batch_spec", -1)):
+        assert R.get_option(name) == default
+        with pytest.raises(ValueError):
+            R.set_option(name, 0)
+        assert R.get_option(name) == default
+
+
 def test_product_library_has_no_ab_scaffolding():
     """The kbench-only K1 variants (RSH_KBENCH) and the old getenv switches are not in librsynchip.so."""
     blob = open(R.LIB_PATH, "rb").read()
