@@ -119,12 +119,12 @@ for step in "$@"; do
         receiver) run 300 python bench.py --workload receiver --steps 2 --warmup 1 > "$O/receiver.json" 2> "$O/receiver.err" ;;
         e2e) run 400 python java-rsync_amd/tools/e2e.py --gib 16 > "$O/e2e_16GiB.json" 2> "$O/e2e.err" ;;
         ab)  # the A/B switches are settable in the diagnostics build only: both arms load it
-            export RSH_LIB="$R/java-rsync_amd/lib/diag/librsynchip.so"
+            DIAG_LIB="$R/java-rsync_amd/lib/diag/librsynchip.so"
             OPTS=""
             for o in $AB_OPTS; do OPTS="$OPTS --opt $o"; done
             for r in $(seq 1 "${REPS:-3}"); do
-                run 300 python bench.py $AB_ARGS --steps 20 --warmup 5 --no-cpu-baseline --no-companions > "$O/a_$r.json" 2> "$O/a_$r.err"
-                run 300 python bench.py $AB_ARGS --steps 20 --warmup 5 --no-cpu-baseline --no-companions $OPTS > "$O/b_$r.json" 2> "$O/b_$r.err"
+                RSH_LIB="$DIAG_LIB" run 300 python bench.py $AB_ARGS --steps 20 --warmup 5 --no-cpu-baseline --no-companions > "$O/a_$r.json" 2> "$O/a_$r.err"
+                RSH_LIB="$DIAG_LIB" run 300 python bench.py $AB_ARGS --steps 20 --warmup 5 --no-cpu-baseline --no-companions $OPTS > "$O/b_$r.json" 2> "$O/b_$r.err"
             done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
