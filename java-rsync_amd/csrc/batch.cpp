@@ -11,6 +11,33 @@
 // round trip per round for the whole segment instead of one per question per file.  The aligned
 // speculation (the sources' own block sums) is one batched K1 launch, deferred like the single-file
 // scan's and cancelled when every resolver finishes first.
+//
+// The fiber scheduler's invariants (match_scan_batch_claimed; Batch, FileScan, fiber_main):
+//  1. Ownership.  Live file i belongs to worker i % W for the whole scan; only that worker's thread ever switches
+//     into its fiber, so a FileScan's resolver state (table, ResolveState, BatchBackend) is touched by one thread
+//     at a time, without locks.  The coordinator reads a FileScan (req, pending, done) and writes its answer only
+//     while every worker is idle (2).
+//  2. Rounds.  A round starts when the coordinator bumps `gen` under `mu` and ends when `idle == nworkers`.  In
+//     between the coordinator touches no FileScan; the workers touch nothing shared but their own slots of
+//     busy_ms / max_fiber_ms / times and (under `mu`) `idle`, `nworkers`.  The release of `mu` (or the
+//     acquire-load of `gen` / `idle` in spin_wait, re-checked under `mu`) orders a round's fiber writes before
+//     the coordinator's reads and the coordinator's answers before the next round's fiber reads.
+//  3. Requests.  A fiber posts at most one request and then switches back to its worker (Batch::post); `pending`
+//     stays set until the worker resumes it in a later round, so every request is answered exactly once.  A WAIT
+//     request is resumed only once `landed` is set; the worker keeps such a file (it does not leave while any of
+//     its files is not done), so the coordinator never waits on a file no worker will run.
+//  4. Termination.  The coordinator ends the scan in the round where no file is pending and every worker is idle
+//     or gone: every fiber has returned (done) and no fiber stack is live.  It sets `quit`, and the workers exit
+//     on their next wake-up; they are detached and keep only `bp` (a shared_ptr) alive, never FileScan or the
+//     stacks, which the next scan reuses.
+//  5. Device work and errors.  Only the coordinator launches device work or synchronises streams during the
+//     rounds (serve_round, the speculation's launch and cancellation); a fiber's device question is answered from
+//     host memory the round's synchronisation made valid.  A failed round records the first HIP error and keeps
+//     serving (the resolvers finish on whatever the round left), and the scan returns RSH_E_DEVICE after the
+//     rounds: no fiber is ever left suspended and no worker blocked.
+//  6. Cores.  W <= min(live files, host cores - 1 when waiters spin, kMaxWorkers); the spinning waiters leave one
+//     core for the coordinator, and rsh_match_scan_batch caps the workers (WorkerCap) so that the multi-buffer
+//     MD5 pool running beside the scan does not oversubscribe the process's cores.
 #include <sched.h>
 #include <ucontext.h>
 

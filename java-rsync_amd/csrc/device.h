@@ -25,8 +25,8 @@ void k1_timing_next(hipEvent_t start, hipEvent_t stop);
 bool k1_timing_taken();
 
 #ifdef RSH_KBENCH
-// kbench only (tools/kbench.cpp, built with -DRSH_KBENCH): the K1 instantiations measured against the production
-// one (variant -1 = production; the numbers are kbench's).  librsynchip.so contains the production kernels only.
+// kbench only (tools/kbench.cpp, built with -DRSH_KBENCH): the single-file K1 launcher with its variant exposed
+// (-1 = production, 0 = every chunk per lane, kbench's parity reference).
 hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks,
                                      uint32_t dl, uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong,
                                      hipStream_t s, const int* abort_flag = nullptr, int abort_gen = 0);
@@ -106,14 +106,6 @@ uint32_t plan_block_sums_files(const K1File* files, int32_t nfiles, std::vector<
                                std::vector<K1Lane>* lanes, int* lane_align, bool* partial = nullptr);
 hipError_t launch_expand_groups(const K1Plan* d_plans, uint32_t nplans, uint32_t ngroups, K1Group* d_groups,
                                 hipStream_t s);
-#ifdef RSH_KBENCH
-// the batched launch as persistent waves (kbench 1006)
-hipError_t launch_block_sums_batch_persist(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes,
-                                           uint32_t nlanes, int lane_align, uint32_t seed_word, hipStream_t s);
-// the same over groups only, at 4 waves per SIMD (block_sums_quad_kernel; kbench 1004: not adopted)
-hipError_t launch_block_sums_batch_quad(const K1Group* d_groups, uint32_t ngroups, uint32_t seed_word, hipStream_t s,
-                                        const int* abort_flag = nullptr, int abort_gen = 0);
-#endif
 bool tail_gather_on();  // option k1_gather = 0: leftover chunks one per lane, no gathered waves
 // partial: some groups have count < 64 (plan_block_sums_files) -- they run as gathered waves of the same launch
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,

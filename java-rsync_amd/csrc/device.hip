@@ -241,28 +241,9 @@ __global__ __launch_bounds__(64) void block_sums_lane_batch_kernel(const K1Lane*
                                                                                           seed, e.weak, e.strong);
 }
 
-// ------------------------------------------------------------------------------------------------
-// K1 (coalesced): one wave owns 64 consecutive full-length chunks (L = B, B % 128 == 0).  A stage is
-// the next 128 B of every chunk: 8 global_load_dwordx4 per lane, each instruction reading 8 whole
-// 128-B lines (8 lanes per line) instead of 64 scattered 16-B pieces; the wave transposes the stage
-// through LDS (row = 8 data slots + 1 pad slot, so the 16-lane ds_read_b128 groups and the 8-lane
-// ds_write_b128 groups are both bank-conflict free) and each lane then runs its chunk's MD5 over the
-// two 64-B blocks.  D stages stay in flight in registers.
-// ------------------------------------------------------------------------------------------------
-// Wave-local ordering of the stage transpose: LDS operations of one wave execute in order, so only
-// the compiler has to be kept from moving the lane-crossing ds_read above the ds_write (or the next
-// stage's ds_write above this stage's ds_read).
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// MODE (diagnostics only, never in the production launch): 0 = real, 1 = compute only (no global
-// loads; stage data synthesised in registers), 2 = loads only (no MD5/weak; words xor-folded).
 typedef int v4i32 __attribute__((ext_vector_type(4)));
 
-// Weak sums on the matrix pipe (MFMAW): per stage, for each group g of 16 chunks and K-half h,
+// Weak sums on the matrix pipe (the shift kernel's form): per stage, for each group g of 16 chunks and K-half h,
 // C_g += W_h x X_{g,h} with v_mfma_i32_16x16x64_i8, where X holds 64 signed bytes of 16 chunks
 // (columns) and W_h has row 0 = ones and row 1 = the byte's index in the 128-B stage (<= 127, int8).
 // Row 0 of C accumulates s1; row 1 accumulates the in-stage-index-weighted sums; R_g += row 0 after
@@ -283,202 +264,13 @@ __device__ __forceinline__ int poll_abort(const int* flag) {
     return v;
 }
 
-template <int D, bool NT, int WAVES = 1, int MODE = 0, bool FUSED = false, bool MFMAW = false, bool STEADY = true,
-          bool ABORT = false, int MD5F = 2, bool PIN = false>
-__global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const uint8_t* __restrict__ data, uint32_t B,
-                                                                  uint32_t dl, uint32_t seed,
-                                                                  int32_t* __restrict__ weak_out,
-                                                                  uint8_t* __restrict__ strong_out,
-                                                                  const int* abort_flag = nullptr,
-                                                                  int abort_gen = 0) {
-    constexpr int ROW = 9;
-    // MODE (diagnostics): 0 production, 1 synthetic stage data (no loads), 2 no MD5, 3 = 1 without the weak-sum
-    // MFMAs, 4 = 3 without the LDS transpose (MD5 on the raw register words)
-    constexpr bool SYN = MODE == 1 || MODE == 3 || MODE == 4;
-    // PIN: claim VGPRs up to v183 so that at most 2 waves fit a SIMD (512 / 184).  The MFMAW body needs 156,
-    // which admits 3; a launch with exactly 2 waves per SIMD of work (16 GiB at B = 128 KiB) then may stack
-    // 3 on some SIMDs and 1 on others when it starts while another kernel drains (5.1 ms instead of 3.2).
-    if constexpr (PIN) asm volatile("; occupancy pin" ::: "v183");
-    extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // sized at launch (occupancy control)
-    const int l = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    uint4* lds = lds_all + wv * 64 * ROW;
-    const uint32_t c0 = (blockIdx.x * WAVES + wv) * 64u;
-    const uint32_t nst = B >> 7;
-    const uint8_t* lp = data + ((size_t)c0 + (size_t)(l >> 3)) * B + 16 * (l & 7);
-    const size_t jstride = (size_t)8 * B;
-    const int wr0 = (l >> 3) * ROW + (l & 7);
-    const int rd0 = l * ROW;
-
-    uint4 q[D][8];
-    uint32_t fold = 0;
-    // MFMAW state: weights (row 0 ones, row 1 in-stage byte index), accumulators, running R
-    v4i32 wA[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-    v4i32 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-    int32_t Racc[4] = {0, 0, 0, 0};
-    int rdB = 0;
-    if constexpr (MFMAW) {
-        const int row = l & 15, ks = l >> 4;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                uint32_t word = 0;
-                if (row == 0) word = 0x01010101u;
-                else if (row == 1)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) word |= (uint32_t)(16 * (4 * h + mfma_sigma(ks)) + 4 * w + b) << (8 * b);
-                wA[h][w] = (int)word;
-            }
-        rdB = mfma_pi(l & 15) * ROW + mfma_sigma(ks);
-    }
-    // host guarantees nst >= 2 * D: the prologue is unconditional (exact vmcnt bookkeeping)
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            if constexpr (SYN) q[d][j] = make_uint4(l + d, j, c0, 7);
-            else q[d][j] = ld16<NT>(lp + 128 * (size_t)d + j * jstride);
-        }
-    }
-    Md5State st = md5_init();
-    int32_t s1 = 0, u = 0;
-    // One stage: registers -> LDS (transpose), refill the registers PF stages ahead, weak sums on the
-    // matrix pipe (MFMAW) and the two MD5 blocks.  Inlined with a compile-time slot d.
-    auto stage = [&](auto dc, uint32_t si, bool refill) __attribute__((always_inline)) {
-        constexpr int d = decltype(dc)::value;
-        uint4 qs[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            qs[j] = q[d][j];
-            if constexpr (MODE != 4) lds[wr0 + j * 8 * ROW] = q[d][j];
-        }
-        if (refill) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if constexpr (SYN) q[d][j] = make_uint4(q[d][j].y + si, q[d][j].x, q[d][j].w ^ si, q[d][j].z);
-                else q[d][j] = ld16<NT>(lp + 128 * (size_t)(si + D) + j * jstride);
-            }
-        }
-        if constexpr (MODE == 4) {
-        } else if constexpr (WAVES == 1) __syncthreads();
-        else wave_lds_sync();
-        if constexpr (MFMAW && MODE != 3 && MODE != 4) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) Racc[g] += acc[g][0];  // R += P_{s-1}
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const uint4 bv = lds[16 * ROW * g + rdB + 4 * h];
-                    const v4i32 b4 = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
-                    acc[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wA[h], b4, acc[g], 0, 0, 0);
-                }
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            uint4 r[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) r[k] = MODE == 4 ? qs[4 * h + k] : lds[rd0 + 4 * h + k];
-            uint32_t m[16];
-            unpack(r, m);
-            if constexpr (MODE == 2) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k) fold ^= m[k];
-            } else if constexpr (MFMAW) {
-                if constexpr (MD5F == 8) md5_compress_rot16n(st, m);
-#ifdef RSH_KBENCH
-    else if constexpr (MD5F == 10) md5_compress_k3s_8(st, m);   // A/B: a + m + K in one v_add3_u32, K from an SGPR
-    else if constexpr (MD5F == 11) md5_compress_k3s_16(st, m);
-    else if constexpr (MD5F == 12) md5_compress_k3s_16_nonop(st, m);
-    else if constexpr (MD5F == 13) md5_compress_k3s_16_nop2(st, m);
-#endif
-                else if constexpr (MD5F == 7) md5_compress_rot4n(st, m);
-                else if constexpr (MD5F == 6) md5_compress_rot16(st, m);
-                else if constexpr (MD5F == 5) md5_compress_rot4(st, m);
-                else if constexpr (MD5F == 4) md5_compress_asm16(st, m);
-                else if constexpr (MD5F == 3) md5_compress_asm4(st, m);
-                else if constexpr (MD5F == 2) md5_compress_asm(st, m);
-                else if constexpr (MD5F == 1) md5_compress_lit(st, m);
-                else md5_compress(st, m);
-            } else if constexpr (FUSED && MD5F == 1) {
-                int32_t wa, wb;
-                md5_compress_lit_weak(st, m, wa, wb);
-                s1 += wa;
-                u += (int32_t)((128 * si + 64 * h) * (uint32_t)wa) + wb;
-            } else if constexpr (FUSED) {
-                md5_weak_block(st, m, s1, u, 128 * si + 64 * h);
-            } else {
-                weak_block(m, s1, u, 128 * si + 64 * h);
-                md5_compress(st, m);
-            }
-        }
-        if constexpr (MODE == 4) {
-        } else if constexpr (WAVES == 1) __syncthreads();
-        else wave_lds_sync();
-    };
-    uint32_t s = 0;
-    if constexpr (!STEADY) {  // A/B reference: conditional refills in one loop
-        for (; s < nst; s += D) {
-            if (s < nst) stage(std::integral_constant<int, 0>{}, s, s + D < nst);
-            if constexpr (D > 1) if (s + 1 < nst) stage(std::integral_constant<int, 1>{}, s + 1, s + 1 + D < nst);
-            if constexpr (D > 2) if (s + 2 < nst) stage(std::integral_constant<int, 2>{}, s + 2, s + 2 + D < nst);
-        }
-    }
-    // steady state: branch-free, every slot refilled, so the compiler's vmcnt bookkeeping stays exact
-    // (with conditional refills it waits for every outstanding load at each stage: prefetch depth 1)
-    for (; s + 2 * D <= nst; s += D) {
-        stage(std::integral_constant<int, 0>{}, s, true);
-        if constexpr (D > 1) stage(std::integral_constant<int, 1>{}, s + 1, true);
-        if constexpr (D > 2) stage(std::integral_constant<int, 2>{}, s + 2, true);
-        if constexpr (D > 3) stage(std::integral_constant<int, 3>{}, s + 3, true);
-        if constexpr (ABORT) {
-            if ((s & 15) == 0 && poll_abort(abort_flag) == abort_gen) return;
-        }
-    }
-    for (; s < nst; s += D) {  // drain (fewer than 2 * D stages left)
-        if (s < nst) stage(std::integral_constant<int, 0>{}, s, s + D < nst);
-        if constexpr (D > 1) if (s + 1 < nst) stage(std::integral_constant<int, 1>{}, s + 1, s + 1 + D < nst);
-        if constexpr (D > 2) if (s + 2 < nst) stage(std::integral_constant<int, 2>{}, s + 2, s + 2 + D < nst);
-        if constexpr (D > 3) if (s + 3 < nst) stage(std::integral_constant<int, 3>{}, s + 3, s + 3 + D < nst);
-    }
-    // final block: seed || 0x80 || zero pad || bit length of (B + 4) bytes
-    {
-        const uint64_t bits = ((uint64_t)B + 4) * 8;
-        uint32_t m[16] = {seed, 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, (uint32_t)bits, (uint32_t)(bits >> 32)};
-        md5_compress(st, m);
-    }
-    if constexpr (MFMAW) {
-        // lanes 0..15 of group g hold (P_last, row1, R) for chunk 16g + pi(lane); move them to lane c
-        int32_t s1g[4], ug[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            Racc[g] += acc[g][0];
-            s1g[g] = acc[g][0];
-            ug[g] = (int32_t)(128u * (nst * (uint32_t)acc[g][0] - (uint32_t)Racc[g])) + acc[g][1];
-        }
-        const int src = mfma_pi_inv(l & 15);
-        int32_t t1[4], tu[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            t1[g] = __shfl(s1g[g], src, 64);
-            tu[g] = __shfl(ug[g], src, 64);
-        }
-        const int gs = l >> 4;
-        s1 = gs == 0 ? t1[0] : gs == 1 ? t1[1] : gs == 2 ? t1[2] : t1[3];
-        u = gs == 0 ? tu[0] : gs == 1 ? tu[1] : gs == 2 ? tu[2] : tu[3];
-    }
-    const uint32_t c = c0 + l;
-    if constexpr (MODE == 2) st.a ^= fold;
-    const int32_t s2 = (int32_t)(B * (uint32_t)s1 - (uint32_t)u);
-    weak_out[c] = (int32_t)(((uint32_t)s1 & 0xFFFFu) | ((uint32_t)s2 << 16));
-    store_digest(strong_out + (size_t)c * dl, st, dl);
-}
-
 // ------------------------------------------------------------------------------------------------
-// K1, software-pipelined (production).  Same data path as block_sums_coalesced_kernel (coalesced
-// 128-B-line loads, LDS transpose with 9-slot rows, weak sums on the matrix pipe, one lane = one chunk),
-// but no LDS round trip ever sits on a wave's critical path: stage s+1 is written to the second LDS
+// K1, software-pipelined (production).  One wave owns 64 consecutive full-length chunks (L = B, B % 128 == 0).
+// A stage is the next 128 B of every chunk: 8 buffer loads per lane, each instruction reading 8 whole 128-B lines
+// (8 lanes per line) instead of 64 scattered 16-B pieces; the wave transposes the stage through LDS (row = 8 data
+// slots + 1 pad slot, so the 8-lane ds_write_b128 and the 16-lane ds_read_b128 groups are bank-conflict free) and
+// each lane then runs its chunk's MD5 over the two 64-B blocks, one lane = one chunk.  No LDS round trip ever sits
+// on a wave's critical path: stage s+1 is written to the second LDS
 // buffer at the top of stage s, its message words and MFMA operands are read back into registers
 // between the two MD5 blocks of stage s, so they have landed long before stage s+1 starts.  The weak-sum
 // MFMAs of stage s sit between its MD5 blocks too.  Two stages of loads stay in flight (slots q[0..1]).
@@ -487,34 +279,9 @@ __global__ __launch_bounds__(64 * WAVES) void block_sums_coalesced_kernel(const 
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
 
-// MD5F == 9 (kbench A/B): the K constants in VGPRs, a + m + K as one v_add3_u32 (gfx950 VOP3 has no literal)
-__device__ __forceinline__ void md5_k3_init(uint32_t (&kv)[64]) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(__gfx950__)
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-        kv[i] = RSH_MD5_KTAB[i];
-        asm volatile("" : "+v"(kv[i]));
-    }
-#endif
-}
-__device__ __forceinline__ void md5_k3_block(Md5State& st, const uint32_t (&m)[16], const uint32_t (&kv)[64]) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(__gfx950__)
-    md5_compress_k3_8(st, m, kv);
-#endif
-}
-template <int MD5F>
-__device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&m)[16]) {
-    if constexpr (MD5F == 8) md5_compress_rot16n(st, m);
-#ifdef RSH_KBENCH
-    else if constexpr (MD5F == 10) md5_compress_k3s_8(st, m);   // A/B: a + m + K in one v_add3_u32, K from an SGPR
-    else if constexpr (MD5F == 11) md5_compress_k3s_16(st, m);
-    else if constexpr (MD5F == 12) md5_compress_k3s_16_nonop(st, m);
-    else if constexpr (MD5F == 13) md5_compress_k3s_16_nop2(st, m);
-#endif
-    else if constexpr (MD5F == 7) md5_compress_rot4n(st, m);
-    else if constexpr (MD5F == 1) md5_compress_lit(st, m);
-    else md5_compress(st, m);
-}
+// The production MD5 step form (md5_asm.inc: 16 steps per asm statement, no s_nop after the rotates; kbench
+// A/Bs of the other forms in DESIGN.md sec. 4)
+__device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&m)[16]) { md5_compress_rot16n(st, m); }
 
 // amdgpu_num_vgpr(192): two waves fill 384 of a SIMD's 512 registers, leaving room for one wave of the
 // resolver's range probe (104) to run beside the Sender's speculation launch in head mode.
@@ -535,15 +302,14 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 // buffer descriptor.  gt != nullptr: chunk i is gt[i] (K1Tail: any file; the segmented launch); else chunk i
 // is data + i B with outputs weak_out[i], strong_out[i dl] (a single launch's partial last wave).  Lanes past
 // gcnt digest chunk 0 again and store nothing.
-// MODE != 0 (A/B and diagnostic forms: synthetic stage data, per-iteration drains or sleeps) exists in the kbench
-// build only (RSH_KBENCH); the product library instantiates MODE 0.
-// WEAKW (production since round 4): the weak sums from the MD5 message words already in registers instead of a second read of
+// Weak sums (since round 4): the weak sums from the MD5 message words already in registers instead of a second read of
 // the stage from LDS in the MFMA operand layout: per 64-B block, four v_mfma_i32_16x16x64_i8 with B = the lane's
 // own 16-byte quarter w of its block and A = rows that select one lane group each (row m reads lane group m & 3:
 // type m >> 2 = 0 ones, 1 the byte's offset 16 w + i in the block), all into one accumulator -- chunk n + 16 q's
 // block sum lands in lane n (element q), its weighted sum in lane n + 16.  Saves the 8 ds_read_b128 per stage: the
-// same cycles at a higher clock, 2.5 % less time (kbench 66 vs 67, profiles/r4/r4e_kbench_weakw_k3s*).
-template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false, bool GATHER = false, bool WEAKW = true>
+// same cycles at a higher clock, 2.5 % less time (kbench A/B, profiles/r4/r4e_kbench_weakw_k3s*).
+// ABORT: the wave polls *abort_flag (never_word() when the launch has no abort word of its own).
+template <bool MULTI = false, bool GATHER = false>
 __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
                                                              uint8_t* __restrict__ strong_out,
@@ -556,9 +322,6 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     constexpr int ROW = 9;
     constexpr int BUF = 64 * ROW;  // uint4 slots per LDS buffer
     constexpr int TAIL_PF = RSH_K1_TAIL_PF;
-#ifndef RSH_KBENCH
-    static_assert(MODE == 0 && MD5F == 8 && WEAKW, "the product library runs the production K1 only");
-#endif
     if constexpr (!MULTI && !GATHER) {
         // tail waves (blockIdx >= main_waves): one lane per chunk left over (a partial last wave, the short last
         // chunk), dispatched with the main waves rather than as a launch queued behind them (a lone wave takes
@@ -572,7 +335,7 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
             return;
         }
     }
-    if constexpr (PIN) asm volatile("; occupancy pin" ::: "v175");
+    asm volatile("; occupancy pin" ::: "v175");  // at most 2 waves per SIMD
     extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // 2 buffers (sized at launch)
     const int l = threadIdx.x;
     uint32_t c0 = blockIdx.x * 64u;
@@ -585,9 +348,7 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         weak_out = g.weak;
         strong_out = g.strong;
         c0 = 0;
-        if constexpr (ABORT) {
-            if (g.abort) abort_flag = g.abort;  // per-file cancellation (batched Sender speculation)
-        }
+        if (g.abort) abort_flag = g.abort;  // per-file cancellation (batched Sender speculation)
     }
     [[maybe_unused]] const uint8_t* rp[8];  // GATHER: row j's lane address (chunk (l >> 3) + 8 j, piece l & 7)
     if constexpr (GATHER) {
@@ -608,27 +369,9 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     const int wr0 = (l >> 3) * ROW + (l & 7);
     const int rd0 = l * ROW;
 
-    v4i32 wA[2];
-    v4i32 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-    int32_t Racc[4] = {0, 0, 0, 0};
+    v4i32 wW[4];  // the A operand for block quarter w
+    v4i32 accW = {0, 0, 0, 0}, RW = {0, 0, 0, 0};
     {
-        const int row = l & 15, ks = l >> 4;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                uint32_t word = 0;
-                if (row == 0) word = 0x01010101u;
-                else if (row == 1)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) word |= (uint32_t)(16 * (4 * h + mfma_sigma(ks)) + 4 * w + b) << (8 * b);
-                wA[h][w] = (int)word;
-            }
-    }
-    const int rdB = mfma_pi(l & 15) * ROW + mfma_sigma(l >> 4);
-    [[maybe_unused]] v4i32 wW[4];  // WEAKW: the A operand for block quarter w
-    [[maybe_unused]] v4i32 accW = {0, 0, 0, 0}, RW = {0, 0, 0, 0};
-    if constexpr (WEAKW) {
         const int m = l & 15, q = l >> 4, type = m >> 2;
 #pragma unroll
         for (int w = 0; w < 4; ++w)
@@ -646,7 +389,6 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     uint4 q[2][8];  // load slots: stage s+1 and s+2 in flight while stage s computes
     uint4 Wa[4];    // words of the current stage's block 0 (then: the next stage's block 0)
     uint4 Wb[4];    // words of the current stage's block 1
-    uint4 Bv[8];    // MFMA operands of the current stage
     // Buffer loads: the wave's 64 chunks (64 * B <= 8 MiB) behind one descriptor, a 32-bit lane offset and
     // a scalar offset per 8-chunk row j -- one VGPR of addressing instead of eight 64-bit pointers.
     const __amdgpu_buffer_rsrc_t rsrc =
@@ -655,12 +397,6 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     auto load = [&](uint4 (&dst)[8], uint32_t stg) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-#ifdef RSH_KBENCH
-            if constexpr (MODE == 1) {  // diagnostics: synthetic stage data, no global loads
-                dst[j] = make_uint4(l + stg, j, c0, 7);
-                continue;
-            }
-#endif
             if constexpr (GATHER) {
                 dst[j] = ld16<false>(rp[j] + 128u * stg);
             } else {
@@ -677,23 +413,13 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
 #pragma unroll
         for (int k = 0; k < 4; ++k) w[k] = lds_all[buf * BUF + rd0 + 4 * h + k];
     };
-    auto get_mfma = [&](int buf) __attribute__((always_inline)) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) Bv[4 * h + g] = lds_all[buf * BUF + 16 * ROW * g + rdB + 4 * h];
-    };
     Md5State st = md5_init();
-    // MD5F == 9 (kbench A/B): a + m + K as one v_add3_u32 per step, the 64 K constants held in VGPRs
-    [[maybe_unused]] uint32_t kv[64];
-    if constexpr (MD5F == 9) md5_k3_init(kv);
     auto md5_block = [&](const uint4 (&w)[4]) __attribute__((always_inline)) {
         uint32_t m[16];
         unpack(w, m);
-        if constexpr (MD5F == 9) md5_k3_block(st, m, kv);
-        else md5_stream_block<MD5F>(st, m);
+        md5_stream_block(st, m);
     };
-    auto weak_words = [&](const uint4 (&w)[4]) __attribute__((always_inline)) {  // WEAKW: one 64-B block
+    auto weak_words = [&](const uint4 (&w)[4]) __attribute__((always_inline)) {  // one 64-B block
 #pragma unroll
         for (int e = 0; e < 4; ++e) RW[e] += accW[e];  // R += P_{b-1}
 #pragma unroll
@@ -702,21 +428,9 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
             accW = __builtin_amdgcn_mfma_i32_16x16x64_i8(wW[k], b4, accW, 0, 0, 0);
         }
     };
-    auto weak_mfma = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) Racc[g] += acc[g][0];  // R += P_{s-1}
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const uint4 bv = Bv[4 * h + g];
-                const v4i32 b4 = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
-                acc[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wA[h], b4, acc[g], 0, 0, 0);
-            }
-    };
     // One stage with compile-time parity P: LDS buffer P holds it, q[P ^ 1] the next stage's data.
-    // Block-1 words and MFMA operands are read at the top (they land during block 0); the next stage's
-    // block-0 words are read between the blocks (they land during block 1).
+    // Block-1 words are read at the top (they land during block 0); the next stage's block-0 words are read
+    // between the blocks (they land during block 1).
     auto stage = [&](auto pc, uint32_t si, bool has_next, bool refill) __attribute__((always_inline)) {
         constexpr int P = decltype(pc)::value;
         if (has_next) {
@@ -724,20 +438,18 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
             if (refill) load(q[P ^ 1], si + 3);
         }
         get_words(Wb, P, 1);
-        if constexpr (!WEAKW) get_mfma(P);
         md5_block(Wa);
-        if constexpr (WEAKW) weak_words(Wa);
-        else weak_mfma();
+        weak_words(Wa);
         compiler_fence();
         if (has_next) get_words(Wa, P ^ 1, 0);
         md5_block(Wb);
-        if constexpr (WEAKW) weak_words(Wb);
+        weak_words(Wb);
         compiler_fence();
     };
 
     load(q[0], 0);
     load(q[1], 1);
-    if constexpr (ABORT && MULTI) {  // a group whose file was resolved before the wave started does nothing
+    if constexpr (MULTI) {  // a group whose file was resolved before the wave started does nothing
         int f0;
         asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(f0) : "s"(abort_flag));
         if (f0 == abort_gen) return;
@@ -748,25 +460,18 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     get_words(Wa, 0, 0);
     uint32_t s = 0;
     // steady state: every stage has a next stage and a refill (branch-free: exact vmcnt bookkeeping)
-    // ABORT: one scalar load (glc: from L2, not the scalar cache) of the abort word per 2 stages, issued at
+    // Abort: one scalar load (glc: from L2, not the scalar cache) of the abort word per 2 stages, issued at
     // the top of the iteration and compared at the bottom, so its latency hides behind the two stages.
     // The compiler does not see the load; its own lgkmcnt(N) waits for LDS stay safe with one extra
     // operation in flight (they only get stricter).
-    [[maybe_unused]] int flag = 0;
-    for (; s + 5 <= nst && (!ABORT || flag != abort_gen); s += 2) {
-        if constexpr (ABORT) asm volatile("s_load_dword %0, %1, 0x0 glc" : "=s"(flag) : "s"(abort_flag));
+    int flag = 0;
+    for (; s + 5 <= nst && flag != abort_gen; s += 2) {
+        asm volatile("s_load_dword %0, %1, 0x0 glc" : "=s"(flag) : "s"(abort_flag));
         stage(std::integral_constant<int, 0>{}, s, true, true);
         stage(std::integral_constant<int, 1>{}, s + 1, true, true);
-        if constexpr (ABORT) asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(flag));
-#ifdef RSH_KBENCH
-        else if constexpr (MODE == 5) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // A/B: the drain alone
-        else if constexpr (MODE == 6) asm volatile("s_sleep 1" ::: "memory");            // A/B: a short sleep
-        else if constexpr (MODE == 7) asm volatile("s_sleep 4" ::: "memory");
-#endif
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(flag));
     }
-    if constexpr (ABORT) {
-        if (flag == abort_gen) return;
-    }
+    if (flag == abort_gen) return;
     for (; s < nst; s += 2) {  // drain
         stage(std::integral_constant<int, 0>{}, s, s + 1 < nst, s + 3 < nst);
         if (s + 1 < nst) stage(std::integral_constant<int, 1>{}, s + 1, s + 2 < nst, s + 4 < nst);
@@ -777,7 +482,7 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         md5_compress(st, m);
     }
     int32_t s1, u;
-    if constexpr (WEAKW) {
+    {
 #pragma unroll
         for (int e = 0; e < 4; ++e) RW[e] += accW[e];
         const int n = l & 15, q = l >> 4;
@@ -793,24 +498,6 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         const int32_t Wq = q == 0 ? tW[0] : q == 1 ? tW[1] : q == 2 ? tW[2] : tW[3];
         s1 = S;
         u = (int32_t)(64u * (2u * nst * (uint32_t)S - (uint32_t)Rq)) + Wq;
-    } else {
-        int32_t s1g[4], ug[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            Racc[g] += acc[g][0];
-            s1g[g] = acc[g][0];
-            ug[g] = (int32_t)(128u * (nst * (uint32_t)acc[g][0] - (uint32_t)Racc[g])) + acc[g][1];
-        }
-        const int src = mfma_pi_inv(l & 15);
-        int32_t t1[4], tu[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            t1[g] = __shfl(s1g[g], src, 64);
-            tu[g] = __shfl(ug[g], src, 64);
-        }
-        const int gs = l >> 4;
-        s1 = gs == 0 ? t1[0] : gs == 1 ? t1[1] : gs == 2 ? t1[2] : t1[3];
-        u = gs == 0 ? tu[0] : gs == 1 ? tu[1] : gs == 2 ? tu[2] : tu[3];
     }
     uint32_t c = c0 + l;
     if constexpr (GATHER) {
@@ -827,7 +514,7 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
     store_digest(strong_out + (size_t)c * dl, st, dl);
 }
 
-template <int MD5F, bool ABORT, bool PIN, int MODE = 0, bool MULTI = false>
+template <bool MULTI = false>
 __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
                                                              uint8_t* __restrict__ strong_out,
@@ -835,15 +522,14 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_kernel(const 
                                                              const K1Group* __restrict__ groups = nullptr,
                                                              int64_t n = 0, uint32_t nchunks = 0,
                                                              uint32_t main_waves = 0xFFFFFFFFu) {
-    block_sums_pipe_body<MD5F, ABORT, PIN, MODE, MULTI>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
-                                                        groups, n, nchunks, main_waves);
+    block_sums_pipe_body<MULTI>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen, groups, n, nchunks,
+                                main_waves);
 }
 // The production K1 with the partial last wave's full-length chunks as a gathered coalesced wave (the tail
 // waves past main_waves: ceil(tail_full / 64) gathered ones, then the short last chunk, if any, per lane).  A
 // per-lane wave runs ~20% slower than a coalesced one and, when every wave runs in the first round, sets the
 // launch's end.  Used only for launches with such a tail: the exact-multiple launches keep
 // block_sums_pipe_kernel.  Its register budget is 256 (2 waves/SIMD): under K1_PIPE_ATTR the two bodies spill.
-template <bool ABORT>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void block_sums_pipe_tailg_kernel(
     const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
     uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen, int64_t n, uint32_t nchunks,
@@ -852,7 +538,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
         const uint32_t tw = blockIdx.x - main_waves, ngw = (tail_full + 63u) / 64u;
         if (tw < ngw) {
             const uint32_t first = main_waves * 64u + 64u * tw;
-            block_sums_pipe_body<8, ABORT, true, 0, false, true>(
+            block_sums_pipe_body<false, true>(
                 data + (size_t)first * B, B, dl, seed, weak_out + first, strong_out + (size_t)first * dl, abort_flag,
                 abort_gen, nullptr, 0, 0, 0xFFFFFFFFu, nullptr, min(64u, tail_full - 64u * tw));
             return;
@@ -861,8 +547,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
         if (c < nchunks) lane_chunk_sums<16, RSH_K1_TAIL_PF, false>(data, n, B, c, dl, seed, weak_out, strong_out);
         return;
     }
-    block_sums_pipe_body<8, ABORT, true, 0, false>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
-                                                   nullptr, n, nchunks, main_waves);
+    block_sums_pipe_body<false>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen, nullptr, n, nchunks,
+                                main_waves);
 }
 bool tail_gather_on() { return opt(OPT_K1_GATHER) != 0; }  // 0: leftover chunks one per lane (options.h)
 
@@ -875,8 +561,8 @@ __global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_clock_kernel(
     uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen, int64_t n, uint32_t nchunks,
     unsigned long long* __restrict__ clk) {
     const uint64_t c0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
-    block_sums_pipe_body<8, true, true, 0, false>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
-                                                   nullptr, n, nchunks, 0xFFFFFFFFu);
+    block_sums_pipe_body<false>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen, nullptr, n, nchunks,
+                                0xFFFFFFFFu);
     const uint64_t c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) {
         atomicAdd(&clk[0], (unsigned long long)(c1 - c0));
@@ -893,31 +579,6 @@ hipError_t launch_k1_clock(const uint8_t* d_data, int64_t n, uint32_t B, uint32_
                        d_weak, d_strong, never_word(), -1, n, nchunks, d_clk);
     return hipGetLastError();
 }
-#ifdef RSH_KBENCH
-// kbench A/B (variant 67): round 3's production form, the weak-sum MFMA operands read from LDS (WEAKW = false)
-__global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_ldsw_kernel(
-    const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
-    uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen) {
-    block_sums_pipe_body<8, true, true, 0, false, false, false>(data, B, dl, seed, weak_out, strong_out, abort_flag,
-                                                                abort_gen, nullptr, 0, 0, 0xFFFFFFFFu);
-}
-// kbench A/B (variant 66): the weak sums from the MD5 words in registers (WEAKW; the production form since round 4)
-__global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_weakw_kernel(
-    const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
-    uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen) {
-    block_sums_pipe_body<8, true, true, 0, false, false, true>(data, B, dl, seed, weak_out, strong_out, abort_flag,
-                                                               abort_gen, nullptr, 0, 0, 0xFFFFFFFFu);
-}
-// kbench A/B (variant 61): MD5F == 9 holds the 64 K constants in VGPRs (176 + 64 registers, still 2 waves/SIMD)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void block_sums_pipe_k3_kernel(
-    const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
-    uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen) {
-    block_sums_pipe_body<9, true, true, 0, false>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen,
-                                                  nullptr, 0, 0, 0xFFFFFFFFu);
-}
-#endif
-
-
 #ifndef RSH_K1_SHIFT_VGPR
 #define RSH_K1_SHIFT_VGPR 256  // 2 waves/SIMD (the LDS ring and the MFMA tiles of the aligned kernel, plus the funnel)
 #endif
@@ -1015,7 +676,7 @@ __device__ __forceinline__ void shift_wave(const uint8_t* __restrict__ gdata, ui
         uint32_t m[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_alignbyte(d[W + i + 1], d[W + i], r);
-        md5_stream_block<8>(st, m);
+        md5_stream_block(st, m);
     };
     auto weak_mfma = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -1134,7 +795,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGP
         const uint32_t tw = blockIdx.x - main_waves, ngw = (tail_full + 63u) / 64u;
         if (tw < ngw) {
             const uint32_t first = main_waves * 64u + 64u * tw;
-            block_sums_pipe_body<8, true, true, 0, false, true>(
+            block_sums_pipe_body<false, true>(
                 data + (size_t)first * B, B, dl, seed, weak_out + first, strong_out + (size_t)first * dl, abort_flag,
                 abort_gen, nullptr, 0, 0, 0xFFFFFFFFu, nullptr, min(64u, tail_full - 64u * tw));
             return;
@@ -1156,15 +817,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGP
 // chunks at any base) 64 to a gathered coalesced wave (block_sums_pipe_body<.., GATHER>), the rest one chunk
 // per lane.  A per-lane wave runs ~20% slower than a coalesced one (its loads and v_dot4 weak sums), and as
 // the launch's last wave it set the launch's end: kbench, 2047 segment waves + one per-lane wave of 64
-// chunks 3.70-3.75 ms against 3.33 ms without it.
-template <int TAIL>
+// chunks 3.70-3.75 ms against 3.33 ms without it.  Leftover lanes read through the funnel-shift form (dword
+// loads at any base; kbench: ahead of wide aligned loads + a per-lane select and of plain unaligned dwordx4).
 __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGPR))) void block_sums_seg_kernel(
     const K1Seg* __restrict__ segs, uint32_t nseg, const K1Tail* __restrict__ tails, uint32_t ntail, uint32_t B,
     uint32_t dl, uint32_t seed, uint32_t ngf, const int* never) {
     if (blockIdx.x >= nseg) {
         const uint32_t tw = blockIdx.x - nseg, ngw = (ngf + 63u) / 64u;
         if (tw < ngw) {
-            block_sums_pipe_body<8, true, true, 0, false, true>(nullptr, B, dl, seed, nullptr, nullptr, never, -1,
+            block_sums_pipe_body<false, true>(nullptr, B, dl, seed, nullptr, nullptr, never, -1,
                                                                nullptr, 0, 0, 0xFFFFFFFFu, tails + 64u * tw,
                                                                min(64u, ngf - 64u * tw));
             return;
@@ -1172,9 +833,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(RSH_K1_SHIFT_VGP
         const uint32_t i = ngf + (tw - ngw) * 64u + threadIdx.x;
         if (i < ntail) {
             const K1Tail t = tails[i];
-            if constexpr (TAIL == 0) lane_chunk_sums<2, 4, false>(t.data, t.n, B, t.c, dl, seed, t.weak, t.strong);
-            else if constexpr (TAIL == 1) lane_chunk_sums<0, 4, false>(t.data, t.n, B, t.c, dl, seed, t.weak, t.strong);
-            else lane_chunk_sums<16, 4, false>(t.data, t.n, B, t.c, dl, seed, t.weak, t.strong);
+            lane_chunk_sums<0, 4, false>(t.data, t.n, B, t.c, dl, seed, t.weak, t.strong);
         }
         return;
     }
@@ -1202,65 +861,13 @@ hipError_t launch_block_sums_segments(const K1Seg* d_segs, uint32_t nseg, const 
     const uint32_t waves = nseg + (ngf + 63) / 64 + (ntail - ngf + 63) / 64;
     // LDS: the shift wave's ring (64 rows of 17 slots); a gathered wave's two 9-slot buffers when there is one
     const size_t lb = ngf > 0 ? 2 * 64 * 9 * sizeof(uint4) : 64 * 17 * sizeof(uint4);
-#ifdef RSH_KBENCH
-    // tail lanes (kbench A/B: RSH_K1_TAIL=1 (production) dword loads + funnel, 0 wide aligned loads + a per-lane
-    // select, 2 plain unaligned dwordx4).  2047 coalesced waves + one tail wave of 64 chunks at offset 1:
-    // 3.70-3.75 / 4.13-4.19 / 4.19-4.28 ms (3.33 ms without the tail wave)
-    const char* tm = getenv("RSH_K1_TAIL");
-    const int mode = tm ? atoi(tm) : 1;
-    if (mode == 2) {
-        hipLaunchKernelGGL(block_sums_seg_kernel<2>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
-                           seed_word, ngf, never);
-        return hipGetLastError();
-    }
-    if (mode == 0) {
-        hipLaunchKernelGGL(block_sums_seg_kernel<0>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
-                           seed_word, ngf, never);
-        return hipGetLastError();
-    }
-#endif
-    hipLaunchKernelGGL(block_sums_seg_kernel<1>, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
+    hipLaunchKernelGGL(block_sums_seg_kernel, dim3(waves), dim3(64), lb, s, d_segs, nseg, d_tails, ntail, B, dl,
                        seed_word, ngf, never);
     return hipGetLastError();
 }
 
 
-#ifdef RSH_KBENCH
-__global__ void block_sums_direct_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed,
-                                         int32_t* __restrict__ weak_out, uint8_t* __restrict__ strong_out,
-                                         const int* abort_flag, int abort_gen);  // device_kbench.inc
-template <int S>
-__global__ void block_sums_dma_kernel(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed,
-                                      int32_t* __restrict__ weak_out, uint8_t* __restrict__ strong_out);  // device_kbench.inc
-// MD5 step form of the coalesced K1 A/Bs: 0 compiler, 1 one asm statement per step, 2 generated blocks
-// (tools/gen_md5_asm.py; the production pipelined K1 uses 2)
-constexpr int kMd5Form = 2;
-#endif
 constexpr uint32_t kCUs = 256;            // MI355X compute units
-constexpr uint32_t kLdsPerCU = 160 * 1024; // bytes
-
-// Dynamic LDS above 64 KiB must be enabled per kernel.
-template <class K>
-void allow_full_lds(K kernel) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)kLdsPerCU);
-}
-
-// variant: -1 = production choice (19: the pipelined K1 with its tail and shift forms, the coalesced kernel above
-// B = 128 KiB, the per-lane kernel for other shapes).  The other variants exist in the kbench build only
-// (RSH_KBENCH): 0..2 per-lane (NT PF4, plain PF4, NT PF8); 3..6 coalesced (D=2 NT, D=3 NT, D=2 plain, D=4 NT),
-// and the numbered A/Bs below.  Non-coalesced variants handle every chunk shape.
-#ifdef RSH_KBENCH
-// RSH_K1_PIN_ALL=0 (kbench A/B): K1 launches of more than 2048 waves (single and batched) without the occupancy
-// pin -- the coalesced kernel for single files, the unpinned pipelined instantiation for batches
-static bool pin_all() {
-    static const bool v = !(getenv("RSH_K1_PIN_ALL") && atoi(getenv("RSH_K1_PIN_ALL")) == 0);
-    return v;
-}
-static bool batch_pin() { return pin_all(); }
-#else
-static bool pin_all() { return true; }
-#endif
 
 // K1 timing (k1_timing_next): the events the next production K1 launch on this thread records with its dispatch.
 namespace {
@@ -1286,6 +893,9 @@ static void k1_launch(void (*kernel)(KArgs...), dim3 grid, dim3 block, uint32_t 
     }
 }
 
+// The single-file K1.  variant -1: the production choice -- the pipelined K1 (with its gathered tail) or, at a base
+// off a 128-B line, the line-aligned shift kernel; the per-lane kernel for the shapes they do not take.  variant 0
+// (kbench's parity reference): the per-lane kernel for every chunk.
 #ifndef RSH_KBENCH
 static
 #endif
@@ -1294,35 +904,13 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
                                      hipStream_t s, const int* abort_flag, int abort_gen) {
     if (nchunks == 0) return hipSuccess;
     const uintptr_t addr = reinterpret_cast<uintptr_t>(d_data);
-    if (variant < 0) variant = 19;  // coalesced, 2 stages in flight, weak sums on the matrix pipe
-#ifdef RSH_KBENCH
-    if (variant == 3000 || variant == 3001 || variant == 3002) {  // kbench A/B: the per-lane path at any base
-        if (variant == 3002)
-            hipLaunchKernelGGL((block_sums_kernel<2, 4, false>), dim3((nchunks + 63) / 64), dim3(64), 0, s, d_data, n,
-                               B, nchunks, dl, seed_word, d_weak, d_strong, 0u);
-        else if (variant == 3000)
-            hipLaunchKernelGGL((block_sums_kernel<16, 4, false>), dim3((nchunks + 63) / 64), dim3(64), 0, s, d_data, n,
-                               B, nchunks, dl, seed_word, d_weak, d_strong, 0u);
-        else
-            hipLaunchKernelGGL((block_sums_kernel<0, 4, false>), dim3((nchunks + 63) / 64), dim3(64), 0, s, d_data, n,
-                               B, nchunks, dl, seed_word, d_weak, d_strong, 0u);
-        return hipGetLastError();
-    }
-#endif
-    uint32_t c_first = 0;
-    const bool deep = variant == 4 || variant == 6 || variant == 7 || variant == 9 || variant == 10 ||
-                      variant == 11 || variant == 12 || variant == 14 || variant == 15 || variant == 16 ||
-                      variant == 18 || variant == 21 || variant >= 50;  // D >= 3 variants need nst >= 2D = 6 (8 for D = 4)
-    // The pipelined K1 also runs at base addresses that are not 16-B aligned (the phase-shifted speculation
-    // starts at src + s for any s): its dwordx4 buffer loads then straddle 16-B boundaries, which gfx950
-    // serves in its unaligned access mode (bit-exact against the oracle at offsets 0..15,
-    // test_k1_unaligned_base).  Option k1_unaligned = 0 (test) sends such bases to the per-lane kernel instead.
-    const bool unaligned_ok = opt(OPT_K1_UNALIGNED) != 0;
+    const uint32_t nst = B >> 7;
+    // the pipelined and shift kernels poll an abort word (never_word() for launches without one of their own)
+    const bool coalesced = variant < 0 && abort_flag && (B % 128) == 0 && nst >= 4 && nst <= 1024;
     // A base that is not 128-B aligned goes to the line-aligned shift kernel when the lines it reads around the
     // data -- a bytes before it, up to 128 - a after the last full wave -- lie in the same allocation (option
     // k1_shift = 0, test: the pipelined kernel at the unaligned base, its path when the lines do not fit).
-    if (variant == 19 && (addr % 128) != 0 && (B % 128) == 0 && (B >> 7) >= 4 && (B >> 7) <= 1024 && abort_flag &&
-        opt(OPT_K1_SHIFT) != 0) {
+    if (coalesced && (addr % 128) != 0 && opt(OPT_K1_SHIFT) != 0) {
         hipDeviceptr_t lo = nullptr;
         size_t size = 0;
         const uint32_t a = (uint32_t)(addr % 128);
@@ -1366,355 +954,43 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
             }
         }
     }
-    if (variant >= 3 && (B % 128) == 0 && (B >> 7) >= (deep ? 8u : 4u) && ((addr % 16) == 0 || unaligned_ok)) {
+    // The pipelined K1 also runs at base addresses that are not 16-B aligned (the phase-shifted speculation
+    // starts at src + s for any s): its dwordx4 buffer loads then straddle 16-B boundaries, which gfx950
+    // serves in its unaligned access mode (bit-exact against the oracle at offsets 0..15,
+    // test_k1_unaligned_base).  Option k1_unaligned = 0 (test) sends such bases to the per-lane kernel instead.
+    const uint32_t waves = (uint32_t)std::min<int64_t>(n / B, nchunks) / 64;
+    if (coalesced && waves > 0 && ((addr % 16) == 0 || opt(OPT_K1_UNALIGNED) != 0)) {
         const uint32_t nfullc = (uint32_t)std::min<int64_t>(n / B, nchunks);  // chunks with L == B
-        const uint32_t waves = nfullc / 64;
-        const uint32_t nst = B >> 7;
         const size_t wave_lds = 64 * 9 * sizeof(uint4);
-#ifdef RSH_KBENCH
-        // LDS per workgroup chosen so that the dispatcher can place at most ceil(groups / CUs) groups
-        // on a CU: every SIMD then holds the same number of equal-work waves (no stacking imbalance).
-        auto lds_for = [&](uint32_t groups, uint32_t waves_per_group) -> size_t {
-            const uint32_t per_cu = std::max<uint32_t>(1, (groups + kCUs - 1) / kCUs);
-            size_t bytes = (size_t)kLdsPerCU / per_cu;
-            bytes &= ~(size_t)255;
-            return std::max(bytes, wave_lds * waves_per_group);
-        };
-        if ((variant == 7 || variant == 8) && waves >= 4) {
-            const uint32_t groups = waves / 4;
-            const size_t lb = lds_for(groups, 4);
-            if (variant == 8) {
-                allow_full_lds(block_sums_coalesced_kernel<2, false, 4>);
-                hipLaunchKernelGGL((block_sums_coalesced_kernel<2, false, 4>), dim3(groups), dim3(256), lb, s, d_data,
-                                   B, dl, seed_word, d_weak, d_strong);
-            } else {
-                allow_full_lds(block_sums_coalesced_kernel<3, false, 4>);
-                hipLaunchKernelGGL((block_sums_coalesced_kernel<3, false, 4>), dim3(groups), dim3(256), lb, s, d_data,
-                                   B, dl, seed_word, d_weak, d_strong);
-            }
-            c_first = groups * 256;
-            variant = 0;
-        } else
-#endif
-        if (waves > 0) {
-#ifdef RSH_KBENCH
-            const size_t lb = variant == 9 ? lds_for(waves, 1) : wave_lds;
-            switch (variant) {
-                case 3:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true>), dim3(waves), dim3(64), lb, s, d_data, B,
-                                       dl, seed_word, d_weak, d_strong);
-                    break;
-                case 5:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, false>), dim3(waves), dim3(64), lb, s, d_data,
-                                       B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 6:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<4, true>), dim3(waves), dim3(64), lb, s, d_data, B,
-                                       dl, seed_word, d_weak, d_strong);
-                    break;
-                case 13:
-                    hipLaunchKernelGGL((block_sums_dma_kernel<2>), dim3(waves), dim3(64), 2 * 512 * 16, s, d_data, B,
-                                       dl, seed_word, d_weak, d_strong);
-                    break;
-                case 14:
-                    hipLaunchKernelGGL((block_sums_dma_kernel<3>), dim3(waves), dim3(64), 3 * 512 * 16, s, d_data, B,
-                                       dl, seed_word, d_weak, d_strong);
-                    break;
-                case 15:
-                    hipLaunchKernelGGL((block_sums_dma_kernel<4>), dim3(waves), dim3(64), 4 * 512 * 16, s, d_data, B,
-                                       dl, seed_word, d_weak, d_strong);
-                    break;
-                case 18:
-                    if (nst <= 1024) {
-                        hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true, 1, 0, false, true>), dim3(waves), dim3(64),
-                                           lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    } else {
-                        hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true>), dim3(waves), dim3(64), lb, s, d_data,
-                                           B, dl, seed_word, d_weak, d_strong);
-                    }
-                    break;
-                case 19:
-#else
-            const size_t lb = wave_lds;
-#endif
-                    // the pipelined K1 at any wave count (occupancy pinned to 2 waves/SIMD; beyond 2048 waves they
-                    // run in rounds): measured 3.19 vs 3.96 ms for 16 GiB at B = 64 KiB (4096 waves) against the
-                    // unpinned instantiation, and ahead of the coalesced kernel at every size
-                    if (nst <= 1024 && nst >= 4 && abort_flag && (waves <= 2 * 4 * kCUs || pin_all())) {
-                        const uint32_t tail_waves = (nchunks - 64 * waves + 63) / 64;  // in the same launch
-                        // the partial last wave's full chunks gathered into a coalesced wave when that adds no
-                        // wave or every wave still fits the chip's slots (2 per SIMD)
-                        const uint32_t tail_full = nfullc - 64 * waves, tail_short = nchunks - nfullc;
-                        const uint32_t gwaves = (tail_full + 63) / 64 + (tail_short + 63) / 64;
-                        if (tail_full > 0 && tail_gather_on() &&
-                            (gwaves == tail_waves || waves + gwaves <= 2 * 4 * kCUs)) {
-                            k1_launch(block_sums_pipe_tailg_kernel<true>, dim3(waves + gwaves), dim3(64),
-                                      (uint32_t)(2 * wave_lds), s, d_data, B, dl, seed_word, d_weak, d_strong,
-                                      abort_flag, abort_gen, n, nchunks, waves, tail_full);
-                            return hipGetLastError();
-                        }
-                        k1_launch(block_sums_pipe_kernel<8, true, true>, dim3(waves + tail_waves), dim3(64),
-                                  (uint32_t)(2 * wave_lds), s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag,
-                                  abort_gen, nullptr, n, nchunks, waves);
-                        return hipGetLastError();
-                    }
-#ifdef RSH_KBENCH
-                    else if (nst <= 1024 && nst >= 4 && (waves <= 2 * 4 * kCUs || pin_all())) {
-                        hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true>), dim3(waves), dim3(64), 2 * wave_lds,
-                                           s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    } else if (nst <= 1024 && abort_flag && waves <= 2 * 4 * kCUs) {
-                        hipLaunchKernelGGL(
-                            (block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, true, kMd5Form, true>),
-                            dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong, abort_flag,
-                            abort_gen);
-                    } else if (nst <= 1024 && abort_flag) {
-                        hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, true>),
-                                           dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong,
-                                           abort_flag, abort_gen);
-                    } else if (nst <= 1024 && waves <= 2 * 4 * kCUs) {
-                        hipLaunchKernelGGL(
-                            (block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, kMd5Form, true>),
-                            dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    } else if (nst <= 1024) {
-                        hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true>), dim3(waves), dim3(64),
-                                           lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    }
-#endif
-                    else {  // B > 128 KiB (the Generator of a file above 2^34 bytes, config 3): the coalesced K1
-                        hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true>), dim3(waves), dim3(64), lb, s, d_data,
-                                           B, dl, seed_word, d_weak, d_strong);
-                    }
-#ifdef RSH_KBENCH
-                    break;
-                case 20:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, false>), dim3(waves),
-                                       dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 21:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true, 1, 0, false, true, false>), dim3(waves),
-                                       dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 24:  // A/B: production with the compiler's MD5 step form
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 0, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 25:  // A/B: one asm statement per MD5 step
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 1, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 30:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 3, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 31:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 4, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 32:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 1, false, true, true, false, 1, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 33:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 3, false, true, true, false, 1, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 34:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 3, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 35:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 4, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 36:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, true, false, true, false, 1, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 37:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 5, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 38:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 6, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 39:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 5, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 40:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 6, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 41:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, true, false, true, false, 1, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 42:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 7, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 43:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 0, false, true, true, false, 8, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 44:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 7, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 45:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 8, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 50:
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 0>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 51:
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<1, false, true, 0>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 52:
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 1>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 53:
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<1, false, true, 1>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 54:
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, false, 0>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 61:  // A/B: MD5 steps with a + m + K as one v_add3_u32 (K in VGPRs), abortable form
-                    hipLaunchKernelGGL(block_sums_pipe_k3_kernel, dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
-                    break;
-                case 62:  // A/B: MD5 steps with a + m + K as one v_add3_u32, K from an SGPR (s_mov per step), abortable
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<10, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
-                    break;
-                case 66:  // A/B: weak sums from the MD5 words in registers (no MFMA-operand LDS reads), abortable
-                    hipLaunchKernelGGL((block_sums_pipe_weakw_kernel), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
-                    break;
-                case 67:  // A/B: round 3's production K1 (weak-sum MFMA operands from LDS), abortable
-                    hipLaunchKernelGGL((block_sums_pipe_ldsw_kernel), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
-                    break;
-                case 68:  // A/B: no LDS -- per-lane loads into registers, weak sums from the MD5 words
-                    hipLaunchKernelGGL(block_sums_direct_kernel, dim3(waves), dim3(64), 0, s, d_data, B, dl, seed_word,
-                                       d_weak, d_strong, never_word(), -1);
-                    break;
-                case 64:  // ... without the s_nop after each step
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<12, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
-                    break;
-                case 65:  // ... an s_nop after every other step
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<13, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
-                    break;
-                case 63:  // ... 16 steps per asm statement
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<11, true, true>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
-                    break;
-                case 58:  // diagnostics (wrong results): the production abortable K1 on synthetic stage data, no
-                          // global loads -- its s_waitcnt time is the LDS / abort-word share (PMC attribution)
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true, 1>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong, never_word(), -1);
-                    break;
-                case 56:  // A/B: the plain kernel with s_sleep 1 / s_sleep 4 per 2 stages
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 6>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 57:
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 7>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 55:  // A/B: the plain kernel with the abortable kernel's lgkmcnt(0) drain per 2 stages
-                    hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 5>), dim3(waves), dim3(64), 2 * wave_lds, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 26:  // diagnostics (wrong results): synthetic data, no weak-sum MFMAs
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 3, false, true, true, false, 2, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 27:  // ... and no LDS transpose, MD5 forms 2 / 1 / 0
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 2, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 28:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 1, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 29:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 4, false, true, true, false, 0, true>),
-                                       dim3(waves), dim3(64), lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 22:  // diagnostic: compute only (synthetic stage data), production instantiation otherwise
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 1, false, true, true, false, 2, true>), dim3(waves), dim3(64),
-                                       lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 23:  // diagnostic: loads + transpose + weak sums, no MD5
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, true, 1, 2, false, true, true, false, 2, true>), dim3(waves), dim3(64),
-                                       lb, s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 16:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true, 1, 0, true>), dim3(waves), dim3(64), lb, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 17:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<2, false, 1, 0, true>), dim3(waves), dim3(64), lb,
-                                       s, d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 10:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, false, 1, 1>), dim3(waves), dim3(64), lb, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 11:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, false, 1, 2>), dim3(waves), dim3(64), lb, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 12:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<4, false, 1, 2>), dim3(waves), dim3(64), lb, s,
-                                       d_data, B, dl, seed_word, d_weak, d_strong);
-                    break;
-                case 9:
-                    allow_full_lds(block_sums_coalesced_kernel<3, false>);
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, false>), dim3(waves), dim3(64), lb, s, d_data,
-                                       B, dl, seed_word, d_weak, d_strong);
-                    break;
-                default:
-                    hipLaunchKernelGGL((block_sums_coalesced_kernel<3, true>), dim3(waves), dim3(64), lb, s, d_data, B,
-                                       dl, seed_word, d_weak, d_strong);
-            }
-#endif
-            c_first = waves * 64;
+        // the pipelined K1 at any wave count (occupancy pinned to 2 waves/SIMD; beyond 2048 waves they run in
+        // rounds): measured 3.19 vs 3.96 ms for 16 GiB at B = 64 KiB (4096 waves) against the unpinned
+        // instantiation, and ahead of the round-1 coalesced kernel at every size
+        const uint32_t tail_waves = (nchunks - 64 * waves + 63) / 64;  // in the same launch
+        // the partial last wave's full chunks gathered into a coalesced wave when that adds no wave or every wave
+        // still fits the chip's slots (2 per SIMD)
+        const uint32_t tail_full = nfullc - 64 * waves, tail_short = nchunks - nfullc;
+        const uint32_t gwaves = (tail_full + 63) / 64 + (tail_short + 63) / 64;
+        if (tail_full > 0 && tail_gather_on() && (gwaves == tail_waves || waves + gwaves <= 2 * 4 * kCUs)) {
+            k1_launch(block_sums_pipe_tailg_kernel, dim3(waves + gwaves), dim3(64), (uint32_t)(2 * wave_lds), s, d_data,
+                      B, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, n, nchunks, waves, tail_full);
+            return hipGetLastError();
         }
-        variant = 0;
+        k1_launch(block_sums_pipe_kernel<false>, dim3(waves + tail_waves), dim3(64), (uint32_t)(2 * wave_lds), s,
+                  d_data, B, dl, seed_word, d_weak, d_strong, abort_flag, abort_gen, nullptr, n, nchunks, waves);
+        return hipGetLastError();
     }
-    if (c_first >= nchunks) return hipGetLastError();
-    const uint32_t rest = nchunks - c_first;
+    // one lane per chunk
     const dim3 block(64);
-    const dim3 grid((rest + 63) / 64);
+    const dim3 grid((nchunks + 63) / 64);
     if ((B % 16) == 0 && (addr % 16) == 0) {
-#ifdef RSH_KBENCH
-        if (variant == 1)
-            hipLaunchKernelGGL((block_sums_kernel<16, 4, false>), grid, block, 0, s, d_data, n, B, nchunks, dl,
-                               seed_word, d_weak, d_strong, c_first);
-        else if (variant == 2)
-            hipLaunchKernelGGL((block_sums_kernel<16, 8, true>), grid, block, 0, s, d_data, n, B, nchunks, dl,
-                               seed_word, d_weak, d_strong, c_first);
-        else
-#endif
-            hipLaunchKernelGGL((block_sums_kernel<16, 4, true>), grid, block, 0, s, d_data, n, B, nchunks, dl,
-                               seed_word, d_weak, d_strong, c_first);
+        hipLaunchKernelGGL((block_sums_kernel<16, 4, true>), grid, block, 0, s, d_data, n, B, nchunks, dl, seed_word,
+                           d_weak, d_strong, 0u);
     } else if ((B % 4) == 0 && (addr % 4) == 0) {
         hipLaunchKernelGGL((block_sums_kernel<4, 2>), grid, block, 0, s, d_data, n, B, nchunks, dl, seed_word, d_weak,
-                           d_strong, c_first);
+                           d_strong, 0u);
     } else {
         hipLaunchKernelGGL((block_sums_kernel<0, 4, false>), grid, block, 0, s, d_data, n, B, nchunks, dl, seed_word,
-                           d_weak, d_strong, c_first);
+                           d_weak, d_strong, 0u);
     }
     return hipGetLastError();
 }
@@ -1830,7 +1106,7 @@ hipError_t launch_expand_groups(const K1Plan* d_plans, uint32_t nplans, uint32_t
 // process, same buffer): the plain instantiation 4.07-4.57 ms, the abortable one 2.99-3.10 ms (the plain one
 // with only the abortable loop's lgkmcnt(0) drain: 4.38 ms); round 1's boxes ran both at ~3.0 ms.  The word
 // must be uncached device memory like the contexts' abort words: polling a __device__ global instead (L2,
-// one line for every wave) made the launch 27.9 ms.  RSH_K1_PLAIN=1 (kbench A/B) launches the plain one.
+// one line for every wave) made the launch 27.9 ms.
 static const int* never_word() {
     static int* ptr[64] = {};
     int dev = 0;
@@ -1843,14 +1119,6 @@ static const int* never_word() {
     }
     return ptr[dev];
 }
-#ifdef RSH_KBENCH
-static bool plain_k1() {
-    static const bool v = getenv("RSH_K1_PLAIN") && atoi(getenv("RSH_K1_PLAIN")) != 0;
-    return v;
-}
-#else
-static bool plain_k1() { return false; }
-#endif
 
 // The batched K1 with its leftovers in the same launch: groups some of which are a file's partial last wave
 // (K1Group::count < 64: the gathered-wave path, one 64-bit pointer per 8-chunk row, lanes past the count store
@@ -1871,29 +1139,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
     }
     const K1Group g = groups[blockIdx.x];
     if (g.count < 64) {
-        block_sums_pipe_body<8, true, true, 0, false, true>(g.data, g.B, g.dl, seed, g.weak, g.strong,
+        block_sums_pipe_body<false, true>(g.data, g.B, g.dl, seed, g.weak, g.strong,
                                                            g.abort ? g.abort : abort_flag, abort_gen, nullptr, 0, 0,
                                                            0xFFFFFFFFu, nullptr, g.count);
         return;
     }
-    block_sums_pipe_body<8, true, true, 0, true>(nullptr, 0u, 0u, seed, nullptr, nullptr, abort_flag, abort_gen, groups);
+    block_sums_pipe_body<true>(nullptr, 0u, 0u, seed, nullptr, nullptr, abort_flag, abort_gen, groups);
 }
-#ifdef RSH_KBENCH
-#include "device_kbench.inc"
-#else
-static bool batch_quad() { return false; }
-#endif
 
 hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, const K1Lane* d_lanes, uint32_t nlanes,
                                    int lane_align, uint32_t seed_word, hipStream_t s, const int* abort_flag,
                                    int abort_gen, bool partial) {
     const size_t lb = 2 * 64 * 9 * sizeof(uint4);
-    static const bool quad = batch_quad();
-    if (!abort_flag && !plain_k1() && (abort_flag = never_word()) != nullptr) abort_gen = -1;  // see never_word
-    // partial groups, or lanes beside groups: one launch (RSH_K1_GATHER=0: the lanes as a second launch)
-    if (partial || (tail_gather_on() && !quad && nlanes > 0 && ngroups > 0)) {
-        if (!abort_flag && (abort_flag = never_word()) != nullptr) abort_gen = -1;
-        if (!abort_flag || quad) return hipErrorInvalidValue;  // the planner makes no partial group for these
+    if (!abort_flag && (abort_flag = never_word()) != nullptr) abort_gen = -1;  // see never_word
+    if (!abort_flag) return hipErrorOutOfMemory;  // never_word() failed: no uncached word for the pinned K1
+    // partial groups, or lanes beside groups: one launch (option k1_gather = 0: the lanes as a second launch)
+    if (partial || (tail_gather_on() && nlanes > 0 && ngroups > 0)) {
         const dim3 grid(ngroups + nlanes);
         if (lane_align == 16)
             hipLaunchKernelGGL((block_sums_pipe_multi_g_kernel<16>), grid, dim3(64), lb, s, d_groups, ngroups, d_lanes,
@@ -1906,33 +1167,9 @@ hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, co
                                seed_word, abort_flag, abort_gen);
         return hipGetLastError();
     }
-#ifdef RSH_KBENCH
-    if (ngroups > 0 && quad) {
-        const hipError_t e = launch_block_sums_batch_quad(d_groups, ngroups, seed_word, s, abort_flag, abort_gen);
-        if (e != hipSuccess) return e;
-        ngroups = 0;
-    }
-#endif
-    if (ngroups > 0) {
-#ifdef RSH_KBENCH
-        if (abort_flag && batch_pin())
-            hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true, 0, true>), dim3(ngroups), dim3(64), lb, s,
-                               nullptr, 0u, 0u, seed_word, nullptr, nullptr, abort_flag, abort_gen, d_groups);
-        else if (abort_flag)
-            hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, false, 0, true>), dim3(ngroups), dim3(64), lb, s,
-                               nullptr, 0u, 0u, seed_word, nullptr, nullptr, abort_flag, abort_gen, d_groups);
-        else if (batch_pin())
-            hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, true, 0, true>), dim3(ngroups), dim3(64), lb, s,
-                               nullptr, 0u, 0u, seed_word, nullptr, nullptr, nullptr, 0, d_groups);
-        else
-            hipLaunchKernelGGL((block_sums_pipe_kernel<8, false, false, 0, true>), dim3(ngroups), dim3(64), lb, s,
-                               nullptr, 0u, 0u, seed_word, nullptr, nullptr, nullptr, 0, d_groups);
-#else
-        if (!abort_flag) return hipErrorOutOfMemory;  // never_word() failed: no uncached word for the pinned K1
-        hipLaunchKernelGGL((block_sums_pipe_kernel<8, true, true, 0, true>), dim3(ngroups), dim3(64), lb, s, nullptr,
-                           0u, 0u, seed_word, nullptr, nullptr, abort_flag, abort_gen, d_groups);
-#endif
-    }
+    if (ngroups > 0)
+        hipLaunchKernelGGL((block_sums_pipe_kernel<true>), dim3(ngroups), dim3(64), lb, s, nullptr, 0u, 0u, seed_word,
+                           nullptr, nullptr, abort_flag, abort_gen, d_groups);
     if (nlanes > 0) {
         if (lane_align == 16)
             hipLaunchKernelGGL((block_sums_lane_batch_kernel<16>), dim3(nlanes), dim3(64), 0, s, d_lanes, seed_word);
@@ -1947,14 +1184,8 @@ hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, co
 hipError_t launch_block_sums(const uint8_t* d_data, int64_t n, uint32_t B, uint32_t nchunks, uint32_t dl,
                              uint32_t seed_word, int32_t* d_weak, uint8_t* d_strong, hipStream_t s,
                              const int* abort_flag, int abort_gen) {
-#ifdef RSH_KBENCH
-    // RSH_K1_VARIANT (kbench A/B) replaces the production variant for non-abortable launches
-    static const int forced = getenv("RSH_K1_VARIANT") ? atoi(getenv("RSH_K1_VARIANT")) : -1;
-#else
-    constexpr int forced = -1;
-#endif
-    if (!abort_flag && forced < 0 && !plain_k1() && (abort_flag = never_word()) != nullptr) abort_gen = -1;
-    return launch_block_sums_variant(abort_flag ? -1 : forced, d_data, n, B, nchunks, dl, seed_word, d_weak, d_strong, s, abort_flag,
+    if (!abort_flag && (abort_flag = never_word()) != nullptr) abort_gen = -1;
+    return launch_block_sums_variant(-1, d_data, n, B, nchunks, dl, seed_word, d_weak, d_strong, s, abort_flag,
                                      abort_gen);
 }
 

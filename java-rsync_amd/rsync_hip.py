@@ -156,11 +156,11 @@ def build(force=False):
 
 
 def stale_sources():
-    """Sources that changed since librsynchip.so was built (the build's sha256 stamp, lib/librsynchip.srchash):
-    a stale library must never be the one a test or the bench measures.  [] when the stamp or the sources are
-    absent (a binary-only install)."""
+    """Sources that changed since the loaded library was built (the build's sha256 stamp next to it,
+    lib/librsynchip.srchash or lib/diag/librsynchip.srchash): a stale library must never be the one a test or the
+    bench measures.  [] when the stamp or the sources are absent (a binary-only install)."""
     import hashlib
-    stamp = os.path.join(HERE, "lib", "librsynchip.srchash")
+    stamp = os.path.splitext(LIB_PATH)[0] + ".srchash"
     if not os.path.exists(stamp):
         return []
     out = []

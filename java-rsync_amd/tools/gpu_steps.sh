@@ -55,7 +55,7 @@ for step in "$@"; do
         pytest) run 900 python -u -m pytest -m gpu -x -v --timeout 400 --timeout-method thread $PYTEST_ARGS \
             > "$O/pytest.log" 2>&1 ;;
         kb-ab)
-            V=${KB_VARIANTS:-"1000 66 64 65"}
+            V=${KB_VARIANTS:-"1000 1001 1003"}
             run 240 "$K" 16384 131072 4 6 $V $V $V > "$O/kb_ab.log" 2>&1
             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace \
                 -d "$O/kb_ab_clock" -o run --output-format csv -- "$K" 16384 131072 4 5 $V > "$O/kb_ab_clock.log" 2>&1) \

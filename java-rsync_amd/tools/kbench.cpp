@@ -6,7 +6,9 @@
 // variant 1002: the batched launch over KBENCH_FILES (128) equal files cut from the buffer (config 4's shape).
 // Its parity check holds when per is a multiple of B (then the files' chunks are the buffer's chunks).
 // variant 1003: the segmented launch (the Sender's prefix + phase speculation kernel) over the buffer.
-// variant 1004: variant 1002 with the 4-waves/SIMD kernel (block_sums_quad_kernel).
+// variant 1005: the production batch planner over ragged files (below).
+// (The rejected K1 forms measured in rounds 1-4 -- the coalesced kernel's MD5 step forms, LDS-DMA stages, 4 waves per
+// SIMD, persistent waves, no-LDS loads -- were deleted after their A/Bs; DESIGN.md sec. 4 keeps the numbers.)
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -198,18 +200,9 @@ int main(int argc, char** argv) {
                                                                            }),
                                                    B, dl, 0x04030201u, s);
         if (v == 1005) return launch_rag();
-        if (v == 1006)
-            return rsh::launch_block_sums_batch_persist(d_groups, (uint32_t)groups.size(), d_lanes, (uint32_t)lanes.size(),
-                                                        lane_align, 0x04030201u, s);
         if (v == 1002)
             return rsh::launch_block_sums_batch(d_groups, (uint32_t)groups.size(), d_lanes, (uint32_t)lanes.size(),
                                                 lane_align, 0x04030201u, s);
-        if (v == 1004) {  // the batched groups at 4 waves/SIMD (+ the lane kernel for the leftovers)
-            hipError_t e = rsh::launch_block_sums_batch_quad(d_groups, (uint32_t)groups.size(), 0x04030201u, s);
-            if (e == hipSuccess && !lanes.empty())
-                e = rsh::launch_block_sums_batch(d_groups, 0, d_lanes, (uint32_t)lanes.size(), lane_align, 0x04030201u, s);
-            return e;
-        }
         if (v == 1000) return rsh::launch_block_sums_variant(-1, d, n, B, C, dl, 0x04030201u, w, sx, s, abort_word, 1);
         if (v == 1001) return rsh::launch_block_sums(d, n, B, C, dl, 0x04030201u, w, sx, s);  // the production entry
         return rsh::launch_block_sums_variant(v, d, n, B, C, dl, 0x04030201u, w, sx, s);
