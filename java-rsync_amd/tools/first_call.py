@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--files", type=int, default=128)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--trace", action="store_true", help="scan_trace = 2 on the first batched scan")
+    ap.add_argument("--only", type=int, default=0, help="4 or 5: that configuration only (0: both)")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -36,6 +37,16 @@ def main():
     out["ctx_create_ms"] = round((time.perf_counter() - t) * 1e3, 3)
     L = R.lib()
     seed = np.frombuffer(bytes([1, 2, 3, 4]), np.uint8).copy()
+    if a.only != 5:
+        config4(a, ctx, L, R, G, seed, out)
+    if a.only != 4:
+        config5(a, ctx, L, R, seed, out)
+    ctx.close()
+    print(json.dumps(out))
+
+
+def config4(a, ctx, L, R, G, seed, out):
+    import torch
     S, B, dl, F = G.CONFIG4_FILE_BYTES, G.CONFIG4_B, G.CONFIG4_DL, a.files
     src = torch.empty(F * S, dtype=torch.uint8, device="cuda")
     basis = torch.empty(F * S, dtype=torch.uint8, device="cuda")
@@ -75,6 +86,10 @@ def main():
     out["config4_half_scan_ms"] = scan
     del src, basis, w, s
     torch.cuda.empty_cache()
+
+
+def config5(a, ctx, L, R, seed, out):
+    import torch
     n = 16 << 30
     B5, dl5 = 131072, 4
     src = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -105,8 +120,6 @@ def main():
                                        ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(st)) == 0
         steps.append(round((time.perf_counter() - t) * 1e3, 3))
     out["config5_half_step_ms"] = steps
-    ctx.close()
-    print(json.dumps(out))
 
 
 if __name__ == "__main__":

@@ -20,9 +20,9 @@
 #   pmc-k1       one PMC pass over kbench: the production K1 against the same kernel without global loads
 #   pmc-walk     two PMC passes (SQ issue/wait/LDS counters) over one config-4 step (VARIANT): the chain walk's
 #                instruction mix and LDS bank conflicts
-#   kbench-k1    kbench: the K1 at B = 128 KiB and 8 KiB, the batched forms (1002, 1005, 1006)
+#   kbench-k1    kbench: the K1 at B = 128 KiB and 8 KiB, the batched forms (1002, 1005)
 #   e2e          java-rsync_amd/tools/e2e.py at config 5 (16 GiB from host memory)
-#   kb-ab        kbench A/Bs of KB_VARIANTS (default: production 1000 against the round-4 K1 forms) at the headline
+#   kb-ab        kbench A/Bs of KB_VARIANTS (default: the production entries 1000 1001 1003) at the headline
 #                shape, interleaved, then one clock pass (GRBM_GUI_ACTIVE) over the same variants
 #   kb-gather    kbench's Receiver block-gather A/Bs (KBENCH_GATHER: 4 GiB as 1 MiB ops)
 #   e2e4         java-rsync_amd/tools/e2e_config4.py: config 4's shard (128 x 128 MiB) from host memory, the segment
@@ -31,6 +31,8 @@
 #   receiver     the Receiver line (combineDataToFile on the config-2 shape)
 #   multi        bench.py --gpus 2 without a launcher (its own rank processes) on a one-GPU box: the N-rank path,
 #                ranks sharing the GPU (a rehearsal, not a scaling point); config 5 and config 4
+#   first        tools/first_call.py: the first calls on a fresh context against the later ones (config 4, config 5)
+#   first-trace  rocprofv3 HIP API + kernel trace of first_call.py --only 5 --reps 2 (where the first step's time goes)
 #   ab           AB_OPTS ("name=value ...") against the default, alternating, REPS times (AB_ARGS: bench args)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
@@ -108,7 +110,7 @@ for step in "$@"; do
                 --no-cpu-baseline --no-companions > "$O/pmc_walk_b.json" 2> "$O/pmc_walk_b.err") || exit 1 ;;
         kbench-k1)
             run 120 "$K" 16384 131072 4 8 1000 > "$O/kbench_128k.log" 2>&1
-            run 120 "$K" 16384 8192 3 8 1000 1002 1005 1006 > "$O/kbench_8k.log" 2>&1 ;;
+            run 120 "$K" 16384 8192 3 8 1000 1002 1005 > "$O/kbench_8k.log" 2>&1 ;;
         multi)
             run 300 python bench.py --gpus 2 --steps 5 --warmup 2 --no-cpu-baseline --no-companions \
                 > "$O/multi_file.json" 2> "$O/multi_file.err"
@@ -118,6 +120,10 @@ for step in "$@"; do
             > "$O/config3.json" 2> "$O/config3.err" ;;
         receiver) run 300 python bench.py --workload receiver --steps 2 --warmup 1 > "$O/receiver.json" 2> "$O/receiver.err" ;;
         e2e) run 400 python java-rsync_amd/tools/e2e.py --gib 16 > "$O/e2e_16GiB.json" 2> "$O/e2e.err" ;;
+        first) run 300 python java-rsync_amd/tools/first_call.py > "$O/first_call.json" 2> "$O/first_call.err" ;;
+        first-trace) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --hip-trace --kernel-trace -d "$O/first_trace" \
+            -o run --output-format csv -- python3 "$R/java-rsync_amd/tools/first_call.py" --only 5 --reps 2 \
+            > "$O/first_trace.json" 2> "$O/first_trace.err") || exit 1 ;;
         ab)  # the A/B switches are settable in the diagnostics build only: both arms load it
             DIAG_LIB="$R/java-rsync_amd/lib/diag/librsynchip.so"
             OPTS=""
