@@ -119,6 +119,12 @@ int rsh_block_sums(rsh_ctx* ctx, const uint8_t* data, int64_t n, const rsh_heade
 int rsh_block_sums_device(rsh_ctx* ctx, const void* d_data, int64_t n, const rsh_header* h, const uint8_t seed[4],
                           void* d_weak, void* d_strong);
 int rsh_ctx_sync(rsh_ctx* ctx);
+/* Releases the context's pass-sized buffers -- the segment passes' HBM (rsh_*_batch: up to 2 x the segment_bytes
+ * budget, 16 GiB by default), the Receiver passes', the host-input staging and the batched scan's tables and hit map --
+ * after waiting for the context's streams.  The next call that needs them allocates them again.  A JVM holding
+ * several contexts on one GPU (a local transfer's Generator and Sender) calls it after each segment; see
+ * INTEGRATION.md "Per-context memory".  Replaces nothing in the reference (its buffers are Java heap). */
+int rsh_ctx_trim(rsh_ctx* ctx);
 
 /* ---- Sender (Sender.java:1098-1148 per-file glue, :1235-1327 scan, :1386-1399 new file) ----
  * h: the header received from the Generator (validated here exactly as Connection.receiveChecksumHeader

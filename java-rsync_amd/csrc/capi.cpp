@@ -1409,6 +1409,26 @@ int rsh_ctx_sync(rsh_ctx* ctx) {
     return RSH_OK;
 }
 
+// The pass-sized buffers back to the device and host allocators (a Generator and a Sender context on one
+// GPU each kept 2 x segment_bytes of HBM between segments).  Small round-trip buffers stay: they are what the next
+// call would otherwise allocate on its latency path.
+int rsh_ctx_trim(rsh_ctx* ctx) {
+    if (!ctx) return RSH_E_INVAL;
+    RSH_CLAIM(ctx);
+    RSH_HIP(hipSetDevice(ctx->device));
+    for (hipStream_t st : {ctx->stream, ctx->aux, ctx->phase}) RSH_HIP(hipStreamSynchronize(st));
+    for (DevBuf* b : {&ctx->data, &ctx->weak, &ctx->strong, &ctx->seg_data, &ctx->seg_tab, &ctx->rcv[0], &ctx->rcv[1],
+                      &ctx->rcv_ops[0], &ctx->rcv_ops[1], &ctx->out})
+        b->release();
+    for (PinnedBuf* b : {&ctx->h_stage, &ctx->h_rcv_ops[0], &ctx->h_rcv_ops[1], &ctx->h_out, &ctx->h_win})
+        b->release();
+    if (ctx->batch) {  // the batched scan's tables, hit map and fiber stacks (rebuilt on the next batched call)
+        rsh::destroy_batch_state(ctx->batch);
+        ctx->batch = nullptr;
+    }
+    return RSH_OK;
+}
+
 // Generator.getBlockLengthFor / pow2SquareRoot (Generator.java:198-206, 219-236).
 int32_t rsh_block_length_for(int64_t file_size) {
     if (file_size <= 0) return 0;

@@ -99,6 +99,20 @@ final class NativeChecksum implements AutoCloseable {
         LIVE.remove(this);
     }
 
+    /**
+     * Releases the context's pass-sized buffers (rsh_ctx_trim: the segment and Receiver passes' HBM, the batched
+     * scan's tables).  The segment loops call it after a segment when more than one context shares the GPU
+     * (INTEGRATION.md "Per-context memory").
+     */
+    public void trim() {
+        lock.lock();
+        try {
+            ctxTrim(handle());
+        } finally {
+            lock.unlock();
+        }
+    }
+
     /** The live handle; the lock is held.  A closed context throws (the shim also rejects handle 0). */
     private long handle() {
         if (ctx == 0) {
@@ -282,6 +296,8 @@ final class NativeChecksum implements AutoCloseable {
     static native long ctxCreate(int device);
 
     static native void ctxDestroy(long ctx);
+
+    static native void ctxTrim(long ctx);
 
     static native int blockLengthFor(long fileSize);
 

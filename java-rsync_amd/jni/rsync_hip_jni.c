@@ -263,6 +263,14 @@ JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksu
     rsh_ctx_destroy((rsh_ctx*)(intptr_t)ctx); /* NULL is a no-op */
 }
 
+/* rsh_ctx_trim: the pass-sized buffers back to the allocators (throws on a device error). */
+JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_ctxTrim(JNIEnv* env, jclass cls,
+                                                                                        jlong ctx) {
+    (void)cls;
+    const int rc = rsh_ctx_trim((rsh_ctx*)(intptr_t)ctx);
+    if (rc != RSH_OK) throw_status(env, rc);
+}
+
 /* Generator.getBlockLengthFor / getDigestLength (Generator.java:198-212, :873). */
 JNIEXPORT jint JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_blockLengthFor(JNIEnv* env, jclass c,
                                                                                                jlong size) {

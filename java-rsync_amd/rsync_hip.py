@@ -138,7 +138,7 @@ EVENT_DTYPE = np.dtype([("offset", "<i8"), ("length", "<i8"), ("kind", "<i4"), (
 # every symbol include/rsync_hip.h declares
 EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_count", "rsh_ctx_create", "rsh_ctx_destroy",
            "rsh_ctx_stream", "rsh_block_length_for", "rsh_digest_length_for", "rsh_header_make",
-           "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_match_scan",
+           "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_ctx_trim", "rsh_match_scan",
            "rsh_match_scan_device", "rsh_match_scan_tiled", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
            "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_receiver_combine",
            "rsh_receiver_combine_device", "rsh_receiver_combine_batch", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_block_sums_batch", "rsh_match_scan_batch", "rsh_file_md5_batch", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
@@ -199,6 +199,7 @@ def lib():
         "rsh_block_sums": ([P, P, I64, HP, P, P, P], ctypes.c_int),
         "rsh_block_sums_device": ([P, P, I64, HP, P, P, P], ctypes.c_int),
         "rsh_ctx_sync": ([P], ctypes.c_int),
+        "rsh_ctx_trim": ([P], ctypes.c_int),
         "rsh_match_scan": ([P, P, I64, HP, P, P, P, P, I64, ctypes.POINTER(I64), P, ctypes.POINTER(I64),
                             ctypes.POINTER(I64), ctypes.POINTER(ScanStats)], ctypes.c_int),
         "rsh_match_scan_device": ([P, P, I64, HP, P, P, P, P, I64, ctypes.POINTER(I64), ctypes.POINTER(I64),
@@ -437,6 +438,10 @@ class Context:
 
     def sync(self):
         _check(lib().rsh_ctx_sync(self._p))
+
+    def trim(self):
+        """Release the pass-sized buffers (rsh_ctx_trim); the next call allocates what it needs again."""
+        _check(lib().rsh_ctx_trim(self._p))
 
     def alloc(self, nbytes):
         """Device buffer (DeviceBuffer) owned by this context's device."""

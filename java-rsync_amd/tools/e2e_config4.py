@@ -9,6 +9,9 @@ pieces).  Times, on one GPU:
              every file's MD5 on the host's cores), and 128 single-file rsh_match_scan calls (what a Java Sender
              without the segment natives would do: one serial file MD5 each)
   rsh_file_md5_batch alone (the 128 file MD5s), multi-buffer and scalar
+  Receiver   rsh_receiver_combine_batch over the 128 token streams (Receiver.receiveFiles in one call: the tokens
+             and the basis replicas from host memory, the gather on the device, the rebuilt files back to host
+             memory, every file's verify MD5 on the host's cores): the native call's time, targets preallocated
 and checks every file's events, literal/matched and file MD5 against the oracle's committed digests.  One JSON line.
 usage: python e2e_config4.py [--forms half,identical] [--reps 3] [--no-single]
 """
@@ -55,6 +58,41 @@ def best(fn, reps):
         out = fn()
         ts.append(time.perf_counter() - t)
     return out, ts
+
+
+def receiver(ctx, L, src, basis, res, h, pieces, F, S, gf, reps):
+    """The segment's Receiver from host memory: the token streams of the scan's events, the bases as replicas."""
+    import ctypes
+    toks = [np.frombuffer(R.tokens(src[i * S:(i + 1) * S], res[i][0], res[i][1]), np.uint8) for i in range(F)]
+    reps_p = [pieces(basis, i) for i in range(F)]
+    plist = [(R.Piece * 2)(*[R.Piece(x.ctypes.data, x.size) for x in rp]) for rp in reps_p]
+    tg = np.empty(F * (S + 64), np.uint8)
+    tg[::4096] = 0  # fault the targets in before the timed calls
+    jobs = (R.CombineJob * F)()
+
+    def call():
+        for i in range(F):
+            j = jobs[i]
+            j.tokens, j.tokens_len, j.h = toks[i].ctypes.data, toks[i].size, h
+            j.replica, j.nreplica = ctypes.cast(plist[i], ctypes.POINTER(R.Piece)), 2
+            j.defer_write, j.target, j.target_cap = 0, tg.ctypes.data + i * (S + 64), S + 64
+        return L.rsh_receiver_combine_batch(ctx.handle, jobs, F)
+    rcs, ts = [], []
+    for _ in range(reps):
+        t = time.perf_counter()
+        rcs.append(call())
+        ts.append(time.perf_counter() - t)
+    assert rcs == [0] * reps, rcs
+    bad = []
+    for i in range(F):
+        r = jobs[i].res
+        if jobs[i].status or r.target_len != S or bytes(r.md5).hex() != gf[i][4] or \
+                not np.array_equal(tg[i * (S + 64):i * (S + 64) + S], src[i * S:(i + 1) * S]):
+            bad.append(i)
+    assert not bad, f"receiver: files {bad[:8]} not rebuilt"
+    return {"receiver_batch_s": [round(t, 4) for t in ts], "receiver_batch_GBps": round(F * S / min(ts) / 1e9, 2),
+            "receiver_tokens_bytes": int(sum(t.size for t in toks)),
+            "receiver_parity": f"all {F} files rebuilt byte for byte, verify MD5 = the oracle's file MD5"}
 
 
 def main():
@@ -120,6 +158,7 @@ def main():
                     bad.append(i)
             assert not bad, f"{form}: files {bad[:8]} differ from the oracle's digests"
             r["parity"] = f"all {F} files: events, literal/matched and file MD5 equal the oracle's digests"
+            r.update(receiver(ctx, L, src, basis, res, h, pieces, F, S, g[form], a.reps))
             if not a.no_single:
                 t = time.perf_counter()
                 one = [ctx.block_sums(basis[i * S:(i + 1) * S], h, SEED) for i in range(F)]

@@ -64,7 +64,7 @@ for step in "$@"; do
                 || exit 1
             python3 java-rsync_amd/tools/clock_summary.py "$O/kb_ab_clock" > "$O/kb_ab_clock.txt" 2>&1 ;;
         kb-gather) KBENCH_GATHER=1048576 run 180 "$K" 4096 0 0 5 0 1 2 3 4 5 6 0 1 2 3 4 5 6 > "$O/kb_gather.log" 2>&1 ;;
-        e2e4) run 900 python java-rsync_amd/tools/e2e_config4.py > "$O/e2e_config4.json" 2> "$O/e2e_config4.err" ;;
+        e2e4) run 900 python java-rsync_amd/tools/e2e_config4.py $E2E4_ARGS > "$O/e2e_config4.json" 2> "$O/e2e_config4.err" ;;
         smoke) run 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.log" 2>&1 ;;
         bench) run 300 python bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
         hl) run 240 python bench.py --no-companions --no-files --no-cpu-baseline --steps 20 --warmup 5 $HL_ARGS \

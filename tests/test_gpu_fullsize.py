@@ -408,5 +408,28 @@ def test_config4_segment_vs_oracle(env, form, shard):
         if j % 40 == 0:
             assert hashlib.md5(memoryview(src[j * S:(j + 1) * S].cpu().numpy())).hexdigest() == fmd5
             _check_delta(torch, evs[j][:sj[j].n_ev], src[j * S:(j + 1) * S], basis[j * S:(j + 1) * S], h, lit, mat)
+    if shard == "gpu1":
+        # the segment's Receiver (rsh_receiver_combine_batch, Receiver.receiveFiles) from host
+        # memory -- every file's token stream (the Sender's, rsh_tokens_write over the events above) and its basis
+        # as the replica in two host pieces.  The oracle's Receiver rebuilds the source, so each file must come back
+        # byte for byte, with the literal / matched counts of the scan and the committed oracle file MD5.
+        hsrc, hbas = src.cpu().numpy(), basis.cpu().numpy()
+        del src, basis
+        torch.cuda.empty_cache()
+        cut = 3 * S // 7 + 5
+        jobs = []
+        for j, i in enumerate(files):
+            x = hsrc[j * S:(j + 1) * S]
+            tok = R.tokens(x, evs[j][:sj[j].n_ev], bytes.fromhex(g[form][i][4]))
+            rep = hbas[j * S:(j + 1) * S]
+            jobs.append((tok, h, [rep[:cut], rep[cut:]], False, S + 64))
+        out = ctx.receiver_combine_batch(jobs)
+        for j, i in enumerate(files):
+            status, tgt, r = out[j]
+            assert status == 0 and r.target_len == S, f"file {i}: status {status}"
+            assert (r.literal, r.matched) == (sj[j].literal, sj[j].matched), f"file {i}"
+            assert bytes(r.md5).hex() == g[form][i][4], f"file {i}: the rebuilt file's MD5"
+            assert tgt == hsrc[j * S:(j + 1) * S].tobytes(), f"file {i}: rebuilt bytes differ from the source"
+        return
     del src, basis
     torch.cuda.empty_cache()

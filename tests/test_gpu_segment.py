@@ -100,6 +100,32 @@ def test_segment_matches_oracle(ctx, rsh_opt, budget):
     assert status == 0 and ev.size == 0 and (lit, mat) == (0, 0) and fm == bytes.fromhex("d41d8cd98f00b204e9800998ecf8427e")
 
 
+def test_trim_releases_pass_buffers(ctx):
+    """rsh_ctx_trim (per-context HBM between segments): after a segment's Generator and Sender the
+    context holds its pass buffers; trim gives them back to the device (free HBM rises by at least the larger side's
+    bytes) and the next segment on the same context allocates them again with the same results."""
+    import torch
+    rng = random.Random(77)
+    files = _segment(rng, 12)
+    heads = [R.header_make(B, dl, basis.size) for basis, _, B, dl in files]
+
+    def run():
+        sums = ctx.block_sums_batch([([basis], h) for (basis, _, _, _), h in zip(files, heads)], SEED)
+        out, _ = ctx.match_scan_batch([([src], h, w, s) for (_, src, _, _), h, (w, s) in zip(files, heads, sums)],
+                                      SEED)
+        return [(w.tobytes(), s.tobytes()) for w, s in sums], [(R.events_as_tuples(o[0], 1), o[1:]) for o in out]
+    first = run()
+    ctx.sync()
+    free0 = torch.cuda.mem_get_info(0)[0]
+    ctx.trim()
+    free1 = torch.cuda.mem_get_info(0)[0]
+    seg = max(sum(basis.size for basis, _, _, _ in files), sum(src.size for _, src, _, _ in files))
+    assert free1 - free0 >= seg, (free0, free1, seg)
+    assert run() == first
+    ctx.trim()
+    ctx.trim()  # idempotent
+
+
 def test_segment_per_file_errors(ctx):
     """A short event buffer fails its own file only (RSH_E_NOSPACE with the count needed); a header that fails
     Checksum.Header's 4-arg checks is that file's RsyncProtocolException (RSH_E_PROTOCOL); the others succeed
