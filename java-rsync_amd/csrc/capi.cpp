@@ -593,6 +593,73 @@ hipError_t spec_buffers_free(rsh_ctx* c) {
     return hipStreamWaitEvent(c->stream, c->ev_rs_tail, 0);
 }
 
+// the segmented K1's descriptors: a wave per 64 windows of the prefix and phase speculations, up to 256 tails
+size_t scan_seg_bytes(int64_t na) { return ((size_t)na / 64 + 4) * sizeof(rsh::K1Seg) + 256 * sizeof(rsh::K1Tail); }
+
+// The single-file scan's per-window and per-chunk buffers for a source of na windows against a table of C chunks
+// (scan_device; ctx_warm sizes them once for a config-5 file).
+hipError_t scan_buffers_ensure(rsh_ctx* c, int64_t C, int64_t dl, int64_t na, bool download) {
+    const int64_t nf = std::min<int64_t>(na, C);
+    const uint32_t ns = pow2_at_least(2 * (uint64_t)C + 2);
+    hipError_t e = hipSuccess;
+    auto ok = [&](hipError_t x) {
+        if (e == hipSuccess) e = x;
+    };
+    if (download) {
+        ok(c->h_weak.ensure((size_t)C * 4 + 4));
+        ok(c->h_strong.ensure((size_t)C * dl + 1));
+    }
+    ok(c->slots.ensure((size_t)ns * sizeof(unsigned long long)));
+    ok(c->src_weak.ensure((size_t)na * 4));
+    ok(c->src_strong.ensure((size_t)na * dl + 1));
+    ok(c->flags.ensure((size_t)nf + 1));
+    ok(c->h_aw.ensure((size_t)na * 4));
+    ok(c->h_as.ensure((size_t)na * dl + 1));
+    ok(c->h_fl.ensure((size_t)nf + 1));
+    ok(c->haw.ensure((size_t)na * 4));
+    for (int i = 0; i < 2; ++i) {
+        ok(c->ph_weak[i].ensure((size_t)na * 4));
+        ok(c->ph_strong[i].ensure((size_t)na * dl + 1));
+        ok(c->h_pw[i].ensure((size_t)na * 4));
+        ok(c->h_ps[i].ensure((size_t)na * dl + 1));
+    }
+    ok(c->segs.ensure(scan_seg_bytes(na)));
+    ok(c->h_segs.ensure(scan_seg_bytes(na)));
+    return e;
+}
+
+// rsh_ctx_create, after the streams (a JVM pays a context's first call once per context).  The
+// runtime loads a file's code object at the first launch of any of its kernels -- 1.8 ms for device.hip's, 0.6 ms
+// for device_scan.hip's on the first config-5 step of a fresh context (rocprofv3 HIP API trace, profiles/r5) -- and
+// the first scan allocated ~25 pinned buffers at ~90 us each, some on its critical path.  Here: one empty launch
+// per code object, and the single-file scan's buffers at a config-5 size (2^17 windows and chunks, dl 16, B 128 KiB):
+// ~13 MiB of pinned host memory and ~16 MiB of HBM per context, which a larger file grows as before.
+hipError_t ctx_warm(rsh_ctx* c) {
+    constexpr int64_t kC = 1 << 17, kDl = 16, kB = 128 << 10;
+    hipError_t e = hipSuccess;
+    auto ok = [&](hipError_t x) {
+        if (e == hipSuccess) e = x;
+    };
+    ok(rsh::launch_warm_k1(c->stream));
+    ok(rsh::launch_warm_scan(c->stream));
+    ok(rsh::launch_warm_io(c->stream));
+    ok(scan_buffers_ensure(c, kC, kDl, kC, true));
+    ok(prep_ensure(c, kLeadWindows + rsh::opt(rsh::OPT_SCAN_SAMPLES) + 1));
+    constexpr size_t kSmall = 64 << 10;  // PinnedBuf's least allocation
+    for (PinnedBuf* b : {&c->h_lead, &c->h_prep, &c->h_pend, &c->h_keys, &c->h_iv, &c->h_tiles, &c->h_ptiles,
+                         &c->h_psegs, &c->h_first, &c->h_bucket, &c->h_files})
+        ok(b->ensure(kSmall));
+    ok(c->h_win0.ensure((size_t)kB + 16));
+    ok(c->h_win.ensure((size_t)kB));
+    ok(c->h_hit.ensure(16 + (size_t)kScanWindows * kB));
+    ok(c->partials.ensure(kSmall));
+    ok(c->bucket.ensure(rsh::HIT_BUCKET_INTS * sizeof(int32_t)));
+    ok(c->first.ensure(kFirstSlots * sizeof(rsh::ProbeOut)));
+    ok(c->dslots.ensure(kSmall));
+    ok(hipStreamSynchronize(c->stream));
+    return e;
+}
+
 // The device-resident Sender scan (everything but the whole-file MD5).  h validated by the caller;
 // n > 0, block_length > 0.  host_weak/host_strong may be null (then copied back from the device).
 //
@@ -617,27 +684,8 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
 
     // every buffer first (hipMalloc may synchronise), then the asynchronous work
     const bool download = !host_weak || !host_strong;
-    if (download) {
-        RSH_HIP(c->h_weak.ensure((size_t)C * 4 + 4));
-        RSH_HIP(c->h_strong.ensure((size_t)C * dl + 1));
-    }
-    RSH_HIP(c->slots.ensure((size_t)ns * sizeof(unsigned long long)));
-    RSH_HIP(c->src_weak.ensure((size_t)na * 4));
-    RSH_HIP(c->src_strong.ensure((size_t)na * dl + 1));
-    RSH_HIP(c->flags.ensure((size_t)nf + 1));
-    RSH_HIP(c->h_aw.ensure((size_t)na * 4));
-    RSH_HIP(c->h_as.ensure((size_t)na * dl + 1));
-    RSH_HIP(c->h_fl.ensure((size_t)nf + 1));
-    RSH_HIP(c->haw.ensure((size_t)na * 4));
-    for (int i = 0; i < 2; ++i) {
-        RSH_HIP(c->ph_weak[i].ensure((size_t)na * 4));
-        RSH_HIP(c->ph_strong[i].ensure((size_t)na * dl + 1));
-        RSH_HIP(c->h_pw[i].ensure((size_t)na * 4));
-        RSH_HIP(c->h_ps[i].ensure((size_t)na * dl + 1));
-    }
-    const size_t seg_bytes = ((size_t)na / 64 + 4) * sizeof(rsh::K1Seg) + 256 * sizeof(rsh::K1Tail);
-    RSH_HIP(c->segs.ensure(seg_bytes));
-    RSH_HIP(c->h_segs.ensure(seg_bytes));
+    RSH_HIP(scan_buffers_ensure(c, C, dl, na, download));
+    const size_t seg_bytes = scan_seg_bytes(na);
     // sample windows for the launch decision: the first nlead, then one every `stride` windows
     const int64_t nlead = std::min<int64_t>(kLeadWindows, nf);
     const int64_t nsamples = std::max<int64_t>(1, rsh::opt(rsh::OPT_SCAN_SAMPLES));
@@ -1386,6 +1434,11 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
         delete c;
         return RSH_E_DEVICE;
     }
+    if (ctx_warm(c) != hipSuccess) {
+        (void)hipStreamSynchronize(c->stream);
+        delete c;
+        return RSH_E_DEVICE;
+    }
     *out = c;
     return RSH_OK;
 }
@@ -1420,8 +1473,9 @@ int rsh_ctx_trim(rsh_ctx* ctx) {
     for (DevBuf* b : {&ctx->data, &ctx->weak, &ctx->strong, &ctx->seg_data, &ctx->seg_tab, &ctx->rcv[0], &ctx->rcv[1],
                       &ctx->rcv_ops[0], &ctx->rcv_ops[1], &ctx->out})
         b->release();
-    for (PinnedBuf* b : {&ctx->h_stage, &ctx->h_rcv_ops[0], &ctx->h_rcv_ops[1], &ctx->h_out, &ctx->h_win})
+    for (PinnedBuf* b : {&ctx->h_stage, &ctx->h_rcv_ops[0], &ctx->h_rcv_ops[1], &ctx->h_out})
         b->release();
+    if (ctx->h_win.cap > (1u << 20)) ctx->h_win.release();  // (a Receiver pass's pieces; the scan's windows are small)
     if (ctx->batch) {  // the batched scan's tables, hit map and fiber stacks (rebuilt on the next batched call)
         rsh::destroy_batch_state(ctx->batch);
         ctx->batch = nullptr;

@@ -117,6 +117,11 @@ hipError_t launch_block_sums_batch(const K1Group* d_groups, uint32_t ngroups, co
 hipError_t launch_chain_flags(const int32_t* d_wsrc, const uint8_t* d_ssrc, const int32_t* d_wbas,
                               const uint8_t* d_sbas, uint32_t count, uint32_t dl, uint8_t* d_flags,
                               hipStream_t s);
+// One empty kernel per code object (device.hip, device_scan.hip, device_io.hip): rsh_ctx_create launches them so that
+// the runtime loads every production kernel before the first call.
+hipError_t launch_warm_k1(hipStream_t s);
+hipError_t launch_warm_scan(hipStream_t s);
+hipError_t launch_warm_io(hipStream_t s);
 // Completion without a marker packet: the launch's last workgroup to finish writes `gen` into *stamp (pinned host
 // memory, system-scope release after every workgroup's stores), which the host polls.  counter: device memory,
 // zero before the launch (the last workgroup zeroes it again).

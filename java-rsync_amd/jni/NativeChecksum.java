@@ -63,6 +63,11 @@ final class NativeChecksum implements AutoCloseable {
         return c;
     }
 
+    /** More live contexts than devices: some GPU holds two of them (trim() between segments, INTEGRATION.md). */
+    static boolean sharesDevice() {
+        return LIVE.size() > Math.max(1, Integer.getInteger("rsync.hip.devices", 1));
+    }
+
     /** Destroys the calling thread's context, if it has one (idempotent). */
     static void releaseForThread() {
         NativeChecksum c = PER_THREAD.get();
