@@ -647,7 +647,7 @@ hipError_t ctx_warm(rsh_ctx* c) {
     ok(prep_ensure(c, kLeadWindows + rsh::opt(rsh::OPT_SCAN_SAMPLES) + 1));
     constexpr size_t kSmall = 64 << 10;  // PinnedBuf's least allocation
     for (PinnedBuf* b : {&c->h_lead, &c->h_prep, &c->h_pend, &c->h_keys, &c->h_iv, &c->h_tiles, &c->h_ptiles,
-                         &c->h_psegs, &c->h_first, &c->h_bucket, &c->h_files})
+                         &c->h_psegs, &c->h_first, &c->h_bucket, &c->h_files, &c->h_pos, &c->h_out})
         ok(b->ensure(kSmall));
     ok(c->h_win0.ensure((size_t)kB + 16));
     ok(c->h_win.ensure((size_t)kB));

@@ -1215,6 +1215,7 @@ hipError_t launch_chain_flags(const int32_t* d_wsrc, const uint8_t* d_ssrc, cons
 // 0.6-1.8 ms on a fresh context, which rsh_ctx_create pays instead of the first call (launch_warm).
 __global__ void warm_k1_kernel() {}
 hipError_t launch_warm_k1(hipStream_t s) {
+    if (!never_word()) return hipErrorOutOfMemory;  // (allocated once per device; the Generator's K1 polls it)
     hipLaunchKernelGGL(warm_k1_kernel, dim3(1), dim3(64), 0, s);
     return hipGetLastError();
 }

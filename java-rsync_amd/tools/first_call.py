@@ -108,7 +108,7 @@ def config5(a, ctx, L, R, seed, out):
     ev = np.zeros(C5 + n // B5 + 4096, R.EVENT_DTYPE)
     n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     st = R.ScanStats()
-    steps = []
+    steps, k1 = [], []
     for r in range(a.reps):
         t = time.perf_counter()
         assert L.rsh_block_sums_device(ctx.handle, ctypes.c_void_p(basis.data_ptr()), n, ctypes.byref(h5),
@@ -119,7 +119,9 @@ def config5(a, ctx, L, R, seed, out):
                                        seed.ctypes.data, ev.ctypes.data, ev.size, ctypes.byref(n_ev),
                                        ctypes.byref(lit), ctypes.byref(mat), ctypes.byref(st)) == 0
         steps.append(round((time.perf_counter() - t) * 1e3, 3))
+        k1.append(round(ctx.kernel_ms(0), 3))
     out["config5_half_step_ms"] = steps
+    out["config5_generator_k1_ms"] = k1
 
 
 if __name__ == "__main__":
