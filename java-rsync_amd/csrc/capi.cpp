@@ -998,10 +998,18 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         }
     }
     if (on_ctx) {  // (aux) the table and the probe hash, after a tentative launch's abort (above)
-        int rc = table_work();
-        if (rc == RSH_OK) rc = table_wait();
+        int rc;
+        {
+            CallTrace tr("table_work", C);
+            rc = table_work();
+        }
+        if (rc == RSH_OK) {
+            CallTrace tr("table_wait", C);
+            rc = table_wait();
+        }
         if (rc != RSH_OK) return rc;
     }
+    if (CallTrace::on()) fprintf(stderr, "[rsh] resolver   starts at %9.3f ms\n", ms_since(t0));
     HipBackend be(c, d_src, n, table, d_weak, seed);
     be.rs_ = rs;
     be.table.slots = c->slots.as<unsigned long long>();

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--trace", action="store_true", help="scan_trace = 2 on the first batched scan")
     ap.add_argument("--only", type=int, default=0, help="4 or 5: that configuration only (0: both)")
+    ap.add_argument("--trace5", action="store_true", help="scan_trace = 1 on every config-5 step (stderr)")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -109,7 +110,11 @@ def config5(a, ctx, L, R, seed, out):
     n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     st = R.ScanStats()
     steps, k1 = [], []
+    if a.trace5:
+        R.set_option("scan_trace", 1)
     for r in range(a.reps):
+        if a.trace5:
+            print(f"[first_call] config-5 step {r}", file=sys.stderr, flush=True)
         t = time.perf_counter()
         assert L.rsh_block_sums_device(ctx.handle, ctypes.c_void_p(basis.data_ptr()), n, ctypes.byref(h5),
                                        seed.ctypes.data, ctypes.c_void_p(w5.data_ptr()),

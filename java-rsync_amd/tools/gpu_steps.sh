@@ -33,6 +33,10 @@
 #                ranks sharing the GPU (a rehearsal, not a scaling point); config 5 and config 4
 #   first        tools/first_call.py: the first calls on a fresh context against the later ones (config 4, config 5)
 #   first-trace  rocprofv3 HIP API + kernel trace of first_call.py --only 5 --reps 2 (where the first step's time goes)
+#   copycb       rocprofv3 --memory-copy-trace over tools/queue_lat.hip (3 D2H hipMemcpyAsync per rep, no librsynchip):
+#                does the profiler report undelivered copy completions for plain runtime copies too
+#   copycb5      rocprofv3 --memory-copy-trace --hip-trace over first_call.py --only 5 (then --only 4): which of the
+#                library's copies the profiler reports undelivered
 #   ab           AB_OPTS ("name=value ...") against the default, alternating, REPS times (AB_ARGS: bench args)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
@@ -120,7 +124,16 @@ for step in "$@"; do
             > "$O/config3.json" 2> "$O/config3.err" ;;
         receiver) run 300 python bench.py --workload receiver --steps 2 --warmup 1 > "$O/receiver.json" 2> "$O/receiver.err" ;;
         e2e) run 400 python java-rsync_amd/tools/e2e.py --gib 16 > "$O/e2e_16GiB.json" 2> "$O/e2e.err" ;;
+        copycb) (cd /tmp && export TMPDIR=/tmp && run 120 rocprofv3 --memory-copy-trace --kernel-trace -d "$O/copycb" \
+            -o run --output-format csv -- "$R/java-rsync_amd/lib/queue_lat" 4 > "$O/copycb.log" 2> "$O/copycb.err") || exit 1 ;;
+        copycb5) for o in 5 4; do
+                (cd /tmp && export TMPDIR=/tmp && run 240 rocprofv3 --memory-copy-trace --hip-trace -d "$O/copycb_$o" \
+                    -o run --output-format csv -- python3 "$R/java-rsync_amd/tools/first_call.py" --only $o --reps 2 \
+                    > "$O/copycb_$o.log" 2> "$O/copycb_$o.err") || exit 1
+            done ;;
         first) run 300 python java-rsync_amd/tools/first_call.py > "$O/first_call.json" 2> "$O/first_call.err" ;;
+        first5) run 300 python java-rsync_amd/tools/first_call.py --only 5 --reps 4 --trace5 > "$O/first5.json" \
+            2> "$O/first5.err" ;;
         first-trace) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --hip-trace --kernel-trace -d "$O/first_trace" \
             -o run --output-format csv -- python3 "$R/java-rsync_amd/tools/first_call.py" --only 5 --reps 2 \
             > "$O/first_trace.json" 2> "$O/first_trace.err") || exit 1 ;;
