@@ -656,6 +656,21 @@ hipError_t ctx_warm(rsh_ctx* c) {
     ok(c->bucket.ensure(rsh::HIT_BUCKET_INTS * sizeof(int32_t)));
     ok(c->first.ensure(kFirstSlots * sizeof(rsh::ProbeOut)));
     ok(c->dslots.ensure(kSmall));
+    // the runtime's copy and fill paths, on each of the context's streams: the first D2H copy of a process took
+    // 6.8 ms (the single-file scan's table download, its first call in a fresh process: scan_trace, profiles/r5)
+    if (e == hipSuccess) {
+        uint8_t* d = c->slots.as<uint8_t>();
+        uint8_t* hp = c->h_keys.as<uint8_t>();
+        for (hipStream_t st : {c->stream, c->aux, c->phase}) {
+            ok(hipMemsetAsync(d, 0, 4096, st));
+            ok(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d + 4096), 0, 1024, st));
+            ok(hipMemcpyAsync(hp, d, 4096, hipMemcpyDeviceToHost, st));
+            ok(hipMemcpyAsync(d + 8192, hp, 4096, hipMemcpyHostToDevice, st));
+            ok(hipMemcpyAsync(d + 12288, d, 4096, hipMemcpyDeviceToDevice, st));
+            ok(hipMemcpyAsync(c->h_weak.p, d, 512 << 10, hipMemcpyDeviceToHost, st));  // table-sized (h_weak: C 4 + 4)
+            ok(hipStreamSynchronize(st));
+        }
+    }
     ok(hipStreamSynchronize(c->stream));
     return e;
 }

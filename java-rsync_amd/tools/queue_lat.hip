@@ -17,6 +17,9 @@
 //  12  busy through hipExtLaunchKernelGGL with a stop event only, then tiny
 //  13  busy, then a 128 KiB D2H hipMemcpyAsync into pinned memory: the host time the call itself takes (printed)
 //  14  busy on stream 1, event, stream 2 waits, a 128 KiB D2H on stream 2: the host time of the copy call (printed)
+//  15  busy, then on stream 2 two 512 KiB D2H hipMemcpyAsync into pinned memory, an event, hipEventSynchronize on it
+//      (the single-file scan's table download: under rocprofv3 --memory-copy-trace, are their completions delivered)
+//  16  the same with 128 KiB copies
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -54,8 +57,8 @@ int main(int argc, char** argv) {
     float* d;
     CK(hipMalloc(&d, 4096 * sizeof(float)));
     unsigned char *hp, *dp;
-    CK(hipHostMalloc(&hp, 1 << 17, hipHostMallocDefault));
-    CK(hipMalloc(&dp, 1 << 17));
+    CK(hipHostMalloc(&hp, 1 << 20, hipHostMallocDefault));
+    CK(hipMalloc(&dp, 1 << 20));
     hipEvent_t en, et, ea, eb, old;
     CK(hipEventCreateWithFlags(&en, hipEventDisableTiming));
     CK(hipEventCreate(&et));
@@ -66,7 +69,7 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s1));
     const dim3 G(256), T(64);
     for (int r = 0; r < reps; ++r) {
-        for (int c = 1; c <= 14; ++c) {
+        for (int c = 1; c <= 16; ++c) {
             const auto t0 = std::chrono::steady_clock::now();
             double call_us = -1;
             if (c == 4) {
@@ -111,6 +114,15 @@ int main(int argc, char** argv) {
                     CK(hipStreamWaitEvent(s2, en, 0));
                     CK(hipMemcpyAsync(hp, dp, 1 << 17, hipMemcpyDeviceToHost, s2));
                     call_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c0).count();
+                    break;
+                }
+                case 15:
+                case 16: {
+                    const size_t sz = c == 15 ? (1u << 19) : (1u << 17);
+                    CK(hipMemcpyAsync(hp, dp, sz, hipMemcpyDeviceToHost, s2));
+                    CK(hipMemcpyAsync(hp + sz, dp + sz, sz, hipMemcpyDeviceToHost, s2));
+                    CK(hipEventRecord(en, s2));
+                    CK(hipEventSynchronize(en));
                     break;
                 }
                 default: break;
