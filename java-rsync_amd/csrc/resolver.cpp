@@ -148,6 +148,74 @@ int64_t first_mismatch(const void* a, const void* b, int64_t count, int64_t esiz
 }
 }  // namespace
 
+void flush_positions(const FlushChain& q, std::vector<int64_t>* tpos, std::vector<int64_t>* bpos) {
+    tpos->clear();
+    bpos->clear();
+    for (int64_t i = 0; i < q.K; ++i) {
+        const int64_t fi = q.f + 10 * q.B * i;
+        tpos->push_back(fi);
+        tpos->push_back(fi + q.B);
+        bpos->push_back(fi);
+        bpos->push_back(fi + 2 * q.B - 1 < q.n ? fi + 2 * q.B - 1 : fi);
+    }
+}
+
+void flush_intervals(const FlushChain& q, std::vector<FlushStep>* steps, std::vector<ProbeInterval>* ivs) {
+    steps->clear();
+    ivs->clear();
+    for (int64_t i = 0; i < q.K; ++i) {
+        const int64_t s2 = q.f + 10 * q.B * i + q.B;
+        steps->push_back(FlushStep{s2, 0u, 0u});
+        if (s2 > q.last) break;
+        const int64_t fn = (s2 + 10 * q.B <= q.n) ? s2 + 9 * q.B : std::numeric_limits<int64_t>::max();
+        ivs->push_back(ProbeInterval{s2, std::min(fn, q.last) + 1, s2, 0u, 0u});
+    }
+}
+
+// The flush bookkeeping of Sender.java:1294-1310 from the rolling value R at each flush point (quirk A): the Java
+// code subtracts x_f with the full window, slides by B, adds the window's new last byte only when the window is
+// still full, and keeps rolling the old value -- so after flush i the desync is E_i = R2_i - T(s2_i).
+void flush_chain_host(const FlushChain& q, const int32_t* tv, const uint8_t* bv, std::vector<FlushStep>* steps,
+                      std::vector<ProbeInterval>* ivs) {
+    flush_intervals(q, steps, ivs);
+    const int64_t B = q.B, n = q.n, last = q.last;
+    auto clampB = [&](int64_t p) { return std::min<int64_t>(p, n - B); };
+    int32_t R = pack16(lo16(tv[0]) + q.el, hi16(tv[0]) + q.eh);
+    for (size_t i = 0; i < steps->size(); ++i) {
+        FlushStep& stp = (*steps)[i];
+        const int32_t R1 = roll_sub(R, (int32_t)B, bv[2 * i]);
+        int32_t R2 = R1;
+        if (stp.s2 <= last && std::min<int64_t>(B, n - stp.s2) == B) R2 = roll_add(R1, bv[2 * i + 1]);  // :1308-1310
+        const int32_t T2 = tv[2 * i + 1];
+        stp.elo = (lo16(R2) - lo16(T2)) & 0xFFFFu;
+        stp.ehi = (hi16(R2) - hi16(T2)) & 0xFFFFu;
+        if (i < ivs->size()) {
+            (*ivs)[i].e_lo = stp.elo;
+            (*ivs)[i].e_hi = stp.ehi;
+        }
+        if (stp.s2 > last) break;
+        if ((int64_t)i + 1 < q.K) {  // the rolling value at the next flush point
+            const int64_t fn = (stp.s2 + 10 * B <= n) ? stp.s2 + 9 * B : std::numeric_limits<int64_t>::max();
+            const uint32_t ehi2 = stp.ehi + stp.elo * (uint32_t)(clampB(fn) - clampB(stp.s2));
+            R = pack16(lo16(tv[2 * i + 2]) + stp.elo, hi16(tv[2 * i + 2]) + ehi2);
+        }
+    }
+}
+
+int64_t ScanBackend::flush_probe(const ProbeInterval* pre, int64_t npre, const FlushChain& q,
+                                 std::vector<FlushStep>* steps, std::vector<ProbeInterval>* ivs,
+                                 const std::vector<int32_t>* keys) {
+    std::vector<int64_t> tpos, bpos;
+    flush_positions(q, &tpos, &bpos);
+    std::vector<int32_t> tv(tpos.size());
+    std::vector<uint8_t> bv(bpos.size());
+    flush_gather(tpos.data(), (int64_t)tpos.size(), tv.data(), bpos.data(), (int64_t)bpos.size(), bv.data());
+    flush_chain_host(q, tv.data(), bv.data(), steps, ivs);
+    std::vector<ProbeInterval> all(pre, pre + npre);
+    all.insert(all.end(), ivs->begin(), ivs->end());
+    return all.empty() ? -1 : first_hit(all.data(), (int64_t)all.size(), keys);
+}
+
 bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* state, ResolveResult* out,
                  const std::function<bool()>& yield) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -227,17 +295,6 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
         if (p % B == 0 && p / B < NAL()) return aw[p / B];
         return be.weak_at(p);
     };
-    // Flush bookkeeping shared by the single and the batched path: from the rolling value R at the
-    // flush point f (window B), the state after FileView slides by a whole window (quirk A).
-    auto after_flush = [&](int64_t f, int32_t R, uint8_t xf, uint8_t xlast, int32_t T2, uint32_t* nelo,
-                           uint32_t* nehi) {
-        const int32_t R1 = roll_sub(R, (int32_t)B, xf);
-        const int64_t s2 = f + B;
-        int32_t R2 = R1;
-        if (s2 <= last && wl(s2) == B) R2 = roll_add(R1, xlast);  // :1308-1310
-        *nelo = (lo16(R2) - lo16(T2)) & 0xFFFFu;
-        *nehi = (hi16(R2) - hi16(T2)) & 0xFFFFu;
-    };
     // FileView flush at f (isFull, Sender.java:1294-1302) with rolling value R at f: the Java code
     // subtracts x_f with the full window, slides by B and keeps rolling the old value.
     auto flush = [&](int64_t f, int32_t R) {
@@ -259,6 +316,60 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
 
     auto elapsed = [&] {
         st.resolver_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    };
+    // The batched flush chain from the flush point f.  No candidate before f: speculate that none occurs in the
+    // next K flush intervals either -- their flush points are f + 10B i (FileView.isFull at mark + 9B), the rolling
+    // value's desync E after each one is a closed-form function of T and two bytes at the flush (flush_chain_host)
+    // -- so one gather, the chain and one probe over all K intervals replace K round trips (the GPU backends do all
+    // three in one).  K doubles while no event turns up (wasted probing <= 2x).  The doubling starts higher when
+    // candidates are rare: a stale digest carried by few chunks leaves about |keys| 10B / 2^32 candidate positions
+    // per interval (x4 for the weak sums' uneven spread), so a poisoned state with a handful of keys probes
+    // thousands of intervals at once instead of climbing from one through a dozen round trips.  The batch size only
+    // decides how much is speculated per probe, never the result.
+    auto flush_chain_at = [&](int64_t f, const std::vector<int32_t>* keys) -> FlushChain {
+        const int64_t nkeys = keys ? (int64_t)keys->size() : (int64_t)table.chunk_count;
+        const int64_t floor_k = std::clamp<int64_t>((int64_t)((1ull << 32) / ((uint64_t)(40 * B) * (uint64_t)std::max<int64_t>(nkeys, 1))), 1, 4096);
+        batch = std::max(batch, floor_k);
+        int64_t K = 1;
+        const int64_t kcap = std::min(max_batch, be.max_batch_at(f));
+        while (K < std::min(batch, kcap) && f + 10 * B * K + B <= n) ++K;
+        FlushChain q;
+        q.f = f, q.K = K, q.B = B, q.n = n, q.last = last;
+        E_at(f, &q.el, &q.eh);
+        return q;
+    };
+    // One round: the intervals pre (E known, ending at pre_end) and the chain's.  A hit inside pre is left in
+    // pre_hit for the caller (returns false); otherwise every flush before the interval holding the hit (all of
+    // them without one) is committed and true is returned.
+    int64_t pre_hit = -1;
+    auto flush_round = [&](const ProbeInterval* pre, int64_t npre, const FlushChain& q, const std::vector<int32_t>* keys,
+                           int64_t pre_end) -> bool {
+        std::vector<FlushStep> chain;
+        std::vector<ProbeInterval> iv;
+        const int64_t hit = be.flush_probe(pre, npre, q, &chain, &iv, keys);
+        if (npre > 0 || !iv.empty()) st.probe_launches++;
+        if (npre > 0 && hit >= 0 && hit <= pre_end) {
+            pre_hit = hit;
+            return false;
+        }
+        // commit every flush whose following interval holds no candidate
+        int64_t commit = (int64_t)chain.size();
+        if (hit >= 0)
+            for (size_t j = 0; j < iv.size(); ++j)
+                if (hit >= iv[j].a && hit < iv[j].b) {
+                    commit = (int64_t)j + 1;  // flushes 0..j happen before the event
+                    break;
+                }
+        for (int64_t i = 0; i < commit; ++i) {
+            emit_lit(m, 10 * B);
+            st.flushes++;
+            m = s = chain[(size_t)i].s2;
+            elo = chain[(size_t)i].elo;
+            ehi = chain[(size_t)i].ehi;
+            anchor = s;
+        }
+        batch = hit >= 0 ? 1 : std::min<int64_t>(batch * 2, 4096);
+        return true;
     };
     while (s <= last) {
         if (yield && yield()) {  // between two steps: the caller resumes with the same state
@@ -363,8 +474,17 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
                 uint32_t el, eh;
                 E_at(a, &el, &eh);
                 const ProbeInterval one{a, stop + 1, a, el, eh};
-                p = be.first_hit(&one, 1, keys);
-                st.probe_launches++;
+                if (md5c_valid && f <= last) {
+                    // A stale digest's few keys: an event before the flush point is unlikely, so the batched flush
+                    // chain after it (below) is probed in the same round trip, this interval first.
+                    const FlushChain q = flush_chain_at(f, keys);
+                    state->clear_from = state->clear_to = -1;
+                    if (flush_round(&one, 1, q, keys, stop)) continue;  // no event in [a, stop]: flushes committed
+                    p = pre_hit;
+                } else {
+                    p = be.first_hit(&one, 1, keys);
+                    st.probe_launches++;
+                }
             }
         }
         state->clear_from = state->clear_to = -1;
@@ -430,83 +550,8 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
             continue;
         }
         if (f <= last) {
-            // No candidate before the flush point.  Speculate that none occurs in the next K flush
-            // intervals either: their flush points are f + 10B i (FileView.isFull at mark + 9B), the
-            // rolling value's desync E after each one is a closed-form function of T and two bytes at
-            // the flush, so one batched gather, a host chain and one probe over all K intervals
-            // replace K round trips.  K doubles while no event turns up (wasted probing <= 2x).
-            // flush i sits at f_i = f + 10B i and happens iff its mark m_i = f_i - 9B has m_i + 10B <= n
-            // The doubling starts higher when candidates are rare: a stale digest carried by few chunks leaves
-            // about |keys| 10B / 2^32 candidate positions per interval (x4 for the weak sums' uneven spread), so a
-            // poisoned state with a handful of keys probes thousands of intervals at once instead of climbing
-            // from one through a dozen round trips.  The batch size only decides how much is speculated per
-            // probe, never the result.
-            const int64_t nkeys = keys ? (int64_t)keys->size() : (int64_t)table.chunk_count;
-            const int64_t floor_k = std::clamp<int64_t>((int64_t)((1ull << 32) / ((uint64_t)(40 * B) * (uint64_t)std::max<int64_t>(nkeys, 1))), 1, 4096);
-            batch = std::max(batch, floor_k);
-            int64_t K = 1;
-            const int64_t kcap = std::min(max_batch, be.max_batch_at(f));
-            while (K < std::min(batch, kcap) && f + 10 * B * K + B <= n) ++K;
-            std::vector<int64_t> tpos, bpos;
-            for (int64_t i = 0; i < K; ++i) {
-                const int64_t fi = f + 10 * B * i;
-                tpos.push_back(fi);
-                tpos.push_back(fi + B);
-                bpos.push_back(fi);
-                bpos.push_back(fi + 2 * B - 1 < n ? fi + 2 * B - 1 : fi);
-            }
-            std::vector<int32_t> tv(tpos.size());
-            std::vector<uint8_t> bv(bpos.size());
-            be.flush_gather(tpos.data(), (int64_t)tpos.size(), tv.data(), bpos.data(), (int64_t)bpos.size(), bv.data());
-            // host chain: state after each flush, the interval it opens
-            struct Step {
-                int64_t s2;
-                uint32_t elo, ehi;
-            };
-            std::vector<Step> chain;
-            std::vector<ProbeInterval> iv;
-            uint32_t el, eh;
-            E_at(f, &el, &eh);
-            int32_t R = pack16(lo16(tv[0]) + el, hi16(tv[0]) + eh);
-            int64_t mm = m;
-            for (int64_t i = 0; i < K; ++i) {
-                const int64_t fi = f + 10 * B * i;
-                Step stp;
-                stp.s2 = fi + B;
-                after_flush(fi, R, bv[2 * i], bv[2 * i + 1], tv[2 * i + 1], &stp.elo, &stp.ehi);
-                chain.push_back(stp);
-                mm = stp.s2;
-                if (stp.s2 > last) break;
-                const int64_t fn = (mm + 10 * B <= n) ? mm + 9 * B : std::numeric_limits<int64_t>::max();
-                iv.push_back(ProbeInterval{stp.s2, std::min(fn, last) + 1, stp.s2, stp.elo, stp.ehi});
-                if (i + 1 < K) {  // rolling value at the next flush point
-                    const uint32_t elo2 = stp.elo;
-                    const uint32_t ehi2 = stp.ehi + stp.elo * (uint32_t)(clampB(fn) - clampB(stp.s2));
-                    R = pack16(lo16(tv[2 * i + 2]) + elo2, hi16(tv[2 * i + 2]) + ehi2);
-                }
-            }
-            int64_t hit = -1;
-            if (!iv.empty()) {
-                hit = be.first_hit(iv.data(), (int64_t)iv.size(), keys);
-                st.probe_launches++;
-            }
-            // commit every flush whose following interval holds no candidate
-            int64_t commit = (int64_t)chain.size();
-            if (hit >= 0)
-                for (size_t j = 0; j < iv.size(); ++j)
-                    if (hit >= iv[j].a && hit < iv[j].b) {
-                        commit = (int64_t)j + 1;  // flushes 0..j happen before the event
-                        break;
-                    }
-            for (int64_t i = 0; i < commit; ++i) {
-                emit_lit(m, 10 * B);
-                st.flushes++;
-                m = s = chain[i].s2;
-                elo = chain[i].elo;
-                ehi = chain[i].ehi;
-                anchor = s;
-            }
-            batch = hit >= 0 ? 1 : std::min<int64_t>(batch * 2, 4096);
+            // No candidate before the flush point: the batched flush chain (flush_round above)
+            flush_round(nullptr, 0, flush_chain_at(f, keys), keys, -1);
             continue;  // the loop re-finds the event (if any) in [s, stop] and resolves it
         }
         break;

@@ -90,6 +90,28 @@ struct ProbeInterval {
     uint32_t e_lo, e_hi;
 };
 
+// The batched flush chain (resolver.cpp step 2; FileView.isFull at mark + 9B, Sender.java:1294-1310): flushes at
+// f_i = f + 10 B i (i < K), flush i from the rolling value R_i at f_i -- R_0 = T(f) + E with E = (el, eh) at f,
+// R_{i+1} = T(f_{i+1}) + E_i(f_{i+1}) -- and E_i = R2_i - T(f_i + B) after it (quirk A: the Java code subtracts x_f
+// with the full window, slides by B and keeps rolling the old value).  Step i opens the interval
+// [s2_i, min(s2_i + 9B, last) + 1) = [f_i + B, ...) with desync (elo_i, ehi_i) anchored at s2_i; a step whose s2 is
+// past `last` ends the chain.
+struct FlushChain {
+    int64_t f = 0, K = 0, B = 0, n = 0, last = 0;
+    uint32_t el = 0, eh = 0;
+};
+struct FlushStep {
+    int64_t s2;
+    uint32_t elo, ehi;
+};
+// the positions the chain reads: T at f_i and f_i + B (tpos, 2K), the bytes at f_i and f_i + 2B - 1 (bpos, 2K)
+void flush_positions(const FlushChain& q, std::vector<int64_t>* tpos, std::vector<int64_t>* bpos);
+// the steps' s2 and their intervals' bounds (E left 0): what does not depend on the sums
+void flush_intervals(const FlushChain& q, std::vector<FlushStep>* steps, std::vector<ProbeInterval>* ivs);
+// the chain itself from the gathered sums and bytes: steps and intervals with their E
+void flush_chain_host(const FlushChain& q, const int32_t* tv, const uint8_t* bv, std::vector<FlushStep>* steps,
+                      std::vector<ProbeInterval>* ivs);
+
 // Speculated sums of the source windows at s0 + kB, k in [0, count) (a phase-shifted speculation: the
 // source's own block sums from s0 on, with the received header's B and dl).  w[k] = T(s0 + kB) over
 // min(B, n - s0 - kB) bytes, st + k * dl = that window's MD5 || seed, cut / zero-padded to dl bytes.
@@ -148,6 +170,14 @@ class ScanBackend {
         weak_many(tpos, nt, tv);
         bytes_many(bpos, nb, bv);
     }
+
+    // The batched flush chain and one probe: the intervals pre[0, npre) (E known; the interval the scan is in),
+    // then the chain's intervals.  Fills *steps and *ivs as flush_chain_host and returns the first hit over
+    // pre + ivs (-1: none).  Default: flush_gather, the chain on the host, first_hit (two round trips); the GPU
+    // backends gather, chain (device.h launch_flush_chain) and probe in one.
+    virtual int64_t flush_probe(const ProbeInterval* pre, int64_t npre, const FlushChain& q,
+                                std::vector<FlushStep>* steps, std::vector<ProbeInterval>* ivs,
+                                const std::vector<int32_t>* keys);
 
     int32_t weak_at(int64_t p) {
         int32_t r;
