@@ -100,6 +100,8 @@ struct BatchState {
     // Sender batch: device
     DevBuf slots, dslots, src_weak, src_strong, flags, haw, partials, bucket, first, k1_groups, k1_lanes;
     DevBuf d_probe;  // a large probe's descriptors (files, intervals, tiles, partial tiles) in device memory
+    DevBuf fc_dev;   // FCHAIN rounds: the chains' gathered sums and bytes
+    PinnedBuf h_fgw, h_fjobs, h_fout;  // ... their gather lists, chain jobs and chain outputs
     // Sender batch: pinned host (read or written by the kernels directly)
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl, h_files, h_hit, h_win0, h_bucket, h_first, h_iv, h_tiles, h_segs,
         h_ptiles, h_req, h_gw, h_gb, h_ow, h_ob, h_win, h_copies, h_tabents, h_flagents, h_flagents_a, h_dkeys, h_ccopies,
@@ -162,12 +164,13 @@ struct BatchState {
         h_glanes.release();
         h_sgroups.release();
         h_slanes.release();
-        for (DevBuf* b : {&d_probe, &g_groups, &g_lanes, &g_plans, &k1_plans, &slots, &dslots, &src_weak, &src_strong, &flags, &haw, &partials, &bucket,
+        for (DevBuf* b : {&d_probe, &fc_dev, &g_groups, &g_lanes, &g_plans, &k1_plans, &slots, &dslots, &src_weak, &src_strong, &flags, &haw, &partials, &bucket,
                           &first, &k1_groups, &k1_lanes})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_files, &h_hit, &h_win0, &h_bucket, &h_first,
                              &h_iv, &h_tiles, &h_segs, &h_ptiles, &h_req, &h_gw, &h_gb, &h_ow, &h_ob, &h_win, &h_copies,
-                             &h_tabents, &h_flagents, &h_flagents_a, &h_dkeys, &h_ccopies, &h_lead})
+                             &h_tabents, &h_flagents, &h_flagents_a, &h_dkeys, &h_ccopies, &h_lead, &h_fgw, &h_fjobs,
+                             &h_fout})
             b->release();
     }
 };
@@ -201,8 +204,11 @@ hipError_t pin(PinnedBuf& b, int64_t count, T** out) {
 // Sender batch
 // ------------------------------------------------------------------------------------------------
 struct Req {
-    // WAIT: until the speculation lands (no device work); FLUSH: WEAK at pos + BYTES at pos2 (one round trip)
-    enum Kind { WEAK, BYTES, WIN, PROBE, WAIT, FLUSH } kind = WEAK;
+    // WAIT: until the speculation lands (no device work); FLUSH: WEAK at pos + BYTES at pos2 (one round trip);
+    // FCHAIN: the batched flush chain in one round trip -- FLUSH's gathers into device memory, the chain on the
+    // device (fchain; chain_out gets every step's desync), then PROBE over iv[0, niv), whose entries from npre on
+    // are the chain's intervals with the desync the chain kernel writes
+    enum Kind { WEAK, BYTES, WIN, PROBE, WAIT, FLUSH, FCHAIN } kind = WEAK;
     const int64_t* pos = nullptr;  // WEAK / BYTES / FLUSH (weak sums)
     int64_t count = 0;
     const int64_t* pos2 = nullptr;  // FLUSH: byte positions
@@ -218,6 +224,9 @@ struct Req {
     bool head = false;
     int64_t result = -1;
     const ProbeOut* out = nullptr;  // the probe's full answer (pinned), for the hit cache
+    FlushChain fchain;              // FCHAIN
+    int64_t npre = 0;
+    uint32_t* chain_out = nullptr;  // FCHAIN: 2 K words
 };
 
 struct Batch;
@@ -261,6 +270,10 @@ class BatchBackend : public ScanBackend {
                       uint8_t* bv) override;
     void md5_at(int64_t p, uint8_t out[16]) override;
     int64_t first_hit(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) override;
+    int64_t flush_probe(const ProbeInterval* pre, int64_t npre, const FlushChain& q, std::vector<FlushStep>* steps,
+                        std::vector<ProbeInterval>* ivs, const std::vector<int32_t>* keys) override;
+  private:
+    int64_t probe_answer(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys);
 };
 
 struct FileScan {
@@ -476,6 +489,12 @@ int64_t BatchBackend::first_hit(const ProbeInterval* iv, int64_t count, const st
     fs.req.keys = keys;
     fs.req.head = head;
     b->post(fs);
+    return probe_answer(iv, count, keys);
+}
+
+// the answer of a PROBE / FCHAIN round: the hit cache, the windows and buckets that came with it
+int64_t BatchBackend::probe_answer(const ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) {
+    FileScan& fs = scan_of(b, f);
     const int64_t p = fs.req.result;
     if (count == 1 && fs.req.out) cache.fill(iv[0], keys, *fs.req.out, n - B);
     else if (fs.req.out) cache.fill_batch(iv, count, keys, *fs.req.out, n - B);
@@ -486,6 +505,43 @@ int64_t BatchBackend::first_hit(const ProbeInterval* iv, int64_t count, const st
     t_val = *reinterpret_cast<const int32_t*>(hit);
     prime_from_probe(*table, *fs.req.out, bucket);
     return p;
+}
+
+int64_t BatchBackend::flush_probe(const ProbeInterval* pre, int64_t npre, const FlushChain& q,
+                                  std::vector<FlushStep>* steps, std::vector<ProbeInterval>* ivs,
+                                  const std::vector<int32_t>* keys) {
+    flush_intervals(q, steps, ivs);
+    if (ivs->empty()) return ScanBackend::flush_probe(pre, npre, q, steps, ivs, keys);  // (no interval opens)
+    std::vector<int64_t> tpos, bpos;
+    flush_positions(q, &tpos, &bpos);
+    std::vector<ProbeInterval> all(pre, pre + npre);
+    all.insert(all.end(), ivs->begin(), ivs->end());
+    std::vector<uint32_t> out((size_t)(2 * q.K));
+    bytes_read += probe_bytes(all.data(), (int64_t)all.size(), B) + (int64_t)tpos.size() * B + (int64_t)bpos.size();
+    FileScan& fs = scan_of(b, f);
+    fs.req = Req{};
+    fs.req.kind = Req::FCHAIN;
+    fs.req.pos = tpos.data();
+    fs.req.count = (int64_t)tpos.size();
+    fs.req.pos2 = bpos.data();
+    fs.req.count2 = (int64_t)bpos.size();
+    fs.req.iv = all.data();
+    fs.req.niv = (int64_t)all.size();
+    fs.req.keys = keys;
+    fs.req.head = head;
+    fs.req.fchain = q;
+    fs.req.npre = npre;
+    fs.req.chain_out = out.data();
+    b->post(fs);
+    for (size_t i = 0; i < steps->size(); ++i) {
+        (*steps)[i].elo = out[2 * i];
+        (*steps)[i].ehi = out[2 * i + 1];
+        if (i < ivs->size()) {
+            (*ivs)[i].e_lo = all[(size_t)npre + i].e_lo = out[2 * i];
+            (*ivs)[i].e_hi = all[(size_t)npre + i].e_hi = out[2 * i + 1];
+        }
+    }
+    return probe_answer(all.data(), (int64_t)all.size(), keys);
 }
 
 // One round: answer every pending request of the batch.  Returns a HIP error (then every request is
@@ -530,6 +586,58 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
     std::vector<DkeyTab> dtabs;
 
     ScanFile* F = S->h_files.as<ScanFile>();
+    // FCHAIN: the chains' gathers (into device memory) and the place of each chain's outputs in h_fout
+    std::vector<GatherEnt> fw, fb;
+    std::vector<int64_t> fw_at(files.size(), -1), fb_at(files.size(), -1), fo_at(files.size(), -1);
+    int64_t nfout = 0;
+    // a PROBE (or FCHAIN) request's intervals, tiles and key set into this round's launch
+    auto plan_probe = [&](int32_t f) {
+        FileScan& fs = files[(size_t)f];
+        Req& r = fs.req;
+        BatchBackend& be = fs.be;
+        F[f].aligned_weak = r.head ? S->haw.as<int32_t>() + fs.off_na : S->src_weak.as<int32_t>() + fs.off_na;
+        F[f].slots = S->slots.as<unsigned long long>() + fs.off_ns;
+        F[f].mask = fs.ns - 1;
+        F[f].nsmall = 0;
+        if (r.keys && !r.keys->empty() && r.keys->size() <= (size_t)PROBE_SMALL_KEYS) {  // compared in registers
+            F[f].nsmall = (int32_t)r.keys->size();
+            for (size_t j = 0; j < r.keys->size(); ++j) F[f].small[j] = (uint32_t)(*r.keys)[j];
+        } else if (r.keys) {  // stale digest: only its chunks' keys (a handful), hashed here
+            const uint32_t nsl = pow2_at_least(2 * r.keys->size() + 2);
+            const int64_t off = (int64_t)dkeys.size();
+            dkeys.resize(dkeys.size() + nsl, 0ull);
+            for (int32_t k : *r.keys) {
+                const unsigned long long v = (1ull << 32) | (uint32_t)k;
+                uint32_t h = slot_hash_host((uint32_t)k) & (nsl - 1);
+                while (dkeys[(size_t)(off + h)] != 0ull && dkeys[(size_t)(off + h)] != v) h = (h + 1) & (nsl - 1);
+                dkeys[(size_t)(off + h)] = v;
+            }
+            dtabs.push_back(DkeyTab{f, off, nsl - 1});
+        }
+        F[f].iv0 = (int32_t)ivs.size();
+        F[f].niv = (int32_t)r.niv;
+        const size_t t0 = tiles.size();
+        int64_t full = 0;
+        for (int64_t i = 0; i < r.niv; ++i) full += probe_full_positions(r.iv[i].a, r.iv[i].b, fs.n, fs.B);
+        const int64_t seg_len = probe_seg_len(full, fs.B);
+        for (int64_t i = 0; i < r.niv; ++i) {
+            const ProbeInterval& v = r.iv[i];
+            ivs.push_back(ProbeIv{v.a, v.b, v.anchor, v.e_lo & 0xFFFFu, v.e_hi & 0xFFFFu, f, 0});
+            probe_plan(v.a, v.b, fs.n, fs.B, (int32_t)(ivs.size() - 1), seg_len, &tiles, &segs);
+        }
+        probe_partials(&tiles, t0, fs.B, f, &ptiles);
+        if (r.head) {  // anchors T(kB) of the blocks these tiles sit in
+            for (size_t t = t0; t < tiles.size(); ++t) {
+                const int64_t k = tiles[t].q0 / fs.B;
+                if (!be.haw_ready[(size_t)k]) {
+                    be.haw_ready[(size_t)k] = 1;
+                    gw.push_back(GatherEnt{k * fs.B, f, 1});
+                }
+            }
+        }
+        preq.push_back(f);
+        max_C = std::max(max_C, fs.C);
+    };
     for (int32_t f : pend) {
         FileScan& fs = files[(size_t)f];
         Req& r = fs.req;
@@ -556,52 +664,18 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
                 win_bytes += pad16(r.w);
                 max_win = std::max(max_win, r.w);
                 break;
-            case Req::PROBE: {
-                BatchBackend& be = fs.be;
-                F[f].aligned_weak = r.head ? S->haw.as<int32_t>() + fs.off_na : S->src_weak.as<int32_t>() + fs.off_na;
-                F[f].slots = S->slots.as<unsigned long long>() + fs.off_ns;
-                F[f].mask = fs.ns - 1;
-                F[f].nsmall = 0;
-                if (r.keys && !r.keys->empty() && r.keys->size() <= (size_t)PROBE_SMALL_KEYS) {  // compared in registers
-                    F[f].nsmall = (int32_t)r.keys->size();
-                    for (size_t j = 0; j < r.keys->size(); ++j) F[f].small[j] = (uint32_t)(*r.keys)[j];
-                } else if (r.keys) {  // stale digest: only its chunks' keys (a handful), hashed here
-                    const uint32_t nsl = pow2_at_least(2 * r.keys->size() + 2);
-                    const int64_t off = (int64_t)dkeys.size();
-                    dkeys.resize(dkeys.size() + nsl, 0ull);
-                    for (int32_t k : *r.keys) {
-                        const unsigned long long v = (1ull << 32) | (uint32_t)k;
-                        uint32_t h = slot_hash_host((uint32_t)k) & (nsl - 1);
-                        while (dkeys[(size_t)(off + h)] != 0ull && dkeys[(size_t)(off + h)] != v) h = (h + 1) & (nsl - 1);
-                        dkeys[(size_t)(off + h)] = v;
-                    }
-                    dtabs.push_back(DkeyTab{f, off, nsl - 1});
-                }
-                F[f].iv0 = (int32_t)ivs.size();
-                F[f].niv = (int32_t)r.niv;
-                const size_t t0 = tiles.size();
-                int64_t full = 0;
-                for (int64_t i = 0; i < r.niv; ++i) full += probe_full_positions(r.iv[i].a, r.iv[i].b, fs.n, fs.B);
-                const int64_t seg_len = probe_seg_len(full, fs.B);
-                for (int64_t i = 0; i < r.niv; ++i) {
-                    const ProbeInterval& v = r.iv[i];
-                    ivs.push_back(ProbeIv{v.a, v.b, v.anchor, v.e_lo & 0xFFFFu, v.e_hi & 0xFFFFu, f, 0});
-                    probe_plan(v.a, v.b, fs.n, fs.B, (int32_t)(ivs.size() - 1), seg_len, &tiles, &segs);
-                }
-                probe_partials(&tiles, t0, fs.B, f, &ptiles);
-                if (r.head) {  // anchors T(kB) of the blocks these tiles sit in
-                    for (size_t t = t0; t < tiles.size(); ++t) {
-                        const int64_t k = tiles[t].q0 / fs.B;
-                        if (!be.haw_ready[(size_t)k]) {
-                            be.haw_ready[(size_t)k] = 1;
-                            gw.push_back(GatherEnt{k * fs.B, f, 1});
-                        }
-                    }
-                }
-                preq.push_back(f);
-                max_C = std::max(max_C, fs.C);
+            case Req::FCHAIN:  // the chain's gathers (device memory), then its probe as PROBE
+                fw_at[(size_t)f] = (int64_t)fw.size();
+                for (int64_t i = 0; i < r.count; ++i) fw.push_back(GatherEnt{r.pos[i], f, 0});
+                fb_at[(size_t)f] = (int64_t)fb.size();
+                for (int64_t i = 0; i < r.count2; ++i) fb.push_back(GatherEnt{r.pos2[i], f, 0});
+                fo_at[(size_t)f] = nfout;
+                nfout += 2 * r.fchain.K;
+                plan_probe(f);
                 break;
-            }
+            case Req::PROBE:
+                plan_probe(f);
+                break;
         }
     }
     // pinned staging of this round's inputs
@@ -630,6 +704,17 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
     chk(pin(S->h_ptiles, (int64_t)ptiles.size(), &hpt));
     chk(pin(S->h_req, (int64_t)preq.size(), &hreq));
     chk(pin(S->h_dkeys, (int64_t)dkeys.size(), &hdk));
+    GatherEnt* hfg = nullptr;
+    FlushChainJob* hfj = nullptr;
+    uint32_t* hfo = nullptr;
+    int32_t nfj = 0;
+    for (int32_t f : pend) nfj += files[(size_t)f].req.kind == Req::FCHAIN;
+    if (nfj > 0) {
+        chk(pin(S->h_fgw, (int64_t)(fw.size() + fb.size()), &hfg));
+        chk(pin(S->h_fjobs, (int64_t)nfj, &hfj));
+        chk(pin(S->h_fout, nfout, &hfo));
+        chk(S->fc_dev.ensure(fw.size() * 4 + fb.size() + 16));
+    }
     chk(S->partials.ensure((ptiles.size() + 1) * sizeof(int4)));
     chk(S->dslots.ensure((dkeys.size() + 1) * sizeof(unsigned long long)));
     if (e != hipSuccess) return e;
@@ -662,6 +747,17 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
     chk(launch_window_weak(F, hgw, (uint32_t)gw.size(), how, st));  // weak sums + head-mode anchors
     chk(launch_gather_bytes(F, hgb, (uint32_t)gb.size(), hob, st));
     chk(launch_copy_many(hcp, (uint32_t)copies.size(), max_win, st));
+    // FCHAIN: the chains' sums and bytes, gathered into device memory for the chain kernel below
+    int32_t* d_ftv = nullptr;
+    uint8_t* d_fbv = nullptr;
+    if (nfj > 0) {
+        memcpy(hfg, fw.data(), fw.size() * sizeof(GatherEnt));
+        memcpy(hfg + fw.size(), fb.data(), fb.size() * sizeof(GatherEnt));
+        d_ftv = S->fc_dev.as<int32_t>();
+        d_fbv = reinterpret_cast<uint8_t*>(d_ftv + fw.size());
+        chk(launch_window_weak(F, hfg, (uint32_t)fw.size(), d_ftv, st));
+        chk(launch_gather_bytes(F, hfg + fw.size(), (uint32_t)fb.size(), d_fbv, st));
+    }
     if (!preq.empty()) {
         // The kernels read their descriptors where they are: pinned host memory, one PCIe round trip per workgroup,
         // which is nothing for a round's few tiles but the whole cost of a probe over a file's rest (a batched flush
@@ -690,6 +786,18 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
             if (!segs.empty())
                 chk(hipMemcpyAsync(d + bf + bi + bt + bp, hsg, segs.size() * sizeof(ProbeSeg), hipMemcpyHostToDevice, st));
             dsg = reinterpret_cast<const ProbeSeg*>(d + bf + bi + bt + bp);
+        }
+        if (nfj > 0) {  // every chain's desync into its intervals where the probe reads them, and to the host
+            int32_t j = 0;
+            for (int32_t f : pend) {
+                const Req& r = files[(size_t)f].req;
+                if (r.kind != Req::FCHAIN) continue;
+                const FlushChain& q = r.fchain;
+                hfj[j++] = FlushChainJob{d_ftv + fw_at[(size_t)f], d_fbv + fb_at[(size_t)f],
+                                         const_cast<ProbeIv*>(div) + F[f].iv0 + r.npre, hfo + fo_at[(size_t)f], q.f, q.B,
+                                         q.n, q.last, (int32_t)q.K, (int32_t)(r.niv - r.npre), q.el, q.eh};
+            }
+            chk(launch_flush_chain(hfj, (uint32_t)nfj, st));
         }
         ProbeArgs A;
         A.files = dF;
@@ -726,6 +834,9 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
             case Req::WIN:
                 r.win = hwin + win_at[(size_t)f];
                 break;
+            case Req::FCHAIN:
+                for (int64_t i = 0; i < 2 * r.fchain.K; ++i) r.chain_out[i] = e == hipSuccess ? hfo[fo_at[(size_t)f] + i] : 0u;
+                [[fallthrough]];
             case Req::PROBE:
                 r.out = e == hipSuccess ? &hf[f] : nullptr;
                 r.result = (e == hipSuccess && hf[f].first != ~0ull) ? (int64_t)hf[f].first : -1;
@@ -1267,6 +1378,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             fs.rs.m = o.m;
             fs.rs.pref = o.pref;
             fs.rs.anchor = o.s;
+            fs.rs.elo = o.elo;  // (0, 0) but after a flush the walk took (CHAIN_WHY_FLUSHED)
+            fs.rs.ehi = o.ehi;
             fs.rs.clear_from = o.clear_to >= 0 ? o.s : -1;  // the walk searched up to the flush point
             fs.rs.clear_to = o.clear_to;
             // a walk that stopped inside the prefix leaves only the prefix speculated (its file's other groups
@@ -1544,7 +1657,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                         ms_since(t_serve), ms_since(t0));
         }
         if (trace) {
-            int kinds[6] = {0, 0, 0, 0, 0, 0};
+            int kinds[7] = {0, 0, 0, 0, 0, 0, 0};
             for (int32_t f : pend) kinds[files[(size_t)f].req.kind]++;
             double bsum = 0, bmax = 0, fmax = 0;
             for (int32_t w = 0; w < W; ++w) {
@@ -1552,9 +1665,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 bmax = std::max(bmax, b.busy_ms[(size_t)w]);
                 fmax = std::max(fmax, b.max_fiber_ms[(size_t)w]);
             }
-            fprintf(stderr, "[rsh-batch] round %3d  pending %3zu (weak %d bytes %d win %d probe %d flush %d)  wait %.3f ms "
-                    "(host work: sum %.3f, max worker %.3f, max fiber %.3f)  serve %.3f ms%s  at %.3f ms\n",
-                    rounds, pend.size(), kinds[0], kinds[1], kinds[2], kinds[3], kinds[5], wait_ms, bsum, bmax, fmax,
+            fprintf(stderr, "[rsh-batch] round %3d  pending %3zu (weak %d bytes %d win %d probe %d flush %d chain %d)  wait "
+                    "%.3f ms (host work: sum %.3f, max worker %.3f, max fiber %.3f)  serve %.3f ms%s  at %.3f ms\n",
+                    rounds, pend.size(), kinds[0], kinds[1], kinds[2], kinds[3], kinds[5], kinds[6], wait_ms, bsum, bmax, fmax,
                     ms_since(t_serve), b.landed.load() ? "  [aligned]" : "", ms_since(t0));
             std::fill(b.busy_ms.begin(), b.busy_ms.end(), 0.0);
             std::fill(b.max_fiber_ms.begin(), b.max_fiber_ms.end(), 0.0);

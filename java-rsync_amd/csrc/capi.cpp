@@ -252,9 +252,41 @@ class HipBackend : public rsh::ScanBackend {
         h.update(seed_, 4);
         h.final(out);
     }
+    // The batched flush chain in one round trip: the gathers into device memory, the chain kernel writing the
+    // chain's intervals' desync into the probe's interval list, then the probe (first_hit with fc_ set).
+    int64_t flush_probe(const rsh::ProbeInterval* pre, int64_t npre, const rsh::FlushChain& q,
+                        std::vector<rsh::FlushStep>* steps, std::vector<rsh::ProbeInterval>* ivs,
+                        const std::vector<int32_t>* keys) override {
+        rsh::flush_intervals(q, steps, ivs);
+        if (ivs->empty()) return ScanBackend::flush_probe(pre, npre, q, steps, ivs, keys);
+        std::vector<int64_t> tpos, bpos;
+        rsh::flush_positions(q, &tpos, &bpos);
+        std::vector<rsh::ProbeInterval> all(pre, pre + npre);
+        all.insert(all.end(), ivs->begin(), ivs->end());
+        std::vector<uint32_t> out((size_t)(2 * q.K));
+        fc_ = Chain{&q, &tpos, &bpos, npre, out.data()};
+        const int64_t p = first_hit(all.data(), (int64_t)all.size(), keys);
+        fc_ = Chain{};
+        for (size_t i = 0; i < steps->size(); ++i) {
+            (*steps)[i].elo = out[2 * i];
+            (*steps)[i].ehi = out[2 * i + 1];
+            if (i < ivs->size()) {
+                (*ivs)[i].e_lo = out[2 * i];
+                (*ivs)[i].e_hi = out[2 * i + 1];
+            }
+        }
+        return p;
+    }
+    struct Chain {  // flush_probe's chain, for the first_hit call it makes
+        const rsh::FlushChain* q = nullptr;
+        const std::vector<int64_t>* tpos = nullptr;
+        const std::vector<int64_t>* bpos = nullptr;
+        int64_t npre = 0;
+        uint32_t* out = nullptr;
+    } fc_;
     int64_t first_hit(const rsh::ProbeInterval* iv, int64_t count, const std::vector<int32_t>* keys) override {
         rsh::ProbeInterval one;
-        if (count == 1) {  // answered by the previous probe's hit list, or cut to its unprobed part
+        if (count == 1 && !fc_.q) {  // answered by the previous probe's hit list, or cut to its unprobed part
             int64_t p = -1, a2 = iv[0].a;
             int32_t T = 0;
             if (cache_.lookup(iv[0], keys, &p, &T, &a2)) {
@@ -268,9 +300,10 @@ class HipBackend : public rsh::ScanBackend {
             one.a = a2;
             iv = &one;
         }
-        CallTrace tr("first_hit", count);
-        ensure(iv[0].a);
+        CallTrace tr(fc_.q ? "flush_chain" : "first_hit", count);
+        ensure(fc_.q ? std::min(iv[0].a, fc_.q->f) : iv[0].a);
         bytes_read += probe_bytes(iv, count, B_);
+        if (fc_.q) bytes_read += (int64_t)fc_.tpos->size() * B_ + (int64_t)fc_.bpos->size();
         rsh::ProbeTable tab = table;
         if (keys) {
             const uint32_t ns = pow2_at_least(2 * keys->size() + 2);
@@ -339,6 +372,25 @@ class HipBackend : public rsh::ScanBackend {
                 ok(rsh::launch_window_weak(F, hp, (uint32_t)anchors_.size(), nullptr, rs_));
             }
         }
+        uint32_t* hfo = nullptr;
+        if (fc_.q) {  // the chain's gathers into device memory, then the chain into hiv[npre, count) and hfo
+            const int64_t nt = (int64_t)fc_.tpos->size(), nb = (int64_t)fc_.bpos->size();
+            rsh::GatherEnt* hfg = pin<rsh::GatherEnt>(c_->h_fgw, nt + nb);
+            rsh::FlushChainJob* hj = pin<rsh::FlushChainJob>(c_->h_fjobs, 1);
+            hfo = pin<uint32_t>(c_->h_fout, 2 * fc_.q->K);
+            ok(c_->fc_dev.ensure((size_t)(nt * 4 + nb + 16)));
+            if (err != hipSuccess) return -1;
+            for (int64_t i = 0; i < nt; ++i) hfg[i] = rsh::GatherEnt{(*fc_.tpos)[(size_t)i], 0, 0};
+            for (int64_t i = 0; i < nb; ++i) hfg[nt + i] = rsh::GatherEnt{(*fc_.bpos)[(size_t)i], 0, 0};
+            int32_t* d_tv = c_->fc_dev.as<int32_t>();
+            uint8_t* d_bv = reinterpret_cast<uint8_t*>(d_tv + nt);
+            ok(rsh::launch_window_weak(F, hfg, (uint32_t)nt, d_tv, rs_));
+            ok(rsh::launch_gather_bytes(F, hfg + nt, (uint32_t)nb, d_bv, rs_));
+            const rsh::FlushChain& q = *fc_.q;
+            *hj = rsh::FlushChainJob{d_tv, d_bv, hiv + fc_.npre, hfo, q.f, q.B, q.n, q.last, (int32_t)q.K,
+                                     (int32_t)(count - fc_.npre), q.el, q.eh};
+            ok(rsh::launch_flush_chain(hj, 1, rs_));
+        }
         rsh::ProbeArgs A;
         A.files = F;
         A.ivs = hiv;
@@ -355,6 +407,14 @@ class HipBackend : public rsh::ScanBackend {
         ok(hipMemcpyAsync(hb, c_->bucket.p, rsh::HIT_BUCKET_INTS * sizeof(int32_t), hipMemcpyDeviceToHost,
                           rs_));
         ok(hipStreamSynchronize(rs_));
+        if (fc_.q && err == hipSuccess) {  // the chain's desync: to the caller, and into the intervals the cache keeps
+            memcpy(fc_.out, hfo, (size_t)(2 * fc_.q->K) * sizeof(uint32_t));
+            rsh::ProbeInterval* civ = const_cast<rsh::ProbeInterval*>(iv);  // (flush_probe's own list)
+            for (int64_t i = fc_.npre; i < count; ++i) {
+                civ[i].e_lo = hfo[2 * (i - fc_.npre)];
+                civ[i].e_hi = hfo[2 * (i - fc_.npre) + 1];
+            }
+        }
         if (count == 1) cache_.fill(iv[0], keys, *hf, n_ - B_);
         else cache_.fill_batch(iv, count, keys, *hf, n_ - B_);
         if (hf->first == ~0ull) return -1;

@@ -134,6 +134,7 @@ struct rsh_ctx {
     DevBuf seg_data, seg_tab;                    // rsh_*_batch (segment.cpp): a pass's files and tables / sums
     DevBuf rcv[2], rcv_ops[2];                   // rsh_receiver_combine_batch: two pass buffers and their gather ops
     DevBuf prep_dev;                             // the stamped launches' counters and the prep launch's scratch
+    DevBuf fc_dev;                               // the batched flush chain's gathered sums and bytes (flush_probe)
     hipStream_t aux = nullptr;                   // the aligned speculation
     hipStream_t phase = nullptr;                 // the phase-shifted speculation (beside a prefix speculation)
     hipEvent_t ev_in = nullptr, ev_tab = nullptr, ev_spec = nullptr;
@@ -163,6 +164,7 @@ struct rsh_ctx {
     PinnedBuf h_rcv_ops[2];  // rsh_receiver_combine_batch: the gather ops of a pass, staged
     PinnedBuf h_prep;        // the prep launch's sample list and outputs (scan_spec_queue)
     PinnedBuf h_stamps;      // the stamped launches' stamps, one 64-B line each
+    PinnedBuf h_fgw, h_fjobs, h_fout;  // flush_probe: the chain's gather list, its job, its outputs
     uint64_t first_used = 0;    // probe result slots handed out (see HipBackend::first_hit)
     // device, uncached, 256 B: the speculation launch of generation g stops once abort_word[0] holds g;
     // a phase-shifted speculation polls abort_word[kPhaseWord] (its own 64-B line)
@@ -179,11 +181,11 @@ struct rsh_ctx {
         for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &ph_weak[0], &ph_strong[0],
                           &ph_weak[1], &ph_strong[1], &slots, &dslots,
                           &dkeys, &pos, &out, &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket, &seg_data, &seg_tab,
-                          &rcv[0], &rcv[1], &rcv_ops[0], &rcv_ops[1], &prep_dev})
+                          &rcv[0], &rcv[1], &rcv_ops[0], &rcv_ops[1], &prep_dev, &fc_dev})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pw[0], &h_ps[0], &h_pw[1], &h_ps[1], &h_lead, &h_pos, &h_out, &h_iv,
                              &h_tiles, &h_keys, &h_first, &h_win, &h_ptiles, &h_psegs, &h_hit, &h_win0, &h_pend, &h_bucket, &h_files,
-                             &h_stage, &h_rcv_ops[0], &h_rcv_ops[1], &h_prep, &h_stamps})
+                             &h_stage, &h_rcv_ops[0], &h_rcv_ops[1], &h_prep, &h_stamps, &h_fgw, &h_fjobs, &h_fout})
             b->release();
         if (abort_word) (void)hipFree(abort_word);
         if (ev_in) (void)hipEventDestroy(ev_in);

@@ -209,6 +209,19 @@ struct ProbeIv {
     int32_t file;
     int32_t pad;
 };
+// The batched flush chain on the device (device_scan.hip flush_chain_kernel; resolver.h FlushChain): from the
+// gathered T(f_i), T(f_i + B) and the bytes at f_i, f_i + 2B - 1, every step's desync (elo, ehi) into out[2i, 2i+1]
+// and into the e_lo / e_hi of the chain's probe intervals iv[0, niv) -- in stream order before the probe reads them.
+struct FlushChainJob {
+    const int32_t* tv;  // 2K weak sums (device memory)
+    const uint8_t* bv;  // 2K bytes (device memory)
+    ProbeIv* iv;        // where the probe reads the chain's intervals
+    uint32_t* out;      // 2K words (pinned host memory: the resolver commits the flushes from them)
+    int64_t f, B, n, last;
+    int32_t K, niv;
+    uint32_t el, eh;
+};
+hipError_t launch_flush_chain(const FlushChainJob* jobs, uint32_t njobs, hipStream_t s);
 struct ProbeTile {
     int64_t q0;     // tile start (multiple of PROBE_TILE from its block start)
     int32_t iv;     // interval index
@@ -348,9 +361,12 @@ struct ChainOut {
     int32_t mapped, first_mapped; // tiles answered from the hit map; the walk's tile count at the first (trace)
     int64_t clear_to;             // stopped before a flush: no candidate in [s, clear_to] (else -1)
     int32_t why, pad2;            // why the walk stopped (CHAIN_WHY_*, trace)
+    uint32_t elo, ehi;            // CHAIN_WHY_FLUSHED: the desync E at s (anchored there) after the walk's flush
 };
+// (CHAIN_WHY_FLUSHHIT: no longer emitted -- the walk takes that flush itself and stops with CHAIN_WHY_FLUSHED)
 enum { CHAIN_WHY_NONE = 0, CHAIN_WHY_EVCAP, CHAIN_WHY_END, CHAIN_WHY_PHASE, CHAIN_WHY_TAIL, CHAIN_WHY_NOKSET,
-       CHAIN_WHY_CUT, CHAIN_WHY_FLUSH, CHAIN_WHY_BUCKET, CHAIN_WHY_FLUSHHIT, CHAIN_WHY_DEADCAP, CHAIN_WHY_CLOSED };
+       CHAIN_WHY_CUT, CHAIN_WHY_FLUSH, CHAIN_WHY_BUCKET, CHAIN_WHY_FLUSHHIT, CHAIN_WHY_DEADCAP, CHAIN_WHY_CLOSED,
+       CHAIN_WHY_FLUSHED };
 // The phase-0 hit map (chain_help): while one file's walk searches tile after tile on its CU, the workgroups whose
 // own walks have ended (and the launch's extra ones) map that file's prefix ahead of it -- in the synced state the
 // key at p is the true weak sum T(p), whatever the walk does.  One 64-bit word per 32 positions: the map's

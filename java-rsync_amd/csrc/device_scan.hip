@@ -556,6 +556,88 @@ hipError_t launch_probe_first(const ProbeArgs& args, uint32_t ntiles, const Part
 
 
 // ------------------------------------------------------------------------------------------------
+// The batched flush chain on the device (resolver.h FlushChain; the host form is resolver.cpp flush_chain_host).
+// Its recurrence is linear in the desync.  With a_i, b_i the (elo, ehi) after flush i, all mod 2^16:
+//   a_i = a_{i-1} + d_i,                       d_i = lo T(f_i) - x_i + add_i y_i - lo T(f_i + B)
+//   b_i = b_{i-1} + a_{i-1} D_i + g_i + add_i a_i,  g_i = hi T(f_i) - B x_i - hi T(f_i + B) + add_i lo T(f_i + B)
+// x_i, y_i the signed bytes at f_i and f_i + 2B - 1; add_i: s2_i = f_i + B <= last and its window is full (the
+// Java code adds the window's new last byte, Sender.java:1308-1310); D_i = min(f_i, n - B) - min(s2_{i-1}, n - B)
+// (E_hi's drift over the interval), D_0 = 0; a_{-1} = el, b_{-1} = eh.  Two block scans give every step at once,
+// on the device between the round's gathers and its probe, instead of a serial host loop between two round trips.
+// One workgroup per chain (K <= 4096: 16 steps per thread).
+// ------------------------------------------------------------------------------------------------
+constexpr int FCHAIN_THREADS = 256;
+__device__ __forceinline__ uint32_t fchain_exscan(uint32_t v, uint32_t* sh) {
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int o = 1; o < FCHAIN_THREADS; o <<= 1) {
+        const uint32_t x = t >= o ? sh[t - o] : 0u;
+        __syncthreads();
+        sh[t] += x;
+        __syncthreads();
+    }
+    const uint32_t incl = sh[t];
+    __syncthreads();
+    return incl - v;
+}
+__global__ __launch_bounds__(FCHAIN_THREADS) void flush_chain_kernel(const FlushChainJob* __restrict__ jobs) {
+    __shared__ uint32_t sh[FCHAIN_THREADS];
+    const FlushChainJob J = jobs[blockIdx.x];
+    const int per = (J.K + FCHAIN_THREADS - 1) / FCHAIN_THREADS;
+    const int i0 = (int)threadIdx.x * per, i1 = min(J.K, i0 + per);
+    const int64_t nB = J.n - J.B;
+    auto clampB = [&](int64_t p) { return p < nB ? p : nB; };
+    // step i's terms (d, g, add, D) from the gathered sums and bytes
+    auto terms = [&](int i, uint32_t& d, uint32_t& g, uint32_t& add, uint32_t& D) {
+        const int64_t fi = J.f + 10 * J.B * (int64_t)i, s2 = fi + J.B;
+        const uint32_t T0 = (uint32_t)J.tv[2 * i], T1 = (uint32_t)J.tv[2 * i + 1];
+        const uint32_t x = (uint32_t)(int32_t)(int8_t)J.bv[2 * i];
+        add = (s2 <= J.last && (J.n - s2 >= J.B)) ? 1u : 0u;
+        const uint32_t y = add ? (uint32_t)(int32_t)(int8_t)J.bv[2 * i + 1] : 0u;
+        d = (T0 & 0xFFFFu) - x + y - (T1 & 0xFFFFu);
+        g = (T0 >> 16) - (uint32_t)J.B * x - (T1 >> 16) + add * (T1 & 0xFFFFu);
+        D = i == 0 ? 0u : (uint32_t)(clampB(fi) - clampB(fi - 9 * J.B));
+    };
+    uint32_t dsum = 0;
+    for (int i = i0; i < i1; ++i) {
+        uint32_t d, g, add, D;
+        terms(i, d, g, add, D);
+        dsum += d;
+    }
+    const uint32_t a_base = J.el + fchain_exscan(dsum, sh);  // a_{i0 - 1}
+    uint32_t a_prev = a_base, hsum = 0;
+    for (int i = i0; i < i1; ++i) {
+        uint32_t d, g, add, D;
+        terms(i, d, g, add, D);
+        const uint32_t a = a_prev + d;
+        hsum += a_prev * D + g + add * a;
+        a_prev = a;
+    }
+    uint32_t b = J.eh + fchain_exscan(hsum, sh);  // b_{i0 - 1}
+    a_prev = a_base;
+    for (int i = i0; i < i1; ++i) {
+        uint32_t d, g, add, D;
+        terms(i, d, g, add, D);
+        const uint32_t a = a_prev + d;
+        b += a_prev * D + g + add * a;
+        a_prev = a;
+        J.out[2 * i] = a & 0xFFFFu;
+        J.out[2 * i + 1] = b & 0xFFFFu;
+        if (i < J.niv) {
+            J.iv[i].e_lo = a & 0xFFFFu;
+            J.iv[i].e_hi = b & 0xFFFFu;
+        }
+    }
+}
+
+hipError_t launch_flush_chain(const FlushChainJob* jobs, uint32_t njobs, hipStream_t s) {
+    if (njobs == 0) return hipSuccess;
+    hipLaunchKernelGGL(flush_chain_kernel, dim3(njobs), dim3(FCHAIN_THREADS), 0, s, jobs);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
 // Chain advance (batched Sender scan, batch.cpp): one workgroup per file walks Sender.sendMatchesAndData
 // (Sender.java:1235-1327) on the device for as long as the state stays synced (no FileView flush since the last
 // match, so R = T) and unpoisoned (localChunkMd5sum == null, :1248) and every candidate digest comes from the
@@ -1103,6 +1185,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     uint32_t dg[4] = {0u, 0u, 0u, 0u};  // the window's digest at the current event (poisoned: the stale one)
     int64_t clear_to = -1;            // stopped at a flush point: no candidate in [s, clear_to]
     int32_t why = CHAIN_WHY_NONE;
+    uint32_t desync_lo = 0, desync_hi = 0;  // CHAIN_WHY_FLUSHED: E at s after the walk's flush
     rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
     bool have = false;
     if (nev > 0) {  // phase 1: the last event stays open (a MATCH run may go on across the prefix's end)
@@ -1640,7 +1723,41 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 if (!dead) continue;  // some chunk carries it: the search goes on from p + 1
                 why = status == CHAIN_DONE ? CHAIN_WHY_CLOSED : CHAIN_WHY_DEADCAP;
             } else {
-                why = CHAIN_WHY_FLUSHHIT;
+                // the candidate sits on the flush point itself: Java takes the flush there (FileView.isFull,
+                // Sender.java:1294-1310) with the window's digest cached (quirk B).  The walk takes it too -- the
+                // literal up to f + B, then the rolling value slid by a whole window (quirk A) -- and hands the
+                // desynced state over (E at s2 = f + B): the resolver probes the rest of the file with the stale
+                // digest's keys and the batched flush chain in one round trip
+                if (!poisoned) {
+                    poisoned = 1;
+                    stale = md5c;
+                }
+                emit_lit(m, p + B - m);
+                ++flushes;
+                const int64_t s2 = p + B;
+                s = m = s2;
+                if (s2 <= last) {
+                    const int32_t jx = (int32_t)(int8_t)F.data[p];
+                    uint32_t rlo = (key & 0xFFFFu) - (uint32_t)jx, rhi = (key >> 16) - (uint32_t)B * (uint32_t)jx;
+                    if (n - s2 >= B) {  // :1308-1310: the window at s2 is full -- its new last byte goes in
+                        rlo += (uint32_t)(int32_t)(int8_t)F.data[s2 + B - 1];
+                        rhi += rlo;
+                    }
+                    uint32_t T2;
+                    if (s2 % B == 0 && s2 / B < na) {
+                        T2 = (uint32_t)F.aw[s2 / B];
+                    } else {  // T(s2) over its window, min(B, n - s2) bytes
+                        const int64_t L2 = n - s2 < B ? n - s2 : B;
+                        int32_t w2[2] = {0, 0};
+                        range_sums(F.data, n, s2, s2 + L2, s2, w2[0], w2[1]);
+                        block_reduce<2>(w2, sh);
+                        const uint32_t S1 = (uint32_t)w2[0], S2 = (uint32_t)L2 * S1 - (uint32_t)w2[1];
+                        T2 = (S1 & 0xFFFFu) | (S2 << 16);
+                    }
+                    desync_lo = (rlo - T2) & 0xFFFFu;
+                    desync_hi = (rhi - (T2 >> 16)) & 0xFFFFu;
+                }
+                why = CHAIN_WHY_FLUSHED;
             }
             break;
         }
@@ -1670,6 +1787,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->mapped = mapped;
         out->clear_to = clear_to;
         out->why = why;
+        out->elo = desync_lo;
+        out->ehi = desync_hi;
         out->first_mapped = first_mapped;
         // a file that needs no more speculation stops its phase-1 K1 groups (they poll this word); any other stop
         // keeps them (the resolver's aligned lookups past the prefix use them)
