@@ -1186,6 +1186,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     int64_t clear_to = -1;            // stopped at a flush point: no candidate in [s, clear_to]
     int32_t why = CHAIN_WHY_NONE;
     uint32_t desync_lo = 0, desync_hi = 0;  // CHAIN_WHY_FLUSHED: E at s after the walk's flush
+    // the loop's first words for the step at pf_s with preferred index pf_pref, loaded by the event before it
+    int64_t pf_s = -1;
+    int32_t pf_pref = -1, pf_aw = 0, pf_tw = 0;
+    uint8_t pf_flag = 0;
     rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
     bool have = false;
     if (nev > 0) {  // phase 1: the last event stays open (a MATCH run may go on across the prefix's end)
@@ -1251,9 +1255,13 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const bool al = s % B == 0;
         // the words steps (1), (1') and (2) look at first, loaded together: one global round trip per step instead of
         // three in sequence (a desynced walk takes these steps once per event)
-        const uint8_t flag_k = (!poisoned && k == pref && k < nflags) ? F.flags[k] : (uint8_t)0;
-        const int32_t aw_k = (al && k < na) ? F.aw[k] : 0;
-        const int32_t tw_pref = (!poisoned && pref < C && k < na) ? F.table_weak[pref] : 0;
+        // (or loaded already: an aligned event's match is usually its own chunk kp, and the event then issued the
+        // next step's words beside its bucket and digests -- see below)
+        const bool pf_use = pf_s == s && pf_pref == pref && !poisoned;
+        const uint8_t flag_k = pf_use ? pf_flag : (!poisoned && k == pref && k < nflags) ? F.flags[k] : (uint8_t)0;
+        const int32_t aw_k = pf_use ? pf_aw : (al && k < na) ? F.aw[k] : 0;
+        const int32_t tw_pref = pf_use ? pf_tw : (!poisoned && pref < C && k < na) ? F.table_weak[pref] : 0;
+        pf_s = -1;
         // (1) aligned chain: preferred index == k and source window k carries chunk k's sums
         if (flag_k) {
             if (t == 0) s_zero = nflags;
@@ -1598,6 +1606,14 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const bool diag = spec_digest && kp < C;
         if (spec_digest) chain_digest_load(F.as + kp * dl, dl, dg);
         if (diag) chain_digest_load(F.table_strong + kp * dl, dl, dgk);
+        if (spec_digest) {  // the next step's first words, should the window match its own chunk kp (s = p + B, pref = kp + 1)
+            const int64_t kn = kp + 1;
+            pf_s = p + B;
+            pf_pref = (int32_t)kn;
+            pf_flag = kn < nflags ? F.flags[kn] : (uint8_t)0;
+            pf_aw = kn < na ? F.aw[kn] : 0;
+            pf_tw = (kn < C && kn < na) ? F.table_weak[kn] : 0;
+        }
         if (t < 64) {
             // every chunk with this key lies on the probe path before the first empty slot: wave 0 reads 64 slots of
             // it per round trip (one, nearly always) instead of one dependent load per slot
