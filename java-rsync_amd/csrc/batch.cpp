@@ -102,6 +102,7 @@ struct BatchState {
     DevBuf d_probe;  // a large probe's descriptors (files, intervals, tiles, partial tiles) in device memory
     DevBuf fc_dev;   // FCHAIN rounds: the chains' gathered sums and bytes
     PinnedBuf h_fgw, h_fjobs, h_fout;  // ... their gather lists, chain jobs and chain outputs
+    PinnedBuf h_early;  // early resolution: one file's copies and its probe hash entry
     // Sender batch: pinned host (read or written by the kernels directly)
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl, h_files, h_hit, h_win0, h_bucket, h_first, h_iv, h_tiles, h_segs,
         h_ptiles, h_req, h_gw, h_gb, h_ow, h_ob, h_win, h_copies, h_tabents, h_flagents, h_flagents_a, h_dkeys, h_ccopies,
@@ -170,7 +171,7 @@ struct BatchState {
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_files, &h_hit, &h_win0, &h_bucket, &h_first,
                              &h_iv, &h_tiles, &h_segs, &h_ptiles, &h_req, &h_gw, &h_gb, &h_ow, &h_ob, &h_win, &h_copies,
                              &h_tabents, &h_flagents, &h_flagents_a, &h_dkeys, &h_ccopies, &h_lead, &h_fgw, &h_fjobs,
-                             &h_fout})
+                             &h_fout, &h_early})
             b->release();
     }
 };
@@ -327,8 +328,15 @@ struct Batch {
     std::vector<double> busy_ms, max_fiber_ms;  // per worker, this round (trace)
     std::vector<HostTimes> times;               // per worker, cumulative (trace)
 
+    // early resolution (match_scan_batch_claimed, while other walks still run): a request is served at once, on
+    // the coordinator's thread, by this
+    std::function<void(FileScan&)> direct;
     // in a resolver fiber: hand the request to the coordinator, yield to the worker until it is answered
     void post(FileScan& fs) {
+        if (direct) {
+            direct(fs);
+            return;
+        }
         fs.pending = true;
         swapcontext(&fs.uc, &worker_uc[(size_t)fs.worker]);
     }
@@ -565,8 +573,8 @@ hipError_t spin_sync(BatchState* S, hipStream_t st) {
     return e != hipSuccess ? e : spin_event(S->ev_sync);
 }
 
-hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, const std::vector<int32_t>& pend) {
-    hipStream_t st = c->stream;
+hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, const std::vector<int32_t>& pend,
+                       hipStream_t st) {
     std::vector<GatherEnt> gw, gb;
     std::vector<CopyEnt> copies;
     std::vector<ProbeIv> ivs;
@@ -1208,6 +1216,110 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         const int r = launch_spec_k1();
         if (r != RSH_OK) return r;
     }
+    // A file's walk record into its resolver's state (prefix_only: the rest of the speculation is not used)
+    std::vector<char> early((size_t)NF, 0);
+    auto take_walk = [&](int32_t f, bool prefix_only) {
+        const ChainOut* co = S->h_chain_out.as<ChainOut>();
+        const rsh_event* ce = S->h_chain_ev.as<rsh_event>();
+        FileScan& fs = files[(size_t)f];
+        const ChainOut& o = co[f];
+        if (o.status == CHAIN_DONE) {  // its events stay where the walk wrote them (copied once, at the end)
+            fs.dev_ev = ce + (int64_t)f * kChainEvents;
+            fs.dev_n = o.n_ev;
+        } else {
+            fs.res.ev.assign(ce + (int64_t)f * kChainEvents, ce + (int64_t)f * kChainEvents + o.n_ev);
+        }
+        fs.res.literal = o.literal;
+        fs.res.matched = o.matched;
+        fs.res.stats.chain_matches += o.chain_matches;
+        fs.res.stats.events += o.events;
+        fs.res.stats.flushes += o.flushes;
+        fs.rs.s = o.s;
+        fs.rs.m = o.m;
+        fs.rs.pref = o.pref;
+        fs.rs.anchor = o.s;
+        fs.rs.elo = o.elo;  // (0, 0) but after a flush the walk took (CHAIN_WHY_FLUSHED)
+        fs.rs.ehi = o.ehi;
+        fs.rs.clear_from = o.clear_to >= 0 ? o.s : -1;  // the walk searched up to the flush point
+        fs.rs.clear_to = o.clear_to;
+        // a walk that stopped inside the prefix leaves only the prefix speculated (its file's other groups
+        // stopped): the resolver's aligned lookups end there
+        fs.be.na = (o.aborted || prefix_only) ? fs.na_a : fs.na;
+        if (o.md5c_valid) {  // poisoned at an unaligned hit: the resolver goes on with the stale digest
+            fs.rs.md5c.assign(o.md5c, o.md5c + fs.dl);
+            fs.rs.md5c_valid = true;
+            fs.rs.dkeys_ready = false;
+        }
+        if (o.status == CHAIN_DONE) fs.rs.done = fs.done = true;
+    };
+    // Early resolution.  Phase 0's walks end file by file (ChainOut::fin).  A walk that took a flush-point flush
+    // (CHAIN_WHY_FLUSHED: poisoned and desynced) leaves its file to a stale digest's probe over the rest -- the
+    // batched flush chain's one round trip -- which needs nothing the other walks produce: that file is resolved at
+    // once, on the phase stream beside the walks still running (its table, probe hash and prefix sums copied there
+    // first), instead of after the last walk.  Its requests are served on the coordinator's thread (Batch::direct).
+    hipError_t early_err = hipSuccess;
+    auto early_resolve = [&](int32_t f) -> hipError_t {
+        FileScan& fs = files[(size_t)f];
+        take_walk(f, true);
+        if (fs.done) return hipSuccess;
+        const auto te0 = std::chrono::steady_clock::now();
+        hipStream_t es = c->phase;
+        hipError_t e = S->h_early.ensure(4096);
+        if (e != hipSuccess) return e;
+        CopyEnt* ec = S->h_early.as<CopyEnt>();
+        TableEnt* et = reinterpret_cast<TableEnt*>(ec + 8);
+        uint32_t ne = 0;
+        const int64_t nal = fs.na_a, nfl = std::min(fs.nf, nal);
+        ec[ne++] = CopyEnt{reinterpret_cast<const uint8_t*>(fs.d_weak), S->h_weak.as<uint8_t>() + 4 * fs.off_tw, (int64_t)fs.C * 4};
+        if (fs.dl > 0) ec[ne++] = CopyEnt{fs.d_strong, S->h_strong.as<uint8_t>() + fs.off_ts, (int64_t)fs.C * fs.dl};
+        if (nfl > 0) ec[ne++] = CopyEnt{S->flags.as<uint8_t>() + fs.off_nf, S->h_fl.as<uint8_t>() + fs.off_nf, nfl};
+        ec[ne++] = CopyEnt{S->src_weak.as<uint8_t>() + 4 * fs.off_na, S->h_aw.as<uint8_t>() + 4 * fs.off_na, nal * 4};
+        if (fs.dl > 0)
+            ec[ne++] = CopyEnt{S->src_strong.as<uint8_t>() + fs.off_as, S->h_as.as<uint8_t>() + fs.off_as, nal * fs.dl};
+        et[0] = TableEnt{S->slots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
+        if ((e = hipStreamWaitEvent(es, S->ev_fa, 0)) != hipSuccess) return e;  // the prefix's sums and flags
+        if ((e = launch_copy_many(ec, ne, std::max<int64_t>((int64_t)fs.C * 4, nal * 4), es)) != hipSuccess) return e;
+        if ((e = launch_table_clear(S->slots.as<unsigned long long>() + fs.off_ns, fs.ns, es)) != hipSuccess) return e;
+        if ((e = launch_table_insert_many(et, 1, fs.C, es)) != hipSuccess) return e;
+        if ((e = spin_sync(S, es)) != hipSuccess) return e;
+        fs.be.head = false;
+        b.landed.store(true);
+        b.aligned.store(true);
+        const int32_t fi = f;
+        b.direct = [&, fi](FileScan&) {
+            const hipError_t x = serve_round(c, S, files, std::vector<int32_t>{fi}, es);
+            if (x != hipSuccess && early_err == hipSuccess) early_err = x;
+        };
+        if (fs.C <= kEagerSortChunks) fs.table.build();
+        resolve_run(fs.n, fs.table, fs.be, &fs.rs, &fs.res, nullptr);
+        b.direct = nullptr;
+        fs.rs.done = fs.done = true;
+        early[(size_t)f] = 1;
+        if (opt(OPT_SCAN_TRACE))
+            fprintf(stderr, "[rsh-batch] file %d resolved while the walks ran: %.3f ms, done at %.3f ms\n", f,
+                    ms_since(te0), ms_since(t0));
+        return early_err;
+    };
+    // the host's wait for phase 0's walks, taking up the files they hand over a flush-chain state early
+    auto await_walks = [&]() -> hipError_t {
+        const ChainOut* co = S->h_chain_out.as<ChainOut>();
+        std::vector<char> seen((size_t)NF, 0);
+        for (;;) {
+            const hipError_t q = hipEventQuery(S->ev_wa);
+            if (q != hipSuccess && q != hipErrorNotReady) return q;
+            if (q == hipSuccess) return hipSuccess;  // the rest goes the usual way
+            for (int32_t f = 0; f < NF; ++f) {
+                if (seen[(size_t)f] || *reinterpret_cast<const volatile int32_t*>(&co[f].fin) == 0) continue;
+                seen[(size_t)f] = 1;
+                std::atomic_thread_fence(std::memory_order_acquire);
+                if (co[f].status == CHAIN_STOP && co[f].why == CHAIN_WHY_FLUSHED) {
+                    const hipError_t e = early_resolve(f);
+                    if (e != hipSuccess) return e;
+                }
+            }
+            _mm_pause();
+        }
+    };
     bool spec_launched = false;
     bool skip_rest = false;  // two phases, and phase 0 finished or handed over every file: no rest speculated
     if (chain_on) {  // the speculation, then the walks on the context stream (beside the sums' download on aux)
@@ -1316,7 +1428,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             // 30720 -- its flags and phase 1 are skipped.  The host waits for phase 0 either way (a few us more before
             // the rest's launch when it is needed).
             if (opt(OPT_BATCH_SKIP_REST) != 0 && opt(OPT_BATCH_CHAIN_OVERLAP) == 0) {
-                RSH_BHIP(spin_event(S->ev_wa));
+                RSH_BHIP(await_walks());
                 skip_rest = true;
                 for (int32_t f = 0; f < NF && skip_rest; ++f) skip_rest = co[f].status != CHAIN_MORE;
             }
@@ -1361,37 +1473,9 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         const rsh_event* ce = S->h_chain_ev.as<rsh_event>();
         int32_t left = 0;
         for (int32_t f = 0; f < NF; ++f) {
-            FileScan& fs = files[(size_t)f];
-            const ChainOut& o = co[f];
-            if (o.status == CHAIN_DONE) {  // its events stay where the walk wrote them (copied once, at the end)
-                fs.dev_ev = ce + (int64_t)f * kChainEvents;
-                fs.dev_n = o.n_ev;
-            } else {
-                fs.res.ev.assign(ce + (int64_t)f * kChainEvents, ce + (int64_t)f * kChainEvents + o.n_ev);
-            }
-            fs.res.literal = o.literal;
-            fs.res.matched = o.matched;
-            fs.res.stats.chain_matches += o.chain_matches;
-            fs.res.stats.events += o.events;
-            fs.res.stats.flushes += o.flushes;
-            fs.rs.s = o.s;
-            fs.rs.m = o.m;
-            fs.rs.pref = o.pref;
-            fs.rs.anchor = o.s;
-            fs.rs.elo = o.elo;  // (0, 0) but after a flush the walk took (CHAIN_WHY_FLUSHED)
-            fs.rs.ehi = o.ehi;
-            fs.rs.clear_from = o.clear_to >= 0 ? o.s : -1;  // the walk searched up to the flush point
-            fs.rs.clear_to = o.clear_to;
-            // a walk that stopped inside the prefix leaves only the prefix speculated (its file's other groups
-            // stopped): the resolver's aligned lookups end there
-            fs.be.na = (o.aborted || skip_rest) ? fs.na_a : fs.na;
-            if (o.md5c_valid) {  // poisoned at an unaligned hit: the resolver goes on with the stale digest
-                fs.rs.md5c.assign(o.md5c, o.md5c + fs.dl);
-                fs.rs.md5c_valid = true;
-                fs.rs.dkeys_ready = false;
-            }
-            if (o.status == CHAIN_DONE) fs.rs.done = fs.done = true;
-            else ++left;
+            if (early[(size_t)f]) continue;  // resolved while the other walks ran
+            take_walk(f, skip_rest);
+            if (!files[(size_t)f].done) ++left;
         }
         b.landed.store(true);  // the walks ran after the speculation's K1 and flags
         if (left > 0) {  // the host resolvers use the speculation's host copies: the left files' flags and sums
@@ -1647,7 +1731,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             if (files[(size_t)f].req.kind != Req::WAIT) work.push_back(f);
         hipError_t e = hipSuccess;
         if (!work.empty()) {
-            e = serve_round(c, S, files, work);
+            e = serve_round(c, S, files, work, c->stream);
         } else if (!b.landed.load()) {  // only waiting files: the speculation carries them
             e = spec_launched ? hipEventSynchronize(c->ev_flags) : hipErrorInvalidValue;
             if (e == hipSuccess) b.landed.store(true, std::memory_order_release);

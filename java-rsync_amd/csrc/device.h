@@ -362,6 +362,8 @@ struct ChainOut {
     int64_t clear_to;             // stopped before a flush: no candidate in [s, clear_to] (else -1)
     int32_t why, pad2;            // why the walk stopped (CHAIN_WHY_*, trace)
     uint32_t elo, ehi;            // CHAIN_WHY_FLUSHED: the desync E at s (anchored there) after the walk's flush
+    int32_t fin, pad3;            // written last (after a system-scope fence): the record is complete -- the host may
+                                  // take the file up while other walks still run (batch.cpp, early resolution)
 };
 // (CHAIN_WHY_FLUSHHIT: no longer emitted -- the walk takes that flush itself and stops with CHAIN_WHY_FLUSHED)
 enum { CHAIN_WHY_NONE = 0, CHAIN_WHY_EVCAP, CHAIN_WHY_END, CHAIN_WHY_PHASE, CHAIN_WHY_TAIL, CHAIN_WHY_NOKSET,

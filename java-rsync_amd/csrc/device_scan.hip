@@ -1818,6 +1818,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->matched = mat;
         out->chain_matches = chain_matches;
         out->events = events;
+        __threadfence_system();  // the record and the events (drained above) before the completion word
+        *(volatile int32_t*)&out->fin = 1;
     }
     if (H != nullptr) {  // this walk is over: its helpers stop, and the workgroup helps the walks still searching
         if (t == 0) chain_st(&H->live, 0);
