@@ -37,6 +37,8 @@
 #                does the profiler report undelivered copy completions for plain runtime copies too
 #   copycb5      rocprofv3 --memory-copy-trace --hip-trace over first_call.py --only 5 (then --only 4): which of the
 #                library's copies the profiler reports undelivered
+#   libab        builds of other commits against each other (LIBS: directories under java-rsync_amd/lib/ab, each holding a
+#                librsynchip.so, loaded through RSH_LIB), alternating, REPS times (AB_ARGS: bench args)
 #   ab           AB_OPTS ("name=value ...") against the default, alternating, REPS times (AB_ARGS: bench args)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
@@ -130,6 +132,13 @@ for step in "$@"; do
                 (cd /tmp && export TMPDIR=/tmp && run 240 rocprofv3 --memory-copy-trace --hip-trace -d "$O/copycb_$o" \
                     -o run --output-format csv -- python3 "$R/java-rsync_amd/tools/first_call.py" --only $o --reps 2 \
                     > "$O/copycb_$o.log" 2> "$O/copycb_$o.err") || exit 1
+            done ;;
+        libab)
+            for r in $(seq 1 "${REPS:-2}"); do
+                for l in $LIBS; do
+                    RSH_LIB="$R/java-rsync_amd/lib/ab/$l/librsynchip.so" run 300 python bench.py $AB_ARGS --steps 20 \
+                        --warmup 5 --no-cpu-baseline --no-companions > "$O/${l}_$r.json" 2> "$O/${l}_$r.err"
+                done
             done ;;
         first) run 300 python java-rsync_amd/tools/first_call.py > "$O/first_call.json" 2> "$O/first_call.err" ;;
         first5) run 300 python java-rsync_amd/tools/first_call.py --only 5 --reps 4 --trace5 > "$O/first5.json" \
