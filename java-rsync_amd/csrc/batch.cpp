@@ -103,6 +103,7 @@ struct BatchState {
     DevBuf fc_dev;   // FCHAIN rounds: the chains' gathered sums and bytes
     PinnedBuf h_fgw, h_fjobs, h_fout;  // ... their gather lists, chain jobs and chain outputs
     PinnedBuf h_early;  // early resolution: one file's copies and its probe hash entry
+    PinnedBuf h_rcp;    // a round's answer copies (serve_round)
     // Sender batch: pinned host (read or written by the kernels directly)
     PinnedBuf h_weak, h_strong, h_aw, h_as, h_fl, h_files, h_hit, h_win0, h_bucket, h_first, h_iv, h_tiles, h_segs,
         h_ptiles, h_req, h_gw, h_gb, h_ow, h_ob, h_win, h_copies, h_tabents, h_flagents, h_flagents_a, h_dkeys, h_ccopies,
@@ -171,7 +172,7 @@ struct BatchState {
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_files, &h_hit, &h_win0, &h_bucket, &h_first,
                              &h_iv, &h_tiles, &h_segs, &h_ptiles, &h_req, &h_gw, &h_gb, &h_ow, &h_ob, &h_win, &h_copies,
                              &h_tabents, &h_flagents, &h_flagents_a, &h_dkeys, &h_ccopies, &h_lead, &h_fgw, &h_fjobs,
-                             &h_fout, &h_early})
+                             &h_fout, &h_early, &h_rcp})
             b->release();
     }
 };
@@ -712,6 +713,8 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
     chk(pin(S->h_ptiles, (int64_t)ptiles.size(), &hpt));
     chk(pin(S->h_req, (int64_t)preq.size(), &hreq));
     chk(pin(S->h_dkeys, (int64_t)dkeys.size(), &hdk));
+    CopyEnt* hrc = nullptr;
+    chk(pin(S->h_rcp, 2, &hrc));
     GatherEnt* hfg = nullptr;
     FlushChainJob* hfj = nullptr;
     uint32_t* hfo = nullptr;
@@ -815,9 +818,12 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
         chk(launch_probe_first(A, (uint32_t)tiles.size(), dpt, (uint32_t)ptiles.size(), st));
         chk(launch_probe_long(A, dsg, (uint32_t)segs.size(), st));
         chk(launch_hit_window(F, hiv, hreq, (int32_t)preq.size(), max_C, st));
-        chk(hipMemcpyAsync(S->h_first.p, S->first.p, files.size() * sizeof(ProbeOut), hipMemcpyDeviceToHost, st));
-        chk(hipMemcpyAsync(S->h_bucket.p, S->bucket.p, files.size() * HIT_BUCKET_INTS * sizeof(int32_t),
-                           hipMemcpyDeviceToHost, st));
+        // the answers into pinned memory by a copy kernel (capi.cpp copy_to_host: no copy-engine hand-off between
+        // kernels, and every copy the profiler traces completes)
+        hrc[0] = CopyEnt{S->first.as<uint8_t>(), S->h_first.as<uint8_t>(), (int64_t)(files.size() * sizeof(ProbeOut))};
+        hrc[1] = CopyEnt{S->bucket.as<uint8_t>(), S->h_bucket.as<uint8_t>(),
+                         (int64_t)(files.size() * HIT_BUCKET_INTS * sizeof(int32_t))};
+        chk(launch_copy_many(hrc, 2, std::max(hrc[0].len, hrc[1].len), st));
     }
     chk(spin_sync(S, st));
 

@@ -27,6 +27,26 @@ namespace {
 // HIP implementation of the resolver's services.
 // ------------------------------------------------------------------------------------------------
 constexpr size_t kFirstSlots = 1024;
+// Device results to pinned host memory by a copy kernel (copy_many_kernel) rather than hipMemcpyAsync: between two
+// kernels a D2H copy cost 47-100 us of idle queue (tools/queue_lat.hip case 8) where a kernel writing pinned memory
+// cost none (case 9), and the profiler's async-copy tracing reported the scan's table downloads as never completed
+// (DESIGN.md section 6).  Each call site has its own descriptor slot (kDesc*) in pinned memory:
+// the kernel reads it after the host returns, so a slot is reused only once its previous copy has been waited for.
+enum { kDescTable = 0, kDescProbe, kDescSums, kDescSlots };
+hipError_t copy_to_host(rsh_ctx* c, int slot, std::initializer_list<rsh::CopyEnt> ents, hipStream_t s) {
+    constexpr int kPer = 4;
+    hipError_t e = c->h_desc.ensure((size_t)kDescSlots * kPer * sizeof(rsh::CopyEnt));
+    if (e != hipSuccess) return e;
+    rsh::CopyEnt* d = c->h_desc.as<rsh::CopyEnt>() + slot * kPer;
+    uint32_t n = 0;
+    int64_t mx = 0;
+    for (const rsh::CopyEnt& x : ents)
+        if (x.len > 0) {
+            d[n++] = x;
+            mx = std::max(mx, x.len);
+        }
+    return rsh::launch_copy_many(d, n, mx, s);
+}
 constexpr int kScanWindows = 2;  // hit windows per probe in the single-file scan (hit_cache.h)
 // Head mode launches the aligned speculation after scan_defer_steps (4) resolver steps or scan_defer_us (500 us;
 // options.h) ...
@@ -88,9 +108,10 @@ class HipBackend : public rsh::ScanBackend {
                 // waits: the copy is tens of microseconds, the generic path's probe and host digest as long or longer
                 CallTrace tr("sums_dl", lazy_na);
                 ok(hipStreamWaitEvent(rs_, c_->ev_flags, 0));
-                ok(hipMemcpyAsync(c_->h_aw.p, c_->src_weak.p, (size_t)lazy_na * 4, hipMemcpyDeviceToHost, rs_));
-                if (dl_ > 0)
-                    ok(hipMemcpyAsync(c_->h_as.p, c_->src_strong.p, (size_t)lazy_na * dl_, hipMemcpyDeviceToHost, rs_));
+                ok(copy_to_host(c_, kDescSums, {rsh::CopyEnt{c_->src_weak.as<uint8_t>(), c_->h_aw.as<uint8_t>(), lazy_na * 4},
+                                                rsh::CopyEnt{c_->src_strong.as<uint8_t>(), c_->h_as.as<uint8_t>(),
+                                                             dl_ > 0 ? lazy_na * dl_ : 0}},
+                                rs_));
                 ok(hipEventRecord(c_->ev_spec, rs_));
                 ok(hipEventSynchronize(c_->ev_spec));
                 lazy_na = -1;
@@ -403,9 +424,12 @@ class HipBackend : public rsh::ScanBackend {
         int32_t* req = hb + rsh::HIT_BUCKET_INTS;
         *req = 0;
         ok(rsh::launch_hit_window(F, hiv, req, 1, t_.chunk_count, rs_));
-        ok(hipMemcpyAsync(hf, d_first, sizeof(rsh::ProbeOut), hipMemcpyDeviceToHost, rs_));
-        ok(hipMemcpyAsync(hb, c_->bucket.p, rsh::HIT_BUCKET_INTS * sizeof(int32_t), hipMemcpyDeviceToHost,
-                          rs_));
+        ok(copy_to_host(c_, kDescProbe,
+                        {rsh::CopyEnt{reinterpret_cast<const uint8_t*>(d_first), reinterpret_cast<uint8_t*>(hf),
+                                      (int64_t)sizeof(rsh::ProbeOut)},
+                         rsh::CopyEnt{c_->bucket.as<uint8_t>(), reinterpret_cast<uint8_t*>(hb),
+                                      (int64_t)(rsh::HIT_BUCKET_INTS * sizeof(int32_t))}},
+                        rs_));
         ok(hipStreamSynchronize(rs_));
         if (fc_.q && err == hipSuccess) {  // the chain's desync: to the caller, and into the intervals the cache keeps
             memcpy(fc_.out, hfo, (size_t)(2 * fc_.q->K) * sizeof(uint32_t));
@@ -948,10 +972,12 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // so that a stopped tentative launch's abort does not queue behind these copies)
     auto table_work = [&]() -> int {
         if (download) {
-            if (C > 0) {
-                RSH_HIP(hipMemcpyAsync(c->h_weak.p, d_weak, (size_t)C * 4, hipMemcpyDeviceToHost, rs));
-                if (dl > 0) RSH_HIP(hipMemcpyAsync(c->h_strong.p, d_strong, (size_t)C * dl, hipMemcpyDeviceToHost, rs));
-            }
+            if (C > 0)
+                RSH_HIP(copy_to_host(c, kDescTable,
+                                     {rsh::CopyEnt{reinterpret_cast<const uint8_t*>(d_weak), c->h_weak.as<uint8_t>(),
+                                                   (int64_t)C * 4},
+                                      rsh::CopyEnt{d_strong, c->h_strong.as<uint8_t>(), (int64_t)C * dl}},
+                                     rs));
             RSH_HIP(hipEventRecord(c->ev_tab, rs));
         }
         // (stream) the device probe hash
