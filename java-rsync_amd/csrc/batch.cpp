@@ -1296,7 +1296,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             const hipError_t x = serve_round(c, S, files, std::vector<int32_t>{fi}, es);
             if (x != hipSuccess && early_err == hipSuccess) early_err = x;
         };
-        if (fs.C <= kEagerSortChunks) fs.table.build();
+        // (no eager sort: a stale digest's flush chain needs no bucket lookups; the index is built if a lookup comes)
         resolve_run(fs.n, fs.table, fs.be, &fs.rs, &fs.res, nullptr);
         b.direct = nullptr;
         fs.rs.done = fs.done = true;
