@@ -37,6 +37,7 @@
 #                does the profiler report undelivered copy completions for plain runtime copies too
 #   copycb5      rocprofv3 --memory-copy-trace --hip-trace over first_call.py --only 5 (then --only 4): which of the
 #                library's copies the profiler reports undelivered
+#   copycb-files the same over the config-4 line (VARIANT): which copies of the timeline run stay undelivered
 #   libab        builds of other commits against each other (LIBS: directories under java-rsync_amd/lib/ab, each holding a
 #                librsynchip.so, loaded through RSH_LIB), alternating, REPS times (AB_ARGS: bench args)
 #   ab           AB_OPTS ("name=value ...") against the default, alternating, REPS times (AB_ARGS: bench args)
@@ -133,6 +134,9 @@ for step in "$@"; do
                     -o run --output-format csv -- python3 "$R/java-rsync_amd/tools/first_call.py" --only $o --reps 2 \
                     > "$O/copycb_$o.log" 2> "$O/copycb_$o.err") || exit 1
             done ;;
+        copycb-files) (cd /tmp && export TMPDIR=/tmp && run 240 rocprofv3 --memory-copy-trace --hip-trace -d "$O/copycb_files" \
+            -o run --output-format csv -- python3 "$R/bench.py" --workload files --variant "$VARIANT" --steps 3 --warmup 1 \
+            --no-cpu-baseline --no-companions > "$O/copycb_files.json" 2> "$O/copycb_files.err") || exit 1 ;;
         libab)
             for r in $(seq 1 "${REPS:-2}"); do
                 for l in $LIBS; do
