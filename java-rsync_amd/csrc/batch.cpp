@@ -1476,7 +1476,6 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     int32_t nwait = 0;
     if (chain_on) {  // the walks have ended (the stream sync above): each resolver resumes where its walk stopped
         const ChainOut* co = S->h_chain_out.as<ChainOut>();
-        const rsh_event* ce = S->h_chain_ev.as<rsh_event>();
         int32_t left = 0;
         for (int32_t f = 0; f < NF; ++f) {
             if (early[(size_t)f]) continue;  // resolved while the other walks ran

@@ -27,25 +27,15 @@ namespace {
 // HIP implementation of the resolver's services.
 // ------------------------------------------------------------------------------------------------
 constexpr size_t kFirstSlots = 1024;
-// Device results to pinned host memory by a copy kernel (copy_many_kernel) rather than hipMemcpyAsync: between two
+// Device results to pinned host memory by a copy kernel (copy_few_kernel) rather than hipMemcpyAsync: between two
 // kernels a D2H copy cost 47-100 us of idle queue (tools/queue_lat.hip case 8) where a kernel writing pinned memory
-// cost none (case 9), and the profiler's async-copy tracing reported the scan's table downloads as never completed
-// (DESIGN.md section 6).  Each call site has its own descriptor slot (kDesc*) in pinned memory:
-// the kernel reads it after the host returns, so a slot is reused only once its previous copy has been waited for.
-enum { kDescTable = 0, kDescProbe, kDescSums, kDescSlots };
-hipError_t copy_to_host(rsh_ctx* c, int slot, std::initializer_list<rsh::CopyEnt> ents, hipStream_t s) {
-    constexpr int kPer = 4;
-    hipError_t e = c->h_desc.ensure((size_t)kDescSlots * kPer * sizeof(rsh::CopyEnt));
-    if (e != hipSuccess) return e;
-    rsh::CopyEnt* d = c->h_desc.as<rsh::CopyEnt>() + slot * kPer;
-    uint32_t n = 0;
-    int64_t mx = 0;
+// cost none (case 9), and the profiler's async-copy tracing reported the copy engine's completions as never
+// delivered.  The ranges travel in the kernel's arguments.
+hipError_t copy_to_host(std::initializer_list<rsh::CopyEnt> ents, hipStream_t s) {
+    rsh::CopyFew f{};
     for (const rsh::CopyEnt& x : ents)
-        if (x.len > 0) {
-            d[n++] = x;
-            mx = std::max(mx, x.len);
-        }
-    return rsh::launch_copy_many(d, n, mx, s);
+        if (x.len > 0 && f.n < 4) f.e[f.n++] = x;
+    return rsh::launch_copy_few(f, s);
 }
 constexpr int kScanWindows = 2;  // hit windows per probe in the single-file scan (hit_cache.h)
 // Head mode launches the aligned speculation after scan_defer_steps (4) resolver steps or scan_defer_us (500 us;
@@ -108,7 +98,7 @@ class HipBackend : public rsh::ScanBackend {
                 // waits: the copy is tens of microseconds, the generic path's probe and host digest as long or longer
                 CallTrace tr("sums_dl", lazy_na);
                 ok(hipStreamWaitEvent(rs_, c_->ev_flags, 0));
-                ok(copy_to_host(c_, kDescSums, {rsh::CopyEnt{c_->src_weak.as<uint8_t>(), c_->h_aw.as<uint8_t>(), lazy_na * 4},
+                ok(copy_to_host({rsh::CopyEnt{c_->src_weak.as<uint8_t>(), c_->h_aw.as<uint8_t>(), lazy_na * 4},
                                                 rsh::CopyEnt{c_->src_strong.as<uint8_t>(), c_->h_as.as<uint8_t>(),
                                                              dl_ > 0 ? lazy_na * dl_ : 0}},
                                 rs_));
@@ -168,14 +158,11 @@ class HipBackend : public rsh::ScanBackend {
             ok(rsh::launch_chain_flags(c_->src_weak.as<int32_t>() + k0, c_->src_strong.as<uint8_t>() + k0 * dl_,
                                        d_table_weak_ + k0, reinterpret_cast<const uint8_t*>(d_table_strong) + k0 * dl_,
                                        (uint32_t)(f1 - k0), (uint32_t)dl_, c_->flags.as<uint8_t>() + k0, rs_));
-        ok(hipMemcpyAsync(c_->h_aw.as<int32_t>() + k0, c_->src_weak.as<int32_t>() + k0, (size_t)(k1 - k0) * 4,
-                          hipMemcpyDeviceToHost, rs_));
-        if (dl_ > 0)
-            ok(hipMemcpyAsync(c_->h_as.as<uint8_t>() + k0 * dl_, c_->src_strong.as<uint8_t>() + k0 * dl_,
-                              (size_t)((k1 - k0) * dl_), hipMemcpyDeviceToHost, rs_));
-        if (f1 > k0)
-            ok(hipMemcpyAsync(c_->h_fl.as<uint8_t>() + k0, c_->flags.as<uint8_t>() + k0, (size_t)(f1 - k0),
-                              hipMemcpyDeviceToHost, rs_));
+        ok(copy_to_host({rsh::CopyEnt{c_->src_weak.as<uint8_t>() + 4 * k0, c_->h_aw.as<uint8_t>() + 4 * k0, (k1 - k0) * 4},
+                         rsh::CopyEnt{c_->src_strong.as<uint8_t>() + k0 * dl_, c_->h_as.as<uint8_t>() + k0 * dl_,
+                                      (k1 - k0) * dl_},
+                         rsh::CopyEnt{c_->flags.as<uint8_t>() + k0, c_->h_fl.as<uint8_t>() + k0, f1 - k0}},
+                        rs_));
         ok(hipStreamSynchronize(rs_));
         bytes_read += std::min(n_, k1 * B_) - k0 * B_;
         aligned_end = k1;
@@ -424,7 +411,7 @@ class HipBackend : public rsh::ScanBackend {
         int32_t* req = hb + rsh::HIT_BUCKET_INTS;
         *req = 0;
         ok(rsh::launch_hit_window(F, hiv, req, 1, t_.chunk_count, rs_));
-        ok(copy_to_host(c_, kDescProbe,
+        ok(copy_to_host(
                         {rsh::CopyEnt{reinterpret_cast<const uint8_t*>(d_first), reinterpret_cast<uint8_t*>(hf),
                                       (int64_t)sizeof(rsh::ProbeOut)},
                          rsh::CopyEnt{c_->bucket.as<uint8_t>(), reinterpret_cast<uint8_t*>(hb),
@@ -491,9 +478,9 @@ class HipBackend : public rsh::ScanBackend {
                                   c_->ph_weak[set].as<int32_t>(), c_->ph_strong[set].as<uint8_t>(), ps,
                                   c_->abort_word + rsh_ctx::kPhaseWord, ph_gen_));
         ok(hipEventRecord(c_->ev_phb[set], ps));
-        ok(hipMemcpyAsync(c_->h_pw[set].p, c_->ph_weak[set].p, (size_t)count * 4, hipMemcpyDeviceToHost, ps));
-        if (dl_ > 0)
-            ok(hipMemcpyAsync(c_->h_ps[set].p, c_->ph_strong[set].p, (size_t)count * dl_, hipMemcpyDeviceToHost, ps));
+        ok(copy_to_host({rsh::CopyEnt{c_->ph_weak[set].as<uint8_t>(), c_->h_pw[set].as<uint8_t>(), count * 4},
+                         rsh::CopyEnt{c_->ph_strong[set].as<uint8_t>(), c_->h_ps[set].as<uint8_t>(), count * dl_}},
+                        ps));
         ok(hipEventRecord(c_->ev_phase[set], ps));
         c_->ph_set = set;
         ph_set_ = set;
@@ -868,7 +855,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             flags_gen = 0;
             RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
                                             (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(), ss));
-            if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, ss));
+            RSH_HIP(copy_to_host({rsh::CopyEnt{c->flags.as<uint8_t>(), c->h_fl.as<uint8_t>(), snf}}, ss));
         }
         RSH_HIP(hipEventRecord(c->ev_flags, ss));
         if (on_ctx) {
@@ -878,9 +865,9 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             spec_sums_na = spec_na;
             return RSH_OK;
         }
-        RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)spec_na * 4, hipMemcpyDeviceToHost, c->aux));
-        if (dl > 0)
-            RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)spec_na * dl, hipMemcpyDeviceToHost, c->aux));
+        RSH_HIP(copy_to_host({rsh::CopyEnt{c->src_weak.as<uint8_t>(), c->h_aw.as<uint8_t>(), spec_na * 4},
+                              rsh::CopyEnt{c->src_strong.as<uint8_t>(), c->h_as.as<uint8_t>(), spec_na * dl}},
+                             c->aux));
         RSH_HIP(hipEventRecord(c->ev_spec, c->aux));
         return RSH_OK;
     };
@@ -973,7 +960,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     auto table_work = [&]() -> int {
         if (download) {
             if (C > 0)
-                RSH_HIP(copy_to_host(c, kDescTable,
+                RSH_HIP(copy_to_host(
                                      {rsh::CopyEnt{reinterpret_cast<const uint8_t*>(d_weak), c->h_weak.as<uint8_t>(),
                                                    (int64_t)C * 4},
                                       rsh::CopyEnt{d_strong, c->h_strong.as<uint8_t>(), (int64_t)C * dl}},
@@ -1254,17 +1241,16 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                     RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak,
                                                     d_strong, (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(),
                                                     ss));
-                    if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, ss));
+                    RSH_HIP(copy_to_host({rsh::CopyEnt{c->flags.as<uint8_t>(), c->h_fl.as<uint8_t>(), snf}}, ss));
                     RSH_HIP(hipEventRecord(c->ev_flags, ss));
-                    RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)P * 4, hipMemcpyDeviceToHost, ss));
-                    if (dl > 0)
-                        RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)P * dl, hipMemcpyDeviceToHost, ss));
+                    RSH_HIP(copy_to_host({rsh::CopyEnt{c->src_weak.as<uint8_t>(), c->h_aw.as<uint8_t>(), P * 4},
+                                          rsh::CopyEnt{c->src_strong.as<uint8_t>(), c->h_as.as<uint8_t>(), P * dl}},
+                                         ss));
                     RSH_HIP(hipEventRecord(c->ev_spec, ss));
-                    RSH_HIP(hipMemcpyAsync(c->h_pw[pset].p, c->ph_weak[pset].p, (size_t)Q * 4, hipMemcpyDeviceToHost,
-                                           ss));
-                    if (dl > 0)
-                        RSH_HIP(hipMemcpyAsync(c->h_ps[pset].p, c->ph_strong[pset].p, (size_t)Q * dl,
-                                               hipMemcpyDeviceToHost, ss));
+                    RSH_HIP(copy_to_host({rsh::CopyEnt{c->ph_weak[pset].as<uint8_t>(), c->h_pw[pset].as<uint8_t>(), Q * 4},
+                                          rsh::CopyEnt{c->ph_strong[pset].as<uint8_t>(), c->h_ps[pset].as<uint8_t>(),
+                                                       Q * dl}},
+                                         ss));
                     RSH_HIP(hipEventRecord(c->ev_phase[pset], ss));
                     c->ph_set = pset;
                     k1_timed = true;     // (the event records around it)

@@ -300,6 +300,13 @@ struct CopyEnt {
     int64_t len;
 };
 hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hipStream_t s, bool bg = false);
+// Up to four device ranges into pinned host memory, the ranges passed by value in the kernel's arguments (nothing
+// for the host to keep alive after the launch); any alignment of source and destination.
+struct CopyFew {
+    CopyEnt e[4];
+    uint32_t n;
+};
+hipError_t launch_copy_few(const CopyFew& f, hipStream_t s);
 // n bytes of device memory into pinned host memory (h_dst 16-byte aligned), by a kernel.
 hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s);
 // Byte ranges between arbitrary (unaligned) device addresses: one op per workgroup, 16-byte stores to

@@ -158,6 +158,39 @@ hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hi
     return hipGetLastError();
 }
 
+// Destination bytes before the first 16-byte boundary are copied one per thread; the rest as copy_piece pieces,
+// with 16-byte loads when the source is then 16-byte aligned as well (a uniform branch per range).
+__global__ __launch_bounds__(256) void copy_few_kernel(CopyFew f) {
+    __builtin_amdgcn_s_setprio(3);
+    if (blockIdx.y >= f.n) return;
+    const CopyEnt e = f.e[blockIdx.y];
+    const int64_t head = min(e.len, (int64_t)((16 - ((uintptr_t)e.dst & 15)) & 15));
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, T = (int64_t)gridDim.x * blockDim.x;
+    if (t < head) e.dst[t] = e.src[t];
+    const uint8_t* src = e.src + head;
+    uint8_t* dst = e.dst + head;
+    const int64_t n = e.len - head;
+    if (((uintptr_t)src & 15) == 0) {
+        for (int64_t o = 16 * t; o < n; o += 16 * T) {
+            if (o + 16 <= n)
+                *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(src + o);
+            else
+                for (int64_t i = o; i < n; ++i) dst[i] = src[i];
+        }
+    } else {
+        for (int64_t o = 16 * t; o < n; o += 16 * T) copy_piece(src, dst, n, o);
+    }
+}
+
+hipError_t launch_copy_few(const CopyFew& f, hipStream_t s) {
+    int64_t mx = 0;
+    for (uint32_t i = 0; i < f.n; ++i) mx = std::max(mx, f.e[i].len);
+    if (f.n == 0 || mx <= 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((mx + 16 * 256 - 1) / (16 * 256), 64);
+    hipLaunchKernelGGL(copy_few_kernel, dim3((uint32_t)blocks, f.n), dim3(256), 0, s, f);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------------
 // True weak sums at arbitrary positions (one workgroup per position).
 // ------------------------------------------------------------------------------------------------

@@ -1722,8 +1722,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     bool any = false;
                     for (int64_t c = t; c < C; c += 2 * CHAIN_THREADS) {
                         const int64_t c2 = c + CHAIN_THREADS < C ? c + CHAIN_THREADS : c;
-                        any |= chain_digest_eq_reg(dg, F.table_strong + c * dl, dl) |
-                               chain_digest_eq_reg(dg, F.table_strong + c2 * dl, dl);
+                        any |= (int)chain_digest_eq_reg(dg, F.table_strong + c * dl, dl) |
+                               (int)chain_digest_eq_reg(dg, F.table_strong + c2 * dl, dl);
                     }
                     if (any) s_any = 1;
                 }
