@@ -616,10 +616,11 @@ namespace rshi {
 // a K1 that rewrites src_weak / src_strong on the context stream first waits for that download, when it is still
 // running (a host-side query: no wait packet in the common case).
 // The stamped launches' device counters and pinned stamps (scan_device under scan_spec_queue): slot 0 the prep
-// launch, slot 1 the chain flags.  prep_dev: the two counters (one 64-B line each), then the prep's scratch sums;
-// zero when allocated, and every stamped launch leaves them zero.
+// launch, slot 1 the chain flags.  prep_dev: each slot's counters (rsh::Stamp: the launch counter and its group
+// counters, 64 B each), then the prep's scratch sums; zero when allocated, and every stamped launch leaves them zero.
+constexpr size_t kStampBytes = 64 * (1 + rsh::kStampGroups), kPrepScratchAt = 2 * kStampBytes;
 hipError_t prep_ensure(rsh_ctx* c, int64_t nsamp) {
-    const size_t need = 256 + (size_t)(2 * nsamp + 2) * 4;
+    const size_t need = kPrepScratchAt + (size_t)(2 * nsamp + 2) * 4;
     if (c->prep_dev.cap < need) {
         hipError_t e = c->prep_dev.ensure(std::max<size_t>(need, 4096));
         if (e == hipSuccess) e = hipMemset(c->prep_dev.p, 0, c->prep_dev.cap);
@@ -632,7 +633,9 @@ hipError_t prep_ensure(rsh_ctx* c, int64_t nsamp) {
     }
     return hipSuccess;
 }
-uint32_t* prep_counter(rsh_ctx* c, int slot) { return reinterpret_cast<uint32_t*>(c->prep_dev.as<uint8_t>() + 64 * slot); }
+uint32_t* prep_counter(rsh_ctx* c, int slot) {
+    return reinterpret_cast<uint32_t*>(c->prep_dev.as<uint8_t>() + kStampBytes * slot);
+}
 int* prep_stamp(rsh_ctx* c, int slot) { return reinterpret_cast<int*>(c->h_stamps.as<uint8_t>() + 64 * slot); }
 
 // Spins until a stamped launch has written `gen` into its stamp.  A launch that fails never writes it: after 10 s
@@ -918,7 +921,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         P.out_w = tw;
         P.w0 = c->h_win0.as<uint8_t>();
         P.w0_len = w0;
-        P.scratch = reinterpret_cast<int32_t*>(c->prep_dev.as<uint8_t>() + 256);
+        P.scratch = reinterpret_cast<int32_t*>(c->prep_dev.as<uint8_t>() + kPrepScratchAt);
         P.st = rsh::Stamp{prep_counter(c, 0), prep_stamp(c, 0), prep_gen};
         RSH_HIP(rsh::launch_scan_prep(P, ss));
         if (head && !spec_launched && nlead > 0 && rsh::opt(rsh::OPT_SCAN_EARLY) != 0 && na <= kRoundWindows &&

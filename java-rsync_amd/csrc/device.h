@@ -125,6 +125,9 @@ hipError_t launch_warm_io(hipStream_t s);
 // Completion without a marker packet: the launch's last workgroup to finish writes `gen` into *stamp (pinned host
 // memory, system-scope release after every workgroup's stores), which the host polls.  counter: device memory,
 // zero before the launch (the last workgroup zeroes it again).
+// counter: kStampLine * (1 + kStampGroups) device words, zero between launches (the launch counter, then the group
+// counters of device_io.hip stamp_arrive, a 64-B line each)
+constexpr uint32_t kStampGroups = 64, kStampLine = 16;
 struct Stamp {
     uint32_t* counter;
     int* stamp;
