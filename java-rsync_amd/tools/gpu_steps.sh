@@ -40,7 +40,8 @@
 #   copycb-files the same over the config-4 line (VARIANT): which copies of the timeline run stay undelivered
 #   libab        builds of other commits against each other (LIBS: directories under java-rsync_amd/lib/ab, each holding a
 #                librsynchip.so, loaded through RSH_LIB), alternating, REPS times (AB_ARGS: bench args)
-#   ab           AB_OPTS ("name=value ...") against the default, alternating, REPS times (AB_ARGS: bench args)
+#   ab           AB_OPTS ("name=value ...") against the default, alternating, REPS times (AB_ARGS: bench args; AB_LIB:
+#                the library both arms load, default the diagnostics build)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/${TAG:-steps}
@@ -150,8 +151,9 @@ for step in "$@"; do
         first-trace) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --hip-trace --kernel-trace -d "$O/first_trace" \
             -o run --output-format csv -- python3 "$R/java-rsync_amd/tools/first_call.py" --only 5 --reps 2 \
             > "$O/first_trace.json" 2> "$O/first_trace.err") || exit 1 ;;
-        ab)  # the A/B switches are settable in the diagnostics build only: both arms load it
-            DIAG_LIB="$R/java-rsync_amd/lib/diag/librsynchip.so"
+        ab)  # the A/B switches are settable in the diagnostics build only: both arms load it (AB_LIB: another build,
+             # for product options)
+            DIAG_LIB=${AB_LIB:-"$R/java-rsync_amd/lib/diag/librsynchip.so"}
             OPTS=""
             for o in $AB_OPTS; do OPTS="$OPTS --opt $o"; done
             for r in $(seq 1 "${REPS:-3}"); do
