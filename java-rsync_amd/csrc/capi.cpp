@@ -741,7 +741,10 @@ hipError_t ctx_warm(rsh_ctx* c) {
             ok(hipMemcpyAsync(hp, d, 4096, hipMemcpyDeviceToHost, st));
             ok(hipMemcpyAsync(d + 8192, hp, 4096, hipMemcpyHostToDevice, st));
             ok(hipMemcpyAsync(d + 12288, d, 4096, hipMemcpyDeviceToDevice, st));
-            ok(hipMemcpyAsync(c->h_weak.p, d, 512 << 10, hipMemcpyDeviceToHost, st));  // table-sized (h_weak: C 4 + 4)
+            // a table-sized download (h_weak: C 4 + 4) the way the scan makes it (copy_to_host); the copy engine's
+            // table-sized D2H is no longer on any scan path, and the profiler's async-copy tracing never saw its
+            // completion (one per stream here: r5z2 copycb_files, hipMemcpyAsync of 512 KiB into pinned memory)
+            ok(copy_to_host({rsh::CopyEnt{d, c->h_weak.as<uint8_t>(), 512 << 10}}, st));
             ok(hipStreamSynchronize(st));
         }
     }
@@ -781,8 +784,8 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     const int64_t stride = std::max<int64_t>(1, (nf + nsamples - 1) / nsamples);
     std::vector<int64_t> samp;
     for (int64_t k = 0; k < nlead; ++k) samp.push_back(k);
-    for (int64_t k = stride; k < nf; k += stride)
-        if (k >= nlead) samp.push_back(k);
+    const int64_t samp_j0 = std::max<int64_t>(1, (nlead + stride - 1) / stride);  // the first multiple kept
+    for (int64_t k = samp_j0 * stride; k < nf; k += stride) samp.push_back(k);
     const int64_t nsamp = (int64_t)samp.size();
     const size_t lead_ents_at = ((size_t)(nsamp + 1) * 4 + 63) & ~(size_t)63;
     RSH_HIP(c->h_lead.ensure(lead_ents_at + (size_t)(nsamp + 1) * sizeof(rsh::GatherEnt) + sizeof(rsh::ScanFile)));
@@ -893,10 +896,8 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         // launch right behind the inputs' producer, then (launch-then-confirm, below) the speculation right behind
         // it: the two K1s are apart by this launch only, and nothing runs beside the speculation's start (the sample
         // kernels on aux beside it cost it ~90 us, r5c/r5e traces)
-        const size_t wins_at = 128, tw_at = wins_at + (((size_t)nsamp * 8 + 63) & ~(size_t)63);
+        const size_t tw_at = 128;
         RSH_HIP(c->h_prep.ensure(tw_at + (size_t)(nsamp + 1) * 4 + 64));
-        auto* wins = reinterpret_cast<int64_t*>(c->h_prep.as<uint8_t>() + wins_at);
-        for (int64_t i = 0; i < nsamp; ++i) wins[i] = samp[(size_t)i];
         int32_t* tw = reinterpret_cast<int32_t*>(c->h_prep.as<uint8_t>() + tw_at);
         {  // the scan as a batch of one for later gathers (the prefix end's window sums)
             auto* ents = reinterpret_cast<rsh::GatherEnt*>(c->h_lead.as<uint8_t>() + lead_ents_at);
@@ -914,7 +915,9 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         P.nsamp = head ? (uint32_t)nsamp : 0u;
         const int64_t pieces_opt = rsh::opt(rsh::OPT_SCAN_PREP_PIECES);
         P.pieces = (uint32_t)std::max<int64_t>(1, pieces_opt > 0 ? pieces_opt : std::min<int64_t>(8, (B + 16383) / 16384));
-        P.wins = wins;
+        P.nlead = (uint32_t)nlead;  // the kernel lists the samples itself (no host reads on its dependent chain)
+        P.stride = stride;
+        P.j0 = samp_j0;
         P.table_weak = d_weak;
         P.C = C;
         P.out_t = lead_w;

@@ -162,7 +162,7 @@ struct rsh_ctx {
     PinnedBuf h_files;   // the scan's rsh::ScanFile (a batch of one for the probe / gather kernels)
     PinnedBuf h_stage;   // file ingest ring (ingest.cpp); never shared with the scan's buffers
     PinnedBuf h_rcv_ops[2];  // rsh_receiver_combine_batch: the gather ops of a pass, staged
-    PinnedBuf h_prep;        // the prep launch's sample list and outputs (scan_spec_queue)
+    PinnedBuf h_prep;        // the prep launch's outputs (scan_spec_queue)
     PinnedBuf h_stamps;      // the stamped launches' stamps, one 64-B line each
     PinnedBuf h_fgw, h_fjobs, h_fout;  // flush_probe: the chain's gather list, its job, its outputs
     uint64_t first_used = 0;    // probe result slots handed out (see HipBackend::first_hit)

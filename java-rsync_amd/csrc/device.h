@@ -146,7 +146,9 @@ struct ScanPrep {
     int64_t n;
     uint32_t B;
     uint32_t nsamp, pieces;
-    const int64_t* wins;        // pinned host: the sampled window indices
+    // the sampled windows: i < nlead: window i; then window stride * (j0 + i - nlead) (capi.cpp scan_device's list)
+    uint32_t nlead;
+    int64_t stride, j0;
     const int32_t* table_weak;  // device: the received table's weak sums
     int32_t C;
     int32_t* out_t;             // pinned host: T(wins[i] B)

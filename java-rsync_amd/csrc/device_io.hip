@@ -122,6 +122,10 @@ hipError_t launch_chain_flags_stamped(const int32_t* d_wsrc, const uint8_t* d_ss
     return hipGetLastError();
 }
 
+__device__ __forceinline__ int64_t prep_window(const ScanPrep& P, uint32_t i) {
+    return i < P.nlead ? (int64_t)i : P.stride * (P.j0 + (int64_t)(i - P.nlead));
+}
+
 // blockIdx.x < nsamp * pieces: piece (blockIdx.x % pieces) of sample window blockIdx.x / pieces; the blocks past them
 // copy window 0 to the host, 4 KiB each.
 __global__ __launch_bounds__(256) void scan_prep_kernel(ScanPrep P) {
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(256) void scan_prep_kernel(ScanPrep P) {
     const uint32_t b = blockIdx.x, nsum = P.nsamp * P.pieces;
     if (b < nsum) {
         const uint32_t i = b / P.pieces, q = b % P.pieces;
-        const int64_t p = P.wins[i] * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
+        const int64_t p = prep_window(P, i) * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
         const int64_t plen = ((w + P.pieces - 1) / P.pieces + 15) & ~(int64_t)15;
         const int64_t lo = p + (int64_t)q * plen, hi = lo + plen < p + w ? lo + plen : p + w;
         int32_t v[2] = {0, 0};
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(256) void scan_prep_kernel(ScanPrep P) {
     }
     if (!stamp_arrive(P.st, &last)) return;
     for (uint32_t i = threadIdx.x; i < P.nsamp; i += blockDim.x) {
-        const int64_t k = P.wins[i], p = k * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
+        const int64_t k = prep_window(P, i), p = k * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
         const uint32_t S1 = (uint32_t)atomicExch(&P.scratch[2 * i], 0);
         const uint32_t U = (uint32_t)atomicExch(&P.scratch[2 * i + 1], 0);
         const uint32_t S2 = (uint32_t)w * S1 - U;
