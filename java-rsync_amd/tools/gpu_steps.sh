@@ -12,7 +12,7 @@
 #   files        the config-4 line, both basis forms (FILES_STEPS steps)
 #   files-trace  one traced config-4 step (VARIANT, default half): the chain walk's breakdown (scan_trace = 2)
 #   prof         rocprofv3 kernel trace + stats of the default line (the summary committed under profiles/)
-#   timeline     rocprofv3 kernel + copy timeline of the config-4 line (VARIANT)
+#   timeline     rocprofv3 kernel + copy timeline of the config-4 line (VARIANT; TL_ARGS: more bench args)
 #   hl           the config-5 headline alone (no companions, no config 4), 20 steps
 #   hl-trace     rocprofv3 kernel + copy trace of the headline alone, and its per-step gaps (tools/step_gaps.py)
 #   fetch        rocprofv3 --pmc FETCH_SIZE passes (counters only, kernel trace) of the default line and the config-4
@@ -93,7 +93,7 @@ for step in "$@"; do
             > "$O/prof_bench.json" 2> "$O/prof_bench.err") || exit 1 ;;
         timeline) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --kernel-trace --memory-copy-trace --stats \
             -d "$O/timeline" -o run --output-format csv -- python3 "$R/bench.py" --workload files --variant "$VARIANT" \
-            --steps 3 --warmup 1 --no-cpu-baseline --no-companions > "$O/timeline.json" 2> "$O/timeline.err") || exit 1 ;;
+            --steps 3 --warmup 1 --no-cpu-baseline --no-companions $TL_ARGS > "$O/timeline.json" 2> "$O/timeline.err") || exit 1 ;;
         fetch)
             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$O/fetch" -o run \
                 --output-format csv -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-companions \
