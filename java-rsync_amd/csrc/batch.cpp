@@ -816,9 +816,7 @@ hipError_t serve_round(rsh_ctx* c, BatchState* S, std::vector<FileScan>& files, 
         A.tiles = dt;
         A.partials = S->partials.as<int4>();
         chk(launch_probe_first(A, (uint32_t)tiles.size(), dpt, (uint32_t)ptiles.size(), st));
-        bool segs_small = true;  // every segment's file compares a few keys in registers
-        for (const ProbeSeg& g : segs) segs_small = segs_small && F[ivs[(size_t)g.iv].file].nsmall > 0;
-        chk(launch_probe_long(A, dsg, (uint32_t)segs.size(), st, segs_small));
+        chk(launch_probe_long(A, dsg, (uint32_t)segs.size(), st));
         chk(launch_hit_window(F, hiv, hreq, (int32_t)preq.size(), max_C, st));
         // the answers into pinned memory by a copy kernel (capi.cpp copy_to_host: no copy-engine hand-off between
         // kernels, and every copy the profiler traces completes)

@@ -270,9 +270,7 @@ int64_t probe_full_positions(int64_t a, int64_t b, int64_t n, int64_t B);
 void probe_plan(int64_t a, int64_t b, int64_t n, int64_t B, int32_t iv, int64_t seg_len, std::vector<ProbeTile>* tiles,
                 std::vector<ProbeSeg>* segs);
 // The segments' launch (writes the same ProbeOut records as the tiles' launch; either order).
-// small: every file of the segments has nsmall > 0 (the register-compare form, its bytes kept in registers)
-hipError_t launch_probe_long(const ProbeArgs& args, const ProbeSeg* segs, uint32_t nsegs, hipStream_t s,
-                             bool small = false);
+hipError_t launch_probe_long(const ProbeArgs& args, const ProbeSeg* segs, uint32_t nsegs, hipStream_t s);
 // Assigns ProbeTile::pbase for tiles[t0 ..] (one file's tiles, ascending) and appends the partial tiles
 // pass 1 computes for them (host side).
 void probe_partials(std::vector<ProbeTile>* tiles, size_t t0, int64_t B, int32_t file, std::vector<PartialTile>* out);

@@ -113,12 +113,10 @@ __device__ __forceinline__ int32_t sbyte_of(const uint32_t (&w)[4], int i) {
 // go out in one burst of independent loads -- most keys are decided by their first slot (load factor <= 1/2), so a
 // lane waits for about one L2 round trip -- and only keys whose first slot holds another key walk the probe path.
 // Branch free but for those walks and the (rare) hits.
-// SMALL_ONLY: the caller knows nsmall > 0 (no hash path in the code, nor in its register budget).
-template <bool SMALL_ONLY = false>
 __device__ __forceinline__ void probe_check16(const ScanFile& F, const ProbeTable& table, int nsmall,
                                               const uint32_t (&key)[16], uint32_t valid, int64_t base) {
     uint32_t m = 0;
-    if (SMALL_ONLY || nsmall > 0) {
+    if (nsmall > 0) {
         // one compare per key and position into a lane mask (the scalar unit ORs them); which positions only when
         // some lane matched (rare: a stale digest's keys over a file's rest)
         bool any = false;
@@ -133,7 +131,7 @@ __device__ __forceinline__ void probe_check16(const ScanFile& F, const ProbeTabl
 #pragma unroll
                 for (int i = 0; i < 16; ++i) m |= (uint32_t)(key[i] == kj) << i;
             }
-    } else if constexpr (!SMALL_ONLY) {
+    } else {
         unsigned long long sl[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) sl[i] = (valid >> i) & 1u ? table.slots[slot_hash(key[i]) & table.mask] : 0ull;
@@ -479,12 +477,7 @@ void probe_plan(int64_t a, int64_t b, int64_t n, int64_t B, int32_t iv, int64_t 
 // streams, weights relative to the sub-segment's start), each lane rolls its 64 positions with the exact Java updates
 // on R = T + E and checks every key as probe_first_kernel does per tile, and the last lane's rolled value (less E)
 // anchors the next sub-segment.  One anchor and one launch slot per segment (up to PROBE_LONG_PASSES passes).
-// SMALL (every file of the launch compares a few keys in registers: the batched flush chain's stale-digest probes over
-// a file's rest): the lane's 64 bytes at p0 and at p0 + B stay in registers for the whole pass, and the next pass's
-// are loaded at the top of this one, in flight across the exscan and this pass's keys.  Otherwise (hash lookups, whose
-// 16 first slots per group need the registers) each group of 16 positions re-reads its bytes from L1.
-template <bool SMALL>
-__global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(SMALL ? 2 : 4))) void probe_long_kernel(ProbeArgs A, const ProbeSeg* __restrict__ segs) {
+__global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void probe_long_kernel(ProbeArgs A, const ProbeSeg* __restrict__ segs) {
     __builtin_amdgcn_s_setprio(3);
     __shared__ int32_t sh[4 * PROBE_THREADS / 64];
     __shared__ int32_t s_next;  // T at the next sub-segment's start (packed halves)
@@ -504,54 +497,20 @@ __global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(S
     const ProbeTable table{F.slots, F.mask};
     const int nsmall = F.nsmall;
     const int t = threadIdx.x;
-    constexpr int G = PROBE_LONG_PPL / 16;
-    // 16 positions: the keys R = T + E, the rolling value's halves kept apart (each exact mod 2^16: the Java
-    // subtract-then-add of Rolling.java:25-60 in two adds each, as the chain walk's tiles) and packed per position;
-    // full windows throughout (w = B, the add always follows)
-    auto keys16 = [&](uint32_t& u1, uint32_t& u2, const uint32_t (&xa)[4], const uint32_t (&xb)[4], uint32_t (&key)[16]) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            key[i] = __builtin_amdgcn_perm(u2, u1, 0x05040100u);  // (u1 & 0xFFFF) | (u2 << 16)
-            const int32_t xo = sbyte_of(xa, i), xi = sbyte_of(xb, i);
-            u1 += (uint32_t)(xi - xo);
-            u2 += u1 - (uint32_t)__mul24((int)B, xo);
-        }
-    };
-    uint32_t ca[SMALL ? G : 1][4], cb[SMALL ? G : 1][4];  // SMALL: this pass's bytes
-    auto fetch = [&](int64_t pp, uint32_t (&xa)[SMALL ? G : 1][4], uint32_t (&xb)[SMALL ? G : 1][4]) {
-#pragma unroll
-        for (int k = 0; k < (SMALL ? G : 1); ++k) {
-            load16(data, n, pp + 16 * k, xa[k]);
-            load16(data, n, pp + B + 16 * k, xb[k]);
-        }
-    };
-    if constexpr (SMALL) fetch(q0 + (int64_t)t * PROBE_LONG_PPL, ca, cb);
     for (int64_t base = q0; base < q1; base += PROBE_LONG_SUB) {
         const int64_t p0 = base + (int64_t)t * PROBE_LONG_PPL;
         int32_t pre[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int k = 0; k < G; ++k) {  // the lane's bytes at p0 and at p0 + B: its sums
+        for (int k = 0; k < PROBE_LONG_PPL / 16; ++k) {  // the lane's bytes at p0 and at p0 + B: its sums
             uint32_t wa[4], wb[4];
-            if constexpr (SMALL) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    wa[j] = ca[k][j];
-                    wb[j] = cb[k][j];
-                }
-            } else {
-                load16(data, n, p0 + 16 * k, wa);
-                load16(data, n, p0 + B + 16 * k, wb);
-            }
+            load16(data, n, p0 + 16 * k, wa);
+            load16(data, n, p0 + B + 16 * k, wb);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 dword_sums(wa[j], (uint32_t)(p0 + 16 * k + 4 * j - base), pre[0], pre[1]);
                 dword_sums(wb[j], (uint32_t)(p0 + B + 16 * k + 4 * j - base), pre[2], pre[3]);
             }
         }
-        const bool more = base + PROBE_LONG_SUB < q1;
-        uint32_t na[SMALL ? G : 1][4], nbx[SMALL ? G : 1][4];
-        if constexpr (SMALL)
-            if (more) fetch(p0 + PROBE_LONG_SUB, na, nbx);
         block_exscan<4>(pre, sh);  // sums over [base, p0) and [base + B, p0 + B), weights j - base
         const bool live = p0 < q1;
         if (live) {
@@ -560,26 +519,24 @@ __global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(S
             const uint32_t s1 = P1e - (uint32_t)pre[0];
             const uint32_t s2 = (uint32_t)(p0 + B - base) * s1 - (P2e - (uint32_t)pre[1]);
             const uint32_t ehi = I.e_hi + I.e_lo * (uint32_t)(clampB(p0) - clampB(I.anchor));
+            // the rolling value's halves kept apart (each exact mod 2^16: the Java subtract-then-add of
+            // Rolling.java:25-60 in two adds each, as the chain walk's tiles), packed into the key per position
             uint32_t u1 = (s1 + I.e_lo) & 0xFFFFu, u2 = (s2 + ehi) & 0xFFFFu;
-            if constexpr (SMALL) {
-#pragma unroll
-                for (int grp = 0; grp < G; ++grp) {
-                    uint32_t key[16];
-                    keys16(u1, u2, ca[grp], cb[grp], key);
-                    const uint32_t valid = probe_valid16(p0 + 16 * grp, I.a, I.b < q1 ? I.b : q1);
-                    if (valid) probe_check16<true>(F, table, nsmall, key, valid, p0 + 16 * grp);
-                }
-            } else {
 #pragma unroll 1
-                for (int grp = 0; grp < G; ++grp) {  // bytes re-read (L1)
-                    uint32_t wa[4], wb[4];
-                    load16(data, n, p0 + 16 * grp, wa);
-                    load16(data, n, p0 + B + 16 * grp, wb);
-                    uint32_t key[16];
-                    keys16(u1, u2, wa, wb, key);
-                    const uint32_t valid = probe_valid16(p0 + 16 * grp, I.a, I.b < q1 ? I.b : q1);
-                    if (valid) probe_check16(F, table, nsmall, key, valid, p0 + 16 * grp);
+            for (int grp = 0; grp < PROBE_LONG_PPL / 16; ++grp) {  // 16 positions at a time (bytes re-read: L1)
+                uint32_t wa[4], wb[4];
+                load16(data, n, p0 + 16 * grp, wa);
+                load16(data, n, p0 + B + 16 * grp, wb);
+                uint32_t key[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {  // full windows throughout: w = B, the add always follows
+                    key[i] = __builtin_amdgcn_perm(u2, u1, 0x05040100u);  // (u1 & 0xFFFF) | (u2 << 16)
+                    const int32_t xo = sbyte_of(wa, i), xi = sbyte_of(wb, i);
+                    u1 += (uint32_t)(xi - xo);
+                    u2 += u1 - (uint32_t)__mul24((int)B, xo);
                 }
+                const uint32_t valid = probe_valid16(p0 + 16 * grp, I.a, I.b < q1 ? I.b : q1);
+                if (valid) probe_check16(F, table, nsmall, key, valid, p0 + 16 * grp);
             }
             if (t == PROBE_THREADS - 1) {  // R(p0 + 64) less E there: the next sub-segment's anchor T
                 const int64_t pn = p0 + PROBE_LONG_PPL;
@@ -592,22 +549,12 @@ __global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(S
         s1o = (uint32_t)s_next & 0xFFFFu;
         s2o = (uint32_t)s_next >> 16;
         __syncthreads();
-        if constexpr (SMALL)
-            if (more)
-#pragma unroll
-                for (int k = 0; k < G; ++k)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        ca[k][j] = na[k][j];
-                        cb[k][j] = nbx[k][j];
-                    }
     }
 }
 
-hipError_t launch_probe_long(const ProbeArgs& args, const ProbeSeg* segs, uint32_t nsegs, hipStream_t s, bool small) {
+hipError_t launch_probe_long(const ProbeArgs& args, const ProbeSeg* segs, uint32_t nsegs, hipStream_t s) {
     if (nsegs == 0) return hipSuccess;
-    if (small) hipLaunchKernelGGL(probe_long_kernel<true>, dim3(nsegs), dim3(PROBE_THREADS), 0, s, args, segs);
-    else hipLaunchKernelGGL(probe_long_kernel<false>, dim3(nsegs), dim3(PROBE_THREADS), 0, s, args, segs);
+    hipLaunchKernelGGL(probe_long_kernel, dim3(nsegs), dim3(PROBE_THREADS), 0, s, args, segs);
     return hipGetLastError();
 }
 
