@@ -1420,11 +1420,13 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             }
             RSH_BHIP(launch_chain_flags_many(fa, (uint32_t)NF, max_na, aux));
             RSH_BHIP(hipEventRecord(S->ev_fa, aux));
+            // the helpers' shared state goes up while the prefix K1 runs (behind the chunk indexes), not between the
+            // flags and the walks
+            if (map_on)
+                RSH_BHIP(hipMemcpyAsync(S->chain_help.p, chh, (size_t)NF * sizeof(ChainHelp), hipMemcpyHostToDevice, st));
             RSH_BHIP(hipStreamWaitEvent(st, S->ev_fa, 0));
             const int gen_b = ++c->gen;
             if (tr) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
-            if (map_on)
-                RSH_BHIP(hipMemcpyAsync(S->chain_help.p, chh, (size_t)NF * sizeof(ChainHelp), hipMemcpyHostToDevice, st));
             RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, 0, gen_b, map_on ? S->chain_help.as<ChainHelp>() : nullptr,
                                           n_help));
             RSH_BHIP(hipEventRecord(S->ev_wa, st));
