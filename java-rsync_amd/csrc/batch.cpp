@@ -1553,12 +1553,11 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             if (S->chain_help.p && two_phase) {  // the map's helpers (device state of the last phase-0 launch)
                 std::vector<ChainHelp> hh((size_t)NF);
                 if (hipMemcpy(hh.data(), S->chain_help.p, (size_t)NF * sizeof(ChainHelp), hipMemcpyDeviceToHost) == hipSuccess) {
-                    int64_t segs = 0, joins = 0, files_helped = 0, dhelped = 0;
+                    int64_t segs = 0, joins = 0, files_helped = 0;
                     for (const ChainHelp& q : hh) {
                         segs += q.mapped;
                         joins += q.joins;
                         files_helped += q.joins > 0;
-                        dhelped += q.dhelped;
                     }
                     const ChainHelp& q = hh[(size_t)fmax];
                     fprintf(stderr, "[rsh-batch]   hit map: %lld segments mapped over %lld files (%lld key sets built); file %d: %d "
@@ -1566,8 +1565,6 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                             "the walk's start\n", (long long)segs, (long long)files_helped, (long long)joins, fmax, q.mapped,
                             q.whole, q.joins, q.joins ? q.t_kset / 100.0 / q.joins : 0.0, q.claim, q.nseg,
                             q.t_first == INT64_MAX ? -1.0 : (q.t_first - q.t_start) / 100.0);
-                    fprintf(stderr, "[rsh-batch]   window digests taken from helpers: %lld (file %d: %d)\n",
-                            (long long)dhelped, fmax, q.dhelped);
                 }
             }
         }

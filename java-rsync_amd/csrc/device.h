@@ -399,12 +399,6 @@ struct ChainHelp {
     int64_t t_kset;            // wall-clock ticks spent building this file's key set in helpers (trace)
     int32_t whole;             // segments mapped whole, before the walk reached them (trace)
     int32_t nhelp;             // helpers currently on this file
-    int32_t dhelped;           // unaligned window digests the walk took from a helper (trace)
-    // One unaligned window digest computed ahead of the walk by a helper: (position << 2) | state, state 0 free,
-    // 1 being computed, 2 in dig (dl bytes packed four to a word).  A helper claims it (CAS) for the first unaligned
-    // hit of a tile it maps ahead of the walk, when it is free or holds a position the walk has passed.
-    unsigned long long dword;
-    uint32_t dig[4];
 };
 constexpr int CHAIN_THREADS = 512;                      // 8 waves (2 per SIMD: 256 VGPRs each)
 constexpr int CHAIN_PPT = 32;                            // wide tiles: positions per lane (two halves of 16)

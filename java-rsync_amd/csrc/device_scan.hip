@@ -928,9 +928,8 @@ __device__ __forceinline__ void chain_st64(int64_t* p, int64_t v) {
 // are the walk's wide-tile keys in the synced state (each lane anchored on its block's aligned sum T(o), the prefix
 // sums from one exscan rebased at each block's first lane, the head of the block the tile starts in); bit i of
 // lane t's word = position q0 + 32 t + i hits the key set.  Stored as (gen << 32) | bits, one 8-byte store.
-// s_first: the tile's first hit whose window has no speculated digest (unaligned, or past the prefix), by atomicMin.
 __device__ void chain_map_tile(const ChainFile& F, int64_t q0, uint32_t gen, const ChainKeySet& kset, int32_t* sh,
-                               int32_t (*s_seg)[4], unsigned long long* s_first) {
+                               int32_t (*s_seg)[4]) {
     const int t = threadIdx.x;
     const int64_t n = F.n, B = F.B, hend = F.hend;
     const int64_t kb0 = q0 / B, o0 = kb0 * B;
@@ -1000,10 +999,6 @@ __device__ void chain_map_tile(const ChainFile& F, int64_t q0, uint32_t gen, con
         if (hend - p0 < 32) bits &= (1u << (uint32_t)(hend - p0)) - 1u;  // windows past hend: not searched
         __hip_atomic_store(&F.hmap[p0 >> 5], ((unsigned long long)gen << 32) | bits, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t ub = bits;
-        const int64_t ia = (B - p0 % B) % B;  // the lane's aligned position (B >= 512: at most one in 32)
-        if (ia < 32 && (p0 + ia) / B < F.na_a) ub &= ~(1u << (uint32_t)ia);  // its digest is speculated
-        if (ub) atomicMin(s_first, (unsigned long long)(p0 + __builtin_ctz(ub)));
     }
     __syncthreads();  // (s_seg and sh: the next tile)
 }
@@ -1020,8 +1015,7 @@ constexpr int CHAIN_HELP_LEAD = 64;   // a helper stays with its file while the 
 __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict__ files, int nfiles, uint32_t gen,
                                                      ChainHelp* help, uint2* ck, int32_t* ck_full,
                                                      int32_t* sh, int32_t (*s_seg)[4], unsigned long long* s_best,
-                                                     int32_t* s_word, int32_t* s_live, unsigned long long* s_first,
-                                                     uint8_t* s_win, uint8_t* s_dig) {
+                                                     int32_t* s_word, int32_t* s_live) {
     const int t = threadIdx.x;
     const ChainKeySet kset{ck, ck_full};
     int cur = -1;
@@ -1096,10 +1090,7 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
         const int64_t lo = (int64_t)seg * CHAIN_MAP_SEG, hi = lo + CHAIN_MAP_SEG < F.hend ? lo + CHAIN_MAP_SEG : F.hend;
         bool whole = true;
         for (int64_t q0 = lo; q0 < hi; q0 += CHAIN_TILE) {
-            if (t == 0) {
-                *s_word = chain_ld(&h->live) != 0 && chain_ld64(&h->pos) < q0 + CHAIN_TILE;
-                *s_first = ~0ull;
-            }
+            if (t == 0) *s_word = chain_ld(&h->live) != 0 && chain_ld64(&h->pos) < q0 + CHAIN_TILE;
             __syncthreads();
             const bool go = *s_word != 0;
             __syncthreads();
@@ -1107,36 +1098,7 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
                 whole = false;
                 break;
             }
-            chain_map_tile(F, q0, gen, kset, sh, s_seg, s_first);
-            // the tile's first hit without a speculated digest, ahead of the walk: its window digest now, for the walk
-            // to take when it gets there (one MD5 chain, ~120-160 us on one lane: file 112's walk in config 4)
-            if (t == 0) {
-                const unsigned long long fp = *s_first;
-                int32_t claimed = 0;
-                if (fp != ~0ull && chain_ld(&h->live) != 0 && (int64_t)fp >= chain_ld64(&h->pos)) {
-                    const unsigned long long w = __hip_atomic_load(&h->dword, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((w & 3ull) == 0ull || ((w & 3ull) == 2ull && (int64_t)(w >> 2) < chain_ld64(&h->pos)))
-                        claimed = atomicCAS(&h->dword, w, (fp << 2) | 1ull) == w;
-                }
-                *s_word = claimed;
-            }
-            __syncthreads();
-            const bool dig = *s_word != 0;
-            const int64_t dp = (int64_t)*s_first;
-            __syncthreads();
-            if (dig) {
-                chain_window_digest(F.data + dp, (uint32_t)F.B, (uint32_t)F.dl, F.seed, s_win, s_dig);
-                if (t == 0) {
-                    uint32_t w4[4];
-                    chain_digest_load(s_dig, F.dl, w4);
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        __hip_atomic_store(&h->dig[j], w4[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&h->dword, ((unsigned long long)dp << 2) | 2ull, __ATOMIC_RELEASE,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-                __syncthreads();
-            }
+            chain_map_tile(F, q0, gen, kset, sh, s_seg);
         }
         if (t == 0) {
             atomicAdd(&h->mapped, 1);
@@ -1167,11 +1129,9 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ rsh_event s_ev[CHAIN_EV_LDS];   // finished events not yet in F.ev
     __shared__ unsigned long long s_best;      // helpers: the file to map next
     __shared__ int32_t s_word, s_live;
-    __shared__ unsigned long long s_first;     // helpers: a mapped tile's first hit without a speculated digest
     const ChainKeySet kset{s_ck, &s_ck_full};
     if ((int)blockIdx.x >= nfiles) {  // a helper workgroup (phase 0): it only maps
-        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live,
-                   &s_first, s_win, s_dig);
+        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live);
         return;
     }
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
@@ -1721,42 +1681,10 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const uint8_t* md5c = poisoned ? stale : F.as + kp * dl;
         if (!spec_digest && !poisoned) {
             const int64_t td0 = (int64_t)wall_clock64();
-            // a helper's digest of this window (ChainHelp::dword): taken when ready, waited for while one is on it;
-            // the words are read between two loads of the state word, which must agree
-            bool got = false;
-            if (H != nullptr) {
-                if (t == 0) {
-                    const unsigned long long want = (unsigned long long)p << 2;
-                    unsigned long long w = __hip_atomic_load(&H->dword, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                    while (w == (want | 1ull)) {
-                        __builtin_amdgcn_s_sleep(16);
-                        w = __hip_atomic_load(&H->dword, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    int32_t ok = 0;
-                    if (w == (want | 2ull)) {
-                        uint32_t d4[4];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            d4[j] = __hip_atomic_load(&H->dig[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (__hip_atomic_load(&H->dword, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == w) {
-                            ok = 1;
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) reinterpret_cast<uint32_t*>(s_dig)[j] = d4[j];
-                            atomicAdd(&H->dhelped, 1);
-                        }
-                    }
-                    s_word = ok;
-                }
-                __syncthreads();
-                got = s_word != 0;
-                __syncthreads();
-            }
-            if (!got) {
-                chain_window_digest(F.data + p, (uint32_t)B, (uint32_t)dl, F.seed, s_win, s_dig);  // (ends with a barrier)
-                ++digests;
-            }
+            chain_window_digest(F.data + p, (uint32_t)B, (uint32_t)dl, F.seed, s_win, s_dig);  // (ends with a barrier)
             md5c = s_dig;
             chain_digest_load(s_dig, dl, dg);
+            ++digests;
             t_digest += (int64_t)wall_clock64() - td0;
         }
         int32_t hit = -1;
@@ -1909,8 +1837,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     if (H != nullptr) {  // this walk is over: its helpers stop, and the workgroup helps the walks still searching
         if (t == 0) chain_st(&H->live, 0);
         __syncthreads();
-        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live,
-                   &s_first, s_win, s_dig);
+        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live);
     }
 }
 
