@@ -134,7 +134,6 @@ struct BatchState {
     hipEvent_t ev_sync = nullptr;  // spin_sync: the latency-path waits poll an event instead of blocking
     hipEvent_t ev_ch0 = nullptr, ev_ch1 = nullptr;  // around the walk (trace)
     hipEvent_t ev_fa = nullptr, ev_wa = nullptr;    // two-phase walk: prefix flags done, phase-0 walk done
-    hipEvent_t ev_ix = nullptr;                     // two-phase walk: chunk indexes, windows 0, helpers' state (aux)
     hipError_t ensure_file_abort(int64_t nf) {
         if (nf <= file_abort_cap) return hipSuccess;
         if (file_abort) (void)hipFree(file_abort);
@@ -157,7 +156,7 @@ struct BatchState {
             if (scopy_pending) (void)hipEventSynchronize(ev_scopy);
             (void)hipEventDestroy(ev_scopy);
         }
-        for (hipEvent_t e : {ev_fk, ev_ch0, ev_ch1, ev_fa, ev_wa, ev_ix, ev_sync})
+        for (hipEvent_t e : {ev_fk, ev_ch0, ev_ch1, ev_fa, ev_wa, ev_sync})
             if (e) (void)hipEventDestroy(e);
         kslots.release();
         for (PinnedBuf* b : {&h_kents, &h_chain, &h_chain_out, &h_chain_ev, &h_chain_help}) b->release();
@@ -1034,10 +1033,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         wc[f] = CopyEnt{fs.d_src, S->h_win0.as<uint8_t>() + fs.off_w0, w0};
         max_w0 = std::max(max_w0, w0);
     }
-    // two-phase chain walk: the prefix K1 takes the context stream right behind whatever produced the inputs, and
-    // this copy and the chunk indexes go to aux beside it (below)
-    const bool k1_on_st = chain_on && two_phase;
-    if (!k1_on_st) RSH_BHIP(launch_copy_many(wc, (uint32_t)NF, max_w0, st));
+    RSH_BHIP(launch_copy_many(wc, (uint32_t)NF, max_w0, st));
     // (stream) T(kB) of each file's first lead windows (the launch decision below, as in scan_device)
     std::vector<int64_t> lead_at((size_t)NF + 1, 0);
     for (int32_t f = 0; f < NF; ++f)
@@ -1104,15 +1100,13 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         // the chunk indexes must be ready when the prefix K1 ends (the phase-0 walks wait for both): the runtime's
         // fill, then the index with several CASes in flight per thread; beside the prefix K1 (which holds every
         // wave slot) both end with it in config 4 (r3s: fill 0.06 ms + index 0.20 ms inside the K1's 0.29 ms)
+        RSH_BHIP(hipMemsetAsync(S->kslots.p, 0, (size_t)tns * 8, st));
         TableEnt* ke = S->h_kents.as<TableEnt>();
         for (int32_t f = 0; f < NF; ++f) {
             FileScan& fs = files[(size_t)f];
             ke[f] = TableEnt{S->kslots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
         }
-        if (!k1_on_st) {
-            RSH_BHIP(hipMemsetAsync(S->kslots.p, 0, (size_t)tns * 8, st));
-            RSH_BHIP(launch_chunk_index(ke, (uint32_t)NF, (int32_t)maxC, st, bg));
-        }
+        RSH_BHIP(launch_chunk_index(ke, (uint32_t)NF, (int32_t)maxC, st, bg));
     }
     if (spec_after_prep && prep_all) RSH_BHIP(hipEventRecord(c->ev_prep, st));
 
@@ -1411,19 +1405,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                 RSH_BHIP(hipMemcpyAsync(S->k1_lanes.p, hl, (nla + nlb) * sizeof(K1Lane), hipMemcpyHostToDevice, aux));
             RSH_BHIP(hipEventRecord(S->ev_scopy, aux));
             S->scopy_pending = true;
-            // (aux) the chunk indexes, windows 0 and the helpers' state, beside the prefix K1; the walks wait for them
-            if (!S->ev_ix) RSH_BHIP(hipEventCreateWithFlags(&S->ev_ix, hipEventDisableTiming));
-            RSH_BHIP(hipStreamWaitEvent(aux, c->ev_in, 0));  // the received tables
-            RSH_BHIP(hipMemsetAsync(S->kslots.p, 0, (size_t)tns * 8, aux));
-            RSH_BHIP(launch_chunk_index(S->h_kents.as<TableEnt>(), (uint32_t)NF, (int32_t)maxC, aux, bg));
-            RSH_BHIP(launch_copy_many(wc, (uint32_t)NF, max_w0, aux));
-            if (map_on)
-                RSH_BHIP(hipMemcpyAsync(S->chain_help.p, chh, (size_t)NF * sizeof(ChainHelp), hipMemcpyHostToDevice, aux));
-            RSH_BHIP(hipEventRecord(S->ev_ix, aux));
-            // (stream) the prefix K1 right behind the inputs' producer (no cross-queue hand-off), then its flags
-            RSH_BHIP(hipStreamWaitEvent(st, S->ev_scopy, 0));  // its groups (uploaded long before, as a rule)
+            RSH_BHIP(hipStreamWaitEvent(aux, c->ev_in, 0));  // the sources only (no lead check in chain mode)
             RSH_BHIP(launch_block_sums_batch(S->k1_groups.as<K1Group>(), ng_a, S->k1_lanes.as<K1Lane>(), (uint32_t)nla,
-                                             align_a, seed_word(seed), st, c->abort_word, gen, partial_a));
+                                             align_a, seed_word(seed), aux, c->abort_word, gen, partial_a));
+            RSH_BHIP(hipStreamWaitEvent(aux, c->ev_in, 0));  // the flags need the received tables
             FlagEnt* fa = S->h_flagents_a.as<FlagEnt>();
             uint32_t max_na = 0;
             for (int32_t f = 0; f < NF; ++f) {
@@ -1433,9 +1418,13 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                                 fs.d_strong, S->flags.as<uint8_t>() + fs.off_nf, nflag, (uint32_t)fs.dl};
                 max_na = std::max(max_na, nflag);
             }
-            RSH_BHIP(launch_chain_flags_many(fa, (uint32_t)NF, max_na, st));
-            RSH_BHIP(hipEventRecord(S->ev_fa, st));
-            RSH_BHIP(hipStreamWaitEvent(st, S->ev_ix, 0));
+            RSH_BHIP(launch_chain_flags_many(fa, (uint32_t)NF, max_na, aux));
+            RSH_BHIP(hipEventRecord(S->ev_fa, aux));
+            // the helpers' shared state goes up while the prefix K1 runs (behind the chunk indexes), not between the
+            // flags and the walks
+            if (map_on)
+                RSH_BHIP(hipMemcpyAsync(S->chain_help.p, chh, (size_t)NF * sizeof(ChainHelp), hipMemcpyHostToDevice, st));
+            RSH_BHIP(hipStreamWaitEvent(st, S->ev_fa, 0));
             const int gen_b = ++c->gen;
             if (tr) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
             RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, 0, gen_b, map_on ? S->chain_help.as<ChainHelp>() : nullptr,
