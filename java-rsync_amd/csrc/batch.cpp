@@ -927,8 +927,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     RSH_BHIP(S->ensure_file_abort(NF));
     for (K1Plan& pl : plans) pl.abort = S->file_abort + pl.file;
     // The chain walk (option batch_chain, with the default speculation policy) runs after the speculation.  Two
-    // phases (option batch_chain_prefix): the speculation over each file's first na_a windows -- about one round of
-    // the chip's wave slots over the whole batch -- and a walk over them; then the rest of the speculation for the
+    // phases (option batch_chain_prefix): the speculation over each file's first na_a windows -- a quarter round of
+    // the chip's wave slots over the whole batch (256 windows per file for config 4's 128 files: its 50%-modified
+    // walks all end inside 2 MiB; a full round, 1024, cost that step 0.3 ms of prefix K1 and the identical one
+    // 0.065 ms less, round 5 r5z6/r5z7) -- and a walk over them; then the rest of the speculation for the
     // files whose walk reached the prefix's end (the others' groups stop at once: the walk wrote their abort words)
     // and a second walk.  A file that leaves the synced state early (an edit) costs its prefix, not its whole length.
     const bool chain_on = opt(OPT_BATCH_CHAIN) != 0 && opt(OPT_BATCH_SPEC) == -1;
@@ -942,7 +944,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     uint32_t ng_a = 0, ng_b = 0;
     for (FileScan& fs : files) fs.na_a = fs.na;
     if (const int64_t pre = opt(OPT_BATCH_CHAIN_PREFIX); chain_on && pre != 0) {
-        const int64_t P = pre > 0 ? pre : 64 * std::max<int64_t>(1, kWaveSlots / std::max<int32_t>(NF, 1));
+        const int64_t P = pre > 0 ? pre : 16 * std::max<int64_t>(1, kWaveSlots / std::max<int32_t>(NF, 1));
         for (FileScan& fs : files) {
             fs.na_a = std::min(fs.na, P);
             two_phase = two_phase || fs.na_a < fs.na;
@@ -1296,7 +1298,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             const hipError_t x = serve_round(c, S, files, std::vector<int32_t>{fi}, es);
             if (x != hipSuccess && early_err == hipSuccess) early_err = x;
         };
-        if (fs.C <= kEagerSortChunks) fs.table.build();
+        // (no eager sort: a stale digest's flush chain needs no bucket lookups; the index is built if a lookup comes)
         resolve_run(fs.n, fs.table, fs.be, &fs.rs, &fs.res, nullptr);
         b.direct = nullptr;
         fs.rs.done = fs.done = true;
@@ -1420,11 +1422,13 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             }
             RSH_BHIP(launch_chain_flags_many(fa, (uint32_t)NF, max_na, aux));
             RSH_BHIP(hipEventRecord(S->ev_fa, aux));
+            // the helpers' shared state goes up while the prefix K1 runs (behind the chunk indexes), not between the
+            // flags and the walks
+            if (map_on)
+                RSH_BHIP(hipMemcpyAsync(S->chain_help.p, chh, (size_t)NF * sizeof(ChainHelp), hipMemcpyHostToDevice, st));
             RSH_BHIP(hipStreamWaitEvent(st, S->ev_fa, 0));
             const int gen_b = ++c->gen;
             if (tr) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
-            if (map_on)
-                RSH_BHIP(hipMemcpyAsync(S->chain_help.p, chh, (size_t)NF * sizeof(ChainHelp), hipMemcpyHostToDevice, st));
             RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, 0, gen_b, map_on ? S->chain_help.as<ChainHelp>() : nullptr,
                                           n_help));
             RSH_BHIP(hipEventRecord(S->ev_wa, st));
@@ -1476,7 +1480,6 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     int32_t nwait = 0;
     if (chain_on) {  // the walks have ended (the stream sync above): each resolver resumes where its walk stopped
         const ChainOut* co = S->h_chain_out.as<ChainOut>();
-        const rsh_event* ce = S->h_chain_ev.as<rsh_event>();
         int32_t left = 0;
         for (int32_t f = 0; f < NF; ++f) {
             if (early[(size_t)f]) continue;  // resolved while the other walks ran

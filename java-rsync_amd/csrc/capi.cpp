@@ -27,25 +27,15 @@ namespace {
 // HIP implementation of the resolver's services.
 // ------------------------------------------------------------------------------------------------
 constexpr size_t kFirstSlots = 1024;
-// Device results to pinned host memory by a copy kernel (copy_many_kernel) rather than hipMemcpyAsync: between two
+// Device results to pinned host memory by a copy kernel (copy_few_kernel) rather than hipMemcpyAsync: between two
 // kernels a D2H copy cost 47-100 us of idle queue (tools/queue_lat.hip case 8) where a kernel writing pinned memory
-// cost none (case 9), and the profiler's async-copy tracing reported the scan's table downloads as never completed
-// (DESIGN.md section 6).  Each call site has its own descriptor slot (kDesc*) in pinned memory:
-// the kernel reads it after the host returns, so a slot is reused only once its previous copy has been waited for.
-enum { kDescTable = 0, kDescProbe, kDescSums, kDescSlots };
-hipError_t copy_to_host(rsh_ctx* c, int slot, std::initializer_list<rsh::CopyEnt> ents, hipStream_t s) {
-    constexpr int kPer = 4;
-    hipError_t e = c->h_desc.ensure((size_t)kDescSlots * kPer * sizeof(rsh::CopyEnt));
-    if (e != hipSuccess) return e;
-    rsh::CopyEnt* d = c->h_desc.as<rsh::CopyEnt>() + slot * kPer;
-    uint32_t n = 0;
-    int64_t mx = 0;
+// cost none (case 9), and the profiler's async-copy tracing reported the copy engine's completions as never
+// delivered.  The ranges travel in the kernel's arguments.
+hipError_t copy_to_host(std::initializer_list<rsh::CopyEnt> ents, hipStream_t s) {
+    rsh::CopyFew f{};
     for (const rsh::CopyEnt& x : ents)
-        if (x.len > 0) {
-            d[n++] = x;
-            mx = std::max(mx, x.len);
-        }
-    return rsh::launch_copy_many(d, n, mx, s);
+        if (x.len > 0 && f.n < 4) f.e[f.n++] = x;
+    return rsh::launch_copy_few(f, s);
 }
 constexpr int kScanWindows = 2;  // hit windows per probe in the single-file scan (hit_cache.h)
 // Head mode launches the aligned speculation after scan_defer_steps (4) resolver steps or scan_defer_us (500 us;
@@ -108,7 +98,7 @@ class HipBackend : public rsh::ScanBackend {
                 // waits: the copy is tens of microseconds, the generic path's probe and host digest as long or longer
                 CallTrace tr("sums_dl", lazy_na);
                 ok(hipStreamWaitEvent(rs_, c_->ev_flags, 0));
-                ok(copy_to_host(c_, kDescSums, {rsh::CopyEnt{c_->src_weak.as<uint8_t>(), c_->h_aw.as<uint8_t>(), lazy_na * 4},
+                ok(copy_to_host({rsh::CopyEnt{c_->src_weak.as<uint8_t>(), c_->h_aw.as<uint8_t>(), lazy_na * 4},
                                                 rsh::CopyEnt{c_->src_strong.as<uint8_t>(), c_->h_as.as<uint8_t>(),
                                                              dl_ > 0 ? lazy_na * dl_ : 0}},
                                 rs_));
@@ -168,14 +158,11 @@ class HipBackend : public rsh::ScanBackend {
             ok(rsh::launch_chain_flags(c_->src_weak.as<int32_t>() + k0, c_->src_strong.as<uint8_t>() + k0 * dl_,
                                        d_table_weak_ + k0, reinterpret_cast<const uint8_t*>(d_table_strong) + k0 * dl_,
                                        (uint32_t)(f1 - k0), (uint32_t)dl_, c_->flags.as<uint8_t>() + k0, rs_));
-        ok(hipMemcpyAsync(c_->h_aw.as<int32_t>() + k0, c_->src_weak.as<int32_t>() + k0, (size_t)(k1 - k0) * 4,
-                          hipMemcpyDeviceToHost, rs_));
-        if (dl_ > 0)
-            ok(hipMemcpyAsync(c_->h_as.as<uint8_t>() + k0 * dl_, c_->src_strong.as<uint8_t>() + k0 * dl_,
-                              (size_t)((k1 - k0) * dl_), hipMemcpyDeviceToHost, rs_));
-        if (f1 > k0)
-            ok(hipMemcpyAsync(c_->h_fl.as<uint8_t>() + k0, c_->flags.as<uint8_t>() + k0, (size_t)(f1 - k0),
-                              hipMemcpyDeviceToHost, rs_));
+        ok(copy_to_host({rsh::CopyEnt{c_->src_weak.as<uint8_t>() + 4 * k0, c_->h_aw.as<uint8_t>() + 4 * k0, (k1 - k0) * 4},
+                         rsh::CopyEnt{c_->src_strong.as<uint8_t>() + k0 * dl_, c_->h_as.as<uint8_t>() + k0 * dl_,
+                                      (k1 - k0) * dl_},
+                         rsh::CopyEnt{c_->flags.as<uint8_t>() + k0, c_->h_fl.as<uint8_t>() + k0, f1 - k0}},
+                        rs_));
         ok(hipStreamSynchronize(rs_));
         bytes_read += std::min(n_, k1 * B_) - k0 * B_;
         aligned_end = k1;
@@ -424,7 +411,7 @@ class HipBackend : public rsh::ScanBackend {
         int32_t* req = hb + rsh::HIT_BUCKET_INTS;
         *req = 0;
         ok(rsh::launch_hit_window(F, hiv, req, 1, t_.chunk_count, rs_));
-        ok(copy_to_host(c_, kDescProbe,
+        ok(copy_to_host(
                         {rsh::CopyEnt{reinterpret_cast<const uint8_t*>(d_first), reinterpret_cast<uint8_t*>(hf),
                                       (int64_t)sizeof(rsh::ProbeOut)},
                          rsh::CopyEnt{c_->bucket.as<uint8_t>(), reinterpret_cast<uint8_t*>(hb),
@@ -491,9 +478,9 @@ class HipBackend : public rsh::ScanBackend {
                                   c_->ph_weak[set].as<int32_t>(), c_->ph_strong[set].as<uint8_t>(), ps,
                                   c_->abort_word + rsh_ctx::kPhaseWord, ph_gen_));
         ok(hipEventRecord(c_->ev_phb[set], ps));
-        ok(hipMemcpyAsync(c_->h_pw[set].p, c_->ph_weak[set].p, (size_t)count * 4, hipMemcpyDeviceToHost, ps));
-        if (dl_ > 0)
-            ok(hipMemcpyAsync(c_->h_ps[set].p, c_->ph_strong[set].p, (size_t)count * dl_, hipMemcpyDeviceToHost, ps));
+        ok(copy_to_host({rsh::CopyEnt{c_->ph_weak[set].as<uint8_t>(), c_->h_pw[set].as<uint8_t>(), count * 4},
+                         rsh::CopyEnt{c_->ph_strong[set].as<uint8_t>(), c_->h_ps[set].as<uint8_t>(), count * dl_}},
+                        ps));
         ok(hipEventRecord(c_->ev_phase[set], ps));
         c_->ph_set = set;
         ph_set_ = set;
@@ -629,10 +616,11 @@ namespace rshi {
 // a K1 that rewrites src_weak / src_strong on the context stream first waits for that download, when it is still
 // running (a host-side query: no wait packet in the common case).
 // The stamped launches' device counters and pinned stamps (scan_device under scan_spec_queue): slot 0 the prep
-// launch, slot 1 the chain flags.  prep_dev: the two counters (one 64-B line each), then the prep's scratch sums;
-// zero when allocated, and every stamped launch leaves them zero.
+// launch, slot 1 the chain flags.  prep_dev: each slot's counters (rsh::Stamp: the launch counter and its group
+// counters, 64 B each), then the prep's scratch sums; zero when allocated, and every stamped launch leaves them zero.
+constexpr size_t kStampBytes = 64 * (1 + rsh::kStampGroups), kPrepScratchAt = 2 * kStampBytes;
 hipError_t prep_ensure(rsh_ctx* c, int64_t nsamp) {
-    const size_t need = 256 + (size_t)(2 * nsamp + 2) * 4;
+    const size_t need = kPrepScratchAt + (size_t)(2 * nsamp + 2) * 4;
     if (c->prep_dev.cap < need) {
         hipError_t e = c->prep_dev.ensure(std::max<size_t>(need, 4096));
         if (e == hipSuccess) e = hipMemset(c->prep_dev.p, 0, c->prep_dev.cap);
@@ -645,7 +633,9 @@ hipError_t prep_ensure(rsh_ctx* c, int64_t nsamp) {
     }
     return hipSuccess;
 }
-uint32_t* prep_counter(rsh_ctx* c, int slot) { return reinterpret_cast<uint32_t*>(c->prep_dev.as<uint8_t>() + 64 * slot); }
+uint32_t* prep_counter(rsh_ctx* c, int slot) {
+    return reinterpret_cast<uint32_t*>(c->prep_dev.as<uint8_t>() + kStampBytes * slot);
+}
 int* prep_stamp(rsh_ctx* c, int slot) { return reinterpret_cast<int*>(c->h_stamps.as<uint8_t>() + 64 * slot); }
 
 // Spins until a stamped launch has written `gen` into its stamp.  A launch that fails never writes it: after 10 s
@@ -751,7 +741,10 @@ hipError_t ctx_warm(rsh_ctx* c) {
             ok(hipMemcpyAsync(hp, d, 4096, hipMemcpyDeviceToHost, st));
             ok(hipMemcpyAsync(d + 8192, hp, 4096, hipMemcpyHostToDevice, st));
             ok(hipMemcpyAsync(d + 12288, d, 4096, hipMemcpyDeviceToDevice, st));
-            ok(hipMemcpyAsync(c->h_weak.p, d, 512 << 10, hipMemcpyDeviceToHost, st));  // table-sized (h_weak: C 4 + 4)
+            // a table-sized download (h_weak: C 4 + 4) the way the scan makes it (copy_to_host); the copy engine's
+            // table-sized D2H is no longer on any scan path, and the profiler's async-copy tracing never saw its
+            // completion (one per stream here: r5z2 copycb_files, hipMemcpyAsync of 512 KiB into pinned memory)
+            ok(copy_to_host({rsh::CopyEnt{d, c->h_weak.as<uint8_t>(), 512 << 10}}, st));
             ok(hipStreamSynchronize(st));
         }
     }
@@ -791,8 +784,8 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     const int64_t stride = std::max<int64_t>(1, (nf + nsamples - 1) / nsamples);
     std::vector<int64_t> samp;
     for (int64_t k = 0; k < nlead; ++k) samp.push_back(k);
-    for (int64_t k = stride; k < nf; k += stride)
-        if (k >= nlead) samp.push_back(k);
+    const int64_t samp_j0 = std::max<int64_t>(1, (nlead + stride - 1) / stride);  // the first multiple kept
+    for (int64_t k = samp_j0 * stride; k < nf; k += stride) samp.push_back(k);
     const int64_t nsamp = (int64_t)samp.size();
     const size_t lead_ents_at = ((size_t)(nsamp + 1) * 4 + 63) & ~(size_t)63;
     RSH_HIP(c->h_lead.ensure(lead_ents_at + (size_t)(nsamp + 1) * sizeof(rsh::GatherEnt) + sizeof(rsh::ScanFile)));
@@ -868,7 +861,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             flags_gen = 0;
             RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak, d_strong,
                                             (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(), ss));
-            if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, ss));
+            RSH_HIP(copy_to_host({rsh::CopyEnt{c->flags.as<uint8_t>(), c->h_fl.as<uint8_t>(), snf}}, ss));
         }
         RSH_HIP(hipEventRecord(c->ev_flags, ss));
         if (on_ctx) {
@@ -878,9 +871,9 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             spec_sums_na = spec_na;
             return RSH_OK;
         }
-        RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)spec_na * 4, hipMemcpyDeviceToHost, c->aux));
-        if (dl > 0)
-            RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)spec_na * dl, hipMemcpyDeviceToHost, c->aux));
+        RSH_HIP(copy_to_host({rsh::CopyEnt{c->src_weak.as<uint8_t>(), c->h_aw.as<uint8_t>(), spec_na * 4},
+                              rsh::CopyEnt{c->src_strong.as<uint8_t>(), c->h_as.as<uint8_t>(), spec_na * dl}},
+                             c->aux));
         RSH_HIP(hipEventRecord(c->ev_spec, c->aux));
         return RSH_OK;
     };
@@ -903,10 +896,8 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         // launch right behind the inputs' producer, then (launch-then-confirm, below) the speculation right behind
         // it: the two K1s are apart by this launch only, and nothing runs beside the speculation's start (the sample
         // kernels on aux beside it cost it ~90 us, r5c/r5e traces)
-        const size_t wins_at = 128, tw_at = wins_at + (((size_t)nsamp * 8 + 63) & ~(size_t)63);
+        const size_t tw_at = 128;
         RSH_HIP(c->h_prep.ensure(tw_at + (size_t)(nsamp + 1) * 4 + 64));
-        auto* wins = reinterpret_cast<int64_t*>(c->h_prep.as<uint8_t>() + wins_at);
-        for (int64_t i = 0; i < nsamp; ++i) wins[i] = samp[(size_t)i];
         int32_t* tw = reinterpret_cast<int32_t*>(c->h_prep.as<uint8_t>() + tw_at);
         {  // the scan as a batch of one for later gathers (the prefix end's window sums)
             auto* ents = reinterpret_cast<rsh::GatherEnt*>(c->h_lead.as<uint8_t>() + lead_ents_at);
@@ -924,14 +915,16 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         P.nsamp = head ? (uint32_t)nsamp : 0u;
         const int64_t pieces_opt = rsh::opt(rsh::OPT_SCAN_PREP_PIECES);
         P.pieces = (uint32_t)std::max<int64_t>(1, pieces_opt > 0 ? pieces_opt : std::min<int64_t>(8, (B + 16383) / 16384));
-        P.wins = wins;
+        P.nlead = (uint32_t)nlead;  // the kernel lists the samples itself (no host reads on its dependent chain)
+        P.stride = stride;
+        P.j0 = samp_j0;
         P.table_weak = d_weak;
         P.C = C;
         P.out_t = lead_w;
         P.out_w = tw;
         P.w0 = c->h_win0.as<uint8_t>();
         P.w0_len = w0;
-        P.scratch = reinterpret_cast<int32_t*>(c->prep_dev.as<uint8_t>() + 256);
+        P.scratch = reinterpret_cast<int32_t*>(c->prep_dev.as<uint8_t>() + kPrepScratchAt);
         P.st = rsh::Stamp{prep_counter(c, 0), prep_stamp(c, 0), prep_gen};
         RSH_HIP(rsh::launch_scan_prep(P, ss));
         if (head && !spec_launched && nlead > 0 && rsh::opt(rsh::OPT_SCAN_EARLY) != 0 && na <= kRoundWindows &&
@@ -973,7 +966,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     auto table_work = [&]() -> int {
         if (download) {
             if (C > 0)
-                RSH_HIP(copy_to_host(c, kDescTable,
+                RSH_HIP(copy_to_host(
                                      {rsh::CopyEnt{reinterpret_cast<const uint8_t*>(d_weak), c->h_weak.as<uint8_t>(),
                                                    (int64_t)C * 4},
                                       rsh::CopyEnt{d_strong, c->h_strong.as<uint8_t>(), (int64_t)C * dl}},
@@ -1254,17 +1247,16 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                     RSH_HIP(rsh::launch_chain_flags(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak,
                                                     d_strong, (uint32_t)snf, (uint32_t)dl, c->flags.as<uint8_t>(),
                                                     ss));
-                    if (snf > 0) RSH_HIP(hipMemcpyAsync(c->h_fl.p, c->flags.p, (size_t)snf, hipMemcpyDeviceToHost, ss));
+                    RSH_HIP(copy_to_host({rsh::CopyEnt{c->flags.as<uint8_t>(), c->h_fl.as<uint8_t>(), snf}}, ss));
                     RSH_HIP(hipEventRecord(c->ev_flags, ss));
-                    RSH_HIP(hipMemcpyAsync(c->h_aw.p, c->src_weak.p, (size_t)P * 4, hipMemcpyDeviceToHost, ss));
-                    if (dl > 0)
-                        RSH_HIP(hipMemcpyAsync(c->h_as.p, c->src_strong.p, (size_t)P * dl, hipMemcpyDeviceToHost, ss));
+                    RSH_HIP(copy_to_host({rsh::CopyEnt{c->src_weak.as<uint8_t>(), c->h_aw.as<uint8_t>(), P * 4},
+                                          rsh::CopyEnt{c->src_strong.as<uint8_t>(), c->h_as.as<uint8_t>(), P * dl}},
+                                         ss));
                     RSH_HIP(hipEventRecord(c->ev_spec, ss));
-                    RSH_HIP(hipMemcpyAsync(c->h_pw[pset].p, c->ph_weak[pset].p, (size_t)Q * 4, hipMemcpyDeviceToHost,
-                                           ss));
-                    if (dl > 0)
-                        RSH_HIP(hipMemcpyAsync(c->h_ps[pset].p, c->ph_strong[pset].p, (size_t)Q * dl,
-                                               hipMemcpyDeviceToHost, ss));
+                    RSH_HIP(copy_to_host({rsh::CopyEnt{c->ph_weak[pset].as<uint8_t>(), c->h_pw[pset].as<uint8_t>(), Q * 4},
+                                          rsh::CopyEnt{c->ph_strong[pset].as<uint8_t>(), c->h_ps[pset].as<uint8_t>(),
+                                                       Q * dl}},
+                                         ss));
                     RSH_HIP(hipEventRecord(c->ev_phase[pset], ss));
                     c->ph_set = pset;
                     k1_timed = true;     // (the event records around it)

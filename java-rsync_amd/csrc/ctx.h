@@ -162,10 +162,9 @@ struct rsh_ctx {
     PinnedBuf h_files;   // the scan's rsh::ScanFile (a batch of one for the probe / gather kernels)
     PinnedBuf h_stage;   // file ingest ring (ingest.cpp); never shared with the scan's buffers
     PinnedBuf h_rcv_ops[2];  // rsh_receiver_combine_batch: the gather ops of a pass, staged
-    PinnedBuf h_prep;        // the prep launch's sample list and outputs (scan_spec_queue)
+    PinnedBuf h_prep;        // the prep launch's outputs (scan_spec_queue)
     PinnedBuf h_stamps;      // the stamped launches' stamps, one 64-B line each
     PinnedBuf h_fgw, h_fjobs, h_fout;  // flush_probe: the chain's gather list, its job, its outputs
-    PinnedBuf h_desc;  // copy_to_host's descriptor slots (capi.cpp)
     uint64_t first_used = 0;    // probe result slots handed out (see HipBackend::first_hit)
     // device, uncached, 256 B: the speculation launch of generation g stops once abort_word[0] holds g;
     // a phase-shifted speculation polls abort_word[kPhaseWord] (its own 64-B line)
@@ -186,7 +185,7 @@ struct rsh_ctx {
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pw[0], &h_ps[0], &h_pw[1], &h_ps[1], &h_lead, &h_pos, &h_out, &h_iv,
                              &h_tiles, &h_keys, &h_first, &h_win, &h_ptiles, &h_psegs, &h_hit, &h_win0, &h_pend, &h_bucket, &h_files,
-                             &h_stage, &h_rcv_ops[0], &h_rcv_ops[1], &h_prep, &h_stamps, &h_fgw, &h_fjobs, &h_fout, &h_desc})
+                             &h_stage, &h_rcv_ops[0], &h_rcv_ops[1], &h_prep, &h_stamps, &h_fgw, &h_fjobs, &h_fout})
             b->release();
         if (abort_word) (void)hipFree(abort_word);
         if (ev_in) (void)hipEventDestroy(ev_in);

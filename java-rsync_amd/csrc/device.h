@@ -125,6 +125,9 @@ hipError_t launch_warm_io(hipStream_t s);
 // Completion without a marker packet: the launch's last workgroup to finish writes `gen` into *stamp (pinned host
 // memory, system-scope release after every workgroup's stores), which the host polls.  counter: device memory,
 // zero before the launch (the last workgroup zeroes it again).
+// counter: kStampLine * (1 + kStampGroups) device words, zero between launches (the launch counter, then the group
+// counters of device_io.hip stamp_arrive, a 64-B line each)
+constexpr uint32_t kStampGroups = 64, kStampLine = 16;
 struct Stamp {
     uint32_t* counter;
     int* stamp;
@@ -143,7 +146,9 @@ struct ScanPrep {
     int64_t n;
     uint32_t B;
     uint32_t nsamp, pieces;
-    const int64_t* wins;        // pinned host: the sampled window indices
+    // the sampled windows: i < nlead: window i; then window stride * (j0 + i - nlead) (capi.cpp scan_device's list)
+    uint32_t nlead;
+    int64_t stride, j0;
     const int32_t* table_weak;  // device: the received table's weak sums
     int32_t C;
     int32_t* out_t;             // pinned host: T(wins[i] B)
@@ -300,6 +305,13 @@ struct CopyEnt {
     int64_t len;
 };
 hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hipStream_t s, bool bg = false);
+// Up to four device ranges into pinned host memory, the ranges passed by value in the kernel's arguments (nothing
+// for the host to keep alive after the launch); any alignment of source and destination.
+struct CopyFew {
+    CopyEnt e[4];
+    uint32_t n;
+};
+hipError_t launch_copy_few(const CopyFew& f, hipStream_t s);
 // n bytes of device memory into pinned host memory (h_dst 16-byte aligned), by a kernel.
 hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s);
 // Byte ranges between arbitrary (unaligned) device addresses: one op per workgroup, 16-byte stores to

@@ -62,10 +62,30 @@ hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, 
 // atomics here), then one thread per workgroup counts the workgroup done with a device atomic; the workgroup that
 // completes the count -- its reads of the others' results are device atomics too -- releases at system scope once and
 // writes the stamp, which the host polls before it reads what the launch wrote to host memory.
+//
+// The count is two-level: device atomics on one address serialise at the memory side (~20 ns each here: a prep launch
+// of 2080 workgroups took 43 us, the chain flags' 512 took 10.7 us -- r5y headline trace), so workgroup b counts on
+// group counter b % kStampGroups (64-B lines of their own), and the last of each group counts on the launch counter.
+// Group g has ceil((blocks - g) / kStampGroups) members; the group's last resets its counter.
 __device__ __forceinline__ bool stamp_arrive(const Stamp& st, bool* sh_last) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) *sh_last = atomicAdd(st.counter, 1u) == gridDim.x * gridDim.y - 1;
+    if (threadIdx.x == 0) {
+        const uint32_t nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
+        bool last;
+        if (nb <= kStampGroups) {
+            last = atomicAdd(st.counter, 1u) == nb - 1;
+        } else {
+            const uint32_t g = b % kStampGroups, members = (nb - g + kStampGroups - 1) / kStampGroups;
+            uint32_t* gc = st.counter + kStampLine * (1 + g);
+            last = false;
+            if (atomicAdd(gc, 1u) == members - 1) {
+                atomicExch(gc, 0u);
+                last = atomicAdd(st.counter, 1u) == kStampGroups - 1;
+            }
+        }
+        *sh_last = last;
+    }
     __syncthreads();
     return *sh_last;
 }
@@ -102,6 +122,10 @@ hipError_t launch_chain_flags_stamped(const int32_t* d_wsrc, const uint8_t* d_ss
     return hipGetLastError();
 }
 
+__device__ __forceinline__ int64_t prep_window(const ScanPrep& P, uint32_t i) {
+    return i < P.nlead ? (int64_t)i : P.stride * (P.j0 + (int64_t)(i - P.nlead));
+}
+
 // blockIdx.x < nsamp * pieces: piece (blockIdx.x % pieces) of sample window blockIdx.x / pieces; the blocks past them
 // copy window 0 to the host, 4 KiB each.
 __global__ __launch_bounds__(256) void scan_prep_kernel(ScanPrep P) {
@@ -110,7 +134,7 @@ __global__ __launch_bounds__(256) void scan_prep_kernel(ScanPrep P) {
     const uint32_t b = blockIdx.x, nsum = P.nsamp * P.pieces;
     if (b < nsum) {
         const uint32_t i = b / P.pieces, q = b % P.pieces;
-        const int64_t p = P.wins[i] * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
+        const int64_t p = prep_window(P, i) * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
         const int64_t plen = ((w + P.pieces - 1) / P.pieces + 15) & ~(int64_t)15;
         const int64_t lo = p + (int64_t)q * plen, hi = lo + plen < p + w ? lo + plen : p + w;
         int32_t v[2] = {0, 0};
@@ -126,7 +150,7 @@ __global__ __launch_bounds__(256) void scan_prep_kernel(ScanPrep P) {
     }
     if (!stamp_arrive(P.st, &last)) return;
     for (uint32_t i = threadIdx.x; i < P.nsamp; i += blockDim.x) {
-        const int64_t k = P.wins[i], p = k * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
+        const int64_t k = prep_window(P, i), p = k * (int64_t)P.B, w = P.n - p < (int64_t)P.B ? P.n - p : (int64_t)P.B;
         const uint32_t S1 = (uint32_t)atomicExch(&P.scratch[2 * i], 0);
         const uint32_t U = (uint32_t)atomicExch(&P.scratch[2 * i + 1], 0);
         const uint32_t S2 = (uint32_t)w * S1 - U;
@@ -155,6 +179,39 @@ hipError_t launch_copy_many(const CopyEnt* ents, uint32_t n, int64_t max_len, hi
     if (n == 0 || max_len <= 0) return hipSuccess;
     const int64_t blocks = bg ? 1 : std::min<int64_t>((max_len + 16 * 256 - 1) / (16 * 256), 64);
     hipLaunchKernelGGL(copy_many_kernel, dim3((uint32_t)blocks, n), dim3(256), 0, s, ents, bg ? 0 : 1);
+    return hipGetLastError();
+}
+
+// Destination bytes before the first 16-byte boundary are copied one per thread; the rest as copy_piece pieces,
+// with 16-byte loads when the source is then 16-byte aligned as well (a uniform branch per range).
+__global__ __launch_bounds__(256) void copy_few_kernel(CopyFew f) {
+    __builtin_amdgcn_s_setprio(3);
+    if (blockIdx.y >= f.n) return;
+    const CopyEnt e = f.e[blockIdx.y];
+    const int64_t head = min(e.len, (int64_t)((16 - ((uintptr_t)e.dst & 15)) & 15));
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, T = (int64_t)gridDim.x * blockDim.x;
+    if (t < head) e.dst[t] = e.src[t];
+    const uint8_t* src = e.src + head;
+    uint8_t* dst = e.dst + head;
+    const int64_t n = e.len - head;
+    if (((uintptr_t)src & 15) == 0) {
+        for (int64_t o = 16 * t; o < n; o += 16 * T) {
+            if (o + 16 <= n)
+                *reinterpret_cast<uint4*>(dst + o) = *reinterpret_cast<const uint4*>(src + o);
+            else
+                for (int64_t i = o; i < n; ++i) dst[i] = src[i];
+        }
+    } else {
+        for (int64_t o = 16 * t; o < n; o += 16 * T) copy_piece(src, dst, n, o);
+    }
+}
+
+hipError_t launch_copy_few(const CopyFew& f, hipStream_t s) {
+    int64_t mx = 0;
+    for (uint32_t i = 0; i < f.n; ++i) mx = std::max(mx, f.e[i].len);
+    if (f.n == 0 || mx <= 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((mx + 16 * 256 - 1) / (16 * 256), 64);
+    hipLaunchKernelGGL(copy_few_kernel, dim3((uint32_t)blocks, f.n), dim3(256), 0, s, f);
     return hipGetLastError();
 }
 

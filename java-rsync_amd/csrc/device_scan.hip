@@ -117,11 +117,20 @@ __device__ __forceinline__ void probe_check16(const ScanFile& F, const ProbeTabl
                                               const uint32_t (&key)[16], uint32_t valid, int64_t base) {
     uint32_t m = 0;
     if (nsmall > 0) {
+        // one compare per key and position into a lane mask (the scalar unit ORs them); which positions only when
+        // some lane matched (rare: a stale digest's keys over a file's rest)
+        bool any = false;
         for (int j = 0; j < nsmall; ++j) {
             const uint32_t kj = F.small[j];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) m |= (uint32_t)(key[i] == kj) << i;
+            for (int i = 0; i < 16; ++i) any |= key[i] == kj;
         }
+        if (__builtin_expect(any, 0))
+            for (int j = 0; j < nsmall; ++j) {
+                const uint32_t kj = F.small[j];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) m |= (uint32_t)(key[i] == kj) << i;
+            }
     } else {
         unsigned long long sl[16];
 #pragma unroll
@@ -510,7 +519,9 @@ __global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(4
             const uint32_t s1 = P1e - (uint32_t)pre[0];
             const uint32_t s2 = (uint32_t)(p0 + B - base) * s1 - (P2e - (uint32_t)pre[1]);
             const uint32_t ehi = I.e_hi + I.e_lo * (uint32_t)(clampB(p0) - clampB(I.anchor));
-            int32_t R = (int32_t)(((s1 + I.e_lo) & 0xFFFFu) | ((s2 + ehi) << 16));
+            // the rolling value's halves kept apart (each exact mod 2^16: the Java subtract-then-add of
+            // Rolling.java:25-60 in two adds each, as the chain walk's tiles), packed into the key per position
+            uint32_t u1 = (s1 + I.e_lo) & 0xFFFFu, u2 = (s2 + ehi) & 0xFFFFu;
 #pragma unroll 1
             for (int grp = 0; grp < PROBE_LONG_PPL / 16; ++grp) {  // 16 positions at a time (bytes re-read: L1)
                 uint32_t wa[4], wb[4];
@@ -519,8 +530,10 @@ __global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(4
                 uint32_t key[16];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {  // full windows throughout: w = B, the add always follows
-                    key[i] = (uint32_t)R;
-                    R = roll_add(roll_sub(R, (int32_t)B, sbyte_of(wa, i)), sbyte_of(wb, i));
+                    key[i] = __builtin_amdgcn_perm(u2, u1, 0x05040100u);  // (u1 & 0xFFFF) | (u2 << 16)
+                    const int32_t xo = sbyte_of(wa, i), xi = sbyte_of(wb, i);
+                    u1 += (uint32_t)(xi - xo);
+                    u2 += u1 - (uint32_t)__mul24((int)B, xo);
                 }
                 const uint32_t valid = probe_valid16(p0 + 16 * grp, I.a, I.b < q1 ? I.b : q1);
                 if (valid) probe_check16(F, table, nsmall, key, valid, p0 + 16 * grp);
@@ -528,7 +541,7 @@ __global__ __launch_bounds__(PROBE_THREADS) __attribute__((amdgpu_waves_per_eu(4
             if (t == PROBE_THREADS - 1) {  // R(p0 + 64) less E there: the next sub-segment's anchor T
                 const int64_t pn = p0 + PROBE_LONG_PPL;
                 const uint32_t en = I.e_hi + I.e_lo * (uint32_t)(clampB(pn) - clampB(I.anchor));
-                const uint32_t r = (uint32_t)R;
+                const uint32_t r = (u1 & 0xFFFFu) | (u2 << 16);
                 s_next = (int32_t)((((r & 0xFFFFu) - I.e_lo) & 0xFFFFu) | (((r >> 16) - en) << 16));
             }
         }
@@ -1709,8 +1722,8 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     bool any = false;
                     for (int64_t c = t; c < C; c += 2 * CHAIN_THREADS) {
                         const int64_t c2 = c + CHAIN_THREADS < C ? c + CHAIN_THREADS : c;
-                        any |= chain_digest_eq_reg(dg, F.table_strong + c * dl, dl) |
-                               chain_digest_eq_reg(dg, F.table_strong + c2 * dl, dl);
+                        any |= (int)chain_digest_eq_reg(dg, F.table_strong + c * dl, dl) |
+                               (int)chain_digest_eq_reg(dg, F.table_strong + c2 * dl, dl);
                     }
                     if (any) s_any = 1;
                 }
