@@ -43,7 +43,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 # production K1 instantiation (device.hip launch_block_sums_variant default); the committed PMC profile
 # for `traffic` is matched on this name so a stale profile of another kernel is never reported
 PROD_KERNEL = "block_sums_pipe_kernel<8, true, true, 0, false>"  # the Generator K1 (non-batched)
-BATCH_KERNEL = "block_sums_pipe_kernel<8, true, true, 0, true>"  # the Generator K1 over a segment
+BATCH_KERNEL = "block_sums_pipe_kernel<true>"  # the Generator K1 over a segment (the batched instantiation)
 KEY_SRC = 0x5EED5EED << 32
 KEY_EDIT = (0x5EED5EED << 32) | 0xED17
 # config 5 inputs = tests/fullsize_golden.py's: source key KEY ^ 5, edits KEY ^ 0xED17, inserted byte KEY ^ 0x1B
@@ -51,8 +51,8 @@ KEY_CASE = KEY_SRC ^ 5
 KEY_INS = KEY_SRC ^ 0x1B
 SHIFT_AT = 155 * 131072 + 4096  # the "config5_shift1" insert position
 WARMUP_MIN_MS = 250.0  # untimed warmup of at least this long (and at least --warmup steps)
-TRAFFIC_CSV = "r4/r4h_bench_fetch_size.csv"
-TRAFFIC_FILES_CSV = "r4/r4h_files_fetch_size.csv"
+TRAFFIC_CSV = "r5/r5m2_bench_fetch_size.csv"
+TRAFFIC_FILES_CSV = "r5/r5m2_files_fetch_size.csv"
 
 
 def parse():
