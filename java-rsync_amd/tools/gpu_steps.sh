@@ -10,7 +10,7 @@
 #   smoke        __graft_entry__.smoke()
 #   bench        the default bench line (config 5, with companions)
 #   files        the config-4 line, both basis forms (FILES_STEPS steps)
-#   files-trace  one traced config-4 step (VARIANT, default half): the chain walk's breakdown (scan_trace = 2)
+#   files-trace  one traced config-4 step (VARIANT, default half; FT_ARGS: more bench args): the chain walk's breakdown
 #   prof         rocprofv3 kernel trace + stats of the default line (the summary committed under profiles/)
 #   timeline     rocprofv3 kernel + copy timeline of the config-4 line (VARIANT; TL_ARGS: more bench args)
 #   hl           the config-5 headline alone (no companions, no config 4), 20 steps
@@ -18,8 +18,8 @@
 #   fetch        rocprofv3 --pmc FETCH_SIZE passes (counters only, kernel trace) of the default line and the config-4
 #                line: the HBM bytes per K1 launch that bench.py reports as roofline.traffic
 #   pmc-k1       one PMC pass over kbench: the production K1 against the same kernel without global loads
-#   pmc-walk     two PMC passes (SQ issue/wait/LDS counters) over one config-4 step (VARIANT): the chain walk's
-#                instruction mix and LDS bank conflicts
+#   pmc-walk     two PMC passes (SQ issue/wait/LDS counters) over one config-4 step (VARIANT; PMC_ARGS: more bench
+#                args): the chain walk's instruction mix and LDS bank conflicts
 #   kbench-k1    kbench: the K1 at B = 128 KiB and 8 KiB, the batched forms (1002, 1005)
 #   e2e          java-rsync_amd/tools/e2e.py at config 5 (16 GiB from host memory)
 #   kb-ab        kbench A/Bs of KB_VARIANTS (default: the production entries 1000 1001 1003) at the headline
@@ -87,7 +87,7 @@ for step in "$@"; do
                     --no-cpu-baseline --no-companions > "$O/files_$v.json" 2> "$O/files_$v.err"
             done ;;
         files-trace) run 300 python bench.py --workload files --variant "$VARIANT" --steps 1 --warmup 1 --no-cpu-baseline \
-            --no-companions --opt scan_trace=2 > "$O/files_${VARIANT}_trace.json" 2> "$O/files_${VARIANT}_trace.err" ;;
+            --no-companions --opt scan_trace=2 $FT_ARGS > "$O/files_${VARIANT}_trace.json" 2> "$O/files_${VARIANT}_trace.err" ;;
         prof) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run \
             --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline \
             > "$O/prof_bench.json" 2> "$O/prof_bench.err") || exit 1 ;;
@@ -112,10 +112,10 @@ for step in "$@"; do
             CB="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES"
             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $CA --kernel-trace -d "$O/pmc_walk_a" -o run \
                 --output-format csv -- python3 "$R/bench.py" --workload files --variant "$VARIANT" --steps 1 --warmup 1 \
-                --no-cpu-baseline --no-companions > "$O/pmc_walk_a.json" 2> "$O/pmc_walk_a.err") || exit 1
+                --no-cpu-baseline --no-companions $PMC_ARGS > "$O/pmc_walk_a.json" 2> "$O/pmc_walk_a.err") || exit 1
             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $CB --kernel-trace -d "$O/pmc_walk_b" -o run \
                 --output-format csv -- python3 "$R/bench.py" --workload files --variant "$VARIANT" --steps 1 --warmup 1 \
-                --no-cpu-baseline --no-companions > "$O/pmc_walk_b.json" 2> "$O/pmc_walk_b.err") || exit 1 ;;
+                --no-cpu-baseline --no-companions $PMC_ARGS > "$O/pmc_walk_b.json" 2> "$O/pmc_walk_b.err") || exit 1 ;;
         kbench-k1)
             run 120 "$K" 16384 131072 4 8 1000 > "$O/kbench_128k.log" 2>&1
             run 120 "$K" 16384 8192 3 8 1000 1002 1005 > "$O/kbench_8k.log" 2>&1 ;;
