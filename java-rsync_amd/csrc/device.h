@@ -399,6 +399,7 @@ struct ChainHelp {
     int64_t t_kset;            // wall-clock ticks spent building this file's key set in helpers (trace)
     int32_t whole;             // segments mapped whole, before the walk reached them (trace)
     int32_t nhelp;             // helpers currently on this file
+    int32_t help_tiles;        // tiles the walk searches before helpers join it (option chain_help_tiles)
 };
 constexpr int CHAIN_THREADS = 512;                      // 8 waves (2 per SIMD: 256 VGPRs each)
 constexpr int CHAIN_PPT = 32;                            // wide tiles: positions per lane (two halves of 16)
