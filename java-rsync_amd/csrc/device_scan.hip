@@ -1202,10 +1202,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     int64_t pf_s = -1;
     int32_t pf_pref = -1, pf_aw = 0, pf_tw = 0;
     uint8_t pf_flag = 0;
-    // ... and the map words of the tile a search from pf_s + 1 starts with (pf_q0 >= 0: loaded by that event)
-    int64_t pf_q0 = -1;
-    unsigned long long pf_wv = 0ull;
-    int32_t pf_awl = 0;
     rsh_event pend{0, 0, 0, 0, 0, 0};  // the event being built (lane 0 writes it when the next one starts)
     bool have = false;
     if (nev > 0) {  // phase 1: the last event stays open (a MATCH run may go on across the prefix's end)
@@ -1383,16 +1379,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     const int64_t pm = q0 + (int64_t)t * CHAIN_PPT;
                     const int64_t lo = a > pm ? a - pm : 0, hi = qlast - pm;
                     const bool need = lo <= 31 && hi >= lo;
-                    // (the words an event loaded for this tile, when this is that tile; a word without this launch's
-                    // generation is read again: a helper may have written it since)
-                    const bool pf_map = q0 == pf_q0;
-                    unsigned long long wv = pf_map ? pf_wv : 0ull;
-                    if (need && (uint32_t)(wv >> 32) != map_gen)
-                        wv = __hip_atomic_load(&F.hmap[pm >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    unsigned long long wv = 0ull;
+                    if (need) wv = __hip_atomic_load(&F.hmap[pm >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     // beside it, the speculation's sum of an aligned window in the lane's range: a hit there needs
                     // no second round trip for its key
                     const bool al_lane = need && pm % B == 0;  // (pm <= qlast < na B)
-                    const int32_t awl = !al_lane ? 0 : pf_map ? pf_awl : F.aw[pm / B];
+                    const int32_t awl = al_lane ? F.aw[pm / B] : 0;
                     if (t == 0) s_hit = 0x7FFFFFFF;
                     if (__syncthreads_and(!need || (uint32_t)(wv >> 32) == map_gen)) {
                         if (need) {
@@ -1633,15 +1625,6 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             pf_flag = kn < nflags ? F.flags[kn] : (uint8_t)0;
             pf_aw = kn < na ? F.aw[kn] : 0;
             pf_tw = (kn < C && kn < na) ? F.table_weak[kn] : 0;
-            // should window kn not carry its chunk's sums either (an edited block after an unedited one), the walk
-            // searches from p + B + 1: that tile's map words (lane t's word and, for a lane on a block start, the
-            // speculation's sum there) come with this event's loads instead of a round trip of the search's own
-            if (map_gen != 0u) {
-                pf_q0 = (p + B + 1) & ~(int64_t)(CHAIN_PPT - 1);
-                const int64_t pm = pf_q0 + (int64_t)t * CHAIN_PPT;
-                pf_wv = pm < F.hend ? __hip_atomic_load(&F.hmap[pm >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-                pf_awl = (pm % B == 0 && pm / B < na) ? F.aw[pm / B] : 0;
-            }
         }
         if (t < 64) {
             // every chunk with this key lies on the probe path before the first empty slot: wave 0 reads 64 slots of
