@@ -85,7 +85,7 @@ inline constexpr OptInfo kOpts[OPT_COUNT] = {
     {"scan_defer_us", 500, true},     {"scan_spec_queue", 1, true},  {"scan_flags_host", 1, true},
     {"scan_prep_pieces", 0, true},    {"time_spec", 0, true},        {"batch_spec", -1, true},
     {"batch_spin_us", 200, true},     {"batch_readahead", 0, true},  {"batch_prep_all", 0, true},
-    {"batch_chain_overlap", 0, true}, {"batch_skip_rest", 1, true},  {"chain_help_tiles", 4, true},
+    {"batch_chain_overlap", 0, true}, {"batch_skip_rest", 1, true},  {"chain_help_tiles", 1, true},
 };
 
 #ifdef RSH_DIAG
