@@ -12,7 +12,7 @@
  *    tools through RSH_LIB); the product library answers RSH_E_INVAL and runs their defaults: scan_diag,
  *    scan_phase, scan_phase_guess, scan_preprobe, scan_sample, scan_spec_order, scan_early, scan_wait,
  *    scan_defer_steps, scan_defer_us, scan_spec_queue, scan_flags_host, scan_prep_pieces, time_spec, batch_spec,
- *    batch_spin_us, batch_readahead, batch_prep_all, batch_chain_overlap, batch_skip_rest.
+ *    batch_spin_us, batch_readahead, batch_prep_all, batch_chain_overlap, batch_skip_rest, chain_help_tiles.
  */
 #ifndef RSYNC_HIP_DEBUG_H
 #define RSYNC_HIP_DEBUG_H

@@ -1369,7 +1369,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                               two_phase ? S->file_abort + f : nullptr, ce + (int64_t)f * kChainEvents, kChainEvents,
                               seed_word(seed), co + f,
                               mw > 0 ? S->chain_map.as<unsigned long long>() + map_off[(size_t)f] : nullptr, hend};
-            if (chh) chh[f] = ChainHelp{(int32_t)((hend + CHAIN_MAP_SEG - 1) / CHAIN_MAP_SEG), 0, 1, 0, 0, 0, 0, 0, INT64_MAX, 0, 0, 0};
+            if (chh) chh[f] = ChainHelp{(int32_t)((hend + CHAIN_MAP_SEG - 1) / CHAIN_MAP_SEG), 0, 1, 0, 0, 0, 0, 0, INT64_MAX, 0, 0, 0,
+                                        (int32_t)opt(OPT_CHAIN_HELP_TILES)};
         }
         const uint32_t n_help = !map_on ? 0u
                                 : helpers_opt > 0 ? (uint32_t)helpers_opt

@@ -391,7 +391,7 @@ struct ChainHelp {
     int32_t nseg;    // map segments of CHAIN_MAP_SEG positions over [0, hend) (0: not mapped)
     int32_t claim;   // next segment a helper takes (atomic)
     int32_t live;    // 1 while the file's walk runs (the walk clears it)
-    int32_t tiles;   // tiles the walk has searched so far (helpers join files that searched at least twice)
+    int32_t tiles;   // tiles the walk has searched so far (helpers join files that searched help_tiles)
     int64_t pos;     // the walk's current search start (helpers skip segments behind it)
     int32_t mapped;  // segments mapped (trace)
     int32_t joins;   // helpers that built this file's key set (trace)
@@ -399,6 +399,8 @@ struct ChainHelp {
     int64_t t_kset;            // wall-clock ticks spent building this file's key set in helpers (trace)
     int32_t whole;             // segments mapped whole, before the walk reached them (trace)
     int32_t nhelp;             // helpers currently on this file
+    int32_t help_tiles;        // tiles the walk searches before helpers join it (A/B switch chain_help_tiles: 1; 4 until
+                               // round 5, 4.625 against 4.57 ms for config 4 half, r5m4)
 };
 constexpr int CHAIN_THREADS = 512;                      // 8 waves (2 per SIMD: 256 VGPRs each)
 constexpr int CHAIN_PPT = 32;                            // wide tiles: positions per lane (two halves of 16)

@@ -1003,9 +1003,8 @@ __device__ void chain_map_tile(const ChainFile& F, int64_t q0, uint32_t gen, con
     __syncthreads();  // (s_seg and sh: the next tile)
 }
 
-constexpr int CHAIN_HELP_TILES = 4;   // a walk gets helpers once it has searched this many tiles
 constexpr int CHAIN_HELP_LEAD = 64;   // a helper stays with its file while the map leads the walk by fewer segments
-// A helper workgroup: while some walk that has searched CHAIN_HELP_TILES tiles is still running, take the next
+// A helper workgroup: while some walk that has searched ChainHelp::help_tiles tiles is still running, take the next
 // unmapped segment of the one whose map leads it least (its own current file while the lead is short: the key set is
 // built per file) -- never the segment the walk is in, which it will finish first -- and map it tile by tile,
 // stopping when the walk ends or has passed the tile.  While walks are running that have not searched that far yet it
@@ -1036,7 +1035,7 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
             const int64_t pos = chain_ld64(&h->pos);
             if (live == 0 || claim >= nseg) continue;
             *s_live = 1;  // a walk that may still search: wait for it rather than leave
-            if (tiles < CHAIN_HELP_TILES) continue;
+            if (tiles < h->help_tiles) continue;
             // the most urgent files first -- the map's frontier least far ahead of the walk, in four levels -- then
             // the fewest helpers, then a hash that spreads the helpers; the current file while the map leads its
             // walk by fewer than CHAIN_HELP_LEAD segments (its key set is built)
@@ -1055,7 +1054,7 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
         __syncthreads();
         if (best == 0ull) {
             if (!any_live) break;  // every mappable walk has ended: nothing will come
-            __builtin_amdgcn_s_sleep(64);  // walks still short of CHAIN_HELP_TILES tiles: look again shortly
+            __builtin_amdgcn_s_sleep(64);  // walks still short of their help_tiles: look again shortly
             continue;
         }
         const int f = (int)(best & 0xFFFFFull);

@@ -62,6 +62,7 @@ enum Opt : int {
     OPT_BATCH_PREP_ALL,    // 1: the batched speculation after all the table work (full-width launches)
     OPT_BATCH_CHAIN_OVERLAP, // 1: the rest of the speculation starts beside the prefix walk (0: after it)
     OPT_BATCH_SKIP_REST,   // 1: the rest of a two-phase speculation only if some phase-0 walk reached the prefix's end
+    OPT_CHAIN_HELP_TILES,  // tiles a phase-0 walk searches before helpers map ahead of it
     OPT_COUNT
 };
 
@@ -84,7 +85,7 @@ inline constexpr OptInfo kOpts[OPT_COUNT] = {
     {"scan_defer_us", 500, true},     {"scan_spec_queue", 1, true},  {"scan_flags_host", 1, true},
     {"scan_prep_pieces", 0, true},    {"time_spec", 0, true},        {"batch_spec", -1, true},
     {"batch_spin_us", 200, true},     {"batch_readahead", 0, true},  {"batch_prep_all", 0, true},
-    {"batch_chain_overlap", 0, true}, {"batch_skip_rest", 1, true},
+    {"batch_chain_overlap", 0, true}, {"batch_skip_rest", 1, true},  {"chain_help_tiles", 1, true},
 };
 
 #ifdef RSH_DIAG
