@@ -42,7 +42,7 @@ import shard  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 # production K1 instantiation (device.hip launch_block_sums_variant default); the committed PMC profile
 # for `traffic` is matched on this name so a stale profile of another kernel is never reported
-PROD_KERNEL = "block_sums_pipe_kernel<8, true, true, 0, false>"  # the Generator K1 (non-batched)
+PROD_KERNEL = "block_sums_pipe_kernel<false>"  # the Generator K1 (non-batched)
 BATCH_KERNEL = "block_sums_pipe_kernel<true>"  # the Generator K1 over a segment (the batched instantiation)
 KEY_SRC = 0x5EED5EED << 32
 KEY_EDIT = (0x5EED5EED << 32) | 0xED17

@@ -121,3 +121,18 @@ def test_rank_device_plan(monkeypatch):
                                                               (0, "gloo", True), (1, "gloo", True)]
     with pytest.raises(RuntimeError):
         shard.rank_device(0, 1, 0)
+
+
+def test_bench_traffic_profiles_name_the_kernels():
+    """bench.py's roofline.traffic comes from committed FETCH_SIZE passes (profiles/, rocprofv3 --pmc): the kernel names
+    it looks for must be the ones those passes recorded, for both lines (a renamed instantiation once left the config-4
+    line's traffic null)."""
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    n = 16 << 30
+    for csv_rel, kernel in ((b.TRAFFIC_CSV, b.PROD_KERNEL), (b.TRAFFIC_FILES_CSV, b.BATCH_KERNEL)):
+        t = b.pmc_traffic(os.path.join(root, "profiles", csv_rel), kernel, n)
+        assert t is not None and 0.95 * n <= t <= 1.1 * n, (csv_rel, kernel, t)
