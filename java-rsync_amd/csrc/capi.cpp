@@ -120,6 +120,7 @@ class HipBackend : public rsh::ScanBackend {
         const int64_t hi = std::min(n_, tile_lo + tile_T + tile_H);
         return std::max<int64_t>(1, std::min<int64_t>(max_batch(), (hi - f - B_ - 1) / (10 * B_)));
     }
+    bool one_round(int64_t a, int64_t b) override { return !tiled || a / tile_T == b / tile_T; }
 
     // ---- tiled source (rsh_match_scan_tiled): HBM holds [tile_lo, tile_lo + tile_T + tile_H) of the
     // source, tile_T a multiple of B and tile_H >= 16 B.  Every device question starts at or after the

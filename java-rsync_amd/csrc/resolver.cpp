@@ -474,9 +474,10 @@ bool resolve_run(int64_t n, ChunkTable& table, ScanBackend& be, ResolveState* st
                 uint32_t el, eh;
                 E_at(a, &el, &eh);
                 const ProbeInterval one{a, stop + 1, a, el, eh};
-                if (md5c_valid && f <= last) {
+                if (md5c_valid && f <= last && be.one_round(a, f)) {
                     // A stale digest's few keys: an event before the flush point is unlikely, so the batched flush
-                    // chain after it (below) is probed in the same round trip, this interval first.
+                    // chain after it (below) is probed in the same round trip, this interval first (when the backend
+                    // can answer both from one tile; else [a, stop] alone first, then the chain below).
                     const FlushChain q = flush_chain_at(f, keys);
                     state->clear_from = state->clear_to = -1;
                     if (flush_round(&one, 1, q, keys, stop)) continue;  // no event in [a, stop]: flushes committed

@@ -155,6 +155,13 @@ class ScanBackend {
         (void)f;
         return max_batch();
     }
+    // Whether one device round may read from positions a through b (a <= b): a tiled backend answers each round
+    // from the tile holding its first position, and tiles only advance, so a probe at a and a flush chain at b go
+    // out together only when both lie in one tile; otherwise the resolver asks in two rounds, in order.
+    virtual bool one_round(int64_t a, int64_t b) {
+        (void)a, (void)b;
+        return true;
+    }
     // Source bytes the backend's device work read for this scan (rsh_scan_stats::device_bytes).
     int64_t bytes_read = 0;
     static int64_t probe_bytes(const ProbeInterval* iv, int64_t count, int64_t B) {

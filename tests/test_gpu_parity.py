@@ -315,6 +315,48 @@ def test_sender_tiled_matches_oracle(ctx, seed_i):
             assert st["head_steps"] >= 2  # tile loads
 
 
+def _weak_preserving_tweak(buf, lo, hi, rng):
+    """+1, -2, +1 on three consecutive signed bytes in [lo, hi): both rolling sums unchanged (Rolling.java:31-46),
+    the digest changed -- the stale cached digest of Sender.java:1259-1263 (quirk B)."""
+    for _ in range(1000):
+        i = rng.randrange(lo, hi - 3)
+        x = [((v + 128) % 256) - 128 for v in buf[i:i + 3]]
+        if x[0] <= 126 and x[1] >= -126 and x[2] <= 126:
+            buf[i], buf[i + 1], buf[i + 2] = (x[0] + 1) & 255, (x[1] - 2) & 255, (x[2] + 1) & 255
+            return
+    raise AssertionError("no tweakable bytes")
+
+
+@pytest.mark.parametrize("seed_i", range(4))
+def test_sender_tiled_stale_digest_chain(ctx, seed_i):
+    """a stale digest (a weak hit whose digest differs, dl = 1 so that other chunks carry it
+    and the stale state keeps probing) followed by a long literal run whose flush points straddle tile
+    boundaries.  The stale-digest branch probes [a, stop] and the batched flush chain from f in one round only
+    when a and f lie in one tile; otherwise in two rounds, in order.  Tiles only advance (loads <= tiles), and
+    the events equal the oracle's."""
+    rng = random.Random(5500 + seed_i)
+    B, dl = 512, 1
+    for i in range(6):
+        nb = rng.randrange(120 * B, 200 * B)
+        key = rng.randrange(1 << 62)
+        basis = O.splitmix(nb, key).tobytes()
+        k = rng.randrange(3, 20)
+        src = bytearray(basis)
+        _weak_preserving_tweak(src, k * B, (k + 1) * B, rng)
+        cut = (k + 1) * B + rng.randrange(B)
+        src = bytes(src[:cut]) + O.splitmix(rng.randrange(30 * B, 70 * B), key ^ 7).tobytes() + bytes(src[cut:])
+        h = O.header(B, dl, len(basis))
+        w, s = O.generator(basis, h, SEED)
+        oev, ofm, olit, omat, _ = O.sender(src, h, w, s, SEED)
+        rh = R.Header(**h.as_dict())
+        tile = rng.choice([16 * B, 17 * B + 100, 19 * B, 23 * B])
+        ev, fm, lit, mat, st = ctx.match_scan_tiled(src, rh, w, s, SEED, tile_bytes=tile)
+        assert R.events_as_tuples(ev, B) == [tuple(e) for e in oev], (i, tile)
+        assert (fm, lit, mat) == (ofm, olit, omat)
+        T = max(16 * B, tile // B * B)
+        assert st["head_steps"] <= -(-len(src) // T), (st["head_steps"], len(src), T)  # tiles only advance
+
+
 def test_contexts_per_thread_on_every_device():
     """The JNI binding's design (NativeChecksum.forThread: one context per calling thread, device = thread id
     mod rsync.hip.devices; RsyncClient.java:431 runs Generator and Sender on separate threads): 2 threads per
