@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RSH_ABI_VERSION 4
+#define RSH_ABI_VERSION 5
 
 /* Status codes (the JNI shim maps them onto the reference's exception types). */
 #define RSH_OK 0
@@ -343,6 +343,28 @@ typedef struct {
     rsh_combine_result res;   /* out */
 } rsh_combine_job;
 int rsh_receiver_combine_batch(rsh_ctx* ctx, rsh_combine_job* jobs, int32_t njobs);
+
+/* ---- a segment over several GPUs (ABI 5) ----
+ * north_star: "files shard embarrassingly across the 8 GPUs of one node".  In the reference one thread walks every
+ * file of a transfer: the Generator sums a segment's files in turn (Generator.java:558-614,806-860), one Sender thread
+ * answers each (Sender.sendFiles, Sender.java:978-1170) and one Receiver thread rebuilds each (Receiver.java:1145-1263).
+ * These forms take the calling thread's contexts ctxs[0 .. nctx) -- distinct contexts, typically one per GPU of the
+ * node (several on one GPU also work: they run side by side there) -- split the segment's files over them by
+ * rsh_shard_files, and run each context's share as the single-context call above (rsh_block_sums_batch,
+ * rsh_match_scan_batch, rsh_receiver_combine_batch) on a host thread of its own, the process's cores shared evenly
+ * among those threads.  No data moves between GPUs.  Every job's outputs and status are exactly what the
+ * single-context call gives that file; a failure on one context marks only the files that context had not finished.
+ * Returns RSH_OK, or the first failing job's status in file order (RSH_E_INVAL for a null or repeated context).
+ * stats: summed over the contexts.  nctx == 1 is the single-context call. */
+int rsh_block_sums_batch_multi(rsh_ctx* const* ctxs, int32_t nctx, rsh_block_batch_job* jobs, int32_t njobs,
+                               const uint8_t seed[4]);
+int rsh_match_scan_batch_multi(rsh_ctx* const* ctxs, int32_t nctx, rsh_scan_batch_job* jobs, int32_t njobs,
+                               const uint8_t seed[4], rsh_scan_stats* stats);
+/* (the Receiver's files are split by max(tokens_len, replica bytes): about the bytes each rebuilds) */
+int rsh_receiver_combine_batch_multi(rsh_ctx* const* ctxs, int32_t nctx, rsh_combine_job* jobs, int32_t njobs);
+/* The split (pure host): part_out[f] = the part (context) file f goes to.  Longest first by bytes (equal sizes in
+ * file order), each file to the part with the fewest bytes so far (ties to the lower part): shard.py's rank rule. */
+int rsh_shard_files(const int64_t* bytes, int32_t nfiles, int32_t nparts, int32_t* part_out);
 
 /* ---- device buffers for the *_device entry points (callers without their own allocator, e.g. JNI) ---- */
 int rsh_dev_alloc(rsh_ctx* ctx, int64_t bytes, void** out);

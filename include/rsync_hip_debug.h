@@ -48,6 +48,13 @@ int rsh_debug_streams_busy(rsh_ctx* ctx, int32_t* mask);
 int rsh_debug_k1_clock(rsh_ctx* ctx, const void* d_data, int64_t n, int32_t block_length, int32_t reps,
                        double* clock_ghz);
 
+/* The multi-context segment driver (rsh_*_batch_multi: split, one member call per part, merge) with a stand-in member
+ * call and no device: part p's call records per job its part (part_out) and its position among the part's files
+ * (order_out); part fail_part (-1: none) finishes its first file and fails the rest with RSH_E_DEVICE.  status_out:
+ * every job's status after the merge.  Returns the driver's status. */
+int rsh_debug_multi_selftest(const int64_t* bytes, int32_t njobs, int32_t nparts, int32_t fail_part, int32_t* part_out,
+                             int32_t* order_out, int32_t* status_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1609,7 +1609,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         for (FileScan& fs : files) fs.be.head = false;
     }
 
-    const int ncpu = WorkerCap::value() > 0 ? std::min(host_cores(), WorkerCap::value()) : host_cores();
+    const int ncpu = WorkerCap::value() > 0 ? std::min(call_cores(), WorkerCap::value()) : call_cores();
     // spinning waiters: one core stays free for the coordinator
     const int32_t ncores = (spin_us() > 0 && ncpu > 2) ? ncpu - 1 : ncpu;
     // only the files still live get a worker: after the chain walks (or a leading speculation) most files are
@@ -1847,7 +1847,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             memcpy(j.ev, fs.dev_ev ? fs.dev_ev : fs.res.ev.data(), (size_t)j.n_ev * sizeof(rsh_event));
         }
     };
-    const int nct = copy_bytes > (1 << 20) ? std::min<int>(8, std::max(1, host_cores())) : 1;
+    const int nct = copy_bytes > (1 << 20) ? std::min<int>(8, std::max(1, call_cores())) : 1;
     if (nct > 1 && copy_files.size() > 1) {
         std::vector<std::thread> ct;
         const size_t per = (copy_files.size() + (size_t)nct - 1) / (size_t)nct;

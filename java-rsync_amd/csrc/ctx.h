@@ -23,6 +23,24 @@ struct BatchState;  // batch.cpp
 void destroy_batch_state(BatchState* b);
 // batch.cpp: the cores this process may use (affinity mask, cgroup quota; option host_cores overrides)
 int host_cores();
+// The cores one call on this thread may use: host_cores(), or this thread's share of them while a multi-context
+// segment call (multi.cpp) runs one member call per context side by side -- each member's MD5 pool, resolver workers
+// and copy threads then stay within its share, and the members together within the process's cores.
+struct CoreShare {
+    static int& value() {
+        static thread_local int v = 0;
+        return v;
+    }
+    int saved;
+    explicit CoreShare(int cores) : saved(value()) { value() = cores; }
+    ~CoreShare() { value() = saved; }
+};
+inline int call_cores() { return CoreShare::value() > 0 ? std::min(host_cores(), CoreShare::value()) : host_cores(); }
+// multi.cpp: whether option fault_inject's bits 0 / 1 apply on this thread (bit 2 limits them to member 1 of a
+// multi-context call; tests only)
+bool fault_here();
+// segment.cpp: one scan's (or pass's) stats added into a call's
+void add_scan_stats(rsh_scan_stats* to, const rsh_scan_stats& s);
 // The batched scan's resolver threads on this thread's calls: at most this many cores (0: host_cores()).  A segment
 // call that digests its files on the other cores meanwhile (segment.cpp) sets it, so that the spinning resolver
 // workers and the MD5 pool together stay within the cores (a cgroup quota throttles the whole process past it).

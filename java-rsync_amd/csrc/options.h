@@ -40,7 +40,8 @@ enum Opt : int {
     OPT_CHAIN_HELPERS,     // phase-0 walk: extra workgroups mapping searching files' prefixes (-1: CUs - files; 0: no map)
     OPT_CHAIN_MAP_BYTES,   // ... the map's HBM budget (bytes; above it the walks search tile by tile)
     OPT_TIME_GEN,          // 1: rsh_block_sums_device's K1 records timing events (rsh_debug_kernel_ms)
-    OPT_FAULT_INJECT,      // tests only: bit 0 a segment / Receiver pass's HBM allocation fails, bit 1 a segment's copies fail
+    OPT_FAULT_INJECT,      // tests only: bit 0 a segment / Receiver pass's HBM allocation fails, bit 1 a segment's copies fail,
+                           // bit 2 bits 0 / 1 only on member 1 of a multi-context call (multi.cpp)
     // ---- A/B switches (the diagnostics build reads them; the product build uses the defaults) ----
     OPT_SCAN_DIAG,         // bit 0: no head mode; bit 1: speculation without an abort word; bit 2: launch at once
     OPT_SCAN_PHASE,        // 1: phase-shifted speculations (chains at kB + delta)

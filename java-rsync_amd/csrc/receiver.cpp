@@ -365,7 +365,7 @@ int combine_passes(rsh_ctx* c, rsh_combine_job* jobs, std::vector<RFile>& files,
             files[f].tgt_at = off;
             off += alignr(files[f].plan.target_len);
         }
-        if ((opt(OPT_FAULT_INJECT) & 1) || c->rcv[set].ensure((size_t)off + kAlignR) != hipSuccess) {
+        if (((opt(OPT_FAULT_INJECT) & 1) && fault_here()) || c->rcv[set].ensure((size_t)off + kAlignR) != hipSuccess) {
             snprintf(g_last_err, sizeof(g_last_err), "receiver pass of %lld bytes: device memory (receiver.cpp)",
                      (long long)off);
             rc = RSH_E_NOMEM;
@@ -561,7 +561,7 @@ int rsh_receiver_combine_batch(rsh_ctx* ctx, rsh_combine_job* jobs, int32_t njob
         md5_in.push_back(Md5File{md5_pieces[k].data(), (int32_t)md5_pieces[k].size()});
     std::vector<uint8_t> md5_out(md5_in.size() * 16 + 16);
     // (host) the digests on the cores beside the device passes: one serial chain per file, up to 16 per core
-    const int md5_threads = std::max(1, host_cores() - (files.empty() ? 0 : 2));
+    const int md5_threads = std::max(1, call_cores() - (files.empty() ? 0 : 2));
     std::thread md5_thread([&] {
         md5_files(md5_in.data(), (int32_t)md5_in.size(), reinterpret_cast<uint8_t(*)[16]>(md5_out.data()), md5_threads,
                   (int)opt(OPT_MD5_WIDTH));

@@ -56,8 +56,10 @@ int64_t budget() { return std::max<int64_t>(kAlign, rsh::opt(rsh::OPT_SEGMENT_BY
 
 // Fault injection (option fault_inject, tests only): the failure paths of a segment call must leave every
 // unfinished file with a failing status.
-bool fail_alloc() { return (rsh::opt(rsh::OPT_FAULT_INJECT) & 1) != 0; }
-hipError_t fail_copy(hipError_t e) { return e == hipSuccess && (rsh::opt(rsh::OPT_FAULT_INJECT) & 2) ? hipErrorInvalidValue : e; }
+bool fail_alloc() { return (rsh::opt(rsh::OPT_FAULT_INJECT) & 1) != 0 && rsh::fault_here(); }
+hipError_t fail_copy(hipError_t e) {
+    return e == hipSuccess && (rsh::opt(rsh::OPT_FAULT_INJECT) & 2) && rsh::fault_here() ? hipErrorInvalidValue : e;
+}
 
 // Passes over the files `idx` (in order): consecutive runs whose aligned sizes fit the budget; a file larger
 // than the budget gets a pass of its own marked `alone`.
@@ -86,7 +88,9 @@ std::vector<Pass> plan_passes(const std::vector<int32_t>& idx, const std::vector
     return out;
 }
 
-void add_stats(rsh_scan_stats* to, const rsh_scan_stats& s) {
+}  // namespace
+
+void rsh::add_scan_stats(rsh_scan_stats* to, const rsh_scan_stats& s) {
     to->chain_matches += s.chain_matches;
     to->events += s.events;
     to->probe_launches += s.probe_launches;
@@ -104,6 +108,8 @@ void add_stats(rsh_scan_stats* to, const rsh_scan_stats& s) {
     to->phase_kernel_ms += s.phase_kernel_ms;
     to->phase_guesses += s.phase_guesses;
 }
+
+namespace {
 
 // rsh_block_sums_batch's device work: the passes over `run` (validated files with chunks); done[f] once file f's
 // sums are on the host.  Any early return is the call's status (the caller marks the unfinished files).
@@ -269,7 +275,7 @@ int rsh_match_scan_batch(rsh_ctx* ctx, rsh_scan_batch_job* jobs, int32_t njobs, 
     // kScanCores, the batched scan's coordinator and resolver workers those (after the chain walks a segment
     // leaves a file or two to the host resolvers); together they stay within the process's cores.
     constexpr int kScanCores = 3;
-    const int cores = rsh::host_cores();
+    const int cores = rsh::call_cores();
     const int md5_threads = std::max(1, cores - kScanCores);
     rsh::WorkerCap cap(std::max(1, cores - md5_threads));
     std::vector<rsh::Md5File> mf;
@@ -313,7 +319,7 @@ int rsh_match_scan_batch(rsh_ctx* ctx, rsh_scan_batch_job* jobs, int32_t njobs, 
             if (j.status == RSH_OK) {
                 j.literal = r.literal;
                 j.matched = r.matched;
-                if (stats) add_stats(stats, r.stats);
+                if (stats) rsh::add_scan_stats(stats, r.stats);
                 j.status = emit_events(ctx, r, j.ev, j.ev_cap, &j.n_ev);
             }
             done[(size_t)pass.files[0]] = 1;
@@ -372,7 +378,7 @@ int rsh_match_scan_batch(rsh_ctx* ctx, rsh_scan_batch_job* jobs, int32_t njobs, 
             j.matched = sj[k].matched;
             if (prc == RSH_OK || prc == RSH_E_NOSPACE) done[(size_t)pass.files[k]] = 1;
         }
-        if (stats) add_stats(stats, ps);
+        if (stats) rsh::add_scan_stats(stats, ps);
         if (prc != RSH_OK && prc != RSH_E_NOSPACE) rc = prc;
     }
     md5_thread.join();

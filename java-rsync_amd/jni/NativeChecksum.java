@@ -51,21 +51,29 @@ final class NativeChecksum implements AutoCloseable {
         }
     }
 
+    /** The node's GPUs this process uses (system property rsync.hip.devices: devices 0 .. n-1). */
+    static int devices() {
+        return Math.max(1, Integer.getInteger("rsync.hip.devices", 1));
+    }
+
     static NativeChecksum forThread() {
         NativeChecksum c = PER_THREAD.get();
         if (c == null) {
-            int devices = Math.max(1, Integer.getInteger("rsync.hip.devices", 1));
+            int devices = devices();
             c = new NativeChecksum(Integer.getInteger("rsync.hip.device",
-                    (int) (Thread.currentThread().getId() % devices)));
+                    (int) (Thread.currentThread().getId() % devices)), devices);
             PER_THREAD.set(c);
             LIVE.add(c);
         }
         return c;
     }
 
-    /** More live contexts than devices: some GPU holds two of them (trim() between segments, INTEGRATION.md). */
+    /**
+     * More than one live NativeChecksum: each holds a context on every GPU of the device set, so the GPUs hold
+     * several contexts each (trim() between segments, INTEGRATION.md).
+     */
     static boolean sharesDevice() {
-        return LIVE.size() > Math.max(1, Integer.getInteger("rsync.hip.devices", 1));
+        return LIVE.size() > 1;
     }
 
     /** Destroys the calling thread's context, if it has one (idempotent). */
@@ -77,13 +85,20 @@ final class NativeChecksum implements AutoCloseable {
         }
     }
 
+    // The thread's home context (single-file calls; device = thread id mod rsync.hip.devices, or rsync.hip.device)
+    // and its device set: one context per GPU of the set, created on the first segment call, over which the
+    // segment calls split their files (rsh_*_batch_multi).  set[device] is ctx (set = {ctx} when the home device
+    // lies outside the set, rsync.hip.device >= rsync.hip.devices).
     private long ctx;
+    private final long[] set;
     // Held for every native call and by close(): a context is never destroyed under a running scan.  One
     // thread uses a context, so the lock is uncontended except against close() and the shutdown hook.
     private final ReentrantLock lock = new ReentrantLock();
 
-    private NativeChecksum(int device) {
+    private NativeChecksum(int device, int devices) {
         ctx = ctxCreate(device);
+        set = new long[device < devices ? devices : 1];
+        set[device < devices ? device : 0] = ctx;
     }
 
     @Override
@@ -97,6 +112,12 @@ final class NativeChecksum implements AutoCloseable {
     }
 
     private void closeLocked() {
+        for (int d = 0; d < set.length; d++) {
+            if (set[d] != 0 && set[d] != ctx) {
+                ctxDestroy(set[d]);
+            }
+            set[d] = 0;
+        }
         if (ctx != 0) {
             ctxDestroy(ctx);
             ctx = 0;
@@ -113,6 +134,11 @@ final class NativeChecksum implements AutoCloseable {
         lock.lock();
         try {
             ctxTrim(handle());
+            for (long c : set) {
+                if (c != 0 && c != ctx) {
+                    ctxTrim(c);
+                }
+            }
         } finally {
             lock.unlock();
         }
@@ -124,6 +150,17 @@ final class NativeChecksum implements AutoCloseable {
             throw new IllegalStateException("NativeChecksum context is closed");
         }
         return ctx;
+    }
+
+    /** The device set's live handles, creating the contexts not made yet; the lock is held. */
+    private long[] handles() {
+        handle();
+        for (int d = 0; d < set.length; d++) {
+            if (set[d] == 0) {
+                set[d] = ctxCreate(d);
+            }
+        }
+        return set;
     }
 
     /** Generator.java:886-895: weak[i] and strong[i*dl .. i*dl+dl) for every chunk of the basis. */
@@ -195,14 +232,19 @@ final class NativeChecksum implements AutoCloseable {
     /**
      * A segment's Generator pass in one call (Generator.itemizeSegment, Generator.java:558-614): basis[f] holds
      * file f's bytes in one or more direct buffers, headers[f] its 3-arg Checksum.Header; weak[f] / strong[f]
-     * receive its sums.  One device launch covers every file of the segment.
+     * receive its sums.  One device launch per GPU covers every file of the segment: with rsync.hip.devices > 1 the
+     * files are split over the thread's contexts on every GPU (rsh_block_sums_batch_multi).
      */
     void blockSumsSegment(ByteBuffer[][] basis, long[] sizes, Checksum.Header[] headers, byte[] seed, int[][] weak,
             byte[][] strong) {
         Segment s = new Segment(basis, headers);
         lock.lock();
         try {
-            blockSumsBatch(handle(), s.buffers, s.filePieces, sizes, s.headers, seed, weak, strong);
+            if (set.length > 1) {
+                blockSumsBatchMulti(handles(), s.buffers, s.filePieces, sizes, s.headers, seed, weak, strong);
+            } else {
+                blockSumsBatch(handle(), s.buffers, s.filePieces, sizes, s.headers, seed, weak, strong);
+            }
         } finally {
             lock.unlock();
         }
@@ -212,7 +254,8 @@ final class NativeChecksum implements AutoCloseable {
      * A segment's Sender pass in one call (Sender.sendFiles, Sender.java:1098-1148): returns, per file, its
      * events as {kind, offset, length, index | count << 32} quadruples (the caller replays each file's as
      * matchScan's, Sender.java:794-809 / 1274 / 1316); fileMd5[f] and sizes[f] = {sizeLiteral, sizeMatch}.
-     * The files' MD5s run on the host's cores beside the device work.
+     * The files' MD5s run on the host's cores beside the device work.  With rsync.hip.devices > 1 the files are split
+     * over the thread's contexts on every GPU (rsh_match_scan_batch_multi), results in file order.
      */
     long[][] matchScanSegment(ByteBuffer[][] source, long[] fileSizes, Checksum.Header[] headers, int[][] weak,
             byte[][] strong, byte[] seed, byte[][] fileMd5, long[][] sizes) {
@@ -223,8 +266,11 @@ final class NativeChecksum implements AutoCloseable {
         long[] flat;
         lock.lock();
         try {
-            flat = matchScanBatch(handle(), s.buffers, s.filePieces, fileSizes, s.headers, weak, strong, seed, md5,
-                    per);
+            flat = set.length > 1
+                    ? matchScanBatchMulti(handles(), s.buffers, s.filePieces, fileSizes, s.headers, weak, strong, seed,
+                            md5, per)
+                    : matchScanBatch(handle(), s.buffers, s.filePieces, fileSizes, s.headers, weak, strong, seed, md5,
+                            per);
         } finally {
             lock.unlock();
         }
@@ -331,6 +377,12 @@ final class NativeChecksum implements AutoCloseable {
 
     static native long[] matchScanBatch(long ctx, ByteBuffer[] src, int[] filePieces, long[] sizes, int[] headers,
             int[][] weak, byte[][] strong, byte[] seed, byte[] fileMd5Out, long[] perFileOut);
+
+    static native void blockSumsBatchMulti(long[] ctxs, ByteBuffer[] data, int[] filePieces, long[] sizes, int[] headers,
+            byte[] seed, int[][] weakOut, byte[][] strongOut);
+
+    static native long[] matchScanBatchMulti(long[] ctxs, ByteBuffer[] src, int[] filePieces, long[] sizes,
+            int[] headers, int[][] weak, byte[][] strong, byte[] seed, byte[] fileMd5Out, long[] perFileOut);
 
     static native boolean receiverCombine(long ctx, ByteBuffer tokens, long tokensLen, int[] header,
             ByteBuffer replica, long replicaLen, boolean deferWrite, ByteBuffer target, long targetCap,

@@ -24,7 +24,9 @@
  *   blockSumsFile / matchScanFile      a path: the library reads the file with FileView's semantics and
  *                                      reports a read error as a flag (the FileViewException of close());
  *   blockSumsBatch / matchScanBatch    a whole file-list segment in one call (Generator.itemizeSegment,
- *                                      Sender.sendFiles): every file's pieces, header and table at once.
+ *                                      Sender.sendFiles): every file's pieces, header and table at once;
+ *   blockSumsBatchMulti / matchScanBatchMulti  the same over the calling thread's contexts on the node's GPUs
+ *                                      (rsh_*_batch_multi: the segment's files split over them).
  * The Sender replays the returned events through its own sendDataFrom/putInt so channel framing is
  * untouched (Sender.java:794-809); INTEGRATION.md shows the replay for each form.
  *
@@ -62,6 +64,35 @@ static void throw_status(JNIEnv* env, int rc) {
 static rsh_ctx* ctx_of(JNIEnv* env, jlong ctx) {
     if (ctx == 0) throw_class(env, "java/lang/IllegalStateException", "NativeChecksum context is closed");
     return (rsh_ctx*)(intptr_t)ctx;
+}
+
+/* The contexts of a NativeChecksum device set (long[] of live handles, one per GPU): malloc'd array (free it), or
+ * NULL with IllegalStateException (a closed context) / IllegalArgumentException (empty) thrown. */
+static rsh_ctx** ctxs_of(JNIEnv* env, jlongArray hs, jint* n) {
+    *n = hs ? (*env)->GetArrayLength(env, hs) : 0;
+    if (*n < 1) {
+        throw_class(env, "java/lang/IllegalArgumentException", "no NativeChecksum contexts");
+        return NULL;
+    }
+    jlong* v = (jlong*)malloc(sizeof(jlong) * (size_t)*n);
+    rsh_ctx** out = (rsh_ctx**)malloc(sizeof(rsh_ctx*) * (size_t)*n);
+    if (!v || !out) {
+        free(v);
+        free(out);
+        throw_status(env, RSH_E_NOMEM);
+        return NULL;
+    }
+    (*env)->GetLongArrayRegion(env, hs, 0, *n, v);
+    for (jint i = 0; i < *n; ++i) {
+        if (!ctx_of(env, v[i])) {
+            free(v);
+            free(out);
+            return NULL;
+        }
+        out[i] = (rsh_ctx*)(intptr_t)v[i];
+    }
+    free(v);
+    return out;
 }
 
 /* The address of a direct buffer that holds at least `need` bytes; NULL (IllegalArgumentException thrown)
@@ -579,12 +610,10 @@ static void throw_file_status(JNIEnv* env, jint f, int rc) {
 }
 
 /* weakOut[f] (int[chunkCount]) and strongOut[f] (byte[chunkCount * digestLength]) receive file f's sums. */
-JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_blockSumsBatch(
-    JNIEnv* env, jclass cls, jlong ctx, jobjectArray data, jintArray filePieces, jlongArray sizes, jintArray hdrs,
-    jbyteArray seed, jobjectArray weakOut, jobjectArray strongOut) {
-    (void)cls;
-    rsh_ctx* c = ctx_of(env, ctx);
-    if (!c) return;
+/* A segment's Generator pass over nctx contexts (rsh_block_sums_batch_multi; nctx 1: rsh_block_sums_batch). */
+static void block_sums_segment(JNIEnv* env, rsh_ctx* const* ctxs, jint nctx, jobjectArray data, jintArray filePieces,
+                               jlongArray sizes, jintArray hdrs, jbyteArray seed, jobjectArray weakOut,
+                               jobjectArray strongOut) {
     jbyte s4[4];
     if (seed_from(env, seed, s4) != RSH_OK) {
         throw_status(env, RSH_E_INVAL);
@@ -617,7 +646,7 @@ JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksu
         if (!jobs[f].weak_out || !jobs[f].strong_out) rc = RSH_E_NOMEM;
     }
     if (rc == RSH_OK) {
-        rc = rsh_block_sums_batch(c, jobs, nf, (const uint8_t*)s4);
+        rc = rsh_block_sums_batch_multi(ctxs, nctx, jobs, nf, (const uint8_t*)s4);
         if (rc != RSH_OK) {
             jint f = 0;
             while (f < nf && jobs[f].status == RSH_OK) ++f;
@@ -644,6 +673,27 @@ JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksu
     free(wo);
     free(so);
     segment_free(&a);
+}
+
+JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_blockSumsBatch(
+    JNIEnv* env, jclass cls, jlong ctx, jobjectArray data, jintArray filePieces, jlongArray sizes, jintArray hdrs,
+    jbyteArray seed, jobjectArray weakOut, jobjectArray strongOut) {
+    (void)cls;
+    rsh_ctx* c = ctx_of(env, ctx);
+    if (!c) return;
+    block_sums_segment(env, &c, 1, data, filePieces, sizes, hdrs, seed, weakOut, strongOut);
+}
+
+/* As blockSumsBatch over the thread's contexts on the node's GPUs: the files are split over them (rsh_shard_files). */
+JNIEXPORT void JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_blockSumsBatchMulti(
+    JNIEnv* env, jclass cls, jlongArray ctxs, jobjectArray data, jintArray filePieces, jlongArray sizes, jintArray hdrs,
+    jbyteArray seed, jobjectArray weakOut, jobjectArray strongOut) {
+    (void)cls;
+    jint n = 0;
+    rsh_ctx** cs = ctxs_of(env, ctxs, &n);
+    if (!cs) return;
+    block_sums_segment(env, cs, n, data, filePieces, sizes, hdrs, seed, weakOut, strongOut);
+    free(cs);
 }
 
 /* An event buffer no scan of n bytes overflows (Sender.java:1251-1316):
@@ -677,12 +727,10 @@ static int rescan_nospace(rsh_ctx* c, rsh_scan_batch_job* jobs, jint nf, const u
 
 /* Returns every file's events, file after file, as {kind, offset, length, index | (count << 32)} quadruples;
  * perFileOut[3f..3f+2] = {event count, sizeLiteral, sizeMatch}, fileMd5Out[16f..16f+15] = file f's MD5. */
-JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_matchScanBatch(
-    JNIEnv* env, jclass cls, jlong ctx, jobjectArray src, jintArray filePieces, jlongArray sizes, jintArray hdrs,
-    jobjectArray weak, jobjectArray strong, jbyteArray seed, jbyteArray fileMd5Out, jlongArray perFileOut) {
-    (void)cls;
-    rsh_ctx* c = ctx_of(env, ctx);
-    if (!c) return NULL;
+/* A segment's Sender pass over nctx contexts (rsh_match_scan_batch_multi; nctx 1: rsh_match_scan_batch). */
+static jlongArray scan_segment(JNIEnv* env, rsh_ctx* const* ctxs, jint nctx, jobjectArray src, jintArray filePieces,
+                               jlongArray sizes, jintArray hdrs, jobjectArray weak, jobjectArray strong, jbyteArray seed,
+                               jbyteArray fileMd5Out, jlongArray perFileOut) {
     jbyte s4[4];
     if (seed_from(env, seed, s4) != RSH_OK) {
         throw_status(env, RSH_E_INVAL);
@@ -724,8 +772,8 @@ JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeC
     }
     jlongArray out = NULL;
     if (rc == RSH_OK) {
-        rc = rsh_match_scan_batch(c, jobs, nf, (const uint8_t*)s4, NULL);
-        if (rc == RSH_E_NOSPACE) rc = rescan_nospace(c, jobs, nf, (const uint8_t*)s4);
+        rc = rsh_match_scan_batch_multi(ctxs, nctx, jobs, nf, (const uint8_t*)s4, NULL);
+        if (rc == RSH_E_NOSPACE) rc = rescan_nospace(ctxs[0], jobs, nf, (const uint8_t*)s4);
         if (rc != RSH_OK) {
             jint f = 0;
             while (f < nf && jobs[f].status == RSH_OK) ++f;
@@ -765,6 +813,28 @@ JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeC
     }
     free(jobs);
     segment_free(&a);
+    return out;
+}
+
+JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_matchScanBatch(
+    JNIEnv* env, jclass cls, jlong ctx, jobjectArray src, jintArray filePieces, jlongArray sizes, jintArray hdrs,
+    jobjectArray weak, jobjectArray strong, jbyteArray seed, jbyteArray fileMd5Out, jlongArray perFileOut) {
+    (void)cls;
+    rsh_ctx* c = ctx_of(env, ctx);
+    if (!c) return NULL;
+    return scan_segment(env, &c, 1, src, filePieces, sizes, hdrs, weak, strong, seed, fileMd5Out, perFileOut);
+}
+
+/* As matchScanBatch over the thread's contexts on the node's GPUs (rsh_match_scan_batch_multi). */
+JNIEXPORT jlongArray JNICALL Java_com_github_java_rsync_internal_session_NativeChecksum_matchScanBatchMulti(
+    JNIEnv* env, jclass cls, jlongArray ctxs, jobjectArray src, jintArray filePieces, jlongArray sizes, jintArray hdrs,
+    jobjectArray weak, jobjectArray strong, jbyteArray seed, jbyteArray fileMd5Out, jlongArray perFileOut) {
+    (void)cls;
+    jint n = 0;
+    rsh_ctx** cs = ctxs_of(env, ctxs, &n);
+    if (!cs) return NULL;
+    jlongArray out = scan_segment(env, cs, n, src, filePieces, sizes, hdrs, weak, strong, seed, fileMd5Out, perFileOut);
+    free(cs);
     return out;
 }
 

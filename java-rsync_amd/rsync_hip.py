@@ -141,10 +141,10 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_coun
            "rsh_header_validate", "rsh_block_sums", "rsh_block_sums_device", "rsh_ctx_sync", "rsh_ctx_trim", "rsh_match_scan",
            "rsh_match_scan_device", "rsh_match_scan_tiled", "rsh_fetch_events", "rsh_file_md5", "rsh_tokens_size", "rsh_tokens_write", "rsh_generator_bytes",
            "rsh_block_sums_batch_device", "rsh_match_scan_batch_device", "rsh_receiver_combine",
-           "rsh_receiver_combine_device", "rsh_receiver_combine_batch", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_block_sums_batch", "rsh_match_scan_batch", "rsh_file_md5_batch", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
+           "rsh_receiver_combine_device", "rsh_receiver_combine_batch", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_block_sums_batch", "rsh_match_scan_batch", "rsh_block_sums_batch_multi", "rsh_match_scan_batch_multi", "rsh_receiver_combine_batch_multi", "rsh_shard_files", "rsh_file_md5_batch", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 # include/rsync_hip_debug.h (testing / diagnostics ABI)
 DEBUG_EXPORTS = ["rsh_debug_set_option", "rsh_debug_get_option", "rsh_debug_reset_options", "rsh_debug_k1_clock",
-                 "rsh_debug_streams_busy", "rsh_debug_kernel_ms"]
+                 "rsh_debug_streams_busy", "rsh_debug_kernel_ms", "rsh_debug_multi_selftest"]
 
 _LIB = None
 
@@ -227,6 +227,11 @@ def lib():
                                    ctypes.POINTER(I64), ctypes.POINTER(I64), ctypes.POINTER(ScanStats)], ctypes.c_int),
         "rsh_block_sums_batch": ([P, ctypes.POINTER(BlockBatchJob), I32, P], ctypes.c_int),
         "rsh_match_scan_batch": ([P, ctypes.POINTER(ScanBatchJob), I32, P, ctypes.POINTER(ScanStats)], ctypes.c_int),
+        "rsh_block_sums_batch_multi": ([ctypes.POINTER(P), I32, ctypes.POINTER(BlockBatchJob), I32, P], ctypes.c_int),
+        "rsh_match_scan_batch_multi": ([ctypes.POINTER(P), I32, ctypes.POINTER(ScanBatchJob), I32, P,
+                                        ctypes.POINTER(ScanStats)], ctypes.c_int),
+        "rsh_receiver_combine_batch_multi": ([ctypes.POINTER(P), I32, ctypes.POINTER(CombineJob), I32], ctypes.c_int),
+        "rsh_shard_files": ([P, I32, I32, P], ctypes.c_int),
         "rsh_file_md5_batch": ([ctypes.POINTER(Md5Job), I32, I32], ctypes.c_int),
         "rsh_dev_alloc": ([P, I64, ctypes.POINTER(P)], ctypes.c_int),
         "rsh_dev_free": ([P, P], ctypes.c_int),
@@ -239,6 +244,7 @@ def lib():
         "rsh_debug_k1_clock": ([P, P, I64, I32, I32, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "rsh_debug_streams_busy": ([P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
         "rsh_debug_kernel_ms": ([P, I32, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+        "rsh_debug_multi_selftest": ([P, I32, I32, I32, P, P, P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -439,6 +445,16 @@ class Context:
     def sync(self):
         _check(lib().rsh_ctx_sync(self._p))
 
+    # the segment calls' entry points (DeviceSet: the multi-context forms)
+    def _block_batch(self, jobs, n, seed):
+        return lib().rsh_block_sums_batch(self._p, jobs, n, seed)
+
+    def _scan_batch(self, jobs, n, seed, stats):
+        return lib().rsh_match_scan_batch(self._p, jobs, n, seed, stats)
+
+    def _combine_batch(self, jobs, n):
+        return lib().rsh_receiver_combine_batch(self._p, jobs, n)
+
     def trim(self):
         """Release the pass-sized buffers (rsh_ctx_trim); the next call allocates what it needs again."""
         _check(lib().rsh_ctx_trim(self._p))
@@ -518,7 +534,7 @@ class Context:
             outs.append((w, st, h))
             jobs[i].pieces, jobs[i].npieces, jobs[i].h = ctypes.cast(pl, ctypes.POINTER(Piece)), len(arrs), h
             jobs[i].weak_out, jobs[i].strong_out = w.ctypes.data, st.ctypes.data
-        rc = lib().rsh_block_sums_batch(self._p, jobs, len(files), _ptr(s))
+        rc = self._block_batch(jobs, len(files), _ptr(s))
         if statuses is not None:
             statuses[:] = [rc] + [jobs[i].status for i in range(len(files))]
         else:
@@ -546,7 +562,7 @@ class Context:
             j.weak, j.strong = (w.ctypes.data if w.size else None), (st.ctypes.data if st.size else None)
             j.ev, j.ev_cap = ev.ctypes.data, cap
         stats = ScanStats()
-        rc = lib().rsh_match_scan_batch(self._p, jobs, len(files), _ptr(s), ctypes.byref(stats))
+        rc = self._scan_batch(jobs, len(files), _ptr(s), ctypes.byref(stats))
         if statuses is not None:
             statuses[:] = [rc]
         elif rc != RSH_E_NOSPACE:
@@ -637,7 +653,7 @@ class Context:
             if replica is not None:
                 j.replica, j.nreplica = ctypes.cast(pl, ctypes.POINTER(Piece)), len(arrs)
             j.defer_write, j.target, j.target_cap = int(bool(defer)), tgt.ctypes.data, cap
-        rc = lib().rsh_receiver_combine_batch(self._p, jobs, len(files))
+        rc = self._combine_batch(jobs, len(files))
         if statuses is not None:
             statuses[:] = [rc]
         elif rc not in (RSH_OK, RSH_E_NOSPACE, RSH_E_PROTOCOL, RSH_E_INVAL):
@@ -662,6 +678,44 @@ class Context:
                                           0 if rep is None else rep.size, int(bool(defer_write)), _ptr(tgt), cap,
                                           ctypes.byref(r)))
         return tgt[:r.target_len].tobytes(), r
+
+
+class DeviceSet(Context):
+    """The calling thread's contexts over several GPUs (rsh_*_batch_multi): the segment calls block_sums_batch,
+    match_scan_batch and receiver_combine_batch split their files over the contexts (rsh_shard_files) and run each
+    context's share beside the others.  devices: one context per entry (a device may repeat).  The single-context
+    methods run on the first context."""
+
+    def __init__(self, devices):
+        self.members = [Context(d) for d in devices]
+        self._p = self.members[0].handle
+        self._arr = (ctypes.c_void_p * len(self.members))(*[c.handle.value for c in self.members])
+
+    def close(self):
+        for c in getattr(self, "members", []):
+            c.close()
+        self.members, self._p = [], ctypes.c_void_p()
+
+    def trim(self):
+        for c in self.members:
+            c.trim()
+
+    def _block_batch(self, jobs, n, seed):
+        return lib().rsh_block_sums_batch_multi(self._arr, len(self.members), jobs, n, seed)
+
+    def _scan_batch(self, jobs, n, seed, stats):
+        return lib().rsh_match_scan_batch_multi(self._arr, len(self.members), jobs, n, seed, stats)
+
+    def _combine_batch(self, jobs, n):
+        return lib().rsh_receiver_combine_batch_multi(self._arr, len(self.members), jobs, n)
+
+
+def shard_files(sizes, parts):
+    """rsh_shard_files: the part (context) each file goes to."""
+    b = np.ascontiguousarray(sizes, dtype=np.int64)
+    out = np.zeros(max(b.size, 1), np.int32)
+    _check(lib().rsh_shard_files(_ptr(b), b.size, parts, _ptr(out)))
+    return out[:b.size]
 
 
 class DeviceBuffer:

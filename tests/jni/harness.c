@@ -146,6 +146,10 @@ void NC(blockSumsBatch)(JNIEnv*, jclass, jlong, jobjectArray, jintArray, jlongAr
                         jobjectArray, jobjectArray);
 jlongArray NC(matchScanBatch)(JNIEnv*, jclass, jlong, jobjectArray, jintArray, jlongArray, jintArray, jobjectArray,
                               jobjectArray, jbyteArray, jbyteArray, jlongArray);
+void NC(blockSumsBatchMulti)(JNIEnv*, jclass, jlongArray, jobjectArray, jintArray, jlongArray, jintArray, jbyteArray,
+                             jobjectArray, jobjectArray);
+jlongArray NC(matchScanBatchMulti)(JNIEnv*, jclass, jlongArray, jobjectArray, jintArray, jlongArray, jintArray,
+                                   jobjectArray, jobjectArray, jbyteArray, jbyteArray, jlongArray);
 jboolean NC(receiverCombine)(JNIEnv*, jclass, jlong, jobject, jlong, jintArray, jobject, jlong, jboolean, jobject, jlong,
                              jlongArray, jbyteArray);
 
@@ -157,6 +161,15 @@ jboolean NC(receiverCombine)(JNIEnv*, jclass, jlong, jobject, jlong, jintArray, 
 static void reset(void) {
     g_exc[0] = 0;
     g_msg[0] = 0;
+}
+
+/* jh_set_multi(ctxs, n): the segment entry points below call the Multi natives (NativeChecksum's device set) with
+ * these contexts as the long[] instead of the single context (n = 0: back to the single-context natives). */
+static jlong g_multi[64];
+static int g_nmulti = 0;
+JNIEXPORT void jh_set_multi(const jlong* ctxs, int n) {
+    g_nmulti = n < 0 ? 0 : n > 64 ? 64 : n;
+    if (g_nmulti) memcpy(g_multi, ctxs, (size_t)g_nmulti * sizeof(jlong));
 }
 
 JNIEXPORT const char* jh_exception(void) { return g_exc; }
@@ -303,7 +316,10 @@ JNIEXPORT void jh_block_sums_batch(jlong ctx, void** bufs, const jlong* caps, in
     OBJ(sz, K_LONG, sizes, nf);
     OBJ(h, K_INT, hdrs, 4 * nf);
     OBJ(s, K_BYTE, seed, 4);
-    NC(blockSumsBatch)(&g_env, NULL, ctx, &arr, fp, sz, h, s, &wa, &sa);
+    fobj cs_o = {K_LONG, g_multi, g_nmulti};
+    jobject cs = &cs_o;
+    if (g_nmulti) NC(blockSumsBatchMulti)(&g_env, NULL, cs, &arr, fp, sz, h, s, &wa, &sa);
+    else NC(blockSumsBatch)(&g_env, NULL, ctx, &arr, fp, sz, h, s, &wa, &sa);
     free(refs);
     free(store);
     free(ws);
@@ -334,7 +350,11 @@ JNIEXPORT jlong jh_match_scan_batch(jlong ctx, void** bufs, const jlong* caps, i
     OBJ(s, K_BYTE, seed, 4);
     OBJ(m, K_BYTE, md5, md5_len);
     OBJ(pf, K_LONG, per_file, per_len);
-    jlong r = events_back(NC(matchScanBatch)(&g_env, NULL, ctx, &arr, fp, sz, h, &wa, &sa, s, m, pf), ev_out, ev_cap);
+    fobj cs_o = {K_LONG, g_multi, g_nmulti};
+    jobject cs = &cs_o;
+    jlongArray o = g_nmulti ? NC(matchScanBatchMulti)(&g_env, NULL, cs, &arr, fp, sz, h, &wa, &sa, s, m, pf)
+                            : NC(matchScanBatch)(&g_env, NULL, ctx, &arr, fp, sz, h, &wa, &sa, s, m, pf);
+    jlong r = events_back(o, ev_out, ev_cap);
     free(refs);
     free(store);
     free(ws);

@@ -35,7 +35,7 @@ def test_library_exports_every_symbol():
     L = ctypes.CDLL(R.LIB_PATH)
     for name in R.EXPORTS + R.DEBUG_EXPORTS:
         assert hasattr(L, name), name
-    assert R.lib().rsh_abi_version() == 4
+    assert R.lib().rsh_abi_version() == 5
 
 
 def test_options_have_defaults_and_no_environment():
@@ -200,3 +200,71 @@ def test_file_md5_batch_matches_hashlib(width):
             for (a, _), d in zip(files, got):
                 assert d == hashlib.md5(a.tobytes()).digest(), (a.size, threads)
     assert R.file_md5_batch([]) == []
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 8])
+def test_shard_files_matches_rank_rule(nparts):
+    """rsh_shard_files (the split of rsh_*_batch_multi) is shard.py's LPT rule: longest first, equal sizes in file
+    order, each file to the part with the fewest bytes so far, ties to the lower part."""
+    import random
+
+    import shard
+    rng = random.Random(nparts)
+    for sizes in ([128 << 20] * 1024, [rng.choice([0, 1, 5 << 20, 128 << 20, 3 << 30]) for _ in range(97)], [7], []):
+        parts = R.shard_files(sizes, nparts)
+        want = shard.shard_files(sizes, nparts)
+        got = [sorted(int(i) for i in np.nonzero(parts == p)[0]) for p in range(nparts)]
+        assert got == want
+
+
+def _selftest(sizes, nparts, fail_part):
+    import ctypes
+    b = np.array(sizes, np.int64)
+    part, order, status = (np.zeros(max(len(sizes), 1), np.int32) for _ in range(3))
+    rc = R.lib().rsh_debug_multi_selftest(ctypes.c_void_p(b.ctypes.data), len(sizes), nparts, fail_part,
+                                          ctypes.c_void_p(part.ctypes.data), ctypes.c_void_p(order.ctypes.data),
+                                          ctypes.c_void_p(status.ctypes.data))
+    n = len(sizes)
+    return rc, part[:n], order[:n], status[:n]
+
+
+def test_multi_merge_order():
+    """The multi-context driver: every file lands on its rsh_shard_files part, a part sees its files in segment order,
+    and each job's outputs come back to the caller's job of the same file (the stand-in member call records them)."""
+    import random
+    rng = random.Random(5)
+    sizes = [rng.randrange(1, 1 << 30) for _ in range(200)]
+    rc, part, order, status = _selftest(sizes, 8, -1)
+    assert rc == R.RSH_OK and (status == R.RSH_OK).all()
+    assert np.array_equal(part, R.shard_files(sizes, 8))
+    for p in range(8):
+        mine = np.nonzero(part == p)[0]
+        assert list(order[mine]) == list(range(mine.size))  # file order within the part
+
+
+def test_multi_failure_marks_one_member():
+    """A member call that fails (after finishing its first file) marks only the files of its own part; the other
+    parts' files are RSH_OK, and the call returns the first failing job's status in file order."""
+    sizes = [100 << 20] * 16 + [1 << 20] * 16
+    rc, part, order, status = _selftest(sizes, 4, 2)
+    mine = np.nonzero(part == 2)[0]
+    assert mine.size > 1
+    failed = np.nonzero(status != R.RSH_OK)[0]
+    assert list(failed) == list(mine[1:]) and (status[failed] == R.RSH_E_DEVICE).all()
+    assert rc == R.RSH_E_DEVICE
+    rc, _, _, status = _selftest(sizes, 4, -1)
+    assert rc == R.RSH_OK and (status == R.RSH_OK).all()
+
+
+def test_multi_entry_points_validate_contexts():
+    """Null or repeated contexts are refused before any work (RSH_E_INVAL): a context serves one call at a time."""
+    import ctypes
+    L = R.lib()
+    seed = np.frombuffer(bytes([1, 2, 3, 4]), np.uint8).copy()
+    fake = (ctypes.c_void_p * 2)(0x1000, 0x1000)
+    nul = (ctypes.c_void_p * 2)(0x1000, None)
+    for arr in (fake, nul):
+        assert L.rsh_block_sums_batch_multi(arr, 2, None, 0, ctypes.c_void_p(seed.ctypes.data)) == R.RSH_E_INVAL
+        assert L.rsh_match_scan_batch_multi(arr, 2, None, 0, ctypes.c_void_p(seed.ctypes.data), None) == R.RSH_E_INVAL
+        assert L.rsh_receiver_combine_batch_multi(arr, 2, None, 0) == R.RSH_E_INVAL
+    assert L.rsh_block_sums_batch_multi(fake, 0, None, 0, ctypes.c_void_p(seed.ctypes.data)) == R.RSH_E_INVAL

@@ -243,13 +243,43 @@ def test_segment_natives_reject_before_the_library(H):
     assert match_scan_batch(H, BOGUS, ok, [w], [st], per_len=2)[0] == IAE
 
 
+def _multi(H, ctxs):
+    """The segment helpers above call blockSumsBatchMulti / matchScanBatchMulti with these contexts ([]: the
+    single-context natives)."""
+    a = np.array(ctxs or [0], np.int64)
+    H.jh_set_multi(_p(a), len(ctxs))
+
+
+def test_multi_natives_reject_closed_contexts(H):
+    """blockSumsBatchMulti / matchScanBatchMulti (NativeChecksum's device set): a closed context anywhere in the
+    long[] is an IllegalStateException before the library is called (the other handle is bogus)."""
+    n, B = 4096, 512
+    data = np.zeros(n, np.uint8)
+    h = O.header(B, 2, n)
+    w, st = np.zeros(8, np.int32), np.zeros(16, np.uint8)
+    ok = [([data], n, h)]
+    try:
+        _multi(H, [BOGUS, 0])
+        assert block_sums_batch(H, BOGUS, ok, [w], [st]) == ISE
+        assert match_scan_batch(H, BOGUS, ok, [w], [st])[0] == ISE
+        _multi(H, [BOGUS, BOGUS + 1])
+        assert block_sums_batch(H, BOGUS, ok, [np.zeros(7, np.int32)], [st]) == IAE  # still checked in the shim
+    finally:
+        _multi(H, [])
+
+
 @pytest.mark.gpu
-def test_segment_natives_match_oracle(H):
-    """A segment through blockSumsBatch / matchScanBatch on a real context: every file's tables, events (the flat
-    long[] split by perFileOut's counts), sizes and file MD5 equal the oracle's; files are cut into several
-    direct buffers; a new file (B = 0) rides along."""
+@pytest.mark.parametrize("nctx", [1, 2])
+def test_segment_natives_match_oracle(H, nctx):
+    """A segment through blockSumsBatch / matchScanBatch on a real context (nctx 2: blockSumsBatchMulti /
+    matchScanBatchMulti over two contexts, the files split between them): every file's tables, events (the flat
+    long[] split by perFileOut's counts), sizes and file MD5 equal the oracle's, in file order; files are cut into
+    several direct buffers; a new file (B = 0) rides along."""
     ctx = H.jh_ctx_create(0)
     assert ctx and exc(H) == "", exc(H)
+    ctx2 = H.jh_ctx_create(min(1, R.device_count() - 1)) if nctx == 2 else 0
+    if nctx == 2:
+        _multi(H, [ctx, ctx2])
     try:
         files, tables, heads, srcs = [], [], [], []
         for k, (n, blen, dl) in enumerate(((100000, 512, 2), (3 << 20, 8192, 3), (1300, 512, 2), (70000, 1024, 4))):
@@ -285,7 +315,10 @@ def test_segment_natives_match_oracle(H):
             assert md5[16 * f:16 * f + 16].tobytes() == ofm and (per[3 * f + 1], per[3 * f + 2]) == (olit, omat)
         assert at == q.shape[0]
     finally:
+        _multi(H, [])
         H.jh_ctx_destroy(ctypes.c_int64(ctx))
+        if ctx2:
+            H.jh_ctx_destroy(ctypes.c_int64(ctx2))
 
 
 @pytest.mark.gpu
