@@ -79,6 +79,13 @@ def parse():
                     help="files workload: the batched entry points (one K1 launch per segment, one round trip "
                          "per round for all files) or one rsh_match_scan_device per file on a context pool")
     ap.add_argument("--cpu-sample-mib", type=int, default=1024)
+    ap.add_argument("--cpu-files-sample-mib", type=int, default=2048,
+                    help="the default line's `files` block: bytes per pair summed over the files the host cores run at "
+                         "once (bounded so the block's CPU baseline takes ~1-3 s)")
+    ap.add_argument("--devices", type=int, default=0,
+                    help="--workload files in one process over N contexts (rsh_*_batch_multi, the drop-in's multi-GPU "
+                         "segment calls; contexts on devices 0..N-1, round-robin over the visible GPUs): the files "
+                         "from host memory, end to end")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="library option for an A/B run (include/rsync_hip_debug.h; reported in the line)")
@@ -174,6 +181,8 @@ def main():
         sys.exit(spawn_ranks(a))
     if a.dry_run:
         return main_dry(a)
+    if a.workload == "files" and a.devices > 0:
+        return main_files_devices(a)
     if a.workload == "files":
         return main_files(a)
     if a.workload == "receiver":
@@ -413,7 +422,7 @@ def main():
         del pairs, src, d_weak, d_strong
         torch.cuda.empty_cache()
         f = run_files(a, ctx, rank, world, red_dev, shared, "identical", a.steps, a.warmup, not a.no_companions,
-                      cpu=False)
+                      cpu=not a.no_cpu_baseline, cpu_sample=a.cpu_files_sample_mib << 20)
         res["files"] = {"value": f["value"], "unit": "GiB/s", "ms_per_step": f["ms_per_step"],
                         "per_rank_ms_per_step": f["per_rank_ms_per_step"], "steps": f["steps"],
                         "workload": f["config"]["workload"], "files_total": f["config"]["files_total"],
@@ -424,6 +433,8 @@ def main():
                         "parity": f["parity"],
                         "variants": {v: {k: r[k] for k in ("value_read", "ms_per_step", "per_rank_ms_per_step",
                                                           "parity")} for v, r in f["variants"].items()}}
+        if "cpu_baseline" in f:  # config 4 on the host's cores, K files at once
+            res["files"]["cpu_baseline"] = f["cpu_baseline"]
     if rank == 0:
         if a.opt:
             res["config"]["options"] = a.opt
@@ -498,7 +509,105 @@ def main_files(a):
         dist.destroy_process_group()
 
 
-def run_files(a, ctx, rank, world, red_dev, shared, variant, steps, warmup, companions, cpu):
+def main_files_devices(a):
+    """--workload files --devices N: BASELINE config 4 through the drop-in's multi-GPU segment calls in ONE process --
+    what a JVM's Generator and Sender threads call (NativeChecksum's device set, rsh_block_sums_batch_multi +
+    rsh_match_scan_batch_multi): N * --files files of --file-mib MiB (the inputs of tests/golden/fullsize_config4.json)
+    in host memory, split over N contexts on devices 0..N-1 (round-robin over the visible GPUs: on a one-GPU box the
+    contexts share it -- a rehearsal of the plumbing, not a scaling point).  One step = the Generator over every basis
+    + the Sender over every source, H2D copies, the device work and every file's MD5 on the host included; value =
+    the bytes handed over (bases + sources) per second.  Every file's events and MD5 are checked against the oracle's
+    committed digests after the clock."""
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import fullsize_golden as G
+    if not os.path.exists(R.LIB_PATH):
+        R.build()
+    apply_opts(a)
+    N, ngpu = a.devices, torch.cuda.device_count()
+    S = a.file_mib << 20
+    F = a.files * N
+    try:  # both sides of every pair stay in host memory: keep them within half of what is free
+        import psutil
+        cap = int(0.5 * psutil.virtual_memory().available) // ((2 if a.variant == "half" else 1) * S)
+        if F > cap:
+            F = max(N, cap - cap % N)
+    except ImportError:
+        pass
+    B = R.block_length_for(S)
+    dl = R.digest_length_for(S, B)
+    h = R.header_make(B, dl, S)
+    devs = [d % ngpu for d in range(N)]
+    ds = R.DeviceSet(devs)
+    ctx = ds.members[0]
+    L = R.lib()
+    dev = torch.empty(2 * S, dtype=torch.uint8, device="cuda")
+    src = np.empty(F * S, np.uint8)
+    basis = np.empty(F * S, np.uint8) if a.variant == "half" else src  # identical: the source's own buffer
+    for i in range(F):  # file i: its own splitmix stream; the 50%-modified basis keeps the source's even blocks
+        assert L.rsh_fill_splitmix_device(ctx.handle, dev.data_ptr(), S, G.config4_key(i), 0) == 0
+        if a.variant == "half":
+            assert L.rsh_fill_splitmix_device(ctx.handle, dev.data_ptr() + S, S, G.KEY_EDIT ^ G.config4_key(i), 0) == 0
+        ctx.sync()
+        if a.variant == "half":
+            dev.view(2, -1, B)[1, ::2] = dev.view(2, -1, B)[0, ::2]
+        host = dev.cpu().numpy()
+        src[i * S:(i + 1) * S] = host[:S]
+        if a.variant == "half":
+            basis[i * S:(i + 1) * S] = host[S:]
+    del dev
+    torch.cuda.empty_cache()
+    seed = bytes([1, 2, 3, 4])
+    bjobs = [([basis[i * S:(i + 1) * S]], h) for i in range(F)]
+    res = None
+
+    def step():
+        nonlocal res
+        sums = ds.block_sums_batch(bjobs, seed)
+        res = ds.match_scan_batch([([src[i * S:(i + 1) * S]], h, sums[i][0], sums[i][1]) for i in range(F)], seed)
+    for _ in range(a.warmup):
+        step()
+    t_step = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+        t_step.append(time.perf_counter())
+    dt = time.perf_counter() - t0
+    out, st = res
+    assert all(o[4] == 0 for o in out), [o[4] for o in out]
+    golden = files_golden(list(range(F)), S, B, dl)
+    parity = "unchecked (no committed oracle digest for this shape)"
+    if golden:
+        for i in range(F):
+            n_ev, lit, mat, sha, fmd5 = golden[a.variant][i]
+            ev, fm, l2, m2, _ = out[i]
+            rec = G.records_from_runs(ev, B)
+            assert (int(rec.size), l2, m2) == (n_ev, lit, mat) and G.events_sha(rec) == sha and fm.hex() == fmd5, \
+                f"file {i}: differs from the oracle's digest"
+        parity = f"every file's events and file MD5 identical to the oracle ({F} per-file digests)"
+    parts = np.bincount(R.shard_files([S] * F, N), minlength=N)
+    line = {
+        "metric": "GiB/s end-to-end from host memory (Generator + Sender segment calls over N contexts; bytes handed "
+                  "over)",
+        "value": round(a.steps * 2 * F * S / dt / (1 << 30), 3), "unit": "GiB/s", "n_gpus": len(set(devs)),
+        "contexts": N, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(dt / a.steps * 1e3, 3),
+        "step_ms": [round((b - a_) * 1e3, 3) for a_, b in zip([t0] + t_step[:-1], t_step)],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64; tests/golden/fullsize_config4.json), host memory",
+        "config": {"workload": f"config4 in one process: {F} files x {a.file_mib} MiB ({VARIANT_TEXT[a.variant]} "
+                               f"bases) from host memory, B={B}, dl={dl}",
+                   "devices": devs, "files_per_context": [int(x) for x in parts],
+                   "parallelism": f"rsh_*_batch_multi over {N} contexts on {len(set(devs))} GPU(s)"
+                   + (" (REHEARSAL: contexts share GPUs, not a scaling point)" if len(set(devs)) < N else "")},
+        "scan": {"stats": st}, "parity": parity,
+    }
+    if a.opt:
+        line["config"]["options"] = a.opt
+    print(json.dumps(line), flush=True)
+    ds.close()
+
+
+def run_files(a, ctx, rank, world, red_dev, shared, variant, steps, warmup, companions, cpu, cpu_sample=None):
     """Config 4 on this rank's shard of the job's file list (main_files' line; the `files` block of the default
     line): returns the line's dict."""
     import concurrent.futures as cf
@@ -656,7 +765,8 @@ def run_files(a, ctx, rank, world, red_dev, shared, variant, steps, warmup, comp
         "scan": head["scan"], "parity": head["parity"], "variants": comp,
     }
     if rank == 0 and world == 1 and cpu:
-        res["cpu_baseline"] = cpu_baseline_files(src, bases[variant], S, F, B, dl, a.cpu_sample_mib << 20)
+        res["cpu_baseline"] = cpu_baseline_files(src, bases[variant], S, F, B, dl,
+                                                 cpu_sample if cpu_sample else a.cpu_sample_mib << 20)
     if ex:
         ex.shutdown()
     for c in pool_ctx:

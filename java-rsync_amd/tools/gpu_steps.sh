@@ -31,6 +31,8 @@
 #   receiver     the Receiver line (combineDataToFile on the config-2 shape)
 #   multi        bench.py --gpus 2 without a launcher (its own rank processes) on a one-GPU box: the N-rank path,
 #                ranks sharing the GPU (a rehearsal, not a scaling point); config 5 and config 4
+#   devices      bench.py --workload files --devices N in one process (rsh_*_batch_multi from host memory): the same 128
+#                files over 1 context and over 2 (both on GPU 0 on a one-GPU box: the plumbing, not a scaling point)
 #   first        tools/first_call.py: the first calls on a fresh context against the later ones (config 4, config 5)
 #   first-trace  rocprofv3 HIP API + kernel trace of first_call.py --only 5 --reps 2 (where the first step's time goes)
 #   copycb       rocprofv3 --memory-copy-trace over tools/queue_lat.hip (3 D2H hipMemcpyAsync per rep, no librsynchip):
@@ -124,6 +126,11 @@ for step in "$@"; do
                 > "$O/multi_file.json" 2> "$O/multi_file.err"
             run 300 python bench.py --gpus 2 --workload files --steps 5 --warmup 2 --no-cpu-baseline --no-companions \
                 > "$O/multi_files.json" 2> "$O/multi_files.err" ;;
+        devices)
+            for d in 1 2; do
+                run 400 python bench.py --workload files --variant "$VARIANT" --devices $d --files $((128 / d)) --steps 3 \
+                    --warmup 1 > "$O/devices_$d.json" 2> "$O/devices_$d.err"
+            done ;;
         config3) run 300 python bench.py --size-gib 64 --digest 5 --steps 3 --warmup 1 --no-companions --no-cpu-baseline \
             > "$O/config3.json" 2> "$O/config3.err" ;;
         receiver) run 300 python bench.py --workload receiver --steps 2 --warmup 1 > "$O/receiver.json" 2> "$O/receiver.err" ;;
