@@ -328,7 +328,9 @@ int rsh_receiver_combine_device(rsh_ctx* ctx, const uint8_t* tokens, int64_t tok
  * blocks and literals are one gather launch, the targets come back) in passes of at most option segment_bytes,
  * overlapped; the verify digests -- one serial MD5 chain per file -- run on the host's cores beside the copies,
  * up to 16 files per core (md5_mb.cpp), over the replica ranges and literal bytes the tokens name, which are
- * exactly the rebuilt file's bytes. */
+ * exactly the rebuilt file's bytes.  A file is never split across passes: one whose token stream, replica ranges and
+ * target together exceed segment_bytes gets a pass of its own of that size, and fails with RSH_E_NOMEM when the
+ * device cannot hold it (the single-file rsh_receiver_combine's limit: its target and replica in HBM at once). */
 typedef struct {
     const uint8_t* tokens;    /* host: the file's token stream, ending with putInt(0) */
     int64_t tokens_len;
