@@ -1,4 +1,4 @@
-// ctx.h -- internals shared by capi.cpp and batch.cpp (not part of the C-ABI): device / pinned buffers,
+// ctx.h -- internals shared by the library's host sources (not part of the C-ABI): device / pinned buffers,
 // the rsh_ctx definition, error capture and the one-call-per-context claim.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -15,6 +15,7 @@
 
 #include "device.h"
 #include "hit_cache.h"
+#include "options.h"
 #include "resolver.h"
 #include "rsync_hip.h"
 
@@ -65,7 +66,7 @@ namespace rshi {
 constexpr int64_t kChunkSize = 8192;        // Sender.java:230 CHUNK_SIZE
 constexpr int64_t kDefaultBlock = 8192;     // FileView.java:38 DEFAULT_BLOCK_SIZE
 constexpr int32_t kMaxBlockLength = 1 << 17;  // Checksum.java:151
-// Speculation launch decision (capi.cpp scan_device, batch.cpp scan_batch): when the first kLeadWindows
+// Speculation launch decision (scan.cpp scan_device, batch.cpp scan_batch): when the first kLeadWindows
 // aligned source windows all carry their chunk's weak sum, a run of aligned matches is likely: the
 // speculation is launched at once and the resolver waits for it instead of taking head-mode steps.
 constexpr int64_t kLeadWindows = 32;
@@ -134,6 +135,21 @@ inline double ms_since(std::chrono::steady_clock::time_point t0) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// rsh_match_scan_tiled: default tile (the device holds one tile + a 16 B halo of the source at a time)
+constexpr int64_t kDefaultTile = 4LL << 30;
+
+// Option scan_trace = 1: one stderr line per resolver round trip (diagnostics).
+struct CallTrace {
+    const char* what;
+    int64_t arg;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    static bool on() { return rsh::opt(rsh::OPT_SCAN_TRACE) != 0; }
+    CallTrace(const char* w, int64_t a) : what(w), arg(a) {}
+    ~CallTrace() {
+        if (on()) fprintf(stderr, "[rsh] %-10s %10lld %9.3f ms\n", what, (long long)arg, ms_since(t0));
+    }
+};
+
 }  // namespace rshi
 using namespace rshi;
 using rsh::HitCache;
@@ -190,7 +206,7 @@ struct rsh_ctx {
     static constexpr int kPhaseWord = 16;
     int gen = 0;
     bool spec_dl_pending = false;  // the last speculation's sums download (aux) may still read src_weak / src_strong
-    int stamp_seq = 0;             // values of the stamped launches (capi.cpp prep_ensure)
+    int stamp_seq = 0;             // values of the stamped launches (scan.cpp prep_ensure)
     std::vector<rsh_event> last_ev;  // kept when the caller's event buffer was too small
     std::atomic<bool> busy{false};   // the staging buffers and last_ev serve one call at a time
     rsh::BatchState* batch = nullptr;  // buffers of the batched (multi-file) entry points, on first use
@@ -221,7 +237,7 @@ struct rsh_ctx {
     }
 };
 
-// Last HIP failure of the calling thread (rsh_last_error): error text and the capi.cpp line.
+// Last HIP failure of the calling thread (rsh_last_error): error text and the source line.
 inline thread_local char g_last_err[256] = "";
 inline void note_error(hipError_t e, int line, const char* file = "capi.cpp") {
     snprintf(g_last_err, sizeof(g_last_err), "%s (%s:%d)", hipGetErrorString(e), file, line);
@@ -231,7 +247,7 @@ inline void note_error(hipError_t e, int line, const char* file = "capi.cpp") {
     do {                                                \
         hipError_t e_ = (call);                         \
         if (e_ != hipSuccess) {                         \
-            note_error(e_, __LINE__);                   \
+            note_error(e_, __LINE__, __FILE__);         \
             return RSH_E_DEVICE;                        \
         }                                               \
     } while (0)
@@ -276,12 +292,14 @@ inline void skip_events(int64_t n, rsh::ResolveResult* r) {
     r->literal = n;
 }
 
-// capi.cpp: the device-resident Sender scan (everything but the whole-file MD5) and the event hand-out.
+// scan.cpp: a new context's warm-up (code objects, the copy paths, a config-5 file's scan buffers: rsh_ctx_create)
+hipError_t ctx_warm(rsh_ctx* c);
+// scan.cpp: the device-resident Sender scan (everything but the whole-file MD5) and the event hand-out.
 int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h, const int32_t* d_weak,
                 const uint8_t* d_strong, const int32_t* host_weak, const uint8_t* host_strong, const uint8_t seed[4],
                 rsh::ResolveResult* res);
 int emit_events(rsh_ctx* c, rsh::ResolveResult& r, rsh_event* ev, int64_t cap, int64_t* n_ev);
-// capi.cpp: the scan with HBM holding one tile of the source at a time (fill copies source bytes to HBM).
+// scan.cpp: the scan with HBM holding one tile of the source at a time (fill copies source bytes to HBM).
 int scan_tiled(rsh_ctx* c, const std::function<hipError_t(uint8_t*, int64_t, int64_t)>& fill, int64_t n,
                const rsh_header* h, const int32_t* d_weak, const uint8_t* d_strong, const int32_t* host_weak,
                const uint8_t* host_strong, const uint8_t seed[4], int64_t tile_bytes, rsh::ResolveResult* res);

@@ -121,6 +121,7 @@ hipError_t launch_chain_flags(const int32_t* d_wsrc, const uint8_t* d_ssrc, cons
 // the runtime loads every production kernel before the first call.
 hipError_t launch_warm_k1(hipStream_t s);
 hipError_t launch_warm_scan(hipStream_t s);
+hipError_t launch_warm_chain(hipStream_t s);
 hipError_t launch_warm_io(hipStream_t s);
 // Completion without a marker packet: the launch's last workgroup to finish writes `gen` into *stamp (pinned host
 // memory, system-scope release after every workgroup's stores), which the host polls.  counter: device memory,
