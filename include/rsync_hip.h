@@ -120,8 +120,10 @@ int rsh_block_sums_device(rsh_ctx* ctx, const void* d_data, int64_t n, const rsh
                           void* d_weak, void* d_strong);
 int rsh_ctx_sync(rsh_ctx* ctx);
 /* Releases the context's pass-sized buffers -- the segment passes' HBM (rsh_*_batch: up to 2 x the segment_bytes
- * budget, 16 GiB by default), the Receiver passes', the host-input staging and the batched scan's tables and hit map --
- * after waiting for the context's streams.  The next call that needs them allocates them again.  A JVM holding
+ * budget, 16 GiB by default), the Receiver passes' and the host-input staging -- after waiting for the context's
+ * streams.  The next call that needs them allocates them again.  The batched scan's state (chunk index, hit map,
+ * descriptors, pinned event buffers: bounded by the largest segment's chunks and option chain_map_bytes) stays, so
+ * that the next segment scan costs what the previous one did.  A JVM holding
  * several contexts on one GPU (a local transfer's Generator and Sender) calls it after each segment; see
  * INTEGRATION.md "Per-context memory".  Replaces nothing in the reference (its buffers are Java heap). */
 int rsh_ctx_trim(rsh_ctx* ctx);

@@ -130,10 +130,9 @@ int rsh_ctx_trim(rsh_ctx* ctx) {
     for (PinnedBuf* b : {&ctx->h_stage, &ctx->h_rcv_ops[0], &ctx->h_rcv_ops[1], &ctx->h_out})
         b->release();
     if (ctx->h_win.cap > (1u << 20)) ctx->h_win.release();  // (a Receiver pass's pieces; the scan's windows are small)
-    if (ctx->batch) {  // the batched scan's tables, hit map and fiber stacks (rebuilt on the next batched call)
-        rsh::destroy_batch_state(ctx->batch);
-        ctx->batch = nullptr;
-    }
+    // The batched scan's state stays: its chunk index, hit map, descriptors, pinned event and
+    // table buffers and fiber stacks are bounded by the largest segment's chunk count and option chain_map_bytes
+    // (INTEGRATION.md "Per-context memory"), and rebuilding them cost the next segment scan ~3.4 ms of allocations.
     return RSH_OK;
 }
 

@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--trace", action="store_true", help="scan_trace = 2 on the first batched scan")
     ap.add_argument("--only", type=int, default=0, help="4 or 5: that configuration only (0: both)")
     ap.add_argument("--trace5", action="store_true", help="scan_trace = 1 on every config-5 step (stderr)")
+    ap.add_argument("--trim", action="store_true", help="config 4: after the reps, rsh_ctx_trim and one more rep")
+    ap.add_argument("--host", action="store_true",
+                    help="config 4 from host memory (rsh_block_sums_batch + rsh_match_scan_batch) instead of HBM")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -39,7 +42,7 @@ def main():
     L = R.lib()
     seed = np.frombuffer(bytes([1, 2, 3, 4]), np.uint8).copy()
     if a.only != 5:
-        config4(a, ctx, L, R, G, seed, out)
+        (config4_host if a.host else config4)(a, ctx, L, R, G, seed, out)
     if a.only != 4:
         config5(a, ctx, L, R, seed, out)
     ctx.close()
@@ -72,12 +75,14 @@ def config4(a, ctx, L, R, G, seed, out):
         sj[j].d_weak, sj[j].d_strong = bj[j].d_weak, bj[j].d_strong
         sj[j].ev, sj[j].ev_cap = evs[j].ctypes.data, cap
     gen, scan = [], []
-    for r in range(a.reps):
+    for r in range(a.reps + (1 if a.trim else 0)):
+        if a.trim and r == a.reps:
+            ctx.trim()  # the rep after it: what a segment costs after rsh_ctx_trim
         t = time.perf_counter()
         assert L.rsh_block_sums_batch_device(ctx.handle, bj, F, seed.ctypes.data) == 0
         ctx.sync()
         gen.append(round((time.perf_counter() - t) * 1e3, 3))
-        if a.trace and r == 0:
+        if a.trace and (r == 0 or r == a.reps):
             R.set_option("scan_trace", 2)
         t = time.perf_counter()
         assert L.rsh_match_scan_batch_device(ctx.handle, sj, F, seed.ctypes.data, None) == 0
@@ -87,6 +92,40 @@ def config4(a, ctx, L, R, G, seed, out):
     out["config4_half_scan_ms"] = scan
     del src, basis, w, s
     torch.cuda.empty_cache()
+
+
+def config4_host(a, ctx, L, R, G, seed, out):
+    """The config-4 shard from host memory (the segment calls a JVM makes): the Generator's segment call, then the
+    Sender's; after the reps (with --trim) rsh_ctx_trim and one more rep."""
+    S, B, dl, F = G.CONFIG4_FILE_BYTES, G.CONFIG4_B, G.CONFIG4_DL, a.files
+    dev = ctx.alloc(2 * S)
+    src = np.empty(F * S, np.uint8)
+    basis = np.empty(F * S, np.uint8)
+    for i in range(F):
+        L.rsh_fill_splitmix_device(ctx.handle, dev.ptr, S, G.config4_key(i), 0)
+        L.rsh_fill_splitmix_device(ctx.handle, dev.ptr.value + S, S, G.KEY_EDIT ^ G.config4_key(i), 0)
+        ctx.sync()
+        both = dev.download()
+        src[i * S:(i + 1) * S] = both[:S]
+        basis[i * S:(i + 1) * S] = both[S:]
+    dev.free()
+    basis.reshape(-1, B)[::2] = src.reshape(-1, B)[::2]
+    h = R.header_make(B, dl, S)
+    bjobs = [([basis[i * S:(i + 1) * S]], h) for i in range(F)]
+    gen, scan = [], []
+    for r in range(a.reps + (1 if a.trim else 0)):
+        if a.trim and r == a.reps:
+            ctx.trim()
+        t = time.perf_counter()
+        sums = ctx.block_sums_batch(bjobs, bytes(seed))
+        gen.append(round((time.perf_counter() - t) * 1e3, 3))
+        sjobs = [([src[i * S:(i + 1) * S]], h, sums[i][0], sums[i][1]) for i in range(F)]
+        t = time.perf_counter()
+        res, _ = ctx.match_scan_batch(sjobs, bytes(seed))
+        scan.append(round((time.perf_counter() - t) * 1e3, 3))
+        assert all(x[4] == 0 for x in res)
+    out["config4_host_generator_ms"] = gen
+    out["config4_host_scan_ms"] = scan
 
 
 def config5(a, ctx, L, R, seed, out):

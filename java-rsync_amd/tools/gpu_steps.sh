@@ -34,6 +34,8 @@
 #   devices      bench.py --workload files --devices N in one process (rsh_*_batch_multi from host memory): the same 128
 #                files over 1 context and over 2 (both on GPU 0 on a one-GPU box: the plumbing, not a scaling point)
 #   first        tools/first_call.py: the first calls on a fresh context against the later ones (config 4, config 5)
+#   first4       first_call.py --only 4 with --trim: the config-4 segment scan's first calls, device-resident (traced) and
+#                from host memory, and a segment after rsh_ctx_trim
 #   first-trace  rocprofv3 HIP API + kernel trace of first_call.py --only 5 --reps 2 (where the first step's time goes)
 #   copycb       rocprofv3 --memory-copy-trace over tools/queue_lat.hip (3 D2H hipMemcpyAsync per rep, no librsynchip):
 #                does the profiler report undelivered copy completions for plain runtime copies too
@@ -153,6 +155,13 @@ for step in "$@"; do
                 done
             done ;;
         first) run 300 python java-rsync_amd/tools/first_call.py > "$O/first_call.json" 2> "$O/first_call.err" ;;
+        first4) run 300 python java-rsync_amd/tools/first_call.py --only 4 --reps 4 --trim --trace > "$O/first4.json" \
+            2> "$O/first4.err"
+            run 300 python java-rsync_amd/tools/first_call.py --only 4 --reps 3 --trim --host > "$O/first4_host.json" \
+            2> "$O/first4_host.err" ;;
+        first4-trace) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --hip-trace --kernel-trace -d "$O/first4_trace" \
+            -o run --output-format csv -- python3 "$R/java-rsync_amd/tools/first_call.py" --only 4 --reps 2 --trim \
+            > "$O/first4_trace.json" 2> "$O/first4_trace.err") || exit 1 ;;
         first5) run 300 python java-rsync_amd/tools/first_call.py --only 5 --reps 4 --trace5 > "$O/first5.json" \
             2> "$O/first5.err" ;;
         first-trace) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --hip-trace --kernel-trace -d "$O/first_trace" \
