@@ -6,7 +6,7 @@
  * are never read from the environment.  The table is per process and applies to calls that start after a change.
  *  - settable in every build (tests force rare paths with them; a few are tunables): k1_gather, k1_shift,
  *    k1_unaligned, scan_trace, scan_segmented, scan_samples, batch_chain, batch_chain_prefix, host_cores,
- *    file_tile, file_tile_above, probe_long, segment_bytes, md5_width, chain_helpers, chain_map_bytes, time_gen,
+ *    file_tile, file_tile_above, probe_long, segment_bytes, md5_width, chain_helpers, chain_map_bytes, time_gen, batch_warm,
  *    fault_inject;
  *  - A/B switches, settable only in the diagnostics build (make diag: lib/diag/librsynchip.so, loaded by the
  *    tools through RSH_LIB); the product library answers RSH_E_INVAL and runs their defaults: scan_diag,

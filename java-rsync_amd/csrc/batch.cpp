@@ -893,6 +893,103 @@ using namespace rsh;
 namespace rsh {
 using namespace batch;
 
+// rsh_ctx_create (scan.cpp ctx_warm): the batched scan's and the batched Generator's state pre-sized for a segment of
+// `nfiles` files of n bytes at block length B, digest length dl -- the sizes scan_batch and block_sums_batch_claimed
+// grow them to for that segment (the same formulas, mirrored here) -- so that a context's first segment scan
+// allocates nothing (~11 ms of pinned allocations on config 4's first call).  Option batch_warm
+// sets nfiles (0: none); the shape is config 4's (128 MiB files, B 8192, dl 4): ~50 MiB pinned, ~0.25 GiB of HBM.
+hipError_t batch_warm(rsh_ctx* c, int32_t nfiles, int64_t n, int64_t B, int32_t dl) {
+    if (nfiles <= 0) return hipSuccess;
+    BatchState* S = state_of(c);
+    if (!S) return hipErrorOutOfMemory;
+    const int64_t NF = std::min<int64_t>(nfiles, kMaxLive);
+    const int64_t C = (n + B - 1) / B, na = C, nf = C, ns = pow2_at_least(2 * (uint64_t)C + 2);
+    const int64_t tw = NF * C, ts = NF * C * dl, tna = NF * na, tas = NF * na * dl, tnf = NF * nf, tns = NF * ns,
+                  thit = NF * pad16(16 + B), tw0 = NF * pad16(std::min<int64_t>(B, n));
+    hipError_t e = hipSuccess;
+    auto ok = [&](hipError_t x) {
+        if (e == hipSuccess) e = x;
+    };
+    // scan_batch: the per-file tables, sums and descriptors
+    ok(S->h_weak.ensure((size_t)tw * 4 + 4));
+    ok(S->h_strong.ensure((size_t)ts + 1));
+    ok(S->slots.ensure((size_t)tns * 8));
+    ok(S->src_weak.ensure((size_t)tna * 4));
+    ok(S->src_strong.ensure((size_t)tas + 1));
+    ok(S->flags.ensure((size_t)tnf + 1));
+    ok(S->haw.ensure((size_t)tna * 4));
+    ok(S->h_aw.ensure((size_t)tna * 4));
+    ok(S->h_as.ensure((size_t)tas + 1));
+    ok(S->h_fl.ensure((size_t)tnf + 1));
+    ok(S->h_files.ensure((size_t)NF * sizeof(ScanFile)));
+    ok(S->h_hit.ensure((size_t)thit));
+    ok(S->h_win0.ensure((size_t)tw0));
+    ok(S->first.ensure((size_t)NF * sizeof(ProbeOut)));
+    ok(S->h_first.ensure((size_t)NF * sizeof(ProbeOut)));
+    ok(S->bucket.ensure((size_t)NF * HIT_BUCKET_INTS * 4));
+    ok(S->h_bucket.ensure((size_t)NF * HIT_BUCKET_INTS * 4));
+    ok(S->h_copies.ensure((size_t)2 * NF * sizeof(CopyEnt)));
+    ok(S->h_ccopies.ensure((size_t)NF * sizeof(CopyEnt) + (size_t)3 * NF * sizeof(CopyEnt)));
+    ok(S->h_tabents.ensure((size_t)NF * sizeof(TableEnt)));
+    ok(S->h_flagents.ensure((size_t)NF * sizeof(FlagEnt)));
+    ok(S->h_flagents_a.ensure((size_t)NF * sizeof(FlagEnt)));
+    ok(S->ensure_file_abort(NF));
+    const int64_t nlead_all = NF * std::min<int64_t>(kLeadWindows, nf);
+    ok(S->h_lead.ensure((((size_t)(nlead_all + 1) * 4 + 63) & ~(size_t)63) + (size_t)(nlead_all + 1) * sizeof(GatherEnt)));
+    // the K1 descriptors of both phases (planned from the shapes alone: the data pointers only set the alignment)
+    std::vector<K1File> kf((size_t)NF), ka((size_t)NF), kb((size_t)NF);
+    const int64_t P = 16 * std::max<int64_t>(1, kWaveSlots / NF), na_a = std::min(na, P);
+    const uint8_t* const al = reinterpret_cast<const uint8_t*>(uintptr_t{4096});  // 128-B aligned stand-in
+    for (int64_t f = 0; f < NF; ++f) {
+        kf[(size_t)f] = K1File{al, n, (uint32_t)B, (uint32_t)dl, (uint32_t)na, nullptr, nullptr};
+        ka[(size_t)f] = K1File{al, std::min<int64_t>(n, na_a * B), (uint32_t)B, (uint32_t)dl, (uint32_t)na_a, nullptr, nullptr};
+        kb[(size_t)f] = K1File{al, n - na_a * B, (uint32_t)B, (uint32_t)dl, (uint32_t)(na - na_a), nullptr, nullptr};
+    }
+    std::vector<K1Plan> plans, pa, pb;
+    std::vector<K1Lane> lanes, la, lb;
+    int al0 = 16, al1 = 16, al2 = 16;
+    bool p0 = tail_gather_on(), p1 = tail_gather_on(), p2 = tail_gather_on();
+    const uint32_t ng = plan_block_sums_files(kf.data(), (int32_t)NF, &plans, &lanes, &al0, &p0);
+    const uint32_t nga = plan_block_sums_files(ka.data(), (int32_t)NF, &pa, &la, &al1, &p1);
+    const uint32_t ngb = na > na_a ? plan_block_sums_files(kb.data(), (int32_t)NF, &pb, &lb, &al2, &p2) : 0;
+    ok(S->k1_groups.ensure(((size_t)std::max(ng, nga + ngb) + 1) * sizeof(K1Group)));
+    ok(S->k1_plans.ensure((std::max(plans.size(), pa.size() + pb.size()) + 1) * sizeof(K1Plan)));
+    ok(S->k1_lanes.ensure((std::max(lanes.size(), la.size() + lb.size()) + 1) * sizeof(K1Lane)));
+    ok(S->h_sgroups.ensure((std::max(plans.size(), pa.size() + pb.size()) + 1) * sizeof(K1Plan)));
+    ok(S->h_slanes.ensure((std::max(lanes.size(), la.size() + lb.size()) + 1) * sizeof(K1Lane)));
+    // the chain walks: chunk indexes, descriptors, events, the phase-0 hit map
+    const int64_t kChainEvents = std::clamp<int64_t>(kChainEventBytes / (NF * (int64_t)sizeof(rsh_event)), 256, kChainEventsMax);
+    ok(S->kslots.ensure((size_t)tns * 8));
+    ok(S->h_kents.ensure((size_t)NF * sizeof(TableEnt)));
+    ok(S->h_chain.ensure((size_t)NF * sizeof(ChainFile)));
+    ok(S->h_chain_out.ensure((size_t)NF * sizeof(ChainOut)));
+    ok(S->h_chain_ev.ensure((size_t)(NF * kChainEvents) * sizeof(rsh_event)));
+    const bool wide = B >= 512 && B % 32 == 0 && CHAIN_TILE / B + 2 <= CHAIN_SEGS;
+    const int64_t words = wide && na > na_a ? NF * ((std::min<int64_t>(na_a * B, n - B + 1) + 31) / 32) : 0;
+    if (words > 0 && words * 8 <= opt(OPT_CHAIN_MAP_BYTES) && (size_t)words * 8 > S->chain_map.cap) {
+        ok(S->chain_map.ensure((size_t)words * 8));
+        if (e == hipSuccess) ok(hipMemset(S->chain_map.p, 0, S->chain_map.cap));  // no stale generation
+    }
+    ok(S->chain_help.ensure((size_t)NF * sizeof(ChainHelp)));
+    ok(S->h_chain_help.ensure((size_t)NF * sizeof(ChainHelp)));
+    ok(S->h_early.ensure(4096));
+    // the resolver rounds' staging (serve_round), at PinnedBuf's least size: ~40 us per pinned allocation
+    for (PinnedBuf* pb : {&S->h_fgw, &S->h_fjobs, &S->h_fout, &S->h_rcp, &S->h_iv, &S->h_tiles, &S->h_segs, &S->h_ptiles,
+                          &S->h_req, &S->h_gw, &S->h_gb, &S->h_ow, &S->h_ob, &S->h_win, &S->h_dkeys})
+        ok(pb->ensure(64 << 10));
+    for (DevBuf* db : {&S->fc_dev, &S->partials, &S->dslots, &S->d_probe}) ok(db->ensure(64 << 10));
+    for (hipEvent_t* ev : {&S->ev_fk, &S->ev_fa, &S->ev_scopy, &S->ev_sync, &S->ev_gcopy})
+        if (!*ev) ok(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    if (!S->ev_wa) ok(hipEventCreate(&S->ev_wa));
+    // block_sums_batch_claimed: the Generator's descriptors
+    ok(S->g_groups.ensure(((size_t)ng + 1) * sizeof(K1Group)));
+    ok(S->g_plans.ensure((plans.size() + 1) * sizeof(K1Plan)));
+    ok(S->g_lanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
+    ok(S->h_ggroups.ensure((plans.size() + 1) * sizeof(K1Plan)));
+    ok(S->h_glanes.ensure((lanes.size() + 1) * sizeof(K1Lane)));
+    return e;
+}
+
 // rsh_block_sums_batch_device with the context already claimed by the caller (segment.cpp builds the host forms
 // on it).
 int block_sums_batch_claimed(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t njobs, const uint8_t seed[4]) {

@@ -54,6 +54,8 @@ struct WorkerCap {
     explicit WorkerCap(int cap) : saved(value()) { value() = cap; }
     ~WorkerCap() { value() = saved; }
 };
+// batch.cpp: the batched scan's state pre-sized for a segment of nfiles files of n bytes (B, dl) at context creation
+hipError_t batch_warm(rsh_ctx* c, int32_t nfiles, int64_t n, int64_t B, int32_t dl);
 // batch.cpp: rsh_block_sums_batch_device / rsh_match_scan_batch_device for a caller that holds the context's
 // claim (segment.cpp's host-memory forms)
 int block_sums_batch_claimed(rsh_ctx* ctx, const rsh_block_job* jobs, int32_t njobs, const uint8_t seed[4]);
@@ -164,7 +166,7 @@ struct rsh_ctx {
     // launch never writes the sums (or their host copies) of the launch it replaces while that one drains
     DevBuf ph_weak[2], ph_strong[2];
     DevBuf segs;                                 // segmented K1 descriptors (prefix + phase speculation)
-    DevBuf slots, dslots, dkeys, pos, out, first, win, ivbuf, tilebuf, haw, partials, bucket;
+    DevBuf slots, dslots, out, first, haw, partials, bucket;
     DevBuf seg_data, seg_tab;                    // rsh_*_batch (segment.cpp): a pass's files and tables / sums
     DevBuf rcv[2], rcv_ops[2];                   // rsh_receiver_combine_batch: two pass buffers and their gather ops
     DevBuf prep_dev;                             // the stamped launches' counters and the prep launch's scratch
@@ -214,7 +216,7 @@ struct rsh_ctx {
         if (batch) rsh::destroy_batch_state(batch);
         for (DevBuf* b : {&data, &weak, &strong, &src_weak, &src_strong, &flags, &ph_weak[0], &ph_strong[0],
                           &ph_weak[1], &ph_strong[1], &slots, &dslots,
-                          &dkeys, &pos, &out, &first, &win, &ivbuf, &tilebuf, &haw, &partials, &bucket, &seg_data, &seg_tab,
+                          &out, &first, &haw, &partials, &bucket, &seg_data, &seg_tab,
                           &rcv[0], &rcv[1], &rcv_ops[0], &rcv_ops[1], &prep_dev, &fc_dev})
             b->release();
         for (PinnedBuf* b : {&h_weak, &h_strong, &h_aw, &h_as, &h_fl, &h_pw[0], &h_ps[0], &h_pw[1], &h_ps[1], &h_lead, &h_pos, &h_out, &h_iv,

@@ -40,6 +40,7 @@ enum Opt : int {
     OPT_CHAIN_HELPERS,     // phase-0 walk: extra workgroups mapping searching files' prefixes (-1: CUs - files; 0: no map)
     OPT_CHAIN_MAP_BYTES,   // ... the map's HBM budget (bytes; above it the walks search tile by tile)
     OPT_TIME_GEN,          // 1: rsh_block_sums_device's K1 records timing events (rsh_debug_kernel_ms)
+    OPT_BATCH_WARM,        // rsh_ctx_create pre-sizes the batched scan's state for this many 128 MiB files (0: none)
     OPT_FAULT_INJECT,      // tests only: bit 0 a segment / Receiver pass's HBM allocation fails, bit 1 a segment's copies fail,
                            // bit 2 bits 0 / 1 only on member 1 of a multi-context call (multi.cpp)
     // ---- A/B switches (the diagnostics build reads them; the product build uses the defaults) ----
@@ -79,7 +80,8 @@ inline constexpr OptInfo kOpts[OPT_COUNT] = {
     {"batch_chain", 1, false},        {"batch_chain_prefix", -1, false}, {"host_cores", 0, false},
     {"file_tile", 4LL << 30, false},  {"file_tile_above", 32LL << 30, false}, {"probe_long", 1, false},
     {"segment_bytes", 16LL << 30, false}, {"md5_width", 0, false}, {"chain_helpers", -1, false},
-    {"chain_map_bytes", 1LL << 30, false}, {"time_gen", 1, false}, {"fault_inject", 0, false},
+    {"chain_map_bytes", 1LL << 30, false}, {"time_gen", 1, false}, {"batch_warm", 128, false},
+    {"fault_inject", 0, false},
     {"scan_diag", 0, true},           {"scan_phase", 1, true},       {"scan_phase_guess", 1, true},
     {"scan_preprobe", 1, true},       {"scan_sample", 1, true},      {"scan_spec_order", 1, true},
     {"scan_early", 1, true},          {"scan_wait", 1, true},        {"scan_defer_steps", 4, true},

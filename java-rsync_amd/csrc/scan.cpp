@@ -124,6 +124,9 @@ hipError_t ctx_warm(rsh_ctx* c) {
     ok(c->bucket.ensure(rsh::HIT_BUCKET_INTS * sizeof(int32_t)));
     ok(c->first.ensure(kFirstSlots * sizeof(rsh::ProbeOut)));
     ok(c->dslots.ensure(kSmall));
+    ok(c->fc_dev.ensure(kSmall));  // the batched flush chain's gathers (a stale digest's first round trip)
+    // the batched scan's state for a config-4 shard (option batch_warm files of 128 MiB, B 8192; dl 4 covers dl 3)
+    ok(rsh::batch_warm(c, (int32_t)rsh::opt(rsh::OPT_BATCH_WARM), 128LL << 20, 8192, 4));
     // the runtime's copy and fill paths, on each of the context's streams: the first D2H copy of a process took
     // 6.8 ms (the single-file scan's table download, its first call in a fresh process: scan_trace, profiles/r5)
     if (e == hipSuccess) {
@@ -139,6 +142,8 @@ hipError_t ctx_warm(rsh_ctx* c) {
             // table-sized D2H is no longer on any scan path, and the profiler's async-copy tracing never saw its
             // completion (one per stream here: r5z2 copycb_files, hipMemcpyAsync of 512 KiB into pinned memory)
             ok(copy_to_host({rsh::CopyEnt{d, c->h_weak.as<uint8_t>(), 512 << 10}}, st));
+            // the stream-write path (the runtime's own blit kernel): the abort of a stopped speculation
+            ok(hipStreamWriteValue32(st, d + 16384, 0, 0));
             ok(hipStreamSynchronize(st));
         }
     }
