@@ -850,13 +850,14 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         }
     };
     const int nct = copy_bytes > (1 << 20) ? std::min<int>(8, std::max(1, call_cores())) : 1;
-    if (nct > 1 && copy_files.size() > 1) {
-        std::vector<std::thread> ct;
+    if (nct > 1 && copy_files.size() > 1) {  // on the context's persistent pool (HostPool, batch.h)
         const size_t per = (copy_files.size() + (size_t)nct - 1) / (size_t)nct;
-        for (size_t i0 = per; i0 < copy_files.size(); i0 += per)
-            ct.emplace_back(copy_range, i0, std::min(copy_files.size(), i0 + per));
-        copy_range(0, std::min(per, copy_files.size()));
-        for (std::thread& x : ct) x.join();
+        const int parts = (int)((copy_files.size() + per - 1) / per);
+        S->pool.ensure(parts - 1);
+        const std::function<void(int)> part = [&](int k) {
+            copy_range((size_t)k * per, std::min(copy_files.size(), (size_t)(k + 1) * per));
+        };
+        S->pool.run(parts, part);
     } else {
         copy_range(0, copy_files.size());
     }
@@ -973,10 +974,14 @@ hipError_t batch_warm(rsh_ctx* c, int32_t nfiles, int64_t n, int64_t B, int32_t 
     ok(S->chain_help.ensure((size_t)NF * sizeof(ChainHelp)));
     ok(S->h_chain_help.ensure((size_t)NF * sizeof(ChainHelp)));
     ok(S->h_early.ensure(4096));
+    S->pool.ensure(7);  // the events' copy threads (scan_batch: up to 8 parts, the caller takes one)
     // the resolver rounds' staging (serve_round), at PinnedBuf's least size: ~40 us per pinned allocation
-    for (PinnedBuf* pb : {&S->h_fgw, &S->h_fjobs, &S->h_fout, &S->h_rcp, &S->h_iv, &S->h_tiles, &S->h_segs, &S->h_ptiles,
-                          &S->h_req, &S->h_gw, &S->h_gb, &S->h_ow, &S->h_ob, &S->h_win, &S->h_dkeys})
+    for (PinnedBuf* pb : {&S->h_fjobs, &S->h_fout, &S->h_rcp, &S->h_req, &S->h_gw, &S->h_gb, &S->h_ow, &S->h_ob, &S->h_win,
+                          &S->h_dkeys})
         ok(pb->ensure(64 << 10));
+    // ... and a stale digest's batched flush chain at its largest (4096 intervals: its gathers, intervals, tiles and
+    // segments; a staging buffer that grows frees the old one first, ~0.3 ms on the first call)
+    for (PinnedBuf* pb : {&S->h_fgw, &S->h_iv, &S->h_tiles, &S->h_segs, &S->h_ptiles}) ok(pb->ensure(512 << 10));
     for (DevBuf* db : {&S->fc_dev, &S->partials, &S->dslots, &S->d_probe}) ok(db->ensure(64 << 10));
     for (hipEvent_t* ev : {&S->ev_fk, &S->ev_fa, &S->ev_scopy, &S->ev_sync, &S->ev_gcopy})
         if (!*ev) ok(hipEventCreateWithFlags(ev, hipEventDisableTiming));

@@ -49,7 +49,65 @@
 
 namespace rsh {
 
+// A few persistent host threads for a batched call's bulk host copies (the events back to the callers' buffers):
+// threads created per call paid a fresh stack mapping each (~30 us; glibc caches only 40 MiB of stacks), the first call
+// for all of them.  run(n, f) calls f(0 .. n-1) on the pool and the calling thread, and returns when all are done.
+struct HostPool {
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    std::vector<std::thread> th;
+    const std::function<void(int)>* job = nullptr;
+    int njobs = 0, next = 0, done = 0;
+    uint64_t gen = 0;
+    bool quit = false;
+    void ensure(int n) {
+        while ((int)th.size() < n) th.emplace_back([this] { work(); });
+    }
+    void work() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> l(mu);
+        for (;;) {
+            cv_work.wait(l, [&] { return quit || gen != seen; });
+            if (quit) return;
+            seen = gen;
+            while (next < njobs) {
+                const int i = next++;
+                l.unlock();
+                (*job)(i);
+                l.lock();
+                if (++done == njobs) cv_done.notify_one();
+            }
+        }
+    }
+    void run(int n, const std::function<void(int)>& f) {
+        if (n <= 0) return;
+        std::unique_lock<std::mutex> l(mu);
+        job = &f;
+        njobs = n, next = 0, done = 0;
+        ++gen;
+        cv_work.notify_all();
+        while (next < njobs) {  // the caller takes part
+            const int i = next++;
+            l.unlock();
+            f(i);
+            l.lock();
+            ++done;
+        }
+        cv_done.wait(l, [&] { return done == njobs; });
+        job = nullptr;
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> l(mu);
+            quit = true;
+        }
+        cv_work.notify_all();
+        for (std::thread& t : th) t.join();
+    }
+};
+
 struct BatchState {
+    HostPool pool;  // the events' copies (scan_batch)
     // Generator batch
     DevBuf g_groups, g_lanes, g_plans, k1_plans;  // K1 groups are expanded on the device from per-file plans
     // Sender batch: device

@@ -23,6 +23,73 @@
 #include "options.h"
 #include "rsync_hip_debug.h"
 
+namespace {
+// rsh_ctx_create, after ctx_warm: one device-resident Generator + Sender pass of each kind over a small synthetic pair --
+// a 50%-modified 8 MiB file at B = 131072 (config 5's shape: the tentative launch and its stop, the poisoned scan's
+// flush chain) and a segment of two 50%-modified 1 MiB files at B = 8192 (config 4's: the chain walks, an early
+// resolution, the events' copies) -- so that a context's first real call finds every path it takes run once: the
+// kernels' first dispatches, the runtime's paths and the library's own code.  A few milliseconds.
+int warm_calls(rsh_ctx* c) {
+    const uint8_t seed[4] = {1, 2, 3, 4};
+    constexpr int64_t n5 = 8 << 20, B5 = 131072, n4 = 1 << 20, B4 = 8192;
+    const int64_t bytes = 2 * n5 + 4 * n4;
+    void* d = nullptr;
+    if (hipMalloc(&d, (size_t)bytes + 4096) != hipSuccess) return RSH_E_DEVICE;
+    uint8_t* src5 = static_cast<uint8_t*>(d);
+    uint8_t* bas5 = src5 + n5;
+    uint8_t* src4 = bas5 + n5;  // two files, then their two bases
+    uint8_t* bas4 = src4 + 2 * n4;
+    int rc = RSH_OK;
+    auto fill_pair = [&](uint8_t* src, uint8_t* bas, int64_t n, int64_t B, uint64_t key) {
+        // the basis keeps the source's even blocks and takes its odd ones from another stream
+        if (rc == RSH_OK && (rsh_fill_splitmix_device(c, src, n, key, 0) != RSH_OK ||
+                             rsh_fill_splitmix_device(c, bas, n, key ^ 0xED17, 0) != RSH_OK ||
+                             hipMemcpy2DAsync(bas, (size_t)(2 * B), src, (size_t)(2 * B), (size_t)B, (size_t)(n / (2 * B)),
+                                              hipMemcpyDeviceToDevice, c->stream) != hipSuccess))
+            rc = RSH_E_DEVICE;
+    };
+    fill_pair(src5, bas5, n5, B5, 0x5EED5EED00000005ull);
+    fill_pair(src4, bas4, 2 * n4, B4, 0x5EED5EED00000004ull);
+    rsh_header h5{}, h4{};
+    if (rc == RSH_OK) rc = rsh_header_make((int32_t)B5, 4, n5, &h5);
+    if (rc == RSH_OK) rc = rsh_header_make((int32_t)B4, 3, n4, &h4);
+    const int64_t C5 = h5.chunk_count, C4 = h4.chunk_count;
+    void* t = nullptr;
+    if (rc == RSH_OK && hipMalloc(&t, (size_t)(C5 * 8 + 2 * C4 * 8) + 256) != hipSuccess) rc = RSH_E_DEVICE;
+    int32_t* w5 = static_cast<int32_t*>(t);
+    uint8_t* s5 = reinterpret_cast<uint8_t*>(w5 + C5);
+    int32_t* w4 = reinterpret_cast<int32_t*>(s5 + C5 * 4);
+    uint8_t* s4 = reinterpret_cast<uint8_t*>(w4 + 2 * C4);
+    std::vector<rsh_event> ev((size_t)(4 * (C5 + C4) + 64));
+    int64_t n_ev = 0, lit = 0, mat = 0;
+    if (rc == RSH_OK) rc = rsh_block_sums_device(c, bas5, n5, &h5, seed, w5, s5);
+    if (rc == RSH_OK)
+        rc = rsh_match_scan_device(c, src5, n5, &h5, w5, s5, seed, ev.data(), (int64_t)ev.size(), &n_ev, &lit, &mat,
+                                   nullptr);
+    if (rc == RSH_OK) {
+        rsh_block_job bj[2];
+        rsh_scan_job sj[2];
+        for (int f = 0; f < 2; ++f) {
+            bj[f] = rsh_block_job{bas4 + f * n4, n4, h4, w4 + f * C4, s4 + f * C4 * 3};
+            sj[f] = rsh_scan_job{};
+            sj[f].d_src = src4 + f * n4;
+            sj[f].n = n4;
+            sj[f].h = h4;
+            sj[f].d_weak = bj[f].d_weak;
+            sj[f].d_strong = bj[f].d_strong;
+            sj[f].ev = ev.data() + (size_t)f * (ev.size() / 2);
+            sj[f].ev_cap = (int64_t)ev.size() / 2;
+        }
+        rc = rsh_block_sums_batch_device(c, bj, 2, seed);
+        if (rc == RSH_OK) rc = rsh_match_scan_batch_device(c, sj, 2, seed, nullptr);
+    }
+    if (rsh_ctx_sync(c) != RSH_OK && rc == RSH_OK) rc = RSH_E_DEVICE;
+    if (t) (void)hipFree(t);
+    (void)hipFree(d);
+    return rc;
+}
+}  // namespace
+
 extern "C" {
 
 int rsh_abi_version(void) { return RSH_ABI_VERSION; }
@@ -88,7 +155,7 @@ int rsh_ctx_create(int device, rsh_ctx** out) {
         delete c;
         return RSH_E_DEVICE;
     }
-    if (ctx_warm(c) != hipSuccess) {
+    if (ctx_warm(c) != hipSuccess || warm_calls(c) != RSH_OK) {
         (void)hipStreamSynchronize(c->stream);
         delete c;
         return RSH_E_DEVICE;

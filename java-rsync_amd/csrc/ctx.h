@@ -73,6 +73,13 @@ constexpr int32_t kMaxBlockLength = 1 << 17;  // Checksum.java:151
 // speculation is launched at once and the resolver waits for it instead of taking head-mode steps.
 constexpr int64_t kLeadWindows = 32;
 
+// Option scan_trace = 1: one stderr line per buffer allocation (where a call's first-use costs go)
+inline void trace_alloc(const char* what, size_t n, std::chrono::steady_clock::time_point t0) {
+    if (rsh::opt(rsh::OPT_SCAN_TRACE) == 1)
+        fprintf(stderr, "[rsh] %-10s %10zu %9.3f ms\n", what, n,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -81,8 +88,10 @@ struct DevBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
+        const auto t0 = std::chrono::steady_clock::now();
         hipError_t e = hipMalloc(&p, n ? n : 1);
         if (e == hipSuccess) cap = n;
+        trace_alloc("dev_alloc", n, t0);
         return e;
     }
     template <class T>
@@ -108,8 +117,10 @@ struct PinnedBuf {
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
+        const auto t0 = std::chrono::steady_clock::now();
         hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
         if (e == hipSuccess) cap = n;
+        trace_alloc("pin_alloc", n, t0);
         return e;
     }
     template <class T>

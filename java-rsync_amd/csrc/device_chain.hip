@@ -1260,8 +1260,20 @@ hipError_t launch_chunk_index(const TableEnt* ents, uint32_t nfiles, int32_t max
 // A kernel that does nothing: its first launch makes the runtime load this file's code object (the chain walk) on a
 // fresh context, which rsh_ctx_create pays instead of the first segment scan (launch_warm).
 __global__ void warm_chain_kernel() {}
+// Scratch: chain_advance_kernel spills ~572 B per lane (256 VGPRs at two waves per SIMD) and its out-of-line helpers
+// keep their saved registers there.  The runtime sizes a queue's scratch at the first dispatch that needs it, which held
+// up the first segment scan's walk by ~0.7 ms; this kernel needs more per lane than the walk, over as many waves as a
+// walk launch can have (256 workgroups of 512), so rsh_ctx_create pays that instead (on the context stream, the walk's).
+constexpr int kWarmScratchWords = 160;  // 640 B per lane
+__global__ __launch_bounds__(CHAIN_THREADS) void warm_scratch_kernel(int32_t sel, int32_t* out) {
+    volatile int32_t a[kWarmScratchWords];
+    for (int i = 0; i < kWarmScratchWords; ++i) a[i] = i ^ sel;
+    const int32_t v = a[(threadIdx.x + (uint32_t)sel) % kWarmScratchWords];
+    if (out && v == 0x7FFFFFFF) out[0] = v;  // never taken (out is null): keeps the array
+}
 hipError_t launch_warm_chain(hipStream_t s) {
     hipLaunchKernelGGL(warm_chain_kernel, dim3(1), dim3(64), 0, s);
+    hipLaunchKernelGGL(warm_scratch_kernel, dim3(256), dim3(CHAIN_THREADS), 0, s, 1, nullptr);
     return hipGetLastError();
 }
 

@@ -484,11 +484,17 @@ RSH_HD void md5_digest_bytes(const Md5State& st, uint8_t out[16]) {
 
 // The first dl bytes of the digest as the Sender keeps them: Arrays.copyOf(digest, dl)
 // (Sender.java:1262) zero-pads past the 16 digest bytes when a peer's header asks for dl > 16.
+// Every byte index is a compile-time constant: a runtime-indexed word (even a select chain over k) became a private
+// array indexed through scratch memory, which put scratch into every K1 (its first launch on a queue then waited for
+// the runtime's scratch allocation).
 RSH_HD void store_digest(uint8_t* o, const Md5State& st, uint32_t dl) {
-    for (uint32_t k = 0; k < dl; ++k) {
-        const uint32_t word = k < 4 ? st.a : k < 8 ? st.b : k < 12 ? st.c : st.d;
-        o[k] = k < 16 ? (uint8_t)(word >> (8 * (k & 3))) : (uint8_t)0;
-    }
+    const uint32_t w[4] = {st.a, st.b, st.c, st.d};
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i)
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+            if (4 * i + j < dl) o[4 * i + j] = (uint8_t)(w[i] >> (8 * j));
+    for (uint32_t k = 16; k < dl; ++k) o[k] = 0;
 }
 
 }  // namespace rsh

@@ -125,6 +125,8 @@ hipError_t ctx_warm(rsh_ctx* c) {
     ok(c->first.ensure(kFirstSlots * sizeof(rsh::ProbeOut)));
     ok(c->dslots.ensure(kSmall));
     ok(c->fc_dev.ensure(kSmall));  // the batched flush chain's gathers (a stale digest's first round trip)
+    for (PinnedBuf* b : {&c->h_fjobs, &c->h_fout}) ok(b->ensure(kSmall));
+    ok(c->h_fgw.ensure(512 << 10));  // ... its gather list at 4096 intervals
     // the batched scan's state for a config-4 shard (option batch_warm files of 128 MiB, B 8192; dl 4 covers dl 3)
     ok(rsh::batch_warm(c, (int32_t)rsh::opt(rsh::OPT_BATCH_WARM), 128LL << 20, 8192, 4));
     // the runtime's copy and fill paths, on each of the context's streams: the first D2H copy of a process took
@@ -148,6 +150,8 @@ hipError_t ctx_warm(rsh_ctx* c) {
         }
     }
     ok(hipStreamSynchronize(c->stream));
+    // a host thread: every scan digests window 0 on one (glibc keeps the stack of a finished thread for the next)
+    std::thread([] {}).join();
     return e;
 }
 
@@ -424,13 +428,19 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         const int rc = table_wait();
         if (rc != RSH_OK) return rc;
     }
+    // the digest of window 0 on a host thread, started once the lead check below has decided on the speculation: the
+    // thread's creation (tens of microseconds) then no longer delays a tentative launch's stop
     uint8_t md5_0[16];
-    std::thread md5_0_thread([&] {
-        rsh::HostMd5 hm;
-        hm.update(c->h_win0.as<uint8_t>(), (size_t)w0);
-        hm.update(seed, 4);
-        hm.final(md5_0);
-    });
+    std::thread md5_0_thread;
+    auto start_md5_0 = [&] {
+        md5_0_thread = std::thread([&] {
+            rsh::HostMd5 hm;
+            hm.update(c->h_win0.as<uint8_t>(), (size_t)w0);
+            hm.update(seed, 4);
+            hm.final(md5_0);
+        });
+    };
+    if (!on_ctx) start_md5_0();
     struct Joiner {
         std::thread& t;
         ~Joiner() {
@@ -448,6 +458,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     const bool seg_on = rsh::opt(rsh::OPT_SCAN_SEGMENTED) != 0;
     const bool wait_on = rsh::opt(rsh::OPT_SCAN_WAIT) != 0;
     const bool sample_on = rsh::opt(rsh::OPT_SCAN_SAMPLE) != 0;
+    if (CallTrace::on()) fprintf(stderr, "[rsh] lead_check at %9.3f ms\n", ms_since(t0));
     if (head && nlead > 0 && (!spec_launched || spec_tentative)) {
         // the table's weak sum at sample i: from the prep launch (scan_spec_queue) or the downloaded table
         auto tw_at = [&](int64_t i) { return lead_tw ? lead_tw[i] : host_weak[samp[(size_t)i]]; };
@@ -472,6 +483,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             }
         }
         if (spec_tentative && (!eager || cover < na)) {  // stop the tentative launch; later ones take a new generation
+            CallTrace tr("spec_stop", cover);
             RSH_HIP(hipStreamWriteValue32(rs, c->abort_word, (uint32_t)gen, 0));
             gen = ++c->gen;
             spec_launched = spec_tentative = false;
@@ -498,6 +510,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             CallTrace tr("table_work", C);
             rc = table_work();
         }
+        start_md5_0();  // beside the table's download
         if (rc == RSH_OK) {
             CallTrace tr("table_wait", C);
             rc = table_wait();

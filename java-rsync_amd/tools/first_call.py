@@ -27,6 +27,10 @@ def main():
     ap.add_argument("--trace", action="store_true", help="scan_trace = 2 on the first batched scan")
     ap.add_argument("--only", type=int, default=0, help="4 or 5: that configuration only (0: both)")
     ap.add_argument("--trace5", action="store_true", help="scan_trace = 1 on every config-5 step (stderr)")
+    ap.add_argument("--preheat", type=float, default=0.0,
+                    help="seconds of busy GPU work (torch, not the library) before the first library call: the chip's "
+                         "clocks ramp under load after idle, which no library call controls")
+    ap.add_argument("--trace-allocs", action="store_true", help="with --trace: scan_trace = 1 (every allocation)")
     ap.add_argument("--trim", action="store_true", help="config 4: after the reps, rsh_ctx_trim and one more rep")
     ap.add_argument("--host", action="store_true",
                     help="config 4 from host memory (rsh_block_sums_batch + rsh_match_scan_batch) instead of HBM")
@@ -38,6 +42,13 @@ def main():
     out = {}
     t = time.perf_counter()
     ctx = R.Context(0)
+    if a.preheat > 0:  # after the context: its creation's own launches are part of the setup, not of the calls
+        x = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+        t1 = time.perf_counter()
+        while time.perf_counter() - t1 < a.preheat:
+            x.add_(1)
+        torch.cuda.synchronize()
+        del x
     out["ctx_create_ms"] = round((time.perf_counter() - t) * 1e3, 3)
     L = R.lib()
     seed = np.frombuffer(bytes([1, 2, 3, 4]), np.uint8).copy()
@@ -67,7 +78,9 @@ def config4(a, ctx, L, R, G, seed, out):
     bj = (R.BlockJob * F)()
     sj = (R.ScanJob * F)()
     cap = C + S // B + 4096
-    evs = [np.zeros(cap, R.EVENT_DTYPE) for _ in range(F)]
+    # the caller's event buffers written once (their pages faulted in): first-touch faults are the caller's memory, not
+    # the library's first-call cost
+    evs = [np.full(cap, 0, R.EVENT_DTYPE) for _ in range(F)]
     for j in range(F):
         bj[j].d_data, bj[j].n, bj[j].h = basis.data_ptr() + j * S, S, h
         bj[j].d_weak, bj[j].d_strong = w.data_ptr() + 4 * j * C, s.data_ptr() + j * C * dl
@@ -83,7 +96,7 @@ def config4(a, ctx, L, R, G, seed, out):
         ctx.sync()
         gen.append(round((time.perf_counter() - t) * 1e3, 3))
         if a.trace and (r == 0 or r == a.reps):
-            R.set_option("scan_trace", 2)
+            R.set_option("scan_trace", 1 if a.trace_allocs else 2)
         t = time.perf_counter()
         assert L.rsh_match_scan_batch_device(ctx.handle, sj, F, seed.ctypes.data, None) == 0
         scan.append(round((time.perf_counter() - t) * 1e3, 3))
@@ -145,7 +158,7 @@ def config5(a, ctx, L, R, seed, out):
     C5 = h5.chunk_count
     w5 = torch.empty(C5, dtype=torch.int32, device="cuda")
     s5 = torch.empty(C5 * dl5, dtype=torch.uint8, device="cuda")
-    ev = np.zeros(C5 + n // B5 + 4096, R.EVENT_DTYPE)
+    ev = np.full(C5 + n // B5 + 4096, 0, R.EVENT_DTYPE)  # (pages faulted in, as config4's)
     n_ev, lit, mat = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     st = R.ScanStats()
     steps, k1 = [], []

@@ -155,14 +155,14 @@ for step in "$@"; do
                 done
             done ;;
         first) run 300 python java-rsync_amd/tools/first_call.py > "$O/first_call.json" 2> "$O/first_call.err" ;;
-        first4) run 300 python java-rsync_amd/tools/first_call.py --only 4 --reps 4 --trim --trace > "$O/first4.json" \
+        first4) run 300 python java-rsync_amd/tools/first_call.py --only 4 --reps 4 --trim --trace $FIRST4_ARGS > "$O/first4.json" \
             2> "$O/first4.err"
             run 300 python java-rsync_amd/tools/first_call.py --only 4 --reps 3 --trim --host > "$O/first4_host.json" \
             2> "$O/first4_host.err" ;;
         first4-trace) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --hip-trace --kernel-trace -d "$O/first4_trace" \
             -o run --output-format csv -- python3 "$R/java-rsync_amd/tools/first_call.py" --only 4 --reps 2 --trim \
             > "$O/first4_trace.json" 2> "$O/first4_trace.err") || exit 1 ;;
-        first5) run 300 python java-rsync_amd/tools/first_call.py --only 5 --reps 4 --trace5 > "$O/first5.json" \
+        first5) run 300 python java-rsync_amd/tools/first_call.py --only 5 --reps 4 --trace5 $FIRST5_ARGS > "$O/first5.json" \
             2> "$O/first5.err" ;;
         first-trace) (cd /tmp && export TMPDIR=/tmp && run 300 rocprofv3 --hip-trace --kernel-trace -d "$O/first_trace" \
             -o run --output-format csv -- python3 "$R/java-rsync_amd/tools/first_call.py" --only 5 --reps 2 \
