@@ -206,6 +206,8 @@ struct ScanFile {
                                       // first hit, then per listed hit j {count, idx[LISTED_IDX]}
     uint8_t* hit;                     // pinned host: T(p) in bytes 0..3, window k of the k-th smallest listed
                                       // hit at 16 + k B (k < HIT_WINDOWS; k = 0: the first hit)
+    int32_t next_sums;                // 0..NEXT_SUMS_MAX: T(p + k B) of the first hit p for k = 1..next_sums too, into hit bytes 4 k
+                                      // (the phase guess's check of four consecutive windows in the same round trip)
     int32_t nsmall;                   // > 0: the round's key set is these few keys (a stale digest's chunks),
     uint32_t small[PROBE_SMALL_KEYS]; // compared in registers instead of looked up in slots
 };
@@ -313,6 +315,8 @@ struct CopyFew {
     uint32_t n;
 };
 hipError_t launch_copy_few(const CopyFew& f, hipStream_t s);
+// The same ranges by one workgroup, then `gen` into the pinned `stamp` (the host spins on it).
+hipError_t launch_copy_few_stamped(const CopyFew& f, int* stamp, int gen, hipStream_t s);
 // n bytes of device memory into pinned host memory (h_dst 16-byte aligned), by a kernel.
 hipError_t launch_copy_to_host(const uint8_t* d_src, int64_t n, uint8_t* h_dst, hipStream_t s);
 // Byte ranges between arbitrary (unaligned) device addresses: one op per workgroup, 16-byte stores to

@@ -206,6 +206,27 @@ __global__ __launch_bounds__(256) void copy_few_kernel(CopyFew f) {
     }
 }
 
+// One workgroup copies every range (a probe's few KiB of results), then stores `gen` into the pinned stamp: the
+// host spins on the stamp (scan.cpp wait_stamp) instead of waking from a stream synchronisation.
+__global__ __launch_bounds__(256) void copy_few_stamped_kernel(CopyFew f, int* stamp, int gen) {
+    __builtin_amdgcn_s_setprio(3);
+    for (uint32_t k = 0; k < f.n; ++k) {
+        const CopyEnt e = f.e[k];
+        for (int64_t o = 16 * (int64_t)threadIdx.x; o < e.len; o += 16 * (int64_t)blockDim.x) copy_piece(e.src, e.dst, e.len, o);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(stamp, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+hipError_t launch_copy_few_stamped(const CopyFew& f, int* stamp, int gen, hipStream_t s) {
+    hipLaunchKernelGGL(copy_few_stamped_kernel, dim3(1), dim3(256), 0, s, f, stamp, gen);
+    return hipGetLastError();
+}
+
 hipError_t launch_copy_few(const CopyFew& f, hipStream_t s) {
     int64_t mx = 0;
     for (uint32_t i = 0; i < f.n; ++i) mx = std::max(mx, f.e[i].len);

@@ -281,7 +281,8 @@ void probe_partials(std::vector<ProbeTile>* tiles, size_t t0, int64_t B, int32_t
     }
 }
 
-// grid (1 + 16, nreq): block 0 computes T(p) and the key, blocks 1..16 copy the window.
+// grid (1 + 16 W + NEXT_SUMS_MAX, nreq): block 0 computes T(p) and the key, blocks 1..16 W copy the windows,
+// the last ones T(p + k B) for k <= next_sums (the phase guess's checks, in parallel with T(p)).
 __global__ __launch_bounds__(256) void hit_window_kernel(const ScanFile* __restrict__ files,
                                                          const ProbeIv* __restrict__ ivs,
                                                          const int32_t* __restrict__ req) {
@@ -318,6 +319,20 @@ __global__ __launch_bounds__(256) void hit_window_kernel(const ScanFile* __restr
             F.bucket[1] = (int32_t)((((uint32_t)T + I.e_lo) & 0xFFFFu) | ((((uint32_t)T >> 16) + ehi) << 16));
         }
         if (threadIdx.x < PROBE_HITS_CAP) F.bucket[2 + HIT_BUCKET_CAP + (1 + LISTED_IDX) * threadIdx.x] = 0;
+        return;
+    }
+    if (blockIdx.x > 16 * HIT_WINDOWS) {  // block 16 W + k: the window at p + k B (the next_sums that follow it)
+        const int k = (int)(blockIdx.x - 16 * HIT_WINDOWS);
+        if (k > F.next_sums) return;
+        const int64_t pk = p + k * B, wk = n - pk < B ? n - pk : B;
+        int32_t u[2] = {0, 0};
+        if (wk > 0) range_sums(data, n, pk, pk + wk, pk, u[0], u[1]);
+        block_reduce<2>(u, sh);
+        if (threadIdx.x == 0) {
+            const uint32_t S1 = (uint32_t)u[0];
+            const uint32_t S2 = (uint32_t)(wk > 0 ? wk : 0) * S1 - (uint32_t)u[1];
+            reinterpret_cast<int32_t*>(F.hit)[k] = (int32_t)((S1 & 0xFFFFu) | (S2 << 16));
+        }
         return;
     }
     // blocks 1 + 16 k .. 16 k + 16 copy window k: the k-th smallest listed hit (k = 0 is the first hit; the
@@ -394,7 +409,7 @@ __global__ __launch_bounds__(256) void hit_bucket_kernel(const ScanFile* __restr
 hipError_t launch_hit_window(const ScanFile* files, const ProbeIv* ivs, const int32_t* req, int32_t nreq, int32_t max_C,
                              hipStream_t s) {
     if (nreq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(hit_window_kernel, dim3(1 + 16 * HIT_WINDOWS, (uint32_t)nreq), dim3(256), 0, s, files, ivs, req);
+    hipLaunchKernelGGL(hit_window_kernel, dim3(1 + 16 * HIT_WINDOWS + NEXT_SUMS_MAX, (uint32_t)nreq), dim3(256), 0, s, files, ivs, req);
     if (max_C > 0)
         hipLaunchKernelGGL(hit_bucket_kernel, dim3((uint32_t)((max_C + 8 * 256 - 1) / (8 * 256)), (uint32_t)nreq),
                            dim3(256), 0, s, files, req);

@@ -29,6 +29,8 @@ struct ProbeOut {
 // 26 to 18 but gave no faster step on 50%-modified bases and a slower one on identical bases (host
 // digests of windows the speculation would have supplied).
 constexpr int HIT_WINDOWS = 4;
+// ScanFile::next_sums at most: the hit buffer's 16-B header holds T(p) and T(p + k B), k = 1..3.
+constexpr int NEXT_SUMS_MAX = 3;
 // Buckets of the listed hits' keys computed with the probe (HitBuckets region of ScanFile::bucket): up
 // to LISTED_IDX chunk indices per listed key, in no particular order.
 constexpr int LISTED_IDX = 3;

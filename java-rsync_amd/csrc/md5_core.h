@@ -9,8 +9,10 @@
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #define RSH_HD __host__ __device__ __forceinline__
+#define RSH_UNROLL _Pragma("unroll")
 #else
 #define RSH_HD static inline
+#define RSH_UNROLL _Pragma("GCC unroll 4")
 #endif
 
 namespace rsh {
@@ -489,9 +491,9 @@ RSH_HD void md5_digest_bytes(const Md5State& st, uint8_t out[16]) {
 // the runtime's scratch allocation).
 RSH_HD void store_digest(uint8_t* o, const Md5State& st, uint32_t dl) {
     const uint32_t w[4] = {st.a, st.b, st.c, st.d};
-#pragma unroll
+    RSH_UNROLL
     for (uint32_t i = 0; i < 4; ++i)
-#pragma unroll
+        RSH_UNROLL
         for (uint32_t j = 0; j < 4; ++j)
             if (4 * i + j < dl) o[4 * i + j] = (uint8_t)(w[i] >> (8 * j));
     for (uint32_t k = 16; k < dl; ++k) o[k] = 0;

@@ -504,12 +504,34 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             spec_wait = wait_on;
         }
     }
+    // The prefix end (below) needs the weak sums of the aligned windows between the run's last matching sample
+    // and the first that does not: launched with the table's work (on_ctx: its hash sync then covers them) or, at
+    // the latest, ahead of the guess's first probe, so that they land in a round trip the scan takes anyway
+    const int64_t pe_lo = run_last + 1, pe_hi = std::min<int64_t>(run_miss, nf - 1), pe_cnt = pe_hi - pe_lo + 1;
+    int32_t* pe_w = nullptr;
+    int64_t pe_bytes = 0;
+    hipError_t pe_err = hipSuccess;
+    auto launch_pe = [&] {
+        if (!(defer_prefix && guess_on && seg_on && run_miss > 0 && pe_cnt > 0 && pe_cnt <= 4096)) return;
+        const size_t ents_at = ((size_t)pe_cnt * 4 + 63) & ~(size_t)63;
+        pe_err = c->h_pend.ensure(ents_at + (size_t)pe_cnt * sizeof(rsh::GatherEnt));
+        if (pe_err != hipSuccess) return;
+        auto* pents = reinterpret_cast<rsh::GatherEnt*>(c->h_pend.as<uint8_t>() + ents_at);
+        for (int64_t i = 0; i < pe_cnt; ++i) pents[i] = rsh::GatherEnt{(pe_lo + i) * B, 0, 0};
+        auto* lf = reinterpret_cast<rsh::ScanFile*>(reinterpret_cast<rsh::GatherEnt*>(c->h_lead.as<uint8_t>() + lead_ents_at) +
+                                                    nsamp + 1);
+        pe_err = rsh::launch_window_weak(lf, pents, (uint32_t)pe_cnt, c->h_pend.as<int32_t>(), rs);
+        if (pe_err != hipSuccess) return;
+        pe_w = c->h_pend.as<int32_t>();
+        pe_bytes = pe_cnt * B;
+    };
     if (on_ctx) {  // (aux) the table and the probe hash, after a tentative launch's abort (above)
         int rc;
         {
             CallTrace tr("table_work", C);
             rc = table_work();
         }
+        if (rc == RSH_OK) launch_pe();
         start_md5_0();  // beside the table's download
         if (rc == RSH_OK) {
             CallTrace tr("table_wait", C);
@@ -538,33 +560,31 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // phase-shifted speculation there instead of once the resolver has walked the prefix.  A wrong guess is
     // stopped when the resolver hints another phase.  RSH_SCAN_PHASE_GUESS=0 (A/B) turns it off.
     int64_t guess = -1;
-    // The prefix end (below) needs the weak sums of the aligned windows between the run's last matching sample
-    // and the first that does not: launched now, ahead of the guess's first probe, so that they land in its
-    // round trip instead of one of their own
-    const int64_t pe_lo = run_last + 1, pe_hi = std::min<int64_t>(run_miss, nf - 1), pe_cnt = pe_hi - pe_lo + 1;
-    int32_t* pe_w = nullptr;
-    if (defer_prefix && guess_on && seg_on && run_miss > 0 && pe_cnt > 0 && pe_cnt <= 4096 && be.err == hipSuccess) {
-        const size_t ents_at = ((size_t)pe_cnt * 4 + 63) & ~(size_t)63;
-        RSH_HIP(c->h_pend.ensure(ents_at + (size_t)pe_cnt * sizeof(rsh::GatherEnt)));
-        pe_w = c->h_pend.as<int32_t>();
-        auto* pents = reinterpret_cast<rsh::GatherEnt*>(c->h_pend.as<uint8_t>() + ents_at);
-        for (int64_t i = 0; i < pe_cnt; ++i) pents[i] = rsh::GatherEnt{(pe_lo + i) * B, 0, 0};
-        auto* lf = reinterpret_cast<rsh::ScanFile*>(reinterpret_cast<rsh::GatherEnt*>(c->h_lead.as<uint8_t>() + lead_ents_at) +
-                                                    nsamp + 1);
-        RSH_HIP(rsh::launch_window_weak(lf, pents, (uint32_t)pe_cnt, pe_w, rs));
-        be.bytes_read += pe_cnt * B;
-    }
+    if (!pe_w) launch_pe();
+    RSH_HIP(pe_err);
+    be.bytes_read += pe_bytes;
     if (guess_on && run_miss > 0 && (spec_launched || defer_prefix) && HipBackend::phase_on() && C >= 4) {
         CallTrace tr("phase_guess", run_miss);
         int64_t a = run_miss * B;
         const int64_t b = std::min<int64_t>(run_miss * B + 2 * B, n - 4 * B + 1);  // the edit may sit in window m
+        // each probe: one round trip that also brings T at p + B, p + 2 B, p + 3 B (HipBackend::guess); the first
+        // over the tile or two at a (a small edit puts the new phase a few bytes past the sample), the rest after
+        be.guess = true;
         for (int tries = 0; tries < 8 && a < b && be.err == hipSuccess; ++tries) {
-            const rsh::ProbeInterval iv{a, b, a, 0, 0};
-            const int64_t p = be.first_hit(&iv, 1, nullptr);
+            const int64_t b1 = std::min(b, a + rsh::PROBE_TILE);
+            rsh::ProbeInterval iv{a, b1, a, 0, 0};
+            int64_t p = be.first_hit(&iv, 1, nullptr);
+            if (p < 0 && b1 < b) {
+                iv = rsh::ProbeInterval{b1, b, b1, 0, 0};
+                p = be.first_hit(&iv, 1, nullptr);
+            }
             if (p < 0) break;
-            const int64_t pos[4] = {p, p + B, p + 2 * B, p + 3 * B};
             int32_t w[4];
-            be.weak_many(pos, 4, w);
+            w[0] = be.weak_at(p);  // (came back with the probe)
+            if (!be.guess_sums(p, w + 1)) {  // (a hit the previous probe's list answered: no sums came with it)
+                const int64_t pos[3] = {p + B, p + 2 * B, p + 3 * B};
+                be.weak_many(pos, 3, w + 1);
+            }
             bool run = false;
             for (int64_t j = 0; j + 3 < C && !run; ++j)
                 run = host_weak[j] == w[0] && host_weak[j + 1] == w[1] && host_weak[j + 2] == w[2] &&
@@ -575,6 +595,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             }
             a = p + 1;
         }
+        be.guess = false;
     }
     // The prefix and the phase-shifted speculation in one segmented K1 launch: as two launches they need one
     // wave more than the chip's wave slots (each has a partial last wave), and that wave starts only when
@@ -645,7 +666,10 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                 if (ntail <= 256 && bytes <= seg_bytes) {
                     spec_na = P;
                     const int64_t snf = std::min<int64_t>(P, C);
-                    RSH_HIP(hipMemcpyAsync(c->segs.p, c->h_segs.p, bytes, hipMemcpyHostToDevice, ss));
+                    // the descriptors by a copy kernel on the launch's own stream: a copy-engine upload cost the
+                    // launch ~20 us more (the engine's completion, then the compute queue's wait on it)
+                    RSH_HIP(copy_to_host({rsh::CopyEnt{c->h_segs.as<uint8_t>(), c->segs.as<uint8_t>(), (int64_t)bytes}},
+                                         ss));
                     if (on_ctx) RSH_HIP(spec_buffers_free(c));
                     else RSH_HIP(hipStreamWaitEvent(ss, c->ev_in, 0));
                     RSH_HIP(hipStreamWaitEvent(ss, c->ev_phase[pset], 0));

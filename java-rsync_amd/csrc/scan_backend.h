@@ -26,10 +26,12 @@ namespace rshi {
 // HIP implementation of the resolver's services.
 // ------------------------------------------------------------------------------------------------
 constexpr size_t kFirstSlots = 1024;
+hipError_t wait_stamp(const int* stamp, int gen, hipStream_t s);  // scan.cpp
 // Device results to pinned host memory by a copy kernel (copy_few_kernel) rather than hipMemcpyAsync: between two
 // kernels a D2H copy cost 47-100 us of idle queue (tools/queue_lat.hip case 8) where a kernel writing pinned memory
 // cost none (case 9), and the profiler's async-copy tracing reported the copy engine's completions as never
-// delivered.  The ranges travel in the kernel's arguments.
+// delivered.  The ranges travel in the kernel's arguments.  The kernel
+// copies pinned host memory to the device as well (the segmented K1's descriptors, scan.cpp).
 inline hipError_t copy_to_host(std::initializer_list<rsh::CopyEnt> ents, hipStream_t s) {
     rsh::CopyFew f{};
     for (const rsh::CopyEnt& x : ents)
@@ -322,7 +324,7 @@ class HipBackend : public rsh::ScanBackend {
         rsh::ProbeTile* ht = pin<rsh::ProbeTile>(c_->h_tiles, (int64_t)tiles_.size() + 1);
         rsh::PartialTile* hpt = pin<rsh::PartialTile>(c_->h_ptiles, (int64_t)ptiles_.size() + 1);
         rsh::ProbeSeg* hsg = pin<rsh::ProbeSeg>(c_->h_psegs, (int64_t)segs_.size() + 1);
-        rsh::ProbeOut* hf = pin<rsh::ProbeOut>(c_->h_first, 1);
+        rsh::ProbeOut* hf = pin<rsh::ProbeOut>(c_->h_first, 2);  // the record, then the copy's stamp
         join_window_digests();  // h_hit is about to be overwritten
         uint8_t* hh = pin<uint8_t>(c_->h_hit, 16 + kScanWindows * B_);
         int32_t* hb = pin<int32_t>(c_->h_bucket, rsh::HIT_BUCKET_INTS + 1);  // + the request list {0}
@@ -348,7 +350,8 @@ class HipBackend : public rsh::ScanBackend {
         F->niv = (int32_t)count;
         F->bucket = c_->bucket.as<int32_t>();
         F->hit = hh;
-        F->nwin = kScanWindows;
+        F->nwin = guess ? 0 : kScanWindows;
+        F->next_sums = guess ? 3 : 0;
         if (head || partial) {  // anchors T(kB) for the blocks these tiles sit in
             anchors_.clear();
             for (const rsh::ProbeTile& t : tiles_) {
@@ -395,14 +398,18 @@ class HipBackend : public rsh::ScanBackend {
         // MD5 of the window at p: answer them in this round trip
         int32_t* req = hb + rsh::HIT_BUCKET_INTS;
         *req = 0;
-        ok(rsh::launch_hit_window(F, hiv, req, 1, t_.chunk_count, rs_));
-        ok(copy_to_host(
-                        {rsh::CopyEnt{reinterpret_cast<const uint8_t*>(d_first), reinterpret_cast<uint8_t*>(hf),
-                                      (int64_t)sizeof(rsh::ProbeOut)},
-                         rsh::CopyEnt{c_->bucket.as<uint8_t>(), reinterpret_cast<uint8_t*>(hb),
-                                      (int64_t)(rsh::HIT_BUCKET_INTS * sizeof(int32_t))}},
-                        rs_));
-        ok(hipStreamSynchronize(rs_));
+        ok(rsh::launch_hit_window(F, hiv, req, 1, guess ? 0 : t_.chunk_count, rs_));
+        // the results by one stamped workgroup; the host spins on the stamp (a stream synchronisation's wake-up
+        // cost each probe round trip ~10-20 us more)
+        rsh::CopyFew cf{};
+        cf.e[cf.n++] = rsh::CopyEnt{reinterpret_cast<const uint8_t*>(d_first), reinterpret_cast<uint8_t*>(hf),
+                                    (int64_t)sizeof(rsh::ProbeOut)};
+        cf.e[cf.n++] = rsh::CopyEnt{c_->bucket.as<uint8_t>(), reinterpret_cast<uint8_t*>(hb),
+                                    (int64_t)(rsh::HIT_BUCKET_INTS * sizeof(int32_t))};
+        int* stamp = reinterpret_cast<int*>(hf + 1);
+        const int sgen = ++c_->stamp_seq;
+        ok(rsh::launch_copy_few_stamped(cf, stamp, sgen, rs_));
+        if (err == hipSuccess) ok(wait_stamp(stamp, sgen, rs_));
         if (fc_.q && err == hipSuccess) {  // the chain's desync: to the caller, and into the intervals the cache keeps
             memcpy(fc_.out, hfo, (size_t)(2 * fc_.q->K) * sizeof(uint32_t));
             rsh::ProbeInterval* civ = const_cast<rsh::ProbeInterval*>(iv);  // (flush_probe's own list)
@@ -414,6 +421,15 @@ class HipBackend : public rsh::ScanBackend {
         if (count == 1) cache_.fill(iv[0], keys, *hf, n_ - B_);
         else cache_.fill_batch(iv, count, keys, *hf, n_ - B_);
         if (hf->first == ~0ull) return -1;
+        if (guess) {  // no windows and no bucket came back: only T(p) and the next three windows' sums
+            for (int64_t& w : win_pos_) w = -1;
+            t_pos_ = (int64_t)hf->first;
+            t_val_ = *reinterpret_cast<const int32_t*>(hh);
+            guess_pos_ = t_pos_;
+            memcpy(guess_sums_, hh + 4, sizeof(guess_sums_));
+            t_.prime_clear();
+            return t_pos_;
+        }
         rsh::window_slots(*hf, kScanWindows, win_pos_);
         for (int k = 1; k < kScanWindows; ++k)
             if (win_pos_[k] >= 0) {
@@ -437,6 +453,16 @@ class HipBackend : public rsh::ScanBackend {
 
     // ---- phase-shifted speculation (resolver.h ScanBackend::phase_hint / phase_sums): K1 over [s0, n) with
     // the received header's B and dl, on the aux stream behind whatever runs there, one at a time ----
+    // The phase guess's probes (scan.cpp): no hit windows and no bucket, but T(p + k B), k = 1..3, of the hit in the
+    // same round trip (hit_window_kernel, ScanFile::next_sums) -- the guess checks four consecutive windows
+    bool guess = false;
+    int64_t guess_pos_ = -1;
+    int32_t guess_sums_[3] = {0, 0, 0};
+    bool guess_sums(int64_t p, int32_t out[3]) const {
+        if (p != guess_pos_) return false;
+        memcpy(out, guess_sums_, sizeof(guess_sums_));
+        return true;
+    }
     int64_t ph_launches = 0;
     double phase_ms = 0;  // the K1s of the phase speculations that landed
     void phase_hint(int64_t s) override {
