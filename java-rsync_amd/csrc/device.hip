@@ -309,7 +309,9 @@ __device__ __forceinline__ void md5_stream_block(Md5State& st, const uint32_t (&
 // block sum lands in lane n (element q), its weighted sum in lane n + 16.  Saves the 8 ds_read_b128 per stage: the
 // same cycles at a higher clock, 2.5 % less time (kbench A/B, profiles/r4/r4e_kbench_weakw_k3s*).
 // ABORT: the wave polls *abort_flag (never_word() when the launch has no abort word of its own).
-template <bool MULTI = false, bool GATHER = false>
+// WEAKV (kbench A/B only, variant 1010): the weak sums on the VALU (weak_block: 32 v_dot4_i32_i8 per 64-B block)
+// instead of the matrix pipe -- the form that drops the MFMAs' power for 8 % more VALU issue.
+template <bool MULTI = false, bool GATHER = false, bool WEAKV = false>
 __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__ data, uint32_t B, uint32_t dl,
                                                              uint32_t seed, int32_t* __restrict__ weak_out,
                                                              uint8_t* __restrict__ strong_out,
@@ -419,13 +421,20 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         unpack(w, m);
         md5_stream_block(st, m);
     };
-    auto weak_words = [&](const uint4 (&w)[4]) __attribute__((always_inline)) {  // one 64-B block
+    [[maybe_unused]] int32_t vs1 = 0, vu = 0;  // WEAKV: the lane's own sums
+    auto weak_words = [&](const uint4 (&w)[4], [[maybe_unused]] uint32_t off) __attribute__((always_inline)) {
+        if constexpr (WEAKV) {  // one 64-B block at chunk offset off
+            uint32_t m[16];
+            unpack(w, m);
+            weak_block(m, vs1, vu, off);
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) RW[e] += accW[e];  // R += P_{b-1}
+            for (int e = 0; e < 4; ++e) RW[e] += accW[e];  // R += P_{b-1}
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const v4i32 b4 = {(int)w[k].x, (int)w[k].y, (int)w[k].z, (int)w[k].w};
-            accW = __builtin_amdgcn_mfma_i32_16x16x64_i8(wW[k], b4, accW, 0, 0, 0);
+            for (int k = 0; k < 4; ++k) {
+                const v4i32 b4 = {(int)w[k].x, (int)w[k].y, (int)w[k].z, (int)w[k].w};
+                accW = __builtin_amdgcn_mfma_i32_16x16x64_i8(wW[k], b4, accW, 0, 0, 0);
+            }
         }
     };
     // One stage with compile-time parity P: LDS buffer P holds it, q[P ^ 1] the next stage's data.
@@ -439,11 +448,11 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         }
         get_words(Wb, P, 1);
         md5_block(Wa);
-        weak_words(Wa);
+        weak_words(Wa, 128u * si);
         compiler_fence();
         if (has_next) get_words(Wa, P ^ 1, 0);
         md5_block(Wb);
-        weak_words(Wb);
+        weak_words(Wb, 128u * si + 64u);
         compiler_fence();
     };
 
@@ -482,7 +491,10 @@ __device__ __forceinline__ void block_sums_pipe_body(const uint8_t* __restrict__
         md5_compress(st, m);
     }
     int32_t s1, u;
-    {
+    if constexpr (WEAKV) {
+        s1 = vs1;
+        u = vu;
+    } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) RW[e] += accW[e];
         const int n = l & 15, q = l >> 4;
@@ -551,6 +563,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_num_vgpr(256))) void bloc
                                 main_waves);
 }
 bool tail_gather_on() { return opt(OPT_K1_GATHER) != 0; }  // 0: leftover chunks one per lane (options.h)
+#ifdef RSH_KBENCH
+__global__ __launch_bounds__(64) K1_PIPE_ATTR void block_sums_pipe_weakv_kernel(
+    const uint8_t* __restrict__ data, uint32_t B, uint32_t dl, uint32_t seed, int32_t* __restrict__ weak_out,
+    uint8_t* __restrict__ strong_out, const int* abort_flag, int abort_gen) {
+    block_sums_pipe_body<false, false, true>(data, B, dl, seed, weak_out, strong_out, abort_flag, abort_gen);
+}
+#endif
 
 // Diagnostic (rsh_debug_k1_clock, MI355X_MICROARCH.md "DVFS give-back" item 6): the Generator's production K1 body
 // with each wave's shader-clock (s_memtime) and 100 MHz (s_memrealtime) ticks stamped around it and summed over the
@@ -905,6 +924,16 @@ hipError_t launch_block_sums_variant(int variant, const uint8_t* d_data, int64_t
     if (nchunks == 0) return hipSuccess;
     const uintptr_t addr = reinterpret_cast<uintptr_t>(d_data);
     const uint32_t nst = B >> 7;
+#ifdef RSH_KBENCH
+    if (variant == 1010) {  // the VALU weak-sum form over whole waves (kbench shapes: n = 64 k B, 128-B aligned)
+        if ((B % 128) != 0 || nst < 4 || nst > 1024 || n != (int64_t)nchunks * B || nchunks % 64 != 0 || (addr % 128) != 0)
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL(block_sums_pipe_weakv_kernel, dim3(nchunks / 64), dim3(64), 2 * 64 * 9 * sizeof(uint4), s,
+                           d_data, B, dl, seed_word, d_weak, d_strong, abort_flag ? abort_flag : never_word(),
+                           abort_flag ? abort_gen : -1);
+        return hipGetLastError();
+    }
+#endif
     // the pipelined and shift kernels poll an abort word (never_word() for launches without one of their own)
     const bool coalesced = variant < 0 && abort_flag && (B % 128) == 0 && nst >= 4 && nst <= 1024;
     // A base that is not 128-B aligned goes to the line-aligned shift kernel when the lines it reads around the

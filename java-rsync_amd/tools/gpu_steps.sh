@@ -120,6 +120,11 @@ for step in "$@"; do
             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $CB --kernel-trace -d "$O/pmc_walk_b" -o run \
                 --output-format csv -- python3 "$R/bench.py" --workload files --variant "$VARIANT" --steps 1 --warmup 1 \
                 --no-cpu-baseline --no-companions $PMC_ARGS > "$O/pmc_walk_b.json" 2> "$O/pmc_walk_b.err") || exit 1 ;;
+        k1-energy)  # the production K1 (1000) against its VALU weak-sum form (1010), interleaved; then one PMC pass
+            run 180 "$K" 16384 131072 4 5 1000 1010 1000 1010 > "$O/k1_energy_kbench.log" 2>&1
+            C="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"
+            (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d "$O/k1_energy_pmc" -o run \
+                --output-format csv -- "$K" 16384 131072 4 3 1000 1010 1000 1010 > "$O/k1_energy_pmc.log" 2>&1) || exit 1 ;;
         kbench-k1)
             run 120 "$K" 16384 131072 4 8 1000 > "$O/kbench_128k.log" 2>&1
             run 120 "$K" 16384 8192 3 8 1000 1002 1005 > "$O/kbench_8k.log" 2>&1 ;;

@@ -7,6 +7,7 @@
 // Its parity check holds when per is a multiple of B (then the files' chunks are the buffer's chunks).
 // variant 1003: the segmented launch (the Sender's prefix + phase speculation kernel) over the buffer.
 // variant 1005: the production batch planner over ragged files (below).
+// variant 1010: the pipelined K1 with its weak sums on the VALU (v_dot4) instead of the MFMAs (energy A/B).
 // (The rejected K1 forms measured in rounds 1-4 -- the coalesced kernel's MD5 step forms, LDS-DMA stages, 4 waves per
 // SIMD, persistent waves, no-LDS loads -- were deleted after their A/Bs; DESIGN.md sec. 4 keeps the numbers.)
 #include <hip/hip_runtime.h>
@@ -204,6 +205,7 @@ int main(int argc, char** argv) {
             return rsh::launch_block_sums_batch(d_groups, (uint32_t)groups.size(), d_lanes, (uint32_t)lanes.size(),
                                                 lane_align, 0x04030201u, s);
         if (v == 1000) return rsh::launch_block_sums_variant(-1, d, n, B, C, dl, 0x04030201u, w, sx, s, abort_word, 1);
+        if (v == 1010) return rsh::launch_block_sums_variant(1010, d, n, B, C, dl, 0x04030201u, w, sx, s, abort_word, 1);
         if (v == 1001) return rsh::launch_block_sums(d, n, B, C, dl, 0x04030201u, w, sx, s);  // the production entry
         return rsh::launch_block_sums_variant(v, d, n, B, C, dl, 0x04030201u, w, sx, s);
     };
