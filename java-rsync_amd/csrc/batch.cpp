@@ -594,7 +594,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             const int gen_b = ++c->gen;
             if (tr) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
             RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, 0, gen_b, map_on ? S->chain_help.as<ChainHelp>() : nullptr,
-                                          n_help));
+                                          n_help, tr));
             RSH_BHIP(hipEventRecord(S->ev_wa, st));
             // (option batch_skip_rest) once phase 0 has ended, the rest of the speculation only if some walk reached
             // the prefix's end (CHAIN_MORE): otherwise every file is done, or left to its resolver with the prefix
@@ -625,7 +625,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             spec_launched = true;
             RSH_BHIP(hipStreamWaitEvent(st, S->ev_fk, 0));
             if (tr && !two_phase) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
-            RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, two_phase ? 1 : 0, 0));
+            RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, two_phase ? 1 : 0, 0, nullptr, 0, tr));
         } else {  // what waits on the speculation's events below finds them complete (phase 0 is)
             RSH_BHIP(hipEventRecord(c->ev_flags, st));
             RSH_BHIP(hipEventRecord(c->ev_spec, st));
@@ -713,9 +713,10 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                             "%lld, phase 1 %d, walk %.1f us)\n", f, (long long)co[f].s, co[f].why, (long long)co[f].events,
                             co[f].tiles, co[f].md5c_valid, (long long)co[f].clear_to, co[f].spec_full, co[f].t_total / 100.0);
             fprintf(stderr, "[rsh-batch]   file %d: walk %.1f us = tiles %.1f (table checks %.1f; %d of %d tiles from the hit map,"
-                    " the first at tile %d) + events %.1f (%d digests: %.1f) + other\n", fmax, x.t_total / 100.0,
+                    " the first at tile %d) + events %.1f (buckets %.1f; %d digests: %.1f) + key set %.1f + steps (1)/(1') %.1f +"
+                    " event drains %.1f + other\n", fmax, x.t_total / 100.0,
                     x.t_tiles / 100.0, x.t_check / 100.0, x.mapped, x.tiles, x.first_mapped, x.t_event / 100.0,
-                    x.digests, x.t_digest / 100.0);
+                    x.t_evb / 100.0, x.digests, x.t_digest / 100.0, x.t_kset / 100.0, x.t_chain / 100.0, x.t_drain / 100.0);
             if (S->chain_help.p && two_phase) {  // the map's helpers (device state of the last phase-0 launch)
                 std::vector<ChainHelp> hh((size_t)NF);
                 if (hipMemcpy(hh.data(), S->chain_help.p, (size_t)NF * sizeof(ChainHelp), hipMemcpyDeviceToHost) == hipSuccess) {

@@ -373,6 +373,8 @@ struct ChainOut {
     int32_t md5c_valid, digests;  // digests: windows the walk digested itself (unaligned hits)
     int64_t flushes;              // FileView flushes of the closed form (a dead poisoned state)
     int64_t t_total, t_tiles, t_check, t_event, t_digest;  // wall-clock ticks (10 ns) of the walk's parts (trace)
+    int64_t t_kset, t_chain, t_drain;  // ... the key set's build, steps (1) and (1'), the event drains (trace)
+    int64_t t_evb;                     // ... the events' first part: their bucket's load and barrier (trace)
     int32_t spec_full;            // phase 1 walked it
     int32_t aborted;              // phase 0 stopped its phase-1 K1 groups: only the prefix is speculated
     int32_t mapped, first_mapped; // tiles answered from the hit map; the walk's tile count at the first (trace)
@@ -443,8 +445,9 @@ hipError_t launch_k1_clock(const uint8_t* d_data, int64_t n, uint32_t B, uint32_
                            int32_t* d_weak, uint8_t* d_strong, unsigned long long* d_clk, hipStream_t s);
 // help (phase 0): the files' ChainHelp array, or null (no map); helpers: extra workgroups beyond nfiles that only
 // map; finished walks map too.  abort_gen is also the map's generation.
+// timed: the walks read the wall clock for their section timers (scan_trace's report; ChainOut::t_*).
 hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s, int phase = 1,
-                                int abort_gen = 0, ChainHelp* help = nullptr, uint32_t helpers = 0);
+                                int abort_gen = 0, ChainHelp* help = nullptr, uint32_t helpers = 0, bool timed = false);
 // The chunk indexes of many files (slots cleared by the caller; TableEnt as for the probe hashes).
 hipError_t launch_chunk_index(const TableEnt* ents, uint32_t nfiles, int32_t max_keys, hipStream_t s, bool bg = false);
 

@@ -34,6 +34,15 @@ namespace rsh {
 // ------------------------------------------------------------------------------------------------
 // CHAIN_THREADS, CHAIN_PPT, CHAIN_TILE, CHAIN_SEGS: device.h (the host sizes the hit map with them)
 constexpr int CHAIN_EV_LDS = 64;  // events a walk holds in LDS before writing them out
+// The walk's section timers (ChainOut::t_*, ChainHelp::t_*: the scan_trace report) read the wall clock only when the
+// launch is traced: each read is a scalar memory operation the walk's next LDS wait also waits for.  Build with
+// -DRSH_CHAIN_TIMERS_ALWAYS for the A/B of the timers' own cost.
+__device__ __forceinline__ int64_t chain_clock(bool timed) {
+#ifdef RSH_CHAIN_TIMERS_ALWAYS
+    timed = true;
+#endif
+    return timed ? (int64_t)wall_clock64() : 0;
+}
 
 // A key's presence in a chunk index (launch_chunk_index: (key << 32) | (i + 1) per chunk, 0 = empty): every chunk
 // with the key lies on the key's probe path before its first empty slot
@@ -380,7 +389,7 @@ constexpr int CHAIN_HELP_LEAD = 64;   // a helper stays with its file while the 
 __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict__ files, int nfiles, uint32_t gen,
                                                      ChainHelp* help, uint2* ck, int32_t* ck_full,
                                                      int32_t* sh, int32_t (*s_seg)[4], unsigned long long* s_best,
-                                                     int32_t* s_word, int32_t* s_live) {
+                                                     int32_t* s_word, int32_t* s_live, bool timed) {
     const int t = threadIdx.x;
     const ChainKeySet kset{ck, ck_full};
     int cur = -1;
@@ -439,11 +448,11 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
                 atomicAdd(&h->nhelp, 1);
             }
             cur = f;
-            const int64_t tb = (int64_t)wall_clock64();
+            const int64_t tb = chain_clock(timed);
             F = files[f];
             chain_kset_build(kset, F.table_weak, F.C);
             if (t == 0) {
-                atomicAdd((unsigned long long*)&h->t_kset, (unsigned long long)((int64_t)wall_clock64() - tb));
+                atomicAdd((unsigned long long*)&h->t_kset, (unsigned long long)(chain_clock(timed) - tb));
                 atomicAdd(&h->joins, 1);
             }
             if (*kset.full) {  // not exact: the walk confirms keys in the chunk index; no map for this file
@@ -469,7 +478,7 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
             atomicAdd(&h->mapped, 1);
             if (whole) {
                 atomicAdd(&h->whole, 1);
-                atomicMin((unsigned long long*)&h->t_first, (unsigned long long)wall_clock64());
+                atomicMin((unsigned long long*)&h->t_first, (unsigned long long)chain_clock(timed));
             }
         }
     }
@@ -477,7 +486,8 @@ __device__ __attribute__((noinline)) void chain_help(const ChainFile* __restrict
 }
 
 __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const ChainFile* __restrict__ files, int phase,
-                                                                      int abort_gen, ChainHelp* help, int nfiles) {
+                                                                      int abort_gen, ChainHelp* help, int nfiles,
+                                                                      int timed) {
     __builtin_amdgcn_s_setprio(3);
     __shared__ int32_t sh[4 * CHAIN_THREADS / 64];
     __shared__ int32_t s_hit;                  // first hit in a tile (offset from the tile start), or INT_MAX
@@ -496,14 +506,15 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t s_word, s_live;
     const ChainKeySet kset{s_ck, &s_ck_full};
     if ((int)blockIdx.x >= nfiles) {  // a helper workgroup (phase 0): it only maps
-        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live);
+        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live,
+                   timed != 0);
         return;
     }
     // the descriptor by value: it sits in pinned host memory, and a reference would let the compiler re-read its
     // fields across the loop (the event stores may alias it) -- a PCIe round trip each
     const ChainFile F = files[blockIdx.x];
     ChainHelp* const H = (phase == 0 && help != nullptr) ? help + blockIdx.x : nullptr;
-    if (H != nullptr && threadIdx.x == 0) chain_st64(&H->t_start, (int64_t)wall_clock64());
+    if (H != nullptr && threadIdx.x == 0) chain_st64(&H->t_start, chain_clock(timed));
     const uint32_t map_gen = (H != nullptr && F.hmap != nullptr) ? (uint32_t)abort_gen : 0u;  // 0: no map
     ChainOut* out = F.out;
     // phase 0 walks over the prefix speculation [0, na_a); phase 1 resumes the walks that reached its end
@@ -550,15 +561,17 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         kset_built = s_zero < nflags;  // (uniform) a break in the chain: the walk will search
         __syncthreads();
     }
+    const int64_t tks0 = chain_clock(timed);
     if (kset_built) chain_kset_build(kset, F.table_weak, C);
+    const int64_t t_kset = chain_clock(timed) - tks0;
     int32_t pref = out->pref;
     int32_t nev = out->n_ev, status = CHAIN_STOP;
     int64_t lit = out->literal, mat = out->matched, chain_matches = out->chain_matches, events = out->events;
     int32_t tiles = out->tiles, digests = out->digests, poisoned = 0, dead = 0, mapped = out->mapped;
     int32_t first_mapped = out->first_mapped;
     int64_t flushes = out->flushes;
-    const int64_t tk0 = (int64_t)wall_clock64();
-    int64_t t_tiles = 0, t_check = 0, t_event = 0, t_digest = 0;
+    const int64_t tk0 = chain_clock(timed);
+    int64_t t_tiles = 0, t_check = 0, t_event = 0, t_digest = 0, t_chain = 0, t_drain = 0, t_evb = 0;
     const uint8_t* stale = nullptr;  // poisoned: the cached digest
     uint32_t dg[4] = {0u, 0u, 0u, 0u};  // the window's digest at the current event (poisoned: the stale one)
     int64_t clear_to = -1;            // stopped at a flush point: no candidate in [s, clear_to]
@@ -580,10 +593,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     // gfx9 the counter covers stores too), so lane 0 writing each event itself held the walk ~1-2 us per event.
     int32_t nev_w = nev;  // events already in F.ev
     auto drain_ev = [&]() {  // (all threads)
+        const int64_t tdr0 = chain_clock(timed);
         __syncthreads();
         for (int32_t i = t; i < nev - nev_w; i += CHAIN_THREADS) F.ev[nev_w + i] = s_ev[i];
         nev_w = nev;
         __syncthreads();
+        t_drain += chain_clock(timed) - tdr0;
     };
     auto flush_pend = [&]() {  // (the loop drains at its top while fewer than CHAIN_EV_LDS - 8 are held)
         if (have) {
@@ -641,6 +656,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         const int32_t tw_pref = pf_use ? pf_tw : (!poisoned && pref < C && k < na) ? F.table_weak[pref] : 0;
         pf_s = -1;
         // (1) aligned chain: preferred index == k and source window k carries chunk k's sums
+        const int64_t tch0 = chain_clock(timed);
         if (flag_k) {
             if (t == 0) s_zero = nflags;
             __syncthreads();
@@ -680,6 +696,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             chain_matches += j - k;
             s = m = p;
             pref = (int32_t)j;
+            t_chain += chain_clock(timed) - tch0;
             continue;
         }
         // (1') the window at s against chunk pref while both sums agree (windows s + iB, chunks pref + i)
@@ -700,9 +717,11 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 emit_match(s, p - s, pref, (int32_t)tt);
                 s = m = p;
                 pref += (int32_t)tt;
+                t_chain += chain_clock(timed) - tch0;
                 continue;
             }
         }
+        t_chain += chain_clock(timed) - tch0;
         // (2) the next candidate event in [s, stop]
         const int64_t f = (m + 10 * B <= n) ? m + 9 * B : INT64_MAX;
         const int64_t stop = f < last ? f : last;
@@ -738,7 +757,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             }
             for (int64_t q0 = a & ~(int64_t)(CHAIN_PPT - 1); p < 0 && q0 <= qlast;) {
                 ++tiles;
-                const int64_t tt0 = (int64_t)wall_clock64();
+                const int64_t tt0 = chain_clock(timed);
                 if (map_gen != 0u) {
                     // the tile from the hit map when every word it needs carries this launch's generation: lane t's
                     // word holds positions [q0 + 32 t, + 32), masked to [a, qlast] (qlast < hend)
@@ -776,7 +795,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                         }
                         if (mapped++ == 0) first_mapped = tiles;
                         q0 += CHAIN_TILE;
-                        t_tiles += (int64_t)wall_clock64() - tt0;
+                        t_tiles += chain_clock(timed) - tt0;
                         continue;
                     }
                 }
@@ -805,7 +824,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 }
                 if (t == 0) s_hit = 0x7FFFFFFF;
                 __syncthreads();
-                const int64_t tc0 = (int64_t)wall_clock64();
+                const int64_t tc0 = chain_clock(timed);
                 int32_t my_hit = 0x7FFFFFFF;
                 uint32_t my_key = 0;
                 if (live) {
@@ -869,7 +888,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     if (my_hit != 0x7FFFFFFF) atomicMin(&s_hit, my_hit);
                 }
                 __syncthreads();
-                t_check += (int64_t)wall_clock64() - tc0;
+                t_check += chain_clock(timed) - tc0;
                 if (my_hit != 0x7FFFFFFF && my_hit == s_hit) s_key = my_key;
                 __syncthreads();
                 if (s_hit != 0x7FFFFFFF) {
@@ -878,7 +897,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 }
                 __syncthreads();
                 q0 += CHAIN_TILE;
-                t_tiles += (int64_t)wall_clock64() - tt0;
+                t_tiles += chain_clock(timed) - tt0;
             }
             cut = p < 0 && stop > lim_spec;  // (lim_spec, stop] has no anchors: not searched
         }
@@ -973,7 +992,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             break;
         }
         // the event at p: its bucket (Multimap order), the candidates of Checksum.getCandidateChunks
-        const int64_t te0 = (int64_t)wall_clock64();
+        const int64_t te0 = chain_clock(timed);
         ++events;
         const int64_t kp = p / B;
         const bool spec_digest = !poisoned && p % B == 0 && kp < na;
@@ -1009,19 +1028,18 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                 cnt += __popcll(hits);
                 more = empty == 0ull;
             }
-            if (t == 0) s_nbk = cnt;
+            if (t == 0) {  // ascending chunk index (insertion order); the wave's LDS operations execute in order
+                s_nbk = cnt;
+                for (int i = 1; i < cnt && i < CHAIN_BUCKET_CAP; ++i)
+                    for (int j = i; j > 0 && s_bk[j - 1] > s_bk[j]; --j) {
+                        const int32_t x = s_bk[j];
+                        s_bk[j] = s_bk[j - 1];
+                        s_bk[j - 1] = x;
+                    }
+            }
         }
         __syncthreads();
-        if (t == 0) {
-            const int32_t cnt = s_nbk;
-            for (int i = 1; i < cnt && i < CHAIN_BUCKET_CAP; ++i)  // ascending chunk index (insertion order)
-                for (int j = i; j > 0 && s_bk[j - 1] > s_bk[j]; --j) {
-                    const int32_t x = s_bk[j];
-                    s_bk[j] = s_bk[j - 1];
-                    s_bk[j - 1] = x;
-                }
-        }
-        __syncthreads();
+        t_evb += chain_clock(timed) - te0;
         const int32_t size = s_nbk;
         if (size == 0 || size > CHAIN_BUCKET_CAP) {
             why = CHAIN_WHY_BUCKET;
@@ -1045,12 +1063,12 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         // the window here (lane_chunk_sums over the B bytes at p, the seed appended), the host path's md5_at
         const uint8_t* md5c = poisoned ? stale : F.as + kp * dl;
         if (!spec_digest && !poisoned) {
-            const int64_t td0 = (int64_t)wall_clock64();
+            const int64_t td0 = chain_clock(timed);
             chain_window_digest(F.data + p, (uint32_t)B, (uint32_t)dl, F.seed, s_win, s_dig);  // (ends with a barrier)
             md5c = s_dig;
             chain_digest_load(s_dig, dl, dg);
             ++digests;
-            t_digest += (int64_t)wall_clock64() - td0;
+            t_digest += chain_clock(timed) - td0;
         }
         int32_t hit = -1;
         for (int32_t it = -1; it < size && hit < 0; ++it) {
@@ -1069,7 +1087,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             if (eq) hit = c;
         }
         __syncthreads();
-        t_event += (int64_t)wall_clock64() - te0;
+        t_event += chain_clock(timed) - te0;
         if (hit < 0) {
             // the cached digest is stale from here on (quirk B): the walk goes on with it from p + 1, comparing every
             // later candidate with it, up to the next flush point (a hit at the flush point itself flushes there: the
@@ -1172,11 +1190,15 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         out->tiles = tiles;
         out->digests = digests;
         out->flushes = flushes;
-        out->t_total += (int64_t)wall_clock64() - tk0;
+        out->t_total += chain_clock(timed) - tk0;
         out->t_tiles += t_tiles;
         out->t_check += t_check;
         out->t_event += t_event;
         out->t_digest += t_digest;
+        out->t_kset += t_kset;
+        out->t_chain += t_chain;
+        out->t_drain += t_drain;
+        out->t_evb += t_evb;
         out->spec_full = phase == 1;
         out->mapped = mapped;
         out->clear_to = clear_to;
@@ -1202,19 +1224,20 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     if (H != nullptr) {  // this walk is over: its helpers stop, and the workgroup helps the walks still searching
         if (t == 0) chain_st(&H->live, 0);
         __syncthreads();
-        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live);
+        chain_help(files, nfiles, (uint32_t)abort_gen, help, s_ck, &s_ck_full, sh, s_seg, &s_best, &s_word, &s_live,
+                   timed != 0);
     }
 }
 
 hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s, int phase, int abort_gen,
-                                ChainHelp* help, uint32_t helpers) {
+                                ChainHelp* help, uint32_t helpers, bool timed) {
     if (nfiles == 0) return hipSuccess;
     if (phase != 0 || help == nullptr || nfiles >= (1u << 20)) {  // (helpers pick files by a 20-bit index)
         help = nullptr;
         helpers = 0;
     }
     hipLaunchKernelGGL(chain_advance_kernel, dim3(nfiles + helpers), dim3(CHAIN_THREADS), 0, s, files, phase,
-                       abort_gen, help, (int)nfiles);
+                       abort_gen, help, (int)nfiles, timed ? 1 : 0);
     return hipGetLastError();
 }
 
