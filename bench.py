@@ -51,8 +51,8 @@ KEY_CASE = KEY_SRC ^ 5
 KEY_INS = KEY_SRC ^ 0x1B
 SHIFT_AT = 155 * 131072 + 4096  # the "config5_shift1" insert position
 WARMUP_MIN_MS = 250.0  # untimed warmup of at least this long (and at least --warmup steps)
-TRAFFIC_CSV = "r5/r5m2_bench_fetch_size.csv"
-TRAFFIC_FILES_CSV = "r5/r5m2_files_fetch_size.csv"
+TRAFFIC_CSV = "r6/r6f_bench_fetch_size.csv"
+TRAFFIC_FILES_CSV = "r6/r6f_files_fetch_size.csv"
 
 
 def parse():
