@@ -243,16 +243,9 @@ __global__ __launch_bounds__(64) void block_sums_lane_batch_kernel(const K1Lane*
 
 typedef int v4i32 __attribute__((ext_vector_type(4)));
 
-// Weak sums on the matrix pipe (the shift kernel's form): per stage, for each group g of 16 chunks and K-half h,
-// C_g += W_h x X_{g,h} with v_mfma_i32_16x16x64_i8, where X holds 64 signed bytes of 16 chunks
-// (columns) and W_h has row 0 = ones and row 1 = the byte's index in the 128-B stage (<= 127, int8).
-// Row 0 of C accumulates s1; row 1 accumulates the in-stage-index-weighted sums; R_g += row 0 after
-// every stage gives sum_s P_s, so u = sum_i i x_i = 128 (nst * P_last - R) + row1.  Column j of group g
-// is chunk 16g + kPi[j] and K-slice s reads piece 4h + kSigma[s]: with the 9-slot LDS rows every
-// 16-lane ds_read_b128 group then hits 16 distinct bank quads (checked exhaustively).
-__device__ __forceinline__ int mfma_pi(int j) { return (int)((0xECA8FDB975316420ull >> (4 * j)) & 15); }
-__device__ __forceinline__ int mfma_pi_inv(int c) { return (int)((0xBFAE9D8C73625140ull >> (4 * c)) & 15); }
-__device__ __forceinline__ int mfma_sigma(int s) { return (0x1302 >> (4 * s)) & 15; }
+// Weak sums on the matrix pipe: see block_sums_pipe_body (weak_words).  Until round 5 the shift kernel summed whole
+// 128-B LDS lines per group of 16 chunks (C_g += W_h x X_{g,h}, a permuted column order against bank conflicts;
+// DESIGN.md sec. 4); since round 6 it uses the pipelined kernel's form as well.
 
 // ABORT (the Sender's speculation only): every 16 stages the wave reads *abort_flag (uncached device
 // memory, set by a stream write-value packet) with a cache-bypassing scalar load and exits when it
@@ -613,8 +606,12 @@ hipError_t launch_k1_clock(const uint8_t* d_data, int64_t n, uint32_t B, uint32_
 //    block-1 words (lines u - 1 and u; a wave's LDS operations execute in order).  A block's words come from
 //    5 slots at slot offset a >> 4 (mod 16) and are funnel-shifted by a & 15 bytes: dword offset
 //    W = (a >> 2) & 3 (template), byte shift a & 3 (v_alignbyte_b32).
-//  * Weak sums: the MFMAs sum whole lines 0..nst in the aligned kernel's operand layout; line 0's bytes before
-//    the chunk (a) and line nst's bytes after it (128 - a) are subtracted per lane (v_dot4 over its own row).
+//  * Weak sums (round 6): from the funnel-shifted MD5 words in registers, in the aligned kernel's form (four MFMAs
+//    per 64-B block, block_sums_pipe_body's weak_words).  Until round 5 the MFMAs summed whole LDS lines read a
+//    second time in the operand layout (8 ds_read_b128 per line) and took the bytes outside the chunk out per lane;
+//    the two forms measured the same (3.32 against 3.32-3.34 ms for 16 GiB at offset 1, profiles/r6/r6u2), this one
+//    with 209 VGPRs instead of 235.  So did unaligned ds_read_b128 instead of the funnel: slower (3.70-4.08 ms; the
+//    LDS's unaligned reads cost more than the 16 half-rate v_alignbyte_b32 per block, ~4 % of the kernel's time).
 //  * Tail waves (blockIdx >= main_waves): one lane per remaining chunk on the per-lane path (any alignment),
 //    dispatched with the main waves rather than as a second launch queued behind them.
 // ------------------------------------------------------------------------------------------------
@@ -628,35 +625,30 @@ __device__ __forceinline__ void shift_wave(const uint8_t* __restrict__ gdata, ui
     constexpr int ROW = 17;
     extern __shared__ __attribute__((aligned(16))) uint4 lds_all[];  // 64 rows of ROW slots
     const int l = threadIdx.x;
-    const uint32_t c0 = 0;
     const uint32_t nst = B >> 7;  // host guarantees 4 <= nst <= 1024
     const uint32_t Q = a >> 4, r = a & 3;
     const int wr0 = (l >> 3) * ROW + (l & 7);
     const int row = l * ROW;
 
-    v4i32 wA[2];
-    v4i32 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-    int32_t Racc[4] = {0, 0, 0, 0};
+    v4i32 wW[4];  // the A operand for block quarter w (block_sums_pipe_body)
+    v4i32 accW = {0, 0, 0, 0}, RW = {0, 0, 0, 0};
     {
-        const int rw = l & 15, ks = l >> 4;
+        const int m = l & 15, q = l >> 4, type = m >> 2;
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
+        for (int w = 0; w < 4; ++w)
 #pragma unroll
-            for (int w = 0; w < 4; ++w) {
+            for (int d = 0; d < 4; ++d) {
                 uint32_t word = 0;
-                if (rw == 0) word = 0x01010101u;
-                else if (rw == 1)
+                if (q == (m & 3) && type == 0) word = 0x01010101u;
+                else if (q == (m & 3) && type == 1)
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) word |= (uint32_t)(16 * (4 * h + mfma_sigma(ks)) + 4 * w + b) << (8 * b);
-                wA[h][w] = (int)word;
+                    for (int b = 0; b < 4; ++b) word |= (uint32_t)(16 * w + 4 * d + b) << (8 * b);
+                wW[w][d] = (int)word;
             }
     }
-    const int rdB = mfma_pi(l & 15) * ROW + mfma_sigma(l >> 4);
-
     uint4 q[2][8];  // line u + 1 and u + 2 in flight while step u computes
     uint4 Wa[5];    // block 0 of the next MD5 stage
     uint4 Wb[5];    // block 1 of the current MD5 stage
-    uint4 Bv[8];    // MFMA operands of the current line
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(gdata), 0, (int)(64 * B + 128), 0x00020000);
     const uint32_t lane_off = (uint32_t)(l >> 3) * B + 16u * (uint32_t)(l & 7);
@@ -676,12 +668,6 @@ __device__ __forceinline__ void shift_wave(const uint8_t* __restrict__ gdata, ui
 #pragma unroll
         for (int k = 0; k < 5; ++k) w[k] = lds_all[row + ((8 * P + 4 * h + Q + k) & 15)];
     };
-    auto get_mfma = [&](int half) __attribute__((always_inline)) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) Bv[4 * h + g] = lds_all[16 * ROW * g + rdB + 8 * half + 4 * h];
-    };
     Md5State st = md5_init();
     auto md5_block = [&](const uint4 (&w)[5]) __attribute__((always_inline)) {
         uint32_t d[20];
@@ -696,34 +682,13 @@ __device__ __forceinline__ void shift_wave(const uint8_t* __restrict__ gdata, ui
 #pragma unroll
         for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_alignbyte(d[W + i + 1], d[W + i], r);
         md5_stream_block(st, m);
-    };
-    auto weak_mfma = [&]() __attribute__((always_inline)) {
+        // the block's weak-sum MFMAs (R += P_{b-1} first), as block_sums_pipe_body's weak_words
 #pragma unroll
-        for (int g = 0; g < 4; ++g) Racc[g] += acc[g][0];
+        for (int e = 0; e < 4; ++e) RW[e] += accW[e];
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const uint4 bv = Bv[4 * h + g];
-                const v4i32 b4 = {(int)bv.x, (int)bv.y, (int)bv.z, (int)bv.w};
-                acc[g] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wA[h], b4, acc[g], 0, 0, 0);
-            }
-    };
-    // signed-byte sums of the lane's own row, line in `half`, over the bytes j with (j < a) == BEFORE
-    auto edge_sums = [&](int half, bool before, int32_t& s, int32_t& u) __attribute__((always_inline)) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint4 v = lds_all[row + 8 * half + k];
-            const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int j0 = 16 * k + 4 * e;
-                const int nb = (int)a - j0;  // bytes of this dword before the chunk
-                const uint32_t lo = nb <= 0 ? 0u : nb >= 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
-                const uint32_t x = dw[e] & (before ? lo : ~lo);
-                s = __builtin_amdgcn_sdot4((int)x, 0x01010101, s, false);
-                u = __builtin_amdgcn_sdot4((int)x, j0 | ((j0 + 1) << 8) | ((j0 + 2) << 16) | ((j0 + 3) << 24), u, false);
-            }
+        for (int k = 0; k < 4; ++k) {
+            const v4i32 b4 = {(int)m[4 * k], (int)m[4 * k + 1], (int)m[4 * k + 2], (int)m[4 * k + 3]};
+            accW = __builtin_amdgcn_mfma_i32_16x16x64_i8(wW[k], b4, accW, 0, 0, 0);
         }
     };
     // Step u: line u sits in half P = u & 1.  PREV: MD5 of stage u - 1; NEXT: write line u + 1 (half P ^ 1) and
@@ -736,9 +701,7 @@ __device__ __forceinline__ void shift_wave(const uint8_t* __restrict__ gdata, ui
             put(q[P ^ 1], P ^ 1);
             if (refill) load(q[P ^ 1], u + 3);
         }
-        get_mfma(P);
         if (prev) md5_block(Wa);
-        weak_mfma();
         compiler_fence();
         if (next) get_words(Wa, P, 0);  // lines u and u + 1
         if (prev) md5_block(Wb);
@@ -750,8 +713,6 @@ __device__ __forceinline__ void shift_wave(const uint8_t* __restrict__ gdata, ui
     put(q[0], 0);
     load(q[0], 2);
     compiler_fence();
-    int32_t hs = 0, hu = 0;  // line 0 before the chunk
-    edge_sums(0, true, hs, hu);
     step(std::integral_constant<int, 0>{}, 0, false, true, true);
     uint32_t u = 1;
     [[maybe_unused]] int flag = 0;
@@ -767,41 +728,29 @@ __device__ __forceinline__ void shift_wave(const uint8_t* __restrict__ gdata, ui
         step(std::integral_constant<int, 1>{}, u, true, u < nst, u + 3 <= nst);
         if (u + 1 <= nst) step(std::integral_constant<int, 0>{}, u + 1, true, u + 1 < nst, u + 4 <= nst);
     }
-    int32_t ts = 0, tj = 0;  // line nst after the chunk
-    edge_sums((int)(nst & 1), false, ts, tj);
     {
         const uint64_t bits = ((uint64_t)B + 4) * 8;
         uint32_t m[16] = {seed, 0x80u, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, (uint32_t)bits, (uint32_t)(bits >> 32)};
         md5_compress(st, m);
     }
-    int32_t s1, uu;
-    {
-        const uint32_t nl = nst + 1;  // lines summed by the MFMAs
-        int32_t s1g[4], ug[4];
+    // as block_sums_pipe_body: chunk n + 16 q's sums in lane n (element q) and lane n + 16
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            Racc[g] += acc[g][0];
-            s1g[g] = acc[g][0];
-            ug[g] = (int32_t)(128u * (nl * (uint32_t)acc[g][0] - (uint32_t)Racc[g])) + acc[g][1];
-        }
-        const int src = mfma_pi_inv(l & 15);
-        int32_t t1[4], tu[4];
+    for (int e = 0; e < 4; ++e) RW[e] += accW[e];
+    const int n = l & 15, qq = l >> 4;
+    int32_t tS[4], tR[4], tW[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            t1[g] = __shfl(s1g[g], src, 64);
-            tu[g] = __shfl(ug[g], src, 64);
-        }
-        const int gs = l >> 4;
-        s1 = gs == 0 ? t1[0] : gs == 1 ? t1[1] : gs == 2 ? t1[2] : t1[3];
-        uu = gs == 0 ? tu[0] : gs == 1 ? tu[1] : gs == 2 ? tu[2] : tu[3];
+    for (int e = 0; e < 4; ++e) {
+        tS[e] = __shfl(accW[e], n, 64);
+        tR[e] = __shfl(RW[e], n, 64);
+        tW[e] = __shfl(accW[e], n + 16, 64);
     }
-    // lines -> chunk: S = S_lines - head - tail; sum over the chunk of (i' - a) x' with i' the line-space index
-    const uint32_t S = (uint32_t)s1 - (uint32_t)hs - (uint32_t)ts;
-    const uint32_t Ui = (uint32_t)uu - (uint32_t)hu - (128u * nst * (uint32_t)ts + (uint32_t)tj) - a * S;
-    const uint32_t c = c0 + l;
-    const int32_t s2 = (int32_t)(B * S - Ui);
-    weak_out[c] = (int32_t)((S & 0xFFFFu) | ((uint32_t)s2 << 16));
-    store_digest(strong_out + (size_t)c * dl, st, dl);
+    const int32_t S = qq == 0 ? tS[0] : qq == 1 ? tS[1] : qq == 2 ? tS[2] : tS[3];
+    const int32_t Rq = qq == 0 ? tR[0] : qq == 1 ? tR[1] : qq == 2 ? tR[2] : tR[3];
+    const int32_t Wq = qq == 0 ? tW[0] : qq == 1 ? tW[1] : qq == 2 ? tW[2] : tW[3];
+    const int32_t uw = (int32_t)(64u * (2u * nst * (uint32_t)S - (uint32_t)Rq)) + Wq;
+    const int32_t s2 = (int32_t)(B * (uint32_t)S - (uint32_t)uw);
+    weak_out[l] = (int32_t)(((uint32_t)S & 0xFFFFu) | ((uint32_t)s2 << 16));
+    store_digest(strong_out + (size_t)l * dl, st, dl);
 }
 
 template <int W>
