@@ -36,6 +36,11 @@ void rsh_debug_reset_options(void);
  * when it ran to completion.  *ms = -1 when that launch was not timed (a shape whose kernel takes no events). */
 int rsh_debug_kernel_ms(rsh_ctx* ctx, int32_t which, double* ms);
 
+/* The context's launch generation (the abort and hit-map words' values): *gen its current value; set >= 0 (at most
+ * the wrap point, 0x7FFFFF00) sets it first -- tests take a context across the wrap, where the device drains and every
+ * abort and map word goes back to 0 (rsh_ctx::next_gen).  set = -1 only reads. */
+int rsh_debug_generation(rsh_ctx* ctx, int32_t set, int32_t* gen);
+
 /* Which of the context's streams still have work queued or running (hipStreamQuery): bit 0 the context stream,
  * bit 1 aux (the aligned speculation), bit 2 phase (the phase-shifted speculation).  After rsh_ctx_sync it is 0. */
 int rsh_debug_streams_busy(rsh_ctx* ctx, int32_t* mask);

@@ -19,6 +19,12 @@
 namespace rsh {
 
 void destroy_batch_state(BatchState* b) { delete b; }
+hipError_t clear_batch_abort_words(BatchState* b) {  // (and the hit map's words: they carry a generation too)
+    if (!b) return hipSuccess;
+    hipError_t e = b->file_abort ? hipMemset(b->file_abort, 0, (size_t)b->file_abort_cap * 4) : hipSuccess;
+    if (e == hipSuccess && b->chain_map.p) e = hipMemset(b->chain_map.p, 0, b->chain_map.cap);
+    return e;
+}
 
 namespace batch {
 namespace {
@@ -276,7 +282,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     if (spec_after_prep && prep_all) RSH_BHIP(hipEventRecord(c->ev_prep, st));
 
     // the batched aligned speculation (deferred; see scan_device in capi.cpp)
-    int gen = ++c->gen;  // a stopped tentative launch's generation; a later launch takes a new one
+    int gen = c->next_gen();  // a stopped tentative launch's generation; a later launch takes a new one
     CopyEnt* sc = S->h_ccopies.as<CopyEnt>() + NF;
     // K1 over the sources needs nothing but the sources; the chain flags need the received tables (ev_in)
     bool k1_launched = false;
@@ -591,7 +597,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
             if (map_on)
                 RSH_BHIP(hipMemcpyAsync(S->chain_help.p, chh, (size_t)NF * sizeof(ChainHelp), hipMemcpyHostToDevice, st));
             RSH_BHIP(hipStreamWaitEvent(st, S->ev_fa, 0));
-            const int gen_b = ++c->gen;
+            const int gen_b = c->next_gen();
             if (tr) RSH_BHIP(hipEventRecord(S->ev_ch0, st));
             RSH_BHIP(launch_chain_advance(cf, (uint32_t)NF, st, 0, gen_b, map_on ? S->chain_help.as<ChainHelp>() : nullptr,
                                           n_help, tr));
@@ -752,7 +758,7 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         } else {  // no file qualifies: stop it (every group polls its file's word); the deferred launch stays
             RSH_BHIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(S->file_abort), gen, (size_t)NF, st));
             RSH_BHIP(hipStreamWaitEvent(st, S->ev_scopy, 0));
-            gen = ++c->gen;
+            gen = c->next_gen();
             k1_launched = false;
         }
         if (trace) fprintf(stderr, "[rsh-batch] lead check: %d of %d files wait for the speculation\n", nwait, NF);

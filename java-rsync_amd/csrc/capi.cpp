@@ -90,6 +90,17 @@ int warm_calls(rsh_ctx* c) {
 }
 }  // namespace
 
+// (ctx.h) the generation wrap: once per ~2^31 launches of a context
+int rsh_ctx::next_gen() {
+    if (gen >= kGenWrapAt) {
+        bool ok = hipDeviceSynchronize() == hipSuccess;  // no launch of this context is running
+        ok = ok && hipMemset(abort_word, 0, 256) == hipSuccess;
+        ok = ok && rsh::clear_batch_abort_words(batch) == hipSuccess;
+        if (ok) gen = 0;  // (a failure leaves the count going: the next call retries)
+    }
+    return ++gen;
+}
+
 extern "C" {
 
 int rsh_abi_version(void) { return RSH_ABI_VERSION; }
@@ -534,6 +545,13 @@ int rsh_debug_kernel_ms(rsh_ctx* ctx, int32_t which, double* ms) {
     float f = 0.f;
     RSH_HIP(hipEventElapsedTime(&f, which == 0 ? ctx->ev_gen_a : ctx->ev_k1a, which == 0 ? ctx->ev_gen_b : ctx->ev_k1b));
     *ms = f;
+    return RSH_OK;
+}
+
+int rsh_debug_generation(rsh_ctx* ctx, int32_t set, int32_t* gen) {
+    if (!ctx || set < -1 || set > rsh_ctx::kGenWrapAt) return RSH_E_INVAL;
+    if (set >= 0) ctx->gen = set;
+    if (gen) *gen = ctx->gen;
     return RSH_OK;
 }
 

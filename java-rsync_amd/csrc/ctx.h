@@ -22,6 +22,7 @@
 namespace rsh {
 struct BatchState;  // batch.cpp
 void destroy_batch_state(BatchState* b);
+hipError_t clear_batch_abort_words(BatchState* b);  // batch.cpp: every file's abort word and map word back to 0
 // batch.cpp: the cores this process may use (affinity mask, cgroup quota; option host_cores overrides)
 int host_cores();
 // The cores one call on this thread may use: host_cores(), or this thread's share of them while a multi-context
@@ -218,8 +219,21 @@ struct rsh_ctx {
     int* abort_word = nullptr;
     static constexpr int kPhaseWord = 16;
     int gen = 0;
+    // The next launch generation.  Launches compare their abort word with their generation for equality, and a word
+    // keeps the last generation it was set to: after 2^31 launches the counter would come back to a value a word still
+    // holds and a fresh launch would stop itself (or a walk trust a stale hit-map word, which carries its launch's
+    // generation).  So before it wraps, the device drains, every abort and map word goes back to 0 and the count
+    // restarts at 1 (once per ~2 billion launches; test_generation_wrap).
+    int next_gen();
+    static constexpr int kGenWrapAt = 0x7FFFFF00;  // below INT32_MAX by more than one call's launches
     bool spec_dl_pending = false;  // the last speculation's sums download (aux) may still read src_weak / src_strong
     int stamp_seq = 0;             // values of the stamped launches (scan.cpp prep_ensure)
+    // the next stamp value, 1..INT32_MAX and wrapping: a stamp is compared for equality, and 0 is a pinned word's
+    // initial value (a context that lives for billions of probes must not overflow the counter)
+    int next_stamp() {
+        stamp_seq = stamp_seq == INT32_MAX ? 1 : stamp_seq + 1;
+        return stamp_seq;
+    }
     std::vector<rsh_event> last_ev;  // kept when the caller's event buffer was too small
     std::atomic<bool> busy{false};   // the staging buffers and last_ev serve one call at a time
     rsh::BatchState* batch = nullptr;  // buffers of the batched (multi-file) entry points, on first use

@@ -210,7 +210,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
     // is launched only once the resolver has taken scan_defer_steps steps or scan_defer_us without finishing
     // (until then the resolver's round trips run on an otherwise idle device: a range probe beside the
     // speculation takes ~0.16 ms instead of tens of microseconds).
-    int gen = ++c->gen;  // a stopped speculation's generation; a later launch takes a new one
+    int gen = c->next_gen();  // a stopped speculation's generation; a later launch takes a new one
     const int diag = (int)rsh::opt(rsh::OPT_SCAN_DIAG);  // diagnostics (options.h)
     int64_t spec_na = na;  // windows the speculation covers: all, or a prefix (sampled launch decision)
     // The speculation K1 starts after the sample kernels on the context stream (window 0's copy and the lead and
@@ -256,7 +256,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         // measured no difference in the old layout (r2_ab2), where the copy was off the critical path.
         const bool flags_host = on_ctx && rsh::opt(rsh::OPT_SCAN_FLAGS_HOST) != 0;
         if (flags_host) {  // stamped: the host polls the stamp instead of waiting for an event
-            flags_gen = ++c->stamp_seq;
+            flags_gen = c->next_stamp();
             RSH_HIP(rsh::launch_chain_flags_stamped(c->src_weak.as<int32_t>(), c->src_strong.as<uint8_t>(), d_weak,
                                                     d_strong, (uint32_t)snf, (uint32_t)dl, c->h_fl.as<uint8_t>(),
                                                     rsh::Stamp{prep_counter(c, 1), prep_stamp(c, 1), flags_gen}, ss));
@@ -310,7 +310,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             lf->n = n;
             lf->B = (uint32_t)B;
         }
-        const int prep_gen = ++c->stamp_seq;
+        const int prep_gen = c->next_stamp();
         rsh::ScanPrep P{};
         P.data = d_src;
         P.n = n;
@@ -485,7 +485,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
         if (spec_tentative && (!eager || cover < na)) {  // stop the tentative launch; later ones take a new generation
             CallTrace tr("spec_stop", cover);
             RSH_HIP(hipStreamWriteValue32(rs, c->abort_word, (uint32_t)gen, 0));
-            gen = ++c->gen;
+            gen = c->next_gen();
             spec_launched = spec_tentative = false;
             tentative_stopped = true;
             res->stats.speculation_aborted = 3;  // overwritten below if a later launch lands or is stopped
@@ -639,7 +639,7 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
                 while (wp > 0 && addr - a0 + (uintptr_t)(wp * 64 * B) + 128 > ahi) --wp;
                 int64_t wq = ((n - s0) / B) / 64;  // full phase waves whose lines stay in the allocation
                 while (wq > 0 && addr + (uintptr_t)s0 - a1 + (uintptr_t)(wq * 64 * B) + 128 > ahi) --wq;
-                const int gph = ++c->gen;
+                const int gph = c->next_gen();
                 const int pset = 1 - c->ph_set;  // the phase part's buffer set (HipBackend::phase_hint)
                 uint32_t nseg = 0;
                 for (int64_t v = 0; v < wp; ++v)

@@ -407,7 +407,7 @@ class HipBackend : public rsh::ScanBackend {
         cf.e[cf.n++] = rsh::CopyEnt{c_->bucket.as<uint8_t>(), reinterpret_cast<uint8_t*>(hb),
                                     (int64_t)(rsh::HIT_BUCKET_INTS * sizeof(int32_t))};
         int* stamp = reinterpret_cast<int*>(hf + 1);
-        const int sgen = ++c_->stamp_seq;
+        const int sgen = c_->next_stamp();
         ok(rsh::launch_copy_few_stamped(cf, stamp, sgen, rs_));
         if (err == hipSuccess) ok(wait_stamp(stamp, sgen, rs_));
         if (fc_.q && err == hipSuccess) {  // the chain's desync: to the caller, and into the intervals the cache keeps
@@ -474,7 +474,7 @@ class HipBackend : public rsh::ScanBackend {
         if (count < kPhaseMinWindows || ph_launches >= kPhaseMaxLaunches || err != hipSuccess || !phase_on()) return;
         phase_stop();  // one at another phase is dead work now
         CallTrace tr("phase_spec", s);
-        ph_gen_ = ++c_->gen;
+        ph_gen_ = c_->next_gen();
         hipStream_t ps = c_->phase;  // its own stream: it does not queue behind a prefix speculation on aux
         // The launch this one replaces may still be draining on another stream (the segmented launch on aux
         // keeps its prefix waves and tail lanes running after the phase word stops its phase waves) and

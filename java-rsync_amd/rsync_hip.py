@@ -144,7 +144,7 @@ EXPORTS = ["rsh_abi_version", "rsh_strerror", "rsh_last_error", "rsh_device_coun
            "rsh_receiver_combine_device", "rsh_receiver_combine_batch", "rsh_block_sums_file", "rsh_match_scan_file", "rsh_block_sums_pieces", "rsh_match_scan_pieces", "rsh_block_sums_batch", "rsh_match_scan_batch", "rsh_block_sums_batch_multi", "rsh_match_scan_batch_multi", "rsh_receiver_combine_batch_multi", "rsh_shard_files", "rsh_file_md5_batch", "rsh_dev_alloc", "rsh_dev_free", "rsh_memcpy_h2d", "rsh_memcpy_d2h", "rsh_fill_splitmix_device"]
 # include/rsync_hip_debug.h (testing / diagnostics ABI)
 DEBUG_EXPORTS = ["rsh_debug_set_option", "rsh_debug_get_option", "rsh_debug_reset_options", "rsh_debug_k1_clock",
-                 "rsh_debug_streams_busy", "rsh_debug_kernel_ms", "rsh_debug_multi_selftest"]
+                 "rsh_debug_streams_busy", "rsh_debug_kernel_ms", "rsh_debug_multi_selftest", "rsh_debug_generation"]
 
 _LIB = None
 
@@ -243,6 +243,7 @@ def lib():
         "rsh_debug_reset_options": ([], None),
         "rsh_debug_k1_clock": ([P, P, I64, I32, I32, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "rsh_debug_streams_busy": ([P, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+        "rsh_debug_generation": ([P, I32, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
         "rsh_debug_kernel_ms": ([P, I32, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
         "rsh_debug_multi_selftest": ([P, I32, I32, I32, P, P, P], ctypes.c_int),
     }
@@ -435,6 +436,12 @@ class Context:
         ms = ctypes.c_double(-1.0)
         _check(lib().rsh_debug_kernel_ms(self._p, which, ctypes.byref(ms)))
         return ms.value
+
+    def generation(self, set_to=-1):
+        """The context's launch generation, after setting it to set_to when >= 0 (rsh_debug_generation)."""
+        g = ctypes.c_int32(0)
+        _check(lib().rsh_debug_generation(self._p, set_to, ctypes.byref(g)))
+        return g.value
 
     def streams_busy(self):
         """Bit mask of the context's streams with work still queued (rsh_debug_streams_busy)."""

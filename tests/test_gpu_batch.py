@@ -510,3 +510,30 @@ def test_batch_poisoned_walk(ctx, prefix, helpers, rsh_opt):
         assert R.events_as_tuples(evs[i][:sj[i].n_ev], B) == oev, f"form {i}"
         assert (sj[i].literal, sj[i].matched) == (olit, omat)
     assert any(e[0] == R.EV_MATCH for e in expect[1][0]), "form 1: the stale digest must match the carrier"
+
+
+def test_generation_wrap(rsh_opt):
+    """A context's launch generation (the values its abort words and hit-map words are compared with) runs up to the
+    wrap point and back to 1 in the middle of a phase-guess scan and a batched segment with walks and helpers: before
+    it wraps the device drains and every abort and map word goes back to 0 (rsh_ctx::next_gen), so no fresh launch can
+    meet a stale word holding its generation.  Events equal the oracle's on both sides of the wrap."""
+    import test_gpu_parity as P
+    R.build()
+    c = R.Context(0)
+    try:
+        wrap_at = 0x7FFFFF00
+        c.generation(wrap_at)  # the scan's first launch wraps
+        B, dl = 65536, 4
+        basis = O.splitmix(64 << 20, 0x5EED5EED0000A11F)
+        x = 300 * B + 777
+        src = np.concatenate([basis[:x], O.splitmix(1, 7), basis[x:]])
+        P._sender_both(c, basis.tobytes(), src.tobytes(), B, dl)
+        g = c.generation()
+        assert 0 < g < 64, g
+        c.generation(wrap_at - 1)  # the segment's second launch wraps
+        test_batch_generator_and_scan_match_oracle(c, "1", "1", 3, rsh_opt)  # two-phase walks, hit map, helpers
+        g = c.generation()
+        assert 0 < g < 64, g
+        P._sender_both(c, basis.tobytes(), src.tobytes(), B, dl)  # and a scan after it
+    finally:
+        c.close()
