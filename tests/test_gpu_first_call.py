@@ -65,20 +65,15 @@ def test_segment_scan_first_and_after_trim():
 
 def test_batch_warm_presizes_at_context_creation():
     """Option batch_warm (default 128 files): rsh_ctx_create holds the batched scan's state for config 4's shard
-    (~0.25 GiB of HBM, ~50 MiB pinned); batch_warm = 0 leaves it to the first segment call."""
-    import torch
-    import rsync_hip as R
-    R.build()
-    torch.cuda.init()
+    (~0.25 GiB of HBM, ~50 MiB pinned); batch_warm = 0 leaves it to the first segment call.  Each context is the first
+    of a fresh process (the runtime's memory pool would let a second context reuse what a first one freed)."""
+    code = ("import sys, torch; sys.path.insert(0, 'java-rsync_amd'); import rsync_hip as R; torch.cuda.init(); "
+            "R.set_option('batch_warm', int(sys.argv[1])); torch.cuda.synchronize(); "
+            "f0 = torch.cuda.mem_get_info(0)[0]; c = R.Context(0); print(f0 - torch.cuda.mem_get_info(0)[0]); c.close()")
     free = []
     for warm in (0, 128):
-        R.set_option("batch_warm", warm)
-        try:
-            torch.cuda.synchronize()
-            f0 = torch.cuda.mem_get_info(0)[0]
-            c = R.Context(0)
-            free.append(f0 - torch.cuda.mem_get_info(0)[0])
-            c.close()
-        finally:
-            R.reset_options()
+        r = subprocess.run([sys.executable, "-c", code, str(warm)], capture_output=True, text=True, timeout=300,
+                           cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        free.append(int(r.stdout.strip().splitlines()[-1]))
     assert free[1] - free[0] >= 150 << 20, free
