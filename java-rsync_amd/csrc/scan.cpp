@@ -388,7 +388,10 @@ int scan_device(rsh_ctx* c, const uint8_t* d_src, int64_t n, const rsh_header* h
             CallTrace tr("table_dl", C);
             if (download) RSH_HIP(hipEventSynchronize(c->ev_tab));
         }
-        {
+        // on the context's stream the host reads nothing this stream still writes (the prep launch's outputs came with
+        // its stamp; the prefix end's gathers are waited for where they are read): the first probe is queued behind
+        // the probe hash at once.  Otherwise the lead and sample sums (lead_w) and window 0 come down on this stream.
+        if (!on_ctx) {
             CallTrace tr("hash_sync", ns);
             RSH_HIP(hipStreamSynchronize(rs));
         }
