@@ -262,8 +262,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
     // the walks stopped -- files whose walk reached the end need none -- instead of taking one device round trip
     // per event from the start.  Its chunk indexes go here.
     if (chain_on) {
-        RSH_BHIP(S->kslots.ensure((size_t)tns * 8));
-        RSH_BHIP(S->h_kents.ensure((size_t)NF * sizeof(TableEnt)));
+        RSH_BHIP(S->kslots.ensure(kslots_bytes(tns, tw)));
+        RSH_BHIP(S->h_kents.ensure((size_t)NF * sizeof(ChunkIndexEnt)));
         RSH_BHIP(S->h_chain.ensure((size_t)NF * sizeof(ChainFile)));
         RSH_BHIP(S->h_chain_out.ensure((size_t)NF * sizeof(ChainOut)));
         RSH_BHIP(S->h_chain_ev.ensure((size_t)NF * kChainEvents * sizeof(rsh_event)));  // (kChainEvents: see above)
@@ -271,11 +271,13 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
         // the chunk indexes must be ready when the prefix K1 ends (the phase-0 walks wait for both): the runtime's
         // fill, then the index with several CASes in flight per thread; beside the prefix K1 (which holds every
         // wave slot) both end with it in config 4 (r3s: fill 0.06 ms + index 0.20 ms inside the K1's 0.29 ms)
-        RSH_BHIP(hipMemsetAsync(S->kslots.p, 0, (size_t)tns * 8, st));
-        TableEnt* ke = S->h_kents.as<TableEnt>();
+        // (one fill clears the slots and the duplicate bytes behind them)
+        RSH_BHIP(hipMemsetAsync(S->kslots.p, 0, (size_t)tns * 8 + (size_t)tw, st));
+        ChunkIndexEnt* ke = S->h_kents.as<ChunkIndexEnt>();
         for (int32_t f = 0; f < NF; ++f) {
             FileScan& fs = files[(size_t)f];
-            ke[f] = TableEnt{S->kslots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C};
+            ke[f] = ChunkIndexEnt{TableEnt{S->kslots.as<unsigned long long>() + fs.off_ns, fs.d_weak, fs.ns - 1, fs.C},
+                                  kslots_dup(S, tns) + fs.off_tw};
         }
         RSH_BHIP(launch_chunk_index(ke, (uint32_t)NF, (int32_t)maxC, st, bg));
     }
@@ -537,7 +539,8 @@ int scan_batch(rsh_ctx* c, rsh_scan_job* jobs, const std::vector<int32_t>& which
                               S->flags.as<uint8_t>() + fs.off_nf, fs.na, fs.na_a,
                               two_phase ? S->file_abort + f : nullptr, ce + (int64_t)f * kChainEvents, kChainEvents,
                               seed_word(seed), co + f,
-                              mw > 0 ? S->chain_map.as<unsigned long long>() + map_off[(size_t)f] : nullptr, hend};
+                              mw > 0 ? S->chain_map.as<unsigned long long>() + map_off[(size_t)f] : nullptr, hend,
+                              kslots_dup(S, tns) + fs.off_tw};
             if (chh) chh[f] = ChainHelp{(int32_t)((hend + CHAIN_MAP_SEG - 1) / CHAIN_MAP_SEG), 0, 1, 0, 0, 0, 0, 0, INT64_MAX, 0, 0, 0,
                                         (int32_t)opt(OPT_CHAIN_HELP_TILES)};
         }
@@ -967,8 +970,8 @@ hipError_t batch_warm(rsh_ctx* c, int32_t nfiles, int64_t n, int64_t B, int32_t 
     ok(S->h_slanes.ensure((std::max(lanes.size(), la.size() + lb.size()) + 1) * sizeof(K1Lane)));
     // the chain walks: chunk indexes, descriptors, events, the phase-0 hit map
     const int64_t kChainEvents = std::clamp<int64_t>(kChainEventBytes / (NF * (int64_t)sizeof(rsh_event)), 256, kChainEventsMax);
-    ok(S->kslots.ensure((size_t)tns * 8));
-    ok(S->h_kents.ensure((size_t)NF * sizeof(TableEnt)));
+    ok(S->kslots.ensure(kslots_bytes(tns, tw)));
+    ok(S->h_kents.ensure((size_t)NF * sizeof(ChunkIndexEnt)));
     ok(S->h_chain.ensure((size_t)NF * sizeof(ChainFile)));
     ok(S->h_chain_out.ensure((size_t)NF * sizeof(ChainOut)));
     ok(S->h_chain_ev.ensure((size_t)(NF * kChainEvents) * sizeof(rsh_event)));

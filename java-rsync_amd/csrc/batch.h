@@ -136,7 +136,7 @@ struct BatchState {
     bool scopy_pending = false;
     // the chain walk (options.h batch_chain): chunk indexes, descriptors, results and events (pinned), and the
     // speculation's flags kernel done on the aux stream (the walk reads the device flags and sums)
-    DevBuf kslots;
+    DevBuf kslots;  // the chunk indexes' slots (8 B each), then one duplicate byte per chunk (launch_chunk_index)
     PinnedBuf h_kents, h_chain, h_chain_out, h_chain_ev;
     // the phase-0 hit map (device.h ChainHelp): the files' shared map state (reset from pinned staging before each
     // launch) and the map words (generation-tagged: zeroed once when allocated, never cleared between scans)
@@ -189,6 +189,11 @@ struct BatchState {
             b->release();
     }
 };
+// BatchState::kslots: the slots of tns chunk-index entries, then tw duplicate bytes (one per chunk)
+inline size_t kslots_bytes(int64_t tns, int64_t tw) { return (size_t)tns * 8 + (size_t)tw + 8; }
+inline uint8_t* kslots_dup(BatchState* S, int64_t tns) {
+    return reinterpret_cast<uint8_t*>(S->kslots.as<unsigned long long>() + tns);
+}
 
 namespace batch {
 

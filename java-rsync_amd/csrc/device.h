@@ -438,6 +438,7 @@ struct ChainFile {
     ChainOut* out;
     unsigned long long* hmap;          // its map words, positions [0, hend) (null: not mapped)
     int64_t hend;                      // min(na_a B, n - B + 1): the positions a phase-0 search may reach
+    const uint8_t* dup;                // per chunk: 1 when another chunk has its weak sum (launch_chunk_index)
 };
 // Diagnostic: the Generator's K1 over n = 64 k B bytes with per-wave clock stamps summed into d_clk[0] (shader clock
 // ticks) and d_clk[1] (100 MHz ticks); the production kernels never stamp.
@@ -448,8 +449,15 @@ hipError_t launch_k1_clock(const uint8_t* d_data, int64_t n, uint32_t B, uint32_
 // timed: the walks read the wall clock for their section timers (scan_trace's report; ChainOut::t_*).
 hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStream_t s, int phase = 1,
                                 int abort_gen = 0, ChainHelp* help = nullptr, uint32_t helpers = 0, bool timed = false);
-// The chunk indexes of many files (slots cleared by the caller; TableEnt as for the probe hashes).
-hipError_t launch_chunk_index(const TableEnt* ents, uint32_t nfiles, int32_t max_keys, hipStream_t s, bool bg = false);
+// The chunk indexes of many files (slots and dup bytes cleared by the caller; TableEnt as for the probe hashes): the
+// index also marks dup[i] = 1 for every chunk i whose weak sum another chunk has, so that the walk decides an aligned
+// hit whose chain flag is set without looking the bucket up.
+struct ChunkIndexEnt {
+    TableEnt t;
+    uint8_t* dup;
+};
+hipError_t launch_chunk_index(const ChunkIndexEnt* ents, uint32_t nfiles, int32_t max_keys, hipStream_t s,
+                              bool bg = false);
 
 // splitmix64 counter stream (bench input): byte i = byte (i % 8) of mix(key + (i / 8 + 1) * golden).
 hipError_t launch_fill_splitmix(uint8_t* d_out, int64_t n, uint64_t key, int64_t byte_offset, hipStream_t s);

@@ -492,6 +492,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
     __shared__ int32_t sh[4 * CHAIN_THREADS / 64];
     __shared__ int32_t s_hit;                  // first hit in a tile (offset from the tile start), or INT_MAX
     __shared__ uint32_t s_key;                 // its key
+    __shared__ int32_t s_sc[4];                // an aligned map hit's own chunk: flag && !dup, then the next step's words
     __shared__ int32_t s_bk[CHAIN_BUCKET_CAP];  // bucket of the key (ascending chunk index)
     __shared__ int32_t s_nbk;
     __shared__ int64_t s_zero;                 // first unset chain flag
@@ -743,6 +744,7 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
             if (s_ck_full ? kslots_has(F.kslots, F.kmask, key) : chain_ck_has(kset, key)) p = s;
             else a = s + 1;
         }
+        bool sc_hit = false;  // the hit came from the map at an aligned window: s_sc holds its chunk's words
         bool cut = false;  // the search reached windows past the speculation (no anchor T(o))
         if (wide) {
             // tiles of CHAIN_TILE positions from a (lane-aligned), across block boundaries: each lane anchors its
@@ -770,6 +772,16 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                     // no second round trip for its key
                     const bool al_lane = need && pm % B == 0;  // (pm <= qlast < na B)
                     const int32_t awl = al_lane ? F.aw[pm / B] : 0;
+                    // ... and its chunk's chain flag and uniqueness with the next step's first words: an aligned hit
+                    // on its own chunk (flag set) whose weak sum no other chunk has is decided without the bucket
+                    const int64_t kl = pm / B, kl1 = kl + 1;
+                    int32_t scw[4] = {0, 0, 0, 0};
+                    if (al_lane && kl < nflags && kl < C) {
+                        scw[0] = (F.flags[kl] != 0 && F.dup[kl] == 0) ? 1 : 0;
+                        scw[1] = kl1 < nflags ? F.flags[kl1] : 0;
+                        scw[2] = kl1 < na ? F.aw[kl1] : 0;
+                        scw[3] = (kl1 < C && kl1 < na) ? F.table_weak[kl1] : 0;
+                    }
                     if (t == 0) s_hit = 0x7FFFFFFF;
                     if (__syncthreads_and(!need || (uint32_t)(wv >> 32) == map_gen)) {
                         if (need) {
@@ -779,12 +791,17 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
                         }
                         __syncthreads();
                         const int32_t hoff = s_hit;
-                        if (hoff != 0x7FFFFFFF && al_lane && pm == q0 + hoff) s_key = (uint32_t)awl;
+                        if (hoff != 0x7FFFFFFF && al_lane && pm == q0 + hoff) {
+                            s_key = (uint32_t)awl;
+#pragma unroll
+                            for (int v = 0; v < 4; ++v) s_sc[v] = scw[v];
+                        }
                         __syncthreads();
                         if (hoff != 0x7FFFFFFF) {  // the key: the window's true weak sum (synced)
                             p = q0 + hoff;
                             if (p % B == 0) {      // an aligned window: the speculation's sum, loaded above
                                 key = s_key;
+                                sc_hit = true;
                             } else {               // else one reduction over its B bytes
                                 int32_t w2[2] = {0, 0};
                                 range_sums(F.data, n, p, p + B, p, w2[0], w2[1]);
@@ -996,6 +1013,24 @@ __global__ __launch_bounds__(CHAIN_THREADS) void chain_advance_kernel(const Chai
         ++events;
         const int64_t kp = p / B;
         const bool spec_digest = !poisoned && p % B == 0 && kp < na;
+        // An aligned hit on its own chunk (chain flag: the speculation's weak sum and digest are chunk kp's) whose weak
+        // sum no other chunk has: the bucket is {kp}, closeIndexOf({kp}, pref) is kp, and the window's digest (the
+        // speculation's) equals chunk kp's -- the match Checksum.getCandidateChunks + Sender.java:1257-1287 find, with
+        // no round trip (config 4's 50%-modified form: every event of a walk on an unedited stretch)
+        if (sc_hit && spec_digest && kp < C && s_sc[0] != 0 && !(kp == C - 1 && F.rem > 0)) {
+            pf_s = p + B;
+            pf_pref = (int32_t)(kp + 1);
+            pf_flag = (uint8_t)s_sc[1];
+            pf_aw = s_sc[2];
+            pf_tw = s_sc[3];
+            emit_lit(m, p - m);
+            emit_match(p, B, (int32_t)kp, 1);
+            pref = (int32_t)(kp + 1);
+            s = m = p + B;
+            poisoned = 0;
+            t_event += chain_clock(timed) - te0;
+            continue;
+        }
         // the speculation's digest of an aligned window, loaded beside the bucket's slots (it depends only on p)
         // ... and chunk kp's own digest beside it: the candidate of a window that sits where its chunk sat (identical
         // stretches, edited blocks in place) is decided without another round trip
@@ -1247,9 +1282,13 @@ hipError_t launch_chain_advance(const ChainFile* files, uint32_t nfiles, hipStre
 // atomics, all in flight at once), and only a CAS that found its slot taken walks the probe path (a serial
 // CAS-then-next loop keeps one atomic round trip in flight per thread).  Config 4's 2 M chunks on the background
 // grid beside the prefix K1: the index now ends inside that launch instead of 0.03 ms after it.
+// Duplicates: of two chunks with one key, the one that ends further along the path found the other's slot taken (its
+// CAS there returned the other's entry), so a failed CAS that returns the inserting chunk's own key marks both chunks;
+// every chunk whose key another chunk has is marked so, at no cost beyond the CASes the insert takes anyway.
 constexpr int CHUNK_INDEX_MLP = 8;
-__global__ void chunk_index_kernel(const TableEnt* __restrict__ ents, uint32_t nfiles) {
-    const TableEnt e = ents[blockIdx.y];
+__global__ void chunk_index_kernel(const ChunkIndexEnt* __restrict__ ents, uint32_t nfiles) {
+    const TableEnt e = ents[blockIdx.y].t;
+    uint8_t* const dup = ents[blockIdx.y].dup;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < e.nkeys; i0 += CHUNK_INDEX_MLP * stride) {
         unsigned long long v[CHUNK_INDEX_MLP], got[CHUNK_INDEX_MLP];
@@ -1266,15 +1305,22 @@ __global__ void chunk_index_kernel(const TableEnt* __restrict__ ents, uint32_t n
             got[j] = i0 + j * stride < e.nkeys ? atomicCAS(&e.slots[h[j]], 0ull, v[j]) : 0ull;
 #pragma unroll
         for (int j = 0; j < CHUNK_INDEX_MLP; ++j) {
-            if (got[j] == 0ull) continue;
-            uint32_t hh = (h[j] + 1) & e.mask;
-            while (atomicCAS(&e.slots[hh], 0ull, v[j]) != 0ull) hh = (hh + 1) & e.mask;
+            unsigned long long g = got[j];
+            uint32_t hh = h[j];
+            while (g != 0ull) {
+                if ((g >> 32) == (v[j] >> 32)) {  // another chunk with this key: both are duplicates
+                    dup[(uint32_t)v[j] - 1] = 1;
+                    dup[(uint32_t)g - 1] = 1;
+                }
+                hh = (hh + 1) & e.mask;
+                g = atomicCAS(&e.slots[hh], 0ull, v[j]);
+            }
         }
     }
     (void)nfiles;
 }
 
-hipError_t launch_chunk_index(const TableEnt* ents, uint32_t nfiles, int32_t max_keys, hipStream_t s, bool bg) {
+hipError_t launch_chunk_index(const ChunkIndexEnt* ents, uint32_t nfiles, int32_t max_keys, hipStream_t s, bool bg) {
     if (nfiles == 0 || max_keys <= 0) return hipSuccess;
     const uint32_t gx = (uint32_t)std::min<int64_t>((max_keys + 255) / 256, bg ? 2 : 64);
     hipLaunchKernelGGL(chunk_index_kernel, dim3(gx, nfiles), dim3(256), 0, s, ents, nfiles);
