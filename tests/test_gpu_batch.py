@@ -453,6 +453,77 @@ def test_batch_chain_hit_map(ctx, helpers, rsh_opt, capfd):
         assert min(mapped) > 0, err[-2000:]
 
 
+def _weak_twin(block, rng):
+    """A block with block's rolling weak sum and other bytes: +1 at i, -1 at i+1, -1 at j, +1 at j+1 leaves both
+    the byte sum and the position-weighted sum unchanged (bytes kept in 1..126: the same signed or unsigned)."""
+    b = block.astype(np.int16).copy()
+    while True:
+        i, j = sorted(rng.sample(range(len(b) - 1), 2))
+        if j > i + 1 and all(2 <= b[k] <= 125 for k in (i, i + 1, j, j + 1)):
+            break
+    b[i] += 1
+    b[i + 1] -= 1
+    b[j] -= 1
+    b[j + 1] += 1
+    return b.astype(np.uint8)
+
+
+def test_batch_chain_duplicate_chunks(ctx, rsh_opt, capfd):
+    """The walk's aligned-hit shortcut (device_chain.hip: an aligned map hit whose chunk is flagged and has a weak
+    sum no other chunk has is a match without its bucket) against the oracle where that must not fire: bases whose
+    chunks repeat exactly (one digest, several chunks) and weak twins of other chunks (one weak sum, two digests),
+    inside the mapped prefix, under sources with every other block replaced."""
+    rsh_opt("batch_chain_prefix", 1024)
+    rsh_opt("chain_helpers", -1)
+    rsh_opt("scan_trace", 2)
+    rng = random.Random(515)
+    files = []
+    for i in range(6):
+        B = [1024, 512, 2048][i % 3]
+        nbk = rng.randrange(1100, 1400)
+        blocks = np.frombuffer(O.splitmix(nbk * B, 9100 + i).tobytes(), np.uint8).reshape(nbk, B).copy()
+        blocks &= 0x7F  # (bytes below 128: twins stay in range)
+        for _ in range(40):
+            a, c = rng.sample(range(min(nbk, 1000)), 2)
+            blocks[c] = blocks[a] if rng.random() < 0.5 else _weak_twin(blocks[a], rng)
+        basis = np.concatenate([blocks.reshape(-1), np.frombuffer(O.splitmix(B // 3, 9900 + i).tobytes(),
+                                                                   np.uint8)])
+        other = np.frombuffer(O.splitmix(len(basis), 9500 + i).tobytes(), np.uint8)
+        src = basis.copy()
+        src[:nbk * B].reshape(-1, B)[1::2] = other[:nbk * B].reshape(-1, B)[1::2]
+        files.append((basis.tobytes(), src.tobytes(), B, [2, 3, 16][i % 3]))
+    d_src, soffs = _pack(ctx, [f[1] for f in files], [0] * len(files))
+    sj = (R.ScanJob * len(files))()
+    evs, keep, expect = [], [], []
+    for i, (basis, src, B, dl) in enumerate(files):
+        h = R.header_make(B, dl, len(basis))
+        w, s = ctx.block_sums(basis, h, SEED)
+        assert len(np.unique(np.frombuffer(bytes(w), np.int32))) < h.chunk_count  # the weak sums do repeat
+        d_w, d_s = ctx.alloc(4 * h.chunk_count), ctx.alloc(dl * h.chunk_count)
+        d_w.upload(w)
+        d_s.upload(s)
+        keep += [d_w, d_s]
+        cap = len(src) // (10 * B) + 2 * h.chunk_count + 64
+        ev = np.zeros(cap, R.EVENT_DTYPE)
+        evs.append(ev)
+        sj[i].d_src, sj[i].n, sj[i].h = d_src.ptr.value + soffs[i], len(src), h
+        sj[i].d_weak, sj[i].d_strong = d_w.ptr.value, d_s.ptr.value
+        sj[i].ev, sj[i].ev_cap = ev.ctypes.data, cap
+        oev, _, olit, omat, _ = O.sender(src, O.header(B, dl, len(basis)), w, s, SEED)
+        expect.append(([tuple(e) for e in oev], olit, omat))
+    capfd.readouterr()
+    for rep in range(2):
+        assert R.lib().rsh_match_scan_batch_device(ctx.handle, sj, len(files), SEED_NP.ctypes.data, None) == 0
+        for i, (basis, src, B, dl) in enumerate(files):
+            oev, olit, omat = expect[i]
+            assert sj[i].status == 0
+            assert R.events_as_tuples(evs[i][:sj[i].n_ev], B) == oev, f"file {i}: B={B} (scan {rep})"
+            assert (sj[i].literal, sj[i].matched) == (olit, omat)
+    import re
+    mapped = [int(m) for m in re.findall(r"\((\d+) from the hit map\)", capfd.readouterr().err)]
+    assert len(mapped) == 2 and sum(mapped) > 0  # (the shortcut takes map hits only)
+
+
 @pytest.mark.parametrize("prefix,helpers", [(-1, -1), (64, -1), (64, 0), (8, -1)])
 def test_batch_poisoned_walk(ctx, prefix, helpers, rsh_opt):
     """The walk past a poisoning (quirk B): a weak twin of chunk 5 poisons the state with a digest another chunk (the
