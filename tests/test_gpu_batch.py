@@ -484,8 +484,15 @@ def test_batch_chain_duplicate_chunks(ctx, rsh_opt, capfd):
         blocks = np.frombuffer(O.splitmix(nbk * B, 9100 + i).tobytes(), np.uint8).reshape(nbk, B).copy()
         blocks &= 0x7F  # (bytes below 128: twins stay in range)
         for _ in range(40):
-            a, c = rng.sample(range(min(nbk, 1000)), 2)
-            blocks[c] = blocks[a] if rng.random() < 0.5 else _weak_twin(blocks[a], rng)
+            a, c = rng.sample(range(2, min(nbk, 1000)), 2)
+            r = rng.random()
+            if r < 0.4:  # chunk c - 1 (replaced in the source) repeats kept chunk c: the Java scan, whose bucket
+                c &= ~1  # search starts at pref = c - 1 after the match of c - 2, matches c - 1 at c's window
+                blocks[c - 1] = blocks[c]
+            elif r < 0.7:
+                blocks[c] = blocks[a]
+            else:
+                blocks[c] = _weak_twin(blocks[a], rng)
         basis = np.concatenate([blocks.reshape(-1), np.frombuffer(O.splitmix(B // 3, 9900 + i).tobytes(),
                                                                    np.uint8)])
         other = np.frombuffer(O.splitmix(len(basis), 9500 + i).tobytes(), np.uint8)
